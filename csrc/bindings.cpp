@@ -1,0 +1,420 @@
+// pybind11 module `inference_arena_amd._C`.
+//
+// Exposes (a) every kernel launcher with a dict of device pointers / sizes,
+// used by the kernel-vs-oracle tests and the Python op wrappers, and (b) the
+// native Executor (csrc/runtime/executor.h), which releases the GIL for host
+// packing, graph launch and result waits.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "kernels/launch.h"
+#include "runtime/executor.h"
+#include "runtime/batcher.h"
+
+namespace py = pybind11;
+using namespace arena;
+
+namespace {
+
+template <typename T>
+T get(const py::dict& d, const char* k, T dflt) {
+  if (!d.contains(k)) return dflt;
+  py::object o = d[k];
+  if (o.is_none()) return dflt;
+  return o.cast<T>();
+}
+template <typename T>
+T req(const py::dict& d, const char* k) {
+  if (!d.contains(k)) throw std::runtime_error(std::string("missing kernel parameter '") + k + "'");
+  return d[k].cast<T>();
+}
+template <typename P>
+P ptr(const py::dict& d, const char* k) {
+  return reinterpret_cast<P>(get<uintptr_t>(d, k, 0));
+}
+hipStream_t stream_of(const py::dict& d) { return reinterpret_cast<hipStream_t>(get<uintptr_t>(d, "stream", 0)); }
+
+void py_conv2d(const py::dict& d) {
+  ConvParams p{};
+  p.x = ptr<const void*>(d, "x");
+  p.B = req<int>(d, "B");
+  p.H = req<int>(d, "H");
+  p.W = req<int>(d, "W");
+  p.xs = req<int>(d, "xs");
+  p.Cin = req<int>(d, "Cin");
+  p.w = ptr<const void*>(d, "w");
+  p.Kpad = req<int>(d, "Kpad");
+  p.bias = ptr<const float*>(d, "bias");
+  p.y = ptr<void*>(d, "y");
+  p.Ho = req<int>(d, "Ho");
+  p.Wo = req<int>(d, "Wo");
+  p.ys = req<int>(d, "ys");
+  p.Cout = req<int>(d, "Cout");
+  p.Cout_pad = req<int>(d, "Cout_pad");
+  p.KH = req<int>(d, "KH");
+  p.KW = req<int>(d, "KW");
+  p.stride = get<int>(d, "stride", 1);
+  p.pad_t = get<int>(d, "pad_t", 0);
+  p.pad_l = get<int>(d, "pad_l", 0);
+  p.res = ptr<const void*>(d, "res");
+  p.rs = get<int>(d, "rs", 0);
+  p.y2 = ptr<void*>(d, "y2");
+  p.y2s = get<int>(d, "y2s", 0);
+  p.act = get<int>(d, "act", 0);
+  p.f32out = get<int>(d, "f32out", 0);
+  p.bdev = ptr<const int*>(d, "bdev");
+  conv2d(p, stream_of(d));
+}
+
+void py_dwconv(const py::dict& d) {
+  DwParams p{};
+  p.x = ptr<const void*>(d, "x");
+  p.B = req<int>(d, "B");
+  p.H = req<int>(d, "H");
+  p.W = req<int>(d, "W");
+  p.xs = req<int>(d, "xs");
+  p.C = req<int>(d, "C");
+  p.w = ptr<const void*>(d, "w");
+  p.bias = ptr<const float*>(d, "bias");
+  p.y = ptr<void*>(d, "y");
+  p.Ho = req<int>(d, "Ho");
+  p.Wo = req<int>(d, "Wo");
+  p.ys = req<int>(d, "ys");
+  p.stride = get<int>(d, "stride", 1);
+  p.act = get<int>(d, "act", 0);
+  p.bdev = ptr<const int*>(d, "bdev");
+  dwconv3x3(p, stream_of(d));
+}
+
+void py_sppf(const py::dict& d) {
+  SppfParams p{};
+  p.buf = ptr<void*>(d, "buf");
+  p.B = req<int>(d, "B");
+  p.H = req<int>(d, "H");
+  p.W = req<int>(d, "W");
+  p.xs = req<int>(d, "xs");
+  p.C = req<int>(d, "C");
+  p.bdev = ptr<const int*>(d, "bdev");
+  sppf_pool(p, stream_of(d));
+}
+
+void py_letterbox(const py::dict& d) {
+  LetterboxParams p{};
+  p.pool = ptr<const uint8_t*>(d, "pool");
+  p.meta = ptr<const ImageMeta*>(d, "meta");
+  p.ctrl = ptr<const Ctrl*>(d, "ctrl");
+  p.out = ptr<void*>(d, "out");
+  p.B = req<int>(d, "B");
+  p.T = req<int>(d, "T");
+  letterbox_s2d(p, stream_of(d));
+}
+
+void py_decode(const py::dict& d) {
+  DecodeParams p{};
+  auto heads = req<std::vector<uintptr_t>>(d, "head");
+  auto hw = req<std::vector<int>>(d, "hw");
+  auto xs = req<std::vector<int>>(d, "xs");
+  auto st = req<std::vector<float>>(d, "strides");
+  for (int l = 0; l < 3; ++l) {
+    p.head[l] = (const void*)heads.at(l);
+    p.hw[l] = hw.at(l);
+    p.xs[l] = xs.at(l);
+    p.stride[l] = st.at(l);
+  }
+  p.B = req<int>(d, "B");
+  p.conf_thr = req<float>(d, "conf_thr");
+  p.cand = ptr<Candidate*>(d, "cand");
+  p.cand_count = ptr<int*>(d, "cand_count");
+  p.cand_cap = req<int>(d, "cand_cap");
+  p.ctrl = ptr<const Ctrl*>(d, "ctrl");
+  detect_decode(p, stream_of(d));
+}
+
+void py_nms(const py::dict& d) {
+  prepare_kernels();
+  NmsParams p{};
+  p.cand = ptr<const Candidate*>(d, "cand");
+  p.cand_count = ptr<const int*>(d, "cand_count");
+  p.cand_cap = req<int>(d, "cand_cap");
+  p.meta = ptr<const ImageMeta*>(d, "meta");
+  p.B = req<int>(d, "B");
+  p.iou_thr = req<float>(d, "iou_thr");
+  p.det = ptr<Detection*>(d, "det");
+  p.det_count = ptr<int*>(d, "det_count");
+  p.max_det = req<int>(d, "max_det");
+  p.ctrl = ptr<const Ctrl*>(d, "ctrl");
+  nms(p, stream_of(d));
+}
+
+void py_crop_plan(const py::dict& d) {
+  CropPlanParams p{};
+  p.det = ptr<const Detection*>(d, "det");
+  p.det_count = ptr<const int*>(d, "det_count");
+  p.max_det = req<int>(d, "max_det");
+  p.meta = ptr<const ImageMeta*>(d, "meta");
+  p.B = req<int>(d, "B");
+  p.crops = ptr<CropRef*>(d, "crops");
+  p.ctrl = ptr<Ctrl*>(d, "ctrl");
+  p.crop_cap = req<int>(d, "crop_cap");
+  crop_plan(p, stream_of(d));
+}
+
+void py_crop_gather(const py::dict& d) {
+  CropGatherParams p{};
+  p.pool = ptr<const uint8_t*>(d, "pool");
+  p.meta = ptr<const ImageMeta*>(d, "meta");
+  p.crops = ptr<const CropRef*>(d, "crops");
+  p.ctrl = ptr<const Ctrl*>(d, "ctrl");
+  p.out = ptr<void*>(d, "out");
+  p.cap = req<int>(d, "cap");
+  p.S = req<int>(d, "S");
+  auto mean = req<std::vector<float>>(d, "mean");
+  auto inv_std = req<std::vector<float>>(d, "inv_std");
+  for (int c = 0; c < 3; ++c) {
+    p.mean[c] = mean.at(c);
+    p.inv_std[c] = inv_std.at(c);
+  }
+  crop_gather_s2d(p, stream_of(d));
+}
+
+void py_avgpool(const py::dict& d) {
+  AvgPoolParams p{};
+  p.x = ptr<const void*>(d, "x");
+  p.B = req<int>(d, "B");
+  p.HW = req<int>(d, "HW");
+  p.C = req<int>(d, "C");
+  p.y = ptr<void*>(d, "y");
+  p.bdev = ptr<const int*>(d, "bdev");
+  global_avgpool(p, stream_of(d));
+}
+
+void py_topk(const py::dict& d) {
+  TopkParams p{};
+  p.logits = ptr<const float*>(d, "logits");
+  p.B = req<int>(d, "B");
+  p.N = req<int>(d, "N");
+  p.ld = req<int>(d, "ld");
+  p.out = ptr<TopkResult*>(d, "out");
+  p.ctrl = ptr<const Ctrl*>(d, "ctrl");
+  p.bdev = ptr<const int*>(d, "bdev");
+  topk_softmax(p, stream_of(d));
+}
+
+ExecutorConfig config_from(const py::dict& d) {
+  ExecutorConfig c;
+  c.device = get<int>(d, "device", c.device);
+  c.max_batch = get<int>(d, "max_batch", c.max_batch);
+  c.max_det = get<int>(d, "max_det", c.max_det);
+  c.cand_cap = get<int>(d, "cand_cap", c.cand_cap);
+  c.crop_cap_per_image = get<int>(d, "crop_cap_per_image", c.crop_cap_per_image);
+  c.min_crop_cap = get<int>(d, "min_crop_cap", c.min_crop_cap);
+  c.pool_bytes_per_image = get<int64_t>(d, "pool_bytes_per_image", c.pool_bytes_per_image);
+  c.det_size = get<int>(d, "det_size", c.det_size);
+  c.cls_size = get<int>(d, "cls_size", c.cls_size);
+  c.host_threads = get<int>(d, "host_threads", c.host_threads);
+  return c;
+}
+
+std::vector<InputImage> images_from(const py::list& imgs, std::vector<py::array>& keep) {
+  std::vector<InputImage> v;
+  v.reserve(imgs.size());
+  for (auto h : imgs) {
+    py::array a = py::array::ensure(h, py::array::c_style);
+    if (!a || a.ndim() != 3 || a.shape(2) != 3 || a.itemsize() != 1)
+      throw std::runtime_error("images must be contiguous uint8 HxWx3 arrays");
+    keep.push_back(a);
+    InputImage im;
+    im.data = (const uint8_t*)a.data();
+    im.h = (int)a.shape(0);
+    im.w = (int)a.shape(1);
+    v.push_back(im);
+  }
+  return v;
+}
+
+py::dict result_to_py(const BatchResult& r, int max_det) {
+  py::dict out;
+  const int n = r.n_images;
+  py::array_t<int32_t> cnt(n);
+  std::memcpy(cnt.mutable_data(), r.det_count.data(), sizeof(int) * n);
+  py::array_t<float> det({n, max_det, 8});
+  static_assert(sizeof(Detection) == 32, "Detection layout");
+  if (n) std::memcpy(det.mutable_data(), r.det.data(), sizeof(Detection) * (size_t)n * max_det);
+  py::array_t<int32_t> offs(n + 1);
+  std::memcpy(offs.mutable_data(), r.crop_offset.data(), sizeof(int) * (n + 1));
+  static_assert(sizeof(TopkResult) == 64, "TopkResult layout");
+  py::array_t<int32_t> tk_idx({(int)r.topk.size(), 5});
+  py::array_t<float> tk_logit({(int)r.topk.size(), 5});
+  py::array_t<float> tk_prob({(int)r.topk.size(), 5});
+  for (size_t i = 0; i < r.topk.size(); ++i)
+    for (int k = 0; k < 5; ++k) {
+      tk_idx.mutable_at(i, k) = r.topk[i].idx[k];
+      tk_logit.mutable_at(i, k) = r.topk[i].logit[k];
+      tk_prob.mutable_at(i, k) = r.topk[i].prob[k];
+    }
+  out["det_count"] = cnt;
+  out["det"] = det;
+  out["crop_offset"] = offs;
+  out["topk_idx"] = tk_idx;
+  out["topk_logit"] = tk_logit;
+  out["topk_prob"] = tk_prob;
+  out["gpu_ms"] = r.gpu_ms;
+  out["bucket"] = r.bucket;
+  out["total_crops"] = r.total_crops;
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native kernels and runtime of inference_arena_amd (gfx950)";
+  m.def("conv2d", &py_conv2d);
+  m.def("dwconv3x3", &py_dwconv);
+  m.def("sppf_pool", &py_sppf);
+  m.def("letterbox_s2d", &py_letterbox);
+  m.def("detect_decode", &py_decode);
+  m.def("nms", &py_nms);
+  m.def("crop_plan", &py_crop_plan);
+  m.def("crop_gather_s2d", &py_crop_gather);
+  m.def("global_avgpool", &py_avgpool);
+  m.def("topk_softmax", &py_topk);
+  m.attr("SIZEOF_IMAGE_META") = (int)sizeof(ImageMeta);
+  m.attr("SIZEOF_CTRL") = (int)sizeof(Ctrl);
+  m.attr("SIZEOF_CANDIDATE") = (int)sizeof(Candidate);
+  m.attr("SIZEOF_DETECTION") = (int)sizeof(Detection);
+  m.attr("SIZEOF_CROPREF") = (int)sizeof(CropRef);
+  m.attr("SIZEOF_TOPK") = (int)sizeof(TopkResult);
+  m.attr("OP_FIELDS") = kOpFields;
+
+  py::class_<Executor, std::shared_ptr<Executor>>(m, "Executor")
+      .def(py::init([](const py::dict& cfg) { return std::make_shared<Executor>(config_from(cfg)); }))
+      .def("set_weights",
+           [](Executor& e, py::array_t<uint8_t, py::array::c_style> blob) { e.set_weights(blob.data(), blob.size()); })
+      .def("set_program",
+           [](Executor& e, py::array_t<int64_t, py::array::c_style> ops, py::array_t<int64_t, py::array::c_style> cls) {
+             if (ops.ndim() != 2 || ops.shape(1) != kOpFields || cls.ndim() != 2 || cls.shape(1) != kOpFields)
+               throw std::runtime_error("programs must be int64 [n, OP_FIELDS]");
+             e.set_program(ops.data(), (int)ops.shape(0), cls.data(), (int)cls.shape(0));
+           })
+      .def("add_bucket",
+           [](Executor& e, int B, py::array_t<int64_t, py::array::c_style> offs, int64_t arena_bytes) {
+             e.add_bucket(B, offs.data(), (int)offs.size(), arena_bytes);
+           })
+      .def("buckets", &Executor::buckets)
+      .def("crop_cap_for", &Executor::crop_cap_for)
+      .def("submit",
+           [](Executor& e, const py::list& imgs) {
+             std::vector<py::array> keep;
+             auto v = images_from(imgs, keep);
+             py::gil_scoped_release nogil;
+             return e.submit(v);
+           })
+      .def("collect",
+           [](Executor& e, int slot) {
+             BatchResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = e.collect(slot);
+             }
+             return result_to_py(r, e.config().max_det);
+           })
+      .def("run",
+           [](Executor& e, const py::list& imgs) {
+             std::vector<py::array> keep;
+             auto v = images_from(imgs, keep);
+             BatchResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = e.run(v);
+             }
+             return result_to_py(r, e.config().max_det);
+           })
+      .def("replay",
+           [](Executor& e, int B, int slot, int iters) {
+             py::gil_scoped_release nogil;
+             e.replay(B, slot, iters);
+           })
+      .def("synchronize",
+           [](Executor& e) {
+             py::gil_scoped_release nogil;
+             e.synchronize();
+           })
+      .def("arena_ptr", &Executor::arena_ptr)
+      .def("weights_ptr", &Executor::weights_ptr)
+      .def("stream", &Executor::stream);
+
+  py::class_<DynamicBatcher>(m, "DynamicBatcher")
+      .def(py::init([](py::list executors, const py::dict& cfg) {
+             std::vector<std::shared_ptr<Executor>> inst;
+             for (auto h : executors) inst.push_back(h.cast<std::shared_ptr<Executor>>());
+             BatcherConfig c;
+             c.max_batch = get<int>(cfg, "max_batch", c.max_batch);
+             c.preferred = get<std::vector<int>>(cfg, "preferred", {});
+             c.max_queue_delay_us = get<int64_t>(cfg, "max_queue_delay_us", c.max_queue_delay_us);
+             c.max_queue_size = get<int64_t>(cfg, "max_queue_size", c.max_queue_size);
+             return new DynamicBatcher(inst, c);
+           }),
+           py::keep_alive<1, 2>())
+      .def("enqueue",
+           [](DynamicBatcher& b, py::array_t<uint8_t, py::array::c_style> img, py::function cb) {
+             if (img.ndim() != 3 || img.shape(2) != 3) throw std::runtime_error("image must be HxWx3 uint8");
+             auto pycb = std::make_shared<py::function>(std::move(cb));
+             ResultCallback f = [pycb](RequestResult&& r) {
+               py::gil_scoped_acquire gil;
+               py::dict d;
+               d["id"] = r.id;
+               d["error"] = r.error;
+               d["det_count"] = r.det_count;
+               const int k = (int)r.det.size();
+               py::array_t<float> det({k, 8});
+               if (k) std::memcpy(det.mutable_data(), r.det.data(), sizeof(Detection) * k);
+               const int t = (int)r.topk.size();
+               py::array_t<int32_t> ti({t, 5});
+               py::array_t<float> tl({t, 5}), tp({t, 5});
+               for (int i = 0; i < t; ++i)
+                 for (int j = 0; j < 5; ++j) {
+                   ti.mutable_at(i, j) = r.topk[i].idx[j];
+                   tl.mutable_at(i, j) = r.topk[i].logit[j];
+                   tp.mutable_at(i, j) = r.topk[i].prob[j];
+                 }
+               d["det"] = det;
+               d["topk_idx"] = ti;
+               d["topk_logit"] = tl;
+               d["topk_prob"] = tp;
+               d["batch_size"] = r.batch_size;
+               d["queue_us"] = r.queue_us;
+               d["compute_us"] = r.compute_us;
+               try {
+                 (*pycb)(d);
+               } catch (py::error_already_set& e) {
+                 e.discard_as_unraisable("DynamicBatcher callback");
+               }
+             };
+             const uint8_t* data = img.data();
+             const int h = (int)img.shape(0), w = (int)img.shape(1);
+             py::gil_scoped_release nogil;
+             return b.enqueue(data, h, w, std::move(f));
+           })
+      .def("stats",
+           [](DynamicBatcher& b) {
+             BatcherStats s = b.stats();
+             py::dict d;
+             d["requests"] = s.requests;
+             d["batches"] = s.batches;
+             d["rejected"] = s.rejected;
+             d["failed"] = s.failed;
+             d["queue_depth"] = s.queue_depth;
+             d["mean_batch"] = s.batches ? s.sum_batch / s.batches : 0.0;
+             d["mean_queue_us"] = s.requests ? s.sum_queue_us / s.requests : 0.0;
+             d["mean_compute_us"] = s.batches ? s.sum_compute_us / s.batches : 0.0;
+             d["batch_hist"] = s.batch_hist;
+             return d;
+           })
+      .def("shutdown", [](DynamicBatcher& b) {
+        py::gil_scoped_release nogil;
+        b.shutdown();
+      });
+}

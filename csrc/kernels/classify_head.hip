@@ -1,0 +1,96 @@
+// Classifier tail: global average pool (K13 first half) and the per-row
+// argmax / softmax / top-5 reduction (K14).
+//
+// Reference semantics: architectures/monolithic/app/inference.py:201-203 and
+// architectures/triton/gateway/app/pipeline.py:181-183 report the top-1 raw
+// logit; architectures/microservices/classification/app/inference.py:112-132
+// reports softmax probabilities and a top-5 list.  The kernel returns both so
+// each topology can reproduce its own reference field.
+#include "common.h"
+#include "launch.h"
+
+namespace arena {
+
+__global__ __launch_bounds__(256) void avgpool_kernel(const AvgPoolParams p) {
+  const int B = live_batch(p.B, p.bdev);
+  const int cg = p.C >> 3;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (long)B * cg) return;
+  const int b = (int)(tid / cg), g = (int)(tid % cg);
+  const bf16* x = (const bf16*)p.x + (size_t)b * p.HW * p.C + g * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < p.HW; ++i) {
+    float v[8];
+    unpack8(*(const uint4*)(x + (size_t)i * p.C), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += v[k];
+  }
+  const float inv = 1.0f / (float)p.HW;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] *= inv;
+  *(uint4*)((bf16*)p.y + (size_t)b * p.C + g * 8) = pack8(acc);
+}
+
+void global_avgpool(const AvgPoolParams& p, hipStream_t s) {
+  if (p.C % 8 != 0) throw std::runtime_error("global_avgpool: C % 8 != 0");
+  const long total = (long)p.B * (p.C / 8);
+  if (total <= 0) return;
+  hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+}
+
+// One wave per row.  Each round finds the (value, first index) maximum over
+// the row with the previously chosen indices excluded.
+__global__ __launch_bounds__(256) void topk_kernel(const TopkParams p) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int B = p.B;
+  if (p.ctrl != nullptr) B = live_batch(p.B, &p.ctrl->n_crops);
+  else if (p.bdev != nullptr) B = live_batch(p.B, p.bdev);
+  if (row >= B) return;
+  const float* x = p.logits + (size_t)row * p.ld;
+  float mx = -INFINITY;
+  for (int i = lane; i < p.N; i += 64) mx = fmaxf(mx, x[i]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int i = lane; i < p.N; i += 64) se += __expf(x[i] - mx);
+  se = wave_sum(se);
+  const float inv = 1.0f / se;
+
+  TopkResult res;
+  int chosen[5] = {-1, -1, -1, -1, -1};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = lane; i < p.N; i += 64) {
+      bool skip = false;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) skip |= (q < k) && (chosen[q] == i);
+      const float v = x[i];
+      if (!skip && (v > bv || (v == bv && i < bi))) { bv = v; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    chosen[k] = bi;
+    res.idx[k] = bi;
+    res.logit[k] = bv;
+    res.prob[k] = __expf(bv - mx) * inv;
+  }
+  res.pad_ = 0;
+  if (lane == 0) {
+    const int base = p.ctrl != nullptr ? p.ctrl->crop_base : 0;
+    p.out[base + row] = res;
+  }
+}
+
+void topk_softmax(const TopkParams& p, hipStream_t s) {
+  if (p.N < 5) throw std::runtime_error("topk_softmax: N < 5");
+  if (p.B <= 0) return;
+  hipLaunchKernelGGL(topk_kernel, dim3((p.B + 3) / 4), dim3(256), 0, s, p);
+}
+
+}  // namespace arena

@@ -1,0 +1,84 @@
+// Shared device-side helpers for the gfx950 (CDNA4) kernels of the arena.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * activations are NHWC bf16; a tensor "view" is (base pointer already
+//     offset to its channel slice, pixel stride in elements). Channel counts,
+//     slice offsets and pixel strides are multiples of 8, so 16-byte vector
+//     loads/stores are always aligned.
+//   * batch sizes may be clamped at run time by a device-side counter
+//     (`bdev`): the hipGraph of a batch bucket is captured once for the
+//     bucket's capacity and the blocks past the live batch exit immediately.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace arena {
+
+enum Act : int { ACT_NONE = 0, ACT_SILU = 1, ACT_RELU6 = 2 };
+
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == ACT_SILU) return v / (1.0f + __expf(-v));
+  if (act == ACT_RELU6) return fminf(fmaxf(v, 0.0f), 6.0f);
+  return v;
+}
+
+// Unpack / pack 8 bf16 carried in a uint4.
+__device__ __forceinline__ void unpack8(uint4 u, float* f) {
+  bf16x8 v = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (bf16)f[i];
+  return __builtin_bit_cast(uint4, v);
+}
+__device__ __forceinline__ void unpack4(uint2 u, float* f) {
+  bf16x4 v = __builtin_bit_cast(bf16x4, u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) f[i] = (float)v[i];
+}
+__device__ __forceinline__ uint2 pack4(const float* f) {
+  bf16x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = (bf16)f[i];
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ int live_batch(int cap, const int* bdev) {
+  if (bdev == nullptr) return cap;
+  int n = *bdev;
+  return n < cap ? (n < 0 ? 0 : n) : cap;
+}
+
+// Wave-level reductions (64 lanes).
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace arena
+
+#define ARENA_HIP_CHECK(expr)                                                     \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+    }                                                                             \
+  } while (0)

@@ -1,0 +1,292 @@
+// Detector tail on the GPU: SPPF pooling (K5), DFL/box decode + class
+// threshold compaction (K7), class-aware greedy NMS with un-letterboxing (K8)
+// and the crop plan that feeds the classifier (first half of K9).
+//
+// Reference semantics:
+//   decode: ultralytics Detect head exported in the ONNX graph — DFL softmax
+//     over 16 bins per side, dist2bbox (ltrb -> xywh) x stride, sigmoid class
+//     scores -> [1,84,8400] (experiment.yaml:199-207).
+//   threshold + NMS: architectures/monolithic/app/postprocess.py:12-160 —
+//     conf = max class score, class = argmax, keep conf >= thr, per-class
+//     greedy NMS suppressing IoU > thr (eps 1e-6), output ordered by class id
+//     ascending then score descending.
+//   un-letterbox + clip: src/shared/processing/transforms.py:183-230.
+//   crop box: src/shared/processing/mobilenet_preprocess.py:236-269.
+#include <string>
+#include <stdexcept>
+#include "common.h"
+#include "launch.h"
+
+namespace arena {
+
+// ------------------------------------------------------------------ SPPF
+__global__ __launch_bounds__(256) void sppf_kernel(const SppfParams p) {
+  const int B = live_batch(p.B, p.bdev);
+  const int cg = p.C >> 3;
+  const long total = (long)B * p.H * p.W * cg;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int g = (int)(tid % cg);
+  const long pix = tid / cg;
+  const int x = (int)(pix % p.W);
+  const int y = (int)((pix / p.W) % p.H);
+  const int b = (int)(pix / ((long)p.W * p.H));
+  bf16* buf = (bf16*)p.buf;
+  float m5[8], m9[8], m13[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m5[i] = m9[i] = m13[i] = -INFINITY;
+  for (int dy = -6; dy <= 6; ++dy) {
+    const int iy = y + dy;
+    if ((unsigned)iy >= (unsigned)p.H) continue;
+    const int ady = dy < 0 ? -dy : dy;
+    for (int dx = -6; dx <= 6; ++dx) {
+      const int ix = x + dx;
+      if ((unsigned)ix >= (unsigned)p.W) continue;
+      const int adx = dx < 0 ? -dx : dx;
+      float v[8];
+      unpack8(*(const uint4*)(buf + ((size_t)(b * p.H + iy) * p.W + ix) * p.xs + g * 8), v);
+      const int r = ady > adx ? ady : adx;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        m13[i] = fmaxf(m13[i], v[i]);
+        if (r <= 4) m9[i] = fmaxf(m9[i], v[i]);
+        if (r <= 2) m5[i] = fmaxf(m5[i], v[i]);
+      }
+    }
+  }
+  bf16* o = buf + ((size_t)(b * p.H + y) * p.W + x) * p.xs + g * 8;
+  *(uint4*)(o + p.C) = pack8(m5);
+  *(uint4*)(o + 2 * p.C) = pack8(m9);
+  *(uint4*)(o + 3 * p.C) = pack8(m13);
+}
+
+void sppf_pool(const SppfParams& p, hipStream_t s) {
+  if (p.C % 8 != 0 || p.xs < 4 * p.C) throw std::runtime_error("sppf_pool: bad geometry");
+  const long total = (long)p.B * p.H * p.W * (p.C / 8);
+  if (total <= 0) return;
+  hipLaunchKernelGGL(sppf_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+}
+
+// ------------------------------------------------------------------ decode
+__global__ __launch_bounds__(256) void decode_kernel(const DecodeParams p) {
+  const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
+  const int A0 = p.hw[0] * p.hw[0], A1 = p.hw[1] * p.hw[1], A2 = p.hw[2] * p.hw[2];
+  const int A = A0 + A1 + A2;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (long)n_img * A) return;
+  const int b = (int)(tid / A);
+  const int a = (int)(tid - (long)b * A);
+  int l, r;
+  if (a < A0) { l = 0; r = a; } else if (a < A0 + A1) { l = 1; r = a - A0; } else { l = 2; r = a - A0 - A1; }
+  const int hw = p.hw[l];
+  const bf16* px = (const bf16*)p.head[l] + ((size_t)b * hw * hw + r) * p.xs[l];
+
+  // class scores: sigmoid, max + first argmax (ties resolved like np.argmax)
+  float best = -1.f;
+  int cls = 0;
+#pragma unroll
+  for (int g = 0; g < 10; ++g) {
+    float v[8];
+    unpack8(*(const uint4*)(px + 64 + g * 8), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sgm = 1.0f / (1.0f + __expf(-v[i]));
+      if (sgm > best) { best = sgm; cls = g * 8 + i; }
+    }
+  }
+  if (!(best >= p.conf_thr)) return;
+
+  float dist[4];
+#pragma unroll
+  for (int side = 0; side < 4; ++side) {
+    float v[16];
+    unpack8(*(const uint4*)(px + side * 16), v);
+    unpack8(*(const uint4*)(px + side * 16 + 8), v + 8);
+    float mx = v[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
+    float se = 0.f, sw = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float e = __expf(v[i] - mx);
+      se += e;
+      sw += e * (float)i;
+    }
+    dist[side] = sw / se;
+  }
+  const int gy = r / hw, gx = r - (r / hw) * hw;
+  const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f;
+  const float s = p.stride[l];
+  const float bx1 = ax - dist[0], by1 = ay - dist[1], bx2 = ax + dist[2], by2 = ay + dist[3];
+  const float cx = (bx1 + bx2) * 0.5f * s, cy = (by1 + by2) * 0.5f * s;
+  const float w = (bx2 - bx1) * s, h = (by2 - by1) * s;
+  const int slot = atomicAdd(&p.cand_count[b], 1);
+  if (slot >= p.cand_cap) return;
+  Candidate c;
+  c.x1 = cx - w * 0.5f;
+  c.y1 = cy - h * 0.5f;
+  c.x2 = cx + w * 0.5f;
+  c.y2 = cy + h * 0.5f;
+  c.score = best;
+  c.cls = cls;
+  c.anchor = a;
+  c.pad_ = 0;
+  p.cand[(size_t)b * p.cand_cap + slot] = c;
+}
+
+void detect_decode(const DecodeParams& p, hipStream_t s) {
+  const long A = (long)p.hw[0] * p.hw[0] + (long)p.hw[1] * p.hw[1] + (long)p.hw[2] * p.hw[2];
+  const long total = A * p.B;
+  if (total <= 0) return;
+  if (p.cand_cap > 16384) throw std::runtime_error("detect_decode: cand_cap > 16384");
+  hipLaunchKernelGGL(decode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+}
+
+// ------------------------------------------------------------------ NMS
+// One 1024-thread workgroup per image.  Candidates are sorted in LDS by a
+// 64-bit key (class asc, score desc, slot) with a bitonic network, then the
+// greedy pass walks the sorted list: a suppressed entry costs nothing, a kept
+// entry costs one parallel IoU sweep over the rest of its class segment and
+// one barrier.
+constexpr int NMS_THREADS = 1024;
+
+__global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const NmsParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
+  if (b >= n_img) return;
+  const int tid = threadIdx.x;
+  int n = p.cand_count[b];
+  n = n < p.cand_cap ? n : p.cand_cap;
+  int P = 2;
+  while (P < n) P <<= 1;
+  unsigned long long* keys = (unsigned long long*)smem;
+  unsigned char* removed = smem + sizeof(unsigned long long) * P;
+  const Candidate* cand = p.cand + (size_t)b * p.cand_cap;
+
+  for (int i = tid; i < P; i += NMS_THREADS) {
+    unsigned long long k = ~0ull;
+    if (i < n) {
+      const Candidate c = cand[i];
+      const unsigned bits = __float_as_uint(c.score);
+      k = ((unsigned long long)(unsigned)c.cls << 44) |
+          ((unsigned long long)(0x3F800000u - bits) << 14) | (unsigned long long)i;
+      removed[i] = 0;
+    }
+    keys[i] = k;
+  }
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += NMS_THREADS) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = keys[i], c = keys[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > c) == up) { keys[i] = c; keys[ixj] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  const ImageMeta m = p.meta[b];
+  const float inv = 1.0f / m.scale;
+  int kept = 0;
+  for (int i = 0; i < n; ++i) {
+    if (removed[i]) continue;  // block-uniform: written before the last barrier
+    const unsigned long long ki = keys[i];
+    const int ci = (int)(ki >> 44);
+    const Candidate bi = cand[ki & 0x3FFF];
+    if (tid == 0 && kept < p.max_det) {
+      Detection d;
+      d.x1 = fminf(fmaxf((bi.x1 - (float)m.pad_w) * inv, 0.f), (float)m.w);
+      d.y1 = fminf(fmaxf((bi.y1 - (float)m.pad_h) * inv, 0.f), (float)m.h);
+      d.x2 = fminf(fmaxf((bi.x2 - (float)m.pad_w) * inv, 0.f), (float)m.w);
+      d.y2 = fminf(fmaxf((bi.y2 - (float)m.pad_h) * inv, 0.f), (float)m.h);
+      d.conf = bi.score;
+      d.cls = bi.cls;
+      d.pad_[0] = d.pad_[1] = 0.f;
+      p.det[(size_t)b * p.max_det + kept] = d;
+    }
+    ++kept;
+    const float area_i = (bi.x2 - bi.x1) * (bi.y2 - bi.y1);
+    for (int j = i + 1 + tid; j < n; j += NMS_THREADS) {
+      const unsigned long long kj = keys[j];
+      if ((int)(kj >> 44) != ci) break;
+      if (removed[j]) continue;
+      const Candidate bj = cand[kj & 0x3FFF];
+      const float xx1 = fmaxf(bi.x1, bj.x1), yy1 = fmaxf(bi.y1, bj.y1);
+      const float xx2 = fminf(bi.x2, bj.x2), yy2 = fminf(bi.y2, bj.y2);
+      const float inter = fmaxf(0.f, xx2 - xx1) * fmaxf(0.f, yy2 - yy1);
+      const float area_j = (bj.x2 - bj.x1) * (bj.y2 - bj.y1);
+      const float iou = inter / (area_i + area_j - inter + 1e-6f);
+      if (iou > p.iou_thr) removed[j] = 1;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) p.det_count[b] = kept;
+}
+
+void prepare_kernels() {
+  static bool done = false;
+  if (done) return;
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+  done = true;
+}
+
+void nms(const NmsParams& p, hipStream_t s) {
+  if (p.cand_cap > 16384) throw std::runtime_error("nms: cand_cap > 16384");
+  int P = 2;
+  while (P < p.cand_cap) P <<= 1;
+  const size_t lds = (size_t)P * 9;
+  if (lds > 160 * 1024) throw std::runtime_error("nms: LDS budget exceeded");
+  if (p.B <= 0) return;
+  hipLaunchKernelGGL(nms_kernel, dim3(p.B), dim3(NMS_THREADS), lds, s, p);
+}
+
+// ------------------------------------------------------------------ crop plan
+__global__ __launch_bounds__(256) void crop_plan_kernel(const CropPlanParams p) {
+  __shared__ int offs[1024 + 1];
+  const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int acc = 0;
+    for (int b = 0; b < n_img; ++b) {
+      offs[b] = acc;
+      int k = p.det_count[b];
+      acc += k < p.max_det ? k : p.max_det;
+    }
+    offs[n_img] = acc;
+    Ctrl* c = p.ctrl;
+    c->total_crops = acc;
+    int rem = acc - c->crop_base;
+    rem = rem < 0 ? 0 : rem;
+    c->n_crops = rem < p.crop_cap ? rem : p.crop_cap;
+  }
+  __syncthreads();
+  for (int b = 0; b < n_img; ++b) {
+    const int k = offs[b + 1] - offs[b];
+    const ImageMeta m = p.meta[b];
+    for (int d = tid; d < k; d += blockDim.x) {
+      const Detection det = p.det[(size_t)b * p.max_det + d];
+      CropRef r;
+      r.img = b;
+      r.x1 = max(0, (int)det.x1);
+      r.y1 = max(0, (int)det.y1);
+      r.x2 = min(m.w, (int)det.x2);
+      r.y2 = min(m.h, (int)det.y2);
+      r.det = d;
+      r.pad_[0] = r.pad_[1] = 0;
+      p.crops[offs[b] + d] = r;
+    }
+  }
+}
+
+void crop_plan(const CropPlanParams& p, hipStream_t s) {
+  if (p.B > 1024) throw std::runtime_error("crop_plan: batch > 1024");
+  hipLaunchKernelGGL(crop_plan_kernel, dim3(1), dim3(256), 0, s, p);
+}
+
+}  // namespace arena

@@ -1,0 +1,199 @@
+// Host-side launch API for every HIP kernel of the arena (gfx950 only).
+//
+// Each launcher takes a plain parameter struct (device pointers + sizes) and a
+// hipStream_t, and only enqueues work: no allocation, no synchronisation, so
+// every launcher can be captured into a hipGraph by the executor
+// (csrc/runtime/executor.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+namespace arena {
+
+// ---------------------------------------------------------------- conv (K2/K3/K4/K6/K10/K11/K13)
+// Implicit-GEMM NHWC convolution on MFMA (v_mfma_f32_16x16x32_bf16) with a
+// fused epilogue: + bias, activation, + residual, store into a channel slice
+// of a concat buffer, optional second store nearest-upsampled x2 (FPN).
+struct ConvParams {
+  const void* x;  // bf16 input, already offset to its channel slice
+  int B, H, W;    // batch capacity and input spatial dims
+  int xs;         // input pixel stride (elements)
+  int Cin;        // input channels (multiple of 8)
+  const void* w;  // bf16 weights [Cout_pad][Kpad], k = (kh*KW+kw)*Cin + ci
+  int Kpad;       // multiple of 32
+  const float* bias;  // fp32 [Cout_pad]
+  void* y;            // output (bf16, or fp32 if f32out)
+  int Ho, Wo, ys;     // output spatial dims and pixel stride (elements)
+  int Cout;           // channels actually stored (multiple of 4)
+  int Cout_pad;       // rows of w / bias (multiple of 16)
+  int KH, KW, stride, pad_t, pad_l;
+  const void* res;  // optional bf16 residual (same geometry as y), pixel stride rs
+  int rs;
+  void* y2;  // optional bf16 second output, 2x nearest upsampled, pixel stride y2s
+  int y2s;
+  int act;      // Act
+  int f32out;   // store fp32 instead of bf16
+  const int* bdev;  // optional live batch count on device
+};
+void conv2d(const ConvParams& p, hipStream_t s);
+
+// ---------------------------------------------------------------- depthwise 3x3 (K12)
+struct DwParams {
+  const void* x;
+  int B, H, W, xs, C;
+  const void* w;  // bf16 [9][C]
+  const float* bias;
+  void* y;
+  int Ho, Wo, ys, stride, act;
+  const int* bdev;
+};
+void dwconv3x3(const DwParams& p, hipStream_t s);
+
+// ---------------------------------------------------------------- SPPF pools (K5)
+// x: [B,H,W] channels [0,C) of a buffer with pixel stride xs; writes the
+// cascaded 5x5 max pools (== 5/9/13 windows) into channel slices C, 2C, 3C.
+struct SppfParams {
+  void* buf;
+  int B, H, W, xs, C;
+  const int* bdev;
+};
+void sppf_pool(const SppfParams& p, hipStream_t s);
+
+// ---------------------------------------------------------------- image metadata
+// Per-image record produced on the host for a batch (lives in device memory).
+struct ImageMeta {
+  int64_t offset;  // byte offset of the RGB uint8 HWC image in the image pool
+  int h, w;        // original size
+  int new_w, new_h;
+  int pad_w, pad_h;
+  float scale;     // letterbox scale
+  float pad_[3];
+};
+static_assert(sizeof(ImageMeta) == 48, "ImageMeta layout");
+
+// Control block shared by the pipeline kernels of one batch.
+struct Ctrl {
+  int n_images;    // live images (host-written)
+  int n_crops;     // crops to classify in this pass (device-written)
+  int crop_base;   // first crop of this pass (host-written for overflow passes)
+  int total_crops; // all crops of the batch (device-written)
+  int pad_[12];
+};
+
+// ---------------------------------------------------------------- letterbox (K1)
+// Bilinear (cv2 INTER_LINEAR geometry) resize + pad(114) + /255 and
+// space-to-depth(2): out [B, T/2, T/2, 16] bf16, channel (p*2+q)*3+c, 12..15 = 0.
+struct LetterboxParams {
+  const uint8_t* pool;
+  const ImageMeta* meta;
+  const Ctrl* ctrl;
+  void* out;
+  int B, T;
+};
+void letterbox_s2d(const LetterboxParams& p, hipStream_t s);
+
+// ---------------------------------------------------------------- detect decode (K7)
+struct Candidate {
+  float x1, y1, x2, y2;  // letterbox coordinates
+  float score;
+  int cls;
+  int anchor;
+  int pad_;
+};
+struct DecodeParams {
+  // Per level l: head output [B, H_l, W_l] with 144 channels (64 DFL box + 80 cls), stride xs_l
+  const void* head[3];
+  int hw[3];      // H_l (== W_l)
+  int xs[3];
+  float stride[3];
+  int B;
+  float conf_thr;
+  Candidate* cand;  // [B][cand_cap]
+  int* cand_count;  // [B]
+  int cand_cap;
+  const Ctrl* ctrl;
+};
+void detect_decode(const DecodeParams& p, hipStream_t s);
+
+// ---------------------------------------------------------------- NMS (K8)
+struct Detection {
+  float x1, y1, x2, y2;  // original-image coordinates, clipped
+  float conf;
+  int cls;
+  float pad_[2];
+};
+struct NmsParams {
+  const Candidate* cand;
+  const int* cand_count;
+  int cand_cap;
+  const ImageMeta* meta;
+  int B;
+  float iou_thr;
+  Detection* det;  // [B][max_det]
+  int* det_count;  // [B] (kept, possibly > max_det)
+  int max_det;
+  const Ctrl* ctrl;
+};
+void nms(const NmsParams& p, hipStream_t s);
+
+// One-time kernel attribute setup (dynamic LDS > 64 KiB for NMS).  Must run
+// before any hipGraph capture that contains the kernels.
+void prepare_kernels();
+
+// ---------------------------------------------------------------- crop plan + gather (K9)
+struct CropRef {
+  int img;
+  int x1, y1, x2, y2;  // int-truncated, clamped; x2<=x1 or y2<=y1 => 1x1 black crop
+  int det;             // index into the image's detections
+  int pad_[2];
+};
+struct CropPlanParams {
+  const Detection* det;
+  const int* det_count;
+  int max_det;
+  const ImageMeta* meta;
+  int B;
+  CropRef* crops;  // [B*max_det]
+  Ctrl* ctrl;
+  int crop_cap;    // crops one classification pass can hold
+};
+void crop_plan(const CropPlanParams& p, hipStream_t s);
+
+struct CropGatherParams {
+  const uint8_t* pool;
+  const ImageMeta* meta;
+  const CropRef* crops;
+  const Ctrl* ctrl;
+  void* out;  // [cap, S/2, S/2, 16] bf16 (space-to-depth, ImageNet-normalised)
+  int cap, S;
+  float mean[3], inv_std[3];
+};
+void crop_gather_s2d(const CropGatherParams& p, hipStream_t s);
+
+// ---------------------------------------------------------------- classification head (K13/K14)
+struct AvgPoolParams {
+  const void* x;
+  int B, HW, C;
+  void* y;  // bf16 [B][C]
+  const int* bdev;
+};
+void global_avgpool(const AvgPoolParams& p, hipStream_t s);
+
+struct TopkResult {
+  int idx[5];
+  float logit[5];
+  float prob[5];
+  int pad_;
+};
+struct TopkParams {
+  const float* logits;  // [B][ld]
+  int B, N, ld;
+  TopkResult* out;       // written at out[ctrl->crop_base + i] when ctrl != null
+  const Ctrl* ctrl;
+  const int* bdev;
+};
+void topk_softmax(const TopkParams& p, hipStream_t s);
+
+}  // namespace arena

@@ -1,0 +1,134 @@
+// Device-side preprocessing: letterbox for the detector (K1) and the
+// crop-gather + resize + ImageNet normalisation for the classifier (K9).
+//
+// Reference semantics reproduced here:
+//   letterbox: src/shared/processing/transforms.py:118-180 (scale =
+//     min(T/h, T/w), new size int-truncated, floor-centred pad, gray 114,
+//     cv2 INTER_LINEAR) followed by /255 and HWC->CHW in
+//     src/shared/processing/yolo_preprocess.py:154-167.
+//   crop: src/shared/processing/mobilenet_preprocess.py:236-269 (int()
+//     truncation, clamp, zero-area -> 1x1 black) and :134-160 (direct 224x224
+//     INTER_LINEAR resize, (x/255-mean)/std).
+// INTER_LINEAR geometry: src = (dst + 0.5) * (src_size / dst_size) - 0.5,
+// clamped to the border; the interpolated uint8 value is rounded before
+// normalisation, as cv2 returns a uint8 image.
+//
+// Both kernels emit space-to-depth(2) layouts so that the stride-2 stem convs
+// become dense stride-1 convs with 16 (12 live) input channels: YOLO's 6x6/s2
+// stem becomes a 3x3/s1 conv, MobileNet's 3x3/s2 stem a 2x2/s1 conv.
+#include "common.h"
+#include "launch.h"
+
+namespace arena {
+
+struct LinTap {
+  int i0, i1;
+  float f;
+};
+
+__device__ __forceinline__ LinTap lin_tap(int d, float scale, int n) {
+  float fx = ((float)d + 0.5f) * scale - 0.5f;
+  int s0 = (int)floorf(fx);
+  float f = fx - (float)s0;
+  if (s0 < 0) { s0 = 0; f = 0.f; }
+  if (s0 >= n - 1) { s0 = n - 1; f = 0.f; }
+  LinTap t;
+  t.i0 = s0;
+  t.i1 = s0 + 1 < n ? s0 + 1 : n - 1;
+  t.f = f;
+  return t;
+}
+
+__device__ __forceinline__ void bilinear_rgb(const uint8_t* img, int stride_px, LinTap ty, LinTap tx,
+                                             float* rgb) {
+  const uint8_t* r0 = img + (size_t)ty.i0 * stride_px * 3;
+  const uint8_t* r1 = img + (size_t)ty.i1 * stride_px * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float a = (float)r0[tx.i0 * 3 + c], b = (float)r0[tx.i1 * 3 + c];
+    const float d = (float)r1[tx.i0 * 3 + c], e = (float)r1[tx.i1 * 3 + c];
+    const float top = a + (b - a) * tx.f;
+    const float bot = d + (e - d) * tx.f;
+    float v = top + (bot - top) * ty.f;
+    rgb[c] = floorf(v + 0.5f);  // cv2 returns uint8: round to nearest
+  }
+}
+
+__global__ __launch_bounds__(256) void letterbox_s2d_kernel(const LetterboxParams p) {
+  const int T2 = p.T >> 1;
+  const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
+  const long total = (long)n_img * T2 * T2;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int X = (int)(tid % T2);
+  const int Y = (int)((tid / T2) % T2);
+  const int b = (int)(tid / ((long)T2 * T2));
+  const ImageMeta m = p.meta[b];
+  const uint8_t* img = p.pool + m.offset;
+  const float sy = (float)((double)m.h / (double)m.new_h);
+  const float sx = (float)((double)m.w / (double)m.new_w);
+  float out[16];
+#pragma unroll
+  for (int pq = 0; pq < 4; ++pq) {
+    const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
+    const int dy = oy - m.pad_h, dx = ox - m.pad_w;
+    float rgb[3] = {114.f, 114.f, 114.f};
+    if (dy >= 0 && dy < m.new_h && dx >= 0 && dx < m.new_w)
+      bilinear_rgb(img, m.w, lin_tap(dy, sy, m.h), lin_tap(dx, sx, m.w), rgb);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = rgb[c] * (1.0f / 255.0f);
+  }
+  out[12] = out[13] = out[14] = out[15] = 0.f;
+  uint4* dst = (uint4*)((bf16*)p.out + (size_t)tid * 16);
+  dst[0] = pack8(out);
+  dst[1] = pack8(out + 8);
+}
+
+void letterbox_s2d(const LetterboxParams& p, hipStream_t s) {
+  if (p.T % 2 != 0) throw std::runtime_error("letterbox_s2d: T must be even");
+  const long total = (long)p.B * (p.T / 2) * (p.T / 2);
+  if (total <= 0) return;
+  hipLaunchKernelGGL(letterbox_s2d_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+}
+
+__global__ __launch_bounds__(256) void crop_gather_s2d_kernel(const CropGatherParams p) {
+  const int S2 = p.S >> 1;
+  int n = p.cap;
+  if (p.ctrl != nullptr) n = live_batch(p.cap, &p.ctrl->n_crops);
+  const long total = (long)n * S2 * S2;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int X = (int)(tid % S2);
+  const int Y = (int)((tid / S2) % S2);
+  const int i = (int)(tid / ((long)S2 * S2));
+  const int base = p.ctrl != nullptr ? p.ctrl->crop_base : 0;
+  const CropRef cr = p.crops[base + i];
+  const ImageMeta m = p.meta[cr.img];
+  const int cw = cr.x2 - cr.x1, ch = cr.y2 - cr.y1;
+  float out[16];
+  const bool empty = cw <= 0 || ch <= 0;
+  const float sx = empty ? 1.f : (float)((double)cw / (double)p.S);
+  const float sy = empty ? 1.f : (float)((double)ch / (double)p.S);
+  const uint8_t* img = p.pool + m.offset + ((size_t)cr.y1 * m.w + cr.x1) * 3;
+#pragma unroll
+  for (int pq = 0; pq < 4; ++pq) {
+    const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
+    float rgb[3] = {0.f, 0.f, 0.f};
+    if (!empty) bilinear_rgb(img, m.w, lin_tap(oy, sy, ch), lin_tap(ox, sx, cw), rgb);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (rgb[c] * (1.0f / 255.0f) - p.mean[c]) * p.inv_std[c];
+  }
+  out[12] = out[13] = out[14] = out[15] = 0.f;
+  uint4* dst = (uint4*)((bf16*)p.out + (size_t)tid * 16);
+  dst[0] = pack8(out);
+  dst[1] = pack8(out + 8);
+}
+
+void crop_gather_s2d(const CropGatherParams& p, hipStream_t s) {
+  if (p.S % 2 != 0) throw std::runtime_error("crop_gather_s2d: S must be even");
+  const long total = (long)p.cap * (p.S / 2) * (p.S / 2);
+  if (total <= 0) return;
+  hipLaunchKernelGGL(crop_gather_s2d_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+}
+
+}  // namespace arena

@@ -1,0 +1,185 @@
+// Native dynamic batcher; see batcher.h.
+#include "batcher.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace arena {
+
+using clk = std::chrono::steady_clock;
+
+DynamicBatcher::DynamicBatcher(std::vector<std::shared_ptr<Executor>> instances, const BatcherConfig& cfg)
+    : inst_(std::move(instances)), cfg_(cfg) {
+  if (inst_.empty()) throw std::runtime_error("DynamicBatcher: no executor instances");
+  int largest = 0;
+  for (auto& e : inst_) {
+    auto b = e->buckets();
+    if (b.empty()) throw std::runtime_error("DynamicBatcher: executor has no buckets");
+    largest = largest == 0 ? b.back() : std::min(largest, b.back());
+  }
+  cfg_.max_batch = std::max(1, std::min(cfg_.max_batch, largest));
+  std::sort(cfg_.preferred.begin(), cfg_.preferred.end());
+  cfg_.preferred.erase(std::remove_if(cfg_.preferred.begin(), cfg_.preferred.end(),
+                                      [&](int v) { return v <= 0 || v > cfg_.max_batch; }),
+                       cfg_.preferred.end());
+  stats_.batch_hist.assign(cfg_.max_batch + 1, 0);
+  for (size_t i = 0; i < inst_.size(); ++i) threads_.emplace_back([this, i]() { instance_loop((int)i); });
+}
+
+DynamicBatcher::~DynamicBatcher() { shutdown(); }
+
+void DynamicBatcher::shutdown() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (stop_ && threads_.empty()) return;
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+}
+
+int64_t DynamicBatcher::enqueue(const uint8_t* rgb, int h, int w, ResultCallback cb) {
+  auto r = std::make_unique<Request>();
+  r->pixels.assign(rgb, rgb + (size_t)h * w * 3);
+  r->h = h;
+  r->w = w;
+  r->cb = std::move(cb);
+  r->t_enq = clk::now();
+  int64_t id;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (stop_) return -1;
+    if (cfg_.max_queue_size > 0 && (int64_t)q_.size() >= cfg_.max_queue_size) {
+      ++stats_.rejected;
+      return -1;
+    }
+    id = next_id_++;
+    r->id = id;
+    q_.push_back(std::move(r));
+    stats_.queue_depth = (int64_t)q_.size();
+  }
+  cv_.notify_one();
+  return id;
+}
+
+bool DynamicBatcher::take_batch(Batch& out, bool can_wait) {
+  std::unique_lock<std::mutex> lk(mu_);
+  const auto delay = std::chrono::microseconds(cfg_.max_queue_delay_us);
+  for (;;) {
+    if (q_.empty()) {
+      if (stop_ || !can_wait) return false;
+      cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      continue;
+    }
+    const int n = (int)q_.size();
+    int take = 0;
+    if (n >= cfg_.max_batch) {
+      take = cfg_.max_batch;
+    } else if (!cfg_.preferred.empty() && n >= cfg_.preferred.back()) {
+      take = cfg_.preferred.back();
+    } else if (stop_ || clk::now() - q_.front()->t_enq >= delay) {
+      take = n;  // delay expired: run what is queued
+    }
+    if (take > 0) {
+      for (int i = 0; i < take; ++i) {
+        out.push_back(std::move(q_.front()));
+        q_.pop_front();
+      }
+      stats_.queue_depth = (int64_t)q_.size();
+      return true;
+    }
+    if (!can_wait) return false;
+    cv_.wait_until(lk, q_.front()->t_enq + delay);
+  }
+}
+
+void DynamicBatcher::finish(Batch& batch, const BatchResult& r, clk::time_point t_submit) {
+  const auto t_done = clk::now();
+  const int max_det = (int)(r.det.size() / std::max<size_t>(1, batch.size()));
+  const double compute_us = std::chrono::duration<double, std::micro>(t_done - t_submit).count();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.batches += 1;
+    stats_.requests += (int64_t)batch.size();
+    stats_.sum_batch += (double)batch.size();
+    stats_.sum_compute_us += compute_us;
+    if ((int)batch.size() < (int)stats_.batch_hist.size()) stats_.batch_hist[batch.size()] += 1;
+    for (auto& rq : batch)
+      stats_.sum_queue_us += std::chrono::duration<double, std::micro>(t_submit - rq->t_enq).count();
+  }
+  for (size_t i = 0; i < batch.size(); ++i) {
+    RequestResult rr;
+    rr.id = batch[i]->id;
+    rr.det_count = r.det_count[i];
+    const int kept = std::min(rr.det_count, max_det);
+    rr.det.assign(r.det.begin() + (size_t)i * max_det, r.det.begin() + (size_t)i * max_det + kept);
+    rr.topk.assign(r.topk.begin() + r.crop_offset[i], r.topk.begin() + r.crop_offset[i + 1]);
+    rr.batch_size = (int)batch.size();
+    rr.queue_us = std::chrono::duration<double, std::micro>(t_submit - batch[i]->t_enq).count();
+    rr.compute_us = compute_us;
+    batch[i]->cb(std::move(rr));
+  }
+}
+
+void DynamicBatcher::fail(Batch& batch, const std::string& err) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stats_.failed += (int64_t)batch.size();
+  }
+  for (auto& rq : batch) {
+    RequestResult rr;
+    rr.id = rq->id;
+    rr.error = err;
+    rq->cb(std::move(rr));
+  }
+}
+
+void DynamicBatcher::instance_loop(int idx) {
+  Executor& ex = *inst_[idx];
+  struct InFlight {
+    int slot;
+    Batch batch;
+    clk::time_point t_submit;
+  };
+  std::deque<InFlight> pending;
+  for (;;) {
+    if (pending.size() < 2) {
+      Batch b;
+      if (take_batch(b, pending.empty())) {
+        std::vector<InputImage> imgs;
+        imgs.reserve(b.size());
+        for (auto& rq : b) imgs.push_back(InputImage{rq->pixels.data(), rq->h, rq->w});
+        try {
+          const auto t = clk::now();
+          const int slot = ex.submit(imgs);
+          pending.push_back(InFlight{slot, std::move(b), t});
+        } catch (const std::exception& e) {
+          fail(b, e.what());
+        }
+        continue;
+      }
+      if (pending.empty()) {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (stop_ && q_.empty()) return;
+        continue;
+      }
+    }
+    InFlight f = std::move(pending.front());
+    pending.pop_front();
+    try {
+      BatchResult r = ex.collect(f.slot);
+      finish(f.batch, r, f.t_submit);
+    } catch (const std::exception& e) {
+      fail(f.batch, e.what());
+    }
+  }
+}
+
+BatcherStats DynamicBatcher::stats() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return stats_;
+}
+
+}  // namespace arena

@@ -1,0 +1,97 @@
+// Native dynamic batcher (the scheduler half of the Triton replacement).
+//
+// The reference's Triton deployment runs the default scheduler with
+// `max_batch_size: 0` (infrastructure/minio/triton_config.py:98-128), i.e. no
+// batching, one request per ONNX Runtime call.  This batcher implements the
+// `dynamic_batching { preferred_batch_size, max_queue_delay_microseconds }`
+// semantics of a model-repository config.pbtxt on top of Executor instances
+// (one per `instance_group` count on the GPU):
+//
+//   * requests wait in one FIFO shared by all instances of the model;
+//   * an idle instance takes a batch as soon as the queue holds max_batch
+//     requests, or a preferred size is available and no larger one can form,
+//     or the oldest request has waited max_queue_delay;
+//   * each instance keeps two batches in flight (the executor's two staging
+//     slots), so packing/H2D of batch i+1 overlaps the graph of batch i;
+//   * completion callbacks run on the instance thread.
+#pragma once
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "executor.h"
+
+namespace arena {
+
+struct RequestResult {
+  int64_t id = 0;
+  int det_count = 0;
+  std::vector<Detection> det;    // min(det_count, max_det) rows
+  std::vector<TopkResult> topk;  // one per kept detection
+  int batch_size = 0;
+  double queue_us = 0, compute_us = 0;
+  std::string error;
+};
+
+using ResultCallback = std::function<void(RequestResult&&)>;
+
+struct BatcherConfig {
+  int max_batch = 32;
+  std::vector<int> preferred;          // preferred batch sizes (ascending)
+  int64_t max_queue_delay_us = 500;
+  int64_t max_queue_size = 4096;       // 0 = unbounded
+};
+
+struct BatcherStats {
+  int64_t requests = 0, batches = 0, rejected = 0, failed = 0;
+  int64_t queue_depth = 0;
+  double sum_batch = 0;
+  double sum_queue_us = 0, sum_compute_us = 0;
+  std::vector<int64_t> batch_hist;  // index = batch size
+};
+
+class DynamicBatcher {
+ public:
+  DynamicBatcher(std::vector<std::shared_ptr<Executor>> instances, const BatcherConfig& cfg);
+  ~DynamicBatcher();
+  DynamicBatcher(const DynamicBatcher&) = delete;
+  DynamicBatcher& operator=(const DynamicBatcher&) = delete;
+
+  // Copies the image; returns the request id, or -1 when the queue is full.
+  int64_t enqueue(const uint8_t* rgb, int h, int w, ResultCallback cb);
+  BatcherStats stats();
+  void shutdown();
+
+ private:
+  struct Request {
+    int64_t id;
+    std::vector<uint8_t> pixels;
+    int h, w;
+    ResultCallback cb;
+    std::chrono::steady_clock::time_point t_enq;
+  };
+  using Batch = std::vector<std::unique_ptr<Request>>;
+
+  void instance_loop(int idx);
+  bool take_batch(Batch& out, bool can_wait);
+  void finish(Batch& batch, const BatchResult& r, std::chrono::steady_clock::time_point t_submit);
+  void fail(Batch& batch, const std::string& err);
+
+  std::vector<std::shared_ptr<Executor>> inst_;
+  BatcherConfig cfg_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::unique_ptr<Request>> q_;
+  bool stop_ = false;
+  int64_t next_id_ = 1;
+  BatcherStats stats_;
+  std::vector<std::thread> threads_;
+};
+
+}  // namespace arena

@@ -1,0 +1,537 @@
+// Native pipeline executor: static op program -> per-bucket hipGraphs.
+// See executor.h for the design; the op record layouts are documented in
+// inference_arena_amd/engine/planner.py (the only producer of programs).
+#include "executor.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../kernels/common.h"
+
+namespace arena {
+
+namespace {
+float bits_to_float(int64_t v) {
+  uint32_t u = (uint32_t)v;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+constexpr size_t kCtrlBytes = 256;
+}  // namespace
+
+Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
+  if (cfg_.max_batch <= 0 || cfg_.max_batch > 1024) throw std::runtime_error("Executor: max_batch out of range");
+  if (cfg_.cand_cap > 16384) throw std::runtime_error("Executor: cand_cap > 16384");
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  prepare_kernels();
+  ARENA_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+  ARENA_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  max_B_ = cfg_.max_batch;
+  alloc_slots();
+  const int nthreads = std::max(1, cfg_.host_threads);
+  for (int t = 0; t < nthreads; ++t) {
+    workers_.emplace_back([this]() {
+      uint64_t seen = 0;
+      for (;;) {
+        std::vector<std::function<void()>>* jobs;
+        {
+          std::unique_lock<std::mutex> lk(pool_mu_);
+          pool_cv_.wait(lk, [&] { return pool_stop_ || pool_gen_ != seen; });
+          if (pool_stop_) return;
+          seen = pool_gen_;
+          jobs = pool_jobs_;
+        }
+        for (;;) {
+          const int i = pool_next_.fetch_add(1);
+          if (jobs == nullptr || i >= (int)jobs->size()) break;
+          (*jobs)[i]();
+          std::lock_guard<std::mutex> lk(pool_mu_);
+          if (--pool_pending_ == 0) pool_done_cv_.notify_all();
+        }
+      }
+    });
+  }
+}
+
+Executor::~Executor() {
+  {
+    std::lock_guard<std::mutex> lk(pool_mu_);
+    pool_stop_ = true;
+  }
+  pool_cv_.notify_all();
+  for (auto& t : workers_) t.join();
+  hipSetDevice(cfg_.device);
+  if (compute_) hipStreamSynchronize(compute_);
+  if (copy_) hipStreamSynchronize(copy_);
+  for (auto& kv : buckets_) {
+    for (int s = 0; s < 2; ++s)
+      if (kv.second.graph[s]) hipGraphExecDestroy(kv.second.graph[s]);
+    if (kv.second.d_arena) hipFree(kv.second.d_arena);
+  }
+  for (auto& sl : slots_) {
+    if (sl.d_in) hipFree(sl.d_in);
+    if (sl.d_out) hipFree(sl.d_out);
+    if (sl.h_in) hipHostFree(sl.h_in);
+    if (sl.h_out) hipHostFree(sl.h_out);
+    if (sl.copied) hipEventDestroy(sl.copied);
+    if (sl.started) hipEventDestroy(sl.started);
+    if (sl.done) hipEventDestroy(sl.done);
+  }
+  if (d_weights_) hipFree(d_weights_);
+  if (compute_) hipStreamDestroy(compute_);
+  if (copy_) hipStreamDestroy(copy_);
+}
+
+// ---------------------------------------------------------------- layout
+size_t Executor::in_bytes_meta() const {
+  return kCtrlBytes + align_up(sizeof(ImageMeta) * (size_t)max_B_, 256);
+}
+size_t Executor::in_bytes_total() const {
+  return in_bytes_meta() + align_up((size_t)cfg_.pool_bytes_per_image * max_B_, 256);
+}
+size_t Executor::out_off_det() const { return align_up(sizeof(int) * (size_t)max_B_, 256); }
+size_t Executor::out_off_topk() const {
+  return out_off_det() + align_up(sizeof(Detection) * (size_t)max_B_ * cfg_.max_det, 256);
+}
+size_t Executor::out_bytes_total() const {
+  return out_off_topk() + sizeof(TopkResult) * (size_t)max_B_ * cfg_.max_det;
+}
+
+void Executor::alloc_slots() {
+  for (auto& sl : slots_) {
+    ARENA_HIP_CHECK(hipMalloc(&sl.d_in, in_bytes_total()));
+    ARENA_HIP_CHECK(hipMalloc(&sl.d_out, out_bytes_total()));
+    ARENA_HIP_CHECK(hipHostMalloc(&sl.h_in, in_bytes_total(), hipHostMallocDefault));
+    ARENA_HIP_CHECK(hipHostMalloc(&sl.h_out, out_bytes_total(), hipHostMallocDefault));
+    ARENA_HIP_CHECK(hipMemset(sl.d_in, 0, in_bytes_total()));
+    ARENA_HIP_CHECK(hipMemset(sl.d_out, 0, out_bytes_total()));
+    std::memset(sl.h_in, 0, in_bytes_meta());
+    ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
+    ARENA_HIP_CHECK(hipEventCreate(&sl.started));
+    ARENA_HIP_CHECK(hipEventCreate(&sl.done));
+  }
+}
+
+void Executor::set_weights(const void* host, size_t bytes) {
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  if (d_weights_) ARENA_HIP_CHECK(hipFree(d_weights_));
+  ARENA_HIP_CHECK(hipMalloc(&d_weights_, bytes));
+  ARENA_HIP_CHECK(hipMemcpy(d_weights_, host, bytes, hipMemcpyHostToDevice));
+  weights_bytes_ = bytes;
+}
+
+void Executor::set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops, int n_cls_ops) {
+  prog_.resize(n_ops);
+  for (int i = 0; i < n_ops; ++i) std::memcpy(prog_[i].data(), ops + (size_t)i * kOpFields, sizeof(OpRecord));
+  cls_prog_.resize(n_cls_ops);
+  for (int i = 0; i < n_cls_ops; ++i)
+    std::memcpy(cls_prog_[i].data(), cls_ops + (size_t)i * kOpFields, sizeof(OpRecord));
+}
+
+int Executor::crop_cap_for(int B) const { return std::max(cfg_.min_crop_cap, B * cfg_.crop_cap_per_image); }
+
+std::vector<int> Executor::buckets() const {
+  std::vector<int> r;
+  for (auto& kv : buckets_) r.push_back(kv.first);
+  return r;
+}
+
+uintptr_t Executor::arena_ptr(int B) const {
+  auto it = buckets_.find(B);
+  return it == buckets_.end() ? 0 : (uintptr_t)it->second.d_arena;
+}
+
+void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes) {
+  if (B <= 0 || B > max_B_) throw std::runtime_error("add_bucket: B outside (0, max_batch]");
+  if (prog_.empty()) throw std::runtime_error("add_bucket: set_program first");
+  if (d_weights_ == nullptr) throw std::runtime_error("add_bucket: set_weights first");
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  Bucket& bk = buckets_[B];
+  bk.info.B = B;
+  bk.info.crop_cap = crop_cap_for(B);
+  bk.info.offsets.assign(offsets, offsets + n_buffers);
+  bk.info.arena_bytes = arena_bytes;
+  if (bk.d_arena) ARENA_HIP_CHECK(hipFree(bk.d_arena));
+  ARENA_HIP_CHECK(hipMalloc(&bk.d_arena, std::max<int64_t>(arena_bytes, 256)));
+  ARENA_HIP_CHECK(hipMemset(bk.d_arena, 0, std::max<int64_t>(arena_bytes, 256)));
+  for (int s = 0; s < 2; ++s) capture(bk, s);
+}
+
+void Executor::capture(Bucket& bk, int s) {
+  Slot& sl = slots_[s];
+  // Validate the program eagerly once (launch errors surface here, not in the graph).
+  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+  hipGraph_t g = nullptr;
+  ARENA_HIP_CHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
+  try {
+    enqueue_program(prog_, bk, sl, compute_);
+    const size_t d2h = out_off_topk() + sizeof(TopkResult) * (size_t)bk.info.crop_cap;
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+  } catch (...) {
+    hipStreamEndCapture(compute_, &g);
+    if (g) hipGraphDestroy(g);
+    throw;
+  }
+  ARENA_HIP_CHECK(hipStreamEndCapture(compute_, &g));
+  if (bk.graph[s]) ARENA_HIP_CHECK(hipGraphExecDestroy(bk.graph[s]));
+  ARENA_HIP_CHECK(hipGraphInstantiate(&bk.graph[s], g, nullptr, nullptr, 0));
+  ARENA_HIP_CHECK(hipGraphDestroy(g));
+}
+
+uint8_t* Executor::resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff, int eb) {
+  uint8_t* base = nullptr;
+  switch (buf) {
+    case BUF_NONE: return nullptr;
+    case BUF_CTRL: base = sl.d_in; break;
+    case BUF_META: base = sl.d_in + kCtrlBytes; break;
+    case BUF_POOL: base = sl.d_in + in_bytes_meta(); break;
+    case BUF_DETCOUNT: base = sl.d_out; break;
+    case BUF_DET: base = sl.d_out + out_off_det(); break;
+    case BUF_TOPK: base = sl.d_out + out_off_topk(); break;
+    default:
+      if (buf < 0 || buf >= (int64_t)bk.info.offsets.size())
+        throw std::runtime_error("program references unknown buffer " + std::to_string(buf));
+      base = bk.d_arena + bk.info.offsets[buf];
+  }
+  return base + coff * eb;
+}
+
+void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s) {
+  Ctrl* ctrl = (Ctrl*)resolve(bk, sl, BUF_CTRL, 0, 1);
+  const ImageMeta* meta = (const ImageMeta*)resolve(bk, sl, BUF_META, 0, 1);
+  const uint8_t* pool = resolve(bk, sl, BUF_POOL, 0, 1);
+  const int B = bk.info.B, CC = bk.info.crop_cap;
+  auto batch = [&](int64_t kind) { return kind == BATCH_CROPS ? CC : B; };
+  auto bdev = [&](int64_t kind) -> const int* { return kind == BATCH_CROPS ? &ctrl->n_crops : &ctrl->n_images; };
+  const uint8_t* W = d_weights_;
+
+  for (const OpRecord& r : prog) {
+    switch (r[0]) {
+      case OP_CONV: {
+        ConvParams p{};
+        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.xs = (int)r[3];
+        p.H = (int)r[4];
+        p.W = (int)r[5];
+        p.Cin = (int)r[6];
+        p.w = W + r[7];
+        p.Kpad = (int)r[8];
+        p.bias = (const float*)(W + r[9]);
+        p.f32out = (int)r[29];
+        p.y = resolve(bk, sl, r[10], r[11], p.f32out ? 4 : 2);
+        p.ys = (int)r[12];
+        p.Ho = (int)r[13];
+        p.Wo = (int)r[14];
+        p.Cout = (int)r[15];
+        p.Cout_pad = (int)r[16];
+        p.KH = (int)r[17];
+        p.KW = (int)r[18];
+        p.stride = (int)r[19];
+        p.pad_t = (int)r[20];
+        p.pad_l = (int)r[21];
+        p.res = resolve(bk, sl, r[22], r[23], 2);
+        p.rs = (int)r[24];
+        p.y2 = resolve(bk, sl, r[25], r[26], 2);
+        p.y2s = (int)r[27];
+        p.act = (int)r[28];
+        p.B = batch(r[30]);
+        p.bdev = bdev(r[30]);
+        conv2d(p, s);
+        break;
+      }
+      case OP_DWCONV: {
+        DwParams p{};
+        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.xs = (int)r[3];
+        p.H = (int)r[4];
+        p.W = (int)r[5];
+        p.C = (int)r[6];
+        p.w = W + r[7];
+        p.bias = (const float*)(W + r[8]);
+        p.y = resolve(bk, sl, r[9], r[10], 2);
+        p.ys = (int)r[11];
+        p.Ho = (int)r[12];
+        p.Wo = (int)r[13];
+        p.stride = (int)r[14];
+        p.act = (int)r[15];
+        p.B = batch(r[16]);
+        p.bdev = bdev(r[16]);
+        dwconv3x3(p, s);
+        break;
+      }
+      case OP_SPPF: {
+        SppfParams p{};
+        p.buf = resolve(bk, sl, r[1], r[2], 2);
+        p.xs = (int)r[3];
+        p.H = (int)r[4];
+        p.W = (int)r[5];
+        p.C = (int)r[6];
+        p.B = batch(r[7]);
+        p.bdev = bdev(r[7]);
+        sppf_pool(p, s);
+        break;
+      }
+      case OP_LETTERBOX: {
+        LetterboxParams p{};
+        p.pool = pool;
+        p.meta = meta;
+        p.ctrl = ctrl;
+        p.out = resolve(bk, sl, r[1], 0, 2);
+        p.B = B;
+        p.T = (int)r[2];
+        letterbox_s2d(p, s);
+        break;
+      }
+      case OP_ZERO: {
+        uint8_t* ptr = resolve(bk, sl, r[1], 0, 1);
+        const size_t bytes = (size_t)r[2] * batch(r[3]);
+        ARENA_HIP_CHECK(hipMemsetAsync(ptr, 0, bytes, s));
+        break;
+      }
+      case OP_DECODE: {
+        DecodeParams p{};
+        for (int l = 0; l < 3; ++l) {
+          p.head[l] = resolve(bk, sl, r[1 + 4 * l], r[2 + 4 * l], 2);
+          p.xs[l] = (int)r[3 + 4 * l];
+          p.hw[l] = (int)r[4 + 4 * l];
+          p.stride[l] = (float)r[13 + l];
+        }
+        p.cand = (Candidate*)resolve(bk, sl, r[16], 0, 1);
+        p.cand_count = (int*)resolve(bk, sl, r[17], 0, 1);
+        p.conf_thr = bits_to_float(r[18]);
+        p.cand_cap = cfg_.cand_cap;
+        p.B = B;
+        p.ctrl = ctrl;
+        detect_decode(p, s);
+        break;
+      }
+      case OP_NMS: {
+        NmsParams p{};
+        p.cand = (const Candidate*)resolve(bk, sl, r[1], 0, 1);
+        p.cand_count = (const int*)resolve(bk, sl, r[2], 0, 1);
+        p.cand_cap = cfg_.cand_cap;
+        p.meta = meta;
+        p.B = B;
+        p.det = (Detection*)resolve(bk, sl, r[3], 0, 1);
+        p.det_count = (int*)resolve(bk, sl, r[4], 0, 1);
+        p.max_det = cfg_.max_det;
+        p.iou_thr = bits_to_float(r[5]);
+        p.ctrl = ctrl;
+        nms(p, s);
+        break;
+      }
+      case OP_CROPPLAN: {
+        CropPlanParams p{};
+        p.det = (const Detection*)resolve(bk, sl, r[1], 0, 1);
+        p.det_count = (const int*)resolve(bk, sl, r[2], 0, 1);
+        p.max_det = cfg_.max_det;
+        p.meta = meta;
+        p.B = B;
+        p.crops = (CropRef*)resolve(bk, sl, r[3], 0, 1);
+        p.ctrl = ctrl;
+        p.crop_cap = CC;
+        crop_plan(p, s);
+        break;
+      }
+      case OP_CROPGATHER: {
+        CropGatherParams p{};
+        p.pool = pool;
+        p.meta = meta;
+        p.crops = (const CropRef*)resolve(bk, sl, r[1], 0, 1);
+        p.ctrl = ctrl;
+        p.out = resolve(bk, sl, r[2], 0, 2);
+        p.cap = CC;
+        p.S = (int)r[3];
+        for (int c = 0; c < 3; ++c) {
+          p.mean[c] = bits_to_float(r[4 + c]);
+          p.inv_std[c] = bits_to_float(r[7 + c]);
+        }
+        crop_gather_s2d(p, s);
+        break;
+      }
+      case OP_AVGPOOL: {
+        AvgPoolParams p{};
+        p.x = resolve(bk, sl, r[1], 0, 2);
+        p.HW = (int)r[2];
+        p.C = (int)r[3];
+        p.y = resolve(bk, sl, r[4], 0, 2);
+        p.B = batch(r[5]);
+        p.bdev = bdev(r[5]);
+        global_avgpool(p, s);
+        break;
+      }
+      case OP_TOPK: {
+        TopkParams p{};
+        p.logits = (const float*)resolve(bk, sl, r[1], 0, 4);
+        p.N = (int)r[2];
+        p.ld = (int)r[3];
+        p.out = (TopkResult*)resolve(bk, sl, r[4], 0, 1);
+        p.B = CC;
+        p.ctrl = ctrl;
+        topk_softmax(p, s);
+        break;
+      }
+      default:
+        throw std::runtime_error("unknown op type " + std::to_string(r[0]));
+    }
+    ARENA_HIP_CHECK(hipGetLastError());
+  }
+}
+
+// ---------------------------------------------------------------- host packing
+void Executor::parallel_copy(std::vector<std::function<void()>>& jobs) {
+  if (jobs.empty()) return;
+  if (jobs.size() == 1 || workers_.empty()) {
+    for (auto& j : jobs) j();
+    return;
+  }
+  std::unique_lock<std::mutex> lk(pool_mu_);
+  pool_jobs_ = &jobs;
+  pool_next_ = 0;
+  pool_pending_ = (int)jobs.size();
+  ++pool_gen_;
+  pool_cv_.notify_all();
+  pool_done_cv_.wait(lk, [&] { return pool_pending_ == 0; });
+  pool_jobs_ = nullptr;
+}
+
+int Executor::pick_bucket(int n) const {
+  for (auto& kv : buckets_)
+    if (kv.first >= n) return kv.first;
+  return -1;
+}
+
+int Executor::submit(const std::vector<InputImage>& imgs) {
+  std::lock_guard<std::mutex> lk(mu_);
+  const int n = (int)imgs.size();
+  if (n <= 0) throw std::runtime_error("submit: empty batch");
+  const int B = pick_bucket(n);
+  if (B < 0) throw std::runtime_error("submit: batch larger than the largest bucket");
+  const int s = next_slot_;
+  Slot& sl = slots_[s];
+  if (sl.busy) throw std::runtime_error("submit: both staging slots in flight; collect() first");
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  // The slot's previous graph has been collected; its input copy was consumed.
+  ImageMeta* meta = (ImageMeta*)(sl.h_in + kCtrlBytes);
+  uint8_t* pool = sl.h_in + in_bytes_meta();
+  const size_t pool_cap = (size_t)cfg_.pool_bytes_per_image * max_B_;
+  size_t off = 0;
+  std::vector<std::function<void()>> jobs;
+  const int T = cfg_.det_size;
+  for (int i = 0; i < n; ++i) {
+    const InputImage& im = imgs[i];
+    if (im.h <= 0 || im.w <= 0) throw std::runtime_error("submit: empty image");
+    const size_t bytes = (size_t)im.h * im.w * 3;
+    if (off + bytes > pool_cap) throw std::runtime_error("submit: batch exceeds the staging pool");
+    ImageMeta& m = meta[i];
+    m.offset = (int64_t)off;
+    m.h = im.h;
+    m.w = im.w;
+    const double sc = std::min((double)T / im.h, (double)T / im.w);
+    m.new_w = (int)(im.w * sc);
+    m.new_h = (int)(im.h * sc);
+    m.pad_w = (T - m.new_w) / 2;
+    m.pad_h = (T - m.new_h) / 2;
+    m.scale = (float)sc;
+    // split large images into 1 MiB copy jobs
+    const size_t chunk = 1 << 20;
+    for (size_t c = 0; c < bytes; c += chunk) {
+      const size_t len = std::min(chunk, bytes - c);
+      uint8_t* dst = pool + off + c;
+      const uint8_t* src = im.data + c;
+      jobs.emplace_back([dst, src, len]() { std::memcpy(dst, src, len); });
+    }
+    off = align_up(off + bytes, 256);
+  }
+  parallel_copy(jobs);
+  Ctrl* ctrl = (Ctrl*)sl.h_in;
+  std::memset(ctrl, 0, sizeof(Ctrl));
+  ctrl->n_images = n;
+  ctrl->crop_base = 0;
+  const size_t bytes = in_bytes_meta() + off;
+  ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, copy_));
+  ARENA_HIP_CHECK(hipEventRecord(sl.copied, copy_));
+  ARENA_HIP_CHECK(hipStreamWaitEvent(compute_, sl.copied, 0));
+  ARENA_HIP_CHECK(hipEventRecord(sl.started, compute_));
+  ARENA_HIP_CHECK(hipGraphLaunch(buckets_.at(B).graph[s], compute_));
+  ARENA_HIP_CHECK(hipEventRecord(sl.done, compute_));
+  sl.busy = true;
+  sl.bucket = B;
+  sl.n_images = n;
+  next_slot_ ^= 1;
+  return s;
+}
+
+BatchResult Executor::collect(int s) {
+  if (s < 0 || s > 1) throw std::runtime_error("collect: bad slot");
+  Slot& sl = slots_[s];
+  if (!sl.busy) throw std::runtime_error("collect: slot not in flight");
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  ARENA_HIP_CHECK(hipEventSynchronize(sl.done));
+  BatchResult res;
+  res.n_images = sl.n_images;
+  res.bucket = sl.bucket;
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, sl.started, sl.done);
+  res.gpu_ms = ms;
+  const int n = sl.n_images;
+  const int* cnt = (const int*)sl.h_out;
+  const Detection* det = (const Detection*)(sl.h_out + out_off_det());
+  res.det_count.assign(cnt, cnt + n);
+  res.det.assign(det, det + (size_t)n * cfg_.max_det);
+  res.crop_offset.resize(n + 1);
+  int total = 0;
+  for (int i = 0; i < n; ++i) {
+    res.crop_offset[i] = total;
+    total += std::min(cnt[i], cfg_.max_det);
+  }
+  res.crop_offset[n] = total;
+  res.total_crops = total;
+  Bucket& bk = buckets_.at(sl.bucket);
+  const int CC = bk.info.crop_cap;
+  if (total > CC) {
+    // Overflow: classify the remaining crops in extra passes of CC crops.
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int base = CC; base < total; base += CC) {
+      Ctrl c{};
+      c.n_images = n;
+      c.crop_base = base;
+      c.total_crops = total;
+      c.n_crops = std::min(CC, total - base);
+      ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, &c, sizeof(Ctrl), hipMemcpyHostToDevice, compute_));
+      enqueue_program(cls_prog_, bk, sl, compute_);
+    }
+    uint8_t* src = sl.d_out + out_off_topk() + sizeof(TopkResult) * (size_t)CC;
+    uint8_t* dst = sl.h_out + out_off_topk() + sizeof(TopkResult) * (size_t)CC;
+    ARENA_HIP_CHECK(hipMemcpyAsync(dst, src, sizeof(TopkResult) * (size_t)(total - CC), hipMemcpyDeviceToHost,
+                                   compute_));
+    ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+  }
+  const TopkResult* tk = (const TopkResult*)(sl.h_out + out_off_topk());
+  res.topk.assign(tk, tk + total);
+  sl.busy = false;
+  return res;
+}
+
+BatchResult Executor::run(const std::vector<InputImage>& imgs) { return collect(submit(imgs)); }
+
+void Executor::replay(int B, int s, int iters) {
+  auto it = buckets_.find(B);
+  if (it == buckets_.end()) throw std::runtime_error("replay: unknown bucket");
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  for (int i = 0; i < iters; ++i) ARENA_HIP_CHECK(hipGraphLaunch(it->second.graph[s], compute_));
+}
+
+void Executor::synchronize() {
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  ARENA_HIP_CHECK(hipStreamSynchronize(copy_));
+  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+}
+
+}  // namespace arena

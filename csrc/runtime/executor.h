@@ -1,0 +1,190 @@
+// Native pipeline executor (ONNX Runtime + Triton-instance replacement).
+//
+// The reference runs each model through an ONNX Runtime CPU session per
+// request (src/shared/model/registry.py:184-254; ModelRegistry.get_session)
+// and moves every intermediate through host memory.  Here one Executor owns a
+// whole GPU-resident two-stage pipeline:
+//
+//   pinned staging --H2D--> [ctrl | image meta | uint8 image pool]
+//     letterbox -> YOLOv5nu convs -> decode -> NMS -> crop plan
+//     -> crop gather -> MobileNetV2 convs -> avgpool -> FC -> top-5
+//   --D2H--> [det counts | detections | classifications]  (pinned)
+//
+// The op sequence is a static program produced by the Python planner
+// (inference_arena_amd/engine/planner.py): fixed-size int64 records that
+// name arena buffers by id.  For every batch bucket the executor resolves the
+// records to device pointers once and captures the whole sequence (including
+// memsets and the result D2H copy) into a hipGraph; a request batch is then
+// one H2D copy on a copy stream + one graph launch on the compute stream.
+// Two staging slots ping-pong so batch i+1 is uploaded while batch i runs.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../kernels/launch.h"
+
+namespace arena {
+
+constexpr int kOpFields = 48;
+using OpRecord = std::array<int64_t, kOpFields>;
+
+enum OpType : int64_t {
+  OP_CONV = 1,
+  OP_DWCONV = 2,
+  OP_SPPF = 3,
+  OP_LETTERBOX = 4,
+  OP_ZERO = 5,
+  OP_DECODE = 6,
+  OP_NMS = 7,
+  OP_CROPPLAN = 8,
+  OP_CROPGATHER = 9,
+  OP_AVGPOOL = 10,
+  OP_TOPK = 11,
+};
+
+// Reserved buffer ids (the planner's arena buffers are ids >= 0).
+enum ReservedBuf : int64_t {
+  BUF_NONE = -1,
+  BUF_CTRL = -10,
+  BUF_META = -11,
+  BUF_POOL = -12,
+  BUF_DET = -13,
+  BUF_DETCOUNT = -14,
+  BUF_TOPK = -15,
+};
+
+// Batch kind of an op: which live count clamps it.
+enum BatchKind : int64_t { BATCH_IMAGES = 0, BATCH_CROPS = 1 };
+
+struct ExecutorConfig {
+  int device = 0;
+  int max_batch = 32;         // largest bucket; sizes the staging slots
+  int max_det = 300;          // detections kept per image (reference: unbounded)
+  int cand_cap = 8400;        // candidates per image entering NMS (= anchors)
+  int crop_cap_per_image = 8; // crops one classification pass holds, per image
+  int min_crop_cap = 16;
+  int64_t pool_bytes_per_image = 640LL * 640 * 3;  // staging bytes per image slot
+  int det_size = 640;
+  int cls_size = 224;
+  int host_threads = 8;
+};
+
+struct BucketInfo {
+  int B = 0;
+  int crop_cap = 0;
+  std::vector<int64_t> offsets;  // arena byte offset per planner buffer id
+  int64_t arena_bytes = 0;
+};
+
+struct InputImage {
+  const uint8_t* data;  // RGB uint8 HWC, contiguous
+  int h, w;
+};
+
+// Per-slot results copied back to pinned memory by the graph.
+struct BatchResult {
+  int n_images = 0;
+  int bucket = 0;
+  int total_crops = 0;
+  std::vector<int> det_count;        // [n]
+  std::vector<Detection> det;        // [n * max_det]
+  std::vector<TopkResult> topk;      // [total crops], in crop-plan order
+  std::vector<int> crop_offset;      // [n + 1] first crop of each image
+  double gpu_ms = 0.0;               // graph wall time from events
+};
+
+class Executor {
+ public:
+  explicit Executor(const ExecutorConfig& cfg);
+  ~Executor();
+  Executor(const Executor&) = delete;
+  Executor& operator=(const Executor&) = delete;
+
+  void set_weights(const void* host, size_t bytes);
+  void set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops, int n_cls_ops);
+  void add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes);
+  std::vector<int> buckets() const;
+  int crop_cap_for(int B) const;
+  const ExecutorConfig& config() const { return cfg_; }
+
+  // Asynchronous pipelined API: submit() packs the images into a free staging
+  // slot, enqueues H2D + graph and returns the slot id; collect() waits for
+  // that slot and returns its results (running overflow classification passes
+  // when a batch produced more crops than one pass holds).
+  int submit(const std::vector<InputImage>& imgs);
+  BatchResult collect(int slot);
+  // Convenience: submit + collect.
+  BatchResult run(const std::vector<InputImage>& imgs);
+
+  // Run only the captured graph of a bucket on already-staged inputs; used by
+  // microbenchmarks to separate host packing from device time.
+  void replay(int B, int slot, int iters);
+  void synchronize();
+
+  // Device pointers for tests / introspection.
+  uintptr_t arena_ptr(int B) const;
+  uintptr_t weights_ptr() const { return (uintptr_t)d_weights_; }
+  uintptr_t stream() const { return (uintptr_t)compute_; }
+
+ private:
+  struct Slot {
+    // device
+    uint8_t* d_in = nullptr;   // ctrl | meta | pool
+    uint8_t* d_out = nullptr;  // det_count | det | topk
+    // pinned host
+    uint8_t* h_in = nullptr;
+    uint8_t* h_out = nullptr;
+    hipEvent_t copied = nullptr, started = nullptr, done = nullptr;
+    bool busy = false;
+    int bucket = 0;
+    int n_images = 0;
+  };
+  struct Bucket {
+    BucketInfo info;
+    uint8_t* d_arena = nullptr;
+    hipGraphExec_t graph[2] = {nullptr, nullptr};
+  };
+
+  void alloc_slots();
+  void capture(Bucket& bk, int slot);
+  void enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s);
+  uint8_t* resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff_elems, int elem_bytes);
+  int pick_bucket(int n) const;
+  size_t in_bytes_meta() const;
+  size_t in_bytes_total() const;
+  size_t out_off_det() const;
+  size_t out_off_topk() const;
+  size_t out_bytes_total() const;
+  void parallel_copy(std::vector<std::function<void()>>& jobs);
+
+  ExecutorConfig cfg_;
+  int max_B_ = 0;
+  hipStream_t compute_ = nullptr, copy_ = nullptr;
+  uint8_t* d_weights_ = nullptr;
+  size_t weights_bytes_ = 0;
+  std::vector<OpRecord> prog_, cls_prog_;
+  std::map<int, Bucket> buckets_;
+  Slot slots_[2];
+  int next_slot_ = 0;
+  std::mutex mu_;
+  // host worker pool for packing images into pinned memory
+  std::vector<std::thread> workers_;
+  std::mutex pool_mu_;
+  std::condition_variable pool_cv_, pool_done_cv_;
+  std::vector<std::function<void()>>* pool_jobs_ = nullptr;
+  std::atomic<int> pool_next_{0};
+  int pool_pending_ = 0;
+  uint64_t pool_gen_ = 0;
+  bool pool_stop_ = false;
+};
+
+}  // namespace arena

@@ -1,0 +1,287 @@
+"""Static program builder for the native executor.
+
+The reference hands each model to ONNX Runtime, which plans memory and
+kernels internally (src/shared/model/registry.py:194-224; ORT's
+``enable_mem_pattern=False`` is set there).  Here the planning is explicit:
+
+* a *program* is a list of fixed-size int64 op records (layouts below) that
+  name arena buffers by id; ``csrc/runtime/executor.cpp`` resolves them to
+  device pointers per batch bucket and captures them into a hipGraph;
+* buffers are NHWC tensors (or raw byte regions) sized per batch item and
+  scaled by the bucket's image count or crop capacity;
+* ``layout()`` assigns arena offsets by lifetime (first/last op that touches a
+  buffer), so dead activations are reused and the working set of a whole
+  batch stays in the MI355X's 256 MiB Infinity Cache where possible;
+* weights (BN folded, kernel layouts, bf16) are packed into one blob.
+
+Op record layouts (index: field) — keep in sync with executor.cpp:
+  CONV   1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 Cin 7 w_off 8 Kpad 9 b_off 10 y_buf
+         11 y_coff 12 y_cs 13 Ho 14 Wo 15 Cout 16 Cout_pad 17 KH 18 KW 19 stride
+         20 pad_t 21 pad_l 22 res_buf 23 res_coff 24 res_cs 25 y2_buf 26 y2_coff
+         27 y2_cs 28 act 29 f32out 30 batch_kind
+  DWCONV 1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 C 7 w_off 8 b_off 9 y_buf 10 y_coff
+         11 y_cs 12 Ho 13 Wo 14 stride 15 act 16 batch_kind
+  SPPF   1 buf 2 coff 3 cs 4 H 5 W 6 C 7 batch_kind
+  LETTERBOX 1 out_buf 2 T
+  ZERO   1 buf 2 bytes_per_item 3 batch_kind
+  DECODE 1-4 / 5-8 / 9-12 (buf, coff, cs, hw) per level, 13-15 strides,
+         16 cand_buf 17 count_buf 18 conf_thr (float bits)
+  NMS    1 cand_buf 2 count_buf 3 det_buf 4 detcount_buf 5 iou_thr (float bits)
+  CROPPLAN 1 det_buf 2 detcount_buf 3 crops_buf
+  CROPGATHER 1 crops_buf 2 out_buf 3 S 4-6 mean 7-9 inv_std (float bits)
+  AVGPOOL 1 x_buf 2 HW 3 C 4 y_buf 5 batch_kind
+  TOPK   1 logits_buf 2 N 3 ld 4 out_buf
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+OP_FIELDS = 48
+OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL, OP_TOPK = range(1, 12)
+BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK = -1, -10, -11, -12, -13, -14, -15
+IMAGES, CROPS = 0, 1
+ACT = {None: 0, "none": 0, "silu": 1, "relu6": 2}
+ALIGN = 256
+
+
+def fbits(v: float) -> int:
+    return struct.unpack("<I", struct.pack("<f", float(v)))[0]
+
+
+def _round(v: int, a: int) -> int:
+    return (v + a - 1) // a * a
+
+
+@dataclass
+class Buffer:
+    id: int
+    name: str
+    per_item: int  # bytes per batch item
+    kind: int  # IMAGES or CROPS
+    H: int = 0
+    W: int = 0
+    C: int = 0
+    elem: int = 2
+    pinned: bool = False  # live until the end of the program
+    first: int = 1 << 30
+    last: int = -1
+
+
+@dataclass
+class View:
+    buf: Buffer | int  # Buffer or a reserved id
+    coff: int = 0
+    C: int = 0
+
+    @property
+    def bid(self) -> int:
+        return self.buf.id if isinstance(self.buf, Buffer) else int(self.buf)
+
+    @property
+    def cs(self) -> int:
+        return self.buf.C if isinstance(self.buf, Buffer) else 0
+
+
+@dataclass
+class Program:
+    ops: np.ndarray
+    cls_ops: np.ndarray
+    buffers: list[Buffer]
+    weights: np.ndarray
+    meta: dict = field(default_factory=dict)
+
+
+class WeightPacker:
+    def __init__(self) -> None:
+        self.chunks: list[bytes] = []
+        self.size = 0
+
+    def add(self, data: bytes) -> int:
+        off = self.size
+        pad = _round(len(data), ALIGN) - len(data)
+        self.chunks.append(data + b"\0" * pad)
+        self.size += len(data) + pad
+        return off
+
+    def blob(self) -> np.ndarray:
+        return np.frombuffer(b"".join(self.chunks), dtype=np.uint8).copy()
+
+
+def bf16_bytes(t: torch.Tensor) -> bytes:
+    return t.detach().float().contiguous().to(torch.bfloat16).view(torch.int16).numpy().tobytes()
+
+
+def pack_conv_weight(w: torch.Tensor, b: torch.Tensor) -> tuple[bytes, bytes, int, int]:
+    """[Cout, Cin, KH, KW] fp32 -> ([Cout_pad][Kpad] bf16 bytes, bias fp32 bytes, Kpad, Cout_pad)."""
+    cout, cin, kh, kw = w.shape
+    k = kh * kw * cin
+    kpad = _round(k, 32)
+    cpad = _round(cout, 16)
+    wk = torch.zeros(cpad, kpad, dtype=torch.float32)
+    wk[:cout, :k] = w.permute(0, 2, 3, 1).reshape(cout, k)
+    bb = torch.zeros(cpad, dtype=torch.float32)
+    bb[:cout] = b
+    return bf16_bytes(wk), bb.numpy().tobytes(), kpad, cpad
+
+
+class ProgramBuilder:
+    def __init__(self) -> None:
+        self.buffers: list[Buffer] = []
+        self.ops: list[list[int]] = []
+        self.cls_start: int | None = None
+        self.weights = WeightPacker()
+        self.meta: dict = {}
+
+    # ------------------------------------------------------------ buffers
+    def tensor(self, name: str, H: int, W: int, C: int, kind: int = IMAGES, elem: int = 2) -> Buffer:
+        if C % 8:
+            raise ValueError(f"{name}: channel count {C} must be a multiple of 8")
+        b = Buffer(len(self.buffers), name, _round(H * W * C * elem, 16), kind, H, W, C, elem)
+        self.buffers.append(b)
+        return b
+
+    def raw(self, name: str, per_item: int, kind: int = IMAGES, pinned: bool = False) -> Buffer:
+        b = Buffer(len(self.buffers), name, _round(per_item, 16), kind, pinned=pinned)
+        self.buffers.append(b)
+        return b
+
+    def _touch(self, *views) -> None:
+        i = len(self.ops)
+        for v in views:
+            if v is None:
+                continue
+            b = v.buf if isinstance(v, View) else v
+            if isinstance(b, Buffer):
+                b.first = min(b.first, i)
+                b.last = max(b.last, i)
+
+    def _emit(self, rec: list[int], *touch) -> None:
+        self._touch(*touch)
+        r = list(rec) + [0] * (OP_FIELDS - len(rec))
+        self.ops.append(r)
+
+    def begin_classifier(self) -> None:
+        """Ops from here on form the overflow classification program."""
+        self.cls_start = len(self.ops)
+
+    # ------------------------------------------------------------ ops
+    def conv(self, src: View, dst: View, w: torch.Tensor, b: torch.Tensor, *, stride: int = 1,
+             pad: int | tuple[int, int] | None = None, act: str | None = "silu", res: View | None = None,
+             dst2: View | None = None, f32out: bool = False, kind: int = IMAGES,
+             out_hw: tuple[int, int] | None = None, src_hw: tuple[int, int] | None = None) -> None:
+        cout, cin, kh, kw = w.shape
+        if cin != src.C:
+            raise ValueError(f"conv: weight Cin {cin} != source view C {src.C}")
+        if cout != dst.C:
+            raise ValueError(f"conv: weight Cout {cout} != destination view C {dst.C}")
+        H, W = src_hw if src_hw else (src.buf.H, src.buf.W)
+        if pad is None:
+            pad = (kh // 2, kw // 2)
+        if isinstance(pad, int):
+            pad = (pad, pad)
+        if out_hw is None:
+            Ho = (H + 2 * pad[0] - kh) // stride + 1
+            Wo = (W + 2 * pad[1] - kw) // stride + 1
+        else:
+            Ho, Wo = out_hw
+        wb, bb, kpad, cpad = pack_conv_weight(w, b)
+        w_off = self.weights.add(wb)
+        b_off = self.weights.add(bb)
+        rec = [OP_CONV, src.bid, src.coff, src.cs, H, W, cin, w_off, kpad, b_off,
+               dst.bid, dst.coff, dst.cs, Ho, Wo, cout, cpad, kh, kw, stride, pad[0], pad[1],
+               res.bid if res else BUF_NONE, res.coff if res else 0, res.cs if res else 0,
+               dst2.bid if dst2 else BUF_NONE, dst2.coff if dst2 else 0, dst2.cs if dst2 else 0,
+               ACT[act], int(f32out), kind]
+        self._emit(rec, src, dst, res, dst2)
+
+    def dwconv(self, src: View, dst: View, w: torch.Tensor, b: torch.Tensor, *, stride: int, act: str = "relu6",
+               kind: int = IMAGES) -> None:
+        C = w.shape[0]
+        if w.shape[1:] != (1, 3, 3) or src.C != C or dst.C != C:
+            raise ValueError("dwconv: expects [C,1,3,3] weights matching the views")
+        H, W = src.buf.H, src.buf.W
+        Ho, Wo = (H + 2 - 3) // stride + 1, (W + 2 - 3) // stride + 1
+        wt = w.reshape(C, 9).t().contiguous()  # [9][C]
+        w_off = self.weights.add(bf16_bytes(wt))
+        b_off = self.weights.add(b.detach().float().numpy().tobytes())
+        rec = [OP_DWCONV, src.bid, src.coff, src.cs, H, W, C, w_off, b_off, dst.bid, dst.coff, dst.cs,
+               Ho, Wo, stride, ACT[act], kind]
+        self._emit(rec, src, dst)
+
+    def sppf(self, buf: Buffer, C: int, kind: int = IMAGES) -> None:
+        self._emit([OP_SPPF, buf.id, 0, buf.C, buf.H, buf.W, C, kind], buf)
+
+    def letterbox(self, out: Buffer, T: int) -> None:
+        self._emit([OP_LETTERBOX, out.id, T], out)
+
+    def zero(self, buf: Buffer, kind: int = IMAGES) -> None:
+        self._emit([OP_ZERO, buf.id, buf.per_item, kind], buf)
+
+    def decode(self, heads: list[View], strides, cand: Buffer, count: Buffer, conf_thr: float) -> None:
+        rec = [OP_DECODE]
+        for v in heads:
+            rec += [v.bid, v.coff, v.cs, v.buf.H]
+        rec += list(int(s) for s in strides) + [cand.id, count.id, fbits(conf_thr)]
+        self._emit(rec, *heads, cand, count)
+
+    def nms(self, cand: Buffer, count: Buffer, iou_thr: float) -> None:
+        self._emit([OP_NMS, cand.id, count.id, BUF_DET, BUF_DETCOUNT, fbits(iou_thr)], cand, count)
+
+    def crop_plan(self, crops: Buffer) -> None:
+        self._emit([OP_CROPPLAN, BUF_DET, BUF_DETCOUNT, crops.id], crops)
+
+    def crop_gather(self, crops: Buffer, out: Buffer, S: int, mean, std) -> None:
+        rec = [OP_CROPGATHER, crops.id, out.id, S] + [fbits(m) for m in mean] + [fbits(1.0 / s) for s in std]
+        self._emit(rec, crops, out)
+
+    def avgpool(self, x: Buffer, y: Buffer, kind: int = CROPS) -> None:
+        self._emit([OP_AVGPOOL, x.id, x.H * x.W, x.C, y.id, kind], x, y)
+
+    def topk(self, logits: Buffer, N: int, ld: int) -> None:
+        self._emit([OP_TOPK, logits.id, N, ld, BUF_TOPK], logits)
+
+    # ------------------------------------------------------------ finalize
+    def build(self, meta: dict | None = None) -> Program:
+        n = len(self.ops)
+        for b in self.buffers:
+            if b.pinned and b.last >= 0:
+                b.last = n
+        ops = np.asarray(self.ops, dtype=np.int64).reshape(n, OP_FIELDS)
+        cs = self.cls_start if self.cls_start is not None else n
+        cls_ops = ops[cs:].copy()
+        m = dict(self.meta)
+        m.update(meta or {})
+        return Program(ops, cls_ops, self.buffers, self.weights.blob(), m)
+
+
+def layout(buffers: list[Buffer], n_images: int, n_crops: int) -> tuple[np.ndarray, int]:
+    """Lifetime-aware first-fit placement; returns (offsets per buffer id, arena bytes)."""
+    sizes = []
+    for b in buffers:
+        cnt = n_crops if b.kind == CROPS else n_images
+        sizes.append(_round(b.per_item * cnt, ALIGN))
+    order = sorted(range(len(buffers)), key=lambda i: (-sizes[i], buffers[i].first))
+    placed: list[tuple[int, int, int]] = []  # (offset, end, id)
+    offsets = np.zeros(len(buffers), dtype=np.int64)
+    total = 0
+    for i in order:
+        b = buffers[i]
+        if b.last < 0:  # never used
+            offsets[i] = 0
+            continue
+        conflicts = sorted(
+            (o, e) for (o, e, j) in placed if not (buffers[j].last < b.first or b.last < buffers[j].first)
+        )
+        off = 0
+        for o, e in conflicts:
+            if off + sizes[i] <= o:
+                break
+            off = max(off, e)
+        offsets[i] = off
+        placed.append((off, off + sizes[i], i))
+        total = max(total, off + sizes[i])
+    return offsets, _round(total, ALIGN)

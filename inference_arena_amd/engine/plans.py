@@ -1,0 +1,197 @@
+"""Lowering of the two oracle networks into one executor program.
+
+The whole request pipeline of the reference's monolithic arm
+(architectures/monolithic/app/inference.py:127-227: decode -> letterbox ->
+YOLO -> NMS -> un-letterbox -> per-detection crop -> MobileNet -> argmax) is
+lowered into a single device-resident program:
+
+  letterbox(s2d) -> 75 YOLOv5nu convs (+SPPF pool) -> decode -> NMS ->
+  crop plan -> crop gather(s2d) -> 52 MobileNetV2 convs/dwconvs -> avgpool ->
+  FC -> top-5
+
+Lowering rules (what replaces ONNX graph nodes):
+  * BN is folded into every conv; SiLU / ReLU6 / residual Add are epilogues.
+  * Concat nodes disappear: producers store into channel slices of a shared
+    buffer; the two FPN Upsample nodes become the conv epilogue's second,
+    2x-nearest store (h10 and h14 feed both a concat at their own resolution
+    and an upsampled concat).
+  * C3's cv1 and cv2 (same input) are one conv with stacked weights; the
+    bottleneck chain updates the cv1 half in place.
+  * Detect's first 3x3 convs of the box and class branches are one conv.
+  * Both stems read space-to-depth inputs: YOLO's 6x6/s2/p2 conv becomes a
+    3x3/s1 conv over 12(+4) channels, MobileNet's 3x3/s2 conv a 2x2/s1 conv.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..models.common import fold, fold_conv_bn
+from ..models.mobilenetv2 import MobileNetV2
+from ..models.yolov5nu import STRIDES, YOLOv5nu
+from .planner import CROPS, IMAGES, BUF_NONE, Program, ProgramBuilder, View
+
+CAND_BYTES = 32
+CROPREF_BYTES = 32
+
+
+def s2d_stem_6x6(w: torch.Tensor) -> torch.Tensor:
+    """[Co,3,6,6] (stride 2, pad 2) -> [Co,16,3,3] (stride 1, pad 1) over space-to-depth input."""
+    co = w.shape[0]
+    out = torch.zeros(co, 16, 3, 3)
+    for a in range(3):
+        for b in range(3):
+            for p in range(2):
+                for q in range(2):
+                    for c in range(3):
+                        out[:, (p * 2 + q) * 3 + c, a, b] = w[:, c, 2 * a + p, 2 * b + q]
+    return out
+
+
+def s2d_stem_3x3(w: torch.Tensor) -> torch.Tensor:
+    """[Co,3,3,3] (stride 2, pad 1) -> [Co,16,2,2] (stride 1, pad top/left 1) over space-to-depth input."""
+    co = w.shape[0]
+    out = torch.zeros(co, 16, 2, 2)
+    tap = {(0, 1): 0, (1, 0): 1, (1, 1): 2}  # (block offset a, phase p) -> original tap i
+    for (a, p), i in tap.items():
+        for (b, q), j in tap.items():
+            for c in range(3):
+                out[:, (p * 2 + q) * 3 + c, a, b] = w[:, c, i, j]
+    return out
+
+
+def _c3(pb: ProgramBuilder, m, src: View, dst: View, H: int, W: int, name: str) -> None:
+    c_ = m.c_
+    T = pb.tensor(f"{name}.T", H, W, 2 * c_)
+    U = pb.tensor(f"{name}.U", H, W, c_)
+    w1, b1 = fold(m.cv1)
+    w2, b2 = fold(m.cv2)
+    pb.conv(src, View(T, 0, 2 * c_), torch.cat([w1, w2]), torch.cat([b1, b2]))
+    for bn in m.m:
+        wa, ba = fold(bn.cv1)
+        pb.conv(View(T, 0, c_), View(U, 0, c_), wa, ba)
+        wb, bb = fold(bn.cv2)
+        pb.conv(View(U, 0, c_), View(T, 0, c_), wb, bb, res=View(T, 0, c_) if bn.add else None)
+    w3, b3 = fold(m.cv3)
+    pb.conv(View(T, 0, 2 * c_), dst, w3, b3)
+
+
+def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640):
+    h = T // 2
+    X0 = pb.tensor("x_s2d", h, h, 16)
+    pb.letterbox(X0, T)
+    A0 = pb.tensor("b0", h, h, 16)
+    w, b = fold(y.b0)
+    pb.conv(View(X0, 0, 16), View(A0, 0, 16), s2d_stem_6x6(w), b)
+    A1 = pb.tensor("b1", h // 2, h // 2, 32)
+    pb.conv(View(A0, 0, 16), View(A1, 0, 32), *fold(y.b1), stride=2)
+    A2 = pb.tensor("b2", h // 2, h // 2, 32)
+    _c3(pb, y.b2, View(A1, 0, 32), View(A2, 0, 32), h // 2, h // 2, "b2")
+    s8 = T // 8
+    A3 = pb.tensor("b3", s8, s8, 64)
+    pb.conv(View(A2, 0, 32), View(A3, 0, 64), *fold(y.b3), stride=2)
+    CAT16 = pb.tensor("cat16", s8, s8, 128)
+    _c3(pb, y.b4, View(A3, 0, 64), View(CAT16, 64, 64), s8, s8, "b4")
+    s16 = T // 16
+    A5 = pb.tensor("b5", s16, s16, 128)
+    pb.conv(View(CAT16, 64, 64), View(A5, 0, 128), *fold(y.b5), stride=2, src_hw=(s8, s8))
+    CAT12 = pb.tensor("cat12", s16, s16, 256)
+    _c3(pb, y.b6, View(A5, 0, 128), View(CAT12, 128, 128), s16, s16, "b6")
+    s32 = T // 32
+    A7 = pb.tensor("b7", s32, s32, 256)
+    pb.conv(View(CAT12, 128, 128), View(A7, 0, 256), *fold(y.b7), stride=2)
+    A8 = pb.tensor("b8", s32, s32, 256)
+    _c3(pb, y.b8, View(A7, 0, 256), View(A8, 0, 256), s32, s32, "b8")
+    S9 = pb.tensor("sppf", s32, s32, 512)
+    c_ = y.b9.c_
+    pb.conv(View(A8, 0, 256), View(S9, 0, c_), *fold(y.b9.cv1))
+    pb.sppf(S9, c_)
+    A9 = pb.tensor("b9", s32, s32, 256)
+    pb.conv(View(S9, 0, 4 * c_), View(A9, 0, 256), *fold(y.b9.cv2))
+    CAT22 = pb.tensor("cat22", s32, s32, 256)
+    pb.conv(View(A9, 0, 256), View(CAT22, 128, 128), *fold(y.h10), dst2=View(CAT12, 0, 128))
+    A13 = pb.tensor("h13", s16, s16, 128)
+    _c3(pb, y.h13, View(CAT12, 0, 256), View(A13, 0, 128), s16, s16, "h13")
+    CAT19 = pb.tensor("cat19", s16, s16, 128)
+    pb.conv(View(A13, 0, 128), View(CAT19, 64, 64), *fold(y.h14), dst2=View(CAT16, 0, 64))
+    P3 = pb.tensor("p3", s8, s8, 64)
+    _c3(pb, y.h17, View(CAT16, 0, 128), View(P3, 0, 64), s8, s8, "h17")
+    pb.conv(View(P3, 0, 64), View(CAT19, 0, 64), *fold(y.h18), stride=2)
+    P4 = pb.tensor("p4", s16, s16, 128)
+    _c3(pb, y.h20, View(CAT19, 0, 128), View(P4, 0, 128), s16, s16, "h20")
+    pb.conv(View(P4, 0, 128), View(CAT22, 0, 128), *fold(y.h21), stride=2)
+    P5 = pb.tensor("p5", s32, s32, 256)
+    _c3(pb, y.h23, View(CAT22, 0, 256), View(P5, 0, 256), s32, s32, "h23")
+
+    d = y.detect
+    c2, c3, nc = d.c2, d.c3, d.nc
+    ch = c2 + c3
+    heads = []
+    for lvl, (P, cin, s) in enumerate(((P3, 64, s8), (P4, 128, s16), (P5, 256, s32))):
+        H1 = pb.tensor(f"det{lvl}.h1", s, s, ch)
+        H2 = pb.tensor(f"det{lvl}.h2", s, s, ch)
+        D = pb.tensor(f"det{lvl}.out", s, s, 4 * d.reg_max + nc)
+        wa, ba = fold(d.cv2[lvl][0])
+        wc, bc = fold(d.cv3[lvl][0])
+        pb.conv(View(P, 0, cin), View(H1, 0, ch), torch.cat([wa, wc]), torch.cat([ba, bc]))
+        pb.conv(View(H1, 0, c2), View(H2, 0, c2), *fold(d.cv2[lvl][1]))
+        pb.conv(View(H1, c2, c3), View(H2, c2, c3), *fold(d.cv3[lvl][1]))
+        pb.conv(View(H2, 0, c2), View(D, 0, 4 * d.reg_max), *fold_conv_bn(d.cv2[lvl][2], None), act=None)
+        pb.conv(View(H2, c2, c3), View(D, 4 * d.reg_max, nc), *fold_conv_bn(d.cv3[lvl][2], None), act=None)
+        heads.append(View(D, 0, 4 * d.reg_max + nc))
+    return heads
+
+
+def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std):
+    h = S // 2
+    X = pb.tensor("crop_s2d", h, h, 16, kind=CROPS)
+    pb.crop_gather(crops, X, S, mean, std)
+    w, b = fold(m.stem)
+    F = pb.tensor("m.stem", h, h, 32, kind=CROPS)
+    pb.conv(View(X, 0, 16), View(F, 0, 32), s2d_stem_3x3(w), b, pad=(1, 1), act="relu6", kind=CROPS,
+            out_hw=(h, h))
+    cur, H = F, h
+    for i, blk in enumerate(m.blocks):
+        Ho = (H + 2 - 3) // blk.stride + 1
+        if blk.expand is not None:
+            E = pb.tensor(f"m{i}.exp", H, H, blk.hidden, kind=CROPS)
+            pb.conv(View(cur, 0, blk.inp), View(E, 0, blk.hidden), *fold(blk.expand), act="relu6", kind=CROPS)
+        else:
+            E = cur
+        Dw = pb.tensor(f"m{i}.dw", Ho, Ho, blk.hidden, kind=CROPS)
+        wd, bd = fold(blk.dw)
+        pb.dwconv(View(E, 0, blk.hidden), View(Dw, 0, blk.hidden), wd, bd, stride=blk.stride, kind=CROPS)
+        O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup, kind=CROPS)
+        pb.conv(View(Dw, 0, blk.hidden), View(O, 0, blk.oup), *fold(blk.project), act=None,
+                res=View(cur, 0, blk.inp) if blk.use_res else None, kind=CROPS)
+        cur, H = O, Ho
+    HD = pb.tensor("m.head", H, H, 1280, kind=CROPS)
+    pb.conv(View(cur, 0, cur.C), View(HD, 0, 1280), *fold(m.head), act="relu6", kind=CROPS)
+    PO = pb.tensor("m.pool", 1, 1, 1280, kind=CROPS)
+    pb.avgpool(HD, PO)
+    ncls = m.fc.out_features
+    LG = pb.tensor("m.logits", 1, 1, ncls + (-ncls % 8), kind=CROPS, elem=4)
+    wfc = m.fc.weight.detach().float().reshape(ncls, 1280, 1, 1)
+    pb.conv(View(PO, 0, 1280), View(LG, 0, ncls), wfc, m.fc.bias.detach().float(), act=None, f32out=True,
+            kind=CROPS)
+    pb.topk(LG, ncls, LG.C)
+
+
+def plan_pipeline(yolo: YOLOv5nu, mnet: MobileNetV2, *, conf_thr: float, iou_thr: float, det_size: int = 640,
+                  cls_size: int = 224, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225),
+                  cand_cap: int = 8400, max_det: int = 300) -> Program:
+    pb = ProgramBuilder()
+    heads = plan_yolo(pb, yolo, det_size)
+    cand = pb.raw("cand", cand_cap * CAND_BYTES)
+    count = pb.raw("cand_count", 4)
+    pb.zero(count)
+    pb.decode(heads, STRIDES, cand, count, conf_thr)
+    pb.nms(cand, count, iou_thr)
+    crops = pb.raw("crops", max_det * CROPREF_BYTES, pinned=True)
+    pb.crop_plan(crops)
+    pb.begin_classifier()
+    plan_mobilenet(pb, mnet, crops, cls_size, mean, std)
+    return pb.build({"conf_thr": conf_thr, "iou_thr": iou_thr, "det_size": det_size, "cls_size": cls_size,
+                     "cand_cap": cand_cap, "max_det": max_det})
+
+
+__all__ = ["plan_pipeline", "plan_yolo", "plan_mobilenet", "s2d_stem_6x6", "s2d_stem_3x3", "BUF_NONE", "IMAGES"]

@@ -1,0 +1,151 @@
+"""Tensor-level wrappers around the HIP kernels (torch tensors on ROCm).
+
+These call the same launchers the executor uses, on the current torch stream,
+so every kernel can be tested against a PyTorch fp32 reference op and used
+outside the executor.  Activations are NHWC bf16 tensors; a "view" into a
+concat buffer is passed as the buffer plus a channel offset.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+
+import numpy as np
+import torch
+
+from ..engine.planner import ACT, pack_conv_weight
+from . import native
+
+IMAGE_META = struct.Struct("<qiiiiiif12x")  # must match arena::ImageMeta (48 bytes)
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: torch.Tensor | None, elem_off: int = 0) -> int:
+    if t is None:
+        return 0
+    return t.data_ptr() + elem_off * t.element_size()
+
+
+def pack_weights(w: torch.Tensor, b: torch.Tensor, device) -> tuple[torch.Tensor, torch.Tensor, int, int]:
+    wb, bb, kpad, cpad = pack_conv_weight(w.detach().cpu().float(), b.detach().cpu().float())
+    wt = torch.frombuffer(bytearray(wb), dtype=torch.bfloat16).to(device)
+    bt = torch.frombuffer(bytearray(bb), dtype=torch.float32).to(device)
+    return wt, bt, kpad, cpad
+
+
+def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: int = 1, pad=None, act=None,
+                x_coff: int = 0, cin: int | None = None, out: torch.Tensor | None = None, out_coff: int = 0,
+                res: torch.Tensor | None = None, res_coff: int = 0, out2: torch.Tensor | None = None,
+                out2_coff: int = 0, f32out: bool = False, out_hw=None, bdev: torch.Tensor | None = None,
+                packed=None) -> torch.Tensor:
+    """NHWC conv with fused bias/act/residual/upsampled copy.
+
+    x: [B, H, W, Cx] bf16 (reads channels [x_coff, x_coff + Cin)); w: [Cout, Cin, KH, KW] fp32.
+    """
+    B, H, W, Cx = x.shape
+    cout, cin_w, kh, kw = w.shape
+    cin = cin or cin_w
+    if pad is None:
+        pad = (kh // 2, kw // 2)
+    if isinstance(pad, int):
+        pad = (pad, pad)
+    if out_hw is None:
+        Ho = (H + 2 * pad[0] - kh) // stride + 1
+        Wo = (W + 2 * pad[1] - kw) // stride + 1
+    else:
+        Ho, Wo = out_hw
+    if out is None:
+        out = torch.empty(B, Ho, Wo, cout, dtype=torch.float32 if f32out else torch.bfloat16, device=x.device)
+    wt, bt, kpad, cpad = packed if packed is not None else pack_weights(w, b, x.device)
+    native().conv2d({
+        "x": _ptr(x, x_coff), "B": B, "H": H, "W": W, "xs": Cx, "Cin": cin,
+        "w": _ptr(wt), "Kpad": kpad, "bias": _ptr(bt),
+        "y": _ptr(out, out_coff), "Ho": Ho, "Wo": Wo, "ys": out.shape[-1], "Cout": cout, "Cout_pad": cpad,
+        "KH": kh, "KW": kw, "stride": stride, "pad_t": pad[0], "pad_l": pad[1],
+        "res": _ptr(res, res_coff), "rs": res.shape[-1] if res is not None else 0,
+        "y2": _ptr(out2, out2_coff), "y2s": out2.shape[-1] if out2 is not None else 0,
+        "act": ACT[act], "f32out": int(f32out), "bdev": _ptr(bdev), "stream": _stream(),
+    })
+    return out
+
+
+def dwconv3x3_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: int = 1, act="relu6",
+                   bdev: torch.Tensor | None = None) -> torch.Tensor:
+    B, H, W, C = x.shape
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y = torch.empty(B, Ho, Wo, C, dtype=torch.bfloat16, device=x.device)
+    wt = w.detach().float().reshape(C, 9).t().contiguous().to(torch.bfloat16).to(x.device)
+    bt = b.detach().float().contiguous().to(x.device)
+    native().dwconv3x3({"x": _ptr(x), "B": B, "H": H, "W": W, "xs": C, "C": C, "w": _ptr(wt), "bias": _ptr(bt),
+                        "y": _ptr(y), "Ho": Ho, "Wo": Wo, "ys": C, "stride": stride, "act": ACT[act],
+                        "bdev": _ptr(bdev), "stream": _stream()})
+    return y
+
+
+def sppf_nhwc(buf: torch.Tensor, C: int) -> torch.Tensor:
+    """In place: buf[..., C:4C] = cascaded 5x5 max pools of buf[..., :C]."""
+    B, H, W, Ct = buf.shape
+    native().sppf_pool({"buf": _ptr(buf), "B": B, "H": H, "W": W, "xs": Ct, "C": C, "stream": _stream()})
+    return buf
+
+
+def image_meta_bytes(images: list[np.ndarray], T: int) -> tuple[bytes, np.ndarray]:
+    """Pack images into one uint8 pool (256-B aligned) + ImageMeta records."""
+    from ..processing.transforms import letterbox_geometry
+
+    metas, chunks, off = [], [], 0
+    for im in images:
+        h, w = im.shape[:2]
+        scale, nw, nh, pw, ph = letterbox_geometry(h, w, T)
+        metas.append(IMAGE_META.pack(off, h, w, nw, nh, pw, ph, scale))
+        data = np.ascontiguousarray(im, np.uint8).tobytes()
+        pad = (-len(data)) % 256
+        chunks.append(data + b"\0" * pad)
+        off += len(data) + pad
+    return b"".join(metas), np.frombuffer(b"".join(chunks), dtype=np.uint8)
+
+
+def ctrl_tensor(n_images: int, device, n_crops: int = 0, crop_base: int = 0) -> torch.Tensor:
+    c = torch.zeros(16, dtype=torch.int32)
+    c[0], c[1], c[2] = n_images, n_crops, crop_base
+    return c.to(device)
+
+
+def letterbox_s2d(images: list[np.ndarray], T: int, device) -> torch.Tensor:
+    meta, pool = image_meta_bytes(images, T)
+    meta_t = torch.frombuffer(bytearray(meta), dtype=torch.uint8).to(device)
+    pool_t = torch.from_numpy(pool.copy()).to(device)
+    ctrl = ctrl_tensor(len(images), device)
+    out = torch.empty(len(images), T // 2, T // 2, 16, dtype=torch.bfloat16, device=device)
+    native().letterbox_s2d({"pool": _ptr(pool_t), "meta": _ptr(meta_t), "ctrl": _ptr(ctrl), "out": _ptr(out),
+                            "B": len(images), "T": T, "stream": _stream()})
+    torch.cuda.current_stream().synchronize()
+    return out
+
+
+def s2d_to_nchw(x: torch.Tensor) -> torch.Tensor:
+    """[B, h, w, 16] space-to-depth (12 live channels) -> [B, 3, 2h, 2w] fp32."""
+    B, h, w, _ = x.shape
+    y = x[..., :12].float().reshape(B, h, w, 2, 2, 3)  # p, q, c
+    return y.permute(0, 5, 1, 3, 2, 4).reshape(B, 3, 2 * h, 2 * w)
+
+
+def avgpool_nhwc(x: torch.Tensor) -> torch.Tensor:
+    B, H, W, C = x.shape
+    y = torch.empty(B, C, dtype=torch.bfloat16, device=x.device)
+    native().global_avgpool({"x": _ptr(x), "B": B, "HW": H * W, "C": C, "y": _ptr(y), "stream": _stream()})
+    return y
+
+
+def topk_softmax(logits: torch.Tensor):
+    """[B, N] fp32 -> (idx [B,5] int32, logit [B,5], prob [B,5])."""
+    B, N = logits.shape
+    out = torch.empty(B, 16, dtype=torch.int32, device=logits.device)
+    native().topk_softmax({"logits": _ptr(logits), "B": B, "N": N, "ld": logits.stride(0), "out": _ptr(out),
+                           "stream": _stream()})
+    torch.cuda.current_stream().synchronize()
+    o = out.cpu()
+    return o[:, 0:5].clone(), o[:, 5:10].view(torch.float32).clone(), o[:, 10:15].view(torch.float32).clone()

@@ -1,0 +1,106 @@
+"""Process-group helpers for one-process-per-GPU replicas.
+
+The reference scales only by container count and has no collectives
+(SURVEY.md §2.4).  Here every GPU replica is its own process; at start-up the
+replicas join one ``torch.distributed`` group — backend ``nccl``, which is
+RCCL over xGMI on MI355X (``gloo`` on CPU for tests) — and rank 0's folded
+weight blob is broadcast to all replicas in one collective, so every replica
+serves bit-identical weights without each one re-reading the model
+repository.  Per-replica statistics are all-reduced / all-gathered at the
+end of a benchmark.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def init_from_env(backend: str | None = None) -> DistInfo:
+    """Join the process group described by torchrun's env vars (no-op for world 1)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world <= 1:
+        return DistInfo(0, 1, local, "none")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    return DistInfo(rank, world, local, backend)
+
+
+def _dev(info: DistInfo) -> torch.device:
+    return torch.device("cuda", info.local_rank) if info.backend == "nccl" else torch.device("cpu")
+
+
+def broadcast_blob(blob: np.ndarray | None, info: DistInfo, src: int = 0) -> np.ndarray:
+    """Broadcast a uint8 blob from ``src`` to every rank (one RCCL broadcast over xGMI)."""
+    if info.world <= 1:
+        assert blob is not None
+        return blob
+    dev = _dev(info)
+    n = torch.tensor([blob.nbytes if blob is not None and info.rank == src else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(n, src)
+    if info.rank == src:
+        t = torch.from_numpy(np.ascontiguousarray(blob)).to(dev)
+    else:
+        t = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
+    dist.broadcast(t, src)
+    return t.cpu().numpy()
+
+
+def broadcast_object(obj, info: DistInfo, src: int = 0):
+    if info.world <= 1:
+        return obj
+    lst = [obj if info.rank == src else None]
+    dist.broadcast_object_list(lst, src, device=_dev(info) if info.backend == "nccl" else None)
+    return lst[0]
+
+
+def allreduce_max(v: float, info: DistInfo) -> float:
+    if info.world <= 1:
+        return float(v)
+    t = torch.tensor([float(v)], dtype=torch.float64, device=_dev(info))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allgather_floats(vals: list[float], info: DistInfo) -> list[list[float]]:
+    if info.world <= 1:
+        return [list(vals)]
+    out: list = [None] * info.world
+    dist.all_gather_object(out, list(vals))
+    return out
+
+
+def barrier(info: DistInfo) -> None:
+    if info.world > 1:
+        if info.backend == "nccl":
+            dist.barrier(device_ids=[info.local_rank])
+        else:
+            dist.barrier()
+
+
+def shutdown(info: DistInfo) -> None:
+    if info.world > 1 and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,118 @@
+"""Decode + NMS + crop plan/gather kernels vs the host reference (MI355X only)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from inference_arena_amd.models.yolov5nu import Detect
+from inference_arena_amd.ops import functional as AF
+from inference_arena_amd.ops import native
+from inference_arena_amd.postprocess import parse_yolo_output
+from inference_arena_amd.processing import MobileNetPreprocessor, extract_crop, scale_boxes
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_decode_nms(maps_nhwc, meta_images, device, conf=0.5, iou=0.45, max_det=300, cap=8400):
+    C = native()
+    B = maps_nhwc[0].shape[0]
+    meta, pool = AF.image_meta_bytes(meta_images, 640)
+    meta_t = torch.frombuffer(bytearray(meta), dtype=torch.uint8).to(device)
+    ctrl = AF.ctrl_tensor(B, device)
+    cand = torch.zeros(B, cap, 8, dtype=torch.int32, device=device)
+    cnt = torch.zeros(B, dtype=torch.int32, device=device)
+    s = torch.cuda.current_stream().cuda_stream
+    C.detect_decode({"head": [m.data_ptr() for m in maps_nhwc], "hw": [m.shape[1] for m in maps_nhwc],
+                     "xs": [m.shape[3] for m in maps_nhwc], "strides": [8.0, 16.0, 32.0], "B": B,
+                     "conf_thr": conf, "cand": cand.data_ptr(), "cand_count": cnt.data_ptr(), "cand_cap": cap,
+                     "ctrl": ctrl.data_ptr(), "stream": s})
+    det = torch.zeros(B, max_det, 8, dtype=torch.float32, device=device)
+    dcnt = torch.zeros(B, dtype=torch.int32, device=device)
+    C.nms({"cand": cand.data_ptr(), "cand_count": cnt.data_ptr(), "cand_cap": cap, "meta": meta_t.data_ptr(),
+           "B": B, "iou_thr": iou, "det": det.data_ptr(), "det_count": dcnt.data_ptr(), "max_det": max_det,
+           "ctrl": ctrl.data_ptr(), "stream": s})
+    torch.cuda.synchronize()
+    return det.cpu().numpy(), dcnt.cpu().numpy(), cnt.cpu().numpy(), (meta_t, pool, ctrl, det, dcnt)
+
+
+def _maps(models, imgs, shift=0.0):
+    from inference_arena_amd.processing import YOLOPreprocessor
+
+    y, _ = models
+    pre = YOLOPreprocessor()
+    x = torch.from_numpy(np.concatenate([pre(i).tensor for i in imgs]))
+    with torch.no_grad():
+        maps = y.head_maps(x)
+    maps = [torch.cat([m[:, :64], m[:, 64:] + shift], 1).to(torch.bfloat16).float() for m in maps]
+    return maps, pre
+
+
+@pytest.mark.parametrize("shift", [0.0, 8.0, 20.0])
+def test_decode_nms_matches_reference(device, models, shift):
+    from inference_arena_amd.data.synthetic import synthetic_images
+
+    imgs = synthetic_images(4, 77)
+    maps, pre = _maps(models, imgs, shift)
+    det_head: Detect = models[0].detect
+    ref_out = det_head.decode(maps).numpy()
+    nhwc = [m.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(device) for m in maps]
+    det, dcnt, ncand, _ = _run_decode_nms(nhwc, imgs, device)
+    for i, im in enumerate(imgs):
+        r = parse_yolo_output(ref_out[i:i + 1], 0.5, 0.45)
+        lb = pre(im)
+        r = scale_boxes(r, lb.scale, lb.padding, lb.original_shape) if len(r) else r
+        k = min(int(dcnt[i]), det.shape[1])
+        got = det[i, :k]
+        # same number of kept boxes (within 1% for razor-edge scores), same order of classes
+        assert abs(k - len(r)) <= max(1, len(r) // 100), (k, len(r), ncand[i])
+        m = min(k, len(r))
+        if m:
+            cls_got = got[:m, 5].copy().view(np.int32)
+            agree = (cls_got == r[:m, 5].astype(np.int32)).mean()
+            assert agree > 0.97
+            same = cls_got == r[:m, 5].astype(np.int32)
+            assert np.allclose(got[:m][same, :4], r[:m][same, :4], atol=0.5, rtol=1e-3)
+            assert np.allclose(got[:m][same, 4], r[:m][same, 4], atol=2e-3)
+
+
+def test_crop_plan_and_gather(device):
+    C = native()
+    rng = np.random.default_rng(3)
+    imgs = [rng.integers(0, 255, (480, 640, 3), dtype=np.uint8), rng.integers(0, 255, (300, 200, 3), dtype=np.uint8)]
+    boxes = [np.array([[10.7, 20.2, 300.9, 400.5], [600.0, 100.0, 640.0, 110.0], [5.0, 5.0, 5.5, 90.0]], np.float32),
+             np.array([[-3.0, 0.0, 150.2, 299.9]], np.float32)]
+    max_det = 8
+    det = np.zeros((2, max_det, 8), np.float32)
+    for i, bx in enumerate(boxes):
+        det[i, :len(bx), :4] = bx
+        det[i, :len(bx), 4] = 0.9
+    dcnt = np.array([len(b) for b in boxes], np.int32)
+    meta, pool = AF.image_meta_bytes(imgs, 640)
+    meta_t = torch.frombuffer(bytearray(meta), dtype=torch.uint8).to(device)
+    pool_t = torch.from_numpy(pool.copy()).to(device)
+    det_t, dcnt_t = torch.from_numpy(det).to(device), torch.from_numpy(dcnt).to(device)
+    crops = torch.zeros(2 * max_det, 8, dtype=torch.int32, device=device)
+    ctrl = AF.ctrl_tensor(2, device)
+    s = torch.cuda.current_stream().cuda_stream
+    C.crop_plan({"det": det_t.data_ptr(), "det_count": dcnt_t.data_ptr(), "max_det": max_det,
+                 "meta": meta_t.data_ptr(), "B": 2, "crops": crops.data_ptr(), "ctrl": ctrl.data_ptr(),
+                 "crop_cap": 16, "stream": s})
+    cap = 16
+    out = torch.zeros(cap, 112, 112, 16, dtype=torch.bfloat16, device=device)
+    mean, std = [0.485, 0.456, 0.406], [0.229, 0.224, 0.225]
+    C.crop_gather_s2d({"pool": pool_t.data_ptr(), "meta": meta_t.data_ptr(), "crops": crops.data_ptr(),
+                       "ctrl": ctrl.data_ptr(), "out": out.data_ptr(), "cap": cap, "S": 224, "mean": mean,
+                       "inv_std": [1 / v for v in std], "stream": s})
+    torch.cuda.synchronize()
+    c = ctrl.cpu().numpy()
+    assert c[3] == 4 and c[1] == 4  # total_crops, n_crops
+    got = AF.s2d_to_nchw(out.cpu()[:4])
+    pre = MobileNetPreprocessor()
+    k = 0
+    for i, bx in enumerate(boxes):
+        for b in bx:
+            ref = torch.from_numpy(pre(extract_crop(imgs[i], b)).tensor[0])
+            err = (got[k] - ref).abs()
+            assert err.max() < 3 * (1 / 255) / 0.224 + 0.05, (k, err.max())
+            k += 1

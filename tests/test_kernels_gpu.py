@@ -1,0 +1,182 @@
+"""HIP kernels vs plain PyTorch fp32 references of the same op (MI355X only)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from inference_arena_amd.ops import functional as AF
+from inference_arena_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2).float()
+
+
+def _ref_conv(x_nhwc, w, b, stride, pad, act, res=None):
+    y = F.conv2d(_nchw(x_nhwc).float(), _bf(w), b.float(), stride=stride, padding=pad)
+    if act == "silu":
+        y = F.silu(y)
+    elif act == "relu6":
+        y = F.relu6(y)
+    if res is not None:
+        y = y + _nchw(res).float()
+    return y
+
+
+def _check(got, ref, rtol=2e-2, atol=2e-2):
+    err = (got.float() - ref.float()).abs()
+    tol = atol + rtol * ref.float().abs()
+    bad = (err > tol).float().mean().item()
+    assert bad < 1e-3, f"{bad*100:.3f}% elements out of tolerance; max err {err.max().item():.4g}"
+
+
+def test_native_loaded():
+    C = native()
+    assert C.SIZEOF_IMAGE_META == 48 and C.SIZEOF_CANDIDATE == 32 and C.SIZEOF_TOPK == 64
+
+
+@pytest.mark.parametrize(
+    "B,H,Cin,Cout,k,s,act",
+    [
+        (2, 40, 32, 64, 3, 1, "silu"),
+        (2, 40, 64, 128, 3, 2, "silu"),
+        (1, 80, 16, 32, 3, 2, "silu"),  # Cin=16: k-groups straddle taps
+        (3, 20, 256, 128, 1, 1, "silu"),
+        (2, 28, 32, 144, 1, 1, "relu6"),  # 9 channel tiles (WC=3)
+        (1, 20, 80, 80, 3, 1, "silu"),  # Cin=80, Cout=80 (WC=5)
+        (2, 14, 96, 24, 1, 1, None),
+        (1, 7, 320, 1280, 1, 1, "relu6"),
+    ],
+)
+def test_conv_matches_torch(device, B, H, Cin, Cout, k, s, act):
+    g = torch.Generator().manual_seed(B * 1000 + H * 10 + Cin)
+    x = torch.randn(B, Cin, H, H, generator=g)
+    w = torch.randn(Cout, Cin, k, k, generator=g) / np.sqrt(Cin * k * k)
+    b = torch.randn(Cout, generator=g) * 0.1
+    xn = _nhwc(x).to(torch.bfloat16).to(device)
+    y = AF.conv2d_nhwc(xn, w, b, stride=s, act=act)
+    ref = _ref_conv(xn.cpu(), w, b, s, k // 2, act)
+    _check(_nchw(y.cpu()), ref)
+
+
+def test_conv_slices_residual_upsample(device):
+    g = torch.Generator().manual_seed(7)
+    B, H, Cbuf, Cin, Cout = 2, 20, 96, 32, 48
+    buf = torch.randn(B, H, H, Cbuf, generator=g).to(torch.bfloat16).to(device)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)
+    b = torch.randn(Cout, generator=g) * 0.1
+    out = torch.zeros(B, H, H, 128, dtype=torch.bfloat16, device=device)
+    res_buf = torch.randn(B, H, H, 64, generator=g).to(torch.bfloat16).to(device)
+    up = torch.zeros(B, 2 * H, 2 * H, 64, dtype=torch.bfloat16, device=device)
+    AF.conv2d_nhwc(buf, w, b, act="silu", x_coff=16, cin=Cin, out=out, out_coff=64, res=res_buf, res_coff=8,
+                   out2=up, out2_coff=8)
+    torch.cuda.synchronize()
+    xs = buf.cpu()[..., 16:16 + Cin]
+    ref = _ref_conv(xs, w, b, 1, 1, "silu", res=res_buf.cpu()[..., 8:8 + Cout])
+    _check(_nchw(out.cpu()[..., 64:64 + Cout]), ref)
+    assert out.cpu()[..., :64].abs().sum() == 0 and out.cpu()[..., 64 + Cout:].abs().sum() == 0
+    upref = F.interpolate(_nchw(out.cpu()[..., 64:64 + Cout]), scale_factor=2, mode="nearest")
+    assert torch.equal(_nchw(up.cpu()[..., 8:8 + Cout]), upref)
+
+
+def test_conv_fp32_out_and_live_batch(device):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(6, 1, 1, 1280, generator=g).to(torch.bfloat16).to(device)
+    w = torch.randn(1000, 1280, 1, 1, generator=g) / np.sqrt(1280)
+    b = torch.randn(1000, generator=g)
+    out = torch.full((6, 1, 1, 1000), -7.0, dtype=torch.float32, device=device)
+    bdev = torch.tensor([4], dtype=torch.int32, device=device)
+    AF.conv2d_nhwc(x, w, b, act=None, f32out=True, out=out, bdev=bdev)
+    torch.cuda.synchronize()
+    ref = x.cpu().float().reshape(6, 1280) @ _bf(w).reshape(1000, 1280).t() + b
+    _check(out.cpu().reshape(6, 1000)[:4], ref[:4], rtol=1e-2, atol=1e-2)
+    assert torch.all(out.cpu()[4:] == -7.0), "rows past the live batch must not be written"
+
+
+def test_stem_s2d_equivalence(device):
+    from inference_arena_amd.engine.plans import s2d_stem_3x3, s2d_stem_6x6
+
+    g = torch.Generator().manual_seed(11)
+    img = torch.rand(2, 3, 64, 64, generator=g)
+    s2d = img.reshape(2, 3, 32, 2, 32, 2).permute(0, 2, 4, 3, 5, 1).reshape(2, 32, 32, 12)
+    s2d = torch.cat([s2d, torch.zeros(2, 32, 32, 4)], -1).to(torch.bfloat16)
+    xin = s2d.to(device)
+    w6 = torch.randn(16, 3, 6, 6, generator=g) * 0.2
+    b = torch.zeros(16)
+    y = AF.conv2d_nhwc(xin, s2d_stem_6x6(w6), b, act=None)
+    ref = F.conv2d(_bf(img), _bf(w6), None, stride=2, padding=2)
+    _check(_nchw(y.cpu()), ref)
+    w3 = torch.randn(32, 3, 3, 3, generator=g) * 0.2
+    y3 = AF.conv2d_nhwc(xin, s2d_stem_3x3(w3), torch.zeros(32), pad=(1, 1), act=None, out_hw=(32, 32))
+    ref3 = F.conv2d(_bf(img), _bf(w3), None, stride=2, padding=1)
+    _check(_nchw(y3.cpu()), ref3)
+
+
+@pytest.mark.parametrize("C,H,s", [(96, 56, 2), (144, 28, 1), (960, 7, 1), (32, 112, 1)])
+def test_dwconv_matches_torch(device, C, H, s):
+    g = torch.Generator().manual_seed(C + H)
+    x = torch.randn(2, C, H, H, generator=g)
+    w = torch.randn(C, 1, 3, 3, generator=g) * 0.3
+    b = torch.randn(C, generator=g) * 0.1
+    xn = _nhwc(x).to(torch.bfloat16).to(device)
+    y = AF.dwconv3x3_nhwc(xn, w, b, stride=s, act="relu6")
+    ref = F.relu6(F.conv2d(_nchw(xn.cpu()), _bf(w), b, stride=s, padding=1, groups=C))
+    _check(_nchw(y.cpu()), ref)
+
+
+def test_sppf_matches_torch(device):
+    g = torch.Generator().manual_seed(5)
+    C = 128
+    buf = torch.zeros(2, 20, 20, 4 * C, dtype=torch.bfloat16)
+    buf[..., :C] = torch.randn(2, 20, 20, C, generator=g).to(torch.bfloat16)
+    d = buf.to(device)
+    AF.sppf_nhwc(d, C)
+    torch.cuda.synchronize()
+    x = _nchw(buf[..., :C])
+    y1 = F.max_pool2d(x, 5, 1, 2)
+    y2 = F.max_pool2d(y1, 5, 1, 2)
+    y3 = F.max_pool2d(y2, 5, 1, 2)
+    got = _nchw(d.cpu())
+    for i, ref in enumerate((y1, y2, y3)):
+        assert torch.equal(got[:, (i + 1) * C:(i + 2) * C], ref)
+
+
+def test_letterbox_matches_host(device):
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.processing import letterbox
+
+    imgs = synthetic_images(3, 5) + [np.random.default_rng(0).integers(0, 255, (300, 1000, 3), dtype=np.uint8)]
+    out = AF.letterbox_s2d(imgs, 640, device)
+    got = AF.s2d_to_nchw(out.cpu())
+    for i, im in enumerate(imgs):
+        ref = torch.from_numpy(letterbox(im, 640)[0].astype(np.float32).transpose(2, 0, 1) / 255.0)
+        err = (got[i] - ref).abs()
+        # bf16 storage (~3 significant digits) + at most one uint8 rounding step
+        assert (err <= 1.0 / 255 + 4e-3).float().mean() > 0.999, err.max()
+        assert err.max() < 3.0 / 255 + 4e-3
+
+
+def test_topk_and_avgpool(device):
+    g = torch.Generator().manual_seed(9)
+    logits = torch.randn(37, 1000, generator=g) * 3
+    idx, lg, pr = AF.topk_softmax(logits.to(device))
+    ref_v, ref_i = torch.topk(logits, 5, dim=1)
+    assert torch.equal(idx.long(), ref_i)
+    assert torch.allclose(lg, ref_v)
+    assert torch.allclose(pr, torch.softmax(logits, 1).gather(1, ref_i), rtol=1e-4, atol=1e-6)
+    x = torch.randn(5, 7, 7, 1280, generator=g).to(torch.bfloat16)
+    y = AF.avgpool_nhwc(x.to(device))
+    torch.cuda.synchronize()
+    _check(y.cpu().float(), x.float().mean((1, 2)), rtol=1e-2, atol=1e-2)

@@ -1,0 +1,88 @@
+"""End-to-end: native GPU pipeline vs the fp32 torch/NumPy reference pipeline."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _iou(a, b):
+    x1 = np.maximum(a[:, None, 0], b[None, :, 0])
+    y1 = np.maximum(a[:, None, 1], b[None, :, 1])
+    x2 = np.minimum(a[:, None, 2], b[None, :, 2])
+    y2 = np.minimum(a[:, None, 3], b[None, :, 3])
+    inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
+    aa = (a[:, 2] - a[:, 0]) * (a[:, 3] - a[:, 1])
+    bb = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    return inter / (aa[:, None] + bb[None, :] - inter + 1e-9)
+
+
+@pytest.fixture(scope="module")
+def dense_models():
+    from inference_arena_amd.models.zoo import make_mobilenet, make_yolo
+
+    return make_yolo(0, cls_shift=-14.0), make_mobilenet(1)
+
+
+@pytest.fixture(scope="module")
+def gpu_pipe(dense_models, device):
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    return GpuPipeline(*dense_models, device=0, buckets=[1, 4, 8])
+
+
+def test_pipeline_matches_reference(gpu_pipe, dense_models):
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.reference import ReferencePipeline
+
+    imgs = synthetic_images(6, 21)
+    ref = ReferencePipeline(*dense_models, device="cuda:0")
+    got = gpu_pipe.infer(imgs)
+    n_ref = n_match = n_cls = 0
+    corr = []
+    for im, g in zip(imgs, got):
+        r = ref(im)
+        n_ref += len(r)
+        if len(r) == 0 or len(g) == 0:
+            continue
+        iou = _iou(g.boxes, r.boxes)
+        for j in range(len(r)):
+            i = int(np.argmax(iou[:, j]))
+            if iou[i, j] > 0.9 and g.classes[i] == r.classes[j]:
+                n_match += 1
+                n_cls += int(g.topk_idx[i, 0] == r.topk_idx[j, 0])
+                corr.append(abs(g.topk_logit[i, 0] - r.topk_logit[j, 0]) / (abs(r.topk_logit[j, 0]) + 1.0))
+    assert n_ref > 5, "test images should produce detections"
+    assert n_match >= 0.9 * n_ref, (n_match, n_ref)
+    assert n_cls >= 0.8 * n_match, (n_cls, n_match)
+    assert np.median(corr) < 0.05
+
+
+def test_buckets_and_partial_batches(gpu_pipe):
+    from inference_arena_amd.data.synthetic import synthetic_images
+
+    imgs = synthetic_images(7, 5)
+    full = gpu_pipe.infer(imgs)  # bucket 8, 7 live images
+    single = [gpu_pipe.infer([im])[0] for im in imgs]  # bucket 1
+    for a, b in zip(full, single):
+        assert len(a) == len(b)
+        if len(a):
+            np.testing.assert_allclose(a.boxes, b.boxes, atol=1e-3)
+            np.testing.assert_array_equal(a.topk_idx, b.topk_idx)
+
+
+def test_overflow_crops_extra_pass(dense_models, device):
+    """More crops than one classification pass holds -> executor runs extra passes."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    tiny = GpuPipeline(*dense_models, device=0, buckets=[4], crop_cap_per_image=1)
+    big = GpuPipeline(*dense_models, device=0, buckets=[4], crop_cap_per_image=64)
+    imgs = synthetic_images(4, 21)
+    a, b = tiny.infer(imgs), big.infer(imgs)
+    assert sum(len(r) for r in a) > 16  # exceeds the tiny pass capacity (max(16, 4*1))
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x.topk_idx, y.topk_idx)
+        np.testing.assert_allclose(x.topk_logit, y.topk_logit, rtol=1e-5, atol=1e-5)
