@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -33,6 +35,10 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
   ARENA_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   ARENA_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   max_B_ = cfg_.max_batch;
+  {
+    const char* e = std::getenv("ARENA_DEBUG_SYNC");
+    debug_sync_ = e != nullptr ? std::atoi(e) : 0;
+  }
   alloc_slots();
   const int nthreads = std::max(1, cfg_.host_threads);
   for (int t = 0; t < nthreads; ++t) {
@@ -46,14 +52,16 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
           if (pool_stop_) return;
           seen = pool_gen_;
           jobs = pool_jobs_;
+          if (jobs == nullptr) continue;
+          ++pool_active_;
         }
         for (;;) {
           const int i = pool_next_.fetch_add(1);
-          if (jobs == nullptr || i >= (int)jobs->size()) break;
+          if (i >= (int)jobs->size()) break;
           (*jobs)[i]();
-          std::lock_guard<std::mutex> lk(pool_mu_);
-          if (--pool_pending_ == 0) pool_done_cv_.notify_all();
         }
+        std::lock_guard<std::mutex> lk(pool_mu_);
+        if (--pool_active_ == 0) pool_done_cv_.notify_all();
       }
     });
   }
@@ -170,9 +178,10 @@ void Executor::capture(Bucket& bk, int s) {
   hipGraph_t g = nullptr;
   ARENA_HIP_CHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
   try {
+    // The result D2H copy is issued after the graph launch, not captured: a
+    // captured device->pinned-host memcpy node faulted on ROCm 7.0 (torch's
+    // runtime) while the same graph without it runs cleanly.
     enqueue_program(prog_, bk, sl, compute_);
-    const size_t d2h = out_off_topk() + sizeof(TopkResult) * (size_t)bk.info.crop_cap;
-    ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
   } catch (...) {
     hipStreamEndCapture(compute_, &g);
     if (g) hipGraphDestroy(g);
@@ -394,11 +403,18 @@ void Executor::parallel_copy(std::vector<std::function<void()>>& jobs) {
   std::unique_lock<std::mutex> lk(pool_mu_);
   pool_jobs_ = &jobs;
   pool_next_ = 0;
-  pool_pending_ = (int)jobs.size();
   ++pool_gen_;
   pool_cv_.notify_all();
-  pool_done_cv_.wait(lk, [&] { return pool_pending_ == 0; });
-  pool_jobs_ = nullptr;
+  lk.unlock();
+  // the caller helps; workers that join late find the counter exhausted
+  for (;;) {
+    const int i = pool_next_.fetch_add(1);
+    if (i >= (int)jobs.size()) break;
+    jobs[i]();
+  }
+  lk.lock();
+  pool_jobs_ = nullptr;  // no worker can pick this generation up any more
+  pool_done_cv_.wait(lk, [&] { return pool_active_ == 0; });
 }
 
 int Executor::pick_bucket(int n) const {
@@ -459,7 +475,58 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   ARENA_HIP_CHECK(hipEventRecord(sl.copied, copy_));
   ARENA_HIP_CHECK(hipStreamWaitEvent(compute_, sl.copied, 0));
   ARENA_HIP_CHECK(hipEventRecord(sl.started, compute_));
-  ARENA_HIP_CHECK(hipGraphLaunch(buckets_.at(B).graph[s], compute_));
+  if (debug_sync_ >= 3) {
+    // 3: whole program as one graph without the D2H node, D2H issued eagerly after it.
+    // 4: whole program graph including the D2H node, built fresh.
+    Bucket& bk = buckets_.at(B);
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    const size_t d2h = out_off_topk() + sizeof(TopkResult) * (size_t)bk.info.crop_cap;
+    ARENA_HIP_CHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
+    enqueue_program(prog_, bk, sl, compute_);
+    if (debug_sync_ == 4) ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+    ARENA_HIP_CHECK(hipStreamEndCapture(compute_, &g));
+    ARENA_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    fprintf(stderr, "[arena debug] launching whole-program graph (mode %d)\n", debug_sync_);
+    ARENA_HIP_CHECK(hipGraphLaunch(ge, compute_));
+    ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+    fprintf(stderr, "[arena debug] graph done\n");
+    if (debug_sync_ == 3) ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+    ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+    hipGraphExecDestroy(ge);
+    hipGraphDestroy(g);
+  } else if (debug_sync_) {
+    // Eager, op-by-op execution with a device sync after every op (ARENA_DEBUG_SYNC=1):
+    // a faulting op is reported by index before the context is lost.
+    Bucket& bk = buckets_.at(B);
+    for (size_t i = 0; i < prog_.size(); ++i) {
+      fprintf(stderr, "[arena debug] op %zu type %lld\n", i, (long long)prog_[i][0]);
+      fflush(stderr);
+      std::vector<OpRecord> one(1, prog_[i]);
+      if (debug_sync_ == 2) {  // same op, but through a one-node hipGraph
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge = nullptr;
+        ARENA_HIP_CHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
+        enqueue_program(one, bk, sl, compute_);
+        ARENA_HIP_CHECK(hipStreamEndCapture(compute_, &g));
+        ARENA_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        ARENA_HIP_CHECK(hipGraphLaunch(ge, compute_));
+        ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+        hipGraphExecDestroy(ge);
+        hipGraphDestroy(g);
+      } else {
+        enqueue_program(one, bk, sl, compute_);
+      }
+      ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+    }
+    const size_t d2h = out_off_topk() + sizeof(TopkResult) * (size_t)bk.info.crop_cap;
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+  } else {
+    Bucket& bk = buckets_.at(B);
+    ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], compute_));
+    const size_t d2h = out_off_topk() + sizeof(TopkResult) * (size_t)bk.info.crop_cap;
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+  }
   ARENA_HIP_CHECK(hipEventRecord(sl.done, compute_));
   sl.busy = true;
   sl.bucket = B;

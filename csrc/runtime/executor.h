@@ -175,6 +175,7 @@ class Executor {
   std::map<int, Bucket> buckets_;
   Slot slots_[2];
   int next_slot_ = 0;
+  int debug_sync_ = 0;  // ARENA_DEBUG_SYNC: 1 eager op-by-op, 2 one graph per op
   std::mutex mu_;
   // host worker pool for packing images into pinned memory
   std::vector<std::thread> workers_;
@@ -182,7 +183,7 @@ class Executor {
   std::condition_variable pool_cv_, pool_done_cv_;
   std::vector<std::function<void()>>* pool_jobs_ = nullptr;
   std::atomic<int> pool_next_{0};
-  int pool_pending_ = 0;
+  int pool_active_ = 0;
   uint64_t pool_gen_ = 0;
   bool pool_stop_ = false;
 };

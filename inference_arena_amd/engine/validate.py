@@ -1,0 +1,127 @@
+"""Static bounds check of an executor program (runs on the CPU).
+
+Before a program is captured into a hipGraph, every op's device accesses are
+replayed symbolically against the buffer sizes of a bucket layout: each
+(view, pixel count, channel slice) must stay inside its buffer.  This catches
+planner bugs as exceptions on the host instead of GPU faults.
+"""
+from __future__ import annotations
+
+from ..engine.planner import (
+    BUF_CTRL,
+    BUF_DET,
+    BUF_DETCOUNT,
+    BUF_META,
+    BUF_NONE,
+    BUF_POOL,
+    BUF_TOPK,
+    CROPS,
+    OP_AVGPOOL,
+    OP_CONV,
+    OP_CROPGATHER,
+    OP_CROPPLAN,
+    OP_DECODE,
+    OP_DWCONV,
+    OP_LETTERBOX,
+    OP_NMS,
+    OP_SPPF,
+    OP_TOPK,
+    OP_ZERO,
+    Program,
+)
+
+CAND_BYTES, DET_BYTES, CROP_BYTES, TOPK_BYTES = 32, 32, 32, 64
+
+
+class ProgramError(ValueError):
+    pass
+
+
+def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand_cap: int) -> None:
+    sizes = {}
+    for b in prog.buffers:
+        sizes[b.id] = b.per_item * (crop_cap if b.kind == CROPS else B)
+    sizes[BUF_DET] = B * max_det * DET_BYTES
+    sizes[BUF_DETCOUNT] = B * 4
+    sizes[BUF_TOPK] = B * max_det * TOPK_BYTES
+    wbytes = prog.weights.nbytes
+    names = {b.id: b.name for b in prog.buffers}
+
+    def need(i, buf, lo, hi, what):
+        if buf in (BUF_CTRL, BUF_META, BUF_POOL):
+            return
+        if buf == BUF_NONE:
+            raise ProgramError(f"op {i}: {what} has no buffer")
+        cap = sizes.get(buf)
+        if cap is None:
+            raise ProgramError(f"op {i}: {what} references unknown buffer {buf}")
+        if lo < 0 or hi > cap:
+            raise ProgramError(f"op {i}: {what} accesses bytes [{lo}, {hi}) of {names.get(buf, buf)} ({cap} bytes)")
+
+    def view(i, buf, coff, cs, npix, C, elem, what):
+        if buf == BUF_NONE:
+            return
+        if cs < coff + C:
+            raise ProgramError(f"op {i}: {what} slice [{coff}, {coff + C}) exceeds pixel stride {cs}")
+        need(i, buf, coff * elem, ((npix - 1) * cs + coff + C) * elem, what)
+
+    def weights(i, off, n, what):
+        if off < 0 or off + n > wbytes:
+            raise ProgramError(f"op {i}: {what} reads weights [{off}, {off + n}) of {wbytes}")
+
+    for i, r in enumerate(prog.ops):
+        op = int(r[0])
+        kind_n = lambda k: crop_cap if int(k) == CROPS else B  # noqa: E731
+        if op == OP_CONV:
+            n = kind_n(r[30])
+            H, W, Cin, Ho, Wo, Cout, Cpad, KH, KW = (int(v) for v in (r[4], r[5], r[6], r[13], r[14], r[15], r[16],
+                                                                      r[17], r[18]))
+            kpad = int(r[8])
+            if kpad < KH * KW * Cin or kpad % 32 or Cpad % 16 or Cout > Cpad:
+                raise ProgramError(f"op {i}: bad conv geometry")
+            view(i, r[1], int(r[2]), int(r[3]), n * H * W, Cin, 2, "conv input")
+            oel = 4 if int(r[29]) else 2
+            view(i, r[10], int(r[11]), int(r[12]), n * Ho * Wo, Cout, oel, "conv output")
+            view(i, r[22], int(r[23]), int(r[24]), n * Ho * Wo, Cout, 2, "conv residual")
+            view(i, r[25], int(r[26]), int(r[27]), n * 4 * Ho * Wo, Cout, 2, "conv upsampled output")
+            weights(i, int(r[7]), Cpad * kpad * 2, "conv weight")
+            weights(i, int(r[9]), Cpad * 4, "conv bias")
+        elif op == OP_DWCONV:
+            n = kind_n(r[16])
+            H, W, C, Ho, Wo = (int(v) for v in (r[4], r[5], r[6], r[12], r[13]))
+            view(i, r[1], int(r[2]), int(r[3]), n * H * W, C, 2, "dw input")
+            view(i, r[9], int(r[10]), int(r[11]), n * Ho * Wo, C, 2, "dw output")
+            weights(i, int(r[7]), 9 * C * 2, "dw weight")
+            weights(i, int(r[8]), C * 4, "dw bias")
+        elif op == OP_SPPF:
+            n = kind_n(r[7])
+            view(i, r[1], int(r[2]), int(r[3]), n * int(r[4]) * int(r[5]), 4 * int(r[6]), 2, "sppf buffer")
+        elif op == OP_LETTERBOX:
+            T2 = int(r[2]) // 2
+            need(i, r[1], 0, B * T2 * T2 * 32, "letterbox output")
+        elif op == OP_ZERO:
+            need(i, r[1], 0, int(r[2]) * kind_n(r[3]), "zero")
+        elif op == OP_DECODE:
+            for lvl in range(3):
+                buf, coff, cs, hw = (int(v) for v in r[1 + 4 * lvl: 5 + 4 * lvl])
+                view(i, buf, coff, cs, B * hw * hw, 144, 2, f"decode head {lvl}")
+            need(i, r[16], 0, B * cand_cap * CAND_BYTES, "candidates")
+            need(i, r[17], 0, B * 4, "candidate counts")
+        elif op == OP_NMS:
+            need(i, r[1], 0, B * cand_cap * CAND_BYTES, "nms candidates")
+            need(i, r[3], 0, B * max_det * DET_BYTES, "nms detections")
+        elif op == OP_CROPPLAN:
+            need(i, r[3], 0, B * max_det * CROP_BYTES, "crop refs")
+        elif op == OP_CROPGATHER:
+            S2 = int(r[3]) // 2
+            need(i, r[1], 0, B * max_det * CROP_BYTES, "crop refs")
+            need(i, r[2], 0, crop_cap * S2 * S2 * 32, "crop gather output")
+        elif op == OP_AVGPOOL:
+            n = kind_n(r[5])
+            need(i, r[1], 0, n * int(r[2]) * int(r[3]) * 2, "avgpool input")
+            need(i, r[4], 0, n * int(r[3]) * 2, "avgpool output")
+        elif op == OP_TOPK:
+            need(i, r[1], 0, crop_cap * int(r[3]) * 4, "topk logits")
+            need(i, r[4], 0, B * max_det * TOPK_BYTES, "topk results")
+        else:
+            raise ProgramError(f"op {i}: unknown op {op}")

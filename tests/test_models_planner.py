@@ -1,0 +1,139 @@
+"""Model oracles, BN folding, stem rewrites and the executor program planner (CPU)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from inference_arena_amd.engine.planner import (
+    CROPS,
+    IMAGES,
+    OP_CONV,
+    OP_FIELDS,
+    ProgramBuilder,
+    View,
+    layout,
+    pack_conv_weight,
+)
+from inference_arena_amd.engine.plans import plan_pipeline, s2d_stem_3x3, s2d_stem_6x6
+from inference_arena_amd.models.common import ConvBNAct, fold, init_random_
+from inference_arena_amd.models.mobilenetv2 import MobileNetV2
+from inference_arena_amd.models.yolov5nu import YOLOv5nu
+
+
+def test_yolo_output_contract():
+    m = init_random_(YOLOv5nu(), 0).eval()
+    with torch.no_grad():
+        y = m(torch.rand(1, 3, 320, 320))
+    assert y.shape == (1, 84, 2100)  # (40^2 + 20^2 + 10^2) anchors at 320
+    assert (y[:, 4:] >= 0).all() and (y[:, 4:] <= 1).all()
+    n_conv = sum(isinstance(x, torch.nn.Conv2d) for x in m.modules())
+    assert n_conv == 75
+
+
+def test_mobilenet_output_contract():
+    m = init_random_(MobileNetV2(), 1).eval()
+    with torch.no_grad():
+        y = m(torch.randn(2, 3, 224, 224))
+    assert y.shape == (2, 1000)
+    assert sum(isinstance(x, torch.nn.Conv2d) for x in m.modules()) == 52
+    macs = 0
+    hooks = []
+
+    def hk(mod, i, o):
+        nonlocal macs
+        macs += o.numel() // o.shape[0] * mod.in_channels // mod.groups * mod.kernel_size[0] * mod.kernel_size[1]
+
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            hooks.append(mod.register_forward_hook(hk))
+    with torch.no_grad():
+        m(torch.randn(1, 3, 224, 224))
+    macs += 1280 * 1000
+    assert 295e6 < macs < 305e6  # 0.30 GMAC
+
+
+def test_bn_fold_equivalence():
+    torch.manual_seed(0)
+    blk = init_random_(torch.nn.Sequential(ConvBNAct(8, 16, 3, 2)), 3)[0].eval()
+    x = torch.randn(2, 8, 9, 9)
+    w, b = fold(blk)
+    with torch.no_grad():
+        ref = blk(x)
+        got = F.silu(F.conv2d(x, w, b, stride=2, padding=1))
+    assert torch.allclose(ref, got, atol=1e-5)
+
+
+def _s2d(img):
+    B, C, H, W = img.shape
+    s = img.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 3, 5, 1, 2, 4).reshape(B, 12, H // 2, W // 2)
+    return torch.cat([s, torch.zeros(B, 4, H // 2, W // 2)], 1)
+
+
+def test_space_to_depth_stems():
+    g = torch.Generator().manual_seed(0)
+    img = torch.randn(2, 3, 32, 32, generator=g)
+    w6 = torch.randn(8, 3, 6, 6, generator=g)
+    ref = F.conv2d(img, w6, stride=2, padding=2)
+    got = F.conv2d(_s2d(img), s2d_stem_6x6(w6), stride=1, padding=1)
+    assert torch.allclose(ref, got, atol=1e-4)
+    w3 = torch.randn(8, 3, 3, 3, generator=g)
+    ref3 = F.conv2d(img, w3, stride=2, padding=1)
+    got3 = F.conv2d(F.pad(_s2d(img), (1, 0, 1, 0)), s2d_stem_3x3(w3))
+    assert torch.allclose(ref3, got3, atol=1e-4)
+
+
+def test_pack_conv_weight_layout():
+    w = torch.arange(2 * 3 * 2 * 2, dtype=torch.float32).reshape(2, 3, 2, 2)
+    wb, bb, kpad, cpad = pack_conv_weight(w, torch.ones(2))
+    assert kpad == 32 and cpad == 16
+    arr = torch.frombuffer(bytearray(wb), dtype=torch.bfloat16).float().reshape(cpad, kpad)
+    # k = (kh*KW + kw)*Cin + ci
+    assert arr[1, (1 * 2 + 0) * 3 + 2].item() == w[1, 2, 1, 0].item()
+    assert arr[2:].abs().sum() == 0 and arr[:, 12:].abs().sum() == 0
+
+
+@pytest.fixture(scope="module")
+def program(models):
+    return plan_pipeline(*models, conf_thr=0.5, iou_thr=0.45)
+
+
+def test_program_shape(program):
+    assert program.ops.shape[1] == OP_FIELDS
+    convs = int((program.ops[:, 0] == OP_CONV).sum())
+    # 75 YOLO convs lowered to 65 (C3 cv1+cv2 and the two detect branches' first convs fused),
+    # 35 MobileNet convs (stem + 16 expand + 17 project + head) + FC
+    assert convs == 65 + 35
+    assert program.cls_ops.shape[0] < program.ops.shape[0]
+    assert program.weights.nbytes % 256 == 0
+
+
+@pytest.mark.parametrize("B", [1, 7, 32])
+def test_layout_respects_lifetimes(program, B):
+    crops = max(16, 8 * B)
+    offs, total = layout(program.buffers, B, crops)
+    bufs = [b for b in program.buffers if b.last >= 0]
+    for i, a in enumerate(bufs):
+        sa = a.per_item * (crops if a.kind == CROPS else B)
+        assert offs[a.id] % 256 == 0 and offs[a.id] + sa <= total
+        for b in bufs[i + 1:]:
+            if a.last < b.first or b.last < a.first:
+                continue
+            sb = b.per_item * (crops if b.kind == CROPS else B)
+            assert offs[a.id] + sa <= offs[b.id] or offs[b.id] + sb <= offs[a.id], (a.name, b.name)
+    naive = sum(b.per_item * (crops if b.kind == CROPS else B) for b in bufs)
+    assert total < 0.5 * naive
+
+
+def test_builder_validates_shapes():
+    pb = ProgramBuilder()
+    a = pb.tensor("a", 8, 8, 16)
+    b = pb.tensor("b", 8, 8, 32)
+    with pytest.raises(ValueError):
+        pb.conv(View(a, 0, 16), View(b, 0, 32), torch.zeros(32, 8, 1, 1), torch.zeros(32))
+    with pytest.raises(ValueError):
+        pb.tensor("bad", 4, 4, 12)
+    pb.conv(View(a, 0, 16), View(b, 0, 32), torch.zeros(32, 16, 3, 3), torch.zeros(32), stride=1)
+    prog = pb.build()
+    assert prog.ops[0, 13] == 8 and prog.ops[0, 30] == IMAGES
