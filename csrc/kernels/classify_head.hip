@@ -94,3 +94,27 @@ void topk_softmax(const TopkParams& p, hipStream_t s) {
 }
 
 }  // namespace arena
+
+namespace arena {
+
+// Zero-fill used inside captured graphs instead of hipMemsetAsync: memset
+// nodes of a hipGraph captured before PyTorch's first H2D copies stopped
+// taking effect afterwards on ROCm 7.0 (kernel nodes were unaffected), so
+// the executor's graphs contain kernel nodes only.
+__global__ __launch_bounds__(256) void zero_fill_kernel(uint4* p, size_t n16, uint8_t* tail, int n_tail) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) p[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (i < (size_t)n_tail) tail[i] = 0;
+}
+
+void zero_fill(void* ptr, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return;
+  if (((uintptr_t)ptr & 15) != 0) throw std::runtime_error("zero_fill: pointer must be 16-byte aligned");
+  const size_t n16 = bytes / 16;
+  const int n_tail = (int)(bytes - n16 * 16);
+  const size_t threads = n16 > (size_t)n_tail ? n16 : (size_t)n_tail;
+  hipLaunchKernelGGL(zero_fill_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, (uint4*)ptr, n16,
+                     (uint8_t*)ptr + n16 * 16, n_tail);
+}
+
+}  // namespace arena

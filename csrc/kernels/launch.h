@@ -196,4 +196,7 @@ struct TopkParams {
 };
 void topk_softmax(const TopkParams& p, hipStream_t s);
 
+// Graph-safe memset replacement (kernel node).
+void zero_fill(void* ptr, size_t bytes, hipStream_t s);
+
 }  // namespace arena

@@ -38,6 +38,8 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
   {
     const char* e = std::getenv("ARENA_DEBUG_SYNC");
     debug_sync_ = e != nullptr ? std::atoi(e) : 0;
+    const char* c = std::getenv("ARENA_COPY_MODE");
+    copy_mode_ = c != nullptr ? std::atoi(c) : 0;
   }
   alloc_slots();
   const int nthreads = std::max(1, cfg_.host_threads);
@@ -128,8 +130,14 @@ void Executor::alloc_slots() {
 
 void Executor::set_weights(const void* host, size_t bytes) {
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
-  if (d_weights_) ARENA_HIP_CHECK(hipFree(d_weights_));
-  ARENA_HIP_CHECK(hipMalloc(&d_weights_, bytes));
+  if (d_weights_ != nullptr && bytes != weights_bytes_) {
+    // captured graphs hold the weight pointer: only a same-size in-place update is allowed
+    if (!buckets_.empty()) throw std::runtime_error("set_weights: size change after buckets were captured");
+    ARENA_HIP_CHECK(hipFree(d_weights_));
+    d_weights_ = nullptr;
+  }
+  if (d_weights_ == nullptr) ARENA_HIP_CHECK(hipMalloc(&d_weights_, bytes));
+  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
   ARENA_HIP_CHECK(hipMemcpy(d_weights_, host, bytes, hipMemcpyHostToDevice));
   weights_bytes_ = bytes;
 }
@@ -169,6 +177,15 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
   ARENA_HIP_CHECK(hipMalloc(&bk.d_arena, std::max<int64_t>(arena_bytes, 256)));
   ARENA_HIP_CHECK(hipMemset(bk.d_arena, 0, std::max<int64_t>(arena_bytes, 256)));
   for (int s = 0; s < 2; ++s) capture(bk, s);
+  if (debug_sync_ || std::getenv("ARENA_DEBUG_ALLOC")) {
+    fprintf(stderr, "[arena alloc] bucket %d arena %p..%p (%lld B)\n", B, (void*)bk.d_arena,
+            (void*)(bk.d_arena + arena_bytes), (long long)arena_bytes);
+    for (int s = 0; s < 2; ++s)
+      fprintf(stderr, "[arena alloc] slot %d in %p..%p out %p..%p\n", s, (void*)slots_[s].d_in,
+              (void*)(slots_[s].d_in + in_bytes_total()), (void*)slots_[s].d_out,
+              (void*)(slots_[s].d_out + out_bytes_total()));
+    fprintf(stderr, "[arena alloc] weights %p..%p\n", (void*)d_weights_, (void*)(d_weights_ + weights_bytes_));
+  }
 }
 
 void Executor::capture(Bucket& bk, int s) {
@@ -300,7 +317,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       case OP_ZERO: {
         uint8_t* ptr = resolve(bk, sl, r[1], 0, 1);
         const size_t bytes = (size_t)r[2] * batch(r[3]);
-        ARENA_HIP_CHECK(hipMemsetAsync(ptr, 0, bytes, s));
+        zero_fill(ptr, bytes, s);
         break;
       }
       case OP_DECODE: {
@@ -471,9 +488,14 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   ctrl->n_images = n;
   ctrl->crop_base = 0;
   const size_t bytes = in_bytes_meta() + off;
-  ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, copy_));
-  ARENA_HIP_CHECK(hipEventRecord(sl.copied, copy_));
-  ARENA_HIP_CHECK(hipStreamWaitEvent(compute_, sl.copied, 0));
+  if (copy_mode_ == 2) {
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, compute_));
+  } else {
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, copy_));
+    ARENA_HIP_CHECK(hipEventRecord(sl.copied, copy_));
+    if (copy_mode_ == 1) ARENA_HIP_CHECK(hipEventSynchronize(sl.copied));
+    ARENA_HIP_CHECK(hipStreamWaitEvent(compute_, sl.copied, 0));
+  }
   ARENA_HIP_CHECK(hipEventRecord(sl.started, compute_));
   if (debug_sync_ >= 3) {
     // 3: whole program as one graph without the D2H node, D2H issued eagerly after it.
@@ -571,7 +593,9 @@ BatchResult Executor::collect(int s) {
       c.crop_base = base;
       c.total_crops = total;
       c.n_crops = std::min(CC, total - base);
-      ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, &c, sizeof(Ctrl), hipMemcpyHostToDevice, compute_));
+      // previous pass must have consumed the control block before it is rewritten
+      ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+      ARENA_HIP_CHECK(hipMemcpy(sl.d_in, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
       enqueue_program(cls_prog_, bk, sl, compute_);
     }
     uint8_t* src = sl.d_out + out_off_topk() + sizeof(TopkResult) * (size_t)CC;

@@ -175,6 +175,7 @@ class Executor {
   std::map<int, Bucket> buckets_;
   Slot slots_[2];
   int next_slot_ = 0;
+  int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on compute stream
   int debug_sync_ = 0;  // ARENA_DEBUG_SYNC: 1 eager op-by-op, 2 one graph per op
   std::mutex mu_;
   // host worker pool for packing images into pinned memory

@@ -170,8 +170,8 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std)
     pb.avgpool(HD, PO)
     ncls = m.fc.out_features
     LG = pb.tensor("m.logits", 1, 1, ncls + (-ncls % 8), kind=CROPS, elem=4)
-    wfc = m.fc.weight.detach().float().reshape(ncls, 1280, 1, 1)
-    pb.conv(View(PO, 0, 1280), View(LG, 0, ncls), wfc, m.fc.bias.detach().float(), act=None, f32out=True,
+    wfc = m.fc.weight.detach().float().cpu().reshape(ncls, 1280, 1, 1)
+    pb.conv(View(PO, 0, 1280), View(LG, 0, ncls), wfc, m.fc.bias.detach().float().cpu(), act=None, f32out=True,
             kind=CROPS)
     pb.topk(LG, ncls, LG.C)
 

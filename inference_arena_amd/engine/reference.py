@@ -8,6 +8,8 @@ It is the CPU arm of the arena and the end-to-end oracle of GpuPipeline.
 """
 from __future__ import annotations
 
+import copy
+
 import numpy as np
 import torch
 
@@ -21,8 +23,8 @@ from .pipeline import ImageResult
 class ReferencePipeline:
     def __init__(self, yolo: YOLOv5nu, mnet: MobileNetV2, conf_thr: float = 0.5, iou_thr: float = 0.45,
                  device: str | torch.device = "cpu", max_det: int | None = None):
-        self.yolo = yolo.to(device).eval()
-        self.mnet = mnet.to(device).eval()
+        self.yolo = copy.deepcopy(yolo).to(device).eval()
+        self.mnet = copy.deepcopy(mnet).to(device).eval()
         self.device = torch.device(device)
         self.conf_thr, self.iou_thr = conf_thr, iou_thr
         self.max_det = max_det

@@ -35,13 +35,13 @@ class ConvBNAct(nn.Module):
 
 def fold_conv_bn(conv: nn.Conv2d, bn: nn.BatchNorm2d | None) -> tuple[torch.Tensor, torch.Tensor]:
     """Fold an eval-mode BatchNorm into the preceding conv: (weight, bias) fp32."""
-    w = conv.weight.detach().float()
-    b = conv.bias.detach().float() if conv.bias is not None else torch.zeros(w.shape[0])
+    w = conv.weight.detach().float().cpu()
+    b = conv.bias.detach().float().cpu() if conv.bias is not None else torch.zeros(w.shape[0])
     if bn is None:
         return w.clone(), b.clone()
-    scale = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+    scale = bn.weight.detach().float().cpu() / torch.sqrt(bn.running_var.detach().float().cpu() + bn.eps)
     w = w * scale.view(-1, 1, 1, 1)
-    b = (b - bn.running_mean.detach().float()) * scale + bn.bias.detach().float()
+    b = (b - bn.running_mean.detach().float().cpu()) * scale + bn.bias.detach().float().cpu()
     return w, b
 
 

@@ -1,0 +1,100 @@
+"""Pieces shared by the HTTP front-ends of all topologies.
+
+* request-id + JSON logging per request (reference: architectures/*/app/
+  main.py sets ``request_id_var`` from a uuid4 and logs endpoint / latency /
+  detections / status_code);
+* multipart ``file`` extraction and image decoding on a bounded thread pool
+  (PIL releases the GIL while decoding, so decoding scales with cores instead
+  of blocking the event loop);
+* result -> ``PredictResponse`` conversion with the per-topology confidence
+  semantics (raw top-1 logit for monolithic / gateway, softmax probability
+  for microservices — the reference's behaviour);
+* optional fault injection (``ARENA_FAULT_EVERY=k`` fails every k-th request)
+  to exercise client/error paths.
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import logging
+import time
+import uuid
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+from fastapi import HTTPException, Request
+
+from ..engine.pipeline import ImageResult
+from ..processing import load_image_from_bytes
+from ..utils.logging import request_id_var
+from .multipart import MultipartError, parse_multipart
+from .schemas import Classification, DetectionBox, DetectionWithClassification, PredictResponse
+
+log = logging.getLogger("arena.server")
+
+
+class DecodePool:
+    def __init__(self, threads: int = 8):
+        self.pool = ThreadPoolExecutor(max_workers=max(1, threads), thread_name_prefix="decode")
+
+    async def decode(self, data: bytes) -> np.ndarray:
+        return await asyncio.get_running_loop().run_in_executor(self.pool, load_image_from_bytes, data)
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=False)
+
+
+async def read_upload(request: Request, field: str = "file") -> bytes:
+    body = await request.body()
+    ctype = request.headers.get("content-type", "")
+    if ctype.lower().startswith("multipart/form-data"):
+        try:
+            parts = parse_multipart(body, ctype)
+        except MultipartError as e:
+            raise HTTPException(status_code=422, detail=str(e)) from e
+        if field not in parts:
+            raise HTTPException(status_code=422, detail=f"missing form field '{field}'")
+        return parts[field][0]
+    if body:
+        return body  # raw image body (application/octet-stream, image/jpeg)
+    raise HTTPException(status_code=422, detail="empty request body")
+
+
+def to_response(rid: str, res: ImageResult, labels: list[str], timing: dict, confidence: str = "logit"
+                ) -> PredictResponse:
+    dets = []
+    for i in range(len(res)):
+        b = res.boxes[i]
+        cid = int(res.topk_idx[i, 0]) if res.topk_idx.shape[0] > i else -1
+        conf = float(res.topk_prob[i, 0] if confidence == "softmax" else res.topk_logit[i, 0]) if cid >= 0 else 0.0
+        dets.append(DetectionWithClassification(
+            detection=DetectionBox(x1=float(b[0]), y1=float(b[1]), x2=float(b[2]), y2=float(b[3]),
+                                   confidence=float(res.scores[i]), class_id=int(res.classes[i])),
+            classification=Classification(class_id=cid, class_name=labels[cid] if 0 <= cid < len(labels) else "",
+                                          confidence=conf),
+        ))
+    return PredictResponse(request_id=rid, detections=dets, timing={k: float(v) for k, v in timing.items()})
+
+
+class FaultInjector:
+    def __init__(self, every: int = 0):
+        self.every = int(every)
+        self._n = itertools.count(1)
+
+    def check(self) -> None:
+        if self.every > 0 and next(self._n) % self.every == 0:
+            raise RuntimeError("injected fault (ARENA_FAULT_EVERY)")
+
+
+def new_request_id() -> str:
+    rid = str(uuid.uuid4())
+    request_id_var.set(rid)
+    return rid
+
+
+class Timer:
+    def __init__(self):
+        self.t0 = time.perf_counter()
+
+    def ms(self) -> float:
+        return (time.perf_counter() - self.t0) * 1e3

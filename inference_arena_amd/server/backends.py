@@ -1,0 +1,173 @@
+"""Inference backends shared by every serving topology.
+
+``GpuBatchedBackend``  the MI355X path: requests (decoded RGB) go into the
+                       native DynamicBatcher (csrc/runtime/batcher.cpp) over
+                       one or more Executor instances; completion callbacks
+                       resolve asyncio futures, so the event loop never blocks
+                       (the reference's ``async def predict`` calls blocking
+                       ONNX Runtime inline and serialises every request,
+                       architectures/monolithic/app/main.py:102-159).
+``CpuReferenceBackend`` the reference-equivalent CPU arm (BASELINE config 1):
+                       the fp32 torch oracles with the upstream 2 intra-op
+                       threads, one request at a time.
+
+Both return ``ImageResult`` + a timing dict with the reference's keys
+(detection_ms, classification_ms, total_ms) plus queue_ms / gpu_ms /
+batch_size.
+"""
+from __future__ import annotations
+
+import asyncio
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from ..engine.pipeline import ImageResult
+
+
+class Overloaded(RuntimeError):
+    """The request queue is full (maps to HTTP 503)."""
+
+
+class Backend:
+    name = "backend"
+
+    def ready(self) -> bool:
+        return True
+
+    async def infer(self, image: np.ndarray) -> tuple[ImageResult, dict]:
+        raise NotImplementedError
+
+    def stats(self) -> dict:
+        return {}
+
+    def close(self) -> None:
+        pass
+
+
+def _result_from_dict(d: dict) -> ImageResult:
+    det = d["det"]
+    return ImageResult(
+        boxes=det[:, :4].copy(),
+        scores=det[:, 4].copy(),
+        classes=det[:, 5].copy().view(np.int32),
+        topk_idx=d["topk_idx"],
+        topk_logit=d["topk_logit"],
+        topk_prob=d["topk_prob"],
+        det_count=int(d["det_count"]),
+    )
+
+
+class GpuBatchedBackend(Backend):
+    name = "gpu"
+
+    def __init__(self, yolo, mnet, *, device: int = 0, instances: int = 1, max_batch: int = 32,
+                 preferred: list[int] | None = None, max_queue_delay_us: int = 500, max_queue_size: int = 4096,
+                 buckets: list[int] | None = None, weights: np.ndarray | None = None):
+        from ..engine.pipeline import GpuPipeline
+        from ..ops import native
+
+        bk = buckets or sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
+        self.pipes = [GpuPipeline(yolo, mnet, device=device, buckets=bk, weights=weights) for _ in range(instances)]
+        self.batcher = native().DynamicBatcher([p.ex for p in self.pipes], {
+            "max_batch": max_batch,
+            "preferred": preferred or [],
+            "max_queue_delay_us": max_queue_delay_us,
+            "max_queue_size": max_queue_size,
+        })
+        self.device = device
+        self._closed = False
+
+    async def infer(self, image: np.ndarray) -> tuple[ImageResult, dict]:
+        loop = asyncio.get_running_loop()
+        fut: asyncio.Future = loop.create_future()
+        t0 = time.perf_counter()
+
+        def done(d):
+            loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(d))
+
+        rid = self.batcher.enqueue(np.ascontiguousarray(image, dtype=np.uint8), done)
+        if rid < 0:
+            raise Overloaded("inference queue full")
+        d = await fut
+        if d["error"]:
+            raise RuntimeError(d["error"])
+        total = (time.perf_counter() - t0) * 1e3
+        q = d["queue_us"] / 1e3
+        gpu = d["compute_us"] / 1e3
+        timing = {"queue_ms": q, "gpu_ms": gpu, "batch_size": float(d["batch_size"]),
+                  "detection_ms": q + gpu, "classification_ms": 0.0, "inference_ms": total}
+        return _result_from_dict(d), timing
+
+    def stats(self) -> dict:
+        return dict(self.batcher.stats())
+
+    def close(self) -> None:
+        if not self._closed:
+            self.batcher.shutdown()
+            self._closed = True
+
+
+class CpuReferenceBackend(Backend):
+    name = "cpu"
+
+    def __init__(self, yolo, mnet, *, threads: int = 2, conf_thr: float = 0.5, iou_thr: float = 0.45):
+        import torch
+
+        from ..engine.reference import ReferencePipeline
+
+        torch.set_num_threads(threads)
+        self.ref = ReferencePipeline(yolo, mnet, conf_thr=conf_thr, iou_thr=iou_thr, device="cpu")
+        # one worker: the reference processes requests one at a time
+        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="cpu-infer")
+        self.lock = threading.Lock()
+
+    def _run(self, image: np.ndarray):
+        from ..processing import extract_crop
+
+        with self.lock:
+            t0 = time.perf_counter()
+            det = self.ref.detect(image)
+            t1 = time.perf_counter()
+            logits = self.ref.classify([extract_crop(image, d) for d in det])
+            t2 = time.perf_counter()
+        k = len(det)
+        order = np.argsort(-logits, axis=1, kind="stable")[:, :5] if k else np.zeros((0, 5), np.int64)
+        top = np.take_along_axis(logits, order, 1) if k else np.zeros((0, 5), np.float32)
+        if k:
+            z = np.exp(logits - logits.max(1, keepdims=True))
+            prob = np.take_along_axis(z / z.sum(1, keepdims=True), order, 1)
+        else:
+            prob = np.zeros((0, 5), np.float32)
+        res = ImageResult(boxes=det[:, :4].astype(np.float32) if k else np.zeros((0, 4), np.float32),
+                          scores=det[:, 4].astype(np.float32) if k else np.zeros((0,), np.float32),
+                          classes=det[:, 5].astype(np.int32) if k else np.zeros((0,), np.int32),
+                          topk_idx=order.astype(np.int32), topk_logit=top.astype(np.float32),
+                          topk_prob=prob.astype(np.float32), det_count=k)
+        return res, {"detection_ms": (t1 - t0) * 1e3, "classification_ms": (t2 - t1) * 1e3}
+
+    async def infer(self, image: np.ndarray) -> tuple[ImageResult, dict]:
+        loop = asyncio.get_running_loop()
+        return await loop.run_in_executor(self.pool, self._run, image)
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=False)
+
+
+def build_backend(settings, *, arch: str = "monolithic") -> Backend:
+    """Backend selected by ARENA_DEVICE (gpu | cpu) with the arena's default models."""
+    from ..config import get_triton_config
+    from ..models.zoo import default_models
+
+    yolo, mnet = default_models(int(settings.ARENA_WEIGHT_SEED))
+    if settings.ARENA_DEVICE == "cpu":
+        from ..config import get_controlled_variable
+
+        return CpuReferenceBackend(yolo, mnet, threads=int(get_controlled_variable("onnx_runtime",
+                                                                                     "intra_op_num_threads")))
+    db = get_triton_config().get("dynamic_batching", {}) or {}
+    return GpuBatchedBackend(yolo, mnet, device=int(settings.ARENA_GPU), max_batch=int(settings.ARENA_MAX_BATCH),
+                             preferred=list(db.get("preferred_batch_size", [])),
+                             max_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))

@@ -1,0 +1,66 @@
+"""Environment-driven service settings (pydantic-settings replacement).
+
+The reference configures each service with pydantic-settings classes
+(architectures/*/app/config.py: LOG_LEVEL, PORT, MODELS_DIR,
+CLASSIFICATION_GRPC_ENDPOINT, LABELS_FILE, TRITON_GRPC_ENDPOINT,
+TRITON_TIMEOUT_SECONDS; case-sensitive names, optional .env file).
+pydantic-settings is not installed here, so ``Settings`` reads the same
+variables from the environment and an optional ``.env`` file itself and
+validates them with pydantic.
+"""
+from __future__ import annotations
+
+import functools
+import os
+from pathlib import Path
+
+from pydantic import BaseModel
+
+
+def _read_dotenv(path: Path) -> dict[str, str]:
+    out: dict[str, str] = {}
+    if not path.exists():
+        return out
+    for line in path.read_text(encoding="utf-8").splitlines():
+        line = line.strip()
+        if not line or line.startswith("#") or "=" not in line:
+            continue
+        k, v = line.split("=", 1)
+        out[k.strip()] = v.strip().strip('"').strip("'")
+    return out
+
+
+class Settings(BaseModel):
+    LOG_LEVEL: str = "INFO"
+    PORT: int = 8100
+    HOST: str = "0.0.0.0"
+    MODELS_DIR: str = "model_repository"
+    LABELS_FILE: str = ""
+    CLASSIFICATION_GRPC_ENDPOINT: str = "127.0.0.1:8201"
+    TRITON_GRPC_ENDPOINT: str = "127.0.0.1:8001"
+    TRITON_HTTP_ENDPOINT: str = "127.0.0.1:8000"
+    TRITON_TIMEOUT_SECONDS: float = 60.0
+    # arena additions
+    ARENA_DEVICE: str = "gpu"          # gpu | cpu
+    ARENA_GPU: int = 0
+    ARENA_MAX_BATCH: int = 32
+    ARENA_QUEUE_DELAY_US: int = 500
+    ARENA_DECODE_THREADS: int = 8
+    ARENA_CONFIDENCE: str = ""          # logit | softmax ('' = topology default)
+    ARENA_CROP_TRANSPORT: str = "jpeg"  # jpeg (reference) | raw
+    ARENA_WEIGHT_SEED: int = 0
+    ARENA_FAULT_EVERY: int = 0          # inject a failure every k-th request (0 = off)
+
+    @classmethod
+    def from_env(cls, env_file: str | Path = ".env", **overrides) -> "Settings":
+        vals: dict[str, str] = _read_dotenv(Path(env_file))
+        for k in cls.model_fields:
+            if k in os.environ:
+                vals[k] = os.environ[k]
+        vals.update({k: v for k, v in overrides.items() if v is not None})
+        return cls(**vals)
+
+
+@functools.lru_cache
+def get_settings() -> Settings:
+    return Settings.from_env()

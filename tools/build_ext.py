@@ -36,6 +36,7 @@ SOURCES = [
     "kernels/classify_head.hip",
     "runtime/executor.cpp",
     "runtime/batcher.cpp",
+    "runtime/probe.hip",
     "bindings.cpp",
 ]
 
