@@ -352,6 +352,15 @@ PYBIND11_MODULE(_C, m) {
              e.synchronize();
            })
       .def("arena_ptr", &Executor::arena_ptr)
+      .def("read_arena",
+           [](Executor& e, int B, int64_t offset, size_t bytes) {
+             py::array_t<uint8_t> out(bytes);
+             {
+               py::gil_scoped_release nogil;
+               e.read_arena(B, offset, out.mutable_data(), bytes);
+             }
+             return out;
+           })
       .def("weights_ptr", &Executor::weights_ptr)
       .def("stream", &Executor::stream);
 

@@ -163,6 +163,16 @@ uintptr_t Executor::arena_ptr(int B) const {
   return it == buckets_.end() ? 0 : (uintptr_t)it->second.d_arena;
 }
 
+void Executor::read_arena(int B, int64_t offset, void* dst, size_t bytes) {
+  auto it = buckets_.find(B);
+  if (it == buckets_.end()) throw std::runtime_error("read_arena: unknown bucket");
+  if (offset < 0 || offset + (int64_t)bytes > it->second.info.arena_bytes)
+    throw std::runtime_error("read_arena: range outside the arena");
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+  ARENA_HIP_CHECK(hipMemcpy(dst, it->second.d_arena + offset, bytes, hipMemcpyDeviceToHost));
+}
+
 void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes) {
   if (B <= 0 || B > max_B_) throw std::runtime_error("add_bucket: B outside (0, max_batch]");
   if (prog_.empty()) throw std::runtime_error("add_bucket: set_program first");

@@ -132,6 +132,8 @@ class Executor {
 
   // Device pointers for tests / introspection.
   uintptr_t arena_ptr(int B) const;
+  // Debug: synchronously copy `bytes` from a bucket's arena at `offset` to host.
+  void read_arena(int B, int64_t offset, void* dst, size_t bytes);
   uintptr_t weights_ptr() const { return (uintptr_t)d_weights_; }
   uintptr_t stream() const { return (uintptr_t)compute_; }
 

@@ -65,7 +65,7 @@ class GpuPipeline:
     def __init__(self, yolo: YOLOv5nu, mnet: MobileNetV2, *, device: int = 0, buckets=None, max_det: int | None = None,
                  crop_cap_per_image: int | None = None, host_threads: int | None = None,
                  max_image_pixels: int = 640 * 640, conf_thr: float | None = None, iou_thr: float | None = None,
-                 weights: np.ndarray | None = None):
+                 weights: np.ndarray | None = None, share_buffers: bool = True):
         gcfg = get_gpu_config()
         ycfg = get_model_config("yolov5n")
         mb = get_controlled_variable("preprocessing", "mobilenet")
@@ -94,11 +94,23 @@ class GpuPipeline:
         self.ex.set_weights(self.program.weights if weights is None else weights)
         self.ex.set_program(self.program.ops, self.program.cls_ops)
         self.arena_bytes = {}
+        self.offsets = {}
         for B in self.buckets:
-            offs, total = layout(self.program.buffers, B, self.ex.crop_cap_for(B))
+            offs, total = layout(self.program.buffers, B, self.ex.crop_cap_for(B), share=share_buffers)
             self.ex.add_bucket(B, offs, total)
             self.arena_bytes[B] = total
+            self.offsets[B] = offs
         self.device = device
+
+    def read_buffer(self, name: str, B: int, item: int = 0) -> np.ndarray:
+        """Debug: NHWC contents of a planner buffer for one batch item (fp32)."""
+        import torch
+
+        buf = next(b for b in self.program.buffers if b.name == name)
+        raw = self.ex.read_arena(B, int(self.offsets[B][buf.id]) + item * buf.per_item, buf.H * buf.W * buf.C * buf.elem)
+        t = torch.from_numpy(raw.copy())
+        t = t.view(torch.bfloat16).float() if buf.elem == 2 else t.view(torch.float32)
+        return t.reshape(buf.H, buf.W, buf.C).numpy()
 
     @property
     def max_batch(self) -> int:

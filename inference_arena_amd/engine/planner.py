@@ -258,8 +258,12 @@ class ProgramBuilder:
         return Program(ops, cls_ops, self.buffers, self.weights.blob(), m)
 
 
-def layout(buffers: list[Buffer], n_images: int, n_crops: int) -> tuple[np.ndarray, int]:
-    """Lifetime-aware first-fit placement; returns (offsets per buffer id, arena bytes)."""
+def layout(buffers: list[Buffer], n_images: int, n_crops: int, share: bool = True) -> tuple[np.ndarray, int]:
+    """Lifetime-aware first-fit placement; returns (offsets per buffer id, arena bytes).
+
+    ``share=False`` gives every buffer its own range (debugging: every
+    intermediate tensor stays readable after a run).
+    """
     sizes = []
     for b in buffers:
         cnt = n_crops if b.kind == CROPS else n_images
@@ -274,7 +278,8 @@ def layout(buffers: list[Buffer], n_images: int, n_crops: int) -> tuple[np.ndarr
             offsets[i] = 0
             continue
         conflicts = sorted(
-            (o, e) for (o, e, j) in placed if not (buffers[j].last < b.first or b.last < buffers[j].first)
+            (o, e) for (o, e, j) in placed
+            if not share or not (buffers[j].last < b.first or b.last < buffers[j].first)
         )
         off = 0
         for o, e in conflicts:

@@ -50,20 +50,30 @@ def fold(m: ConvBNAct) -> tuple[torch.Tensor, torch.Tensor]:
 
 
 @torch.no_grad()
-def init_random_(model: nn.Module, seed: int) -> nn.Module:
-    """Deterministic random init that keeps activations O(1) through depth.
+def init_random_(model: nn.Module, seed: int, alpha: float = 1.0, beta: float = 0.3) -> nn.Module:
+    """Deterministic, numerically well-conditioned random init.
 
-    Conv weights ~ N(0, (gain / sqrt(fan_in))^2) with a gain that matches the
-    following activation's second moment; BN affine/statistics are perturbed
-    around identity so the folding path is exercised with non-trivial values.
+    Every Conv+BN weight is ``alpha * I + beta * N(0, 1/fan_in)`` where ``I``
+    routes output channel o to input channel o mod Cin at the centre tap
+    (identity for depthwise convs).  Plain random deep networks whose BN is
+    calibrated to unit variance are chaotic: bf16 rounding noise grows ~2x
+    every ~10 layers (25-40 % relative error at the YOLO head after 60 convs,
+    measured against fp32).  The identity-dominant form keeps the same
+    architecture, FLOPs and data-dependent outputs but behaves like a trained
+    network under bf16 (~4 % head error), so GPU-vs-fp32 parity tests are
+    meaningful.  Bare Conv2d/Linear layers (detect outputs, classifier) are
+    N(0, 1/fan_in).
     """
     g = torch.Generator().manual_seed(int(seed))
     for mod in model.modules():
         if isinstance(mod, ConvBNAct):
             c = mod.conv
-            fan_in = c.in_channels // c.groups * c.kernel_size[0] * c.kernel_size[1]
-            gain = {"silu": 1.6, "relu6": 1.4, None: 1.0}[mod.act_name]
-            c.weight.copy_(torch.randn(c.weight.shape, generator=g) * (gain / math.sqrt(fan_in)))
+            co, ci, kh, kw = c.weight.shape
+            fan_in = ci * kh * kw
+            w = torch.randn(c.weight.shape, generator=g) * (beta / math.sqrt(fan_in))
+            idx = torch.arange(co)
+            w[idx, idx % ci if c.groups == 1 else torch.zeros_like(idx), kh // 2, kw // 2] += alpha
+            c.weight.copy_(w)
             bn = mod.bn
             n = bn.num_features
             bn.weight.copy_(0.9 + 0.2 * torch.rand(n, generator=g))
@@ -80,7 +90,7 @@ def init_random_(model: nn.Module, seed: int) -> nn.Module:
 
 
 @torch.no_grad()
-def calibrate_bn_(model: nn.Module, batch: torch.Tensor, seed: int) -> nn.Module:
+def calibrate_bn_(model: nn.Module, batch: torch.Tensor, seed: int, var_floor: float = 0.5) -> nn.Module:
     """Set every BN's running statistics from a calibration batch.
 
     One forward pass in train mode with ``momentum=None`` (cumulative average)
@@ -100,6 +110,9 @@ def calibrate_bn_(model: nn.Module, batch: torch.Tensor, seed: int) -> nn.Module
     model(batch)
     model.eval()
     for bn in bns:
+        # floor tiny variances: near-constant channels would otherwise be
+        # amplified by 1/sqrt(var) and dominate rounding-noise growth
+        bn.running_var.clamp_(min=float(var_floor) * float(bn.running_var.median()))
         n = bn.num_features
         bn.weight.copy_(0.8 + 0.4 * torch.rand(n, generator=g))
         bn.bias.copy_(0.1 * torch.randn(n, generator=g))

@@ -7,7 +7,7 @@ import numpy as np, torch
 from inference_arena_amd.models.zoo import make_yolo, make_mobilenet
 from inference_arena_amd.engine.pipeline import GpuPipeline
 from inference_arena_amd.data.synthetic import synthetic_images
-pipe = GpuPipeline(make_yolo(0, cls_shift=-14.0), make_mobilenet(1), device=0, buckets=[1, 4, 8])
+pipe = GpuPipeline(make_yolo(0, cls_shift=-20.0), make_mobilenet(1), device=0, buckets=[1, 4, 8])
 out = []
 for n in (3, 6, 1):
     res = pipe.infer(synthetic_images(n, 21))

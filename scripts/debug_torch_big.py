@@ -12,7 +12,7 @@ from inference_arena_amd.models.zoo import make_yolo, make_mobilenet
 from inference_arena_amd.engine.pipeline import GpuPipeline
 from inference_arena_amd.engine.planner import layout
 from inference_arena_amd.data.synthetic import synthetic_images
-dm = make_yolo(0, cls_shift=-14.0), make_mobilenet(1)
+dm = make_yolo(0, cls_shift=-20.0), make_mobilenet(1)
 big = []
 def torch_big():
     big.append(torch.randn(64, 1024, 1024, device="cuda:0"))   # 256 MB

@@ -10,7 +10,7 @@ if MODE == "torch_first":
 from inference_arena_amd.models.zoo import make_yolo, make_mobilenet
 from inference_arena_amd.engine.pipeline import GpuPipeline
 from inference_arena_amd.data.synthetic import synthetic_images
-pipe = GpuPipeline(make_yolo(0, cls_shift=-14.0), make_mobilenet(1), device=0, buckets=[1, 4, 8])
+pipe = GpuPipeline(make_yolo(0, cls_shift=-20.0), make_mobilenet(1), device=0, buckets=[1, 4, 8])
 if MODE == "torch_after":
     torch.zeros(1, device="cuda:0"); torch.nn.functional.conv2d(torch.randn(1,3,32,32,device="cuda:0"), torch.randn(4,3,3,3,device="cuda:0"))
 if MODE == "alloc_after":
