@@ -144,7 +144,7 @@ void detect_decode(const DecodeParams& p, hipStream_t s) {
 
 // ------------------------------------------------------------------ NMS
 // One 1024-thread workgroup per image.  Candidates are sorted in LDS by a
-// 64-bit key (class asc, score desc, slot) with a bitonic network, then the
+// 64-bit key (class asc, score desc, anchor asc) with a bitonic network, then the
 // greedy pass walks the sorted list: a suppressed entry costs nothing, a kept
 // entry costs one parallel IoU sweep over the rest of its class segment and
 // one barrier.
@@ -167,10 +167,14 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const NmsParams p) {
   for (int i = tid; i < P; i += NMS_THREADS) {
     unsigned long long k = ~0ull;
     if (i < n) {
+      // key = [cls:7][score desc:29][anchor:14][slot:14]: class asc, score desc, ties broken by
+      // anchor index (deterministic; atomics make slot order vary), slot recovers the candidate
       const Candidate c = cand[i];
       const unsigned bits = __float_as_uint(c.score);
-      k = ((unsigned long long)(unsigned)c.cls << 44) |
-          ((unsigned long long)(0x3F800000u - bits) << 14) | (unsigned long long)i;
+      unsigned diff = bits <= 0x3F800000u ? 0x3F800000u - bits : 0u;
+      diff = diff < (1u << 29) ? diff : (1u << 29) - 1u;
+      k = ((unsigned long long)(unsigned)(c.cls & 127) << 57) | ((unsigned long long)diff << 28) |
+          ((unsigned long long)(unsigned)(c.anchor & 0x3FFF) << 14) | (unsigned long long)i;
       removed[i] = 0;
     }
     keys[i] = k;
@@ -196,7 +200,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const NmsParams p) {
   for (int i = 0; i < n; ++i) {
     if (removed[i]) continue;  // block-uniform: written before the last barrier
     const unsigned long long ki = keys[i];
-    const int ci = (int)(ki >> 44);
+    const int ci = (int)(ki >> 57);
     const Candidate bi = cand[ki & 0x3FFF];
     if (tid == 0 && kept < p.max_det) {
       Detection d;
@@ -213,7 +217,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(const NmsParams p) {
     const float area_i = (bi.x2 - bi.x1) * (bi.y2 - bi.y1);
     for (int j = i + 1 + tid; j < n; j += NMS_THREADS) {
       const unsigned long long kj = keys[j];
-      if ((int)(kj >> 44) != ci) break;
+      if ((int)(kj >> 57) != ci) break;
       if (removed[j]) continue;
       const Candidate bj = cand[kj & 0x3FFF];
       const float xx1 = fmaxf(bi.x1, bj.x1), yy1 = fmaxf(bi.y1, bj.y1);
