@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Map a rocprofv3 kernel trace of the executor back to program ops.
+
+The executor's hipGraph replays the program's ops in order, one kernel per
+op, so the k-th arena kernel of each replay is op k.  This tool takes the last
+``--replays`` complete replays from ``*_kernel_trace.csv``, averages each op's
+duration and prints a per-op table (op index, kind, layer shape, kernel
+variant, VGPRs, grid, mean us, share) plus per-kind totals.
+
+    python tools/analyze_trace.py gpurun_out/prof/bench_kernel_trace.csv --bucket 32
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+KIND = {1: "conv", 2: "dwconv", 3: "sppf", 4: "letterbox", 5: "zero", 6: "decode", 7: "nms", 8: "cropplan",
+        9: "cropgather", 10: "avgpool", 11: "topk"}
+
+
+def describe(rec) -> str:
+    t = int(rec[0])
+    if t == 1:
+        return (f"{int(rec[4])}x{int(rec[5])}x{int(rec[6])}->{int(rec[13])}x{int(rec[14])}x{int(rec[15])} "
+                f"k{int(rec[17])} s{int(rec[19])}{' res' if rec[22] != -1 else ''}{' up2' if rec[25] != -1 else ''}"
+                f"{' crops' if rec[30] == 1 else ''}")
+    if t == 2:
+        return f"dw {int(rec[4])}x{int(rec[5])}x{int(rec[6])} s{int(rec[14])}"
+    return ""
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--replays", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default=None, help="write the table as markdown")
+    a = ap.parse_args(argv)
+
+    from inference_arena_amd.engine.plans import plan_pipeline
+    from inference_arena_amd.models.zoo import default_models
+
+    prog = plan_pipeline(*default_models(a.seed), conf_thr=0.5, iou_thr=0.45)
+    n_ops = prog.ops.shape[0]
+    rows = [r for r in csv.DictReader(open(a.trace)) if "arena::" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # replays start with the letterbox kernel
+    starts = [i for i, r in enumerate(rows) if "letterbox" in r["Kernel_Name"]]
+    replays = [rows[s:s + n_ops] for s in starts if s + n_ops <= len(rows)]
+    replays = [rp for rp in replays if len(rp) == n_ops][-a.replays:]
+    if not replays:
+        print("no complete replay found", file=sys.stderr)
+        return 1
+    dur = defaultdict(list)
+    for rp in replays:
+        for k, r in enumerate(rp):
+            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    total = sum(sum(v) / len(v) for v in dur.values())
+    lines = ["| op | kind | shape | kernel | vgpr | grid | mean us | share |", "|---|---|---|---|---|---|---|---|"]
+    per_kind = defaultdict(float)
+    for k in range(n_ops):
+        r = replays[-1][k]
+        us = sum(dur[k]) / len(dur[k])
+        kind = KIND.get(int(prog.ops[k][0]), "?")
+        per_kind[kind] += us
+        name = r["Kernel_Name"].replace("void arena::", "").replace("arena::", "").split("(")[0]
+        grid = f"{int(r['Grid_Size_X']) // max(1, int(r['Workgroup_Size_X']))}x{r['Grid_Size_Y']}"
+        lines.append(f"| {k} | {kind} | {describe(prog.ops[k])} | {name} | {r['VGPR_Count']}+{r['Accum_VGPR_Count']} "
+                     f"| {grid} | {us:.1f} | {100 * us / total:.1f}% |")
+    lines.append("")
+    lines.append(f"replays averaged: {len(replays)}; device time per replay: {total:.1f} us")
+    lines.append("")
+    lines.append("| kind | us per replay | share |")
+    lines.append("|---|---|---|")
+    for kind, us in sorted(per_kind.items(), key=lambda kv: -kv[1]):
+        lines.append(f"| {kind} | {us:.1f} | {100 * us / total:.1f}% |")
+    text = "\n".join(lines)
+    print(text)
+    if a.out:
+        Path(a.out).write_text(text + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
