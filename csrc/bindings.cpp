@@ -278,6 +278,8 @@ py::dict result_to_py(const BatchResult& r, int max_det) {
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native kernels and runtime of inference_arena_amd (gfx950)";
   m.def("conv2d", &py_conv2d);
+  m.def("set_conv_impl", &set_conv_impl);
+  m.def("get_conv_impl", &get_conv_impl);
   m.def("dwconv3x3", &py_dwconv);
   m.def("sppf_pool", &py_sppf);
   m.def("letterbox_s2d", &py_letterbox);

@@ -47,6 +47,15 @@ def test_native_loaded():
     assert C.SIZEOF_IMAGE_META == 48 and C.SIZEOF_CANDIDATE == 32 and C.SIZEOF_TOPK == 64
 
 
+@pytest.fixture(params=[2, 1], ids=["lds", "direct"])
+def conv_impl(request):
+    C = native()
+    old = C.get_conv_impl()
+    C.set_conv_impl(request.param)
+    yield request.param
+    C.set_conv_impl(old)
+
+
 @pytest.mark.parametrize(
     "B,H,Cin,Cout,k,s,act",
     [
@@ -58,9 +67,12 @@ def test_native_loaded():
         (1, 20, 80, 80, 3, 1, "silu"),  # Cin=80, Cout=80 (WC=5)
         (2, 14, 96, 24, 1, 1, None),
         (1, 7, 320, 1280, 1, 1, "relu6"),
+        (3, 20, 128, 64, 3, 2, "silu"),  # stride-2 tile with a partial column tile
+        (2, 27, 64, 48, 3, 1, None),  # odd spatial size, 3 channel tiles
+        (1, 20, 256, 144, 3, 1, "silu"),  # 8 input-channel slices
     ],
 )
-def test_conv_matches_torch(device, B, H, Cin, Cout, k, s, act):
+def test_conv_matches_torch(device, conv_impl, B, H, Cin, Cout, k, s, act):
     g = torch.Generator().manual_seed(B * 1000 + H * 10 + Cin)
     x = torch.randn(B, Cin, H, H, generator=g)
     w = torch.randn(Cout, Cin, k, k, generator=g) / np.sqrt(Cin * k * k)
@@ -71,7 +83,7 @@ def test_conv_matches_torch(device, B, H, Cin, Cout, k, s, act):
     _check(_nchw(y.cpu()), ref)
 
 
-def test_conv_slices_residual_upsample(device):
+def test_conv_slices_residual_upsample(device, conv_impl):
     g = torch.Generator().manual_seed(7)
     B, H, Cbuf, Cin, Cout = 2, 20, 96, 32, 48
     buf = torch.randn(B, H, H, Cbuf, generator=g).to(torch.bfloat16).to(device)
@@ -91,7 +103,7 @@ def test_conv_slices_residual_upsample(device):
     assert torch.equal(_nchw(up.cpu()[..., 8:8 + Cout]), upref)
 
 
-def test_conv_fp32_out_and_live_batch(device):
+def test_conv_fp32_out_and_live_batch(device, conv_impl):
     g = torch.Generator().manual_seed(3)
     x = torch.randn(6, 1, 1, 1280, generator=g).to(torch.bfloat16).to(device)
     w = torch.randn(1000, 1280, 1, 1, generator=g) / np.sqrt(1280)
@@ -105,7 +117,7 @@ def test_conv_fp32_out_and_live_batch(device):
     assert torch.all(out.cpu()[4:] == -7.0), "rows past the live batch must not be written"
 
 
-def test_stem_s2d_equivalence(device):
+def test_stem_s2d_equivalence(device, conv_impl):
     from inference_arena_amd.engine.plans import s2d_stem_3x3, s2d_stem_6x6
 
     g = torch.Generator().manual_seed(11)
