@@ -157,14 +157,15 @@ void py_nms(const py::dict& d) {
 
 void py_crop_plan(const py::dict& d) {
   CropPlanParams p{};
-  p.det = ptr<const Detection*>(d, "det");
-  p.det_count = ptr<const int*>(d, "det_count");
+  p.det = ptr<Detection*>(d, "det");
+  p.det_count = ptr<int*>(d, "det_count");
   p.max_det = req<int>(d, "max_det");
   p.meta = ptr<const ImageMeta*>(d, "meta");
   p.B = req<int>(d, "B");
   p.crops = ptr<CropRef*>(d, "crops");
   p.ctrl = ptr<Ctrl*>(d, "ctrl");
   p.crop_cap = req<int>(d, "crop_cap");
+  p.whole = get<int>(d, "whole", 0);
   crop_plan(p, stream_of(d));
 }
 
@@ -221,6 +222,7 @@ ExecutorConfig config_from(const py::dict& d) {
   c.det_size = get<int>(d, "det_size", c.det_size);
   c.cls_size = get<int>(d, "cls_size", c.cls_size);
   c.host_threads = get<int>(d, "host_threads", c.host_threads);
+  c.raw_out_bytes = get<int64_t>(d, "raw_out_bytes", c.raw_out_bytes);
   return c;
 }
 
@@ -229,13 +231,19 @@ std::vector<InputImage> images_from(const py::list& imgs, std::vector<py::array>
   v.reserve(imgs.size());
   for (auto h : imgs) {
     py::array a = py::array::ensure(h, py::array::c_style);
-    if (!a || a.ndim() != 3 || a.shape(2) != 3 || a.itemsize() != 1)
-      throw std::runtime_error("images must be contiguous uint8 HxWx3 arrays");
-    keep.push_back(a);
+    if (!a) throw std::runtime_error("inputs must be numpy arrays");
     InputImage im;
+    if (a.ndim() == 3 && a.shape(2) == 3 && a.itemsize() == 1) {  // RGB uint8 HWC image
+      im.h = (int)a.shape(0);
+      im.w = (int)a.shape(1);
+    } else if (a.ndim() == 3 && a.shape(0) == 3 && a.itemsize() == 4 && a.shape(1) == a.shape(2)) {
+      im.h = im.w = (int)a.shape(1);  // fp32 CHW [3, S, S] tensor (reference tensor contract)
+      im.bytes = (int64_t)a.nbytes();
+    } else {
+      throw std::runtime_error("inputs must be uint8 HxWx3 images or float32 [3,S,S] tensors");
+    }
+    keep.push_back(a);
     im.data = (const uint8_t*)a.data();
-    im.h = (int)a.shape(0);
-    im.w = (int)a.shape(1);
     v.push_back(im);
   }
   return v;
@@ -270,6 +278,11 @@ py::dict result_to_py(const BatchResult& r, int max_det) {
   out["gpu_ms"] = r.gpu_ms;
   out["bucket"] = r.bucket;
   out["total_crops"] = r.total_crops;
+  if (!r.raw.empty()) {
+    py::array_t<uint8_t> raw((py::ssize_t)r.raw.size());
+    std::memcpy(raw.mutable_data(), r.raw.data(), r.raw.size());
+    out["raw"] = raw;
+  }
   return out;
 }
 
@@ -379,8 +392,20 @@ PYBIND11_MODULE(_C, m) {
            }),
            py::keep_alive<1, 2>())
       .def("enqueue",
-           [](DynamicBatcher& b, py::array_t<uint8_t, py::array::c_style> img, py::function cb) {
-             if (img.ndim() != 3 || img.shape(2) != 3) throw std::runtime_error("image must be HxWx3 uint8");
+           [](DynamicBatcher& b, py::array img_in, py::function cb) {
+             py::array img = py::array::ensure(img_in, py::array::c_style);
+             int h = 0, w = 0;
+             int64_t bytes = 0;
+             if (img && img.ndim() == 3 && img.shape(2) == 3 && img.itemsize() == 1) {
+               h = (int)img.shape(0);
+               w = (int)img.shape(1);
+             } else if (img && img.ndim() == 3 && img.shape(0) == 3 && img.itemsize() == 4 &&
+                        img.shape(1) == img.shape(2)) {
+               h = w = (int)img.shape(1);
+               bytes = (int64_t)img.nbytes();
+             } else {
+               throw std::runtime_error("input must be a uint8 HxWx3 image or a float32 [3,S,S] tensor");
+             }
              auto pycb = std::make_shared<py::function>(std::move(cb));
              ResultCallback f = [pycb](RequestResult&& r) {
                py::gil_scoped_acquire gil;
@@ -404,6 +429,11 @@ PYBIND11_MODULE(_C, m) {
                d["topk_idx"] = ti;
                d["topk_logit"] = tl;
                d["topk_prob"] = tp;
+               if (!r.raw.empty()) {
+                 py::array_t<uint8_t> raw((py::ssize_t)r.raw.size());
+                 std::memcpy(raw.mutable_data(), r.raw.data(), r.raw.size());
+                 d["raw"] = raw;
+               }
                d["batch_size"] = r.batch_size;
                d["queue_us"] = r.queue_us;
                d["compute_us"] = r.compute_us;
@@ -413,10 +443,9 @@ PYBIND11_MODULE(_C, m) {
                  e.discard_as_unraisable("DynamicBatcher callback");
                }
              };
-             const uint8_t* data = img.data();
-             const int h = (int)img.shape(0), w = (int)img.shape(1);
+             const uint8_t* data = (const uint8_t*)img.data();
              py::gil_scoped_release nogil;
-             return b.enqueue(data, h, w, std::move(f));
+             return b.enqueue(data, h, w, std::move(f), bytes);
            })
       .def("stats",
            [](DynamicBatcher& b) {

@@ -255,6 +255,28 @@ __global__ __launch_bounds__(256) void crop_plan_kernel(const CropPlanParams p) 
   __shared__ int offs[1024 + 1];
   const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
   const int tid = threadIdx.x;
+  if (p.whole) {
+    // classifier-only programs: image b is crop b (its full extent)
+    for (int b = tid; b < n_img; b += blockDim.x) {
+      const ImageMeta m = p.meta[b];
+      Detection d;
+      d.x1 = 0.f; d.y1 = 0.f; d.x2 = (float)m.w; d.y2 = (float)m.h;
+      d.conf = 1.f; d.cls = -1; d.pad_[0] = d.pad_[1] = 0.f;
+      p.det[(size_t)b * p.max_det] = d;
+      p.det_count[b] = 1;
+      CropRef r;
+      r.img = b; r.x1 = 0; r.y1 = 0; r.x2 = m.w; r.y2 = m.h; r.det = 0; r.pad_[0] = r.pad_[1] = 0;
+      p.crops[b] = r;
+    }
+    if (tid == 0) {
+      Ctrl* c = p.ctrl;
+      c->total_crops = n_img;
+      int rem = n_img - c->crop_base;
+      rem = rem < 0 ? 0 : rem;
+      c->n_crops = rem < p.crop_cap ? rem : p.crop_cap;
+    }
+    return;
+  }
   if (tid == 0) {
     int acc = 0;
     for (int b = 0; b < n_img; ++b) {
@@ -291,6 +313,68 @@ __global__ __launch_bounds__(256) void crop_plan_kernel(const CropPlanParams p) 
 void crop_plan(const CropPlanParams& p, hipStream_t s) {
   if (p.B > 1024) throw std::runtime_error("crop_plan: batch > 1024");
   hipLaunchKernelGGL(crop_plan_kernel, dim3(1), dim3(256), 0, s, p);
+}
+
+}  // namespace arena
+
+namespace arena {
+
+// Raw detector output in the reference's ONNX contract: per image
+// [4 + nc, A] fp32 = (cx, cy, w, h) in letterbox pixels followed by the
+// sigmoid class scores, for all A = 8400 anchors (experiment.yaml:199-207),
+// i.e. what Triton's "yolov5n" model returns to the reference gateway.
+__global__ __launch_bounds__(256) void yolo_raw_kernel(const YoloRawParams p) {
+  const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
+  const int A0 = p.hw[0] * p.hw[0], A1 = p.hw[1] * p.hw[1], A2 = p.hw[2] * p.hw[2];
+  const int A = A0 + A1 + A2;
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (long)n_img * A) return;
+  const int b = (int)(tid / A);
+  const int a = (int)(tid - (long)b * A);
+  int l, r;
+  if (a < A0) { l = 0; r = a; } else if (a < A0 + A1) { l = 1; r = a - A0; } else { l = 2; r = a - A0 - A1; }
+  const int hw = p.hw[l];
+  const bf16* px = (const bf16*)p.head[l] + ((size_t)b * hw * hw + r) * p.xs[l];
+  float* out = (float*)((uint8_t*)p.out + (size_t)b * p.out_stride);
+  float dist[4];
+#pragma unroll
+  for (int side = 0; side < 4; ++side) {
+    float v[16];
+    unpack8(*(const uint4*)(px + side * 16), v);
+    unpack8(*(const uint4*)(px + side * 16 + 8), v + 8);
+    float mx = v[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
+    float se = 0.f, sw = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float e = __expf(v[i] - mx);
+      se += e;
+      sw += e * (float)i;
+    }
+    dist[side] = sw / se;
+  }
+  const int gy = r / hw, gx = r - (r / hw) * hw;
+  const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f, s = p.stride[l];
+  const float x1 = ax - dist[0], y1 = ay - dist[1], x2 = ax + dist[2], y2 = ay + dist[3];
+  out[0 * A + a] = (x1 + x2) * 0.5f * s;
+  out[1 * A + a] = (y1 + y2) * 0.5f * s;
+  out[2 * A + a] = (x2 - x1) * s;
+  out[3 * A + a] = (y2 - y1) * s;
+  for (int g = 0; g < 10; ++g) {
+    float v[8];
+    unpack8(*(const uint4*)(px + 64 + g * 8), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[(size_t)(4 + g * 8 + i) * A + a] = 1.0f / (1.0f + __expf(-v[i]));
+  }
+}
+
+void yolo_raw(const YoloRawParams& p, hipStream_t s) {
+  const long A = (long)p.hw[0] * p.hw[0] + (long)p.hw[1] * p.hw[1] + (long)p.hw[2] * p.hw[2];
+  if (p.out_stride < (size_t)A * 84 * 4) throw std::runtime_error("yolo_raw: output stride too small");
+  const long total = A * p.B;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(yolo_raw_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
 }
 
 }  // namespace arena

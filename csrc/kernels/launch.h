@@ -97,6 +97,16 @@ struct LetterboxParams {
 };
 void letterbox_s2d(const LetterboxParams& p, hipStream_t s);
 
+// fp32 NCHW [3,S,S] tensors in the image pool -> space-to-depth bf16.
+struct TensorInParams {
+  const uint8_t* pool;
+  const ImageMeta* meta;
+  const Ctrl* ctrl;
+  void* out;
+  int B, S;
+};
+void tensor_in_s2d(const TensorInParams& p, hipStream_t s);
+
 // ---------------------------------------------------------------- detect decode (K7)
 struct Candidate {
   float x1, y1, x2, y2;  // letterbox coordinates
@@ -119,6 +129,19 @@ struct DecodeParams {
   const Ctrl* ctrl;
 };
 void detect_decode(const DecodeParams& p, hipStream_t s);
+
+// Raw [84, A] fp32 detector output per image (reference ONNX contract).
+struct YoloRawParams {
+  const void* head[3];
+  int hw[3];
+  int xs[3];
+  float stride[3];
+  int B;
+  void* out;          // image b at out + b * out_stride
+  size_t out_stride;  // bytes
+  const Ctrl* ctrl;
+};
+void yolo_raw(const YoloRawParams& p, hipStream_t s);
 
 // ---------------------------------------------------------------- NMS (K8)
 struct Detection {
@@ -153,14 +176,15 @@ struct CropRef {
   int pad_[2];
 };
 struct CropPlanParams {
-  const Detection* det;
-  const int* det_count;
+  Detection* det;
+  int* det_count;
   int max_det;
   const ImageMeta* meta;
   int B;
   CropRef* crops;  // [B*max_det]
   Ctrl* ctrl;
   int crop_cap;    // crops one classification pass can hold
+  int whole;       // 1: every image is one crop (classifier-only programs); writes det/det_count
 };
 void crop_plan(const CropPlanParams& p, hipStream_t s);
 

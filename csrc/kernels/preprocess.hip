@@ -132,3 +132,41 @@ void crop_gather_s2d(const CropGatherParams& p, hipStream_t s) {
 }
 
 }  // namespace arena
+
+namespace arena {
+
+// Reference-contract tensor input (KServe "images" / "input": FP32 NCHW
+// [3, S, S], already normalised by the client as in the reference gateway,
+// architectures/triton/gateway/app/pipeline.py:131-139) -> space-to-depth
+// bf16 [S/2, S/2, 16] for the s2d stem convs.
+__global__ __launch_bounds__(256) void tensor_in_s2d_kernel(const TensorInParams p) {
+  const int S2 = p.S >> 1;
+  const int n = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
+  const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (long)n * S2 * S2) return;
+  const int X = (int)(tid % S2);
+  const int Y = (int)((tid / S2) % S2);
+  const int b = (int)(tid / ((long)S2 * S2));
+  const float* src = (const float*)(p.pool + p.meta[b].offset);
+  const size_t plane = (size_t)p.S * p.S;
+  float out[16];
+#pragma unroll
+  for (int pq = 0; pq < 4; ++pq) {
+    const int y = 2 * Y + (pq >> 1), x = 2 * X + (pq & 1);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = src[c * plane + (size_t)y * p.S + x];
+  }
+  out[12] = out[13] = out[14] = out[15] = 0.f;
+  uint4* dst = (uint4*)((bf16*)p.out + (size_t)tid * 16);
+  dst[0] = pack8(out);
+  dst[1] = pack8(out + 8);
+}
+
+void tensor_in_s2d(const TensorInParams& p, hipStream_t s) {
+  if (p.S % 2 != 0) throw std::runtime_error("tensor_in_s2d: S must be even");
+  const long total = (long)p.B * (p.S / 2) * (p.S / 2);
+  if (total <= 0) return;
+  hipLaunchKernelGGL(tensor_in_s2d_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+}
+
+}  // namespace arena

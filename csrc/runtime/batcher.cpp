@@ -40,11 +40,12 @@ void DynamicBatcher::shutdown() {
   threads_.clear();
 }
 
-int64_t DynamicBatcher::enqueue(const uint8_t* rgb, int h, int w, ResultCallback cb) {
+int64_t DynamicBatcher::enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes) {
   auto r = std::make_unique<Request>();
-  r->pixels.assign(rgb, rgb + (size_t)h * w * 3);
+  r->pixels.assign(data, data + (bytes > 0 ? (size_t)bytes : (size_t)h * w * 3));
   r->h = h;
   r->w = w;
+  r->bytes = bytes;
   r->cb = std::move(cb);
   r->t_enq = clk::now();
   int64_t id;
@@ -95,7 +96,7 @@ bool DynamicBatcher::take_batch(Batch& out, bool can_wait) {
   }
 }
 
-void DynamicBatcher::finish(Batch& batch, const BatchResult& r, clk::time_point t_submit) {
+void DynamicBatcher::finish(Batch& batch, const BatchResult& r, clk::time_point t_submit, size_t raw_bytes) {
   const auto t_done = clk::now();
   const int max_det = (int)(r.det.size() / std::max<size_t>(1, batch.size()));
   const double compute_us = std::chrono::duration<double, std::micro>(t_done - t_submit).count();
@@ -112,10 +113,14 @@ void DynamicBatcher::finish(Batch& batch, const BatchResult& r, clk::time_point 
   for (size_t i = 0; i < batch.size(); ++i) {
     RequestResult rr;
     rr.id = batch[i]->id;
-    rr.det_count = r.det_count[i];
+    rr.det_count = i < r.det_count.size() ? r.det_count[i] : 0;
     const int kept = std::min(rr.det_count, max_det);
-    rr.det.assign(r.det.begin() + (size_t)i * max_det, r.det.begin() + (size_t)i * max_det + kept);
-    rr.topk.assign(r.topk.begin() + r.crop_offset[i], r.topk.begin() + r.crop_offset[i + 1]);
+    if (kept > 0)
+      rr.det.assign(r.det.begin() + (size_t)i * max_det, r.det.begin() + (size_t)i * max_det + kept);
+    if (i + 1 < r.crop_offset.size())
+      rr.topk.assign(r.topk.begin() + r.crop_offset[i], r.topk.begin() + r.crop_offset[i + 1]);
+    if (raw_bytes > 0 && r.raw.size() >= (i + 1) * raw_bytes)
+      rr.raw.assign(r.raw.begin() + i * raw_bytes, r.raw.begin() + (i + 1) * raw_bytes);
     rr.batch_size = (int)batch.size();
     rr.queue_us = std::chrono::duration<double, std::micro>(t_submit - batch[i]->t_enq).count();
     rr.compute_us = compute_us;
@@ -150,7 +155,11 @@ void DynamicBatcher::instance_loop(int idx) {
       if (take_batch(b, pending.empty())) {
         std::vector<InputImage> imgs;
         imgs.reserve(b.size());
-        for (auto& rq : b) imgs.push_back(InputImage{rq->pixels.data(), rq->h, rq->w});
+        for (auto& rq : b) {
+          InputImage im{rq->pixels.data(), rq->h, rq->w};
+          im.bytes = rq->bytes;
+          imgs.push_back(im);
+        }
         try {
           const auto t = clk::now();
           const int slot = ex.submit(imgs);
@@ -170,7 +179,7 @@ void DynamicBatcher::instance_loop(int idx) {
     pending.pop_front();
     try {
       BatchResult r = ex.collect(f.slot);
-      finish(f.batch, r, f.t_submit);
+      finish(f.batch, r, f.t_submit, (size_t)std::max<int64_t>(0, ex.config().raw_out_bytes));
     } catch (const std::exception& e) {
       fail(f.batch, e.what());
     }

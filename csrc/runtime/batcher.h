@@ -34,6 +34,7 @@ struct RequestResult {
   int det_count = 0;
   std::vector<Detection> det;    // min(det_count, max_det) rows
   std::vector<TopkResult> topk;  // one per kept detection
+  std::vector<uint8_t> raw;      // raw tensor output (raw-output programs)
   int batch_size = 0;
   double queue_us = 0, compute_us = 0;
   std::string error;
@@ -63,8 +64,10 @@ class DynamicBatcher {
   DynamicBatcher(const DynamicBatcher&) = delete;
   DynamicBatcher& operator=(const DynamicBatcher&) = delete;
 
-  // Copies the image; returns the request id, or -1 when the queue is full.
-  int64_t enqueue(const uint8_t* rgb, int h, int w, ResultCallback cb);
+  // Copies the input; returns the request id, or -1 when the queue is full.
+  // `bytes` == 0: RGB uint8 HxWx3 image; otherwise an fp32 [3, h, w] tensor of
+  // that many bytes (reference tensor contract of the model server).
+  int64_t enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes = 0);
   BatcherStats stats();
   void shutdown();
 
@@ -73,6 +76,7 @@ class DynamicBatcher {
     int64_t id;
     std::vector<uint8_t> pixels;
     int h, w;
+    int64_t bytes;
     ResultCallback cb;
     std::chrono::steady_clock::time_point t_enq;
   };
@@ -80,7 +84,7 @@ class DynamicBatcher {
 
   void instance_loop(int idx);
   bool take_batch(Batch& out, bool can_wait);
-  void finish(Batch& batch, const BatchResult& r, std::chrono::steady_clock::time_point t_submit);
+  void finish(Batch& batch, const BatchResult& r, std::chrono::steady_clock::time_point t_submit, size_t raw_bytes);
   void fail(Batch& batch, const std::string& err);
 
   std::vector<std::shared_ptr<Executor>> inst_;

@@ -109,9 +109,10 @@ size_t Executor::out_off_det() const { return align_up(sizeof(int) * (size_t)max
 size_t Executor::out_off_topk() const {
   return out_off_det() + align_up(sizeof(Detection) * (size_t)max_B_ * cfg_.max_det, 256);
 }
-size_t Executor::out_bytes_total() const {
-  return out_off_topk() + sizeof(TopkResult) * (size_t)max_B_ * cfg_.max_det;
+size_t Executor::out_off_raw() const {
+  return align_up(out_off_topk() + sizeof(TopkResult) * (size_t)max_B_ * cfg_.max_det, 256);
 }
+size_t Executor::out_bytes_total() const { return out_off_raw() + (size_t)cfg_.raw_out_bytes * max_B_; }
 
 void Executor::alloc_slots() {
   for (auto& sl : slots_) {
@@ -148,6 +149,13 @@ void Executor::set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops
   cls_prog_.resize(n_cls_ops);
   for (int i = 0; i < n_cls_ops; ++i)
     std::memcpy(cls_prog_[i].data(), cls_ops + (size_t)i * kOpFields, sizeof(OpRecord));
+  has_topk_ = has_det_ = has_raw_ = false;
+  for (const auto& r : prog_) {
+    has_topk_ |= r[0] == OP_TOPK;
+    has_det_ |= r[0] == OP_NMS || r[0] == OP_CROPPLAN;
+    for (int f = 1; f < kOpFields; ++f) has_raw_ |= r[f] == BUF_RAWOUT && (r[0] == OP_YOLORAW || r[0] == OP_CONV);
+  }
+  if (has_raw_ && cfg_.raw_out_bytes <= 0) throw std::runtime_error("program exports raw outputs: raw_out_bytes = 0");
 }
 
 int Executor::crop_cap_for(int B) const { return std::max(cfg_.min_crop_cap, B * cfg_.crop_cap_per_image); }
@@ -230,6 +238,7 @@ uint8_t* Executor::resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff, int 
     case BUF_DETCOUNT: base = sl.d_out; break;
     case BUF_DET: base = sl.d_out + out_off_det(); break;
     case BUF_TOPK: base = sl.d_out + out_off_topk(); break;
+    case BUF_RAWOUT: base = sl.d_out + out_off_raw(); break;
     default:
       if (buf < 0 || buf >= (int64_t)bk.info.offsets.size())
         throw std::runtime_error("program references unknown buffer " + std::to_string(buf));
@@ -364,14 +373,15 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       }
       case OP_CROPPLAN: {
         CropPlanParams p{};
-        p.det = (const Detection*)resolve(bk, sl, r[1], 0, 1);
-        p.det_count = (const int*)resolve(bk, sl, r[2], 0, 1);
+        p.det = (Detection*)resolve(bk, sl, r[1], 0, 1);
+        p.det_count = (int*)resolve(bk, sl, r[2], 0, 1);
         p.max_det = cfg_.max_det;
         p.meta = meta;
         p.B = B;
         p.crops = (CropRef*)resolve(bk, sl, r[3], 0, 1);
         p.ctrl = ctrl;
         p.crop_cap = CC;
+        p.whole = (int)r[4];
         crop_plan(p, s);
         break;
       }
@@ -413,6 +423,32 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         topk_softmax(p, s);
         break;
       }
+      case OP_TENSORIN: {
+        TensorInParams p{};
+        p.pool = pool;
+        p.meta = meta;
+        p.ctrl = ctrl;
+        p.out = resolve(bk, sl, r[1], 0, 2);
+        p.B = B;
+        p.S = (int)r[2];
+        tensor_in_s2d(p, s);
+        break;
+      }
+      case OP_YOLORAW: {
+        YoloRawParams p{};
+        for (int l = 0; l < 3; ++l) {
+          p.head[l] = resolve(bk, sl, r[1 + 4 * l], r[2 + 4 * l], 2);
+          p.xs[l] = (int)r[3 + 4 * l];
+          p.hw[l] = (int)r[4 + 4 * l];
+          p.stride[l] = (float)r[13 + l];
+        }
+        p.B = B;
+        p.out = resolve(bk, sl, r[16], 0, 1);
+        p.out_stride = (size_t)cfg_.raw_out_bytes;
+        p.ctrl = ctrl;
+        yolo_raw(p, s);
+        break;
+      }
       default:
         throw std::runtime_error("unknown op type " + std::to_string(r[0]));
     }
@@ -450,6 +486,15 @@ int Executor::pick_bucket(int n) const {
   return -1;
 }
 
+void Executor::enqueue_results_d2h(Bucket& bk, Slot& sl, int n) {
+  size_t d2h = out_off_topk();
+  if (has_topk_) d2h += sizeof(TopkResult) * (size_t)bk.info.crop_cap;
+  ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+  if (has_raw_)
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out + out_off_raw(), sl.d_out + out_off_raw(), (size_t)cfg_.raw_out_bytes * n,
+                                   hipMemcpyDeviceToHost, compute_));
+}
+
 int Executor::submit(const std::vector<InputImage>& imgs) {
   std::lock_guard<std::mutex> lk(mu_);
   const int n = (int)imgs.size();
@@ -470,7 +515,7 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   for (int i = 0; i < n; ++i) {
     const InputImage& im = imgs[i];
     if (im.h <= 0 || im.w <= 0) throw std::runtime_error("submit: empty image");
-    const size_t bytes = (size_t)im.h * im.w * 3;
+    const size_t bytes = im.bytes > 0 ? (size_t)im.bytes : (size_t)im.h * im.w * 3;
     if (off + bytes > pool_cap) throw std::runtime_error("submit: batch exceeds the staging pool");
     ImageMeta& m = meta[i];
     m.offset = (int64_t)off;
@@ -551,13 +596,11 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
       }
       ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
     }
-    const size_t d2h = out_off_topk() + sizeof(TopkResult) * (size_t)bk.info.crop_cap;
-    ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+    enqueue_results_d2h(bk, sl, n);
   } else {
     Bucket& bk = buckets_.at(B);
     ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], compute_));
-    const size_t d2h = out_off_topk() + sizeof(TopkResult) * (size_t)bk.info.crop_cap;
-    ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+    enqueue_results_d2h(bk, sl, n);
   }
   ARENA_HIP_CHECK(hipEventRecord(sl.done, compute_));
   sl.busy = true;
@@ -588,13 +631,15 @@ BatchResult Executor::collect(int s) {
   int total = 0;
   for (int i = 0; i < n; ++i) {
     res.crop_offset[i] = total;
-    total += std::min(cnt[i], cfg_.max_det);
+    if (has_topk_) total += std::min(cnt[i], cfg_.max_det);
   }
   res.crop_offset[n] = total;
   res.total_crops = total;
+  if (has_raw_) res.raw.assign(sl.h_out + out_off_raw(), sl.h_out + out_off_raw() + (size_t)cfg_.raw_out_bytes * n);
+  if (!has_det_) res.det_count.assign(n, 0);
   Bucket& bk = buckets_.at(sl.bucket);
   const int CC = bk.info.crop_cap;
-  if (total > CC) {
+  if (has_topk_ && total > CC) {
     // Overflow: classify the remaining crops in extra passes of CC crops.
     std::lock_guard<std::mutex> lk(mu_);
     for (int base = CC; base < total; base += CC) {

@@ -49,6 +49,8 @@ enum OpType : int64_t {
   OP_CROPGATHER = 9,
   OP_AVGPOOL = 10,
   OP_TOPK = 11,
+  OP_TENSORIN = 12,
+  OP_YOLORAW = 13,
 };
 
 // Reserved buffer ids (the planner's arena buffers are ids >= 0).
@@ -60,6 +62,7 @@ enum ReservedBuf : int64_t {
   BUF_DET = -13,
   BUF_DETCOUNT = -14,
   BUF_TOPK = -15,
+  BUF_RAWOUT = -16,
 };
 
 // Batch kind of an op: which live count clamps it.
@@ -76,6 +79,7 @@ struct ExecutorConfig {
   int det_size = 640;
   int cls_size = 224;
   int host_threads = 8;
+  int64_t raw_out_bytes = 0;  // per-image raw output region (reference tensor contracts)
 };
 
 struct BucketInfo {
@@ -86,8 +90,9 @@ struct BucketInfo {
 };
 
 struct InputImage {
-  const uint8_t* data;  // RGB uint8 HWC, contiguous
+  const uint8_t* data;  // RGB uint8 HWC, contiguous (or an fp32 tensor when bytes != 0)
   int h, w;
+  int64_t bytes = 0;    // explicit payload size (tensor inputs); 0 = h*w*3
 };
 
 // Per-slot results copied back to pinned memory by the graph.
@@ -100,6 +105,7 @@ struct BatchResult {
   std::vector<TopkResult> topk;      // [total crops], in crop-plan order
   std::vector<int> crop_offset;      // [n + 1] first crop of each image
   double gpu_ms = 0.0;               // graph wall time from events
+  std::vector<uint8_t> raw;          // [n * raw_out_bytes] when the program exports raw tensors
 };
 
 class Executor {
@@ -159,6 +165,7 @@ class Executor {
   void alloc_slots();
   void capture(Bucket& bk, int slot);
   void enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s);
+  void enqueue_results_d2h(Bucket& bk, Slot& sl, int n);
   uint8_t* resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff_elems, int elem_bytes);
   int pick_bucket(int n) const;
   size_t in_bytes_meta() const;
@@ -166,6 +173,7 @@ class Executor {
   size_t out_off_det() const;
   size_t out_off_topk() const;
   size_t out_bytes_total() const;
+  size_t out_off_raw() const;
   void parallel_copy(std::vector<std::function<void()>>& jobs);
 
   ExecutorConfig cfg_;
@@ -177,6 +185,7 @@ class Executor {
   std::map<int, Bucket> buckets_;
   Slot slots_[2];
   int next_slot_ = 0;
+  bool has_topk_ = false, has_det_ = false, has_raw_ = false;
   int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on compute stream
   int debug_sync_ = 0;  // ARENA_DEBUG_SYNC: 1 eager op-by-op, 2 one graph per op
   std::mutex mu_;

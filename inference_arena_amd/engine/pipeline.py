@@ -18,7 +18,8 @@ from ..models.mobilenetv2 import MobileNetV2
 from ..models.yolov5nu import YOLOv5nu
 from ..ops import native
 from .planner import layout
-from .plans import plan_pipeline
+from .plans import plan_classifier, plan_detector, plan_mobilenet_raw, plan_pipeline, plan_yolo_raw
+from .validate import validate_program
 
 
 @dataclass
@@ -61,46 +62,55 @@ def split_results(res: dict, n: int, gpu_ms: float | None = None) -> list[ImageR
     return out
 
 
-class GpuPipeline:
-    def __init__(self, yolo: YOLOv5nu, mnet: MobileNetV2, *, device: int = 0, buckets=None, max_det: int | None = None,
+class GpuProgramRunner:
+    """One native Executor running one program, with a hipGraph per batch bucket.
+
+    Base of every GPU model object: the fused pipeline (``GpuPipeline``), the
+    split detector / classifier programs used by the microservices arm and the
+    reference-contract tensor models served by the model server.
+    """
+
+    def __init__(self, program, *, device: int = 0, buckets=None, max_det: int | None = None,
                  crop_cap_per_image: int | None = None, host_threads: int | None = None,
-                 max_image_pixels: int = 640 * 640, conf_thr: float | None = None, iou_thr: float | None = None,
-                 weights: np.ndarray | None = None, share_buffers: bool = True):
+                 pool_bytes_per_image: int = 640 * 640 * 3, weights: np.ndarray | None = None,
+                 share_buffers: bool = True):
         gcfg = get_gpu_config()
-        ycfg = get_model_config("yolov5n")
-        mb = get_controlled_variable("preprocessing", "mobilenet")
-        det_size = int(get_controlled_variable("preprocessing", "yolo")["target_size"])
-        cls_size = int(mb["target_size"])
+        self.program = program
         self.buckets = sorted(int(b) for b in (buckets or gcfg["batch_buckets"]))
-        self.max_det = int(max_det or gcfg["max_det"])
-        self.conf_thr = float(conf_thr if conf_thr is not None else ycfg["confidence_threshold"])
-        self.iou_thr = float(iou_thr if iou_thr is not None else ycfg["iou_threshold"])
-        self.program = plan_pipeline(yolo, mnet, conf_thr=self.conf_thr, iou_thr=self.iou_thr, det_size=det_size,
-                                     cls_size=cls_size, mean=mb["mean"], std=mb["std"], max_det=self.max_det)
+        self.max_det = int(max_det or program.meta.get("max_det") or gcfg["max_det"])
+        self.raw_out_bytes = int(program.meta.get("raw_out_bytes", 0))
         C = native()
         self.ex = C.Executor({
             "device": int(device),
             "max_batch": self.buckets[-1],
             "max_det": self.max_det,
-            "cand_cap": 8400,
+            "cand_cap": int(program.meta.get("cand_cap", 8400)),
             "crop_cap_per_image": int(crop_cap_per_image or gcfg["crop_cap_per_image"]),
-            "pool_bytes_per_image": int(max_image_pixels) * 3,
-            "det_size": det_size,
-            "cls_size": cls_size,
+            "pool_bytes_per_image": int(pool_bytes_per_image),
+            "det_size": int(program.meta.get("det_size", 640)),
+            "cls_size": int(program.meta.get("cls_size", 224)),
             "host_threads": int(host_threads or gcfg["host_threads"]),
+            "raw_out_bytes": self.raw_out_bytes,
         })
-        if weights is not None and weights.nbytes != self.program.weights.nbytes:
+        if weights is not None and weights.nbytes != program.weights.nbytes:
             raise ValueError("weight blob does not match the program's layout")
-        self.ex.set_weights(self.program.weights if weights is None else weights)
-        self.ex.set_program(self.program.ops, self.program.cls_ops)
+        self.ex.set_weights(program.weights if weights is None else weights)
+        self.ex.set_program(program.ops, program.cls_ops)
         self.arena_bytes = {}
         self.offsets = {}
         for B in self.buckets:
-            offs, total = layout(self.program.buffers, B, self.ex.crop_cap_for(B), share=share_buffers)
+            cc = self.ex.crop_cap_for(B)
+            validate_program(program, B, cc, max_det=self.max_det, cand_cap=int(program.meta.get("cand_cap", 8400)),
+                             raw_out_bytes=self.raw_out_bytes)
+            offs, total = layout(program.buffers, B, cc, share=share_buffers)
             self.ex.add_bucket(B, offs, total)
             self.arena_bytes[B] = total
             self.offsets[B] = offs
         self.device = device
+
+    @property
+    def kind(self) -> str:
+        return str(self.program.meta.get("kind", "pipeline"))
 
     def read_buffer(self, name: str, B: int, item: int = 0) -> np.ndarray:
         """Debug: NHWC contents of a planner buffer for one batch item (fp32)."""
@@ -116,6 +126,35 @@ class GpuPipeline:
     def max_batch(self) -> int:
         return self.buckets[-1]
 
+    def run_raw(self, inputs: list[np.ndarray]) -> list[dict]:
+        """Run ``inputs`` through the executor in max-batch chunks; raw result dicts."""
+        out = []
+        for k in range(0, len(inputs), self.max_batch):
+            out.append(self.ex.run(list(inputs[k: k + self.max_batch])))
+        return out
+
+class GpuPipeline(GpuProgramRunner):
+    """The fused detect -> crop -> classify program (monolithic / model-server ensemble)."""
+
+    def __init__(self, yolo: YOLOv5nu, mnet: MobileNetV2, *, device: int = 0, buckets=None, max_det: int | None = None,
+                 crop_cap_per_image: int | None = None, host_threads: int | None = None,
+                 max_image_pixels: int = 640 * 640, conf_thr: float | None = None, iou_thr: float | None = None,
+                 weights: np.ndarray | None = None, share_buffers: bool = True):
+        gcfg = get_gpu_config()
+        ycfg = get_model_config("yolov5n")
+        mb = get_controlled_variable("preprocessing", "mobilenet")
+        det_size = int(get_controlled_variable("preprocessing", "yolo")["target_size"])
+        cls_size = int(mb["target_size"])
+        self.conf_thr = float(conf_thr if conf_thr is not None else ycfg["confidence_threshold"])
+        self.iou_thr = float(iou_thr if iou_thr is not None else ycfg["iou_threshold"])
+        max_det = int(max_det or gcfg["max_det"])
+        program = plan_pipeline(yolo, mnet, conf_thr=self.conf_thr, iou_thr=self.iou_thr, det_size=det_size,
+                                cls_size=cls_size, mean=mb["mean"], std=mb["std"], max_det=max_det)
+        super().__init__(program, device=device, buckets=buckets, max_det=max_det,
+                         crop_cap_per_image=crop_cap_per_image, host_threads=host_threads,
+                         pool_bytes_per_image=int(max_image_pixels) * 3, weights=weights,
+                         share_buffers=share_buffers)
+
     def submit(self, images: list[np.ndarray]) -> int:
         return self.ex.submit([np.ascontiguousarray(i, dtype=np.uint8) for i in images])
 
@@ -129,3 +168,82 @@ class GpuPipeline:
             res = self.ex.run([np.ascontiguousarray(i, dtype=np.uint8) for i in chunk])
             out.extend(split_results(res, len(chunk)))
         return out
+
+
+class GpuDetector(GpuProgramRunner):
+    """Detection-only program (microservices detection service): letterbox -> YOLO -> decode -> NMS."""
+
+    def __init__(self, yolo: YOLOv5nu, *, device: int = 0, buckets=None, conf_thr: float | None = None,
+                 iou_thr: float | None = None, max_det: int | None = None, max_image_pixels: int = 640 * 640,
+                 **kw):
+        ycfg = get_model_config("yolov5n")
+        det_size = int(get_controlled_variable("preprocessing", "yolo")["target_size"])
+        self.conf_thr = float(conf_thr if conf_thr is not None else ycfg["confidence_threshold"])
+        self.iou_thr = float(iou_thr if iou_thr is not None else ycfg["iou_threshold"])
+        max_det = int(max_det or get_gpu_config()["max_det"])
+        prog = plan_detector(yolo, conf_thr=self.conf_thr, iou_thr=self.iou_thr, det_size=det_size, max_det=max_det)
+        super().__init__(prog, device=device, buckets=buckets, max_det=max_det,
+                         pool_bytes_per_image=int(max_image_pixels) * 3, **kw)
+
+    def infer(self, images: list[np.ndarray]) -> list[ImageResult]:
+        imgs = [np.ascontiguousarray(i, dtype=np.uint8) for i in images]
+        out: list[ImageResult] = []
+        for k, res in enumerate(self.run_raw(imgs)):
+            n = min(self.max_batch, len(imgs) - k * self.max_batch)
+            out.extend(split_results(res, n))
+        return out
+
+
+class GpuClassifier(GpuProgramRunner):
+    """Classification-only program (microservices classification service): every input is one crop,
+    resized to 224 and normalised on the device, then MobileNetV2 + top-5 softmax."""
+
+    def __init__(self, mnet: MobileNetV2, *, device: int = 0, buckets=None, max_image_pixels: int = 640 * 640,
+                 **kw):
+        mb = get_controlled_variable("preprocessing", "mobilenet")
+        prog = plan_classifier(mnet, cls_size=int(mb["target_size"]), mean=mb["mean"], std=mb["std"])
+        super().__init__(prog, device=device, buckets=buckets, pool_bytes_per_image=int(max_image_pixels) * 3, **kw)
+
+    def infer(self, crops: list[np.ndarray]) -> list[tuple[np.ndarray, np.ndarray, np.ndarray]]:
+        """Per crop: (top-5 class ids, raw logits, softmax probabilities)."""
+        imgs = [np.ascontiguousarray(i, dtype=np.uint8) for i in crops]
+        out = []
+        for res in self.run_raw(imgs):
+            offs = res["crop_offset"]
+            for i in range(len(offs) - 1):
+                a = int(offs[i])
+                out.append((res["topk_idx"][a], res["topk_logit"][a], res["topk_prob"][a]))
+        return out
+
+
+class GpuTensorModel(GpuProgramRunner):
+    """Reference tensor contract models served by the model server:
+
+    * ``yolov5n``: FP32 [3, 640, 640] -> FP32 [84, 8400] (raw detection head)
+    * ``mobilenetv2``: FP32 [3, 224, 224] (ImageNet-normalised) -> FP32 [1000] logits
+    """
+
+    def __init__(self, program, *, device: int = 0, buckets=None, **kw):
+        S = int(program.meta.get("det_size") if program.meta["kind"] == "yolo_raw" else program.meta["cls_size"])
+        self.input_shape = (3, S, S)
+        self.output_shape = tuple(program.meta["output_shape"])
+        super().__init__(program, device=device, buckets=buckets, pool_bytes_per_image=3 * S * S * 4, **kw)
+
+    @classmethod
+    def yolo(cls, yolo: YOLOv5nu, **kw) -> "GpuTensorModel":
+        det_size = int(get_controlled_variable("preprocessing", "yolo")["target_size"])
+        return cls(plan_yolo_raw(yolo, det_size=det_size), **kw)
+
+    @classmethod
+    def mobilenet(cls, mnet: MobileNetV2, **kw) -> "GpuTensorModel":
+        cls_size = int(get_controlled_variable("preprocessing", "mobilenet")["target_size"])
+        return cls(plan_mobilenet_raw(mnet, cls_size=cls_size), **kw)
+
+    def infer(self, tensors) -> np.ndarray:
+        """``tensors``: float32 [N, 3, S, S] (or a list of [3, S, S]); returns float32 [N, *output_shape]."""
+        xs = [np.ascontiguousarray(t, dtype=np.float32) for t in tensors]
+        for x in xs:
+            if x.shape != self.input_shape:
+                raise ValueError(f"expected input shape {self.input_shape}, got {x.shape}")
+        outs = [r["raw"].view(np.float32).reshape(-1, *self.output_shape) for r in self.run_raw(xs)]
+        return np.concatenate(outs, 0) if outs else np.zeros((0, *self.output_shape), np.float32)

@@ -27,10 +27,12 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   DECODE 1-4 / 5-8 / 9-12 (buf, coff, cs, hw) per level, 13-15 strides,
          16 cand_buf 17 count_buf 18 conf_thr (float bits)
   NMS    1 cand_buf 2 count_buf 3 det_buf 4 detcount_buf 5 iou_thr (float bits)
-  CROPPLAN 1 det_buf 2 detcount_buf 3 crops_buf
+  CROPPLAN 1 det_buf 2 detcount_buf 3 crops_buf 4 whole (1: each image is one crop)
   CROPGATHER 1 crops_buf 2 out_buf 3 S 4-6 mean 7-9 inv_std (float bits)
   AVGPOOL 1 x_buf 2 HW 3 C 4 y_buf 5 batch_kind
   TOPK   1 logits_buf 2 N 3 ld 4 out_buf
+  TENSORIN 1 out_buf 2 S   (fp32 [3,S,S] pool tensors -> space-to-depth bf16)
+  YOLORAW  1-12 heads as DECODE, 13-15 strides, 16 out_buf (raw [84, A] fp32 per image)
 """
 from __future__ import annotations
 
@@ -41,8 +43,9 @@ import numpy as np
 import torch
 
 OP_FIELDS = 48
-OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL, OP_TOPK = range(1, 12)
-BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK = -1, -10, -11, -12, -13, -14, -15
+(OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
+ OP_TOPK, OP_TENSORIN, OP_YOLORAW) = range(1, 14)
+BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK, BUF_RAWOUT = -1, -10, -11, -12, -13, -14, -15, -16
 IMAGES, CROPS = 0, 1
 ACT = {None: 0, "none": 0, "silu": 1, "relu6": 2}
 ALIGN = 256
@@ -172,12 +175,14 @@ class ProgramBuilder:
     def conv(self, src: View, dst: View, w: torch.Tensor, b: torch.Tensor, *, stride: int = 1,
              pad: int | tuple[int, int] | None = None, act: str | None = "silu", res: View | None = None,
              dst2: View | None = None, f32out: bool = False, kind: int = IMAGES,
-             out_hw: tuple[int, int] | None = None, src_hw: tuple[int, int] | None = None) -> None:
+             out_hw: tuple[int, int] | None = None, src_hw: tuple[int, int] | None = None,
+             raw_cs: int | None = None) -> None:
         cout, cin, kh, kw = w.shape
         if cin != src.C:
             raise ValueError(f"conv: weight Cin {cin} != source view C {src.C}")
         if cout != dst.C:
             raise ValueError(f"conv: weight Cout {cout} != destination view C {dst.C}")
+        dst_cs = dst.cs if raw_cs is None else int(raw_cs)
         H, W = src_hw if src_hw else (src.buf.H, src.buf.W)
         if pad is None:
             pad = (kh // 2, kw // 2)
@@ -192,7 +197,7 @@ class ProgramBuilder:
         w_off = self.weights.add(wb)
         b_off = self.weights.add(bb)
         rec = [OP_CONV, src.bid, src.coff, src.cs, H, W, cin, w_off, kpad, b_off,
-               dst.bid, dst.coff, dst.cs, Ho, Wo, cout, cpad, kh, kw, stride, pad[0], pad[1],
+               dst.bid, dst.coff, dst_cs, Ho, Wo, cout, cpad, kh, kw, stride, pad[0], pad[1],
                res.bid if res else BUF_NONE, res.coff if res else 0, res.cs if res else 0,
                dst2.bid if dst2 else BUF_NONE, dst2.coff if dst2 else 0, dst2.cs if dst2 else 0,
                ACT[act], int(f32out), kind]
@@ -231,14 +236,24 @@ class ProgramBuilder:
     def nms(self, cand: Buffer, count: Buffer, iou_thr: float) -> None:
         self._emit([OP_NMS, cand.id, count.id, BUF_DET, BUF_DETCOUNT, fbits(iou_thr)], cand, count)
 
-    def crop_plan(self, crops: Buffer) -> None:
-        self._emit([OP_CROPPLAN, BUF_DET, BUF_DETCOUNT, crops.id], crops)
+    def crop_plan(self, crops: Buffer, whole: bool = False) -> None:
+        self._emit([OP_CROPPLAN, BUF_DET, BUF_DETCOUNT, crops.id, int(whole)], crops)
+
+    def tensor_in(self, out: Buffer, S: int) -> None:
+        self._emit([OP_TENSORIN, out.id, S], out)
+
+    def yolo_raw(self, heads: list[View], strides) -> None:
+        rec = [OP_YOLORAW]
+        for v in heads:
+            rec += [v.bid, v.coff, v.cs, v.buf.H]
+        rec += list(int(s) for s in strides) + [BUF_RAWOUT]
+        self._emit(rec, *heads)
 
     def crop_gather(self, crops: Buffer, out: Buffer, S: int, mean, std) -> None:
         rec = [OP_CROPGATHER, crops.id, out.id, S] + [fbits(m) for m in mean] + [fbits(1.0 / s) for s in std]
         self._emit(rec, crops, out)
 
-    def avgpool(self, x: Buffer, y: Buffer, kind: int = CROPS) -> None:
+    def avgpool(self, x: Buffer, y: Buffer, kind: int = CROPS) -> None:  # noqa: D401
         self._emit([OP_AVGPOOL, x.id, x.H * x.W, x.C, y.id, kind], x, y)
 
     def topk(self, logits: Buffer, N: int, ld: int) -> None:

@@ -28,7 +28,7 @@ import torch
 from ..models.common import fold, fold_conv_bn
 from ..models.mobilenetv2 import MobileNetV2
 from ..models.yolov5nu import STRIDES, YOLOv5nu
-from .planner import CROPS, IMAGES, BUF_NONE, Program, ProgramBuilder, View
+from .planner import BUF_NONE, BUF_RAWOUT, CROPS, IMAGES, Program, ProgramBuilder, View
 
 CAND_BYTES = 32
 CROPREF_BYTES = 32
@@ -75,10 +75,13 @@ def _c3(pb: ProgramBuilder, m, src: View, dst: View, H: int, W: int, name: str) 
     pb.conv(View(T, 0, 2 * c_), dst, w3, b3)
 
 
-def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640):
+def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool = False):
     h = T // 2
     X0 = pb.tensor("x_s2d", h, h, 16)
-    pb.letterbox(X0, T)
+    if tensor_input:
+        pb.tensor_in(X0, T)
+    else:
+        pb.letterbox(X0, T)
     A0 = pb.tensor("b0", h, h, 16)
     w, b = fold(y.b0)
     pb.conv(View(X0, 0, 16), View(A0, 0, 16), s2d_stem_6x6(w), b)
@@ -141,38 +144,49 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640):
     return heads
 
 
-def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std):
+def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std, *, kind: int = CROPS,
+                   raw_logits: bool = False):
+    """MobileNetV2 over crop-gathered inputs (``crops`` = CropRef buffer) or, with
+    ``crops=None``, over fp32 [3,S,S] tensors of the image batch (``kind=IMAGES``)."""
+    CROPS_ = kind
     h = S // 2
-    X = pb.tensor("crop_s2d", h, h, 16, kind=CROPS)
-    pb.crop_gather(crops, X, S, mean, std)
+    X = pb.tensor("crop_s2d", h, h, 16, kind=CROPS_)
+    if crops is None:
+        pb.tensor_in(X, S)
+    else:
+        pb.crop_gather(crops, X, S, mean, std)
     w, b = fold(m.stem)
-    F = pb.tensor("m.stem", h, h, 32, kind=CROPS)
-    pb.conv(View(X, 0, 16), View(F, 0, 32), s2d_stem_3x3(w), b, pad=(1, 1), act="relu6", kind=CROPS,
+    F = pb.tensor("m.stem", h, h, 32, kind=CROPS_)
+    pb.conv(View(X, 0, 16), View(F, 0, 32), s2d_stem_3x3(w), b, pad=(1, 1), act="relu6", kind=CROPS_,
             out_hw=(h, h))
     cur, H = F, h
     for i, blk in enumerate(m.blocks):
         Ho = (H + 2 - 3) // blk.stride + 1
         if blk.expand is not None:
-            E = pb.tensor(f"m{i}.exp", H, H, blk.hidden, kind=CROPS)
-            pb.conv(View(cur, 0, blk.inp), View(E, 0, blk.hidden), *fold(blk.expand), act="relu6", kind=CROPS)
+            E = pb.tensor(f"m{i}.exp", H, H, blk.hidden, kind=CROPS_)
+            pb.conv(View(cur, 0, blk.inp), View(E, 0, blk.hidden), *fold(blk.expand), act="relu6", kind=CROPS_)
         else:
             E = cur
-        Dw = pb.tensor(f"m{i}.dw", Ho, Ho, blk.hidden, kind=CROPS)
+        Dw = pb.tensor(f"m{i}.dw", Ho, Ho, blk.hidden, kind=CROPS_)
         wd, bd = fold(blk.dw)
-        pb.dwconv(View(E, 0, blk.hidden), View(Dw, 0, blk.hidden), wd, bd, stride=blk.stride, kind=CROPS)
-        O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup, kind=CROPS)
+        pb.dwconv(View(E, 0, blk.hidden), View(Dw, 0, blk.hidden), wd, bd, stride=blk.stride, kind=CROPS_)
+        O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup, kind=CROPS_)
         pb.conv(View(Dw, 0, blk.hidden), View(O, 0, blk.oup), *fold(blk.project), act=None,
-                res=View(cur, 0, blk.inp) if blk.use_res else None, kind=CROPS)
+                res=View(cur, 0, blk.inp) if blk.use_res else None, kind=CROPS_)
         cur, H = O, Ho
-    HD = pb.tensor("m.head", H, H, 1280, kind=CROPS)
-    pb.conv(View(cur, 0, cur.C), View(HD, 0, 1280), *fold(m.head), act="relu6", kind=CROPS)
-    PO = pb.tensor("m.pool", 1, 1, 1280, kind=CROPS)
-    pb.avgpool(HD, PO)
+    HD = pb.tensor("m.head", H, H, 1280, kind=CROPS_)
+    pb.conv(View(cur, 0, cur.C), View(HD, 0, 1280), *fold(m.head), act="relu6", kind=CROPS_)
+    PO = pb.tensor("m.pool", 1, 1, 1280, kind=CROPS_)
+    pb.avgpool(HD, PO, kind=CROPS_)
     ncls = m.fc.out_features
-    LG = pb.tensor("m.logits", 1, 1, ncls + (-ncls % 8), kind=CROPS, elem=4)
     wfc = m.fc.weight.detach().float().cpu().reshape(ncls, 1280, 1, 1)
+    if raw_logits:  # reference contract: [1000] fp32 logits per input, straight into the output region
+        pb.conv(View(PO, 0, 1280), View(BUF_RAWOUT, 0, ncls), wfc, m.fc.bias.detach().float().cpu(), act=None,
+                f32out=True, kind=CROPS_, raw_cs=ncls)
+        return
+    LG = pb.tensor("m.logits", 1, 1, ncls + (-ncls % 8), kind=CROPS_, elem=4)
     pb.conv(View(PO, 0, 1280), View(LG, 0, ncls), wfc, m.fc.bias.detach().float().cpu(), act=None, f32out=True,
-            kind=CROPS)
+            kind=CROPS_)
     pb.topk(LG, ncls, LG.C)
 
 
@@ -190,8 +204,51 @@ def plan_pipeline(yolo: YOLOv5nu, mnet: MobileNetV2, *, conf_thr: float, iou_thr
     pb.crop_plan(crops)
     pb.begin_classifier()
     plan_mobilenet(pb, mnet, crops, cls_size, mean, std)
-    return pb.build({"conf_thr": conf_thr, "iou_thr": iou_thr, "det_size": det_size, "cls_size": cls_size,
+    return pb.build({"kind": "pipeline", "conf_thr": conf_thr, "iou_thr": iou_thr, "det_size": det_size, "cls_size": cls_size,
                      "cand_cap": cand_cap, "max_det": max_det})
 
 
-__all__ = ["plan_pipeline", "plan_yolo", "plan_mobilenet", "s2d_stem_6x6", "s2d_stem_3x3", "BUF_NONE", "IMAGES"]
+__all__ = ["plan_pipeline", "plan_detector", "plan_classifier", "plan_yolo_raw", "plan_mobilenet_raw", "plan_yolo", "plan_mobilenet", "s2d_stem_6x6", "s2d_stem_3x3", "BUF_NONE", "IMAGES"]
+
+
+def plan_detector(yolo: YOLOv5nu, *, conf_thr: float, iou_thr: float, det_size: int = 640, cand_cap: int = 8400,
+                  max_det: int = 300) -> Program:
+    """Detection only (microservices detection service): detections per image."""
+    pb = ProgramBuilder()
+    heads = plan_yolo(pb, yolo, det_size)
+    cand = pb.raw("cand", cand_cap * CAND_BYTES)
+    count = pb.raw("cand_count", 4)
+    pb.zero(count)
+    pb.decode(heads, STRIDES, cand, count, conf_thr)
+    pb.nms(cand, count, iou_thr)
+    return pb.build({"kind": "detector", "conf_thr": conf_thr, "iou_thr": iou_thr, "det_size": det_size,
+                     "cand_cap": cand_cap, "max_det": max_det})
+
+
+def plan_classifier(mnet: MobileNetV2, *, cls_size: int = 224, mean=(0.485, 0.456, 0.406),
+                    std=(0.229, 0.224, 0.225), max_det: int = 300) -> Program:
+    """Classification only (microservices classification service): every input image is one crop."""
+    pb = ProgramBuilder()
+    crops = pb.raw("crops", max_det * CROPREF_BYTES, pinned=True)
+    pb.crop_plan(crops, whole=True)
+    pb.begin_classifier()
+    plan_mobilenet(pb, mnet, crops, cls_size, mean, std)
+    return pb.build({"kind": "classifier", "cls_size": cls_size, "max_det": max_det})
+
+
+def plan_yolo_raw(yolo: YOLOv5nu, *, det_size: int = 640) -> Program:
+    """Reference tensor contract of model 'yolov5n': fp32 [3,640,640] -> fp32 [84, 8400]."""
+    pb = ProgramBuilder()
+    heads = plan_yolo(pb, yolo, det_size, tensor_input=True)
+    pb.yolo_raw(heads, STRIDES)
+    A = sum((det_size // s) ** 2 for s in STRIDES)
+    return pb.build({"kind": "yolo_raw", "det_size": det_size, "raw_out_bytes": 84 * A * 4,
+                     "output_shape": [84, A]})
+
+
+def plan_mobilenet_raw(mnet: MobileNetV2, *, cls_size: int = 224) -> Program:
+    """Reference tensor contract of model 'mobilenetv2': fp32 [3,224,224] -> fp32 [1000]."""
+    pb = ProgramBuilder()
+    plan_mobilenet(pb, mnet, None, cls_size, None, None, kind=IMAGES, raw_logits=True)
+    n = mnet.fc.out_features
+    return pb.build({"kind": "mobilenet_raw", "cls_size": cls_size, "raw_out_bytes": n * 4, "output_shape": [n]})

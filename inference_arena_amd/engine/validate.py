@@ -14,6 +14,7 @@ from ..engine.planner import (
     BUF_META,
     BUF_NONE,
     BUF_POOL,
+    BUF_RAWOUT,
     BUF_TOPK,
     CROPS,
     OP_AVGPOOL,
@@ -25,7 +26,9 @@ from ..engine.planner import (
     OP_LETTERBOX,
     OP_NMS,
     OP_SPPF,
+    OP_TENSORIN,
     OP_TOPK,
+    OP_YOLORAW,
     OP_ZERO,
     Program,
 )
@@ -37,13 +40,16 @@ class ProgramError(ValueError):
     pass
 
 
-def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand_cap: int) -> None:
+def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand_cap: int,
+                     raw_out_bytes: int | None = None) -> None:
     sizes = {}
     for b in prog.buffers:
         sizes[b.id] = b.per_item * (crop_cap if b.kind == CROPS else B)
     sizes[BUF_DET] = B * max_det * DET_BYTES
     sizes[BUF_DETCOUNT] = B * 4
     sizes[BUF_TOPK] = B * max_det * TOPK_BYTES
+    raw = int(raw_out_bytes if raw_out_bytes is not None else prog.meta.get("raw_out_bytes", 0))
+    sizes[BUF_RAWOUT] = B * raw
     wbytes = prog.weights.nbytes
     names = {b.id: b.name for b in prog.buffers}
 
@@ -123,5 +129,16 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         elif op == OP_TOPK:
             need(i, r[1], 0, crop_cap * int(r[3]) * 4, "topk logits")
             need(i, r[4], 0, B * max_det * TOPK_BYTES, "topk results")
+        elif op == OP_TENSORIN:
+            S2 = int(r[2]) // 2
+            need(i, r[1], 0, B * S2 * S2 * 32, "tensor input output")
+        elif op == OP_YOLORAW:
+            A = 0
+            for lvl in range(3):
+                buf, coff, cs, hw = (int(v) for v in r[1 + 4 * lvl: 5 + 4 * lvl])
+                view(i, buf, coff, cs, B * hw * hw, 144, 2, f"raw head {lvl}")
+                A += hw * hw
+            if int(r[16]) != BUF_RAWOUT or 84 * A * 4 > raw:
+                raise ProgramError(f"op {i}: raw output needs {84 * A * 4} bytes per image, have {raw}")
         else:
             raise ProgramError(f"op {i}: unknown op {op}")

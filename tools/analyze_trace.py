@@ -20,7 +20,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 KIND = {1: "conv", 2: "dwconv", 3: "sppf", 4: "letterbox", 5: "zero", 6: "decode", 7: "nms", 8: "cropplan",
-        9: "cropgather", 10: "avgpool", 11: "topk"}
+        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw"}
 
 
 def describe(rec) -> str:
