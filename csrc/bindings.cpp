@@ -406,7 +406,11 @@ PYBIND11_MODULE(_C, m) {
              } else {
                throw std::runtime_error("input must be a uint8 HxWx3 image or a float32 [3,S,S] tensor");
              }
-             auto pycb = std::make_shared<py::function>(std::move(cb));
+             // The callback is released on a batcher thread: drop the Python reference under the GIL.
+             std::shared_ptr<py::function> pycb(new py::function(std::move(cb)), [](py::function* fn) {
+               py::gil_scoped_acquire gil;
+               delete fn;
+             });
              ResultCallback f = [pycb](RequestResult&& r) {
                py::gil_scoped_acquire gil;
                py::dict d;
