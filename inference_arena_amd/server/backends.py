@@ -25,10 +25,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 from ..engine.pipeline import ImageResult
-
-
-class Overloaded(RuntimeError):
-    """The request queue is full (maps to HTTP 503)."""
+from .batching import AsyncBatcher, Overloaded  # noqa: F401  (re-exported)
 
 
 class Backend:
@@ -67,33 +64,16 @@ class GpuBatchedBackend(Backend):
                  preferred: list[int] | None = None, max_queue_delay_us: int = 500, max_queue_size: int = 4096,
                  buckets: list[int] | None = None, weights: np.ndarray | None = None):
         from ..engine.pipeline import GpuPipeline
-        from ..ops import native
 
         bk = buckets or sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
         self.pipes = [GpuPipeline(yolo, mnet, device=device, buckets=bk, weights=weights) for _ in range(instances)]
-        self.batcher = native().DynamicBatcher([p.ex for p in self.pipes], {
-            "max_batch": max_batch,
-            "preferred": preferred or [],
-            "max_queue_delay_us": max_queue_delay_us,
-            "max_queue_size": max_queue_size,
-        })
+        self.batcher = AsyncBatcher(self.pipes, max_batch=max_batch, preferred=preferred,
+                                    max_queue_delay_us=max_queue_delay_us, max_queue_size=max_queue_size)
         self.device = device
-        self._closed = False
 
     async def infer(self, image: np.ndarray) -> tuple[ImageResult, dict]:
-        loop = asyncio.get_running_loop()
-        fut: asyncio.Future = loop.create_future()
         t0 = time.perf_counter()
-
-        def done(d):
-            loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(d))
-
-        rid = self.batcher.enqueue(np.ascontiguousarray(image, dtype=np.uint8), done)
-        if rid < 0:
-            raise Overloaded("inference queue full")
-        d = await fut
-        if d["error"]:
-            raise RuntimeError(d["error"])
+        d = await self.batcher.run(np.ascontiguousarray(image, dtype=np.uint8))
         total = (time.perf_counter() - t0) * 1e3
         q = d["queue_us"] / 1e3
         gpu = d["compute_us"] / 1e3
@@ -102,12 +82,10 @@ class GpuBatchedBackend(Backend):
         return _result_from_dict(d), timing
 
     def stats(self) -> dict:
-        return dict(self.batcher.stats())
+        return self.batcher.stats()
 
     def close(self) -> None:
-        if not self._closed:
-            self.batcher.shutdown()
-            self._closed = True
+        self.batcher.close()
 
 
 class CpuReferenceBackend(Backend):

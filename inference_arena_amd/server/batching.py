@@ -1,0 +1,84 @@
+"""asyncio / thread front of the native DynamicBatcher (csrc/runtime/batcher.cpp).
+
+``AsyncBatcher`` owns a DynamicBatcher over the executors of one or more
+``GpuProgramRunner`` instances (the Triton ``instance_group.count``
+equivalent).  ``await run(x)`` enqueues one input (uint8 HxWx3 image or fp32
+[3,S,S] tensor) and resolves when its batch has been collected; the C++
+worker threads call back with the GIL only for the result conversion, so the
+event loop never blocks on GPU work.  ``run_sync`` is the same for threads
+(sync gRPC handlers).
+"""
+from __future__ import annotations
+
+import asyncio
+import threading
+
+import numpy as np
+
+
+class Overloaded(RuntimeError):
+    """The request queue is full (HTTP 503 / gRPC RESOURCE_EXHAUSTED)."""
+
+
+class AsyncBatcher:
+    def __init__(self, runners, *, max_batch: int, preferred: list[int] | None = None,
+                 max_queue_delay_us: int = 500, max_queue_size: int = 4096):
+        from ..ops import native
+
+        self.runners = list(runners)
+        self.max_batch = int(max_batch)
+        self._b = native().DynamicBatcher([r.ex for r in self.runners], {
+            "max_batch": self.max_batch,
+            "preferred": sorted(int(p) for p in (preferred or []) if int(p) <= self.max_batch),
+            "max_queue_delay_us": int(max_queue_delay_us),
+            "max_queue_size": int(max_queue_size),
+        })
+        self._closed = False
+
+    @staticmethod
+    def _prep(x: np.ndarray) -> np.ndarray:
+        if x.dtype == np.uint8:
+            return np.ascontiguousarray(x)
+        return np.ascontiguousarray(x, dtype=np.float32)
+
+    async def run(self, x: np.ndarray) -> dict:
+        loop = asyncio.get_running_loop()
+        fut: asyncio.Future = loop.create_future()
+
+        def done(d):
+            loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(d))
+
+        if self._b.enqueue(self._prep(x), done) < 0:
+            raise Overloaded("inference queue full")
+        d = await fut
+        if d["error"]:
+            raise RuntimeError(d["error"])
+        return d
+
+    async def run_many(self, xs: list[np.ndarray]) -> list[dict]:
+        return list(await asyncio.gather(*(self.run(x) for x in xs)))
+
+    def run_sync(self, x: np.ndarray, timeout: float | None = 60.0) -> dict:
+        ev = threading.Event()
+        box: list = []
+
+        def done(d):
+            box.append(d)
+            ev.set()
+
+        if self._b.enqueue(self._prep(x), done) < 0:
+            raise Overloaded("inference queue full")
+        if not ev.wait(timeout):
+            raise TimeoutError("inference timed out")
+        d = box[0]
+        if d["error"]:
+            raise RuntimeError(d["error"])
+        return d
+
+    def stats(self) -> dict:
+        return dict(self._b.stats())
+
+    def close(self) -> None:
+        if not self._closed:
+            self._closed = True
+            self._b.shutdown()

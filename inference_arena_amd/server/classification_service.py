@@ -1,0 +1,134 @@
+"""Arch B — classification service: gRPC ``inference.ClassificationService`` on :8201.
+
+Reference: architectures/microservices/classification/app/main.py:29-105
+(``grpc.aio`` server, 50 MB message limits, SIGTERM/SIGINT with a 5 s grace)
+and servicer.py:45-159 (``Classify`` decodes the crop, runs MobileNetV2,
+returns softmax top-1 + top-5 with ``TimingInfo``; failures are reported
+in-band in ``error``; ``ClassifyBatch`` loops over ``Classify``).
+
+MI355X design: every RPC only decodes (thread pool) and enqueues its crop
+into the GPU classifier's dynamic batcher, so crops of concurrent requests —
+and all crops of one ``ClassifyBatch`` — run as one batched MobileNetV2 graph
+replay.  ``Health/Check`` is implemented (declared only upstream).
+
+Run: ``python -m inference_arena_amd.server.classification_service``.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import signal
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import grpc
+
+from ..labels import load_labels
+from ..proto import inference_api as pb
+from ..utils.logging import request_id_var, setup_logging
+from ..utils.settings import Settings
+from .crop_codec import decode_crop
+from .service_backends import ClassifierBackend, build_classifier_backend
+
+log = logging.getLogger("arena.classification")
+
+MAX_MESSAGE = 50 * 1024 * 1024
+GRPC_OPTIONS = [("grpc.max_send_message_length", MAX_MESSAGE), ("grpc.max_receive_message_length", MAX_MESSAGE)]
+
+
+class ClassificationServicer:
+    def __init__(self, backend: ClassifierBackend, labels: list[str], decode_threads: int = 8):
+        self.backend = backend
+        self.labels = labels
+        self.pool = ThreadPoolExecutor(max_workers=max(1, decode_threads), thread_name_prefix="crop-decode")
+        self.n_requests = 0
+        self.n_errors = 0
+
+    def _name(self, cid: int) -> str:
+        return self.labels[cid] if 0 <= cid < len(self.labels) else ""
+
+    async def Classify(self, request, context=None):
+        t0 = time.perf_counter()
+        request_id_var.set(request.request_id)
+        self.n_requests += 1
+        try:
+            crop = await asyncio.get_running_loop().run_in_executor(self.pool, decode_crop, request.image_crop)
+            t1 = time.perf_counter()
+            idx, _logit, prob = await self.backend.classify(crop)
+            t2 = time.perf_counter()
+            resp = pb.ClassificationResponse(request_id=request.request_id)
+            cid = int(idx[0])
+            resp.result.class_id = cid
+            resp.result.class_name = self._name(cid)
+            resp.result.confidence = float(prob[0])
+            for k in range(len(idx)):
+                resp.top_k.add(class_id=int(idx[k]), class_name=self._name(int(idx[k])), confidence=float(prob[k]))
+            t3 = time.perf_counter()
+            resp.timing.preprocessing_ms = (t1 - t0) * 1e3
+            resp.timing.inference_ms = (t2 - t1) * 1e3
+            resp.timing.postprocessing_ms = (t3 - t2) * 1e3
+            resp.timing.total_ms = (t3 - t0) * 1e3
+            return resp
+        except Exception as e:  # in-band error, like the reference
+            self.n_errors += 1
+            log.error(f"Classification failed: {e}")
+            return pb.ClassificationResponse(request_id=request.request_id, error=str(e))
+
+    async def ClassifyBatch(self, request, context=None):
+        t0 = time.perf_counter()
+        responses = await asyncio.gather(*(self.Classify(r, context) for r in request.requests))
+        out = pb.BatchClassificationResponse(responses=list(responses))
+        out.batch_timing.total_ms = (time.perf_counter() - t0) * 1e3
+        return out
+
+    def close(self) -> None:
+        self.pool.shutdown(wait=False)
+
+
+class HealthServicer:
+    def __init__(self, ready=lambda: True):
+        self.ready = ready
+
+    async def Check(self, request, context=None):
+        return pb.HealthCheckResponse(status=pb.SERVING if self.ready() else pb.NOT_SERVING)
+
+
+async def start_server(settings: Settings, backend: ClassifierBackend | None = None, port: int | None = None):
+    """Create and start the aio server; returns (server, servicer, bound_port)."""
+    backend = backend or build_classifier_backend(settings)
+    servicer = ClassificationServicer(backend, load_labels(settings.LABELS_FILE or None),
+                                      settings.ARENA_DECODE_THREADS)
+    server = grpc.aio.server(options=GRPC_OPTIONS)
+    server.add_generic_rpc_handlers((pb.ClassificationService.handler(servicer),
+                                     pb.Health.handler(HealthServicer())))
+    bound = server.add_insecure_port(f"{settings.HOST}:{port if port is not None else settings.PORT}")
+    await server.start()
+    log.info("classification service listening", extra={"port": bound})
+    return server, servicer, bound
+
+
+async def serve(settings: Settings) -> None:
+    setup_logging(settings.LOG_LEVEL)
+    server, servicer, _ = await start_server(settings)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        loop.add_signal_handler(sig, stop.set)
+    await stop.wait()
+    log.info("shutting down classification service (5 s grace)")
+    await server.stop(grace=5)
+    servicer.backend.close()
+    servicer.close()
+
+
+def main() -> None:
+    import os
+
+    s = Settings.from_env()
+    if "PORT" not in os.environ:
+        s.PORT = 8201
+    asyncio.run(serve(s))
+
+
+if __name__ == "__main__":
+    main()

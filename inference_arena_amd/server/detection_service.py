@@ -1,0 +1,149 @@
+"""Arch B — detection service: FastAPI ``POST /predict`` on :8200.
+
+Reference: architectures/microservices/detection/app/main.py:29-121 and
+inference.py:99-206 — decode, YOLO in-process, extract every crop, fan the
+crops out to the classification service with one ``Classify`` RPC each via
+``asyncio.gather``, drop crops whose response carries ``error``, answer with
+the shared ``PredictResponse`` (confidence = softmax probability, as the
+classification service returns it).
+
+MI355X design: detection is the ``GpuDetector`` program behind the native
+dynamic batcher (concurrent requests share one batched YOLO replay); the
+event loop never blocks.  ``ARENA_FANOUT=batch`` sends one ``ClassifyBatch``
+per request instead of N RPCs; ``ARENA_CROP_TRANSPORT`` picks jpeg (reference)
+/ png / raw crops.
+
+Run: ``python -m inference_arena_amd.server.detection_service``.
+"""
+from __future__ import annotations
+
+import logging
+from contextlib import asynccontextmanager
+
+from fastapi import FastAPI, HTTPException, Request
+from fastapi.responses import Response
+
+from ..metrics import ArenaMetrics
+from ..processing import extract_crop
+from ..utils.logging import request_id_var, setup_logging
+from ..utils.settings import Settings
+from .app_common import DecodePool, FaultInjector, Timer, new_request_id, read_upload
+from .batching import Overloaded
+from .grpc_client import ClassificationClient
+from .schemas import Classification, DetectionBox, DetectionWithClassification, HealthResponse, PredictResponse
+from .service_backends import DetectorBackend, build_detector_backend
+
+log = logging.getLogger("arena.detection")
+
+
+def create_app(settings: Settings | None = None, detector: DetectorBackend | None = None,
+               client: ClassificationClient | None = None) -> FastAPI:
+    settings = settings or Settings.from_env(PORT=None)
+    state: dict = {"detector": detector, "client": client}
+
+    @asynccontextmanager
+    async def lifespan(app: FastAPI):
+        setup_logging(settings.LOG_LEVEL)
+        log.info("starting detection service", extra={"port": settings.PORT})
+        state["decode"] = DecodePool(settings.ARENA_DECODE_THREADS)
+        state["metrics"] = ArenaMetrics("microservices", str(settings.ARENA_GPU))
+        state["faults"] = FaultInjector(settings.ARENA_FAULT_EVERY)
+        if state["detector"] is None:
+            state["detector"] = build_detector_backend(settings)
+        if state["client"] is None:
+            state["client"] = ClassificationClient(settings.CLASSIFICATION_GRPC_ENDPOINT,
+                                                   transport=settings.ARENA_CROP_TRANSPORT)
+        if not state["client"].connected:
+            await state["client"].connect(ready_timeout=30.0)
+        log.info("service ready")
+        yield
+        await state["client"].close()
+        state["detector"].close()
+        state["decode"].close()
+
+    app = FastAPI(title="Detection Service (MI355X)", version="2.0.0", lifespan=lifespan)
+    app.state.arena = state
+
+    @app.post("/predict", response_model=PredictResponse)
+    async def predict(request: Request):
+        rid = new_request_id()
+        tm = Timer()
+        det_be: DetectorBackend | None = state.get("detector")
+        cl: ClassificationClient | None = state.get("client")
+        metrics: ArenaMetrics = state["metrics"]
+        if det_be is None or cl is None or not cl.connected:
+            metrics.observe("unavailable")
+            raise HTTPException(status_code=503, detail="Service not ready")
+        data = await read_upload(request)
+        try:
+            state["faults"].check()
+            image = await state["decode"].decode(data)
+            t_det = Timer()
+            det, dtiming = await det_be.detect(image)
+            detection_ms = t_det.ms()
+            t_cls = Timer()
+            crops, boxes = [], []
+            for d in det:
+                crops.append(extract_crop(image, d))
+                boxes.append({"x1": float(d[0]), "y1": float(d[1]), "x2": float(d[2]), "y2": float(d[3]),
+                              "confidence": float(d[4]), "class_id": int(d[5])})
+            if not crops:
+                responses = []
+            elif settings.ARENA_FANOUT == "batch":
+                responses = await cl.classify_batch(rid, crops, boxes)
+            else:
+                responses = await cl.classify_parallel(rid, crops, boxes)
+            results = []
+            for box, r in zip(boxes, responses):
+                if r.error:
+                    log.warning(f"Classification error for {r.request_id}: {r.error}")
+                    continue
+                results.append(DetectionWithClassification(
+                    detection=DetectionBox(**box),
+                    classification=Classification(class_id=r.result.class_id, class_name=r.result.class_name,
+                                                  confidence=r.result.confidence)))
+            classification_ms = t_cls.ms()
+        except Overloaded as e:
+            metrics.observe("overloaded")
+            raise HTTPException(status_code=503, detail=str(e)) from e
+        except HTTPException:
+            raise
+        except Exception as e:
+            metrics.observe("error")
+            log.error(f"Predict failed: {e}", extra={"endpoint": "/predict", "status_code": 500})
+            raise HTTPException(status_code=500, detail=str(e)) from e
+        timing = {"detection_ms": detection_ms, "classification_ms": classification_ms, "total_ms": tm.ms()}
+        timing.update({k: float(v) for k, v in dtiming.items()})
+        metrics.observe("ok", {k: v for k, v in timing.items() if k.endswith("_ms")}, len(results),
+                        int(dtiming.get("batch_size", 1)))
+        log.info("Predict complete", extra={"endpoint": "/predict", "latency_ms": timing["total_ms"],
+                                            "detections": len(results), "status_code": 200})
+        return PredictResponse(request_id=rid, detections=results, timing=timing)
+
+    @app.get("/health", response_model=HealthResponse)
+    async def health():
+        request_id_var.set(None)
+        cl = state.get("client")
+        return HealthResponse(status="healthy",
+                              models_loaded=state.get("detector") is not None and cl is not None and cl.connected)
+
+    @app.get("/metrics")
+    async def metrics_ep():
+        return Response(state["metrics"].render(), media_type="text/plain; version=0.0.4")
+
+    return app
+
+
+def main() -> None:
+    import os
+
+    import uvicorn
+
+    s = Settings.from_env()
+    if "PORT" not in os.environ:
+        s.PORT = 8200
+    uvicorn.run(create_app(s), host=s.HOST, port=s.PORT, log_level="warning", access_log=False)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+"""Async client of ``inference.ClassificationService`` (arm B detection side).
+
+Reference: architectures/microservices/detection/app/grpc_client.py:52-168 —
+``grpc.aio`` channel with 50 MB limits, ``connect`` waits for the channel to
+be ready (30 s), ``classify`` encodes the crop (PIL JPEG q95) into a
+``ClassificationRequest{request_id=f"{rid}_{i}", image_crop, source_box}``,
+``classify_parallel`` fans all crops of a request out with
+``asyncio.gather`` (the H1b mechanism).
+
+Additions: ``transport`` selects jpeg (reference) / png / raw crops, and
+``classify_batch`` sends all crops in one ``ClassifyBatch`` RPC.
+"""
+from __future__ import annotations
+
+import asyncio
+
+import grpc
+import numpy as np
+
+from ..proto import inference_api as pb
+from .classification_service import GRPC_OPTIONS
+from .crop_codec import encode_crop
+
+
+class ClassificationClient:
+    def __init__(self, endpoint: str, transport: str = "jpeg", timeout_s: float = 30.0):
+        self.endpoint = endpoint
+        self.transport = transport
+        self.timeout_s = timeout_s
+        self.channel = None
+        self.stub = None
+        self.health = None
+
+    async def connect(self, ready_timeout: float = 30.0) -> None:
+        self.channel = grpc.aio.insecure_channel(self.endpoint, options=GRPC_OPTIONS)
+        await asyncio.wait_for(self.channel.channel_ready(), timeout=ready_timeout)
+        self.stub = pb.ClassificationService.stub(self.channel)
+        self.health = pb.Health.stub(self.channel)
+
+    async def close(self) -> None:
+        if self.channel is not None:
+            await self.channel.close()
+            self.channel = None
+
+    @property
+    def connected(self) -> bool:
+        return self.stub is not None
+
+    def _request(self, rid: str, crop: np.ndarray, box: dict | None):
+        req = pb.ClassificationRequest(request_id=rid, image_crop=encode_crop(crop, self.transport))
+        if box:
+            req.source_box.x1 = float(box["x1"])
+            req.source_box.y1 = float(box["y1"])
+            req.source_box.x2 = float(box["x2"])
+            req.source_box.y2 = float(box["y2"])
+            req.source_box.confidence = float(box["confidence"])
+            req.source_box.class_id = int(box["class_id"])
+        return req
+
+    async def classify(self, rid: str, crop: np.ndarray, box: dict | None = None):
+        try:
+            return await self.stub.Classify(self._request(rid, crop, box), timeout=self.timeout_s)
+        except grpc.aio.AioRpcError as e:
+            return pb.ClassificationResponse(request_id=rid, error=f"{e.code().name}: {e.details()}")
+
+    async def classify_parallel(self, request_id: str, crops: list[np.ndarray], boxes: list[dict]):
+        return await asyncio.gather(*(self.classify(f"{request_id}_{i}", c, b)
+                                      for i, (c, b) in enumerate(zip(crops, boxes))))
+
+    async def classify_batch(self, request_id: str, crops: list[np.ndarray], boxes: list[dict]):
+        breq = pb.BatchClassificationRequest(requests=[self._request(f"{request_id}_{i}", c, b)
+                                                       for i, (c, b) in enumerate(zip(crops, boxes))])
+        try:
+            return list((await self.stub.ClassifyBatch(breq, timeout=self.timeout_s)).responses)
+        except grpc.aio.AioRpcError as e:
+            return [pb.ClassificationResponse(request_id=r.request_id, error=f"{e.code().name}: {e.details()}")
+                    for r in breq.requests]
+
+    async def check_health(self) -> bool:
+        r = await self.health.Check(pb.HealthCheckRequest(), timeout=self.timeout_s)
+        return r.status == pb.SERVING

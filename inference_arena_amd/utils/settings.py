@@ -47,7 +47,9 @@ class Settings(BaseModel):
     ARENA_QUEUE_DELAY_US: int = 500
     ARENA_DECODE_THREADS: int = 8
     ARENA_CONFIDENCE: str = ""          # logit | softmax ('' = topology default)
-    ARENA_CROP_TRANSPORT: str = "jpeg"  # jpeg (reference) | raw
+    ARENA_CROP_TRANSPORT: str = "jpeg"  # jpeg (reference) | png | raw
+    ARENA_FANOUT: str = "parallel"      # parallel (one Classify per crop, reference) | batch (one ClassifyBatch)
+    ARENA_INSTANCES: int = 1            # executor instances per GPU behind one batcher
     ARENA_WEIGHT_SEED: int = 0
     ARENA_FAULT_EVERY: int = 0          # inject a failure every k-th request (0 = off)
 
