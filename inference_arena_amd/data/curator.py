@@ -180,3 +180,12 @@ def curate(counter: Callable[[list[np.ndarray]], Iterable[int]], cfg: CurationCo
 def load_manifest_images(man: DatasetManifest) -> list[np.ndarray]:
     seed = int(man.config.get("stream_seed", 7))
     return [stream_image(seed, int(r["filename"].rsplit("_", 1)[1])) for r in man.images]
+
+
+def workload_images(n: int | None = None, weight_seed: int = 0, n_images: int = 100) -> list[np.ndarray]:
+    """Images of the committed curated workload (``data/synthetic_set/manifest_w<seed>_n<N>.json``)."""
+    root = Path(__file__).resolve().parents[2] / "data" / "synthetic_set"
+    man = DatasetManifest.load(root / f"manifest_w{weight_seed}_n{n_images}.json")
+    if n is not None:
+        man.images = man.images[:n]
+    return load_manifest_images(man)

@@ -51,3 +51,12 @@ def encode_jpeg(img: np.ndarray, quality: int = 90) -> bytes:
     buf = io.BytesIO()
     Image.fromarray(img).save(buf, format="JPEG", quality=quality)
     return buf.getvalue()
+
+
+def encode_png(img: np.ndarray) -> bytes:
+    """Lossless encoding (tests compare server results against in-process runs on the same pixels)."""
+    from PIL import Image
+
+    buf = io.BytesIO()
+    Image.fromarray(img).save(buf, format="PNG", compress_level=1)
+    return buf.getvalue()

@@ -101,7 +101,31 @@ _CONTENTS = {"FP32": "fp32_contents", "FP64": "fp64_contents", "INT32": "int_con
              "UINT32": "uint_contents", "UINT64": "uint64_contents", "BOOL": "bool_contents"}
 
 
+def serialize_bytes(items) -> bytes:
+    """BYTES tensor wire form (Triton/KServe raw contents): 4-byte LE length + payload per element."""
+    out = bytearray()
+    for it in items:
+        b = it if isinstance(it, (bytes, bytearray)) else str(it).encode()
+        out += len(b).to_bytes(4, "little") + b
+    return bytes(out)
+
+
+def deserialize_bytes(buf: bytes) -> list[bytes]:
+    out, i = [], 0
+    while i < len(buf):
+        if i + 4 > len(buf):
+            raise ValueError("truncated BYTES tensor")
+        n = int.from_bytes(buf[i:i + 4], "little")
+        if i + 4 + n > len(buf):
+            raise ValueError("truncated BYTES element")
+        out.append(bytes(buf[i + 4:i + 4 + n]))
+        i += 4 + n
+    return out
+
+
 def datatype_of(arr: np.ndarray) -> str:
+    if arr.dtype == np.object_:
+        return "BYTES"
     for k, v in DTYPES.items():
         if arr.dtype == v:
             return k
@@ -111,10 +135,18 @@ def datatype_of(arr: np.ndarray) -> str:
 def decode_input(req, i: int) -> np.ndarray:
     """Tensor ``i`` of a ModelInferRequest (raw_input_contents or typed contents)."""
     t = req.inputs[i]
+    shape = tuple(int(s) for s in t.shape)
+    if t.datatype == "BYTES":
+        items = (deserialize_bytes(req.raw_input_contents[i]) if len(req.raw_input_contents) > i
+                 else list(t.contents.bytes_contents))
+        if len(items) != int(np.prod(shape)):
+            raise ValueError(f"input '{t.name}': {len(items)} elements for shape {list(shape)}")
+        arr = np.empty(len(items), dtype=object)
+        arr[:] = items
+        return arr.reshape(shape)
     dt = DTYPES.get(t.datatype)
     if dt is None:
         raise ValueError(f"unsupported datatype {t.datatype}")
-    shape = tuple(int(s) for s in t.shape)
     if len(req.raw_input_contents) > i:
         raw = req.raw_input_contents[i]
         a = np.frombuffer(raw, dtype=dt)
@@ -136,10 +168,10 @@ def make_infer_request(model: str, inputs: dict[str, np.ndarray], outputs: list[
                        request_id: str = "", version: str = ""):
     req = ModelInferRequest(model_name=model, model_version=version, id=request_id)  # noqa: F821
     for name, arr in inputs.items():
-        arr = np.ascontiguousarray(arr)
+        arr = np.asarray(arr) if isinstance(arr, np.ndarray) and arr.dtype == np.object_ else np.ascontiguousarray(arr)
         t = req.inputs.add(name=name, datatype=datatype_of(arr))
         t.shape.extend(int(s) for s in arr.shape)
-        req.raw_input_contents.append(arr.tobytes())
+        req.raw_input_contents.append(serialize_bytes(arr.ravel()) if arr.dtype == np.object_ else arr.tobytes())
     for name in outputs or []:
         req.outputs.add(name=name)
     return req

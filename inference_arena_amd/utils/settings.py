@@ -49,6 +49,7 @@ class Settings(BaseModel):
     ARENA_CONFIDENCE: str = ""          # logit | softmax ('' = topology default)
     ARENA_CROP_TRANSPORT: str = "jpeg"  # jpeg (reference) | png | raw
     ARENA_FANOUT: str = "parallel"      # parallel (one Classify per crop, reference) | batch (one ClassifyBatch)
+    ARENA_GATEWAY_MODE: str = "pipeline"  # pipeline (one fused ensemble RPC) | tensor (reference per-model RPCs)
     ARENA_INSTANCES: int = 1            # executor instances per GPU behind one batcher
     ARENA_WEIGHT_SEED: int = 0
     ARENA_FAULT_EVERY: int = 0          # inject a failure every k-th request (0 = off)
