@@ -1,0 +1,173 @@
+"""Closed-loop HTTP load generator for the three topologies.
+
+Semantics follow the reference's experiment spec (experiment.yaml
+``load_testing``): N concurrent users, each sending
+``POST /predict`` (multipart ``file``) and immediately the next request when
+the response arrives (no think time), with warmup / measurement / cooldown
+phases and several runs per (architecture, users) configuration.  Only
+requests *completed* inside the measurement window count.
+
+Outputs per level: a per-request CSV (t, user, latency_ms, status,
+detections), a Locust-compatible ``*_stats.csv`` row set, and a summary
+(p50/p90/p95/p99 latency, throughput_rps, error_rate_percent) — the metrics
+experiment.yaml lists for the hypotheses.
+
+Many users need many sockets: the generator runs one aiohttp session per
+process and can fan out over ``procs`` processes (multiprocessing) so that
+the client is never the bottleneck at high load.
+"""
+from __future__ import annotations
+
+import asyncio
+import csv
+import json
+import multiprocessing as mp
+import random
+import time
+from dataclasses import asdict, dataclass, field
+from pathlib import Path
+
+import numpy as np
+
+
+@dataclass
+class LoadConfig:
+    url: str = "http://127.0.0.1:8100/predict"
+    users: int = 1
+    warmup_s: float = 60.0
+    measure_s: float = 180.0
+    cooldown_s: float = 30.0
+    timeout_s: float = 30.0
+    procs: int = 1
+    seed: int = 42
+    field: str = "file"
+
+
+@dataclass
+class PhaseResult:
+    users: int
+    samples: list = field(default_factory=list)  # (t_end_rel, user, latency_ms, status, detections)
+    wall_s: float = 0.0
+
+
+def _multipart(payload: bytes, fieldname: str):
+    import aiohttp
+
+    fd = aiohttp.FormData()
+    fd.add_field(fieldname, payload, filename="image.jpg", content_type="image/jpeg")
+    return fd
+
+
+async def _user_loop(session, cfg: LoadConfig, uid: int, images: list[bytes], t_start: float, t_stop: float,
+                     out: list) -> None:
+    import aiohttp
+
+    rng = random.Random(cfg.seed * 1000 + uid)
+    while time.perf_counter() < t_stop:
+        img = images[rng.randrange(len(images))]
+        t0 = time.perf_counter()
+        status, ndet = 0, -1
+        try:
+            async with session.post(cfg.url, data=_multipart(img, cfg.field)) as r:
+                body = await r.read()
+                status = r.status
+                if status == 200:
+                    try:
+                        ndet = len(json.loads(body)["detections"])
+                    except (ValueError, KeyError):
+                        ndet = -1
+        except (aiohttp.ClientError, asyncio.TimeoutError):
+            status = 599
+        t1 = time.perf_counter()
+        out.append((t1 - t_start, uid, (t1 - t0) * 1e3, status, ndet))
+
+
+async def _drive(cfg: LoadConfig, users: range, images: list[bytes]) -> list:
+    import aiohttp
+
+    total = cfg.warmup_s + cfg.measure_s + cfg.cooldown_s
+    conn = aiohttp.TCPConnector(limit=0, force_close=False)
+    timeout = aiohttp.ClientTimeout(total=cfg.timeout_s)
+    out: list = []
+    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:
+        t_start = time.perf_counter()
+        await asyncio.gather(*(_user_loop(s, cfg, u, images, t_start, t_start + total, out) for u in users))
+    return out
+
+
+def _proc_main(args):
+    cfg, users, images = args
+    return asyncio.run(_drive(cfg, users, images))
+
+
+def run_level(cfg: LoadConfig, images: list[bytes]) -> PhaseResult:
+    """Run one (users) level with all phases; returns every completed request."""
+    t0 = time.perf_counter()
+    procs = max(1, min(cfg.procs, cfg.users))
+    if procs == 1:
+        samples = asyncio.run(_drive(cfg, range(cfg.users), images))
+    else:
+        chunks = [range(i, cfg.users, procs) for i in range(procs)]
+        with mp.get_context("spawn").Pool(procs) as pool:
+            parts = pool.map(_proc_main, [(cfg, c, images) for c in chunks])
+        samples = [s for p in parts for s in p]
+    return PhaseResult(cfg.users, sorted(samples), time.perf_counter() - t0)
+
+
+def summarize(res: PhaseResult, cfg: LoadConfig) -> dict:
+    lo, hi = cfg.warmup_s, cfg.warmup_s + cfg.measure_s
+    win = [s for s in res.samples if lo <= s[0] < hi]
+    lat = np.array([s[2] for s in win if s[3] == 200], dtype=np.float64)
+    n_err = sum(1 for s in win if s[3] != 200)
+    n = len(win)
+    q = (lambda p: float(np.percentile(lat, p)) if lat.size else float("nan"))  # noqa: E731
+    ndet = [s[4] for s in win if s[3] == 200 and s[4] >= 0]
+    return {
+        "users": res.users,
+        "requests": n,
+        "failures": n_err,
+        "throughput_rps": (n - n_err) / cfg.measure_s if cfg.measure_s > 0 else float("nan"),
+        "error_rate_percent": 100.0 * n_err / n if n else 0.0,
+        "p50_latency_ms": q(50), "p90_latency_ms": q(90), "p95_latency_ms": q(95), "p99_latency_ms": q(99),
+        "mean_latency_ms": float(lat.mean()) if lat.size else float("nan"),
+        "max_latency_ms": float(lat.max()) if lat.size else float("nan"),
+        "mean_detections": float(np.mean(ndet)) if ndet else float("nan"),
+        "measure_s": cfg.measure_s,
+    }
+
+
+def write_level(out_dir: Path, tag: str, res: PhaseResult, summary: dict) -> None:
+    out_dir.mkdir(parents=True, exist_ok=True)
+    with open(out_dir / f"{tag}_requests.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["t_s", "user", "latency_ms", "status", "detections"])
+        w.writerows(res.samples)
+    # Locust-compatible aggregate (the spec'd tool's stats layout)
+    with open(out_dir / f"{tag}_stats.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Type", "Name", "Request Count", "Failure Count", "Median Response Time",
+                    "Average Response Time", "Max Response Time", "Requests/s", "95%", "99%"])
+        w.writerow(["POST", "/predict", summary["requests"], summary["failures"], summary["p50_latency_ms"],
+                    summary["mean_latency_ms"], summary["max_latency_ms"], summary["throughput_rps"],
+                    summary["p95_latency_ms"], summary["p99_latency_ms"]])
+    (out_dir / f"{tag}_summary.json").write_text(json.dumps(summary, indent=2) + "\n")
+
+
+def run_sweep(base: LoadConfig, user_levels: list[int], runs: int, images: list[bytes], out_dir: Path,
+              arch: str, log=print) -> list[dict]:
+    rows = []
+    for users in user_levels:
+        for run in range(1, runs + 1):
+            cfg = LoadConfig(**{**asdict(base), "users": users, "seed": base.seed + run})
+            res = run_level(cfg, images)
+            s = summarize(res, cfg)
+            s.update({"architecture": arch, "run": run})
+            write_level(out_dir, f"{arch}_u{users}_r{run}", res, s)
+            rows.append(s)
+            log(f"[{arch}] users={users} run={run}: {s['throughput_rps']:.1f} req/s "
+                f"p50={s['p50_latency_ms']:.1f} ms p99={s['p99_latency_ms']:.1f} ms err={s['error_rate_percent']:.2f}%")
+    with open(out_dir / f"{arch}_sweep.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+    return rows
