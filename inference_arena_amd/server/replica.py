@@ -1,0 +1,114 @@
+"""One serving replica per GPU (data parallelism for the serving topologies).
+
+Launched by ``parallel.replicas.launch`` with torchrun-style env (RANK,
+WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).  Start-up:
+
+1. join the process group (``nccl`` = RCCL over xGMI on MI355X; ``gloo``
+   for the CPU device),
+2. rank 0 produces the folded weight blob of the arm's program and
+   broadcasts it in one collective; every replica serves identical weights,
+3. bind the HTTP port with ``SO_REUSEPORT`` — all replicas share one port
+   and the kernel spreads connections over them (no proxy hop), or
+   ``--port-stride`` gives each replica its own port behind ``router.py``,
+4. serve the arm (monolithic / detection / gateway) on GPU ``LOCAL_RANK``.
+
+Each response carries ``x-arena-replica: <rank>``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import os
+import socket
+
+
+def _socket(host: str, port: int, reuse_port: bool) -> socket.socket:
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    if reuse_port:
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    s.bind((host, port))
+    s.listen(2048)
+    s.setblocking(False)
+    return s
+
+
+def build_app(arch: str, settings, info):
+    """The arm's FastAPI app with weights broadcast from rank 0."""
+    import numpy as np
+
+    from ..models.zoo import default_models
+    from ..parallel import dist as D
+
+    if arch == "monolithic":
+        from .monolithic import create_app
+
+        if settings.ARENA_DEVICE == "cpu":
+            from .backends import build_backend
+
+            backend = build_backend(settings)
+            D.broadcast_object(None, info)
+        else:
+            from ..config import get_triton_config
+            from ..engine.plans import plan_pipeline
+            from .backends import GpuBatchedBackend
+
+            yolo, mnet = default_models(int(settings.ARENA_WEIGHT_SEED))
+            blob = plan_pipeline(yolo, mnet, conf_thr=0.5, iou_thr=0.45).weights if info.is_main else None
+            blob = D.broadcast_blob(blob, info)
+            db = get_triton_config().get("dynamic_batching", {}) or {}
+            backend = GpuBatchedBackend(yolo, mnet, device=int(settings.ARENA_GPU),
+                                        instances=int(settings.ARENA_INSTANCES),
+                                        max_batch=int(settings.ARENA_MAX_BATCH),
+                                        preferred=list(db.get("preferred_batch_size", [])),
+                                        max_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US),
+                                        weights=np.ascontiguousarray(blob))
+        return create_app(settings, backend)
+    if arch == "detection":
+        from .detection_service import create_app
+
+        return create_app(settings)
+    if arch == "gateway":
+        from .gateway import create_app
+
+        return create_app(settings)
+    raise ValueError(f"unknown arch '{arch}'")
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arch", default="monolithic", choices=["monolithic", "detection", "gateway"])
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=8100)
+    ap.add_argument("--port-stride", type=int, default=0, help="0: shared SO_REUSEPORT port; k: port + k*rank")
+    a = ap.parse_args(argv)
+
+    import uvicorn
+
+    from ..parallel import dist as D
+    from ..utils.settings import Settings
+
+    settings = Settings.from_env()
+    backend = "gloo" if settings.ARENA_DEVICE == "cpu" else None
+    info = D.init_from_env(backend)
+    if settings.ARENA_DEVICE != "cpu":
+        settings.ARENA_GPU = info.local_rank
+    app = build_app(a.arch, settings, info)
+    D.barrier(info)
+    D.shutdown(info)  # the group is only needed for start-up
+
+    @app.middleware("http")
+    async def tag(request, call_next):
+        resp = await call_next(request)
+        resp.headers["x-arena-replica"] = str(info.rank)
+        return resp
+
+    port = a.port + a.port_stride * info.rank
+    sock = _socket(a.host, port, reuse_port=a.port_stride == 0)
+    server = uvicorn.Server(uvicorn.Config(app, log_level="warning", access_log=False))
+    asyncio.run(server.serve(sockets=[sock]))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

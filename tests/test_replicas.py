@@ -1,0 +1,69 @@
+"""Multi-process data-parallel serving on CPU: 2 replicas (gloo group for the
+start-up broadcast) sharing one SO_REUSEPORT port; and the RCCL/gloo blob
+broadcast helper at world size 2."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import urllib.request
+
+import pytest
+
+from inference_arena_amd.data.synthetic import encode_jpeg, synthetic_images
+from inference_arena_amd.parallel.replicas import free_port, launch
+from inference_arena_amd.server.multipart import encode_multipart
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_broadcast_blob_world2():
+    code = r"""
+import numpy as np, torch.distributed as dist
+from inference_arena_amd.parallel import dist as D
+info = D.init_from_env("gloo")
+blob = np.arange(1000, dtype=np.uint8) if info.rank == 0 else None
+out = D.broadcast_blob(blob, info)
+assert out.nbytes == 1000 and out[999] == 999 % 256
+obj = D.broadcast_object({"a": 1} if info.rank == 0 else None, info)
+assert obj == {"a": 1}
+assert D.allreduce_max(float(info.rank), info) == 1.0
+g = D.allgather_floats([float(info.rank)] * 2, info)
+assert g == [[0.0, 0.0], [1.0, 1.0]]
+D.barrier(info); D.shutdown(info)
+print("ok", info.rank)
+"""
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), PYTHONPATH=ROOT)
+        procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "ok 0" in outs[0] and "ok 1" in outs[1]
+
+
+@pytest.mark.slow
+def test_two_cpu_replicas_share_port(tmp_path):
+    port = free_port()
+    rep = launch("monolithic", 2, port=port, env={"ARENA_DEVICE": "cpu", "LOG_LEVEL": "WARNING",
+                                                   "PYTHONPATH": ROOT}, log_dir=str(tmp_path))
+    try:
+        assert rep.wait_ready(240), [open(tmp_path / f"replica_{r}.log").read()[-2000:] for r in range(2)]
+        body, ctype = encode_multipart("file", encode_jpeg(synthetic_images(1, 3, hw=(96, 128))[0]))
+        seen = set()
+        for _ in range(40):  # fresh connection per request -> kernel spreads them over replicas
+            req = urllib.request.Request(f"http://127.0.0.1:{port}/predict", data=body,
+                                         headers={"content-type": ctype})
+            with urllib.request.urlopen(req, timeout=60) as r:
+                assert r.status == 200
+                seen.add(r.headers["x-arena-replica"])
+                assert "detections" in json.loads(r.read())
+            if len(seen) == 2:
+                break
+        assert seen == {"0", "1"}
+    finally:
+        rep.stop()
