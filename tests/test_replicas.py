@@ -67,3 +67,44 @@ def test_two_cpu_replicas_share_port(tmp_path):
         assert seen == {"0", "1"}
     finally:
         rep.stop()
+
+
+def test_router_least_outstanding():
+    import asyncio
+
+    from inference_arena_amd.server.router import Router
+
+    r = Router(["a:1", "b:2", "c:3"])
+    r.inflight.update({"http://a:1": 3, "http://b:2": 1, "http://c:3": 1})
+    picks = {r.pick() for _ in range(4)}
+    assert picks == {"http://b:2", "http://c:3"}
+    r.healthy["http://b:2"] = False
+    assert r.pick() == "http://c:3"
+    asyncio.run(asyncio.sleep(0))
+
+
+def test_router_forwards_to_live_replicas(tmp_path):
+    """Router over two fake monolithic services on separate ports."""
+    from fastapi.testclient import TestClient
+
+    from tests.test_loadgen import _serve
+    from tests.test_server_monolithic import FakeBackend
+
+    from inference_arena_amd.server.monolithic import create_app as mono
+    from inference_arena_amd.server.router import create_app
+    from inference_arena_amd.utils.settings import Settings
+
+    servers = [_serve(mono(Settings(LOG_LEVEL="WARNING"), FakeBackend())) for _ in range(2)]
+    try:
+        app = create_app([f"127.0.0.1:{p}" for _, _, p in servers])
+        body, ctype = encode_multipart("file", encode_jpeg(synthetic_images(1, 3, hw=(64, 64))[0]))
+        with TestClient(app) as c:
+            for _ in range(6):
+                r = c.post("/predict", content=body, headers={"content-type": ctype})
+                assert r.status_code == 200 and len(r.json()["detections"]) == 2
+            served = c.get("/router/stats").json()["served"]
+        assert sum(served.values()) == 6 and all(v >= 1 for v in served.values())
+    finally:
+        for s, t, _ in servers:
+            s.should_exit = True
+            t.join(10)
