@@ -95,6 +95,36 @@ void py_dwconv(const py::dict& d) {
   dwconv3x3(p, stream_of(d));
 }
 
+void py_ir_block(const py::dict& d) {
+  IrParams p{};
+  p.x = ptr<const void*>(d, "x");
+  p.x_cs = req<int>(d, "x_cs");
+  p.H = req<int>(d, "H");
+  p.W = req<int>(d, "W");
+  p.inp = req<int>(d, "inp");
+  p.inp_pad = req<int>(d, "inp_pad");
+  p.hid_pad = req<int>(d, "hid_pad");
+  p.oup = req<int>(d, "oup");
+  p.oup_pad = req<int>(d, "oup_pad");
+  p.stride = req<int>(d, "stride");
+  p.expand = req<int>(d, "expand");
+  p.res = get<int>(d, "res", 0);
+  p.we = ptr<const void*>(d, "we");
+  p.be = ptr<const float*>(d, "be");
+  p.wd = ptr<const void*>(d, "wd");
+  p.bd = ptr<const float*>(d, "bd");
+  p.wp = ptr<const void*>(d, "wp");
+  p.bp = ptr<const float*>(d, "bp");
+  p.y = ptr<void*>(d, "y");
+  p.y_cs = req<int>(d, "y_cs");
+  p.Ho = req<int>(d, "Ho");
+  p.Wo = req<int>(d, "Wo");
+  p.B = req<int>(d, "B");
+  p.bdev = ptr<const int*>(d, "bdev");
+  prepare_kernels();
+  ir_block(p, stream_of(d));
+}
+
 void py_sppf(const py::dict& d) {
   SppfParams p{};
   p.buf = ptr<void*>(d, "buf");
@@ -295,6 +325,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("get_conv_impl", &get_conv_impl);
   m.def("dwconv3x3", &py_dwconv);
   m.def("sppf_pool", &py_sppf);
+  m.def("ir_block", &py_ir_block);
   m.def("letterbox_s2d", &py_letterbox);
   m.def("detect_decode", &py_decode);
   m.def("nms", &py_nms);

@@ -237,6 +237,7 @@ void prepare_kernels() {
   if (done) return;
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
+  ir_prepare();
   done = true;
 }
 

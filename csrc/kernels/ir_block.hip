@@ -1,0 +1,272 @@
+// Fused MobileNetV2 inverted-residual block on CDNA4 matrix cores.
+//
+// Reference computation (ONNX Runtime, per crop, architectures/monolithic/
+// app/inference.py:196 running torchvision's mobilenet_v2): Conv1x1+BN+Clip
+// (expand) -> depthwise Conv3x3+BN+Clip -> Conv1x1+BN (project) [-> Add].
+// Unfused, the expanded tensor is the largest activation of the network
+// (112x112x96 per crop in block 2) and is written to and re-read from HBM
+// twice.  Here one workgroup owns a TH x TW output tile of one crop:
+//
+//   X tile (input + 1-px halo, stride-aware) ........ LDS, loaded once
+//   for each chunk of 32 hidden channels:
+//     E = relu6(X . We^T + be)   MFMA 16x16x32 ...... LDS (zero outside the image:
+//                                                      the depthwise pads the *expanded* map)
+//     D = relu6(dw3x3_S(E) + bd)  VALU, 8 ch / lane .. LDS
+//     acc += Wp[:, chunk] . D     MFMA, accumulators stay in VGPRs
+//   y = acc + bp (+ x)  -> NHWC bf16, 8-byte stores
+//
+// All LDS images use 64-byte rows (32 bf16 channels) whose 16-byte chunks are
+// XOR-swizzled with g[(row>>2)&3], g = {0,2,3,1}: for the 16x16x32 operand
+// read (lane l: row l&15, chunk l>>4) every ds_read_b128 lane group
+// ({0-3,12-15,20-27}, ...) then touches 16 distinct 16-byte bank slots.
+#include "common.h"
+#include "launch.h"
+
+namespace arena {
+
+__device__ __forceinline__ int swz(int row, int chunk) {
+  return row * 64 + ((chunk ^ ((0x78 >> (((row >> 2) & 3) * 2)) & 3)) << 4);
+}
+
+__device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
+
+template <int S, int TH, int TW, int MP, bool EXPAND>
+__global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
+  constexpr int PIN = PH * PW, PIN_PAD = (PIN + 15) / 16 * 16;
+  constexpr int POUT = TH * TW, POUT_PAD = (POUT + 15) / 16 * 16;
+  constexpr int NE = PIN_PAD / 16, NP = POUT_PAD / 16, NPW = (NP + 3) / 4;
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int nslab = p.inp_pad >> 5;
+  uint8_t* Xs = lds;                                    // [nslab][PIN_PAD] rows
+  uint8_t* Es = Xs + nslab * PIN_PAD * 64;              // [PIN_PAD] rows (EXPAND)
+  uint8_t* Ds = Es + (EXPAND ? PIN_PAD * 64 : 0);       // [POUT_PAD] rows
+  uint8_t* Wps = Ds + POUT_PAD * 64;                    // [MP*16] rows
+  uint8_t* Wes = Wps + MP * 16 * 64;                    // [nslab][32] rows (EXPAND)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = lane & 15, kq = lane >> 4;
+  const int tiles_x = (p.Wo + TW - 1) / TW, tiles_y = (p.Ho + TH - 1) / TH;
+  const int tiles = tiles_x * tiles_y;
+  const int b = blockIdx.x / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int t = blockIdx.x - b * tiles;
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  const bf16* xb = (const bf16*)p.x + (size_t)b * p.H * p.W * p.x_cs;
+
+  // ---- input tile (with halo) -> LDS, zero outside the image / past inp
+  const int cpr = p.inp_pad >> 3;
+  for (int i = tid; i < PIN_PAD * cpr; i += 256) {
+    const int pix = i / cpr, c = i - pix * cpr;
+    const int py = pix / PW, px = pix - py * PW;
+    const int iy = iy0 + py, ix = ix0 + px;
+    uint4 v = {0u, 0u, 0u, 0u};
+    if (pix < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && c * 8 < p.inp)
+      v = *(const uint4*)(xb + ((size_t)iy * p.W + ix) * p.x_cs + c * 8);
+    *(uint4*)(Xs + (c >> 2) * PIN_PAD * 64 + swz(pix, c & 3)) = v;
+  }
+
+  f32x4 acc[NPW][MP];
+#pragma unroll
+  for (int q = 0; q < NPW; ++q)
+#pragma unroll
+    for (int m = 0; m < MP; ++m) acc[q][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nchunks = p.hid_pad >> 5;
+  for (int h = 0; h < nchunks; ++h) {
+    const int h0 = h * 32;
+    __syncthreads();  // previous chunk's readers are done; X tile visible
+    for (int i = tid; i < MP * 16 * 4; i += 256) {
+      const int r = i >> 2, c = i & 3;
+      *(uint4*)(Wps + swz(r, c)) = *(const uint4*)((const bf16*)p.wp + (size_t)r * p.hid_pad + h0 + c * 8);
+    }
+    if constexpr (EXPAND) {
+      for (int i = tid; i < 32 * cpr; i += 256) {
+        const int r = i / cpr, c = i - r * cpr;
+        *(uint4*)(Wes + (c >> 2) * 32 * 64 + swz(r, c & 3)) =
+            *(const uint4*)((const bf16*)p.we + (size_t)(h0 + r) * p.inp_pad + c * 8);
+      }
+    }
+    __syncthreads();
+
+    const uint8_t* Esrc;
+    if constexpr (EXPAND) {
+      // E[pix][32 hidden] = relu6(We_chunk . X^T + be): A = We rows (hidden), B = X rows (pixels)
+      for (int j = wave; j < NE; j += 4) {
+        f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
+        for (int sl = 0; sl < nslab; ++sl) {
+          const bf16x8 bv = *(const bf16x8*)(Xs + sl * PIN_PAD * 64 + swz(j * 16 + row, kq));
+          const bf16x8 a0 = *(const bf16x8*)(Wes + sl * 32 * 64 + swz(row, kq));
+          const bf16x8 a1 = *(const bf16x8*)(Wes + sl * 32 * 64 + swz(16 + row, kq));
+          e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bv, e0, 0, 0, 0);
+          e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bv, e1, 0, 0, 0);
+        }
+        const int pix = j * 16 + row;
+        const int py = pix / PW, px = pix - py * PW;
+        const int iy = iy0 + py, ix = ix0 + px;
+        const bool inb = pix < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int hc = mt * 16 + kq * 4;
+          const float4 bb = *(const float4*)(p.be + h0 + hc);
+          const f32x4 e = mt ? e1 : e0;
+          float v[4] = {relu6(e[0] + bb.x), relu6(e[1] + bb.y), relu6(e[2] + bb.z), relu6(e[3] + bb.w)};
+          if (!inb) v[0] = v[1] = v[2] = v[3] = 0.f;
+          *(uint2*)(Es + swz(pix, hc >> 3) + (hc & 7) * 2) = pack4(v);
+        }
+      }
+      __syncthreads();
+      Esrc = Es;
+    } else {
+      Esrc = Xs + h * PIN_PAD * 64;  // hidden == input channels
+    }
+
+    // depthwise 3x3 stride S: one (output pixel, 8-channel chunk) per item
+    for (int i = tid; i < POUT_PAD * 4; i += 256) {
+      const int q = i >> 2, c = i & 3;
+      uint4 outv = {0u, 0u, 0u, 0u};
+      if (q < POUT) {
+        const int oy = q / TW, ox = q - oy * TW;
+        float a[8];
+        const float4 b0 = *(const float4*)(p.bd + h0 + c * 8);
+        const float4 b1 = *(const float4*)(p.bd + h0 + c * 8 + 4);
+        a[0] = b0.x; a[1] = b0.y; a[2] = b0.z; a[3] = b0.w;
+        a[4] = b1.x; a[5] = b1.y; a[6] = b1.z; a[7] = b1.w;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int pin = (oy * S + ky) * PW + ox * S + kx;
+            float e[8], w[8];
+            unpack8(*(const uint4*)(Esrc + swz(pin, c)), e);
+            unpack8(*(const uint4*)((const bf16*)p.wd + (ky * 3 + kx) * p.hid_pad + h0 + c * 8), w);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a[k] = fmaf(e[k], w[k], a[k]);
+          }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] = relu6(a[k]);
+        outv = pack8(a);
+      }
+      *(uint4*)(Ds + swz(q, c)) = outv;
+    }
+    __syncthreads();
+
+    // project: acc[pixel tile][oup tile] += Wp[oup][chunk] . D[chunk][pixels]
+#pragma unroll
+    for (int q = 0; q < NPW; ++q) {
+      const int j = wave + 4 * q;
+      if (j < NP) {
+        const bf16x8 bv = *(const bf16x8*)(Ds + swz(j * 16 + row, kq));
+#pragma unroll
+        for (int m = 0; m < MP; ++m) {
+          const bf16x8 av = *(const bf16x8*)(Wps + swz(m * 16 + row, kq));
+          acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[q][m], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: bias (+ residual from the staged input tile) -> NHWC bf16
+  bf16* yb = (bf16*)p.y + (size_t)b * p.Ho * p.Wo * p.y_cs;
+#pragma unroll
+  for (int q = 0; q < NPW; ++q) {
+    const int j = wave + 4 * q;
+    if (j >= NP) continue;
+    const int pix = j * 16 + row;
+    if (pix >= POUT) continue;
+    const int ly = pix / TW, lx = pix - (pix / TW) * TW;
+    const int oy = oy0 + ly, ox = ox0 + lx;
+    if (oy >= p.Ho || ox >= p.Wo) continue;
+    bf16* yp = yb + ((size_t)oy * p.Wo + ox) * p.y_cs;
+    const int rpix = (ly * S + 1) * PW + lx * S + 1;  // same pixel in the input tile (S == 1 when res)
+#pragma unroll
+    for (int m = 0; m < MP; ++m) {
+      const int oc = m * 16 + kq * 4;
+      if (oc >= p.oup) continue;
+      const float4 bb = *(const float4*)(p.bp + oc);
+      float v[4] = {acc[q][m][0] + bb.x, acc[q][m][1] + bb.y, acc[q][m][2] + bb.z, acc[q][m][3] + bb.w};
+      if (p.res) {
+        float r[4];
+        unpack4(*(const uint2*)(Xs + (oc >> 5) * PIN_PAD * 64 + swz(rpix, (oc & 31) >> 3) + (oc & 7) * 2), r);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] += r[k];
+      }
+      *(uint2*)(yp + oc) = pack4(v);
+    }
+  }
+}
+
+template <int S, int TH, int TW, int MP, bool EXPAND>
+static size_t ir_lds_bytes(int inp_pad) {
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
+  constexpr int PIN_PAD = (PH * PW + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
+  const int nslab = inp_pad / 32;
+  return (size_t)nslab * PIN_PAD * 64 + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64 + MP * 16 * 64 +
+         (EXPAND ? nslab * 32 * 64 : 0);
+}
+
+template <int S, int TH, int TW, int MP, bool EXPAND>
+static void ir_launch(const IrParams& p, hipStream_t s) {
+  const size_t lds = ir_lds_bytes<S, TH, TW, MP, EXPAND>(p.inp_pad);
+  if (lds > 160 * 1024) throw std::runtime_error("ir_block: LDS budget exceeded");
+  const int tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW);
+  const long grid = (long)p.B * tiles;
+  if (grid <= 0) return;
+  hipLaunchKernelGGL((ir_block_kernel<S, TH, TW, MP, EXPAND>), dim3((unsigned)grid), dim3(256), lds, s, p);
+}
+
+template <int S, int TH, int TW, int MP, bool EXPAND>
+static void ir_set_attr() {
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_block_kernel<S, TH, TW, MP, EXPAND>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+
+// Supported (stride, tile, oup tiles, expand) combinations: the 17 blocks of
+// MobileNetV2 at 224 (8x8 tiles at 112/56, 7x7 tiles from 28 down).
+#define ARENA_IR_CONFIGS(X)                                          \
+  X(1, 8, 8, 1, false)                                               \
+  X(2, 8, 8, 2, true)                                                \
+  X(1, 8, 8, 2, true)                                                \
+  X(2, 7, 7, 2, true)                                                \
+  X(1, 7, 7, 2, true)                                                \
+  X(2, 7, 7, 4, true)                                                \
+  X(1, 7, 7, 4, true)                                                \
+  X(1, 7, 7, 6, true)                                                \
+  X(2, 7, 7, 10, true)                                               \
+  X(1, 7, 7, 10, true)                                               \
+  X(1, 7, 7, 20, true)
+
+void ir_prepare() {
+#define X(S, TH, TW, MP, E) ir_set_attr<S, TH, TW, MP, E>();
+  ARENA_IR_CONFIGS(X)
+#undef X
+}
+
+int ir_tile(int Ho) { return (Ho % 8 == 0 && Ho >= 56) ? 8 : 7; }
+
+void ir_block(const IrParams& p, hipStream_t s) {
+  if (p.inp_pad % 32 || p.hid_pad % 32 || p.oup_pad % 16 || p.inp % 8 || p.oup % 4 || p.oup > p.oup_pad ||
+      p.inp > p.inp_pad)
+    throw std::runtime_error("ir_block: bad channel geometry");
+  if (!p.expand && p.hid_pad != p.inp_pad) throw std::runtime_error("ir_block: no-expand needs hid_pad == inp_pad");
+  if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_block: residual needs s1, inp == oup");
+  if (p.Ho != (p.H + 2 - 3) / p.stride + 1 || p.Wo != (p.W + 2 - 3) / p.stride + 1)
+    throw std::runtime_error("ir_block: output size mismatch");
+  const int T = ir_tile(p.Ho);
+  const int MP = p.oup_pad / 16;
+  const bool E = p.expand != 0;
+#define X(S_, TH_, TW_, MP_, E_)                                                     \
+  if (p.stride == S_ && T == TH_ && MP == MP_ && E == E_) {                         \
+    ir_launch<S_, TH_, TW_, MP_, E_>(p, s);                                         \
+    return;                                                                         \
+  }
+  ARENA_IR_CONFIGS(X)
+#undef X
+  throw std::runtime_error("ir_block: unsupported configuration (stride " + std::to_string(p.stride) + ", tile " +
+                           std::to_string(T) + ", oup_pad " + std::to_string(p.oup_pad) + ", expand " +
+                           std::to_string(p.expand) + ")");
+}
+
+}  // namespace arena

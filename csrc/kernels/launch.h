@@ -54,6 +54,31 @@ struct DwParams {
 };
 void dwconv3x3(const DwParams& p, hipStream_t s);
 
+// ---------------------------------------------------------------- fused inverted residual (K11+K12)
+// MobileNetV2 block: 1x1 expand (+ReLU6) -> 3x3 depthwise stride S (+ReLU6)
+// -> 1x1 project (+ residual).  The expanded and depthwise tensors live only
+// in LDS (one output tile per workgroup, hidden channels in chunks of 32).
+struct IrParams {
+  const void* x;            // NHWC bf16 view (base already at its channel offset)
+  int x_cs, H, W;
+  int inp, inp_pad;         // inp_pad: multiple of 32
+  int hid_pad;              // multiple of 32 (no-expand blocks: == inp_pad)
+  int oup, oup_pad;         // oup_pad: multiple of 16
+  int stride, expand, res;
+  const void* we;           // bf16 [hid_pad][inp_pad]
+  const float* be;          // [hid_pad]
+  const void* wd;           // bf16 [9][hid_pad]
+  const float* bd;          // [hid_pad]
+  const void* wp;           // bf16 [oup_pad][hid_pad]
+  const float* bp;          // [oup_pad]
+  void* y;
+  int y_cs, Ho, Wo;
+  int B;
+  const int* bdev;
+};
+void ir_block(const IrParams& p, hipStream_t s);
+void ir_prepare();
+
 // ---------------------------------------------------------------- SPPF pools (K5)
 // x: [B,H,W] channels [0,C) of a buffer with pixel stride xs; writes the
 // cascaded 5x5 max pools (== 5/9/13 windows) into channel slices C, 2C, 3C.

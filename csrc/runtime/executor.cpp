@@ -310,6 +310,35 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         dwconv3x3(p, s);
         break;
       }
+      case OP_IRBLOCK: {
+        IrParams p{};
+        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.x_cs = (int)r[3];
+        p.H = (int)r[4];
+        p.W = (int)r[5];
+        p.inp = (int)r[6];
+        p.inp_pad = (int)r[7];
+        p.hid_pad = (int)r[8];
+        p.oup = (int)r[9];
+        p.oup_pad = (int)r[10];
+        p.stride = (int)r[11];
+        p.expand = (int)r[12];
+        p.res = (int)r[13];
+        p.we = W + r[14];
+        p.be = (const float*)(W + r[15]);
+        p.wd = W + r[16];
+        p.bd = (const float*)(W + r[17]);
+        p.wp = W + r[18];
+        p.bp = (const float*)(W + r[19]);
+        p.y = resolve(bk, sl, r[20], r[21], 2);
+        p.y_cs = (int)r[22];
+        p.Ho = (int)r[23];
+        p.Wo = (int)r[24];
+        p.B = batch(r[25]);
+        p.bdev = bdev(r[25]);
+        ir_block(p, s);
+        break;
+      }
       case OP_SPPF: {
         SppfParams p{};
         p.buf = resolve(bk, sl, r[1], r[2], 2);

@@ -51,6 +51,7 @@ enum OpType : int64_t {
   OP_TOPK = 11,
   OP_TENSORIN = 12,
   OP_YOLORAW = 13,
+  OP_IRBLOCK = 14,
 };
 
 // Reserved buffer ids (the planner's arena buffers are ids >= 0).

@@ -33,6 +33,9 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   TOPK   1 logits_buf 2 N 3 ld 4 out_buf
   TENSORIN 1 out_buf 2 S   (fp32 [3,S,S] pool tensors -> space-to-depth bf16)
   YOLORAW  1-12 heads as DECODE, 13-15 strides, 16 out_buf (raw [84, A] fp32 per image)
+  IRBLOCK  1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 inp 7 inp_pad 8 hid_pad 9 oup 10 oup_pad 11 stride
+           12 expand 13 res 14 we 15 be 16 wd 17 bd 18 wp 19 bp 20 y_buf 21 y_coff 22 y_cs 23 Ho 24 Wo
+           25 batch_kind   (fused MobileNetV2 inverted residual, csrc/kernels/ir_block.hip)
 """
 from __future__ import annotations
 
@@ -44,7 +47,7 @@ import torch
 
 OP_FIELDS = 48
 (OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
- OP_TOPK, OP_TENSORIN, OP_YOLORAW) = range(1, 14)
+ OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK) = range(1, 15)
 BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK, BUF_RAWOUT = -1, -10, -11, -12, -13, -14, -15, -16
 IMAGES, CROPS = 0, 1
 ACT = {None: 0, "none": 0, "silu": 1, "relu6": 2}
@@ -131,6 +134,34 @@ def pack_conv_weight(w: torch.Tensor, b: torch.Tensor) -> tuple[bytes, bytes, in
     return bf16_bytes(wk), bb.numpy().tobytes(), kpad, cpad
 
 
+def pack_ir_weights(expand, dw, project, inp: int) -> dict:
+    """Padded operand layouts of the fused inverted-residual kernel (csrc/kernels/ir_block.hip):
+    we [hid_pad][inp_pad], wd [9][hid_pad], wp [oup_pad][hid_pad] (bf16) + fp32 biases."""
+    wd, bd = dw
+    wp, bp = project
+    hid, oup = wd.shape[0], wp.shape[0]
+    inp_pad = _round(inp, 32)
+    hid_pad = inp_pad if expand is None else _round(hid, 32)
+    oup_pad = _round(oup, 16)
+    if expand is None and hid != inp:
+        raise ValueError("ir_block without expand needs hidden == inp")
+    we = torch.zeros(hid_pad, inp_pad)
+    be = torch.zeros(hid_pad)
+    if expand is not None:
+        we[:hid, :inp] = expand[0].reshape(hid, inp)
+        be[:hid] = expand[1]
+    wdp = torch.zeros(9, hid_pad)
+    wdp[:, :hid] = wd.reshape(hid, 9).t()
+    bdp = torch.zeros(hid_pad)
+    bdp[:hid] = bd
+    wpp = torch.zeros(oup_pad, hid_pad)
+    wpp[:oup, :hid] = wp.reshape(oup, hid)
+    bpp = torch.zeros(oup_pad)
+    bpp[:oup] = bp
+    return {"we": we, "be": be, "wd": wdp, "bd": bdp, "wp": wpp, "bp": bpp, "inp": inp, "inp_pad": inp_pad,
+            "hid_pad": hid_pad, "oup": oup, "oup_pad": oup_pad}
+
+
 class ProgramBuilder:
     def __init__(self) -> None:
         self.buffers: list[Buffer] = []
@@ -215,6 +246,24 @@ class ProgramBuilder:
         b_off = self.weights.add(b.detach().float().numpy().tobytes())
         rec = [OP_DWCONV, src.bid, src.coff, src.cs, H, W, C, w_off, b_off, dst.bid, dst.coff, dst.cs,
                Ho, Wo, stride, ACT[act], kind]
+        self._emit(rec, src, dst)
+
+    def ir_block(self, src: View, dst: View, expand, dw, project, *, stride: int, res: bool,
+                 kind: int = CROPS) -> None:
+        """Fused inverted residual: ``expand`` = (w [hid,inp,1,1], b) or None (t = 1 blocks),
+        ``dw`` = (w [hid,1,3,3], b), ``project`` = (w [oup,hid,1,1], b); BN already folded."""
+        if dst.C != project[0].shape[0]:
+            raise ValueError(f"ir_block: destination C {dst.C} != oup {project[0].shape[0]}")
+        pk = pack_ir_weights(expand, dw, project, src.C)
+        inp, inp_pad, hid_pad, oup, oup_pad = pk["inp"], pk["inp_pad"], pk["hid_pad"], pk["oup"], pk["oup_pad"]
+        f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
+        offs = [self.weights.add(bf16_bytes(pk["we"])), self.weights.add(f32(pk["be"])),
+                self.weights.add(bf16_bytes(pk["wd"])), self.weights.add(f32(pk["bd"])),
+                self.weights.add(bf16_bytes(pk["wp"])), self.weights.add(f32(pk["bp"]))]
+        H, W = src.buf.H, src.buf.W
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        rec = [OP_IRBLOCK, src.bid, src.coff, src.cs, H, W, inp, inp_pad, hid_pad, oup, oup_pad, stride,
+               int(expand is not None), int(res), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind]
         self._emit(rec, src, dst)
 
     def sppf(self, buf: Buffer, C: int, kind: int = IMAGES) -> None:

@@ -23,6 +23,8 @@ Lowering rules (what replaces ONNX graph nodes):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..models.common import fold, fold_conv_bn
@@ -144,11 +146,22 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
     return heads
 
 
+def fuse_ir_default() -> bool:
+    """Fused inverted-residual blocks (csrc/kernels/ir_block.hip) unless ARENA_FUSE_IR=0."""
+    return os.environ.get("ARENA_FUSE_IR", "1") != "0"
+
+
 def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std, *, kind: int = CROPS,
-                   raw_logits: bool = False):
+                   raw_logits: bool = False, fuse_ir: bool | None = None):
     """MobileNetV2 over crop-gathered inputs (``crops`` = CropRef buffer) or, with
-    ``crops=None``, over fp32 [3,S,S] tensors of the image batch (``kind=IMAGES``)."""
+    ``crops=None``, over fp32 [3,S,S] tensors of the image batch (``kind=IMAGES``).
+
+    ``fuse_ir``: each inverted-residual block is one fused kernel (expand ->
+    depthwise -> project, intermediates in LDS) instead of three ops with the
+    expanded tensor round-tripping through HBM."""
     CROPS_ = kind
+    if fuse_ir is None:
+        fuse_ir = fuse_ir_default()
     h = S // 2
     X = pb.tensor("crop_s2d", h, h, 16, kind=CROPS_)
     if crops is None:
@@ -162,6 +175,13 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
     cur, H = F, h
     for i, blk in enumerate(m.blocks):
         Ho = (H + 2 - 3) // blk.stride + 1
+        if fuse_ir:
+            O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup, kind=CROPS_)
+            pb.ir_block(View(cur, 0, blk.inp), View(O, 0, blk.oup),
+                        fold(blk.expand) if blk.expand is not None else None, fold(blk.dw), fold(blk.project),
+                        stride=blk.stride, res=blk.use_res, kind=CROPS_)
+            cur, H = O, Ho
+            continue
         if blk.expand is not None:
             E = pb.tensor(f"m{i}.exp", H, H, blk.hidden, kind=CROPS_)
             pb.conv(View(cur, 0, blk.inp), View(E, 0, blk.hidden), *fold(blk.expand), act="relu6", kind=CROPS_)

@@ -23,6 +23,7 @@ from ..engine.planner import (
     OP_CROPPLAN,
     OP_DECODE,
     OP_DWCONV,
+    OP_IRBLOCK,
     OP_LETTERBOX,
     OP_NMS,
     OP_SPPF,
@@ -99,6 +100,24 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             view(i, r[9], int(r[10]), int(r[11]), n * Ho * Wo, C, 2, "dw output")
             weights(i, int(r[7]), 9 * C * 2, "dw weight")
             weights(i, int(r[8]), C * 4, "dw bias")
+        elif op == OP_IRBLOCK:
+            n = kind_n(r[25])
+            H, W, inp, inp_pad, hid_pad, oup, oup_pad, S = (int(v) for v in r[4:12])
+            Ho, Wo = int(r[23]), int(r[24])
+            if inp_pad % 32 or hid_pad % 32 or oup_pad % 16 or inp > inp_pad or oup > oup_pad or inp % 8:
+                raise ProgramError(f"op {i}: bad ir_block channel geometry")
+            if Ho != (H - 1) // S + 1 or Wo != (W - 1) // S + 1:
+                raise ProgramError(f"op {i}: ir_block output size mismatch")
+            if int(r[13]) and (S != 1 or inp != oup):
+                raise ProgramError(f"op {i}: ir_block residual needs stride 1 and inp == oup")
+            view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, 2, "ir input")
+            view(i, r[20], int(r[21]), int(r[22]), n * Ho * Wo, oup, 2, "ir output")
+            weights(i, int(r[14]), hid_pad * inp_pad * 2, "ir expand weight")
+            weights(i, int(r[15]), hid_pad * 4, "ir expand bias")
+            weights(i, int(r[16]), 9 * hid_pad * 2, "ir dw weight")
+            weights(i, int(r[17]), hid_pad * 4, "ir dw bias")
+            weights(i, int(r[18]), oup_pad * hid_pad * 2, "ir project weight")
+            weights(i, int(r[19]), oup_pad * 4, "ir project bias")
         elif op == OP_SPPF:
             n = kind_n(r[7])
             view(i, r[1], int(r[2]), int(r[3]), n * int(r[4]) * int(r[5]), 4 * int(r[6]), 2, "sppf buffer")

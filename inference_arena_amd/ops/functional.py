@@ -85,6 +85,27 @@ def dwconv3x3_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride:
     return y
 
 
+def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: bool = False,
+                  bdev: torch.Tensor | None = None) -> torch.Tensor:
+    """Fused MobileNetV2 inverted residual (expand 1x1+ReLU6 -> dw3x3+ReLU6 -> project 1x1 [+x]).
+    ``expand``/``dw``/``project`` are (weight, bias) pairs with BN folded; ``expand`` None for t=1."""
+    from ..engine.planner import pack_ir_weights
+
+    B, H, W, C = x.shape
+    pk = pack_ir_weights(expand, dw, project, C)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y = torch.empty(B, Ho, Wo, pk["oup"], dtype=torch.bfloat16, device=x.device)
+    dev = {k: (pk[k].to(torch.bfloat16) if k in ("we", "wd", "wp") else pk[k].float()).contiguous().to(x.device)
+           for k in ("we", "be", "wd", "bd", "wp", "bp")}
+    native().ir_block({"x": _ptr(x), "x_cs": C, "H": H, "W": W, "inp": C, "inp_pad": pk["inp_pad"],
+                       "hid_pad": pk["hid_pad"], "oup": pk["oup"], "oup_pad": pk["oup_pad"], "stride": stride,
+                       "expand": int(expand is not None), "res": int(res),
+                       **{k: _ptr(v) for k, v in dev.items()}, "y": _ptr(y), "y_cs": pk["oup"], "Ho": Ho,
+                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "stream": _stream()})
+    torch.cuda.synchronize(x.device)  # keep the packed weights alive until the kernel ran
+    return y
+
+
 def sppf_nhwc(buf: torch.Tensor, C: int) -> torch.Tensor:
     """In place: buf[..., C:4C] = cascaded 5x5 max pools of buf[..., :C]."""
     B, H, W, Ct = buf.shape

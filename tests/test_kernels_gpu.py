@@ -192,3 +192,59 @@ def test_topk_and_avgpool(device):
     y = AF.avgpool_nhwc(x.to(device))
     torch.cuda.synchronize()
     _check(y.cpu().float(), x.float().mean((1, 2)), rtol=1e-2, atol=1e-2)
+
+
+def _ref_ir(x_nhwc, expand, dw, project, stride, res):
+    """fp32 torch reference of one inverted residual on bf16-rounded operands."""
+    x = _nchw(x_nhwc).float()
+    h = x
+    if expand is not None:
+        h = F.relu6(F.conv2d(h, _bf(expand[0]), expand[1].float()))
+        h = _bf(h)  # the kernel stores the expanded tile as bf16
+    hid = dw[0].shape[0]
+    h = F.relu6(F.conv2d(h, _bf(dw[0]), dw[1].float(), stride=stride, padding=1, groups=hid))
+    h = _bf(h)
+    y = F.conv2d(h, _bf(project[0]), project[1].float())
+    return y + x if res else y
+
+
+@pytest.mark.parametrize(
+    "B,H,inp,hid,oup,s,res",
+    [
+        (2, 112, 32, 32, 16, 1, False),   # block 1: no expand
+        (2, 112, 16, 96, 24, 2, False),   # block 2: 112 -> 56
+        (2, 56, 24, 144, 24, 1, True),    # hidden 144 padded to 160
+        (1, 56, 24, 144, 32, 2, False),
+        (2, 28, 32, 192, 32, 1, True),
+        (1, 28, 32, 192, 64, 2, False),
+        (3, 14, 64, 384, 96, 1, False),
+        (1, 14, 96, 576, 160, 2, False),
+        (2, 7, 160, 960, 160, 1, True),
+        (2, 7, 160, 960, 320, 1, False),
+        (1, 20, 24, 144, 24, 1, True),    # partial 8x8 tiles are not used at 20 -> 7x7 tiles, partial edge
+    ],
+)
+def test_ir_block_matches_torch(device, B, H, inp, hid, oup, s, res):
+    g = torch.Generator().manual_seed(H * 100 + inp + oup)
+    x = (torch.rand(B, inp, H, H, generator=g) * 2).to(torch.bfloat16)
+    expand = None if hid == inp and H == 112 and inp == 32 else (
+        torch.randn(hid, inp, 1, 1, generator=g) / np.sqrt(inp), torch.randn(hid, generator=g) * 0.1)
+    dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
+    project = (torch.randn(oup, hid, 1, 1, generator=g) / np.sqrt(hid), torch.randn(oup, generator=g) * 0.1)
+    xn = _nhwc(x).to(device)
+    y = AF.ir_block_nhwc(xn, expand, dw, project, stride=s, res=res)
+    ref = _ref_ir(xn.cpu(), expand, dw, project, s, res)
+    _check(_nchw(y.cpu()), ref, rtol=3e-2, atol=3e-2)
+
+
+def test_ir_block_live_batch(device):
+    """Crops past the device-side live count are not written."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(4, 28, 28, 32, generator=g).to(torch.bfloat16).to(device)
+    expand = (torch.randn(192, 32, 1, 1, generator=g) / 6, torch.zeros(192))
+    dw = (torch.randn(192, 1, 3, 3, generator=g) / 3, torch.zeros(192))
+    project = (torch.randn(64, 192, 1, 1, generator=g) / 14, torch.zeros(64))
+    bdev = torch.tensor([2], dtype=torch.int32, device=device)
+    y = AF.ir_block_nhwc(x, expand, dw, project, stride=2, bdev=bdev)
+    full = AF.ir_block_nhwc(x, expand, dw, project, stride=2)
+    assert torch.equal(y[:2].cpu(), full[:2].cpu())

@@ -102,11 +102,26 @@ def program(models):
 def test_program_shape(program):
     assert program.ops.shape[1] == OP_FIELDS
     convs = int((program.ops[:, 0] == OP_CONV).sum())
-    # 75 YOLO convs lowered to 65 (C3 cv1+cv2 and the two detect branches' first convs fused),
-    # 35 MobileNet convs (stem + 16 expand + 17 project + head) + FC
-    assert convs == 65 + 35
+    # 75 YOLO convs lowered to 64 (C3 cv1+cv2 and the two detect branches' first convs fused);
+    # MobileNet: stem + head + FC convs, the 17 inverted-residual blocks as fused ops
+    # (unfused: 35 convs = stem + 16 expand + 17 project + head, plus FC)
+    from inference_arena_amd.engine.planner import OP_IRBLOCK
+
+    irs = int((program.ops[:, 0] == OP_IRBLOCK).sum())
+    assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0))
     assert program.cls_ops.shape[0] < program.ops.shape[0]
     assert program.weights.nbytes % 256 == 0
+
+
+def test_unfused_program_shape(models):
+    from inference_arena_amd.engine.plans import plan_mobilenet
+    from inference_arena_amd.engine.planner import ProgramBuilder
+
+    for fuse, want in ((False, 36), (True, 3)):
+        pb = ProgramBuilder()
+        crops = pb.raw("crops", 300 * 32)
+        plan_mobilenet(pb, models[1], crops, 224, (0.5,) * 3, (0.25,) * 3, fuse_ir=fuse)
+        assert int((pb.build().ops[:, 0] == OP_CONV).sum()) == want
 
 
 @pytest.mark.parametrize("B", [1, 7, 32])

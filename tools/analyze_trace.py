@@ -20,7 +20,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 KIND = {1: "conv", 2: "dwconv", 3: "sppf", 4: "letterbox", 5: "zero", 6: "decode", 7: "nms", 8: "cropplan",
-        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw"}
+        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw", 14: "irblock"}
 
 
 def describe(rec) -> str:
@@ -31,6 +31,9 @@ def describe(rec) -> str:
                 f"{' crops' if rec[30] == 1 else ''}")
     if t == 2:
         return f"dw {int(rec[4])}x{int(rec[5])}x{int(rec[6])} s{int(rec[14])}"
+    if t == 14:
+        return (f"ir {int(rec[4])}x{int(rec[5])}x{int(rec[6])}->{int(rec[23])}x{int(rec[24])}x{int(rec[9])} "
+                f"hid{int(rec[8])} s{int(rec[11])}{' res' if rec[13] else ''}")
     return ""
 
 

@@ -31,6 +31,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = [
     "kernels/conv_mfma.hip",
     "kernels/dwconv.hip",
+    "kernels/ir_block.hip",
     "kernels/preprocess.hip",
     "kernels/detect.hip",
     "kernels/classify_head.hip",
