@@ -36,13 +36,18 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   constexpr int PIN = PH * PW, PIN_PAD = (PIN + 15) / 16 * 16;
   constexpr int POUT = TH * TW, POUT_PAD = (POUT + 15) / 16 * 16;
   constexpr int NE = PIN_PAD / 16, NP = POUT_PAD / 16, NPW = (NP + 3) / 4;
+  constexpr int WP_PER_T = (MP * 64 + 255) / 256;  // 16-B pieces of a Wp chunk per thread
+  constexpr int WE_PER_T = 3;                       // inp_pad <= 192 -> 32*24/256
   extern __shared__ __align__(16) uint8_t lds[];
   const int nslab = p.inp_pad >> 5;
+  const int cpr = p.inp_pad >> 3;
   uint8_t* Xs = lds;                                    // [nslab][PIN_PAD] rows
   uint8_t* Es = Xs + nslab * PIN_PAD * 64;              // [PIN_PAD] rows (EXPAND)
   uint8_t* Ds = Es + (EXPAND ? PIN_PAD * 64 : 0);       // [POUT_PAD] rows
-  uint8_t* Wps = Ds + POUT_PAD * 64;                    // [MP*16] rows
-  uint8_t* Wes = Wps + MP * 16 * 64;                    // [nslab][32] rows (EXPAND)
+  uint8_t* Wps = Ds + POUT_PAD * 64;                    // 2 x [MP*16] rows
+  uint8_t* Wds = Wps + 2 * MP * 16 * 64;                // 2 x [9][32] bf16 + [32] fp32 bias
+  uint8_t* Wes = Wds + 2 * 704;                         // 2 x [nslab][32] rows (EXPAND)
+  const int we_buf = nslab * 32 * 64;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = lane & 15, kq = lane >> 4;
@@ -55,9 +60,56 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   const bf16* xb = (const bf16*)p.x + (size_t)b * p.H * p.W * p.x_cs;
+  const bf16* wp = (const bf16*)p.wp;
+  const bf16* we = (const bf16*)p.we;
+  const bf16* wd = (const bf16*)p.wd;
+
+  // Per-chunk weights (Wp columns, We rows, dw taps + bias) are prefetched into
+  // registers one chunk ahead and written to the idle LDS buffer after the
+  // current chunk's last read of it, so their global latency hides behind MFMA.
+  uint4 rwp[WP_PER_T], rwe[WE_PER_T], rwd;
+  auto fetch = [&](int h0) {
+#pragma unroll
+    for (int k = 0; k < WP_PER_T; ++k) {
+      const int i = tid + k * 256;
+      if (i < MP * 64) rwp[k] = *(const uint4*)(wp + (size_t)(i >> 2) * p.hid_pad + h0 + (i & 3) * 8);
+    }
+    if constexpr (EXPAND) {
+#pragma unroll
+      for (int k = 0; k < WE_PER_T; ++k) {
+        const int i = tid + k * 256;
+        if (i < 32 * cpr) {
+          const int r = i / cpr, c = i - r * cpr;
+          rwe[k] = *(const uint4*)(we + (size_t)(h0 + r) * p.inp_pad + c * 8);
+        }
+      }
+    }
+    if (tid < 36) rwd = *(const uint4*)(wd + (tid >> 2) * p.hid_pad + h0 + (tid & 3) * 8);
+    else if (tid < 44) rwd = *(const uint4*)(p.bd + h0 + (tid - 36) * 4);
+  };
+  auto stash = [&](int buf) {
+    uint8_t* wps = Wps + buf * MP * 16 * 64;
+#pragma unroll
+    for (int k = 0; k < WP_PER_T; ++k) {
+      const int i = tid + k * 256;
+      if (i < MP * 64) *(uint4*)(wps + swz(i >> 2, i & 3)) = rwp[k];
+    }
+    if constexpr (EXPAND) {
+      uint8_t* wes = Wes + buf * we_buf;
+#pragma unroll
+      for (int k = 0; k < WE_PER_T; ++k) {
+        const int i = tid + k * 256;
+        if (i < 32 * cpr) {
+          const int r = i / cpr, c = i - r * cpr;
+          *(uint4*)(wes + (c >> 2) * 32 * 64 + swz(r, c & 3)) = rwe[k];
+        }
+      }
+    }
+    if (tid < 44) *(uint4*)(Wds + buf * 704 + tid * 16) = rwd;  // [9][32] bf16 taps, then 32 fp32 biases
+  };
 
   // ---- input tile (with halo) -> LDS, zero outside the image / past inp
-  const int cpr = p.inp_pad >> 3;
+  fetch(0);
   for (int i = tid; i < PIN_PAD * cpr; i += 256) {
     const int pix = i / cpr, c = i - pix * cpr;
     const int py = pix / PW, px = pix - py * PW;
@@ -67,6 +119,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
       v = *(const uint4*)(xb + ((size_t)iy * p.W + ix) * p.x_cs + c * 8);
     *(uint4*)(Xs + (c >> 2) * PIN_PAD * 64 + swz(pix, c & 3)) = v;
   }
+  stash(0);
 
   f32x4 acc[NPW][MP];
 #pragma unroll
@@ -75,31 +128,22 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
     for (int m = 0; m < MP; ++m) acc[q][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = p.hid_pad >> 5;
+  __syncthreads();
   for (int h = 0; h < nchunks; ++h) {
-    const int h0 = h * 32;
-    __syncthreads();  // previous chunk's readers are done; X tile visible
-    for (int i = tid; i < MP * 16 * 4; i += 256) {
-      const int r = i >> 2, c = i & 3;
-      *(uint4*)(Wps + swz(r, c)) = *(const uint4*)((const bf16*)p.wp + (size_t)r * p.hid_pad + h0 + c * 8);
-    }
-    if constexpr (EXPAND) {
-      for (int i = tid; i < 32 * cpr; i += 256) {
-        const int r = i / cpr, c = i - r * cpr;
-        *(uint4*)(Wes + (c >> 2) * 32 * 64 + swz(r, c & 3)) =
-            *(const uint4*)((const bf16*)p.we + (size_t)(h0 + r) * p.inp_pad + c * 8);
-      }
-    }
-    __syncthreads();
+    const int cur = h & 1;
+    const bool more = h + 1 < nchunks;
+    if (more) fetch((h + 1) * 32);
 
     const uint8_t* Esrc;
     if constexpr (EXPAND) {
-      // E[pix][32 hidden] = relu6(We_chunk . X^T + be): A = We rows (hidden), B = X rows (pixels)
+      const uint8_t* wes = Wes + cur * we_buf;
+      const float* be = p.be + h * 32;
       for (int j = wave; j < NE; j += 4) {
         f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
         for (int sl = 0; sl < nslab; ++sl) {
           const bf16x8 bv = *(const bf16x8*)(Xs + sl * PIN_PAD * 64 + swz(j * 16 + row, kq));
-          const bf16x8 a0 = *(const bf16x8*)(Wes + sl * 32 * 64 + swz(row, kq));
-          const bf16x8 a1 = *(const bf16x8*)(Wes + sl * 32 * 64 + swz(16 + row, kq));
+          const bf16x8 a0 = *(const bf16x8*)(wes + sl * 32 * 64 + swz(row, kq));
+          const bf16x8 a1 = *(const bf16x8*)(wes + sl * 32 * 64 + swz(16 + row, kq));
           e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bv, e0, 0, 0, 0);
           e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bv, e1, 0, 0, 0);
         }
@@ -110,7 +154,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
           const int hc = mt * 16 + kq * 4;
-          const float4 bb = *(const float4*)(p.be + h0 + hc);
+          const float4 bb = *(const float4*)(be + hc);
           const f32x4 e = mt ? e1 : e0;
           float v[4] = {relu6(e[0] + bb.x), relu6(e[1] + bb.y), relu6(e[2] + bb.z), relu6(e[3] + bb.w)};
           if (!inb) v[0] = v[1] = v[2] = v[3] = 0.f;
@@ -124,14 +168,15 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
     }
 
     // depthwise 3x3 stride S: one (output pixel, 8-channel chunk) per item
+    const uint8_t* wdl = Wds + cur * 704;
     for (int i = tid; i < POUT_PAD * 4; i += 256) {
       const int q = i >> 2, c = i & 3;
       uint4 outv = {0u, 0u, 0u, 0u};
       if (q < POUT) {
         const int oy = q / TW, ox = q - oy * TW;
         float a[8];
-        const float4 b0 = *(const float4*)(p.bd + h0 + c * 8);
-        const float4 b1 = *(const float4*)(p.bd + h0 + c * 8 + 4);
+        const float4 b0 = *(const float4*)(wdl + 576 + c * 32);
+        const float4 b1 = *(const float4*)(wdl + 576 + c * 32 + 16);
         a[0] = b0.x; a[1] = b0.y; a[2] = b0.z; a[3] = b0.w;
         a[4] = b1.x; a[5] = b1.y; a[6] = b1.z; a[7] = b1.w;
 #pragma unroll
@@ -141,7 +186,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
             const int pin = (oy * S + ky) * PW + ox * S + kx;
             float e[8], w[8];
             unpack8(*(const uint4*)(Esrc + swz(pin, c)), e);
-            unpack8(*(const uint4*)((const bf16*)p.wd + (ky * 3 + kx) * p.hid_pad + h0 + c * 8), w);
+            unpack8(*(const uint4*)(wdl + (ky * 3 + kx) * 64 + c * 16), w);
 #pragma unroll
             for (int k = 0; k < 8; ++k) a[k] = fmaf(e[k], w[k], a[k]);
           }
@@ -154,6 +199,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
     __syncthreads();
 
     // project: acc[pixel tile][oup tile] += Wp[oup][chunk] . D[chunk][pixels]
+    const uint8_t* wps = Wps + cur * MP * 16 * 64;
 #pragma unroll
     for (int q = 0; q < NPW; ++q) {
       const int j = wave + 4 * q;
@@ -161,11 +207,13 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
         const bf16x8 bv = *(const bf16x8*)(Ds + swz(j * 16 + row, kq));
 #pragma unroll
         for (int m = 0; m < MP; ++m) {
-          const bf16x8 av = *(const bf16x8*)(Wps + swz(m * 16 + row, kq));
+          const bf16x8 av = *(const bf16x8*)(wps + swz(m * 16 + row, kq));
           acc[q][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[q][m], 0, 0, 0);
         }
       }
     }
+    if (more) stash(cur ^ 1);
+    __syncthreads();  // next chunk: weights visible, E/D free
   }
 
   // ---- epilogue: bias (+ residual from the staged input tile) -> NHWC bf16
@@ -203,8 +251,8 @@ static size_t ir_lds_bytes(int inp_pad) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   constexpr int PIN_PAD = (PH * PW + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
   const int nslab = inp_pad / 32;
-  return (size_t)nslab * PIN_PAD * 64 + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64 + MP * 16 * 64 +
-         (EXPAND ? nslab * 32 * 64 : 0);
+  return (size_t)nslab * PIN_PAD * 64 + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64 + 2 * MP * 16 * 64 +
+         2 * 704 + (EXPAND ? 2 * nslab * 32 * 64 : 0);
 }
 
 template <int S, int TH, int TW, int MP, bool EXPAND>
@@ -250,6 +298,7 @@ void ir_block(const IrParams& p, hipStream_t s) {
   if (p.inp_pad % 32 || p.hid_pad % 32 || p.oup_pad % 16 || p.inp % 8 || p.oup % 4 || p.oup > p.oup_pad ||
       p.inp > p.inp_pad)
     throw std::runtime_error("ir_block: bad channel geometry");
+  if (p.inp_pad > 192) throw std::runtime_error("ir_block: inp_pad > 192");
   if (!p.expand && p.hid_pad != p.inp_pad) throw std::runtime_error("ir_block: no-expand needs hid_pad == inp_pad");
   if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_block: residual needs s1, inp == oup");
   if (p.Ho != (p.H + 2 - 3) / p.stride + 1 || p.Wo != (p.W + 2 - 3) / p.stride + 1)

@@ -146,13 +146,25 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
     return heads
 
 
-def fuse_ir_default() -> bool:
-    """Fused inverted-residual blocks (csrc/kernels/ir_block.hip) unless ARENA_FUSE_IR=0."""
-    return os.environ.get("ARENA_FUSE_IR", "1") != "0"
+def fuse_ir_default() -> str:
+    """Inverted-residual fusion policy (``ARENA_FUSE_IR``): ``auto`` (default), ``all`` or ``none``/``0``."""
+    v = os.environ.get("ARENA_FUSE_IR", "auto").lower()
+    return {"0": "none", "1": "all", "false": "none", "true": "all"}.get(v, v)
+
+
+def fuse_block(blk, H: int, policy) -> bool:
+    """``auto``: fuse where the tile kernel wins on MI355X — blocks at >= 28x28 input, and the 14x14
+    blocks with <= 384 hidden / <= 64 output channels.  Deeper blocks have too few output tiles per
+    crop (1-4 workgroups) and run faster as batched 1x1 GEMMs + depthwise over all crops."""
+    if policy in (True, "all"):
+        return True
+    if policy in (False, None, "none"):
+        return False
+    return H >= 28 or (H >= 14 and blk.hidden <= 384 and blk.oup <= 64)
 
 
 def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std, *, kind: int = CROPS,
-                   raw_logits: bool = False, fuse_ir: bool | None = None):
+                   raw_logits: bool = False, fuse_ir: bool | str | None = None):
     """MobileNetV2 over crop-gathered inputs (``crops`` = CropRef buffer) or, with
     ``crops=None``, over fp32 [3,S,S] tensors of the image batch (``kind=IMAGES``).
 
@@ -175,7 +187,7 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
     cur, H = F, h
     for i, blk in enumerate(m.blocks):
         Ho = (H + 2 - 3) // blk.stride + 1
-        if fuse_ir:
+        if fuse_block(blk, H, fuse_ir):
             O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup, kind=CROPS_)
             pb.ir_block(View(cur, 0, blk.inp), View(O, 0, blk.oup),
                         fold(blk.expand) if blk.expand is not None else None, fold(blk.dw), fold(blk.project),

@@ -108,7 +108,8 @@ def test_program_shape(program):
     from inference_arena_amd.engine.planner import OP_IRBLOCK
 
     irs = int((program.ops[:, 0] == OP_IRBLOCK).sum())
-    assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0))
+    # auto policy: blocks 1-10 fused, 11-17 as expand/project convs (2 each, block 17 included)
+    assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0), (64 + 3 + 14, 10))
     assert program.cls_ops.shape[0] < program.ops.shape[0]
     assert program.weights.nbytes % 256 == 0
 
