@@ -69,3 +69,26 @@ def default_models(seed: int = 0) -> tuple[YOLOv5nu, MobileNetV2]:
     """(detector, classifier) for a weight seed; cached per process."""
     with torch.random.fork_rng():
         return make_yolo(seed), make_mobilenet(seed + 1)
+
+
+def resolve_models(models_dir: str | None = None, seed: int = 0) -> tuple[YOLOv5nu, MobileNetV2]:
+    """Models for a service: weights from ``models_dir`` when present — flat
+    ``<dir>/<name>.safetensors`` files (monolithic/microservices init layout) or a
+    repository ``<dir>/<name>/<v>/model.safetensors`` — otherwise the seeded networks.
+    (Reference services verify their model files at start-up:
+    architectures/monolithic/app/main.py:46-67.)"""
+    from pathlib import Path
+
+    if models_dir:
+        from ..repository.store import load_module, scan_repository
+
+        d = Path(models_dir)
+        flat = [d / "yolov5n.safetensors", d / "mobilenetv2.safetensors"]
+        if all(f.exists() for f in flat):
+            return load_module(flat[0], "yolov5n"), load_module(flat[1], "mobilenetv2")
+        if d.is_dir():
+            e = scan_repository(d)
+            if "yolov5n" in e and "mobilenetv2" in e:
+                return (load_module(e["yolov5n"].model_file(), "yolov5n"),
+                        load_module(e["mobilenetv2"].model_file(), "mobilenetv2"))
+    return default_models(seed)

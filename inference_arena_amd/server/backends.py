@@ -137,9 +137,9 @@ class CpuReferenceBackend(Backend):
 def build_backend(settings, *, arch: str = "monolithic") -> Backend:
     """Backend selected by ARENA_DEVICE (gpu | cpu) with the arena's default models."""
     from ..config import get_triton_config
-    from ..models.zoo import default_models
+    from ..models.zoo import resolve_models
 
-    yolo, mnet = default_models(int(settings.ARENA_WEIGHT_SEED))
+    yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
     if settings.ARENA_DEVICE == "cpu":
         from ..config import get_controlled_variable
 

@@ -37,7 +37,7 @@ def build_app(arch: str, settings, info):
     """The arm's FastAPI app with weights broadcast from rank 0."""
     import numpy as np
 
-    from ..models.zoo import default_models
+    from ..models.zoo import resolve_models
     from ..parallel import dist as D
 
     if arch == "monolithic":
@@ -53,7 +53,7 @@ def build_app(arch: str, settings, info):
             from ..engine.plans import plan_pipeline
             from .backends import GpuBatchedBackend
 
-            yolo, mnet = default_models(int(settings.ARENA_WEIGHT_SEED))
+            yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
             blob = plan_pipeline(yolo, mnet, conf_thr=0.5, iou_thr=0.45).weights if info.is_main else None
             blob = D.broadcast_blob(blob, info)
             db = get_triton_config().get("dynamic_batching", {}) or {}

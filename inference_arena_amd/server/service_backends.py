@@ -180,9 +180,9 @@ class CpuDetectorBackend(DetectorBackend):
 
 def build_classifier_backend(settings) -> ClassifierBackend:
     from ..config import get_controlled_variable
-    from ..models.zoo import default_models
+    from ..models.zoo import resolve_models
 
-    _, mnet = default_models(int(settings.ARENA_WEIGHT_SEED))
+    _, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
     if settings.ARENA_DEVICE == "cpu":
         return CpuClassifierBackend(mnet, threads=int(get_controlled_variable("onnx_runtime",
                                                                               "intra_op_num_threads")))
@@ -192,9 +192,9 @@ def build_classifier_backend(settings) -> ClassifierBackend:
 
 def build_detector_backend(settings) -> DetectorBackend:
     from ..config import get_controlled_variable, get_model_config
-    from ..models.zoo import default_models
+    from ..models.zoo import resolve_models
 
-    yolo, _ = default_models(int(settings.ARENA_WEIGHT_SEED))
+    yolo, _ = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
     if settings.ARENA_DEVICE == "cpu":
         y = get_model_config("yolov5n")
         return CpuDetectorBackend(yolo, threads=int(get_controlled_variable("onnx_runtime", "intra_op_num_threads")),

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Start one topology as local processes (replaces the reference's docker compose files and
+scripts/start-*.sh): each service is a child process; Ctrl-C stops them all.
+
+  monolithic     replicas of :8100 (one per GPU, shared port)
+  microservices  classification gRPC :8201 (GPU 0) + detection HTTP :8200
+  triton         model server :8000/:8001/:8002 + gateway :8300
+
+Example: python scripts/start_arena.py --arch triton --gpus 1
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def spawn(args, env, log_dir: Path, name: str):
+    log = open(log_dir / f"{name}.log", "w")
+    return subprocess.Popen([sys.executable, "-m", *args], env=env, stdout=log, stderr=subprocess.STDOUT, cwd=ROOT)
+
+
+def wait_http(url: str, timeout: float, procs) -> bool:
+    import urllib.request
+
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if any(p.poll() is not None for p in procs):
+            return False
+        try:
+            with urllib.request.urlopen(url, timeout=2) as r:
+                if r.status == 200:
+                    return True
+        except OSError:
+            pass
+        time.sleep(0.5)
+    return False
+
+
+def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = "model_repository",
+          extra_env: dict | None = None):
+    env = dict(os.environ, PYTHONPATH=str(ROOT), HSA_ENABLE_IPC_MODE_LEGACY="0", ARENA_DEVICE=device,
+               **(extra_env or {}))
+    log_dir.mkdir(parents=True, exist_ok=True)
+    procs = []
+    if arch == "monolithic":
+        procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "monolithic", "--gpus", str(gpus),
+                            "--port", "8100"], env, log_dir, "monolithic"))
+        ok = wait_http("http://127.0.0.1:8100/health", 600, procs)
+    elif arch == "microservices":
+        procs.append(spawn(["inference_arena_amd.server.classification_service"], dict(env, PORT="8201"), log_dir,
+                           "classification"))
+        time.sleep(1)
+        procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "detection", "--gpus", str(gpus),
+                            "--port", "8200"], dict(env, CLASSIFICATION_GRPC_ENDPOINT="127.0.0.1:8201"), log_dir,
+                           "detection"))
+        ok = wait_http("http://127.0.0.1:8200/health", 600, procs)
+    elif arch == "triton":
+        if not (Path(repo) / "yolov5n" / "config.pbtxt").exists():
+            subprocess.run([sys.executable, str(ROOT / "scripts" / "upload_models.py"), "--repository", repo],
+                           check=True, env=env)
+        procs.append(spawn(["inference_arena_amd.server.model_server", "--model-repository", repo, "--device", device],
+                           env, log_dir, "model_server"))
+        ok = wait_http("http://127.0.0.1:8000/v2/health/ready", 600, procs)
+        if ok:
+            procs.append(spawn(["inference_arena_amd.server.gateway"],
+                               dict(env, PORT="8300", TRITON_GRPC_ENDPOINT="127.0.0.1:8001"), log_dir, "gateway"))
+            ok = wait_http("http://127.0.0.1:8300/health", 300, procs)
+    else:
+        raise ValueError(arch)
+    return procs, ok
+
+
+def stop(procs) -> None:
+    for p in reversed(procs):
+        if p.poll() is None:
+            p.send_signal(signal.SIGINT)
+    for p in reversed(procs):
+        try:
+            p.wait(20)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait(5)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--arch", required=True, choices=["monolithic", "microservices", "triton"])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--logs", default="logs")
+    a = ap.parse_args(argv)
+    procs, ok = start(a.arch, a.gpus, Path(a.logs), a.device)
+    print(f"{a.arch}: {'ready' if ok else 'FAILED (see ' + a.logs + ')'}", flush=True)
+    try:
+        while ok and all(p.poll() is None for p in procs):
+            time.sleep(1)
+    except KeyboardInterrupt:
+        pass
+    finally:
+        stop(procs)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
