@@ -526,7 +526,7 @@ static int g_conv_impl = [] {
 static int conv_impl() { return g_conv_impl; }
 
 void set_conv_impl(int v) {
-  if (v != 1 && v != 2) throw std::runtime_error("conv impl must be 1 (direct) or 2 (LDS)");
+  if (v < 1 || v > 3) throw std::runtime_error("conv impl must be 1 (direct), 2 (LDS tiles) or 3 (igemm)");
   g_conv_impl = v;
 }
 int get_conv_impl() { return g_conv_impl; }
@@ -565,6 +565,10 @@ void conv2d(const ConvParams& p, hipStream_t s) {
   const long M = (long)p.B * p.Ho * p.Wo;
   if (M <= 0) return;
   if (M > 0x7fffffffL) throw std::runtime_error("conv2d: M overflows int");
+  if (conv_impl() == 3) {
+    conv_igemm(p, s);
+    return;
+  }
   if (conv_impl() == 2) {
     if (tile_ok(p)) {
       if (p.stride == 1)

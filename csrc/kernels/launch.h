@@ -38,6 +38,7 @@ struct ConvParams {
   const int* bdev;  // optional live batch count on device
 };
 void conv2d(const ConvParams& p, hipStream_t s);
+void conv_igemm(const ConvParams& p, hipStream_t s);  // LDS-pipelined implicit GEMM (impl 3)
 // Conv kernel family: 1 = direct global->VGPR loads, 2 = LDS-staged (default).
 void set_conv_impl(int v);
 int get_conv_impl();

@@ -47,7 +47,7 @@ def test_native_loaded():
     assert C.SIZEOF_IMAGE_META == 48 and C.SIZEOF_CANDIDATE == 32 and C.SIZEOF_TOPK == 64
 
 
-@pytest.fixture(params=[2, 1], ids=["lds", "direct"])
+@pytest.fixture(params=[2, 1, 3], ids=["lds", "direct", "igemm"])
 def conv_impl(request):
     C = native()
     old = C.get_conv_impl()

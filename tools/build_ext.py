@@ -32,6 +32,7 @@ SOURCES = [
     "kernels/conv_mfma.hip",
     "kernels/dwconv.hip",
     "kernels/ir_block.hip",
+    "kernels/conv_igemm.hip",
     "kernels/preprocess.hip",
     "kernels/detect.hip",
     "kernels/classify_head.hip",
