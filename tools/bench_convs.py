@@ -32,6 +32,7 @@ def main(argv=None) -> int:
     ap.add_argument("--images", type=int, default=32)
     ap.add_argument("--crops", type=int, default=128)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ops", default=None, help="comma-separated op indices to run (default: all convs)")
     a = ap.parse_args(argv)
     C = native()
     impls = [int(i) for i in a.impls.split(",")]
@@ -42,7 +43,7 @@ def main(argv=None) -> int:
              "|---|---|" + "---|" * len(impls) + "---|---|"]
     tot = {i: 0.0 for i in impls}
     for k, r in enumerate(prog.ops):
-        if int(r[0]) != OP_CONV:
+        if int(r[0]) != OP_CONV or (a.ops and str(k) not in a.ops.split(",")):
             continue
         H, W, Cin, Ho, Wo, Cout, KH, KW, S, pt, pl = (int(v) for v in (r[4], r[5], r[6], r[13], r[14], r[15],
                                                                        r[17], r[18], r[19], r[20], r[21]))
