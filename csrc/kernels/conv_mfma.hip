@@ -524,6 +524,12 @@ static int g_conv_impl = [] {
   return e ? std::atoi(e) : 2;
 }();
 static int conv_impl() { return g_conv_impl; }
+static bool g_conv_pw = [] {
+  const char* e = std::getenv("ARENA_CONV_PW");
+  return e ? std::atoi(e) != 0 : true;
+}();
+static bool conv_pw_enabled() { return g_conv_pw; }
+void set_conv_pw(bool v) { g_conv_pw = v; }
 
 void set_conv_impl(int v) {
   if (v < 1 || v > 3) throw std::runtime_error("conv impl must be 1 (direct), 2 (LDS tiles) or 3 (igemm)");
@@ -570,6 +576,7 @@ void conv2d(const ConvParams& p, hipStream_t s) {
     return;
   }
   if (conv_impl() == 2) {
+    if (conv_pw_enabled() && conv_pw(p, s)) return;
     if (tile_ok(p)) {
       if (p.stride == 1)
         launch_tile_s<1>(p, s);

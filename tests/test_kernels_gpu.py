@@ -248,3 +248,46 @@ def test_ir_block_live_batch(device):
     y = AF.ir_block_nhwc(x, expand, dw, project, stride=2, bdev=bdev)
     full = AF.ir_block_nhwc(x, expand, dw, project, stride=2)
     assert torch.equal(y[:2].cpu(), full[:2].cpu())
+
+
+@pytest.mark.parametrize(
+    "B,H,Cin,Cout",
+    [(2, 40, 64, 64), (2, 40, 128, 64), (1, 20, 80, 80), (2, 14, 64, 384), (2, 14, 96, 576), (2, 7, 160, 960),
+     (2, 20, 256, 256), (3, 20, 128, 128), (2, 33, 16, 16), (2, 30, 32, 32), (1, 14, 384, 96)],
+)
+def test_pointwise_fast_path(device, B, H, Cin, Cout):
+    """1x1 fast path (conv_pw.hip) vs torch, with residual; and identical to the generic kernel."""
+    C = native()
+    g = torch.Generator().manual_seed(Cin * 7 + Cout)
+    x = torch.randn(B, Cin, H, H, generator=g)
+    w = torch.randn(Cout, Cin, 1, 1, generator=g) / np.sqrt(Cin)
+    b = torch.randn(Cout, generator=g) * 0.1
+    xn = _nhwc(x).to(torch.bfloat16).to(device)
+    res = torch.randn(B, H, H, Cout, generator=g).to(torch.bfloat16).to(device)
+    y = AF.conv2d_nhwc(xn, w, b, act="silu", res=res)
+    ref = _ref_conv(xn.cpu(), w, b, 1, 0, "silu", res=res.cpu())
+    _check(_nchw(y.cpu()), ref)
+    C.set_conv_pw(False)
+    try:
+        y2 = AF.conv2d_nhwc(xn, w, b, act="silu", res=res)
+    finally:
+        C.set_conv_pw(True)
+    assert (y.float() - y2.float()).abs().max().item() <= 0.0625
+
+
+def test_pointwise_slices_and_upsample(device):
+    g = torch.Generator().manual_seed(17)
+    B, H, Cbuf, Cin, Cout = 2, 20, 384, 256, 128
+    buf = torch.randn(B, H, H, Cbuf, generator=g).to(torch.bfloat16).to(device)
+    w = torch.randn(Cout, Cin, 1, 1, generator=g) / np.sqrt(Cin)
+    b = torch.randn(Cout, generator=g) * 0.1
+    out = torch.zeros(B, H, H, 256, dtype=torch.bfloat16, device=device)
+    up = torch.zeros(B, 2 * H, 2 * H, 192, dtype=torch.bfloat16, device=device)
+    AF.conv2d_nhwc(buf, w, b, act="silu", x_coff=64, cin=Cin, out=out, out_coff=128, out2=up, out2_coff=64)
+    torch.cuda.synchronize()
+    ref = _ref_conv(buf.cpu()[..., 64:64 + Cin], w, b, 1, 0, "silu")
+    _check(_nchw(out.cpu()[..., 128:]), ref)
+    assert out.cpu()[..., :128].abs().sum() == 0
+    upref = F.interpolate(_nchw(out.cpu()[..., 128:]), scale_factor=2, mode="nearest")
+    assert torch.equal(_nchw(up.cpu()[..., 64:]), upref)
+    assert up.cpu()[..., :64].abs().sum() == 0

@@ -33,6 +33,7 @@ SOURCES = [
     "kernels/dwconv.hip",
     "kernels/ir_block.hip",
     "kernels/conv_igemm.hip",
+    "kernels/conv_pw.hip",
     "kernels/preprocess.hip",
     "kernels/detect.hip",
     "kernels/classify_head.hip",
