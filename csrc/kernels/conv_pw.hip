@@ -162,23 +162,20 @@ bool conv_pw(const ConvParams& p, hipStream_t s) {
     return false;
   const long M = (long)p.B * p.Ho * p.Wo;
   const int NT = p.Cout_pad / 16, KS = p.Kpad / 32;
-#define PW(nt, ks, mf, split)                     \
-  if (NT == nt * split && KS == ks) {             \
-    pw_launch<nt, ks, mf>(p, s, M, split);        \
-    return true;                                  \
+#define PW(nt, ks, mf, split)                                                    \
+  if (NT == nt * split && KS == ks && (M + 64 * mf - 1) / (64 * mf) >= 512) {    \
+    pw_launch<nt, ks, mf>(p, s, M, split);                                       \
+    return true;                                                                 \
   }
+  // Measured on MI355X (profiles/r1_pw_ops.md): wins for large pixel counts with
+  // <= 32 KB weight slices; small maps (20x20, 14x14 crops) and wide/deep weight
+  // slices stay on the generic kernels, which amortise weights better.
   PW(1, 1, 4, 1)
   PW(2, 1, 4, 1)
   PW(4, 2, 2, 1)
   PW(4, 4, 2, 1)
   PW(5, 3, 2, 1)
   PW(8, 4, 2, 1)
-  PW(8, 8, 1, 1)
-  PW(8, 8, 1, 2)
-  PW(6, 12, 1, 1)
-  PW(12, 2, 1, 2)
-  PW(12, 3, 1, 3)
-  PW(12, 5, 1, 5)
 #undef PW
   return false;
 }
