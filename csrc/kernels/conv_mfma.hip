@@ -529,6 +529,11 @@ static bool g_conv_pw = [] {
   return e ? std::atoi(e) != 0 : true;
 }();
 static bool conv_pw_enabled() { return g_conv_pw; }
+static bool g_conv_v3 = [] {
+  const char* e = std::getenv("ARENA_CONV_V3");
+  return e ? std::atoi(e) != 0 : true;
+}();
+void set_conv_v3(bool v) { g_conv_v3 = v; }
 void set_conv_pw(bool v) { g_conv_pw = v; }
 
 void set_conv_impl(int v) {
@@ -577,6 +582,7 @@ void conv2d(const ConvParams& p, hipStream_t s) {
   }
   if (conv_impl() == 2) {
     if (conv_pw_enabled() && conv_pw(p, s)) return;
+    if (g_conv_v3 && conv3x3_v3(p, s)) return;
     if (tile_ok(p)) {
       if (p.stride == 1)
         launch_tile_s<1>(p, s);

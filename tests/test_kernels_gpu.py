@@ -291,3 +291,23 @@ def test_pointwise_slices_and_upsample(device):
     upref = F.interpolate(_nchw(out.cpu()[..., 128:]), scale_factor=2, mode="nearest")
     assert torch.equal(_nchw(up.cpu()[..., 64:]), upref)
     assert up.cpu()[..., :64].abs().sum() == 0
+
+
+@pytest.mark.parametrize("H,Cin,Cout,s", [(40, 64, 64, 1), (80, 64, 144, 1), (20, 256, 144, 1), (40, 128, 256, 2),
+                                          (27, 96, 80, 2), (13, 32, 48, 1)])
+def test_conv3x3_v3_matches_v2(device, H, Cin, Cout, s):
+    """v3 halo-tile kernel == v2 tile kernel (same math, different staging) and close to torch."""
+    C = native()
+    g = torch.Generator().manual_seed(H + Cin + Cout)
+    x = torch.randn(2, Cin, H, H, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)
+    b = torch.randn(Cout, generator=g) * 0.1
+    xn = _nhwc(x).to(torch.bfloat16).to(device)
+    y3 = AF.conv2d_nhwc(xn, w, b, stride=s, act="silu")
+    C.set_conv_v3(False)
+    try:
+        y2 = AF.conv2d_nhwc(xn, w, b, stride=s, act="silu")
+    finally:
+        C.set_conv_v3(True)
+    assert (y3.float() - y2.float()).abs().max().item() <= 0.0625
+    _check(_nchw(y3.cpu()), _ref_conv(xn.cpu(), w, b, s, 1, "silu"))

@@ -34,6 +34,7 @@ SOURCES = [
     "kernels/ir_block.hip",
     "kernels/conv_igemm.hip",
     "kernels/conv_pw.hip",
+    "kernels/conv3x3_v3.hip",
     "kernels/preprocess.hip",
     "kernels/detect.hip",
     "kernels/classify_head.hip",
