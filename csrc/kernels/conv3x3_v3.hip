@@ -84,13 +84,11 @@ __global__ __launch_bounds__(256) void conv3x3_v3_kernel(const ConvParams p) {
   }
 
   uint4 rin[G::IN_IT], rw[G::W_IT];
-  const uint4 zero = {0u, 0u, 0u, 0u};
   auto fetch = [&](int c0) {
 #pragma unroll
-    for (int i = 0; i < G::IN_IT; ++i) rin[i] = in_goff[i] >= 0 ? *(const uint4*)(x + in_goff[i] + c0) : zero;
+    for (int i = 0; i < G::IN_IT; ++i) rin[i] = load16_or_zero(x + in_goff[i] + c0, x, in_goff[i] >= 0);
 #pragma unroll
-    for (int i = 0; i < G::W_IT; ++i)
-      if (w_goff[i] >= 0) rw[i] = *(const uint4*)(w + w_goff[i] + c0);
+    for (int i = 0; i < G::W_IT; ++i) rw[i] = load16_or_zero(w + w_goff[i] + c0, w, w_goff[i] >= 0);
   };
   auto stash = [&]() {
 #pragma unroll

@@ -87,15 +87,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(const ConvParams p) {
     for (int j = 0; j < BPT; ++j) {
       const int iy = biy[j] + kh, ix = bix[j] + kw;
       const bool ok = tv && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-      rb[j] = ok ? *(const uint4*)(bptr[j] + ((size_t)iy * p.W + ix) * p.xs + ci) : zero;
+      rb[j] = load16_or_zero(bptr[j] + ((size_t)iy * p.W + ix) * p.xs + ci, x, ok);
     }
 #pragma unroll
     for (int j = 0; j < APT; ++j) {
       const int i = tid + j * 256;
       const int n = i / CPR, c = i - n * CPR;
       const int k = ks * BK + c * 8;
-      ra[j] = (i < BN * CPR && n0 + n < p.Cout_pad && k < p.Kpad)
-                  ? *(const uint4*)(w + (size_t)(n0 + n) * p.Kpad + k) : zero;
+      ra[j] = load16_or_zero(w + (size_t)(n0 + n) * p.Kpad + k, w, i < BN * CPR && n0 + n < p.Cout_pad && k < p.Kpad);
     }
     // advance this thread's (tap, ci) by BK
     ci += BK;

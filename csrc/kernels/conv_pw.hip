@@ -49,7 +49,6 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(const ConvParams p) {
 
   // 1. activation fragments for every K-step (independent loads, all in flight)
   uint4 bv[MF][KS];
-  const uint4 zero = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int pix = wpix + f * 16 + row;
@@ -58,7 +57,7 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(const ConvParams p) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int k = ks * 32 + kq * 8;
-      bv[f][ks] = (pv && k < p.Cin) ? *(const uint4*)(xp + ks * 32) : zero;
+      bv[f][ks] = load16_or_zero(xp + ks * 32, x, pv && k < p.Cin);
     }
   }
   // 2. weight slice -> LDS
@@ -66,8 +65,7 @@ __global__ __launch_bounds__(256) void conv_pw_kernel(const ConvParams p) {
   for (int i = tid; i < KS * BNR * 4; i += 256) {
     const int r = i / (KS * 4), rem = i - r * (KS * 4);
     const int ks = rem >> 2, c = rem & 3;
-    uint4 v = zero;
-    if (n0 + r < p.Cout_pad) v = *(const uint4*)(w + (size_t)(n0 + r) * p.Kpad + ks * 32 + c * 8);
+    const uint4 v = load16_or_zero(w + (size_t)(n0 + r) * p.Kpad + ks * 32 + c * 8, w, n0 + r < p.Cout_pad);
     *(uint4*)(wl + ks * BNR * 64 + pswz(r, c)) = v;
   }
   __syncthreads();

@@ -72,20 +72,19 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
 #pragma unroll
     for (int k = 0; k < WP_PER_T; ++k) {
       const int i = tid + k * 256;
-      if (i < MP * 64) rwp[k] = *(const uint4*)(wp + (size_t)(i >> 2) * p.hid_pad + h0 + (i & 3) * 8);
+      rwp[k] = load16_or_zero(wp + (size_t)(i >> 2) * p.hid_pad + h0 + (i & 3) * 8, wp, i < MP * 64);
     }
     if constexpr (EXPAND) {
 #pragma unroll
       for (int k = 0; k < WE_PER_T; ++k) {
         const int i = tid + k * 256;
-        if (i < 32 * cpr) {
-          const int r = i / cpr, c = i - r * cpr;
-          rwe[k] = *(const uint4*)(we + (size_t)(h0 + r) * p.inp_pad + c * 8);
-        }
+        const int r = i / cpr, c = i - r * cpr;
+        rwe[k] = load16_or_zero(we + (size_t)(h0 + r) * p.inp_pad + c * 8, we, i < 32 * cpr);
       }
     }
-    if (tid < 36) rwd = *(const uint4*)(wd + (tid >> 2) * p.hid_pad + h0 + (tid & 3) * 8);
-    else if (tid < 44) rwd = *(const uint4*)(p.bd + h0 + (tid - 36) * 4);
+    const void* pd = tid < 36 ? (const void*)(wd + (tid >> 2) * p.hid_pad + h0 + (tid & 3) * 8)
+                              : (const void*)(p.bd + h0 + (tid - 36) * 4);
+    rwd = load16_or_zero(pd, wd, tid < 44);
   };
   auto stash = [&](int buf) {
     uint8_t* wps = Wps + buf * MP * 16 * 64;
@@ -114,9 +113,8 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
     const int pix = i / cpr, c = i - pix * cpr;
     const int py = pix / PW, px = pix - py * PW;
     const int iy = iy0 + py, ix = ix0 + px;
-    uint4 v = {0u, 0u, 0u, 0u};
-    if (pix < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && c * 8 < p.inp)
-      v = *(const uint4*)(xb + ((size_t)iy * p.W + ix) * p.x_cs + c * 8);
+    const bool ok = pix < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && c * 8 < p.inp;
+    const uint4 v = load16_or_zero(xb + ((size_t)iy * p.W + ix) * p.x_cs + c * 8, xb, ok);
     *(uint4*)(Xs + (c >> 2) * PIN_PAD * 64 + swz(pix, c & 3)) = v;
   }
   stash(0);

@@ -189,3 +189,43 @@ def workload_images(n: int | None = None, weight_seed: int = 0, n_images: int = 
     if n is not None:
         man.images = man.images[:n]
     return load_manifest_images(man)
+
+
+class DetectionCounter:
+    """Count detections in a raw detector output, accepting the three layouts the
+    reference's counter understands (src/shared/data/curator.py:226-321):
+
+    * YOLOv8/v5u head ``[1, 84, N]`` (or ``[84, N]``): 4 box + 80 class scores;
+    * classic YOLOv5 ``[1, N, 85]``: 4 box + objectness + 80 class scores
+      (confidence = objectness x class score);
+    * post-NMS ``[1, N, 6]`` / ``[N, 6]``: x1, y1, x2, y2, conf, cls.
+
+    Raw layouts go through the reference's class-aware NMS (``postprocess``).
+    """
+
+    def __init__(self, confidence_threshold: float = 0.5, iou_threshold: float = 0.45):
+        self.conf = confidence_threshold
+        self.iou = iou_threshold
+
+    def count(self, output: np.ndarray) -> int:
+        a = np.asarray(output, dtype=np.float32)
+        if a.ndim == 3:
+            a = a[0]
+        if a.ndim != 2:
+            raise ValueError(f"unsupported detector output shape {np.shape(output)}")
+        if a.shape[1] == 6 and a.shape[0] != 84:
+            return int((a[:, 4] >= self.conf).sum())
+        if a.shape[0] == 84:
+            return self._raw(a[:4].T, a[4:].T)
+        if a.shape[1] == 85:
+            return self._raw(a[:, :4], a[:, 5:] * a[:, 4:5])
+        if a.shape[1] == 84:
+            return self._raw(a[:, :4], a[:, 4:])
+        raise ValueError(f"unsupported detector output shape {np.shape(output)}")
+
+    def _raw(self, xywh: np.ndarray, cls_scores: np.ndarray) -> int:
+        from ..postprocess import apply_nms
+
+        conf = cls_scores.max(axis=1)
+        cls = cls_scores.argmax(axis=1)
+        return len(apply_nms(xywh, conf, cls, self.conf, self.iou))
