@@ -1,0 +1,87 @@
+"""Dataset utilities, detection counter, registry surface and proto text generation (CPU)."""
+from __future__ import annotations
+
+import io
+import zipfile
+
+import numpy as np
+import pytest
+
+from inference_arena_amd.data.curator import DetectionCounter
+from inference_arena_amd.data.synthetic import encode_jpeg, synthetic_images
+
+
+def _raw84(boxes_xywh, cls, conf, n=50):
+    out = np.zeros((1, 84, n), np.float32)
+    for i, (b, c, s) in enumerate(zip(boxes_xywh, cls, conf)):
+        out[0, :4, i] = b
+        out[0, 4 + c, i] = s
+    return out
+
+
+def test_detection_counter_formats():
+    boxes = [(50, 50, 20, 20), (51, 51, 20, 20), (200, 200, 30, 30), (400, 100, 10, 10)]
+    cls = [1, 1, 2, 3]
+    conf = [0.9, 0.8, 0.7, 0.3]
+    dc = DetectionCounter(0.5, 0.45)
+    raw = _raw84(boxes, cls, conf)
+    assert dc.count(raw) == 2  # overlapping pair suppressed, low score dropped
+    assert dc.count(raw[0]) == 2
+    v5 = np.zeros((1, 50, 85), np.float32)
+    for i, (b, c, s) in enumerate(zip(boxes, cls, conf)):
+        v5[0, i, :4] = b
+        v5[0, i, 4] = 1.0
+        v5[0, i, 5 + c] = s
+    assert dc.count(v5) == 2
+    post = np.array([[0, 0, 10, 10, 0.9, 1], [0, 0, 5, 5, 0.4, 2], [1, 1, 4, 4, 0.6, 0]], np.float32)
+    assert dc.count(post[None]) == 2
+    with pytest.raises(ValueError):
+        dc.count(np.zeros((3, 3, 3, 3)))
+
+
+def test_coco_utils(tmp_path):
+    from inference_arena_amd.data import coco
+
+    ok, msg = coco.is_coco_downloaded(tmp_path)
+    assert not ok and "does not exist" in msg
+    with pytest.raises(FileNotFoundError):
+        coco.download_coco_val2017(tmp_path)
+    buf = io.BytesIO()
+    with zipfile.ZipFile(buf, "w") as z:
+        for i, im in enumerate(synthetic_images(3, 1, hw=(40, 60))):
+            z.writestr(f"val2017/{i:012d}.jpg", encode_jpeg(im))
+    (tmp_path / "val2017.zip").write_bytes(buf.getvalue())
+    d = coco.download_coco_val2017(tmp_path)
+    assert d.is_dir() and len(coco.get_coco_image_paths(tmp_path)) == 3
+    ok, msg = coco.is_coco_downloaded(tmp_path)
+    assert not ok and "3 of 5000" in msg
+    imgs = list(coco.iter_coco_images(tmp_path, limit=2))
+    assert len(imgs) == 2 and imgs[0][1].shape == (40, 60, 3)
+
+
+def test_registry_surface():
+    from inference_arena_amd.engine.registry import ModelRegistry, SessionConfig, get_default_registry, \
+        reset_default_registry
+
+    r = ModelRegistry(config=SessionConfig(device=0, buckets=[1, 4]))
+    assert set(r.list_available()) >= {"yolov5n", "mobilenetv2", "pipeline"}
+    assert not r.is_loaded("pipeline")
+    with pytest.raises(KeyError):
+        r._build("resnet")
+    reset_default_registry()
+    assert get_default_registry() is get_default_registry()
+    reset_default_registry()
+
+
+def test_generate_proto_text(tmp_path):
+    import subprocess
+    import sys
+
+    subprocess.run([sys.executable, "scripts/generate_proto.py", "--out", str(tmp_path)], check=True)
+    inf = (tmp_path / "inference.proto").read_text()
+    assert "rpc Classify(ClassificationRequest) returns (ClassificationResponse);" in inf
+    assert "bytes image_crop = 2;" in inf
+    kv = (tmp_path / "kserve_v2.proto").read_text()
+    assert "map<string, InferParameter> parameters = 4;" in kv and "oneof parameter_choice" in kv
+    mc = (tmp_path / "model_config.proto").read_text()
+    assert "repeated ModelInstanceGroup instance_group = 7;" in mc
