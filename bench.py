@@ -185,6 +185,8 @@ def main(argv=None) -> int:
             "p50_ms": round(float(np.percentile(flat, 50)), 3),
             "p99_ms": round(float(np.percentile(flat, 99)), 3),
             "mean_crops_per_request": round(fan, 3),
+            "conv_kernel_choice": {f"impl{k}": v for k, v in sorted(__import__("collections").Counter(
+                c for c in pipe.ex.conv_choices(B) if c).items())},
             "bs1_p50_ms": round(float(np.percentile(bs1, 50)) * 1e3, 3) if bs1 else None,
             "bs1_p99_ms": round(float(np.percentile(bs1, 99)) * 1e3, 3) if bs1 else None,
         }

@@ -72,6 +72,7 @@ void py_conv2d(const py::dict& d) {
   p.act = get<int>(d, "act", 0);
   p.f32out = get<int>(d, "f32out", 0);
   p.bdev = ptr<const int*>(d, "bdev");
+  p.impl = get<int>(d, "impl", 0);
   conv2d(p, stream_of(d));
 }
 
@@ -410,6 +411,7 @@ PYBIND11_MODULE(_C, m) {
              return out;
            })
       .def("weights_ptr", &Executor::weights_ptr)
+      .def("conv_choices", &Executor::conv_choices)
       .def("stream", &Executor::stream);
 
   py::class_<DynamicBatcher>(m, "DynamicBatcher")

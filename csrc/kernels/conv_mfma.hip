@@ -576,11 +576,12 @@ void conv2d(const ConvParams& p, hipStream_t s) {
   const long M = (long)p.B * p.Ho * p.Wo;
   if (M <= 0) return;
   if (M > 0x7fffffffL) throw std::runtime_error("conv2d: M overflows int");
-  if (conv_impl() == 3) {
+  const int impl = p.impl ? p.impl : conv_impl();
+  if (impl == 3) {
     conv_igemm(p, s);
     return;
   }
-  if (conv_impl() == 2) {
+  if (impl == 2) {
     if (conv_pw_enabled() && conv_pw(p, s)) return;
     if (g_conv_v3 && conv3x3_v3(p, s)) return;
     if (tile_ok(p)) {

@@ -36,6 +36,7 @@ struct ConvParams {
   int act;      // Act
   int f32out;   // store fp32 instead of bf16
   const int* bdev;  // optional live batch count on device
+  int impl;         // kernel family for this call (0 = process default, see set_conv_impl)
 };
 void conv2d(const ConvParams& p, hipStream_t s);
 void conv_igemm(const ConvParams& p, hipStream_t s);  // LDS-pipelined implicit GEMM (impl 3)

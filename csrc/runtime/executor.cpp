@@ -38,6 +38,8 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
   {
     const char* e = std::getenv("ARENA_DEBUG_SYNC");
     debug_sync_ = e != nullptr ? std::atoi(e) : 0;
+    const char* at = std::getenv("ARENA_AUTOTUNE");
+    autotune_ = at != nullptr ? std::atoi(at) : 1;
     const char* c = std::getenv("ARENA_COPY_MODE");
     copy_mode_ = c != nullptr ? std::atoi(c) : 0;
   }
@@ -194,6 +196,8 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
   if (bk.d_arena) ARENA_HIP_CHECK(hipFree(bk.d_arena));
   ARENA_HIP_CHECK(hipMalloc(&bk.d_arena, std::max<int64_t>(arena_bytes, 256)));
   ARENA_HIP_CHECK(hipMemset(bk.d_arena, 0, std::max<int64_t>(arena_bytes, 256)));
+  bk.impl.assign(prog_.size(), 0);
+  if (autotune_) autotune(bk);
   for (int s = 0; s < 2; ++s) capture(bk, s);
   if (debug_sync_ || std::getenv("ARENA_DEBUG_ALLOC")) {
     fprintf(stderr, "[arena alloc] bucket %d arena %p..%p (%lld B)\n", B, (void*)bk.d_arena,
@@ -204,6 +208,50 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
               (void*)(slots_[s].d_out + out_bytes_total()));
     fprintf(stderr, "[arena alloc] weights %p..%p\n", (void*)d_weights_, (void*)(d_weights_ + weights_bytes_));
   }
+}
+
+// Per-bucket conv kernel selection: every conv op of the program is timed
+// eagerly (bucket capacity, full live counts) with each kernel family — 1
+// direct MFMA, 2 tiled/LDS (pointwise fast path, 3x3 halo tiles, weight-
+// stationary), 3 LDS-pipelined implicit GEMM — and the fastest is recorded
+// for the graph capture.  Costs ~100 ms per bucket; ARENA_AUTOTUNE=0 disables.
+void Executor::autotune(Bucket& bk) {
+  Slot& sl = slots_[0];
+  Ctrl c{};
+  c.n_images = bk.info.B;
+  c.n_crops = bk.info.crop_cap;
+  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+  ARENA_HIP_CHECK(hipMemcpy(sl.d_in, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  ARENA_HIP_CHECK(hipEventCreate(&e0));
+  ARENA_HIP_CHECK(hipEventCreate(&e1));
+  const int reps = 3;
+  for (size_t i = 0; i < prog_.size(); ++i) {
+    if (prog_[i][0] != OP_CONV) continue;
+    std::vector<OpRecord> one(1, prog_[i]);
+    float best = 1e30f;
+    int best_impl = 0;
+    for (int impl = 1; impl <= 3; ++impl) {
+      enqueue_program(one, bk, sl, compute_, (int)i, impl);  // warm-up (instruction cache, L2)
+      ARENA_HIP_CHECK(hipEventRecord(e0, compute_));
+      for (int k = 0; k < reps; ++k) enqueue_program(one, bk, sl, compute_, (int)i, impl);
+      ARENA_HIP_CHECK(hipEventRecord(e1, compute_));
+      ARENA_HIP_CHECK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      ARENA_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best * 0.97f || best_impl == 0) {  // prefer the lower family on near-ties
+        if (ms < best) best = ms;
+        best_impl = impl;
+      }
+    }
+    bk.impl[i] = (int8_t)best_impl;
+    if (autotune_ > 1)
+      fprintf(stderr, "[arena autotune] B=%d op %zu -> impl %d (%.1f us)\n", bk.info.B, i, best_impl,
+              best * 1e3f / reps);
+  }
+  ARENA_HIP_CHECK(hipEventDestroy(e0));
+  ARENA_HIP_CHECK(hipEventDestroy(e1));
+  ARENA_HIP_CHECK(hipMemset(bk.d_arena, 0, std::max<int64_t>(bk.info.arena_bytes, 256)));
 }
 
 void Executor::capture(Bucket& bk, int s) {
@@ -247,7 +295,8 @@ uint8_t* Executor::resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff, int 
   return base + coff * eb;
 }
 
-void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s) {
+void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s,
+                               int op_offset, int force_impl) {
   Ctrl* ctrl = (Ctrl*)resolve(bk, sl, BUF_CTRL, 0, 1);
   const ImageMeta* meta = (const ImageMeta*)resolve(bk, sl, BUF_META, 0, 1);
   const uint8_t* pool = resolve(bk, sl, BUF_POOL, 0, 1);
@@ -256,10 +305,13 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
   auto bdev = [&](int64_t kind) -> const int* { return kind == BATCH_CROPS ? &ctrl->n_crops : &ctrl->n_images; };
   const uint8_t* W = d_weights_;
 
-  for (const OpRecord& r : prog) {
+  for (size_t oi = 0; oi < prog.size(); ++oi) {
+    const OpRecord& r = prog[oi];
     switch (r[0]) {
       case OP_CONV: {
         ConvParams p{};
+        const size_t gi = (size_t)op_offset + oi;
+        p.impl = force_impl ? force_impl : (gi < bk.impl.size() ? bk.impl[gi] : 0);
         p.x = resolve(bk, sl, r[1], r[2], 2);
         p.xs = (int)r[3];
         p.H = (int)r[4];
@@ -680,7 +732,7 @@ BatchResult Executor::collect(int s) {
       // previous pass must have consumed the control block before it is rewritten
       ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
       ARENA_HIP_CHECK(hipMemcpy(sl.d_in, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
-      enqueue_program(cls_prog_, bk, sl, compute_);
+      enqueue_program(cls_prog_, bk, sl, compute_, (int)(prog_.size() - cls_prog_.size()));
     }
     uint8_t* src = sl.d_out + out_off_topk() + sizeof(TopkResult) * (size_t)CC;
     uint8_t* dst = sl.h_out + out_off_topk() + sizeof(TopkResult) * (size_t)CC;

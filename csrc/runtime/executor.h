@@ -161,11 +161,24 @@ class Executor {
     BucketInfo info;
     uint8_t* d_arena = nullptr;
     hipGraphExec_t graph[2] = {nullptr, nullptr};
+    std::vector<int8_t> impl;  // per op of prog_: conv kernel family chosen by autotune (0 = default)
   };
 
   void alloc_slots();
   void capture(Bucket& bk, int slot);
-  void enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s);
+  void enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s,
+                       int op_offset = 0, int force_impl = 0);
+  void autotune(Bucket& bk);
+
+ public:
+  // conv kernel family per program op chosen for bucket B (0 = default / not a conv)
+  std::vector<int> conv_choices(int B) const {
+    auto it = buckets_.find(B);
+    if (it == buckets_.end()) return {};
+    return std::vector<int>(it->second.impl.begin(), it->second.impl.end());
+  }
+
+ private:
   void enqueue_results_d2h(Bucket& bk, Slot& sl, int n);
   uint8_t* resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff_elems, int elem_bytes);
   int pick_bucket(int n) const;
@@ -188,6 +201,7 @@ class Executor {
   int next_slot_ = 0;
   bool has_topk_ = false, has_det_ = false, has_raw_ = false;
   int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on compute stream
+  int autotune_ = 1;  // ARENA_AUTOTUNE: 0 off, 1 on, 2 on + report
   int debug_sync_ = 0;  // ARENA_DEBUG_SYNC: 1 eager op-by-op, 2 one graph per op
   std::mutex mu_;
   // host worker pool for packing images into pinned memory
