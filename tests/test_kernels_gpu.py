@@ -311,3 +311,26 @@ def test_conv3x3_v3_matches_v2(device, H, Cin, Cout, s):
         C.set_conv_v3(True)
     assert (y3.float() - y2.float()).abs().max().item() <= 0.0625
     _check(_nchw(y3.cpu()), _ref_conv(xn.cpu(), w, b, s, 1, "silu"))
+
+
+def test_executor_autotune_choices(device):
+    """Autotuned conv kernel choices are recorded per bucket and results match the default kernels."""
+    import os
+
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+    from inference_arena_amd.models.zoo import make_mobilenet, make_yolo
+
+    yolo, mnet = make_yolo(0, cls_shift=-20.0), make_mobilenet(1)
+    imgs = synthetic_images(4, 77)
+    pipe = GpuPipeline(yolo, mnet, device=0, buckets=[4])
+    choices = pipe.ex.conv_choices(4)
+    assert set(c for c in choices if c) <= {1, 2, 3} and sum(1 for c in choices if c) >= 60
+    tuned = pipe.infer(imgs)
+    os.environ["ARENA_AUTOTUNE"] = "0"
+    try:
+        plain = GpuPipeline(yolo, mnet, device=0, buckets=[4]).infer(imgs)
+    finally:
+        os.environ.pop("ARENA_AUTOTUNE")
+    for a, b in zip(tuned, plain):
+        assert abs(len(a) - len(b)) <= 1
