@@ -38,6 +38,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   constexpr int NE = PIN_PAD / 16, NP = POUT_PAD / 16, NPW = (NP + 3) / 4;
   constexpr int WP_PER_T = (MP * 64 + 255) / 256;  // 16-B pieces of a Wp chunk per thread
   constexpr int WE_PER_T = 3;                       // inp_pad <= 192 -> 32*24/256
+  constexpr int WD_BYTES = 9 * 32 * 4 + 32 * 4;       // dw taps + bias of one chunk, fp32
   extern __shared__ __align__(16) uint8_t lds[];
   const int nslab = p.inp_pad >> 5;
   const int cpr = p.inp_pad >> 3;
@@ -45,8 +46,8 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   uint8_t* Es = Xs + nslab * PIN_PAD * 64;              // [PIN_PAD] rows (EXPAND)
   uint8_t* Ds = Es + (EXPAND ? PIN_PAD * 64 : 0);       // [POUT_PAD] rows
   uint8_t* Wps = Ds + POUT_PAD * 64;                    // 2 x [MP*16] rows
-  uint8_t* Wds = Wps + 2 * MP * 16 * 64;                // 2 x [9][32] bf16 + [32] fp32 bias
-  uint8_t* Wes = Wds + 2 * 704;                         // 2 x [nslab][32] rows (EXPAND)
+  uint8_t* Wds = Wps + 2 * MP * 16 * 64;                // 2 x ([9][32] fp32 taps + [32] fp32 bias)
+  uint8_t* Wes = Wds + 2 * WD_BYTES;                    // 2 x [nslab][32] rows (EXPAND)
   const int we_buf = nslab * 32 * 64;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -104,7 +105,16 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
         }
       }
     }
-    if (tid < 44) *(uint4*)(Wds + buf * 704 + tid * 16) = rwd;  // [9][32] bf16 taps, then 32 fp32 biases
+    // taps: 8 bf16 -> 8 fp32 (two 16-B stores) at [tap][chunk*8]; biases: 4 fp32 at 1152 + 16*(tid-36)
+    uint8_t* wdl = Wds + buf * WD_BYTES;
+    if (tid < 36) {
+      float f[8];
+      unpack8(rwd, f);
+      *(float4*)(wdl + (tid >> 2) * 128 + (tid & 3) * 32) = make_float4(f[0], f[1], f[2], f[3]);
+      *(float4*)(wdl + (tid >> 2) * 128 + (tid & 3) * 32 + 16) = make_float4(f[4], f[5], f[6], f[7]);
+    } else if (tid < 44) {
+      *(uint4*)(wdl + 1152 + (tid - 36) * 16) = rwd;
+    }
   };
 
   // ---- input tile (with halo) -> LDS, zero outside the image / past inp
@@ -166,15 +176,15 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
     }
 
     // depthwise 3x3 stride S: one (output pixel, 8-channel chunk) per item
-    const uint8_t* wdl = Wds + cur * 704;
+    const uint8_t* wdl = Wds + cur * WD_BYTES;
     for (int i = tid; i < POUT_PAD * 4; i += 256) {
       const int q = i >> 2, c = i & 3;
       uint4 outv = {0u, 0u, 0u, 0u};
       if (q < POUT) {
         const int oy = q / TW, ox = q - oy * TW;
         float a[8];
-        const float4 b0 = *(const float4*)(wdl + 576 + c * 32);
-        const float4 b1 = *(const float4*)(wdl + 576 + c * 32 + 16);
+        const float4 b0 = *(const float4*)(wdl + 1152 + c * 32);
+        const float4 b1 = *(const float4*)(wdl + 1152 + c * 32 + 16);
         a[0] = b0.x; a[1] = b0.y; a[2] = b0.z; a[3] = b0.w;
         a[4] = b1.x; a[5] = b1.y; a[6] = b1.z; a[7] = b1.w;
 #pragma unroll
@@ -182,11 +192,14 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx) {
             const int pin = (oy * S + ky) * PW + ox * S + kx;
-            float e[8], w[8];
+            float e[8];
             unpack8(*(const uint4*)(Esrc + swz(pin, c)), e);
-            unpack8(*(const uint4*)(wdl + (ky * 3 + kx) * 64 + c * 16), w);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a[k] = fmaf(e[k], w[k], a[k]);
+            const float4 w0 = *(const float4*)(wdl + (ky * 3 + kx) * 128 + c * 32);
+            const float4 w1 = *(const float4*)(wdl + (ky * 3 + kx) * 128 + c * 32 + 16);
+            a[0] = fmaf(e[0], w0.x, a[0]); a[1] = fmaf(e[1], w0.y, a[1]);
+            a[2] = fmaf(e[2], w0.z, a[2]); a[3] = fmaf(e[3], w0.w, a[3]);
+            a[4] = fmaf(e[4], w1.x, a[4]); a[5] = fmaf(e[5], w1.y, a[5]);
+            a[6] = fmaf(e[6], w1.z, a[6]); a[7] = fmaf(e[7], w1.w, a[7]);
           }
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[k] = relu6(a[k]);
@@ -250,7 +263,7 @@ static size_t ir_lds_bytes(int inp_pad) {
   constexpr int PIN_PAD = (PH * PW + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
   const int nslab = inp_pad / 32;
   return (size_t)nslab * PIN_PAD * 64 + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64 + 2 * MP * 16 * 64 +
-         2 * 704 + (EXPAND ? 2 * nslab * 32 * 64 : 0);
+         2 * (9 * 32 * 4 + 32 * 4) + (EXPAND ? 2 * nslab * 32 * 64 : 0);
 }
 
 template <int S, int TH, int TW, int MP, bool EXPAND>

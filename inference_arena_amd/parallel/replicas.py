@@ -71,14 +71,20 @@ class Replicas:
 
 
 def launch(arch: str, n: int, *, port: int = 8100, stride: int = 0, host: str = "127.0.0.1",
-           env: dict | None = None, log_dir: str | None = None) -> Replicas:
+           env: dict | None = None, log_dir: str | None = None, procs_per_gpu: int = 1) -> Replicas:
+    """``n`` GPUs x ``procs_per_gpu`` serving processes.  Several processes per GPU
+    scale the CPU side (HTTP parsing, JPEG decode) while sharing the device; the
+    start-up weight broadcast then runs over gloo, because one RCCL
+    communicator cannot hold two ranks of the same GPU."""
     master = free_port()
     procs = []
-    for r in range(n):
+    world = n * procs_per_gpu
+    for r in range(world):
         e = dict(os.environ)
         e.update(env or {})
-        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
-                  "MASTER_PORT": str(master), "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": str(master), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+                  "ARENA_PROCS_PER_GPU": str(procs_per_gpu)})
         out = open(os.path.join(log_dir, f"replica_{r}.log"), "w") if log_dir else subprocess.DEVNULL
         procs.append(subprocess.Popen([sys.executable, "-m", "inference_arena_amd.server.replica", "--arch", arch,
                                        "--host", host, "--port", str(port), "--port-stride", str(stride)],
@@ -93,11 +99,13 @@ def main(argv=None) -> int:
     ap.add_argument("--port", type=int, default=8100)
     ap.add_argument("--stride", type=int, default=0)
     ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--procs-per-gpu", type=int, default=int(os.environ.get("ARENA_PROCS_PER_GPU", "1")))
     a = ap.parse_args(argv)
-    rep = launch(a.arch, a.gpus, port=a.port, stride=a.stride, host=a.host)
+    rep = launch(a.arch, a.gpus, port=a.port, stride=a.stride, host=a.host, procs_per_gpu=a.procs_per_gpu)
     try:
         ok = rep.wait_ready()
-        print(f"{a.gpus} replica(s) {'ready' if ok else 'FAILED'} on port(s) {rep.ports()}", flush=True)
+        print(f"{a.gpus} GPU(s) x {a.procs_per_gpu} process(es) {'ready' if ok else 'FAILED'} on port(s) "
+              f"{rep.ports()}", flush=True)
         while rep.alive():
             time.sleep(1)
     except KeyboardInterrupt:

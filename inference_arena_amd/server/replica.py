@@ -27,10 +27,34 @@ def _socket(host: str, port: int, reuse_port: bool) -> socket.socket:
     s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     if reuse_port:
         s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    # accepted connections inherit TCP_NODELAY on Linux; without it a response written
+    # as header + body segments waits on the client's delayed ACK (~40 ms per request)
+    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
     s.bind((host, port))
     s.listen(2048)
     s.setblocking(False)
     return s
+
+
+class ReplicaTag:
+    """Pure-ASGI wrapper adding ``x-arena-replica`` to every HTTP response (a
+    Starlette BaseHTTPMiddleware costs ~1 ms per request)."""
+
+    def __init__(self, app, rank: int):
+        self.app = app
+        self.tag = str(rank).encode()
+
+    async def __call__(self, scope, receive, send):
+        if scope["type"] != "http":
+            return await self.app(scope, receive, send)
+
+        async def send_tagged(msg):
+            if msg["type"] == "http.response.start":
+                msg = dict(msg)
+                msg["headers"] = list(msg.get("headers", [])) + [(b"x-arena-replica", self.tag)]
+            await send(msg)
+
+        await self.app(scope, receive, send_tagged)
 
 
 def build_app(arch: str, settings, info):
@@ -88,24 +112,25 @@ def main(argv=None) -> int:
     from ..parallel import dist as D
     from ..utils.settings import Settings
 
+    import os
+
     settings = Settings.from_env()
-    backend = "gloo" if settings.ARENA_DEVICE == "cpu" else None
+    per_gpu = max(1, int(os.environ.get("ARENA_PROCS_PER_GPU", "1")))
+    backend = "gloo" if settings.ARENA_DEVICE == "cpu" or per_gpu > 1 else None
     info = D.init_from_env(backend)
     if settings.ARENA_DEVICE != "cpu":
-        settings.ARENA_GPU = info.local_rank
+        settings.ARENA_GPU = info.local_rank // per_gpu
+        if backend == "gloo":
+            import torch
+
+            torch.cuda.set_device(settings.ARENA_GPU)
     app = build_app(a.arch, settings, info)
     D.barrier(info)
     D.shutdown(info)  # the group is only needed for start-up
 
-    @app.middleware("http")
-    async def tag(request, call_next):
-        resp = await call_next(request)
-        resp.headers["x-arena-replica"] = str(info.rank)
-        return resp
-
     port = a.port + a.port_stride * info.rank
     sock = _socket(a.host, port, reuse_port=a.port_stride == 0)
-    server = uvicorn.Server(uvicorn.Config(app, log_level="warning", access_log=False))
+    server = uvicorn.Server(uvicorn.Config(ReplicaTag(app, info.rank), log_level="warning", access_log=False))
     asyncio.run(server.serve(sockets=[sock]))
     return 0
 

@@ -36,13 +36,14 @@ def main(argv=None) -> int:
     ap.add_argument("--procs", type=int, default=4)
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--out", default="gpurun_out/load")
+    ap.add_argument("--procs-per-gpu", type=int, default=1)
     a = ap.parse_args(argv)
     out = Path(a.out)
     images = [encode_jpeg(im, quality=95) for im in workload_images(100)]
     ports = {"monolithic": 8100, "microservices": 8200, "triton": 8300}
     rows = []
     for arch in a.archs.split(","):
-        procs, ok = start(arch, a.gpus, out / f"logs_{arch}", a.device)
+        procs, ok = start(arch, a.gpus, out / f"logs_{arch}", a.device, procs_per_gpu=a.procs_per_gpu)
         try:
             if not ok:
                 print(f"{arch}: failed to start", flush=True)

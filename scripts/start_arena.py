@@ -44,22 +44,22 @@ def wait_http(url: str, timeout: float, procs) -> bool:
 
 
 def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = "model_repository",
-          extra_env: dict | None = None):
+          extra_env: dict | None = None, procs_per_gpu: int = 1):
     env = dict(os.environ, PYTHONPATH=str(ROOT), HSA_ENABLE_IPC_MODE_LEGACY="0", ARENA_DEVICE=device,
                **(extra_env or {}))
     log_dir.mkdir(parents=True, exist_ok=True)
     procs = []
     if arch == "monolithic":
         procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "monolithic", "--gpus", str(gpus),
-                            "--port", "8100"], env, log_dir, "monolithic"))
+                            "--port", "8100", "--procs-per-gpu", str(procs_per_gpu)], env, log_dir, "monolithic"))
         ok = wait_http("http://127.0.0.1:8100/health", 600, procs)
     elif arch == "microservices":
         procs.append(spawn(["inference_arena_amd.server.classification_service"], dict(env, PORT="8201"), log_dir,
                            "classification"))
         time.sleep(1)
         procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "detection", "--gpus", str(gpus),
-                            "--port", "8200"], dict(env, CLASSIFICATION_GRPC_ENDPOINT="127.0.0.1:8201"), log_dir,
-                           "detection"))
+                            "--port", "8200", "--procs-per-gpu", str(procs_per_gpu)],
+                           dict(env, CLASSIFICATION_GRPC_ENDPOINT="127.0.0.1:8201"), log_dir, "detection"))
         ok = wait_http("http://127.0.0.1:8200/health", 600, procs)
     elif arch == "triton":
         if not (Path(repo) / "yolov5n" / "config.pbtxt").exists():
@@ -95,8 +95,9 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--logs", default="logs")
+    ap.add_argument("--procs-per-gpu", type=int, default=1)
     a = ap.parse_args(argv)
-    procs, ok = start(a.arch, a.gpus, Path(a.logs), a.device)
+    procs, ok = start(a.arch, a.gpus, Path(a.logs), a.device, procs_per_gpu=a.procs_per_gpu)
     print(f"{a.arch}: {'ready' if ok else 'FAILED (see ' + a.logs + ')'}", flush=True)
     try:
         while ok and all(p.poll() is None for p in procs):

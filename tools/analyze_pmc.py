@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Per-op hardware-counter table from rocprofv3 --pmc runs of bench.py.
+
+Each ``<dir>/run_counter_collection.csv`` holds one counter set for every
+dispatch.  The program's ops are located as in analyze_trace.py (a replay
+starts at the letterbox kernel; the k-th arena dispatch of a replay is op k);
+values are averaged over the last complete replays and per-op ratios are
+derived: VALU and LDS instructions per MFMA, LDS bank-conflict share, waves.
+
+    python tools/analyze_pmc.py gpurun_out/pmc2/*/run_counter_collection.csv --out profiles/r1_pmc_ops.md
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def replays(path: Path, n_ops: int, keep: int):
+    rows = [r for r in csv.DictReader(open(path)) if "arena::" in r["Kernel_Name"]]
+    by_dispatch = defaultdict(dict)
+    names = {}
+    for r in rows:
+        d = int(r["Dispatch_Id"])
+        by_dispatch[d][r["Counter_Name"]] = float(r["Counter_Value"])
+        names[d] = r["Kernel_Name"]
+    order = sorted(by_dispatch)
+    starts = [i for i, d in enumerate(order) if "letterbox" in names[d]]
+    out = []
+    for s in starts:
+        seq = order[s:s + n_ops]
+        if len(seq) == n_ops:
+            out.append([(names[d], by_dispatch[d]) for d in seq])
+    return out[-keep:]
+
+
+def main(argv=None) -> int:
+    from inference_arena_amd.engine.plans import plan_pipeline
+    from inference_arena_amd.models.zoo import default_models
+    from tools.analyze_trace import KIND, describe
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csvs", nargs="+")
+    ap.add_argument("--replays", type=int, default=2)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args(argv)
+    prog = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45)
+    n_ops = prog.ops.shape[0]
+    vals = defaultdict(lambda: defaultdict(list))
+    kname = {}
+    for f in a.csvs:
+        for rp in replays(Path(f), n_ops, a.replays):
+            for k, (name, cnt) in enumerate(rp):
+                kname[k] = name.replace("void arena::", "").split("(")[0]
+                for c, v in cnt.items():
+                    vals[k][c].append(v)
+    counters = sorted({c for k in vals for c in vals[k]})
+    lines = ["| op | kind | shape | kernel | " + " | ".join(counters) + " | valu/mfma | lds/mfma | conflict % |",
+             "|" + "---|" * (4 + len(counters) + 3)]
+    for k in range(n_ops):
+        if k not in vals:
+            continue
+        m = {c: sum(v) / len(v) for c, v in vals[k].items()}
+        mf = m.get("SQ_INSTS_MFMA", 0.0)
+        vr = f"{m['SQ_INSTS_VALU'] / mf:.1f}" if mf and "SQ_INSTS_VALU" in m else "-"
+        lr = f"{m['SQ_INSTS_LDS'] / mf:.2f}" if mf and "SQ_INSTS_LDS" in m else "-"
+        cf = (f"{100 * m['SQ_LDS_BANK_CONFLICT'] / m['SQ_LDS_IDX_ACTIVE']:.1f}"
+              if m.get("SQ_LDS_IDX_ACTIVE") else "-")
+        kind = KIND.get(int(prog.ops[k][0]), "?")
+        lines.append(f"| {k} | {kind} | {describe(prog.ops[k])} | {kname[k]} | "
+                     + " | ".join(f"{m[c]:.3g}" if c in m else "-" for c in counters) + f" | {vr} | {lr} | {cf} |")
+    text = "\n".join(lines)
+    print(text)
+    if a.out:
+        Path(a.out).write_text(text + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
