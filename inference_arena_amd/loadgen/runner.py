@@ -50,25 +50,24 @@ class PhaseResult:
     wall_s: float = 0.0
 
 
-def _multipart(payload: bytes, fieldname: str):
-    import aiohttp
+def _bodies(images: list[bytes], fieldname: str) -> list[tuple[bytes, str]]:
+    """Pre-encoded multipart bodies: one buffer per request, no per-request form building."""
+    from ..server.multipart import encode_multipart
 
-    fd = aiohttp.FormData()
-    fd.add_field(fieldname, payload, filename="image.jpg", content_type="image/jpeg")
-    return fd
+    return [encode_multipart(fieldname, img, "image.jpg") for img in images]
 
 
-async def _user_loop(session, cfg: LoadConfig, uid: int, images: list[bytes], t_start: float, t_stop: float,
-                     out: list) -> None:
+async def _user_loop(session, cfg: LoadConfig, uid: int, bodies: list[tuple[bytes, str]], t_start: float,
+                     t_stop: float, out: list) -> None:
     import aiohttp
 
     rng = random.Random(cfg.seed * 1000 + uid)
     while time.perf_counter() < t_stop:
-        img = images[rng.randrange(len(images))]
+        body, ctype = bodies[rng.randrange(len(bodies))]
         t0 = time.perf_counter()
         status, ndet = 0, -1
         try:
-            async with session.post(cfg.url, data=_multipart(img, cfg.field)) as r:
+            async with session.post(cfg.url, data=body, headers={"content-type": ctype}) as r:
                 body = await r.read()
                 status = r.status
                 if status == 200:
@@ -89,9 +88,10 @@ async def _drive(cfg: LoadConfig, users: range, images: list[bytes]) -> list:
     conn = aiohttp.TCPConnector(limit=0, force_close=False)
     timeout = aiohttp.ClientTimeout(total=cfg.timeout_s)
     out: list = []
+    bodies = _bodies(images, cfg.field)
     async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:
         t_start = time.perf_counter()
-        await asyncio.gather(*(_user_loop(s, cfg, u, images, t_start, t_start + total, out) for u in users))
+        await asyncio.gather(*(_user_loop(s, cfg, u, bodies, t_start, t_start + total, out) for u in users))
     return out
 
 
