@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void conv3x3_v3_kernel(const ConvParams p) {
     const int pix = sq + 64 * i;
     const int r = pix / IC, c = pix - r * IC;
     const int iy = iy_base + r, ix = ix_base + c;
-    const bool ok = pix < G::IN_PIX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+    const bool ok = pix < G::IN_PIX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && sc * 8 < Cin;
     in_goff[i] = ok ? (iy * p.W + ix) * p.xs + sc * 8 : -1;
     const int lp = r * ICP + c;
     in_loff[i] = pix < G::IN_PIX ? lp * 64 + v3swz(lp, sc) : -1;
@@ -79,8 +79,8 @@ __global__ __launch_bounds__(256) void conv3x3_v3_kernel(const ConvParams p) {
     const int tap = R / BN, n = R - tap * BN;
     int co = cout0 + n;
     co = co < p.Cout_pad ? co : p.Cout_pad - 1;
-    w_goff[i] = R < 9 * BN ? co * p.Kpad + tap * Cin + sc * 8 : -1;
-    w_loff[i] = R * 64 + v3swz(n, sc);
+    w_goff[i] = R < 9 * BN && sc * 8 < Cin ? co * p.Kpad + tap * Cin + sc * 8 : -1;
+    w_loff[i] = R < 9 * BN ? R * 64 + v3swz(n, sc) : -1;  // masked chunks still store zeros
   }
 
   uint4 rin[G::IN_IT], rw[G::W_IT];
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void conv3x3_v3_kernel(const ConvParams p) {
       if (in_loff[i] >= 0) *(uint4*)(sin + in_loff[i]) = rin[i];
 #pragma unroll
     for (int i = 0; i < G::W_IT; ++i)
-      if (w_goff[i] >= 0) *(uint4*)(sw + w_loff[i]) = rw[i];
+      if (w_loff[i] >= 0) *(uint4*)(sw + w_loff[i]) = rw[i];
   };
 
   // ---- fragment read bases: B (input) per kw, A (weights) per lane
@@ -196,8 +196,9 @@ static void v3_nf(const ConvParams& p, hipStream_t s) {
 }
 
 bool conv3x3_v3(const ConvParams& p, hipStream_t s) {
-  if (!(p.KH == 3 && p.KW == 3 && (p.stride == 1 || p.stride == 2) && p.Cin % 32 == 0 && !p.f32out &&
-        p.Kpad >= 9 * p.Cin))
+  // Cin = 16 (s2d stems, YOLO's first C3) runs as one half-empty 32-channel slab
+  if (!(p.KH == 3 && p.KW == 3 && (p.stride == 1 || p.stride == 2) && (p.Cin % 32 == 0 || p.Cin == 16) &&
+        !p.f32out && p.Kpad >= 9 * p.Cin))
     return false;
   if ((long)p.H * p.W * p.xs >= (1L << 31)) return false;  // 32-bit staging offsets
   const int ncf = p.Cout_pad / 16;

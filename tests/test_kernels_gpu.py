@@ -334,3 +334,23 @@ def test_executor_autotune_choices(device):
         os.environ.pop("ARENA_AUTOTUNE")
     for a, b in zip(tuned, plain):
         assert abs(len(a) - len(b)) <= 1
+
+
+@pytest.mark.parametrize("H,s", [(64, 1), (64, 2), (37, 1)])
+def test_conv3x3_v3_cin16(device, H, s):
+    """Cin = 16 (s2d stems, first C3) through the v3 halo-tile kernel as a half-empty slab."""
+    C = native()
+    g = torch.Generator().manual_seed(H * 3 + s)
+    x = torch.randn(2, 16, H, H, generator=g)
+    w = torch.randn(32, 16, 3, 3, generator=g) / 12
+    b = torch.randn(32, generator=g) * 0.1
+    xn = _nhwc(x).to(torch.bfloat16).to(device)
+    old = C.get_conv_impl()
+    C.set_conv_impl(2)
+    try:
+        C.set_conv_pw(False)
+        y = AF.conv2d_nhwc(xn, w, b, stride=s, act="silu")
+    finally:
+        C.set_conv_pw(True)
+        C.set_conv_impl(old)
+    _check(_nchw(y.cpu()), _ref_conv(xn.cpu(), w, b, s, 1, "silu"))
