@@ -308,15 +308,20 @@ async def serve(args) -> None:
     import uvicorn
 
     setup_logging(args.log_level)
+    from .replica import _socket
+
     server = ModelServer(args.model_repository, device=args.device, gpu=args.gpu)
+    # every port is opened with SO_REUSEPORT (gRPC's default), so several server processes on
+    # one GPU can share :8000/:8001/:8002 and the kernel spreads connections over them
     g, _ = await start_grpc(server, args.host, args.grpc_port)
-    servers = [uvicorn.Server(uvicorn.Config(create_http_app(server), host=args.host, port=args.http_port,
-                                             log_level="warning", access_log=False)),
-               uvicorn.Server(uvicorn.Config(create_metrics_app(server), host=args.host, port=args.metrics_port,
-                                             log_level="warning", access_log=False))]
+    apps = [(create_http_app(server), args.http_port), (create_metrics_app(server), args.metrics_port)]
+    servers, socks = [], []
+    for app, port in apps:
+        socks.append(_socket(args.host, port, reuse_port=True))
+        servers.append(uvicorn.Server(uvicorn.Config(app, log_level="warning", access_log=False)))
     log.info(f"model server ready: grpc {args.grpc_port} http {args.http_port} metrics {args.metrics_port}")
     try:
-        await asyncio.gather(*(s.serve() for s in servers))
+        await asyncio.gather(*(s.serve(sockets=[k]) for s, k in zip(servers, socks)))
     finally:
         await g.stop(grace=5)
         server.close()

@@ -65,12 +65,15 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
         if not (Path(repo) / "yolov5n" / "config.pbtxt").exists():
             subprocess.run([sys.executable, str(ROOT / "scripts" / "upload_models.py"), "--repository", repo],
                            check=True, env=env)
-        procs.append(spawn(["inference_arena_amd.server.model_server", "--model-repository", repo, "--device", device],
-                           env, log_dir, "model_server"))
+        for k in range(max(1, procs_per_gpu)):  # server processes share :8000/:8001/:8002 (SO_REUSEPORT)
+            procs.append(spawn(["inference_arena_amd.server.model_server", "--model-repository", repo, "--device",
+                                device], env, log_dir, f"model_server_{k}"))
         ok = wait_http("http://127.0.0.1:8000/v2/health/ready", 600, procs)
         if ok:
-            procs.append(spawn(["inference_arena_amd.server.gateway"],
-                               dict(env, PORT="8300", TRITON_GRPC_ENDPOINT="127.0.0.1:8001"), log_dir, "gateway"))
+            procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "gateway", "--gpus", "1",
+                                "--port", "8300", "--procs-per-gpu", str(procs_per_gpu)],
+                               dict(env, TRITON_GRPC_ENDPOINT="127.0.0.1:8001", ARENA_DEVICE="cpu"), log_dir,
+                               "gateway"))
             ok = wait_http("http://127.0.0.1:8300/health", 300, procs)
     else:
         raise ValueError(arch)
