@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   constexpr int NE = PIN_PAD / 16, NP = POUT_PAD / 16, NPW = (NP + 3) / 4;
   constexpr int WP_PER_T = (MP * 64 + 255) / 256;  // 16-B pieces of a Wp chunk per thread
   constexpr int WE_PER_T = 3;                       // inp_pad <= 192 -> 32*24/256
-  constexpr int WD_BYTES = 9 * 32 * 4 + 32 * 4;       // dw taps + bias of one chunk, fp32
+  constexpr int WD_BYTES = 768;  // per chunk: tap pairs [4][32] bf16x2, tap 8 [32] fp32, bias [32] fp32
   extern __shared__ __align__(16) uint8_t lds[];
   const int nslab = p.inp_pad >> 5;
   const int cpr = p.inp_pad >> 3;
@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   uint8_t* Es = Xs + nslab * PIN_PAD * 64;              // [PIN_PAD] rows (EXPAND)
   uint8_t* Ds = Es + (EXPAND ? PIN_PAD * 64 : 0);       // [POUT_PAD] rows
   uint8_t* Wps = Ds + POUT_PAD * 64;                    // 2 x [MP*16] rows
-  uint8_t* Wds = Wps + 2 * MP * 16 * 64;                // 2 x ([9][32] fp32 taps + [32] fp32 bias)
+  uint8_t* Wds = Wps + 2 * MP * 16 * 64;                // 2 x dw taps (packed pairs) + bias
   uint8_t* Wes = Wds + 2 * WD_BYTES;                    // 2 x [nslab][32] rows (EXPAND)
   const int we_buf = nslab * 32 * 64;
 
@@ -105,15 +105,36 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
         }
       }
     }
-    // taps: 8 bf16 -> 8 fp32 (two 16-B stores) at [tap][chunk*8]; biases: 4 fp32 at 1152 + 16*(tid-36)
+    // Depthwise taps are stored as bf16 PAIRS (tap 2p, tap 2p+1) per channel, the layout
+    // v_dot2c_f32_bf16 consumes: thread tid (< 36) holds tap tid>>2, channels (tid&3)*8..+8;
+    // its partner tap sits 4 lanes up in the same wave.  Tap 8 is kept as fp32.
     uint8_t* wdl = Wds + buf * WD_BYTES;
-    if (tid < 36) {
-      float f[8];
-      unpack8(rwd, f);
-      *(float4*)(wdl + (tid >> 2) * 128 + (tid & 3) * 32) = make_float4(f[0], f[1], f[2], f[3]);
-      *(float4*)(wdl + (tid >> 2) * 128 + (tid & 3) * 32 + 16) = make_float4(f[4], f[5], f[6], f[7]);
-    } else if (tid < 44) {
-      *(uint4*)(wdl + 1152 + (tid - 36) * 16) = rwd;
+    if (tid < 64) {
+      uint4 nb;
+      nb.x = __shfl_down(rwd.x, 4, 64);
+      nb.y = __shfl_down(rwd.y, 4, 64);
+      nb.z = __shfl_down(rwd.z, 4, 64);
+      nb.w = __shfl_down(rwd.w, 4, 64);
+      const int tap = tid >> 2, c = tid & 3;
+      if (tid < 32 && (tap & 1) == 0) {
+        const unsigned a[4] = {rwd.x, rwd.y, rwd.z, rwd.w}, b2[4] = {nb.x, nb.y, nb.z, nb.w};
+        unsigned q[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          q[2 * j] = __builtin_amdgcn_perm(b2[j], a[j], 0x05040100u);      // (ch 2j: tap, tap+1)
+          q[2 * j + 1] = __builtin_amdgcn_perm(b2[j], a[j], 0x07060302u);  // (ch 2j+1: tap, tap+1)
+        }
+        uint4* dst = (uint4*)(wdl + (tap >> 1) * 128 + c * 32);
+        dst[0] = make_uint4(q[0], q[1], q[2], q[3]);
+        dst[1] = make_uint4(q[4], q[5], q[6], q[7]);
+      } else if (tap == 8) {
+        float f[8];
+        unpack8(rwd, f);
+        *(float4*)(wdl + 512 + c * 32) = make_float4(f[0], f[1], f[2], f[3]);
+        *(float4*)(wdl + 512 + c * 32 + 16) = make_float4(f[4], f[5], f[6], f[7]);
+      } else if (tid >= 36 && tid < 44) {
+        *(uint4*)(wdl + 640 + (tid - 36) * 16) = rwd;
+      }
     }
   };
 
@@ -183,24 +204,44 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
       if (q < POUT) {
         const int oy = q / TW, ox = q - oy * TW;
         float a[8];
-        const float4 b0 = *(const float4*)(wdl + 1152 + c * 32);
-        const float4 b1 = *(const float4*)(wdl + 1152 + c * 32 + 16);
+        const float4 b0 = *(const float4*)(wdl + 640 + c * 32);
+        const float4 b1 = *(const float4*)(wdl + 640 + c * 32 + 16);
         a[0] = b0.x; a[1] = b0.y; a[2] = b0.z; a[3] = b0.w;
         a[4] = b1.x; a[5] = b1.y; a[6] = b1.z; a[7] = b1.w;
+        // taps (2p, 2p+1): regroup each channel's two taps with v_perm, multiply-add with v_dot2c
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+        for (int pp = 0; pp < 4; ++pp) {
+          const int t0 = 2 * pp, t1 = 2 * pp + 1;
+          const int pin0 = (oy * S + t0 / 3) * PW + ox * S + t0 % 3;
+          const int pin1 = (oy * S + t1 / 3) * PW + ox * S + t1 % 3;
+          const uint4 e0 = *(const uint4*)(Esrc + swz(pin0, c));
+          const uint4 e1 = *(const uint4*)(Esrc + swz(pin1, c));
+          const uint4 wa = *(const uint4*)(wdl + pp * 128 + c * 32);
+          const uint4 wb = *(const uint4*)(wdl + pp * 128 + c * 32 + 16);
+          const unsigned x0[4] = {e0.x, e0.y, e0.z, e0.w}, x1[4] = {e1.x, e1.y, e1.z, e1.w};
+          const unsigned wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int pin = (oy * S + ky) * PW + ox * S + kx;
-            float e[8];
-            unpack8(*(const uint4*)(Esrc + swz(pin, c)), e);
-            const float4 w0 = *(const float4*)(wdl + (ky * 3 + kx) * 128 + c * 32);
-            const float4 w1 = *(const float4*)(wdl + (ky * 3 + kx) * 128 + c * 32 + 16);
-            a[0] = fmaf(e[0], w0.x, a[0]); a[1] = fmaf(e[1], w0.y, a[1]);
-            a[2] = fmaf(e[2], w0.z, a[2]); a[3] = fmaf(e[3], w0.w, a[3]);
-            a[4] = fmaf(e[4], w1.x, a[4]); a[5] = fmaf(e[5], w1.y, a[5]);
-            a[6] = fmaf(e[6], w1.z, a[6]); a[7] = fmaf(e[7], w1.w, a[7]);
+          for (int j = 0; j < 4; ++j) {
+            const unsigned lo = __builtin_amdgcn_perm(x1[j], x0[j], 0x05040100u);
+            const unsigned hi = __builtin_amdgcn_perm(x1[j], x0[j], 0x07060302u);
+            a[2 * j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, lo),
+                                                       __builtin_bit_cast(bf16x2, wv[2 * j]), a[2 * j], false);
+            a[2 * j + 1] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, hi),
+                                                           __builtin_bit_cast(bf16x2, wv[2 * j + 1]), a[2 * j + 1],
+                                                           false);
           }
+        }
+        {  // tap 8 (ky = kx = 2)
+          const int pin = (oy * S + 2) * PW + ox * S + 2;
+          float e[8];
+          unpack8(*(const uint4*)(Esrc + swz(pin, c)), e);
+          const float4 w0 = *(const float4*)(wdl + 512 + c * 32);
+          const float4 w1 = *(const float4*)(wdl + 512 + c * 32 + 16);
+          a[0] = fmaf(e[0], w0.x, a[0]); a[1] = fmaf(e[1], w0.y, a[1]);
+          a[2] = fmaf(e[2], w0.z, a[2]); a[3] = fmaf(e[3], w0.w, a[3]);
+          a[4] = fmaf(e[4], w1.x, a[4]); a[5] = fmaf(e[5], w1.y, a[5]);
+          a[6] = fmaf(e[6], w1.z, a[6]); a[7] = fmaf(e[7], w1.w, a[7]);
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[k] = relu6(a[k]);
         outv = pack8(a);
@@ -263,7 +304,7 @@ static size_t ir_lds_bytes(int inp_pad) {
   constexpr int PIN_PAD = (PH * PW + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
   const int nslab = inp_pad / 32;
   return (size_t)nslab * PIN_PAD * 64 + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64 + 2 * MP * 16 * 64 +
-         2 * (9 * 32 * 4 + 32 * 4) + (EXPAND ? 2 * nslab * 32 * 64 : 0);
+         2 * 768 + (EXPAND ? 2 * nslab * 32 * 64 : 0);
 }
 
 template <int S, int TH, int TW, int MP, bool EXPAND>
