@@ -14,10 +14,11 @@
 namespace arena {
 
 // Each thread computes a vertical strip of R output rows for one pixel column
-// and one 8-channel group: the (R-1)*S+3 input rows it needs are loaded and
-// converted once and reused by every output row they touch, and the 9 taps'
-// weights stay in registers (fp32) for the whole strip.  All index math is
-// 32-bit (v1 used 64-bit div/mod per thread).
+// and one 8-channel group: the (R-1)*S+3 input rows it needs are loaded once
+// and reused by every output row they touch, and the 9 taps' weights stay in
+// registers for the whole strip.  Horizontal tap pairs (kx = 0, 1) run as
+// v_dot2c_f32_bf16 on channel-regrouped bf16 pairs (v_perm), kx = 2 as an fp32
+// FMA.  All index math is 32-bit (v1 used 64-bit div/mod per thread).
 template <int R, int S>
 __global__ __launch_bounds__(256) void dwconv3x3_kernel(const DwParams p) {
   const int B = live_batch(p.B, p.bdev);
@@ -37,9 +38,22 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(const DwParams p) {
 
   const bf16* x = (const bf16*)p.x + (size_t)b * p.H * p.W * p.xs + c0;
   const bf16* w = (const bf16*)p.w + c0;
-  float wt[9][8];
+  // Per kernel row ky: taps (kx=0, kx=1) as bf16 pairs per channel for v_dot2c_f32_bf16,
+  // tap kx=2 as fp32.
+  unsigned wp[3][8];
+  float w2[3][8];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) unpack8(*(const uint4*)(w + k * p.C), wt[k]);
+  for (int ky = 0; ky < 3; ++ky) {
+    const uint4 a = *(const uint4*)(w + (ky * 3 + 0) * p.C);
+    const uint4 bq = *(const uint4*)(w + (ky * 3 + 1) * p.C);
+    const unsigned av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      wp[ky][2 * j] = __builtin_amdgcn_perm(bv[j], av[j], 0x05040100u);
+      wp[ky][2 * j + 1] = __builtin_amdgcn_perm(bv[j], av[j], 0x07060302u);
+    }
+    unpack8(*(const uint4*)(w + (ky * 3 + 2) * p.C), w2[ky]);
+  }
   float acc[R][8];
   {
     const float4 b0 = *(const float4*)(p.bias + c0);
@@ -56,18 +70,29 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(const DwParams p) {
   for (int ri = 0; ri < NIN; ++ri) {
     const int iy = iy0 + ri;
     if ((unsigned)iy >= (unsigned)p.H) continue;
+    const bf16* row = x + iy * p.W * p.xs;
+    // the three input pixels of this row (zero outside the image: padding)
+    const uint4 v0 = load16_or_zero(row + ix0 * p.xs, x, (unsigned)ix0 < (unsigned)p.W);
+    const uint4 v1 = load16_or_zero(row + (ix0 + 1) * p.xs, x, (unsigned)(ix0 + 1) < (unsigned)p.W);
+    const uint4 v2 = load16_or_zero(row + (ix0 + 2) * p.xs, x, (unsigned)(ix0 + 2) < (unsigned)p.W);
+    const unsigned a0[4] = {v0.x, v0.y, v0.z, v0.w}, a1[4] = {v1.x, v1.y, v1.z, v1.w};
+    unsigned pr[8];
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int ix = ix0 + kx;
-      if ((unsigned)ix >= (unsigned)p.W) continue;
-      float xv[8];
-      unpack8(*(const uint4*)(x + (iy * p.W + ix) * p.xs), xv);
+    for (int j = 0; j < 4; ++j) {
+      pr[2 * j] = __builtin_amdgcn_perm(a1[j], a0[j], 0x05040100u);
+      pr[2 * j + 1] = __builtin_amdgcn_perm(a1[j], a0[j], 0x07060302u);
+    }
+    float x2[8];
+    unpack8(v2, x2);
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int ky = ri - r * S;
-        if (ky < 0 || ky > 2) continue;  // compile-time after unrolling
+    for (int r = 0; r < R; ++r) {
+      const int ky = ri - r * S;
+      if (ky < 0 || ky > 2) continue;  // compile-time after unrolling
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[r][i] = fmaf(xv[i], wt[ky * 3 + kx][i], acc[r][i]);
+      for (int i = 0; i < 8; ++i) {
+        acc[r][i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, pr[i]),
+                                                    __builtin_bit_cast(bf16x2, wp[ky][i]), acc[r][i], false);
+        acc[r][i] = fmaf(x2[i], w2[ky][i], acc[r][i]);
       }
     }
   }
