@@ -30,6 +30,10 @@ __device__ __forceinline__ int swz(int row, int chunk) {
 
 __device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
 
+// i / d for small non-negative ints via a float reciprocal (1/d rounds up for every
+// divisor used here, and i * 1e-7 relative error stays far below 1/d for i < 2^20).
+__device__ __forceinline__ int fdiv(int i, float inv_d) { return (int)((float)i * inv_d); }
+
 template <int S, int TH, int TW, int MP, bool EXPAND>
 __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
@@ -69,6 +73,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   // registers one chunk ahead and written to the idle LDS buffer after the
   // current chunk's last read of it, so their global latency hides behind MFMA.
   uint4 rwp[WP_PER_T], rwe[WE_PER_T], rwd;
+  const float inv_cpr_w = 1.0f / (float)cpr;
   auto fetch = [&](int h0) {
 #pragma unroll
     for (int k = 0; k < WP_PER_T; ++k) {
@@ -79,7 +84,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
 #pragma unroll
       for (int k = 0; k < WE_PER_T; ++k) {
         const int i = tid + k * 256;
-        const int r = i / cpr, c = i - r * cpr;
+        const int r = fdiv(i, inv_cpr_w), c = i - r * cpr;
         rwe[k] = load16_or_zero(we + (size_t)(h0 + r) * p.inp_pad + c * 8, we, i < 32 * cpr);
       }
     }
@@ -100,7 +105,7 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
       for (int k = 0; k < WE_PER_T; ++k) {
         const int i = tid + k * 256;
         if (i < 32 * cpr) {
-          const int r = i / cpr, c = i - r * cpr;
+          const int r = fdiv(i, inv_cpr_w), c = i - r * cpr;
           *(uint4*)(wes + (c >> 2) * 32 * 64 + swz(r, c & 3)) = rwe[k];
         }
       }
@@ -140,8 +145,9 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
 
   // ---- input tile (with halo) -> LDS, zero outside the image / past inp
   fetch(0);
+  const float inv_cpr = 1.0f / (float)cpr;
   for (int i = tid; i < PIN_PAD * cpr; i += 256) {
-    const int pix = i / cpr, c = i - pix * cpr;
+    const int pix = fdiv(i, inv_cpr), c = i - pix * cpr;
     const int py = pix / PW, px = pix - py * PW;
     const int iy = iy0 + py, ix = ix0 + px;
     const bool ok = pix < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && c * 8 < p.inp;
@@ -156,6 +162,25 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
 #pragma unroll
     for (int m = 0; m < MP; ++m) acc[q][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Expand-epilogue row info is chunk-invariant: per owned N-tile, whether the
+  // pixel is inside the image (the depthwise zero-pads the EXPANDED map) and the
+  // swizzled LDS addresses of this lane's two 4-channel groups.
+  constexpr int NEW = (NE + 3) / 4;
+  bool e_inb[NEW];
+  int e_addr[NEW][2];
+#pragma unroll
+  for (int q = 0; q < NEW; ++q) {
+    const int pix = (wave + 4 * q) * 16 + row;
+    const int py = pix / PW, px = pix - py * PW;
+    const int iy = iy0 + py, ix = ix0 + px;
+    e_inb[q] = pix < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int hc = mt * 16 + kq * 4;
+      e_addr[q][mt] = swz(pix, hc >> 3) + (hc & 7) * 2;
+    }
+  }
+
   const int nchunks = p.hid_pad >> 5;
   __syncthreads();
   for (int h = 0; h < nchunks; ++h) {
@@ -167,7 +192,10 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
     if constexpr (EXPAND) {
       const uint8_t* wes = Wes + cur * we_buf;
       const float* be = p.be + h * 32;
-      for (int j = wave; j < NE; j += 4) {
+#pragma unroll
+      for (int q = 0; q < NEW; ++q) {
+        const int j = wave + 4 * q;
+        if (j >= NE) break;
         f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
         for (int sl = 0; sl < nslab; ++sl) {
           const bf16x8 bv = *(const bf16x8*)(Xs + sl * PIN_PAD * 64 + swz(j * 16 + row, kq));
@@ -176,18 +204,14 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
           e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bv, e0, 0, 0, 0);
           e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bv, e1, 0, 0, 0);
         }
-        const int pix = j * 16 + row;
-        const int py = pix / PW, px = pix - py * PW;
-        const int iy = iy0 + py, ix = ix0 + px;
-        const bool inb = pix < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
           const int hc = mt * 16 + kq * 4;
           const float4 bb = *(const float4*)(be + hc);
           const f32x4 e = mt ? e1 : e0;
           float v[4] = {relu6(e[0] + bb.x), relu6(e[1] + bb.y), relu6(e[2] + bb.z), relu6(e[3] + bb.w)};
-          if (!inb) v[0] = v[1] = v[2] = v[3] = 0.f;
-          *(uint2*)(Es + swz(pix, hc >> 3) + (hc & 7) * 2) = pack4(v);
+          if (!e_inb[q]) v[0] = v[1] = v[2] = v[3] = 0.f;
+          *(uint2*)(Es + e_addr[q][mt]) = pack4(v);
         }
       }
       __syncthreads();
