@@ -19,6 +19,8 @@
 // XOR-swizzled with g[(row>>2)&3], g = {0,2,3,1}: for the 16x16x32 operand
 // read (lane l: row l&15, chunk l>>4) every ds_read_b128 lane group
 // ({0-3,12-15,20-27}, ...) then touches 16 distinct 16-byte bank slots.
+#include <cstdlib>
+
 #include "common.h"
 #include "launch.h"
 
@@ -362,7 +364,16 @@ static void ir_set_attr() {
   X(1, 7, 7, 10, true)                                               \
   X(1, 7, 7, 20, true)
 
+void ir_wave_prepare();
+bool ir_block_wave(const IrParams& p, int tile, hipStream_t s);
+static bool g_ir_wave = [] {
+  const char* e = std::getenv("ARENA_IR_WAVE");
+  return e ? std::atoi(e) != 0 : true;
+}();
+void set_ir_wave(bool v) { g_ir_wave = v; }
+
 void ir_prepare() {
+  ir_wave_prepare();
 #define X(S, TH, TW, MP, E) ir_set_attr<S, TH, TW, MP, E>();
   ARENA_IR_CONFIGS(X)
 #undef X
@@ -380,6 +391,7 @@ void ir_block(const IrParams& p, hipStream_t s) {
   if (p.Ho != (p.H + 2 - 3) / p.stride + 1 || p.Wo != (p.W + 2 - 3) / p.stride + 1)
     throw std::runtime_error("ir_block: output size mismatch");
   const int T = ir_tile(p.Ho);
+  if (g_ir_wave && ir_block_wave(p, T, s)) return;
   const int MP = p.oup_pad / 16;
   const bool E = p.expand != 0;
 #define X(S_, TH_, TW_, MP_, E_)                                                     \

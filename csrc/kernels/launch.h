@@ -84,6 +84,7 @@ struct IrParams {
 };
 void ir_block(const IrParams& p, hipStream_t s);
 void ir_prepare();
+void set_ir_wave(bool v);  // ARENA_IR_WAVE=0: stride-1 blocks use the block-cooperative kernel
 
 // ---------------------------------------------------------------- SPPF pools (K5)
 // x: [B,H,W] channels [0,C) of a buffer with pixel stride xs; writes the

@@ -354,3 +354,25 @@ def test_conv3x3_v3_cin16(device, H, s):
         C.set_conv_pw(True)
         C.set_conv_impl(old)
     _check(_nchw(y.cpu()), _ref_conv(xn.cpu(), w, b, s, 1, "silu"))
+
+
+@pytest.mark.parametrize("H,inp,hid,oup,res", [(112, 32, 32, 16, False), (56, 24, 144, 24, True),
+                                               (28, 32, 192, 32, True), (14, 64, 384, 64, True),
+                                               (20, 24, 144, 24, True)])
+def test_ir_wave_matches_block_kernel(device, H, inp, hid, oup, res):
+    """Wave-per-tile stride-1 IR kernel == block-cooperative kernel (same math)."""
+    C = native()
+    g = torch.Generator().manual_seed(H + hid)
+    x = (torch.rand(2, inp, H, H, generator=g) * 2).to(torch.bfloat16)
+    expand = None if hid == inp else (torch.randn(hid, inp, 1, 1, generator=g) / np.sqrt(inp),
+                                      torch.randn(hid, generator=g) * 0.1)
+    dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
+    project = (torch.randn(oup, hid, 1, 1, generator=g) / np.sqrt(hid), torch.randn(oup, generator=g) * 0.1)
+    xn = _nhwc(x).to(device)
+    yw = AF.ir_block_nhwc(xn, expand, dw, project, stride=1, res=res)
+    C.set_ir_wave(False)
+    try:
+        yb = AF.ir_block_nhwc(xn, expand, dw, project, stride=1, res=res)
+    finally:
+        C.set_ir_wave(True)
+    assert (yw.float() - yb.float()).abs().max().item() <= 0.07

@@ -32,6 +32,7 @@ SOURCES = [
     "kernels/conv_mfma.hip",
     "kernels/dwconv.hip",
     "kernels/ir_block.hip",
+    "kernels/ir_block_wave.hip",
     "kernels/conv_igemm.hip",
     "kernels/conv_pw.hip",
     "kernels/conv3x3_v3.hip",
