@@ -62,12 +62,12 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
   wave_lds_sync();
 
   // chunk-invariant: which expand rows (halo pixels) are inside the image
-  bool e_inb[NE];
+  unsigned e_inb = 0;  // bit j: halo pixel j*16+row inside the image
 #pragma unroll
   for (int j = 0; j < NE; ++j) {
     const int pix = j * 16 + row;
     const int py = pix / PW, px = pix - py * PW;
-    e_inb[j] = pix < PIN && (unsigned)(iy0 + py) < (unsigned)p.H && (unsigned)(ix0 + px) < (unsigned)p.W;
+    if (pix < PIN && (unsigned)(iy0 + py) < (unsigned)p.H && (unsigned)(ix0 + px) < (unsigned)p.W) e_inb |= 1u << j;
   }
 
   f32x4 acc[NP][MP];
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
       }
       const float4 be0 = *(const float4*)(p.be + h0 + kq * 4);
       const float4 be1 = *(const float4*)(p.be + h0 + 16 + kq * 4);
-#pragma unroll
+#pragma unroll 2
       for (int j = 0; j < NE; ++j) {
         f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
         const int pix = j * 16 + row;
         float v0[4] = {relu6w(e0[0] + be0.x), relu6w(e0[1] + be0.y), relu6w(e0[2] + be0.z), relu6w(e0[3] + be0.w)};
         float v1[4] = {relu6w(e1[0] + be1.x), relu6w(e1[1] + be1.y), relu6w(e1[2] + be1.z), relu6w(e1[3] + be1.w)};
-        if (!e_inb[j]) {
+        if (!((e_inb >> j) & 1u)) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) v0[k] = v1[k] = 0.f;
         }
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
     }
 
     // depthwise: this lane handles pixels q = (lane >> 2) + 16 k, channel group dc
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < POUT_PAD / 16; ++k) {
       const int q = (lane >> 2) + 16 * k;
       uint4 outv = {0u, 0u, 0u, 0u};
@@ -232,11 +232,11 @@ static void irw_launch(const IrParams& p, hipStream_t s) {
                      p);
 }
 
+// Measured (profiles/r1_irwave_ops.md): the wave kernel wins on the 56x56 and 28x28
+// expand blocks; block 1 (no expand) and the 14x14 blocks stay block-cooperative.
 #define ARENA_IRW_CONFIGS(X) \
-  X(8, 8, 1, 1, false)       \
   X(8, 8, 2, 1, true)        \
-  X(7, 7, 2, 1, true)        \
-  X(7, 7, 4, 2, true)
+  X(7, 7, 2, 1, true)
 
 void ir_wave_prepare() {
 #define X(TH, TW, MP, NS, E)                                                                          \
