@@ -31,6 +31,10 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
   constexpr int NE = PIN_PAD / 16, NP = POUT_PAD / 16;
   constexpr int XB = NS * PIN_PAD * 64, EB = EXPAND ? PIN_PAD * 64 : 0, DB = POUT_PAD * 64;
   constexpr int WAVE_BYTES = XB + EB + DB;
+  // unroll depth per shape (measured: full unroll is best for 7x7 tiles; the 8x8 tile
+  // needs the lighter unroll to stay at 2 waves/SIMD without AGPR spills)
+  constexpr int E_UNROLL = TH == 8 ? 2 : NE;
+  constexpr int D_UNROLL = TH == 8 ? 1 : POUT_PAD / 16;
   extern __shared__ __align__(16) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int row = lane & 15, kq = lane >> 4;
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
       }
       const float4 be0 = *(const float4*)(p.be + h0 + kq * 4);
       const float4 be1 = *(const float4*)(p.be + h0 + 16 + kq * 4);
-#pragma unroll 2
+#pragma unroll E_UNROLL
       for (int j = 0; j < NE; ++j) {
         f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
     }
 
     // depthwise: this lane handles pixels q = (lane >> 2) + 16 k, channel group dc
-#pragma unroll 1
+#pragma unroll D_UNROLL
     for (int k = 0; k < POUT_PAD / 16; ++k) {
       const int q = (lane >> 2) + 16 * k;
       uint4 outv = {0u, 0u, 0u, 0u};
