@@ -30,9 +30,12 @@ __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
 // the bf16 rounding of every stored activation.
 __device__ __forceinline__ float silu(float v) { return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v)); }
 
+// ReLU6 as one v_med3_f32
+__device__ __forceinline__ float relu6f(float v) { return __builtin_amdgcn_fmed3f(v, 0.0f, 6.0f); }
+
 __device__ __forceinline__ float apply_act(float v, int act) {
   if (act == ACT_SILU) return silu(v);
-  if (act == ACT_RELU6) return fminf(fmaxf(v, 0.0f), 6.0f);
+  if (act == ACT_RELU6) return relu6f(v);
   return v;
 }
 

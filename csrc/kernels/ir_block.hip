@@ -30,7 +30,7 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   return row * 64 + ((chunk ^ ((0x78 >> (((row >> 2) & 3) * 2)) & 3)) << 4);
 }
 
-__device__ __forceinline__ float relu6(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
+__device__ __forceinline__ float relu6(float v) { return relu6f(v); }
 
 // i / d for small non-negative ints via a float reciprocal (1/d rounds up for every
 // divisor used here, and i * 1e-7 relative error stays far below 1/d for i < 2^20).
@@ -198,7 +198,9 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
       for (int q = 0; q < NEW; ++q) {
         const int j = wave + 4 * q;
         if (j >= NE) break;
-        f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
+        const float4 bq0 = *(const float4*)(be + kq * 4);
+        const float4 bq1 = *(const float4*)(be + 16 + kq * 4);
+        f32x4 e0 = {bq0.x, bq0.y, bq0.z, bq0.w}, e1 = {bq1.x, bq1.y, bq1.z, bq1.w};  // bias folded into init
         for (int sl = 0; sl < nslab; ++sl) {
           const bf16x8 bv = *(const bf16x8*)(Xs + sl * PIN_PAD * 64 + swz(j * 16 + row, kq));
           const bf16x8 a0 = *(const bf16x8*)(wes + sl * 32 * 64 + swz(row, kq));
@@ -209,9 +211,8 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
           const int hc = mt * 16 + kq * 4;
-          const float4 bb = *(const float4*)(be + hc);
           const f32x4 e = mt ? e1 : e0;
-          float v[4] = {relu6(e[0] + bb.x), relu6(e[1] + bb.y), relu6(e[2] + bb.z), relu6(e[3] + bb.w)};
+          float v[4] = {relu6(e[0]), relu6(e[1]), relu6(e[2]), relu6(e[3])};
           if (!e_inb[q]) v[0] = v[1] = v[2] = v[3] = 0.f;
           *(uint2*)(Es + e_addr[q][mt]) = pack4(v);
         }

@@ -17,7 +17,7 @@ namespace arena {
 __device__ __forceinline__ int wswz(int row, int chunk) {
   return row * 64 + ((chunk ^ ((0x78 >> (((row >> 2) & 3) * 2)) & 3)) << 4);
 }
-__device__ __forceinline__ float relu6w(float v) { return fminf(fmaxf(v, 0.f), 6.f); }
+__device__ __forceinline__ float relu6w(float v) { return relu6f(v); }
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes have completed
   __builtin_amdgcn_wave_barrier();
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
       const float4 be1 = *(const float4*)(p.be + h0 + 16 + kq * 4);
 #pragma unroll E_UNROLL
       for (int j = 0; j < NE; ++j) {
-        f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
+        f32x4 e0 = {be0.x, be0.y, be0.z, be0.w}, e1 = {be1.x, be1.y, be1.z, be1.w};  // bias folded into init
 #pragma unroll
         for (int sl = 0; sl < NS; ++sl) {
           const bf16x8 bv = *(const bf16x8*)(Xs + sl * PIN_PAD * 64 + wswz(j * 16 + row, kq));
@@ -133,8 +133,8 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
           e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[sl], bv, e1, 0, 0, 0);
         }
         const int pix = j * 16 + row;
-        float v0[4] = {relu6w(e0[0] + be0.x), relu6w(e0[1] + be0.y), relu6w(e0[2] + be0.z), relu6w(e0[3] + be0.w)};
-        float v1[4] = {relu6w(e1[0] + be1.x), relu6w(e1[1] + be1.y), relu6w(e1[2] + be1.z), relu6w(e1[3] + be1.w)};
+        float v0[4] = {relu6w(e0[0]), relu6w(e0[1]), relu6w(e0[2]), relu6w(e0[3])};
+        float v1[4] = {relu6w(e1[0]), relu6w(e1[1]), relu6w(e1[2]), relu6w(e1[3])};
         if (!((e_inb >> j) & 1u)) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) v0[k] = v1[k] = 0.f;
