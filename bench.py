@@ -14,7 +14,11 @@ environment).  Each rank:
     batch of ``--batch`` requests through the full device pipeline (host
     staging copy of the decoded RGB images, H2D, letterbox, 75 detector convs,
     decode, NMS, crop gather, 52 classifier layers, top-5, D2H, per-request
-    result split); two batches are kept in flight as in the model server.
+    result split).  As in the model server's instance loop, up to one batch
+    per executor staging slot is in flight; every slot runs its hipGraph on
+    its own stream and activation arena, so consecutive batches overlap on
+    the device (the small 20x20 / 7x7 layers of one batch leave CUs free for
+    the other) while the next batch's H2D copy streams in.
 Rank 0 prints one JSON line; ``value`` is total requests/s over all ranks
 (time = max over ranks), latencies are per-batch completion latencies.
 """
@@ -111,12 +115,14 @@ def main(argv=None) -> int:
         s = (off + step * B) % n
         return [images[(s + i) % n] for i in range(B)]
 
+    depth = pipe.ex.num_slots()  # batches in flight, as the model server's instance loop keeps them
+
     def run(steps, lat, crops):
         q = deque()
         for st in range(steps):
             imgs = batch_at(st)
             q.append((pipe.submit(imgs), time.perf_counter()))
-            if len(q) == 2:
+            if len(q) == depth:
                 slot, ts = q.popleft()
                 res = pipe.collect(slot, B)
                 lat.append(time.perf_counter() - ts)

@@ -396,6 +396,7 @@ PYBIND11_MODULE(_C, m) {
              py::gil_scoped_release nogil;
              e.replay(B, slot, iters);
            })
+      .def("num_slots", &Executor::num_slots)
       .def("synchronize",
            [](Executor& e) {
              py::gil_scoped_release nogil;

@@ -150,7 +150,7 @@ void DynamicBatcher::instance_loop(int idx) {
   };
   std::deque<InFlight> pending;
   for (;;) {
-    if (pending.size() < 2) {
+    if ((int)pending.size() < ex.num_slots()) {
       Batch b;
       if (take_batch(b, pending.empty())) {
         std::vector<InputImage> imgs;

@@ -32,8 +32,6 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
   if (cfg_.cand_cap > 16384) throw std::runtime_error("Executor: cand_cap > 16384");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   prepare_kernels();
-  ARENA_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
-  ARENA_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
   max_B_ = cfg_.max_batch;
   {
     const char* e = std::getenv("ARENA_DEBUG_SYNC");
@@ -42,6 +40,18 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
     autotune_ = at != nullptr ? std::atoi(at) : 1;
     const char* c = std::getenv("ARENA_COPY_MODE");
     copy_mode_ = c != nullptr ? std::atoi(c) : 0;
+    const char* cc = std::getenv("ARENA_CONCURRENT");
+    concurrent_ = cc != nullptr ? std::atoi(cc) : 1;
+    if (debug_sync_) concurrent_ = 0;
+    const char* ns = std::getenv("ARENA_SLOTS");
+    n_slots_ = concurrent_ ? std::min(kMaxSlots, std::max(2, ns != nullptr ? std::atoi(ns) : 3)) : 2;
+  }
+  ARENA_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+  ARENA_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  for (int s = 0; s < n_slots_; ++s) {
+    slots_[s].idx = s;
+    if (s == 0 || !concurrent_) slots_[s].stream = compute_;
+    else ARENA_HIP_CHECK(hipStreamCreateWithFlags(&slots_[s].stream, hipStreamNonBlocking));
   }
   alloc_slots();
   const int nthreads = std::max(1, cfg_.host_threads);
@@ -79,14 +89,18 @@ Executor::~Executor() {
   pool_cv_.notify_all();
   for (auto& t : workers_) t.join();
   hipSetDevice(cfg_.device);
-  if (compute_) hipStreamSynchronize(compute_);
+  for (int s = 0; s < n_slots_; ++s)
+    if (slots_[s].stream) hipStreamSynchronize(slots_[s].stream);
   if (copy_) hipStreamSynchronize(copy_);
   for (auto& kv : buckets_) {
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < n_slots_; ++s)
       if (kv.second.graph[s]) hipGraphExecDestroy(kv.second.graph[s]);
-    if (kv.second.d_arena) hipFree(kv.second.d_arena);
+    free_arenas(kv.second);
   }
-  for (auto& sl : slots_) {
+  for (int s = 1; s < n_slots_; ++s)
+    if (slots_[s].stream && slots_[s].stream != compute_) hipStreamDestroy(slots_[s].stream);
+  for (int s = 0; s < n_slots_; ++s) {
+    Slot& sl = slots_[s];
     if (sl.d_in) hipFree(sl.d_in);
     if (sl.d_out) hipFree(sl.d_out);
     if (sl.h_in) hipHostFree(sl.h_in);
@@ -116,8 +130,23 @@ size_t Executor::out_off_raw() const {
 }
 size_t Executor::out_bytes_total() const { return out_off_raw() + (size_t)cfg_.raw_out_bytes * max_B_; }
 
+void Executor::sync_slots() {
+  for (int s = 0; s < n_slots_; ++s) ARENA_HIP_CHECK(hipStreamSynchronize(slots_[s].stream));
+}
+
+void Executor::free_arenas(Bucket& bk) {
+  for (int s = 0; s < n_slots_; ++s) {
+    if (bk.d_arena[s] == nullptr) continue;
+    bool first = true;  // free each distinct allocation once (aliased when not concurrent)
+    for (int t = 0; t < s; ++t) first &= bk.d_arena[t] != bk.d_arena[s];
+    if (first) hipFree(bk.d_arena[s]);
+  }
+  for (int s = 0; s < kMaxSlots; ++s) bk.d_arena[s] = nullptr;
+}
+
 void Executor::alloc_slots() {
-  for (auto& sl : slots_) {
+  for (int s = 0; s < n_slots_; ++s) {
+    Slot& sl = slots_[s];
     ARENA_HIP_CHECK(hipMalloc(&sl.d_in, in_bytes_total()));
     ARENA_HIP_CHECK(hipMalloc(&sl.d_out, out_bytes_total()));
     ARENA_HIP_CHECK(hipHostMalloc(&sl.h_in, in_bytes_total(), hipHostMallocDefault));
@@ -140,7 +169,7 @@ void Executor::set_weights(const void* host, size_t bytes) {
     d_weights_ = nullptr;
   }
   if (d_weights_ == nullptr) ARENA_HIP_CHECK(hipMalloc(&d_weights_, bytes));
-  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+  sync_slots();
   ARENA_HIP_CHECK(hipMemcpy(d_weights_, host, bytes, hipMemcpyHostToDevice));
   weights_bytes_ = bytes;
 }
@@ -170,7 +199,7 @@ std::vector<int> Executor::buckets() const {
 
 uintptr_t Executor::arena_ptr(int B) const {
   auto it = buckets_.find(B);
-  return it == buckets_.end() ? 0 : (uintptr_t)it->second.d_arena;
+  return it == buckets_.end() ? 0 : (uintptr_t)it->second.d_arena[0];
 }
 
 void Executor::read_arena(int B, int64_t offset, void* dst, size_t bytes) {
@@ -179,8 +208,8 @@ void Executor::read_arena(int B, int64_t offset, void* dst, size_t bytes) {
   if (offset < 0 || offset + (int64_t)bytes > it->second.info.arena_bytes)
     throw std::runtime_error("read_arena: range outside the arena");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
-  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
-  ARENA_HIP_CHECK(hipMemcpy(dst, it->second.d_arena + offset, bytes, hipMemcpyDeviceToHost));
+  sync_slots();
+  ARENA_HIP_CHECK(hipMemcpy(dst, it->second.d_arena[it->second.last_slot] + offset, bytes, hipMemcpyDeviceToHost));
 }
 
 void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes) {
@@ -193,16 +222,24 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
   bk.info.crop_cap = crop_cap_for(B);
   bk.info.offsets.assign(offsets, offsets + n_buffers);
   bk.info.arena_bytes = arena_bytes;
-  if (bk.d_arena) ARENA_HIP_CHECK(hipFree(bk.d_arena));
-  ARENA_HIP_CHECK(hipMalloc(&bk.d_arena, std::max<int64_t>(arena_bytes, 256)));
-  ARENA_HIP_CHECK(hipMemset(bk.d_arena, 0, std::max<int64_t>(arena_bytes, 256)));
+  sync_slots();
+  free_arenas(bk);
+  const size_t abytes = (size_t)std::max<int64_t>(arena_bytes, 256);
+  for (int s = 0; s < n_slots_; ++s) {
+    if (s > 0 && !concurrent_) {
+      bk.d_arena[s] = bk.d_arena[0];
+      continue;
+    }
+    ARENA_HIP_CHECK(hipMalloc(&bk.d_arena[s], abytes));
+    ARENA_HIP_CHECK(hipMemset(bk.d_arena[s], 0, abytes));
+  }
   bk.impl.assign(prog_.size(), 0);
   if (autotune_) autotune(bk);
-  for (int s = 0; s < 2; ++s) capture(bk, s);
+  for (int s = 0; s < n_slots_; ++s) capture(bk, s);
   if (debug_sync_ || std::getenv("ARENA_DEBUG_ALLOC")) {
-    fprintf(stderr, "[arena alloc] bucket %d arena %p..%p (%lld B)\n", B, (void*)bk.d_arena,
-            (void*)(bk.d_arena + arena_bytes), (long long)arena_bytes);
-    for (int s = 0; s < 2; ++s)
+    fprintf(stderr, "[arena alloc] bucket %d arena %p..%p (%lld B)\n", B, (void*)bk.d_arena[0],
+            (void*)(bk.d_arena[0] + arena_bytes), (long long)arena_bytes);
+    for (int s = 0; s < n_slots_; ++s)
       fprintf(stderr, "[arena alloc] slot %d in %p..%p out %p..%p\n", s, (void*)slots_[s].d_in,
               (void*)(slots_[s].d_in + in_bytes_total()), (void*)slots_[s].d_out,
               (void*)(slots_[s].d_out + out_bytes_total()));
@@ -251,26 +288,27 @@ void Executor::autotune(Bucket& bk) {
   }
   ARENA_HIP_CHECK(hipEventDestroy(e0));
   ARENA_HIP_CHECK(hipEventDestroy(e1));
-  ARENA_HIP_CHECK(hipMemset(bk.d_arena, 0, std::max<int64_t>(bk.info.arena_bytes, 256)));
+  ARENA_HIP_CHECK(hipMemset(bk.d_arena[0], 0, std::max<int64_t>(bk.info.arena_bytes, 256)));
 }
 
 void Executor::capture(Bucket& bk, int s) {
   Slot& sl = slots_[s];
+  hipStream_t st = sl.stream;
   // Validate the program eagerly once (launch errors surface here, not in the graph).
-  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+  ARENA_HIP_CHECK(hipStreamSynchronize(st));
   hipGraph_t g = nullptr;
-  ARENA_HIP_CHECK(hipStreamBeginCapture(compute_, hipStreamCaptureModeThreadLocal));
+  ARENA_HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
   try {
     // The result D2H copy is issued after the graph launch, not captured: a
     // captured device->pinned-host memcpy node faulted on ROCm 7.0 (torch's
     // runtime) while the same graph without it runs cleanly.
-    enqueue_program(prog_, bk, sl, compute_);
+    enqueue_program(prog_, bk, sl, st);
   } catch (...) {
-    hipStreamEndCapture(compute_, &g);
+    hipStreamEndCapture(st, &g);
     if (g) hipGraphDestroy(g);
     throw;
   }
-  ARENA_HIP_CHECK(hipStreamEndCapture(compute_, &g));
+  ARENA_HIP_CHECK(hipStreamEndCapture(st, &g));
   if (bk.graph[s]) ARENA_HIP_CHECK(hipGraphExecDestroy(bk.graph[s]));
   ARENA_HIP_CHECK(hipGraphInstantiate(&bk.graph[s], g, nullptr, nullptr, 0));
   ARENA_HIP_CHECK(hipGraphDestroy(g));
@@ -290,7 +328,7 @@ uint8_t* Executor::resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff, int 
     default:
       if (buf < 0 || buf >= (int64_t)bk.info.offsets.size())
         throw std::runtime_error("program references unknown buffer " + std::to_string(buf));
-      base = bk.d_arena + bk.info.offsets[buf];
+      base = bk.d_arena[sl.idx] + bk.info.offsets[buf];
   }
   return base + coff * eb;
 }
@@ -570,10 +608,10 @@ int Executor::pick_bucket(int n) const {
 void Executor::enqueue_results_d2h(Bucket& bk, Slot& sl, int n) {
   size_t d2h = out_off_topk();
   if (has_topk_) d2h += sizeof(TopkResult) * (size_t)bk.info.crop_cap;
-  ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, compute_));
+  ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, sl.stream));
   if (has_raw_)
     ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out + out_off_raw(), sl.d_out + out_off_raw(), (size_t)cfg_.raw_out_bytes * n,
-                                   hipMemcpyDeviceToHost, compute_));
+                                   hipMemcpyDeviceToHost, sl.stream));
 }
 
 int Executor::submit(const std::vector<InputImage>& imgs) {
@@ -584,7 +622,7 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   if (B < 0) throw std::runtime_error("submit: batch larger than the largest bucket");
   const int s = next_slot_;
   Slot& sl = slots_[s];
-  if (sl.busy) throw std::runtime_error("submit: both staging slots in flight; collect() first");
+  if (sl.busy) throw std::runtime_error("submit: every staging slot is in flight; collect() first");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   // The slot's previous graph has been collected; its input copy was consumed.
   ImageMeta* meta = (ImageMeta*)(sl.h_in + kCtrlBytes);
@@ -625,14 +663,14 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   ctrl->crop_base = 0;
   const size_t bytes = in_bytes_meta() + off;
   if (copy_mode_ == 2) {
-    ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, compute_));
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, sl.stream));
   } else {
     ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, copy_));
     ARENA_HIP_CHECK(hipEventRecord(sl.copied, copy_));
     if (copy_mode_ == 1) ARENA_HIP_CHECK(hipEventSynchronize(sl.copied));
-    ARENA_HIP_CHECK(hipStreamWaitEvent(compute_, sl.copied, 0));
+    ARENA_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.copied, 0));
   }
-  ARENA_HIP_CHECK(hipEventRecord(sl.started, compute_));
+  ARENA_HIP_CHECK(hipEventRecord(sl.started, sl.stream));
   if (debug_sync_ >= 3) {
     // 3: whole program as one graph without the D2H node, D2H issued eagerly after it.
     // 4: whole program graph including the D2H node, built fresh.
@@ -680,19 +718,20 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     enqueue_results_d2h(bk, sl, n);
   } else {
     Bucket& bk = buckets_.at(B);
-    ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], compute_));
+    ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], sl.stream));
     enqueue_results_d2h(bk, sl, n);
   }
-  ARENA_HIP_CHECK(hipEventRecord(sl.done, compute_));
+  buckets_.at(B).last_slot = s;
+  ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
   sl.busy = true;
   sl.bucket = B;
   sl.n_images = n;
-  next_slot_ ^= 1;
+  next_slot_ = (next_slot_ + 1) % n_slots_;
   return s;
 }
 
 BatchResult Executor::collect(int s) {
-  if (s < 0 || s > 1) throw std::runtime_error("collect: bad slot");
+  if (s < 0 || s >= n_slots_) throw std::runtime_error("collect: bad slot");
   Slot& sl = slots_[s];
   if (!sl.busy) throw std::runtime_error("collect: slot not in flight");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
@@ -730,15 +769,15 @@ BatchResult Executor::collect(int s) {
       c.total_crops = total;
       c.n_crops = std::min(CC, total - base);
       // previous pass must have consumed the control block before it is rewritten
-      ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+      ARENA_HIP_CHECK(hipStreamSynchronize(sl.stream));
       ARENA_HIP_CHECK(hipMemcpy(sl.d_in, &c, sizeof(Ctrl), hipMemcpyHostToDevice));
-      enqueue_program(cls_prog_, bk, sl, compute_, (int)(prog_.size() - cls_prog_.size()));
+      enqueue_program(cls_prog_, bk, sl, sl.stream, (int)(prog_.size() - cls_prog_.size()));
     }
     uint8_t* src = sl.d_out + out_off_topk() + sizeof(TopkResult) * (size_t)CC;
     uint8_t* dst = sl.h_out + out_off_topk() + sizeof(TopkResult) * (size_t)CC;
     ARENA_HIP_CHECK(hipMemcpyAsync(dst, src, sizeof(TopkResult) * (size_t)(total - CC), hipMemcpyDeviceToHost,
-                                   compute_));
-    ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+                                   sl.stream));
+    ARENA_HIP_CHECK(hipStreamSynchronize(sl.stream));
   }
   const TopkResult* tk = (const TopkResult*)(sl.h_out + out_off_topk());
   res.topk.assign(tk, tk + total);
@@ -752,13 +791,14 @@ void Executor::replay(int B, int s, int iters) {
   auto it = buckets_.find(B);
   if (it == buckets_.end()) throw std::runtime_error("replay: unknown bucket");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
-  for (int i = 0; i < iters; ++i) ARENA_HIP_CHECK(hipGraphLaunch(it->second.graph[s], compute_));
+  if (s < 0 || s >= n_slots_) throw std::runtime_error("replay: bad slot");
+  for (int i = 0; i < iters; ++i) ARENA_HIP_CHECK(hipGraphLaunch(it->second.graph[s], slots_[s].stream));
 }
 
 void Executor::synchronize() {
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   ARENA_HIP_CHECK(hipStreamSynchronize(copy_));
-  ARENA_HIP_CHECK(hipStreamSynchronize(compute_));
+  sync_slots();
 }
 
 }  // namespace arena

@@ -15,8 +15,10 @@
 // name arena buffers by id.  For every batch bucket the executor resolves the
 // records to device pointers once and captures the whole sequence (including
 // memsets and the result D2H copy) into a hipGraph; a request batch is then
-// one H2D copy on a copy stream + one graph launch on the compute stream.
-// Two staging slots ping-pong so batch i+1 is uploaded while batch i runs.
+// one H2D copy on a copy stream + one graph launch on the slot's stream.
+// Two staging slots ping-pong so batch i+1 is uploaded while batch i runs;
+// each slot owns a stream and an activation arena, so the two batches'
+// graphs also execute concurrently on the device.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -35,6 +37,7 @@
 namespace arena {
 
 constexpr int kOpFields = 48;
+constexpr int kMaxSlots = 4;
 using OpRecord = std::array<int64_t, kOpFields>;
 
 enum OpType : int64_t {
@@ -136,6 +139,8 @@ class Executor {
   // microbenchmarks to separate host packing from device time.
   void replay(int B, int slot, int iters);
   void synchronize();
+  // Staging slots = batches that may be in flight at once (submit() throws when all are busy).
+  int num_slots() const { return n_slots_; }
 
   // Device pointers for tests / introspection.
   uintptr_t arena_ptr(int B) const;
@@ -153,18 +158,27 @@ class Executor {
     uint8_t* h_in = nullptr;
     uint8_t* h_out = nullptr;
     hipEvent_t copied = nullptr, started = nullptr, done = nullptr;
+    // Each slot runs its graph on its own stream against its own activation
+    // arena, so two in-flight batches overlap on the device: the small-grid
+    // tail of one batch's layers (20x20 / 7x7 maps leave most of the 256 CUs
+    // idle) is filled by the other batch's work.
+    hipStream_t stream = nullptr;
+    int idx = 0;
     bool busy = false;
     int bucket = 0;
     int n_images = 0;
   };
   struct Bucket {
     BucketInfo info;
-    uint8_t* d_arena = nullptr;
-    hipGraphExec_t graph[2] = {nullptr, nullptr};
+    uint8_t* d_arena[kMaxSlots] = {};  // per slot (all aliased when concurrency is off)
+    int last_slot = 0;                 // slot whose arena read_arena() inspects
+    hipGraphExec_t graph[kMaxSlots] = {};
     std::vector<int8_t> impl;  // per op of prog_: conv kernel family chosen by autotune (0 = default)
   };
 
   void alloc_slots();
+  void sync_slots();
+  void free_arenas(Bucket& bk);
   void capture(Bucket& bk, int slot);
   void enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s,
                        int op_offset = 0, int force_impl = 0);
@@ -197,10 +211,14 @@ class Executor {
   size_t weights_bytes_ = 0;
   std::vector<OpRecord> prog_, cls_prog_;
   std::map<int, Bucket> buckets_;
-  Slot slots_[2];
+  Slot slots_[kMaxSlots];
+  int n_slots_ = 2;
   int next_slot_ = 0;
   bool has_topk_ = false, has_det_ = false, has_raw_ = false;
   int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on compute stream
+  // ARENA_CONCURRENT: 1 = per-slot streams + arenas (in-flight batches overlap on the device),
+  // 0 = two slots serialised on one stream sharing one arena.  ARENA_SLOTS: slots when concurrent (2-3).
+  int concurrent_ = 1;
   int autotune_ = 1;  // ARENA_AUTOTUNE: 0 off, 1 on, 2 on + report
   int debug_sync_ = 0;  // ARENA_DEBUG_SYNC: 1 eager op-by-op, 2 one graph per op
   std::mutex mu_;
