@@ -9,7 +9,9 @@ in-band in ``error``; ``ClassifyBatch`` loops over ``Classify``).
 MI355X design: every RPC only decodes (thread pool) and enqueues its crop
 into the GPU classifier's dynamic batcher, so crops of concurrent requests —
 and all crops of one ``ClassifyBatch`` — run as one batched MobileNetV2 graph
-replay.  ``Health/Check`` is implemented (declared only upstream).
+replay.  ``Health/Check`` is implemented (declared only upstream), and with
+``ARENA_INFER_SERVICE=1`` so is ``InferenceService/Infer`` (also declared
+only upstream; see server/inference_service.py).
 
 Run: ``python -m inference_arena_amd.server.classification_service``.
 """
@@ -43,6 +45,7 @@ class ClassificationServicer:
         self.pool = ThreadPoolExecutor(max_workers=max(1, decode_threads), thread_name_prefix="crop-decode")
         self.n_requests = 0
         self.n_errors = 0
+        self.infer = None  # InferenceServicer when the server also serves InferenceService
 
     def _name(self, cid: int) -> str:
         return self.labels[cid] if 0 <= cid < len(self.labels) else ""
@@ -83,6 +86,9 @@ class ClassificationServicer:
 
     def close(self) -> None:
         self.pool.shutdown(wait=False)
+        if self.infer is not None:
+            self.infer.backend.close()
+            self.infer.close()
 
 
 class HealthServicer:
@@ -93,14 +99,27 @@ class HealthServicer:
         return pb.HealthCheckResponse(status=pb.SERVING if self.ready() else pb.NOT_SERVING)
 
 
-async def start_server(settings: Settings, backend: ClassifierBackend | None = None, port: int | None = None):
-    """Create and start the aio server; returns (server, servicer, bound_port)."""
+async def start_server(settings: Settings, backend: ClassifierBackend | None = None, port: int | None = None,
+                       pipeline_backend=None):
+    """Create and start the aio server; returns (server, servicer, bound_port).
+
+    With ``pipeline_backend`` (or ``ARENA_INFER_SERVICE=1``, which builds one) the same
+    server also answers ``inference.InferenceService/Infer`` (server/inference_service.py)."""
     backend = backend or build_classifier_backend(settings)
-    servicer = ClassificationServicer(backend, load_labels(settings.LABELS_FILE or None),
-                                      settings.ARENA_DECODE_THREADS)
+    labels = load_labels(settings.LABELS_FILE or None)
+    servicer = ClassificationServicer(backend, labels, settings.ARENA_DECODE_THREADS)
+    handlers = [pb.ClassificationService.handler(servicer), pb.Health.handler(HealthServicer())]
+    if pipeline_backend is None and int(settings.ARENA_INFER_SERVICE):
+        from .inference_service import build_pipeline_backend
+
+        pipeline_backend = build_pipeline_backend(settings)
+    if pipeline_backend is not None:
+        from .inference_service import InferenceServicer
+
+        servicer.infer = InferenceServicer(pipeline_backend, labels, settings.ARENA_DECODE_THREADS)
+        handlers.append(pb.InferenceService.handler(servicer.infer))
     server = grpc.aio.server(options=GRPC_OPTIONS)
-    server.add_generic_rpc_handlers((pb.ClassificationService.handler(servicer),
-                                     pb.Health.handler(HealthServicer())))
+    server.add_generic_rpc_handlers(tuple(handlers))
     bound = server.add_insecure_port(f"{settings.HOST}:{port if port is not None else settings.PORT}")
     await server.start()
     log.info("classification service listening", extra={"port": bound})

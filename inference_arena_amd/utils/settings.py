@@ -53,6 +53,7 @@ class Settings(BaseModel):
     ARENA_INSTANCES: int = 1            # executor instances per GPU behind one batcher
     ARENA_WEIGHT_SEED: int = 0
     ARENA_FAULT_EVERY: int = 0          # inject a failure every k-th request (0 = off)
+    ARENA_INFER_SERVICE: int = 0        # classification gRPC server also serves inference.InferenceService/Infer
 
     @classmethod
     def from_env(cls, env_file: str | Path = ".env", **overrides) -> "Settings":
