@@ -8,7 +8,7 @@ namespace arena {
 
 using clk = std::chrono::steady_clock;
 
-DynamicBatcher::DynamicBatcher(std::vector<std::shared_ptr<Executor>> instances, const BatcherConfig& cfg)
+DynamicBatcher::DynamicBatcher(std::vector<std::shared_ptr<BatchInstance>> instances, const BatcherConfig& cfg)
     : inst_(std::move(instances)), cfg_(cfg) {
   if (inst_.empty()) throw std::runtime_error("DynamicBatcher: no executor instances");
   int largest = 0;
@@ -142,7 +142,7 @@ void DynamicBatcher::fail(Batch& batch, const std::string& err) {
 }
 
 void DynamicBatcher::instance_loop(int idx) {
-  Executor& ex = *inst_[idx];
+  BatchInstance& ex = *inst_[idx];
   struct InFlight {
     int slot;
     Batch batch;
@@ -179,7 +179,7 @@ void DynamicBatcher::instance_loop(int idx) {
     pending.pop_front();
     try {
       BatchResult r = ex.collect(f.slot);
-      finish(f.batch, r, f.t_submit, (size_t)std::max<int64_t>(0, ex.config().raw_out_bytes));
+      finish(f.batch, r, f.t_submit, (size_t)std::max<int64_t>(0, ex.raw_out_bytes()));
     } catch (const std::exception& e) {
       fail(f.batch, e.what());
     }

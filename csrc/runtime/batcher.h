@@ -11,8 +11,9 @@
 //   * an idle instance takes a batch as soon as the queue holds max_batch
 //     requests, or a preferred size is available and no larger one can form,
 //     or the oldest request has waited max_queue_delay;
-//   * each instance keeps two batches in flight (the executor's two staging
-//     slots), so packing/H2D of batch i+1 overlaps the graph of batch i;
+//   * each instance keeps one batch in flight per staging slot (the executor
+//     runs each slot on its own stream), so packing/H2D of the next batch
+//     overlaps the graphs of the previous ones;
 //   * completion callbacks run on the instance thread.
 #pragma once
 #include <chrono>
@@ -25,7 +26,7 @@
 #include <thread>
 #include <vector>
 
-#include "executor.h"
+#include "instance.h"
 
 namespace arena {
 
@@ -59,7 +60,7 @@ struct BatcherStats {
 
 class DynamicBatcher {
  public:
-  DynamicBatcher(std::vector<std::shared_ptr<Executor>> instances, const BatcherConfig& cfg);
+  DynamicBatcher(std::vector<std::shared_ptr<BatchInstance>> instances, const BatcherConfig& cfg);
   ~DynamicBatcher();
   DynamicBatcher(const DynamicBatcher&) = delete;
   DynamicBatcher& operator=(const DynamicBatcher&) = delete;
@@ -87,7 +88,7 @@ class DynamicBatcher {
   void finish(Batch& batch, const BatchResult& r, std::chrono::steady_clock::time_point t_submit, size_t raw_bytes);
   void fail(Batch& batch, const std::string& err);
 
-  std::vector<std::shared_ptr<Executor>> inst_;
+  std::vector<std::shared_ptr<BatchInstance>> inst_;
   BatcherConfig cfg_;
   std::mutex mu_;
   std::condition_variable cv_;

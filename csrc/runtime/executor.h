@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "../kernels/launch.h"
+#include "instance.h"
 
 namespace arena {
 
@@ -93,45 +94,28 @@ struct BucketInfo {
   int64_t arena_bytes = 0;
 };
 
-struct InputImage {
-  const uint8_t* data;  // RGB uint8 HWC, contiguous (or an fp32 tensor when bytes != 0)
-  int h, w;
-  int64_t bytes = 0;    // explicit payload size (tensor inputs); 0 = h*w*3
-};
-
-// Per-slot results copied back to pinned memory by the graph.
-struct BatchResult {
-  int n_images = 0;
-  int bucket = 0;
-  int total_crops = 0;
-  std::vector<int> det_count;        // [n]
-  std::vector<Detection> det;        // [n * max_det]
-  std::vector<TopkResult> topk;      // [total crops], in crop-plan order
-  std::vector<int> crop_offset;      // [n + 1] first crop of each image
-  double gpu_ms = 0.0;               // graph wall time from events
-  std::vector<uint8_t> raw;          // [n * raw_out_bytes] when the program exports raw tensors
-};
-
-class Executor {
+class Executor : public BatchInstance {
  public:
   explicit Executor(const ExecutorConfig& cfg);
-  ~Executor();
+  ~Executor() override;
   Executor(const Executor&) = delete;
   Executor& operator=(const Executor&) = delete;
 
   void set_weights(const void* host, size_t bytes);
   void set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops, int n_cls_ops);
   void add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes);
-  std::vector<int> buckets() const;
+  std::vector<int> buckets() const override;
   int crop_cap_for(int B) const;
   const ExecutorConfig& config() const { return cfg_; }
+  int max_det() const override { return cfg_.max_det; }
+  int64_t raw_out_bytes() const override { return cfg_.raw_out_bytes; }
 
   // Asynchronous pipelined API: submit() packs the images into a free staging
   // slot, enqueues H2D + graph and returns the slot id; collect() waits for
   // that slot and returns its results (running overflow classification passes
   // when a batch produced more crops than one pass holds).
-  int submit(const std::vector<InputImage>& imgs);
-  BatchResult collect(int slot);
+  int submit(const std::vector<InputImage>& imgs) override;
+  BatchResult collect(int slot) override;
   // Convenience: submit + collect.
   BatchResult run(const std::vector<InputImage>& imgs);
 
@@ -140,7 +124,7 @@ class Executor {
   void replay(int B, int slot, int iters);
   void synchronize();
   // Staging slots = batches that may be in flight at once (submit() throws when all are busy).
-  int num_slots() const { return n_slots_; }
+  int num_slots() const override { return n_slots_; }
 
   // Device pointers for tests / introspection.
   uintptr_t arena_ptr(int B) const;

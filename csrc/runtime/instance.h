@@ -1,0 +1,46 @@
+// The interface the dynamic batcher schedules onto: one "model instance"
+// (Triton's instance_group entry) that accepts batches of requests into a
+// fixed number of in-flight slots.  The GPU Executor (executor.h) is the
+// production implementation; tests drive the batcher with CPU fakes under
+// ThreadSanitizer / AddressSanitizer (csrc/tests/batcher_stress.cpp).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "../kernels/launch.h"
+
+namespace arena {
+
+struct InputImage {
+  const uint8_t* data;  // RGB uint8 HWC, contiguous (or an fp32 tensor when bytes != 0)
+  int h, w;
+  int64_t bytes = 0;    // explicit payload size (tensor inputs); 0 = h*w*3
+};
+
+// Per-slot results copied back to pinned memory after the slot's graph.
+struct BatchResult {
+  int n_images = 0;
+  int bucket = 0;
+  int total_crops = 0;
+  std::vector<int> det_count;        // [n]
+  std::vector<Detection> det;        // [n * max_det]
+  std::vector<TopkResult> topk;      // [total crops], in crop-plan order
+  std::vector<int> crop_offset;      // [n + 1] first crop of each image
+  double gpu_ms = 0.0;               // graph wall time from events
+  std::vector<uint8_t> raw;          // [n * raw_out_bytes] when the program exports raw tensors
+};
+
+class BatchInstance {
+ public:
+  virtual ~BatchInstance() = default;
+  virtual std::vector<int> buckets() const = 0;  // batch capacities, ascending (last = largest)
+  virtual int num_slots() const = 0;             // batches that may be in flight at once
+  virtual int max_det() const = 0;               // detection rows per image in BatchResult::det
+  virtual int64_t raw_out_bytes() const = 0;     // raw output bytes per image (0 = none)
+  // Start a batch; returns the slot id.  Throws when every slot is in flight.
+  virtual int submit(const std::vector<InputImage>& imgs) = 0;
+  // Wait for a slot's batch and return its results (the slot becomes free).
+  virtual BatchResult collect(int slot) = 0;
+};
+
+}  // namespace arena

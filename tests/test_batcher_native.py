@@ -1,0 +1,46 @@
+"""Race detection for the native runtime (SURVEY.md §5 "race detection /
+sanitizers"): the C++ DynamicBatcher (csrc/runtime/batcher.cpp) is compiled
+host-only with ThreadSanitizer and AddressSanitizer and driven by CPU fake
+instances from many producer threads (csrc/tests/batcher_stress.cpp).  The
+reference has no sanitizer story (its only thread-safety device is a
+``threading.Lock`` around the ORT session cache, src/shared/model/
+registry.py:128,155-159)."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SRCS = [ROOT / "csrc" / "tests" / "batcher_stress.cpp", ROOT / "csrc" / "runtime" / "batcher.cpp"]
+
+
+def _build(sanitizer: str) -> Path:
+    if not (Path(HIPCC).exists() or shutil.which(HIPCC)):
+        pytest.skip("hipcc not available")
+    out = ROOT / "build" / f"batcher_stress_{sanitizer}"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    newest = max(p.stat().st_mtime for p in SRCS + list((ROOT / "csrc" / "runtime").glob("*.h")))
+    if not out.exists() or out.stat().st_mtime < newest:
+        # host code only: each -fsanitize= goes right after -Xarch_host
+        cmd = [HIPCC, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", f"-fsanitize={sanitizer}",
+               "-I" + str(ROOT / "csrc"), *map(str, SRCS), "-o", str(out)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-4000:]
+    return out
+
+
+@pytest.mark.parametrize("sanitizer", ["thread", "address"])
+def test_batcher_stress_under_sanitizer(sanitizer):
+    exe = _build(sanitizer)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1",
+               ASAN_OPTIONS="detect_leaks=1:halt_on_error=1")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    report = r.stdout + r.stderr
+    assert "ThreadSanitizer" not in report and "AddressSanitizer" not in report, report[-6000:]
+    assert r.returncode == 0, report[-6000:]
+    assert "batcher_stress: ok" in r.stdout
