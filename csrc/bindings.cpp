@@ -418,7 +418,7 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<DynamicBatcher>(m, "DynamicBatcher")
       .def(py::init([](py::list executors, const py::dict& cfg) {
-             std::vector<std::shared_ptr<Executor>> inst;
+             std::vector<std::shared_ptr<BatchInstance>> inst;
              for (auto h : executors) inst.push_back(h.cast<std::shared_ptr<Executor>>());
              BatcherConfig c;
              c.max_batch = get<int>(cfg, "max_batch", c.max_batch);
