@@ -216,6 +216,9 @@ void conv_igemm(const ConvParams& p, hipStream_t s) {
   } else if (N <= 64) {
     if (enough(128, 64)) igemm_launch<128, 64, 2, 2, 64>(p, s, M);
     else igemm_launch<64, 64, 4, 1, 64>(p, s, M);
+  } else if (N == 80) {  // Detect class branch (nc = 80): exact 5-fragment width, no padded MFMA column
+    if (enough(128, 80)) igemm_launch<128, 80, 4, 1, 64>(p, s, M);
+    else igemm_launch<64, 80, 4, 1, 64>(p, s, M);
   } else if (N <= 96) {
     if (enough(128, 96)) igemm_launch<128, 96, 4, 1, 64>(p, s, M);
     else igemm_launch<64, 96, 4, 1, 64>(p, s, M);
