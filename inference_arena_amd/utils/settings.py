@@ -26,7 +26,12 @@ def _read_dotenv(path: Path) -> dict[str, str]:
         if not line or line.startswith("#") or "=" not in line:
             continue
         k, v = line.split("=", 1)
-        out[k.strip()] = v.strip().strip('"').strip("'")
+        v = v.strip()
+        if v[:1] in ("'", '"') and v[0] in v[1:]:
+            v = v[1:v.index(v[0], 1)]  # quoted value: keep '#' inside the quotes
+        else:
+            v = v.split(" #", 1)[0].split("\t#", 1)[0].strip()  # unquoted: drop an inline comment
+        out[k.strip()] = v
     return out
 
 
