@@ -50,11 +50,17 @@ def _decode(data: bytes | Path | str, what: str) -> np.ndarray:
     return np.ascontiguousarray(arr)
 
 
+class ImageLoadError(ValueError, FileNotFoundError):
+    """A missing image file: a ``ValueError`` like the reference's ``load_image``
+    (src/shared/processing/transforms.py:67-71, cv2.imread -> None), and a
+    ``FileNotFoundError`` for callers that expect the OS error."""
+
+
 def load_image(image_path: str | Path) -> np.ndarray:
     """Load an image file as RGB uint8 [H, W, 3]."""
     p = Path(image_path)
     if not p.exists():
-        raise FileNotFoundError(f"Image not found: {p}")
+        raise ImageLoadError(f"Failed to load image: {p} (not found)")
     return _decode(p, f"Failed to load image {p}")
 
 
