@@ -231,6 +231,30 @@ struct CropGatherParams {
 };
 void crop_gather_s2d(const CropGatherParams& p, hipStream_t s);
 
+// ---------------------------------------------------------------- fused preprocessing + stem conv
+// src 0: letterbox (images) -> YOLOv5nu stem (3x3 over s2d, 16 -> 16, SiLU);
+// src 1: crop gather (crops) -> MobileNetV2 stem (2x2 over s2d, 16 -> 32, ReLU6).
+// The s2d input tile lives only in LDS (csrc/kernels/stem_fused.hip).
+struct StemFusedParams {
+  int src;                  // 0 letterbox, 1 crop gather
+  const uint8_t* pool;
+  const ImageMeta* meta;
+  const Ctrl* ctrl;         // live counts (n_images / n_crops, crop_base)
+  const CropRef* crops;     // src 1
+  int cap;                  // batch capacity (images or crops)
+  int S;                    // full-resolution side (letterbox T / crop S); output map is S/2 x S/2
+  float mean[3], inv_std[3];  // src 1
+  int KS;                   // stem kernel size over the s2d map (3 or 2)
+  const void* w;            // bf16 [Cout][Kpad], k = tap*16 + c
+  int Kpad;
+  const float* bias;
+  int Cout;
+  void* y;                  // bf16 [cap, S/2, S/2, ys]
+  int ys;
+  int act;
+};
+void stem_fused(const StemFusedParams& p, hipStream_t s);
+
 // ---------------------------------------------------------------- classification head (K13/K14)
 struct AvgPoolParams {
   const void* x;

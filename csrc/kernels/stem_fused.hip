@@ -1,0 +1,231 @@
+// Fused preprocessing + stem convolution (K1+K2 for YOLOv5nu, K9+K10 for
+// MobileNetV2): the space-to-depth input tile of one workgroup is computed
+// straight from the uint8 source image into LDS (letterbox for the detector,
+// crop gather + ImageNet normalisation for the classifier) and the stem conv
+// runs on it with MFMA, so the bf16 s2d tensor never goes to HBM.
+//
+// Unfused, the detector's front end wrote a [B,320,320,16] bf16 letterbox
+// tensor (105 MB at B = 32) and the stem conv read it back ~9x through L2;
+// here each workgroup recomputes its halo ring instead (10x34 input pixels
+// for an 8x32 output tile: 1.33x the bilinear work, no round trip).
+//
+// Per workgroup (256 threads = 4 waves): one output tile of TH x TW pixels
+// (256) x NF*16 channels of one image / crop.
+//   phase 1  every thread builds s2d pixels of the (TH+KS-1) x (TW+KS-1)
+//            halo tile: 4 sub-pixels x RGB by cv2-INTER_LINEAR bilinear
+//            sampling, 16 bf16 channels (12 live) = 32 B per pixel in LDS;
+//            pixels outside the map are the conv's zero padding.
+//   phase 2  each wave owns 4 fragments of 16 pixels; K = KS*KS taps x 16
+//            channels in 32-deep slabs, weights held in registers; one
+//            v_mfma_f32_16x16x32_bf16 per (fragment, N-fragment, slab).
+//   epilogue bias + activation, 8-byte stores of 4 channels per lane.
+// Blocks are mapped so that all tiles of an image run on one XCD (the
+// source image's rows are re-read by neighbouring tiles from that L2).
+//
+// Numerics are identical to letterbox_s2d / crop_gather_s2d followed by the
+// stem conv: the same float ops produce the same bf16 s2d values.
+#include "common.h"
+#include "launch.h"
+
+namespace arena {
+
+namespace {
+
+struct LinTap2 {
+  int i0, i1;
+  float f;
+};
+
+__device__ __forceinline__ LinTap2 tap_of(int d, float scale, int n) {
+  float fx = ((float)d + 0.5f) * scale - 0.5f;
+  int s0 = (int)floorf(fx);
+  float f = fx - (float)s0;
+  if (s0 < 0) { s0 = 0; f = 0.f; }
+  if (s0 >= n - 1) { s0 = n - 1; f = 0.f; }
+  LinTap2 t;
+  t.i0 = s0;
+  t.i1 = s0 + 1 < n ? s0 + 1 : n - 1;
+  t.f = f;
+  return t;
+}
+
+__device__ __forceinline__ void sample_rgb(const uint8_t* img, int stride_px, LinTap2 ty, LinTap2 tx, float* rgb) {
+  const uint8_t* r0 = img + (size_t)ty.i0 * stride_px * 3;
+  const uint8_t* r1 = img + (size_t)ty.i1 * stride_px * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float a = (float)r0[tx.i0 * 3 + c], b = (float)r0[tx.i1 * 3 + c];
+    const float d = (float)r1[tx.i0 * 3 + c], e = (float)r1[tx.i1 * 3 + c];
+    const float top = a + (b - a) * tx.f;
+    const float bot = d + (e - d) * tx.f;
+    rgb[c] = floorf(top + (bot - top) * ty.f + 0.5f);  // cv2 returns uint8
+  }
+}
+
+// Source geometry of one batch item, uniform over the workgroup.
+struct Src {
+  const uint8_t* img;  // top-left of the sampled region
+  int stride_px;       // image row stride in pixels
+  int h, w;            // sampled region size (letterbox: new_h/new_w of the resized image)
+  int rh, rw;          // region size the taps clamp to (source pixels)
+  int pad_h, pad_w;    // letterbox padding (0 for crops)
+  float sy, sx;
+  bool empty;          // zero-area crop -> black
+};
+
+}  // namespace
+
+template <int SRC, int KS, int NF, int TH, int TW>
+__global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p) {
+  constexpr int HH = TH + KS - 1, HW = TW + KS - 1, NPIX = HH * HW;
+  constexpr int SLABS = (KS * KS * 16 + 31) / 32;
+  static_assert(TH * TW == 256, "one 256-pixel tile per workgroup (4 waves x 4 fragments)");
+  __shared__ __align__(16) uint4 tile[NPIX * 2];  // 32 B per s2d pixel
+
+  const int S2 = p.S >> 1;
+  const int tiles_x = (S2 + TW - 1) / TW, tiles_y = (S2 + TH - 1) / TH, ntiles = tiles_x * tiles_y;
+  const int id = blockIdx.x, xcd = id & 7, j = id >> 3;
+  const int item = (j / ntiles) * 8 + xcd;  // every tile of one item lands on one XCD
+  const int t = j - (j / ntiles) * ntiles;
+  const int n_live = live_batch(p.cap, SRC == 0 ? &p.ctrl->n_images : &p.ctrl->n_crops);
+  if (item >= n_live) return;
+  const int ty0 = (t / tiles_x) * TH, tx0 = (t % tiles_x) * TW;
+
+  Src g;
+  if constexpr (SRC == 0) {
+    const ImageMeta m = p.meta[item];
+    g.img = p.pool + m.offset;
+    g.stride_px = m.w;
+    g.h = m.new_h;
+    g.w = m.new_w;
+    g.rh = m.h;
+    g.rw = m.w;
+    g.pad_h = m.pad_h;
+    g.pad_w = m.pad_w;
+    g.sy = (float)((double)m.h / (double)m.new_h);
+    g.sx = (float)((double)m.w / (double)m.new_w);
+    g.empty = false;
+  } else {
+    const CropRef cr = p.crops[p.ctrl->crop_base + item];
+    const ImageMeta m = p.meta[cr.img];
+    const int cw = cr.x2 - cr.x1, ch = cr.y2 - cr.y1;
+    g.empty = cw <= 0 || ch <= 0;
+    g.img = p.pool + m.offset + ((size_t)cr.y1 * m.w + cr.x1) * 3;
+    g.stride_px = m.w;
+    g.h = g.rh = ch;
+    g.w = g.rw = cw;
+    g.pad_h = g.pad_w = 0;
+    g.sy = g.empty ? 1.f : (float)((double)ch / (double)p.S);
+    g.sx = g.empty ? 1.f : (float)((double)cw / (double)p.S);
+  }
+
+  // ---- phase 1: s2d halo tile into LDS
+  for (int i = threadIdx.x; i < NPIX; i += 256) {
+    const int hy = i / HW, hx = i - (i / HW) * HW;
+    const int Y = ty0 - 1 + hy, X = tx0 - 1 + hx;
+    float out[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) out[k] = 0.f;
+    if ((unsigned)Y < (unsigned)S2 && (unsigned)X < (unsigned)S2) {
+#pragma unroll
+      for (int pq = 0; pq < 4; ++pq) {
+        const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
+        float rgb[3];
+        if constexpr (SRC == 0) {
+          const int dy = oy - g.pad_h, dx = ox - g.pad_w;
+          rgb[0] = rgb[1] = rgb[2] = 114.f;
+          if (dy >= 0 && dy < g.h && dx >= 0 && dx < g.w)
+            sample_rgb(g.img, g.stride_px, tap_of(dy, g.sy, g.rh), tap_of(dx, g.sx, g.rw), rgb);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) out[pq * 3 + c] = rgb[c] * (1.0f / 255.0f);
+        } else {
+          rgb[0] = rgb[1] = rgb[2] = 0.f;
+          if (!g.empty) sample_rgb(g.img, g.stride_px, tap_of(oy, g.sy, g.rh), tap_of(ox, g.sx, g.rw), rgb);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (rgb[c] * (1.0f / 255.0f) - p.mean[c]) * p.inv_std[c];
+        }
+      }
+    }
+    tile[i * 2] = pack8(out);
+    tile[i * 2 + 1] = pack8(out + 8);
+  }
+
+  // ---- weights of this lane's rows into registers (overlaps the barrier)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = lane & 15, kq = lane >> 4;
+  const bf16* __restrict__ w = (const bf16*)p.w;
+  bf16x8 wf[NF][SLABS];
+#pragma unroll
+  for (int a = 0; a < NF; ++a)
+#pragma unroll
+    for (int s = 0; s < SLABS; ++s) wf[a][s] = *(const bf16x8*)(w + (size_t)(a * 16 + row) * p.Kpad + s * 32 + kq * 8);
+  __syncthreads();
+
+  // ---- phase 2: MFMA over the LDS tile
+  f32x4 acc[NF][4];
+#pragma unroll
+  for (int a = 0; a < NF; ++a)
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[a][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < SLABS; ++s) {
+    int tap = 2 * s + (kq >> 1);
+    if (tap >= KS * KS) tap = 0;  // zero weight rows; any finite LDS value will do
+    const int kh = tap / KS, kw = tap - (tap / KS) * KS, chunk = kq & 1;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int P = (wave * 4 + f) * 16 + row;
+      const int py = P / TW, px = P - (P / TW) * TW;
+      const bf16x8 bv = *(const bf16x8*)&tile[((py + kh) * HW + px + kw) * 2 + chunk];
+#pragma unroll
+      for (int a = 0; a < NF; ++a) acc[a][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a][s], bv, acc[a][f], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue
+  bf16* __restrict__ y = (bf16*)p.y;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int P = (wave * 4 + f) * 16 + row;
+    const int oy = ty0 + P / TW, ox = tx0 + (P - (P / TW) * TW);
+    if (oy >= S2 || ox >= S2) continue;
+    const size_t base = ((size_t)item * S2 * S2 + (size_t)oy * S2 + ox) * p.ys;
+#pragma unroll
+    for (int a = 0; a < NF; ++a) {
+      const int cb = a * 16 + kq * 4;
+      const float4 bias = *(const float4*)(p.bias + cb);
+      float v[4] = {acc[a][f][0] + bias.x, acc[a][f][1] + bias.y, acc[a][f][2] + bias.z, acc[a][f][3] + bias.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      *(uint2*)(y + base + cb) = pack4(v);
+    }
+  }
+}
+
+template <int SRC, int KS, int NF, int TH, int TW>
+static void stem_launch(const StemFusedParams& p, hipStream_t s) {
+  const int S2 = p.S / 2;
+  const int ntiles = ((S2 + TW - 1) / TW) * ((S2 + TH - 1) / TH);
+  const long blocks = (long)((p.cap + 7) / 8) * 8 * ntiles;
+  hipLaunchKernelGGL((stem_fused_kernel<SRC, KS, NF, TH, TW>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+}
+
+void stem_fused(const StemFusedParams& p, hipStream_t s) {
+  if (p.S % 2 != 0 || p.S <= 0) throw std::runtime_error("stem_fused: S must be positive and even");
+  if (p.ctrl == nullptr) throw std::runtime_error("stem_fused: needs the control block (live counts)");
+  if (p.ys % 4 != 0) throw std::runtime_error("stem_fused: output pixel stride must be a multiple of 4");
+  if (p.cap <= 0) return;
+  if (p.src == 0) {  // YOLOv5nu: letterbox -> 6x6/s2 stem as 3x3/s1 over s2d, 16 channels, SiLU
+    if (p.KS != 3 || p.Cout != 16 || p.Kpad != 160)
+      throw std::runtime_error("stem_fused: detector stem must be 3x3 (s2d) x 16 -> 16, Kpad 160");
+    stem_launch<0, 3, 1, 8, 32>(p, s);
+  } else if (p.src == 1) {  // MobileNetV2: crop gather -> 3x3/s2 stem as 2x2/s1 over s2d, 32 channels, ReLU6
+    if (p.KS != 2 || p.Cout != 32 || p.Kpad != 64 || p.crops == nullptr)
+      throw std::runtime_error("stem_fused: classifier stem must be 2x2 (s2d) x 16 -> 32, Kpad 64");
+    stem_launch<1, 2, 2, 16, 16>(p, s);
+  } else {
+    throw std::runtime_error("stem_fused: unknown source");
+  }
+}
+
+}  // namespace arena

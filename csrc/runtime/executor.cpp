@@ -520,6 +520,30 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         crop_gather_s2d(p, s);
         break;
       }
+      case OP_STEMFUSED: {
+        StemFusedParams p{};
+        p.src = (int)r[1];
+        p.y = resolve(bk, sl, r[2], r[3], 2);
+        p.ys = (int)r[4];
+        p.S = (int)r[5];
+        p.w = W + r[6];
+        p.Kpad = (int)r[7];
+        p.bias = (const float*)(W + r[8]);
+        p.Cout = (int)r[9];
+        p.act = (int)r[10];
+        p.crops = p.src == 1 ? (const CropRef*)resolve(bk, sl, r[11], 0, 1) : nullptr;
+        for (int c = 0; c < 3; ++c) {
+          p.mean[c] = bits_to_float(r[12 + c]);
+          p.inv_std[c] = bits_to_float(r[15 + c]);
+        }
+        p.cap = batch(r[18]);
+        p.KS = (int)r[19];
+        p.pool = pool;
+        p.meta = meta;
+        p.ctrl = ctrl;
+        stem_fused(p, s);
+        break;
+      }
       case OP_AVGPOOL: {
         AvgPoolParams p{};
         p.x = resolve(bk, sl, r[1], 0, 2);

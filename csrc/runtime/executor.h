@@ -56,6 +56,7 @@ enum OpType : int64_t {
   OP_TENSORIN = 12,
   OP_YOLORAW = 13,
   OP_IRBLOCK = 14,
+  OP_STEMFUSED = 15,
 };
 
 // Reserved buffer ids (the planner's arena buffers are ids >= 0).

@@ -36,6 +36,10 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   IRBLOCK  1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 inp 7 inp_pad 8 hid_pad 9 oup 10 oup_pad 11 stride
            12 expand 13 res 14 we 15 be 16 wd 17 bd 18 wp 19 bp 20 y_buf 21 y_coff 22 y_cs 23 Ho 24 Wo
            25 batch_kind   (fused MobileNetV2 inverted residual, csrc/kernels/ir_block.hip)
+  STEMFUSED 1 src (0 letterbox, 1 crop gather) 2 y_buf 3 y_coff 4 y_cs 5 S 6 w_off 7 Kpad 8 b_off
+           9 Cout 10 act 11 crops_buf 12-14 mean 15-17 inv_std (float bits) 18 batch_kind 19 KS
+           (preprocessing fused into the stem conv; the s2d input exists only in LDS,
+            csrc/kernels/stem_fused.hip)
 """
 from __future__ import annotations
 
@@ -47,7 +51,7 @@ import torch
 
 OP_FIELDS = 48
 (OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
- OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK) = range(1, 15)
+ OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED) = range(1, 16)
 BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK, BUF_RAWOUT = -1, -10, -11, -12, -13, -14, -15, -16
 IMAGES, CROPS = 0, 1
 ACT = {None: 0, "none": 0, "silu": 1, "relu6": 2}
@@ -271,6 +275,26 @@ class ProgramBuilder:
 
     def letterbox(self, out: Buffer, T: int) -> None:
         self._emit([OP_LETTERBOX, out.id, T], out)
+
+    def stem_fused(self, dst: View, w: torch.Tensor, b: torch.Tensor, *, S: int, act: str, crops: Buffer | None = None,
+                   mean=None, std=None, kind: int = IMAGES) -> None:
+        """Letterbox (``crops=None``) or crop gather + normalisation, fused with the s2d stem conv
+        (``w``: [Cout, 16, KS, KS] over the space-to-depth input, pad top/left 1)."""
+        cout, cin, ks, ks2 = w.shape
+        if cin != 16 or ks != ks2 or cout != dst.C:
+            raise ValueError("stem_fused: weights must be [Cout, 16, KS, KS] with Cout == dst.C")
+        wb, bb, kpad, cpad = pack_conv_weight(w, b)
+        if cpad != cout:
+            raise ValueError("stem_fused: Cout must be a multiple of 16")
+        w_off = self.weights.add(wb)
+        b_off = self.weights.add(bb)
+        src = 0 if crops is None else 1
+        mean = mean if mean is not None else (0.0, 0.0, 0.0)
+        std = std if std is not None else (1.0, 1.0, 1.0)
+        rec = [OP_STEMFUSED, src, dst.bid, dst.coff, dst.cs, S, w_off, kpad, b_off, cout, ACT[act],
+               crops.id if crops is not None else BUF_NONE] + [fbits(m) for m in mean] + \
+              [fbits(1.0 / s) for s in std] + [kind, ks]
+        self._emit(rec, dst, crops)
 
     def zero(self, buf: Buffer, kind: int = IMAGES) -> None:
         self._emit([OP_ZERO, buf.id, buf.per_item, kind], buf)

@@ -20,6 +20,8 @@ Lowering rules (what replaces ONNX graph nodes):
   * Detect's first 3x3 convs of the box and class branches are one conv.
   * Both stems read space-to-depth inputs: YOLO's 6x6/s2/p2 conv becomes a
     3x3/s1 conv over 12(+4) channels, MobileNet's 3x3/s2 conv a 2x2/s1 conv.
+  * With ``ARENA_FUSE_STEM`` (default) the letterbox / crop gather is fused
+    into those stem convs (stem_fused op): the s2d input only exists in LDS.
 """
 from __future__ import annotations
 
@@ -77,16 +79,27 @@ def _c3(pb: ProgramBuilder, m, src: View, dst: View, H: int, W: int, name: str) 
     pb.conv(View(T, 0, 2 * c_), dst, w3, b3)
 
 
-def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool = False):
+def fuse_stem_default() -> bool:
+    """``ARENA_FUSE_STEM`` (default 1): preprocessing fused into the stem convs (stem_fused op)."""
+    return os.environ.get("ARENA_FUSE_STEM", "1").lower() not in ("0", "false", "no", "off")
+
+
+def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool = False,
+              fuse_stem: bool | None = None):
     h = T // 2
-    X0 = pb.tensor("x_s2d", h, h, 16)
-    if tensor_input:
-        pb.tensor_in(X0, T)
-    else:
-        pb.letterbox(X0, T)
     A0 = pb.tensor("b0", h, h, 16)
     w, b = fold(y.b0)
-    pb.conv(View(X0, 0, 16), View(A0, 0, 16), s2d_stem_6x6(w), b)
+    if fuse_stem is None:
+        fuse_stem = fuse_stem_default()
+    if fuse_stem and not tensor_input:
+        pb.stem_fused(View(A0, 0, 16), s2d_stem_6x6(w), b, S=T, act="silu")
+    else:
+        X0 = pb.tensor("x_s2d", h, h, 16)
+        if tensor_input:
+            pb.tensor_in(X0, T)
+        else:
+            pb.letterbox(X0, T)
+        pb.conv(View(X0, 0, 16), View(A0, 0, 16), s2d_stem_6x6(w), b)
     A1 = pb.tensor("b1", h // 2, h // 2, 32)
     pb.conv(View(A0, 0, 16), View(A1, 0, 32), *fold(y.b1), stride=2)
     A2 = pb.tensor("b2", h // 2, h // 2, 32)
@@ -164,7 +177,7 @@ def fuse_block(blk, H: int, policy) -> bool:
 
 
 def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std, *, kind: int = CROPS,
-                   raw_logits: bool = False, fuse_ir: bool | str | None = None):
+                   raw_logits: bool = False, fuse_ir: bool | str | None = None, fuse_stem: bool | None = None):
     """MobileNetV2 over crop-gathered inputs (``crops`` = CropRef buffer) or, with
     ``crops=None``, over fp32 [3,S,S] tensors of the image batch (``kind=IMAGES``).
 
@@ -175,15 +188,21 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
     if fuse_ir is None:
         fuse_ir = fuse_ir_default()
     h = S // 2
-    X = pb.tensor("crop_s2d", h, h, 16, kind=CROPS_)
-    if crops is None:
-        pb.tensor_in(X, S)
-    else:
-        pb.crop_gather(crops, X, S, mean, std)
+    if fuse_stem is None:
+        fuse_stem = fuse_stem_default()
     w, b = fold(m.stem)
     F = pb.tensor("m.stem", h, h, 32, kind=CROPS_)
-    pb.conv(View(X, 0, 16), View(F, 0, 32), s2d_stem_3x3(w), b, pad=(1, 1), act="relu6", kind=CROPS_,
-            out_hw=(h, h))
+    if fuse_stem and crops is not None:
+        pb.stem_fused(View(F, 0, 32), s2d_stem_3x3(w), b, S=S, act="relu6", crops=crops, mean=mean, std=std,
+                      kind=CROPS_)
+    else:
+        X = pb.tensor("crop_s2d", h, h, 16, kind=CROPS_)
+        if crops is None:
+            pb.tensor_in(X, S)
+        else:
+            pb.crop_gather(crops, X, S, mean, std)
+        pb.conv(View(X, 0, 16), View(F, 0, 32), s2d_stem_3x3(w), b, pad=(1, 1), act="relu6", kind=CROPS_,
+                out_hw=(h, h))
     cur, H = F, h
     for i, blk in enumerate(m.blocks):
         Ho = (H + 2 - 3) // blk.stride + 1

@@ -27,6 +27,7 @@ from ..engine.planner import (
     OP_LETTERBOX,
     OP_NMS,
     OP_SPPF,
+    OP_STEMFUSED,
     OP_TENSORIN,
     OP_TOPK,
     OP_YOLORAW,
@@ -124,6 +125,17 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         elif op == OP_LETTERBOX:
             T2 = int(r[2]) // 2
             need(i, r[1], 0, B * T2 * T2 * 32, "letterbox output")
+        elif op == OP_STEMFUSED:
+            src, S, kpad, cout, kind, ks = int(r[1]), int(r[5]), int(r[7]), int(r[9]), int(r[18]), int(r[19])
+            n = kind_n(kind)
+            expect = {0: (3, 16, 160, 0), 1: (2, 32, 64, CROPS)}.get(src)
+            if expect is None or (ks, cout, kpad, kind) != expect or S % 2:
+                raise ProgramError(f"op {i}: bad stem_fused geometry (src {src}, KS {ks}, Cout {cout}, Kpad {kpad})")
+            view(i, r[2], int(r[3]), int(r[4]), n * (S // 2) ** 2, cout, 2, "stem output")
+            if src == 1:
+                need(i, r[11], 0, B * max_det * CROP_BYTES, "crop refs")
+            weights(i, int(r[6]), cout * kpad * 2, "stem weight")
+            weights(i, int(r[8]), cout * 4, "stem bias")
         elif op == OP_ZERO:
             need(i, r[1], 0, int(r[2]) * kind_n(r[3]), "zero")
         elif op == OP_DECODE:

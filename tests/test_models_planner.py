@@ -107,7 +107,13 @@ def test_program_shape(program):
     # (unfused: 35 convs = stem + 16 expand + 17 project + head, plus FC)
     from inference_arena_amd.engine.planner import OP_IRBLOCK
 
+    from inference_arena_amd.engine.planner import OP_STEMFUSED
+
     irs = int((program.ops[:, 0] == OP_IRBLOCK).sum())
+    stems = int((program.ops[:, 0] == OP_STEMFUSED).sum())
+    # the two stem convs become stem_fused ops (preprocessing fused in) unless ARENA_FUSE_STEM=0
+    assert stems in (0, 2)
+    convs += stems
     # auto policy: blocks 1-10 fused, 11-17 as expand/project convs (2 each, block 17 included)
     assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0), (64 + 3 + 14, 10))
     assert program.cls_ops.shape[0] < program.ops.shape[0]
@@ -121,7 +127,7 @@ def test_unfused_program_shape(models):
     for fuse, want in ((False, 36), (True, 3)):
         pb = ProgramBuilder()
         crops = pb.raw("crops", 300 * 32)
-        plan_mobilenet(pb, models[1], crops, 224, (0.5,) * 3, (0.25,) * 3, fuse_ir=fuse)
+        plan_mobilenet(pb, models[1], crops, 224, (0.5,) * 3, (0.25,) * 3, fuse_ir=fuse, fuse_stem=False)
         assert int((pb.build().ops[:, 0] == OP_CONV).sum()) == want
 
 

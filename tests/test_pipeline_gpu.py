@@ -90,3 +90,27 @@ def test_overflow_crops_extra_pass(dense_models, device):
     for x, y in zip(a, b):
         np.testing.assert_array_equal(x.topk_idx, y.topk_idx)
         np.testing.assert_allclose(x.topk_logit, y.topk_logit, rtol=1e-5, atol=1e-5)
+
+
+def test_fused_stem_matches_unfused(dense_models, device, monkeypatch):
+    """stem_fused (letterbox / crop gather computed into LDS inside the stem convs) vs the unfused
+    letterbox_s2d + conv and crop_gather_s2d + conv programs: same stem activations and results."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    imgs = synthetic_images(5, 33) + synthetic_images(1, 34, hw=(333, 500))
+    monkeypatch.setenv("ARENA_FUSE_STEM", "0")
+    plain = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)  # keep b0 readable
+    monkeypatch.setenv("ARENA_FUSE_STEM", "1")
+    fused = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)
+    assert any(int(op[0]) == 15 for op in fused.program.ops) and not any(int(op[0]) == 15 for op in plain.program.ops)
+    a, b = plain.infer(imgs), fused.infer(imgs)
+    for i in range(len(imgs)):
+        s_plain, s_fused = plain.read_buffer("b0", 8, i), fused.read_buffer("b0", 8, i)
+        np.testing.assert_allclose(s_fused, s_plain, atol=0.02 + 0.01 * np.abs(s_plain).max())
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        if len(x):
+            np.testing.assert_allclose(y.boxes, x.boxes, atol=0.5)
+            assert (x.topk_idx[:, 0] == y.topk_idx[:, 0]).mean() >= 0.9
+            np.testing.assert_allclose(y.topk_logit[:, 0], x.topk_logit[:, 0], rtol=0.05, atol=0.05)

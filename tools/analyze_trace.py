@@ -20,7 +20,8 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 KIND = {1: "conv", 2: "dwconv", 3: "sppf", 4: "letterbox", 5: "zero", 6: "decode", 7: "nms", 8: "cropplan",
-        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw", 14: "irblock"}
+        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw", 14: "irblock", 15: "stemfused"}
+FIRST_KERNEL = {4: "letterbox", 12: "tensor_in", 15: "stem_fused"}
 
 
 def describe(rec) -> str:
@@ -31,6 +32,8 @@ def describe(rec) -> str:
                 f"{' crops' if rec[30] == 1 else ''}")
     if t == 2:
         return f"dw {int(rec[4])}x{int(rec[5])}x{int(rec[6])} s{int(rec[14])}"
+    if t == 15:
+        return f"{'letterbox' if rec[1] == 0 else 'crop gather'} + stem k{int(rec[19])} -> {int(rec[9])}"
     if t == 14:
         return (f"ir {int(rec[4])}x{int(rec[5])}x{int(rec[6])}->{int(rec[23])}x{int(rec[24])}x{int(rec[9])} "
                 f"hid{int(rec[8])} s{int(rec[11])}{' res' if rec[13] else ''}")
@@ -51,11 +54,21 @@ def main(argv=None) -> int:
     prog = plan_pipeline(*default_models(a.seed), conf_thr=0.5, iou_thr=0.45)
     n_ops = prog.ops.shape[0]
     rows = [r for r in csv.DictReader(open(a.trace)) if "arena::" in r["Kernel_Name"]]
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # replays start with the letterbox kernel
-    starts = [i for i, r in enumerate(rows) if "letterbox" in r["Kernel_Name"]]
-    replays = [rows[s:s + n_ops] for s in starts if s + n_ops <= len(rows)]
-    replays = [rp for rp in replays if len(rp) == n_ops][-a.replays:]
+    # the executor runs each staging slot on its own stream: slice replays per hardware queue so that
+    # kernels of concurrently running graphs are not interleaved
+    qkey = next((k for k in ("Queue_Id", "Stream_Id") if rows and k in rows[0]), None)
+    by_q = defaultdict(list)
+    for r in rows:
+        by_q[r[qkey] if qkey else 0].append(r)
+    first = FIRST_KERNEL.get(int(prog.ops[0][0]), "letterbox")
+    replays = []
+    for q in by_q.values():
+        q.sort(key=lambda r: int(r["Start_Timestamp"]))
+        starts = [i for i, r in enumerate(q) if first in r["Kernel_Name"]]
+        replays += [q[s:s + n_ops] for s in starts if s + n_ops <= len(q)]
+    replays = [rp for rp in replays if len(rp) == n_ops]
+    replays.sort(key=lambda rp: int(rp[0]["Start_Timestamp"]))
+    replays = replays[-a.replays:]
     if not replays:
         print("no complete replay found", file=sys.stderr)
         return 1

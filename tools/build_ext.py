@@ -37,6 +37,7 @@ SOURCES = [
     "kernels/conv_pw.hip",
     "kernels/conv3x3_v3.hip",
     "kernels/preprocess.hip",
+    "kernels/stem_fused.hip",
     "kernels/detect.hip",
     "kernels/classify_head.hip",
     "runtime/executor.cpp",
