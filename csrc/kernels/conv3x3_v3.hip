@@ -1,4 +1,4 @@
-// 3x3 convolution (stride 1 or 2, Cin % 32 == 0) — halo-tile kernel, v3.
+// 3x3 convolution (stride 1 or 2, Cin % 16 == 0) — halo-tile kernel, v3.
 //
 // Block = 4 waves; output tile = (4*MF) rows x 16 columns of one image, BN =
 // NF*16 output channels.  Per 32-channel input slab the block stages
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void conv3x3_v3_kernel(const ConvParams p) {
     const int pix = sq + 64 * i;
     const int r = pix / IC, c = pix - r * IC;
     const int iy = iy_base + r, ix = ix_base + c;
-    const bool ok = pix < G::IN_PIX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && sc * 8 < Cin;
+    const bool ok = pix < G::IN_PIX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
     in_goff[i] = ok ? (iy * p.W + ix) * p.xs + sc * 8 : -1;
     const int lp = r * ICP + c;
     in_loff[i] = pix < G::IN_PIX ? lp * 64 + v3swz(lp, sc) : -1;
@@ -79,16 +79,17 @@ __global__ __launch_bounds__(256) void conv3x3_v3_kernel(const ConvParams p) {
     const int tap = R / BN, n = R - tap * BN;
     int co = cout0 + n;
     co = co < p.Cout_pad ? co : p.Cout_pad - 1;
-    w_goff[i] = R < 9 * BN && sc * 8 < Cin ? co * p.Kpad + tap * Cin + sc * 8 : -1;
+    w_goff[i] = R < 9 * BN ? co * p.Kpad + tap * Cin + sc * 8 : -1;
     w_loff[i] = R < 9 * BN ? R * 64 + v3swz(n, sc) : -1;  // masked chunks still store zeros
   }
 
   uint4 rin[G::IN_IT], rw[G::W_IT];
   auto fetch = [&](int c0) {
+    const bool cv = c0 + sc * 8 < Cin;  // this thread's 8-channel chunk exists in slab c0 (Cin % 32 == 16: half slab)
 #pragma unroll
-    for (int i = 0; i < G::IN_IT; ++i) rin[i] = load16_or_zero(x + in_goff[i] + c0, x, in_goff[i] >= 0);
+    for (int i = 0; i < G::IN_IT; ++i) rin[i] = load16_or_zero(x + in_goff[i] + c0, x, cv && in_goff[i] >= 0);
 #pragma unroll
-    for (int i = 0; i < G::W_IT; ++i) rw[i] = load16_or_zero(w + w_goff[i] + c0, w, w_goff[i] >= 0);
+    for (int i = 0; i < G::W_IT; ++i) rw[i] = load16_or_zero(w + w_goff[i] + c0, w, cv && w_goff[i] >= 0);
   };
   auto stash = [&]() {
 #pragma unroll
@@ -196,8 +197,8 @@ static void v3_nf(const ConvParams& p, hipStream_t s) {
 }
 
 bool conv3x3_v3(const ConvParams& p, hipStream_t s) {
-  // Cin = 16 (s2d stems, YOLO's first C3) runs as one half-empty 32-channel slab
-  if (!(p.KH == 3 && p.KW == 3 && (p.stride == 1 || p.stride == 2) && (p.Cin % 32 == 0 || p.Cin == 16) &&
+  // Cin % 32 == 16 (s2d stems, YOLO's first C3, the 80-class detect branch) ends in a half-empty slab
+  if (!(p.KH == 3 && p.KW == 3 && (p.stride == 1 || p.stride == 2) && p.Cin % 16 == 0 &&
         !p.f32out && p.Kpad >= 9 * p.Cin))
     return false;
   if ((long)p.H * p.W * p.xs >= (1L << 31)) return false;  // 32-bit staging offsets

@@ -44,14 +44,17 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
     concurrent_ = cc != nullptr ? std::atoi(cc) : 1;
     if (debug_sync_) concurrent_ = 0;
     const char* ns = std::getenv("ARENA_SLOTS");
-    n_slots_ = concurrent_ ? std::min(kMaxSlots, std::max(2, ns != nullptr ? std::atoi(ns) : 3)) : 2;
+    n_slots_ = concurrent_ ? std::min(kMaxSlots, std::max(2, ns != nullptr ? std::atoi(ns) : 4)) : 2;
+    const char* nc = std::getenv("ARENA_CONCURRENCY");
+    n_streams_ = concurrent_ ? std::min(n_slots_, std::max(1, nc != nullptr ? std::atoi(nc) : 3)) : 1;
   }
   ARENA_HIP_CHECK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
   ARENA_HIP_CHECK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+  streams_[0] = compute_;
+  for (int i = 1; i < n_streams_; ++i) ARENA_HIP_CHECK(hipStreamCreateWithFlags(&streams_[i], hipStreamNonBlocking));
   for (int s = 0; s < n_slots_; ++s) {
     slots_[s].idx = s;
-    if (s == 0 || !concurrent_) slots_[s].stream = compute_;
-    else ARENA_HIP_CHECK(hipStreamCreateWithFlags(&slots_[s].stream, hipStreamNonBlocking));
+    slots_[s].stream = streams_[s % n_streams_];
   }
   alloc_slots();
   const int nthreads = std::max(1, cfg_.host_threads);
@@ -89,16 +92,16 @@ Executor::~Executor() {
   pool_cv_.notify_all();
   for (auto& t : workers_) t.join();
   hipSetDevice(cfg_.device);
-  for (int s = 0; s < n_slots_; ++s)
-    if (slots_[s].stream) hipStreamSynchronize(slots_[s].stream);
+  for (int i = 0; i < n_streams_; ++i)
+    if (streams_[i]) hipStreamSynchronize(streams_[i]);
   if (copy_) hipStreamSynchronize(copy_);
   for (auto& kv : buckets_) {
     for (int s = 0; s < n_slots_; ++s)
       if (kv.second.graph[s]) hipGraphExecDestroy(kv.second.graph[s]);
     free_arenas(kv.second);
   }
-  for (int s = 1; s < n_slots_; ++s)
-    if (slots_[s].stream && slots_[s].stream != compute_) hipStreamDestroy(slots_[s].stream);
+  for (int i = 1; i < n_streams_; ++i)
+    if (streams_[i]) hipStreamDestroy(streams_[i]);
   for (int s = 0; s < n_slots_; ++s) {
     Slot& sl = slots_[s];
     if (sl.d_in) hipFree(sl.d_in);
@@ -131,7 +134,7 @@ size_t Executor::out_off_raw() const {
 size_t Executor::out_bytes_total() const { return out_off_raw() + (size_t)cfg_.raw_out_bytes * max_B_; }
 
 void Executor::sync_slots() {
-  for (int s = 0; s < n_slots_; ++s) ARENA_HIP_CHECK(hipStreamSynchronize(slots_[s].stream));
+  for (int i = 0; i < n_streams_; ++i) ARENA_HIP_CHECK(hipStreamSynchronize(streams_[i]));
 }
 
 void Executor::free_arenas(Bucket& bk) {
@@ -648,6 +651,10 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   Slot& sl = slots_[s];
   if (sl.busy) throw std::runtime_error("submit: every staging slot is in flight; collect() first");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  // Batches go round-robin over the compute streams: batch q runs on stream q % n_streams_, behind
+  // batch q - n_streams_, so at most n_streams_ graphs execute at once while the staging (pack + H2D)
+  // of the next n_slots_ - n_streams_ batches proceeds.
+  sl.stream = streams_[seq_++ % n_streams_];
   // The slot's previous graph has been collected; its input copy was consumed.
   ImageMeta* meta = (ImageMeta*)(sl.h_in + kCtrlBytes);
   uint8_t* pool = sl.h_in + in_bytes_meta();
@@ -816,7 +823,7 @@ void Executor::replay(int B, int s, int iters) {
   if (it == buckets_.end()) throw std::runtime_error("replay: unknown bucket");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   if (s < 0 || s >= n_slots_) throw std::runtime_error("replay: bad slot");
-  for (int i = 0; i < iters; ++i) ARENA_HIP_CHECK(hipGraphLaunch(it->second.graph[s], slots_[s].stream));
+  for (int i = 0; i < iters; ++i) ARENA_HIP_CHECK(hipGraphLaunch(it->second.graph[s], streams_[s % n_streams_]));
 }
 
 void Executor::synchronize() {

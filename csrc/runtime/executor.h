@@ -15,10 +15,11 @@
 // name arena buffers by id.  For every batch bucket the executor resolves the
 // records to device pointers once and captures the whole sequence (including
 // memsets and the result D2H copy) into a hipGraph; a request batch is then
-// one H2D copy on a copy stream + one graph launch on the slot's stream.
-// Two staging slots ping-pong so batch i+1 is uploaded while batch i runs;
-// each slot owns a stream and an activation arena, so the two batches'
-// graphs also execute concurrently on the device.
+// one H2D copy on a copy stream + one graph launch on a compute stream.
+// Staging slots (pinned + device input/output, activation arena, one graph
+// per bucket) outnumber the compute streams: up to ARENA_CONCURRENCY graphs
+// execute concurrently on the device while the next batches are packed and
+// uploaded into the remaining slots.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -38,7 +39,7 @@
 namespace arena {
 
 constexpr int kOpFields = 48;
-constexpr int kMaxSlots = 4;
+constexpr int kMaxSlots = 6;
 using OpRecord = std::array<int64_t, kOpFields>;
 
 enum OpType : int64_t {
@@ -143,11 +144,13 @@ class Executor : public BatchInstance {
     uint8_t* h_in = nullptr;
     uint8_t* h_out = nullptr;
     hipEvent_t copied = nullptr, started = nullptr, done = nullptr;
-    // Each slot runs its graph on its own stream against its own activation
-    // arena, so two in-flight batches overlap on the device: the small-grid
-    // tail of one batch's layers (20x20 / 7x7 maps leave most of the 256 CUs
-    // idle) is filled by the other batch's work.
-    hipStream_t stream = nullptr;
+    // Each slot owns an activation arena; its batch runs on one of the
+    // executor's compute streams (round-robin by submission), so in-flight
+    // batches overlap on the device: the small-grid tail of one batch's layers
+    // (20x20 / 7x7 maps leave most of the 256 CUs idle) is filled by another
+    // batch's work.  More slots than streams lets the next batches' packing
+    // and H2D copies run ahead while the device is busy.
+    hipStream_t stream = nullptr;  // stream of the slot's current batch
     int idx = 0;
     bool busy = false;
     int bucket = 0;
@@ -199,10 +202,14 @@ class Executor : public BatchInstance {
   Slot slots_[kMaxSlots];
   int n_slots_ = 2;
   int next_slot_ = 0;
+  hipStream_t streams_[kMaxSlots] = {};  // compute streams (streams_[0] == compute_)
+  int n_streams_ = 1;
+  uint64_t seq_ = 0;                     // batches submitted
   bool has_topk_ = false, has_det_ = false, has_raw_ = false;
   int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on compute stream
   // ARENA_CONCURRENT: 1 = per-slot streams + arenas (in-flight batches overlap on the device),
-  // 0 = two slots serialised on one stream sharing one arena.  ARENA_SLOTS: slots when concurrent (2-3).
+  // 0 = two slots serialised on one stream sharing one arena.  ARENA_SLOTS: staging slots when concurrent
+  // (default 4), ARENA_CONCURRENCY: compute streams = graphs running at once (default 3).
   int concurrent_ = 1;
   int autotune_ = 1;  // ARENA_AUTOTUNE: 0 off, 1 on, 2 on + report
   int debug_sync_ = 0;  // ARENA_DEBUG_SYNC: 1 eager op-by-op, 2 one graph per op

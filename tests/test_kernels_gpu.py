@@ -336,14 +336,16 @@ def test_executor_autotune_choices(device):
         assert abs(len(a) - len(b)) <= 1
 
 
-@pytest.mark.parametrize("H,s", [(64, 1), (64, 2), (37, 1)])
-def test_conv3x3_v3_cin16(device, H, s):
-    """Cin = 16 (s2d stems, first C3) through the v3 halo-tile kernel as a half-empty slab."""
+@pytest.mark.parametrize("H,s,Cin,Cout", [(64, 1, 16, 32), (64, 2, 16, 32), (37, 1, 16, 32), (40, 1, 80, 80),
+                                          (21, 2, 80, 80), (20, 1, 48, 64)])
+def test_conv3x3_v3_cin16(device, H, s, Cin, Cout):
+    """Cin % 32 == 16 (s2d stems, first C3, the 80-class detect branch) through the v3 halo-tile kernel:
+    the last 32-channel slab is half empty."""
     C = native()
-    g = torch.Generator().manual_seed(H * 3 + s)
-    x = torch.randn(2, 16, H, H, generator=g)
-    w = torch.randn(32, 16, 3, 3, generator=g) / 12
-    b = torch.randn(32, generator=g) * 0.1
+    g = torch.Generator().manual_seed(H * 3 + s + Cin)
+    x = torch.randn(2, Cin, H, H, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / np.sqrt(Cin * 9)
+    b = torch.randn(Cout, generator=g) * 0.1
     xn = _nhwc(x).to(torch.bfloat16).to(device)
     old = C.get_conv_impl()
     C.set_conv_impl(2)

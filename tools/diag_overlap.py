@@ -80,6 +80,32 @@ def main(argv=None) -> int:
     out["submit_host_ms_p50"] = float(np.median(sub) * 1e3)
     out["collect_wait_ms_p50"] = float(np.median(col) * 1e3)
     out["image_bytes_per_batch_MB"] = sum(i.nbytes for i in imgs) / 2**20
+    # raw H2D bandwidth from pinned memory (the executor's staging path), alone and under compute
+    nb = sum(i.nbytes for i in imgs)
+    src = torch.empty(nb, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.Stream()
+    for _ in range(3):
+        with torch.cuda.stream(st):
+            dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(st):
+        e0.record(st)
+        for _ in range(10):
+            dst.copy_(src, non_blocking=True)
+        e1.record(st)
+    torch.cuda.synchronize()
+    out["h2d_GBps_idle"] = nb * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    ex.replay(B, 1, 4)
+    with torch.cuda.stream(st):
+        e0.record(st)
+        for _ in range(10):
+            dst.copy_(src, non_blocking=True)
+        e1.record(st)
+    torch.cuda.synchronize()
+    ex.synchronize()
+    out["h2d_GBps_under_compute"] = nb * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
     print(json.dumps({k: round(v, 3) for k, v in out.items()}), flush=True)
     return 0
 
