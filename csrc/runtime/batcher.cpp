@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cstring>
 
+#include "trace.h"
+
 namespace arena {
 
 using clk = std::chrono::steady_clock;
@@ -161,6 +163,7 @@ void DynamicBatcher::instance_loop(int idx) {
           imgs.push_back(im);
         }
         try {
+          trace::mark("arena.batch");
           const auto t = clk::now();
           const int slot = ex.submit(imgs);
           pending.push_back(InFlight{slot, std::move(b), t});
@@ -179,6 +182,7 @@ void DynamicBatcher::instance_loop(int idx) {
     pending.pop_front();
     try {
       BatchResult r = ex.collect(f.slot);
+      trace::Range tf("arena.batcher.callbacks");
       finish(f.batch, r, f.t_submit, (size_t)std::max<int64_t>(0, ex.raw_out_bytes()));
     } catch (const std::exception& e) {
       fail(f.batch, e.what());

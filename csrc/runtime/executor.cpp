@@ -13,6 +13,7 @@
 #include <string>
 
 #include "../kernels/common.h"
+#include "trace.h"
 
 namespace arena {
 
@@ -642,6 +643,7 @@ void Executor::enqueue_results_d2h(Bucket& bk, Slot& sl, int n) {
 }
 
 int Executor::submit(const std::vector<InputImage>& imgs) {
+  trace::Range tr("arena.submit");
   std::lock_guard<std::mutex> lk(mu_);
   const int n = (int)imgs.size();
   if (n <= 0) throw std::runtime_error("submit: empty batch");
@@ -687,7 +689,10 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     }
     off = align_up(off + bytes, 256);
   }
-  parallel_copy(jobs);
+  {
+    trace::Range tp("arena.pack");
+    parallel_copy(jobs);
+  }
   Ctrl* ctrl = (Ctrl*)sl.h_in;
   std::memset(ctrl, 0, sizeof(Ctrl));
   ctrl->n_images = n;
@@ -766,7 +771,11 @@ BatchResult Executor::collect(int s) {
   Slot& sl = slots_[s];
   if (!sl.busy) throw std::runtime_error("collect: slot not in flight");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
-  ARENA_HIP_CHECK(hipEventSynchronize(sl.done));
+  {
+    trace::Range tw("arena.collect.wait");
+    ARENA_HIP_CHECK(hipEventSynchronize(sl.done));
+  }
+  trace::Range tu("arena.collect.unpack");
   BatchResult res;
   res.n_images = sl.n_images;
   res.bucket = sl.bucket;

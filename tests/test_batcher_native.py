@@ -16,7 +16,8 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SRCS = [ROOT / "csrc" / "tests" / "batcher_stress.cpp", ROOT / "csrc" / "runtime" / "batcher.cpp"]
+SRCS = [ROOT / "csrc" / "tests" / "batcher_stress.cpp", ROOT / "csrc" / "runtime" / "batcher.cpp",
+        ROOT / "csrc" / "runtime" / "trace.cpp"]
 
 
 def _build(sanitizer: str) -> Path:
@@ -28,7 +29,7 @@ def _build(sanitizer: str) -> Path:
     if not out.exists() or out.stat().st_mtime < newest:
         # host code only: each -fsanitize= goes right after -Xarch_host
         cmd = [HIPCC, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", f"-fsanitize={sanitizer}",
-               "-I" + str(ROOT / "csrc"), *map(str, SRCS), "-o", str(out)]
+               "-I" + str(ROOT / "csrc"), *map(str, SRCS), "-ldl", "-o", str(out)]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-4000:]
     return out

@@ -68,6 +68,11 @@ def main(argv=None) -> int:
         replays += [q[s:s + n_ops] for s in starts if s + n_ops <= len(q)]
     replays = [rp for rp in replays if len(rp) == n_ops]
     replays.sort(key=lambda rp: int(rp[0]["Start_Timestamp"]))
+    # keep replays whose kernel sequence matches the program's final one (drops slices that straddle
+    # autotuning / overflow passes), then use per-op medians
+    if replays:
+        ref = [r["Kernel_Name"] for r in replays[-1]]
+        replays = [rp for rp in replays if [r["Kernel_Name"] for r in rp] == ref]
     replays = replays[-a.replays:]
     if not replays:
         print("no complete replay found", file=sys.stderr)
@@ -76,12 +81,13 @@ def main(argv=None) -> int:
     for rp in replays:
         for k, r in enumerate(rp):
             dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    total = sum(sum(v) / len(v) for v in dur.values())
+    med = {k: sorted(v)[len(v) // 2] for k, v in dur.items()}
+    total = sum(med.values())
     lines = ["| op | kind | shape | kernel | vgpr | grid | mean us | share |", "|---|---|---|---|---|---|---|---|"]
     per_kind = defaultdict(float)
     for k in range(n_ops):
         r = replays[-1][k]
-        us = sum(dur[k]) / len(dur[k])
+        us = med[k]
         kind = KIND.get(int(prog.ops[k][0]), "?")
         per_kind[kind] += us
         name = r["Kernel_Name"].replace("void arena::", "").replace("arena::", "").split("(")[0]
@@ -89,7 +95,7 @@ def main(argv=None) -> int:
         lines.append(f"| {k} | {kind} | {describe(prog.ops[k])} | {name} | {r['VGPR_Count']}+{r['Accum_VGPR_Count']} "
                      f"| {grid} | {us:.1f} | {100 * us / total:.1f}% |")
     lines.append("")
-    lines.append(f"replays averaged: {len(replays)}; device time per replay: {total:.1f} us")
+    lines.append(f"replays: {len(replays)} (per-op medians); device time per replay: {total:.1f} us")
     lines.append("")
     lines.append("| kind | us per replay | share |")
     lines.append("|---|---|---|")

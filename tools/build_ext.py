@@ -42,6 +42,7 @@ SOURCES = [
     "kernels/classify_head.hip",
     "runtime/executor.cpp",
     "runtime/batcher.cpp",
+    "runtime/trace.cpp",
     "runtime/probe.hip",
     "bindings.cpp",
 ]
@@ -108,7 +109,7 @@ def build(force: bool = False, verbose: bool = False, jobs: int | None = None) -
             for f in futs:
                 f.result()
     if work or force or not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
-        link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(out)] + [str(o) for o in objs]
+        link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(out)] + [str(o) for o in objs] + ["-ldl"]
         tl = _torch_lib()
         if tl:
             link += [f"-Wl,-rpath,{tl}"]
