@@ -75,12 +75,35 @@ struct Src {
 
 }  // namespace
 
+// Source pixels a tile samples are first copied into LDS with aligned dword
+// loads (a 640x480 image at scale 1 needs ~21 rows x 69 px = 4.3 KB per
+// 8x32 tile), then the bilinear taps read LDS bytes: one global dword load
+// per 4 source bytes instead of 12 byte loads per sub-pixel.  Regions above
+// the budget (strongly downscaled images, large crops) sample global memory.
+constexpr int kSrcBudget = 16384;
+
+// rows r0/r1 of the staged region start `s0`/`s1` bytes into their LDS row (dword alignment shift)
+__device__ __forceinline__ void sample_rgb_lds2(const uint8_t* reg, int pitch, int r0, int r1, int s0, int s1, int x0,
+                                                int x1, float fy, float fx, float* rgb) {
+  const uint8_t* p0 = reg + r0 * pitch + s0;
+  const uint8_t* p1 = reg + r1 * pitch + s1;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float a = (float)p0[x0 + c], b = (float)p0[x1 + c];
+    const float d = (float)p1[x0 + c], e = (float)p1[x1 + c];
+    const float top = a + (b - a) * fx;
+    const float bot = d + (e - d) * fx;
+    rgb[c] = floorf(top + (bot - top) * fy + 0.5f);
+  }
+}
+
 template <int SRC, int KS, int NF, int TH, int TW>
 __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p) {
   constexpr int HH = TH + KS - 1, HW = TW + KS - 1, NPIX = HH * HW;
   constexpr int SLABS = (KS * KS * 16 + 31) / 32;
   static_assert(TH * TW == 256, "one 256-pixel tile per workgroup (4 waves x 4 fragments)");
   __shared__ __align__(16) uint4 tile[NPIX * 2];  // 32 B per s2d pixel
+  __shared__ __align__(16) uint32_t region[kSrcBudget / 4];
 
   const int S2 = p.S >> 1;
   const int tiles_x = (S2 + TW - 1) / TW, tiles_y = (S2 + TH - 1) / TH, ntiles = tiles_x * tiles_y;
@@ -119,6 +142,36 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
     g.sx = g.empty ? 1.f : (float)((double)cw / (double)p.S);
   }
 
+  // ---- phase 0: source rows / columns this tile samples -> LDS (when they fit)
+  // sub-pixel rows/cols of the halo tile, clamped to the sampled area
+  const int lim_y = SRC == 0 ? g.h : p.S, lim_x = SRC == 0 ? g.w : p.S;
+  const int sy_lo = max(2 * (ty0 - 1) - g.pad_h, 0), sy_hi = min(2 * (ty0 + TH) + 1 - g.pad_h, lim_y - 1);
+  const int sx_lo = max(2 * (tx0 - 1) - g.pad_w, 0), sx_hi = min(2 * (tx0 + TW) + 1 - g.pad_w, lim_x - 1);
+  bool staged = false;
+  int r_lo = 0, c_lo = 0, pitch = 0;
+  const size_t row_bytes = (size_t)g.stride_px * 3;
+  if (!g.empty && sy_lo <= sy_hi && sx_lo <= sx_hi) {
+    r_lo = tap_of(sy_lo, g.sy, g.rh).i0;
+    c_lo = tap_of(sx_lo, g.sx, g.rw).i0;
+    const int r_hi = tap_of(sy_hi, g.sy, g.rh).i1, c_hi = tap_of(sx_hi, g.sx, g.rw).i1;
+    const int nrows = r_hi - r_lo + 1, rbytes = (c_hi - c_lo + 1) * 3;
+    const int ndw = (rbytes + 3 + 3) >> 2;  // up to 3 bytes of alignment shift in front
+    pitch = ndw * 4;
+    staged = nrows * pitch <= kSrcBudget;
+    if (staged) {
+      const uint8_t* base = g.img + (size_t)r_lo * row_bytes + (size_t)c_lo * 3;
+      for (int i = threadIdx.x; i < nrows * ndw; i += 256) {
+        const int r = i / ndw, k = i - (i / ndw) * ndw;
+        const uint8_t* src = base + (size_t)r * row_bytes;
+        const uint32_t* a = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
+        region[r * ndw + k] = a[k];
+      }
+      __syncthreads();
+    }
+  }
+  const uint8_t* reg = (const uint8_t*)region;
+  const uintptr_t base_addr = (uintptr_t)(g.img + (size_t)r_lo * row_bytes + (size_t)c_lo * 3);
+
   // ---- phase 1: s2d halo tile into LDS
   for (int i = threadIdx.x; i < NPIX; i += 256) {
     const int hy = i / HW, hx = i - (i / HW) * HW;
@@ -134,13 +187,32 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
         if constexpr (SRC == 0) {
           const int dy = oy - g.pad_h, dx = ox - g.pad_w;
           rgb[0] = rgb[1] = rgb[2] = 114.f;
-          if (dy >= 0 && dy < g.h && dx >= 0 && dx < g.w)
-            sample_rgb(g.img, g.stride_px, tap_of(dy, g.sy, g.rh), tap_of(dx, g.sx, g.rw), rgb);
+          if (dy >= 0 && dy < g.h && dx >= 0 && dx < g.w) {
+            const LinTap2 ty = tap_of(dy, g.sy, g.rh), tx = tap_of(dx, g.sx, g.rw);
+            if (staged) {
+              const int r0 = ty.i0 - r_lo, r1 = ty.i1 - r_lo;
+              const int s0 = (int)((base_addr + (size_t)r0 * row_bytes) & 3), s1 = (int)((base_addr + (size_t)r1 * row_bytes) & 3);
+              const int x0 = (tx.i0 - c_lo) * 3, x1 = (tx.i1 - c_lo) * 3;
+              sample_rgb_lds2(reg, pitch, r0, r1, s0, s1, x0, x1, ty.f, tx.f, rgb);
+            } else {
+              sample_rgb(g.img, g.stride_px, ty, tx, rgb);
+            }
+          }
 #pragma unroll
           for (int c = 0; c < 3; ++c) out[pq * 3 + c] = rgb[c] * (1.0f / 255.0f);
         } else {
           rgb[0] = rgb[1] = rgb[2] = 0.f;
-          if (!g.empty) sample_rgb(g.img, g.stride_px, tap_of(oy, g.sy, g.rh), tap_of(ox, g.sx, g.rw), rgb);
+          if (!g.empty) {
+            const LinTap2 ty = tap_of(oy, g.sy, g.rh), tx = tap_of(ox, g.sx, g.rw);
+            if (staged) {
+              const int r0 = ty.i0 - r_lo, r1 = ty.i1 - r_lo;
+              const int s0 = (int)((base_addr + (size_t)r0 * row_bytes) & 3), s1 = (int)((base_addr + (size_t)r1 * row_bytes) & 3);
+              const int x0 = (tx.i0 - c_lo) * 3, x1 = (tx.i1 - c_lo) * 3;
+              sample_rgb_lds2(reg, pitch, r0, r1, s0, s1, x0, x1, ty.f, tx.f, rgb);
+            } else {
+              sample_rgb(g.img, g.stride_px, ty, tx, rgb);
+            }
+          }
 #pragma unroll
           for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (rgb[c] * (1.0f / 255.0f) - p.mean[c]) * p.inv_std[c];
         }

@@ -151,7 +151,9 @@ void Executor::free_arenas(Bucket& bk) {
 void Executor::alloc_slots() {
   for (int s = 0; s < n_slots_; ++s) {
     Slot& sl = slots_[s];
-    ARENA_HIP_CHECK(hipMalloc(&sl.d_in, in_bytes_total()));
+    // +256 B slack: the fused stem kernels fetch source image rows as aligned dwords, which may
+    // run up to 3 bytes past the last image of a full staging pool
+    ARENA_HIP_CHECK(hipMalloc(&sl.d_in, in_bytes_total() + 256));
     ARENA_HIP_CHECK(hipMalloc(&sl.d_out, out_bytes_total()));
     ARENA_HIP_CHECK(hipHostMalloc(&sl.h_in, in_bytes_total(), hipHostMallocDefault));
     ARENA_HIP_CHECK(hipHostMalloc(&sl.h_out, out_bytes_total(), hipHostMallocDefault));
