@@ -14,6 +14,8 @@
 // Counters on v2 (same tiling, addresses recomputed per access, no prefetch)
 // showed ~11 VALU instructions per MFMA: address/index math, not MFMA, set
 // the pace.  v3 cuts that to a few per slab.
+#include <cstdlib>
+
 #include "common.h"
 #include "launch.h"
 
@@ -184,10 +186,25 @@ static void v3_launch(const ConvParams& p, hipStream_t s) {
   hipLaunchKernelGGL((conv3x3_v3_kernel<S, MF, NF>), grid, dim3(256), 0, s, p);
 }
 
+static int v3_max_mf() {
+  static const int v = [] {
+    const char* e = std::getenv("ARENA_V3_MF");
+    return e != nullptr ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
 template <int S, int NF>
 static void v3_nf(const ConvParams& p, hipStream_t s) {
-  const long blocks2 = (long)p.B * ((p.Wo + 15) / 16) * ((p.Ho + 7) / 8) * ((p.Cout_pad + NF * 16 - 1) / (NF * 16));
+  const long ngrp = (p.Cout_pad + NF * 16 - 1) / (NF * 16);
+  const long blocks2 = (long)p.B * ((p.Wo + 15) / 16) * ((p.Ho + 7) / 8) * ngrp;
+  const long blocks4 = (long)p.B * ((p.Wo + 15) / 16) * ((p.Ho + 15) / 16) * ngrp;
   if constexpr (S == 1) {
+    // 4 output rows per wave: ~2x the MFMAs per staged slab, fewer halo re-reads (LDS 36 KB input tile)
+    if (v3_max_mf() >= 4 && p.Ho >= 32 && blocks4 >= 512) {
+      v3_launch<S, 4, NF>(p, s);
+      return;
+    }
     if (p.Ho >= 16 && blocks2 >= 512) {
       v3_launch<S, 2, NF>(p, s);
       return;
