@@ -18,8 +18,10 @@ Layout (same as the reference's bucket / Triton repository)::
     <root>/arena_pipeline/1/
 
 Weights are safetensors (torch state_dict of the unfolded network, loaded
-without executing anything from the file); MinIO is replaced by a
-local-filesystem store (``sync`` copies between two repositories).
+without executing anything from the file).  The repository lives on a local
+or shared filesystem (``sync`` copies between two repositories) and can be
+pushed to / pulled from a MinIO or S3 bucket with the same keys
+(``repository/s3.py``: SigV4-signed REST, no SDK).
 """
 from __future__ import annotations
 

@@ -21,7 +21,22 @@ def main(argv=None) -> int:
     ap.add_argument("--arch", required=True, choices=["monolithic", "microservices", "triton"])
     ap.add_argument("--repository", default="model_repository")
     ap.add_argument("--dst", required=True)
+    ap.add_argument("--s3", action="store_true",
+                    help="first fetch the repository from the MinIO/S3 bucket (experiment.yaml infrastructure.minio, "
+                         "MINIO_* env overrides) into --repository, like the reference's init containers")
+    ap.add_argument("--bucket", default=None)
     a = ap.parse_args(argv)
+    if a.s3:
+        import os
+
+        from inference_arena_amd.config import get_minio_config
+        from inference_arena_amd.repository.s3 import S3Client, download_repository
+
+        client = S3Client.from_config()
+        bucket = a.bucket or os.environ.get("MINIO_BUCKET") or get_minio_config().get("bucket", "models")
+        client.wait_ready(bucket)
+        got = download_repository(client, bucket, a.repository)
+        print(f"fetched {len(got)} object(s) from s3://{bucket} -> {a.repository}")
     bad = {k: v for k, v in verify_repository(a.repository).items() if v}
     if bad:
         print(f"repository problems: {bad}", file=sys.stderr)

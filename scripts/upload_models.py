@@ -28,6 +28,11 @@ def main(argv=None) -> int:
     ap.add_argument("--reference-compat", action="store_true",
                     help="configs exactly like the reference (max_batch_size 0, no dynamic batching)")
     ap.add_argument("--from", dest="src", default=None, help="copy this repository instead of exporting")
+    ap.add_argument("--s3", action="store_true",
+                    help="also upload the repository to the MinIO/S3 bucket of experiment.yaml infrastructure.minio "
+                         "(MINIO_* env overrides; skip-if-present unless --force)")
+    ap.add_argument("--bucket", default=None, help="bucket (default: infrastructure.minio.bucket / MINIO_BUCKET)")
+    ap.add_argument("--endpoint", default=None, help="S3 endpoint host:port (default: MINIO_INTERNAL_ENDPOINT)")
     a = ap.parse_args(argv)
     if not a.verify:
         if a.src:
@@ -39,7 +44,21 @@ def main(argv=None) -> int:
     problems = verify_repository(a.repository)
     for name, p in problems.items():
         print(f"{name}: {'OK' if not p else '; '.join(p)}")
-    return 1 if any(problems.values()) else 0
+    if any(problems.values()):
+        return 1
+    if a.s3 and not a.verify:
+        import os
+
+        from inference_arena_amd.config import get_minio_config
+        from inference_arena_amd.repository.s3 import S3Client, upload_repository
+
+        client = S3Client.from_config(endpoint=a.endpoint)
+        bucket = a.bucket or os.environ.get("MINIO_BUCKET") or get_minio_config().get("bucket", "models")
+        client.wait_ready(bucket)
+        done = upload_repository(a.repository, client, bucket, force=a.force)
+        n_up = sum(1 for v in done.values() if v == "uploaded")
+        print(f"s3://{bucket}: {n_up} uploaded, {len(done) - n_up} already present")
+    return 0
 
 
 if __name__ == "__main__":

@@ -144,7 +144,8 @@ def test_env_template_keys_are_known_settings():
     env = _read_dotenv(ROOT / ".env.example")
     known = set(Settings.model_fields) | {"ARENA_FUSE_IR", "ARENA_CONV_IMPL", "HSA_ENABLE_IPC_MODE_LEGACY",
                                           "MASTER_ADDR", "GRAFANA_ADMIN_USER", "GRAFANA_ADMIN_PASSWORD",
-                                          "PROMETHEUS_PORT", "GRAFANA_PORT"}
+                                          "PROMETHEUS_PORT", "GRAFANA_PORT", "MINIO_INTERNAL_ENDPOINT",
+                                          "MINIO_ACCESS_KEY", "MINIO_SECRET_KEY", "MINIO_BUCKET", "MINIO_SECURE"}
     assert set(env) <= known, set(env) - known
     # the template's values are valid settings (inline comments stripped)
     s = Settings(**{k: v for k, v in env.items() if k in Settings.model_fields})
