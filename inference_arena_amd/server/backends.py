@@ -71,6 +71,13 @@ class GpuBatchedBackend(Backend):
                                     max_queue_delay_us=max_queue_delay_us, max_queue_size=max_queue_size)
         self.device = device
 
+    def ready(self) -> bool:
+        return self.batcher.healthy
+
+    @property
+    def device_error(self) -> str | None:
+        return self.batcher.device_error
+
     async def infer(self, image: np.ndarray) -> tuple[ImageResult, dict]:
         t0 = time.perf_counter()
         d = await self.batcher.run(np.ascontiguousarray(image, dtype=np.uint8))

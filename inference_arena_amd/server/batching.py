@@ -20,6 +20,13 @@ class Overloaded(RuntimeError):
     """The request queue is full (HTTP 503 / gRPC RESOURCE_EXHAUSTED)."""
 
 
+def is_device_fault(message: str) -> bool:
+    """A HIP runtime error (ARENA_HIP_CHECK in csrc/kernels/common.h): the device context of this
+    process is no longer trustworthy, so the instance must be taken out of service (SURVEY.md §5
+    failure detection: "a HIP error marks the instance unhealthy")."""
+    return message.startswith("HIP error")
+
+
 class AsyncBatcher:
     def __init__(self, runners, *, max_batch: int, preferred: list[int] | None = None,
                  max_queue_delay_us: int = 500, max_queue_size: int = 4096):
@@ -34,6 +41,19 @@ class AsyncBatcher:
             "max_queue_size": int(max_queue_size),
         })
         self._closed = False
+        self.device_error: str | None = None  # first HIP error seen; the instance is unhealthy from then on
+
+    def _check(self, d: dict) -> dict:
+        err = d["error"]
+        if err:
+            if self.device_error is None and is_device_fault(err):
+                self.device_error = err
+            raise RuntimeError(err)
+        return d
+
+    @property
+    def healthy(self) -> bool:
+        return self.device_error is None
 
     @staticmethod
     def _prep(x: np.ndarray) -> np.ndarray:
@@ -50,10 +70,7 @@ class AsyncBatcher:
 
         if self._b.enqueue(self._prep(x), done) < 0:
             raise Overloaded("inference queue full")
-        d = await fut
-        if d["error"]:
-            raise RuntimeError(d["error"])
-        return d
+        return self._check(await fut)
 
     async def run_many(self, xs: list[np.ndarray]) -> list[dict]:
         return list(await asyncio.gather(*(self.run(x) for x in xs)))
@@ -70,10 +87,7 @@ class AsyncBatcher:
             raise Overloaded("inference queue full")
         if not ev.wait(timeout):
             raise TimeoutError("inference timed out")
-        d = box[0]
-        if d["error"]:
-            raise RuntimeError(d["error"])
-        return d
+        return self._check(box[0])
 
     def stats(self) -> dict:
         return dict(self._b.stats())

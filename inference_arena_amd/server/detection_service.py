@@ -21,7 +21,7 @@ import logging
 from contextlib import asynccontextmanager
 
 from fastapi import FastAPI, HTTPException, Request
-from fastapi.responses import Response
+from fastapi.responses import JSONResponse, Response
 
 from ..metrics import ArenaMetrics
 from ..processing import extract_crop
@@ -124,8 +124,10 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
     async def health():
         request_id_var.set(None)
         cl = state.get("client")
-        return HealthResponse(status="healthy",
-                              models_loaded=state.get("detector") is not None and cl is not None and cl.connected)
+        det = state.get("detector")
+        if det is not None and getattr(det, "device_error", None):
+            return JSONResponse(status_code=503, content={"status": "unhealthy", "models_loaded": False})
+        return HealthResponse(status="healthy", models_loaded=det is not None and cl is not None and cl.connected)
 
     @app.get("/metrics")
     async def metrics_ep():

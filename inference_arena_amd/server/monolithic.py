@@ -15,7 +15,7 @@ import logging
 from contextlib import asynccontextmanager
 
 from fastapi import FastAPI, HTTPException, Request
-from fastapi.responses import Response
+from fastapi.responses import JSONResponse, Response
 
 from ..labels import load_labels
 from ..metrics import ArenaMetrics
@@ -88,6 +88,9 @@ def create_app(settings: Settings | None = None, backend: Backend | None = None)
     async def health():
         request_id_var.set(None)
         be = state.get("backend")
+        if be is not None and getattr(be, "device_error", None):
+            # device fault: 503 so probes / the replica router take this instance out of rotation
+            return JSONResponse(status_code=503, content={"status": "unhealthy", "models_loaded": False})
         return HealthResponse(status="healthy", models_loaded=be is not None and be.ready())
 
     @app.get("/metrics")

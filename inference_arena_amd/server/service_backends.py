@@ -57,6 +57,13 @@ class GpuClassifierBackend(ClassifierBackend):
         self.batcher = AsyncBatcher(self.runners, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us)
 
+    def ready(self) -> bool:
+        return self.batcher.healthy
+
+    @property
+    def device_error(self) -> str | None:
+        return self.batcher.device_error
+
     async def classify(self, crop: np.ndarray):
         d = await self.batcher.run(np.ascontiguousarray(crop, dtype=np.uint8))
         return d["topk_idx"][0], d["topk_logit"][0], d["topk_prob"][0]
@@ -126,6 +133,13 @@ class GpuDetectorBackend(DetectorBackend):
         self.runners = [GpuDetector(yolo, device=device, buckets=bk) for _ in range(instances)]
         self.batcher = AsyncBatcher(self.runners, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us)
+
+    def ready(self) -> bool:
+        return self.batcher.healthy
+
+    @property
+    def device_error(self) -> str | None:
+        return self.batcher.device_error
 
     async def detect(self, image: np.ndarray):
         d = await self.batcher.run(np.ascontiguousarray(image, dtype=np.uint8))

@@ -91,3 +91,40 @@ def test_cpu_reference_backend_end_to_end(models):
         r = c.post("/predict", content=body, headers={"content-type": ctype})
         assert r.status_code == 200, r.text
         assert r.json()["timing"]["total_ms"] > 0
+
+
+def test_device_fault_marks_instance_unhealthy():
+    """A HIP error from the native batcher takes the instance out of rotation: /health -> 503
+    (the replica router drops it), while ordinary request errors do not."""
+    from inference_arena_amd.server.batching import AsyncBatcher, is_device_fault
+
+    class FakeNativeBatcher:
+        def __init__(self):
+            self.errors = []
+
+        def enqueue(self, x, cb):
+            cb({"error": self.errors.pop(0) if self.errors else "", "det": np.zeros((0, 6), np.float32)})
+            return 1
+
+    ab = AsyncBatcher.__new__(AsyncBatcher)
+    ab._b, ab._closed, ab.device_error = FakeNativeBatcher(), False, None
+    ab._b.errors = ["submit: batch exceeds the staging pool",
+                    "HIP error an illegal memory access was encountered at executor.cpp:700"]
+    with pytest.raises(RuntimeError, match="staging pool"):
+        ab.run_sync(np.zeros((2, 2, 3), np.uint8))
+    assert ab.healthy
+    with pytest.raises(RuntimeError, match="HIP error"):
+        ab.run_sync(np.zeros((2, 2, 3), np.uint8))
+    assert not ab.healthy and is_device_fault(ab.device_error)
+
+    class FaultedBackend(FakeBackend):
+        device_error = "HIP error hipErrorLaunchFailure"
+
+        def ready(self):
+            return False
+
+    with _client(FaultedBackend()) as c:
+        r = c.get("/health")
+        assert r.status_code == 503 and r.json() == {"status": "unhealthy", "models_loaded": False}
+    with _client(FakeBackend()) as c:
+        assert c.get("/health").json() == {"status": "healthy", "models_loaded": True}
