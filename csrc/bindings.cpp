@@ -73,6 +73,13 @@ void py_conv2d(const py::dict& d) {
   p.f32out = get<int>(d, "f32out", 0);
   p.bdev = ptr<const int*>(d, "bdev");
   p.impl = get<int>(d, "impl", 0);
+  p.pw_w = ptr<const void*>(d, "pw_w");
+  p.pw_bias = ptr<const float*>(d, "pw_bias");
+  p.pw_y = ptr<void*>(d, "pw_y");
+  p.pw_ys = get<int>(d, "pw_ys", 0);
+  p.pw_cout = get<int>(d, "pw_cout", 0);
+  p.pw_kpad = get<int>(d, "pw_kpad", 0);
+  p.pw_act = get<int>(d, "pw_act", 0);
   conv2d(p, stream_of(d));
 }
 

@@ -39,7 +39,9 @@ __device__ __forceinline__ int v3swz(int pix, int chunk) {
   return (chunk ^ ((0x78 >> (((pix >> 2) & 3) * 2)) & 3)) << 4;
 }
 
-template <int S, int MF, int NF>
+// PWNF > 0: a pointwise conv (PWNF*16 -> PWNF*16 channels, K = PWNF*16 padded to 32) runs on the
+// activated 3x3 tile in the epilogue (Detect head: 3x3 -> 1x1 without the intermediate round trip).
+template <int S, int MF, int NF, int PWNF = 0>
 __global__ __launch_bounds__(256) void conv3x3_v3_kernel(const ConvParams p) {
   using G = V3Geom<S, MF, NF>;
   constexpr int TH = G::TH, BN = G::BN, IC = G::IC, ICP = G::ICP;
@@ -142,6 +144,71 @@ __global__ __launch_bounds__(256) void conv3x3_v3_kernel(const ConvParams p) {
     }
   }
 
+  if constexpr (PWNF > 0) {
+    // ---- fused pointwise: H = act(acc + bias) -> LDS [slab][pixel][32 ch] (swizzled 64-B rows, reusing the
+    // weight area), then pw_y = W2 . H + b2 with this wave's own pixels as the B operand.
+    static_assert(NF == PWNF, "the 3x3 tile must cover every input channel of the pointwise conv");
+    constexpr int NPX = TH * 16, SL2 = (PWNF * 16 + 31) / 32;
+    static_assert(SL2 * NPX * 64 <= G::W_BYTES, "H tile must fit the weight area");
+    __syncthreads();  // every wave is done with the last slab's weights
+    for (int i = tid; i < SL2 * NPX * 4; i += 256) *(uint4*)(sw + i * 16) = uint4{0u, 0u, 0u, 0u};
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int cb = j * 16 + kq * 4;
+      const float4 bias = *(const float4*)(p.bias + cb);
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        const int P = (wave * MF + f) * 16 + col;
+        float v[4] = {acc[j][f][0] + bias.x, acc[j][f][1] + bias.y, acc[j][f][2] + bias.z, acc[j][f][3] + bias.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+        *(uint2*)(sw + (cb >> 5) * NPX * 64 + P * 64 + ((((cb & 31) >> 3) ^ ((0x78 >> (((P >> 2) & 3) * 2)) & 3)) << 4) +
+                  (cb & 7) * 2) = pack4(v);
+      }
+    }
+    __syncthreads();
+    const bf16* __restrict__ w2 = (const bf16*)p.pw_w;
+    f32x4 acc2[PWNF][MF];
+#pragma unroll
+    for (int n = 0; n < PWNF; ++n)
+#pragma unroll
+      for (int f = 0; f < MF; ++f) acc2[n][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sl = 0; sl < SL2; ++sl) {
+      bf16x8 hb[MF];
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        const int P = (wave * MF + f) * 16 + col;
+        hb[f] = *(const bf16x8*)(sw + sl * NPX * 64 + P * 64 + ((kq ^ ((0x78 >> (((P >> 2) & 3) * 2)) & 3)) << 4));
+      }
+#pragma unroll
+      for (int n = 0; n < PWNF; ++n) {
+        const bf16x8 a = *(const bf16x8*)(w2 + (size_t)(n * 16 + col) * p.pw_kpad + sl * 32 + kq * 8);
+#pragma unroll
+        for (int f = 0; f < MF; ++f) acc2[n][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hb[f], acc2[n][f], 0, 0, 0);
+      }
+    }
+    const int oxp = tx0 + col;
+#pragma unroll
+    for (int n = 0; n < PWNF; ++n) {
+      const int oc = n * 16 + kq * 4;
+      if (oc >= p.pw_cout) continue;
+      const float4 b2 = *(const float4*)(p.pw_bias + oc);
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        const int oy = ty0 + wave * MF + f;
+        if (oy >= p.Ho || oxp >= p.Wo) continue;
+        const size_t pix = ((size_t)b * p.Ho + oy) * p.Wo + oxp;
+        float v[4] = {acc2[n][f][0] + b2.x, acc2[n][f][1] + b2.y, acc2[n][f][2] + b2.z, acc2[n][f][3] + b2.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.pw_act);
+        *(uint2*)((bf16*)p.pw_y + pix * p.pw_ys + oc) = pack4(v);
+      }
+    }
+    return;
+  }
+
   // ---- epilogue
   const int ox = tx0 + col;
 #pragma unroll
@@ -183,6 +250,16 @@ static void v3_launch(const ConvParams& p, hipStream_t s) {
   constexpr int TH = 4 * MF;
   const int tiles = ((p.Wo + 15) / 16) * ((p.Ho + TH - 1) / TH);
   dim3 grid(p.B * tiles, (p.Cout_pad + NF * 16 - 1) / (NF * 16));
+  if (p.pw_w != nullptr) {
+    if constexpr (S == 1 && MF <= 2 && (NF == 4 || NF == 5)) {
+      if (grid.y != 1 || p.pw_cout > NF * 16 || p.pw_kpad != (NF * 16 + 31) / 32 * 32 || p.res != nullptr ||
+          p.y2 != nullptr || p.f32out)
+        throw std::runtime_error("conv3x3_v3: unsupported fused pointwise geometry");
+      hipLaunchKernelGGL((conv3x3_v3_kernel<S, MF, NF, NF>), grid, dim3(256), 0, s, p);
+      return;
+    }
+    throw std::runtime_error("conv3x3_v3: fused pointwise needs stride 1 and 64 or 80 channels");
+  }
   hipLaunchKernelGGL((conv3x3_v3_kernel<S, MF, NF>), grid, dim3(256), 0, s, p);
 }
 
@@ -201,7 +278,7 @@ static void v3_nf(const ConvParams& p, hipStream_t s) {
   const long blocks4 = (long)p.B * ((p.Wo + 15) / 16) * ((p.Ho + 15) / 16) * ngrp;
   if constexpr (S == 1) {
     // 4 output rows per wave: ~2x the MFMAs per staged slab, fewer halo re-reads (LDS 36 KB input tile)
-    if (v3_max_mf() >= 4 && p.Ho >= 32 && blocks4 >= 512) {
+    if (v3_max_mf() >= 4 && p.pw_w == nullptr && p.Ho >= 32 && blocks4 >= 512) {
       v3_launch<S, 4, NF>(p, s);
       return;
     }

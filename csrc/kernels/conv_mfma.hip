@@ -576,6 +576,10 @@ void conv2d(const ConvParams& p, hipStream_t s) {
   const long M = (long)p.B * p.Ho * p.Wo;
   if (M <= 0) return;
   if (M > 0x7fffffffL) throw std::runtime_error("conv2d: M overflows int");
+  if (p.pw_w != nullptr) {  // fused pointwise epilogue: only the v3 halo-tile kernel implements it
+    if (!conv3x3_v3(p, s)) throw std::runtime_error("conv2d: fused pointwise epilogue needs a v3-eligible 3x3 conv");
+    return;
+  }
   const int impl = p.impl ? p.impl : conv_impl();
   if (impl == 3) {
     conv_igemm(p, s);

@@ -37,6 +37,12 @@ struct ConvParams {
   int f32out;   // store fp32 instead of bf16
   const int* bdev;  // optional live batch count on device
   int impl;         // kernel family for this call (0 = process default, see set_conv_impl)
+  // Optional pointwise conv fused into the epilogue (3x3 halo-tile kernel only; YOLO Detect head):
+  //   pw_y = W2 . act(conv(x) + bias) + pw_bias  (act2 = pw_act); the 3x3 result itself is not stored.
+  const void* pw_w;     // bf16 [pw_cout_pad][pw_kpad], k = channel of the 3x3 output
+  const float* pw_bias; // fp32 [pw_cout_pad]
+  void* pw_y;           // bf16 output, pixel stride pw_ys
+  int pw_ys, pw_cout, pw_kpad, pw_act;
 };
 void conv2d(const ConvParams& p, hipStream_t s);
 void conv_igemm(const ConvParams& p, hipStream_t s);  // LDS-pipelined implicit GEMM (impl 3)

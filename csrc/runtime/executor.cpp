@@ -271,6 +271,10 @@ void Executor::autotune(Bucket& bk) {
   const int reps = 3;
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;
+    if (prog_[i][34] > 0) {  // fused pointwise epilogue: only the v3 halo-tile kernel implements it
+      bk.impl[i] = 2;
+      continue;
+    }
     std::vector<OpRecord> one(1, prog_[i]);
     float best = 1e30f;
     int best_impl = 0;
@@ -383,6 +387,16 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.act = (int)r[28];
         p.B = batch(r[30]);
         p.bdev = bdev(r[30]);
+        if (r[34] > 0) {  // fused pointwise epilogue (Detect head 3x3 -> 1x1)
+          p.pw_w = W + r[31];
+          p.pw_kpad = (int)r[32];
+          p.pw_bias = (const float*)(W + r[33]);
+          p.pw_cout = (int)r[34];
+          p.pw_y = resolve(bk, sl, r[36], r[37], 2);
+          p.pw_ys = (int)r[38];
+          p.pw_act = (int)r[39];
+          p.impl = 2;
+        }
         conv2d(p, s);
         break;
       }

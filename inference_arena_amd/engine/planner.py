@@ -19,6 +19,8 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
          11 y_coff 12 y_cs 13 Ho 14 Wo 15 Cout 16 Cout_pad 17 KH 18 KW 19 stride
          20 pad_t 21 pad_l 22 res_buf 23 res_coff 24 res_cs 25 y2_buf 26 y2_coff
          27 y2_cs 28 act 29 f32out 30 batch_kind
+         31 pw_w_off 32 pw_kpad 33 pw_b_off 34 pw_cout (0 = none) 35 pw_cout_pad 36 pw_y_buf 37 pw_y_coff
+         38 pw_y_cs 39 pw_act   (pointwise conv fused into the 3x3 epilogue; y_buf may then be BUF_NONE)
   DWCONV 1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 C 7 w_off 8 b_off 9 y_buf 10 y_coff
          11 y_cs 12 Ho 13 Wo 14 stride 15 act 16 batch_kind
   SPPF   1 buf 2 coff 3 cs 4 H 5 W 6 C 7 batch_kind
@@ -211,7 +213,9 @@ class ProgramBuilder:
              pad: int | tuple[int, int] | None = None, act: str | None = "silu", res: View | None = None,
              dst2: View | None = None, f32out: bool = False, kind: int = IMAGES,
              out_hw: tuple[int, int] | None = None, src_hw: tuple[int, int] | None = None,
-             raw_cs: int | None = None) -> None:
+             raw_cs: int | None = None, pw: tuple | None = None) -> None:
+        """``pw=(w2, b2, dst2_view, act2)``: a 1x1 conv applied to this conv's activated output inside the
+        kernel epilogue (the 3x3 result is not stored when ``dst`` is ``View(BUF_NONE, 0, Cout)``)."""
         cout, cin, kh, kw = w.shape
         if cin != src.C:
             raise ValueError(f"conv: weight Cin {cin} != source view C {src.C}")
@@ -236,7 +240,16 @@ class ProgramBuilder:
                res.bid if res else BUF_NONE, res.coff if res else 0, res.cs if res else 0,
                dst2.bid if dst2 else BUF_NONE, dst2.coff if dst2 else 0, dst2.cs if dst2 else 0,
                ACT[act], int(f32out), kind]
-        self._emit(rec, src, dst, res, dst2)
+        pw_dst = None
+        if pw is not None:
+            w2, b2, pw_dst, act2 = pw
+            co2, ci2 = w2.shape[0], w2.shape[1]
+            if ci2 != cout or w2.shape[2:] != (1, 1) or co2 != pw_dst.C:
+                raise ValueError("conv: fused pointwise weights must be [C2, Cout, 1, 1] with C2 == pw dst C")
+            wb2, bb2, kpad2, cpad2 = pack_conv_weight(w2, b2)
+            rec += [self.weights.add(wb2), kpad2, self.weights.add(bb2), co2, cpad2, pw_dst.bid, pw_dst.coff,
+                    pw_dst.cs, ACT[act2]]
+        self._emit(rec, src, dst, res, dst2, pw_dst)
 
     def dwconv(self, src: View, dst: View, w: torch.Tensor, b: torch.Tensor, *, stride: int, act: str = "relu6",
                kind: int = IMAGES) -> None:

@@ -142,6 +142,7 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
 
     d = y.detect
     c2, c3, nc = d.c2, d.c3, d.nc
+    fuse_head = os.environ.get("ARENA_FUSE_HEAD", "1").lower() not in ("0", "false", "no", "off")
     ch = c2 + c3
     heads = []
     for lvl, (P, cin, s) in enumerate(((P3, 64, s8), (P4, 128, s16), (P5, 256, s32))):
@@ -151,10 +152,17 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
         wa, ba = fold(d.cv2[lvl][0])
         wc, bc = fold(d.cv3[lvl][0])
         pb.conv(View(P, 0, cin), View(H1, 0, ch), torch.cat([wa, wc]), torch.cat([ba, bc]))
-        pb.conv(View(H1, 0, c2), View(H2, 0, c2), *fold(d.cv2[lvl][1]))
-        pb.conv(View(H1, c2, c3), View(H2, c2, c3), *fold(d.cv3[lvl][1]))
-        pb.conv(View(H2, 0, c2), View(D, 0, 4 * d.reg_max), *fold_conv_bn(d.cv2[lvl][2], None), act=None)
-        pb.conv(View(H2, c2, c3), View(D, 4 * d.reg_max, nc), *fold_conv_bn(d.cv3[lvl][2], None), act=None)
+        if fuse_head and c2 in (64, 80) and c3 in (64, 80):
+            # second 3x3 of each branch with its final 1x1 in the epilogue: the 3x3 output never leaves LDS
+            pb.conv(View(H1, 0, c2), View(BUF_NONE, 0, c2), *fold(d.cv2[lvl][1]),
+                    pw=(*fold_conv_bn(d.cv2[lvl][2], None), View(D, 0, 4 * d.reg_max), None))
+            pb.conv(View(H1, c2, c3), View(BUF_NONE, 0, c3), *fold(d.cv3[lvl][1]),
+                    pw=(*fold_conv_bn(d.cv3[lvl][2], None), View(D, 4 * d.reg_max, nc), None))
+        else:
+            pb.conv(View(H1, 0, c2), View(H2, 0, c2), *fold(d.cv2[lvl][1]))
+            pb.conv(View(H1, c2, c3), View(H2, c2, c3), *fold(d.cv3[lvl][1]))
+            pb.conv(View(H2, 0, c2), View(D, 0, 4 * d.reg_max), *fold_conv_bn(d.cv2[lvl][2], None), act=None)
+            pb.conv(View(H2, c2, c3), View(D, 4 * d.reg_max, nc), *fold_conv_bn(d.cv3[lvl][2], None), act=None)
         heads.append(View(D, 0, 4 * d.reg_max + nc))
     return heads
 

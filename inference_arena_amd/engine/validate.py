@@ -94,6 +94,14 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             view(i, r[25], int(r[26]), int(r[27]), n * 4 * Ho * Wo, Cout, 2, "conv upsampled output")
             weights(i, int(r[7]), Cpad * kpad * 2, "conv weight")
             weights(i, int(r[9]), Cpad * 4, "conv bias")
+            if int(r[34]) > 0:  # fused pointwise epilogue
+                co2, kpad2, cpad2 = int(r[34]), int(r[32]), int(r[35])
+                if KH != 3 or KW != 3 or int(r[19]) != 1 or Cout not in (64, 80) or kpad2 != (Cout + 31) // 32 * 32 \
+                        or co2 > Cout or int(r[22]) != BUF_NONE or int(r[25]) != BUF_NONE:
+                    raise ProgramError(f"op {i}: unsupported fused pointwise geometry")
+                view(i, r[36], int(r[37]), int(r[38]), n * Ho * Wo, co2, 2, "fused pointwise output")
+                weights(i, int(r[31]), cpad2 * kpad2 * 2, "pointwise weight")
+                weights(i, int(r[33]), cpad2 * 4, "pointwise bias")
         elif op == OP_DWCONV:
             n = kind_n(r[16])
             H, W, C, Ho, Wo = (int(v) for v in (r[4], r[5], r[6], r[12], r[13]))

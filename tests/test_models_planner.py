@@ -114,6 +114,10 @@ def test_program_shape(program):
     # the two stem convs become stem_fused ops (preprocessing fused in) unless ARENA_FUSE_STEM=0
     assert stems in (0, 2)
     convs += stems
+    # the Detect head's final 1x1 convs ride in the epilogue of the preceding 3x3s unless ARENA_FUSE_HEAD=0
+    pw = int(((program.ops[:, 0] == OP_CONV) & (program.ops[:, 34] > 0)).sum())
+    assert pw in (0, 6)
+    convs += pw
     # auto policy: blocks 1-10 fused, 11-17 as expand/project convs (2 each, block 17 included)
     assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0), (64 + 3 + 14, 10))
     assert program.cls_ops.shape[0] < program.ops.shape[0]

@@ -114,3 +114,27 @@ def test_fused_stem_matches_unfused(dense_models, device, monkeypatch):
             np.testing.assert_allclose(y.boxes, x.boxes, atol=0.5)
             assert (x.topk_idx[:, 0] == y.topk_idx[:, 0]).mean() >= 0.9
             np.testing.assert_allclose(y.topk_logit[:, 0], x.topk_logit[:, 0], rtol=0.05, atol=0.05)
+
+
+def test_fused_head_pointwise_matches_unfused(dense_models, device, monkeypatch):
+    """Detect head: second 3x3 of each branch with the final 1x1 fused into its epilogue (v3 kernel) vs
+    the separate 3x3 + 1x1 convs: same head outputs at every level and the same detections."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    imgs = synthetic_images(4, 41)
+    monkeypatch.setenv("ARENA_FUSE_HEAD", "0")
+    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    monkeypatch.setenv("ARENA_FUSE_HEAD", "1")
+    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    n_pw = sum(1 for op in fused.program.ops if int(op[0]) == 1 and int(op[34]) > 0)
+    assert n_pw == 6 and len(fused.program.ops) == len(plain.program.ops) - 6
+    a, b = plain.infer(imgs), fused.infer(imgs)
+    for lvl in range(3):
+        for i in range(len(imgs)):
+            x, y = plain.read_buffer(f"det{lvl}.out", 4, i), fused.read_buffer(f"det{lvl}.out", 4, i)
+            np.testing.assert_allclose(y, x, atol=0.05 + 0.01 * np.abs(x).max())
+    for x, y in zip(a, b):
+        assert abs(len(x) - len(y)) <= 1
+        if len(x) == len(y) and len(x):
+            np.testing.assert_allclose(y.boxes, x.boxes, atol=1.0)

@@ -29,7 +29,7 @@ def describe(rec) -> str:
     if t == 1:
         return (f"{int(rec[4])}x{int(rec[5])}x{int(rec[6])}->{int(rec[13])}x{int(rec[14])}x{int(rec[15])} "
                 f"k{int(rec[17])} s{int(rec[19])}{' res' if rec[22] != -1 else ''}{' up2' if rec[25] != -1 else ''}"
-                f"{' crops' if rec[30] == 1 else ''}")
+                f"{' crops' if rec[30] == 1 else ''}{f' +pw1x1->{int(rec[34])}' if rec[34] > 0 else ''}")
     if t == 2:
         return f"dw {int(rec[4])}x{int(rec[5])}x{int(rec[6])} s{int(rec[14])}"
     if t == 15:
