@@ -707,7 +707,12 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   }
   {
     trace::Range tp("arena.pack");
-    parallel_copy(jobs);
+    // timing experiments only: ARENA_DEBUG_SKIP_PACK=n reuses the staged pixels after the first n batches
+    static const long skip_after = [] {
+      const char* e = std::getenv("ARENA_DEBUG_SKIP_PACK");
+      return e != nullptr ? std::atol(e) : -1L;
+    }();
+    if (skip_after < 0 || (long)seq_ <= skip_after) parallel_copy(jobs);
   }
   Ctrl* ctrl = (Ctrl*)sl.h_in;
   std::memset(ctrl, 0, sizeof(Ctrl));
