@@ -17,12 +17,6 @@
 namespace py = pybind11;
 using namespace arena;
 
-namespace arena {
-void* probe_create(int base);
-std::vector<int> probe_launch(void* h);
-void probe_destroy(void* h);
-}  // namespace arena
-
 namespace {
 
 template <typename T>
@@ -351,9 +345,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("SIZEOF_CROPREF") = (int)sizeof(CropRef);
   m.attr("SIZEOF_TOPK") = (int)sizeof(TopkResult);
   m.attr("OP_FIELDS") = kOpFields;
-  m.def("probe_create", [](int base) { return (uintptr_t)probe_create(base); });
-  m.def("probe_launch", [](uintptr_t h) { return probe_launch((void*)h); });
-  m.def("probe_destroy", [](uintptr_t h) { probe_destroy((void*)h); });
 
   py::class_<Executor, std::shared_ptr<Executor>>(m, "Executor")
       .def(py::init([](const py::dict& cfg) { return std::make_shared<Executor>(config_from(cfg)); }))

@@ -43,7 +43,6 @@ SOURCES = [
     "runtime/executor.cpp",
     "runtime/batcher.cpp",
     "runtime/trace.cpp",
-    "runtime/probe.hip",
     "bindings.cpp",
 ]
 
