@@ -92,6 +92,30 @@ void ir_block(const IrParams& p, hipStream_t s);
 void ir_prepare();
 void set_ir_wave(bool v);  // ARENA_IR_WAVE=0: stride-1 blocks use the block-cooperative kernel
 
+// ---------------------------------------------------------------- fused C3 block (K2/K3/K4 at 160x160 / 80x80)
+// cv1|cv2 (1x1) -> NB x Bottleneck(1x1, 3x3 [+res]) -> cv3 (1x1) with every intermediate in LDS
+// (csrc/kernels/c3_fused.hip).  Weight layouts as the conv kernels ([Cout_pad][Kpad], k = tap*C + c);
+// the bottleneck 1x1 weights are [CH][32] (zero columns past CH).
+struct C3Params {
+  const void* x;  // bf16 NHWC input view, pixel stride xs
+  int xs;
+  int B, H, W;    // output size == input size (stride 1)
+  const int* bdev;
+  int C1, CH, NB, res;
+  const void* w12;  // [2CH][C1]
+  const float* b12;
+  const void* wb1[2];  // [CH][32]
+  const float* bb1[2];
+  const void* wb2[2];  // [CH][round32(9*CH)]
+  const float* bb2[2];
+  const void* w3;   // [2CH][2CH]
+  const float* b3;
+  void* y;          // bf16 NHWC output view, pixel stride ys, 2CH channels
+  int ys;
+};
+bool c3_fused_supported(int C1, int CH, int NB, bool res, int H, int W);
+void c3_fused(const C3Params& p, hipStream_t s);
+
 // ---------------------------------------------------------------- SPPF pools (K5)
 // x: [B,H,W] channels [0,C) of a buffer with pixel stride xs; writes the
 // cascaded 5x5 max pools (== 5/9/13 windows) into channel slices C, 2C, 3C.

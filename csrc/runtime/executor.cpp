@@ -540,6 +540,33 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         crop_gather_s2d(p, s);
         break;
       }
+      case OP_C3FUSED: {
+        C3Params p{};
+        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.xs = (int)r[3];
+        p.H = (int)r[4];
+        p.W = (int)r[5];
+        p.C1 = (int)r[6];
+        p.CH = (int)r[7];
+        p.NB = (int)r[8];
+        p.res = (int)r[9];
+        p.w12 = W + r[10];
+        p.b12 = (const float*)(W + r[11]);
+        for (int k = 0; k < 2; ++k) {
+          p.wb1[k] = W + r[12 + 4 * k];
+          p.bb1[k] = (const float*)(W + r[13 + 4 * k]);
+          p.wb2[k] = W + r[14 + 4 * k];
+          p.bb2[k] = (const float*)(W + r[15 + 4 * k]);
+        }
+        p.w3 = W + r[20];
+        p.b3 = (const float*)(W + r[21]);
+        p.y = resolve(bk, sl, r[22], r[23], 2);
+        p.ys = (int)r[24];
+        p.B = batch(r[25]);
+        p.bdev = bdev(r[25]);
+        c3_fused(p, s);
+        break;
+      }
       case OP_STEMFUSED: {
         StemFusedParams p{};
         p.src = (int)r[1];

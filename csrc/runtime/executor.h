@@ -58,6 +58,7 @@ enum OpType : int64_t {
   OP_YOLORAW = 13,
   OP_IRBLOCK = 14,
   OP_STEMFUSED = 15,
+  OP_C3FUSED = 16,
 };
 
 // Reserved buffer ids (the planner's arena buffers are ids >= 0).

@@ -42,6 +42,9 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
            9 Cout 10 act 11 crops_buf 12-14 mean 15-17 inv_std (float bits) 18 batch_kind 19 KS
            (preprocessing fused into the stem conv; the s2d input exists only in LDS,
             csrc/kernels/stem_fused.hip)
+  C3FUSED 1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 C1 7 CH 8 NB 9 res 10 w12 11 b12 12-15 (wb1, bb1, wb2, bb2) of
+           bottleneck 0, 16-19 of bottleneck 1, 20 w3 21 b3 22 y_buf 23 y_coff 24 y_cs 25 batch_kind
+           (whole YOLOv5 C3 block, intermediates in LDS, csrc/kernels/c3_fused.hip)
 """
 from __future__ import annotations
 
@@ -53,7 +56,7 @@ import torch
 
 OP_FIELDS = 48
 (OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
- OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED) = range(1, 16)
+ OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED) = range(1, 17)
 BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK, BUF_RAWOUT = -1, -10, -11, -12, -13, -14, -15, -16
 IMAGES, CROPS = 0, 1
 ACT = {None: 0, "none": 0, "silu": 1, "relu6": 2}
@@ -288,6 +291,30 @@ class ProgramBuilder:
 
     def letterbox(self, out: Buffer, T: int) -> None:
         self._emit([OP_LETTERBOX, out.id, T], out)
+
+    def c3_fused(self, src: View, dst: View, H: int, W: int, cv12: tuple, bottlenecks: list, cv3: tuple, *,
+                 res: bool, kind: int = IMAGES) -> None:
+        """A whole C3 block as one op: ``cv12`` = (w, b) of cv1|cv2 stacked [2CH, C1, 1, 1]; ``bottlenecks`` =
+        [((w1, b1), (w2, b2)), ...] with w1 [CH, CH, 1, 1], w2 [CH, CH, 3, 3]; ``cv3`` = (w, b) [2CH, 2CH, 1, 1]."""
+        w12, b12 = cv12
+        ch2, c1 = w12.shape[0], w12.shape[1]
+        CH, NB = ch2 // 2, len(bottlenecks)
+        if c1 != src.C or dst.C != ch2 or not 1 <= NB <= 2:
+            raise ValueError("c3_fused: channel / bottleneck count mismatch")
+        rec = [OP_C3FUSED, src.bid, src.coff, src.cs, H, W, c1, CH, NB, int(res)]
+        wb, bb, _, _ = pack_conv_weight(w12, b12)
+        rec += [self.weights.add(wb), self.weights.add(bb)]
+        for k in range(2):
+            (w1, b1), (w2, b2) = bottlenecks[min(k, NB - 1)]
+            w1p = torch.zeros(CH, 32, 1, 1)  # [CH][32]: k >= CH columns zero (the kernel reads T's first 32 ch)
+            w1p[:, :CH] = w1.reshape(CH, CH, 1, 1)
+            wa, ba, _, _ = pack_conv_weight(w1p, b1)
+            wc, bc, _, _ = pack_conv_weight(w2, b2)
+            rec += [self.weights.add(wa), self.weights.add(ba), self.weights.add(wc), self.weights.add(bc)]
+        w3, b3 = cv3
+        wd, bd, _, _ = pack_conv_weight(w3, b3)
+        rec += [self.weights.add(wd), self.weights.add(bd), dst.bid, dst.coff, dst.cs, kind]
+        self._emit(rec, src, dst)
 
     def stem_fused(self, dst: View, w: torch.Tensor, b: torch.Tensor, *, S: int, act: str, crops: Buffer | None = None,
                    mean=None, std=None, kind: int = IMAGES) -> None:

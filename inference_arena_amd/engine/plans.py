@@ -63,8 +63,33 @@ def s2d_stem_3x3(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# (C1, c_, bottlenecks, shortcut) combinations csrc/kernels/c3_fused.hip implements (YOLOv5n's 160x160 and
+# 80x80 C3 blocks); H % 8 == 0 and W % 16 == 0 are also required.
+C3_FUSED = {(32, 16, 1, True), (64, 32, 2, True), (128, 32, 1, False)}
+# Where the fused kernel measured faster on MI355X (batch 32, serial kernel trace): the 160x160 block
+# (c_ = 16: 56 us vs 90 us for its four convs).  At 80x80 (c_ = 32) the fused kernels are LDS-occupancy
+# bound (69-75 KB per workgroup) and only break even (b4) or lose (h17), so they stay unfused by default.
+C3_FUSED_AUTO = {(32, 16, 1, True)}
+
+
+def fuse_c3_policy() -> str:
+    """``ARENA_FUSE_C3``: ``auto`` (default, measured-faster shapes only), ``all`` or ``none``/``0``."""
+    v = os.environ.get("ARENA_FUSE_C3", "auto").lower()
+    return {"0": "none", "false": "none", "off": "none", "1": "auto", "true": "auto"}.get(v, v)
+
+
 def _c3(pb: ProgramBuilder, m, src: View, dst: View, H: int, W: int, name: str) -> None:
     c_ = m.c_
+    res = bool(m.m[0].add)
+    policy = fuse_c3_policy()
+    allowed = C3_FUSED if policy == "all" else C3_FUSED_AUTO if policy == "auto" else set()
+    if ((src.C, c_, len(m.m), res) in allowed and H % 8 == 0 and W % 16 == 0
+            and all(bool(bn.add) == res for bn in m.m)):
+        w1, b1 = fold(m.cv1)
+        w2, b2 = fold(m.cv2)
+        pb.c3_fused(src, dst, H, W, (torch.cat([w1, w2]), torch.cat([b1, b2])),
+                    [(fold(bn.cv1), fold(bn.cv2)) for bn in m.m], fold(m.cv3), res=res)
+        return
     T = pb.tensor(f"{name}.T", H, W, 2 * c_)
     U = pb.tensor(f"{name}.U", H, W, c_)
     w1, b1 = fold(m.cv1)

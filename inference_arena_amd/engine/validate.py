@@ -18,6 +18,7 @@ from ..engine.planner import (
     BUF_TOPK,
     CROPS,
     OP_AVGPOOL,
+    OP_C3FUSED,
     OP_CONV,
     OP_CROPGATHER,
     OP_CROPPLAN,
@@ -133,6 +134,24 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         elif op == OP_LETTERBOX:
             T2 = int(r[2]) // 2
             need(i, r[1], 0, B * T2 * T2 * 32, "letterbox output")
+        elif op == OP_C3FUSED:
+            n = kind_n(r[25])
+            H, W, C1, CH, NB, res = (int(v) for v in r[4:10])
+            if (C1, CH, NB, bool(res)) not in {(32, 16, 1, True), (64, 32, 2, True), (128, 32, 1, False)} \
+                    or H % 8 or W % 16:
+                raise ProgramError(f"op {i}: unsupported fused C3 geometry {(C1, CH, NB, res, H, W)}")
+            view(i, r[1], int(r[2]), int(r[3]), n * H * W, C1, 2, "c3 input")
+            view(i, r[22], int(r[23]), int(r[24]), n * H * W, 2 * CH, 2, "c3 output")
+            weights(i, int(r[10]), 2 * CH * C1 * 2, "c3 cv1|cv2 weight")
+            weights(i, int(r[11]), 2 * CH * 4, "c3 cv1|cv2 bias")
+            k3 = (9 * CH + 31) // 32 * 32
+            for k in range(NB):
+                weights(i, int(r[12 + 4 * k]), CH * 32 * 2, f"c3 bottleneck {k} cv1 weight")
+                weights(i, int(r[13 + 4 * k]), CH * 4, f"c3 bottleneck {k} cv1 bias")
+                weights(i, int(r[14 + 4 * k]), CH * k3 * 2, f"c3 bottleneck {k} cv2 weight")
+                weights(i, int(r[15 + 4 * k]), CH * 4, f"c3 bottleneck {k} cv2 bias")
+            weights(i, int(r[20]), 4 * CH * CH * 2, "c3 cv3 weight")
+            weights(i, int(r[21]), 2 * CH * 4, "c3 cv3 bias")
         elif op == OP_STEMFUSED:
             src, S, kpad, cout, kind, ks = int(r[1]), int(r[5]), int(r[7]), int(r[9]), int(r[18]), int(r[19])
             n = kind_n(kind)

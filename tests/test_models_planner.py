@@ -118,6 +118,12 @@ def test_program_shape(program):
     pw = int(((program.ops[:, 0] == OP_CONV) & (program.ops[:, 34] > 0)).sum())
     assert pw in (0, 6)
     convs += pw
+    # whole C3 blocks at 160x160 / 80x80 (cv1|cv2, NB bottlenecks x 2 convs, cv3) unless ARENA_FUSE_C3=0
+    from inference_arena_amd.engine.planner import OP_C3FUSED
+
+    c3 = program.ops[program.ops[:, 0] == OP_C3FUSED]
+    assert len(c3) in (0, 1, 3)  # none / auto (160x160 block) / all
+    convs += int(sum(2 + 2 * int(r[8]) for r in c3))
     # auto policy: blocks 1-10 fused, 11-17 as expand/project convs (2 each, block 17 included)
     assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0), (64 + 3 + 14, 10))
     assert program.cls_ops.shape[0] < program.ops.shape[0]

@@ -138,3 +138,27 @@ def test_fused_head_pointwise_matches_unfused(dense_models, device, monkeypatch)
         assert abs(len(x) - len(y)) <= 1
         if len(x) == len(y) and len(x):
             np.testing.assert_allclose(y.boxes, x.boxes, atol=1.0)
+
+
+def test_fused_c3_matches_unfused(dense_models, device, monkeypatch):
+    """Whole C3 blocks as one kernel (160x160 c_=16 n=1, 80x80 c_=32 n=2, head P3 c_=32 n=1 without
+    shortcut) vs the per-conv program: same block outputs and the same detections."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    imgs = synthetic_images(3, 51) + synthetic_images(1, 52, hw=(333, 500))
+    monkeypatch.setenv("ARENA_FUSE_C3", "0")
+    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    monkeypatch.setenv("ARENA_FUSE_C3", "all")
+    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    assert sum(1 for op in fused.program.ops if int(op[0]) == 16) == 3
+    a, b = plain.infer(imgs), fused.infer(imgs)
+    for name in ("b2", "cat16", "p3"):
+        for i in range(len(imgs)):
+            x, y = plain.read_buffer(name, 4, i), fused.read_buffer(name, 4, i)
+            scale = np.abs(x).max()
+            np.testing.assert_allclose(y, x, atol=0.03 + 0.02 * scale, err_msg=name)
+    for x, y in zip(a, b):
+        assert abs(len(x) - len(y)) <= 1
+        if len(x) == len(y) and len(x):
+            np.testing.assert_allclose(y.boxes, x.boxes, atol=1.5)

@@ -20,7 +20,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 KIND = {1: "conv", 2: "dwconv", 3: "sppf", 4: "letterbox", 5: "zero", 6: "decode", 7: "nms", 8: "cropplan",
-        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw", 14: "irblock", 15: "stemfused"}
+        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw", 14: "irblock", 15: "stemfused", 16: "c3fused"}
 FIRST_KERNEL = {4: "letterbox", 12: "tensor_in", 15: "stem_fused"}
 
 
@@ -32,6 +32,9 @@ def describe(rec) -> str:
                 f"{' crops' if rec[30] == 1 else ''}{f' +pw1x1->{int(rec[34])}' if rec[34] > 0 else ''}")
     if t == 2:
         return f"dw {int(rec[4])}x{int(rec[5])}x{int(rec[6])} s{int(rec[14])}"
+    if t == 16:
+        return (f"c3 {int(rec[4])}x{int(rec[5])}x{int(rec[6])} c_={int(rec[7])} n={int(rec[8])}"
+                f"{' res' if rec[9] else ''}")
     if t == 15:
         return f"{'letterbox' if rec[1] == 0 else 'crop gather'} + stem k{int(rec[19])} -> {int(rec[9])}"
     if t == 14:

@@ -36,6 +36,7 @@ SOURCES = [
     "kernels/conv_igemm.hip",
     "kernels/conv_pw.hip",
     "kernels/conv3x3_v3.hip",
+    "kernels/c3_fused.hip",
     "kernels/preprocess.hip",
     "kernels/stem_fused.hip",
     "kernels/detect.hip",
