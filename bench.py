@@ -80,6 +80,8 @@ def main(argv=None) -> int:
     ap.add_argument("--seed", type=int, default=0, help="weight seed")
     ap.add_argument("--images", type=int, default=100, help="curated workload size")
     ap.add_argument("--bs1-requests", type=int, default=100, help="sequential bs=1 requests for the latency probe")
+    ap.add_argument("--crop-cap", type=int, default=None,
+                    help="crops per image one classification pass holds (default: experiment.yaml gpu.crop_cap_per_image)")
     a = ap.parse_args(argv)
 
     import torch
@@ -97,7 +99,7 @@ def main(argv=None) -> int:
     t0 = time.time()
     yolo, mnet = default_models(a.seed)
     buckets = sorted({1, a.batch})
-    pipe = GpuPipeline(yolo, mnet, device=info.local_rank, buckets=buckets)
+    pipe = GpuPipeline(yolo, mnet, device=info.local_rank, buckets=buckets, crop_cap_per_image=a.crop_cap)
     blob = D.broadcast_blob(pipe.program.weights if info.is_main else None, info)
     if info.world > 1:
         if not np.array_equal(blob, pipe.program.weights):

@@ -1,4 +1,4 @@
-// Fused inverted residual, stride 1: one output tile per WAVE (no block barriers).
+// Fused inverted residual: one output tile per WAVE (no block barriers).
 //
 // The block-cooperative kernel (ir_block.hip) splits each tile's expand /
 // depthwise / project phases across 4 waves with three __syncthreads per
@@ -9,6 +9,9 @@
 // 16-B global loads), depthwise (tap pairs via v_perm + v_dot2c_f32_bf16,
 // weights in registers), project (MFMA, accumulators in VGPRs).  LDS traffic
 // between phases is ordered by the wave's own instruction stream.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "launch.h"
 
@@ -23,9 +26,9 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int TH, int TW, int MP, int NS, bool EXPAND>
+template <int S, int TH, int TW, int MP, int NS, bool EXPAND>
 __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
-  constexpr int PH = TH + 2, PW = TW + 2;
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   constexpr int PIN = PH * PW, PIN_PAD = (PIN + 15) / 16 * 16;
   constexpr int POUT = TH * TW, POUT_PAD = (POUT + 15) / 16 * 16;
   constexpr int NE = PIN_PAD / 16, NP = POUT_PAD / 16;
@@ -44,13 +47,15 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
 
   const int tiles_x = (p.Wo + TW - 1) / TW, tiles_y = (p.Ho + TH - 1) / TH;
   const int tiles = tiles_x * tiles_y;
-  const int gt = blockIdx.x * 4 + wave;  // global tile index
+  // Waves stride over the live tiles (the grid covers launch_B items, not the whole capacity);
+  // LDS ops of one wave complete in order, so the next tile's staging cannot overtake this one's reads.
+  const int n_gt = live_batch(p.B, p.bdev) * tiles;
+  for (int gt = blockIdx.x * 4 + wave; gt < n_gt; gt += gridDim.x * 4) {
   const int b = gt / tiles;
-  if (b >= live_batch(p.B, p.bdev)) return;  // whole wave exits; no block barrier follows
   const int t = gt - b * tiles;
   const int ty = t / tiles_x, tx = t - ty * tiles_x;
   const int oy0 = ty * TH, ox0 = tx * TW;
-  const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   const bf16* xb = (const bf16*)p.x + (size_t)b * p.H * p.W * p.x_cs;
 
   // ---- input halo tile -> this wave's LDS (zero outside the image / past inp)
@@ -162,8 +167,8 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
 #pragma unroll
         for (int pp = 0; pp < 4; ++pp) {
           const int t0 = 2 * pp, t1 = 2 * pp + 1;
-          const uint4 e0 = *(const uint4*)(Esrc + wswz((oy + t0 / 3) * PW + ox + t0 % 3, dc));
-          const uint4 e1 = *(const uint4*)(Esrc + wswz((oy + t1 / 3) * PW + ox + t1 % 3, dc));
+          const uint4 e0 = *(const uint4*)(Esrc + wswz((oy * S + t0 / 3) * PW + ox * S + t0 % 3, dc));
+          const uint4 e1 = *(const uint4*)(Esrc + wswz((oy * S + t1 / 3) * PW + ox * S + t1 % 3, dc));
           const unsigned x0[4] = {e0.x, e0.y, e0.z, e0.w}, x1[4] = {e1.x, e1.y, e1.z, e1.w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
           }
         }
         float e8[8];
-        unpack8(*(const uint4*)(Esrc + wswz((oy + 2) * PW + ox + 2, dc)), e8);
+        unpack8(*(const uint4*)(Esrc + wswz((oy * S + 2) * PW + ox * S + 2, dc)), e8);
 #pragma unroll
         for (int i = 0; i < 8; ++i) a[i] = relu6w(fmaf(e8[i], w8[i], a[i]));
         outv = pack8(a);
@@ -214,7 +219,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
       if (oc >= p.oup) continue;
       const float4 bb = *(const float4*)(p.bp + oc);
       float v[4] = {acc[q][m][0] + bb.x, acc[q][m][1] + bb.y, acc[q][m][2] + bb.z, acc[q][m][3] + bb.w};
-      if (p.res) {
+      if (S == 1 && p.res) {
         float r[4];
         unpack4(*(const uint2*)(Xs + (oc >> 5) * PIN_PAD * 64 + wswz(rpix, (oc & 31) >> 3) + (oc & 7) * 2), r);
 #pragma unroll
@@ -223,42 +228,56 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
       *(uint2*)(yp + oc) = pack4(v);
     }
   }
+  }  // gt
 }
 
-template <int TH, int TW, int MP, int NS, bool EXPAND>
+template <int S, int TH, int TW, int MP, int NS, bool EXPAND>
 static void irw_launch(const IrParams& p, hipStream_t s) {
-  constexpr int PIN_PAD = ((TH + 2) * (TW + 2) + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
+  constexpr int PIN_PAD = (((TH - 1) * S + 3) * ((TW - 1) * S + 3) + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
   constexpr size_t lds = 4 * (size_t)(NS * PIN_PAD * 64 + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64);
   static_assert(lds <= 160 * 1024, "LDS");
-  const long tiles = (long)((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
+  const long tiles = (long)((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) *
+                     (p.launch_B > 0 ? std::min(p.launch_B, p.B) : p.B);
   if (tiles <= 0) return;
-  hipLaunchKernelGGL((ir_wave_kernel<TH, TW, MP, NS, EXPAND>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), lds, s,
+  hipLaunchKernelGGL((ir_wave_kernel<S, TH, TW, MP, NS, EXPAND>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), lds, s,
                      p);
 }
 
 // Measured (profiles/r1_irwave_ops.md): the wave kernel wins on the 56x56 and 28x28
 // expand blocks; block 1 (no expand) and the 14x14 blocks stay block-cooperative.
+// Stride 2 uses 4x4 output tiles (9x9 halo: 13 KB of LDS per wave).
 #define ARENA_IRW_CONFIGS(X) \
-  X(8, 8, 2, 1, true)        \
-  X(7, 7, 2, 1, true)
+  X(1, 8, 8, 2, 1, true)     \
+  X(1, 7, 7, 2, 1, true)     \
+  X(2, 4, 4, 2, 1, true)
 
 void ir_wave_prepare() {
-#define X(TH, TW, MP, NS, E)                                                                          \
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_wave_kernel<TH, TW, MP, NS, E>,                 \
+#define X(S, TH, TW, MP, NS, E)                                                                       \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_wave_kernel<S, TH, TW, MP, NS, E>,                 \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   ARENA_IRW_CONFIGS(X)
 #undef X
 }
 
 // Stride-1 blocks with a supported (tile, oup tiles, input slabs) shape; false otherwise.
+static const bool g_irw_s2 = [] {
+  const char* e = std::getenv("ARENA_IRW_S2");
+  return e ? std::atoi(e) != 0 : true;
+}();
+
 bool ir_block_wave(const IrParams& p, int tile, hipStream_t s) {
-  if (p.stride != 1) return false;
+  if (p.stride == 2) {
+    if (!g_irw_s2 || p.Ho % 4 || p.Wo % 4) return false;
+    tile = 4;
+  } else if (p.stride != 1) {
+    return false;
+  }
   const int MP = p.oup_pad / 16, NS = p.inp_pad / 32;
   const bool E = p.expand != 0;
-#define X(TH_, TW_, MP_, NS_, E_)                                \
-  if (tile == TH_ && MP == MP_ && NS == NS_ && E == E_) {        \
-    irw_launch<TH_, TW_, MP_, NS_, E_>(p, s);                    \
-    return true;                                                 \
+#define X(S_, TH_, TW_, MP_, NS_, E_)                                              \
+  if (p.stride == S_ && tile == TH_ && MP == MP_ && NS == NS_ && E == E_) {        \
+    irw_launch<S_, TH_, TW_, MP_, NS_, E_>(p, s);                                  \
+    return true;                                                                   \
   }
   ARENA_IRW_CONFIGS(X)
 #undef X

@@ -24,6 +24,8 @@
 //
 // Numerics are identical to letterbox_s2d / crop_gather_s2d followed by the
 // stem conv: the same float ops produce the same bf16 s2d values.
+#include <algorithm>
+
 #include "common.h"
 #include "launch.h"
 
@@ -49,16 +51,44 @@ __device__ __forceinline__ LinTap2 tap_of(int d, float scale, int n) {
   return t;
 }
 
-__device__ __forceinline__ void sample_rgb(const uint8_t* img, int stride_px, LinTap2 ty, LinTap2 tx, float* rgb) {
-  const uint8_t* r0 = img + (size_t)ty.i0 * stride_px * 3;
-  const uint8_t* r1 = img + (size_t)ty.i1 * stride_px * 3;
+struct RowTap {
+  int o0, o1;  // byte offsets of the two taps (o0 < 0: outside the sampled area)
+  float f;     // weight of tap 1
+};
+
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+// Both sub-pixel columns of one sub-pixel row (the pair shares the row taps),
+// in packed fp32 (v_pk_fma_f32 / v_pk_add_f32).  `ident` (scale exactly 1,
+// so every lerp weight is 0): the sample is the source byte itself, as
+// cv2.resize copies at equal sizes.  Columns outside the sampled area keep
+// `pad`.
+__device__ __forceinline__ void bilinear_pair(const uint8_t* base, const RowTap& ry, const RowTap& c0,
+                                              const RowTap& c1, bool ident, float pad, float2v* rgb) {
+  const bool v0 = c0.o0 >= 0, v1 = c1.o0 >= 0;
+  if (!v0 && !v1) return;
+  const int a0 = v0 ? c0.o0 : c1.o0, a1 = v1 ? c1.o0 : c0.o0;  // an invalid column reads its valid neighbour
+  const uint8_t* p0 = base + ry.o0;
+  if (ident) {
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const float a = (float)r0[tx.i0 * 3 + c], b = (float)r0[tx.i1 * 3 + c];
-    const float d = (float)r1[tx.i0 * 3 + c], e = (float)r1[tx.i1 * 3 + c];
-    const float top = a + (b - a) * tx.f;
-    const float bot = d + (e - d) * tx.f;
-    rgb[c] = floorf(top + (bot - top) * ty.f + 0.5f);  // cv2 returns uint8
+    for (int c = 0; c < 3; ++c) rgb[c] = float2v{(float)p0[a0 + c], (float)p0[a1 + c]};
+  } else {
+    const int b0 = v0 ? c0.o1 : c1.o1, b1 = v1 ? c1.o1 : c0.o1;
+    const uint8_t* p1 = base + ry.o1;
+    const float2v fx = {c0.f, c1.f}, fy = {ry.f, ry.f}, half = {0.5f, 0.5f};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float2v va = {(float)p0[a0 + c], (float)p0[a1 + c]}, vb = {(float)p0[b0 + c], (float)p0[b1 + c]};
+      const float2v vd = {(float)p1[a0 + c], (float)p1[a1 + c]}, ve = {(float)p1[b0 + c], (float)p1[b1 + c]};
+      const float2v top = va + (vb - va) * fx;
+      const float2v bot = vd + (ve - vd) * fx;
+      const float2v r = top + (bot - top) * fy + half;
+      rgb[c] = float2v{floorf(r.x), floorf(r.y)};  // cv2 returns uint8
+    }
+  }
+  if (!v0 || !v1) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) rgb[c] = float2v{v0 ? rgb[c].x : pad, v1 ? rgb[c].y : pad};
   }
 }
 
@@ -80,38 +110,29 @@ struct Src {
 // 8x32 tile), then the bilinear taps read LDS bytes: one global dword load
 // per 4 source bytes instead of 12 byte loads per sub-pixel.  Regions above
 // the budget (strongly downscaled images, large crops) sample global memory.
-constexpr int kSrcBudget = 16384;
-
-// rows r0/r1 of the staged region start `s0`/`s1` bytes into their LDS row (dword alignment shift)
-__device__ __forceinline__ void sample_rgb_lds2(const uint8_t* reg, int pitch, int r0, int r1, int s0, int s1, int x0,
-                                                int x1, float fy, float fx, float* rgb) {
-  const uint8_t* p0 = reg + r0 * pitch + s0;
-  const uint8_t* p1 = reg + r1 * pitch + s1;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const float a = (float)p0[x0 + c], b = (float)p0[x1 + c];
-    const float d = (float)p1[x0 + c], e = (float)p1[x1 + c];
-    const float top = a + (b - a) * fx;
-    const float bot = d + (e - d) * fx;
-    rgb[c] = floorf(top + (bot - top) * fy + 0.5f);
-  }
-}
+constexpr int kSrcBudget = 8192;  // 16 KB measured slower: LDS held occupancy at 5 workgroups / CU
 
 template <int SRC, int KS, int NF, int TH, int TW>
 __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p) {
   constexpr int HH = TH + KS - 1, HW = TW + KS - 1, NPIX = HH * HW;
   constexpr int SLABS = (KS * KS * 16 + 31) / 32;
   static_assert(TH * TW == 256, "one 256-pixel tile per workgroup (4 waves x 4 fragments)");
+  static_assert(2 * HH <= 64 && 2 * HW <= 192, "tap tables are built by waves 0 / 1-3");
   __shared__ __align__(16) uint4 tile[NPIX * 2];  // 32 B per s2d pixel
   __shared__ __align__(16) uint32_t region[kSrcBudget / 4];
 
   const int S2 = p.S >> 1;
   const int tiles_x = (S2 + TW - 1) / TW, tiles_y = (S2 + TH - 1) / TH, ntiles = tiles_x * tiles_y;
-  const int id = blockIdx.x, xcd = id & 7, j = id >> 3;
+  const int n_live = live_batch(p.cap, SRC == 0 ? &p.ctrl->n_images : &p.ctrl->n_crops);
+  // The grid covers launch_cap items (a multiple of 8 x ntiles workgroups, so a workgroup keeps its
+  // XCD); workgroups stride over the live items, so dead capacity costs no dispatches.
+  const int n_vb = (n_live + 7) / 8 * 8 * ntiles;
+  for (int id = blockIdx.x; id < n_vb; id += gridDim.x) {
+  if (id != (int)blockIdx.x) __syncthreads();  // previous item's LDS reads are done
+  const int xcd = id & 7, j = id >> 3;
   const int item = (j / ntiles) * 8 + xcd;  // every tile of one item lands on one XCD
   const int t = j - (j / ntiles) * ntiles;
-  const int n_live = live_batch(p.cap, SRC == 0 ? &p.ctrl->n_images : &p.ctrl->n_crops);
-  if (item >= n_live) return;
+  if (item >= n_live) continue;
   const int ty0 = (t / tiles_x) * TH, tx0 = (t % tiles_x) * TW;
 
   Src g;
@@ -166,13 +187,52 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
         const uint32_t* a = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
         region[r * ndw + k] = a[k];
       }
-      __syncthreads();
     }
   }
   const uint8_t* reg = (const uint8_t*)region;
   const uintptr_t base_addr = (uintptr_t)(g.img + (size_t)r_lo * row_bytes + (size_t)c_lo * 3);
 
+  // ---- tap tables: one entry per sub-pixel row / column of the halo tile
+  // (byte offsets of both source rows / pixels in the staged region or the
+  // image, and the lerp weight), so the per-sub-pixel work below is lookups,
+  // 12 byte loads and the lerps.  o0 < 0 marks a row / column outside the
+  // sampled area (letterbox border -> 114, empty crop -> 0).
+  __shared__ RowTap rtab[2 * HH];
+  __shared__ RowTap ctab[2 * HW];
+  if (threadIdx.x < 2 * HH) {
+    const int d = 2 * (ty0 - 1) + (int)threadIdx.x - g.pad_h;
+    RowTap e{-1, -1, 0.f};
+    if (!g.empty && d >= 0 && d < (SRC == 0 ? g.h : p.S)) {
+      const LinTap2 t = tap_of(d, g.sy, g.rh);
+      if (staged) {
+        const int r0 = t.i0 - r_lo, r1 = t.i1 - r_lo;
+        e.o0 = r0 * pitch + (int)((base_addr + (size_t)r0 * row_bytes) & 3);
+        e.o1 = r1 * pitch + (int)((base_addr + (size_t)r1 * row_bytes) & 3);
+      } else {
+        e.o0 = (int)((size_t)t.i0 * row_bytes);
+        e.o1 = (int)((size_t)t.i1 * row_bytes);
+      }
+      e.f = t.f;
+    }
+    rtab[threadIdx.x] = e;
+  } else if (threadIdx.x >= 64 && threadIdx.x < 64 + 2 * HW) {
+    const int k = (int)threadIdx.x - 64;
+    const int d = 2 * (tx0 - 1) + k - g.pad_w;
+    RowTap e{-1, -1, 0.f};
+    if (!g.empty && d >= 0 && d < (SRC == 0 ? g.w : p.S)) {
+      const LinTap2 t = tap_of(d, g.sx, g.rw);
+      const int c0 = staged ? c_lo : 0;
+      e.o0 = (t.i0 - c0) * 3;
+      e.o1 = (t.i1 - c0) * 3;
+      e.f = t.f;
+    }
+    ctab[k] = e;
+  }
+  __syncthreads();
+
   // ---- phase 1: s2d halo tile into LDS
+  const float pad_val = SRC == 0 ? 114.f : 0.f;
+  const bool ident = g.sy == 1.f && g.sx == 1.f;
   for (int i = threadIdx.x; i < NPIX; i += 256) {
     const int hy = i / HW, hx = i - (i / HW) * HW;
     const int Y = ty0 - 1 + hy, X = tx0 - 1 + hx;
@@ -180,41 +240,24 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
 #pragma unroll
     for (int k = 0; k < 16; ++k) out[k] = 0.f;
     if ((unsigned)Y < (unsigned)S2 && (unsigned)X < (unsigned)S2) {
+      const RowTap c0 = ctab[2 * hx], c1 = ctab[2 * hx + 1];
 #pragma unroll
-      for (int pq = 0; pq < 4; ++pq) {
-        const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
-        float rgb[3];
-        if constexpr (SRC == 0) {
-          const int dy = oy - g.pad_h, dx = ox - g.pad_w;
-          rgb[0] = rgb[1] = rgb[2] = 114.f;
-          if (dy >= 0 && dy < g.h && dx >= 0 && dx < g.w) {
-            const LinTap2 ty = tap_of(dy, g.sy, g.rh), tx = tap_of(dx, g.sx, g.rw);
-            if (staged) {
-              const int r0 = ty.i0 - r_lo, r1 = ty.i1 - r_lo;
-              const int s0 = (int)((base_addr + (size_t)r0 * row_bytes) & 3), s1 = (int)((base_addr + (size_t)r1 * row_bytes) & 3);
-              const int x0 = (tx.i0 - c_lo) * 3, x1 = (tx.i1 - c_lo) * 3;
-              sample_rgb_lds2(reg, pitch, r0, r1, s0, s1, x0, x1, ty.f, tx.f, rgb);
-            } else {
-              sample_rgb(g.img, g.stride_px, ty, tx, rgb);
-            }
+      for (int a = 0; a < 2; ++a) {
+        const RowTap ry = rtab[2 * hy + a];
+        float2v rgb[3] = {{pad_val, pad_val}, {pad_val, pad_val}, {pad_val, pad_val}};  // (column 0, column 1)
+        if (ry.o0 >= 0) {
+          // separate calls keep the staged path on ds_read (not flat) loads
+          if (staged) bilinear_pair(reg, ry, c0, c1, ident, pad_val, rgb);
+          else bilinear_pair(g.img, ry, c0, c1, ident, pad_val, rgb);
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const float v = b ? rgb[c].y : rgb[c].x;
+            if constexpr (SRC == 0) out[(a * 2 + b) * 3 + c] = v * (1.0f / 255.0f);
+            else out[(a * 2 + b) * 3 + c] = (v * (1.0f / 255.0f) - p.mean[c]) * p.inv_std[c];
           }
-#pragma unroll
-          for (int c = 0; c < 3; ++c) out[pq * 3 + c] = rgb[c] * (1.0f / 255.0f);
-        } else {
-          rgb[0] = rgb[1] = rgb[2] = 0.f;
-          if (!g.empty) {
-            const LinTap2 ty = tap_of(oy, g.sy, g.rh), tx = tap_of(ox, g.sx, g.rw);
-            if (staged) {
-              const int r0 = ty.i0 - r_lo, r1 = ty.i1 - r_lo;
-              const int s0 = (int)((base_addr + (size_t)r0 * row_bytes) & 3), s1 = (int)((base_addr + (size_t)r1 * row_bytes) & 3);
-              const int x0 = (tx.i0 - c_lo) * 3, x1 = (tx.i1 - c_lo) * 3;
-              sample_rgb_lds2(reg, pitch, r0, r1, s0, s1, x0, x1, ty.f, tx.f, rgb);
-            } else {
-              sample_rgb(g.img, g.stride_px, ty, tx, rgb);
-            }
-          }
-#pragma unroll
-          for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (rgb[c] * (1.0f / 255.0f) - p.mean[c]) * p.inv_std[c];
         }
       }
     }
@@ -272,13 +315,15 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
       *(uint2*)(y + base + cb) = pack4(v);
     }
   }
+  }  // id
 }
 
 template <int SRC, int KS, int NF, int TH, int TW>
 static void stem_launch(const StemFusedParams& p, hipStream_t s) {
   const int S2 = p.S / 2;
   const int ntiles = ((S2 + TW - 1) / TW) * ((S2 + TH - 1) / TH);
-  const long blocks = (long)((p.cap + 7) / 8) * 8 * ntiles;
+  const int items = p.launch_cap > 0 ? std::min(p.launch_cap, p.cap) : p.cap;
+  const long blocks = (long)((items + 7) / 8) * 8 * ntiles;
   hipLaunchKernelGGL((stem_fused_kernel<SRC, KS, NF, TH, TW>), dim3((unsigned)blocks), dim3(256), 0, s, p);
 }
 

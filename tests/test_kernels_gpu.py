@@ -237,6 +237,30 @@ def test_ir_block_matches_torch(device, B, H, inp, hid, oup, s, res):
     _check(_nchw(y.cpu()), ref, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("H,inp,hid,oup,s,res,wave", [(112, 16, 96, 24, 2, False, True),
+                                                       (56, 24, 144, 24, 1, True, True),
+                                                       (28, 32, 192, 64, 2, False, False),
+                                                       (14, 64, 384, 64, 1, True, False)])
+def test_ir_block_grid_stride(device, H, inp, hid, oup, s, res, wave):
+    """Grid narrower than the live batch (launch_B < live count): workgroups / waves loop over the
+    remaining items and produce the full-grid result; items past the live count stay untouched."""
+    C = native()
+    g = torch.Generator().manual_seed(H + oup)
+    B = 5
+    x = (torch.rand(B, H, H, inp, generator=g) * 2).to(torch.bfloat16).to(device)
+    expand = (torch.randn(hid, inp, 1, 1, generator=g) / np.sqrt(inp), torch.randn(hid, generator=g) * 0.1)
+    dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
+    project = (torch.randn(oup, hid, 1, 1, generator=g) / np.sqrt(hid), torch.randn(oup, generator=g) * 0.1)
+    bdev = torch.tensor([4], dtype=torch.int32, device=device)
+    C.set_ir_wave(wave)
+    try:
+        full = AF.ir_block_nhwc(x, expand, dw, project, stride=s, res=res)
+        narrow = AF.ir_block_nhwc(x, expand, dw, project, stride=s, res=res, bdev=bdev, launch_B=1)
+    finally:
+        C.set_ir_wave(True)
+    assert torch.equal(narrow[:4].cpu(), full[:4].cpu())
+
+
 def test_ir_block_live_batch(device):
     """Crops past the device-side live count are not written."""
     g = torch.Generator().manual_seed(5)
@@ -358,11 +382,12 @@ def test_conv3x3_v3_cin16(device, H, s, Cin, Cout):
     _check(_nchw(y.cpu()), _ref_conv(xn.cpu(), w, b, s, 1, "silu"))
 
 
-@pytest.mark.parametrize("H,inp,hid,oup,res", [(112, 32, 32, 16, False), (56, 24, 144, 24, True),
-                                               (28, 32, 192, 32, True), (14, 64, 384, 64, True),
-                                               (20, 24, 144, 24, True)])
-def test_ir_wave_matches_block_kernel(device, H, inp, hid, oup, res):
-    """Wave-per-tile stride-1 IR kernel == block-cooperative kernel (same math)."""
+@pytest.mark.parametrize("H,inp,hid,oup,res,s", [(112, 32, 32, 16, False, 1), (56, 24, 144, 24, True, 1),
+                                                 (28, 32, 192, 32, True, 1), (14, 64, 384, 64, True, 1),
+                                                 (20, 24, 144, 24, True, 1), (112, 16, 96, 24, False, 2),
+                                                 (56, 24, 144, 32, False, 2)])
+def test_ir_wave_matches_block_kernel(device, H, inp, hid, oup, res, s):
+    """Wave-per-tile IR kernel (stride 1: 8x8 / 7x7 tiles, stride 2: 4x4) == block-cooperative kernel."""
     C = native()
     g = torch.Generator().manual_seed(H + hid)
     x = (torch.rand(2, inp, H, H, generator=g) * 2).to(torch.bfloat16)
@@ -371,10 +396,10 @@ def test_ir_wave_matches_block_kernel(device, H, inp, hid, oup, res):
     dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
     project = (torch.randn(oup, hid, 1, 1, generator=g) / np.sqrt(hid), torch.randn(oup, generator=g) * 0.1)
     xn = _nhwc(x).to(device)
-    yw = AF.ir_block_nhwc(xn, expand, dw, project, stride=1, res=res)
+    yw = AF.ir_block_nhwc(xn, expand, dw, project, stride=s, res=res)
     C.set_ir_wave(False)
     try:
-        yb = AF.ir_block_nhwc(xn, expand, dw, project, stride=1, res=res)
+        yb = AF.ir_block_nhwc(xn, expand, dw, project, stride=s, res=res)
     finally:
         C.set_ir_wave(True)
     assert (yw.float() - yb.float()).abs().max().item() <= 0.07
