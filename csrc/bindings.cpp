@@ -123,7 +123,6 @@ void py_ir_block(const py::dict& d) {
   p.Wo = req<int>(d, "Wo");
   p.B = req<int>(d, "B");
   p.bdev = ptr<const int*>(d, "bdev");
-  p.launch_B = get<int>(d, "launch_B", 0);
   prepare_kernels();
   ir_block(p, stream_of(d));
 }
@@ -251,7 +250,6 @@ ExecutorConfig config_from(const py::dict& d) {
   c.cand_cap = get<int>(d, "cand_cap", c.cand_cap);
   c.crop_cap_per_image = get<int>(d, "crop_cap_per_image", c.crop_cap_per_image);
   c.min_crop_cap = get<int>(d, "min_crop_cap", c.min_crop_cap);
-  c.crop_launch_per_image = get<int>(d, "crop_launch_per_image", c.crop_launch_per_image);
   c.pool_bytes_per_image = get<int64_t>(d, "pool_bytes_per_image", c.pool_bytes_per_image);
   c.det_size = get<int>(d, "det_size", c.det_size);
   c.cls_size = get<int>(d, "cls_size", c.cls_size);

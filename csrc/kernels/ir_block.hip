@@ -19,7 +19,6 @@
 // XOR-swizzled with g[(row>>2)&3], g = {0,2,3,1}: for the 16x16x32 operand
 // read (lane l: row l&15, chunk l>>4) every ds_read_b128 lane group
 // ({0-3,12-15,20-27}, ...) then touches 16 distinct 16-byte bank slots.
-#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -61,13 +60,9 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
   const int row = lane & 15, kq = lane >> 4;
   const int tiles_x = (p.Wo + TW - 1) / TW, tiles_y = (p.Ho + TH - 1) / TH;
   const int tiles = tiles_x * tiles_y;
-  // The grid covers launch_B items (the expected live count); workgroups stride over the live
-  // items (the capacity may be larger), so dead capacity costs no dispatches.
-  const int n_vb = live_batch(p.B, p.bdev) * tiles;
-  for (int vb = blockIdx.x; vb < n_vb; vb += gridDim.x) {
-  if (vb != (int)blockIdx.x) __syncthreads();  // previous tile's LDS reads are done
-  const int b = vb / tiles;
-  const int t = vb - b * tiles;
+  const int b = blockIdx.x / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int t = blockIdx.x - b * tiles;
   const int ty = t / tiles_x, tx = t - ty * tiles_x;
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
@@ -328,7 +323,6 @@ __global__ __launch_bounds__(256) void ir_block_kernel(const IrParams p) {
       *(uint2*)(yp + oc) = pack4(v);
     }
   }
-  }  // vb
 }
 
 template <int S, int TH, int TW, int MP, bool EXPAND>
@@ -345,7 +339,7 @@ static void ir_launch(const IrParams& p, hipStream_t s) {
   const size_t lds = ir_lds_bytes<S, TH, TW, MP, EXPAND>(p.inp_pad);
   if (lds > 160 * 1024) throw std::runtime_error("ir_block: LDS budget exceeded");
   const int tiles = ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW);
-  const long grid = (long)(p.launch_B > 0 ? std::min(p.launch_B, p.B) : p.B) * tiles;
+  const long grid = (long)p.B * tiles;
   if (grid <= 0) return;
   hipLaunchKernelGGL((ir_block_kernel<S, TH, TW, MP, EXPAND>), dim3((unsigned)grid), dim3(256), lds, s, p);
 }

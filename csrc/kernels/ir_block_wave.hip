@@ -9,7 +9,6 @@
 // 16-B global loads), depthwise (tap pairs via v_perm + v_dot2c_f32_bf16,
 // weights in registers), project (MFMA, accumulators in VGPRs).  LDS traffic
 // between phases is ordered by the wave's own instruction stream.
-#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -47,11 +46,9 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
 
   const int tiles_x = (p.Wo + TW - 1) / TW, tiles_y = (p.Ho + TH - 1) / TH;
   const int tiles = tiles_x * tiles_y;
-  // Waves stride over the live tiles (the grid covers launch_B items, not the whole capacity);
-  // LDS ops of one wave complete in order, so the next tile's staging cannot overtake this one's reads.
-  const int n_gt = live_batch(p.B, p.bdev) * tiles;
-  for (int gt = blockIdx.x * 4 + wave; gt < n_gt; gt += gridDim.x * 4) {
+  const int gt = blockIdx.x * 4 + wave;  // global tile index
   const int b = gt / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;  // whole wave exits; no block barrier follows
   const int t = gt - b * tiles;
   const int ty = t / tiles_x, tx = t - ty * tiles_x;
   const int oy0 = ty * TH, ox0 = tx * TW;
@@ -228,7 +225,6 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
       *(uint2*)(yp + oc) = pack4(v);
     }
   }
-  }  // gt
 }
 
 template <int S, int TH, int TW, int MP, int NS, bool EXPAND>
@@ -236,8 +232,7 @@ static void irw_launch(const IrParams& p, hipStream_t s) {
   constexpr int PIN_PAD = (((TH - 1) * S + 3) * ((TW - 1) * S + 3) + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
   constexpr size_t lds = 4 * (size_t)(NS * PIN_PAD * 64 + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64);
   static_assert(lds <= 160 * 1024, "LDS");
-  const long tiles = (long)((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) *
-                     (p.launch_B > 0 ? std::min(p.launch_B, p.B) : p.B);
+  const long tiles = (long)((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   if (tiles <= 0) return;
   hipLaunchKernelGGL((ir_wave_kernel<S, TH, TW, MP, NS, EXPAND>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), lds, s,
                      p);

@@ -87,7 +87,6 @@ struct IrParams {
   int y_cs, Ho, Wo;
   int B;
   const int* bdev;
-  int launch_B;             // batch items the grid covers (0: B); workgroups loop over live items past it
 };
 void ir_block(const IrParams& p, hipStream_t s);
 void ir_prepare();
@@ -273,7 +272,6 @@ struct StemFusedParams {
   const Ctrl* ctrl;         // live counts (n_images / n_crops, crop_base)
   const CropRef* crops;     // src 1
   int cap;                  // batch capacity (images or crops)
-  int launch_cap;           // items the grid covers (0: cap); workgroups loop over live items past it
   int S;                    // full-resolution side (letterbox T / crop S); output map is S/2 x S/2
   float mean[3], inv_std[3];  // src 1
   int KS;                   // stem kernel size over the s2d map (3 or 2)

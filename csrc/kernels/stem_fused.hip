@@ -24,8 +24,6 @@
 //
 // Numerics are identical to letterbox_s2d / crop_gather_s2d followed by the
 // stem conv: the same float ops produce the same bf16 s2d values.
-#include <algorithm>
-
 #include "common.h"
 #include "launch.h"
 
@@ -123,16 +121,11 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
 
   const int S2 = p.S >> 1;
   const int tiles_x = (S2 + TW - 1) / TW, tiles_y = (S2 + TH - 1) / TH, ntiles = tiles_x * tiles_y;
-  const int n_live = live_batch(p.cap, SRC == 0 ? &p.ctrl->n_images : &p.ctrl->n_crops);
-  // The grid covers launch_cap items (a multiple of 8 x ntiles workgroups, so a workgroup keeps its
-  // XCD); workgroups stride over the live items, so dead capacity costs no dispatches.
-  const int n_vb = (n_live + 7) / 8 * 8 * ntiles;
-  for (int id = blockIdx.x; id < n_vb; id += gridDim.x) {
-  if (id != (int)blockIdx.x) __syncthreads();  // previous item's LDS reads are done
-  const int xcd = id & 7, j = id >> 3;
+  const int id = blockIdx.x, xcd = id & 7, j = id >> 3;
   const int item = (j / ntiles) * 8 + xcd;  // every tile of one item lands on one XCD
   const int t = j - (j / ntiles) * ntiles;
-  if (item >= n_live) continue;
+  const int n_live = live_batch(p.cap, SRC == 0 ? &p.ctrl->n_images : &p.ctrl->n_crops);
+  if (item >= n_live) return;
   const int ty0 = (t / tiles_x) * TH, tx0 = (t % tiles_x) * TW;
 
   Src g;
@@ -315,15 +308,13 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
       *(uint2*)(y + base + cb) = pack4(v);
     }
   }
-  }  // id
 }
 
 template <int SRC, int KS, int NF, int TH, int TW>
 static void stem_launch(const StemFusedParams& p, hipStream_t s) {
   const int S2 = p.S / 2;
   const int ntiles = ((S2 + TW - 1) / TW) * ((S2 + TH - 1) / TH);
-  const int items = p.launch_cap > 0 ? std::min(p.launch_cap, p.cap) : p.cap;
-  const long blocks = (long)((items + 7) / 8) * 8 * ntiles;
+  const long blocks = (long)((p.cap + 7) / 8) * 8 * ntiles;
   hipLaunchKernelGGL((stem_fused_kernel<SRC, KS, NF, TH, TW>), dim3((unsigned)blocks), dim3(256), 0, s, p);
 }
 

@@ -350,11 +350,6 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
   const uint8_t* pool = resolve(bk, sl, BUF_POOL, 0, 1);
   const int B = bk.info.B, CC = bk.info.crop_cap;
   auto batch = [&](int64_t kind) { return kind == BATCH_CROPS ? CC : B; };
-  // grid width of the crop kernels that stride over live items (ir_block / ir_wave / stem_fused)
-  const int CL = cfg_.crop_launch_per_image > 0
-                     ? std::min(CC, std::max(cfg_.min_crop_cap, B * cfg_.crop_launch_per_image))
-                     : CC;
-  auto launch = [&](int64_t kind) { return kind == BATCH_CROPS ? CL : B; };
   auto bdev = [&](int64_t kind) -> const int* { return kind == BATCH_CROPS ? &ctrl->n_crops : &ctrl->n_images; };
   const uint8_t* W = d_weights_;
 
@@ -451,7 +446,6 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.Wo = (int)r[24];
         p.B = batch(r[25]);
         p.bdev = bdev(r[25]);
-        p.launch_B = launch(r[25]);
         ir_block(p, s);
         break;
       }
@@ -590,7 +584,6 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
           p.inv_std[c] = bits_to_float(r[15 + c]);
         }
         p.cap = batch(r[18]);
-        p.launch_cap = launch(r[18]);
         p.KS = (int)r[19];
         p.pool = pool;
         p.meta = meta;

@@ -83,10 +83,6 @@ struct ExecutorConfig {
   int cand_cap = 8400;        // candidates per image entering NMS (= anchors)
   int crop_cap_per_image = 8; // crops one classification pass holds, per image
   int min_crop_cap = 16;
-  // Grid width (crops per image) of the crop kernels that stride over the live crops: dispatching
-  // workgroups for the whole capacity would mostly launch dead ones (mean fan-out ~4 of 8).
-  // 0 = cover the capacity.
-  int crop_launch_per_image = 4;
   int64_t pool_bytes_per_image = 640LL * 640 * 3;  // staging bytes per image slot
   int det_size = 640;
   int cls_size = 224;

@@ -9,8 +9,6 @@ detection, the classifier's top-5 (ids, raw logits, softmax probabilities).
 """
 from __future__ import annotations
 
-import os
-
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -88,7 +86,6 @@ class GpuProgramRunner:
             "max_det": self.max_det,
             "cand_cap": int(program.meta.get("cand_cap", 8400)),
             "crop_cap_per_image": int(crop_cap_per_image or gcfg["crop_cap_per_image"]),
-            "crop_launch_per_image": int(os.environ.get("ARENA_CROP_LAUNCH", gcfg.get("crop_launch_per_image", 4))),
             "pool_bytes_per_image": int(pool_bytes_per_image),
             "det_size": int(program.meta.get("det_size", 640)),
             "cls_size": int(program.meta.get("cls_size", 224)),

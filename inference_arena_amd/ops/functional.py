@@ -86,10 +86,9 @@ def dwconv3x3_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride:
 
 
 def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: bool = False,
-                  bdev: torch.Tensor | None = None, launch_B: int = 0) -> torch.Tensor:
+                  bdev: torch.Tensor | None = None) -> torch.Tensor:
     """Fused MobileNetV2 inverted residual (expand 1x1+ReLU6 -> dw3x3+ReLU6 -> project 1x1 [+x]).
-    ``expand``/``dw``/``project`` are (weight, bias) pairs with BN folded; ``expand`` None for t=1.
-    ``launch_B`` > 0 sizes the grid for that many items; workgroups loop over the rest."""
+    ``expand``/``dw``/``project`` are (weight, bias) pairs with BN folded; ``expand`` None for t=1."""
     from ..engine.planner import pack_ir_weights
 
     B, H, W, C = x.shape
@@ -102,7 +101,7 @@ def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: boo
                        "hid_pad": pk["hid_pad"], "oup": pk["oup"], "oup_pad": pk["oup_pad"], "stride": stride,
                        "expand": int(expand is not None), "res": int(res),
                        **{k: _ptr(v) for k, v in dev.items()}, "y": _ptr(y), "y_cs": pk["oup"], "Ho": Ho,
-                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "launch_B": int(launch_B), "stream": _stream()})
+                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "stream": _stream()})
     torch.cuda.synchronize(x.device)  # keep the packed weights alive until the kernel ran
     return y
 

@@ -237,30 +237,6 @@ def test_ir_block_matches_torch(device, B, H, inp, hid, oup, s, res):
     _check(_nchw(y.cpu()), ref, rtol=3e-2, atol=3e-2)
 
 
-@pytest.mark.parametrize("H,inp,hid,oup,s,res,wave", [(112, 16, 96, 24, 2, False, True),
-                                                       (56, 24, 144, 24, 1, True, True),
-                                                       (28, 32, 192, 64, 2, False, False),
-                                                       (14, 64, 384, 64, 1, True, False)])
-def test_ir_block_grid_stride(device, H, inp, hid, oup, s, res, wave):
-    """Grid narrower than the live batch (launch_B < live count): workgroups / waves loop over the
-    remaining items and produce the full-grid result; items past the live count stay untouched."""
-    C = native()
-    g = torch.Generator().manual_seed(H + oup)
-    B = 5
-    x = (torch.rand(B, H, H, inp, generator=g) * 2).to(torch.bfloat16).to(device)
-    expand = (torch.randn(hid, inp, 1, 1, generator=g) / np.sqrt(inp), torch.randn(hid, generator=g) * 0.1)
-    dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
-    project = (torch.randn(oup, hid, 1, 1, generator=g) / np.sqrt(hid), torch.randn(oup, generator=g) * 0.1)
-    bdev = torch.tensor([4], dtype=torch.int32, device=device)
-    C.set_ir_wave(wave)
-    try:
-        full = AF.ir_block_nhwc(x, expand, dw, project, stride=s, res=res)
-        narrow = AF.ir_block_nhwc(x, expand, dw, project, stride=s, res=res, bdev=bdev, launch_B=1)
-    finally:
-        C.set_ir_wave(True)
-    assert torch.equal(narrow[:4].cpu(), full[:4].cpu())
-
-
 def test_ir_block_live_batch(device):
     """Crops past the device-side live count are not written."""
     g = torch.Generator().manual_seed(5)
