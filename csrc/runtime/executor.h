@@ -81,7 +81,7 @@ struct ExecutorConfig {
   int max_batch = 32;         // largest bucket; sizes the staging slots
   int max_det = 300;          // detections kept per image (reference: unbounded)
   int cand_cap = 8400;        // candidates per image entering NMS (= anchors)
-  int crop_cap_per_image = 8; // crops one classification pass holds, per image
+  int crop_cap_per_image = 6; // crops one classification pass holds, per image (overflow -> extra pass)
   int min_crop_cap = 16;
   int64_t pool_bytes_per_image = 640LL * 640 * 3;  // staging bytes per image slot
   int det_size = 640;

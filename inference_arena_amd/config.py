@@ -137,7 +137,7 @@ def get_gpu_config() -> dict[str, Any]:
         "replicas": [1],
         "dtype": "bf16",
         "batch_buckets": [1, 2, 4, 8, 16, 32],
-        "crop_cap_per_image": 8,
+        "crop_cap_per_image": 6,
         "max_det": 300,
         "weight_seed": 0,
         "fanout_target_mean": 4.0,
