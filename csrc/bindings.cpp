@@ -219,6 +219,25 @@ void py_crop_gather(const py::dict& d) {
   crop_gather_s2d(p, stream_of(d));
 }
 
+void py_head_pool(const py::dict& d) {
+  HeadPoolParams p{};
+  p.x = ptr<const void*>(d, "x");
+  p.xs = req<int>(d, "xs");
+  p.HW = req<int>(d, "HW");
+  p.K = req<int>(d, "K");
+  p.w = ptr<const void*>(d, "w");
+  p.Kpad = req<int>(d, "Kpad");
+  p.bias = ptr<const float*>(d, "bias");
+  p.N = req<int>(d, "N");
+  p.Npad = req<int>(d, "Npad");
+  p.y = ptr<void*>(d, "y");
+  p.ys = req<int>(d, "ys");
+  p.act = get<int>(d, "act", 0);
+  p.B = req<int>(d, "B");
+  p.bdev = ptr<const int*>(d, "bdev");
+  head_pool(p, stream_of(d));
+}
+
 void py_avgpool(const py::dict& d) {
   AvgPoolParams p{};
   p.x = ptr<const void*>(d, "x");
@@ -337,6 +356,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("crop_plan", &py_crop_plan);
   m.def("crop_gather_s2d", &py_crop_gather);
   m.def("global_avgpool", &py_avgpool);
+  m.def("head_pool", &py_head_pool);
   m.def("topk_softmax", &py_topk);
   m.attr("SIZEOF_IMAGE_META") = (int)sizeof(ImageMeta);
   m.attr("SIZEOF_CTRL") = (int)sizeof(Ctrl);

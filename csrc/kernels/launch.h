@@ -294,6 +294,23 @@ struct AvgPoolParams {
 };
 void global_avgpool(const AvgPoolParams& p, hipStream_t s);
 
+// MobileNetV2 head 1x1 conv + activation fused with the global average pool (csrc/kernels/head_pool.hip):
+// y[b][n] = mean_p act(sum_k x[b][p][k] w[n][k] + bias[n]), bf16 out.
+struct HeadPoolParams {
+  const void* x;            // bf16 [B][HW][xs]
+  int xs, HW, K;            // K = input channels (<= Kpad)
+  const void* w;            // bf16 [Npad][Kpad]
+  int Kpad;
+  const float* bias;        // [Npad]
+  int N, Npad;
+  void* y;                  // bf16 [B][ys]
+  int ys;
+  int act;
+  int B;
+  const int* bdev;
+};
+void head_pool(const HeadPoolParams& p, hipStream_t s);
+
 struct TopkResult {
   int idx[5];
   float logit[5];

@@ -591,6 +591,25 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         stem_fused(p, s);
         break;
       }
+      case OP_HEADPOOL: {
+        HeadPoolParams p{};
+        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.xs = (int)r[3];
+        p.HW = (int)r[4];
+        p.K = (int)r[5];
+        p.w = W + r[6];
+        p.Kpad = (int)r[7];
+        p.bias = (const float*)(W + r[8]);
+        p.N = (int)r[9];
+        p.Npad = (int)r[10];
+        p.y = resolve(bk, sl, r[11], r[12], 2);
+        p.ys = (int)r[13];
+        p.act = (int)r[14];
+        p.B = batch(r[15]);
+        p.bdev = bdev(r[15]);
+        head_pool(p, s);
+        break;
+      }
       case OP_AVGPOOL: {
         AvgPoolParams p{};
         p.x = resolve(bk, sl, r[1], 0, 2);

@@ -59,6 +59,7 @@ enum OpType : int64_t {
   OP_IRBLOCK = 14,
   OP_STEMFUSED = 15,
   OP_C3FUSED = 16,
+  OP_HEADPOOL = 17,
 };
 
 // Reserved buffer ids (the planner's arena buffers are ids >= 0).

@@ -45,6 +45,9 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   C3FUSED 1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 C1 7 CH 8 NB 9 res 10 w12 11 b12 12-15 (wb1, bb1, wb2, bb2) of
            bottleneck 0, 16-19 of bottleneck 1, 20 w3 21 b3 22 y_buf 23 y_coff 24 y_cs 25 batch_kind
            (whole YOLOv5 C3 block, intermediates in LDS, csrc/kernels/c3_fused.hip)
+  HEADPOOL 1 x_buf 2 x_coff 3 x_cs 4 HW 5 K 6 w_off 7 Kpad 8 b_off 9 N 10 Npad 11 y_buf 12 y_coff 13 y_cs
+           14 act 15 batch_kind
+           (MobileNetV2 head 1x1 conv + activation + global average pool, csrc/kernels/head_pool.hip)
 """
 from __future__ import annotations
 
@@ -56,7 +59,7 @@ import torch
 
 OP_FIELDS = 48
 (OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
- OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED) = range(1, 17)
+ OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL) = range(1, 18)
 BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK, BUF_RAWOUT = -1, -10, -11, -12, -13, -14, -15, -16
 IMAGES, CROPS = 0, 1
 ACT = {None: 0, "none": 0, "silu": 1, "relu6": 2}
@@ -365,6 +368,17 @@ class ProgramBuilder:
     def crop_gather(self, crops: Buffer, out: Buffer, S: int, mean, std) -> None:
         rec = [OP_CROPGATHER, crops.id, out.id, S] + [fbits(m) for m in mean] + [fbits(1.0 / s) for s in std]
         self._emit(rec, crops, out)
+
+    def head_pool(self, src: View, dst: View, w: torch.Tensor, b: torch.Tensor, *, act: str | None = "relu6",
+                  kind: int = CROPS) -> None:
+        """1x1 conv + activation + global average pool in one kernel: ``dst`` is a 1x1 map."""
+        cout, cin, kh, kw = w.shape
+        if (kh, kw) != (1, 1) or cin != src.C or cout != dst.C or dst.buf.H * dst.buf.W != 1:
+            raise ValueError("head_pool: expects 1x1 weights [N, C, 1, 1] and a 1x1 destination")
+        wb, bb, kpad, cpad = pack_conv_weight(w, b)
+        rec = [OP_HEADPOOL, src.bid, src.coff, src.cs, src.buf.H * src.buf.W, cin, self.weights.add(wb), kpad,
+               self.weights.add(bb), cout, cpad, dst.bid, dst.coff, dst.cs, ACT[act], kind]
+        self._emit(rec, src, dst)
 
     def avgpool(self, x: Buffer, y: Buffer, kind: int = CROPS) -> None:  # noqa: D401
         self._emit([OP_AVGPOOL, x.id, x.H * x.W, x.C, y.id, kind], x, y)

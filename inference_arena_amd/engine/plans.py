@@ -109,6 +109,12 @@ def fuse_stem_default() -> bool:
     return os.environ.get("ARENA_FUSE_STEM", "1").lower() not in ("0", "false", "no", "off")
 
 
+def fuse_head_pool_default() -> bool:
+    """``ARENA_FUSE_POOL`` (default 1): MobileNetV2's last 1x1 conv and the global average pool run as one
+    kernel (head_pool op); the 7x7x1280 map is never stored."""
+    return os.environ.get("ARENA_FUSE_POOL", "1").lower() not in ("0", "false", "no", "off")
+
+
 def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool = False,
               fuse_stem: bool | None = None):
     h = T // 2
@@ -258,10 +264,13 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
         pb.conv(View(Dw, 0, blk.hidden), View(O, 0, blk.oup), *fold(blk.project), act=None,
                 res=View(cur, 0, blk.inp) if blk.use_res else None, kind=CROPS_)
         cur, H = O, Ho
-    HD = pb.tensor("m.head", H, H, 1280, kind=CROPS_)
-    pb.conv(View(cur, 0, cur.C), View(HD, 0, 1280), *fold(m.head), act="relu6", kind=CROPS_)
     PO = pb.tensor("m.pool", 1, 1, 1280, kind=CROPS_)
-    pb.avgpool(HD, PO, kind=CROPS_)
+    if fuse_head_pool_default() and H * H <= 64 and cur.C == 320:
+        pb.head_pool(View(cur, 0, cur.C), View(PO, 0, 1280), *fold(m.head), act="relu6", kind=CROPS_)
+    else:
+        HD = pb.tensor("m.head", H, H, 1280, kind=CROPS_)
+        pb.conv(View(cur, 0, cur.C), View(HD, 0, 1280), *fold(m.head), act="relu6", kind=CROPS_)
+        pb.avgpool(HD, PO, kind=CROPS_)
     ncls = m.fc.out_features
     wfc = m.fc.weight.detach().float().cpu().reshape(ncls, 1280, 1, 1)
     if raw_logits:  # reference contract: [1000] fp32 logits per input, straight into the output region

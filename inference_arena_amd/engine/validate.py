@@ -19,6 +19,7 @@ from ..engine.planner import (
     CROPS,
     OP_AVGPOOL,
     OP_C3FUSED,
+    OP_HEADPOOL,
     OP_CONV,
     OP_CROPGATHER,
     OP_CROPPLAN,
@@ -180,6 +181,15 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             S2 = int(r[3]) // 2
             need(i, r[1], 0, B * max_det * CROP_BYTES, "crop refs")
             need(i, r[2], 0, crop_cap * S2 * S2 * 32, "crop gather output")
+        elif op == OP_HEADPOOL:
+            n = kind_n(r[15])
+            HW, K, Kpad, N, Npad = int(r[4]), int(r[5]), int(r[7]), int(r[9]), int(r[10])
+            if not (0 < HW <= 64) or Kpad != 320 or K > Kpad or N % 4 or Npad % 16 or Npad < N:
+                raise ProgramError(f"op {i}: head_pool geometry HW={HW} K={K} Kpad={Kpad} N={N} unsupported")
+            view(i, r[1], int(r[2]), int(r[3]), n * HW, K, 2, "head_pool input")
+            weights(i, int(r[6]), Npad * Kpad * 2, "head_pool weight")
+            weights(i, int(r[8]), Npad * 4, "head_pool bias")
+            view(i, r[11], int(r[12]), int(r[13]), n, N, 2, "head_pool output")
         elif op == OP_AVGPOOL:
             n = kind_n(r[5])
             need(i, r[1], 0, n * int(r[2]) * int(r[3]) * 2, "avgpool input")

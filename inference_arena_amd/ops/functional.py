@@ -161,6 +161,24 @@ def avgpool_nhwc(x: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def head_pool_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, act: str | None = "relu6",
+                   bdev: torch.Tensor | None = None) -> torch.Tensor:
+    """mean over pixels of act(conv1x1(x, w) + b): [B,H,W,C] bf16 -> [B, N] bf16 (head_pool.hip)."""
+    from ..engine.planner import ACT, pack_conv_weight
+
+    B, H, W, C = x.shape
+    N = w.shape[0]
+    wb, bb, kpad, npad = pack_conv_weight(w, b)
+    wd = torch.frombuffer(bytearray(wb), dtype=torch.bfloat16).to(x.device)
+    bd = torch.frombuffer(bytearray(bb), dtype=torch.float32).to(x.device)
+    y = torch.empty(B, N, dtype=torch.bfloat16, device=x.device)
+    native().head_pool({"x": _ptr(x), "xs": C, "HW": H * W, "K": C, "w": _ptr(wd), "Kpad": kpad, "bias": _ptr(bd),
+                        "N": N, "Npad": npad, "y": _ptr(y), "ys": N, "act": ACT[act], "B": B, "bdev": _ptr(bdev),
+                        "stream": _stream()})
+    torch.cuda.synchronize(x.device)  # keep the packed weights alive until the kernel ran
+    return y
+
+
 def topk_softmax(logits: torch.Tensor):
     """[B, N] fp32 -> (idx [B,5] int32, logit [B,5], prob [B,5])."""
     B, N = logits.shape

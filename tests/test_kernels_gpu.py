@@ -237,6 +237,22 @@ def test_ir_block_matches_torch(device, B, H, inp, hid, oup, s, res):
     _check(_nchw(y.cpu()), ref, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("B,HW,live", [(3, 7, None), (5, 7, 3), (2, 8, None)])
+def test_head_pool_matches_torch(device, B, HW, live):
+    """Fused head 1x1 conv (320 -> 1280) + ReLU6 + global average pool vs fp32 torch; crops past the
+    device-side live count are not written."""
+    g = torch.Generator().manual_seed(B * 10 + HW)
+    x = (torch.rand(B, 320, HW, HW, generator=g) * 2).to(torch.bfloat16)
+    w = torch.randn(1280, 320, 1, 1, generator=g) / np.sqrt(320)
+    b = torch.randn(1280, generator=g) * 0.5
+    xn = _nhwc(x).to(device)
+    bdev = None if live is None else torch.tensor([live], dtype=torch.int32, device=device)
+    y = AF.head_pool_nhwc(xn, w, b, "relu6", bdev=bdev)
+    ref = F.relu6(F.conv2d(x.float(), _bf(w), b.float())).mean(dim=(2, 3))
+    n = B if live is None else live
+    _check(y[:n].float().cpu(), ref[:n], rtol=2e-2, atol=2e-2)
+
+
 def test_ir_block_live_batch(device):
     """Crops past the device-side live count are not written."""
     g = torch.Generator().manual_seed(5)

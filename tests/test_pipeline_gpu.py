@@ -116,6 +116,31 @@ def test_fused_stem_matches_unfused(dense_models, device, monkeypatch):
             np.testing.assert_allclose(y.topk_logit[:, 0], x.topk_logit[:, 0], rtol=0.05, atol=0.05)
 
 
+def test_fused_head_pool_matches_unfused(dense_models, device, monkeypatch):
+    """MobileNetV2 head conv + global average pool as one kernel (head_pool) vs conv + avgpool: same pooled
+    features (fp32 sum before one bf16 rounding vs per-pixel bf16) and the same classifications."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    imgs = synthetic_images(4, 51)
+    monkeypatch.setenv("ARENA_FUSE_POOL", "0")
+    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    monkeypatch.setenv("ARENA_FUSE_POOL", "1")
+    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    assert any(int(op[0]) == 17 for op in fused.program.ops) and not any(int(op[0]) == 17 for op in plain.program.ops)
+    a, b = plain.infer(imgs), fused.infer(imgs)
+    n = sum(len(r) for r in a)
+    assert n > 0
+    for c in range(min(n, 8)):
+        pa, pb = plain.read_buffer("m.pool", 4, c), fused.read_buffer("m.pool", 4, c)
+        np.testing.assert_allclose(pb, pa, atol=0.02 + 0.01 * np.abs(pa).max())
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        if len(x):
+            assert (x.topk_idx[:, 0] == y.topk_idx[:, 0]).mean() >= 0.9
+            np.testing.assert_allclose(y.topk_logit[:, 0], x.topk_logit[:, 0], rtol=0.03, atol=0.05)
+
+
 def test_fused_head_pointwise_matches_unfused(dense_models, device, monkeypatch):
     """Detect head: second 3x3 of each branch with the final 1x1 fused into its epilogue (v3 kernel) vs
     the separate 3x3 + 1x1 convs: same head outputs at every level and the same detections."""

@@ -20,7 +20,8 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 KIND = {1: "conv", 2: "dwconv", 3: "sppf", 4: "letterbox", 5: "zero", 6: "decode", 7: "nms", 8: "cropplan",
-        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw", 14: "irblock", 15: "stemfused", 16: "c3fused"}
+        9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw", 14: "irblock", 15: "stemfused", 16: "c3fused",
+        17: "headpool"}
 FIRST_KERNEL = {4: "letterbox", 12: "tensor_in", 15: "stem_fused"}
 
 

@@ -41,6 +41,7 @@ SOURCES = [
     "kernels/stem_fused.hip",
     "kernels/detect.hip",
     "kernels/classify_head.hip",
+    "kernels/head_pool.hip",
     "runtime/executor.cpp",
     "runtime/batcher.cpp",
     "runtime/trace.cpp",
