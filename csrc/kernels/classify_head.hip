@@ -38,6 +38,8 @@ void global_avgpool(const AvgPoolParams& p, hipStream_t s) {
   hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
 }
 
+constexpr int kTopkPer = 16;  // row elements per lane held in registers
+
 // One wave per row.  Each round finds the (value, first index) maximum over
 // the row with the previously chosen indices excluded.
 __global__ __launch_bounds__(256) void topk_kernel(const TopkParams p) {
@@ -48,37 +50,78 @@ __global__ __launch_bounds__(256) void topk_kernel(const TopkParams p) {
   else if (p.bdev != nullptr) B = live_batch(p.B, p.bdev);
   if (row >= B) return;
   const float* x = p.logits + (size_t)row * p.ld;
-  float mx = -INFINITY;
-  for (int i = lane; i < p.N; i += 64) mx = fmaxf(mx, x[i]);
-  mx = wave_max(mx);
-  float se = 0.f;
-  for (int i = lane; i < p.N; i += 64) se += __expf(x[i] - mx);
-  se = wave_sum(se);
-  const float inv = 1.0f / se;
-
   TopkResult res;
-  int chosen[5] = {-1, -1, -1, -1, -1};
+  if (p.N <= 64 * kTopkPer) {
+    // Whole row in registers (16 values per lane for N <= 1024): the seven passes over it (max, sum,
+    // 5 selection rounds) read no memory, so one load latency per row instead of seven chains.
+    float v[kTopkPer];
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int i = lane; i < p.N; i += 64) {
-      bool skip = false;
-#pragma unroll
-      for (int q = 0; q < 5; ++q) skip |= (q < k) && (chosen[q] == i);
-      const float v = x[i];
-      if (!skip && (v > bv || (v == bv && i < bi))) { bv = v; bi = i; }
+    for (int j = 0; j < kTopkPer; ++j) {
+      const int i = lane + 64 * j;
+      v[j] = i < p.N ? x[i] : -INFINITY;
     }
+    float mx = -INFINITY;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    for (int j = 0; j < kTopkPer; ++j) mx = fmaxf(mx, v[j]);
+    mx = wave_max(mx);
+    float se = 0.f;
+#pragma unroll
+    for (int j = 0; j < kTopkPer; ++j)
+      if (lane + 64 * j < p.N) se += __expf(v[j] - mx);
+    se = wave_sum(se);
+    const float inv = 1.0f / se;
+    unsigned taken = 0;  // bit j: element lane + 64 j already chosen
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < kTopkPer; ++j) {
+        const int i = lane + 64 * j;
+        if (i < p.N && !((taken >> j) & 1u) && (v[j] > bv || (v[j] == bv && i < bi))) { bv = v[j]; bi = i; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      if ((bi & 63) == lane) taken |= 1u << (bi >> 6);
+      res.idx[k] = bi;
+      res.logit[k] = bv;
+      res.prob[k] = __expf(bv - mx) * inv;
     }
-    chosen[k] = bi;
-    res.idx[k] = bi;
-    res.logit[k] = bv;
-    res.prob[k] = __expf(bv - mx) * inv;
+  } else {
+    float mx = -INFINITY;
+    for (int i = lane; i < p.N; i += 64) mx = fmaxf(mx, x[i]);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int i = lane; i < p.N; i += 64) se += __expf(x[i] - mx);
+    se = wave_sum(se);
+    const float inv = 1.0f / se;
+    int chosen[5] = {-1, -1, -1, -1, -1};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int i = lane; i < p.N; i += 64) {
+        bool skip = false;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) skip |= (q < k) && (chosen[q] == i);
+        const float v = x[i];
+        if (!skip && (v > bv || (v == bv && i < bi))) { bv = v; bi = i; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      chosen[k] = bi;
+      res.idx[k] = bi;
+      res.logit[k] = bv;
+      res.prob[k] = __expf(bv - mx) * inv;
+    }
   }
   res.pad_ = 0;
   if (lane == 0) {

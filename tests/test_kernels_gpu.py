@@ -188,6 +188,13 @@ def test_topk_and_avgpool(device):
     assert torch.equal(idx.long(), ref_i)
     assert torch.allclose(lg, ref_v)
     assert torch.allclose(pr, torch.softmax(logits, 1).gather(1, ref_i), rtol=1e-4, atol=1e-6)
+    # ties resolve to the lowest index (register path, N <= 1024) and the streaming path (N > 1024)
+    for N in (1000, 77, 1500):
+        t = torch.randint(0, 6, (9, N), generator=g).float()
+        idx, lg, _ = AF.topk_softmax(t.to(device))
+        order = np.lexsort((np.arange(N)[None, :].repeat(9, 0), -t.numpy()), axis=1)[:, :5]
+        assert np.array_equal(idx.cpu().numpy(), order), N
+        assert torch.equal(lg.cpu(), t.gather(1, torch.from_numpy(order)))
     x = torch.randn(5, 7, 7, 1280, generator=g).to(torch.bfloat16)
     y = AF.avgpool_nhwc(x.to(device))
     torch.cuda.synchronize()
