@@ -580,6 +580,7 @@ void conv2d(const ConvParams& p, hipStream_t s) {
     if (!conv3x3_v3(p, s)) throw std::runtime_error("conv2d: fused pointwise epilogue needs a v3-eligible 3x3 conv");
     return;
   }
+  if (conv_fc(p, s)) return;  // classifier FC: split-K GEMM, whatever the family
   const int impl = p.impl ? p.impl : conv_impl();
   if (impl == 3) {
     conv_igemm(p, s);

@@ -49,6 +49,7 @@ void conv_igemm(const ConvParams& p, hipStream_t s);  // LDS-pipelined implicit 
 bool conv_pw(const ConvParams& p, hipStream_t s);     // 1x1 stride-1 fast path; false if unsupported
 void set_conv_pw(bool v);                             // ARENA_CONV_PW=0 disables the fast path
 bool conv3x3_v3(const ConvParams& p, hipStream_t s);  // 3x3 halo-tile v3; false if unsupported
+bool conv_fc(const ConvParams& p, hipStream_t s);     // 1x1 conv on a 1x1 map, K 1280 (split-K FC); false if not
 void set_conv_v3(bool v);                             // ARENA_CONV_V3=0 falls back to the v2 tile kernel
 // Conv kernel family: 1 = direct global->VGPR loads, 2 = LDS-staged (default).
 void set_conv_impl(int v);

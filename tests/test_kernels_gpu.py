@@ -260,6 +260,20 @@ def test_head_pool_matches_torch(device, B, HW, live):
     _check(y[:n].float().cpu(), ref[:n], rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("B,live,f32", [(37, None, True), (20, 9, True), (16, None, False)])
+def test_fc_splitk_matches_torch(device, B, live, f32):
+    """Classifier FC (1x1 conv on a 1x1 map, 1280 -> 1000) on the split-K kernel vs fp32 torch."""
+    g = torch.Generator().manual_seed(B)
+    x = torch.randn(B, 1280, 1, 1, generator=g).to(torch.bfloat16)
+    w = torch.randn(1000, 1280, 1, 1, generator=g) / np.sqrt(1280)
+    b = torch.randn(1000, generator=g)
+    bdev = None if live is None else torch.tensor([live], dtype=torch.int32, device=device)
+    y = AF.conv2d_nhwc(_nhwc(x).to(device), w, b, f32out=f32, bdev=bdev)
+    ref = F.conv2d(x.float(), _bf(w), b.float())
+    n = B if live is None else live
+    _check(_nchw(y.cpu()).float()[:n], ref[:n], rtol=1e-2, atol=1e-2)
+
+
 def test_ir_block_live_batch(device):
     """Crops past the device-side live count are not written."""
     g = torch.Generator().manual_seed(5)

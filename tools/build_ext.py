@@ -42,6 +42,7 @@ SOURCES = [
     "kernels/detect.hip",
     "kernels/classify_head.hip",
     "kernels/head_pool.hip",
+    "kernels/fc_splitk.hip",
     "runtime/executor.cpp",
     "runtime/batcher.cpp",
     "runtime/trace.cpp",
