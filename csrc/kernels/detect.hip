@@ -327,36 +327,57 @@ __global__ __launch_bounds__(256) void crop_plan_kernel(const CropPlanParams p) 
     }
     return;
   }
-  if (tid == 0) {
-    int acc = 0;
-    for (int b = 0; b < n_img; ++b) {
-      offs[b] = acc;
-      int k = p.det_count[b];
-      acc += k < p.max_det ? k : p.max_det;
+  // Per-image crop offsets: every count is loaded at once, wave 0 scans them in 64-wide chunks
+  // (a serial loop over det_count[] paid one global latency per image).
+  for (int b = tid; b < n_img; b += blockDim.x) {
+    const int k = p.det_count[b];
+    offs[b + 1] = k < p.max_det ? k : p.max_det;
+  }
+  if (tid == 0) offs[0] = 0;
+  __syncthreads();
+  if (tid < 64) {
+    int carry = 0;
+    for (int base = 0; base < n_img; base += 64) {
+      const int i = base + tid;
+      int v = i < n_img ? offs[i + 1] : 0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(v, o, 64);
+        if (tid >= o) v += u;
+      }
+      if (i < n_img) offs[i + 1] = v + carry;
+      carry += __shfl(v, 63, 64);
     }
-    offs[n_img] = acc;
-    Ctrl* c = p.ctrl;
-    c->total_crops = acc;
-    int rem = acc - c->crop_base;
-    rem = rem < 0 ? 0 : rem;
-    c->n_crops = rem < p.crop_cap ? rem : p.crop_cap;
+    if (tid == 0) {
+      Ctrl* c = p.ctrl;
+      c->total_crops = carry;
+      int rem = carry - c->crop_base;
+      rem = rem < 0 ? 0 : rem;
+      c->n_crops = rem < p.crop_cap ? rem : p.crop_cap;
+    }
   }
   __syncthreads();
-  for (int b = 0; b < n_img; ++b) {
-    const int k = offs[b + 1] - offs[b];
-    const ImageMeta m = p.meta[b];
-    for (int d = tid; d < k; d += blockDim.x) {
-      const Detection det = p.det[(size_t)b * p.max_det + d];
-      CropRef r;
-      r.img = b;
-      r.x1 = max(0, (int)det.x1);
-      r.y1 = max(0, (int)det.y1);
-      r.x2 = min(m.w, (int)det.x2);
-      r.y2 = min(m.h, (int)det.y2);
-      r.det = d;
-      r.pad_[0] = r.pad_[1] = 0;
-      p.crops[offs[b] + d] = r;
+  // one crop per thread: image = last b with offs[b] <= i (binary search over the LDS offsets)
+  const int total = offs[n_img];
+  for (int i = tid; i < total; i += blockDim.x) {
+    int lo = 0, hi = n_img - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (offs[mid] <= i) lo = mid;
+      else hi = mid - 1;
     }
+    const int b = lo, d = i - offs[lo];
+    const ImageMeta m = p.meta[b];
+    const Detection det = p.det[(size_t)b * p.max_det + d];
+    CropRef r;
+    r.img = b;
+    r.x1 = max(0, (int)det.x1);
+    r.y1 = max(0, (int)det.y1);
+    r.x2 = min(m.w, (int)det.x2);
+    r.y2 = min(m.h, (int)det.y2);
+    r.det = d;
+    r.pad_[0] = r.pad_[1] = 0;
+    p.crops[i] = r;
   }
 }
 

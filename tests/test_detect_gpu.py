@@ -139,3 +139,34 @@ def test_crop_plan_and_gather(device):
             err = (got[k] - ref).abs()
             assert err.max() < 3 * (1 / 255) / 0.224 + 0.05, (k, err.max())
             k += 1
+
+
+def test_crop_plan_offsets_many_images(device):
+    """Crop offsets over 70 images (more than one 64-wide scan chunk), empty images and counts above
+    max_det: every crop lands at its image's offset in image-major / detection-minor order."""
+    C = native()
+    rng = np.random.default_rng(11)
+    B, max_det = 70, 8
+    imgs = [np.zeros((16, 24, 3), np.uint8) for _ in range(B)]
+    counts = rng.integers(0, 12, B).astype(np.int32)
+    counts[[0, 5, 63, 64, 69]] = 0
+    det = np.zeros((B, max_det, 8), np.float32)
+    det[:, :, 2], det[:, :, 3] = 20.0, 10.0
+    meta, _ = AF.image_meta_bytes(imgs, 640)
+    meta_t = torch.frombuffer(bytearray(meta), dtype=torch.uint8).to(device)
+    det_t, dcnt_t = torch.from_numpy(det).to(device), torch.from_numpy(counts).to(device)
+    crops = torch.full((B * max_det, 8), -1, dtype=torch.int32, device=device)
+    ctrl = AF.ctrl_tensor(B, device)
+    C.crop_plan({"det": det_t.data_ptr(), "det_count": dcnt_t.data_ptr(), "max_det": max_det,
+                 "meta": meta_t.data_ptr(), "B": B, "crops": crops.data_ptr(), "ctrl": ctrl.data_ptr(),
+                 "crop_cap": 100, "stream": torch.cuda.current_stream().cuda_stream})
+    torch.cuda.synchronize()
+    kept = np.minimum(counts, max_det)
+    total = int(kept.sum())
+    c = ctrl.cpu().numpy()
+    assert c[3] == total and c[1] == min(total, 100)
+    got = crops.cpu().numpy()[:total]
+    want_img = np.repeat(np.arange(B), kept)
+    want_det = np.concatenate([np.arange(k) for k in kept])
+    assert np.array_equal(got[:, 0], want_img) and np.array_equal(got[:, 5], want_det)
+    assert (got[:, 3] == 20).all() and (got[:, 4] == 10).all()  # x2 / y2 clamped to the 24x16 image
