@@ -41,9 +41,18 @@ __global__ __launch_bounds__(256) void sppf_kernel(const SppfParams p) {
   uint4* h9 = sp + 4 * HW;
   uint4* h13 = sp + 6 * HW;
   bf16* buf = (bf16*)p.buf + (size_t)b * HW * p.xs;
-  for (int i = threadIdx.x; i < HW * 2; i += 256) {
-    const int pix = i >> 1, c = i & 1;
-    in[i] = *(const uint4*)(buf + (size_t)pix * p.xs + c0 + c * 8);
+  // all loads issued before the first LDS store: one memory latency, not one per 256 pieces
+  constexpr int kIt = (SPPF_MAX_PIX * 2 + 255) / 256;
+  uint4 tmp[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int i = threadIdx.x + it * 256;
+    if (i < HW * 2) tmp[it] = *(const uint4*)(buf + (size_t)(i >> 1) * p.xs + c0 + (i & 1) * 8);
+  }
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int i = threadIdx.x + it * 256;
+    if (i < HW * 2) in[i] = tmp[it];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < HW * 2; i += 256) {
