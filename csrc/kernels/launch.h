@@ -280,9 +280,17 @@ struct StemFusedParams {
   int Kpad;
   const float* bias;
   int Cout;
-  void* y;                  // bf16 [cap, S/2, S/2, ys]
+  void* y;                  // bf16 [cap, S/2, S/2, ys] (unused when w2 is set)
   int ys;
   int act;
+  // Optional second conv (detector only): 3x3 stride 2, 16 -> Cout2, pad 1, on the stem output, which then
+  // stays in LDS; y2 = bf16 [cap, S/4, S/4, y2s].
+  const void* w2;           // bf16 [Cout2][Kpad2], k = tap*16 + c
+  int Kpad2;
+  const float* bias2;
+  int Cout2, act2;
+  void* y2;
+  int y2s;
 };
 void stem_fused(const StemFusedParams& p, hipStream_t s);
 

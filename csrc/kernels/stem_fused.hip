@@ -110,24 +110,9 @@ struct Src {
 // the budget (strongly downscaled images, large crops) sample global memory.
 constexpr int kSrcBudget = 8192;  // 16 KB measured slower: LDS held occupancy at 5 workgroups / CU
 
-template <int SRC, int KS, int NF, int TH, int TW>
-__global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p) {
-  constexpr int HH = TH + KS - 1, HW = TW + KS - 1, NPIX = HH * HW;
-  constexpr int SLABS = (KS * KS * 16 + 31) / 32;
-  static_assert(TH * TW == 256, "one 256-pixel tile per workgroup (4 waves x 4 fragments)");
-  static_assert(2 * HH <= 64 && 2 * HW <= 192, "tap tables are built by waves 0 / 1-3");
-  __shared__ __align__(16) uint4 tile[NPIX * 2];  // 32 B per s2d pixel
-  __shared__ __align__(16) uint32_t region[kSrcBudget / 4];
-
-  const int S2 = p.S >> 1;
-  const int tiles_x = (S2 + TW - 1) / TW, tiles_y = (S2 + TH - 1) / TH, ntiles = tiles_x * tiles_y;
-  const int id = blockIdx.x, xcd = id & 7, j = id >> 3;
-  const int item = (j / ntiles) * 8 + xcd;  // every tile of one item lands on one XCD
-  const int t = j - (j / ntiles) * ntiles;
-  const int n_live = live_batch(p.cap, SRC == 0 ? &p.ctrl->n_images : &p.ctrl->n_crops);
-  if (item >= n_live) return;
-  const int ty0 = (t / tiles_x) * TH, tx0 = (t % tiles_x) * TW;
-
+// Source geometry of batch item `item` (image letterboxed to p.S, or crop resized to p.S x p.S).
+template <int SRC>
+__device__ __forceinline__ Src make_src(const StemFusedParams& p, int item) {
   Src g;
   if constexpr (SRC == 0) {
     const ImageMeta m = p.meta[item];
@@ -156,11 +141,25 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
     g.sx = g.empty ? 1.f : (float)((double)cw / (double)p.S);
   }
 
+  return g;
+}
+
+// Space-to-depth halo tile of HH x HW s2d pixels starting at s2d position (sY0, sX0): phase 0
+// stages the source bytes it samples in `region` (when they fit in BUDGET bytes), the tap tables
+// are built, and phase 1 writes 32 B (16 bf16 channels, 12 live) per s2d pixel into `tile`;
+// pixels outside the S/2 x S/2 map are zero (the stem conv's padding).  Ends with the tile
+// written by this thread (callers barrier before reading it).
+template <int SRC, int HH, int HW, int BUDGET>
+__device__ __forceinline__ void build_s2d_tile(const StemFusedParams& p, const Src& g, int sY0, int sX0, uint4* tile,
+                                               uint32_t* region, RowTap* rtab, RowTap* ctab) {
+  constexpr int NPIX = HH * HW;
+  static_assert(2 * HH <= 64 && 2 * HW <= 192, "tap tables are built by waves 0 / 1-3");
+  const int S2 = p.S >> 1;
   // ---- phase 0: source rows / columns this tile samples -> LDS (when they fit)
   // sub-pixel rows/cols of the halo tile, clamped to the sampled area
   const int lim_y = SRC == 0 ? g.h : p.S, lim_x = SRC == 0 ? g.w : p.S;
-  const int sy_lo = max(2 * (ty0 - 1) - g.pad_h, 0), sy_hi = min(2 * (ty0 + TH) + 1 - g.pad_h, lim_y - 1);
-  const int sx_lo = max(2 * (tx0 - 1) - g.pad_w, 0), sx_hi = min(2 * (tx0 + TW) + 1 - g.pad_w, lim_x - 1);
+  const int sy_lo = max(2 * sY0 - g.pad_h, 0), sy_hi = min(2 * (sY0 + HH - 1) + 1 - g.pad_h, lim_y - 1);
+  const int sx_lo = max(2 * sX0 - g.pad_w, 0), sx_hi = min(2 * (sX0 + HW - 1) + 1 - g.pad_w, lim_x - 1);
   bool staged = false;
   int r_lo = 0, c_lo = 0, pitch = 0;
   const size_t row_bytes = (size_t)g.stride_px * 3;
@@ -171,7 +170,7 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
     const int nrows = r_hi - r_lo + 1, rbytes = (c_hi - c_lo + 1) * 3;
     const int ndw = (rbytes + 3 + 3) >> 2;  // up to 3 bytes of alignment shift in front
     pitch = ndw * 4;
-    staged = nrows * pitch <= kSrcBudget;
+    staged = nrows * pitch <= BUDGET;
     if (staged) {
       const uint8_t* base = g.img + (size_t)r_lo * row_bytes + (size_t)c_lo * 3;
       for (int i = threadIdx.x; i < nrows * ndw; i += 256) {
@@ -190,10 +189,8 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
   // image, and the lerp weight), so the per-sub-pixel work below is lookups,
   // 12 byte loads and the lerps.  o0 < 0 marks a row / column outside the
   // sampled area (letterbox border -> 114, empty crop -> 0).
-  __shared__ RowTap rtab[2 * HH];
-  __shared__ RowTap ctab[2 * HW];
   if (threadIdx.x < 2 * HH) {
-    const int d = 2 * (ty0 - 1) + (int)threadIdx.x - g.pad_h;
+    const int d = 2 * sY0 + (int)threadIdx.x - g.pad_h;
     RowTap e{-1, -1, 0.f};
     if (!g.empty && d >= 0 && d < (SRC == 0 ? g.h : p.S)) {
       const LinTap2 t = tap_of(d, g.sy, g.rh);
@@ -210,7 +207,7 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
     rtab[threadIdx.x] = e;
   } else if (threadIdx.x >= 64 && threadIdx.x < 64 + 2 * HW) {
     const int k = (int)threadIdx.x - 64;
-    const int d = 2 * (tx0 - 1) + k - g.pad_w;
+    const int d = 2 * sX0 + k - g.pad_w;
     RowTap e{-1, -1, 0.f};
     if (!g.empty && d >= 0 && d < (SRC == 0 ? g.w : p.S)) {
       const LinTap2 t = tap_of(d, g.sx, g.rw);
@@ -228,7 +225,7 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
   const bool ident = g.sy == 1.f && g.sx == 1.f;
   for (int i = threadIdx.x; i < NPIX; i += 256) {
     const int hy = i / HW, hx = i - (i / HW) * HW;
-    const int Y = ty0 - 1 + hy, X = tx0 - 1 + hx;
+    const int Y = sY0 + hy, X = sX0 + hx;
     float out[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) out[k] = 0.f;
@@ -257,6 +254,30 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
     tile[i * 2] = pack8(out);
     tile[i * 2 + 1] = pack8(out + 8);
   }
+
+}
+
+template <int SRC, int KS, int NF, int TH, int TW>
+__global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p) {
+  constexpr int HH = TH + KS - 1, HW = TW + KS - 1, NPIX = HH * HW;
+  constexpr int SLABS = (KS * KS * 16 + 31) / 32;
+  static_assert(TH * TW == 256, "one 256-pixel tile per workgroup (4 waves x 4 fragments)");
+  __shared__ __align__(16) uint4 tile[NPIX * 2];  // 32 B per s2d pixel
+  __shared__ __align__(16) uint32_t region[kSrcBudget / 4];
+
+  const int S2 = p.S >> 1;
+  const int tiles_x = (S2 + TW - 1) / TW, tiles_y = (S2 + TH - 1) / TH, ntiles = tiles_x * tiles_y;
+  const int id = blockIdx.x, xcd = id & 7, j = id >> 3;
+  const int item = (j / ntiles) * 8 + xcd;  // every tile of one item lands on one XCD
+  const int t = j - (j / ntiles) * ntiles;
+  const int n_live = live_batch(p.cap, SRC == 0 ? &p.ctrl->n_images : &p.ctrl->n_crops);
+  if (item >= n_live) return;
+  const int ty0 = (t / tiles_x) * TH, tx0 = (t % tiles_x) * TW;
+
+  const Src g = make_src<SRC>(p, item);
+  __shared__ RowTap rtab[2 * HH];
+  __shared__ RowTap ctab[2 * HW];
+  build_s2d_tile<SRC, HH, HW, kSrcBudget>(p, g, ty0 - 1, tx0 - 1, tile, region, rtab, ctab);
 
   // ---- weights of this lane's rows into registers (overlaps the barrier)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -310,6 +331,109 @@ __global__ __launch_bounds__(256) void stem_fused_kernel(const StemFusedParams p
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Detector front end in one kernel: letterbox -> stem (3x3 s1 over s2d, 16 ch, SiLU) -> second conv
+// (3x3 s2, 16 -> 32, SiLU).  The 320x320x16 stem output (105 MB at B = 32, written once and read
+// back ~2.3x by the next conv) never leaves LDS.  Per workgroup: a TH2 x TW2 tile of the second
+// conv's output needs a (2TH2+1) x (2TW2+1) stem-output tile, which needs a (2TH2+3) x (2TW2+3)
+// s2d tile: the s2d work per image equals the single-stage kernel's (665 vs 2 x 340 halo pixels
+// per 256 stem outputs), the stem MFMA work grows 1.1x for the halo.
+constexpr int kSrc2Budget = 12288;  // ~8.4 KB source bytes per tile at scale 1 (aliases the stem output)
+
+template <int TH2, int TW2>
+__global__ __launch_bounds__(256) void stem2_kernel(const StemFusedParams p) {
+  constexpr int SR = 2 * TH2 + 1, SC = 2 * TW2 + 1;  // stem-output tile
+  constexpr int HH = SR + 2, HW = SC + 2;            // s2d tile
+  constexpr int NS = SR * SC, NSF = (NS + 15) / 16;  // stem-output pixels / 16-pixel fragments
+  constexpr int SLABS = 5;                           // 9 taps x 16 channels in 32-deep slabs (both convs)
+  static_assert(TH2 * TW2 == 128, "8 second-conv fragments: 2 per wave");
+  // The staged source bytes are dead once the s2d tile is built, so they share LDS with the stem
+  // output: 40.5 KB per workgroup = 4 workgroups per CU (53 KB without the alias: 3).
+  constexpr int SCRATCH = NS * 2 > kSrc2Budget / 16 ? NS * 2 : kSrc2Budget / 16;  // uint4 units
+  __shared__ __align__(16) uint4 tile[HH * HW * 2];
+  __shared__ __align__(16) uint4 scratch[SCRATCH];
+  uint4* sout = scratch;                   // stem output, 32 B per pixel (after the s2d tile is built)
+  uint32_t* region = (uint32_t*)scratch;  // staged source bytes (while the s2d tile is built)
+  __shared__ RowTap rtab[2 * HH];
+  __shared__ RowTap ctab[2 * HW];
+
+  const int S2 = p.S >> 1, S4 = S2 >> 1;
+  const int tiles_x = S4 / TW2, ntiles = tiles_x * (S4 / TH2);
+  const int id = blockIdx.x, xcd = id & 7, j = id >> 3;
+  const int item = (j / ntiles) * 8 + xcd;  // every tile of one image lands on one XCD
+  const int t = j - (j / ntiles) * ntiles;
+  if (item >= live_batch(p.cap, &p.ctrl->n_images)) return;
+  const int oy0 = (t / tiles_x) * TH2, ox0 = (t % tiles_x) * TW2;
+  const int Y0 = 2 * oy0 - 1, X0 = 2 * ox0 - 1;  // stem-output tile origin (second conv: pad 1)
+
+  const Src g = make_src<0>(p, item);
+  build_s2d_tile<0, HH, HW, kSrc2Budget>(p, g, Y0 - 1, X0 - 1, tile, region, rtab, ctab);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = lane & 15, kq = lane >> 4;
+  const bf16* __restrict__ w = (const bf16*)p.w;
+  const bf16* __restrict__ w2 = (const bf16*)p.w2;
+  bf16x8 wf[SLABS], w2f[2][SLABS];
+#pragma unroll
+  for (int s = 0; s < SLABS; ++s) {
+    wf[s] = *(const bf16x8*)(w + (size_t)row * p.Kpad + s * 32 + kq * 8);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) w2f[a][s] = *(const bf16x8*)(w2 + (size_t)(a * 16 + row) * p.Kpad2 + s * 32 + kq * 8);
+  }
+  const float4 sb = *(const float4*)(p.bias + kq * 4);
+  __syncthreads();
+
+  // ---- stem conv over the s2d tile -> sout (zero outside the S/2 map: the second conv's padding)
+  for (int fr = wave; fr < NSF; fr += 4) {
+    const int P = fr * 16 + row;
+    const int Pc = P < NS ? P : NS - 1;  // padded rows read a valid pixel; their results are unused
+    const int sy = Pc / SC, sx = Pc - (Pc / SC) * SC;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < SLABS; ++s) {
+      int tap = 2 * s + (kq >> 1);
+      if (tap >= 9) tap = 0;  // zero weight rows
+      const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+      const bf16x8 bv = *(const bf16x8*)&tile[((sy + kh) * HW + sx + kw) * 2 + (kq & 1)];
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], bv, acc, 0, 0, 0);
+    }
+    const bool inside = (unsigned)(Y0 + sy) < (unsigned)S2 && (unsigned)(X0 + sx) < (unsigned)S2;
+    float v[4] = {apply_act(acc[0] + sb.x, p.act), apply_act(acc[1] + sb.y, p.act), apply_act(acc[2] + sb.z, p.act),
+                  apply_act(acc[3] + sb.w, p.act)};
+    if (!inside) v[0] = v[1] = v[2] = v[3] = 0.f;
+    if (P < NS) *(uint2*)((uint8_t*)sout + P * 32 + kq * 8) = pack4(v);
+  }
+  __syncthreads();
+
+  // ---- second conv (3x3 stride 2) over sout -> global
+  bf16* __restrict__ y2 = (bf16*)p.y2;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int Q = (wave * 2 + q) * 16 + row;
+    const int qy = Q / TW2, qx = Q - (Q / TW2) * TW2;
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < SLABS; ++s) {
+      int tap = 2 * s + (kq >> 1);
+      if (tap >= 9) tap = 0;
+      const int kh = tap / 3, kw = tap - (tap / 3) * 3;
+      const bf16x8 bv = *(const bf16x8*)&sout[((2 * qy + kh) * SC + 2 * qx + kw) * 2 + (kq & 1)];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[a][s], bv, acc[a], 0, 0, 0);
+    }
+    const size_t base = ((size_t)item * S4 * S4 + (size_t)(oy0 + qy) * S4 + ox0 + qx) * p.y2s;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int cb = a * 16 + kq * 4;
+      const float4 bias = *(const float4*)(p.bias2 + cb);
+      float v[4] = {acc[a][0] + bias.x, acc[a][1] + bias.y, acc[a][2] + bias.z, acc[a][3] + bias.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act2);
+      *(uint2*)(y2 + base + cb) = pack4(v);
+    }
+  }
+}
+
 template <int SRC, int KS, int NF, int TH, int TW>
 static void stem_launch(const StemFusedParams& p, hipStream_t s) {
   const int S2 = p.S / 2;
@@ -326,6 +450,14 @@ void stem_fused(const StemFusedParams& p, hipStream_t s) {
   if (p.src == 0) {  // YOLOv5nu: letterbox -> 6x6/s2 stem as 3x3/s1 over s2d, 16 channels, SiLU
     if (p.KS != 3 || p.Cout != 16 || p.Kpad != 160)
       throw std::runtime_error("stem_fused: detector stem must be 3x3 (s2d) x 16 -> 16, Kpad 160");
+    if (p.w2 != nullptr) {
+      if (p.Cout2 != 32 || p.Kpad2 != 160 || p.S % 64 != 0 || p.y2s % 4 != 0 || p.y2 == nullptr)
+        throw std::runtime_error("stem_fused: second conv must be 3x3 s2 16 -> 32 (Kpad 160) with S % 64 == 0");
+      const int S4 = p.S / 4;
+      const long blocks = (long)((p.cap + 7) / 8) * 8 * (S4 / 8) * (S4 / 16);
+      hipLaunchKernelGGL((stem2_kernel<8, 16>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+      return;
+    }
     stem_launch<0, 3, 1, 8, 32>(p, s);
   } else if (p.src == 1) {  // MobileNetV2: crop gather -> 3x3/s2 stem as 2x2/s1 over s2d, 32 channels, ReLU6
     if (p.KS != 2 || p.Cout != 32 || p.Kpad != 64 || p.crops == nullptr)

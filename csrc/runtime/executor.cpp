@@ -585,6 +585,16 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         }
         p.cap = batch(r[18]);
         p.KS = (int)r[19];
+        if (r[20]) {  // second conv fused: the destination is its output, the stem output stays in LDS
+          p.w2 = W + r[21];
+          p.Kpad2 = (int)r[22];
+          p.bias2 = (const float*)(W + r[23]);
+          p.Cout2 = (int)r[24];
+          p.act2 = (int)r[25];
+          p.y2 = p.y;
+          p.y2s = p.ys;
+          p.y = nullptr;
+        }
         p.pool = pool;
         p.meta = meta;
         p.ctrl = ctrl;

@@ -40,6 +40,7 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
            25 batch_kind   (fused MobileNetV2 inverted residual, csrc/kernels/ir_block.hip)
   STEMFUSED 1 src (0 letterbox, 1 crop gather) 2 y_buf 3 y_coff 4 y_cs 5 S 6 w_off 7 Kpad 8 b_off
            9 Cout 10 act 11 crops_buf 12-14 mean 15-17 inv_std (float bits) 18 batch_kind 19 KS
+           20 second-conv flag 21 w2_off 22 Kpad2 23 b2_off 24 Cout2 25 act2 (y = the second conv's output)
            (preprocessing fused into the stem conv; the s2d input exists only in LDS,
             csrc/kernels/stem_fused.hip)
   C3FUSED 1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 C1 7 CH 8 NB 9 res 10 w12 11 b12 12-15 (wb1, bb1, wb2, bb2) of
@@ -320,12 +321,15 @@ class ProgramBuilder:
         self._emit(rec, src, dst)
 
     def stem_fused(self, dst: View, w: torch.Tensor, b: torch.Tensor, *, S: int, act: str, crops: Buffer | None = None,
-                   mean=None, std=None, kind: int = IMAGES) -> None:
+                   mean=None, std=None, kind: int = IMAGES, second: tuple | None = None) -> None:
         """Letterbox (``crops=None``) or crop gather + normalisation, fused with the s2d stem conv
-        (``w``: [Cout, 16, KS, KS] over the space-to-depth input, pad top/left 1)."""
+        (``w``: [Cout, 16, KS, KS] over the space-to-depth input, pad top/left 1).
+
+        ``second=(w2, b2, act2)`` (detector only): the following 3x3 stride-2 conv runs in the same
+        kernel on the stem output kept in LDS; ``dst`` is then that conv's output (S/4 x S/4)."""
         cout, cin, ks, ks2 = w.shape
-        if cin != 16 or ks != ks2 or cout != dst.C:
-            raise ValueError("stem_fused: weights must be [Cout, 16, KS, KS] with Cout == dst.C")
+        if cin != 16 or ks != ks2:
+            raise ValueError("stem_fused: weights must be [Cout, 16, KS, KS]")
         wb, bb, kpad, cpad = pack_conv_weight(w, b)
         if cpad != cout:
             raise ValueError("stem_fused: Cout must be a multiple of 16")
@@ -334,9 +338,19 @@ class ProgramBuilder:
         src = 0 if crops is None else 1
         mean = mean if mean is not None else (0.0, 0.0, 0.0)
         std = std if std is not None else (1.0, 1.0, 1.0)
+        if second is not None:
+            w2, b2, act2 = second
+            co2, ci2, kh2, kw2 = w2.shape
+            if crops is not None or ci2 != cout or (kh2, kw2) != (3, 3) or co2 != dst.C:
+                raise ValueError("stem_fused: second conv must be 3x3 [C2, Cout, 3, 3] with C2 == dst.C")
+        elif cout != dst.C:
+            raise ValueError("stem_fused: Cout must match dst.C")
         rec = [OP_STEMFUSED, src, dst.bid, dst.coff, dst.cs, S, w_off, kpad, b_off, cout, ACT[act],
                crops.id if crops is not None else BUF_NONE] + [fbits(m) for m in mean] + \
               [fbits(1.0 / s) for s in std] + [kind, ks]
+        if second is not None:
+            wb2, bb2, kpad2, _ = pack_conv_weight(w2, b2)
+            rec += [1, self.weights.add(wb2), kpad2, self.weights.add(bb2), co2, ACT[act2]]
         self._emit(rec, dst, crops)
 
     def zero(self, buf: Buffer, kind: int = IMAGES) -> None:

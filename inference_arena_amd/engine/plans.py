@@ -109,6 +109,12 @@ def fuse_stem_default() -> bool:
     return os.environ.get("ARENA_FUSE_STEM", "1").lower() not in ("0", "false", "no", "off")
 
 
+def fuse_stem2_default() -> bool:
+    """``ARENA_FUSE_STEM2`` (default 1): with the fused stem, the detector's second conv (3x3 s2,
+    16 -> 32) runs in the same kernel; the 320x320x16 stem output is never stored."""
+    return os.environ.get("ARENA_FUSE_STEM2", "1").lower() not in ("0", "false", "no", "off")
+
+
 def fuse_head_pool_default() -> bool:
     """``ARENA_FUSE_POOL`` (default 1): MobileNetV2's last 1x1 conv and the global average pool run as one
     kernel (head_pool op); the 7x7x1280 map is never stored."""
@@ -118,21 +124,27 @@ def fuse_head_pool_default() -> bool:
 def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool = False,
               fuse_stem: bool | None = None):
     h = T // 2
-    A0 = pb.tensor("b0", h, h, 16)
     w, b = fold(y.b0)
     if fuse_stem is None:
         fuse_stem = fuse_stem_default()
-    if fuse_stem and not tensor_input:
+    A1 = pb.tensor("b1", h // 2, h // 2, 32)
+    if fuse_stem and not tensor_input and fuse_stem2_default() and T % 64 == 0:
+        # letterbox + stem + b1 (3x3 s2) in one kernel: the 320x320x16 stem output stays in LDS
+        w1, b1 = fold(y.b1)
+        pb.stem_fused(View(A1, 0, 32), s2d_stem_6x6(w), b, S=T, act="silu", second=(w1, b1, "silu"))
+    elif fuse_stem and not tensor_input:
+        A0 = pb.tensor("b0", h, h, 16)
         pb.stem_fused(View(A0, 0, 16), s2d_stem_6x6(w), b, S=T, act="silu")
+        pb.conv(View(A0, 0, 16), View(A1, 0, 32), *fold(y.b1), stride=2)
     else:
+        A0 = pb.tensor("b0", h, h, 16)
         X0 = pb.tensor("x_s2d", h, h, 16)
         if tensor_input:
             pb.tensor_in(X0, T)
         else:
             pb.letterbox(X0, T)
         pb.conv(View(X0, 0, 16), View(A0, 0, 16), s2d_stem_6x6(w), b)
-    A1 = pb.tensor("b1", h // 2, h // 2, 32)
-    pb.conv(View(A0, 0, 16), View(A1, 0, 32), *fold(y.b1), stride=2)
+        pb.conv(View(A0, 0, 16), View(A1, 0, 32), *fold(y.b1), stride=2)
     A2 = pb.tensor("b2", h // 2, h // 2, 32)
     _c3(pb, y.b2, View(A1, 0, 32), View(A2, 0, 32), h // 2, h // 2, "b2")
     s8 = T // 8

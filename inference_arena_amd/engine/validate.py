@@ -159,7 +159,14 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             expect = {0: (3, 16, 160, 0), 1: (2, 32, 64, CROPS)}.get(src)
             if expect is None or (ks, cout, kpad, kind) != expect or S % 2:
                 raise ProgramError(f"op {i}: bad stem_fused geometry (src {src}, KS {ks}, Cout {cout}, Kpad {kpad})")
-            view(i, r[2], int(r[3]), int(r[4]), n * (S // 2) ** 2, cout, 2, "stem output")
+            if int(r[20]):  # second conv fused: 3x3 s2 16 -> 32, output S/4
+                if src != 0 or int(r[24]) != 32 or int(r[22]) != 160 or S % 64:
+                    raise ProgramError(f"op {i}: bad fused second conv (Cout2 {int(r[24])}, Kpad2 {int(r[22])})")
+                view(i, r[2], int(r[3]), int(r[4]), n * (S // 4) ** 2, 32, 2, "stem second-conv output")
+                weights(i, int(r[21]), 32 * 160 * 2, "stem second-conv weight")
+                weights(i, int(r[23]), 32 * 4, "stem second-conv bias")
+            else:
+                view(i, r[2], int(r[3]), int(r[4]), n * (S // 2) ** 2, cout, 2, "stem output")
             if src == 1:
                 need(i, r[11], 0, B * max_det * CROP_BYTES, "crop refs")
             weights(i, int(r[6]), cout * kpad * 2, "stem weight")

@@ -114,6 +114,8 @@ def test_program_shape(program):
     # the two stem convs become stem_fused ops (preprocessing fused in) unless ARENA_FUSE_STEM=0
     assert stems in (0, 2)
     convs += stems
+    # the detector stem op may also carry the following 3x3 s2 conv (ARENA_FUSE_STEM2)
+    convs += int(((program.ops[:, 0] == OP_STEMFUSED) & (program.ops[:, 20] > 0)).sum())
     # the Detect head's final 1x1 convs ride in the epilogue of the preceding 3x3s unless ARENA_FUSE_HEAD=0
     pw = int(((program.ops[:, 0] == OP_CONV) & (program.ops[:, 34] > 0)).sum())
     assert pw in (0, 6)

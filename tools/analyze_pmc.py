@@ -29,7 +29,8 @@ def replays(path: Path, n_ops: int, keep: int):
         by_dispatch[d][r["Counter_Name"]] = float(r["Counter_Value"])
         names[d] = r["Kernel_Name"]
     order = sorted(by_dispatch)
-    starts = [i for i, d in enumerate(order) if "letterbox" in names[d] or "stem_fused_kernel<0" in names[d]]
+    starts = [i for i, d in enumerate(order) if "letterbox" in names[d] or "stem_fused_kernel<0" in names[d]
+              or "stem2_kernel" in names[d]]
     out = []
     for s in starts:
         seq = order[s:s + n_ops]

@@ -37,7 +37,8 @@ def describe(rec) -> str:
         return (f"c3 {int(rec[4])}x{int(rec[5])}x{int(rec[6])} c_={int(rec[7])} n={int(rec[8])}"
                 f"{' res' if rec[9] else ''}")
     if t == 15:
-        return f"{'letterbox' if rec[1] == 0 else 'crop gather'} + stem k{int(rec[19])} -> {int(rec[9])}"
+        d = f"{'letterbox' if rec[1] == 0 else 'crop gather'} + stem k{int(rec[19])} -> {int(rec[9])}"
+        return d + (f" + k3 s2 -> {int(rec[24])}" if int(rec[20]) else "")
     if t == 14:
         return (f"ir {int(rec[4])}x{int(rec[5])}x{int(rec[6])}->{int(rec[23])}x{int(rec[24])}x{int(rec[9])} "
                 f"hid{int(rec[8])} s{int(rec[11])}{' res' if rec[13] else ''}")
@@ -64,7 +65,10 @@ def main(argv=None) -> int:
     by_q = defaultdict(list)
     for r in rows:
         by_q[r[qkey] if qkey else 0].append(r)
-    first = FIRST_KERNEL.get(int(prog.ops[0][0]), "letterbox")
+    op0 = prog.ops[0]
+    first = FIRST_KERNEL.get(int(op0[0]), "letterbox")
+    if int(op0[0]) == 15:  # detector stem: single-stage kernel or letterbox+stem+conv (stem2_kernel)
+        first = "stem2_kernel" if int(op0[20]) else "stem_fused_kernel<0"
     replays = []
     for q in by_q.values():
         q.sort(key=lambda r: int(r["Start_Timestamp"]))
