@@ -291,6 +291,15 @@ struct StemFusedParams {
   int Cout2, act2;
   void* y2;
   int y2s;
+  // Optional first inverted residual (classifier only; t = 1: depthwise 3x3 + ReLU6 on the 32-channel stem
+  // output, then project 32 -> 16, no residual) on the stem output kept in LDS; ir_y = bf16 [cap, S/2, S/2, ir_ys].
+  // Layouts as ir_block: wd [9][32] bf16, bd [32] fp32, wp [16][32] bf16, bp [16] fp32.
+  const void* ir_wd;
+  const float* ir_bd;
+  const void* ir_wp;
+  const float* ir_bp;
+  void* ir_y;
+  int ir_ys;
 };
 void stem_fused(const StemFusedParams& p, hipStream_t s);
 

@@ -434,6 +434,154 @@ __global__ __launch_bounds__(256) void stem2_kernel(const StemFusedParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Classifier front end in one kernel: crop gather (resize 224, ImageNet normalisation) -> stem
+// (2x2 over s2d, 32 ch, ReLU6) -> MobileNetV2 block 1 (t = 1: depthwise 3x3 + ReLU6, project
+// 32 -> 16).  The 112x112x32 stem output (101 MB for 126 crops, written once and read once) only
+// exists in LDS.  Per workgroup: a T x T tile of block 1's output needs a (T+2)^2 stem-output tile,
+// which needs a (T+3)^2 s2d tile.
+constexpr int kSrcIrBudget = 8192;
+
+__device__ __forceinline__ int ir_swz(int row, int chunk) {
+  return row * 64 + ((chunk ^ ((0x78 >> (((row >> 2) & 3) * 2)) & 3)) << 4);
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void stem_ir_kernel(const StemFusedParams p) {
+  constexpr int FT = T + 2, HT = FT + 1;                  // stem-output tile, s2d tile
+  constexpr int NFP = FT * FT, NFF = (NFP + 15) / 16;     // stem-output pixels / fragments
+  constexpr int NOUT = T * T;
+  static_assert(NOUT % 64 == 0 && 2 * HT <= 64, "tile geometry");
+  // LDS A: s2d tile, later the depthwise output D; LDS B: staged source bytes, later the stem output F.
+  constexpr int A_BYTES = HT * HT * 32 > NOUT * 64 ? HT * HT * 32 : NOUT * 64;
+  constexpr int B_BYTES = NFP * 64 > kSrcIrBudget ? NFP * 64 : kSrcIrBudget;
+  __shared__ __align__(16) uint8_t lA[A_BYTES];
+  __shared__ __align__(16) uint8_t lB[B_BYTES];
+  __shared__ RowTap rtab[2 * HT];
+  __shared__ RowTap ctab[2 * HT];
+  uint4* tile = (uint4*)lA;
+  uint8_t* Ds = lA;
+  uint32_t* region = (uint32_t*)lB;
+  uint8_t* Fs = lB;
+
+  const int S2 = p.S >> 1;
+  const int tiles_x = S2 / T, ntiles = tiles_x * tiles_x;
+  const int id = blockIdx.x, xcd = id & 7, j = id >> 3;
+  const int item = (j / ntiles) * 8 + xcd;  // every tile of one crop lands on one XCD
+  const int t = j - (j / ntiles) * ntiles;
+  if (item >= live_batch(p.cap, &p.ctrl->n_crops)) return;
+  const int oy0 = (t / tiles_x) * T, ox0 = (t % tiles_x) * T;
+  const int Y0 = oy0 - 1, X0 = ox0 - 1;  // stem-output tile origin (depthwise pad 1)
+
+  const Src g = make_src<1>(p, item);
+  build_s2d_tile<1, HT, HT, kSrcIrBudget>(p, g, Y0 - 1, X0 - 1, tile, region, rtab, ctab);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = lane & 15, kq = lane >> 4;
+  const bf16* __restrict__ w = (const bf16*)p.w;
+  bf16x8 wf[2][2];  // [N-fragment][slab]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) wf[a][s] = *(const bf16x8*)(w + (size_t)(a * 16 + row) * p.Kpad + s * 32 + kq * 8);
+  const float4 sb0 = *(const float4*)(p.bias + kq * 4), sb1 = *(const float4*)(p.bias + 16 + kq * 4);
+  // depthwise taps of this thread's 8-channel group (items tid + 256 k keep tid & 3), as bf16 tap pairs
+  const int dc = tid & 3;
+  const bf16* wd = (const bf16*)p.ir_wd;
+  unsigned wpair[4][8];
+  float w8[8], bd[8];
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) {
+    const uint4 a = *(const uint4*)(wd + (2 * pp) * 32 + dc * 8);
+    const uint4 c2 = *(const uint4*)(wd + (2 * pp + 1) * 32 + dc * 8);
+    const unsigned av[4] = {a.x, a.y, a.z, a.w}, cv[4] = {c2.x, c2.y, c2.z, c2.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      wpair[pp][2 * q] = __builtin_amdgcn_perm(cv[q], av[q], 0x05040100u);
+      wpair[pp][2 * q + 1] = __builtin_amdgcn_perm(cv[q], av[q], 0x07060302u);
+    }
+  }
+  unpack8(*(const uint4*)(wd + 8 * 32 + dc * 8), w8);
+  {
+    const float4 b0 = *(const float4*)(p.ir_bd + dc * 8), b1 = *(const float4*)(p.ir_bd + dc * 8 + 4);
+    bd[0] = b0.x; bd[1] = b0.y; bd[2] = b0.z; bd[3] = b0.w;
+    bd[4] = b1.x; bd[5] = b1.y; bd[6] = b1.z; bd[7] = b1.w;
+  }
+  const bf16x8 wpa = *(const bf16x8*)((const bf16*)p.ir_wp + row * 32 + kq * 8);
+  __syncthreads();
+
+  // ---- stem conv (2x2 over s2d, 32 channels, ReLU6) -> F (zero outside the S/2 map: depthwise padding)
+  for (int fr = wave; fr < NFF; fr += 4) {
+    const int P = fr * 16 + row;
+    const int Pc = P < NFP ? P : NFP - 1;
+    const int sy = Pc / FT, sx = Pc - (Pc / FT) * FT;
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int tap = 2 * s + (kq >> 1), kh = tap >> 1, kw = tap & 1;
+      const bf16x8 bv = *(const bf16x8*)&tile[((sy + kh) * HT + sx + kw) * 2 + (kq & 1)];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) acc[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a][s], bv, acc[a], 0, 0, 0);
+    }
+    const bool inside = (unsigned)(Y0 + sy) < (unsigned)S2 && (unsigned)(X0 + sx) < (unsigned)S2;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const float4 bb = a ? sb1 : sb0;
+      float v[4] = {apply_act(acc[a][0] + bb.x, p.act), apply_act(acc[a][1] + bb.y, p.act),
+                    apply_act(acc[a][2] + bb.z, p.act), apply_act(acc[a][3] + bb.w, p.act)};
+      if (!inside) v[0] = v[1] = v[2] = v[3] = 0.f;
+      if (P < NFP) *(uint2*)(Fs + P * 64 + (a * 16 + kq * 4) * 2) = pack4(v);
+    }
+  }
+  __syncthreads();
+
+  // ---- depthwise 3x3 + ReLU6 -> D (swizzled rows for the project MFMA)
+#pragma unroll
+  for (int k = 0; k < NOUT * 4 / 256; ++k) {
+    const int q = (tid + 256 * k) >> 2;
+    const int oy = q / T, ox = q - (q / T) * T;
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = bd[i];
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) {
+      const int t0 = 2 * pp, t1 = 2 * pp + 1;
+      const uint4 e0 = *(const uint4*)(Fs + ((oy + t0 / 3) * FT + ox + t0 % 3) * 64 + dc * 16);
+      const uint4 e1 = *(const uint4*)(Fs + ((oy + t1 / 3) * FT + ox + t1 % 3) * 64 + dc * 16);
+      const unsigned x0[4] = {e0.x, e0.y, e0.z, e0.w}, x1[4] = {e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const unsigned lo = __builtin_amdgcn_perm(x1[jj], x0[jj], 0x05040100u);
+        const unsigned hi = __builtin_amdgcn_perm(x1[jj], x0[jj], 0x07060302u);
+        acc[2 * jj] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, lo),
+                                                      __builtin_bit_cast(bf16x2, wpair[pp][2 * jj]), acc[2 * jj], false);
+        acc[2 * jj + 1] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, hi),
+                                                          __builtin_bit_cast(bf16x2, wpair[pp][2 * jj + 1]),
+                                                          acc[2 * jj + 1], false);
+      }
+    }
+    float e8[8];
+    unpack8(*(const uint4*)(Fs + ((oy + 2) * FT + ox + 2) * 64 + dc * 16), e8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = relu6f(fmaf(e8[i], w8[i], acc[i]));
+    *(uint4*)(Ds + ir_swz(q, dc)) = pack8(acc);
+  }
+  __syncthreads();
+
+  // ---- project 32 -> 16 (+ bias, no activation) -> global
+  bf16* __restrict__ y = (bf16*)p.ir_y;
+  const float4 pb = *(const float4*)(p.ir_bp + kq * 4);
+#pragma unroll
+  for (int f = 0; f < NOUT / 64; ++f) {
+    const int fr = wave * (NOUT / 64) + f;
+    const bf16x8 bv = *(const bf16x8*)(Ds + ir_swz(fr * 16 + row, kq));
+    f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wpa, bv, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    const int q = fr * 16 + row, oy = q / T, ox = q - (q / T) * T;
+    float v[4] = {acc[0] + pb.x, acc[1] + pb.y, acc[2] + pb.z, acc[3] + pb.w};
+    *(uint2*)(y + ((size_t)item * S2 * S2 + (size_t)(oy0 + oy) * S2 + ox0 + ox) * p.ir_ys + kq * 4) = pack4(v);
+  }
+}
+
 template <int SRC, int KS, int NF, int TH, int TW>
 static void stem_launch(const StemFusedParams& p, hipStream_t s) {
   const int S2 = p.S / 2;
@@ -462,6 +610,15 @@ void stem_fused(const StemFusedParams& p, hipStream_t s) {
   } else if (p.src == 1) {  // MobileNetV2: crop gather -> 3x3/s2 stem as 2x2/s1 over s2d, 32 channels, ReLU6
     if (p.KS != 2 || p.Cout != 32 || p.Kpad != 64 || p.crops == nullptr)
       throw std::runtime_error("stem_fused: classifier stem must be 2x2 (s2d) x 16 -> 32, Kpad 64");
+    if (p.ir_wd != nullptr) {
+      if (p.S % 32 != 0 || p.ir_ys % 4 != 0 || p.ir_y == nullptr || p.ir_bd == nullptr || p.ir_wp == nullptr ||
+          p.ir_bp == nullptr)
+        throw std::runtime_error("stem_fused: fused first block needs S % 32 == 0 and its weights / output");
+      const int S2 = p.S / 2;
+      const long blocks = (long)((p.cap + 7) / 8) * 8 * (S2 / 16) * (S2 / 16);
+      hipLaunchKernelGGL((stem_ir_kernel<16>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+      return;
+    }
     stem_launch<1, 2, 2, 16, 16>(p, s);
   } else {
     throw std::runtime_error("stem_fused: unknown source");

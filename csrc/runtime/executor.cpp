@@ -595,6 +595,15 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
           p.y2s = p.ys;
           p.y = nullptr;
         }
+        if (r[26]) {  // first inverted residual fused: the destination is its output
+          p.ir_wd = W + r[27];
+          p.ir_bd = (const float*)(W + r[28]);
+          p.ir_wp = W + r[29];
+          p.ir_bp = (const float*)(W + r[30]);
+          p.ir_y = p.y;
+          p.ir_ys = p.ys;
+          p.y = nullptr;
+        }
         p.pool = pool;
         p.meta = meta;
         p.ctrl = ctrl;

@@ -41,6 +41,7 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   STEMFUSED 1 src (0 letterbox, 1 crop gather) 2 y_buf 3 y_coff 4 y_cs 5 S 6 w_off 7 Kpad 8 b_off
            9 Cout 10 act 11 crops_buf 12-14 mean 15-17 inv_std (float bits) 18 batch_kind 19 KS
            20 second-conv flag 21 w2_off 22 Kpad2 23 b2_off 24 Cout2 25 act2 (y = the second conv's output)
+           26 first-IR-block flag 27 wd_off 28 bd_off 29 wp_off 30 bp_off 31 oup (y = the block's output)
            (preprocessing fused into the stem conv; the s2d input exists only in LDS,
             csrc/kernels/stem_fused.hip)
   C3FUSED 1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 C1 7 CH 8 NB 9 res 10 w12 11 b12 12-15 (wb1, bb1, wb2, bb2) of
@@ -321,12 +322,15 @@ class ProgramBuilder:
         self._emit(rec, src, dst)
 
     def stem_fused(self, dst: View, w: torch.Tensor, b: torch.Tensor, *, S: int, act: str, crops: Buffer | None = None,
-                   mean=None, std=None, kind: int = IMAGES, second: tuple | None = None) -> None:
+                   mean=None, std=None, kind: int = IMAGES, second: tuple | None = None,
+                   ir: tuple | None = None) -> None:
         """Letterbox (``crops=None``) or crop gather + normalisation, fused with the s2d stem conv
         (``w``: [Cout, 16, KS, KS] over the space-to-depth input, pad top/left 1).
 
         ``second=(w2, b2, act2)`` (detector only): the following 3x3 stride-2 conv runs in the same
-        kernel on the stem output kept in LDS; ``dst`` is then that conv's output (S/4 x S/4)."""
+        kernel on the stem output kept in LDS; ``dst`` is then that conv's output (S/4 x S/4).
+        ``ir=(dw, project)`` (classifier only): MobileNetV2 block 1 (t = 1, 32 -> 16, stride 1, no
+        residual) runs on the stem output in LDS; ``dst`` is then the block's output (S/2 x S/2 x 16)."""
         cout, cin, ks, ks2 = w.shape
         if cin != 16 or ks != ks2:
             raise ValueError("stem_fused: weights must be [Cout, 16, KS, KS]")
@@ -343,6 +347,11 @@ class ProgramBuilder:
             co2, ci2, kh2, kw2 = w2.shape
             if crops is not None or ci2 != cout or (kh2, kw2) != (3, 3) or co2 != dst.C:
                 raise ValueError("stem_fused: second conv must be 3x3 [C2, Cout, 3, 3] with C2 == dst.C")
+        elif ir is not None:
+            (wd, _), (wp, _) = ir
+            if crops is None or wd.shape != (cout, 1, 3, 3) or wp.shape[1:] != (cout, 1, 1) or wp.shape[0] != dst.C \
+                    or cout != 32 or dst.C != 16:
+                raise ValueError("stem_fused: fused block must be depthwise [32,1,3,3] + project [16,32,1,1]")
         elif cout != dst.C:
             raise ValueError("stem_fused: Cout must match dst.C")
         rec = [OP_STEMFUSED, src, dst.bid, dst.coff, dst.cs, S, w_off, kpad, b_off, cout, ACT[act],
@@ -351,6 +360,13 @@ class ProgramBuilder:
         if second is not None:
             wb2, bb2, kpad2, _ = pack_conv_weight(w2, b2)
             rec += [1, self.weights.add(wb2), kpad2, self.weights.add(bb2), co2, ACT[act2]]
+        else:
+            rec += [0] * 6
+        if ir is not None:
+            pk = pack_ir_weights(None, ir[0], ir[1], cout)
+            f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
+            rec += [1, self.weights.add(bf16_bytes(pk["wd"])), self.weights.add(f32(pk["bd"])),
+                    self.weights.add(bf16_bytes(pk["wp"])), self.weights.add(f32(pk["bp"])), pk["oup"]]
         self._emit(rec, dst, crops)
 
     def zero(self, buf: Buffer, kind: int = IMAGES) -> None:

@@ -115,6 +115,12 @@ def fuse_stem2_default() -> bool:
     return os.environ.get("ARENA_FUSE_STEM2", "1").lower() not in ("0", "false", "no", "off")
 
 
+def fuse_stem_ir_default() -> bool:
+    """``ARENA_FUSE_STEM_IR`` (default 1): with the fused stem, MobileNetV2's first inverted residual
+    (t = 1) runs in the same kernel; the 112x112x32 stem output is never stored."""
+    return os.environ.get("ARENA_FUSE_STEM_IR", "1").lower() not in ("0", "false", "no", "off")
+
+
 def fuse_head_pool_default() -> bool:
     """``ARENA_FUSE_POOL`` (default 1): MobileNetV2's last 1x1 conv and the global average pool run as one
     kernel (head_pool op); the 7x7x1280 map is never stored."""
@@ -242,11 +248,22 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
     if fuse_stem is None:
         fuse_stem = fuse_stem_default()
     w, b = fold(m.stem)
-    F = pb.tensor("m.stem", h, h, 32, kind=CROPS_)
-    if fuse_stem and crops is not None:
+    b0 = m.blocks[0]
+    first_fused = (fuse_stem and crops is not None and fuse_stem_ir_default() and S % 32 == 0
+                   and b0.expand is None and b0.stride == 1 and not b0.use_res and b0.inp == 32 and b0.oup == 16
+                   and fuse_block(b0, h, fuse_ir))
+    if first_fused:
+        # crop gather + stem + block 1 in one kernel: the 112x112x32 stem output stays in LDS
+        O0 = pb.tensor("m0.out", h, h, b0.oup, kind=CROPS_)
+        pb.stem_fused(View(O0, 0, b0.oup), s2d_stem_3x3(w), b, S=S, act="relu6", crops=crops, mean=mean, std=std,
+                      kind=CROPS_, ir=(fold(b0.dw), fold(b0.project)))
+        F = O0
+    elif fuse_stem and crops is not None:
+        F = pb.tensor("m.stem", h, h, 32, kind=CROPS_)
         pb.stem_fused(View(F, 0, 32), s2d_stem_3x3(w), b, S=S, act="relu6", crops=crops, mean=mean, std=std,
                       kind=CROPS_)
     else:
+        F = pb.tensor("m.stem", h, h, 32, kind=CROPS_)
         X = pb.tensor("crop_s2d", h, h, 16, kind=CROPS_)
         if crops is None:
             pb.tensor_in(X, S)
@@ -256,6 +273,8 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
                 out_hw=(h, h))
     cur, H = F, h
     for i, blk in enumerate(m.blocks):
+        if i == 0 and first_fused:
+            continue
         Ho = (H + 2 - 3) // blk.stride + 1
         if fuse_block(blk, H, fuse_ir):
             O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup, kind=CROPS_)

@@ -165,6 +165,13 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 view(i, r[2], int(r[3]), int(r[4]), n * (S // 4) ** 2, 32, 2, "stem second-conv output")
                 weights(i, int(r[21]), 32 * 160 * 2, "stem second-conv weight")
                 weights(i, int(r[23]), 32 * 4, "stem second-conv bias")
+            elif int(r[26]):  # first inverted residual fused: 32 -> 16 at S/2
+                if src != 1 or int(r[31]) != 16 or S % 32:
+                    raise ProgramError(f"op {i}: bad fused first block (oup {int(r[31])}, S {S})")
+                view(i, r[2], int(r[3]), int(r[4]), n * (S // 2) ** 2, 16, 2, "stem first-block output")
+                for off, nb, what in ((r[27], 9 * 32 * 2, "dw weight"), (r[28], 32 * 4, "dw bias"),
+                                      (r[29], 16 * 32 * 2, "project weight"), (r[30], 16 * 4, "project bias")):
+                    weights(i, int(off), nb, f"stem first-block {what}")
             else:
                 view(i, r[2], int(r[3]), int(r[4]), n * (S // 2) ** 2, cout, 2, "stem output")
             if src == 1:

@@ -116,6 +116,8 @@ def test_program_shape(program):
     convs += stems
     # the detector stem op may also carry the following 3x3 s2 conv (ARENA_FUSE_STEM2)
     convs += int(((program.ops[:, 0] == OP_STEMFUSED) & (program.ops[:, 20] > 0)).sum())
+    # ... or MobileNetV2's first inverted residual (ARENA_FUSE_STEM_IR)
+    irs += int(((program.ops[:, 0] == OP_STEMFUSED) & (program.ops[:, 26] > 0)).sum())
     # the Detect head's final 1x1 convs ride in the epilogue of the preceding 3x3s unless ARENA_FUSE_HEAD=0
     pw = int(((program.ops[:, 0] == OP_CONV) & (program.ops[:, 34] > 0)).sum())
     assert pw in (0, 6)

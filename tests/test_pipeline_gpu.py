@@ -138,6 +138,31 @@ def test_two_stage_stem_matches_single_stage(dense_models, device, monkeypatch):
         assert len(x) == len(y)
 
 
+def test_stem_first_block_matches_unfused(dense_models, device, monkeypatch):
+    """crop gather + stem + MobileNetV2 block 1 in one kernel (stem output in LDS) vs the fused stem
+    followed by the ir_block kernel: same block-1 activations and classifications."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    imgs = synthetic_images(4, 71) + synthetic_images(1, 72, hw=(333, 500))
+    monkeypatch.setenv("ARENA_FUSE_STEM_IR", "0")
+    one = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)
+    monkeypatch.setenv("ARENA_FUSE_STEM_IR", "1")
+    two = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)
+    assert any(int(op[0]) == 15 and int(op[26]) for op in two.program.ops)
+    assert not any(int(op[0]) == 15 and int(op[26]) for op in one.program.ops)
+    a, b = one.infer(imgs), two.infer(imgs)
+    n = sum(len(r) for r in a)
+    assert n > 0
+    for c in range(min(n, 12)):
+        x1, x2 = one.read_buffer("m0.out", 8, c), two.read_buffer("m0.out", 8, c)
+        np.testing.assert_allclose(x2, x1, atol=0.03 + 0.01 * np.abs(x1).max())
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        if len(x):
+            assert (x.topk_idx[:, 0] == y.topk_idx[:, 0]).mean() >= 0.9
+
+
 def test_fused_head_pool_matches_unfused(dense_models, device, monkeypatch):
     """MobileNetV2 head conv + global average pool as one kernel (head_pool) vs conv + avgpool: same pooled
     features (fp32 sum before one bf16 rounding vs per-pixel bf16) and the same classifications."""

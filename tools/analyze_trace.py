@@ -38,7 +38,8 @@ def describe(rec) -> str:
                 f"{' res' if rec[9] else ''}")
     if t == 15:
         d = f"{'letterbox' if rec[1] == 0 else 'crop gather'} + stem k{int(rec[19])} -> {int(rec[9])}"
-        return d + (f" + k3 s2 -> {int(rec[24])}" if int(rec[20]) else "")
+        return d + (f" + k3 s2 -> {int(rec[24])}" if int(rec[20]) else "") + \
+            (f" + ir t1 -> {int(rec[31])}" if int(rec[26]) else "")
     if t == 14:
         return (f"ir {int(rec[4])}x{int(rec[5])}x{int(rec[6])}->{int(rec[23])}x{int(rec[24])}x{int(rec[9])} "
                 f"hid{int(rec[8])} s{int(rec[11])}{' res' if rec[13] else ''}")
