@@ -364,7 +364,9 @@ static void ir_set_attr() {
   X(1, 7, 7, 6, true)                                                \
   X(2, 7, 7, 10, true)                                               \
   X(1, 7, 7, 10, true)                                               \
-  X(1, 7, 7, 20, true)
+  X(1, 7, 7, 20, true)                                               \
+  X(1, 14, 14, 4, true)                                              \
+  X(1, 14, 14, 6, true)
 
 void ir_wave_prepare();
 bool ir_block_wave(const IrParams& p, int tile, hipStream_t s);
@@ -387,7 +389,17 @@ static const bool g_ir_t16 = [] {
   const char* e = std::getenv("ARENA_IR_T16");
   return e ? std::atoi(e) != 0 : true;
 }();
-int ir_tile(int Ho) { return (g_ir_t16 && Ho >= 112 && Ho % 16 == 0) ? 16 : (Ho % 8 == 0 && Ho >= 56) ? 8 : 7; }
+// Whole-crop 14x14 tiles for the stride-1 14x14 blocks (ARENA_IR_T14=1): one workgroup per crop, 16
+// output N-tiles per hidden chunk instead of 4, and no 9x9-for-7x7 halo recompute of the expansion.
+static bool g_ir_t14 = [] {
+  const char* e = std::getenv("ARENA_IR_T14");
+  return e ? std::atoi(e) != 0 : false;
+}();
+void set_ir_t14(bool v) { g_ir_t14 = v; }
+int ir_tile(int Ho, int stride) {
+  if (g_ir_t14 && Ho == 14 && stride == 1) return 14;
+  return (g_ir_t16 && Ho >= 112 && Ho % 16 == 0) ? 16 : (Ho % 8 == 0 && Ho >= 56) ? 8 : 7;
+}
 
 void ir_block(const IrParams& p, hipStream_t s) {
   if (p.inp_pad % 32 || p.hid_pad % 32 || p.oup_pad % 16 || p.inp % 8 || p.oup % 4 || p.oup > p.oup_pad ||
@@ -398,7 +410,7 @@ void ir_block(const IrParams& p, hipStream_t s) {
   if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_block: residual needs s1, inp == oup");
   if (p.Ho != (p.H + 2 - 3) / p.stride + 1 || p.Wo != (p.W + 2 - 3) / p.stride + 1)
     throw std::runtime_error("ir_block: output size mismatch");
-  const int T = ir_tile(p.Ho);
+  const int T = ir_tile(p.Ho, p.stride);
   if (g_ir_wave && ir_block_wave(p, T, s)) return;
   const int MP = p.oup_pad / 16;
   const bool E = p.expand != 0;

@@ -91,6 +91,7 @@ struct IrParams {
 };
 void ir_block(const IrParams& p, hipStream_t s);
 void ir_prepare();
+void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole-crop tile
 void set_ir_wave(bool v);  // ARENA_IR_WAVE=0: stride-1 blocks use the block-cooperative kernel
 
 // ---------------------------------------------------------------- fused C3 block (K2/K3/K4 at 160x160 / 80x80)

@@ -223,14 +223,16 @@ def fuse_ir_default() -> str:
 
 
 def fuse_block(blk, H: int, policy) -> bool:
-    """``auto``: fuse where the tile kernel wins on MI355X — blocks at >= 28x28 input, and the 14x14
-    blocks with <= 384 hidden / <= 64 output channels.  Deeper blocks have too few output tiles per
-    crop (1-4 workgroups) and run faster as batched 1x1 GEMMs + depthwise over all crops."""
+    """``auto``: fuse where the tile kernel wins on MI355X — blocks at >= 28x28 input and the stride-1
+    14x14 blocks (hid 576: 46 us fused vs 28 + 18 + 17 us as expand / depthwise / project ops;
+    profiles/r1_irpolicy14_ops.md).  The 14 -> 7 stride-2 block and the 7x7 blocks have one
+    output tile per crop and a 18-30 chunk serial loop: they run faster as batched 1x1 GEMMs +
+    depthwise over all crops (59 vs 52 us, 80 vs 50 us)."""
     if policy in (True, "all"):
         return True
     if policy in (False, None, "none"):
         return False
-    return H >= 28 or (H >= 14 and blk.hidden <= 384 and blk.oup <= 64)
+    return H >= 28 or (H >= 14 and blk.stride == 1)
 
 
 def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std, *, kind: int = CROPS,

@@ -416,3 +416,24 @@ def test_ir_wave_matches_block_kernel(device, H, inp, hid, oup, res, s):
     finally:
         C.set_ir_wave(True)
     assert (yw.float() - yb.float()).abs().max().item() <= 0.07
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,inp,hid,oup,res", [(3, 64, 384, 64, True), (2, 64, 384, 96, False),
+                                                 (3, 96, 576, 96, True)])
+def test_ir_block_whole_crop_14(device, B, inp, hid, oup, res):
+    """Stride-1 14x14 blocks as one whole-crop tile per workgroup (ARENA_IR_T14) == torch fp32 reference."""
+    C = native()
+    g = torch.Generator().manual_seed(hid + oup)
+    x = (torch.rand(B, inp, 14, 14, generator=g) * 2).to(torch.bfloat16)
+    expand = (torch.randn(hid, inp, 1, 1, generator=g) / np.sqrt(inp), torch.randn(hid, generator=g) * 0.1)
+    dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
+    project = (torch.randn(oup, hid, 1, 1, generator=g) / np.sqrt(hid), torch.randn(oup, generator=g) * 0.1)
+    xn = _nhwc(x).to(device)
+    C.set_ir_t14(True)
+    try:
+        y = AF.ir_block_nhwc(xn, expand, dw, project, stride=1, res=res)
+    finally:
+        C.set_ir_t14(False)
+    ref = _ref_ir(xn.cpu(), expand, dw, project, 1, res)
+    _check(_nchw(y.cpu()), ref, rtol=3e-2, atol=3e-2)

@@ -134,8 +134,8 @@ def test_program_shape(program):
     hp = int((program.ops[:, 0] == OP_HEADPOOL).sum())
     assert hp + int((program.ops[:, 0] == OP_AVGPOOL).sum()) == 1
     convs += hp
-    # auto policy: blocks 1-10 fused, 11-17 as expand/project convs (2 each, block 17 included)
-    assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0), (64 + 3 + 14, 10))
+    # auto policy: blocks 1-13 fused, 14-17 as expand/project convs (2 each, block 17 included)
+    assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0), (64 + 3 + 8, 13))
     assert program.cls_ops.shape[0] < program.ops.shape[0]
     assert program.weights.nbytes % 256 == 0
 
