@@ -369,6 +369,8 @@ static void ir_set_attr() {
   X(1, 14, 14, 6, true)
 
 void ir_wave_prepare();
+void ir_crop_prepare();
+bool ir_block_crop(const IrParams& p, hipStream_t s);
 bool ir_block_wave(const IrParams& p, int tile, hipStream_t s);
 static bool g_ir_wave = [] {
   const char* e = std::getenv("ARENA_IR_WAVE");
@@ -378,6 +380,7 @@ void set_ir_wave(bool v) { g_ir_wave = v; }
 
 void ir_prepare() {
   ir_wave_prepare();
+  ir_crop_prepare();
 #define X(S, TH, TW, MP, E) ir_set_attr<S, TH, TW, MP, E>();
   ARENA_IR_CONFIGS(X)
 #undef X
@@ -410,6 +413,7 @@ void ir_block(const IrParams& p, hipStream_t s) {
   if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_block: residual needs s1, inp == oup");
   if (p.Ho != (p.H + 2 - 3) / p.stride + 1 || p.Wo != (p.W + 2 - 3) / p.stride + 1)
     throw std::runtime_error("ir_block: output size mismatch");
+  if (ir_block_crop(p, s)) return;
   const int T = ir_tile(p.Ho, p.stride);
   if (g_ir_wave && ir_block_wave(p, T, s)) return;
   const int MP = p.oup_pad / 16;

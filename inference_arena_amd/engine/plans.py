@@ -222,17 +222,27 @@ def fuse_ir_default() -> str:
     return {"0": "none", "1": "all", "false": "none", "true": "all"}.get(v, v)
 
 
+def ir_crop_default() -> bool:
+    """``ARENA_IR_CROP`` (default 1): MobileNetV2 blocks with a 7x7 output map and <= 160 output channels
+    run fused as one workgroup per crop (the native side reads the same variable)."""
+    return os.environ.get("ARENA_IR_CROP", "1").lower() not in ("0", "false", "no", "off")
+
+
 def fuse_block(blk, H: int, policy) -> bool:
     """``auto``: fuse where the tile kernel wins on MI355X — blocks at >= 28x28 input and the stride-1
     14x14 blocks (hid 576: 46 us fused vs 28 + 18 + 17 us as expand / depthwise / project ops;
     profiles/r1_irpolicy14_ops.md).  The 14 -> 7 stride-2 block and the 7x7 blocks have one
-    output tile per crop and a 18-30 chunk serial loop: they run faster as batched 1x1 GEMMs +
-    depthwise over all crops (59 vs 52 us, 80 vs 50 us)."""
+    output tile per crop and a 18-30 chunk serial loop in the tile kernel: unless the whole-crop
+    kernel takes them (``ARENA_IR_CROP``, default 1: csrc/kernels/ir_crop.hip, waves split the hidden
+    channels; <= 160 output channels) they run as batched 1x1 GEMMs + depthwise over all crops."""
     if policy in (True, "all"):
         return True
     if policy in (False, None, "none"):
         return False
-    return H >= 28 or (H >= 14 and blk.stride == 1)
+    if H >= 28 or (H >= 14 and blk.stride == 1):
+        return True
+    Ho = (H + 2 - 3) // blk.stride + 1
+    return ir_crop_default() and Ho == 7 and blk.expand is not None and blk.oup <= 160
 
 
 def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std, *, kind: int = CROPS,

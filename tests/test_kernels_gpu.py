@@ -437,3 +437,29 @@ def test_ir_block_whole_crop_14(device, B, inp, hid, oup, res):
         C.set_ir_t14(False)
     ref = _ref_ir(xn.cpu(), expand, dw, project, 1, res)
     _check(_nchw(y.cpu()), ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,inp,hid,oup,s,res", [(14, 96, 576, 160, 2, False), (7, 160, 960, 160, 1, True),
+                                                 (7, 160, 960, 160, 1, False)])
+def test_ir_crop_matches_tile_kernel_and_torch(device, H, inp, hid, oup, s, res):
+    """Whole-crop IR kernel (waves split the hidden channels, ir_crop.hip) == torch fp32 reference and the
+    7x7-tile kernel; crops past the device-side live count are not written."""
+    C = native()
+    g = torch.Generator().manual_seed(H * 7 + hid)
+    x = (torch.rand(5, inp, H, H, generator=g) * 2).to(torch.bfloat16)
+    expand = (torch.randn(hid, inp, 1, 1, generator=g) / np.sqrt(inp), torch.randn(hid, generator=g) * 0.1)
+    dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
+    project = (torch.randn(oup, hid, 1, 1, generator=g) / np.sqrt(hid), torch.randn(oup, generator=g) * 0.1)
+    xn = _nhwc(x).to(device)
+    y = AF.ir_block_nhwc(xn, expand, dw, project, stride=s, res=res)
+    _check(_nchw(y.cpu()), _ref_ir(xn.cpu(), expand, dw, project, s, res), rtol=3e-2, atol=3e-2)
+    C.set_ir_crop(False)
+    try:
+        yt = AF.ir_block_nhwc(xn, expand, dw, project, stride=s, res=res)
+    finally:
+        C.set_ir_crop(True)
+    assert (y.float() - yt.float()).abs().max().item() <= 0.07
+    bdev = torch.tensor([3], dtype=torch.int32, device=device)
+    yl = AF.ir_block_nhwc(xn, expand, dw, project, stride=s, res=res, bdev=bdev)
+    assert torch.equal(yl[:3].cpu(), y[:3].cpu())

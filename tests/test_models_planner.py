@@ -134,8 +134,9 @@ def test_program_shape(program):
     hp = int((program.ops[:, 0] == OP_HEADPOOL).sum())
     assert hp + int((program.ops[:, 0] == OP_AVGPOOL).sum()) == 1
     convs += hp
-    # auto policy: blocks 1-13 fused, 14-17 as expand/project convs (2 each, block 17 included)
-    assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0), (64 + 3 + 8, 13))
+    # auto policy: blocks 1-16 fused, block 17 (320 out) as expand/project convs (+ 2); ARENA_IR_CROP=0:
+    # blocks 14-17 unfused
+    assert (convs, irs) in ((64 + 3, 17), (64 + 36, 0), (64 + 3 + 8, 13), (64 + 3 + 2, 16))
     assert program.cls_ops.shape[0] < program.ops.shape[0]
     assert program.weights.nbytes % 256 == 0
 

@@ -33,6 +33,7 @@ SOURCES = [
     "kernels/dwconv.hip",
     "kernels/ir_block.hip",
     "kernels/ir_block_wave.hip",
+    "kernels/ir_crop.hip",
     "kernels/conv_igemm.hip",
     "kernels/conv_pw.hip",
     "kernels/conv3x3_v3.hip",
