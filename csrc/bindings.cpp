@@ -352,6 +352,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_ir_wave", &set_ir_wave);
   m.def("set_ir_t14", &set_ir_t14);
   m.def("set_ir_crop", &set_ir_crop);
+  m.def("set_ir_crop_split", &set_ir_crop_split);
   m.def("letterbox_s2d", &py_letterbox);
   m.def("detect_decode", &py_decode);
   m.def("nms", &py_nms);

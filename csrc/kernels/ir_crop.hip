@@ -33,22 +33,27 @@ __device__ __forceinline__ void crop_wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int S, int NSLAB, int MP>
+// RS workgroups per crop split its 7 output rows (RS = 2: rows 0-3 and 4-6; each recomputes the
+// expansion of the 1-2 input rows the two halves share, and the grid covers the whole chip).
+template <int S, int NSLAB, int MP, int RS>
 struct IrCropGeom {
   static constexpr int HI = 7 * S;                       // input map side
-  static constexpr int PIN = HI * HI, PIN_PAD = (PIN + 15) / 16 * 16;
+  static constexpr int NOR = RS == 1 ? 7 : 4;            // max output rows per workgroup
+  static constexpr int IR = RS == 1 ? HI : (S == 1 ? 5 : 8);  // max input rows per workgroup
+  static constexpr int PIN = IR * HI, PIN_PAD = (PIN + 15) / 16 * 16;
   static constexpr int NE = PIN_PAD / 16;                // expand N-tiles
+  static constexpr int NP = (NOR * 7 + 15) / 16;         // project N-tiles
   static constexpr int X_BYTES = NSLAB * PIN_PAD * 64;
-  static constexpr int WAVE_BYTES = PIN_PAD * 64 + 64 * 64;  // E rows + D rows (64 output rows)
-  static constexpr int R_BYTES = 64 * MP * 16 * 4;           // fp32 [64 px][oup_pad]
+  static constexpr int WAVE_BYTES = PIN_PAD * 64 + NP * 16 * 64;  // E rows + D rows
+  static constexpr int R_BYTES = NP * 16 * MP * 16 * 4;           // fp32 [px][oup_pad]
   static constexpr int TAIL = 4 * WAVE_BYTES > R_BYTES ? 4 * WAVE_BYTES : R_BYTES;
   static constexpr int LDS = X_BYTES + TAIL;
 };
 
-template <int S, int NSLAB, int MP>
+template <int S, int NSLAB, int MP, int RS>
 __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
-  using G = IrCropGeom<S, NSLAB, MP>;
-  constexpr int HI = G::HI, PIN = G::PIN, PIN_PAD = G::PIN_PAD, NE = G::NE;
+  using G = IrCropGeom<S, NSLAB, MP, RS>;
+  constexpr int HI = G::HI, PIN = G::PIN, PIN_PAD = G::PIN_PAD, NE = G::NE, NP = G::NP;
   extern __shared__ __align__(16) uint8_t lds[];
   uint8_t* Xs = lds;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -57,9 +62,13 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
   uint8_t* Ds = Es + PIN_PAD * 64;
   float* R = (float*)(lds + G::X_BYTES);
 
-  const int b = blockIdx.x;
+  const int b = blockIdx.x / RS, part = blockIdx.x - b * RS;
   if (b >= live_batch(p.B, p.bdev)) return;
-  const bf16* xb = (const bf16*)p.x + (size_t)b * HI * HI * p.x_cs;
+  const int oy0 = part * 4, nor = RS == 1 ? 7 : (part ? 3 : 4), nout = nor * 7;
+  const int iy_lo = oy0 * S - 1 < 0 ? 0 : oy0 * S - 1;
+  const int iy_hi = (oy0 + nor - 1) * S + 2 > HI ? HI : (oy0 + nor - 1) * S + 2;  // exclusive
+  const int pin = (iy_hi - iy_lo) * HI;
+  const bf16* xb = (const bf16*)p.x + ((size_t)b * HI * HI + (size_t)iy_lo * HI) * p.x_cs;
   const bf16* we = (const bf16*)p.we;
   const bf16* wd = (const bf16*)p.wd;
   const bf16* wp = (const bf16*)p.wp;
@@ -80,15 +89,15 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
   // whole input map -> LDS (zero past inp)
   for (int i = tid; i < PIN_PAD * cpr; i += 256) {
     const int pix = i / cpr, c = i - pix * cpr;
-    const bool ok = pix < PIN && c * 8 < p.inp;
+    const bool ok = pix < pin && c * 8 < p.inp;
     const uint4 v = load16_or_zero(xb + (size_t)pix * p.x_cs + c * 8, xb, ok);
     *(uint4*)(Xs + (c >> 2) * PIN_PAD * 64 + cswz(pix, c & 3)) = v;
   }
   __syncthreads();
 
-  f32x4 acc[4][MP];
+  f32x4 acc[NP][MP];
 #pragma unroll
-  for (int n = 0; n < 4; ++n)
+  for (int n = 0; n < NP; ++n)
 #pragma unroll
     for (int m = 0; m < MP; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -106,7 +115,8 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
 
     // ---- expand: E[pix][32] = relu6(We[h0..h0+32] . X[pix] + be)
     const float4 be0 = *(const float4*)(p.be + h0 + kq * 4), be1 = *(const float4*)(p.be + h0 + 16 + kq * 4);
-#pragma unroll(S == 1 ? 4 : 1)
+    constexpr int EU = NE <= 4 ? 4 : 1;
+#pragma unroll EU
     for (int j = 0; j < NE; ++j) {
       f32x4 e0 = {be0.x, be0.y, be0.z, be0.w}, e1 = {be1.x, be1.y, be1.z, be1.w};
 #pragma unroll
@@ -144,16 +154,16 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
     float w8[8];
     unpack8(wdr[8], w8);
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < NP; ++it) {
       const int q = it * 16 + (lane >> 2);
       uint4 outv = {0u, 0u, 0u, 0u};
-      if (q < 49) {
-        const int oy = q / 7, ox = q - (q / 7) * 7;
+      if (q < nout) {
+        const int oy = oy0 + q / 7, ox = q - (q / 7) * 7;
         float a[8] = {bd0.x, bd0.y, bd0.z, bd0.w, bd1.x, bd1.y, bd1.z, bd1.w};
         auto tap = [&](int t) {
           const int iy = oy * S - 1 + t / 3, ix = ox * S - 1 + t % 3;
           const bool ok = (unsigned)iy < (unsigned)HI && (unsigned)ix < (unsigned)HI;
-          const uint4 v = *(const uint4*)(Es + cswz(ok ? iy * HI + ix : 0, dc));
+          const uint4 v = *(const uint4*)(Es + cswz(ok ? (iy - iy_lo) * HI + ix : 0, dc));
           return ok ? v : make_uint4(0u, 0u, 0u, 0u);
         };
 #pragma unroll
@@ -183,7 +193,7 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
 
     // ---- project: acc[px tile][oup tile] += Wp[oup][h0..h0+32] . D
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NP; ++n) {
       const bf16x8 bv = *(const bf16x8*)(Ds + cswz(n * 16 + row, kq));
 #pragma unroll
       for (int m = 0; m < MP; ++m)
@@ -201,9 +211,9 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
     __syncthreads();
     if (wave == w) {
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
+      for (int n = 0; n < NP; ++n) {
         const int pix = n * 16 + row;
-        if (pix < 49) {
+        if (pix < nout) {
 #pragma unroll
           for (int m = 0; m < MP; ++m) {
             float4* r = (float4*)(R + pix * OP + m * 16 + kq * 4);
@@ -221,16 +231,17 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
   __syncthreads();
 
   // ---- epilogue: + bp (+ residual from the staged input map, stride 1) -> NHWC bf16
-  bf16* yb = (bf16*)p.y + (size_t)b * 49 * p.y_cs;
+  bf16* yb = (bf16*)p.y + ((size_t)b * 49 + oy0 * 7) * p.y_cs;
   const int g4 = p.oup >> 2;
-  for (int i = tid; i < 49 * g4; i += 256) {
+  const int rshift = (oy0 - iy_lo) * 7;  // output pixel -> its input pixel in the staged rows (S == 1)
+  for (int i = tid; i < nout * g4; i += 256) {
     const int pix = i / g4, oc = (i - pix * g4) * 4;
     const float4 rv = *(const float4*)(R + pix * OP + oc);
     const float4 bb = *(const float4*)(p.bp + oc);
     float v[4] = {rv.x + bb.x, rv.y + bb.y, rv.z + bb.z, rv.w + bb.w};
     if (S == 1 && p.res) {
       float r[4];
-      unpack4(*(const uint2*)(Xs + (oc >> 5) * PIN_PAD * 64 + cswz(pix, (oc & 31) >> 3) + (oc & 7) * 2), r);
+      unpack4(*(const uint2*)(Xs + (oc >> 5) * PIN_PAD * 64 + cswz(pix + rshift, (oc & 31) >> 3) + (oc & 7) * 2), r);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] += r[k];
     }
@@ -238,12 +249,12 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
   }
 }
 
-template <int S, int NSLAB, int MP>
+template <int S, int NSLAB, int MP, int RS>
 static void ir_crop_launch(const IrParams& p, hipStream_t s) {
-  using G = IrCropGeom<S, NSLAB, MP>;
+  using G = IrCropGeom<S, NSLAB, MP, RS>;
   static_assert(G::LDS <= 160 * 1024, "ir_crop: LDS budget");
   if (p.B <= 0) return;
-  hipLaunchKernelGGL((ir_crop_kernel<S, NSLAB, MP>), dim3((unsigned)p.B), dim3(256), G::LDS, s, p);
+  hipLaunchKernelGGL((ir_crop_kernel<S, NSLAB, MP, RS>), dim3((unsigned)(p.B * RS)), dim3(256), G::LDS, s, p);
 }
 
 #define ARENA_IR_CROP_CONFIGS(X) \
@@ -251,8 +262,10 @@ static void ir_crop_launch(const IrParams& p, hipStream_t s) {
   X(1, 5, 10)
 
 void ir_crop_prepare() {
-#define X(S_, NS_, MP_)                                                                         \
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_crop_kernel<S_, NS_, MP_>,               \
+#define X(S_, NS_, MP_)                                                                            \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_crop_kernel<S_, NS_, MP_, 1>,               \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));    \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_crop_kernel<S_, NS_, MP_, 2>,               \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   ARENA_IR_CROP_CONFIGS(X)
 #undef X
@@ -263,6 +276,11 @@ static bool g_ir_crop = [] {
   return e ? std::atoi(e) != 0 : true;
 }();
 void set_ir_crop(bool v) { g_ir_crop = v; }
+static int g_ir_crop_split = [] {
+  const char* e = std::getenv("ARENA_IR_CROP_SPLIT");
+  return e ? (std::atoi(e) == 1 ? 1 : 2) : 2;
+}();
+void set_ir_crop_split(int v) { g_ir_crop_split = v == 1 ? 1 : 2; }
 
 // Blocks with a 7x7 output map (input 7 at stride 1 or 14 at stride 2), an expansion and <= 160
 // output channels; false = not handled here (the caller falls back to the tile kernels).
@@ -272,7 +290,10 @@ bool ir_block_crop(const IrParams& p, hipStream_t s) {
   const int ns = p.inp_pad / 32;
 #define X(S_, NS_, MP_)                                    \
   if (p.stride == S_ && ns == NS_ && p.oup_pad == MP_ * 16) { \
-    ir_crop_launch<S_, NS_, MP_>(p, s);                    \
+    if (g_ir_crop_split == 2)                              \
+      ir_crop_launch<S_, NS_, MP_, 2>(p, s);               \
+    else                                                   \
+      ir_crop_launch<S_, NS_, MP_, 1>(p, s);               \
     return true;                                           \
   }
   ARENA_IR_CROP_CONFIGS(X)

@@ -440,12 +440,15 @@ def test_ir_block_whole_crop_14(device, B, inp, hid, oup, res):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("split", [1, 2])
 @pytest.mark.parametrize("H,inp,hid,oup,s,res", [(14, 96, 576, 160, 2, False), (7, 160, 960, 160, 1, True),
                                                  (7, 160, 960, 160, 1, False)])
-def test_ir_crop_matches_tile_kernel_and_torch(device, H, inp, hid, oup, s, res):
-    """Whole-crop IR kernel (waves split the hidden channels, ir_crop.hip) == torch fp32 reference and the
-    7x7-tile kernel; crops past the device-side live count are not written."""
+def test_ir_crop_matches_tile_kernel_and_torch(device, H, inp, hid, oup, s, res, split):
+    """Whole-crop IR kernel (waves split the hidden channels, ir_crop.hip; ``split`` workgroups per crop
+    split its output rows) == torch fp32 reference and the 7x7-tile kernel; crops past the device-side
+    live count are not written."""
     C = native()
+    C.set_ir_crop_split(split)
     g = torch.Generator().manual_seed(H * 7 + hid)
     x = (torch.rand(5, inp, H, H, generator=g) * 2).to(torch.bfloat16)
     expand = (torch.randn(hid, inp, 1, 1, generator=g) / np.sqrt(inp), torch.randn(hid, generator=g) * 0.1)
@@ -462,4 +465,5 @@ def test_ir_crop_matches_tile_kernel_and_torch(device, H, inp, hid, oup, s, res)
     assert (y.float() - yt.float()).abs().max().item() <= 0.07
     bdev = torch.tensor([3], dtype=torch.int32, device=device)
     yl = AF.ir_block_nhwc(xn, expand, dw, project, stride=s, res=res, bdev=bdev)
+    C.set_ir_crop_split(2)
     assert torch.equal(yl[:3].cpu(), y[:3].cpu())
