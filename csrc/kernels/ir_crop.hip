@@ -1,6 +1,6 @@
-// Whole-crop inverted residual for MobileNetV2's 7x7-output blocks (14 -> 7 stride 2, hid 576 and the
-// two 7x7 hid-960 residual blocks; reference: torchvision mobilenet_v2 features[14..16], run per crop
-// by architectures/monolithic/app/inference.py:196).
+// Whole-crop inverted residual for MobileNetV2's 7x7-output blocks (14 -> 7 stride 2, hid 576, the
+// two 7x7 hid-960 residual blocks and the 160 -> 320 block; reference: torchvision mobilenet_v2
+// features[14..17], run per crop by architectures/monolithic/app/inference.py:196).
 //
 // At 7x7 the tile kernels (ir_block.hip) get one output tile per crop and walk 18-30 hidden chunks
 // with three workgroup barriers each; unfused, the 7x7x960 expanded map makes two HBM round trips
@@ -62,7 +62,11 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
   uint8_t* Ds = Es + PIN_PAD * 64;
   float* R = (float*)(lds + G::X_BYTES);
 
-  const int b = blockIdx.x / RS, part = blockIdx.x - b * RS;
+  // OG = oup_pad / (16 MP) output-channel groups per crop (320-out block: 2); each group recomputes the
+  // expansion + depthwise and projects onto its own 16 MP output channels
+  const int og_n = p.oup_pad / (MP * 16);
+  const int b = blockIdx.x / (RS * og_n), rem = blockIdx.x - b * RS * og_n;
+  const int part = rem / og_n, og = rem - part * og_n, oc_base = og * MP * 16;
   if (b >= live_batch(p.B, p.bdev)) return;
   const int oy0 = part * 4, nor = RS == 1 ? 7 : (part ? 3 : 4), nout = nor * 7;
   const int iy_lo = oy0 * S - 1 < 0 ? 0 : oy0 * S - 1;
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
     const float4 bd0 = *(const float4*)(p.bd + h0 + dc * 8), bd1 = *(const float4*)(p.bd + h0 + dc * 8 + 4);
     uint4 rwp[MP];
 #pragma unroll
-    for (int m = 0; m < MP; ++m) rwp[m] = *(const uint4*)(wp + (size_t)(m * 16 + row) * p.hid_pad + h0 + kq * 8);
+    for (int m = 0; m < MP; ++m) rwp[m] = *(const uint4*)(wp + (size_t)(oc_base + m * 16 + row) * p.hid_pad + h0 + kq * 8);
 
     // ---- expand: E[pix][32] = relu6(We[h0..h0+32] . X[pix] + be)
     const float4 be0 = *(const float4*)(p.be + h0 + kq * 4), be1 = *(const float4*)(p.be + h0 + 16 + kq * 4);
@@ -232,12 +236,12 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
 
   // ---- epilogue: + bp (+ residual from the staged input map, stride 1) -> NHWC bf16
   bf16* yb = (bf16*)p.y + ((size_t)b * 49 + oy0 * 7) * p.y_cs;
-  const int g4 = p.oup >> 2;
+  const int g4 = (p.oup - oc_base < OP ? p.oup - oc_base : OP) >> 2;
   const int rshift = (oy0 - iy_lo) * 7;  // output pixel -> its input pixel in the staged rows (S == 1)
   for (int i = tid; i < nout * g4; i += 256) {
     const int pix = i / g4, oc = (i - pix * g4) * 4;
     const float4 rv = *(const float4*)(R + pix * OP + oc);
-    const float4 bb = *(const float4*)(p.bp + oc);
+    const float4 bb = *(const float4*)(p.bp + oc_base + oc);
     float v[4] = {rv.x + bb.x, rv.y + bb.y, rv.z + bb.z, rv.w + bb.w};
     if (S == 1 && p.res) {
       float r[4];
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(256) void ir_crop_kernel(const IrParams p) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] += r[k];
     }
-    *(uint2*)(yb + (size_t)pix * p.y_cs + oc) = pack4(v);
+    *(uint2*)(yb + (size_t)pix * p.y_cs + oc_base + oc) = pack4(v);
   }
 }
 
@@ -254,7 +258,7 @@ static void ir_crop_launch(const IrParams& p, hipStream_t s) {
   using G = IrCropGeom<S, NSLAB, MP, RS>;
   static_assert(G::LDS <= 160 * 1024, "ir_crop: LDS budget");
   if (p.B <= 0) return;
-  hipLaunchKernelGGL((ir_crop_kernel<S, NSLAB, MP, RS>), dim3((unsigned)(p.B * RS)), dim3(256), G::LDS, s, p);
+  hipLaunchKernelGGL((ir_crop_kernel<S, NSLAB, MP, RS>), dim3((unsigned)(p.B * RS * (p.oup_pad / (MP * 16)))), dim3(256), G::LDS, s, p);
 }
 
 #define ARENA_IR_CROP_CONFIGS(X) \
@@ -282,15 +286,16 @@ static int g_ir_crop_split = [] {
 }();
 void set_ir_crop_split(int v) { g_ir_crop_split = v == 1 ? 1 : 2; }
 
-// Blocks with a 7x7 output map (input 7 at stride 1 or 14 at stride 2), an expansion and <= 160
-// output channels; false = not handled here (the caller falls back to the tile kernels).
+// Blocks with a 7x7 output map (input 7 at stride 1 or 14 at stride 2), an expansion and 160 or 320
+// output channels (320: two workgroups per crop, one per 160-channel group, each over all 7 rows:
+// splitting rows as well doubles the recomputed expansion and measured 60 us vs 51 unfused); false = not handled here (the caller falls back to the tile kernels).
 bool ir_block_crop(const IrParams& p, hipStream_t s) {
   if (!g_ir_crop || !p.expand || p.Ho != 7 || p.Wo != 7 || p.H != 7 * p.stride || p.W != p.H) return false;
-  if (p.oup_pad != 160 || p.oup % 4 || (p.res && p.stride != 1)) return false;
+  if (p.oup_pad % 160 || p.oup_pad > 320 || p.oup % 4 || (p.res && (p.stride != 1 || p.oup_pad != 160))) return false;
   const int ns = p.inp_pad / 32;
 #define X(S_, NS_, MP_)                                    \
-  if (p.stride == S_ && ns == NS_ && p.oup_pad == MP_ * 16) { \
-    if (g_ir_crop_split == 2)                              \
+  if (p.stride == S_ && ns == NS_ && p.oup_pad % (MP_ * 16) == 0) { \
+    if (g_ir_crop_split == 2 && p.oup_pad == MP_ * 16)     \
       ir_crop_launch<S_, NS_, MP_, 2>(p, s);               \
     else                                                   \
       ir_crop_launch<S_, NS_, MP_, 1>(p, s);               \

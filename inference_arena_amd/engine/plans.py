@@ -223,7 +223,7 @@ def fuse_ir_default() -> str:
 
 
 def ir_crop_default() -> bool:
-    """``ARENA_IR_CROP`` (default 1): MobileNetV2 blocks with a 7x7 output map and <= 160 output channels
+    """``ARENA_IR_CROP`` (default 1): MobileNetV2 blocks with a 7x7 output map and <= 160 (or 320) output channels
     run fused as one workgroup per crop (the native side reads the same variable)."""
     return os.environ.get("ARENA_IR_CROP", "1").lower() not in ("0", "false", "no", "off")
 
@@ -234,7 +234,7 @@ def fuse_block(blk, H: int, policy) -> bool:
     profiles/r1_irpolicy14_ops.md).  The 14 -> 7 stride-2 block and the 7x7 blocks have one
     output tile per crop and a 18-30 chunk serial loop in the tile kernel: unless the whole-crop
     kernel takes them (``ARENA_IR_CROP``, default 1: csrc/kernels/ir_crop.hip, waves split the hidden
-    channels; <= 160 output channels) they run as batched 1x1 GEMMs + depthwise over all crops."""
+    channels; <= 160 or 320 output channels) they run as batched 1x1 GEMMs + depthwise over all crops."""
     if policy in (True, "all"):
         return True
     if policy in (False, None, "none"):
@@ -242,7 +242,7 @@ def fuse_block(blk, H: int, policy) -> bool:
     if H >= 28 or (H >= 14 and blk.stride == 1):
         return True
     Ho = (H + 2 - 3) // blk.stride + 1
-    return ir_crop_default() and Ho == 7 and blk.expand is not None and blk.oup <= 160
+    return ir_crop_default() and Ho == 7 and blk.expand is not None and (blk.oup <= 160 or blk.oup == 320)
 
 
 def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std, *, kind: int = CROPS,

@@ -362,7 +362,8 @@ def test_executor_autotune_choices(device):
     imgs = synthetic_images(4, 77)
     pipe = GpuPipeline(yolo, mnet, device=0, buckets=[4])
     choices = pipe.ex.conv_choices(4)
-    assert set(c for c in choices if c) <= {1, 2, 3} and sum(1 for c in choices if c) >= 60
+    # ~50 conv ops remain once the C3 / inverted-residual / stem / head fusions have absorbed the rest
+    assert set(c for c in choices if c) <= {1, 2, 3} and sum(1 for c in choices if c) >= 45
     tuned = pipe.infer(imgs)
     os.environ["ARENA_AUTOTUNE"] = "0"
     try:
@@ -442,7 +443,7 @@ def test_ir_block_whole_crop_14(device, B, inp, hid, oup, res):
 @pytest.mark.gpu
 @pytest.mark.parametrize("split", [1, 2])
 @pytest.mark.parametrize("H,inp,hid,oup,s,res", [(14, 96, 576, 160, 2, False), (7, 160, 960, 160, 1, True),
-                                                 (7, 160, 960, 160, 1, False)])
+                                                 (7, 160, 960, 160, 1, False), (7, 160, 960, 320, 1, False)])
 def test_ir_crop_matches_tile_kernel_and_torch(device, H, inp, hid, oup, s, res, split):
     """Whole-crop IR kernel (waves split the hidden channels, ir_crop.hip; ``split`` workgroups per crop
     split its output rows) == torch fp32 reference and the 7x7-tile kernel; crops past the device-side
