@@ -31,7 +31,11 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
   constexpr int PIN = PH * PW, PIN_PAD = (PIN + 15) / 16 * 16;
   constexpr int POUT = TH * TW, POUT_PAD = (POUT + 15) / 16 * 16;
   constexpr int NE = PIN_PAD / 16, NP = POUT_PAD / 16;
-  constexpr int XB = NS * PIN_PAD * 64, EB = EXPAND ? PIN_PAD * 64 : 0, DB = POUT_PAD * 64;
+  // Stride-2 expand blocks (one input slab, no residual): each lane keeps its expand B operands (halo
+  // pixel j*16+row, channels kq*8..+8) in NE VGPR quads instead of staging the tile in LDS; LDS per
+  // workgroup 53 -> 28 KB, so occupancy is no longer LDS-bound at 3 waves per SIMD
+  constexpr bool XREG = S == 2 && NS == 1 && EXPAND;
+  constexpr int XB = XREG ? 0 : NS * PIN_PAD * 64, EB = EXPAND ? PIN_PAD * 64 : 0, DB = POUT_PAD * 64;
   constexpr int WAVE_BYTES = XB + EB + DB;
   // unroll depth per shape (measured: full unroll is best for 7x7 tiles; the 8x8 tile
   // needs the lighter unroll to stay at 2 waves/SIMD without AGPR spills)
@@ -55,9 +59,20 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   const bf16* xb = (const bf16*)p.x + (size_t)b * p.H * p.W * p.x_cs;
 
-  // ---- input halo tile -> this wave's LDS (zero outside the image / past inp)
+  // ---- input halo tile -> this wave's LDS (zero outside the image / past inp), or -> xr (XREG)
+  bf16x8 xr[XREG ? NE : 1];
+  if constexpr (XREG) {
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const int pix = j * 16 + row;
+      const int py = pix / PW, px = pix - py * PW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      const bool ok = pix < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && kq * 8 < p.inp;
+      xr[j] = __builtin_bit_cast(bf16x8, load16_or_zero(xb + ((size_t)iy * p.W + ix) * p.x_cs + kq * 8, xb, ok));
+    }
+  }
   constexpr int CPR = NS * 4;
-  for (int i = lane; i < PIN_PAD * CPR; i += 64) {
+  for (int i = lane; !XREG && i < PIN_PAD * CPR; i += 64) {
     const int pix = i / CPR, c = i - pix * CPR;  // CPR is a compile-time power of two
     const int py = pix / PW, px = pix - py * PW;
     const int iy = iy0 + py, ix = ix0 + px;
@@ -130,7 +145,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
         f32x4 e0 = {be0.x, be0.y, be0.z, be0.w}, e1 = {be1.x, be1.y, be1.z, be1.w};  // bias folded into init
 #pragma unroll
         for (int sl = 0; sl < NS; ++sl) {
-          const bf16x8 bv = *(const bf16x8*)(Xs + sl * PIN_PAD * 64 + wswz(j * 16 + row, kq));
+          const bf16x8 bv = XREG ? xr[j] : *(const bf16x8*)(Xs + sl * PIN_PAD * 64 + wswz(j * 16 + row, kq));
           e0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa0[sl], bv, e0, 0, 0, 0);
           e1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[sl], bv, e1, 0, 0, 0);
         }
@@ -216,7 +231,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
       if (oc >= p.oup) continue;
       const float4 bb = *(const float4*)(p.bp + oc);
       float v[4] = {acc[q][m][0] + bb.x, acc[q][m][1] + bb.y, acc[q][m][2] + bb.z, acc[q][m][3] + bb.w};
-      if (S == 1 && p.res) {
+      if (S == 1 && !XREG && p.res) {
         float r[4];
         unpack4(*(const uint2*)(Xs + (oc >> 5) * PIN_PAD * 64 + wswz(rpix, (oc & 31) >> 3) + (oc & 7) * 2), r);
 #pragma unroll
@@ -230,7 +245,8 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
 template <int S, int TH, int TW, int MP, int NS, bool EXPAND>
 static void irw_launch(const IrParams& p, hipStream_t s) {
   constexpr int PIN_PAD = (((TH - 1) * S + 3) * ((TW - 1) * S + 3) + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
-  constexpr size_t lds = 4 * (size_t)(NS * PIN_PAD * 64 + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64);
+  constexpr bool XREG = S == 2 && NS == 1 && EXPAND;
+  constexpr size_t lds = 4 * (size_t)((XREG ? 0 : NS * PIN_PAD * 64) + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64);
   static_assert(lds <= 160 * 1024, "LDS");
   const long tiles = (long)((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
   if (tiles <= 0) return;
