@@ -25,6 +25,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef IRW_XREG_S1
+#define IRW_XREG_S1 1
+#endif
+
 template <int S, int TH, int TW, int MP, int NS, bool EXPAND>
 __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
@@ -34,12 +38,12 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
   // Stride-2 expand blocks (one input slab, no residual): each lane keeps its expand B operands (halo
   // pixel j*16+row, channels kq*8..+8) in NE VGPR quads instead of staging the tile in LDS; LDS per
   // workgroup 53 -> 28 KB, so occupancy is no longer LDS-bound at 3 waves per SIMD
-  constexpr bool XREG = S == 2 && NS == 1 && EXPAND;
+  constexpr bool XREG = NS == 1 && EXPAND && (S == 2 || IRW_XREG_S1);
   constexpr int XB = XREG ? 0 : NS * PIN_PAD * 64, EB = EXPAND ? PIN_PAD * 64 : 0, DB = POUT_PAD * 64;
   constexpr int WAVE_BYTES = XB + EB + DB;
   // unroll depth per shape (measured: full unroll is best for 7x7 tiles; the 8x8 tile
   // needs the lighter unroll to stay at 2 waves/SIMD without AGPR spills)
-  constexpr int E_UNROLL = TH == 8 ? 2 : NE;
+  constexpr int E_UNROLL = TH == 8 && !XREG ? 2 : NE;  // xr[j] needs static indices
   constexpr int D_UNROLL = TH == 8 ? 1 : POUT_PAD / 16;
   extern __shared__ __align__(16) uint8_t lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -231,9 +235,12 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
       if (oc >= p.oup) continue;
       const float4 bb = *(const float4*)(p.bp + oc);
       float v[4] = {acc[q][m][0] + bb.x, acc[q][m][1] + bb.y, acc[q][m][2] + bb.z, acc[q][m][3] + bb.w};
-      if (S == 1 && !XREG && p.res) {
+      if (S == 1 && p.res) {
         float r[4];
-        unpack4(*(const uint2*)(Xs + (oc >> 5) * PIN_PAD * 64 + wswz(rpix, (oc & 31) >> 3) + (oc & 7) * 2), r);
+        if constexpr (XREG)  // the tile was never staged: residual straight from global (L2-hot)
+          unpack4(*(const uint2*)(xb + ((size_t)oy * p.W + ox) * p.x_cs + oc), r);
+        else
+          unpack4(*(const uint2*)(Xs + (oc >> 5) * PIN_PAD * 64 + wswz(rpix, (oc & 31) >> 3) + (oc & 7) * 2), r);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] += r[k];
       }
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(256) void ir_wave_kernel(const IrParams p) {
 template <int S, int TH, int TW, int MP, int NS, bool EXPAND>
 static void irw_launch(const IrParams& p, hipStream_t s) {
   constexpr int PIN_PAD = (((TH - 1) * S + 3) * ((TW - 1) * S + 3) + 15) / 16 * 16, POUT_PAD = (TH * TW + 15) / 16 * 16;
-  constexpr bool XREG = S == 2 && NS == 1 && EXPAND;
+  constexpr bool XREG = NS == 1 && EXPAND && (S == 2 || IRW_XREG_S1);
   constexpr size_t lds = 4 * (size_t)((XREG ? 0 : NS * PIN_PAD * 64) + (EXPAND ? PIN_PAD * 64 : 0) + POUT_PAD * 64);
   static_assert(lds <= 160 * 1024, "LDS");
   const long tiles = (long)((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * p.B;
