@@ -263,7 +263,8 @@ static void irw_launch(const IrParams& p, hipStream_t s) {
 
 // Measured (profiles/r1_irwave_ops.md): the wave kernel wins on the 56x56 and 28x28
 // expand blocks; block 1 (no expand) and the 14x14 blocks stay block-cooperative.
-// Stride 2 uses 4x4 output tiles (9x9 halo: 13 KB of LDS per wave).
+// Stride 2 uses 4x4 output tiles (9x9 halo).  Single-slab expand blocks keep the halo in VGPRs
+// (IRW_XREG_S1=0 at build time restores LDS staging for stride 1: profiles/r1_irwave_xreg_ops.md).
 #define ARENA_IRW_CONFIGS(X) \
   X(1, 8, 8, 2, 1, true)     \
   X(1, 7, 7, 2, 1, true)     \
