@@ -74,7 +74,10 @@ void py_conv2d(const py::dict& d) {
   p.pw_cout = get<int>(d, "pw_cout", 0);
   p.pw_kpad = get<int>(d, "pw_kpad", 0);
   p.pw_act = get<int>(d, "pw_act", 0);
-  conv2d(p, stream_of(d));
+  if (get<int>(d, "f32", 0))
+    conv2d_f32(p, stream_of(d));
+  else
+    conv2d(p, stream_of(d));
 }
 
 void py_dwconv(const py::dict& d) {
@@ -94,7 +97,10 @@ void py_dwconv(const py::dict& d) {
   p.stride = get<int>(d, "stride", 1);
   p.act = get<int>(d, "act", 0);
   p.bdev = ptr<const int*>(d, "bdev");
-  dwconv3x3(p, stream_of(d));
+  if (get<int>(d, "f32", 0))
+    dwconv3x3_f32(p, stream_of(d));
+  else
+    dwconv3x3(p, stream_of(d));
 }
 
 void py_ir_block(const py::dict& d) {
@@ -136,7 +142,10 @@ void py_sppf(const py::dict& d) {
   p.xs = req<int>(d, "xs");
   p.C = req<int>(d, "C");
   p.bdev = ptr<const int*>(d, "bdev");
-  sppf_pool(p, stream_of(d));
+  if (get<int>(d, "f32", 0))
+    sppf_pool_f32(p, stream_of(d));
+  else
+    sppf_pool(p, stream_of(d));
 }
 
 void py_letterbox(const py::dict& d) {
@@ -147,6 +156,7 @@ void py_letterbox(const py::dict& d) {
   p.out = ptr<void*>(d, "out");
   p.B = req<int>(d, "B");
   p.T = req<int>(d, "T");
+  p.f32 = get<int>(d, "f32", 0);
   letterbox_s2d(p, stream_of(d));
 }
 
@@ -168,6 +178,7 @@ void py_decode(const py::dict& d) {
   p.cand_count = ptr<int*>(d, "cand_count");
   p.cand_cap = req<int>(d, "cand_cap");
   p.ctrl = ptr<const Ctrl*>(d, "ctrl");
+  p.f32 = get<int>(d, "f32", 0);
   detect_decode(p, stream_of(d));
 }
 
@@ -216,6 +227,7 @@ void py_crop_gather(const py::dict& d) {
     p.mean[c] = mean.at(c);
     p.inv_std[c] = inv_std.at(c);
   }
+  p.f32 = get<int>(d, "f32", 0);
   crop_gather_s2d(p, stream_of(d));
 }
 
@@ -246,6 +258,7 @@ void py_avgpool(const py::dict& d) {
   p.C = req<int>(d, "C");
   p.y = ptr<void*>(d, "y");
   p.bdev = ptr<const int*>(d, "bdev");
+  p.f32 = get<int>(d, "f32", 0);
   global_avgpool(p, stream_of(d));
 }
 

@@ -11,31 +11,41 @@
 
 namespace arena {
 
+template <typename T>
 __global__ __launch_bounds__(256) void avgpool_kernel(const AvgPoolParams p) {
   const int B = live_batch(p.B, p.bdev);
   const int cg = p.C >> 3;
   const long tid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= (long)B * cg) return;
   const int b = (int)(tid / cg), g = (int)(tid % cg);
-  const bf16* x = (const bf16*)p.x + (size_t)b * p.HW * p.C + g * 8;
+  const T* x = (const T*)p.x + (size_t)b * p.HW * p.C + g * 8;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = 0; i < p.HW; ++i) {
     float v[8];
-    unpack8(*(const uint4*)(x + (size_t)i * p.C), v);
+    load8(x + (size_t)i * p.C, v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] += v[k];
   }
-  const float inv = 1.0f / (float)p.HW;
+  if constexpr (sizeof(T) == 4) {  // exact-fp32 pipeline: mean as sum / HW (torch adaptive_avg_pool2d)
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] *= inv;
-  *(uint4*)((bf16*)p.y + (size_t)b * p.C + g * 8) = pack8(acc);
+    for (int k = 0; k < 8; ++k) acc[k] /= (float)p.HW;
+  } else {
+    const float inv = 1.0f / (float)p.HW;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] *= inv;
+  }
+  store8((T*)p.y + (size_t)b * p.C + g * 8, acc);
 }
 
 void global_avgpool(const AvgPoolParams& p, hipStream_t s) {
   if (p.C % 8 != 0) throw std::runtime_error("global_avgpool: C % 8 != 0");
   const long total = (long)p.B * (p.C / 8);
   if (total <= 0) return;
-  hipLaunchKernelGGL(avgpool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (p.f32)
+    hipLaunchKernelGGL(avgpool_kernel<float>, grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(avgpool_kernel<bf16>, grid, dim3(256), 0, s, p);
 }
 
 constexpr int kTopkPer = 16;  // row elements per lane held in registers

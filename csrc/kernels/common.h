@@ -63,6 +63,20 @@ __device__ __forceinline__ uint2 pack4(const float* f) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// 8 consecutive elements of an NHWC row as fp32, for kernels templated on the
+// activation type (bf16 pipeline / exact-fp32 pipeline).
+__device__ __forceinline__ void load8(const bf16* p, float* v) { unpack8(*(const uint4*)p, v); }
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void store8(bf16* p, const float* v) { *(uint4*)p = pack8(v); }
+__device__ __forceinline__ void store8(float* p, const float* v) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
 // 16-byte global load that is zero when !ok, without a branch and without
 // the "select(ok, global ptr, &local_zero)" pattern the compiler otherwise
 // forms for `ok ? *p : zero` — that pattern turns the load into a FLAT load

@@ -1,0 +1,381 @@
+// Exact-fp32 pipeline kernels: implicit-GEMM convolution on the fp32-input
+// matrix cores, depthwise 3x3 and SPPF pooling over fp32 NHWC activations.
+//
+// The reference executes both networks as fp32 ONNX graphs on ONNX Runtime's
+// CPU EP (reference: experiment.yaml:202,207,220,225 declare float32 I/O;
+// src/shared/model/registry.py:220-224 creates the sessions).  This file is
+// the MI355X counterpart at the same precision: every product is an fp32
+// product with fp32 accumulation (v_mfma_f32_16x16x4_f32: one rounding per
+// product, a k-ordered fma chain — bit-for-bit an fp32 dot product in a
+// different summation order), activations are stored as fp32.
+//
+// GEMM mapping (v_mfma_f32_16x16x4_f32, wave64): lane l supplies
+//   A[i = l&15][k = l>>4]  (weights: row = output channel)
+//   B[k = l>>4][j = l&15]  (im2col: column = output pixel)
+// and receives D[row = 4*(l>>4) + r][col = l&15], r = 0..3.  A K-chunk of 16
+// is four MFMAs: in step s lane l supplies k = 16*chunk + 4*(l>>4) + s, so a
+// lane's four k-values of a chunk are four consecutive input channels of one
+// tap (K is ordered (kh, kw, ci)) — one 16-byte float4 load from NHWC memory,
+// and the weight fragment is one float4 of the weight row.  The accumulator
+// holds 4 consecutive output channels of one pixel: one float4 NHWC store.
+//
+// fp32 MFMA issues at 1/16 of the bf16 rate (32 cycles per 16x16x4 per SIMD),
+// so these kernels are matrix-core bound at realistic occupancy: each wave
+// keeps WC x WP independent 16x16 accumulators (>= 2 hide the 40-cycle
+// dependent latency) and prefetches the next K-chunk's operands into
+// registers while the current chunk's MFMAs run.
+#include <algorithm>
+#include <cstdlib>
+#include <stdexcept>
+
+#include "common.h"
+#include "launch.h"
+
+namespace arena {
+
+__device__ __forceinline__ float4 load_f4_or_zero(const float* p, const float* safe, bool ok) {
+  const float4 v = *(const float4*)(ok ? p : safe);
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ float f4_get(const float4& v, int s) {
+  return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
+}
+
+// Bijective XCD-aware block remap (8 XCDs, round-robin dispatch): consecutive
+// logical tiles land on the same XCD so neighbouring pixel tiles share its L2.
+__device__ __forceinline__ int xcd_remap(int bx, int nx) {
+  const int q = nx / 8, r = nx % 8, x = bx % 8, y = bx / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
+}
+
+template <int WC, int WP>
+__global__ __launch_bounds__(256) void conv_f32_kernel(const ConvParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int col = lane & 15;
+  const int kq = lane >> 4;
+
+  const int B = live_batch(p.B, p.bdev);
+  const int HWo = p.Ho * p.Wo;
+  const int M = B * HWo;
+  const int bx = xcd_remap(blockIdx.x, gridDim.x);
+  const int blk_pix = bx * (4 * WP * 16);
+  if (blk_pix >= M) return;
+  const int pix0 = blk_pix + wave * (WP * 16);
+  const int cout0 = blockIdx.y * (WC * 16);
+
+  const float* __restrict__ x = (const float*)p.x;
+  const int H = p.H, W = p.W, xs = p.xs, Cin = p.Cin, KW = p.KW;
+  const int taps = p.KH * p.KW;
+
+  int pbase[WP], iy0[WP], ix0[WP];
+  bool pv[WP];
+#pragma unroll
+  for (int q = 0; q < WP; ++q) {
+    const int pix = pix0 + q * 16 + col;
+    pv[q] = pix < M;
+    const int pp = pv[q] ? pix : 0;
+    const int b = pp / HWo;
+    const int r = pp - b * HWo;
+    const int oy = r / p.Wo;
+    const int ox = r - oy * p.Wo;
+    pbase[q] = b * H * W;
+    iy0[q] = oy * p.stride - p.pad_t;
+    ix0[q] = ox * p.stride - p.pad_l;
+  }
+
+  const float* wrow[WC];
+#pragma unroll
+  for (int c = 0; c < WC; ++c) {
+    int row = cout0 + c * 16 + col;
+    row = row < p.Cout_pad ? row : p.Cout_pad - 1;
+    wrow[c] = (const float*)p.w + (size_t)row * p.Kpad + kq * 4;
+  }
+
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int c = 0; c < WC; ++c)
+#pragma unroll
+    for (int q = 0; q < WP; ++q) acc[c][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // (tap, ci) of this lane's k-group in the current chunk
+  int ci = (kq * 4) % Cin;
+  int tap = (kq * 4) / Cin;
+  int kh = tap / KW, kw = tap - (tap / KW) * KW;
+
+  float4 a[WC], bv[WP];
+  auto load_chunk = [&](int ks, float4* av, float4* bq) {
+#pragma unroll
+    for (int c = 0; c < WC; ++c) av[c] = *(const float4*)(wrow[c] + ks * 16);
+    const bool tv = tap < taps;
+#pragma unroll
+    for (int q = 0; q < WP; ++q) {
+      const int iy = iy0[q] + kh;
+      const int ix = ix0[q] + kw;
+      const bool ok = pv[q] && tv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      bq[q] = load_f4_or_zero(x + (size_t)(pbase[q] + iy * W + ix) * xs + ci, x, ok);
+    }
+    ci += 16;
+    while (ci >= Cin) {
+      ci -= Cin;
+      ++tap;
+      if (++kw == KW) { kw = 0; ++kh; }
+    }
+  };
+
+  const int nks = p.Kpad >> 4;
+  load_chunk(0, a, bv);
+  for (int ks = 0; ks < nks; ++ks) {
+    float4 an[WC], bn[WP];
+    if (ks + 1 < nks) load_chunk(ks + 1, an, bn);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int c = 0; c < WC; ++c) {
+        const float av = f4_get(a[c], s);
+#pragma unroll
+        for (int q = 0; q < WP; ++q)
+          acc[c][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, f4_get(bv[q], s), acc[c][q], 0, 0, 0);
+      }
+    }
+    if (ks + 1 < nks) {
+#pragma unroll
+      for (int c = 0; c < WC; ++c) a[c] = an[c];
+#pragma unroll
+      for (int q = 0; q < WP; ++q) bv[q] = bn[q];
+    }
+  }
+
+  // Epilogue: bias -> activation -> residual -> store (+ 2x nearest-upsampled copy).
+#pragma unroll
+  for (int c = 0; c < WC; ++c) {
+    const int cb = cout0 + c * 16 + kq * 4;
+    if (cb >= p.Cout) continue;
+    const float4 bias = *(const float4*)(p.bias + cb);
+#pragma unroll
+    for (int q = 0; q < WP; ++q) {
+      if (!pv[q]) continue;
+      const int pix = pix0 + q * 16 + col;
+      float v[4] = {acc[c][q][0] + bias.x, acc[c][q][1] + bias.y, acc[c][q][2] + bias.z, acc[c][q][3] + bias.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      if (p.res != nullptr) {
+        const float4 rv = *(const float4*)((const float*)p.res + (size_t)pix * p.rs + cb);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      }
+      const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)p.y + (size_t)pix * p.ys + cb) = o;
+      if (p.y2 != nullptr) {
+        const int b = pix / HWo;
+        const int r = pix - b * HWo;
+        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+        const int W2 = 2 * p.Wo;
+        float* y2 = (float*)p.y2;
+        const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+        *(float4*)(y2 + base * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + 1) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2 + 1) * p.y2s + cb) = o;
+      }
+    }
+  }
+}
+
+template <int WC, int WP>
+static void launch_f32(const ConvParams& p, hipStream_t s, long M) {
+  dim3 grid((unsigned)((M + 4 * WP * 16 - 1) / (4 * WP * 16)), (unsigned)((p.Cout_pad + WC * 16 - 1) / (WC * 16)));
+  hipLaunchKernelGGL((conv_f32_kernel<WC, WP>), grid, dim3(256), 0, s, p);
+}
+
+template <int WC>
+static void launch_f32_wc(const ConvParams& p, hipStream_t s, long M) {
+  const long ny = (p.Cout_pad + WC * 16 - 1) / (WC * 16);
+  // widest pixel tile that still gives >= 2 workgroups per CU (256 CUs)
+  if (((M + 255) / 256) * ny >= 512)
+    launch_f32<WC, 4>(p, s, M);
+  else if (((M + 127) / 128) * ny >= 512)
+    launch_f32<WC, 2>(p, s, M);
+  else
+    launch_f32<WC, 1>(p, s, M);
+}
+
+void conv2d_f32(const ConvParams& p, hipStream_t s) {
+  if (p.Cin % 4 != 0 || p.xs % 4 != 0 || p.Kpad % 16 != 0 || p.Cout_pad % 16 != 0 || p.Cout % 4 != 0 ||
+      p.Cout > p.Cout_pad || p.ys % 4 != 0)
+    throw std::runtime_error("conv2d_f32: unsupported geometry (Cin/xs/ys %4, Kpad %16, Cout_pad %16, Cout %4)");
+  if (p.Cin < 16) throw std::runtime_error("conv2d_f32: Cin must be >= 16");
+  if (p.Kpad < p.KH * p.KW * p.Cin) throw std::runtime_error("conv2d_f32: Kpad < KH*KW*Cin");
+  if (p.pw_w != nullptr) throw std::runtime_error("conv2d_f32: fused pointwise epilogue is bf16-only");
+  if (p.res != nullptr && p.rs % 4 != 0) throw std::runtime_error("conv2d_f32: residual stride % 4");
+  if (p.y2 != nullptr && p.y2s % 4 != 0) throw std::runtime_error("conv2d_f32: upsampled stride % 4");
+  const long M = (long)p.B * p.Ho * p.Wo;
+  if (M <= 0) return;
+  if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
+  // channel tile: the widest of 4/3/2 x 16 channels that wastes no more than the narrower ones
+  const int ncf = p.Cout_pad / 16;
+  if (ncf % 4 == 0 || ncf > 12)
+    launch_f32_wc<4>(p, s, M);
+  else if (ncf % 3 == 0)
+    launch_f32_wc<3>(p, s, M);
+  else if (ncf % 2 == 0)
+    launch_f32_wc<2>(p, s, M);
+  else if (ncf == 5)
+    launch_f32_wc<5>(p, s, M);
+  else
+    launch_f32_wc<1>(p, s, M);
+}
+
+// ---------------------------------------------------------------- depthwise 3x3 (fp32)
+// One thread = 4 consecutive channels (one float4) of a vertical strip of R
+// output rows; the (R-1)*S+3 input rows are loaded once per strip and the 9
+// taps' weights stay in registers.  Consecutive threads take consecutive
+// channel groups of the same pixel (coalesced NHWC rows).
+template <int R, int S>
+__global__ __launch_bounds__(256) void dwconv_f32_kernel(const DwParams p) {
+  const int B = live_batch(p.B, p.bdev);
+  const int cg = p.C >> 2;
+  const int strips = (p.Ho + R - 1) / R;
+  const int total = B * strips * p.Wo * cg;
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int g = tid % cg;
+  int t = tid / cg;
+  const int ox = t % p.Wo;
+  t /= p.Wo;
+  const int st = t % strips;
+  const int b = t / strips;
+  const int c0 = g * 4;
+  const int oy0 = st * R;
+  const float* x = (const float*)p.x + (size_t)b * p.H * p.W * p.xs + c0;
+  const float* w = (const float*)p.w + c0;
+  float4 wt[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wt[k] = *(const float4*)(w + k * p.C);
+  const float4 bias = *(const float4*)(p.bias + c0);
+  float4 acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = bias;
+  constexpr int NIN = (R - 1) * S + 3;
+  const int iy0 = oy0 * S - 1, ix0 = ox * S - 1;
+#pragma unroll
+  for (int ri = 0; ri < NIN; ++ri) {
+    const int iy = iy0 + ri;
+    if ((unsigned)iy >= (unsigned)p.H) continue;
+    const float* row = x + (size_t)iy * p.W * p.xs;
+    float4 v[3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+      v[kx] = load_f4_or_zero(row + (ix0 + kx) * p.xs, x, (unsigned)(ix0 + kx) < (unsigned)p.W);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int ky = ri - r * S;
+      if (ky < 0 || ky > 2) continue;  // compile-time after unrolling
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const float4 ww = wt[ky * 3 + kx];
+        acc[r].x = fmaf(v[kx].x, ww.x, acc[r].x);
+        acc[r].y = fmaf(v[kx].y, ww.y, acc[r].y);
+        acc[r].z = fmaf(v[kx].z, ww.z, acc[r].z);
+        acc[r].w = fmaf(v[kx].w, ww.w, acc[r].w);
+      }
+    }
+  }
+  float* y = (float*)p.y + (size_t)b * p.Ho * p.Wo * p.ys + c0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int oy = oy0 + r;
+    if (oy >= p.Ho) break;
+    const float4 o = make_float4(apply_act(acc[r].x, p.act), apply_act(acc[r].y, p.act), apply_act(acc[r].z, p.act),
+                                 apply_act(acc[r].w, p.act));
+    *(float4*)(y + (size_t)(oy * p.Wo + ox) * p.ys) = o;
+  }
+}
+
+template <int R, int S>
+static void dw_f32_launch(const DwParams& p, hipStream_t s) {
+  const long total = (long)p.B * ((p.Ho + R - 1) / R) * p.Wo * (p.C / 4);
+  if (total <= 0) return;
+  if (total >= (1L << 31) || (long)p.B * p.H * p.W * p.xs >= (1L << 31))
+    throw std::runtime_error("dwconv3x3_f32: too large");
+  hipLaunchKernelGGL((dwconv_f32_kernel<R, S>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+}
+
+void dwconv3x3_f32(const DwParams& p, hipStream_t s) {
+  if (p.C % 4 != 0 || p.xs % 4 != 0 || p.ys % 4 != 0)
+    throw std::runtime_error("dwconv3x3_f32: C, xs, ys must be multiples of 4");
+  if (p.stride == 1)
+    dw_f32_launch<4, 1>(p, s);
+  else if (p.stride == 2)
+    dw_f32_launch<2, 2>(p, s);
+  else
+    throw std::runtime_error("dwconv3x3_f32: stride must be 1 or 2");
+}
+
+// ---------------------------------------------------------------- SPPF (fp32)
+// Cascaded 5x5 stride-1 max pools (== 5/9/13 windows, -inf padding) as two
+// separable passes through LDS; one workgroup = one image x 4 channels.
+constexpr int SPPF_F32_MAX_PIX = 512;  // YOLO: 20x20 = 400
+
+__global__ __launch_bounds__(256) void sppf_f32_kernel(const SppfParams p) {
+  __shared__ float4 in[SPPF_F32_MAX_PIX];
+  __shared__ float4 h5[SPPF_F32_MAX_PIX], h9[SPPF_F32_MAX_PIX], h13[SPPF_F32_MAX_PIX];
+  const int B = live_batch(p.B, p.bdev);
+  const int groups = p.C >> 2;
+  const int b = blockIdx.x / groups;
+  if (b >= B) return;
+  const int c0 = (blockIdx.x - b * groups) * 4;
+  const int H = p.H, W = p.W, HW = H * W;
+  float* buf = (float*)p.buf + (size_t)b * HW * p.xs;
+  for (int i = threadIdx.x; i < HW; i += 256) in[i] = *(const float4*)(buf + (size_t)i * p.xs + c0);
+  __syncthreads();
+  auto mx = [](float4 a, float4 v) {
+    return make_float4(fmaxf(a.x, v.x), fmaxf(a.y, v.y), fmaxf(a.z, v.z), fmaxf(a.w, v.w));
+  };
+  const float4 ninf = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  for (int i = threadIdx.x; i < HW; i += 256) {
+    const int y = i / W, xx = i - y * W;
+    float4 m5 = ninf, m9 = ninf, m13 = ninf;
+#pragma unroll
+    for (int dx = -6; dx <= 6; ++dx) {
+      const int ix = xx + dx;
+      if ((unsigned)ix >= (unsigned)W) continue;
+      const float4 v = in[y * W + ix];
+      const int a = dx < 0 ? -dx : dx;
+      m13 = mx(m13, v);
+      if (a <= 4) m9 = mx(m9, v);
+      if (a <= 2) m5 = mx(m5, v);
+    }
+    h5[i] = m5;
+    h9[i] = m9;
+    h13[i] = m13;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < HW; i += 256) {
+    const int y = i / W, xx = i - y * W;
+    float4 m5 = ninf, m9 = ninf, m13 = ninf;
+#pragma unroll
+    for (int dy = -6; dy <= 6; ++dy) {
+      const int iy = y + dy;
+      if ((unsigned)iy >= (unsigned)H) continue;
+      const int j = iy * W + xx;
+      const int a = dy < 0 ? -dy : dy;
+      m13 = mx(m13, h13[j]);
+      if (a <= 4) m9 = mx(m9, h9[j]);
+      if (a <= 2) m5 = mx(m5, h5[j]);
+    }
+    float* o = buf + (size_t)i * p.xs + c0;
+    *(float4*)(o + p.C) = m5;
+    *(float4*)(o + 2 * p.C) = m9;
+    *(float4*)(o + 3 * p.C) = m13;
+  }
+}
+
+void sppf_pool_f32(const SppfParams& p, hipStream_t s) {
+  if (p.C % 4 != 0 || p.xs < 4 * p.C || p.xs % 4 != 0 || p.H * p.W > SPPF_F32_MAX_PIX)
+    throw std::runtime_error("sppf_pool_f32: bad geometry (C % 4, xs >= 4C, H*W <= 512)");
+  if (p.B <= 0) return;
+  hipLaunchKernelGGL(sppf_f32_kernel, dim3((unsigned)(p.B * (p.C / 4))), dim3(256), 0, s, p);
+}
+
+}  // namespace arena

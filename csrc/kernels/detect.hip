@@ -124,6 +124,15 @@ void sppf_pool(const SppfParams& p, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ decode
+// T = bf16 (default pipeline) or float (exact-fp32 pipeline) head activations.  The fp32 pipeline uses the
+// correctly rounded expf (the reference's torch sigmoid / softmax) instead of the v_exp_f32 approximation.
+template <typename T>
+__device__ __forceinline__ float exp_t(float v) {
+  if constexpr (sizeof(T) == 4) return expf(v);
+  else return __expf(v);
+}
+
+template <typename T>
 __global__ __launch_bounds__(256) void decode_kernel(const DecodeParams p) {
   const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
   const int A0 = p.hw[0] * p.hw[0], A1 = p.hw[1] * p.hw[1], A2 = p.hw[2] * p.hw[2];
@@ -135,7 +144,7 @@ __global__ __launch_bounds__(256) void decode_kernel(const DecodeParams p) {
   int l, r;
   if (a < A0) { l = 0; r = a; } else if (a < A0 + A1) { l = 1; r = a - A0; } else { l = 2; r = a - A0 - A1; }
   const int hw = p.hw[l];
-  const bf16* px = (const bf16*)p.head[l] + ((size_t)b * hw * hw + r) * p.xs[l];
+  const T* px = (const T*)p.head[l] + ((size_t)b * hw * hw + r) * p.xs[l];
 
   // class scores: sigmoid, max + first argmax (ties resolved like np.argmax)
   float best = -1.f;
@@ -143,10 +152,10 @@ __global__ __launch_bounds__(256) void decode_kernel(const DecodeParams p) {
 #pragma unroll
   for (int g = 0; g < 10; ++g) {
     float v[8];
-    unpack8(*(const uint4*)(px + 64 + g * 8), v);
+    load8(px + 64 + g * 8, v);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float sgm = 1.0f / (1.0f + __expf(-v[i]));
+      const float sgm = 1.0f / (1.0f + exp_t<T>(-v[i]));
       if (sgm > best) { best = sgm; cls = g * 8 + i; }
     }
   }
@@ -156,15 +165,15 @@ __global__ __launch_bounds__(256) void decode_kernel(const DecodeParams p) {
 #pragma unroll
   for (int side = 0; side < 4; ++side) {
     float v[16];
-    unpack8(*(const uint4*)(px + side * 16), v);
-    unpack8(*(const uint4*)(px + side * 16 + 8), v + 8);
+    load8(px + side * 16, v);
+    load8(px + side * 16 + 8, v + 8);
     float mx = v[0];
 #pragma unroll
     for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
     float se = 0.f, sw = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float e = __expf(v[i] - mx);
+      const float e = exp_t<T>(v[i] - mx);
       se += e;
       sw += e * (float)i;
     }
@@ -195,7 +204,10 @@ void detect_decode(const DecodeParams& p, hipStream_t s) {
   const long total = A * p.B;
   if (total <= 0) return;
   if (p.cand_cap > 16384) throw std::runtime_error("detect_decode: cand_cap > 16384");
-  hipLaunchKernelGGL(decode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  if (p.f32)
+    hipLaunchKernelGGL(decode_kernel<float>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(decode_kernel<bf16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
 }
 
 // ------------------------------------------------------------------ NMS
@@ -403,6 +415,7 @@ namespace arena {
 // [4 + nc, A] fp32 = (cx, cy, w, h) in letterbox pixels followed by the
 // sigmoid class scores, for all A = 8400 anchors (experiment.yaml:199-207),
 // i.e. what Triton's "yolov5n" model returns to the reference gateway.
+template <typename T>
 __global__ __launch_bounds__(256) void yolo_raw_kernel(const YoloRawParams p) {
   const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
   const int A0 = p.hw[0] * p.hw[0], A1 = p.hw[1] * p.hw[1], A2 = p.hw[2] * p.hw[2];
@@ -414,21 +427,21 @@ __global__ __launch_bounds__(256) void yolo_raw_kernel(const YoloRawParams p) {
   int l, r;
   if (a < A0) { l = 0; r = a; } else if (a < A0 + A1) { l = 1; r = a - A0; } else { l = 2; r = a - A0 - A1; }
   const int hw = p.hw[l];
-  const bf16* px = (const bf16*)p.head[l] + ((size_t)b * hw * hw + r) * p.xs[l];
+  const T* px = (const T*)p.head[l] + ((size_t)b * hw * hw + r) * p.xs[l];
   float* out = (float*)((uint8_t*)p.out + (size_t)b * p.out_stride);
   float dist[4];
 #pragma unroll
   for (int side = 0; side < 4; ++side) {
     float v[16];
-    unpack8(*(const uint4*)(px + side * 16), v);
-    unpack8(*(const uint4*)(px + side * 16 + 8), v + 8);
+    load8(px + side * 16, v);
+    load8(px + side * 16 + 8, v + 8);
     float mx = v[0];
 #pragma unroll
     for (int i = 1; i < 16; ++i) mx = fmaxf(mx, v[i]);
     float se = 0.f, sw = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float e = __expf(v[i] - mx);
+      const float e = exp_t<T>(v[i] - mx);
       se += e;
       sw += e * (float)i;
     }
@@ -443,9 +456,9 @@ __global__ __launch_bounds__(256) void yolo_raw_kernel(const YoloRawParams p) {
   out[3 * A + a] = (y2 - y1) * s;
   for (int g = 0; g < 10; ++g) {
     float v[8];
-    unpack8(*(const uint4*)(px + 64 + g * 8), v);
+    load8(px + 64 + g * 8, v);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) out[(size_t)(4 + g * 8 + i) * A + a] = 1.0f / (1.0f + __expf(-v[i]));
+    for (int i = 0; i < 8; ++i) out[(size_t)(4 + g * 8 + i) * A + a] = 1.0f / (1.0f + exp_t<T>(-v[i]));
   }
 }
 
@@ -454,7 +467,10 @@ void yolo_raw(const YoloRawParams& p, hipStream_t s) {
   if (p.out_stride < (size_t)A * 84 * 4) throw std::runtime_error("yolo_raw: output stride too small");
   const long total = A * p.B;
   if (total <= 0) return;
-  hipLaunchKernelGGL(yolo_raw_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  if (p.f32)
+    hipLaunchKernelGGL(yolo_raw_kernel<float>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(yolo_raw_kernel<bf16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
 }
 
 }  // namespace arena

@@ -55,6 +55,11 @@ void set_conv_v3(bool v);                             // ARENA_CONV_V3=0 falls b
 void set_conv_impl(int v);
 int get_conv_impl();
 
+// Exact-fp32 pipeline (csrc/kernels/conv_f32.hip): the same ConvParams geometry and epilogue with fp32
+// activations, fp32 weights [Cout_pad][Kpad] (Kpad a multiple of 16) and v_mfma_f32_16x16x4_f32 (one
+// rounding per product, fp32 accumulation: the reference's ONNX Runtime fp32 numerics).
+void conv2d_f32(const ConvParams& p, hipStream_t s);
+
 // ---------------------------------------------------------------- depthwise 3x3 (K12)
 struct DwParams {
   const void* x;
@@ -66,6 +71,7 @@ struct DwParams {
   const int* bdev;
 };
 void dwconv3x3(const DwParams& p, hipStream_t s);
+void dwconv3x3_f32(const DwParams& p, hipStream_t s);  // fp32 activations, fp32 weights [9][C]
 
 // ---------------------------------------------------------------- fused inverted residual (K11+K12)
 // MobileNetV2 block: 1x1 expand (+ReLU6) -> 3x3 depthwise stride S (+ReLU6)
@@ -129,6 +135,7 @@ struct SppfParams {
   const int* bdev;
 };
 void sppf_pool(const SppfParams& p, hipStream_t s);
+void sppf_pool_f32(const SppfParams& p, hipStream_t s);  // fp32 buffer
 
 // ---------------------------------------------------------------- image metadata
 // Per-image record produced on the host for a batch (lives in device memory).
@@ -160,6 +167,7 @@ struct LetterboxParams {
   const Ctrl* ctrl;
   void* out;
   int B, T;
+  int f32;  // fp32 output (exact-fp32 pipeline) instead of bf16
 };
 void letterbox_s2d(const LetterboxParams& p, hipStream_t s);
 
@@ -170,6 +178,7 @@ struct TensorInParams {
   const Ctrl* ctrl;
   void* out;
   int B, S;
+  int f32;
 };
 void tensor_in_s2d(const TensorInParams& p, hipStream_t s);
 
@@ -193,6 +202,7 @@ struct DecodeParams {
   int* cand_count;  // [B]
   int cand_cap;
   const Ctrl* ctrl;
+  int f32;  // head activations are fp32
 };
 void detect_decode(const DecodeParams& p, hipStream_t s);
 
@@ -206,6 +216,7 @@ struct YoloRawParams {
   void* out;          // image b at out + b * out_stride
   size_t out_stride;  // bytes
   const Ctrl* ctrl;
+  int f32;
 };
 void yolo_raw(const YoloRawParams& p, hipStream_t s);
 
@@ -262,6 +273,7 @@ struct CropGatherParams {
   void* out;  // [cap, S/2, S/2, 16] bf16 (space-to-depth, ImageNet-normalised)
   int cap, S;
   float mean[3], inv_std[3];
+  int f32;
 };
 void crop_gather_s2d(const CropGatherParams& p, hipStream_t s);
 
@@ -310,8 +322,9 @@ void stem_fused(const StemFusedParams& p, hipStream_t s);
 struct AvgPoolParams {
   const void* x;
   int B, HW, C;
-  void* y;  // bf16 [B][C]
+  void* y;  // [B][C], bf16 (or fp32 with f32)
   const int* bdev;
+  int f32;
 };
 void global_avgpool(const AvgPoolParams& p, hipStream_t s);
 

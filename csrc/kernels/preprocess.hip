@@ -27,6 +27,7 @@ struct LinTap {
 };
 
 __device__ __forceinline__ LinTap lin_tap(int d, float scale, int n) {
+#pragma clang fp contract(off)  // (d + 0.5) * scale - 0.5 rounded twice, as the host computes it
   float fx = ((float)d + 0.5f) * scale - 0.5f;
   int s0 = (int)floorf(fx);
   float f = fx - (float)s0;
@@ -41,6 +42,9 @@ __device__ __forceinline__ LinTap lin_tap(int d, float scale, int n) {
 
 __device__ __forceinline__ void bilinear_rgb(const uint8_t* img, int stride_px, LinTap ty, LinTap tx,
                                              float* rgb) {
+  // separately rounded multiply and add, as the host resize (numpy) computes them: a fused multiply-add
+  // moves values that sit at x.5 to the other side of the uint8 rounding
+#pragma clang fp contract(off)
   const uint8_t* r0 = img + (size_t)ty.i0 * stride_px * 3;
   const uint8_t* r1 = img + (size_t)ty.i1 * stride_px * 3;
 #pragma unroll
@@ -54,6 +58,21 @@ __device__ __forceinline__ void bilinear_rgb(const uint8_t* img, int stride_px, 
   }
 }
 
+// /255 of a uint8 value: the exact-fp32 pipeline divides as the host preprocessor does; the bf16 pipeline
+// multiplies by the reciprocal (the difference is far below its rounding).
+template <typename T>
+__device__ __forceinline__ float div255(float v) {
+  if constexpr (sizeof(T) == 4) return v / 255.0f;
+  else return v * (1.0f / 255.0f);
+}
+
+template <typename T>
+__device__ __forceinline__ void store16(T* dst, const float* v) {
+  store8(dst, v);
+  store8(dst + 8, v + 8);
+}
+
+template <typename T>
 __global__ __launch_bounds__(256) void letterbox_s2d_kernel(const LetterboxParams p) {
   const int T2 = p.T >> 1;
   const int n_img = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
@@ -76,21 +95,24 @@ __global__ __launch_bounds__(256) void letterbox_s2d_kernel(const LetterboxParam
     if (dy >= 0 && dy < m.new_h && dx >= 0 && dx < m.new_w)
       bilinear_rgb(img, m.w, lin_tap(dy, sy, m.h), lin_tap(dx, sx, m.w), rgb);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = rgb[c] * (1.0f / 255.0f);
+    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = div255<T>(rgb[c]);
   }
   out[12] = out[13] = out[14] = out[15] = 0.f;
-  uint4* dst = (uint4*)((bf16*)p.out + (size_t)tid * 16);
-  dst[0] = pack8(out);
-  dst[1] = pack8(out + 8);
+  store16((T*)p.out + (size_t)tid * 16, out);
 }
 
 void letterbox_s2d(const LetterboxParams& p, hipStream_t s) {
   if (p.T % 2 != 0) throw std::runtime_error("letterbox_s2d: T must be even");
   const long total = (long)p.B * (p.T / 2) * (p.T / 2);
   if (total <= 0) return;
-  hipLaunchKernelGGL(letterbox_s2d_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (p.f32)
+    hipLaunchKernelGGL(letterbox_s2d_kernel<float>, grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(letterbox_s2d_kernel<bf16>, grid, dim3(256), 0, s, p);
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void crop_gather_s2d_kernel(const CropGatherParams p) {
   const int S2 = p.S >> 1;
   int n = p.cap;
@@ -116,19 +138,21 @@ __global__ __launch_bounds__(256) void crop_gather_s2d_kernel(const CropGatherPa
     float rgb[3] = {0.f, 0.f, 0.f};
     if (!empty) bilinear_rgb(img, m.w, lin_tap(oy, sy, ch), lin_tap(ox, sx, cw), rgb);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (rgb[c] * (1.0f / 255.0f) - p.mean[c]) * p.inv_std[c];
+    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (div255<T>(rgb[c]) - p.mean[c]) * p.inv_std[c];
   }
   out[12] = out[13] = out[14] = out[15] = 0.f;
-  uint4* dst = (uint4*)((bf16*)p.out + (size_t)tid * 16);
-  dst[0] = pack8(out);
-  dst[1] = pack8(out + 8);
+  store16((T*)p.out + (size_t)tid * 16, out);
 }
 
 void crop_gather_s2d(const CropGatherParams& p, hipStream_t s) {
   if (p.S % 2 != 0) throw std::runtime_error("crop_gather_s2d: S must be even");
   const long total = (long)p.cap * (p.S / 2) * (p.S / 2);
   if (total <= 0) return;
-  hipLaunchKernelGGL(crop_gather_s2d_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (p.f32)
+    hipLaunchKernelGGL(crop_gather_s2d_kernel<float>, grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(crop_gather_s2d_kernel<bf16>, grid, dim3(256), 0, s, p);
 }
 
 }  // namespace arena
@@ -138,7 +162,8 @@ namespace arena {
 // Reference-contract tensor input (KServe "images" / "input": FP32 NCHW
 // [3, S, S], already normalised by the client as in the reference gateway,
 // architectures/triton/gateway/app/pipeline.py:131-139) -> space-to-depth
-// bf16 [S/2, S/2, 16] for the s2d stem convs.
+// [S/2, S/2, 16] (bf16 or fp32) for the s2d stem convs.
+template <typename T>
 __global__ __launch_bounds__(256) void tensor_in_s2d_kernel(const TensorInParams p) {
   const int S2 = p.S >> 1;
   const int n = live_batch(p.B, p.ctrl ? &p.ctrl->n_images : nullptr);
@@ -157,16 +182,18 @@ __global__ __launch_bounds__(256) void tensor_in_s2d_kernel(const TensorInParams
     for (int c = 0; c < 3; ++c) out[pq * 3 + c] = src[c * plane + (size_t)y * p.S + x];
   }
   out[12] = out[13] = out[14] = out[15] = 0.f;
-  uint4* dst = (uint4*)((bf16*)p.out + (size_t)tid * 16);
-  dst[0] = pack8(out);
-  dst[1] = pack8(out + 8);
+  store16((T*)p.out + (size_t)tid * 16, out);
 }
 
 void tensor_in_s2d(const TensorInParams& p, hipStream_t s) {
   if (p.S % 2 != 0) throw std::runtime_error("tensor_in_s2d: S must be even");
   const long total = (long)p.B * (p.S / 2) * (p.S / 2);
   if (total <= 0) return;
-  hipLaunchKernelGGL(tensor_in_s2d_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (p.f32)
+    hipLaunchKernelGGL(tensor_in_s2d_kernel<float>, grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(tensor_in_s2d_kernel<bf16>, grid, dim3(256), 0, s, p);
 }
 
 }  // namespace arena

@@ -270,7 +270,7 @@ void Executor::autotune(Bucket& bk) {
   ARENA_HIP_CHECK(hipEventCreate(&e1));
   const int reps = 3;
   for (size_t i = 0; i < prog_.size(); ++i) {
-    if (prog_[i][0] != OP_CONV) continue;
+    if (prog_[i][0] != OP_CONV || prog_[i][kDtypeField] == 1) continue;  // one fp32 conv kernel family
     if (prog_[i][34] > 0) {  // fused pointwise epilogue: only the v3 halo-tile kernel implements it
       bk.impl[i] = 2;
       continue;
@@ -355,12 +355,17 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
 
   for (size_t oi = 0; oi < prog.size(); ++oi) {
     const OpRecord& r = prog[oi];
+    // field 47: activation precision of the op (0 bf16, 1 exact fp32; planner.OP_DTYPE_FIELD)
+    const bool f32 = r[kDtypeField] == 1;
+    const int eb = f32 ? 4 : 2;
+    if (f32 && (r[0] == OP_IRBLOCK || r[0] == OP_STEMFUSED || r[0] == OP_C3FUSED || r[0] == OP_HEADPOOL))
+      throw std::runtime_error("op " + std::to_string(r[0]) + " has no fp32 kernel");
     switch (r[0]) {
       case OP_CONV: {
         ConvParams p{};
         const size_t gi = (size_t)op_offset + oi;
         p.impl = force_impl ? force_impl : (gi < bk.impl.size() ? bk.impl[gi] : 0);
-        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.x = resolve(bk, sl, r[1], r[2], eb);
         p.xs = (int)r[3];
         p.H = (int)r[4];
         p.W = (int)r[5];
@@ -369,7 +374,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.Kpad = (int)r[8];
         p.bias = (const float*)(W + r[9]);
         p.f32out = (int)r[29];
-        p.y = resolve(bk, sl, r[10], r[11], p.f32out ? 4 : 2);
+        p.y = resolve(bk, sl, r[10], r[11], p.f32out ? 4 : eb);
         p.ys = (int)r[12];
         p.Ho = (int)r[13];
         p.Wo = (int)r[14];
@@ -380,9 +385,9 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.stride = (int)r[19];
         p.pad_t = (int)r[20];
         p.pad_l = (int)r[21];
-        p.res = resolve(bk, sl, r[22], r[23], 2);
+        p.res = resolve(bk, sl, r[22], r[23], eb);
         p.rs = (int)r[24];
-        p.y2 = resolve(bk, sl, r[25], r[26], 2);
+        p.y2 = resolve(bk, sl, r[25], r[26], eb);
         p.y2s = (int)r[27];
         p.act = (int)r[28];
         p.B = batch(r[30]);
@@ -397,19 +402,22 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
           p.pw_act = (int)r[39];
           p.impl = 2;
         }
-        conv2d(p, s);
+        if (f32)
+          conv2d_f32(p, s);
+        else
+          conv2d(p, s);
         break;
       }
       case OP_DWCONV: {
         DwParams p{};
-        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.x = resolve(bk, sl, r[1], r[2], eb);
         p.xs = (int)r[3];
         p.H = (int)r[4];
         p.W = (int)r[5];
         p.C = (int)r[6];
         p.w = W + r[7];
         p.bias = (const float*)(W + r[8]);
-        p.y = resolve(bk, sl, r[9], r[10], 2);
+        p.y = resolve(bk, sl, r[9], r[10], eb);
         p.ys = (int)r[11];
         p.Ho = (int)r[12];
         p.Wo = (int)r[13];
@@ -417,7 +425,10 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.act = (int)r[15];
         p.B = batch(r[16]);
         p.bdev = bdev(r[16]);
-        dwconv3x3(p, s);
+        if (f32)
+          dwconv3x3_f32(p, s);
+        else
+          dwconv3x3(p, s);
         break;
       }
       case OP_IRBLOCK: {
@@ -451,14 +462,17 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       }
       case OP_SPPF: {
         SppfParams p{};
-        p.buf = resolve(bk, sl, r[1], r[2], 2);
+        p.buf = resolve(bk, sl, r[1], r[2], eb);
         p.xs = (int)r[3];
         p.H = (int)r[4];
         p.W = (int)r[5];
         p.C = (int)r[6];
         p.B = batch(r[7]);
         p.bdev = bdev(r[7]);
-        sppf_pool(p, s);
+        if (f32)
+          sppf_pool_f32(p, s);
+        else
+          sppf_pool(p, s);
         break;
       }
       case OP_LETTERBOX: {
@@ -466,9 +480,10 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.pool = pool;
         p.meta = meta;
         p.ctrl = ctrl;
-        p.out = resolve(bk, sl, r[1], 0, 2);
+        p.out = resolve(bk, sl, r[1], 0, eb);
         p.B = B;
         p.T = (int)r[2];
+        p.f32 = f32;
         letterbox_s2d(p, s);
         break;
       }
@@ -481,7 +496,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       case OP_DECODE: {
         DecodeParams p{};
         for (int l = 0; l < 3; ++l) {
-          p.head[l] = resolve(bk, sl, r[1 + 4 * l], r[2 + 4 * l], 2);
+          p.head[l] = resolve(bk, sl, r[1 + 4 * l], r[2 + 4 * l], eb);
           p.xs[l] = (int)r[3 + 4 * l];
           p.hw[l] = (int)r[4 + 4 * l];
           p.stride[l] = (float)r[13 + l];
@@ -492,6 +507,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.cand_cap = cfg_.cand_cap;
         p.B = B;
         p.ctrl = ctrl;
+        p.f32 = f32;
         detect_decode(p, s);
         break;
       }
@@ -530,7 +546,8 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.meta = meta;
         p.crops = (const CropRef*)resolve(bk, sl, r[1], 0, 1);
         p.ctrl = ctrl;
-        p.out = resolve(bk, sl, r[2], 0, 2);
+        p.out = resolve(bk, sl, r[2], 0, eb);
+        p.f32 = f32;
         p.cap = CC;
         p.S = (int)r[3];
         for (int c = 0; c < 3; ++c) {
@@ -631,10 +648,11 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       }
       case OP_AVGPOOL: {
         AvgPoolParams p{};
-        p.x = resolve(bk, sl, r[1], 0, 2);
+        p.x = resolve(bk, sl, r[1], 0, eb);
         p.HW = (int)r[2];
         p.C = (int)r[3];
-        p.y = resolve(bk, sl, r[4], 0, 2);
+        p.y = resolve(bk, sl, r[4], 0, eb);
+        p.f32 = f32;
         p.B = batch(r[5]);
         p.bdev = bdev(r[5]);
         global_avgpool(p, s);
@@ -656,16 +674,17 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.pool = pool;
         p.meta = meta;
         p.ctrl = ctrl;
-        p.out = resolve(bk, sl, r[1], 0, 2);
+        p.out = resolve(bk, sl, r[1], 0, eb);
         p.B = B;
         p.S = (int)r[2];
+        p.f32 = f32;
         tensor_in_s2d(p, s);
         break;
       }
       case OP_YOLORAW: {
         YoloRawParams p{};
         for (int l = 0; l < 3; ++l) {
-          p.head[l] = resolve(bk, sl, r[1 + 4 * l], r[2 + 4 * l], 2);
+          p.head[l] = resolve(bk, sl, r[1 + 4 * l], r[2 + 4 * l], eb);
           p.xs[l] = (int)r[3 + 4 * l];
           p.hw[l] = (int)r[4 + 4 * l];
           p.stride[l] = (float)r[13 + l];
@@ -674,6 +693,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.out = resolve(bk, sl, r[16], 0, 1);
         p.out_stride = (size_t)cfg_.raw_out_bytes;
         p.ctrl = ctrl;
+        p.f32 = f32;
         yolo_raw(p, s);
         break;
       }

@@ -39,6 +39,7 @@
 namespace arena {
 
 constexpr int kOpFields = 48;
+constexpr int kDtypeField = 47;  // per-op activation precision: 0 bf16, 1 exact fp32
 constexpr int kMaxSlots = 6;
 using OpRecord = std::array<int64_t, kOpFields>;
 

@@ -135,7 +135,7 @@ def get_gpu_config() -> dict[str, Any]:
     dflt = {
         "arch": "gfx950",
         "replicas": [1],
-        "dtype": "bf16",
+        "dtype": "fp32",
         "batch_buckets": [1, 2, 4, 8, 16, 32],
         "crop_cap_per_image": 6,
         "max_det": 300,

@@ -9,6 +9,7 @@ detection, the classifier's top-5 (ids, raw logits, softmax probabilities).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -62,6 +63,18 @@ def split_results(res: dict, n: int, gpu_ms: float | None = None) -> list[ImageR
     return out
 
 
+def resolve_dtype(dtype: str | None = None) -> str:
+    """Pipeline precision: the explicit argument, else ``ARENA_DTYPE``, else experiment.yaml ``gpu.dtype``.
+
+    ``fp32`` (default) reproduces the reference's fp32 ONNX Runtime numerics with the exact-fp32 kernels;
+    ``bf16`` selects the tuned bf16 kernels (fp32 accumulation)."""
+    d = dtype or os.environ.get("ARENA_DTYPE") or str(get_gpu_config().get("dtype", "fp32"))
+    d = {"float32": "fp32", "f32": "fp32", "bfloat16": "bf16"}.get(d.lower(), d.lower())
+    if d not in ("fp32", "bf16"):
+        raise ValueError(f"unsupported pipeline dtype {d!r} (fp32 or bf16)")
+    return d
+
+
 class GpuProgramRunner:
     """One native Executor running one program, with a hipGraph per batch bucket.
 
@@ -112,6 +125,10 @@ class GpuProgramRunner:
     def kind(self) -> str:
         return str(self.program.meta.get("kind", "pipeline"))
 
+    @property
+    def dtype(self) -> str:
+        return str(self.program.meta.get("dtype", "bf16"))
+
     def read_buffer(self, name: str, B: int, item: int = 0) -> np.ndarray:
         """Debug: NHWC contents of a planner buffer for one batch item (fp32)."""
         import torch
@@ -139,7 +156,7 @@ class GpuPipeline(GpuProgramRunner):
     def __init__(self, yolo: YOLOv5nu, mnet: MobileNetV2, *, device: int = 0, buckets=None, max_det: int | None = None,
                  crop_cap_per_image: int | None = None, host_threads: int | None = None,
                  max_image_pixels: int = 640 * 640, conf_thr: float | None = None, iou_thr: float | None = None,
-                 weights: np.ndarray | None = None, share_buffers: bool = True):
+                 weights: np.ndarray | None = None, share_buffers: bool = True, dtype: str | None = None):
         gcfg = get_gpu_config()
         ycfg = get_model_config("yolov5n")
         mb = get_controlled_variable("preprocessing", "mobilenet")
@@ -149,7 +166,8 @@ class GpuPipeline(GpuProgramRunner):
         self.iou_thr = float(iou_thr if iou_thr is not None else ycfg["iou_threshold"])
         max_det = int(max_det or gcfg["max_det"])
         program = plan_pipeline(yolo, mnet, conf_thr=self.conf_thr, iou_thr=self.iou_thr, det_size=det_size,
-                                cls_size=cls_size, mean=mb["mean"], std=mb["std"], max_det=max_det)
+                                cls_size=cls_size, mean=mb["mean"], std=mb["std"], max_det=max_det,
+                                dtype=resolve_dtype(dtype))
         super().__init__(program, device=device, buckets=buckets, max_det=max_det,
                          crop_cap_per_image=crop_cap_per_image, host_threads=host_threads,
                          pool_bytes_per_image=int(max_image_pixels) * 3, weights=weights,
@@ -175,13 +193,14 @@ class GpuDetector(GpuProgramRunner):
 
     def __init__(self, yolo: YOLOv5nu, *, device: int = 0, buckets=None, conf_thr: float | None = None,
                  iou_thr: float | None = None, max_det: int | None = None, max_image_pixels: int = 640 * 640,
-                 **kw):
+                 dtype: str | None = None, **kw):
         ycfg = get_model_config("yolov5n")
         det_size = int(get_controlled_variable("preprocessing", "yolo")["target_size"])
         self.conf_thr = float(conf_thr if conf_thr is not None else ycfg["confidence_threshold"])
         self.iou_thr = float(iou_thr if iou_thr is not None else ycfg["iou_threshold"])
         max_det = int(max_det or get_gpu_config()["max_det"])
-        prog = plan_detector(yolo, conf_thr=self.conf_thr, iou_thr=self.iou_thr, det_size=det_size, max_det=max_det)
+        prog = plan_detector(yolo, conf_thr=self.conf_thr, iou_thr=self.iou_thr, det_size=det_size, max_det=max_det,
+                             dtype=resolve_dtype(dtype))
         super().__init__(prog, device=device, buckets=buckets, max_det=max_det,
                          pool_bytes_per_image=int(max_image_pixels) * 3, **kw)
 
@@ -199,9 +218,10 @@ class GpuClassifier(GpuProgramRunner):
     resized to 224 and normalised on the device, then MobileNetV2 + top-5 softmax."""
 
     def __init__(self, mnet: MobileNetV2, *, device: int = 0, buckets=None, max_image_pixels: int = 640 * 640,
-                 **kw):
+                 dtype: str | None = None, **kw):
         mb = get_controlled_variable("preprocessing", "mobilenet")
-        prog = plan_classifier(mnet, cls_size=int(mb["target_size"]), mean=mb["mean"], std=mb["std"])
+        prog = plan_classifier(mnet, cls_size=int(mb["target_size"]), mean=mb["mean"], std=mb["std"],
+                               dtype=resolve_dtype(dtype))
         super().__init__(prog, device=device, buckets=buckets, pool_bytes_per_image=int(max_image_pixels) * 3, **kw)
 
     def infer(self, crops: list[np.ndarray]) -> list[tuple[np.ndarray, np.ndarray, np.ndarray]]:
@@ -230,14 +250,14 @@ class GpuTensorModel(GpuProgramRunner):
         super().__init__(program, device=device, buckets=buckets, pool_bytes_per_image=3 * S * S * 4, **kw)
 
     @classmethod
-    def yolo(cls, yolo: YOLOv5nu, **kw) -> "GpuTensorModel":
+    def yolo(cls, yolo: YOLOv5nu, dtype: str | None = None, **kw) -> "GpuTensorModel":
         det_size = int(get_controlled_variable("preprocessing", "yolo")["target_size"])
-        return cls(plan_yolo_raw(yolo, det_size=det_size), **kw)
+        return cls(plan_yolo_raw(yolo, det_size=det_size, dtype=resolve_dtype(dtype)), **kw)
 
     @classmethod
-    def mobilenet(cls, mnet: MobileNetV2, **kw) -> "GpuTensorModel":
+    def mobilenet(cls, mnet: MobileNetV2, dtype: str | None = None, **kw) -> "GpuTensorModel":
         cls_size = int(get_controlled_variable("preprocessing", "mobilenet")["target_size"])
-        return cls(plan_mobilenet_raw(mnet, cls_size=cls_size), **kw)
+        return cls(plan_mobilenet_raw(mnet, cls_size=cls_size, dtype=resolve_dtype(dtype)), **kw)
 
     def infer(self, tensors) -> np.ndarray:
         """``tensors``: float32 [N, 3, S, S] (or a list of [3, S, S]); returns float32 [N, *output_shape]."""

@@ -50,6 +50,13 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   HEADPOOL 1 x_buf 2 x_coff 3 x_cs 4 HW 5 K 6 w_off 7 Kpad 8 b_off 9 N 10 Npad 11 y_buf 12 y_coff 13 y_cs
            14 act 15 batch_kind
            (MobileNetV2 head 1x1 conv + activation + global average pool, csrc/kernels/head_pool.hip)
+
+Every record: field 47 (``OP_DTYPE_FIELD``) = activation precision of the op, 0 = bf16 activations and
+weights with fp32 accumulation (the tuned fused kernels), 1 = exact fp32 (fp32 activations and weights,
+v_mfma_f32_16x16x4_f32; csrc/kernels/conv_f32.hip) — the reference's ONNX Runtime precision
+(reference experiment.yaml:202,207,220,225).  fp32 programs use the unfused op set (CONV, DWCONV, SPPF,
+LETTERBOX, DECODE, CROPGATHER, AVGPOOL, TENSORIN, YOLORAW + the dtype-free NMS / CROPPLAN / TOPK / ZERO);
+their conv weights are fp32 [Cout_pad][Kpad] with Kpad a multiple of 16.
 """
 from __future__ import annotations
 
@@ -60,6 +67,8 @@ import numpy as np
 import torch
 
 OP_FIELDS = 48
+OP_DTYPE_FIELD = 47
+DTYPES = ("bf16", "fp32")
 (OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
  OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL) = range(1, 18)
 BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK, BUF_RAWOUT = -1, -10, -11, -12, -13, -14, -15, -16
@@ -135,17 +144,24 @@ def bf16_bytes(t: torch.Tensor) -> bytes:
     return t.detach().float().contiguous().to(torch.bfloat16).view(torch.int16).numpy().tobytes()
 
 
-def pack_conv_weight(w: torch.Tensor, b: torch.Tensor) -> tuple[bytes, bytes, int, int]:
-    """[Cout, Cin, KH, KW] fp32 -> ([Cout_pad][Kpad] bf16 bytes, bias fp32 bytes, Kpad, Cout_pad)."""
+def f32_bytes(t: torch.Tensor) -> bytes:
+    return t.detach().float().contiguous().numpy().tobytes()
+
+
+def pack_conv_weight(w: torch.Tensor, b: torch.Tensor, dtype: str = "bf16") -> tuple[bytes, bytes, int, int]:
+    """[Cout, Cin, KH, KW] fp32 -> ([Cout_pad][Kpad] weight bytes, bias fp32 bytes, Kpad, Cout_pad).
+
+    bf16: Kpad a multiple of 32 (one v_mfma_f32_16x16x32_bf16 K-step); fp32: fp32 weights, Kpad a
+    multiple of 16 (four v_mfma_f32_16x16x4_f32 steps)."""
     cout, cin, kh, kw = w.shape
     k = kh * kw * cin
-    kpad = _round(k, 32)
+    kpad = _round(k, 16 if dtype == "fp32" else 32)
     cpad = _round(cout, 16)
     wk = torch.zeros(cpad, kpad, dtype=torch.float32)
-    wk[:cout, :k] = w.permute(0, 2, 3, 1).reshape(cout, k)
+    wk[:cout, :k] = w.detach().float().permute(0, 2, 3, 1).reshape(cout, k)
     bb = torch.zeros(cpad, dtype=torch.float32)
-    bb[:cout] = b
-    return bf16_bytes(wk), bb.numpy().tobytes(), kpad, cpad
+    bb[:cout] = b.detach().float()
+    return (f32_bytes(wk) if dtype == "fp32" else bf16_bytes(wk)), bb.numpy().tobytes(), kpad, cpad
 
 
 def pack_ir_weights(expand, dw, project, inp: int) -> dict:
@@ -177,15 +193,25 @@ def pack_ir_weights(expand, dw, project, inp: int) -> dict:
 
 
 class ProgramBuilder:
-    def __init__(self) -> None:
+    def __init__(self, dtype: str = "bf16") -> None:
+        if dtype not in DTYPES:
+            raise ValueError(f"dtype must be one of {DTYPES}, got {dtype!r}")
+        self.dtype = dtype
+        self.f32 = dtype == "fp32"
+        self.elem = 4 if self.f32 else 2
         self.buffers: list[Buffer] = []
         self.ops: list[list[int]] = []
         self.cls_start: int | None = None
         self.weights = WeightPacker()
-        self.meta: dict = {}
+        self.meta: dict = {"dtype": dtype}
+
+    def _bf16_only(self, what: str) -> None:
+        if self.f32:
+            raise ValueError(f"{what} is a bf16-only fused kernel; fp32 programs use the unfused ops")
 
     # ------------------------------------------------------------ buffers
-    def tensor(self, name: str, H: int, W: int, C: int, kind: int = IMAGES, elem: int = 2) -> Buffer:
+    def tensor(self, name: str, H: int, W: int, C: int, kind: int = IMAGES, elem: int | None = None) -> Buffer:
+        elem = self.elem if elem is None else elem
         if C % 8:
             raise ValueError(f"{name}: channel count {C} must be a multiple of 8")
         b = Buffer(len(self.buffers), name, _round(H * W * C * elem, 16), kind, H, W, C, elem)
@@ -209,7 +235,10 @@ class ProgramBuilder:
 
     def _emit(self, rec: list[int], *touch) -> None:
         self._touch(*touch)
+        if len(rec) > OP_DTYPE_FIELD:
+            raise ValueError("op record overlaps the dtype field")
         r = list(rec) + [0] * (OP_FIELDS - len(rec))
+        r[OP_DTYPE_FIELD] = int(self.f32)
         self.ops.append(r)
 
     def begin_classifier(self) -> None:
@@ -240,7 +269,7 @@ class ProgramBuilder:
             Wo = (W + 2 * pad[1] - kw) // stride + 1
         else:
             Ho, Wo = out_hw
-        wb, bb, kpad, cpad = pack_conv_weight(w, b)
+        wb, bb, kpad, cpad = pack_conv_weight(w, b, self.dtype)
         w_off = self.weights.add(wb)
         b_off = self.weights.add(bb)
         rec = [OP_CONV, src.bid, src.coff, src.cs, H, W, cin, w_off, kpad, b_off,
@@ -250,6 +279,7 @@ class ProgramBuilder:
                ACT[act], int(f32out), kind]
         pw_dst = None
         if pw is not None:
+            self._bf16_only("conv with a fused pointwise epilogue")
             w2, b2, pw_dst, act2 = pw
             co2, ci2 = w2.shape[0], w2.shape[1]
             if ci2 != cout or w2.shape[2:] != (1, 1) or co2 != pw_dst.C:
@@ -266,8 +296,8 @@ class ProgramBuilder:
             raise ValueError("dwconv: expects [C,1,3,3] weights matching the views")
         H, W = src.buf.H, src.buf.W
         Ho, Wo = (H + 2 - 3) // stride + 1, (W + 2 - 3) // stride + 1
-        wt = w.reshape(C, 9).t().contiguous()  # [9][C]
-        w_off = self.weights.add(bf16_bytes(wt))
+        wt = w.detach().float().reshape(C, 9).t().contiguous()  # [9][C]
+        w_off = self.weights.add(f32_bytes(wt) if self.f32 else bf16_bytes(wt))
         b_off = self.weights.add(b.detach().float().numpy().tobytes())
         rec = [OP_DWCONV, src.bid, src.coff, src.cs, H, W, C, w_off, b_off, dst.bid, dst.coff, dst.cs,
                Ho, Wo, stride, ACT[act], kind]
@@ -277,6 +307,7 @@ class ProgramBuilder:
                  kind: int = CROPS) -> None:
         """Fused inverted residual: ``expand`` = (w [hid,inp,1,1], b) or None (t = 1 blocks),
         ``dw`` = (w [hid,1,3,3], b), ``project`` = (w [oup,hid,1,1], b); BN already folded."""
+        self._bf16_only("ir_block")
         if dst.C != project[0].shape[0]:
             raise ValueError(f"ir_block: destination C {dst.C} != oup {project[0].shape[0]}")
         pk = pack_ir_weights(expand, dw, project, src.C)
@@ -301,6 +332,7 @@ class ProgramBuilder:
                  res: bool, kind: int = IMAGES) -> None:
         """A whole C3 block as one op: ``cv12`` = (w, b) of cv1|cv2 stacked [2CH, C1, 1, 1]; ``bottlenecks`` =
         [((w1, b1), (w2, b2)), ...] with w1 [CH, CH, 1, 1], w2 [CH, CH, 3, 3]; ``cv3`` = (w, b) [2CH, 2CH, 1, 1]."""
+        self._bf16_only("c3_fused")
         w12, b12 = cv12
         ch2, c1 = w12.shape[0], w12.shape[1]
         CH, NB = ch2 // 2, len(bottlenecks)
@@ -331,6 +363,7 @@ class ProgramBuilder:
         kernel on the stem output kept in LDS; ``dst`` is then that conv's output (S/4 x S/4).
         ``ir=(dw, project)`` (classifier only): MobileNetV2 block 1 (t = 1, 32 -> 16, stride 1, no
         residual) runs on the stem output in LDS; ``dst`` is then the block's output (S/2 x S/2 x 16)."""
+        self._bf16_only("stem_fused")
         cout, cin, ks, ks2 = w.shape
         if cin != 16 or ks != ks2:
             raise ValueError("stem_fused: weights must be [Cout, 16, KS, KS]")
@@ -402,6 +435,7 @@ class ProgramBuilder:
     def head_pool(self, src: View, dst: View, w: torch.Tensor, b: torch.Tensor, *, act: str | None = "relu6",
                   kind: int = CROPS) -> None:
         """1x1 conv + activation + global average pool in one kernel: ``dst`` is a 1x1 map."""
+        self._bf16_only("head_pool")
         cout, cin, kh, kw = w.shape
         if (kh, kw) != (1, 1) or cin != src.C or cout != dst.C or dst.buf.H * dst.buf.W != 1:
             raise ValueError("head_pool: expects 1x1 weights [N, C, 1, 1] and a 1x1 destination")

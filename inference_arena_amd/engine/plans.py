@@ -22,6 +22,11 @@ Lowering rules (what replaces ONNX graph nodes):
     3x3/s1 conv over 12(+4) channels, MobileNet's 3x3/s2 conv a 2x2/s1 conv.
   * With ``ARENA_FUSE_STEM`` (default) the letterbox / crop gather is fused
     into those stem convs (stem_fused op): the s2d input only exists in LDS.
+
+Precision (``dtype``): ``"bf16"`` lowers onto the tuned bf16 kernels and every
+fusion above; ``"fp32"`` lowers onto the exact-fp32 kernels (fp32 activations
+and weights, fp32 MFMA; csrc/kernels/conv_f32.hip) with the unfused op set —
+the reference's numerics (ONNX Runtime fp32, reference experiment.yaml:202-225).
 """
 from __future__ import annotations
 
@@ -81,7 +86,7 @@ def fuse_c3_policy() -> str:
 def _c3(pb: ProgramBuilder, m, src: View, dst: View, H: int, W: int, name: str) -> None:
     c_ = m.c_
     res = bool(m.m[0].add)
-    policy = fuse_c3_policy()
+    policy = fuse_c3_policy() if not pb.f32 else "none"
     allowed = C3_FUSED if policy == "all" else C3_FUSED_AUTO if policy == "auto" else set()
     if ((src.C, c_, len(m.m), res) in allowed and H % 8 == 0 and W % 16 == 0
             and all(bool(bn.add) == res for bn in m.m)):
@@ -133,6 +138,7 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
     w, b = fold(y.b0)
     if fuse_stem is None:
         fuse_stem = fuse_stem_default()
+    fuse_stem = fuse_stem and not pb.f32
     A1 = pb.tensor("b1", h // 2, h // 2, 32)
     if fuse_stem and not tensor_input and fuse_stem2_default() and T % 64 == 0:
         # letterbox + stem + b1 (3x3 s2) in one kernel: the 320x320x16 stem output stays in LDS
@@ -191,7 +197,7 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
 
     d = y.detect
     c2, c3, nc = d.c2, d.c3, d.nc
-    fuse_head = os.environ.get("ARENA_FUSE_HEAD", "1").lower() not in ("0", "false", "no", "off")
+    fuse_head = os.environ.get("ARENA_FUSE_HEAD", "1").lower() not in ("0", "false", "no", "off") and not pb.f32
     ch = c2 + c3
     heads = []
     for lvl, (P, cin, s) in enumerate(((P3, 64, s8), (P4, 128, s16), (P5, 256, s32))):
@@ -259,6 +265,8 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
     h = S // 2
     if fuse_stem is None:
         fuse_stem = fuse_stem_default()
+    if pb.f32:  # the fused MobileNet kernels are bf16-only
+        fuse_ir, fuse_stem = "none", False
     w, b = fold(m.stem)
     b0 = m.blocks[0]
     first_fused = (fuse_stem and crops is not None and fuse_stem_ir_default() and S % 32 == 0
@@ -308,7 +316,7 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
                 res=View(cur, 0, blk.inp) if blk.use_res else None, kind=CROPS_)
         cur, H = O, Ho
     PO = pb.tensor("m.pool", 1, 1, 1280, kind=CROPS_)
-    if fuse_head_pool_default() and H * H <= 64 and cur.C == 320:
+    if fuse_head_pool_default() and not pb.f32 and H * H <= 64 and cur.C == 320:
         pb.head_pool(View(cur, 0, cur.C), View(PO, 0, 1280), *fold(m.head), act="relu6", kind=CROPS_)
     else:
         HD = pb.tensor("m.head", H, H, 1280, kind=CROPS_)
@@ -328,8 +336,8 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
 
 def plan_pipeline(yolo: YOLOv5nu, mnet: MobileNetV2, *, conf_thr: float, iou_thr: float, det_size: int = 640,
                   cls_size: int = 224, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225),
-                  cand_cap: int = 8400, max_det: int = 300) -> Program:
-    pb = ProgramBuilder()
+                  cand_cap: int = 8400, max_det: int = 300, dtype: str = "bf16") -> Program:
+    pb = ProgramBuilder(dtype)
     heads = plan_yolo(pb, yolo, det_size)
     cand = pb.raw("cand", cand_cap * CAND_BYTES)
     count = pb.raw("cand_count", 4)
@@ -348,9 +356,9 @@ __all__ = ["plan_pipeline", "plan_detector", "plan_classifier", "plan_yolo_raw",
 
 
 def plan_detector(yolo: YOLOv5nu, *, conf_thr: float, iou_thr: float, det_size: int = 640, cand_cap: int = 8400,
-                  max_det: int = 300) -> Program:
+                  max_det: int = 300, dtype: str = "bf16") -> Program:
     """Detection only (microservices detection service): detections per image."""
-    pb = ProgramBuilder()
+    pb = ProgramBuilder(dtype)
     heads = plan_yolo(pb, yolo, det_size)
     cand = pb.raw("cand", cand_cap * CAND_BYTES)
     count = pb.raw("cand_count", 4)
@@ -362,9 +370,9 @@ def plan_detector(yolo: YOLOv5nu, *, conf_thr: float, iou_thr: float, det_size: 
 
 
 def plan_classifier(mnet: MobileNetV2, *, cls_size: int = 224, mean=(0.485, 0.456, 0.406),
-                    std=(0.229, 0.224, 0.225), max_det: int = 300) -> Program:
+                    std=(0.229, 0.224, 0.225), max_det: int = 300, dtype: str = "bf16") -> Program:
     """Classification only (microservices classification service): every input image is one crop."""
-    pb = ProgramBuilder()
+    pb = ProgramBuilder(dtype)
     crops = pb.raw("crops", max_det * CROPREF_BYTES, pinned=True)
     pb.crop_plan(crops, whole=True)
     pb.begin_classifier()
@@ -372,9 +380,9 @@ def plan_classifier(mnet: MobileNetV2, *, cls_size: int = 224, mean=(0.485, 0.45
     return pb.build({"kind": "classifier", "cls_size": cls_size, "max_det": max_det})
 
 
-def plan_yolo_raw(yolo: YOLOv5nu, *, det_size: int = 640) -> Program:
+def plan_yolo_raw(yolo: YOLOv5nu, *, det_size: int = 640, dtype: str = "bf16") -> Program:
     """Reference tensor contract of model 'yolov5n': fp32 [3,640,640] -> fp32 [84, 8400]."""
-    pb = ProgramBuilder()
+    pb = ProgramBuilder(dtype)
     heads = plan_yolo(pb, yolo, det_size, tensor_input=True)
     pb.yolo_raw(heads, STRIDES)
     A = sum((det_size // s) ** 2 for s in STRIDES)
@@ -382,9 +390,9 @@ def plan_yolo_raw(yolo: YOLOv5nu, *, det_size: int = 640) -> Program:
                      "output_shape": [84, A]})
 
 
-def plan_mobilenet_raw(mnet: MobileNetV2, *, cls_size: int = 224) -> Program:
+def plan_mobilenet_raw(mnet: MobileNetV2, *, cls_size: int = 224, dtype: str = "bf16") -> Program:
     """Reference tensor contract of model 'mobilenetv2': fp32 [3,224,224] -> fp32 [1000]."""
-    pb = ProgramBuilder()
+    pb = ProgramBuilder(dtype)
     plan_mobilenet(pb, mnet, None, cls_size, None, None, kind=IMAGES, raw_logits=True)
     n = mnet.fc.out_features
     return pb.build({"kind": "mobilenet_raw", "cls_size": cls_size, "raw_out_bytes": n * 4, "output_shape": [n]})

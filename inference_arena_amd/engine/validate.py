@@ -34,6 +34,7 @@ from ..engine.planner import (
     OP_TOPK,
     OP_YOLORAW,
     OP_ZERO,
+    OP_DTYPE_FIELD,
     Program,
 )
 
@@ -79,22 +80,31 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         if off < 0 or off + n > wbytes:
             raise ProgramError(f"op {i}: {what} reads weights [{off}, {off + n}) of {wbytes}")
 
+    fused = (OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL)
     for i, r in enumerate(prog.ops):
         op = int(r[0])
         kind_n = lambda k: crop_cap if int(k) == CROPS else B  # noqa: E731
+        f32 = int(r[OP_DTYPE_FIELD]) == 1
+        if int(r[OP_DTYPE_FIELD]) not in (0, 1):
+            raise ProgramError(f"op {i}: bad dtype field {int(r[OP_DTYPE_FIELD])}")
+        if f32 and op in fused:
+            raise ProgramError(f"op {i}: fused op {op} has no fp32 kernel")
+        el = 4 if f32 else 2  # activation bytes
         if op == OP_CONV:
             n = kind_n(r[30])
             H, W, Cin, Ho, Wo, Cout, Cpad, KH, KW = (int(v) for v in (r[4], r[5], r[6], r[13], r[14], r[15], r[16],
                                                                       r[17], r[18]))
             kpad = int(r[8])
-            if kpad < KH * KW * Cin or kpad % 32 or Cpad % 16 or Cout > Cpad:
+            if kpad < KH * KW * Cin or kpad % (16 if f32 else 32) or Cpad % 16 or Cout > Cpad:
                 raise ProgramError(f"op {i}: bad conv geometry")
-            view(i, r[1], int(r[2]), int(r[3]), n * H * W, Cin, 2, "conv input")
-            oel = 4 if int(r[29]) else 2
+            if f32 and (Cin < 16 or Cin % 4 or int(r[34]) > 0):
+                raise ProgramError(f"op {i}: unsupported fp32 conv geometry")
+            view(i, r[1], int(r[2]), int(r[3]), n * H * W, Cin, el, "conv input")
+            oel = 4 if int(r[29]) else el
             view(i, r[10], int(r[11]), int(r[12]), n * Ho * Wo, Cout, oel, "conv output")
-            view(i, r[22], int(r[23]), int(r[24]), n * Ho * Wo, Cout, 2, "conv residual")
-            view(i, r[25], int(r[26]), int(r[27]), n * 4 * Ho * Wo, Cout, 2, "conv upsampled output")
-            weights(i, int(r[7]), Cpad * kpad * 2, "conv weight")
+            view(i, r[22], int(r[23]), int(r[24]), n * Ho * Wo, Cout, el, "conv residual")
+            view(i, r[25], int(r[26]), int(r[27]), n * 4 * Ho * Wo, Cout, el, "conv upsampled output")
+            weights(i, int(r[7]), Cpad * kpad * el, "conv weight")
             weights(i, int(r[9]), Cpad * 4, "conv bias")
             if int(r[34]) > 0:  # fused pointwise epilogue
                 co2, kpad2, cpad2 = int(r[34]), int(r[32]), int(r[35])
@@ -107,9 +117,9 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         elif op == OP_DWCONV:
             n = kind_n(r[16])
             H, W, C, Ho, Wo = (int(v) for v in (r[4], r[5], r[6], r[12], r[13]))
-            view(i, r[1], int(r[2]), int(r[3]), n * H * W, C, 2, "dw input")
-            view(i, r[9], int(r[10]), int(r[11]), n * Ho * Wo, C, 2, "dw output")
-            weights(i, int(r[7]), 9 * C * 2, "dw weight")
+            view(i, r[1], int(r[2]), int(r[3]), n * H * W, C, el, "dw input")
+            view(i, r[9], int(r[10]), int(r[11]), n * Ho * Wo, C, el, "dw output")
+            weights(i, int(r[7]), 9 * C * el, "dw weight")
             weights(i, int(r[8]), C * 4, "dw bias")
         elif op == OP_IRBLOCK:
             n = kind_n(r[25])
@@ -131,10 +141,12 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             weights(i, int(r[19]), oup_pad * 4, "ir project bias")
         elif op == OP_SPPF:
             n = kind_n(r[7])
-            view(i, r[1], int(r[2]), int(r[3]), n * int(r[4]) * int(r[5]), 4 * int(r[6]), 2, "sppf buffer")
+            if f32 and int(r[4]) * int(r[5]) > 512:
+                raise ProgramError(f"op {i}: fp32 SPPF supports H*W <= 512")
+            view(i, r[1], int(r[2]), int(r[3]), n * int(r[4]) * int(r[5]), 4 * int(r[6]), el, "sppf buffer")
         elif op == OP_LETTERBOX:
             T2 = int(r[2]) // 2
-            need(i, r[1], 0, B * T2 * T2 * 32, "letterbox output")
+            need(i, r[1], 0, B * T2 * T2 * 16 * el, "letterbox output")
         elif op == OP_C3FUSED:
             n = kind_n(r[25])
             H, W, C1, CH, NB, res = (int(v) for v in r[4:10])
@@ -183,7 +195,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         elif op == OP_DECODE:
             for lvl in range(3):
                 buf, coff, cs, hw = (int(v) for v in r[1 + 4 * lvl: 5 + 4 * lvl])
-                view(i, buf, coff, cs, B * hw * hw, 144, 2, f"decode head {lvl}")
+                view(i, buf, coff, cs, B * hw * hw, 144, el, f"decode head {lvl}")
             need(i, r[16], 0, B * cand_cap * CAND_BYTES, "candidates")
             need(i, r[17], 0, B * 4, "candidate counts")
         elif op == OP_NMS:
@@ -194,7 +206,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         elif op == OP_CROPGATHER:
             S2 = int(r[3]) // 2
             need(i, r[1], 0, B * max_det * CROP_BYTES, "crop refs")
-            need(i, r[2], 0, crop_cap * S2 * S2 * 32, "crop gather output")
+            need(i, r[2], 0, crop_cap * S2 * S2 * 16 * el, "crop gather output")
         elif op == OP_HEADPOOL:
             n = kind_n(r[15])
             HW, K, Kpad, N, Npad = int(r[4]), int(r[5]), int(r[7]), int(r[9]), int(r[10])
@@ -206,19 +218,19 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             view(i, r[11], int(r[12]), int(r[13]), n, N, 2, "head_pool output")
         elif op == OP_AVGPOOL:
             n = kind_n(r[5])
-            need(i, r[1], 0, n * int(r[2]) * int(r[3]) * 2, "avgpool input")
-            need(i, r[4], 0, n * int(r[3]) * 2, "avgpool output")
+            need(i, r[1], 0, n * int(r[2]) * int(r[3]) * el, "avgpool input")
+            need(i, r[4], 0, n * int(r[3]) * el, "avgpool output")
         elif op == OP_TOPK:
             need(i, r[1], 0, crop_cap * int(r[3]) * 4, "topk logits")
             need(i, r[4], 0, B * max_det * TOPK_BYTES, "topk results")
         elif op == OP_TENSORIN:
             S2 = int(r[2]) // 2
-            need(i, r[1], 0, B * S2 * S2 * 32, "tensor input output")
+            need(i, r[1], 0, B * S2 * S2 * 16 * el, "tensor input output")
         elif op == OP_YOLORAW:
             A = 0
             for lvl in range(3):
                 buf, coff, cs, hw = (int(v) for v in r[1 + 4 * lvl: 5 + 4 * lvl])
-                view(i, buf, coff, cs, B * hw * hw, 144, 2, f"raw head {lvl}")
+                view(i, buf, coff, cs, B * hw * hw, 144, el, f"raw head {lvl}")
                 A += hw * hw
             if int(r[16]) != BUF_RAWOUT or 84 * A * 4 > raw:
                 raise ProgramError(f"op {i}: raw output needs {84 * A * 4} bytes per image, have {raw}")

@@ -2,8 +2,9 @@
 
 These call the same launchers the executor uses, on the current torch stream,
 so every kernel can be tested against a PyTorch fp32 reference op and used
-outside the executor.  Activations are NHWC bf16 tensors; a "view" into a
-concat buffer is passed as the buffer plus a channel offset.
+outside the executor.  Activations are NHWC tensors — bf16 for the tuned bf16
+kernels, float32 for the exact-fp32 kernels (selected by the input dtype); a
+"view" into a concat buffer is passed as the buffer plus a channel offset.
 """
 from __future__ import annotations
 
@@ -29,9 +30,9 @@ def _ptr(t: torch.Tensor | None, elem_off: int = 0) -> int:
     return t.data_ptr() + elem_off * t.element_size()
 
 
-def pack_weights(w: torch.Tensor, b: torch.Tensor, device) -> tuple[torch.Tensor, torch.Tensor, int, int]:
-    wb, bb, kpad, cpad = pack_conv_weight(w.detach().cpu().float(), b.detach().cpu().float())
-    wt = torch.frombuffer(bytearray(wb), dtype=torch.bfloat16).to(device)
+def pack_weights(w: torch.Tensor, b: torch.Tensor, device, dtype: str = "bf16") -> tuple[torch.Tensor, torch.Tensor, int, int]:
+    wb, bb, kpad, cpad = pack_conv_weight(w.detach().cpu().float(), b.detach().cpu().float(), dtype)
+    wt = torch.frombuffer(bytearray(wb), dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(device)
     bt = torch.frombuffer(bytearray(bb), dtype=torch.float32).to(device)
     return wt, bt, kpad, cpad
 
@@ -43,8 +44,10 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
                 packed=None) -> torch.Tensor:
     """NHWC conv with fused bias/act/residual/upsampled copy.
 
-    x: [B, H, W, Cx] bf16 (reads channels [x_coff, x_coff + Cin)); w: [Cout, Cin, KH, KW] fp32.
+    x: [B, H, W, Cx] bf16 or float32 (reads channels [x_coff, x_coff + Cin)); w: [Cout, Cin, KH, KW] fp32.
+    A float32 ``x`` runs the exact-fp32 kernel (fp32 weights, v_mfma_f32_16x16x4_f32, fp32 output).
     """
+    f32 = x.dtype == torch.float32
     B, H, W, Cx = x.shape
     cout, cin_w, kh, kw = w.shape
     cin = cin or cin_w
@@ -58,8 +61,8 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
     else:
         Ho, Wo = out_hw
     if out is None:
-        out = torch.empty(B, Ho, Wo, cout, dtype=torch.float32 if f32out else torch.bfloat16, device=x.device)
-    wt, bt, kpad, cpad = packed if packed is not None else pack_weights(w, b, x.device)
+        out = torch.empty(B, Ho, Wo, cout, dtype=torch.float32 if (f32out or f32) else torch.bfloat16, device=x.device)
+    wt, bt, kpad, cpad = packed if packed is not None else pack_weights(w, b, x.device, "fp32" if f32 else "bf16")
     native().conv2d({
         "x": _ptr(x, x_coff), "B": B, "H": H, "W": W, "xs": Cx, "Cin": cin,
         "w": _ptr(wt), "Kpad": kpad, "bias": _ptr(bt),
@@ -67,7 +70,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
         "KH": kh, "KW": kw, "stride": stride, "pad_t": pad[0], "pad_l": pad[1],
         "res": _ptr(res, res_coff), "rs": res.shape[-1] if res is not None else 0,
         "y2": _ptr(out2, out2_coff), "y2s": out2.shape[-1] if out2 is not None else 0,
-        "act": ACT[act], "f32out": int(f32out), "bdev": _ptr(bdev), "stream": _stream(),
+        "act": ACT[act], "f32out": int(f32out), "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32),
     })
     return out
 
@@ -75,13 +78,14 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
 def dwconv3x3_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: int = 1, act="relu6",
                    bdev: torch.Tensor | None = None) -> torch.Tensor:
     B, H, W, C = x.shape
+    f32 = x.dtype == torch.float32
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
-    y = torch.empty(B, Ho, Wo, C, dtype=torch.bfloat16, device=x.device)
-    wt = w.detach().float().reshape(C, 9).t().contiguous().to(torch.bfloat16).to(x.device)
+    y = torch.empty(B, Ho, Wo, C, dtype=x.dtype, device=x.device)
+    wt = w.detach().float().reshape(C, 9).t().contiguous().to(x.dtype).to(x.device)
     bt = b.detach().float().contiguous().to(x.device)
     native().dwconv3x3({"x": _ptr(x), "B": B, "H": H, "W": W, "xs": C, "C": C, "w": _ptr(wt), "bias": _ptr(bt),
                         "y": _ptr(y), "Ho": Ho, "Wo": Wo, "ys": C, "stride": stride, "act": ACT[act],
-                        "bdev": _ptr(bdev), "stream": _stream()})
+                        "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32)})
     return y
 
 
@@ -109,7 +113,8 @@ def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: boo
 def sppf_nhwc(buf: torch.Tensor, C: int) -> torch.Tensor:
     """In place: buf[..., C:4C] = cascaded 5x5 max pools of buf[..., :C]."""
     B, H, W, Ct = buf.shape
-    native().sppf_pool({"buf": _ptr(buf), "B": B, "H": H, "W": W, "xs": Ct, "C": C, "stream": _stream()})
+    native().sppf_pool({"buf": _ptr(buf), "B": B, "H": H, "W": W, "xs": Ct, "C": C, "stream": _stream(),
+                        "f32": int(buf.dtype == torch.float32)})
     return buf
 
 
@@ -135,14 +140,14 @@ def ctrl_tensor(n_images: int, device, n_crops: int = 0, crop_base: int = 0) -> 
     return c.to(device)
 
 
-def letterbox_s2d(images: list[np.ndarray], T: int, device) -> torch.Tensor:
+def letterbox_s2d(images: list[np.ndarray], T: int, device, dtype=torch.bfloat16) -> torch.Tensor:
     meta, pool = image_meta_bytes(images, T)
     meta_t = torch.frombuffer(bytearray(meta), dtype=torch.uint8).to(device)
     pool_t = torch.from_numpy(pool.copy()).to(device)
     ctrl = ctrl_tensor(len(images), device)
-    out = torch.empty(len(images), T // 2, T // 2, 16, dtype=torch.bfloat16, device=device)
+    out = torch.empty(len(images), T // 2, T // 2, 16, dtype=dtype, device=device)
     native().letterbox_s2d({"pool": _ptr(pool_t), "meta": _ptr(meta_t), "ctrl": _ptr(ctrl), "out": _ptr(out),
-                            "B": len(images), "T": T, "stream": _stream()})
+                            "B": len(images), "T": T, "stream": _stream(), "f32": int(dtype == torch.float32)})
     torch.cuda.current_stream().synchronize()
     return out
 
@@ -156,8 +161,9 @@ def s2d_to_nchw(x: torch.Tensor) -> torch.Tensor:
 
 def avgpool_nhwc(x: torch.Tensor) -> torch.Tensor:
     B, H, W, C = x.shape
-    y = torch.empty(B, C, dtype=torch.bfloat16, device=x.device)
-    native().global_avgpool({"x": _ptr(x), "B": B, "HW": H * W, "C": C, "y": _ptr(y), "stream": _stream()})
+    y = torch.empty(B, C, dtype=x.dtype, device=x.device)
+    native().global_avgpool({"x": _ptr(x), "B": B, "HW": H * W, "C": C, "y": _ptr(y), "stream": _stream(),
+                             "f32": int(x.dtype == torch.float32)})
     return y
 
 

@@ -181,7 +181,7 @@ def test_gpu_section_defaults_and_values():
     assert g["batch_buckets"] == sorted(g["batch_buckets"])
     assert g["batch_buckets"][-1] == C.get_triton_config()["dynamic_batching"]["max_batch_size"]
     assert g["replicas"] == [1, 2, 4, 8]
-    assert g["dtype"] == "bf16"
+    assert g["dtype"] == "fp32"  # the reference's precision (ONNX Runtime fp32); bf16 is opt-in
     ports = g["ports"]
     assert (ports["monolithic"], ports["detection"], ports["classification"], ports["gateway"]) == (8100, 8200, 8201,
                                                                                                       8300)

@@ -1,0 +1,232 @@
+"""Exact-fp32 pipeline (csrc/kernels/conv_f32.hip + the fp32 instantiations of the
+preprocessing / decode / pooling kernels) against plain PyTorch fp32/fp64 references.
+
+The reference runs both networks as fp32 ONNX graphs (reference experiment.yaml:202,207,
+220,225); these tests pin the MI355X fp32 path at that precision: kernel errors at the
+fp32 rounding level, and the whole request pipeline equal to the fp32 torch/NumPy
+reference pipeline (engine/reference.py) in detection counts, boxes, labels and logits.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from inference_arena_amd.ops import functional as AF
+
+pytestmark = pytest.mark.gpu
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _act64(y, act):
+    if act == "silu":
+        return y * torch.sigmoid(y)
+    if act == "relu6":
+        return y.clamp(0.0, 6.0)
+    return y
+
+
+def _fp32_check(got, ref64, scale64, rel=2e-6):
+    """|got - ref| <= rel * sum|x||w| (+ a denormal floor): fp32 products, fp32 accumulation."""
+    err = (got.double().cpu() - ref64).abs()
+    bound = rel * scale64 + 1e-30
+    worst = (err / bound).max().item()
+    assert worst <= 1.0, f"max error {err.max().item():.3g} is {worst:.2f}x the fp32 bound"
+
+
+@pytest.mark.parametrize(
+    "B,H,Cin,Cout,k,s,act,res,up",
+    [
+        (2, 20, 16, 16, 3, 1, "silu", False, False),    # s2d stem geometry (3x3 over 16 channels)
+        (2, 40, 16, 32, 3, 2, "silu", False, False),    # 3x3 stride 2
+        (3, 20, 32, 32, 3, 1, "silu", True, False),     # bottleneck with residual
+        (2, 10, 64, 128, 1, 1, "silu", False, True),    # 1x1 with the 2x upsampled second store
+        (4, 7, 160, 960, 1, 1, "relu6", False, False),  # MobileNet expand
+        (4, 7, 960, 160, 1, 1, None, True, False),      # MobileNet project + residual
+        (2, 10, 256, 144, 3, 1, "silu", False, False),  # detect head stacked cv2|cv3 (Cout 144: 9 tiles)
+        (2, 20, 64, 80, 3, 1, "silu", False, False),    # Cout 80 (5 tiles)
+        (5, 1, 1280, 1000, 1, 1, None, False, False),   # classifier FC as a 1x1 conv on a 1x1 map
+    ],
+)
+def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
+    g = torch.Generator().manual_seed(B * 100 + H + Cin + Cout)
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g, dtype=torch.float64) * 0.1
+    x32, w32, b32 = x.float(), w.float(), b.float()  # the kernel sees fp32 operands
+    pad = k // 2
+    ref = _act64(F.conv2d(x32.double(), w32.double(), b32.double(), stride=s, padding=pad), act)
+    scale = F.conv2d(x32.double().abs(), w32.double().abs(), b32.double().abs(), stride=s, padding=pad)
+    Ho = ref.shape[2]
+    r = torch.randn(B, Cout, Ho, Ho, generator=g).float() if res else None
+    if res:
+        ref = ref + r.double()
+        scale = scale + r.double().abs()
+    out2 = torch.zeros(B, 2 * Ho, 2 * Ho, Cout, device=device) if up else None
+    y = AF.conv2d_nhwc(_nhwc(x32).to(device), w32, b32, stride=s, act=act,
+                       res=_nhwc(r).to(device) if res else None, out2=out2)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.float32
+    _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
+    if up:
+        up_ref = y.repeat_interleave(2, 1).repeat_interleave(2, 2)
+        assert torch.equal(out2, up_ref)
+
+
+def test_conv_f32_channel_slices(device):
+    """Reads channels [x_coff, x_coff + Cin) of a wider buffer and stores into a channel slice (concat)."""
+    g = torch.Generator().manual_seed(7)
+    buf = torch.randn(2, 12, 12, 96, generator=g)
+    w = torch.randn(32, 48, 3, 3, generator=g) * 0.05
+    b = torch.randn(32, generator=g) * 0.1
+    out = torch.full((2, 12, 12, 64), 7.0, device=device)
+    AF.conv2d_nhwc(buf.to(device), w, b, x_coff=16, cin=48, out=out, out_coff=32, act=None)
+    torch.cuda.synchronize()
+    ref = F.conv2d(buf[..., 16:64].permute(0, 3, 1, 2).double(), w.double(), b.double(), padding=1)
+    o = out.cpu()
+    assert torch.all(o[..., :32] == 7.0)  # untouched slice
+    np.testing.assert_allclose(o[..., 32:].permute(0, 3, 1, 2).double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("stride,H", [(1, 14), (2, 28), (1, 7), (2, 112)])
+def test_dwconv_f32(device, stride, H):
+    g = torch.Generator().manual_seed(stride * 10 + H)
+    C = 96
+    x = torch.randn(3, C, H, H, generator=g)
+    w = torch.randn(C, 1, 3, 3, generator=g) * 0.3
+    b = torch.randn(C, generator=g) * 0.1
+    y = AF.dwconv3x3_nhwc(_nhwc(x).to(device), w, b, stride=stride, act="relu6")
+    torch.cuda.synchronize()
+    ref = F.relu6(F.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=1, groups=C))
+    np.testing.assert_allclose(y.permute(0, 3, 1, 2).double().cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_sppf_f32_exact(device):
+    g = torch.Generator().manual_seed(3)
+    C = 128
+    buf = torch.zeros(2, 20, 20, 4 * C)
+    buf[..., :C] = torch.randn(2, 20, 20, C, generator=g)
+    got = AF.sppf_nhwc(buf.to(device), C).cpu()
+    x = buf[..., :C].permute(0, 3, 1, 2)
+    y1 = F.max_pool2d(x, 5, 1, 2)
+    y2 = F.max_pool2d(y1, 5, 1, 2)
+    y3 = F.max_pool2d(y2, 5, 1, 2)
+    for i, ref in enumerate((y1, y2, y3), start=1):
+        assert torch.equal(got[..., i * C:(i + 1) * C], ref.permute(0, 2, 3, 1)), i
+
+
+def test_letterbox_f32_equals_host(device):
+    """Device letterbox in fp32 == the host reference preprocessor (uint8 rounding + /255), bit for bit."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.processing import YOLOPreprocessor
+
+    imgs = synthetic_images(2, 5) + synthetic_images(1, 6, hw=(333, 500)) + synthetic_images(1, 7, hw=(640, 427))
+    out = AF.letterbox_s2d(imgs, 640, device, dtype=torch.float32)
+    got = AF.s2d_to_nchw(out.cpu())
+    pre = YOLOPreprocessor()
+    for i, im in enumerate(imgs):
+        ref = torch.from_numpy(pre(im).tensor[0])
+        assert torch.equal(got[i], ref), (i, (got[i] - ref).abs().max().item())
+
+
+def test_avgpool_f32(device):
+    x = torch.randn(5, 7, 7, 1280)
+    y = AF.avgpool_nhwc(x.to(device)).cpu()
+    np.testing.assert_allclose(y.numpy(), x.double().mean((1, 2)).numpy(), rtol=1e-6, atol=1e-6)
+
+
+# ---------------------------------------------------------------------------- whole programs
+def _iou(a, b):
+    x1 = np.maximum(a[:, None, 0], b[None, :, 0])
+    y1 = np.maximum(a[:, None, 1], b[None, :, 1])
+    x2 = np.minimum(a[:, None, 2], b[None, :, 2])
+    y2 = np.minimum(a[:, None, 3], b[None, :, 3])
+    inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
+    aa = (a[:, 2] - a[:, 0]) * (a[:, 3] - a[:, 1])
+    bb = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    return inter / (aa[:, None] + bb[None, :] - inter + 1e-9)
+
+
+@pytest.fixture(scope="module")
+def dense_models():
+    from inference_arena_amd.models.zoo import make_mobilenet, make_yolo
+
+    return make_yolo(0, cls_shift=-20.0), make_mobilenet(1)
+
+
+def test_fp32_pipeline_matches_reference(dense_models, device):
+    """The fp32 device pipeline equals the fp32 reference pipeline (torch CPU + host preprocessing +
+    reference NMS): identical detection count per image, matched boxes with IoU > 0.99 and the same
+    class, >= 99 % top-1 agreement and top-1 logit relative error < 1e-3."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+    from inference_arena_amd.engine.reference import ReferencePipeline
+
+    imgs = synthetic_images(10, 21) + synthetic_images(2, 22, hw=(333, 500)) + synthetic_images(2, 23, hw=(640, 427))
+    pipe = GpuPipeline(*dense_models, device=0, buckets=[1, 8, 16], dtype="fp32")
+    assert pipe.dtype == "fp32"
+    got = pipe.infer(imgs)
+    ref = ReferencePipeline(*dense_models, device="cpu")
+    n_det = n_top1 = 0
+    rel = []
+    for i, (im, g) in enumerate(zip(imgs, got)):
+        r = ref(im)
+        assert len(g) == len(r), f"image {i}: {len(g)} detections vs reference {len(r)}"
+        if not len(r):
+            continue
+        iou = _iou(r.boxes, g.boxes)
+        for j in range(len(r)):
+            k = int(np.argmax(iou[j]))
+            assert iou[j, k] > 0.99, (i, j, iou[j, k])
+            assert g.classes[k] == r.classes[j]
+            assert abs(float(g.scores[k]) - float(r.scores[j])) < 1e-4
+            n_det += 1
+            n_top1 += int(g.topk_idx[k, 0] == r.topk_idx[j, 0])
+            rel.append(abs(float(g.topk_logit[k, 0]) - float(r.topk_logit[j, 0])) / (abs(float(r.topk_logit[j, 0])) + 1e-6))
+    assert n_det >= 20, n_det
+    assert n_top1 >= 0.99 * n_det, (n_top1, n_det)
+    assert max(rel) < 1e-3, max(rel)
+
+
+def test_fp32_tensor_models_match_torch(models, device):
+    """Reference tensor contracts in fp32: yolov5n [3,640,640] -> [84,8400], mobilenetv2 -> [1000]."""
+    from inference_arena_amd.engine.pipeline import GpuTensorModel
+
+    yolo, mnet = models
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(2, 3, 640, 640, generator=g)
+    tm = GpuTensorModel.yolo(yolo, device=0, buckets=[2], dtype="fp32")
+    got = torch.from_numpy(tm.infer(x.numpy()))
+    with torch.no_grad():
+        ref = yolo.eval()(x).float()
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-3, atol=2e-3)
+    c = torch.randn(3, 3, 224, 224, generator=g)
+    cm = GpuTensorModel.mobilenet(mnet, device=0, buckets=[4], dtype="fp32")
+    got = cm.infer(c.numpy())
+    with torch.no_grad():
+        ref = mnet.eval()(c).float().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-3, atol=1e-3 * np.abs(ref).max())
+
+
+def test_fp32_split_programs_match_pipeline(dense_models, device):
+    """Detector-only and classifier-only fp32 programs (microservices arm) agree with the fused fp32 program."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuClassifier, GpuDetector, GpuPipeline
+    from inference_arena_amd.processing import extract_crop
+
+    yolo, mnet = dense_models
+    imgs = synthetic_images(4, 31)
+    full = GpuPipeline(yolo, mnet, device=0, buckets=[4], dtype="fp32").infer(imgs)
+    det = GpuDetector(yolo, device=0, buckets=[4], dtype="fp32").infer(imgs)
+    cls = GpuClassifier(mnet, device=0, buckets=[16], dtype="fp32")
+    for a, d, im in zip(full, det, imgs):
+        assert len(a) == len(d)
+        np.testing.assert_allclose(a.boxes, d.boxes, atol=1e-3)
+        if len(a):
+            crops = [extract_crop(im, np.concatenate([bx, [0.0, 0.0]])) for bx in a.boxes]
+            out = cls.infer(crops)
+            assert [int(o[0][0]) for o in out] == [int(t) for t in a.topk_idx[:, 0]]

@@ -360,14 +360,14 @@ def test_executor_autotune_choices(device):
 
     yolo, mnet = make_yolo(0, cls_shift=-20.0), make_mobilenet(1)
     imgs = synthetic_images(4, 77)
-    pipe = GpuPipeline(yolo, mnet, device=0, buckets=[4])
+    pipe = GpuPipeline(yolo, mnet, device=0, buckets=[4], dtype="bf16")
     choices = pipe.ex.conv_choices(4)
     # ~50 conv ops remain once the C3 / inverted-residual / stem / head fusions have absorbed the rest
     assert set(c for c in choices if c) <= {1, 2, 3} and sum(1 for c in choices if c) >= 45
     tuned = pipe.infer(imgs)
     os.environ["ARENA_AUTOTUNE"] = "0"
     try:
-        plain = GpuPipeline(yolo, mnet, device=0, buckets=[4]).infer(imgs)
+        plain = GpuPipeline(yolo, mnet, device=0, buckets=[4], dtype="bf16").infer(imgs)
     finally:
         os.environ.pop("ARENA_AUTOTUNE")
     for a, b in zip(tuned, plain):

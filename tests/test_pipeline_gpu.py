@@ -30,7 +30,7 @@ def dense_models():
 def gpu_pipe(dense_models, device):
     from inference_arena_amd.engine.pipeline import GpuPipeline
 
-    return GpuPipeline(*dense_models, device=0, buckets=[1, 4, 8])
+    return GpuPipeline(*dense_models, device=0, buckets=[1, 4, 8], dtype="bf16")
 
 
 def test_pipeline_matches_reference(gpu_pipe, dense_models):
@@ -82,8 +82,8 @@ def test_overflow_crops_extra_pass(dense_models, device):
     from inference_arena_amd.data.synthetic import synthetic_images
     from inference_arena_amd.engine.pipeline import GpuPipeline
 
-    tiny = GpuPipeline(*dense_models, device=0, buckets=[4], crop_cap_per_image=1)
-    big = GpuPipeline(*dense_models, device=0, buckets=[4], crop_cap_per_image=64)
+    tiny = GpuPipeline(*dense_models, device=0, buckets=[4], crop_cap_per_image=1, dtype="bf16")
+    big = GpuPipeline(*dense_models, device=0, buckets=[4], crop_cap_per_image=64, dtype="bf16")
     imgs = synthetic_images(4, 21)
     a, b = tiny.infer(imgs), big.infer(imgs)
     assert sum(len(r) for r in a) > 16  # exceeds the tiny pass capacity (max(16, 4*1))
@@ -100,9 +100,9 @@ def test_fused_stem_matches_unfused(dense_models, device, monkeypatch):
 
     imgs = synthetic_images(5, 33) + synthetic_images(1, 34, hw=(333, 500))
     monkeypatch.setenv("ARENA_FUSE_STEM", "0")
-    plain = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)  # keep b0 readable
+    plain = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="bf16")  # keep b0 readable
     monkeypatch.setenv("ARENA_FUSE_STEM", "1")
-    fused = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)
+    fused = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="bf16")
     assert any(int(op[0]) == 15 for op in fused.program.ops) and not any(int(op[0]) == 15 for op in plain.program.ops)
     a, b = plain.infer(imgs), fused.infer(imgs)
     for i in range(len(imgs)):
@@ -125,9 +125,9 @@ def test_two_stage_stem_matches_single_stage(dense_models, device, monkeypatch):
 
     imgs = synthetic_images(3, 61) + synthetic_images(1, 62, hw=(333, 500)) + synthetic_images(1, 63, hw=(640, 427))
     monkeypatch.setenv("ARENA_FUSE_STEM2", "0")
-    one = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)
+    one = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="bf16")
     monkeypatch.setenv("ARENA_FUSE_STEM2", "1")
-    two = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)
+    two = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="bf16")
     assert any(int(op[0]) == 15 and int(op[20]) for op in two.program.ops)
     assert not any(int(op[0]) == 15 and int(op[20]) for op in one.program.ops)
     a, b = one.infer(imgs), two.infer(imgs)
@@ -146,9 +146,9 @@ def test_stem_first_block_matches_unfused(dense_models, device, monkeypatch):
 
     imgs = synthetic_images(4, 71) + synthetic_images(1, 72, hw=(333, 500))
     monkeypatch.setenv("ARENA_FUSE_STEM_IR", "0")
-    one = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)
+    one = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="bf16")
     monkeypatch.setenv("ARENA_FUSE_STEM_IR", "1")
-    two = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False)
+    two = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="bf16")
     assert any(int(op[0]) == 15 and int(op[26]) for op in two.program.ops)
     assert not any(int(op[0]) == 15 and int(op[26]) for op in one.program.ops)
     a, b = one.infer(imgs), two.infer(imgs)
@@ -171,9 +171,9 @@ def test_fused_head_pool_matches_unfused(dense_models, device, monkeypatch):
 
     imgs = synthetic_images(4, 51)
     monkeypatch.setenv("ARENA_FUSE_POOL", "0")
-    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False, dtype="bf16")
     monkeypatch.setenv("ARENA_FUSE_POOL", "1")
-    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False, dtype="bf16")
     assert any(int(op[0]) == 17 for op in fused.program.ops) and not any(int(op[0]) == 17 for op in plain.program.ops)
     a, b = plain.infer(imgs), fused.infer(imgs)
     n = sum(len(r) for r in a)
@@ -196,9 +196,9 @@ def test_fused_head_pointwise_matches_unfused(dense_models, device, monkeypatch)
 
     imgs = synthetic_images(4, 41)
     monkeypatch.setenv("ARENA_FUSE_HEAD", "0")
-    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False, dtype="bf16")
     monkeypatch.setenv("ARENA_FUSE_HEAD", "1")
-    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False, dtype="bf16")
     n_pw = sum(1 for op in fused.program.ops if int(op[0]) == 1 and int(op[34]) > 0)
     assert n_pw == 6 and len(fused.program.ops) == len(plain.program.ops) - 6
     a, b = plain.infer(imgs), fused.infer(imgs)
@@ -220,9 +220,9 @@ def test_fused_c3_matches_unfused(dense_models, device, monkeypatch):
 
     imgs = synthetic_images(3, 51) + synthetic_images(1, 52, hw=(333, 500))
     monkeypatch.setenv("ARENA_FUSE_C3", "0")
-    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False, dtype="bf16")
     monkeypatch.setenv("ARENA_FUSE_C3", "all")
-    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False)
+    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False, dtype="bf16")
     assert sum(1 for op in fused.program.ops if int(op[0]) == 16) == 3
     a, b = plain.infer(imgs), fused.infer(imgs)
     for name in ("b2", "cat16", "p3"):

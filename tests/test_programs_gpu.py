@@ -24,13 +24,14 @@ def dense_models():
     return make_yolo(0, cls_shift=-20.0), make_mobilenet(1)
 
 
-def test_yolo_tensor_model_matches_torch(dense_models, device):
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_yolo_tensor_model_matches_torch(dense_models, device, dtype):
     from inference_arena_amd.data.synthetic import synthetic_images
     from inference_arena_amd.engine.pipeline import GpuTensorModel
     from inference_arena_amd.processing import YOLOPreprocessor
 
     yolo, _ = dense_models
-    tm = GpuTensorModel.yolo(yolo, device=0, buckets=[1, 4])
+    tm = GpuTensorModel.yolo(yolo, device=0, buckets=[1, 4], dtype=dtype)
     pre = YOLOPreprocessor()
     xs = np.concatenate([pre(im).tensor for im in synthetic_images(3, 31)], 0)
     got = tm.infer(xs)
@@ -44,13 +45,14 @@ def test_yolo_tensor_model_matches_torch(dense_models, device):
     assert np.median(box_err) < 1.0 and np.quantile(box_err, 0.99) < 8.0, (np.median(box_err), box_err.max())
 
 
-def test_mobilenet_tensor_model_matches_torch(dense_models, device):
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_mobilenet_tensor_model_matches_torch(dense_models, device, dtype):
     from inference_arena_amd.data.synthetic import synthetic_images
     from inference_arena_amd.engine.pipeline import GpuTensorModel
     from inference_arena_amd.processing import MobileNetPreprocessor
 
     _, mnet = dense_models
-    tm = GpuTensorModel.mobilenet(mnet, device=0, buckets=[2, 8])
+    tm = GpuTensorModel.mobilenet(mnet, device=0, buckets=[2, 8], dtype=dtype)
     xs = MobileNetPreprocessor().preprocess_batch(synthetic_images(5, 37))
     got = tm.infer(xs)
     assert got.shape == (5, 1000)
@@ -61,16 +63,17 @@ def test_mobilenet_tensor_model_matches_torch(dense_models, device):
     assert (got.argmax(1) == ref.argmax(1)).mean() >= 0.6
 
 
-def test_detector_and_classifier_match_fused_pipeline(dense_models, device):
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_detector_and_classifier_match_fused_pipeline(dense_models, device, dtype):
     from inference_arena_amd.data.synthetic import synthetic_images
     from inference_arena_amd.engine.pipeline import GpuClassifier, GpuDetector, GpuPipeline
     from inference_arena_amd.processing import extract_crop
 
     yolo, mnet = dense_models
     imgs = synthetic_images(5, 41)
-    fused = GpuPipeline(yolo, mnet, device=0, buckets=[8]).infer(imgs)
-    det = GpuDetector(yolo, device=0, buckets=[8]).infer(imgs)
-    cls = GpuClassifier(mnet, device=0, buckets=[4, 16])
+    fused = GpuPipeline(yolo, mnet, device=0, buckets=[8], dtype=dtype).infer(imgs)
+    det = GpuDetector(yolo, device=0, buckets=[8], dtype=dtype).infer(imgs)
+    cls = GpuClassifier(mnet, device=0, buckets=[4, 16], dtype=dtype)
     assert sum(len(r) for r in fused) > 3
     for im, f, d in zip(imgs, fused, det):
         assert len(f) == len(d)
