@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "common.h"
 #include "launch.h"
@@ -200,6 +201,195 @@ static void launch_f32_wc(const ConvParams& p, hipStream_t s, long M) {
     launch_f32<WC, 1>(p, s, M);
 }
 
+// ---------------------------------------------------------------------------
+// LDS-tiled implicit GEMM (default).  The direct kernel above re-reads each
+// wave's weight rows and im2col fragments from L1/L2 for every K-chunk; here a
+// workgroup stages a [BM pixels x 32 k] activation tile and a [BN channels x
+// 32 k] weight tile in LDS once per K-chunk (double-buffered: the next chunk's
+// global loads are in flight while the current chunk's MFMAs run, one barrier
+// per chunk) and its four waves (WM x WN layout) read their fragments with
+// ds_read_b128.  The staging assignment gives each thread a fixed k-group (4
+// consecutive k = 4 input channels of one tap) and BM/32 fixed pixels, so the
+// im2col address math is one (tap, ci) split per chunk plus a bounds test per
+// pixel.  LDS rows are padded to 36 floats: the 8 rows a ds_read_b128 quarter-
+// wave touches start 4 banks apart (conflict-free).
+constexpr int F32_KC = 32;            // k per LDS chunk
+constexpr int F32_PITCH = F32_KC + 4;  // floats per LDS row
+
+template <int MF, int NF, int WM, int WN>
+__global__ __launch_bounds__(256) void conv_f32_lds_kernel(const ConvParams p) {
+  constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
+  constexpr int PPT = BM / 32;                      // staged pixels per thread
+  constexpr int WPT = (BN * 8 + 255) / 256;         // staged weight float4 per thread
+  __shared__ __attribute__((aligned(16))) float sB[2][BM * F32_PITCH];
+  __shared__ __attribute__((aligned(16))) float sA[2][BN * F32_PITCH];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int wm = wave % WM, wn = wave / WM;
+
+  const int Bl = live_batch(p.B, p.bdev);
+  const int HWo = p.Ho * p.Wo;
+  const int M = Bl * HWo;
+  const int bx = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = bx * BM;
+  if (m0 >= M) return;
+  const int n0 = blockIdx.y * BN;
+
+  const float* __restrict__ x = (const float*)p.x;
+  const float* __restrict__ w = (const float*)p.w;
+  const int H = p.H, W = p.W, xs = p.xs, Cin = p.Cin, KW = p.KW, Kpad = p.Kpad;
+  const int taps = p.KH * p.KW;
+
+  // staging roles: k-group g (4 consecutive k), pixels tid/8 + 32*j
+  const int g = tid & 7;
+  int pb[PPT], py[PPT], px[PPT];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    const int m = m0 + (tid >> 3) + 32 * j;
+    if (m < M) {
+      const int b = m / HWo, r = m - b * HWo;
+      const int oy = r / p.Wo, ox = r - oy * p.Wo;
+      pb[j] = b * H * W;
+      py[j] = oy * p.stride - p.pad_t;
+      px[j] = ox * p.stride - p.pad_l;
+    } else {
+      pb[j] = 0;
+      py[j] = -(1 << 20);  // fails the bounds test: zero fill
+      px[j] = 0;
+    }
+  }
+  float4 rb[PPT], ra[WPT];
+  auto gload = [&](int kc) {
+    const int k = kc * F32_KC + 4 * g;
+    const int tap = k / Cin, ci = k - tap * Cin;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    const bool tv = tap < taps;
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int iy = py[j] + kh, ix = px[j] + kw;
+      const bool ok = tv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      rb[j] = load_f4_or_zero(x + (size_t)(pb[j] + iy * W + ix) * xs + ci, x, ok);
+    }
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+      const int e = tid + 256 * j;  // (row, group) of the weight tile
+      const int row = e >> 3, gg = e & 7;
+      const int kk = kc * F32_KC + 4 * gg;
+      const bool ok = e < BN * 8 && n0 + row < p.Cout_pad && kk < Kpad;
+      ra[j] = load_f4_or_zero(w + (size_t)(n0 + row) * Kpad + kk, w, ok);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < PPT; ++j)
+      *(float4*)&sB[buf][((tid >> 3) + 32 * j) * F32_PITCH + 4 * g] = rb[j];
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e < BN * 8) *(float4*)&sA[buf][(e >> 3) * F32_PITCH + 4 * (e & 7)] = ra[j];
+    }
+  };
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (Kpad + F32_KC - 1) / F32_KC;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    if (kc + 1 < nk) gload(kc + 1);
+#pragma unroll
+    for (int u = 0; u < F32_KC / 16; ++u) {
+      float4 af[NF], bf[MF];
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+        af[j] = *(const float4*)&sA[cur][((wn * NF + j) * 16 + col) * F32_PITCH + 16 * u + 4 * kq];
+#pragma unroll
+      for (int f = 0; f < MF; ++f)
+        bf[f] = *(const float4*)&sB[cur][((wm * MF + f) * 16 + col) * F32_PITCH + 16 * u + 4 * kq];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+#pragma unroll
+          for (int f = 0; f < MF; ++f)
+            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4_get(af[j], t), f4_get(bf[f], t), acc[f][j], 0, 0, 0);
+    }
+    if (kc + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // Epilogue: lane holds 4 consecutive output channels (rows 4*kq..+3 of the 16x16 tile) of pixel col.
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int cb = n0 + (wn * NF + j) * 16 + kq * 4;
+    if (cb >= p.Cout) continue;
+    const float4 bias = *(const float4*)(p.bias + cb);
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int pix = m0 + (wm * MF + f) * 16 + col;
+      if (pix >= M) continue;
+      float v[4] = {acc[f][j][0] + bias.x, acc[f][j][1] + bias.y, acc[f][j][2] + bias.z, acc[f][j][3] + bias.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      if (p.res != nullptr) {
+        const float4 rv = *(const float4*)((const float*)p.res + (size_t)pix * p.rs + cb);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      }
+      const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)p.y + (size_t)pix * p.ys + cb) = o;
+      if (p.y2 != nullptr) {
+        const int b = pix / HWo;
+        const int r = pix - b * HWo;
+        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+        const int W2 = 2 * p.Wo;
+        float* y2 = (float*)p.y2;
+        const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+        *(float4*)(y2 + base * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + 1) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2 + 1) * p.y2s + cb) = o;
+      }
+    }
+  }
+}
+
+template <int MF, int NF, int WM, int WN>
+static void launch_lds(const ConvParams& p, hipStream_t s, long M) {
+  constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
+  dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((p.Cout_pad + BN - 1) / BN));
+  hipLaunchKernelGGL((conv_f32_lds_kernel<MF, NF, WM, WN>), grid, dim3(256), 0, s, p);
+}
+
+// Pixel-tile depth: the largest MF that still launches >= 2 workgroups per CU.  BM is capped at 128 pixels
+// (WM = 4 layouts stop at MF = 2): a 256-pixel tile needs 74+ KB of LDS and drops to one wave per SIMD.
+template <int NF, int WM, int WN>
+static void launch_lds_m(const ConvParams& p, hipStream_t s, long M) {
+  constexpr int BN = WN * NF * 16;
+  const long ny = (p.Cout_pad + BN - 1) / BN;
+  if (WM * 64 <= 128 && ((M + WM * 64 - 1) / (WM * 64)) * ny >= 512)
+    launch_lds<(WM * 64 <= 128 ? 4 : 2), NF, WM, WN>(p, s, M);
+  else if (((M + WM * 32 - 1) / (WM * 32)) * ny >= 512)
+    launch_lds<2, NF, WM, WN>(p, s, M);
+  else
+    launch_lds<1, NF, WM, WN>(p, s, M);
+}
+
+static int f32_conv_family() {
+  static const int v = [] {
+    const char* e = std::getenv("ARENA_F32_CONV");  // "direct" = the register-streamed kernel
+    return (e != nullptr && std::string(e) == "direct") ? 1 : 2;
+  }();
+  return v;
+}
+
 void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (p.Cin % 4 != 0 || p.xs % 4 != 0 || p.Kpad % 16 != 0 || p.Cout_pad % 16 != 0 || p.Cout % 4 != 0 ||
       p.Cout > p.Cout_pad || p.ys % 4 != 0)
@@ -212,8 +402,25 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   const long M = (long)p.B * p.Ho * p.Wo;
   if (M <= 0) return;
   if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
-  // channel tile: the widest of 4/3/2 x 16 channels that wastes no more than the narrower ones
   const int ncf = p.Cout_pad / 16;
+  const int impl = p.impl == 1 ? 1 : p.impl >= 2 ? 2 : f32_conv_family();
+  if (impl == 2) {
+    // channel tile per workgroup (BN = WN*NF*16) by output-channel count
+    if (ncf == 1)
+      launch_lds_m<1, 4, 1>(p, s, M);   // BN 16
+    else if (ncf == 2)
+      launch_lds_m<2, 4, 1>(p, s, M);   // BN 32
+    else if (ncf == 3 || ncf == 9)
+      launch_lds_m<3, 4, 1>(p, s, M);   // BN 48 (144 = 3 x 48: the stacked detect-head convs)
+    else if (ncf == 5)
+      launch_lds_m<5, 4, 1>(p, s, M);   // BN 80 (the 80-class branch)
+    else if (ncf == 6)
+      launch_lds_m<3, 2, 2>(p, s, M);   // BN 96
+    else
+      launch_lds_m<2, 2, 2>(p, s, M);   // BN 64
+    return;
+  }
+  // channel tile: the widest of 4/3/2 x 16 channels that wastes no more than the narrower ones
   if (ncf % 4 == 0 || ncf > 12)
     launch_f32_wc<4>(p, s, M);
   else if (ncf % 3 == 0)

@@ -52,12 +52,13 @@ def main(argv=None) -> int:
     ap.add_argument("--replays", type=int, default=10)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None, help="write the table as markdown")
+    ap.add_argument("--dtype", default="bf16", help="program precision the trace was taken with")
     a = ap.parse_args(argv)
 
     from inference_arena_amd.engine.plans import plan_pipeline
     from inference_arena_amd.models.zoo import default_models
 
-    prog = plan_pipeline(*default_models(a.seed), conf_thr=0.5, iou_thr=0.45)
+    prog = plan_pipeline(*default_models(a.seed), conf_thr=0.5, iou_thr=0.45, dtype=a.dtype)
     n_ops = prog.ops.shape[0]
     rows = [r for r in csv.DictReader(open(a.trace)) if "arena::" in r["Kernel_Name"]]
     # the executor runs each staging slot on its own stream: slice replays per hardware queue so that

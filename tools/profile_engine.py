@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Engine-only driver for rocprofv3: runs ``--batches`` full batches of the curated workload through
+one GpuPipeline (``--dtype``), sequentially, so a kernel trace maps one graph replay per batch onto
+the program's ops (tools/analyze_trace.py)."""
+from __future__ import annotations
+
+import argparse
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--batches", type=int, default=20)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args(argv)
+    import torch
+
+    from inference_arena_amd.data.curator import DatasetManifest, load_manifest_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+    from inference_arena_amd.models.zoo import default_models
+
+    root = Path(__file__).resolve().parents[1]
+    sfx = "" if a.dtype == "fp32" else f"_{a.dtype}"
+    man = DatasetManifest.load(root / "data" / "synthetic_set" / f"manifest_w{a.seed}_n100{sfx}.json")
+    images = load_manifest_images(man)
+    pipe = GpuPipeline(*default_models(a.seed), device=0, buckets=[a.batch], dtype=a.dtype)
+    B = a.batch
+    for i in range(3):
+        pipe.ex.run([images[(i * B + k) % len(images)] for k in range(B)])
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    gpu = []
+    for i in range(a.batches):
+        r = pipe.ex.run([images[(i * B + k) % len(images)] for k in range(B)])
+        gpu.append(r["gpu_ms"])
+    dt = time.perf_counter() - t
+    gpu.sort()
+    print(f"{a.dtype}: {a.batches} sequential batches of {B}: {dt / a.batches * 1e3:.3f} ms/batch wall, "
+          f"gpu_ms p50 {gpu[len(gpu) // 2]:.3f}", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
