@@ -25,6 +25,10 @@ DynamicBatcher::DynamicBatcher(std::vector<std::shared_ptr<BatchInstance>> insta
                                       [&](int v) { return v <= 0 || v > cfg_.max_batch; }),
                        cfg_.preferred.end());
   stats_.batch_hist.assign(cfg_.max_batch + 1, 0);
+  for (auto& e : inst_) {
+    const int64_t cap = e->staging_bytes();
+    if (cap > 0) staging_cap_ = staging_cap_ > 0 ? std::min(staging_cap_, cap) : cap;
+  }
   for (size_t i = 0; i < inst_.size(); ++i) threads_.emplace_back([this, i]() { instance_loop((int)i); });
 }
 
@@ -42,7 +46,19 @@ void DynamicBatcher::shutdown() {
   threads_.clear();
 }
 
+namespace {
+int64_t staged_size(int64_t bytes, int h, int w) {
+  const int64_t b = bytes > 0 ? bytes : (int64_t)h * w * 3;
+  return (b + 255) / 256 * 256;
+}
+}  // namespace
+
 int64_t DynamicBatcher::enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes) {
+  if (staging_cap_ > 0 && staged_size(bytes, h, w) > staging_cap_) {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++stats_.rejected;
+    return -2;
+  }
   auto r = std::make_unique<Request>();
   r->pixels.assign(data, data + (bytes > 0 ? (size_t)bytes : (size_t)h * w * 3));
   r->h = h;
@@ -76,7 +92,28 @@ bool DynamicBatcher::take_batch(Batch& out, bool can_wait) {
       cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
       continue;
     }
-    const int n = (int)q_.size();
+    // Requests that fit the staging pool together (in FIFO order, at least one): a batch of large
+    // images is cut short instead of failing every request in it at submit.
+    int n = (int)q_.size();
+    if (staging_cap_ > 0) {
+      int64_t sum = 0;
+      int fit = 0;
+      for (auto& rq : q_) {
+        if (fit >= cfg_.max_batch) break;
+        const int64_t b = staged_size(rq->bytes, rq->h, rq->w);
+        if (fit > 0 && sum + b > staging_cap_) break;
+        sum += b;
+        ++fit;
+      }
+      if (fit < n && fit < cfg_.max_batch) {
+        for (int i = 0; i < fit; ++i) {
+          out.push_back(std::move(q_.front()));
+          q_.pop_front();
+        }
+        stats_.queue_depth = (int64_t)q_.size();
+        return true;
+      }
+    }
     int take = 0;
     if (n >= cfg_.max_batch) {
       take = cfg_.max_batch;

@@ -65,7 +65,8 @@ class DynamicBatcher {
   DynamicBatcher(const DynamicBatcher&) = delete;
   DynamicBatcher& operator=(const DynamicBatcher&) = delete;
 
-  // Copies the input; returns the request id, or -1 when the queue is full.
+  // Copies the input; returns the request id, -1 when the queue is full, -2 when the input is larger than
+  // an instance can stage in one batch (the caller answers 413 / INVALID_ARGUMENT).
   // `bytes` == 0: RGB uint8 HxWx3 image; otherwise an fp32 [3, h, w] tensor of
   // that many bytes (reference tensor contract of the model server).
   int64_t enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes = 0);
@@ -94,6 +95,7 @@ class DynamicBatcher {
   std::condition_variable cv_;
   std::deque<std::unique_ptr<Request>> q_;
   bool stop_ = false;
+  int64_t staging_cap_ = 0;  // smallest staging capacity of the instances (0 = unlimited)
   int64_t next_id_ = 1;
   BatcherStats stats_;
   std::vector<std::thread> threads_;

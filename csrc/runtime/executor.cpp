@@ -231,11 +231,10 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
   sync_slots();
   free_arenas(bk);
   const size_t abytes = (size_t)std::max<int64_t>(arena_bytes, 256);
+  // Every slot owns its arena, also when the slots are serialised on one stream (ARENA_CONCURRENT=0):
+  // collect() of slot s may replay the classifier program for overflow crops after slot s+1's graph has
+  // run, and that pass reads slot s's crop plan and activations.
   for (int s = 0; s < n_slots_; ++s) {
-    if (s > 0 && !concurrent_) {
-      bk.d_arena[s] = bk.d_arena[0];
-      continue;
-    }
     ARENA_HIP_CHECK(hipMalloc(&bk.d_arena[s], abytes));
     ARENA_HIP_CHECK(hipMemset(bk.d_arena[s], 0, abytes));
   }

@@ -114,6 +114,7 @@ class Executor : public BatchInstance {
   const ExecutorConfig& config() const { return cfg_; }
   int max_det() const override { return cfg_.max_det; }
   int64_t raw_out_bytes() const override { return cfg_.raw_out_bytes; }
+  int64_t staging_bytes() const override { return cfg_.pool_bytes_per_image * (int64_t)max_B_; }
 
   // Asynchronous pipelined API: submit() packs the images into a free staging
   // slot, enqueues H2D + graph and returns the slot id; collect() waits for

@@ -37,6 +37,9 @@ class BatchInstance {
   virtual int num_slots() const = 0;             // batches that may be in flight at once
   virtual int max_det() const = 0;               // detection rows per image in BatchResult::det
   virtual int64_t raw_out_bytes() const = 0;     // raw output bytes per image (0 = none)
+  // Bytes one batch may stage in total (each input rounded up to 256); 0 = unlimited.  The batcher
+  // closes a batch before it would exceed this and rejects an input that can never fit.
+  virtual int64_t staging_bytes() const { return 0; }
   // Start a batch; returns the slot id.  Throws when every slot is in flight.
   virtual int submit(const std::vector<InputImage>& imgs) = 0;
   // Wait for a slot's batch and return its results (the slot becomes free).

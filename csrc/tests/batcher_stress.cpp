@@ -9,7 +9,10 @@
 //     num_slots() batches in flight;
 //   * a submit() failure is reported to every request of that batch;
 //   * a full queue rejects (enqueue returns -1) instead of blocking;
-//   * shutdown() drains queued work and joins cleanly.
+//   * shutdown() drains queued work and joins cleanly;
+//   * batches never stage more bytes than the instance's staging capacity, and an
+//     input that can never fit is rejected at enqueue (-2) (a large
+//     image must not fail the small requests it shares a batch with).
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -44,7 +47,9 @@ std::atomic<int> fails{0};
 
 class FakeInstance : public BatchInstance {
  public:
-  FakeInstance(int slots, int max_batch) : slots_(slots), max_batch_(max_batch), busy_(slots, false), work_(slots) {}
+  FakeInstance(int slots, int max_batch, int64_t staging = 0)
+      : slots_(slots), max_batch_(max_batch), staging_(staging), busy_(slots, false), work_(slots) {}
+  int64_t staging_bytes() const override { return staging_; }
   std::vector<int> buckets() const override { return {1, 2, 4, max_batch_}; }
   int num_slots() const override { return slots_; }
   int max_det() const override { return kMaxDet; }
@@ -52,6 +57,13 @@ class FakeInstance : public BatchInstance {
 
   int submit(const std::vector<InputImage>& imgs) override {
     CHECK(!imgs.empty() && (int)imgs.size() <= max_batch_, "batch size %zu", imgs.size());
+    if (staging_ > 0) {
+      int64_t sum = 0;
+      for (auto& im : imgs) sum += ((int64_t)im.h * im.w * 3 + 255) / 256 * 256;
+      CHECK(sum <= staging_, "batch stages %lld bytes > capacity %lld", (long long)sum, (long long)staging_);
+      if (sum > staging_) throw std::runtime_error("batch exceeds the staging pool");
+      max_staged_ = std::max(max_staged_, sum);
+    }
     int s = -1;
     for (int i = 0; i < slots_; ++i)
       if (!busy_[i]) { s = i; break; }
@@ -106,9 +118,11 @@ class FakeInstance : public BatchInstance {
   }
 
   int max_in_flight() const { return max_in_flight_; }
+  int64_t max_staged() const { return max_staged_; }
 
  private:
   int slots_, max_batch_;
+  int64_t staging_ = 0, max_staged_ = 0;
   std::vector<bool> busy_;
   std::vector<std::future<BatchResult>> work_;
   int in_flight_ = 0, max_in_flight_ = 0;
@@ -234,9 +248,47 @@ void run_failures_and_rejection() {
   CHECK(errored >= 1 && out[0].error.find("poisoned") != std::string::npos, "poisoned batch not reported");
 }
 
+void run_staging_capacity() {
+  // capacity = 4 x 1 KiB-aligned small images; "large" 20x20 images (1200 B -> 1280 staged) fill 3 slots
+  const int64_t cap = 4096;
+  auto a = std::make_shared<FakeInstance>(2, 8, cap);
+  BatcherConfig cfg;
+  cfg.max_batch = 8;
+  cfg.max_queue_delay_us = 100;
+  cfg.max_queue_size = 0;
+  std::vector<Outcome> out(64);
+  {
+    DynamicBatcher bat({a}, cfg);
+    std::vector<uint8_t> big((size_t)40 * 40 * 3, 9);  // 4800 B: can never fit
+    Outcome dummy;
+    const int64_t rej = bat.enqueue(big.data(), 40, 40, [&](RequestResult&&) { dummy.calls.fetch_add(1); });
+    CHECK(rej == -2, "oversized input not rejected (%lld)", (long long)rej);
+    for (int i = 0; i < 64; ++i) {
+      const int side = (i % 3 == 0) ? 20 : 4;
+      std::vector<uint8_t> img((size_t)side * side * 3, (uint8_t)(1 + i % 200));
+      Outcome* o = &out[i];
+      const int64_t id = bat.enqueue(img.data(), side, side, [o](RequestResult&& r) {
+        o->error = r.error;
+        o->calls.fetch_add(1);
+      });
+      CHECK(id > 0, "request %d rejected", i);
+    }
+    for (int spin = 0; spin < 20000 && bat.stats().requests + bat.stats().failed < 64; ++spin)
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    bat.shutdown();
+    CHECK(dummy.calls.load() == 0, "rejected request got a callback");
+  }
+  for (int i = 0; i < 64; ++i) {
+    CHECK(out[i].calls.load() == 1, "request %d got %d callbacks", i, out[i].calls.load());
+    CHECK(out[i].error.empty(), "request %d failed: %s", i, out[i].error.c_str());
+  }
+  CHECK(a->max_staged() > 0 && a->max_staged() <= cap, "staged %lld", (long long)a->max_staged());
+}
+
 }  // namespace
 
 int main() {
+  run_staging_capacity();
   run_stress();
   run_failures_and_rejection();
   if (fails.load()) {

@@ -32,6 +32,9 @@ class Replicas:
     procs: list
     port: int
     stride: int
+    specs: list = None  # (argv, env, gpu, log path) per replica, for restarts
+    restarts: int = 0
+    stopping: bool = False
 
     def ports(self) -> list[int]:
         return [self.port + self.stride * r for r in range(len(self.procs))] if self.stride else [self.port]
@@ -57,7 +60,30 @@ class Replicas:
             time.sleep(0.5)
         return not pending
 
+    def supervise(self) -> int:
+        """Restart replicas that exited with a non-zero code (device fault: code 3) as fresh child
+        processes on the same GPU and port; returns the number restarted by this call."""
+        n = 0
+        if self.stopping or not self.specs:
+            return 0
+        for i, p in enumerate(self.procs):
+            rc = p.poll()
+            if rc is None or rc == 0:
+                continue
+            argv, env, gpu, log = self.specs[i]
+            e = dict(env)
+            # the start-up process group is gone: the new process serves alone with the seeded weights
+            e.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "ARENA_REPLICA_GPU": str(gpu),
+                      "ARENA_RESTARTED": str(self.restarts + 1)})
+            e.pop("MASTER_PORT", None)
+            out = open(log, "a") if log else subprocess.DEVNULL
+            self.procs[i] = subprocess.Popen(argv, env=e, stdout=out, stderr=subprocess.STDOUT)
+            self.restarts += 1
+            n += 1
+        return n
+
     def stop(self, timeout: float = 20.0) -> None:
+        self.stopping = True
         for p in self.procs:
             if p.poll() is None:
                 p.send_signal(signal.SIGINT)
@@ -71,25 +97,28 @@ class Replicas:
 
 
 def launch(arch: str, n: int, *, port: int = 8100, stride: int = 0, host: str = "127.0.0.1",
-           env: dict | None = None, log_dir: str | None = None, procs_per_gpu: int = 1) -> Replicas:
+           env: dict | None = None, log_dir: str | None = None, procs_per_gpu: int = 1,
+           first_gpu: int = 0) -> Replicas:
     """``n`` GPUs x ``procs_per_gpu`` serving processes.  Several processes per GPU
     scale the CPU side (HTTP parsing, JPEG decode) while sharing the device; the
     start-up weight broadcast then runs over gloo, because one RCCL
     communicator cannot hold two ranks of the same GPU."""
     master = free_port()
-    procs = []
+    procs, specs = [], []
     world = n * procs_per_gpu
     for r in range(world):
         e = dict(os.environ)
         e.update(env or {})
         e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
                   "MASTER_PORT": str(master), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
-                  "ARENA_PROCS_PER_GPU": str(procs_per_gpu)})
-        out = open(os.path.join(log_dir, f"replica_{r}.log"), "w") if log_dir else subprocess.DEVNULL
-        procs.append(subprocess.Popen([sys.executable, "-m", "inference_arena_amd.server.replica", "--arch", arch,
-                                       "--host", host, "--port", str(port), "--port-stride", str(stride)],
-                                      env=e, stdout=out, stderr=subprocess.STDOUT))
-    return Replicas(procs, port, stride)
+                  "ARENA_PROCS_PER_GPU": str(procs_per_gpu), "ARENA_FIRST_GPU": str(first_gpu)})
+        log = os.path.join(log_dir, f"replica_{r}.log") if log_dir else None
+        out = open(log, "w") if log else subprocess.DEVNULL
+        argv = [sys.executable, "-m", "inference_arena_amd.server.replica", "--arch", arch, "--host", host,
+                "--port", str(port), "--port-stride", str(stride)]
+        procs.append(subprocess.Popen(argv, env=e, stdout=out, stderr=subprocess.STDOUT))
+        specs.append((argv, e, first_gpu + r // procs_per_gpu, log))
+    return Replicas(procs, port, stride, specs)
 
 
 def main(argv=None) -> int:
@@ -100,14 +129,20 @@ def main(argv=None) -> int:
     ap.add_argument("--stride", type=int, default=0)
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--procs-per-gpu", type=int, default=int(os.environ.get("ARENA_PROCS_PER_GPU", "1")))
+    ap.add_argument("--first-gpu", type=int, default=int(os.environ.get("ARENA_FIRST_GPU", "0")))
     a = ap.parse_args(argv)
-    rep = launch(a.arch, a.gpus, port=a.port, stride=a.stride, host=a.host, procs_per_gpu=a.procs_per_gpu)
+    rep = launch(a.arch, a.gpus, port=a.port, stride=a.stride, host=a.host, procs_per_gpu=a.procs_per_gpu,
+                 first_gpu=a.first_gpu)
     try:
         ok = rep.wait_ready()
         print(f"{a.gpus} GPU(s) x {a.procs_per_gpu} process(es) {'ready' if ok else 'FAILED'} on port(s) "
               f"{rep.ports()}", flush=True)
-        while rep.alive():
-            time.sleep(1)
+        while True:
+            if rep.supervise():
+                print(f"restarted replica(s); {rep.restarts} restart(s) so far", flush=True)
+            if all(p.poll() == 0 for p in rep.procs):
+                break
+            time.sleep(0.5)
     except KeyboardInterrupt:
         pass
     finally:

@@ -139,14 +139,16 @@ def validate(cfg) -> list[str]:
     return errs
 
 
-def generate(model_name: str, *, reference_compat: bool = False) -> object:
+def generate(model_name: str, *, reference_compat: bool = False, gpus: list[int] | None = None) -> object:
     """ModelConfig for a model of experiment.yaml.
 
     ``reference_compat=True`` reproduces the reference's config exactly in
     content (max_batch_size 0, full-rank dims incl. the batch 1, no
     dynamic_batching); the default enables the server-side dynamic batcher
     (``triton.dynamic_batching``) with batch-less dims.  Instance kind/count
-    and the thread parameters come from the ``triton`` section.
+    and the thread parameters come from the ``triton`` section; ``gpus`` (or
+    ``triton.instance_group.gpus``) lists the devices of a KIND_GPU group —
+    ``count`` instances on each (Triton semantics, parallel/placement.py).
     """
     from ..config import get_model_config, get_triton_config
 
@@ -162,7 +164,10 @@ def generate(model_name: str, *, reference_compat: bool = False) -> object:
         t.dims.extend(dims[1:] if batched else dims)
     ig = tc.get("instance_group", {}) or {}
     kind = str(ig.get("kind", "KIND_GPU"))
-    cfg.instance_group.add(count=int(ig.get("count", 1)), kind=Kind.Value(kind))
+    g = cfg.instance_group.add(count=int(ig.get("count", 1)), kind=Kind.Value(kind))
+    dev = gpus if gpus is not None else ig.get("gpus")
+    if dev and kind != "KIND_CPU" and not reference_compat:
+        g.gpus.extend(int(x) for x in dev)
     for k, v in (tc.get("parameters") or {}).items():
         cfg.parameters[k].string_value = str(v)
     if batched:

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import asyncio
 import itertools
+import os
 import logging
 import time
 import uuid
@@ -77,13 +78,30 @@ def to_response(rid: str, res: ImageResult, labels: list[str], timing: dict, con
 
 
 class FaultInjector:
-    def __init__(self, every: int = 0):
+    """``ARENA_FAULT_EVERY=k`` fails every k-th request.  ``ARENA_FAULT_MODE=device`` makes the injected
+    failure a device fault (a message starting with "HIP error", as ARENA_HIP_CHECK raises): the service
+    then reports itself unhealthy and a supervised replica exits so its launcher starts a fresh process."""
+
+    def __init__(self, every: int = 0, mode: str | None = None):
         self.every = int(every)
+        self.mode = (mode if mode is not None else os.environ.get("ARENA_FAULT_MODE", "request")).lower()
         self._n = itertools.count(1)
+        self.device_error: str | None = None
 
     def check(self) -> None:
         if self.every > 0 and next(self._n) % self.every == 0:
+            if self.mode == "device":
+                self.device_error = "HIP error (injected by ARENA_FAULT_MODE=device)"
+                raise RuntimeError(self.device_error)
             raise RuntimeError("injected fault (ARENA_FAULT_EVERY)")
+
+
+def device_fault(state: dict) -> str | None:
+    """The first device fault of a service (its backend's or an injected one), else None."""
+    be = state.get("backend") or state.get("detector")
+    err = getattr(be, "device_error", None) if be is not None else None
+    f = state.get("faults")
+    return err or (f.device_error if f is not None else None)
 
 
 def new_request_id() -> str:

@@ -57,16 +57,28 @@ def _result_from_dict(d: dict) -> ImageResult:
     )
 
 
+def settings_devices(settings) -> list[int]:
+    """GPUs one service process drives: ``ARENA_GPUS`` ("0,1" / "0-3"), else ``ARENA_GPU``."""
+    from ..parallel.placement import parse_gpu_list
+
+    return parse_gpu_list(getattr(settings, "ARENA_GPUS", "") or "", default=int(settings.ARENA_GPU))
+
+
 class GpuBatchedBackend(Backend):
     name = "gpu"
 
     def __init__(self, yolo, mnet, *, device: int = 0, instances: int = 1, max_batch: int = 32,
                  preferred: list[int] | None = None, max_queue_delay_us: int = 500, max_queue_size: int = 4096,
-                 buckets: list[int] | None = None, weights: np.ndarray | None = None):
+                 buckets: list[int] | None = None, weights: np.ndarray | None = None,
+                 devices: list[int] | None = None):
+        """``instances`` pipelines on each GPU of ``devices`` (default: ``[device]``) behind one batcher queue:
+        each instance thread pulls the next batch for its own GPU (data parallel within one process)."""
         from ..engine.pipeline import GpuPipeline
 
         bk = buckets or sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
-        self.pipes = [GpuPipeline(yolo, mnet, device=device, buckets=bk, weights=weights) for _ in range(instances)]
+        self.devices = [int(d) for d in (devices or [device])]
+        self.pipes = [GpuPipeline(yolo, mnet, device=d, buckets=bk, weights=weights)
+                      for d in self.devices for _ in range(instances)]
         self.batcher = AsyncBatcher(self.pipes, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us, max_queue_size=max_queue_size)
         self.device = device
@@ -153,6 +165,7 @@ def build_backend(settings, *, arch: str = "monolithic") -> Backend:
         return CpuReferenceBackend(yolo, mnet, threads=int(get_controlled_variable("onnx_runtime",
                                                                                      "intra_op_num_threads")))
     db = get_triton_config().get("dynamic_batching", {}) or {}
-    return GpuBatchedBackend(yolo, mnet, device=int(settings.ARENA_GPU), max_batch=int(settings.ARENA_MAX_BATCH),
+    return GpuBatchedBackend(yolo, mnet, device=int(settings.ARENA_GPU), devices=settings_devices(settings),
+                             max_batch=int(settings.ARENA_MAX_BATCH),
                              preferred=list(db.get("preferred_batch_size", [])),
                              max_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))

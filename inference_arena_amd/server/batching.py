@@ -20,6 +20,17 @@ class Overloaded(RuntimeError):
     """The request queue is full (HTTP 503 / gRPC RESOURCE_EXHAUSTED)."""
 
 
+class TooLarge(ValueError):
+    """The input exceeds what one batch can stage on the device (HTTP 413 / gRPC INVALID_ARGUMENT)."""
+
+
+def _enqueue_or_raise(rid: int) -> None:
+    if rid == -2:
+        raise TooLarge("input larger than the device staging pool of one batch")
+    if rid < 0:
+        raise Overloaded("inference queue full")
+
+
 def is_device_fault(message: str) -> bool:
     """A HIP runtime error (ARENA_HIP_CHECK in csrc/kernels/common.h): the device context of this
     process is no longer trustworthy, so the instance must be taken out of service (SURVEY.md §5
@@ -68,8 +79,7 @@ class AsyncBatcher:
         def done(d):
             loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(d))
 
-        if self._b.enqueue(self._prep(x), done) < 0:
-            raise Overloaded("inference queue full")
+        _enqueue_or_raise(self._b.enqueue(self._prep(x), done))
         return self._check(await fut)
 
     async def run_many(self, xs: list[np.ndarray]) -> list[dict]:
@@ -83,8 +93,7 @@ class AsyncBatcher:
             box.append(d)
             ev.set()
 
-        if self._b.enqueue(self._prep(x), done) < 0:
-            raise Overloaded("inference queue full")
+        _enqueue_or_raise(self._b.enqueue(self._prep(x), done))
         if not ev.wait(timeout):
             raise TimeoutError("inference timed out")
         return self._check(box[0])

@@ -27,9 +27,9 @@ from ..metrics import ArenaMetrics
 from ..processing import extract_crop
 from ..utils.logging import request_id_var, setup_logging
 from ..utils.settings import Settings
-from .app_common import DecodePool, FaultInjector, Timer, new_request_id, read_upload
+from .app_common import DecodePool, FaultInjector, Timer, device_fault, new_request_id, read_upload
 from .batching import Overloaded
-from .grpc_client import ClassificationClient
+from .grpc_client import ClassificationClient, make_classification_client
 from .schemas import Classification, DetectionBox, DetectionWithClassification, HealthResponse, PredictResponse
 from .service_backends import DetectorBackend, build_detector_backend
 
@@ -51,8 +51,9 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
         if state["detector"] is None:
             state["detector"] = build_detector_backend(settings)
         if state["client"] is None:
-            state["client"] = ClassificationClient(settings.CLASSIFICATION_GRPC_ENDPOINT,
-                                                   transport=settings.ARENA_CROP_TRANSPORT)
+            # one endpoint, or a least-outstanding pool over one classification service per GPU
+            state["client"] = make_classification_client(settings.CLASSIFICATION_GRPC_ENDPOINT,
+                                                         transport=settings.ARENA_CROP_TRANSPORT)
         if not state["client"].connected:
             await state["client"].connect(ready_timeout=30.0)
         log.info("service ready")
@@ -125,7 +126,7 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
         request_id_var.set(None)
         cl = state.get("client")
         det = state.get("detector")
-        if det is not None and getattr(det, "device_error", None):
+        if device_fault(state):
             return JSONResponse(status_code=503, content={"status": "unhealthy", "models_loaded": False})
         return HealthResponse(status="healthy", models_loaded=det is not None and cl is not None and cl.connected)
 

@@ -79,3 +79,67 @@ class ClassificationClient:
     async def check_health(self) -> bool:
         r = await self.health.Check(pb.HealthCheckRequest(), timeout=self.timeout_s)
         return r.status == pb.SERVING
+
+
+class ClassificationClientPool:
+    """Detection-side view of several classification services (one per GPU: scripts/start_arena.py
+    ``--arch microservices --gpus N``).  ``CLASSIFICATION_GRPC_ENDPOINT`` may list endpoints separated by
+    commas; each crop RPC goes to the endpoint with the fewest outstanding RPCs (ties: round robin), so the
+    fan-out of one request spreads over the classification GPUs.  Same interface as
+    ``ClassificationClient``."""
+
+    def __init__(self, endpoints: list[str], transport: str = "jpeg", timeout_s: float = 30.0):
+        if not endpoints:
+            raise ValueError("no classification endpoints")
+        self.clients = [ClassificationClient(e, transport, timeout_s) for e in endpoints]
+        self.endpoint = ",".join(endpoints)
+        self.transport = transport
+        self.outstanding = [0] * len(self.clients)
+        self._rr = 0
+
+    async def connect(self, ready_timeout: float = 30.0) -> None:
+        await asyncio.gather(*(c.connect(ready_timeout) for c in self.clients))
+
+    async def close(self) -> None:
+        await asyncio.gather(*(c.close() for c in self.clients))
+
+    @property
+    def connected(self) -> bool:
+        return all(c.connected for c in self.clients)
+
+    def pick(self) -> int:
+        n = len(self.clients)
+        best = min(range(n), key=lambda k: (self.outstanding[(self._rr + k) % n], k))
+        i = (self._rr + best) % n
+        self._rr = (i + 1) % n
+        return i
+
+    async def _on(self, i: int, coro):
+        self.outstanding[i] += 1
+        try:
+            return await coro
+        finally:
+            self.outstanding[i] -= 1
+
+    async def classify(self, rid: str, crop: np.ndarray, box: dict | None = None):
+        i = self.pick()
+        return await self._on(i, self.clients[i].classify(rid, crop, box))
+
+    async def classify_parallel(self, request_id: str, crops: list[np.ndarray], boxes: list[dict]):
+        return await asyncio.gather(*(self.classify(f"{request_id}_{i}", c, b)
+                                      for i, (c, b) in enumerate(zip(crops, boxes))))
+
+    async def classify_batch(self, request_id: str, crops: list[np.ndarray], boxes: list[dict]):
+        i = self.pick()
+        return await self._on(i, self.clients[i].classify_batch(request_id, crops, boxes))
+
+    async def check_health(self) -> bool:
+        return all(await asyncio.gather(*(c.check_health() for c in self.clients)))
+
+
+def make_classification_client(spec: str, transport: str = "jpeg", timeout_s: float = 30.0):
+    """One client for a single endpoint, a least-outstanding pool for a comma-separated list."""
+    eps = [e.strip() for e in spec.split(",") if e.strip()]
+    if len(eps) == 1:
+        return ClassificationClient(eps[0], transport, timeout_s)
+    return ClassificationClientPool(eps, transport, timeout_s)

@@ -21,6 +21,7 @@ Here every model of the repository is compiled into executor programs
 from __future__ import annotations
 
 import asyncio
+import os
 import logging
 import threading
 import time
@@ -120,10 +121,13 @@ class TensorModel(ModelHandle):
         if device == "gpu":
             from ..engine.pipeline import GpuTensorModel
 
-            count = max(1, sum(g.count for g in cfg.instance_group) or 1)
+            from ..parallel.placement import instance_devices
+
+            # Triton semantics: `count` instances on each GPU of the group (all visible GPUs when none listed)
+            self.devices = instance_devices(list(cfg.instance_group), default_gpu=gpu)
             buckets = sorted({b for b in (1, 2, 4, 8, 16, 32, self.max_batch) if b <= max(self.max_batch, 1)})
             make = GpuTensorModel.yolo if arch == "yolov5nu" else GpuTensorModel.mobilenet
-            self.runners = [make(module, device=gpu, buckets=buckets) for _ in range(count)]
+            self.runners = [make(module, device=d, buckets=buckets) for d in self.devices]
             db = cfg.dynamic_batching if cfg.HasField("dynamic_batching") else None
             self.batcher = AsyncBatcher(self.runners, max_batch=self.max_batch,
                                         preferred=list(db.preferred_batch_size) if db else None,
@@ -196,8 +200,13 @@ class PipelineModel(ModelHandle):
         if device == "gpu":
             from .backends import GpuBatchedBackend
 
+            from ..parallel.placement import parse_gpu_list
+
             mb = int(params.get("max_batch", 32))
-            self.backend = GpuBatchedBackend(yolo, mnet, device=gpu, instances=int(params.get("instance_count", 1)),
+            # ensemble parameter "gpus" ("0,1" / "0-7") or ARENA_GPUS: one fused pipeline per GPU per instance
+            devs = parse_gpu_list(params.get("gpus") or os.environ.get("ARENA_GPUS") or "", default=gpu)
+            self.backend = GpuBatchedBackend(yolo, mnet, device=gpu, devices=devs,
+                                             instances=int(params.get("instance_count", 1)),
                                              max_batch=mb,
                                              max_queue_delay_us=int(params.get("max_queue_delay_microseconds", 500)))
         else:

@@ -21,8 +21,9 @@ from ..labels import load_labels
 from ..metrics import ArenaMetrics
 from ..utils.logging import request_id_var, setup_logging
 from ..utils.settings import Settings
-from .app_common import DecodePool, FaultInjector, Timer, new_request_id, read_upload, to_response
+from .app_common import DecodePool, FaultInjector, Timer, device_fault, new_request_id, read_upload, to_response
 from .backends import Backend, Overloaded, build_backend
+from .batching import TooLarge
 from .schemas import HealthResponse, PredictResponse
 
 log = logging.getLogger("arena.monolithic")
@@ -70,6 +71,9 @@ def create_app(settings: Settings | None = None, backend: Backend | None = None)
         except Overloaded as e:
             metrics.observe("overloaded")
             raise HTTPException(status_code=503, detail=str(e)) from e
+        except TooLarge as e:
+            metrics.observe("too_large")
+            raise HTTPException(status_code=413, detail=str(e)) from e
         except Exception as e:  # reference: any failure -> 500 with detail=str(e)
             metrics.observe("error")
             log.error(f"Predict failed: {e}", extra={"endpoint": "/predict", "status_code": 500})
@@ -88,7 +92,7 @@ def create_app(settings: Settings | None = None, backend: Backend | None = None)
     async def health():
         request_id_var.set(None)
         be = state.get("backend")
-        if be is not None and getattr(be, "device_error", None):
+        if device_fault(state):
             # device fault: 503 so probes / the replica router take this instance out of rotation
             return JSONResponse(status_code=503, content={"status": "unhealthy", "models_loaded": False})
         return HealthResponse(status="healthy", models_loaded=be is not None and be.ready())

@@ -13,6 +13,13 @@ WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT).  Start-up:
 4. serve the arm (monolithic / detection / gateway) on GPU ``LOCAL_RANK``.
 
 Each response carries ``x-arena-replica: <rank>``.
+
+Failover (SURVEY.md §5 failure detection): a watchdog polls the arm's device
+fault state; on a HIP fault the replica stops accepting (closes its listening
+socket, drains in-flight requests) and exits with code 3, and the supervisor
+in ``parallel.replicas`` starts a fresh child process for the same GPU (never
+an exec of the faulted process).  A restarted replica runs with world size 1
+(``ARENA_REPLICA_GPU`` names its device) and derives the same seeded weights.
 """
 from __future__ import annotations
 
@@ -78,10 +85,13 @@ def build_app(arch: str, settings, info):
             from .backends import GpuBatchedBackend
 
             yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
-            blob = plan_pipeline(yolo, mnet, conf_thr=0.5, iou_thr=0.45).weights if info.is_main else None
+            from ..engine.pipeline import resolve_dtype
+
+            blob = plan_pipeline(yolo, mnet, conf_thr=0.5, iou_thr=0.45,
+                                 dtype=resolve_dtype()).weights if info.is_main else None
             blob = D.broadcast_blob(blob, info)
             db = get_triton_config().get("dynamic_batching", {}) or {}
-            backend = GpuBatchedBackend(yolo, mnet, device=int(settings.ARENA_GPU),
+            backend = GpuBatchedBackend(yolo, mnet, device=int(settings.ARENA_GPU),  # one GPU per replica
                                         instances=int(settings.ARENA_INSTANCES),
                                         max_batch=int(settings.ARENA_MAX_BATCH),
                                         preferred=list(db.get("preferred_batch_size", [])),
@@ -119,7 +129,9 @@ def main(argv=None) -> int:
     backend = "gloo" if settings.ARENA_DEVICE == "cpu" or per_gpu > 1 else None
     info = D.init_from_env(backend)
     if settings.ARENA_DEVICE != "cpu":
-        settings.ARENA_GPU = info.local_rank // per_gpu
+        override = os.environ.get("ARENA_REPLICA_GPU")
+        first = int(os.environ.get("ARENA_FIRST_GPU", "0"))
+        settings.ARENA_GPU = int(override) if override else first + info.local_rank // per_gpu
         if backend == "gloo":
             import torch
 
@@ -131,7 +143,30 @@ def main(argv=None) -> int:
     port = a.port + a.port_stride * info.rank
     sock = _socket(a.host, port, reuse_port=a.port_stride == 0)
     server = uvicorn.Server(uvicorn.Config(ReplicaTag(app, info.rank), log_level="warning", access_log=False))
-    asyncio.run(server.serve(sockets=[sock]))
+    fault: list[str] = []
+
+    async def watchdog():
+        from .app_common import device_fault
+
+        while not server.should_exit:
+            await asyncio.sleep(0.2)
+            err = device_fault(getattr(app.state, "arena", {}) or {})
+            if err:
+                fault.append(err)
+                # uvicorn's shutdown first closes the listening socket (the kernel stops routing new
+                # connections to this process), then drains in-flight requests and returns
+                server.should_exit = True
+                return
+
+    async def serve():
+        task = asyncio.create_task(watchdog())
+        await server.serve(sockets=[sock])
+        task.cancel()
+
+    asyncio.run(serve())
+    if fault and os.environ.get("ARENA_EXIT_ON_FAULT", "1") == "1":
+        print(f"replica {info.rank}: device fault, exiting for restart: {fault[0]}", flush=True)
+        return 3
     return 0
 
 

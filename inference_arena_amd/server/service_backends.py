@@ -49,11 +49,13 @@ class GpuClassifierBackend(ClassifierBackend):
     name = "gpu"
 
     def __init__(self, mnet, *, device: int = 0, instances: int = 1, max_batch: int = 64,
-                 max_queue_delay_us: int = 300, preferred: list[int] | None = None):
+                 max_queue_delay_us: int = 300, preferred: list[int] | None = None,
+                 devices: list[int] | None = None):
         from ..engine.pipeline import GpuClassifier
 
         bk = _default_buckets(max_batch)
-        self.runners = [GpuClassifier(mnet, device=device, buckets=bk) for _ in range(instances)]
+        self.devices = [int(d) for d in (devices or [device])]
+        self.runners = [GpuClassifier(mnet, device=d, buckets=bk) for d in self.devices for _ in range(instances)]
         self.batcher = AsyncBatcher(self.runners, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us)
 
@@ -126,11 +128,13 @@ class GpuDetectorBackend(DetectorBackend):
     name = "gpu"
 
     def __init__(self, yolo, *, device: int = 0, instances: int = 1, max_batch: int = 32,
-                 max_queue_delay_us: int = 500, preferred: list[int] | None = None):
+                 max_queue_delay_us: int = 500, preferred: list[int] | None = None,
+                 devices: list[int] | None = None):
         from ..engine.pipeline import GpuDetector
 
         bk = _default_buckets(max_batch)
-        self.runners = [GpuDetector(yolo, device=device, buckets=bk) for _ in range(instances)]
+        self.devices = [int(d) for d in (devices or [device])]
+        self.runners = [GpuDetector(yolo, device=d, buckets=bk) for d in self.devices for _ in range(instances)]
         self.batcher = AsyncBatcher(self.runners, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us)
 
@@ -200,7 +204,10 @@ def build_classifier_backend(settings) -> ClassifierBackend:
     if settings.ARENA_DEVICE == "cpu":
         return CpuClassifierBackend(mnet, threads=int(get_controlled_variable("onnx_runtime",
                                                                               "intra_op_num_threads")))
-    return GpuClassifierBackend(mnet, device=int(settings.ARENA_GPU), max_batch=max(32, int(settings.ARENA_MAX_BATCH)),
+    from .backends import settings_devices
+
+    return GpuClassifierBackend(mnet, device=int(settings.ARENA_GPU), devices=settings_devices(settings),
+                                max_batch=max(32, int(settings.ARENA_MAX_BATCH)),
                                 max_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))
 
 
@@ -213,5 +220,8 @@ def build_detector_backend(settings) -> DetectorBackend:
         y = get_model_config("yolov5n")
         return CpuDetectorBackend(yolo, threads=int(get_controlled_variable("onnx_runtime", "intra_op_num_threads")),
                                   conf_thr=float(y["confidence_threshold"]), iou_thr=float(y["iou_threshold"]))
-    return GpuDetectorBackend(yolo, device=int(settings.ARENA_GPU), max_batch=int(settings.ARENA_MAX_BATCH),
+    from .backends import settings_devices
+
+    return GpuDetectorBackend(yolo, device=int(settings.ARENA_GPU), devices=settings_devices(settings),
+                              max_batch=int(settings.ARENA_MAX_BATCH),
                               max_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))

@@ -48,6 +48,7 @@ class Settings(BaseModel):
     # arena additions
     ARENA_DEVICE: str = "gpu"          # gpu | cpu
     ARENA_GPU: int = 0
+    ARENA_GPUS: str = ""               # GPUs one process drives ("0,1" / "0-7"); '' = ARENA_GPU only
     ARENA_MAX_BATCH: int = 32
     ARENA_QUEUE_DELAY_US: int = 500
     ARENA_DECODE_THREADS: int = 8

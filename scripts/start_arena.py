@@ -3,8 +3,12 @@
 scripts/start-*.sh): each service is a child process; Ctrl-C stops them all.
 
   monolithic     replicas of :8100 (one per GPU, shared port)
-  microservices  classification gRPC :8201 (GPU 0) + detection HTTP :8200
-  triton         model server :8000/:8001/:8002 + gateway :8300
+  microservices  one classification gRPC service per GPU (:8201, :8211, ... on GPU 0, 1, ...) +
+                 detection HTTP :8200 replicas (one per GPU) fanning crops over all classification services
+                 (least-outstanding gRPC channel pool); --split puts detection on the first half of the
+                 GPUs and classification on the second half
+  triton         model server :8000/:8001/:8002 driving every GPU (ensemble pipeline on each listed GPU,
+                 tensor models: instance_group gpus) + gateway :8300
 
 Example: python scripts/start_arena.py --arch triton --gpus 1
 """
@@ -43,8 +47,25 @@ def wait_http(url: str, timeout: float, procs) -> bool:
     return False
 
 
+def classification_ports(n: int, base: int = 8201) -> list[int]:
+    return [base + 10 * i for i in range(max(1, n))]
+
+
+def plan_microservices(gpus: int, split: bool = False) -> dict:
+    """GPU assignment of the microservices arm: detection GPUs, classification (GPU, port) pairs."""
+    if split and gpus >= 2:
+        det = list(range(gpus // 2))
+        cls = list(range(gpus // 2, gpus))
+    else:
+        det = list(range(max(1, gpus)))
+        cls = list(range(max(1, gpus)))
+    ports = classification_ports(len(cls))
+    return {"detection_gpus": det, "classification": list(zip(cls, ports)),
+            "endpoint": ",".join(f"127.0.0.1:{p}" for p in ports)}
+
+
 def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = "model_repository",
-          extra_env: dict | None = None, procs_per_gpu: int = 1):
+          extra_env: dict | None = None, procs_per_gpu: int = 1, split: bool = False):
     env = dict(os.environ, PYTHONPATH=str(ROOT), HSA_ENABLE_IPC_MODE_LEGACY="0", ARENA_DEVICE=device,
                **(extra_env or {}))
     log_dir.mkdir(parents=True, exist_ok=True)
@@ -54,20 +75,24 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
                             "--port", "8100", "--procs-per-gpu", str(procs_per_gpu)], env, log_dir, "monolithic"))
         ok = wait_http("http://127.0.0.1:8100/health", 600, procs)
     elif arch == "microservices":
-        procs.append(spawn(["inference_arena_amd.server.classification_service"], dict(env, PORT="8201"), log_dir,
-                           "classification"))
+        plan = plan_microservices(gpus, split)
+        for g, port in plan["classification"]:
+            procs.append(spawn(["inference_arena_amd.server.classification_service"],
+                               dict(env, PORT=str(port), ARENA_GPU=str(g)), log_dir, f"classification_gpu{g}"))
         time.sleep(1)
-        procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "detection", "--gpus", str(gpus),
-                            "--port", "8200", "--procs-per-gpu", str(procs_per_gpu)],
-                           dict(env, CLASSIFICATION_GRPC_ENDPOINT="127.0.0.1:8201"), log_dir, "detection"))
+        det = plan["detection_gpus"]
+        procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "detection", "--gpus", str(len(det)),
+                            "--first-gpu", str(det[0]), "--port", "8200", "--procs-per-gpu", str(procs_per_gpu)],
+                           dict(env, CLASSIFICATION_GRPC_ENDPOINT=plan["endpoint"]), log_dir, "detection"))
         ok = wait_http("http://127.0.0.1:8200/health", 600, procs)
     elif arch == "triton":
         if not (Path(repo) / "yolov5n" / "config.pbtxt").exists():
             subprocess.run([sys.executable, str(ROOT / "scripts" / "upload_models.py"), "--repository", repo],
                            check=True, env=env)
+        ms_env = dict(env, ARENA_GPUS=f"0-{max(1, gpus) - 1}")  # the ensemble pipeline runs on every GPU
         for k in range(max(1, procs_per_gpu)):  # server processes share :8000/:8001/:8002 (SO_REUSEPORT)
             procs.append(spawn(["inference_arena_amd.server.model_server", "--model-repository", repo, "--device",
-                                device], env, log_dir, f"model_server_{k}"))
+                                device], ms_env, log_dir, f"model_server_{k}"))
         ok = wait_http("http://127.0.0.1:8000/v2/health/ready", 600, procs)
         if ok:
             procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "gateway", "--gpus", "1",
@@ -99,8 +124,10 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--logs", default="logs")
     ap.add_argument("--procs-per-gpu", type=int, default=1)
+    ap.add_argument("--split", action="store_true",
+                    help="microservices: detection and classification on disjoint GPU halves")
     a = ap.parse_args(argv)
-    procs, ok = start(a.arch, a.gpus, Path(a.logs), a.device, procs_per_gpu=a.procs_per_gpu)
+    procs, ok = start(a.arch, a.gpus, Path(a.logs), a.device, procs_per_gpu=a.procs_per_gpu, split=a.split)
     print(f"{a.arch}: {'ready' if ok else 'FAILED (see ' + a.logs + ')'}", flush=True)
     try:
         while ok and all(p.poll() is None for p in procs):
