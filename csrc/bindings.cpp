@@ -13,6 +13,7 @@
 #include "kernels/launch.h"
 #include "runtime/executor.h"
 #include "runtime/batcher.h"
+#include "runtime/split.h"
 
 namespace py = pybind11;
 using namespace arena;
@@ -447,13 +448,48 @@ PYBIND11_MODULE(_C, m) {
              return out;
            })
       .def("weights_ptr", &Executor::weights_ptr)
+      .def("set_peer_stage", &Executor::set_peer_stage)
+      .def("device", &Executor::device)
+      .def("submit_peer",
+           [](Executor& e, Executor& src, int slot) {
+             py::gil_scoped_release nogil;
+             return e.submit_peer(src, slot);
+           })
       .def("conv_choices", &Executor::conv_choices)
       .def("stream", &Executor::stream);
+
+  py::class_<SplitInstance, std::shared_ptr<SplitInstance>>(m, "SplitInstance")
+      .def(py::init([](std::shared_ptr<Executor> det, std::shared_ptr<Executor> cls) {
+        return std::make_shared<SplitInstance>(det, cls);
+      }))
+      .def("submit",
+           [](SplitInstance& s, const py::list& imgs) {
+             std::vector<py::array> keep;
+             auto v = images_from(imgs, keep);
+             py::gil_scoped_release nogil;
+             return s.submit(v);
+           })
+      .def("collect",
+           [](SplitInstance& s, int slot) {
+             BatchResult r;
+             {
+               py::gil_scoped_release nogil;
+               r = s.collect(slot);
+             }
+             return result_to_py(r, s.max_det());
+           })
+      .def("num_slots", &SplitInstance::num_slots)
+      .def("buckets", &SplitInstance::buckets);
 
   py::class_<DynamicBatcher>(m, "DynamicBatcher")
       .def(py::init([](py::list executors, const py::dict& cfg) {
              std::vector<std::shared_ptr<BatchInstance>> inst;
-             for (auto h : executors) inst.push_back(h.cast<std::shared_ptr<Executor>>());
+             for (auto h : executors) {
+               if (py::isinstance<SplitInstance>(h))
+                 inst.push_back(h.cast<std::shared_ptr<SplitInstance>>());
+               else
+                 inst.push_back(h.cast<std::shared_ptr<Executor>>());
+             }
              BatcherConfig c;
              c.max_batch = get<int>(cfg, "max_batch", c.max_batch);
              c.preferred = get<std::vector<int>>(cfg, "preferred", {});

@@ -132,7 +132,10 @@ size_t Executor::out_off_topk() const {
 size_t Executor::out_off_raw() const {
   return align_up(out_off_topk() + sizeof(TopkResult) * (size_t)max_B_ * cfg_.max_det, 256);
 }
-size_t Executor::out_bytes_total() const { return out_off_raw() + (size_t)cfg_.raw_out_bytes * max_B_; }
+size_t Executor::out_off_xcrops() const { return align_up(out_off_raw() + (size_t)cfg_.raw_out_bytes * max_B_, 256); }
+size_t Executor::out_bytes_total() const {
+  return out_off_xcrops() + sizeof(CropRef) * (size_t)max_B_ * cfg_.max_det;
+}
 
 void Executor::sync_slots() {
   for (int i = 0; i < n_streams_; ++i) ARENA_HIP_CHECK(hipStreamSynchronize(streams_[i]));
@@ -334,6 +337,7 @@ uint8_t* Executor::resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff, int 
     case BUF_DET: base = sl.d_out + out_off_det(); break;
     case BUF_TOPK: base = sl.d_out + out_off_topk(); break;
     case BUF_RAWOUT: base = sl.d_out + out_off_raw(); break;
+    case BUF_XCROPS: base = sl.d_out + out_off_xcrops(); break;
     default:
       if (buf < 0 || buf >= (int64_t)bk.info.offsets.size())
         throw std::runtime_error("program references unknown buffer " + std::to_string(buf));
@@ -803,6 +807,7 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   ctrl->n_images = n;
   ctrl->crop_base = 0;
   const size_t bytes = in_bytes_meta() + off;
+  sl.in_used = bytes;
   if (copy_mode_ == 2) {
     ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, sl.stream));
   } else {
@@ -901,7 +906,7 @@ BatchResult Executor::collect(int s) {
   res.crop_offset[n] = total;
   res.total_crops = total;
   if (has_raw_) res.raw.assign(sl.h_out + out_off_raw(), sl.h_out + out_off_raw() + (size_t)cfg_.raw_out_bytes * n);
-  if (!has_det_) res.det_count.assign(n, 0);
+  if (!has_det_ && !peer_stage_) res.det_count.assign(n, 0);
   Bucket& bk = buckets_.at(sl.bucket);
   const int CC = bk.info.crop_cap;
   if (has_topk_ && total > CC) {
@@ -931,6 +936,60 @@ BatchResult Executor::collect(int s) {
 }
 
 BatchResult Executor::run(const std::vector<InputImage>& imgs) { return collect(submit(imgs)); }
+
+int Executor::submit_peer(Executor& src, int src_slot) {
+  trace::Range tr("arena.submit_peer");
+  if (!peer_stage_) throw std::runtime_error("submit_peer: executor is not a peer stage (set_peer_stage)");
+  if (src_slot < 0 || src_slot >= src.n_slots_ || !src.slots_[src_slot].busy)
+    throw std::runtime_error("submit_peer: source slot not in flight");
+  if (src.max_B_ != max_B_ || src.cfg_.max_det != cfg_.max_det || src.in_bytes_total() != in_bytes_total())
+    throw std::runtime_error("submit_peer: source and peer stage need the same max_batch / max_det / staging");
+  Slot& ss = src.slots_[src_slot];
+  std::lock_guard<std::mutex> lk(mu_);
+  const int B = ss.bucket;
+  auto it = buckets_.find(B);
+  if (it == buckets_.end()) throw std::runtime_error("submit_peer: peer stage lacks bucket " + std::to_string(B));
+  const int s = next_slot_;
+  Slot& sl = slots_[s];
+  if (sl.busy) throw std::runtime_error("submit_peer: every staging slot is in flight; collect() first");
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  const int sdev = src.cfg_.device;
+  if (sdev != cfg_.device && std::find(peer_enabled_.begin(), peer_enabled_.end(), sdev) == peer_enabled_.end()) {
+    int can = 0;
+    ARENA_HIP_CHECK(hipDeviceCanAccessPeer(&can, cfg_.device, sdev));
+    if (can) {
+      const hipError_t e = hipDeviceEnablePeerAccess(sdev, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) ARENA_HIP_CHECK(e);
+      (void)hipGetLastError();
+    }
+    peer_enabled_.push_back(sdev);
+  }
+  sl.stream = streams_[seq_++ % n_streams_];
+  // the detector's graph (and its result copy) finished on the source device
+  ARENA_HIP_CHECK(hipStreamWaitEvent(sl.stream, ss.done, 0));
+  auto copy = [&](uint8_t* dst, const uint8_t* srcp, size_t n) {
+    if (n == 0) return;
+    if (sdev == cfg_.device)
+      ARENA_HIP_CHECK(hipMemcpyAsync(dst, srcp, n, hipMemcpyDeviceToDevice, sl.stream));
+    else
+      ARENA_HIP_CHECK(hipMemcpyPeerAsync(dst, cfg_.device, srcp, sdev, n, sl.stream));
+  };
+  copy(sl.d_in, ss.d_in, ss.in_used);                                                // ctrl, meta, images
+  copy(sl.d_out, ss.d_out, out_off_topk());                                          // det counts + dets
+  copy(sl.d_out + out_off_xcrops(), ss.d_out + out_off_xcrops(), sizeof(CropRef) * (size_t)max_B_ * cfg_.max_det);
+  ARENA_HIP_CHECK(hipEventRecord(sl.started, sl.stream));
+  Bucket& bk = it->second;
+  ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], sl.stream));
+  enqueue_results_d2h(bk, sl, ss.n_images);
+  bk.last_slot = s;
+  ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
+  sl.busy = true;
+  sl.bucket = B;
+  sl.n_images = ss.n_images;
+  sl.in_used = ss.in_used;
+  next_slot_ = (next_slot_ + 1) % n_slots_;
+  return s;
+}
 
 void Executor::replay(int B, int s, int iters) {
   auto it = buckets_.find(B);

@@ -73,6 +73,7 @@ enum ReservedBuf : int64_t {
   BUF_DETCOUNT = -14,
   BUF_TOPK = -15,
   BUF_RAWOUT = -16,
+  BUF_XCROPS = -17,  // crop plan exported for a second-stage executor (split topology), in the output block
 };
 
 // Batch kind of an op: which live count clamps it.
@@ -125,6 +126,18 @@ class Executor : public BatchInstance {
   // Convenience: submit + collect.
   BatchResult run(const std::vector<InputImage>& imgs);
 
+  // Split topology (detection on one GPU, classification on another): enqueue this executor's program on
+  // the batch that `src` (a detector + crop-plan program on any device) runs in `src_slot`.  On this
+  // executor's stream, after src's slot completes: peer copies (xGMI) of src's staged input block (ctrl
+  // with the crop counts, image metadata, the decoded images), its detections and its exported crop
+  // plan (BUF_XCROPS), then this program's graph (crop gather + classifier) and the result D2H.  The
+  // result of collect() on this executor is the whole request result (detections + classifications).
+  int submit_peer(Executor& src, int src_slot);
+  // Mark this executor as a second stage (its detections arrive from a peer, see submit_peer).
+  void set_peer_stage(bool v) { peer_stage_ = v; }
+  bool peer_stage() const { return peer_stage_; }
+  int device() const { return cfg_.device; }
+
   // Run only the captured graph of a bucket on already-staged inputs; used by
   // microbenchmarks to separate host packing from device time.
   void replay(int B, int slot, int iters);
@@ -159,6 +172,7 @@ class Executor : public BatchInstance {
     bool busy = false;
     int bucket = 0;
     int n_images = 0;
+    size_t in_used = 0;  // staged input bytes (ctrl + meta + images) of the current batch
   };
   struct Bucket {
     BucketInfo info;
@@ -194,6 +208,8 @@ class Executor : public BatchInstance {
   size_t out_off_topk() const;
   size_t out_bytes_total() const;
   size_t out_off_raw() const;
+  size_t out_off_xcrops() const;
+  int acquire_slot();
   void parallel_copy(std::vector<std::function<void()>>& jobs);
 
   ExecutorConfig cfg_;
@@ -210,6 +226,8 @@ class Executor : public BatchInstance {
   int n_streams_ = 1;
   uint64_t seq_ = 0;                     // batches submitted
   bool has_topk_ = false, has_det_ = false, has_raw_ = false;
+  bool peer_stage_ = false;
+  std::vector<int> peer_enabled_;  // devices this executor's device has peer access to
   int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on compute stream
   // ARENA_CONCURRENT: 1 = per-slot streams + arenas (in-flight batches overlap on the device),
   // 0 = two slots serialised on one stream sharing one arena.  ARENA_SLOTS: staging slots when concurrent

@@ -19,7 +19,8 @@ from ..models.mobilenetv2 import MobileNetV2
 from ..models.yolov5nu import YOLOv5nu
 from ..ops import native
 from .planner import layout
-from .plans import plan_classifier, plan_detector, plan_mobilenet_raw, plan_pipeline, plan_yolo_raw
+from .plans import (plan_classifier, plan_detector, plan_mobilenet_raw, plan_pipeline, plan_split_classifier,
+                    plan_split_detector, plan_yolo_raw)
 from .validate import validate_program
 
 
@@ -185,6 +186,50 @@ class GpuPipeline(GpuProgramRunner):
             chunk = images[k : k + self.max_batch]
             res = self.ex.run([np.ascontiguousarray(i, dtype=np.uint8) for i in chunk])
             out.extend(split_results(res, len(chunk)))
+        return out
+
+
+class SplitPipeline:
+    """Split topology: detection on GPU ``det_device``, classification on GPU ``cls_device``; the crop plan,
+    detections and decoded images move device to device (xGMI peer copies, csrc/runtime/split.h) instead of
+    the reference's per-crop JPEG + gRPC hop.  Same results as ``GpuPipeline``; ``instance`` is a batch
+    instance for the native DynamicBatcher."""
+
+    def __init__(self, yolo: YOLOv5nu, mnet: MobileNetV2, *, det_device: int = 0, cls_device: int = 1,
+                 buckets=None, max_det: int | None = None, crop_cap_per_image: int | None = None,
+                 conf_thr: float | None = None, iou_thr: float | None = None, dtype: str | None = None,
+                 max_image_pixels: int = 640 * 640):
+        gcfg = get_gpu_config()
+        ycfg = get_model_config("yolov5n")
+        mb = get_controlled_variable("preprocessing", "mobilenet")
+        det_size = int(get_controlled_variable("preprocessing", "yolo")["target_size"])
+        d = resolve_dtype(dtype)
+        max_det = int(max_det or gcfg["max_det"])
+        conf = float(conf_thr if conf_thr is not None else ycfg["confidence_threshold"])
+        iou = float(iou_thr if iou_thr is not None else ycfg["iou_threshold"])
+        kw = dict(buckets=buckets, max_det=max_det, crop_cap_per_image=crop_cap_per_image,
+                  pool_bytes_per_image=int(max_image_pixels) * 3)
+        self.det = GpuProgramRunner(plan_split_detector(yolo, conf_thr=conf, iou_thr=iou, det_size=det_size,
+                                                        max_det=max_det, dtype=d), device=det_device, **kw)
+        self.cls = GpuProgramRunner(plan_split_classifier(mnet, cls_size=int(mb["target_size"]), mean=mb["mean"],
+                                                          std=mb["std"], max_det=max_det, dtype=d),
+                                    device=cls_device, **kw)
+        self.cls.ex.set_peer_stage(True)
+        self.instance = native().SplitInstance(self.det.ex, self.cls.ex)
+        self.max_batch = self.det.max_batch
+        self.dtype = d
+
+    def submit(self, images: list[np.ndarray]) -> int:
+        return self.instance.submit([np.ascontiguousarray(i, dtype=np.uint8) for i in images])
+
+    def collect(self, slot: int, n: int) -> list[ImageResult]:
+        return split_results(self.instance.collect(slot), n)
+
+    def infer(self, images: list[np.ndarray]) -> list[ImageResult]:
+        out: list[ImageResult] = []
+        for k in range(0, len(images), self.max_batch):
+            chunk = images[k: k + self.max_batch]
+            out.extend(self.collect(self.submit(chunk), len(chunk)))
         return out
 
 

@@ -72,6 +72,13 @@ DTYPES = ("bf16", "fp32")
 (OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
  OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL) = range(1, 18)
 BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK, BUF_RAWOUT = -1, -10, -11, -12, -13, -14, -15, -16
+BUF_XCROPS = -17  # crop plan exported to a second-stage executor (split topology; executor.h)
+
+
+@dataclass(frozen=True)
+class Reserved:
+    """A reserved (executor-owned) region used where a planner Buffer is expected."""
+    id: int
 IMAGES, CROPS = 0, 1
 ACT = {None: 0, "none": 0, "silu": 1, "relu6": 2}
 ALIGN = 256

@@ -37,7 +37,7 @@ import torch
 from ..models.common import fold, fold_conv_bn
 from ..models.mobilenetv2 import MobileNetV2
 from ..models.yolov5nu import STRIDES, YOLOv5nu
-from .planner import BUF_NONE, BUF_RAWOUT, CROPS, IMAGES, Program, ProgramBuilder, View
+from .planner import BUF_NONE, BUF_RAWOUT, BUF_XCROPS, CROPS, IMAGES, Program, ProgramBuilder, Reserved, View
 
 CAND_BYTES = 32
 CROPREF_BYTES = 32
@@ -378,6 +378,32 @@ def plan_classifier(mnet: MobileNetV2, *, cls_size: int = 224, mean=(0.485, 0.45
     pb.begin_classifier()
     plan_mobilenet(pb, mnet, crops, cls_size, mean, std)
     return pb.build({"kind": "classifier", "cls_size": cls_size, "max_det": max_det})
+
+
+def plan_split_detector(yolo: YOLOv5nu, *, conf_thr: float, iou_thr: float, det_size: int = 640,
+                        cand_cap: int = 8400, max_det: int = 300, dtype: str = "bf16") -> Program:
+    """First stage of the split topology (GPU i): detection + crop plan exported in BUF_XCROPS, which the
+    classifier stage on GPU j pulls over xGMI (csrc/runtime/split.h)."""
+    pb = ProgramBuilder(dtype)
+    heads = plan_yolo(pb, yolo, det_size)
+    cand = pb.raw("cand", cand_cap * CAND_BYTES)
+    count = pb.raw("cand_count", 4)
+    pb.zero(count)
+    pb.decode(heads, STRIDES, cand, count, conf_thr)
+    pb.nms(cand, count, iou_thr)
+    pb.crop_plan(Reserved(BUF_XCROPS))
+    return pb.build({"kind": "split_detector", "conf_thr": conf_thr, "iou_thr": iou_thr, "det_size": det_size,
+                     "cand_cap": cand_cap, "max_det": max_det})
+
+
+def plan_split_classifier(mnet: MobileNetV2, *, cls_size: int = 224, mean=(0.485, 0.456, 0.406),
+                          std=(0.229, 0.224, 0.225), max_det: int = 300, dtype: str = "bf16") -> Program:
+    """Second stage of the split topology (GPU j): crop gather from the peer-copied images with the peer's
+    crop plan (BUF_XCROPS) -> MobileNetV2 -> top-5; the whole program is the classification pass."""
+    pb = ProgramBuilder(dtype)
+    pb.begin_classifier()
+    plan_mobilenet(pb, mnet, Reserved(BUF_XCROPS), cls_size, mean, std)
+    return pb.build({"kind": "split_classifier", "cls_size": cls_size, "max_det": max_det})
 
 
 def plan_yolo_raw(yolo: YOLOv5nu, *, det_size: int = 640, dtype: str = "bf16") -> Program:

@@ -16,6 +16,7 @@ from ..engine.planner import (
     BUF_POOL,
     BUF_RAWOUT,
     BUF_TOPK,
+    BUF_XCROPS,
     CROPS,
     OP_AVGPOOL,
     OP_C3FUSED,
@@ -53,6 +54,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
     sizes[BUF_DET] = B * max_det * DET_BYTES
     sizes[BUF_DETCOUNT] = B * 4
     sizes[BUF_TOPK] = B * max_det * TOPK_BYTES
+    sizes[BUF_XCROPS] = B * max_det * CROP_BYTES
     raw = int(raw_out_bytes if raw_out_bytes is not None else prog.meta.get("raw_out_bytes", 0))
     sizes[BUF_RAWOUT] = B * raw
     wbytes = prog.weights.nbytes

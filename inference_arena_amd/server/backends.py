@@ -107,6 +107,30 @@ class GpuBatchedBackend(Backend):
         self.batcher.close()
 
 
+class GpuSplitBackend(GpuBatchedBackend):
+    """Monolithic arm in the split topology: detection on ``det_device``, classification on ``cls_device``
+    (engine.pipeline.SplitPipeline: crop plan, detections and images handed over device to device) behind
+    the native dynamic batcher."""
+
+    def __init__(self, yolo, mnet, *, det_device: int = 0, cls_device: int = 1, instances: int = 1,
+                 max_batch: int = 32, preferred: list[int] | None = None, max_queue_delay_us: int = 500,
+                 max_queue_size: int = 4096, buckets: list[int] | None = None):
+        from ..engine.pipeline import SplitPipeline
+
+        bk = buckets or sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
+        self.devices = [int(det_device), int(cls_device)]
+        self.pipes = [SplitPipeline(yolo, mnet, det_device=det_device, cls_device=cls_device, buckets=bk)
+                      for _ in range(instances)]
+
+        class _Inst:  # AsyncBatcher schedules `.ex`: the split batch instance
+            def __init__(self, p):
+                self.ex = p.instance
+
+        self.batcher = AsyncBatcher([_Inst(p) for p in self.pipes], max_batch=max_batch, preferred=preferred,
+                                    max_queue_delay_us=max_queue_delay_us, max_queue_size=max_queue_size)
+        self.device = det_device
+
+
 class CpuReferenceBackend(Backend):
     name = "cpu"
 
@@ -165,6 +189,11 @@ def build_backend(settings, *, arch: str = "monolithic") -> Backend:
         return CpuReferenceBackend(yolo, mnet, threads=int(get_controlled_variable("onnx_runtime",
                                                                                      "intra_op_num_threads")))
     db = get_triton_config().get("dynamic_batching", {}) or {}
+    if int(getattr(settings, "ARENA_CLS_GPU", -1)) >= 0:  # split topology: classification on another GPU
+        return GpuSplitBackend(yolo, mnet, det_device=int(settings.ARENA_GPU), cls_device=int(settings.ARENA_CLS_GPU),
+                               max_batch=int(settings.ARENA_MAX_BATCH),
+                               preferred=list(db.get("preferred_batch_size", [])),
+                               max_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))
     return GpuBatchedBackend(yolo, mnet, device=int(settings.ARENA_GPU), devices=settings_devices(settings),
                              max_batch=int(settings.ARENA_MAX_BATCH),
                              preferred=list(db.get("preferred_batch_size", [])),

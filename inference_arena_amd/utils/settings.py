@@ -49,6 +49,7 @@ class Settings(BaseModel):
     ARENA_DEVICE: str = "gpu"          # gpu | cpu
     ARENA_GPU: int = 0
     ARENA_GPUS: str = ""               # GPUs one process drives ("0,1" / "0-7"); '' = ARENA_GPU only
+    ARENA_CLS_GPU: int = -1            # split topology: classification GPU (crops handed over device to device)
     ARENA_MAX_BATCH: int = 32
     ARENA_QUEUE_DELAY_US: int = 500
     ARENA_DECODE_THREADS: int = 8
