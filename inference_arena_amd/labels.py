@@ -2,11 +2,11 @@
 
 The reference ships the 1000 ImageNet class names
 (src/shared/data/imagenet_labels.txt) and refuses to start unless exactly
-1000 lines load (architectures/monolithic/app/inference.py:96-125).  The arena
-uses random-init weights, so the label *names* carry no meaning; it loads a
-real 1000-line label file when one is configured (``LABELS_FILE`` or the
-model repository's ``labels.txt``) and otherwise generates stable
-placeholder names ``imagenet_class_XXX``.
+1000 lines load (architectures/monolithic/app/inference.py:96-125).  The same
+constant table ships here (``inference_arena_amd/data/imagenet_labels.txt``,
+the standard ImageNet-1k class names) and is the default; ``LABELS_FILE`` (or
+a model repository's ``labels.txt``) overrides it.  ``placeholder_labels``
+remains for tests that want synthetic names.
 """
 from __future__ import annotations
 
@@ -19,10 +19,12 @@ def placeholder_labels(n: int = NUM_CLASSES) -> list[str]:
     return [f"imagenet_class_{i:03d}" for i in range(n)]
 
 
+DEFAULT_LABELS = Path(__file__).resolve().parent / "data" / "imagenet_labels.txt"
+
+
 def load_labels(path: str | Path | None = None, n: int = NUM_CLASSES) -> list[str]:
-    if not path:
-        return placeholder_labels(n)
-    p = Path(path)
+    """The configured label file, else the shipped ImageNet table; exactly ``n`` names (reference check)."""
+    p = Path(path) if path else DEFAULT_LABELS
     if not p.exists():
         raise FileNotFoundError(f"labels file not found: {p}")
     labels = [ln.strip() for ln in p.read_text(encoding="utf-8").splitlines()]

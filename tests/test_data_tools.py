@@ -85,3 +85,14 @@ def test_generate_proto_text(tmp_path):
     assert "map<string, InferParameter> parameters = 4;" in kv and "oneof parameter_choice" in kv
     mc = (tmp_path / "model_config.proto").read_text()
     assert "repeated ModelInstanceGroup instance_group = 7;" in mc
+
+
+def test_default_labels_are_the_imagenet_table():
+    """The reference ships the 1000 ImageNet names and refuses to start without exactly 1000
+    (reference architectures/monolithic/app/inference.py:96-125): same default here."""
+    from inference_arena_amd.labels import DEFAULT_LABELS, load_labels
+
+    labels = load_labels()
+    assert len(labels) == 1000 and DEFAULT_LABELS.exists()
+    assert labels[0] == "tench" and labels[1] == "goldfish" and labels[999] == "toilet tissue"
+    assert len(set(labels)) > 990

@@ -139,7 +139,7 @@ def test_classify_rpcs_and_health(fake_server):
     par, bat, bad, healthy, raw = asyncio.run(go())
     assert [r.request_id for r in par] == ["rq_0", "rq_1", "rq_2"]
     assert [r.result.class_id for r in par] == [11, 12, 13] == [r.result.class_id for r in bat]
-    assert par[0].result.class_name == "imagenet_class_011"
+    assert par[0].result.class_name == "goldfinch"
     assert abs(par[0].result.confidence - 0.6) < 1e-6 and len(par[0].top_k) == 5
     assert par[0].timing.total_ms > 0
     assert bad.error == "" and healthy

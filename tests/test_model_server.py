@@ -13,6 +13,7 @@ import torch
 from fastapi.testclient import TestClient
 
 from inference_arena_amd.data.synthetic import encode_jpeg, synthetic_images
+from inference_arena_amd.labels import load_labels
 from inference_arena_amd.proto import kserve as kv
 from inference_arena_amd.repository import model_config as mc
 from inference_arena_amd.repository import store
@@ -231,7 +232,7 @@ def _gateway_predict(model_server, mode):
     assert {"detection_ms", "classification_ms", "total_ms"} <= set(js["timing"])
     for d in js["detections"]:
         assert set(d["detection"]) == {"x1", "y1", "x2", "y2", "confidence", "class_id"}
-        assert d["classification"]["class_name"].startswith("imagenet_class_")
+        assert d["classification"]["class_name"] in set(load_labels())
     return js
 
 

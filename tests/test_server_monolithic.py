@@ -54,8 +54,8 @@ def test_predict_schema_and_health():
         assert {"detection_ms", "classification_ms", "total_ms"} <= set(js["timing"])
         d0 = js["detections"][0]
         assert set(d0["detection"]) == {"x1", "y1", "x2", "y2", "confidence", "class_id"}
-        assert d0["classification"] == {"class_id": 5, "class_name": "imagenet_class_005", "confidence": 2.5}
-        assert js["detections"][1]["classification"]["class_name"] == "imagenet_class_999"
+        assert d0["classification"] == {"class_id": 5, "class_name": "electric ray", "confidence": 2.5}
+        assert js["detections"][1]["classification"]["class_name"] == "toilet tissue"
         m = c.get("/metrics").text
         assert 'arena_requests_total{arch="monolithic",status="ok"} 1.0' in m
 
