@@ -177,6 +177,38 @@ def curate(counter: Callable[[list[np.ndarray]], Iterable[int]], cfg: CurationCo
     return res, man
 
 
+def curate_paths(counter: Callable[[list[np.ndarray]], Iterable[int]], paths, cfg: CurationConfig | None = None, *,
+                 loader: Callable | None = None, batch: int = 32, log: Callable[[str], None] | None = None
+                 ) -> tuple[CurationResult, DatasetManifest]:
+    """Curate a local image collection (COCO val2017, reference src/shared/data/curator.py:480-599): count
+    the detections of every file, keep those with min..max detections, sample the 25/50/25 mix."""
+    from ..processing.transforms import load_image
+
+    cfg = cfg or CurationConfig()
+    loader = loader or load_image
+    targets = sampling_targets(cfg)
+    cands: dict[int, list[ImageRecord]] = {d: [] for d in targets}
+    res = CurationResult()
+    t0 = time.time()
+    paths = list(paths)
+    for s in range(0, len(paths), batch):
+        chunk = paths[s: s + batch]
+        for p, c in zip(chunk, counter([loader(p) for p in chunk])):
+            res.total_scanned += 1
+            c = int(c)
+            if c < cfg.min_detections:
+                res.skipped_low += 1
+            elif c > cfg.max_detections:
+                res.skipped_high += 1
+            else:
+                cands[c].append(ImageRecord(str(p), c))
+        if log and (s // batch) % 20 == 0:
+            log(f"curate: scanned {res.total_scanned}/{len(paths)}, {time.time() - t0:.1f}s")
+    res.images = sample_balanced(cands, cfg)
+    res.total_selected = len(res.images)
+    return res, make_manifest(res, cfg, source="local image collection")
+
+
 def load_manifest_images(man: DatasetManifest) -> list[np.ndarray]:
     seed = int(man.config.get("stream_seed", 7))
     return [stream_image(seed, int(r["filename"].rsplit("_", 1)[1])) for r in man.images]

@@ -87,7 +87,7 @@ def build_app(arch: str, settings, info):
             yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
             from ..engine.pipeline import resolve_dtype
 
-            blob = plan_pipeline(yolo, mnet, conf_thr=0.5, iou_thr=0.45,
+            blob = plan_pipeline(yolo, mnet, conf_thr=0.0, iou_thr=0.0,  # weights only: thresholds unused
                                  dtype=resolve_dtype()).weights if info.is_main else None
             blob = D.broadcast_blob(blob, info)
             db = get_triton_config().get("dynamic_batching", {}) or {}

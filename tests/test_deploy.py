@@ -103,11 +103,64 @@ def test_prometheus_scrape_config():
     jobs = {j["job_name"]: j for j in p["scrape_configs"]}
     assert {"prometheus", "arena-services", "arena-model-server", "arena-gpu", "cadvisor"} <= set(jobs)
     targets = [t for sc in jobs["arena-services"]["static_configs"] for t in sc["targets"]]
-    assert {"127.0.0.1:8100", "127.0.0.1:8200", "127.0.0.1:8300"} <= set(targets)
+    assert {"monolithic:8100", "detection:8200", "gateway:8300"} <= set(targets)
     archs = {sc["labels"]["architecture"] for sc in jobs["arena-services"]["static_configs"]}
     assert archs == {"monolithic", "microservices", "triton"}
     ms = [t for sc in jobs["arena-model-server"]["static_configs"] for t in sc["targets"]]
     assert any(t.endswith(":8002") for t in ms)
+    local = yaml.safe_load((ROOT / "monitoring" / "prometheus.local.yml").read_text())
+    lt = [t for j in local["scrape_configs"] for sc in j["static_configs"] for t in sc["targets"]]
+    assert all(t.startswith("127.0.0.1:") for t in lt)  # process mode
+
+
+def _container_ports(svc) -> set[int]:
+    ports = {int(str(p).split(":")[-1]) for p in svc.get("ports", [])}
+    return ports | {int(p) for p in svc.get("expose", [])}
+
+
+def test_every_scrape_target_resolves_to_a_compose_service(compose):
+    """Inside the compose network 127.0.0.1 is the Prometheus container itself: every target must
+    name a compose service that listens on that port."""
+    p = yaml.safe_load(PROM.read_text())
+    svcs = compose["services"]
+    for job in p["scrape_configs"]:
+        for sc in job["static_configs"]:
+            for t in sc["targets"]:
+                host, port = t.rsplit(":", 1)
+                assert host in svcs, (job["job_name"], t)
+                assert int(port) in _container_ports(svcs[host]), (job["job_name"], t)
+
+
+def test_resource_limits_on_every_service_container(compose):
+    """Reference: every container is limited to ${CONTAINER_VCPU:-2} CPUs / ${CONTAINER_MEMORY:-4096}M
+    (reference architectures/monolithic/docker-compose.yml:95-98)."""
+    for name in ("init-models", "monolithic", "classification", "detection", "model-server", "gateway",
+                 "gpu-exporter"):
+        lim = compose["services"][name]["deploy"]["resources"]["limits"]
+        assert lim["cpus"].startswith("${CONTAINER_VCPU") and lim["memory"].startswith("${CONTAINER_MEMORY"), name
+    env = (ROOT / ".env.example").read_text()
+    assert "CONTAINER_VCPU=" in env and "CONTAINER_MEMORY=" in env
+
+
+def test_monitoring_stack_has_cadvisor_and_gpu_exporter(compose):
+    s = compose["services"]
+    assert s["cadvisor"]["privileged"] is True and "8080:8080" in s["cadvisor"]["ports"]
+    assert s["gpu-exporter"]["command"][:3] == ["python", "-m", "inference_arena_amd.metrics.gpu"]
+    assert "/dev/kfd" in s["gpu-exporter"]["devices"]
+
+
+def test_per_arm_compose_files_in_sync():
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, str(ROOT / "scripts" / "gen_compose.py"), "--check"], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for arm, must in (("monolithic", {"init-models", "monolithic"}), ("microservices", {"classification", "detection"}),
+                      ("triton", {"model-server", "gateway"}), ("infra", {"prometheus", "grafana", "cadvisor"})):
+        doc = yaml.safe_load((ROOT / "deploy" / "compose" / f"{arm}.yml").read_text())
+        assert must <= set(doc["services"]), arm
+        assert doc["networks"]["backend"]["name"] == "inference-arena-backend"
 
 
 @pytest.mark.parametrize("arch", ["monolithic", "microservices", "triton"])
@@ -135,7 +188,10 @@ def test_grafana_provisioning():
 
 def test_ci_workflow_runs_cpu_and_gpu_tiers():
     w = yaml.safe_load((ROOT / ".github" / "workflows" / "ci.yml").read_text())
-    assert {"cpu-tests", "gpu-tests"} <= set(w["jobs"])
+    assert {"cpu-tests", "gpu-tests", "code-quality", "build", "validate-config", "program-bounds", "compose-check",
+            "security", "single-source-of-truth", "summary"} <= set(w["jobs"])
+    v = yaml.safe_load((ROOT / ".github" / "workflows" / "validate-experiment-config.yml").read_text())
+    assert "validate" in v["jobs"]
     text = (ROOT / ".github" / "workflows" / "ci.yml").read_text()
     assert 'not gpu' in text and "-m gpu" in text
 
@@ -145,7 +201,9 @@ def test_env_template_keys_are_known_settings():
     known = set(Settings.model_fields) | {"ARENA_FUSE_IR", "ARENA_CONV_IMPL", "HSA_ENABLE_IPC_MODE_LEGACY",
                                           "MASTER_ADDR", "GRAFANA_ADMIN_USER", "GRAFANA_ADMIN_PASSWORD",
                                           "PROMETHEUS_PORT", "GRAFANA_PORT", "MINIO_INTERNAL_ENDPOINT",
-                                          "MINIO_ACCESS_KEY", "MINIO_SECRET_KEY", "MINIO_BUCKET", "MINIO_SECURE"}
+                                          "MINIO_ACCESS_KEY", "MINIO_SECRET_KEY", "MINIO_BUCKET", "MINIO_SECURE",
+                                          # compose interpolation (deploy/docker-compose.yml)
+                                          "CONTAINER_VCPU", "CONTAINER_MEMORY", "GPUS", "LAST_GPU", "ARENA_DTYPE"}
     assert set(env) <= known, set(env) - known
     # the template's values are valid settings (inline comments stripped)
     s = Settings(**{k: v for k, v in env.items() if k in Settings.model_fields})
