@@ -131,7 +131,10 @@ void py_ir_block(const py::dict& d) {
   p.B = req<int>(d, "B");
   p.bdev = ptr<const int*>(d, "bdev");
   prepare_kernels();
-  ir_block(p, stream_of(d));
+  if (get<int>(d, "f32", 0))
+    ir_block_f32(p, stream_of(d));
+  else
+    ir_block(p, stream_of(d));
 }
 
 void py_sppf(const py::dict& d) {

@@ -1,0 +1,241 @@
+// Fused MobileNetV2 inverted residual in exact fp32 (the fp32 counterpart of
+// ir_block.hip).  Reference computation (ONNX Runtime fp32 per crop,
+// architectures/monolithic/app/inference.py:196 running torchvision's
+// mobilenet_v2): Conv1x1+BN+Clip (expand) -> depthwise Conv3x3+BN+Clip ->
+// Conv1x1+BN (project) [-> Add].
+//
+// Unfused, the fp32 expanded tensor of the 112x112 blocks is 112x112x96x4 B =
+// 4.8 MB per crop and crosses HBM twice; the profile of the unfused fp32
+// program put the >= 28x28 MobileNetV2 blocks at ~1.7 ms per batch of 32
+// requests (profiles/r2_fp32_lds_ops.md), almost all memory traffic.  Here one
+// workgroup owns a TH x TW output tile of one crop:
+//
+//   X halo tile ((TH-1)*S+3 x (TW-1)*S+3 pixels, zero outside the image) ... LDS
+//   for each chunk of 32 hidden channels:
+//     E = relu6(X . We^T + be), zeroed outside the image   v_mfma_f32_16x16x4_f32 -> LDS
+//         (the depthwise conv pads the *expanded* map with zeros)
+//     D = relu6(dw3x3_S(E) + bd)                            fp32 FMA (VALU)          -> LDS
+//     acc += Wp[:, chunk] . D                               v_mfma_f32_16x16x4_f32, registers
+//   y = acc + bp (+ x)                                      fp32 NHWC, 16-byte stores
+//
+// Operand reads use the float4-per-lane k mapping of conv_f32.hip (lane l holds
+// k = 4*(l>>4) .. +3 of a 16-deep K chunk, consumed by four MFMAs).  LDS rows
+// are padded to K + 4 floats (an odd multiple of 4): the 8 rows of a
+// ds_read_b128 lane group start in distinct 4-bank groups.
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "launch.h"
+
+namespace arena {
+
+namespace {
+
+constexpr int IRF_HC = 32;            // hidden channels per chunk
+constexpr int IRF_EP = IRF_HC + 4;    // E / D row pitch (floats)
+
+__device__ __forceinline__ float f4c(const float4& v, int s) {
+  return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
+}
+
+__device__ __forceinline__ float4 relu6x4(float4 v) {
+  return make_float4(relu6f(v.x), relu6f(v.y), relu6f(v.z), relu6f(v.w));
+}
+
+}  // namespace
+
+template <int S, int TH, int TW, int NTO, bool EXPAND>
+__global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
+  constexpr int PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
+  constexpr int POUT = TH * TW, MT_OUT = POUT / 16;
+  static_assert(POUT % 16 == 0, "output tile must be a multiple of 16 pixels");
+  constexpr int PAIRS = MT_OUT * NTO, PPW = (PAIRS + 3) / 4;
+  extern __shared__ __attribute__((aligned(16))) float irf_lds[];
+  const int XP = p.inp_pad + 4;
+  float* Xs = irf_lds;                                   // [ROWS][XP]
+  float* Es = Xs + ROWS * XP;                            // [ROWS][IRF_EP] (EXPAND)
+  float* Ds = Es + (EXPAND ? ROWS * IRF_EP : 0);         // [POUT][IRF_EP]
+  float* Ms = Ds + POUT * IRF_EP;                        // [ROWS] 1 inside the image, 0 outside
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int tiles_x = (p.Wo + TW - 1) / TW, tiles_y = (p.Ho + TH - 1) / TH;
+  const int tiles = tiles_x * tiles_y;
+  const int b = blockIdx.x / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int t = blockIdx.x - b * tiles;
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  const float* xb = (const float*)p.x + (size_t)b * p.H * p.W * p.x_cs;
+  const float* we = (const float*)p.we;
+  const float* wd = (const float*)p.wd;
+  const float* wp = (const float*)p.wp;
+
+  // ---- A: the input halo tile (channels >= inp and pixels outside the image are zero)
+  const int cg = p.inp_pad >> 2;
+  for (int i = tid; i < ROWS * cg; i += 256) {
+    const int r = i / cg, g = i - r * cg;
+    const int iy = iy0 + r / PW, ix = ix0 + r % PW;
+    const bool in = r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (in && 4 * g < p.inp) v = *(const float4*)(xb + ((size_t)iy * p.W + ix) * p.x_cs + 4 * g);
+    *(float4*)&Xs[r * XP + 4 * g] = v;
+    if (g == 0) Ms[r] = in ? 1.f : 0.f;
+  }
+  __syncthreads();
+
+  f32x4 acc[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int h0 = 0; h0 < p.hid_pad; h0 += IRF_HC) {
+    // ---- B: expand GEMM for this chunk, rows = hidden channel, columns = halo pixel
+    const float* E;
+    int ep;
+    if constexpr (EXPAND) {
+      for (int tt = wave; tt < MT_IN * 2; tt += 4) {
+        const int mt = tt >> 1, nt = tt & 1;
+        f32x4 e = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* wrow = we + (size_t)(h0 + nt * 16 + col) * p.inp_pad + 4 * kq;
+        const float* xrow = Xs + (mt * 16 + col) * XP + 4 * kq;
+        for (int kc = 0; kc < p.inp_pad; kc += 16) {
+          const float4 a = *(const float4*)(wrow + kc);
+          const float4 bb = *(const float4*)(xrow + kc);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) e = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(a, s), f4c(bb, s), e, 0, 0, 0);
+        }
+        const int pix = mt * 16 + col;
+        const int hc = nt * 16 + 4 * kq;
+        const float4 be = *(const float4*)((const float*)p.be + h0 + hc);
+        const float m = Ms[pix];
+        float4 v = make_float4(relu6f(e[0] + be.x) * m, relu6f(e[1] + be.y) * m, relu6f(e[2] + be.z) * m,
+                               relu6f(e[3] + be.w) * m);
+        *(float4*)&Es[pix * IRF_EP + hc] = v;
+      }
+      __syncthreads();
+      E = Es;
+      ep = IRF_EP;
+    } else {
+      E = Xs + h0;  // t = 1 block: the depthwise runs on the input channels themselves
+      ep = XP;
+    }
+
+    // ---- C: depthwise 3x3 (stride S) + bias + ReLU6 on the chunk; 4 channels per thread item
+    {
+      const int g = tid & 7;  // channel group of this thread (256 % 8 == 0: fixed across items)
+      float4 wk[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)(wd + (size_t)k * p.hid_pad + h0 + 4 * g);
+      const float4 bd = *(const float4*)((const float*)p.bd + h0 + 4 * g);
+      for (int q = tid >> 3; q < POUT; q += 32) {
+        const int oy = q / TW, ox = q - oy * TW;
+        float4 a = bd;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const float4 v = *(const float4*)&E[((oy * S + ky) * PW + ox * S + kx) * ep + 4 * g];
+            const float4 w = wk[ky * 3 + kx];
+            a.x = fmaf(v.x, w.x, a.x);
+            a.y = fmaf(v.y, w.y, a.y);
+            a.z = fmaf(v.z, w.z, a.z);
+            a.w = fmaf(v.w, w.w, a.w);
+          }
+        *(float4*)&Ds[q * IRF_EP + 4 * g] = relu6x4(a);
+      }
+    }
+    __syncthreads();
+
+    // ---- D: project GEMM accumulate, rows = output channel, columns = output pixel
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int pr = wave + 4 * j;
+      if (pr >= PAIRS) break;
+      const int mt = pr / NTO, nt = pr - mt * NTO;
+      const float* wrow = wp + (size_t)(nt * 16 + col) * p.hid_pad + h0 + 4 * kq;
+      const float* drow = Ds + (mt * 16 + col) * IRF_EP + 4 * kq;
+#pragma unroll
+      for (int kc = 0; kc < IRF_HC; kc += 16) {
+        const float4 a = *(const float4*)(wrow + kc);
+        const float4 bb = *(const float4*)(drow + kc);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(a, s), f4c(bb, s), acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: + bias (+ residual) -> NHWC fp32
+  float* yb = (float*)p.y + (size_t)b * p.Ho * p.Wo * p.y_cs;
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int pr = wave + 4 * j;
+    if (pr >= PAIRS) break;
+    const int mt = pr / NTO, nt = pr - mt * NTO;
+    const int q = mt * 16 + col;
+    const int oy = oy0 + q / TW, ox = ox0 + q % TW;
+    const int co = nt * 16 + 4 * kq;
+    if (oy >= p.Ho || ox >= p.Wo || co >= p.oup) continue;
+    const float4 bp = *(const float4*)((const float*)p.bp + co);
+    float4 v = make_float4(acc[j][0] + bp.x, acc[j][1] + bp.y, acc[j][2] + bp.z, acc[j][3] + bp.w);
+    if (p.res) {
+      const float4 r = *(const float4*)(xb + ((size_t)oy * p.W + ox) * p.x_cs + co);
+      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    *(float4*)(yb + ((size_t)oy * p.Wo + ox) * p.y_cs + co) = v;
+  }
+}
+
+// LDS bytes of one workgroup (kept <= 64 KiB: no dynamic-LDS attribute, which must not be set during capture)
+static size_t irf_lds_bytes(int S, int inp_pad, int expand) {
+  const int TH = S == 1 ? 8 : 4, TW = 8;
+  const int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
+  const size_t rows = (size_t)(PH * PW + 15) / 16 * 16;
+  return sizeof(float) * (rows * (inp_pad + 4) + (expand ? rows * IRF_EP : 0) + (size_t)TH * TW * IRF_EP + rows);
+}
+
+template <int S, int TH, int TW, int NTO, bool EXPAND>
+static void irf_launch(const IrParams& p, hipStream_t s) {
+  const size_t lds = irf_lds_bytes(S, p.inp_pad, EXPAND);
+  const int tiles = ((p.Wo + TW - 1) / TW) * ((p.Ho + TH - 1) / TH);
+  hipLaunchKernelGGL((ir_f32_kernel<S, TH, TW, NTO, EXPAND>), dim3((unsigned)(p.B * tiles)), dim3(256), lds, s, p);
+}
+
+template <int S, int TH, int TW, bool EXPAND>
+static bool irf_nto(const IrParams& p, hipStream_t s) {
+  switch (p.oup_pad / 16) {
+    case 1: irf_launch<S, TH, TW, 1, EXPAND>(p, s); return true;
+    case 2: irf_launch<S, TH, TW, 2, EXPAND>(p, s); return true;
+    case 4: irf_launch<S, TH, TW, 4, EXPAND>(p, s); return true;
+    case 6: irf_launch<S, TH, TW, 6, EXPAND>(p, s); return true;
+    default: return false;
+  }
+}
+
+bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand) {
+  const int nto = oup_pad / 16;
+  return (stride == 1 || stride == 2) && inp_pad % 16 == 0 && hid_pad % IRF_HC == 0 && oup_pad % 16 == 0 &&
+         (nto == 1 || nto == 2 || nto == 4 || nto == 6) && (expand || hid_pad == inp_pad) &&
+         irf_lds_bytes(stride, inp_pad, expand) <= 64 * 1024;
+}
+
+void ir_block_f32(const IrParams& p, hipStream_t s) {
+  if (!ir_block_f32_supported(p.stride, p.inp_pad, p.hid_pad, p.oup_pad, p.expand) || p.inp % 4 || p.oup % 4 ||
+      p.inp > p.inp_pad || p.oup > p.oup_pad || p.x_cs % 4 || p.y_cs % 4)
+    throw std::runtime_error("ir_block_f32: unsupported channel geometry");
+  if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_block_f32: residual needs s1, inp == oup");
+  if (p.Ho != (p.H + 2 - 3) / p.stride + 1 || p.Wo != (p.W + 2 - 3) / p.stride + 1)
+    throw std::runtime_error("ir_block_f32: output size mismatch");
+  if (p.B <= 0) return;
+  bool ok;
+  if (p.stride == 1)
+    ok = p.expand ? irf_nto<1, 8, 8, true>(p, s) : irf_nto<1, 8, 8, false>(p, s);
+  else
+    ok = p.expand ? irf_nto<2, 4, 8, true>(p, s) : irf_nto<2, 4, 8, false>(p, s);
+  if (!ok) throw std::runtime_error("ir_block_f32: no kernel for oup_pad " + std::to_string(p.oup_pad));
+}
+
+}  // namespace arena

@@ -361,7 +361,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
     // field 47: activation precision of the op (0 bf16, 1 exact fp32; planner.OP_DTYPE_FIELD)
     const bool f32 = r[kDtypeField] == 1;
     const int eb = f32 ? 4 : 2;
-    if (f32 && (r[0] == OP_IRBLOCK || r[0] == OP_STEMFUSED || r[0] == OP_C3FUSED || r[0] == OP_HEADPOOL))
+    if (f32 && (r[0] == OP_STEMFUSED || r[0] == OP_C3FUSED || r[0] == OP_HEADPOOL))
       throw std::runtime_error("op " + std::to_string(r[0]) + " has no fp32 kernel");
     switch (r[0]) {
       case OP_CONV: {
@@ -436,7 +436,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       }
       case OP_IRBLOCK: {
         IrParams p{};
-        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.x = resolve(bk, sl, r[1], r[2], eb);
         p.x_cs = (int)r[3];
         p.H = (int)r[4];
         p.W = (int)r[5];
@@ -454,13 +454,16 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.bd = (const float*)(W + r[17]);
         p.wp = W + r[18];
         p.bp = (const float*)(W + r[19]);
-        p.y = resolve(bk, sl, r[20], r[21], 2);
+        p.y = resolve(bk, sl, r[20], r[21], eb);
         p.y_cs = (int)r[22];
         p.Ho = (int)r[23];
         p.Wo = (int)r[24];
         p.B = batch(r[25]);
         p.bdev = bdev(r[25]);
-        ir_block(p, s);
+        if (f32)
+          ir_block_f32(p, s);
+        else
+          ir_block(p, s);
         break;
       }
       case OP_SPPF: {

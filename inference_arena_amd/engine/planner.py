@@ -171,13 +171,14 @@ def pack_conv_weight(w: torch.Tensor, b: torch.Tensor, dtype: str = "bf16") -> t
     return (f32_bytes(wk) if dtype == "fp32" else bf16_bytes(wk)), bb.numpy().tobytes(), kpad, cpad
 
 
-def pack_ir_weights(expand, dw, project, inp: int) -> dict:
-    """Padded operand layouts of the fused inverted-residual kernel (csrc/kernels/ir_block.hip):
-    we [hid_pad][inp_pad], wd [9][hid_pad], wp [oup_pad][hid_pad] (bf16) + fp32 biases."""
+def pack_ir_weights(expand, dw, project, inp: int, k_align: int = 32) -> dict:
+    """Padded operand layouts of the fused inverted-residual kernels (csrc/kernels/ir_block.hip, ir_f32.hip):
+    we [hid_pad][inp_pad], wd [9][hid_pad], wp [oup_pad][hid_pad] + fp32 biases.  ``k_align``: inp_pad
+    granularity (32 for the bf16 MFMA K-step, 16 for the fp32 kernel's K-chunk)."""
     wd, bd = dw
     wp, bp = project
     hid, oup = wd.shape[0], wp.shape[0]
-    inp_pad = _round(inp, 32)
+    inp_pad = _round(inp, k_align)
     hid_pad = inp_pad if expand is None else _round(hid, 32)
     oup_pad = _round(oup, 16)
     if expand is None and hid != inp:
@@ -314,15 +315,15 @@ class ProgramBuilder:
                  kind: int = CROPS) -> None:
         """Fused inverted residual: ``expand`` = (w [hid,inp,1,1], b) or None (t = 1 blocks),
         ``dw`` = (w [hid,1,3,3], b), ``project`` = (w [oup,hid,1,1], b); BN already folded."""
-        self._bf16_only("ir_block")
         if dst.C != project[0].shape[0]:
             raise ValueError(f"ir_block: destination C {dst.C} != oup {project[0].shape[0]}")
-        pk = pack_ir_weights(expand, dw, project, src.C)
+        pk = pack_ir_weights(expand, dw, project, src.C, k_align=16 if self.f32 else 32)
         inp, inp_pad, hid_pad, oup, oup_pad = pk["inp"], pk["inp_pad"], pk["hid_pad"], pk["oup"], pk["oup_pad"]
         f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
-        offs = [self.weights.add(bf16_bytes(pk["we"])), self.weights.add(f32(pk["be"])),
-                self.weights.add(bf16_bytes(pk["wd"])), self.weights.add(f32(pk["bd"])),
-                self.weights.add(bf16_bytes(pk["wp"])), self.weights.add(f32(pk["bp"]))]
+        mat = f32 if self.f32 else bf16_bytes  # exact-fp32 programs keep fp32 weights
+        offs = [self.weights.add(mat(pk["we"])), self.weights.add(f32(pk["be"])),
+                self.weights.add(mat(pk["wd"])), self.weights.add(f32(pk["bd"])),
+                self.weights.add(mat(pk["wp"])), self.weights.add(f32(pk["bp"]))]
         H, W = src.buf.H, src.buf.W
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
         rec = [OP_IRBLOCK, src.bid, src.coff, src.cs, H, W, inp, inp_pad, hid_pad, oup, oup_pad, stride,

@@ -234,7 +234,21 @@ def ir_crop_default() -> bool:
     return os.environ.get("ARENA_IR_CROP", "1").lower() not in ("0", "false", "no", "off")
 
 
+def fuse_block_f32(blk, H: int) -> bool:
+    """fp32 policy (csrc/kernels/ir_f32.hip): fuse the memory-bound blocks at >= 28x28 input, where the
+    unfused fp32 expanded map (up to 4.8 MB per crop) round-trips HBM; below that the batched 1x1 GEMMs
+    are compute-bound and stay unfused."""
+    from .validate import ir_f32_supported
+
+    inp_pad = (blk.inp + 15) // 16 * 16
+    hid_pad = inp_pad if blk.expand is None else (blk.hidden + 31) // 32 * 32
+    oup_pad = (blk.oup + 15) // 16 * 16
+    return H >= 28 and ir_f32_supported(blk.stride, inp_pad, hid_pad, oup_pad, int(blk.expand is not None))
+
+
 def fuse_block(blk, H: int, policy) -> bool:
+    if policy == "f32":
+        return fuse_block_f32(blk, H)
     """``auto``: fuse where the tile kernel wins on MI355X — blocks at >= 28x28 input and the stride-1
     14x14 blocks (hid 576: 46 us fused vs 28 + 18 + 17 us as expand / depthwise / project ops;
     profiles/r1_irpolicy14_ops.md).  The 14 -> 7 stride-2 block and the 7x7 blocks have one
@@ -265,8 +279,9 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
     h = S // 2
     if fuse_stem is None:
         fuse_stem = fuse_stem_default()
-    if pb.f32:  # the fused MobileNet kernels are bf16-only
-        fuse_ir, fuse_stem = "none", False
+    if pb.f32:  # fp32: the fused stem is bf16-only; blocks fuse by the fp32 policy (fuse_block_f32)
+        fuse_stem = False
+        fuse_ir = "f32" if fuse_ir in ("auto", True, "all", "f32") else "none"
     w, b = fold(m.stem)
     b0 = m.blocks[0]
     first_fused = (fuse_stem and crops is not None and fuse_stem_ir_default() and S % 32 == 0

@@ -46,6 +46,21 @@ class ProgramError(ValueError):
     pass
 
 
+def ir_f32_lds_bytes(stride: int, inp_pad: int, expand: bool) -> int:
+    """LDS of one csrc/kernels/ir_f32.hip workgroup (must mirror irf_lds_bytes)."""
+    th, tw = (8, 8) if stride == 1 else (4, 8)
+    ph, pw = (th - 1) * stride + 3, (tw - 1) * stride + 3
+    rows = (ph * pw + 15) // 16 * 16
+    return 4 * (rows * (inp_pad + 4) + (rows * 36 if expand else 0) + th * tw * 36 + rows)
+
+
+def ir_f32_supported(stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
+    """Mirror of arena::ir_block_f32_supported."""
+    return (stride in (1, 2) and inp_pad % 16 == 0 and hid_pad % 32 == 0 and oup_pad % 16 == 0
+            and oup_pad // 16 in (1, 2, 4, 6) and (bool(expand) or hid_pad == inp_pad)
+            and ir_f32_lds_bytes(stride, inp_pad, bool(expand)) <= 64 * 1024)
+
+
 def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand_cap: int,
                      raw_out_bytes: int | None = None) -> None:
     sizes = {}
@@ -82,7 +97,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         if off < 0 or off + n > wbytes:
             raise ProgramError(f"op {i}: {what} reads weights [{off}, {off + n}) of {wbytes}")
 
-    fused = (OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL)
+    fused = (OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL)
     for i, r in enumerate(prog.ops):
         op = int(r[0])
         kind_n = lambda k: crop_cap if int(k) == CROPS else B  # noqa: E731
@@ -127,19 +142,22 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             n = kind_n(r[25])
             H, W, inp, inp_pad, hid_pad, oup, oup_pad, S = (int(v) for v in r[4:12])
             Ho, Wo = int(r[23]), int(r[24])
-            if inp_pad % 32 or hid_pad % 32 or oup_pad % 16 or inp > inp_pad or oup > oup_pad or inp % 8:
+            if inp_pad % (16 if f32 else 32) or hid_pad % 32 or oup_pad % 16 or inp > inp_pad or oup > oup_pad \
+                    or inp % (4 if f32 else 8):
                 raise ProgramError(f"op {i}: bad ir_block channel geometry")
+            if f32 and not ir_f32_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])):
+                raise ProgramError(f"op {i}: no fp32 fused kernel for this block")
             if Ho != (H - 1) // S + 1 or Wo != (W - 1) // S + 1:
                 raise ProgramError(f"op {i}: ir_block output size mismatch")
             if int(r[13]) and (S != 1 or inp != oup):
                 raise ProgramError(f"op {i}: ir_block residual needs stride 1 and inp == oup")
-            view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, 2, "ir input")
-            view(i, r[20], int(r[21]), int(r[22]), n * Ho * Wo, oup, 2, "ir output")
-            weights(i, int(r[14]), hid_pad * inp_pad * 2, "ir expand weight")
+            view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, el, "ir input")
+            view(i, r[20], int(r[21]), int(r[22]), n * Ho * Wo, oup, el, "ir output")
+            weights(i, int(r[14]), hid_pad * inp_pad * el, "ir expand weight")
             weights(i, int(r[15]), hid_pad * 4, "ir expand bias")
-            weights(i, int(r[16]), 9 * hid_pad * 2, "ir dw weight")
+            weights(i, int(r[16]), 9 * hid_pad * el, "ir dw weight")
             weights(i, int(r[17]), hid_pad * 4, "ir dw bias")
-            weights(i, int(r[18]), oup_pad * hid_pad * 2, "ir project weight")
+            weights(i, int(r[18]), oup_pad * hid_pad * el, "ir project weight")
             weights(i, int(r[19]), oup_pad * 4, "ir project bias")
         elif op == OP_SPPF:
             n = kind_n(r[7])

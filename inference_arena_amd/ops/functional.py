@@ -96,16 +96,18 @@ def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: boo
     from ..engine.planner import pack_ir_weights
 
     B, H, W, C = x.shape
-    pk = pack_ir_weights(expand, dw, project, C)
+    f32 = x.dtype == torch.float32  # exact-fp32 kernel (csrc/kernels/ir_f32.hip)
+    pk = pack_ir_weights(expand, dw, project, C, k_align=16 if f32 else 32)
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
-    y = torch.empty(B, Ho, Wo, pk["oup"], dtype=torch.bfloat16, device=x.device)
-    dev = {k: (pk[k].to(torch.bfloat16) if k in ("we", "wd", "wp") else pk[k].float()).contiguous().to(x.device)
+    y = torch.empty(B, Ho, Wo, pk["oup"], dtype=x.dtype, device=x.device)
+    mat = torch.float32 if f32 else torch.bfloat16
+    dev = {k: (pk[k].to(mat) if k in ("we", "wd", "wp") else pk[k].float()).contiguous().to(x.device)
            for k in ("we", "be", "wd", "bd", "wp", "bp")}
     native().ir_block({"x": _ptr(x), "x_cs": C, "H": H, "W": W, "inp": C, "inp_pad": pk["inp_pad"],
                        "hid_pad": pk["hid_pad"], "oup": pk["oup"], "oup_pad": pk["oup_pad"], "stride": stride,
                        "expand": int(expand is not None), "res": int(res),
                        **{k: _ptr(v) for k, v in dev.items()}, "y": _ptr(y), "y_cs": pk["oup"], "Ho": Ho,
-                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "stream": _stream()})
+                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32)})
     torch.cuda.synchronize(x.device)  # keep the packed weights alive until the kernel ran
     return y
 

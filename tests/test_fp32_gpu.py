@@ -230,3 +230,45 @@ def test_fp32_split_programs_match_pipeline(dense_models, device):
             crops = [extract_crop(im, np.concatenate([bx, [0.0, 0.0]])) for bx in a.boxes]
             out = cls.infer(crops)
             assert [int(o[0][0]) for o in out] == [int(t) for t in a.topk_idx[:, 0]]
+
+
+def _ir_ref64(x, expand, dw, project, stride, res):
+    h = x.double()
+    if expand is not None:
+        h = F.conv2d(h, expand[0].double(), expand[1].double()).clamp(0, 6)
+    C = dw[0].shape[0]
+    h = F.conv2d(h, dw[0].double(), dw[1].double(), stride=stride, padding=1, groups=C).clamp(0, 6)
+    y = F.conv2d(h, project[0].double(), project[1].double())
+    return y + x.double() if res else y
+
+
+@pytest.mark.parametrize("inp,hid,oup,stride,H,res", [
+    (32, 32, 16, 1, 40, False),    # t = 1 block (no expand), MobileNetV2 block 1 geometry
+    (16, 96, 24, 2, 37, False),    # block 2: 16 -> 24, stride 2, odd size
+    (24, 144, 24, 1, 28, True),    # block 3 (hid 144 -> 160 padded chunks), residual
+    (24, 144, 32, 2, 28, False),   # block 4
+    (32, 192, 32, 1, 28, True),    # block 5/6
+    (32, 192, 64, 2, 28, False),   # block 7 (4 output tiles of 16)
+])
+def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res):
+    g = torch.Generator().manual_seed(inp * 7 + hid + stride)
+    x = torch.randn(3, inp, H, H, generator=g)
+    expand = None if hid == inp else (torch.randn(hid, inp, 1, 1, generator=g) / inp ** 0.5,
+                                      torch.randn(hid, generator=g) * 0.1)
+    dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
+    project = (torch.randn(oup, hid, 1, 1, generator=g) / hid ** 0.5, torch.randn(oup, generator=g) * 0.1)
+    y = AF.ir_block_nhwc(_nhwc(x).to(device), expand, dw, project, stride=stride, res=res)
+    ref = _ir_ref64(x, expand, dw, project, stride, res)
+    got = y.permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs().max().item()
+    assert err < 2e-5 * (1.0 + ref.abs().max().item()), err
+
+
+def test_fp32_program_fuses_the_high_resolution_blocks():
+    from inference_arena_amd.engine.plans import plan_pipeline
+    from inference_arena_amd.models.zoo import default_models
+
+    p = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="fp32")
+    fused = [(int(o[4]), int(o[11])) for o in p.ops if int(o[0]) == 14]
+    assert [h for h, _ in fused] == [112, 112, 56, 56, 28, 28, 28]
+    assert all(int(o[47]) == 1 for o in p.ops)
