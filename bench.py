@@ -290,9 +290,14 @@ def main(argv=None) -> int:
         buckets = sorted({1, a.batch})
         pipe = GpuPipeline(yolo, mnet, device=info.local_rank, buckets=buckets, crop_cap_per_image=a.crop_cap,
                            dtype=a.dtype)
-        blob = D.broadcast_blob(pipe.program.weights if info.is_main else None, info)
         if info.world > 1:
-            pipe.ex.set_weights(blob)
+            # rank 0's folded weights, broadcast with RCCL over xGMI straight into each replica's GPU memory
+            blob = D.broadcast_blob_device(pipe.program.weights if info.is_main else None, info)
+            if blob.is_cuda:
+                pipe.ex.set_weights_device(blob.data_ptr(), blob.numel())
+            else:
+                pipe.ex.set_weights(blob.cpu().numpy())
+            torch.cuda.synchronize()
         log(f"[rank {info.rank}/{info.world} {info.backend}] {a.dtype} pipeline ready in {time.time() - t0:.1f}s; "
             f"arena MB {({b: round(v / 2**20, 1) for b, v in pipe.arena_bytes.items()})}; decode workers {workers}")
 

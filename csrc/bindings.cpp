@@ -390,6 +390,11 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init([](const py::dict& cfg) { return std::make_shared<Executor>(config_from(cfg)); }))
       .def("set_weights",
            [](Executor& e, py::array_t<uint8_t, py::array::c_style> blob) { e.set_weights(blob.data(), blob.size()); })
+      .def("set_weights_device",
+           [](Executor& e, uintptr_t ptr, size_t bytes) {
+             py::gil_scoped_release nogil;
+             e.set_weights_device((const void*)ptr, bytes);
+           })
       .def("set_program",
            [](Executor& e, py::array_t<int64_t, py::array::c_style> ops, py::array_t<int64_t, py::array::c_style> cls) {
              if (ops.ndim() != 2 || ops.shape(1) != kOpFields || cls.ndim() != 2 || cls.shape(1) != kOpFields)
@@ -397,9 +402,16 @@ PYBIND11_MODULE(_C, m) {
              e.set_program(ops.data(), (int)ops.shape(0), cls.data(), (int)cls.shape(0));
            })
       .def("add_bucket",
-           [](Executor& e, int B, py::array_t<int64_t, py::array::c_style> offs, int64_t arena_bytes) {
-             e.add_bucket(B, offs.data(), (int)offs.size(), arena_bytes);
-           })
+           [](Executor& e, int B, py::array_t<int64_t, py::array::c_style> offs, int64_t arena_bytes,
+              py::object impl) {
+             if (impl.is_none()) {
+               e.add_bucket(B, offs.data(), (int)offs.size(), arena_bytes);
+             } else {
+               const std::vector<int> v = impl.cast<std::vector<int>>();
+               e.add_bucket(B, offs.data(), (int)offs.size(), arena_bytes, &v);
+             }
+           },
+           py::arg("B"), py::arg("offsets"), py::arg("arena_bytes"), py::arg("impl") = py::none())
       .def("buckets", &Executor::buckets)
       .def("crop_cap_for", &Executor::crop_cap_for)
       .def("submit",

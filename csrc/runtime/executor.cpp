@@ -183,6 +183,14 @@ void Executor::set_weights(const void* host, size_t bytes) {
   weights_bytes_ = bytes;
 }
 
+void Executor::set_weights_device(const void* dev, size_t bytes) {
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  if (d_weights_ == nullptr || bytes != weights_bytes_)
+    throw std::runtime_error("set_weights_device: only a same-size update of uploaded weights is supported");
+  sync_slots();
+  ARENA_HIP_CHECK(hipMemcpy(d_weights_, dev, bytes, hipMemcpyDeviceToDevice));
+}
+
 void Executor::set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops, int n_cls_ops) {
   prog_.resize(n_ops);
   for (int i = 0; i < n_ops; ++i) std::memcpy(prog_[i].data(), ops + (size_t)i * kOpFields, sizeof(OpRecord));
@@ -221,7 +229,8 @@ void Executor::read_arena(int B, int64_t offset, void* dst, size_t bytes) {
   ARENA_HIP_CHECK(hipMemcpy(dst, it->second.d_arena[it->second.last_slot] + offset, bytes, hipMemcpyDeviceToHost));
 }
 
-void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes) {
+void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes,
+                          const std::vector<int>* impl) {
   if (B <= 0 || B > max_B_) throw std::runtime_error("add_bucket: B outside (0, max_batch]");
   if (prog_.empty()) throw std::runtime_error("add_bucket: set_program first");
   if (d_weights_ == nullptr) throw std::runtime_error("add_bucket: set_weights first");
@@ -242,7 +251,16 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
     ARENA_HIP_CHECK(hipMemset(bk.d_arena[s], 0, abytes));
   }
   bk.impl.assign(prog_.size(), 0);
-  if (autotune_) autotune(bk);
+  if (impl != nullptr) {
+    if (impl->size() != prog_.size()) throw std::runtime_error("add_bucket: tuning table does not match the program");
+    for (size_t i = 0; i < prog_.size(); ++i) {
+      const int v = (*impl)[i];
+      if (v < 0 || v > 3 || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
+      bk.impl[i] = (int8_t)v;
+    }
+  } else if (autotune_) {
+    autotune(bk);
+  }
   for (int s = 0; s < n_slots_; ++s) capture(bk, s);
   if (debug_sync_ || std::getenv("ARENA_DEBUG_ALLOC")) {
     fprintf(stderr, "[arena alloc] bucket %d arena %p..%p (%lld B)\n", B, (void*)bk.d_arena[0],

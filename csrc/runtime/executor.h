@@ -108,8 +108,13 @@ class Executor : public BatchInstance {
   Executor& operator=(const Executor&) = delete;
 
   void set_weights(const void* host, size_t bytes);
+  // Same-size update from device memory of this executor's GPU (e.g. an RCCL broadcast buffer): D2D copy.
+  void set_weights_device(const void* dev, size_t bytes);
   void set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops, int n_cls_ops);
-  void add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes);
+  // `impl` (optional, one entry per program op): conv kernel family per op from a persisted tuning table;
+  // when given, the bucket is captured with exactly these choices and no timing runs (deterministic).
+  void add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t arena_bytes,
+                  const std::vector<int>* impl = nullptr);
   std::vector<int> buckets() const override;
   int crop_cap_for(int B) const;
   const ExecutorConfig& config() const { return cfg_; }

@@ -117,10 +117,29 @@ class GpuProgramRunner:
             validate_program(program, B, cc, max_det=self.max_det, cand_cap=int(program.meta.get("cand_cap", 8400)),
                              raw_out_bytes=self.raw_out_bytes)
             offs, total = layout(program.buffers, B, cc, share=share_buffers)
-            self.ex.add_bucket(B, offs, total)
+            self._add_bucket(B, offs, total)
             self.arena_bytes[B] = total
             self.offsets[B] = offs
         self.device = device
+
+    def _add_bucket(self, B: int, offs, total: int) -> None:
+        """Capture bucket B with conv kernel choices from the persisted tuning table (engine/tuning.py)."""
+        from . import tuning
+
+        ops = self.program.ops
+        m = tuning.mode()
+        if m == "off" or not tuning.needs_tuning(ops):
+            self.ex.add_bucket(B, offs, total, [0] * len(ops) if m == "off" else None)
+            self.tuning_source = "off" if m == "off" else "n/a"
+            return
+        table = tuning.lookup(ops, B) if m == "table" else None
+        if table is not None:
+            self.ex.add_bucket(B, offs, total, table)
+            self.tuning_source = "table"
+            return
+        self.ex.add_bucket(B, offs, total)  # times every conv family, captures the fastest
+        tuning.store(ops, B, self.ex.conv_choices(B))
+        self.tuning_source = "tuned"
 
     @property
     def kind(self) -> str:

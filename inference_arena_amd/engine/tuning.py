@@ -1,0 +1,80 @@
+"""Persisted conv-kernel selection (deterministic programs across boxes).
+
+The executor can time every bf16 conv op of a bucket with each kernel family
+(csrc/runtime/executor.cpp ``autotune``) and capture the fastest; timing noise
+made the choice differ from box to box (impl2:30/impl3:21 on one
+box, 27/24 on another), so the same commit ran different programs.  Here the
+choices are a table keyed by (program fingerprint, bucket): ``ARENA_TUNING``
+
+* ``table`` (default): use the table entry when present; otherwise tune once,
+  store the choices (best effort) and use them;
+* ``retune``: tune and overwrite the entry;
+* ``off``: no timing, kernel defaults everywhere.
+
+The table lives in ``data/tuning/conv_tuning.json`` (``ARENA_TUNING_FILE``);
+tools/tune_programs.py regenerates it on a GPU box.  fp32 programs have one
+conv kernel family and need no entries.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import threading
+from pathlib import Path
+
+import numpy as np
+
+DEFAULT_FILE = Path(__file__).resolve().parents[2] / "data" / "tuning" / "conv_tuning.json"
+_lock = threading.Lock()
+
+
+def mode() -> str:
+    m = os.environ.get("ARENA_TUNING", "table").lower()
+    return m if m in ("table", "retune", "off") else "table"
+
+
+def table_path() -> Path:
+    return Path(os.environ.get("ARENA_TUNING_FILE", str(DEFAULT_FILE)))
+
+
+def fingerprint(ops: np.ndarray) -> str:
+    """Program identity: the op records (kinds, shapes, buffer ids, weight offsets), not the weight values."""
+    return hashlib.sha256(np.ascontiguousarray(ops, dtype=np.int64).tobytes()).hexdigest()[:24]
+
+
+def load_table(path: Path | None = None) -> dict:
+    p = path or table_path()
+    try:
+        return json.loads(p.read_text())
+    except (OSError, ValueError):
+        return {}
+
+
+def lookup(ops: np.ndarray, B: int, path: Path | None = None) -> list[int] | None:
+    e = load_table(path).get(f"{fingerprint(ops)}:{B}")
+    if e is None or len(e) != len(ops):
+        return None
+    return [int(v) for v in e]
+
+
+def store(ops: np.ndarray, B: int, choices: list[int], path: Path | None = None) -> bool:
+    p = path or table_path()
+    with _lock:
+        t = load_table(p)
+        t[f"{fingerprint(ops)}:{B}"] = [int(v) for v in choices]
+        try:
+            p.parent.mkdir(parents=True, exist_ok=True)
+            tmp = p.with_suffix(".tmp")
+            tmp.write_text(json.dumps(t, indent=0, sort_keys=True) + "\n")
+            tmp.replace(p)
+            return True
+        except OSError:
+            return False
+
+
+def needs_tuning(ops: np.ndarray) -> bool:
+    """Only bf16 conv ops have kernel families to choose from (OP_CONV with dtype field 0)."""
+    from .planner import OP_CONV, OP_DTYPE_FIELD
+
+    return bool(np.any((ops[:, 0] == OP_CONV) & (ops[:, OP_DTYPE_FIELD] == 0)))

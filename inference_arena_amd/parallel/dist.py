@@ -69,6 +69,23 @@ def broadcast_blob(blob: np.ndarray | None, info: DistInfo, src: int = 0) -> np.
     return t.cpu().numpy()
 
 
+def broadcast_blob_device(blob: np.ndarray | None, info: DistInfo, src: int = 0) -> torch.Tensor:
+    """As ``broadcast_blob`` but the result stays on this rank's GPU (RCCL over xGMI lands it there): hand it
+    to ``Executor.set_weights_device`` (device-to-device copy, no host round trip)."""
+    dev = _dev(info)
+    if info.world <= 1:
+        assert blob is not None
+        return torch.from_numpy(np.ascontiguousarray(blob)).to(dev)
+    n = torch.tensor([blob.nbytes if blob is not None and info.rank == src else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(n, src)
+    if info.rank == src:
+        t = torch.from_numpy(np.ascontiguousarray(blob)).to(dev)
+    else:
+        t = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
+    dist.broadcast(t, src)
+    return t
+
+
 def broadcast_object(obj, info: DistInfo, src: int = 0):
     if info.world <= 1:
         return obj

@@ -35,14 +35,43 @@ log = logging.getLogger("arena.server")
 
 
 class DecodePool:
-    def __init__(self, threads: int = 8):
-        self.pool = ThreadPoolExecutor(max_workers=max(1, threads), thread_name_prefix="decode")
+    """Upload decode off the event loop.  ``procs`` > 0 (``ARENA_DECODE_PROCS``): spawned decode processes
+    with shared-memory delivery (server/decode_pool.py; scales with cores, unlike PIL threads whose
+    numpy conversion holds the GIL); otherwise a thread pool of ``threads``."""
+
+    def __init__(self, threads: int = 8, procs: int | None = None):
+        procs = int(os.environ.get("ARENA_DECODE_PROCS", "0")) if procs is None else int(procs)
+        self.procs = None
+        self.pool = None
+        if procs > 0:
+            from .decode_pool import ProcessDecodePool
+
+            self.procs = ProcessDecodePool(workers=procs, slots=max(64, 8 * procs))
+        else:
+            self.pool = ThreadPoolExecutor(max_workers=max(1, threads), thread_name_prefix="decode")
 
     async def decode(self, data: bytes) -> np.ndarray:
-        return await asyncio.get_running_loop().run_in_executor(self.pool, load_image_from_bytes, data)
+        if self.procs is None:
+            return await asyncio.get_running_loop().run_in_executor(self.pool, load_image_from_bytes, data)
+        loop = asyncio.get_running_loop()
+        fut: asyncio.Future = loop.create_future()
+
+        def done(_tag, img, err):
+            # runs on the pool's collector thread; the shared-memory slot is reused after return: copy out
+            res = (None, err) if err is not None else (np.array(img), None)
+            loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(res))
+
+        await loop.run_in_executor(None, self.procs.submit, data, None, done)
+        img, err = await fut
+        if err is not None:
+            raise ValueError(err)
+        return img
 
     def close(self) -> None:
-        self.pool.shutdown(wait=False)
+        if self.pool is not None:
+            self.pool.shutdown(wait=False)
+        if self.procs is not None:
+            self.procs.close()
 
 
 async def read_upload(request: Request, field: str = "file") -> bytes:

@@ -203,7 +203,8 @@ def test_env_template_keys_are_known_settings():
                                           "PROMETHEUS_PORT", "GRAFANA_PORT", "MINIO_INTERNAL_ENDPOINT",
                                           "MINIO_ACCESS_KEY", "MINIO_SECRET_KEY", "MINIO_BUCKET", "MINIO_SECURE",
                                           # compose interpolation (deploy/docker-compose.yml)
-                                          "CONTAINER_VCPU", "CONTAINER_MEMORY", "GPUS", "LAST_GPU", "ARENA_DTYPE"}
+                                          "CONTAINER_VCPU", "CONTAINER_MEMORY", "GPUS", "LAST_GPU", "ARENA_DTYPE",
+                                          "ARENA_DECODE_PROCS"}
     assert set(env) <= known, set(env) - known
     # the template's values are valid settings (inline comments stripped)
     s = Settings(**{k: v for k, v in env.items() if k in Settings.model_fields})

@@ -350,26 +350,34 @@ def test_conv3x3_v3_matches_v2(device, H, Cin, Cout, s):
     _check(_nchw(y3.cpu()), _ref_conv(xn.cpu(), w, b, s, 1, "silu"))
 
 
-def test_executor_autotune_choices(device):
-    """Autotuned conv kernel choices are recorded per bucket and results match the default kernels."""
-    import os
-
+def test_executor_autotune_choices(device, tmp_path, monkeypatch):
+    """Autotuned conv kernel choices are persisted per (program, bucket) and a table-driven capture runs
+    exactly the same kernels: identical choices and bitwise-identical results (engine/tuning.py)."""
     from inference_arena_amd.data.synthetic import synthetic_images
     from inference_arena_amd.engine.pipeline import GpuPipeline
     from inference_arena_amd.models.zoo import make_mobilenet, make_yolo
 
     yolo, mnet = make_yolo(0, cls_shift=-20.0), make_mobilenet(1)
     imgs = synthetic_images(4, 77)
+    monkeypatch.setenv("ARENA_TUNING_FILE", str(tmp_path / "tuning.json"))
+    monkeypatch.setenv("ARENA_TUNING", "retune")
     pipe = GpuPipeline(yolo, mnet, device=0, buckets=[4], dtype="bf16")
+    assert pipe.tuning_source == "tuned"
     choices = pipe.ex.conv_choices(4)
     # ~50 conv ops remain once the C3 / inverted-residual / stem / head fusions have absorbed the rest
     assert set(c for c in choices if c) <= {1, 2, 3} and sum(1 for c in choices if c) >= 45
     tuned = pipe.infer(imgs)
-    os.environ["ARENA_AUTOTUNE"] = "0"
-    try:
-        plain = GpuPipeline(yolo, mnet, device=0, buckets=[4], dtype="bf16").infer(imgs)
-    finally:
-        os.environ.pop("ARENA_AUTOTUNE")
+    monkeypatch.setenv("ARENA_TUNING", "table")
+    again = GpuPipeline(yolo, mnet, device=0, buckets=[4], dtype="bf16")
+    assert again.tuning_source == "table" and again.ex.conv_choices(4) == choices
+    table = again.infer(imgs)
+    for a, b in zip(tuned, table):
+        assert len(a) == len(b)
+        ka, kb = np.lexsort(a.boxes.T), np.lexsort(b.boxes.T)
+        np.testing.assert_array_equal(a.boxes[ka], b.boxes[kb])
+        np.testing.assert_array_equal(a.topk_logit[ka], b.topk_logit[kb])
+    monkeypatch.setenv("ARENA_TUNING", "off")
+    plain = GpuPipeline(yolo, mnet, device=0, buckets=[4], dtype="bf16").infer(imgs)
     for a, b in zip(tuned, plain):
         assert abs(len(a) - len(b)) <= 1
 

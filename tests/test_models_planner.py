@@ -207,3 +207,28 @@ def test_program_variants_validate(variant):
         assert prog.meta["raw_out_bytes"] == 1000 * 4
     if variant == "classifier":
         assert prog.cls_ops.shape[0] > 0  # overflow passes re-run the classifier part
+
+
+def test_tuning_table_roundtrip(tmp_path, monkeypatch):
+    """Persisted conv kernel choices (engine/tuning.py): keyed by program fingerprint and bucket."""
+    import numpy as np
+
+    from inference_arena_amd.engine import tuning
+    from inference_arena_amd.engine.plans import plan_pipeline
+    from inference_arena_amd.models.zoo import default_models
+
+    f = tmp_path / "t.json"
+    monkeypatch.setenv("ARENA_TUNING_FILE", str(f))
+    p = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="bf16")
+    assert tuning.needs_tuning(p.ops)
+    assert not tuning.needs_tuning(plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="fp32").ops)
+    assert tuning.lookup(p.ops, 8) is None
+    ch = [2 if int(o[0]) == 1 else 0 for o in p.ops]
+    assert tuning.store(p.ops, 8, ch)
+    assert tuning.lookup(p.ops, 8) == ch and tuning.lookup(p.ops, 4) is None
+    other = p.ops.copy()
+    other[3, 4] += 1
+    assert tuning.fingerprint(other) != tuning.fingerprint(p.ops) and tuning.lookup(other, 8) is None
+    monkeypatch.setenv("ARENA_TUNING", "bogus")
+    assert tuning.mode() == "table"
+    assert np.asarray(tuning.load_table()[f"{tuning.fingerprint(p.ops)}:8"]).shape == (len(p.ops),)

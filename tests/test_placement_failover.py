@@ -4,6 +4,8 @@ failover (device fault -> replica exits -> supervisor starts a fresh process).  
 from __future__ import annotations
 
 import asyncio
+
+import numpy as np
 import os
 import sys
 import time
@@ -128,3 +130,27 @@ def test_replica_restarts_after_device_fault(tmp_path):
         assert _get(url, body, {"content-type": ctype}) == 200  # the fresh process serves
     finally:
         rep.stop()
+
+
+def test_async_decode_pool_processes():
+    """The servers' DecodePool with spawned decode processes (ARENA_DECODE_PROCS) decodes like the
+    thread path, and reports undecodable uploads."""
+    from inference_arena_amd.data.synthetic import encode_jpeg, synthetic_images
+    from inference_arena_amd.processing.transforms import load_image_from_bytes
+    from inference_arena_amd.server.app_common import DecodePool
+
+    jpegs = [encode_jpeg(im) for im in synthetic_images(4, 9, hw=(48, 64))]
+
+    async def go():
+        pool = DecodePool(procs=2)
+        try:
+            out = await asyncio.gather(*(pool.decode(j) for j in jpegs))
+            with pytest.raises(ValueError):
+                await pool.decode(b"not an image")
+            return out
+        finally:
+            pool.close()
+
+    out = asyncio.run(go())
+    for j, im in zip(jpegs, out):
+        assert np.array_equal(im, load_image_from_bytes(j))
