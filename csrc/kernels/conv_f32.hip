@@ -390,6 +390,158 @@ static int f32_conv_family() {
   return v;
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 halo-tile kernel (stride 1 or 2): a workgroup owns TH output rows x 16
+// output columns of one image and BN = NF*16 output channels.  Per 16-channel
+// input chunk it stages the input halo ((TH-1)*S+3 rows x 15*S+3 columns) and
+// the chunk's [BN][9][16] weights in LDS once, then runs all nine taps from
+// LDS: the im2col kernel above re-fetched each input pixel once per tap (9x
+// the global/L2 traffic for 3x3 convs; these convs are 2.4 ms of the fp32
+// detector, profiles/r2_fp32_irfused_ops.md).  Wave w computes output rows
+// w, w+4, ... (MF = TH/4 rows of 16 pixels) x NF channel tiles.
+constexpr int HALO_CK = 16;             // input channels per chunk
+constexpr int HALO_CP = HALO_CK + 4;    // LDS pitch of a halo pixel (floats)
+constexpr int HALO_WP = 9 * HALO_CK + 4;  // LDS pitch of a weight row (floats)
+
+template <int S, int TH, int NF>
+__global__ __launch_bounds__(256) void conv_f32_halo_kernel(const ConvParams p) {
+  constexpr int TW = 16, MF = TH / 4, BN = NF * 16;
+  constexpr int HR = (TH - 1) * S + 3, HC = (TW - 1) * S + 3, HPIX = HR * HC;
+  __shared__ __attribute__((aligned(16))) float sX[HPIX * HALO_CP];
+  __shared__ __attribute__((aligned(16))) float sW[BN * HALO_WP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int tiles_x = (p.Wo + TW - 1) / TW, tiles_y = (p.Ho + TH - 1) / TH;
+  const int tiles = tiles_x * tiles_y;
+  const int bx = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bx / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int t = bx - b * tiles;
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - p.pad_t, ix0 = ox0 * S - p.pad_l;
+  const int n0 = blockIdx.y * BN;
+  const float* __restrict__ x = (const float*)p.x + (size_t)b * p.H * p.W * p.xs;
+  const float* __restrict__ w = (const float*)p.w;
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c0 = 0; c0 < p.Cin; c0 += HALO_CK) {
+    // stage the halo (zero outside the image) and the chunk's weights
+    for (int i = tid; i < HPIX * 4; i += 256) {
+      const int px = i >> 2, g = i & 3;
+      const int hy = px / HC, hx = px - hy * HC;
+      const int iy = iy0 + hy, ix = ix0 + hx;
+      const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      *(float4*)&sX[px * HALO_CP + 4 * g] = load_f4_or_zero(x + ((size_t)iy * p.W + ix) * p.xs + c0 + 4 * g, x, ok);
+    }
+    for (int i = tid; i < BN * 36; i += 256) {  // [BN][9 taps][4 groups] float4
+      const int row = i / 36, e = i - row * 36;
+      const int tap = e >> 2, g = e & 3;
+      const int n = n0 + row;
+      const bool ok = n < p.Cout_pad;
+      *(float4*)&sW[row * HALO_WP + tap * HALO_CK + 4 * g] =
+          load_f4_or_zero(w + (size_t)n * p.Kpad + tap * p.Cin + c0 + 4 * g, w, ok);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - ky * 3;
+      float4 af[NF], bf[MF];
+#pragma unroll
+      for (int j = 0; j < NF; ++j) af[j] = *(const float4*)&sW[(j * 16 + col) * HALO_WP + tap * HALO_CK + 4 * kq];
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        const int oy = wave + 4 * f;
+        bf[f] = *(const float4*)&sX[((oy * S + ky) * HC + col * S + kx) * HALO_CP + 4 * kq];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+#pragma unroll
+          for (int f = 0; f < MF; ++f)
+            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4_get(af[j], u), f4_get(bf[f], u), acc[f][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  const int HWo = p.Ho * p.Wo;
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int cb = n0 + j * 16 + kq * 4;
+    if (cb >= p.Cout) continue;
+    const float4 bias = *(const float4*)(p.bias + cb);
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int oy = oy0 + wave + 4 * f, ox = ox0 + col;
+      if (oy >= p.Ho || ox >= p.Wo) continue;
+      const size_t pix = (size_t)b * HWo + (size_t)oy * p.Wo + ox;
+      float v[4] = {acc[f][j][0] + bias.x, acc[f][j][1] + bias.y, acc[f][j][2] + bias.z, acc[f][j][3] + bias.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      if (p.res != nullptr) {
+        const float4 rv = *(const float4*)((const float*)p.res + pix * p.rs + cb);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      }
+      const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)p.y + pix * p.ys + cb) = o;
+      if (p.y2 != nullptr) {
+        const int W2 = 2 * p.Wo;
+        float* y2 = (float*)p.y2;
+        const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+        *(float4*)(y2 + base * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + 1) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2 + 1) * p.y2s + cb) = o;
+      }
+    }
+  }
+}
+
+template <int S, int TH, int NF>
+static void launch_halo(const ConvParams& p, hipStream_t s) {
+  constexpr int BN = NF * 16;
+  const int tiles = ((p.Wo + 15) / 16) * ((p.Ho + TH - 1) / TH);
+  dim3 grid((unsigned)(p.B * tiles), (unsigned)((p.Cout_pad + BN - 1) / BN));
+  hipLaunchKernelGGL((conv_f32_halo_kernel<S, TH, NF>), grid, dim3(256), 0, s, p);
+}
+
+template <int S, int TH>
+static bool launch_halo_n(const ConvParams& p, hipStream_t s) {
+  const int ncf = p.Cout_pad / 16;
+  if (ncf == 1) launch_halo<S, TH, 1>(p, s);
+  else if (ncf == 2) launch_halo<S, TH, 2>(p, s);
+  else if (ncf == 3 || ncf == 9) launch_halo<S, TH, 3>(p, s);
+  else if (ncf == 5) launch_halo<S, TH, 5>(p, s);
+  else if (ncf % 4 == 0) launch_halo<S, TH, 4>(p, s);
+  else return false;
+  return true;
+}
+
+// Where the halo kernel runs (measured per layer on MI355X, profiles/r2_fp32_halo_ops.md vs
+// r2_fp32_irfused_ops.md): stride-1 3x3 convs on >= 40-wide maps with <= 128 input channels — the
+// s2d stem 333 -> 199 us, the 160x160 C3 bottleneck 89 -> 54 us, the 80x80 detect-head convs 375 -> 332
+// and 196 -> 171 us.  Stride-2 convs (2-3x the halo per output pixel) and the 20x20 maps (16-wide tiles
+// waste 37 % of a 20-wide row) stay on the im2col kernel, which was faster there.
+// ARENA_F32_HALO=0 disables it, =2 forces it for every eligible 3x3 conv.
+static bool halo_f32(const ConvParams& p, hipStream_t s) {
+  static const int mode = [] {
+    const char* e = std::getenv("ARENA_F32_HALO");
+    return e == nullptr ? 1 : std::atoi(e);
+  }();
+  if (mode == 0 || p.KH != 3 || p.KW != 3 || p.Cin % HALO_CK != 0 || p.Kpad != 9 * p.Cin) return false;
+  if (mode == 1 && !(p.stride == 1 && p.Wo >= 40 && p.Cin <= 128)) return false;
+  if (p.stride == 1) return launch_halo_n<1, 8>(p, s);
+  if (p.stride == 2) return launch_halo_n<2, 4>(p, s);
+  return false;
+}
+
 void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (p.Cin % 4 != 0 || p.xs % 4 != 0 || p.Kpad % 16 != 0 || p.Cout_pad % 16 != 0 || p.Cout % 4 != 0 ||
       p.Cout > p.Cout_pad || p.ys % 4 != 0)
@@ -404,6 +556,7 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
   const int ncf = p.Cout_pad / 16;
   const int impl = p.impl == 1 ? 1 : p.impl >= 2 ? 2 : f32_conv_family();
+  if (impl == 2 && halo_f32(p, s)) return;
   if (impl == 2) {
     // channel tile per workgroup (BN = WN*NF*16) by output-channel count
     if (ncf == 1)

@@ -171,7 +171,7 @@ def test_fp32_pipeline_matches_reference(dense_models, device):
     assert pipe.dtype == "fp32"
     got = pipe.infer(imgs)
     ref = ReferencePipeline(*dense_models, device="cpu")
-    n_det = n_top1 = 0
+    n_det = n_top1 = n_same_crop = 0
     rel = []
     for i, (im, g) in enumerate(zip(imgs, got)):
         r = ref(im)
@@ -186,9 +186,15 @@ def test_fp32_pipeline_matches_reference(dense_models, device):
             assert abs(float(g.scores[k]) - float(r.scores[j])) < 1e-4
             n_det += 1
             n_top1 += int(g.topk_idx[k, 0] == r.topk_idx[j, 0])
-            rel.append(abs(float(g.topk_logit[k, 0]) - float(r.topk_logit[j, 0])) / (abs(float(r.topk_logit[j, 0])) + 1e-6))
+            # the crop is the int-truncated box (reference extract_crop): a box coordinate within fp32 rounding
+            # of an integer may truncate one pixel apart, which is a different crop, not a precision error
+            if np.array_equal(np.trunc(g.boxes[k]), np.trunc(r.boxes[j])):
+                n_same_crop += 1
+                rel.append(abs(float(g.topk_logit[k, 0]) - float(r.topk_logit[j, 0]))
+                           / (abs(float(r.topk_logit[j, 0])) + 1e-6))
     assert n_det >= 20, n_det
     assert n_top1 >= 0.99 * n_det, (n_top1, n_det)
+    assert n_same_crop >= 0.95 * n_det, (n_same_crop, n_det)
     assert max(rel) < 1e-3, max(rel)
 
 
