@@ -211,16 +211,20 @@ static void launch_f32_wc(const ConvParams& p, hipStream_t s, long M) {
 // ds_read_b128.  The staging assignment gives each thread a fixed k-group (4
 // consecutive k = 4 input channels of one tap) and BM/32 fixed pixels, so the
 // im2col address math is one (tap, ci) split per chunk plus a bounds test per
-// pixel.  LDS rows are padded to 36 floats: the 8 rows a ds_read_b128 quarter-
-// wave touches start 4 banks apart (conflict-free).
-constexpr int F32_KC = 32;            // k per LDS chunk
-constexpr int F32_PITCH = F32_KC + 4;  // floats per LDS row
+// pixel.  LDS rows are padded to KC + 8 floats (see the pitch note below).
 
-template <int MF, int NF, int WM, int WN>
+template <int MF, int NF, int WM, int WN, int KC = 32>
 __global__ __launch_bounds__(256) void conv_f32_lds_kernel(const ConvParams p) {
   constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
-  constexpr int PPT = BM / 32;                      // staged pixels per thread
-  constexpr int WPT = (BN * 8 + 255) / 256;         // staged weight float4 per thread
+  // k per LDS chunk; floats per LDS row: KC + 8 makes the row pitch 2 (mod 4) 16-byte slots, which puts the
+  // 16 rows x 4 k-groups of every ds_read_b128 lane group on 16 distinct slots of the 256-B bank row
+  // (KC + 4, an odd slot count, is 2-way: 31-36 % SQ_LDS_BANK_CONFLICT in profiles/r2_fp32_pmc_ops.md)
+  constexpr int F32_KC = KC, F32_PITCH = KC + 8;
+  constexpr int GROUPS = KC / 4;                    // float4 k-groups per row
+  constexpr int RPP = 256 / GROUPS;                 // rows staged per pass of the workgroup
+  constexpr int PPT = BM / RPP;                     // staged pixels per thread
+  constexpr int WPT = (BN * GROUPS + 255) / 256;    // staged weight float4 per thread
+  static_assert(BM % RPP == 0, "pixel tile must be a multiple of the staging pass");
   __shared__ __attribute__((aligned(16))) float sB[2][BM * F32_PITCH];
   __shared__ __attribute__((aligned(16))) float sA[2][BN * F32_PITCH];
 
@@ -242,12 +246,12 @@ __global__ __launch_bounds__(256) void conv_f32_lds_kernel(const ConvParams p) {
   const int H = p.H, W = p.W, xs = p.xs, Cin = p.Cin, KW = p.KW, Kpad = p.Kpad;
   const int taps = p.KH * p.KW;
 
-  // staging roles: k-group g (4 consecutive k), pixels tid/8 + 32*j
-  const int g = tid & 7;
+  // staging roles: k-group g (4 consecutive k), pixels tid/GROUPS + RPP*j
+  const int g = tid % GROUPS;
   int pb[PPT], py[PPT], px[PPT];
 #pragma unroll
   for (int j = 0; j < PPT; ++j) {
-    const int m = m0 + (tid >> 3) + 32 * j;
+    const int m = m0 + tid / GROUPS + RPP * j;
     if (m < M) {
       const int b = m / HWo, r = m - b * HWo;
       const int oy = r / p.Wo, ox = r - oy * p.Wo;
@@ -275,20 +279,20 @@ __global__ __launch_bounds__(256) void conv_f32_lds_kernel(const ConvParams p) {
 #pragma unroll
     for (int j = 0; j < WPT; ++j) {
       const int e = tid + 256 * j;  // (row, group) of the weight tile
-      const int row = e >> 3, gg = e & 7;
+      const int row = e / GROUPS, gg = e % GROUPS;
       const int kk = kc * F32_KC + 4 * gg;
-      const bool ok = e < BN * 8 && n0 + row < p.Cout_pad && kk < Kpad;
+      const bool ok = e < BN * GROUPS && n0 + row < p.Cout_pad && kk < Kpad;
       ra[j] = load_f4_or_zero(w + (size_t)(n0 + row) * Kpad + kk, w, ok);
     }
   };
   auto sstore = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < PPT; ++j)
-      *(float4*)&sB[buf][((tid >> 3) + 32 * j) * F32_PITCH + 4 * g] = rb[j];
+      *(float4*)&sB[buf][(tid / GROUPS + RPP * j) * F32_PITCH + 4 * g] = rb[j];
 #pragma unroll
     for (int j = 0; j < WPT; ++j) {
       const int e = tid + 256 * j;
-      if (e < BN * 8) *(float4*)&sA[buf][(e >> 3) * F32_PITCH + 4 * (e & 7)] = ra[j];
+      if (e < BN * GROUPS) *(float4*)&sA[buf][(e / GROUPS) * F32_PITCH + 4 * (e % GROUPS)] = ra[j];
     }
   };
 
@@ -361,11 +365,259 @@ __global__ __launch_bounds__(256) void conv_f32_lds_kernel(const ConvParams p) {
   }
 }
 
-template <int MF, int NF, int WM, int WN>
+template <int MF, int NF, int WM, int WN, int KC = 32>
 static void launch_lds(const ConvParams& p, hipStream_t s, long M) {
   constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
   dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((p.Cout_pad + BN - 1) / BN));
-  hipLaunchKernelGGL((conv_f32_lds_kernel<MF, NF, WM, WN>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((conv_f32_lds_kernel<MF, NF, WM, WN, KC>), grid, dim3(256), 0, s, p);
+}
+
+// ---------------------------------------------------------------------------
+// fp32-accurate implicit GEMM on the bf16 matrix cores ("x3": triple-bf16
+// split).  fp32 MFMA issues at 1/16 of the bf16 rate, so the fp32 kernels above
+// are matrix-core bound.  Every fp32 operand is split exactly into three bf16
+// terms, v = h + m + l (h = rn_bf16(v), m = rn_bf16(v - h), l = rn_bf16(v - h
+// - m); each residual is exact in fp32 and 3 x 8 significant bits cover fp32's
+// 24), and the product is formed from the six partial products whose order is
+// <= 2^-16 of |a||b|:
+//   a*b ~= ah*bh + ah*bm + am*bh + ah*bl + al*bh + am*bm
+// The dropped terms (am*bl, al*bm, al*bl) are below 2^-24 |a||b| — the size of
+// fp32's own product rounding — and bf16 products are exact in the fp32
+// accumulator, so the result has fp32-level error (tests/test_fp32_gpu.py
+// compares it to fp64 next to the exact-fp32 kernel).  Six 16x16x32 bf16 MFMAs
+// (16 cycles each) replace eight 16x16x4 fp32 MFMAs (32 cycles each) per 32-deep
+// k chunk: 2.7x less matrix-core time.
+//
+// Staging is the fp32 LDS kernel's (float4 of 4 consecutive k per thread, same
+// fp32 weight blob), split on the way into LDS: a row holds the chunk's 32 k as
+// three bf16 planes [h | m | l] (96 bf16 + 16 pad = 224 B = 14 x 16-B slots:
+// a pitch of 2 (mod 4) slots keeps each ds_read_b128 lane group on 16
+// distinct slots).  Lane l reads its bf16x8 fragment (k = 8*(l>>4)..+7 of row l&15) of
+// each plane with one ds_read_b128.
+constexpr int X3_KC = 32;
+constexpr int X3_PITCH = 3 * X3_KC + 16;  // bf16 per LDS row: 14 slots = 2 (mod 4), conflict-free b128 reads
+
+__device__ __forceinline__ void split3(float v, bf16& h, bf16& m, bf16& l) {
+  h = (bf16)v;
+  const float r = v - (float)h;
+  m = (bf16)r;
+  l = (bf16)(r - (float)m);
+}
+
+__device__ __forceinline__ void store_split4(bf16* row, int k, const float4& v) {
+  bf16x4 h, m, l;
+  bf16 th, tm, tl;
+  split3(v.x, th, tm, tl); h[0] = th; m[0] = tm; l[0] = tl;
+  split3(v.y, th, tm, tl); h[1] = th; m[1] = tm; l[1] = tl;
+  split3(v.z, th, tm, tl); h[2] = th; m[2] = tm; l[2] = tl;
+  split3(v.w, th, tm, tl); h[3] = th; m[3] = tm; l[3] = tl;
+  *(bf16x4*)(row + k) = h;
+  *(bf16x4*)(row + X3_KC + k) = m;
+  *(bf16x4*)(row + 2 * X3_KC + k) = l;
+}
+
+template <int MF, int NF, int WM, int WN>
+__global__ __launch_bounds__(256) void conv_x3_lds_kernel(const ConvParams p) {
+  constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
+  constexpr int GROUPS = X3_KC / 4;              // float4 k-groups per row
+  constexpr int RPP = 256 / GROUPS;              // rows staged per pass of the workgroup
+  constexpr int PPT = BM / RPP;                  // staged pixels per thread
+  constexpr int WPT = (BN * GROUPS + 255) / 256; // staged weight float4 per thread
+  static_assert(BM % RPP == 0, "pixel tile must be a multiple of the staging pass");
+  __shared__ __attribute__((aligned(16))) bf16 sB[2][BM * X3_PITCH];
+  __shared__ __attribute__((aligned(16))) bf16 sA[2][BN * X3_PITCH];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int wm = wave % WM, wn = wave / WM;
+
+  const int Bl = live_batch(p.B, p.bdev);
+  const int HWo = p.Ho * p.Wo;
+  const int M = Bl * HWo;
+  const int bx = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = bx * BM;
+  if (m0 >= M) return;
+  const int n0 = blockIdx.y * BN;
+
+  const float* __restrict__ x = (const float*)p.x;
+  const float* __restrict__ w = (const float*)p.w;
+  const int H = p.H, W = p.W, xs = p.xs, Cin = p.Cin, KW = p.KW, Kpad = p.Kpad;
+  const int taps = p.KH * p.KW;
+
+  const int g = tid % GROUPS;
+  int pb[PPT], py[PPT], px[PPT];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    const int m = m0 + tid / GROUPS + RPP * j;
+    if (m < M) {
+      const int b = m / HWo, r = m - b * HWo;
+      const int oy = r / p.Wo, ox = r - oy * p.Wo;
+      pb[j] = b * H * W;
+      py[j] = oy * p.stride - p.pad_t;
+      px[j] = ox * p.stride - p.pad_l;
+    } else {
+      pb[j] = 0;
+      py[j] = -(1 << 20);  // fails the bounds test: zero fill
+      px[j] = 0;
+    }
+  }
+  float4 rb[PPT], ra[WPT];
+  auto gload = [&](int kc) {
+    const int k = kc * X3_KC + 4 * g;
+    const int tap = k / Cin, ci = k - tap * Cin;
+    const int kh = tap / KW, kw = tap - kh * KW;
+    const bool tv = tap < taps;
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int iy = py[j] + kh, ix = px[j] + kw;
+      const bool ok = tv && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      rb[j] = load_f4_or_zero(x + (size_t)(pb[j] + iy * W + ix) * xs + ci, x, ok);
+    }
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+      const int e = tid + 256 * j;
+      const int row = e / GROUPS, gg = e % GROUPS;
+      const int kk = kc * X3_KC + 4 * gg;
+      const bool ok = e < BN * GROUPS && n0 + row < p.Cout_pad && kk < Kpad;
+      ra[j] = load_f4_or_zero(w + (size_t)(n0 + row) * Kpad + kk, w, ok);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) store_split4(&sB[buf][(tid / GROUPS + RPP * j) * X3_PITCH], 4 * g, rb[j]);
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e < BN * GROUPS) store_split4(&sA[buf][(e / GROUPS) * X3_PITCH], 4 * (e % GROUPS), ra[j]);
+    }
+  };
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (Kpad + X3_KC - 1) / X3_KC;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    if (kc + 1 < nk) gload(kc + 1);
+    bf16x8 ah[NF], am[NF], al[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const bf16* r = &sA[cur][((wn * NF + j) * 16 + col) * X3_PITCH + 8 * kq];
+      ah[j] = *(const bf16x8*)r;
+      am[j] = *(const bf16x8*)(r + X3_KC);
+      al[j] = *(const bf16x8*)(r + 2 * X3_KC);
+    }
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const bf16* r = &sB[cur][((wm * MF + f) * 16 + col) * X3_PITCH + 8 * kq];
+      const bf16x8 bh = *(const bf16x8*)r;
+      const bf16x8 bm = *(const bf16x8*)(r + X3_KC);
+      const bf16x8 bl = *(const bf16x8*)(r + 2 * X3_KC);
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        // smallest terms first: they are added while the accumulator is smallest
+        f32x4 c = acc[f][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[j], bm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[j], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[j], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bm, c, 0, 0, 0);
+        acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bh, c, 0, 0, 0);
+      }
+    }
+    if (kc + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int cb = n0 + (wn * NF + j) * 16 + kq * 4;
+    if (cb >= p.Cout) continue;
+    const float4 bias = *(const float4*)(p.bias + cb);
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int pix = m0 + (wm * MF + f) * 16 + col;
+      if (pix >= M) continue;
+      float v[4] = {acc[f][j][0] + bias.x, acc[f][j][1] + bias.y, acc[f][j][2] + bias.z, acc[f][j][3] + bias.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      if (p.res != nullptr) {
+        const float4 rv = *(const float4*)((const float*)p.res + (size_t)pix * p.rs + cb);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      }
+      const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)p.y + (size_t)pix * p.ys + cb) = o;
+      if (p.y2 != nullptr) {
+        const int b = pix / HWo;
+        const int r = pix - b * HWo;
+        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+        const int W2 = 2 * p.Wo;
+        float* y2 = (float*)p.y2;
+        const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+        *(float4*)(y2 + base * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + 1) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2 + 1) * p.y2s + cb) = o;
+      }
+    }
+  }
+}
+
+template <int MF, int NF, int WM, int WN>
+static void launch_x3(const ConvParams& p, hipStream_t s, long M) {
+  constexpr int BM = WM * MF * 16, BN = WN * NF * 16;
+  dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((p.Cout_pad + BN - 1) / BN));
+  hipLaunchKernelGGL((conv_x3_lds_kernel<MF, NF, WM, WN>), grid, dim3(256), 0, s, p);
+}
+
+// x3 tile variants (ConvParams.impl = kF32X3 + index)
+static bool launch_x3_variant(const ConvParams& p, hipStream_t s, long M, int v) {
+  switch (v) {
+    case 0: launch_x3<2, 2, 2, 2>(p, s, M); return true;  // 64 x 64
+    case 1: launch_x3<4, 2, 2, 2>(p, s, M); return true;  // 128 x 64
+    case 2: launch_x3<2, 4, 2, 2>(p, s, M); return true;  // 64 x 128
+    case 3: launch_x3<4, 4, 2, 2>(p, s, M); return true;  // 128 x 128
+    case 4: launch_x3<2, 2, 4, 1>(p, s, M); return true;  // 128 x 32
+    case 5: launch_x3<1, 4, 4, 1>(p, s, M); return true;  // 64 x 64 (4 x 1 waves)
+    case 6: launch_x3<2, 4, 4, 1>(p, s, M); return true;  // 128 x 64 (4 x 1 waves)
+    case 7: launch_x3<1, 2, 2, 2>(p, s, M); return true;  // 32 x 64
+    case 8: launch_x3<2, 3, 4, 1>(p, s, M); return true;  // 128 x 48
+    case 9: launch_x3<2, 5, 4, 1>(p, s, M); return true;  // 128 x 80
+    case 10: launch_x3<1, 1, 4, 1>(p, s, M); return true; // 64 x 16
+    case 11: launch_x3<2, 1, 4, 1>(p, s, M); return true; // 128 x 16
+    default: return false;
+  }
+}
+
+// Explicit tile variants (ConvParams.impl = 10 + index): the sweep table of tools/bench_f32_convs.py.
+// (MF, NF, WM, WN, KC): BM = WM*MF*16 pixels x BN = WN*NF*16 channels, KC k per LDS chunk.
+static bool launch_lds_variant(const ConvParams& p, hipStream_t s, long M, int v) {
+  switch (v) {
+    case 0: launch_lds<2, 2, 2, 2, 32>(p, s, M); return true;   // 64 x 64
+    case 1: launch_lds<4, 2, 2, 2, 32>(p, s, M); return true;   // 128 x 64
+    case 2: launch_lds<2, 4, 2, 2, 32>(p, s, M); return true;   // 64 x 128
+    case 3: launch_lds<4, 4, 2, 2, 32>(p, s, M); return true;   // 128 x 128
+    case 4: launch_lds<2, 2, 2, 2, 64>(p, s, M); return true;   // 64 x 64, K64
+    case 5: launch_lds<4, 2, 2, 2, 64>(p, s, M); return true;   // 128 x 64, K64
+    case 6: launch_lds<2, 4, 2, 2, 64>(p, s, M); return true;   // 64 x 128, K64
+    case 7: launch_lds<2, 2, 4, 1, 32>(p, s, M); return true;   // 128 x 32
+    case 8: launch_lds<4, 1, 4, 1, 32>(p, s, M); return true;   // 256 x 16
+    case 9: launch_lds<2, 3, 4, 1, 32>(p, s, M); return true;   // 128 x 48
+    case 10: launch_lds<2, 5, 4, 1, 32>(p, s, M); return true;  // 128 x 80
+    case 11: launch_lds<1, 4, 4, 1, 32>(p, s, M); return true;  // 64 x 64 (4 x 1 waves)
+    case 12: launch_lds<2, 4, 4, 1, 32>(p, s, M); return true;  // 128 x 64 (4 x 1 waves)
+    case 13: launch_lds<1, 2, 2, 2, 32>(p, s, M); return true;  // 32 x 64
+    case 14: launch_lds<2, 2, 4, 1, 64>(p, s, M); return true;  // 128 x 32, K64
+    case 15: launch_lds<2, 3, 4, 1, 64>(p, s, M); return true;  // 128 x 48, K64
+    default: return false;
+  }
 }
 
 // Pixel-tile depth: the largest MF that still launches >= 2 workgroups per CU.  BM is capped at 128 pixels
@@ -399,14 +651,19 @@ static int f32_conv_family() {
 // the global/L2 traffic for 3x3 convs; these convs are 2.4 ms of the fp32
 // detector, profiles/r2_fp32_irfused_ops.md).  Wave w computes output rows
 // w, w+4, ... (MF = TH/4 rows of 16 pixels) x NF channel tiles.
+// LDS pitches (floats) chosen so every ds_read_b128 lane group (16 lanes: 16 consecutive pixels or weight
+// rows x 4 k-groups) lands on 16 distinct 16-B slots of the 256-B bank row: the stride between the lanes'
+// rows must be 2 (mod 4) slots — 6 slots per halo pixel at stride 1 (2 x 5 = 10 slots between the pixels
+// read by neighbouring lanes at stride 2), 38 slots per weight row.
 constexpr int HALO_CK = 16;             // input channels per chunk
-constexpr int HALO_CP = HALO_CK + 4;    // LDS pitch of a halo pixel (floats)
-constexpr int HALO_WP = 9 * HALO_CK + 4;  // LDS pitch of a weight row (floats)
+constexpr int HALO_WP = 9 * HALO_CK + 8;  // LDS pitch of a weight row (floats)
+__host__ __device__ constexpr int halo_cp(int S) { return S == 1 ? HALO_CK + 8 : HALO_CK + 4; }
 
 template <int S, int TH, int NF>
 __global__ __launch_bounds__(256) void conv_f32_halo_kernel(const ConvParams p) {
   constexpr int TW = 16, MF = TH / 4, BN = NF * 16;
   constexpr int HR = (TH - 1) * S + 3, HC = (TW - 1) * S + 3, HPIX = HR * HC;
+  constexpr int HALO_CP = halo_cp(S);
   __shared__ __attribute__((aligned(16))) float sX[HPIX * HALO_CP];
   __shared__ __attribute__((aligned(16))) float sW[BN * HALO_WP];
 
@@ -524,17 +781,209 @@ static bool launch_halo_n(const ConvParams& p, hipStream_t s) {
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 stride-1 halo tiles on the bf16 matrix cores with the triple-bf16 split
+// (x3, see conv_x3_lds_kernel): the large detect-head / neck 3x3 convs are the
+// one place the fp32 kernels are matrix-core bound (50-65 % MFMA busy,
+// profiles/r2_fp32_pmc_ops.md), and here each staged input element feeds nine
+// taps, so splitting it on the way into LDS costs 1/9 per use.
+//
+// Workgroup: TH = 8 output rows x 16 columns of one image x BN = NF*16 output
+// channels; wave w computes rows w and w+4 (MF = 2).  Per 32-channel input
+// chunk the (10 x 18)-pixel halo is staged once (three bf16 planes per pixel,
+// 224-B pitch = 14 slots: conflict-free ds_read_b128 for 16 consecutive
+// pixels); the chunk's weights are staged one kernel row (ky) at a time —
+// [BN][3 taps][3 planes x 32] at a 608-B (38-slot) pitch — so LDS stays at
+// 40 KB + BN x 0.6 KB.  The next stage's global loads (the next ky's weights,
+// and at ky = 2 the next chunk's halo) are issued into registers before the
+// current stage's 3 taps x MF x NF x 6 MFMAs run.  Cin need not be a multiple
+// of 32: the tail chunk's missing channels stage as zeros.
+constexpr int X3H_TH = 8, X3H_TW = 16, X3H_HR = X3H_TH + 2, X3H_HC = X3H_TW + 2, X3H_HPIX = X3H_HR * X3H_HC;
+constexpr int X3H_XP = 3 * 32 + 16;      // bf16 per halo pixel (224 B)
+constexpr int X3H_WP = 3 * 3 * 32 + 16;  // bf16 per weight row of one ky (3 taps x 3 planes x 32 k; 608 B)
+constexpr int X3H_XV = (X3H_HPIX * 8 + 255) / 256;  // halo float4 per thread
+
+template <int NF>
+__global__ __launch_bounds__(256) void conv_x3_halo_kernel(const ConvParams p) {
+  constexpr int BN = NF * 16, MF = 2;
+  constexpr int WV = (BN * 3 * 8 + 255) / 256;  // weight float4 per thread per ky stage
+  __shared__ __attribute__((aligned(16))) bf16 sX[X3H_HPIX * X3H_XP];
+  __shared__ __attribute__((aligned(16))) bf16 sW[BN * X3H_WP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int tiles_x = (p.Wo + X3H_TW - 1) / X3H_TW, tiles_y = (p.Ho + X3H_TH - 1) / X3H_TH;
+  const int tiles = tiles_x * tiles_y;
+  const int bx = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bx / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int t = bx - b * tiles;
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int oy0 = ty * X3H_TH, ox0 = tx * X3H_TW;
+  const int iy0 = oy0 - p.pad_t, ix0 = ox0 - p.pad_l;
+  const int n0 = blockIdx.y * BN;
+  const int Cin = p.Cin;
+  const float* __restrict__ x = (const float*)p.x + (size_t)b * p.H * p.W * p.xs;
+  const float* __restrict__ w = (const float*)p.w;
+
+  float4 rx[X3H_XV], rw[WV];
+  auto load_x = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < X3H_XV; ++j) {
+      const int i = tid + 256 * j;
+      const int px = i >> 3, g = i & 7;
+      const int hy = px / X3H_HC, hx = px - hy * X3H_HC;
+      const int iy = iy0 + hy, ix = ix0 + hx, c = c0 + 4 * g;
+      const bool ok = i < X3H_HPIX * 8 && c < Cin && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      rx[j] = load_f4_or_zero(x + ((size_t)iy * p.W + ix) * p.xs + c, x, ok);
+    }
+  };
+  auto load_w = [&](int c0, int ky) {
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int i = tid + 256 * j;  // (row, kx, g)
+      const int row = i / 24, e = i - row * 24;
+      const int kx = e >> 3, g = e & 7;
+      const int n = n0 + row, c = c0 + 4 * g;
+      const bool ok = i < BN * 24 && n < p.Cout_pad && c < Cin;
+      rw[j] = load_f4_or_zero(w + (size_t)n * p.Kpad + (ky * 3 + kx) * Cin + c, w, ok);
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int j = 0; j < X3H_XV; ++j) {
+      const int i = tid + 256 * j;
+      if (i < X3H_HPIX * 8) store_split4(&sX[(i >> 3) * X3H_XP], 4 * (i & 7), rx[j]);
+    }
+  };
+  auto store_w = [&]() {
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int i = tid + 256 * j;
+      if (i < BN * 24) {
+        const int row = i / 24, e = i - row * 24;
+        store_split4(&sW[row * X3H_WP + (e >> 3) * 96], 4 * (e & 7), rw[j]);
+      }
+    }
+  };
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nstage = ((Cin + 31) / 32) * 3;
+  load_x(0);
+  load_w(0, 0);
+  for (int st = 0; st < nstage; ++st) {
+    const int c0 = (st / 3) * 32, ky = st - (st / 3) * 3;
+    if (ky == 0) store_x();
+    store_w();
+    __syncthreads();
+    if (st + 1 < nstage) {  // next stage's global loads overlap this stage's MFMAs
+      const int nc0 = ((st + 1) / 3) * 32, nky = (st + 1) - ((st + 1) / 3) * 3;
+      if (nky == 0) load_x(nc0);
+      load_w(nc0, nky);
+    }
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      bf16x8 ah[NF], am[NF], al[NF];
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const bf16* r = &sW[(j * 16 + col) * X3H_WP + kx * 96 + 8 * kq];
+        ah[j] = *(const bf16x8*)r;
+        am[j] = *(const bf16x8*)(r + 32);
+        al[j] = *(const bf16x8*)(r + 64);
+      }
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        const int oy = wave + 4 * f;
+        const bf16* r = &sX[((oy + ky) * X3H_HC + col + kx) * X3H_XP + 8 * kq];
+        const bf16x8 bh = *(const bf16x8*)r;
+        const bf16x8 bm = *(const bf16x8*)(r + 32);
+        const bf16x8 bl = *(const bf16x8*)(r + 64);
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+          f32x4 c = acc[f][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[j], bm, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[j], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[j], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bm, c, 0, 0, 0);
+          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bh, c, 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  const int HWo = p.Ho * p.Wo;
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int cb = n0 + j * 16 + kq * 4;
+    if (cb >= p.Cout) continue;
+    const float4 bias = *(const float4*)(p.bias + cb);
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int oy = oy0 + wave + 4 * f, ox = ox0 + col;
+      if (oy >= p.Ho || ox >= p.Wo) continue;
+      const size_t pix = (size_t)b * HWo + (size_t)oy * p.Wo + ox;
+      float v[4] = {acc[f][j][0] + bias.x, acc[f][j][1] + bias.y, acc[f][j][2] + bias.z, acc[f][j][3] + bias.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      if (p.res != nullptr) {
+        const float4 rv = *(const float4*)((const float*)p.res + pix * p.rs + cb);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      }
+      const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)p.y + pix * p.ys + cb) = o;
+      if (p.y2 != nullptr) {
+        const int W2 = 2 * p.Wo;
+        float* y2 = (float*)p.y2;
+        const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+        *(float4*)(y2 + base * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + 1) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2 + 1) * p.y2s + cb) = o;
+      }
+    }
+  }
+}
+
+template <int NF>
+static void launch_x3_halo(const ConvParams& p, hipStream_t s) {
+  constexpr int BN = NF * 16;
+  const int tiles = ((p.Wo + X3H_TW - 1) / X3H_TW) * ((p.Ho + X3H_TH - 1) / X3H_TH);
+  dim3 grid((unsigned)(p.B * tiles), (unsigned)((p.Cout_pad + BN - 1) / BN));
+  hipLaunchKernelGGL((conv_x3_halo_kernel<NF>), grid, dim3(256), 0, s, p);
+}
+
+// impl kF32X3Halo: 3x3 stride-1 convs with Kpad == 9 * Cin (tap-major K) and Cin % 4 == 0
+static bool x3_halo(const ConvParams& p, hipStream_t s) {
+  if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.Kpad != 9 * p.Cin || p.Cin % 4 != 0) return false;
+  const int ncf = p.Cout_pad / 16;
+  if (ncf == 1) launch_x3_halo<1>(p, s);
+  else if (ncf == 2) launch_x3_halo<2>(p, s);
+  else if (ncf == 3 || ncf == 9) launch_x3_halo<3>(p, s);
+  else if (ncf == 5) launch_x3_halo<5>(p, s);
+  else if (ncf % 4 == 0) launch_x3_halo<4>(p, s);
+  else return false;
+  return true;
+}
+
 // Where the halo kernel runs (measured per layer on MI355X, profiles/r2_fp32_halo_ops.md vs
 // r2_fp32_irfused_ops.md): stride-1 3x3 convs on >= 40-wide maps with <= 128 input channels — the
 // s2d stem 333 -> 199 us, the 160x160 C3 bottleneck 89 -> 54 us, the 80x80 detect-head convs 375 -> 332
 // and 196 -> 171 us.  Stride-2 convs (2-3x the halo per output pixel) and the 20x20 maps (16-wide tiles
 // waste 37 % of a 20-wide row) stay on the im2col kernel, which was faster there.
 // ARENA_F32_HALO=0 disables it, =2 forces it for every eligible 3x3 conv.
-static bool halo_f32(const ConvParams& p, hipStream_t s) {
-  static const int mode = [] {
+static bool halo_f32(const ConvParams& p, hipStream_t s, bool force = false) {
+  static const int env_mode = [] {
     const char* e = std::getenv("ARENA_F32_HALO");
     return e == nullptr ? 1 : std::atoi(e);
   }();
+  const int mode = force ? 2 : env_mode;
   if (mode == 0 || p.KH != 3 || p.KW != 3 || p.Cin % HALO_CK != 0 || p.Kpad != 9 * p.Cin) return false;
   if (mode == 1 && !(p.stride == 1 && p.Wo >= 40 && p.Cin <= 128)) return false;
   if (p.stride == 1) return launch_halo_n<1, 8>(p, s);
@@ -555,6 +1004,23 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (M <= 0) return;
   if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
   const int ncf = p.Cout_pad / 16;
+  if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
+    if (p.impl == kF32X3Halo) {
+      if (!x3_halo(p, s)) throw std::runtime_error("conv2d_f32: not an x3-halo-eligible conv");
+      return;
+    }
+    if (p.impl == kF32Halo) {
+      if (!halo_f32(p, s, true)) throw std::runtime_error("conv2d_f32: not a halo-eligible conv");
+      return;
+    }
+    if (p.impl >= kF32X3) {
+      if (p.impl >= kF32X3 + kF32X3Variants || !launch_x3_variant(p, s, M, p.impl - kF32X3))
+        throw std::runtime_error("conv2d_f32: unknown x3 variant");
+      return;
+    }
+    if (p.impl >= 10 + kF32Variants || !launch_lds_variant(p, s, M, p.impl - 10)) throw std::runtime_error("conv2d_f32: unknown variant");
+    return;
+  }
   const int impl = p.impl == 1 ? 1 : p.impl >= 2 ? 2 : f32_conv_family();
   if (impl == 2 && halo_f32(p, s)) return;
   if (impl == 2) {

@@ -19,9 +19,21 @@
 //   y = acc + bp (+ x)                                      fp32 NHWC, 16-byte stores
 //
 // Operand reads use the float4-per-lane k mapping of conv_f32.hip (lane l holds
-// k = 4*(l>>4) .. +3 of a 16-deep K chunk, consumed by four MFMAs).  LDS rows
-// are padded to K + 4 floats (an odd multiple of 4): the 8 rows of a
-// ds_read_b128 lane group start in distinct 4-bank groups.
+// k = 4*(l>>4) .. +3 of a 16-deep K chunk, consumed by four MFMAs).
+//
+// LDS layouts (ds_read_b128 serves 16-lane groups from one 256-B bank row of
+// 16 slots of 16 B; MI355X_MICROARCH.md §LDS), measured 38-45 % bank-conflict
+// cycles with the previous odd-slot pitches (profiles/r2_fp32_pmc_ops.md):
+//   * MFMA operand rows (X for the expand GEMM, D for the project GEMM): lanes
+//     read 16 rows x 4 k-groups, conflict-free when the row pitch is 2 (mod 4)
+//     slots: K + 8 floats;
+//   * the expanded chunk E (and X of a t = 1 block, which the depthwise reads
+//     directly): the depthwise reads 8 lanes per pixel, and the expand epilogue
+//     writes 16 pixels x 4 groups; 32 floats per pixel with the group index
+//     XOR-swizzled by (p ^ 4*(p>>2)) & 7 at stride 1 makes the depthwise reads
+//     conflict-free at the cost of a 2-way conflict on the (6x rarer) epilogue
+//     writes; at stride 2 the conflict-free layout (48 floats) cost more in
+//     occupancy than it saved, so E keeps 36 floats there.
 #include <stdexcept>
 #include <string>
 
@@ -33,7 +45,16 @@ namespace arena {
 namespace {
 
 constexpr int IRF_HC = 32;            // hidden channels per chunk
-constexpr int IRF_EP = IRF_HC + 4;    // E / D row pitch (floats)
+constexpr int IRF_DP = IRF_HC + 8;    // D row pitch (floats): MFMA operand rows
+__host__ __device__ constexpr int irf_ep(int S) { return S == 1 ? IRF_HC : IRF_HC + 4; }  // E pixel pitch
+__host__ __device__ constexpr int irf_xp(int inp_pad, bool expand) { return expand ? inp_pad + 8 : inp_pad; }
+
+// swizzled 4-channel group of pixel `pix` in E (and in X of a t = 1 block)
+template <int S>
+__device__ __forceinline__ int eswz(int pix, int g) {
+  const int f = S == 1 ? ((pix ^ (4 * (pix >> 2))) & 7) : 0;
+  return (g & ~7) | ((g & 7) ^ f);
+}
 
 __device__ __forceinline__ float f4c(const float4& v, int s) {
   return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
@@ -53,11 +74,12 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
   static_assert(POUT % 16 == 0, "output tile must be a multiple of 16 pixels");
   constexpr int PAIRS = MT_OUT * NTO, PPW = (PAIRS + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) float irf_lds[];
-  const int XP = p.inp_pad + 4;
+  constexpr int EP = irf_ep(S);
+  const int XP = irf_xp(p.inp_pad, EXPAND);
   float* Xs = irf_lds;                                   // [ROWS][XP]
-  float* Es = Xs + ROWS * XP;                            // [ROWS][IRF_EP] (EXPAND)
-  float* Ds = Es + (EXPAND ? ROWS * IRF_EP : 0);         // [POUT][IRF_EP]
-  float* Ms = Ds + POUT * IRF_EP;                        // [ROWS] 1 inside the image, 0 outside
+  float* Es = Xs + ROWS * XP;                            // [ROWS][EP] (EXPAND)
+  float* Ds = Es + (EXPAND ? ROWS * EP : 0);             // [POUT][IRF_DP]
+  float* Ms = Ds + POUT * IRF_DP;                        // [ROWS] 1 inside the image, 0 outside
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, kq = lane >> 4;
@@ -82,7 +104,7 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
     const bool in = r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (in && 4 * g < p.inp) v = *(const float4*)(xb + ((size_t)iy * p.W + ix) * p.x_cs + 4 * g);
-    *(float4*)&Xs[r * XP + 4 * g] = v;
+    *(float4*)&Xs[r * XP + 4 * (EXPAND ? g : eswz<S>(r, g))] = v;
     if (g == 0) Ms[r] = in ? 1.f : 0.f;
   }
   __syncthreads();
@@ -113,11 +135,11 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
         const float m = Ms[pix];
         float4 v = make_float4(relu6f(e[0] + be.x) * m, relu6f(e[1] + be.y) * m, relu6f(e[2] + be.z) * m,
                                relu6f(e[3] + be.w) * m);
-        *(float4*)&Es[pix * IRF_EP + hc] = v;
+        *(float4*)&Es[pix * EP + 4 * eswz<S>(pix, hc >> 2)] = v;
       }
       __syncthreads();
       E = Es;
-      ep = IRF_EP;
+      ep = EP;
     } else {
       E = Xs + h0;  // t = 1 block: the depthwise runs on the input channels themselves
       ep = XP;
@@ -137,14 +159,15 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx) {
-            const float4 v = *(const float4*)&E[((oy * S + ky) * PW + ox * S + kx) * ep + 4 * g];
+            const int px = (oy * S + ky) * PW + ox * S + kx;
+            const float4 v = *(const float4*)&E[px * ep + 4 * eswz<S>(px, g)];
             const float4 w = wk[ky * 3 + kx];
             a.x = fmaf(v.x, w.x, a.x);
             a.y = fmaf(v.y, w.y, a.y);
             a.z = fmaf(v.z, w.z, a.z);
             a.w = fmaf(v.w, w.w, a.w);
           }
-        *(float4*)&Ds[q * IRF_EP + 4 * g] = relu6x4(a);
+        *(float4*)&Ds[q * IRF_DP + 4 * g] = relu6x4(a);
       }
     }
     __syncthreads();
@@ -156,7 +179,7 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
       if (pr >= PAIRS) break;
       const int mt = pr / NTO, nt = pr - mt * NTO;
       const float* wrow = wp + (size_t)(nt * 16 + col) * p.hid_pad + h0 + 4 * kq;
-      const float* drow = Ds + (mt * 16 + col) * IRF_EP + 4 * kq;
+      const float* drow = Ds + (mt * 16 + col) * IRF_DP + 4 * kq;
 #pragma unroll
       for (int kc = 0; kc < IRF_HC; kc += 16) {
         const float4 a = *(const float4*)(wrow + kc);
@@ -194,7 +217,8 @@ static size_t irf_lds_bytes(int S, int inp_pad, int expand) {
   const int TH = S == 1 ? 8 : 4, TW = 8;
   const int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   const size_t rows = (size_t)(PH * PW + 15) / 16 * 16;
-  return sizeof(float) * (rows * (inp_pad + 4) + (expand ? rows * IRF_EP : 0) + (size_t)TH * TW * IRF_EP + rows);
+  return sizeof(float) * (rows * irf_xp(inp_pad, expand) + (expand ? rows * irf_ep(S) : 0) +
+                          (size_t)TH * TW * IRF_DP + rows);
 }
 
 template <int S, int TH, int TW, int NTO, bool EXPAND>

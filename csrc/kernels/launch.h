@@ -58,6 +58,14 @@ int get_conv_impl();
 // Exact-fp32 pipeline (csrc/kernels/conv_f32.hip): the same ConvParams geometry and epilogue with fp32
 // activations, fp32 weights [Cout_pad][Kpad] (Kpad a multiple of 16) and v_mfma_f32_16x16x4_f32 (one
 // rounding per product, fp32 accumulation: the reference's ONNX Runtime fp32 numerics).
+// fp32 conv ConvParams.impl values beyond the families 0 (policy) / 1 (direct) / 2 (LDS): 10 + v selects LDS
+// implicit-GEMM tile variant v < kF32Variants (conv_f32.hip launch_lds_variant), kF32Halo the 3x3 halo kernel.
+// kF32X3 + v the fp32-accurate triple-bf16-split implicit GEMM variant v < kF32X3Variants (launch_x3_variant).
+constexpr int kF32Variants = 16;
+constexpr int kF32X3 = 40;
+constexpr int kF32X3Variants = 12;
+constexpr int kF32Halo = 100;
+constexpr int kF32X3Halo = 101;  // 3x3 stride-1 halo tiles with the triple-bf16 split
 void conv2d_f32(const ConvParams& p, hipStream_t s);
 
 // ---------------------------------------------------------------- depthwise 3x3 (K12)

@@ -255,7 +255,11 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
     if (impl->size() != prog_.size()) throw std::runtime_error("add_bucket: tuning table does not match the program");
     for (size_t i = 0; i < prog_.size(); ++i) {
       const int v = (*impl)[i];
-      if (v < 0 || v > 3 || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
+      const bool f32 = prog_[i][kDtypeField] == 1;
+      const bool ok = f32 ? (v >= 0 && v <= 2) || (v >= 10 && v < 10 + kF32Variants) ||
+                                (v >= kF32X3 && v < kF32X3 + kF32X3Variants) || v == kF32Halo || v == kF32X3Halo
+                          : v >= 0 && v <= 3;
+      if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
       bk.impl[i] = (int8_t)v;
     }
   } else if (autotune_) {
@@ -274,10 +278,15 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
 }
 
 // Per-bucket conv kernel selection: every conv op of the program is timed
-// eagerly (bucket capacity, full live counts) with each kernel family — 1
-// direct MFMA, 2 tiled/LDS (pointwise fast path, 3x3 halo tiles, weight-
-// stationary), 3 LDS-pipelined implicit GEMM — and the fastest is recorded
-// for the graph capture.  Costs ~100 ms per bucket; ARENA_AUTOTUNE=0 disables.
+// eagerly (bucket capacity, full live counts) with each kernel family — bf16:
+// 1 direct MFMA, 2 tiled/LDS (pointwise fast path, 3x3 halo tiles, weight-
+// stationary), 3 LDS-pipelined implicit GEMM; fp32: the default policy (0),
+// the exact-fp32 LDS implicit-GEMM tile variants that won somewhere in the
+// standalone sweep (profiles/r2_fp32_variants.md, impl 10 + v), the 3x3 halo
+// kernel (impl 100) and the fp32-accurate triple-bf16-split kernels (impl
+// 40 + v, 101) — and the fastest is recorded for the graph capture.  Costs
+// ~100-300 ms per bucket; ARENA_AUTOTUNE=0 disables.  Production starts load
+// the persisted table instead (engine/tuning.py), so the choice is fixed.
 void Executor::autotune(Bucket& bk) {
   Slot& sl = slots_[0];
   Ctrl c{};
@@ -288,30 +297,44 @@ void Executor::autotune(Bucket& bk) {
   hipEvent_t e0, e1;
   ARENA_HIP_CHECK(hipEventCreate(&e0));
   ARENA_HIP_CHECK(hipEventCreate(&e1));
-  const int reps = 3;
+  static const int kF32Candidates[] = {0,      12,     13,     14,     17,     19,     20,         21,
+                                       23,     24,     kF32Halo, kF32X3, kF32X3 + 1, kF32X3 + 4, kF32X3 + 5,
+                                       kF32X3 + 6, kF32X3 + 7, kF32X3 + 8, kF32X3Halo};
+  static const int kBf16Candidates[] = {1, 2, 3};
   for (size_t i = 0; i < prog_.size(); ++i) {
-    if (prog_[i][0] != OP_CONV || prog_[i][kDtypeField] == 1) continue;  // one fp32 conv kernel family
-    if (prog_[i][34] > 0) {  // fused pointwise epilogue: only the v3 halo-tile kernel implements it
+    if (prog_[i][0] != OP_CONV) continue;
+    const bool f32 = prog_[i][kDtypeField] == 1;
+    if (!f32 && prog_[i][34] > 0) {  // fused pointwise epilogue: only the v3 halo-tile kernel implements it
       bk.impl[i] = 2;
       continue;
     }
+    const int reps = f32 ? 5 : 3;
     std::vector<OpRecord> one(1, prog_[i]);
     float best = 1e30f;
-    int best_impl = 0;
-    for (int impl = 1; impl <= 3; ++impl) {
-      enqueue_program(one, bk, sl, compute_, (int)i, impl);  // warm-up (instruction cache, L2)
+    int best_impl = -1;
+    const int* cand = f32 ? kF32Candidates : kBf16Candidates;
+    const int n_cand = f32 ? (int)(sizeof(kF32Candidates) / sizeof(int)) : 3;
+    for (int ci = 0; ci < n_cand; ++ci) {
+      const int impl = cand[ci];
+      // warm-up (instruction cache, L2); impl 0 reads bk.impl[i], still 0 here = the default policy.
+      // A variant that does not apply to the shape (halo on a non-3x3 conv) throws before launching.
+      try {
+        enqueue_program(one, bk, sl, compute_, (int)i, impl);
+      } catch (const std::runtime_error&) {
+        continue;
+      }
       ARENA_HIP_CHECK(hipEventRecord(e0, compute_));
       for (int k = 0; k < reps; ++k) enqueue_program(one, bk, sl, compute_, (int)i, impl);
       ARENA_HIP_CHECK(hipEventRecord(e1, compute_));
       ARENA_HIP_CHECK(hipEventSynchronize(e1));
       float ms = 0.f;
       ARENA_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-      if (ms < best * 0.97f || best_impl == 0) {  // prefer the lower family on near-ties
-        if (ms < best) best = ms;
+      if (best_impl < 0 || ms < best * 0.97f) {  // a later candidate must win by 3% (stable choices)
+        best = ms;
         best_impl = impl;
       }
     }
-    bk.impl[i] = (int8_t)best_impl;
+    bk.impl[i] = (int8_t)std::max(best_impl, 0);
     if (autotune_ > 1)
       fprintf(stderr, "[arena autotune] B=%d op %zu -> impl %d (%.1f us)\n", bk.info.B, i, best_impl,
               best * 1e3f / reps);

@@ -1,6 +1,8 @@
 """Persisted conv-kernel selection (deterministic programs across boxes).
 
-The executor can time every bf16 conv op of a bucket with each kernel family
+The executor can time every conv op of a bucket with each kernel family (bf16:
+direct / LDS / pipelined implicit GEMM; fp32: default policy, LDS tile
+variants, 3x3 halo tiles)
 (csrc/runtime/executor.cpp ``autotune``) and capture the fastest; timing noise
 made the choice differ from box to box (impl2:30/impl3:21 on one
 box, 27/24 on another), so the same commit ran different programs.  Here the
@@ -12,8 +14,7 @@ choices are a table keyed by (program fingerprint, bucket): ``ARENA_TUNING``
 * ``off``: no timing, kernel defaults everywhere.
 
 The table lives in ``data/tuning/conv_tuning.json`` (``ARENA_TUNING_FILE``);
-tools/tune_programs.py regenerates it on a GPU box.  fp32 programs have one
-conv kernel family and need no entries.
+tools/tune_programs.py regenerates it on a GPU box.
 """
 from __future__ import annotations
 
@@ -74,7 +75,7 @@ def store(ops: np.ndarray, B: int, choices: list[int], path: Path | None = None)
 
 
 def needs_tuning(ops: np.ndarray) -> bool:
-    """Only bf16 conv ops have kernel families to choose from (OP_CONV with dtype field 0)."""
-    from .planner import OP_CONV, OP_DTYPE_FIELD
+    """Conv ops (bf16 and fp32) have kernel families to choose from."""
+    from .planner import OP_CONV
 
-    return bool(np.any((ops[:, 0] == OP_CONV) & (ops[:, OP_DTYPE_FIELD] == 0)))
+    return bool(np.any(ops[:, 0] == OP_CONV))

@@ -51,7 +51,9 @@ def ir_f32_lds_bytes(stride: int, inp_pad: int, expand: bool) -> int:
     th, tw = (8, 8) if stride == 1 else (4, 8)
     ph, pw = (th - 1) * stride + 3, (tw - 1) * stride + 3
     rows = (ph * pw + 15) // 16 * 16
-    return 4 * (rows * (inp_pad + 4) + (rows * 36 if expand else 0) + th * tw * 36 + rows)
+    xp = inp_pad + 8 if expand else inp_pad
+    ep = 32 if stride == 1 else 36
+    return 4 * (rows * xp + (rows * ep if expand else 0) + th * tw * 40 + rows)
 
 
 def ir_f32_supported(stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:

@@ -41,11 +41,13 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
                 x_coff: int = 0, cin: int | None = None, out: torch.Tensor | None = None, out_coff: int = 0,
                 res: torch.Tensor | None = None, res_coff: int = 0, out2: torch.Tensor | None = None,
                 out2_coff: int = 0, f32out: bool = False, out_hw=None, bdev: torch.Tensor | None = None,
-                packed=None) -> torch.Tensor:
+                packed=None, impl: int = 0) -> torch.Tensor:
     """NHWC conv with fused bias/act/residual/upsampled copy.
 
     x: [B, H, W, Cx] bf16 or float32 (reads channels [x_coff, x_coff + Cin)); w: [Cout, Cin, KH, KW] fp32.
     A float32 ``x`` runs the exact-fp32 kernel (fp32 weights, v_mfma_f32_16x16x4_f32, fp32 output).
+    ``impl`` pins a kernel (0 = the dispatch policy; fp32: 1 direct, 2 LDS, 10 + v LDS tile variant v,
+    40 + v triple-bf16-split variant v, 100 halo, 101 split halo — csrc/kernels/launch.h).
     """
     f32 = x.dtype == torch.float32
     B, H, W, Cx = x.shape
@@ -71,6 +73,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
         "res": _ptr(res, res_coff), "rs": res.shape[-1] if res is not None else 0,
         "y2": _ptr(out2, out2_coff), "y2s": out2.shape[-1] if out2 is not None else 0,
         "act": ACT[act], "f32out": int(f32out), "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32),
+        "impl": int(impl),
     })
     return out
 

@@ -43,11 +43,29 @@ def _decode(data: bytes | Path | str, what: str) -> np.ndarray:
     try:
         src = io.BytesIO(data) if isinstance(data, (bytes, bytearray, memoryview)) else str(data)
         with Image.open(src) as im:
-            im = im.convert("RGB")
+            if im.mode != "RGB":  # convert() of an RGB image is a full copy
+                im = im.convert("RGB")
             arr = np.asarray(im, dtype=np.uint8)
     except (UnidentifiedImageError, OSError, ValueError) as e:
         raise ValueError(f"{what}: {e}") from e
     return np.ascontiguousarray(arr)
+
+
+def decode_rgb(data: bytes | memoryview) -> tuple[int, int, bytes]:
+    """The decode of ``load_image_from_bytes`` returning (h, w, packed RGB bytes): one pack of PIL's
+    RGBX raster and no numpy round trip (the decode-pool workers copy the bytes into shared memory)."""
+    from PIL import Image, UnidentifiedImageError
+
+    if not len(data):
+        raise ValueError("Failed to decode image: empty payload")
+    try:
+        with Image.open(io.BytesIO(data)) as im:
+            if im.mode != "RGB":
+                im = im.convert("RGB")
+            w, h = im.size
+            return h, w, im.tobytes()
+    except (UnidentifiedImageError, OSError, ValueError) as e:
+        raise ValueError(f"Failed to decode image: {e}") from e
 
 
 class ImageLoadError(ValueError, FileNotFoundError):

@@ -1,26 +1,40 @@
-"""Multi-process JPEG decode pool with shared-memory delivery.
+"""Multi-process JPEG decode pool with shared-memory transport both ways.
 
 The reference decodes every upload on the request thread (cv2.imdecode in
 src/shared/processing/transforms.py:77-110; PIL in
 architectures/microservices/classification/app/servicer.py:65-76).  At GPU
 request rates the decode is the host's largest per-request cost (about
-1.5-3 ms of CPU per COCO-sized JPEG), and a thread pool does not scale: the
+1-3 ms of CPU per COCO-sized JPEG), and a thread pool does not scale: the
 PIL -> numpy conversion holds the GIL (measured here: 8 threads decode only
 1.4x faster than one).  This pool decodes in ``workers`` separate processes
 (spawned, never forked: the parent may already hold GPU state) with the same
-``load_image_from_bytes`` as every other path, writes the RGB pixels into a
-slot of one shared-memory segment and hands the parent a zero-copy numpy view
-of the slot.  The parent passes the view straight to the native batcher
-(whose ``enqueue`` copies it) and the slot returns to the free list.
+decoder as every other path (``processing.transforms.decode_rgb``).
 
-Images larger than a slot travel back pickled through the result queue
-(correct, just slower); undecodable uploads come back as an error string.
+Transport is built so the parent does O(1) Python work per image and never
+pickles a payload (the first version moved JPEG bytes and results through
+``multiprocessing.Queue``s and saturated at ~6k decodes/s on a 16-core share,
+profiles/r2_decode_rate.log, with the parent's pickling and queue locks as
+the limit):
+
+* one shared-memory segment of ``slots`` slots; a slot holds the upload
+  (``in_bytes``) followed by room for its decoded RGB pixels (``slot_pixels``);
+* the parent copies the upload into the slot and sends a 16-byte task record
+  on the chosen worker's own pipe (least outstanding work first); uploads
+  larger than ``in_bytes`` travel inline on that pipe instead;
+* workers decode straight from the slot, write the packed RGB pixels into it
+  and post a 32-byte completion record on ONE shared result pipe (writes of
+  <= PIPE_BUF bytes are atomic, so no lock is needed across workers);
+* the collector thread reads completion records in bulk and hands the callback
+  a zero-copy numpy view of the slot; the slot is freed when the callback
+  returns.  Images too large for a slot follow their record on the worker's
+  result connection; undecodable uploads return their error text in the slot.
 """
 from __future__ import annotations
 
 import multiprocessing as mp
 import os
 import queue
+import struct
 import threading
 from multiprocessing import shared_memory
 from typing import Callable
@@ -29,31 +43,44 @@ import numpy as np
 
 DecodeCallback = Callable[[object, "np.ndarray | None", "str | None"], None]
 
+_TASK = struct.Struct("<qii")      # key, slot, payload length (-1: payload inline after the record)
+_DONE = struct.Struct("<qiiiiq")   # key, slot, h, w, status, aux
+_OK, _ERR, _BIG = 0, 1, 2          # pixels in slot / error text in slot (aux = length) / pixels on worker conn
 
-def _worker(shm_name: str, slot_bytes: int, tasks, results) -> None:  # pragma: no cover - runs in a child
-    from ..processing.transforms import load_image_from_bytes
+
+def _worker(idx: int, shm_name: str, in_bytes: int, slot_bytes: int, tasks, results_w, big_w) -> None:  # pragma: no cover - runs in a child
+    from ..processing.transforms import decode_rgb
 
     shm = shared_memory.SharedMemory(name=shm_name)
+    buf = shm.buf
+    rfd = results_w.fileno()
+    stride = in_bytes + slot_bytes
     try:
         while True:
-            t = tasks.get()
-            if t is None:
+            msg = tasks.recv_bytes()
+            if not msg:
                 return
-            tag, slot, data = t
+            key, slot, n = _TASK.unpack_from(msg)
+            base = slot * stride
+            data = msg[_TASK.size:] if n < 0 else buf[base:base + n]
             try:
-                img = load_image_from_bytes(data)
-            except Exception as e:  # noqa: BLE001 - reported to the caller
-                results.put((tag, slot, 0, 0, None, str(e)))
+                h, w, px = decode_rgb(data)
+            except ValueError as e:
+                text = str(e).encode()[:slot_bytes]
+                buf[base + in_bytes:base + in_bytes + len(text)] = text
+                os.write(rfd, _DONE.pack(key, slot, 0, 0, _ERR, len(text)))
                 continue
-            h, w = img.shape[:2]
-            if h * w * 3 <= slot_bytes:
-                view = np.ndarray((h, w, 3), dtype=np.uint8, buffer=shm.buf, offset=slot * slot_bytes)
-                view[...] = img
-                del view
-                results.put((tag, slot, h, w, None, None))
+            finally:
+                if n >= 0:
+                    del data  # release the memoryview of the slot
+            if len(px) <= slot_bytes:
+                buf[base + in_bytes:base + in_bytes + len(px)] = px
+                os.write(rfd, _DONE.pack(key, slot, h, w, _OK, 0))
             else:
-                results.put((tag, slot, h, w, np.ascontiguousarray(img).tobytes(), None))
+                os.write(rfd, _DONE.pack(key, slot, h, w, _BIG, idx))
+                big_w.send_bytes(px)
     finally:
+        del buf
         shm.close()
 
 
@@ -61,22 +88,34 @@ class ProcessDecodePool:
     """``submit(jpeg_bytes, tag, callback)``; ``callback(tag, rgb_view_or_None, error_or_None)`` runs on the
     pool's collector thread and must consume the view before returning (the slot is reused afterwards)."""
 
-    def __init__(self, workers: int | None = None, slots: int = 256, slot_pixels: int = 1024 * 1024):
+    def __init__(self, workers: int | None = None, slots: int = 256, slot_pixels: int = 1024 * 1024,
+                 in_bytes: int = 1 << 20):
         self.workers = max(1, int(workers or min(16, os.cpu_count() or 4)))
         self.slots = int(slots)
         self.slot_bytes = int(slot_pixels) * 3
-        self.shm = shared_memory.SharedMemory(create=True, size=self.slots * self.slot_bytes)
+        self.in_bytes = int(in_bytes)
+        self._stride = self.in_bytes + self.slot_bytes
+        self.shm = shared_memory.SharedMemory(create=True, size=self.slots * self._stride)
         ctx = mp.get_context("spawn")
-        self.tasks = ctx.Queue()
-        self.results = ctx.Queue()
-        self.procs = [ctx.Process(target=_worker, args=(self.shm.name, self.slot_bytes, self.tasks, self.results),
-                                  daemon=True, name=f"arena-decode-{i}") for i in range(self.workers)]
-        for p in self.procs:
+        self._res_r, self._res_w = ctx.Pipe(duplex=False)
+        self._tasks, self._big, self.procs = [], [], []
+        for i in range(self.workers):
+            tr, tw = ctx.Pipe(duplex=False)
+            br, bw = ctx.Pipe(duplex=False)
+            p = ctx.Process(target=_worker, args=(i, self.shm.name, self.in_bytes, self.slot_bytes, tr,
+                                                  self._res_w, bw), daemon=True, name=f"arena-decode-{i}")
             p.start()
+            tr.close()
+            bw.close()
+            self._tasks.append(tw)
+            self._big.append(br)
+            self.procs.append(p)
+        self._send_locks = [threading.Lock() for _ in range(self.workers)]
+        self._load = [0] * self.workers
         self._free: queue.SimpleQueue = queue.SimpleQueue()
         for s in range(self.slots):
             self._free.put(s)
-        self._cbs: dict[int, tuple[object, DecodeCallback]] = {}
+        self._cbs: dict[int, tuple[object, DecodeCallback, int]] = {}
         self._lock = threading.Lock()
         self._seq = 0
         self._closed = False
@@ -88,47 +127,77 @@ class ProcessDecodePool:
         if self._closed:
             raise RuntimeError("decode pool is closed")
         slot = self._free.get()
+        n = len(data)
         with self._lock:
             self._seq += 1
             key = self._seq
-            self._cbs[key] = (tag, callback)
-        self.tasks.put((key, slot, data))
+            w = min(range(self.workers), key=self._load.__getitem__)
+            self._load[w] += 1
+            self._cbs[key] = (tag, callback, w)
+        if n <= self.in_bytes:
+            base = slot * self._stride
+            self.shm.buf[base:base + n] = data
+            msg = _TASK.pack(key, slot, n)
+        else:
+            msg = _TASK.pack(key, slot, -1) + bytes(data)
+        with self._send_locks[w]:
+            self._tasks[w].send_bytes(msg)
 
     def _collect(self) -> None:
+        fd = self._res_r.fileno()
+        pending = b""
+        rec = _DONE.size
         while True:
-            r = self.results.get()
-            if r is None:
+            chunk = os.read(fd, 64 * rec)
+            if not chunk:
                 return
-            key, slot, h, w, payload, err = r
-            with self._lock:
-                tag, cb = self._cbs.pop(key)
-            try:
-                if err is not None:
-                    cb(tag, None, err)
-                elif payload is not None:
-                    cb(tag, np.frombuffer(payload, dtype=np.uint8).reshape(h, w, 3), None)
-                else:
-                    cb(tag, np.ndarray((h, w, 3), dtype=np.uint8, buffer=self.shm.buf,
-                                       offset=slot * self.slot_bytes), None)
-            except Exception as e:  # noqa: BLE001 - a failing consumer must not stop the pool
-                import sys
+            pending += chunk
+            full = len(pending) - len(pending) % rec
+            for off in range(0, full, rec):
+                key, slot, h, w, status, aux = _DONE.unpack_from(pending, off)
+                if key < 0:
+                    return
+                self._complete(key, slot, h, w, status, aux)
+            pending = pending[full:]
 
-                print(f"decode pool callback failed: {e!r}", file=sys.stderr)
-            finally:
-                self._free.put(slot)
+    def _complete(self, key, slot, h, w, status, aux) -> None:
+        with self._lock:
+            tag, cb, worker = self._cbs.pop(key)
+            self._load[worker] -= 1
+        out = slot * self._stride + self.in_bytes
+        try:
+            if status == _ERR:
+                cb(tag, None, bytes(self.shm.buf[out:out + aux]).decode(errors="replace"))
+            elif status == _BIG:
+                px = self._big[aux].recv_bytes()
+                cb(tag, np.frombuffer(px, dtype=np.uint8).reshape(h, w, 3), None)
+            else:
+                cb(tag, np.ndarray((h, w, 3), dtype=np.uint8, buffer=self.shm.buf, offset=out), None)
+        except Exception as e:  # noqa: BLE001 - a failing consumer must not stop the pool
+            import sys
+
+            print(f"decode pool callback failed: {e!r}", file=sys.stderr)
+        finally:
+            self._free.put(slot)
 
     def close(self) -> None:
         if self._closed:
             return
         self._closed = True
-        for _ in self.procs:
-            self.tasks.put(None)
+        for w, conn in enumerate(self._tasks):
+            try:
+                with self._send_locks[w]:
+                    conn.send_bytes(b"")
+            except OSError:
+                pass
         for p in self.procs:
             p.join(timeout=5)
             if p.is_alive():
                 p.terminate()
-        self.results.put(None)
+        os.write(self._res_w.fileno(), _DONE.pack(-1, 0, 0, 0, 0, 0))
         self._collector.join(timeout=5)
+        for c in self._tasks + self._big + [self._res_r, self._res_w]:
+            c.close()
         try:
             self.shm.close()
             self.shm.unlink()

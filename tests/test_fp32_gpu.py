@@ -77,6 +77,52 @@ def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
         assert torch.equal(out2, up_ref)
 
 
+X3_IMPLS = [40 + v for v in range(12)] + [101]  # triple-bf16-split tile variants + split halo (launch.h)
+
+
+@pytest.mark.parametrize(
+    "B,H,Cin,Cout,k,s,act,res",
+    [
+        (2, 20, 32, 32, 3, 1, "silu", True),       # bottleneck 3x3 with residual
+        (2, 24, 80, 80, 3, 1, "silu", False),      # Cin 80: a partial 32-channel chunk in the halo kernel
+        (2, 20, 64, 144, 3, 1, "silu", False),     # detect head (Cout 144)
+        (2, 40, 16, 32, 3, 2, "silu", False),      # 3x3 stride 2
+        (4, 7, 160, 960, 1, 1, "relu6", False),    # MobileNet expand
+        (4, 7, 960, 160, 1, 1, None, True),        # MobileNet project + residual
+    ],
+)
+def test_conv_x3_split_matches_fp64(device, B, H, Cin, Cout, k, s, act, res):
+    """The fp32-accurate triple-bf16-split kernels (bf16 matrix cores, six partial products) meet the same
+    fp32 error bound as the exact-fp32 kernels, for every tile variant."""
+    g = torch.Generator().manual_seed(B * 100 + H + Cin + Cout)
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g, dtype=torch.float64) * 0.1
+    x32, w32, b32 = x.float(), w.float(), b.float()
+    pad = k // 2
+    ref = _act64(F.conv2d(x32.double(), w32.double(), b32.double(), stride=s, padding=pad), act)
+    scale = F.conv2d(x32.double().abs(), w32.double().abs(), b32.double().abs(), stride=s, padding=pad)
+    Ho = ref.shape[2]
+    r = torch.randn(B, Cout, Ho, Ho, generator=g).float() if res else None
+    if res:
+        ref = ref + r.double()
+        scale = scale + r.double().abs()
+    xd = _nhwc(x32).to(device)
+    rd = _nhwc(r).to(device) if res else None
+    packed = AF.pack_weights(w32, b32, device, "fp32")
+    ran = 0
+    for impl in X3_IMPLS:
+        try:
+            y = AF.conv2d_nhwc(xd, w32, b32, stride=s, act=act, res=rd, packed=packed, impl=impl)
+        except RuntimeError as e:
+            assert "eligible" in str(e), e  # the split halo only takes 3x3 stride-1 convs
+            continue
+        torch.cuda.synchronize()
+        _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
+        ran += 1
+    assert ran >= 12
+
+
 def test_conv_f32_channel_slices(device):
     """Reads channels [x_coff, x_coff + Cin) of a wider buffer and stores into a channel slice (concat)."""
     g = torch.Generator().manual_seed(7)

@@ -221,7 +221,7 @@ def test_tuning_table_roundtrip(tmp_path, monkeypatch):
     monkeypatch.setenv("ARENA_TUNING_FILE", str(f))
     p = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="bf16")
     assert tuning.needs_tuning(p.ops)
-    assert not tuning.needs_tuning(plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="fp32").ops)
+    assert tuning.needs_tuning(plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="fp32").ops)
     assert tuning.lookup(p.ops, 8) is None
     ch = [2 if int(o[0]) == 1 else 0 for o in p.ops]
     assert tuning.store(p.ops, 8, ch)

@@ -5,7 +5,9 @@ Each ``<dir>/run_counter_collection.csv`` holds one counter set for every
 dispatch.  The program's ops are located as in analyze_trace.py (a replay
 starts at the letterbox kernel; the k-th arena dispatch of a replay is op k);
 values are averaged over the last complete replays and per-op ratios are
-derived: VALU and LDS instructions per MFMA, LDS bank-conflict share, waves.
+derived: VALU and LDS instructions per MFMA, LDS bank-conflict share, waves,
+and the MFMA-busy share of the SIMDs (SQ_VALU_MFMA_BUSY_CYCLES over
+GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs).
 
     python tools/analyze_pmc.py gpurun_out/pmc2/*/run_counter_collection.csv --out profiles/r1_pmc_ops.md
 """
@@ -48,8 +50,9 @@ def main(argv=None) -> int:
     ap.add_argument("csvs", nargs="+")
     ap.add_argument("--replays", type=int, default=2)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     a = ap.parse_args(argv)
-    prog = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45)
+    prog = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype=a.dtype)
     n_ops = prog.ops.shape[0]
     vals = defaultdict(lambda: defaultdict(list))
     kname = {}
@@ -60,8 +63,8 @@ def main(argv=None) -> int:
                 for c, v in cnt.items():
                     vals[k][c].append(v)
     counters = sorted({c for k in vals for c in vals[k]})
-    lines = ["| op | kind | shape | kernel | " + " | ".join(counters) + " | valu/mfma | lds/mfma | conflict % |",
-             "|" + "---|" * (4 + len(counters) + 3)]
+    lines = ["| op | kind | shape | kernel | " + " | ".join(counters) + " | valu/mfma | lds/mfma | conflict % | mfma busy % |",
+             "|" + "---|" * (4 + len(counters) + 4)]
     for k in range(n_ops):
         if k not in vals:
             continue
@@ -71,9 +74,13 @@ def main(argv=None) -> int:
         lr = f"{m['SQ_INSTS_LDS'] / mf:.2f}" if mf and "SQ_INSTS_LDS" in m else "-"
         cf = (f"{100 * m['SQ_LDS_BANK_CONFLICT'] / m['SQ_LDS_IDX_ACTIVE']:.1f}"
               if m.get("SQ_LDS_IDX_ACTIVE") else "-")
+        # MFMA busy share of the SIMDs while the kernel runs: SQ_VALU_MFMA_BUSY_CYCLES is summed over the
+        # 1024 SIMDs, GRBM_GUI_ACTIVE over the 8 XCDs (GRBM/8 reproduces the kernel-trace durations)
+        mb = (f"{100 * m['SQ_VALU_MFMA_BUSY_CYCLES'] / (m['GRBM_GUI_ACTIVE'] / 8 * 1024):.1f}"
+              if m.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in m else "-")
         kind = KIND.get(int(prog.ops[k][0]), "?")
         lines.append(f"| {k} | {kind} | {describe(prog.ops[k])} | {kname[k]} | "
-                     + " | ".join(f"{m[c]:.3g}" if c in m else "-" for c in counters) + f" | {vr} | {lr} | {cf} |")
+                     + " | ".join(f"{m[c]:.3g}" if c in m else "-" for c in counters) + f" | {vr} | {lr} | {cf} | {mb} |")
     text = "\n".join(lines)
     print(text)
     if a.out:
