@@ -66,7 +66,7 @@ __device__ __forceinline__ float4 relu6x4(float4 v) {
 
 }  // namespace
 
-template <int S, int TH, int TW, int NTO, bool EXPAND>
+template <int S, int TH, int TW, int NTO, bool EXPAND, int KIN>
 __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   constexpr int PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
@@ -113,28 +113,75 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
 #pragma unroll
   for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Per-chunk weights live in registers and are fetched one phase ahead of their use (the first
+  // version read them from global memory inside each MFMA tile loop and waited on every fetch):
+  //   expand weights/bias of chunk h+1 and depthwise taps/bias of chunk h+1 during chunk h's project GEMM,
+  //   project weights of chunk h during chunk h's depthwise.
+  // A wave's expand tiles all share one hidden-channel half (tt = wave + 4i keeps tt & 1 = wave & 1), so
+  // its expand weights are one row per lane; its ET tiles run as interleaved accumulation chains.
+  constexpr int KIN_MAX = KIN;                   // inp_pad / 16 (a template parameter: a runtime bound kept
+                                                 // every unrolled k-step's registers live)
+  constexpr int ET = (MT_IN * 2 + 3) / 4;        // expand tiles per wave
+  const int nt_e = wave & 1;
+  const int g = tid & 7;                         // depthwise channel group of this thread
+  float4 wexp[KIN_MAX], bexp, wk[9], bdw, wprj[PPW][2];
+  auto load_expand = [&](int h0) {
+#pragma unroll
+    for (int kc = 0; kc < KIN_MAX; ++kc)
+        wexp[kc] = *(const float4*)(we + (size_t)(h0 + nt_e * 16 + col) * p.inp_pad + 16 * kc + 4 * kq);
+    bexp = *(const float4*)((const float*)p.be + h0 + nt_e * 16 + 4 * kq);
+  };
+  auto load_dw = [&](int h0) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)(wd + (size_t)k * p.hid_pad + h0 + 4 * g);
+    bdw = *(const float4*)((const float*)p.bd + h0 + 4 * g);
+  };
+  auto load_project = [&](int h0) {
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int pr = wave + 4 * j;
+      if (pr >= PAIRS) break;
+      const int nt = pr % NTO;
+      const float* wrow = wp + (size_t)(nt * 16 + col) * p.hid_pad + h0 + 4 * kq;
+      wprj[j][0] = *(const float4*)wrow;
+      wprj[j][1] = *(const float4*)(wrow + 16);
+    }
+  };
+  // Holding the next chunk's 9 depthwise taps across the project GEMM costs 40 VGPRs: at stride 1 (8x8
+  // tiles, 3 blocks per CU by LDS) that dropped occupancy and measured slower, so there they load at use.
+  constexpr bool PREFETCH_DW = S == 2;
+  if constexpr (EXPAND) load_expand(0);
+  if constexpr (PREFETCH_DW) load_dw(0);
+
   for (int h0 = 0; h0 < p.hid_pad; h0 += IRF_HC) {
     // ---- B: expand GEMM for this chunk, rows = hidden channel, columns = halo pixel
     const float* E;
     int ep;
     if constexpr (EXPAND) {
-      for (int tt = wave; tt < MT_IN * 2; tt += 4) {
-        const int mt = tt >> 1, nt = tt & 1;
-        f32x4 e = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* wrow = we + (size_t)(h0 + nt * 16 + col) * p.inp_pad + 4 * kq;
-        const float* xrow = Xs + (mt * 16 + col) * XP + 4 * kq;
-        for (int kc = 0; kc < p.inp_pad; kc += 16) {
-          const float4 a = *(const float4*)(wrow + kc);
-          const float4 bb = *(const float4*)(xrow + kc);
+      f32x4 e[ET];
 #pragma unroll
-          for (int s = 0; s < 4; ++s) e = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(a, s), f4c(bb, s), e, 0, 0, 0);
+      for (int i = 0; i < ET; ++i) e[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < KIN_MAX; ++kc) {
+#pragma unroll
+        for (int i = 0; i < ET; ++i) {
+          const int tt = wave + 4 * i;
+          if (tt >= MT_IN * 2) break;
+          const float4 bb = *(const float4*)(Xs + ((tt >> 1) * 16 + col) * XP + 16 * kc + 4 * kq);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            e[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(wexp[kc], s4), f4c(bb, s4), e[i], 0, 0, 0);
         }
-        const int pix = mt * 16 + col;
-        const int hc = nt * 16 + 4 * kq;
-        const float4 be = *(const float4*)((const float*)p.be + h0 + hc);
+      }
+#pragma unroll
+      for (int i = 0; i < ET; ++i) {
+        const int tt = wave + 4 * i;
+        if (tt >= MT_IN * 2) break;
+        const int pix = (tt >> 1) * 16 + col;
+        const int hc = nt_e * 16 + 4 * kq;
         const float m = Ms[pix];
-        float4 v = make_float4(relu6f(e[0] + be.x) * m, relu6f(e[1] + be.y) * m, relu6f(e[2] + be.z) * m,
-                               relu6f(e[3] + be.w) * m);
+        const float4 v = make_float4(relu6f(e[i][0] + bexp.x) * m, relu6f(e[i][1] + bexp.y) * m,
+                                     relu6f(e[i][2] + bexp.z) * m, relu6f(e[i][3] + bexp.w) * m);
         *(float4*)&Es[pix * EP + 4 * eswz<S>(pix, hc >> 2)] = v;
       }
       __syncthreads();
@@ -144,48 +191,45 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
       E = Xs + h0;  // t = 1 block: the depthwise runs on the input channels themselves
       ep = XP;
     }
+    load_project(h0);
+    if constexpr (!PREFETCH_DW) load_dw(h0);
 
     // ---- C: depthwise 3x3 (stride S) + bias + ReLU6 on the chunk; 4 channels per thread item
-    {
-      const int g = tid & 7;  // channel group of this thread (256 % 8 == 0: fixed across items)
-      float4 wk[9];
+    for (int q = tid >> 3; q < POUT; q += 32) {
+      const int oy = q / TW, ox = q - oy * TW;
+      float4 a = bdw;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)(wd + (size_t)k * p.hid_pad + h0 + 4 * g);
-      const float4 bd = *(const float4*)((const float*)p.bd + h0 + 4 * g);
-      for (int q = tid >> 3; q < POUT; q += 32) {
-        const int oy = q / TW, ox = q - oy * TW;
-        float4 a = bd;
+      for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int px = (oy * S + ky) * PW + ox * S + kx;
-            const float4 v = *(const float4*)&E[px * ep + 4 * eswz<S>(px, g)];
-            const float4 w = wk[ky * 3 + kx];
-            a.x = fmaf(v.x, w.x, a.x);
-            a.y = fmaf(v.y, w.y, a.y);
-            a.z = fmaf(v.z, w.z, a.z);
-            a.w = fmaf(v.w, w.w, a.w);
-          }
-        *(float4*)&Ds[q * IRF_DP + 4 * g] = relu6x4(a);
-      }
+        for (int kx = 0; kx < 3; ++kx) {
+          const int px = (oy * S + ky) * PW + ox * S + kx;
+          const float4 v = *(const float4*)&E[px * ep + 4 * eswz<S>(px, g)];
+          const float4 w = wk[ky * 3 + kx];
+          a.x = fmaf(v.x, w.x, a.x);
+          a.y = fmaf(v.y, w.y, a.y);
+          a.z = fmaf(v.z, w.z, a.z);
+          a.w = fmaf(v.w, w.w, a.w);
+        }
+      *(float4*)&Ds[q * IRF_DP + 4 * g] = relu6x4(a);
     }
     __syncthreads();
+    if (h0 + IRF_HC < p.hid_pad) {  // next chunk's expand / depthwise weights, in flight during the project GEMM
+      if constexpr (EXPAND) load_expand(h0 + IRF_HC);
+      if constexpr (PREFETCH_DW) load_dw(h0 + IRF_HC);
+    }
 
     // ---- D: project GEMM accumulate, rows = output channel, columns = output pixel
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int pr = wave + 4 * j;
-      if (pr >= PAIRS) break;
-      const int mt = pr / NTO, nt = pr - mt * NTO;
-      const float* wrow = wp + (size_t)(nt * 16 + col) * p.hid_pad + h0 + 4 * kq;
-      const float* drow = Ds + (mt * 16 + col) * IRF_DP + 4 * kq;
+    for (int kc = 0; kc < 2; ++kc) {
 #pragma unroll
-      for (int kc = 0; kc < IRF_HC; kc += 16) {
-        const float4 a = *(const float4*)(wrow + kc);
-        const float4 bb = *(const float4*)(drow + kc);
+      for (int j = 0; j < PPW; ++j) {
+        const int pr = wave + 4 * j;
+        if (pr >= PAIRS) break;
+        const int mt = pr / NTO;
+        const float4 bb = *(const float4*)(Ds + (mt * 16 + col) * IRF_DP + 16 * kc + 4 * kq);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(a, s), f4c(bb, s), acc[j], 0, 0, 0);
+        for (int s4 = 0; s4 < 4; ++s4)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(wprj[j][kc], s4), f4c(bb, s4), acc[j], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -221,11 +265,26 @@ static size_t irf_lds_bytes(int S, int inp_pad, int expand) {
                           (size_t)TH * TW * IRF_DP + rows);
 }
 
-template <int S, int TH, int TW, int NTO, bool EXPAND>
-static void irf_launch(const IrParams& p, hipStream_t s) {
+template <int S, int TH, int TW, int NTO, bool EXPAND, int KIN>
+static void irf_launch_k(const IrParams& p, hipStream_t s) {
   const size_t lds = irf_lds_bytes(S, p.inp_pad, EXPAND);
   const int tiles = ((p.Wo + TW - 1) / TW) * ((p.Ho + TH - 1) / TH);
-  hipLaunchKernelGGL((ir_f32_kernel<S, TH, TW, NTO, EXPAND>), dim3((unsigned)(p.B * tiles)), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((ir_f32_kernel<S, TH, TW, NTO, EXPAND, KIN>), dim3((unsigned)(p.B * tiles)), dim3(256), lds, s,
+                     p);
+}
+
+template <int S, int TH, int TW, int NTO, bool EXPAND>
+static void irf_launch(const IrParams& p, hipStream_t s) {
+  if constexpr (!EXPAND) {
+    irf_launch_k<S, TH, TW, NTO, false, 1>(p, s);
+  } else {
+    switch (p.inp_pad / 16) {
+      case 1: irf_launch_k<S, TH, TW, NTO, true, 1>(p, s); break;
+      case 2: irf_launch_k<S, TH, TW, NTO, true, 2>(p, s); break;
+      case 3: irf_launch_k<S, TH, TW, NTO, true, 3>(p, s); break;
+      default: irf_launch_k<S, TH, TW, NTO, true, 4>(p, s); break;  // inp_pad <= 64 (supported())
+    }
+  }
 }
 
 template <int S, int TH, int TW, bool EXPAND>
@@ -241,7 +300,8 @@ static bool irf_nto(const IrParams& p, hipStream_t s) {
 
 bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand) {
   const int nto = oup_pad / 16;
-  return (stride == 1 || stride == 2) && inp_pad % 16 == 0 && hid_pad % IRF_HC == 0 && oup_pad % 16 == 0 &&
+  return (stride == 1 || stride == 2) && inp_pad % 16 == 0 && inp_pad <= 64 && hid_pad % IRF_HC == 0 &&
+         oup_pad % 16 == 0 &&
          (nto == 1 || nto == 2 || nto == 4 || nto == 6) && (expand || hid_pad == inp_pad) &&
          irf_lds_bytes(stride, inp_pad, expand) <= 64 * 1024;
 }

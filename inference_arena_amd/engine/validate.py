@@ -58,7 +58,7 @@ def ir_f32_lds_bytes(stride: int, inp_pad: int, expand: bool) -> int:
 
 def ir_f32_supported(stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
     """Mirror of arena::ir_block_f32_supported."""
-    return (stride in (1, 2) and inp_pad % 16 == 0 and hid_pad % 32 == 0 and oup_pad % 16 == 0
+    return (stride in (1, 2) and inp_pad % 16 == 0 and inp_pad <= 64 and hid_pad % 32 == 0 and oup_pad % 16 == 0
             and oup_pad // 16 in (1, 2, 4, 6) and (bool(expand) or hid_pad == inp_pad)
             and ir_f32_lds_bytes(stride, inp_pad, bool(expand)) <= 64 * 1024)
 
