@@ -36,7 +36,33 @@ class ModelInfo:
     source: str
 
 
-MODEL_KINDS = ("yolov5n", "mobilenetv2", "pipeline", "detector", "classifier")
+MODEL_KINDS = ("yolov5n", "mobilenetv2", "pipeline", "detector", "classifier", "split")
+
+
+def build_session(kind: str, yolo=None, mnet=None, *, device: int = 0, buckets=None, dtype: str | None = None,
+                  **kw):
+    """The one construction point of a compiled GPU model (every server backend and the registry use it).
+
+    kind: ``yolov5n`` / ``mobilenetv2`` (raw tensor models, the model server's per-model entries),
+    ``pipeline`` (fused detector -> crops -> classifier), ``detector`` / ``classifier`` (the microservices
+    halves) or ``split`` (pipeline with detection on ``device`` and classification on ``cls_device``).
+    Extra keywords go to the engine class (weights, host_threads, crop_cap_per_image, cls_device)."""
+    from .pipeline import GpuClassifier, GpuDetector, GpuPipeline, GpuTensorModel, SplitPipeline
+
+    common = dict(buckets=buckets, dtype=dtype)
+    if kind == "yolov5n":
+        return GpuTensorModel.yolo(yolo, device=device, **common)
+    if kind == "mobilenetv2":
+        return GpuTensorModel.mobilenet(mnet, device=device, **common)
+    if kind == "pipeline":
+        return GpuPipeline(yolo, mnet, device=device, **common, **kw)
+    if kind == "detector":
+        return GpuDetector(yolo, device=device, **common)
+    if kind == "classifier":
+        return GpuClassifier(mnet, device=device, **common)
+    if kind == "split":
+        return SplitPipeline(yolo, mnet, det_device=device, cls_device=int(kw.pop("cls_device", 1)), **common, **kw)
+    raise KeyError(f"unknown model '{kind}' (available: {', '.join(MODEL_KINDS)})")
 
 
 class ModelRegistry:
@@ -55,22 +81,12 @@ class ModelRegistry:
         return resolve_models(str(self.models_dir) if self.models_dir else None, self.config.weight_seed)
 
     def _build(self, name: str):
-        from .pipeline import GpuClassifier, GpuDetector, GpuPipeline, GpuTensorModel
-
         yolo, mnet = self._modules()
         c = self.config
-        kw = dict(device=c.device, buckets=c.buckets)
-        if name == "yolov5n":
-            return GpuTensorModel.yolo(yolo, **kw)
-        if name == "mobilenetv2":
-            return GpuTensorModel.mobilenet(mnet, **kw)
+        kw = {}
         if name == "pipeline":
-            return GpuPipeline(yolo, mnet, host_threads=c.host_threads, crop_cap_per_image=c.crop_cap_per_image, **kw)
-        if name == "detector":
-            return GpuDetector(yolo, **kw)
-        if name == "classifier":
-            return GpuClassifier(mnet, **kw)
-        raise KeyError(f"unknown model '{name}' (available: {', '.join(MODEL_KINDS)})")
+            kw = dict(host_threads=c.host_threads, crop_cap_per_image=c.crop_cap_per_image)
+        return build_session(name, yolo, mnet, device=c.device, buckets=c.buckets, **kw)
 
     def get_session(self, name: str):
         with self._lock:

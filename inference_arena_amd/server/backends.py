@@ -73,11 +73,11 @@ class GpuBatchedBackend(Backend):
                  devices: list[int] | None = None):
         """``instances`` pipelines on each GPU of ``devices`` (default: ``[device]``) behind one batcher queue:
         each instance thread pulls the next batch for its own GPU (data parallel within one process)."""
-        from ..engine.pipeline import GpuPipeline
+        from ..engine.registry import build_session
 
         bk = buckets or sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
         self.devices = [int(d) for d in (devices or [device])]
-        self.pipes = [GpuPipeline(yolo, mnet, device=d, buckets=bk, weights=weights)
+        self.pipes = [build_session("pipeline", yolo, mnet, device=d, buckets=bk, weights=weights)
                       for d in self.devices for _ in range(instances)]
         self.batcher = AsyncBatcher(self.pipes, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us, max_queue_size=max_queue_size)
@@ -115,11 +115,11 @@ class GpuSplitBackend(GpuBatchedBackend):
     def __init__(self, yolo, mnet, *, det_device: int = 0, cls_device: int = 1, instances: int = 1,
                  max_batch: int = 32, preferred: list[int] | None = None, max_queue_delay_us: int = 500,
                  max_queue_size: int = 4096, buckets: list[int] | None = None):
-        from ..engine.pipeline import SplitPipeline
+        from ..engine.registry import build_session
 
         bk = buckets or sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
         self.devices = [int(det_device), int(cls_device)]
-        self.pipes = [SplitPipeline(yolo, mnet, det_device=det_device, cls_device=cls_device, buckets=bk)
+        self.pipes = [build_session("split", yolo, mnet, device=det_device, cls_device=cls_device, buckets=bk)
                       for _ in range(instances)]
 
         class _Inst:  # AsyncBatcher schedules `.ex`: the split batch instance

@@ -119,15 +119,14 @@ class TensorModel(ModelHandle):
         self.arch = arch
         self.device = device
         if device == "gpu":
-            from ..engine.pipeline import GpuTensorModel
-
+            from ..engine.registry import build_session
             from ..parallel.placement import instance_devices
 
             # Triton semantics: `count` instances on each GPU of the group (all visible GPUs when none listed)
             self.devices = instance_devices(list(cfg.instance_group), default_gpu=gpu)
             buckets = sorted({b for b in (1, 2, 4, 8, 16, 32, self.max_batch) if b <= max(self.max_batch, 1)})
-            make = GpuTensorModel.yolo if arch == "yolov5nu" else GpuTensorModel.mobilenet
-            self.runners = [make(module, device=d, buckets=buckets) for d in self.devices]
+            kind = "yolov5n" if arch == "yolov5nu" else "mobilenetv2"
+            self.runners = [build_session(kind, module, module, device=d, buckets=buckets) for d in self.devices]
             db = cfg.dynamic_batching if cfg.HasField("dynamic_batching") else None
             self.batcher = AsyncBatcher(self.runners, max_batch=self.max_batch,
                                         preferred=list(db.preferred_batch_size) if db else None,

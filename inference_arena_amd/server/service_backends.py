@@ -51,11 +51,12 @@ class GpuClassifierBackend(ClassifierBackend):
     def __init__(self, mnet, *, device: int = 0, instances: int = 1, max_batch: int = 64,
                  max_queue_delay_us: int = 300, preferred: list[int] | None = None,
                  devices: list[int] | None = None):
-        from ..engine.pipeline import GpuClassifier
+        from ..engine.registry import build_session
 
         bk = _default_buckets(max_batch)
         self.devices = [int(d) for d in (devices or [device])]
-        self.runners = [GpuClassifier(mnet, device=d, buckets=bk) for d in self.devices for _ in range(instances)]
+        self.runners = [build_session("classifier", mnet=mnet, device=d, buckets=bk)
+                        for d in self.devices for _ in range(instances)]
         self.batcher = AsyncBatcher(self.runners, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us)
 
@@ -130,11 +131,12 @@ class GpuDetectorBackend(DetectorBackend):
     def __init__(self, yolo, *, device: int = 0, instances: int = 1, max_batch: int = 32,
                  max_queue_delay_us: int = 500, preferred: list[int] | None = None,
                  devices: list[int] | None = None):
-        from ..engine.pipeline import GpuDetector
+        from ..engine.registry import build_session
 
         bk = _default_buckets(max_batch)
         self.devices = [int(d) for d in (devices or [device])]
-        self.runners = [GpuDetector(yolo, device=d, buckets=bk) for d in self.devices for _ in range(instances)]
+        self.runners = [build_session("detector", yolo, device=d, buckets=bk)
+                        for d in self.devices for _ in range(instances)]
         self.batcher = AsyncBatcher(self.runners, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us)
 

@@ -73,6 +73,40 @@ def test_registry_surface():
     reset_default_registry()
 
 
+def test_build_session_is_the_construction_point(monkeypatch):
+    """Every server backend builds its GPU models through engine.registry.build_session (one factory for
+    the registry and the three serving arms); it dispatches each model kind to its engine class."""
+    import inspect
+
+    from inference_arena_amd.engine import pipeline as P
+    from inference_arena_amd.engine import registry as R
+    from inference_arena_amd.server import backends, modelserver_core, service_backends
+
+    made = []
+
+    def fake(tag):
+        def ctor(*a, **kw):
+            made.append((tag, kw.get("device", kw.get("det_device")), kw.get("dtype")))
+            return tag
+        return ctor
+    monkeypatch.setattr(P, "GpuPipeline", fake("pipeline"))
+    monkeypatch.setattr(P, "GpuDetector", fake("detector"))
+    monkeypatch.setattr(P, "GpuClassifier", fake("classifier"))
+    monkeypatch.setattr(P, "SplitPipeline", fake("split"))
+    monkeypatch.setattr(P.GpuTensorModel, "yolo", classmethod(lambda cls, m, **kw: fake("yolo")(**kw)))
+    monkeypatch.setattr(P.GpuTensorModel, "mobilenet", classmethod(lambda cls, m, **kw: fake("mnet")(**kw)))
+    for kind, tag in (("pipeline", "pipeline"), ("detector", "detector"), ("classifier", "classifier"),
+                      ("split", "split"), ("yolov5n", "yolo"), ("mobilenetv2", "mnet")):
+        assert R.build_session(kind, object(), object(), device=3, buckets=[1], dtype="fp32") == tag
+    assert all(d == 3 and dt == "fp32" for _, d, dt in made)
+    with pytest.raises(KeyError):
+        R.build_session("resnet")
+    for mod in (backends, service_backends, modelserver_core):
+        src = inspect.getsource(mod)
+        assert "build_session(" in src
+        assert "GpuPipeline(" not in src and "GpuDetector(" not in src and "GpuClassifier(" not in src
+
+
 def test_generate_proto_text(tmp_path):
     import subprocess
     import sys
