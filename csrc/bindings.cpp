@@ -12,6 +12,8 @@
 
 #include "kernels/launch.h"
 #include "runtime/executor.h"
+#include "runtime/echo_instance.h"
+#include "runtime/http_front.h"
 #include "runtime/batcher.h"
 #include "runtime/split.h"
 
@@ -496,12 +498,17 @@ PYBIND11_MODULE(_C, m) {
       .def("num_slots", &SplitInstance::num_slots)
       .def("buckets", &SplitInstance::buckets);
 
+  py::class_<EchoInstance, std::shared_ptr<EchoInstance>>(m, "EchoInstance")
+      .def(py::init<int, int, int>(), py::arg("slots") = 2, py::arg("max_batch") = 32, py::arg("max_det") = 4);
+
   py::class_<DynamicBatcher>(m, "DynamicBatcher")
       .def(py::init([](py::list executors, const py::dict& cfg) {
              std::vector<std::shared_ptr<BatchInstance>> inst;
              for (auto h : executors) {
                if (py::isinstance<SplitInstance>(h))
                  inst.push_back(h.cast<std::shared_ptr<SplitInstance>>());
+               else if (py::isinstance<EchoInstance>(h))
+                 inst.push_back(h.cast<std::shared_ptr<EchoInstance>>());
                else
                  inst.push_back(h.cast<std::shared_ptr<Executor>>());
              }
@@ -591,5 +598,60 @@ PYBIND11_MODULE(_C, m) {
       .def("shutdown", [](DynamicBatcher& b) {
         py::gil_scoped_release nogil;
         b.shutdown();
+      });
+
+  py::class_<HttpFrontEnd>(m, "HttpFrontEnd")
+      .def(py::init([](DynamicBatcher& batcher, const py::dict& ch, std::vector<std::string> labels,
+                       const py::dict& cfg) {
+             DecodeChannel dc;
+             dc.shm = (uint8_t*)(uintptr_t)get<int64_t>(ch, "shm_addr", 0);
+             dc.stride = get<int64_t>(ch, "stride", 0);
+             dc.in_bytes = get<int64_t>(ch, "in_bytes", 0);
+             dc.slot_bytes = get<int64_t>(ch, "slot_bytes", 0);
+             dc.slots = get<int>(ch, "slots", 0);
+             dc.task_fds = get<std::vector<int>>(ch, "task_fds", {});
+             dc.big_fds = get<std::vector<int>>(ch, "big_fds", {});
+             dc.result_fd = get<int>(ch, "result_fd", -1);
+             dc.result_wfd = get<int>(ch, "result_wfd", -1);
+             FrontConfig c;
+             c.host = get<std::string>(cfg, "host", c.host);
+             c.port = get<int>(cfg, "port", c.port);
+             c.io_threads = get<int>(cfg, "io_threads", c.io_threads);
+             c.reuse_port = get<bool>(cfg, "reuse_port", c.reuse_port);
+             c.softmax_confidence = get<bool>(cfg, "softmax_confidence", c.softmax_confidence);
+             c.max_body = get<int64_t>(cfg, "max_body", c.max_body);
+             c.replica_tag = get<std::string>(cfg, "replica_tag", c.replica_tag);
+             py::gil_scoped_release nogil;
+             return new HttpFrontEnd(&batcher, dc, std::move(labels), c);
+           }),
+           py::keep_alive<1, 2>())
+      .def_property_readonly("port", &HttpFrontEnd::port)
+      .def("set_healthy", &HttpFrontEnd::set_healthy)
+      .def("set_metrics_text", &HttpFrontEnd::set_metrics_text)
+      .def("stats",
+           [](HttpFrontEnd& f) {
+             FrontStats s = f.stats();
+             py::dict d;
+             d["requests"] = s.requests;
+             d["ok"] = s.ok;
+             d["bad_request"] = s.bad_request;
+             d["too_large"] = s.too_large;
+             d["unavailable"] = s.unavailable;
+             d["errors"] = s.errors;
+             d["not_found"] = s.not_found;
+             d["connections"] = s.connections;
+             d["open_connections"] = s.open_connections;
+             d["detections"] = s.detections;
+             d["sum_total_ms"] = s.sum_total_ms;
+             d["sum_decode_ms"] = s.sum_decode_ms;
+             d["sum_queue_ms"] = s.sum_queue_ms;
+             d["sum_gpu_ms"] = s.sum_gpu_ms;
+             d["latency_hist"] = s.latency_hist;
+             d["latency_buckets_ms"] = kLatencyBucketsMs;
+             return d;
+           })
+      .def("stop", [](HttpFrontEnd& f) {
+        py::gil_scoped_release nogil;
+        f.stop();
       });
 }

@@ -1,0 +1,90 @@
+// A host-only BatchInstance: answers every image with a deterministic set of
+// detections derived from its size and first pixel, without a GPU.  It lets
+// the dynamic batcher and the native HTTP front end (http_front.h) be tested
+// end to end on CPU machines (tests/test_native_http.py) and measured for
+// their own host cost (tools/http_overhead.py --native).
+#pragma once
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <vector>
+
+#include "instance.h"
+
+namespace arena {
+
+class EchoInstance : public BatchInstance {
+ public:
+  EchoInstance(int slots, int max_batch, int max_det = 4) : slots_(slots), max_batch_(max_batch), max_det_(max_det),
+                                                            results_(slots), busy_(slots, false) {}
+  std::vector<int> buckets() const override {
+    std::vector<int> b;
+    for (int v = 1; v < max_batch_; v *= 2) b.push_back(v);
+    b.push_back(max_batch_);
+    return b;
+  }
+  int num_slots() const override { return slots_; }
+  int max_det() const override { return max_det_; }
+  int64_t raw_out_bytes() const override { return 0; }
+
+  // Image i of a batch gets min(max_det, 1 + first_byte % max_det) detections: box k spans
+  // (k, k, w - k, h - k), confidence 0.9 - 0.1 k, COCO class k; crop top-5 = classes 10k .. 10k + 4.
+  int submit(const std::vector<InputImage>& imgs) override {
+    if (imgs.empty() || (int)imgs.size() > max_batch_) throw std::runtime_error("EchoInstance: bad batch size");
+    std::lock_guard<std::mutex> lk(mu_);
+    int s = -1;
+    for (int i = 0; i < slots_; ++i)
+      if (!busy_[i]) { s = i; break; }
+    if (s < 0) throw std::runtime_error("EchoInstance: all slots busy");
+    BatchResult r;
+    const int n = (int)imgs.size();
+    r.n_images = n;
+    r.det_count.resize(n);
+    r.det.resize((size_t)n * max_det_);
+    r.crop_offset.resize(n + 1);
+    int total = 0;
+    for (int i = 0; i < n; ++i) {
+      const int k_n = std::min(max_det_, 1 + imgs[i].data[0] % max_det_);
+      r.det_count[i] = k_n;
+      r.crop_offset[i] = total;
+      for (int k = 0; k < k_n; ++k) {
+        Detection& d = r.det[(size_t)i * max_det_ + k];
+        d.x1 = (float)k;
+        d.y1 = (float)k;
+        d.x2 = (float)(imgs[i].w - k);
+        d.y2 = (float)(imgs[i].h - k);
+        d.conf = 0.9f - 0.1f * (float)k;
+        d.cls = k;
+        TopkResult t{};
+        for (int j = 0; j < 5; ++j) {
+          t.idx[j] = 10 * k + j;
+          t.logit[j] = 5.0f - (float)j;
+          t.prob[j] = 0.5f / (float)(j + 1);
+        }
+        r.topk.push_back(t);
+      }
+      total += k_n;
+    }
+    r.crop_offset[n] = total;
+    r.total_crops = total;
+    results_[s] = std::move(r);
+    busy_[s] = true;
+    return s;
+  }
+
+  BatchResult collect(int slot) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (slot < 0 || slot >= slots_ || !busy_[slot]) throw std::runtime_error("EchoInstance: bad slot");
+    busy_[slot] = false;
+    return std::move(results_[slot]);
+  }
+
+ private:
+  int slots_, max_batch_, max_det_;
+  std::vector<BatchResult> results_;
+  std::vector<bool> busy_;
+  std::mutex mu_;
+};
+
+}  // namespace arena

@@ -1,0 +1,804 @@
+// Native HTTP/1.1 front end (see http_front.h).
+#include "http_front.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <stdexcept>
+
+namespace arena {
+
+const std::vector<double> kLatencyBucketsMs = {1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, 2000, 5000};
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+std::string lower(std::string s) {
+  for (auto& ch : s) ch = (char)std::tolower((unsigned char)ch);
+  return s;
+}
+
+std::string trim(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
+  while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t' || s[b - 1] == '\r')) --b;
+  return s.substr(a, b - a);
+}
+
+void json_escape(std::string& out, const std::string& s) {
+  out.push_back('"');
+  for (unsigned char ch : s) {
+    if (ch == '"') out += "\\\"";
+    else if (ch == '\\') out += "\\\\";
+    else if (ch < 0x20) {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", ch);
+      out += b;
+    } else out.push_back((char)ch);
+  }
+  out.push_back('"');
+}
+
+void json_num(std::string& out, double v) {
+  if (!std::isfinite(v)) {
+    out += "null";
+    return;
+  }
+  char b[32];
+  snprintf(b, sizeof b, "%.9g", v);
+  out += b;
+}
+
+std::string detail_json(const std::string& msg) {
+  std::string s = "{\"detail\":";
+  json_escape(s, msg);
+  s += "}";
+  return s;
+}
+
+std::string uuid4() {
+  thread_local std::mt19937_64 rng(std::random_device{}() ^ (uint64_t)Clock::now().time_since_epoch().count());
+  uint64_t a = rng(), b = rng();
+  a = (a & 0xffffffffffff0fffULL) | 0x0000000000004000ULL;  // version 4
+  b = (b & 0x3fffffffffffffffULL) | 0x8000000000000000ULL;  // variant 10
+  char s[40];
+  snprintf(s, sizeof s, "%08x-%04x-%04x-%04x-%012llx", (unsigned)(a >> 32), (unsigned)((a >> 16) & 0xffff),
+           (unsigned)(a & 0xffff), (unsigned)(b >> 48), (unsigned long long)(b & 0xffffffffffffULL));
+  return s;
+}
+
+const char* reason(int code) {
+  switch (code) {
+    case 200: return "OK";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 411: return "Length Required";
+    case 413: return "Payload Too Large";
+    case 422: return "Unprocessable Entity";
+    case 431: return "Request Header Fields Too Large";
+    case 500: return "Internal Server Error";
+    case 503: return "Service Unavailable";
+    default: return "Unknown";
+  }
+}
+
+bool write_all(int fd, const void* p, size_t n) {
+  const char* c = (const char*)p;
+  while (n > 0) {
+    const ssize_t k = ::write(fd, c, n);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+bool read_all(int fd, void* p, size_t n) {
+  char* c = (char*)p;
+  while (n > 0) {
+    const ssize_t k = ::read(fd, c, n);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+// multipart/form-data: the part named `field`; returns false when absent / malformed
+bool multipart_field(const std::string& body, const std::string& ctype, const std::string& field, size_t& off,
+                     size_t& len, std::string& err) {
+  const std::string lc = lower(ctype);
+  size_t bp = lc.find("boundary=");
+  if (bp == std::string::npos) {
+    err = "multipart body without a boundary";
+    return false;
+  }
+  std::string boundary = ctype.substr(bp + 9);
+  const size_t semi = boundary.find(';');
+  if (semi != std::string::npos) boundary = boundary.substr(0, semi);
+  boundary = trim(boundary);
+  if (boundary.size() >= 2 && boundary.front() == '"' && boundary.back() == '"')
+    boundary = boundary.substr(1, boundary.size() - 2);
+  if (boundary.empty()) {
+    err = "multipart body without a boundary";
+    return false;
+  }
+  const std::string delim = "--" + boundary;
+  size_t pos = body.find(delim);
+  while (pos != std::string::npos) {
+    pos += delim.size();
+    if (body.compare(pos, 2, "--") == 0) break;  // closing delimiter
+    if (body.compare(pos, 2, "\r\n") == 0) pos += 2;
+    const size_t hend = body.find("\r\n\r\n", pos);
+    if (hend == std::string::npos) break;
+    const std::string headers = lower(body.substr(pos, hend - pos));
+    const size_t dstart = hend + 4;
+    const size_t dend = body.find("\r\n" + delim, dstart);
+    if (dend == std::string::npos) break;
+    const std::string want = "name=\"" + lower(field) + "\"";
+    if (headers.find("content-disposition") != std::string::npos && headers.find(want) != std::string::npos) {
+      off = dstart;
+      len = dend - dstart;
+      return true;
+    }
+    pos = dend + 2;
+  }
+  err = "missing form field '" + field + "'";
+  return false;
+}
+
+}  // namespace
+
+struct HttpFrontEnd::Conn {
+  int fd = -1, ep = -1;
+  std::mutex mu;             // out / closed / busy (the response may come from any thread)
+  std::string in;            // I/O thread only
+  std::string out;
+  size_t out_off = 0;
+  bool closed = false, busy = false, close_after = false;
+};
+
+struct HttpFrontEnd::Pending {
+  std::shared_ptr<Conn> conn;
+  int worker = 0;
+  Clock::time_point t0, t_dec;
+};
+
+HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vector<std::string> labels,
+                           FrontConfig cfg)
+    : batcher_(batcher), dc_(std::move(dc)), labels_(std::move(labels)), cfg_(std::move(cfg)) {
+  if (batcher_ == nullptr) throw std::runtime_error("HttpFrontEnd: no batcher");
+  if (dc_.shm == nullptr || dc_.slots <= 0 || dc_.task_fds.empty() || dc_.result_fd < 0 || dc_.result_wfd < 0)
+    throw std::runtime_error("HttpFrontEnd: incomplete decode channel");
+  if (dc_.big_fds.size() != dc_.task_fds.size()) throw std::runtime_error("HttpFrontEnd: big_fds / task_fds mismatch");
+  stats_.latency_hist.assign(kLatencyBucketsMs.size() + 1, 0);
+  for (int s = dc_.slots - 1; s >= 0; --s) free_slots_.push_back(s);
+  for (size_t i = 0; i < dc_.task_fds.size(); ++i) task_mu_.emplace_back(new std::mutex);
+  load_ = std::vector<std::atomic<int>>(dc_.task_fds.size());
+  for (auto& l : load_) l.store(0);
+
+  listen_fd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (listen_fd_ < 0) throw std::runtime_error("HttpFrontEnd: socket() failed");
+  int one = 1;
+  setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  if (cfg_.reuse_port) setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+  sockaddr_in addr{};
+  addr.sin_family = AF_INET;
+  addr.sin_port = htons((uint16_t)cfg_.port);
+  if (inet_pton(AF_INET, cfg_.host.c_str(), &addr.sin_addr) != 1) addr.sin_addr.s_addr = htonl(INADDR_ANY);
+  if (::bind(listen_fd_, (sockaddr*)&addr, sizeof addr) != 0 || ::listen(listen_fd_, 1024) != 0) {
+    const std::string e = strerror(errno);
+    ::close(listen_fd_);
+    throw std::runtime_error("HttpFrontEnd: cannot listen on port " + std::to_string(cfg_.port) + ": " + e);
+  }
+  socklen_t al = sizeof addr;
+  getsockname(listen_fd_, (sockaddr*)&addr, &al);
+  port_ = ntohs(addr.sin_port);
+  stop_efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+
+  const int n = std::max(1, cfg_.io_threads);
+  for (int i = 0; i < n; ++i) {
+    const int ep = epoll_create1(EPOLL_CLOEXEC);
+    epoll_event ev{};
+    ev.events = EPOLLIN | EPOLLEXCLUSIVE;
+    ev.data.fd = listen_fd_;
+    epoll_ctl(ep, EPOLL_CTL_ADD, listen_fd_, &ev);
+    epoll_event sv{};
+    sv.events = EPOLLIN;
+    sv.data.fd = stop_efd_;
+    epoll_ctl(ep, EPOLL_CTL_ADD, stop_efd_, &sv);
+    epfds_.push_back(ep);
+  }
+  for (int i = 0; i < n; ++i) io_threads_.emplace_back([this, i] { io_loop(i); });
+  collector_ = std::thread([this] { collector_loop(); });
+}
+
+HttpFrontEnd::~HttpFrontEnd() { stop(); }
+
+void HttpFrontEnd::stop() {
+  if (stop_.exchange(true)) return;
+  uint64_t one = 1;
+  if (write(stop_efd_, &one, sizeof one) < 0) { /* the flag alone stops the loops on their next wakeup */ }
+  // wake the collector with a sentinel completion record (key < 0)
+  int64_t rec[4] = {-1, 0, 0, 0};
+  write_all(dc_.result_wfd, rec, sizeof rec);
+  for (auto& t : io_threads_)
+    if (t.joinable()) t.join();
+  if (collector_.joinable()) collector_.join();
+  for (int ep : epfds_) ::close(ep);
+  epfds_.clear();
+  if (listen_fd_ >= 0) ::close(listen_fd_);
+  listen_fd_ = -1;
+  if (stop_efd_ >= 0) ::close(stop_efd_);
+  stop_efd_ = -1;
+  std::lock_guard<std::mutex> lk(pend_mu_);
+  pending_.clear();
+}
+
+void HttpFrontEnd::set_metrics_text(std::string text) {
+  std::lock_guard<std::mutex> lk(metrics_mu_);
+  metrics_text_ = std::move(text);
+}
+
+FrontStats HttpFrontEnd::stats() {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  return stats_;
+}
+
+void HttpFrontEnd::io_loop(int idx) {
+  const int ep = epfds_[idx];
+  std::unordered_map<int, std::shared_ptr<Conn>> conns;
+  std::vector<epoll_event> evs(256);
+  while (!stop_.load()) {
+    const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 200);
+    for (int i = 0; i < n && !stop_.load(); ++i) {
+      const int fd = evs[i].data.fd;
+      if (fd == stop_efd_) continue;
+      if (fd == listen_fd_) {
+        while (true) {
+          const int c = accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (c < 0) break;
+          int one = 1;
+          setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+          auto conn = std::make_shared<Conn>();
+          conn->fd = c;
+          conn->ep = ep;
+          conns[c] = conn;
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.fd = c;
+          epoll_ctl(ep, EPOLL_CTL_ADD, c, &ev);
+          std::lock_guard<std::mutex> lk(stats_mu_);
+          ++stats_.connections;
+          ++stats_.open_connections;
+        }
+        continue;
+      }
+      auto it = conns.find(fd);
+      if (it == conns.end()) continue;
+      auto c = it->second;
+      if (evs[i].events & EPOLLOUT) handle_writable(ep, c);
+      if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) handle_readable(ep, c);
+      bool closed;
+      {
+        std::lock_guard<std::mutex> lk(c->mu);
+        closed = c->closed;
+      }
+      if (closed) conns.erase(fd);
+    }
+  }
+  for (auto& kv : conns) close_conn(ep, kv.second);
+}
+
+void HttpFrontEnd::close_conn(int ep, const std::shared_ptr<Conn>& c) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->closed) return;
+  c->closed = true;
+  epoll_ctl(ep, EPOLL_CTL_DEL, c->fd, nullptr);
+  ::close(c->fd);  // under the lock: a response thread never touches a reused descriptor
+  std::lock_guard<std::mutex> sl(stats_mu_);
+  --stats_.open_connections;
+}
+
+void HttpFrontEnd::handle_readable(int ep, const std::shared_ptr<Conn>& c) {
+  char buf[65536];
+  bool eof = false;
+  while (true) {
+    const ssize_t k = ::read(c->fd, buf, sizeof buf);
+    if (k > 0) {
+      c->in.append(buf, (size_t)k);
+      continue;
+    }
+    if (k == 0) eof = true;
+    else if (errno == EINTR) continue;
+    else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
+    break;
+  }
+  while (true) {
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (c->busy || c->closed) break;
+    }
+    if (!parse_one(c)) break;
+  }
+  if (eof) {
+    bool busy;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      busy = c->busy;
+      c->close_after = true;
+    }
+    if (!busy) close_conn(ep, c);
+    else {  // the peer half-closed with a request in flight: answer it, then close
+      epoll_event ev{};
+      ev.events = 0;
+      ev.data.fd = c->fd;
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (!c->closed) epoll_ctl(ep, EPOLL_CTL_MOD, c->fd, &ev);
+    }
+  }
+}
+
+void HttpFrontEnd::handle_writable(int ep, const std::shared_ptr<Conn>& c) {
+  bool done = false, close_now = false;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->closed) return;
+    while (c->out_off < c->out.size()) {
+      const ssize_t k = ::send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+      if (k > 0) {
+        c->out_off += (size_t)k;
+        continue;
+      }
+      if (k < 0 && errno == EINTR) continue;
+      if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+      close_now = true;  // peer gone
+      break;
+    }
+    if (!close_now && c->out_off >= c->out.size()) {
+      c->out.clear();
+      c->out_off = 0;
+      c->busy = false;
+      done = true;
+      if (c->close_after) close_now = true;
+      else {
+        epoll_event ev{};
+        ev.events = EPOLLIN | EPOLLRDHUP;
+        ev.data.fd = c->fd;
+        epoll_ctl(ep, EPOLL_CTL_MOD, c->fd, &ev);
+      }
+    }
+  }
+  if (close_now) {
+    close_conn(ep, c);
+    return;
+  }
+  if (done) {
+    while (true) {  // requests the client sent ahead (pipelining)
+      {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (c->busy || c->closed) break;
+      }
+      if (!parse_one(c)) break;
+    }
+  }
+}
+
+bool HttpFrontEnd::parse_one(const std::shared_ptr<Conn>& c) {
+  std::string& in = c->in;
+  const size_t hend = in.find("\r\n\r\n");
+  if (hend == std::string::npos) {
+    if (in.size() > 65536) {
+      {
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->busy = true;
+        c->close_after = true;
+      }
+      in.clear();
+      respond(c, 431, "application/json", detail_json("request headers too large"));
+      return true;
+    }
+    return false;
+  }
+  const size_t le = in.find("\r\n");
+  const std::string line = in.substr(0, le);
+  const size_t s1 = line.find(' '), s2 = line.rfind(' ');
+  auto bad = [&](int code, const std::string& msg) {
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->busy = true;
+      c->close_after = true;
+    }
+    in.clear();
+    {
+      std::lock_guard<std::mutex> sl(stats_mu_);
+      ++stats_.requests;
+      ++stats_.bad_request;
+    }
+    respond(c, code, "application/json", detail_json(msg));
+    return true;
+  };
+  if (s1 == std::string::npos || s2 == s1) return bad(400, "malformed request line");
+  const std::string method = line.substr(0, s1);
+  std::string path = line.substr(s1 + 1, s2 - s1 - 1);
+  const std::string version = line.substr(s2 + 1);
+  const size_t q = path.find('?');
+  if (q != std::string::npos) path = path.substr(0, q);
+  int64_t clen = -1;
+  bool chunked = false, close_req = version == "HTTP/1.0";
+  std::string ctype;
+  size_t p = le + 2;
+  while (p < hend) {
+    size_t e = in.find("\r\n", p);
+    if (e == std::string::npos || e > hend) e = hend;
+    const std::string h = in.substr(p, e - p);
+    const size_t colon = h.find(':');
+    if (colon != std::string::npos) {
+      const std::string name = lower(trim(h.substr(0, colon)));
+      const std::string val = trim(h.substr(colon + 1));
+      if (name == "content-length") clen = std::atoll(val.c_str());
+      else if (name == "transfer-encoding") chunked = lower(val).find("chunked") != std::string::npos;
+      else if (name == "content-type") ctype = val;
+      else if (name == "connection") {
+        const std::string v = lower(val);
+        if (v.find("close") != std::string::npos) close_req = true;
+        else if (v.find("keep-alive") != std::string::npos) close_req = false;
+      }
+    }
+    p = e + 2;
+  }
+  const size_t body0 = hend + 4;
+  std::string body;
+  size_t consumed;
+  if (chunked) {
+    size_t pos = body0;
+    while (true) {
+      const size_t e = in.find("\r\n", pos);
+      if (e == std::string::npos) return false;
+      const long long n = std::strtoll(in.substr(pos, e - pos).c_str(), nullptr, 16);
+      if (n < 0) return bad(400, "malformed chunk size");
+      if ((int64_t)body.size() + n > cfg_.max_body) return bad(413, "request body too large");
+      if (in.size() < e + 2 + (size_t)n + 2) return false;
+      if (n == 0) {  // last chunk, then optional trailers ending with an empty line
+        const size_t tend = in.find("\r\n\r\n", e);
+        if (in.compare(e + 2, 2, "\r\n") == 0) consumed = e + 4;
+        else if (tend != std::string::npos) consumed = tend + 4;
+        else return false;
+        break;
+      }
+      body.append(in, e + 2, (size_t)n);
+      pos = e + 2 + (size_t)n + 2;
+    }
+  } else {
+    if (clen < 0) clen = 0;
+    if (clen > cfg_.max_body) return bad(413, "request body too large");
+    if (in.size() < body0 + (size_t)clen) return false;
+    body.assign(in, body0, (size_t)clen);
+    consumed = body0 + (size_t)clen;
+  }
+  in.erase(0, consumed);
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->busy = true;
+    c->close_after = close_req;
+  }
+  dispatch(c, method, path, ctype, std::move(body));
+  return true;
+}
+
+void HttpFrontEnd::dispatch(const std::shared_ptr<Conn>& c, const std::string& method, const std::string& path,
+                            const std::string& ctype, std::string&& body) {
+  if (path == "/predict") {
+    if (method != "POST") {
+      respond(c, 405, "application/json", detail_json("Method Not Allowed"));
+      return;
+    }
+    predict(c, std::move(body), ctype);
+    return;
+  }
+  if (path == "/health" && method == "GET") {
+    if (healthy_.load())
+      respond(c, 200, "application/json", "{\"status\":\"healthy\",\"models_loaded\":true}");
+    else
+      respond(c, 503, "application/json", "{\"status\":\"unhealthy\",\"models_loaded\":false}");
+    return;
+  }
+  if (path == "/metrics" && method == "GET") {
+    std::string t;
+    {
+      std::lock_guard<std::mutex> lk(metrics_mu_);
+      t = metrics_text_;
+    }
+    respond(c, 200, "text/plain; version=0.0.4; charset=utf-8", t);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    ++stats_.not_found;
+  }
+  respond(c, 404, "application/json", detail_json("Not Found"));
+}
+
+void HttpFrontEnd::respond(const std::shared_ptr<Conn>& c, int code, const std::string& ctype,
+                           const std::string& body, bool) {
+  std::string r;
+  r.reserve(body.size() + 160);
+  char head[256];
+  bool close_after;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    close_after = c->close_after;
+  }
+  snprintf(head, sizeof head, "HTTP/1.1 %d %s\r\nContent-Type: %s\r\nContent-Length: %zu\r\n%s", code,
+           reason(code), ctype.c_str(), body.size(), close_after ? "Connection: close\r\n" : "");
+  r += head;
+  if (!cfg_.replica_tag.empty()) r += "x-arena-replica: " + cfg_.replica_tag + "\r\n";
+  r += "\r\n";
+  r += body;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (c->closed) return;
+  c->out += r;
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;  // the connection's I/O thread writes it
+  ev.data.fd = c->fd;
+  epoll_ctl(c->ep, EPOLL_CTL_MOD, c->fd, &ev);
+}
+
+void HttpFrontEnd::release_slot(int slot) {
+  std::lock_guard<std::mutex> lk(slot_mu_);
+  free_slots_.push_back(slot);
+}
+
+void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, const std::string& ctype) {
+  const auto t0 = Clock::now();
+  auto fail = [&](int code, const std::string& msg) {
+    {
+      std::lock_guard<std::mutex> sl(stats_mu_);
+      ++stats_.requests;
+      if (code == 413) ++stats_.too_large;
+      else if (code == 503) ++stats_.unavailable;
+      else if (code >= 500) ++stats_.errors;
+      else ++stats_.bad_request;
+    }
+    respond(c, code, "application/json", detail_json(msg));
+  };
+  if (!healthy_.load()) return fail(503, "Service not ready");
+  size_t off = 0, len = body.size();
+  if (lower(ctype).rfind("multipart/form-data", 0) == 0) {
+    std::string err;
+    if (!multipart_field(body, ctype, "file", off, len, err)) return fail(422, err);
+  }
+  if (len == 0) return fail(422, "empty request body");
+  int slot;
+  {
+    std::lock_guard<std::mutex> lk(slot_mu_);
+    if (free_slots_.empty()) slot = -1;
+    else {
+      slot = free_slots_.back();
+      free_slots_.pop_back();
+    }
+  }
+  if (slot < 0) return fail(503, "decode pool is saturated");
+  auto pend = std::make_shared<Pending>();
+  pend->conn = c;
+  pend->t0 = t0;
+  pend->t_dec = Clock::now();
+  const uint64_t key = next_key_.fetch_add(1);
+  // task record (server/decode_pool.py _TASK "<qii": key, slot, payload length or -1 = inline)
+  struct __attribute__((packed)) Task {
+    int64_t key;
+    int32_t slot, n;
+  } task{(int64_t)key, slot, (int32_t)len};
+  std::string msg;
+  if ((int64_t)len <= dc_.in_bytes) {
+    std::memcpy(dc_.shm + (size_t)slot * dc_.stride, body.data() + off, len);
+    msg.assign((const char*)&task, sizeof task);
+  } else {
+    task.n = -1;
+    msg.assign((const char*)&task, sizeof task);
+    msg.append(body, off, len);
+  }
+  int w = 0;
+  for (int i = 1; i < (int)load_.size(); ++i)
+    if (load_[i].load() < load_[w].load()) w = i;
+  load_[w].fetch_add(1);
+  pend->worker = w;
+  {
+    std::lock_guard<std::mutex> lk(pend_mu_);
+    pending_[key] = pend;
+  }
+  const uint32_t be = htonl((uint32_t)msg.size());  // multiprocessing Connection framing
+  bool ok;
+  {
+    std::lock_guard<std::mutex> lk(*task_mu_[w]);
+    ok = write_all(dc_.task_fds[w], &be, 4) && write_all(dc_.task_fds[w], msg.data(), msg.size());
+  }
+  if (!ok) {
+    load_[w].fetch_sub(1);
+    {
+      std::lock_guard<std::mutex> lk(pend_mu_);
+      pending_.erase(key);
+    }
+    release_slot(slot);
+    return fail(503, "decode workers unavailable");
+  }
+  // the worker's load is released when its completion record arrives (finish_decode)
+}
+
+void HttpFrontEnd::collector_loop() {
+  // completion record (server/decode_pool.py _DONE "<qiiiiq": key, slot, h, w, status, aux)
+  struct __attribute__((packed)) Done {
+    int64_t key;
+    int32_t slot, h, w, status;
+    int64_t aux;
+  };
+  static_assert(sizeof(Done) == 32, "completion record is 32 bytes");
+  Done d;
+  while (read_all(dc_.result_fd, &d, sizeof d)) {
+    if (d.key < 0 || stop_.load()) break;
+    finish_decode((uint64_t)d.key, d.slot, d.h, d.w, d.status, d.aux);
+  }
+}
+
+void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int status, int64_t aux) {
+  std::shared_ptr<Pending> pend;
+  {
+    std::lock_guard<std::mutex> lk(pend_mu_);
+    auto it = pending_.find(key);
+    if (it != pending_.end()) {
+      pend = it->second;
+      pending_.erase(it);
+    }
+  }
+  if (pend) load_[pend->worker].fetch_sub(1);
+  const uint8_t* out = dc_.shm + (size_t)slot * dc_.stride + dc_.in_bytes;
+  std::vector<uint8_t> big;
+  if (status == 2) {  // oversize result on worker `aux`'s pipe: Connection framing (4-byte BE length)
+    const int fd = dc_.big_fds[(size_t)aux];
+    uint32_t be = 0;
+    if (read_all(fd, &be, 4)) {
+      int64_t n = (int32_t)ntohl(be);
+      if (n == -1) {
+        uint64_t be8 = 0;
+        read_all(fd, &be8, 8);
+        n = (int64_t)__builtin_bswap64(be8);
+      }
+      big.resize((size_t)std::max<int64_t>(n, 0));
+      read_all(fd, big.data(), big.size());
+    }
+    out = big.data();
+  }
+  if (!pend) {
+    release_slot(slot);
+    return;
+  }
+  auto conn = pend->conn;
+  auto fail = [&](int code, const std::string& msg) {
+    {
+      std::lock_guard<std::mutex> sl(stats_mu_);
+      ++stats_.requests;
+      if (code == 413) ++stats_.too_large;
+      else if (code == 503) ++stats_.unavailable;
+      else ++stats_.errors;
+    }
+    respond(conn, code, "application/json", detail_json(msg));
+  };
+  if (status == 1) {
+    const std::string text((const char*)out, (size_t)std::max<int64_t>(0, std::min<int64_t>(aux, dc_.slot_bytes)));
+    release_slot(slot);
+    return fail(500, text);
+  }
+  if (status == 2 && big.size() != (size_t)h * w * 3) {
+    release_slot(slot);
+    return fail(500, "decode worker result lost");
+  }
+  const double decode_ms = ms_since(pend->t_dec);
+  const auto t_inf = Clock::now();
+  const bool softmax = cfg_.softmax_confidence;
+  const std::vector<std::string>* labels = &labels_;
+  FrontStats* stats = &stats_;
+  std::mutex* smu = &stats_mu_;
+  HttpFrontEnd* self = this;
+  const auto t0 = pend->t0;
+  ResultCallback cb = [self, conn, t0, t_inf, decode_ms, softmax, labels, stats, smu](RequestResult&& r) {
+    if (!r.error.empty()) {
+      {
+        std::lock_guard<std::mutex> sl(*smu);
+        ++stats->requests;
+        ++stats->errors;
+      }
+      self->respond(conn, 500, "application/json", detail_json(r.error));
+      return;
+    }
+    const double queue_ms = r.queue_us / 1e3, gpu_ms = r.compute_us / 1e3;
+    const double inference_ms = ms_since(t_inf);
+    std::string s;
+    s.reserve(512 + 256 * r.det.size());
+    s += "{\"request_id\":";
+    json_escape(s, uuid4());
+    s += ",\"detections\":[";
+    for (size_t i = 0; i < r.det.size(); ++i) {
+      const Detection& d = r.det[i];
+      if (i) s += ',';
+      s += "{\"detection\":{\"x1\":";
+      json_num(s, d.x1);
+      s += ",\"y1\":";
+      json_num(s, d.y1);
+      s += ",\"x2\":";
+      json_num(s, d.x2);
+      s += ",\"y2\":";
+      json_num(s, d.y2);
+      s += ",\"confidence\":";
+      json_num(s, d.conf);
+      s += ",\"class_id\":" + std::to_string(d.cls) + "},\"classification\":{\"class_id\":";
+      int cid = -1;
+      double conf = 0.0;
+      if (i < r.topk.size()) {
+        cid = r.topk[i].idx[0];
+        conf = softmax ? r.topk[i].prob[0] : r.topk[i].logit[0];
+      }
+      s += std::to_string(cid) + ",\"class_name\":";
+      json_escape(s, (cid >= 0 && cid < (int)labels->size()) ? (*labels)[cid] : std::string());
+      s += ",\"confidence\":";
+      json_num(s, conf);
+      s += "}}";
+    }
+    const double total_ms = ms_since(t0);
+    s += "],\"timing\":{\"queue_ms\":";
+    json_num(s, queue_ms);
+    s += ",\"gpu_ms\":";
+    json_num(s, gpu_ms);
+    s += ",\"batch_size\":";
+    json_num(s, r.batch_size);
+    s += ",\"detection_ms\":";
+    json_num(s, queue_ms + gpu_ms + decode_ms);
+    s += ",\"classification_ms\":0.0,\"inference_ms\":";
+    json_num(s, inference_ms);
+    s += ",\"decode_ms\":";
+    json_num(s, decode_ms);
+    s += ",\"total_ms\":";
+    json_num(s, total_ms);
+    s += "}}";
+    {
+      std::lock_guard<std::mutex> sl(*smu);
+      ++stats->requests;
+      ++stats->ok;
+      stats->detections += (int64_t)r.det.size();
+      stats->sum_total_ms += total_ms;
+      stats->sum_decode_ms += decode_ms;
+      stats->sum_queue_ms += queue_ms;
+      stats->sum_gpu_ms += gpu_ms;
+      size_t b = 0;
+      while (b < kLatencyBucketsMs.size() && total_ms > kLatencyBucketsMs[b]) ++b;
+      ++stats->latency_hist[b];
+    }
+    self->respond(conn, 200, "application/json", s);
+  };
+  const int64_t id = batcher_->enqueue(out, h, w, std::move(cb));
+  release_slot(slot);  // the batcher copied the pixels
+  if (id == -1) return fail(503, "request queue is full");
+  if (id == -2) return fail(413, "image exceeds the staging capacity of one batch");
+}
+
+}  // namespace arena

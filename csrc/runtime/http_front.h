@@ -1,0 +1,129 @@
+// Native HTTP/1.1 front end for the monolithic arm: POST /predict end to end
+// without the Python request path.
+//
+// The reference serves /predict from FastAPI (architectures/monolithic/app/
+// main.py:120-190: multipart upload -> cv2 decode -> ONNX detection ->
+// crops -> ONNX classification -> JSON).  The Python port of that handler
+// (server/monolithic.py) measured ~0.7-1.4 ms of interpreter time per request
+// (h11 parsing, starlette/fastapi dispatch, pydantic, logging; tools/
+// http_overhead.py), which capped one serving process far below the engine.
+// Here the whole request path is C++:
+//
+//   epoll I/O threads: accept, HTTP/1.1 keep-alive parsing (Content-Length or
+//   chunked), multipart/form-data field "file" or a raw image body
+//     -> the JPEG bytes go into a slot of the decode pool's shared memory and a
+//        16-byte task record to the least-loaded decode worker (the spawned PIL
+//        processes of server/decode_pool.py — JPEG decode stays in PIL)
+//   collector thread: completion records from the workers' shared pipe
+//     -> DynamicBatcher::enqueue straight from the shared-memory pixels
+//   batcher instance threads: results
+//     -> the reference's JSON schema (request_id, detections[{detection,
+//        classification}], timing) -> the connection's I/O thread writes it.
+//
+// GET /health (503 once set_healthy(false)), GET /metrics (text supplied by
+// the Python owner, which renders Prometheus from stats()).  Errors follow the
+// FastAPI handler: 422 bad upload, 413 too large, 503 queue full / not ready,
+// 500 decode or device failure, each with {"detail": ...}.
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "batcher.h"
+
+namespace arena {
+
+// The decode pool's transport (server/decode_pool.py ProcessDecodePool): shared memory of `slots` slots of
+// `stride` bytes (upload region of `in_bytes`, then the decoded pixels), one task pipe per worker
+// (multiprocessing Connection framing: 4-byte big-endian length + payload), the workers' shared completion
+// pipe (raw 32-byte records) and its write end (to wake the collector on stop), one pipe per worker for
+// oversize results (Connection framing).
+struct DecodeChannel {
+  uint8_t* shm = nullptr;
+  int64_t stride = 0, in_bytes = 0, slot_bytes = 0;
+  int slots = 0;
+  std::vector<int> task_fds, big_fds;
+  int result_fd = -1, result_wfd = -1;
+};
+
+struct FrontConfig {
+  std::string host = "0.0.0.0";
+  int port = 8100;
+  int io_threads = 4;
+  bool reuse_port = true;
+  bool softmax_confidence = false;  // ARENA_CONFIDENCE=softmax (default: the top-1 logit, as the reference)
+  int64_t max_body = 64 << 20;
+  std::string replica_tag;  // non-empty: an "x-arena-replica" header on every response (server/replica.py)
+};
+
+struct FrontStats {
+  int64_t requests = 0, ok = 0, bad_request = 0, too_large = 0, unavailable = 0, errors = 0, not_found = 0;
+  int64_t connections = 0, open_connections = 0, detections = 0;
+  double sum_total_ms = 0, sum_decode_ms = 0, sum_queue_ms = 0, sum_gpu_ms = 0;
+  std::vector<int64_t> latency_hist;  // counts per bucket of kLatencyBucketsMs (last = +Inf)
+};
+
+extern const std::vector<double> kLatencyBucketsMs;
+
+class HttpFrontEnd {
+ public:
+  HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vector<std::string> labels, FrontConfig cfg);
+  ~HttpFrontEnd();
+  HttpFrontEnd(const HttpFrontEnd&) = delete;
+  HttpFrontEnd& operator=(const HttpFrontEnd&) = delete;
+
+  int port() const { return port_; }
+  void set_healthy(bool h) { healthy_.store(h); }
+  void set_metrics_text(std::string text);
+  FrontStats stats();
+  void stop();
+
+  struct Conn;
+  struct Pending;
+
+ private:
+  void io_loop(int idx);
+  void collector_loop();
+  void handle_readable(int ep, const std::shared_ptr<Conn>& c);
+  void handle_writable(int ep, const std::shared_ptr<Conn>& c);
+  bool parse_one(const std::shared_ptr<Conn>& c);  // true: a full request was consumed
+  void dispatch(const std::shared_ptr<Conn>& c, const std::string& method, const std::string& path,
+                const std::string& ctype, std::string&& body);
+  void predict(const std::shared_ptr<Conn>& c, std::string&& body, const std::string& ctype);
+  void respond(const std::shared_ptr<Conn>& c, int code, const std::string& ctype, const std::string& body,
+               bool count_latency = false);
+  void close_conn(int ep, const std::shared_ptr<Conn>& c);
+  void finish_decode(uint64_t key, int slot, int h, int w, int status, int64_t aux);
+  void release_slot(int slot);
+
+  DynamicBatcher* batcher_;
+  DecodeChannel dc_;
+  std::vector<std::string> labels_;
+  FrontConfig cfg_;
+  int listen_fd_ = -1, port_ = 0, stop_efd_ = -1;
+  std::atomic<bool> stop_{false}, healthy_{true};
+  std::vector<std::thread> io_threads_;
+  std::thread collector_;
+  std::vector<int> epfds_;
+
+  std::mutex slot_mu_;
+  std::vector<int> free_slots_;
+  std::vector<std::unique_ptr<std::mutex>> task_mu_;
+  std::vector<std::atomic<int>> load_;
+
+  std::mutex pend_mu_;
+  std::unordered_map<uint64_t, std::shared_ptr<Pending>> pending_;
+  std::atomic<uint64_t> next_key_{1};
+
+  std::mutex metrics_mu_;
+  std::string metrics_text_;
+  std::mutex stats_mu_;
+  FrontStats stats_;
+};
+
+}  // namespace arena

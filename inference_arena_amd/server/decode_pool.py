@@ -89,7 +89,9 @@ class ProcessDecodePool:
     pool's collector thread and must consume the view before returning (the slot is reused afterwards)."""
 
     def __init__(self, workers: int | None = None, slots: int = 256, slot_pixels: int = 1024 * 1024,
-                 in_bytes: int = 1 << 20):
+                 in_bytes: int = 1 << 20, native: bool = False):
+        """``native=True``: the parent side of the transport is driven by C++ (the native HTTP front end,
+        csrc/runtime/http_front.h) through ``native_channel()``; no collector thread runs here."""
         self.workers = max(1, int(workers or min(16, os.cpu_count() or 4)))
         self.slots = int(slots)
         self.slot_bytes = int(slot_pixels) * 3
@@ -119,13 +121,32 @@ class ProcessDecodePool:
         self._lock = threading.Lock()
         self._seq = 0
         self._closed = False
-        self._collector = threading.Thread(target=self._collect, name="arena-decode-collector", daemon=True)
-        self._collector.start()
+        self.native = bool(native)
+        self._native_view = None
+        self._collector = None
+        if not self.native:
+            self._collector = threading.Thread(target=self._collect, name="arena-decode-collector", daemon=True)
+            self._collector.start()
+
+    def native_channel(self) -> dict:
+        """Shared-memory address, geometry and pipe descriptors for a native driver (see __init__)."""
+        import ctypes
+
+        if not self.native:
+            raise RuntimeError("native_channel() needs ProcessDecodePool(native=True)")
+        if self._native_view is None:
+            self._native_view = ctypes.c_char.from_buffer(self.shm.buf)
+        return {"shm_addr": ctypes.addressof(self._native_view), "stride": self._stride, "in_bytes": self.in_bytes,
+                "slot_bytes": self.slot_bytes, "slots": self.slots,
+                "task_fds": [c.fileno() for c in self._tasks], "big_fds": [c.fileno() for c in self._big],
+                "result_fd": self._res_r.fileno(), "result_wfd": self._res_w.fileno()}
 
     def submit(self, data: bytes, tag, callback: DecodeCallback) -> None:
         """Queue one encoded image; blocks while every slot is in use."""
         if self._closed:
             raise RuntimeError("decode pool is closed")
+        if self.native:
+            raise RuntimeError("a native decode pool is driven through native_channel()")
         slot = self._free.get()
         n = len(data)
         with self._lock:
@@ -194,8 +215,10 @@ class ProcessDecodePool:
             p.join(timeout=5)
             if p.is_alive():
                 p.terminate()
-        os.write(self._res_w.fileno(), _DONE.pack(-1, 0, 0, 0, 0, 0))
-        self._collector.join(timeout=5)
+        if self._collector is not None:
+            os.write(self._res_w.fileno(), _DONE.pack(-1, 0, 0, 0, 0, 0))
+            self._collector.join(timeout=5)
+        self._native_view = None
         for c in self._tasks + self._big + [self._res_r, self._res_w]:
             c.close()
         try:

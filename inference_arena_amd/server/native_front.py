@@ -1,0 +1,165 @@
+"""Monolithic arm with the native HTTP front end (csrc/runtime/http_front.h).
+
+Same contract as ``server/monolithic.py`` (reference architectures/monolithic/app/main.py: ``POST
+/predict`` multipart field ``file`` -> detections with classifications and timing; ``GET /health``;
+``GET /metrics``), but the request path never enters Python: C++ epoll threads parse HTTP, hand the
+JPEG to the spawned PIL decode processes through shared memory (server/decode_pool.py, native mode),
+enqueue the pixels into the native dynamic batcher and write the JSON response.  Python only builds
+the engines, renders Prometheus text once a second and watches for device faults.
+
+Run: ``python -m inference_arena_amd.server.native_front`` (PORT, ARENA_GPUS / ARENA_GPU,
+ARENA_INSTANCES, ARENA_DECODE_PROCS, ARENA_HTTP_THREADS, ...) or ``ARENA_NATIVE_HTTP=1`` with the
+replica launcher (parallel/replicas.py).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import signal
+import threading
+import time
+
+from prometheus_client import CollectorRegistry, generate_latest
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, HistogramMetricFamily
+
+from ..labels import load_labels
+from ..utils.logging import setup_logging
+from ..utils.settings import Settings
+from .decode_pool import ProcessDecodePool
+
+log = logging.getLogger("arena.native_front")
+
+
+class _Collector:
+    """Prometheus families of server/metrics (arena_*) rendered from the native counters."""
+
+    def __init__(self, front: "NativeFrontEnd", arch: str, gpu: str):
+        self.front, self.arch, self.gpu = front, arch, gpu
+
+    def collect(self):
+        s = self.front.stats()
+        b = self.front.batcher.stats()
+        req = CounterMetricFamily("arena_requests_total", "Requests by status", labels=["arch", "status"])
+        for status, key in (("ok", "ok"), ("bad_request", "bad_request"), ("too_large", "too_large"),
+                            ("unavailable", "unavailable"), ("error", "errors")):
+            req.add_metric([self.arch, status], s[key])
+        yield req
+        det = CounterMetricFamily("arena_detections_total", "Detections returned", labels=["arch"])
+        det.add_metric([self.arch], s["detections"])
+        yield det
+        bounds = [v / 1e3 for v in s["latency_buckets_ms"]]
+        cum, buckets = 0, []
+        for i, n in enumerate(s["latency_hist"]):
+            cum += n
+            buckets.append((str(bounds[i]) if i < len(bounds) else "+Inf", cum))
+        lat = HistogramMetricFamily("arena_request_latency_seconds", "Request latency by stage",
+                                    labels=["arch", "stage"])
+        lat.add_metric([self.arch, "total"], buckets, s["sum_total_ms"] / 1e3)
+        yield lat
+        q = GaugeMetricFamily("arena_queue_depth", "Requests waiting in the dynamic batcher", labels=["arch", "gpu"])
+        q.add_metric([self.arch, self.gpu], b["queue_depth"])
+        yield q
+        hist = b.get("batch_hist", [])
+        cum, bb, total = 0, [], 0.0
+        for size in (1, 2, 4, 8, 16, 24, 32, 48, 64):
+            cum = sum(hist[:size + 1])
+            bb.append((str(size), cum))
+        total = float(sum(i * n for i, n in enumerate(hist)))
+        bb.append(("+Inf", sum(hist)))
+        bs = HistogramMetricFamily("arena_batch_size", "Executed batch sizes", labels=["arch"])
+        bs.add_metric([self.arch], bb, total)
+        yield bs
+        oc = GaugeMetricFamily("arena_open_connections", "Open HTTP connections", labels=["arch"])
+        oc.add_metric([self.arch], s["open_connections"])
+        yield oc
+
+
+class NativeFrontEnd:
+    """The native HTTP server over a DynamicBatcher plus its decode processes."""
+
+    def __init__(self, batcher, labels: list[str], *, port: int = 8100, host: str = "0.0.0.0",
+                 io_threads: int = 4, decode_procs: int = 8, slots: int = 512, softmax: bool = False,
+                 arch: str = "monolithic", gpu: str = "0", replica_tag: str = ""):
+        from ..ops import native
+
+        self.batcher = batcher
+        self.pool = ProcessDecodePool(workers=decode_procs, slots=slots, native=True)
+        self.fe = native().HttpFrontEnd(batcher, self.pool.native_channel(), list(labels),
+                                        {"host": host, "port": int(port), "io_threads": int(io_threads),
+                                         "softmax_confidence": bool(softmax), "replica_tag": str(replica_tag)})
+        self.registry = CollectorRegistry()
+        self.registry.register(_Collector(self, arch, gpu))
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._refresh, name="native-front-metrics", daemon=True)
+        self._thread.start()
+
+    @property
+    def port(self) -> int:
+        return self.fe.port
+
+    def stats(self) -> dict:
+        return self.fe.stats()
+
+    def set_healthy(self, ok: bool) -> None:
+        self.fe.set_healthy(bool(ok))
+
+    def _refresh(self) -> None:
+        while not self._stop.is_set():
+            try:
+                self.fe.set_metrics_text(generate_latest(self.registry).decode())
+            except Exception as e:  # noqa: BLE001 - metrics must never stop the server
+                log.warning(f"metrics refresh failed: {e}")
+            self._stop.wait(1.0)
+
+    def close(self) -> None:
+        self._stop.set()
+        self.fe.stop()
+        self.pool.close()
+
+
+def serve(settings: Settings | None = None, *, weights=None, replica_tag: str = "", devices=None) -> int:
+    """Monolithic arm, native front end: engines on ``devices`` (default ARENA_GPUS / ARENA_GPU) behind one
+    batcher; ``weights``: a folded weight blob (the replica launcher's broadcast).  Returns 3 after a device
+    fault (the replica supervisor restarts the process), 0 on SIGTERM / SIGINT."""
+    from ..engine.registry import build_session
+    from ..models.zoo import resolve_models
+    from ..ops import native
+    from .backends import settings_devices
+
+    settings = settings or Settings.from_env()
+    setup_logging(settings.LOG_LEVEL)
+    devices = list(devices) if devices is not None else settings_devices(settings)
+    instances = max(1, int(settings.ARENA_INSTANCES))
+    max_batch = int(settings.ARENA_MAX_BATCH)
+    yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
+    buckets = sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
+    pipes = [build_session("pipeline", yolo, mnet, device=d, buckets=buckets, weights=weights) for d in devices
+             for _ in range(instances)]
+    batcher = native().DynamicBatcher([p.ex for p in pipes], {
+        "max_batch": max_batch, "max_queue_delay_us": int(settings.ARENA_QUEUE_DELAY_US),
+        "max_queue_size": int(os.environ.get("ARENA_MAX_QUEUE", "4096"))})
+    front = NativeFrontEnd(batcher, load_labels(settings.LABELS_FILE or None), port=int(settings.PORT),
+                           io_threads=int(os.environ.get("ARENA_HTTP_THREADS", "4")),
+                           decode_procs=int(os.environ.get("ARENA_DECODE_PROCS", "0") or 8),
+                           softmax=(settings.ARENA_CONFIDENCE or "logit") == "softmax",
+                           gpu=",".join(str(d) for d in devices), replica_tag=replica_tag)
+    log.info("native monolithic front end ready", extra={"port": front.port, "gpus": devices})
+    done = threading.Event()
+    if threading.current_thread() is threading.main_thread():
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            signal.signal(sig, lambda *_: done.set())
+    rc = 0
+    while not done.wait(0.5):
+        if batcher.stats()["failed"] > 0:  # a failed batch = a device fault: leave rotation, let the launcher restart
+            log.error("device fault: batches failed; exiting for a restart")
+            front.set_healthy(False)
+            time.sleep(1.0)
+            rc = 3
+            break
+    front.close()
+    batcher.shutdown()
+    return rc
+
+
+if __name__ == "__main__":
+    raise SystemExit(serve())

@@ -109,6 +109,28 @@ def build_app(arch: str, settings, info):
     raise ValueError(f"unknown arch '{arch}'")
 
 
+def _serve_native(settings, info, port: int) -> int:
+    """``ARENA_NATIVE_HTTP=1``: the monolithic replica behind the native C++ front end
+    (server/native_front.py) with rank 0's broadcast weights; exits 3 after a device fault."""
+    import numpy as np
+
+    from ..engine.pipeline import resolve_dtype
+    from ..engine.plans import plan_pipeline
+    from ..models.zoo import resolve_models
+    from ..parallel import dist as D
+    from .native_front import serve
+
+    yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
+    blob = plan_pipeline(yolo, mnet, conf_thr=0.0, iou_thr=0.0,  # weights only: thresholds unused
+                         dtype=resolve_dtype()).weights if info.is_main else None
+    blob = D.broadcast_blob(blob, info)
+    D.barrier(info)
+    D.shutdown(info)
+    settings.PORT = port
+    return serve(settings, weights=np.ascontiguousarray(blob), replica_tag=str(info.rank),
+                 devices=[int(settings.ARENA_GPU)])
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--arch", default="monolithic", choices=["monolithic", "detection", "gateway"])
@@ -136,6 +158,8 @@ def main(argv=None) -> int:
             import torch
 
             torch.cuda.set_device(settings.ARENA_GPU)
+    if a.arch == "monolithic" and settings.ARENA_DEVICE != "cpu" and os.environ.get("ARENA_NATIVE_HTTP") == "1":
+        return _serve_native(settings, info, a.port + a.port_stride * info.rank)
     app = build_app(a.arch, settings, info)
     D.barrier(info)
     D.shutdown(info)  # the group is only needed for start-up

@@ -1,0 +1,148 @@
+"""Native HTTP front end (csrc/runtime/http_front.h) end to end on CPU: real sockets, the spawned PIL
+decode processes (native-mode decode pool) and the native dynamic batcher over the host-only
+EchoInstance.  Pins the /predict wire contract of server/monolithic.py (reference
+architectures/monolithic/app/main.py): JSON schema, label names, error codes, keep-alive, chunked
+bodies and concurrent clients."""
+from __future__ import annotations
+
+import http.client
+import io
+import json
+import threading
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from inference_arena_amd.labels import load_labels
+from inference_arena_amd.ops import native
+from inference_arena_amd.server.native_front import NativeFrontEnd
+
+
+def _jpeg(h, w, first):
+    arr = np.full((h, w, 3), 128, np.uint8)
+    arr[:8, :8] = first  # the decoded first pixel picks the echo instance's detection count
+    b = io.BytesIO()
+    Image.fromarray(arr).save(b, format="PNG")  # lossless: the first byte survives the round trip
+    return b.getvalue()
+
+
+def _multipart(data: bytes, field="file"):
+    bnd = "arenaboundary123"
+    body = (f"--{bnd}\r\nContent-Disposition: form-data; name=\"{field}\"; filename=\"x.png\"\r\n"
+            f"Content-Type: image/png\r\n\r\n").encode() + data + f"\r\n--{bnd}--\r\n".encode()
+    return body, f"multipart/form-data; boundary={bnd}"
+
+
+@pytest.fixture(scope="module")
+def server():
+    C = native()
+    batcher = C.DynamicBatcher([C.EchoInstance(2, 8, 4)], {"max_batch": 8, "max_queue_delay_us": 200})
+    labels = load_labels(None)
+    fe = NativeFrontEnd(batcher, labels, port=0, host="127.0.0.1", io_threads=2, decode_procs=2, slots=16)
+    yield fe, labels
+    fe.close()
+    batcher.shutdown()
+
+
+def _post(port, body, ctype, conn=None, headers=None):
+    c = conn or http.client.HTTPConnection("127.0.0.1", port, timeout=30)
+    c.request("POST", "/predict", body=body, headers={"Content-Type": ctype, **(headers or {})})
+    r = c.getresponse()
+    data = r.read()
+    return r.status, data, c
+
+
+def test_predict_schema_and_labels(server):
+    fe, labels = server
+    body, ct = _multipart(_jpeg(48, 64, 2))
+    st, data, c = _post(fe.port, body, ct)
+    assert st == 200
+    d = json.loads(data)
+    assert set(d) == {"request_id", "detections", "timing"} and len(d["request_id"]) == 36
+    assert len(d["detections"]) == 3  # 1 + first_byte % max_det
+    for k, det in enumerate(d["detections"]):
+        box = det["detection"]
+        assert (box["x1"], box["y1"], box["x2"], box["y2"]) == (k, k, 64 - k, 48 - k)
+        assert box["class_id"] == k and abs(box["confidence"] - (0.9 - 0.1 * k)) < 1e-6
+        cls = det["classification"]
+        assert cls["class_id"] == 10 * k and cls["class_name"] == labels[10 * k] and cls["confidence"] == 5.0
+    for key in ("queue_ms", "gpu_ms", "batch_size", "detection_ms", "classification_ms", "inference_ms",
+                "decode_ms", "total_ms"):
+        assert key in d["timing"]
+    # keep-alive: a second request on the same connection
+    st2, data2, _ = _post(fe.port, body, ct, conn=c)
+    assert st2 == 200 and json.loads(data2)["request_id"] != d["request_id"]
+    c.close()
+
+
+def test_raw_body_chunked_and_errors(server):
+    fe, _ = server
+    img = _jpeg(32, 32, 0)
+    st, data, c = _post(fe.port, img, "image/png")
+    assert st == 200 and len(json.loads(data)["detections"]) == 1
+    c.close()
+    # chunked transfer encoding
+    c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=30)
+    c.request("POST", "/predict", body=iter([img[:100], img[100:]]), headers={"Content-Type": "image/png"},
+              encode_chunked=True)
+    r = c.getresponse()
+    assert r.status == 200 and len(json.loads(r.read())["detections"]) == 1
+    c.close()
+    body, ct = _multipart(img, field="other")
+    st, data, c = _post(fe.port, body, ct)
+    assert st == 422 and "file" in json.loads(data)["detail"]
+    c.close()
+    st, data, c = _post(fe.port, b"not an image", "image/jpeg")
+    assert st == 500 and "Failed to decode image" in json.loads(data)["detail"]
+    c.close()
+    st, data, c = _post(fe.port, b"", "image/jpeg")
+    assert st == 422
+    c.close()
+    c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=30)
+    c.request("GET", "/nope")
+    assert c.getresponse().status == 404
+    c.close()
+
+
+def test_health_metrics_and_concurrency(server):
+    fe, _ = server
+    c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=30)
+    c.request("GET", "/health")
+    r = c.getresponse()
+    assert r.status == 200 and json.loads(r.read()) == {"status": "healthy", "models_loaded": True}
+    errors, n_ok = [], []
+
+    def worker(i):
+        try:
+            conn = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=30)
+            for j in range(6):
+                body, ct = _multipart(_jpeg(24 + i, 40, (i + j) % 4))
+                st, data, conn = _post(fe.port, body, ct, conn=conn)
+                assert st == 200, data
+                assert len(json.loads(data)["detections"]) == 1 + (i + j) % 4
+                n_ok.append(1)
+            conn.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors and len(n_ok) == 48
+    s = fe.stats()
+    assert s["ok"] >= 48 and s["errors"] >= 1
+    import time
+
+    time.sleep(1.2)  # the metrics text refreshes once a second
+    c.request("GET", "/metrics")
+    r = c.getresponse()
+    text = r.read().decode()
+    assert r.status == 200 and 'arena_requests_total{arch="monolithic",status="ok"}' in text
+    fe.set_healthy(False)
+    c.request("GET", "/health")
+    r = c.getresponse()
+    assert r.status == 503 and json.loads(r.read())["status"] == "unhealthy"
+    fe.set_healthy(True)
+    c.close()

@@ -48,6 +48,7 @@ SOURCES = [
     "kernels/fc_splitk.hip",
     "runtime/executor.cpp",
     "runtime/batcher.cpp",
+    "runtime/http_front.cpp",
     "runtime/trace.cpp",
     "bindings.cpp",
 ]
