@@ -57,6 +57,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cpus() -> int:
+    """CPUs this job may use: the affinity mask, capped by a cgroup-v2 CPU quota (cpu.max) when one is set —
+    on the GPU pool the mask shows the whole machine while the quota is the job's share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def self_launch(argv: list[str], n: int) -> int:
     """Re-run this script under torch.distributed.run with N ranks (child process, no exec)."""
     import socket
@@ -269,7 +282,7 @@ def main(argv=None) -> int:
     # decode workers are spawned before this process touches the GPU
     from inference_arena_amd.server.decode_pool import ProcessDecodePool
 
-    ncpu = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
+    ncpu = host_cpus()
     workers = a.decode_workers or max(2, min(15, ncpu // max(1, world) - 1))
     pool = ProcessDecodePool(workers=workers, slots=max(256, a.users + 64))
 
@@ -280,15 +293,18 @@ def main(argv=None) -> int:
     from inference_arena_amd.models.zoo import default_models
     from inference_arena_amd.parallel import dist as D
 
-    info = D.init_from_env()
+    info = D.init_from_env(os.environ.get("ARENA_DIST_BACKEND") or None)
     assert info.world == a.gpus, (info.world, a.gpus)
-    torch.cuda.set_device(info.local_rank)
+    # ARENA_SHARED_GPU=1 (+ ARENA_DIST_BACKEND=gloo): rehearse the N-rank path on a 1-GPU box, every rank on
+    # device 0 (the driver's 8-GPU run uses one GPU per rank over RCCL)
+    dev = 0 if os.environ.get("ARENA_SHARED_GPU") == "1" else info.local_rank
+    torch.cuda.set_device(dev)
     torch.set_num_threads(2)
     try:
         t0 = time.time()
         yolo, mnet = default_models(a.seed)
         buckets = sorted({1, a.batch})
-        pipe = GpuPipeline(yolo, mnet, device=info.local_rank, buckets=buckets, crop_cap_per_image=a.crop_cap,
+        pipe = GpuPipeline(yolo, mnet, device=dev, buckets=buckets, crop_cap_per_image=a.crop_cap,
                            dtype=a.dtype)
         if info.world > 1:
             # rank 0's folded weights, broadcast with RCCL over xGMI straight into each replica's GPU memory
@@ -313,7 +329,7 @@ def main(argv=None) -> int:
         bs1 = bs1_latency(pipe, pool, jpegs, a.bs1_requests, a) if (info.is_main and a.bs1_requests > 0) else []
         sec = {}
         if a.secondary_bf16 and a.dtype != "bf16":
-            alt = GpuPipeline(yolo, mnet, device=info.local_rank, buckets=buckets, crop_cap_per_image=a.crop_cap,
+            alt = GpuPipeline(yolo, mnet, device=dev, buckets=buckets, crop_cap_per_image=a.crop_cap,
                               dtype="bf16")
             w2, lat2, _, _, _ = measure(alt, pool, jpegs, a, info, D, torch)
             w2 = D.allreduce_max(w2, info)
