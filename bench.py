@@ -217,7 +217,13 @@ def measure(pipe, pool, jpegs, a, info, D, torch):
     loop = ClosedLoop(pool, batcher, jpegs, a.users, offset=(info.rank * 37) % len(jpegs))
     loop.start()
     try:
-        loop.wait_for(a.warmup * B)
+        # W warm-up steps at least; the closed loop also has to leave its start-up transient (all users
+        # arrive at once, first graph replays) before the window opens: >= 4 requests per user and
+        # --min-warmup-s seconds, so the window's value does not depend on --steps / --warmup
+        tw = time.perf_counter()
+        loop.wait_for(max(a.warmup * B, 4 * a.users))
+        while time.perf_counter() - tw < a.min_warmup_s:
+            time.sleep(0.05)
         D.barrier(info)
         torch.cuda.synchronize()
         with loop.lock:
@@ -256,6 +262,7 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100, help="timed steps (a step = --batch completed requests)")
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--min-warmup-s", type=float, default=2.0, help="minimum warm-up time of the closed loop")
     ap.add_argument("--batch", type=int, default=32, help="requests per step = dynamic batcher max_batch")
     ap.add_argument("--users", type=int, default=192, help="closed-loop clients per GPU")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
