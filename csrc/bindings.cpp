@@ -132,6 +132,7 @@ void py_ir_block(const py::dict& d) {
   p.Wo = req<int>(d, "Wo");
   p.B = req<int>(d, "B");
   p.bdev = ptr<const int*>(d, "bdev");
+  p.x3w = get<int>(d, "x3w", 0);
   prepare_kernels();
   if (get<int>(d, "f32", 0))
     ir_block_f32(p, stream_of(d));

@@ -307,6 +307,7 @@ bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, i
 }
 
 void ir_block_f32(const IrParams& p, hipStream_t s) {
+  if (ir_block_crop_f32(p, s)) return;  // 14x14 / 7x7 maps: whole-map x3 kernel (ir_crop_f32.hip)
   if (!ir_block_f32_supported(p.stride, p.inp_pad, p.hid_pad, p.oup_pad, p.expand) || p.inp % 4 || p.oup % 4 ||
       p.inp > p.inp_pad || p.oup > p.oup_pad || p.x_cs % 4 || p.y_cs % 4)
     throw std::runtime_error("ir_block_f32: unsupported channel geometry");

@@ -102,12 +102,17 @@ struct IrParams {
   int y_cs, Ho, Wo;
   int B;
   const int* bdev;
+  int x3w;                  // fp32: we / wp pre-split into bf16 [h|m|l] planes for ir_crop_f32.hip
 };
 void ir_block(const IrParams& p, hipStream_t s);
 // Exact-fp32 fused block (csrc/kernels/ir_f32.hip): fp32 views / weights; we [hid_pad][inp_pad],
 // wd [9][hid_pad], wp [oup_pad][hid_pad] fp32; inp_pad % 16, hid_pad % 32, oup_pad in {16, 32, 64, 96}.
 void ir_block_f32(const IrParams& p, hipStream_t s);
 bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
+// Whole-map fp32-accurate block for the 14x14 / 7x7 stages (csrc/kernels/ir_crop_f32.hip, triple-bf16-split
+// MFMA); ir_block_f32 dispatches blocks with split-plane weights (x3w, set by the planner) to it.
+bool ir_block_crop_f32(const IrParams& p, hipStream_t s);
+bool ir_block_crop_f32_supported(int H, int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
 void ir_prepare();
 void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole-crop tile
 void set_ir_crop(bool v);

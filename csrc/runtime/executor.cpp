@@ -501,6 +501,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.Wo = (int)r[24];
         p.B = batch(r[25]);
         p.bdev = bdev(r[25]);
+        p.x3w = (int)r[26];
         if (f32)
           ir_block_f32(p, s);
         else

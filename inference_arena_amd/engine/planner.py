@@ -60,6 +60,8 @@ their conv weights are fp32 [Cout_pad][Kpad] with Kpad a multiple of 16.
 """
 from __future__ import annotations
 
+import os
+
 import struct
 from dataclasses import dataclass, field
 
@@ -151,6 +153,22 @@ def bf16_bytes(t: torch.Tensor) -> bytes:
     return t.detach().float().contiguous().to(torch.bfloat16).view(torch.int16).numpy().tobytes()
 
 
+def split_bf16x3(t: torch.Tensor) -> torch.Tensor:
+    """fp32 [..., K] -> bf16 [..., 3, K]: planes h = rn(t), m = rn(t - h), l = rn(t - h - m) (round to nearest
+    even, as v_cvt_pk_bf16_f32): h + m + l equals t to fp32 rounding.  The operand format of the
+    triple-bf16-split kernels (csrc/kernels/ir_crop_f32.hip)."""
+    t = t.detach().float()
+    h = t.to(torch.bfloat16)
+    r = t - h.float()
+    m = r.to(torch.bfloat16)
+    lo = (r - m.float()).to(torch.bfloat16)
+    return torch.stack([h, m, lo], dim=-2).contiguous()
+
+
+def bf16_raw_bytes(t: torch.Tensor) -> bytes:
+    return t.contiguous().view(torch.int16).numpy().tobytes()
+
+
 def f32_bytes(t: torch.Tensor) -> bytes:
     return t.detach().float().contiguous().numpy().tobytes()
 
@@ -198,6 +216,20 @@ def pack_ir_weights(expand, dw, project, inp: int, k_align: int = 32) -> dict:
     bpp[:oup] = bp
     return {"we": we, "be": be, "wd": wdp, "bd": bdp, "wp": wpp, "bp": bpp, "inp": inp, "inp_pad": inp_pad,
             "hid_pad": hid_pad, "oup": oup, "oup_pad": oup_pad}
+
+
+def ir_crop_f32_enabled() -> bool:
+    """``ARENA_IRC_F32=1`` (default 0): fp32 programs run MobileNetV2's 14x14 / 7x7 blocks as the fused
+    whole-map kernel (csrc/kernels/ir_crop_f32.hip).  Off by default: on MI355X it measured slower than the
+    unfused batched 1x1 GEMMs + depthwise (1.21 ms vs 1.07 ms per batch of 32 requests;
+    profiles/r2_irc_f32_experiment.md)."""
+    return os.environ.get("ARENA_IRC_F32", "0").lower() in ("1", "true", "yes", "on")
+
+
+def ir_crop_f32_planned(H: int, stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
+    from .validate import ir_crop_f32_supported
+
+    return ir_crop_f32_enabled() and ir_crop_f32_supported(H, stride, inp_pad, hid_pad, oup_pad, expand)
 
 
 class ProgramBuilder:
@@ -321,13 +353,17 @@ class ProgramBuilder:
         inp, inp_pad, hid_pad, oup, oup_pad = pk["inp"], pk["inp_pad"], pk["hid_pad"], pk["oup"], pk["oup_pad"]
         f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
         mat = f32 if self.f32 else bf16_bytes  # exact-fp32 programs keep fp32 weights
-        offs = [self.weights.add(mat(pk["we"])), self.weights.add(f32(pk["be"])),
-                self.weights.add(mat(pk["wd"])), self.weights.add(f32(pk["bd"])),
-                self.weights.add(mat(pk["wp"])), self.weights.add(f32(pk["bp"]))]
         H, W = src.buf.H, src.buf.W
+        # fp32 14x14 / 7x7 blocks: whole-map kernel with pre-split [h|m|l] bf16 expand / project weights
+        x3w = int(self.f32 and H == W and ir_crop_f32_planned(H, stride, inp_pad, hid_pad, oup_pad,
+                                                              int(expand is not None)))
+        mat_x3 = (lambda t: bf16_raw_bytes(split_bf16x3(t))) if x3w else mat  # noqa: E731
+        offs = [self.weights.add(mat_x3(pk["we"])), self.weights.add(f32(pk["be"])),
+                self.weights.add(mat(pk["wd"])), self.weights.add(f32(pk["bd"])),
+                self.weights.add(mat_x3(pk["wp"])), self.weights.add(f32(pk["bp"]))]
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
         rec = [OP_IRBLOCK, src.bid, src.coff, src.cs, H, W, inp, inp_pad, hid_pad, oup, oup_pad, stride,
-               int(expand is not None), int(res), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind]
+               int(expand is not None), int(res), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind, x3w]
         self._emit(rec, src, dst)
 
     def sppf(self, buf: Buffer, C: int, kind: int = IMAGES) -> None:

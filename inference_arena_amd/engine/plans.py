@@ -235,15 +235,20 @@ def ir_crop_default() -> bool:
 
 
 def fuse_block_f32(blk, H: int) -> bool:
-    """fp32 policy (csrc/kernels/ir_f32.hip): fuse the memory-bound blocks at >= 28x28 input, where the
-    unfused fp32 expanded map (up to 4.8 MB per crop) round-trips HBM; below that the batched 1x1 GEMMs
-    are compute-bound and stay unfused."""
+    """fp32 policy: fuse the memory-bound blocks at >= 28x28 input (csrc/kernels/ir_f32.hip), where the
+    unfused fp32 expanded map (up to 4.8 MB per crop) round-trips HBM, and the 14x14 / 7x7 blocks the
+    whole-map triple-bf16-split kernel covers when enabled (csrc/kernels/ir_crop_f32.hip, ``ARENA_IRC_F32``); the
+    rest run as batched 1x1 GEMMs + depthwise."""
+    from .planner import ir_crop_f32_planned
     from .validate import ir_f32_supported
 
     inp_pad = (blk.inp + 15) // 16 * 16
     hid_pad = inp_pad if blk.expand is None else (blk.hidden + 31) // 32 * 32
     oup_pad = (blk.oup + 15) // 16 * 16
-    return H >= 28 and ir_f32_supported(blk.stride, inp_pad, hid_pad, oup_pad, int(blk.expand is not None))
+    expand = int(blk.expand is not None)
+    if H >= 28:
+        return ir_f32_supported(blk.stride, inp_pad, hid_pad, oup_pad, expand)
+    return ir_crop_f32_planned(H, blk.stride, inp_pad, hid_pad, oup_pad, expand)
 
 
 def fuse_block(blk, H: int, policy) -> bool:

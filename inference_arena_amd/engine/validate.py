@@ -63,6 +63,18 @@ def ir_f32_supported(stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expa
             and ir_f32_lds_bytes(stride, inp_pad, bool(expand)) <= 64 * 1024)
 
 
+# (output side, stride, inp_pad, oup_pad) of csrc/kernels/ir_crop_f32.hip ARENA_IRC_F32_CONFIGS
+# (oup_pad may be 1 or 2 output-channel groups of the configuration's width: 160 -> 320 runs as 2 x 160)
+IR_CROP_F32_CONFIGS = {(14, 1, 64, 64), (14, 1, 64, 96), (14, 1, 96, 96), (7, 2, 96, 160), (7, 1, 160, 160)}
+
+
+def ir_crop_f32_supported(H: int, stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
+    """Mirror of arena::ir_block_crop_f32_supported (whole-map x3 kernel for the 14x14 / 7x7 stages)."""
+    Ho = (H - 1) // stride + 1
+    return (bool(expand) and hid_pad % 32 == 0 and H == Ho * stride
+            and any((Ho, stride, inp_pad) == c[:3] and oup_pad in (c[3], 2 * c[3]) for c in IR_CROP_F32_CONFIGS))
+
+
 def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand_cap: int,
                      raw_out_bytes: int | None = None) -> None:
     sizes = {}
@@ -147,7 +159,10 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             if inp_pad % (16 if f32 else 32) or hid_pad % 32 or oup_pad % 16 or inp > inp_pad or oup > oup_pad \
                     or inp % (4 if f32 else 8):
                 raise ProgramError(f"op {i}: bad ir_block channel geometry")
-            if f32 and not ir_f32_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])):
+            x3w = int(r[26])
+            if x3w and not (f32 and H == W and ir_crop_f32_supported(H, S, inp_pad, hid_pad, oup_pad, int(r[12]))):
+                raise ProgramError(f"op {i}: split-plane weights for a block the whole-map kernel does not take")
+            if f32 and not x3w and not ir_f32_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])):
                 raise ProgramError(f"op {i}: no fp32 fused kernel for this block")
             if Ho != (H - 1) // S + 1 or Wo != (W - 1) // S + 1:
                 raise ProgramError(f"op {i}: ir_block output size mismatch")
@@ -155,11 +170,12 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 raise ProgramError(f"op {i}: ir_block residual needs stride 1 and inp == oup")
             view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, el, "ir input")
             view(i, r[20], int(r[21]), int(r[22]), n * Ho * Wo, oup, el, "ir output")
-            weights(i, int(r[14]), hid_pad * inp_pad * el, "ir expand weight")
+            wel = 6 if x3w else el  # three bf16 planes per weight
+            weights(i, int(r[14]), hid_pad * inp_pad * wel, "ir expand weight")
             weights(i, int(r[15]), hid_pad * 4, "ir expand bias")
             weights(i, int(r[16]), 9 * hid_pad * el, "ir dw weight")
             weights(i, int(r[17]), hid_pad * 4, "ir dw bias")
-            weights(i, int(r[18]), oup_pad * hid_pad * el, "ir project weight")
+            weights(i, int(r[18]), oup_pad * hid_pad * wel, "ir project weight")
             weights(i, int(r[19]), oup_pad * 4, "ir project bias")
         elif op == OP_SPPF:
             n = kind_n(r[7])

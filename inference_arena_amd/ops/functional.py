@@ -96,21 +96,26 @@ def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: boo
                   bdev: torch.Tensor | None = None) -> torch.Tensor:
     """Fused MobileNetV2 inverted residual (expand 1x1+ReLU6 -> dw3x3+ReLU6 -> project 1x1 [+x]).
     ``expand``/``dw``/``project`` are (weight, bias) pairs with BN folded; ``expand`` None for t=1."""
-    from ..engine.planner import pack_ir_weights
+    from ..engine.planner import ir_crop_f32_planned, pack_ir_weights, split_bf16x3
 
     B, H, W, C = x.shape
-    f32 = x.dtype == torch.float32  # exact-fp32 kernel (csrc/kernels/ir_f32.hip)
+    f32 = x.dtype == torch.float32  # exact-fp32 kernels (csrc/kernels/ir_f32.hip, ir_crop_f32.hip)
     pk = pack_ir_weights(expand, dw, project, C, k_align=16 if f32 else 32)
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     y = torch.empty(B, Ho, Wo, pk["oup"], dtype=x.dtype, device=x.device)
     mat = torch.float32 if f32 else torch.bfloat16
+    x3w = int(f32 and H == W and ir_crop_f32_planned(H, stride, pk["inp_pad"], pk["hid_pad"], pk["oup_pad"],
+                                                     int(expand is not None)))
     dev = {k: (pk[k].to(mat) if k in ("we", "wd", "wp") else pk[k].float()).contiguous().to(x.device)
            for k in ("we", "be", "wd", "bd", "wp", "bp")}
+    if x3w:  # the whole-map kernel reads pre-split [h|m|l] bf16 expand / project weights
+        dev["we"] = split_bf16x3(pk["we"]).to(x.device)
+        dev["wp"] = split_bf16x3(pk["wp"]).to(x.device)
     native().ir_block({"x": _ptr(x), "x_cs": C, "H": H, "W": W, "inp": C, "inp_pad": pk["inp_pad"],
                        "hid_pad": pk["hid_pad"], "oup": pk["oup"], "oup_pad": pk["oup_pad"], "stride": stride,
                        "expand": int(expand is not None), "res": int(res),
                        **{k: _ptr(v) for k, v in dev.items()}, "y": _ptr(y), "y_cs": pk["oup"], "Ho": Ho,
-                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32)})
+                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32), "x3w": x3w})
     torch.cuda.synchronize(x.device)  # keep the packed weights alive until the kernel ran
     return y
 

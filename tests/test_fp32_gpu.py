@@ -301,8 +301,17 @@ def _ir_ref64(x, expand, dw, project, stride, res):
     (24, 144, 32, 2, 28, False),   # block 4
     (32, 192, 32, 1, 28, True),    # block 5/6
     (32, 192, 64, 2, 28, False),   # block 7 (4 output tiles of 16)
+    # whole-map x3 kernel (csrc/kernels/ir_crop_f32.hip)
+    (64, 384, 64, 1, 14, True),    # blocks 8-10
+    (64, 384, 96, 1, 14, False),   # block 11
+    (96, 576, 96, 1, 14, True),    # blocks 12-13
+    (96, 576, 160, 2, 14, False),  # block 14 (14 -> 7)
+    (160, 960, 160, 1, 7, True),   # blocks 15-16
+    (160, 960, 320, 1, 7, False),  # block 17
 ])
-def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res):
+def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, monkeypatch):
+    if H <= 14:  # the whole-map kernel is opt-in for programs; the wrapper takes it when enabled
+        monkeypatch.setenv("ARENA_IRC_F32", "1")
     g = torch.Generator().manual_seed(inp * 7 + hid + stride)
     x = torch.randn(3, inp, H, H, generator=g)
     expand = None if hid == inp else (torch.randn(hid, inp, 1, 1, generator=g) / inp ** 0.5,
@@ -322,5 +331,6 @@ def test_fp32_program_fuses_the_high_resolution_blocks():
 
     p = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="fp32")
     fused = [(int(o[4]), int(o[11])) for o in p.ops if int(o[0]) == 14]
+    # >= 28x28: ir_f32.hip tile kernel; 14x14 and 7x7 run unfused (ir_crop_f32.hip is opt-in)
     assert [h for h, _ in fused] == [112, 112, 56, 56, 28, 28, 28]
     assert all(int(o[47]) == 1 for o in p.ops)

@@ -232,3 +232,34 @@ def test_tuning_table_roundtrip(tmp_path, monkeypatch):
     monkeypatch.setenv("ARENA_TUNING", "bogus")
     assert tuning.mode() == "table"
     assert np.asarray(tuning.load_table()[f"{tuning.fingerprint(p.ops)}:8"]).shape == (len(p.ops),)
+
+
+def test_split_bf16x3_is_exact_to_fp32_rounding():
+    """Triple-bf16 split of the x3 kernels' weights: h + m + l reproduces fp32 values to fp32 rounding."""
+    from inference_arena_amd.engine.planner import split_bf16x3
+
+    g = torch.Generator().manual_seed(3)
+    t = torch.randn(64, 96, generator=g) * torch.logspace(-4, 3, 96)
+    p = split_bf16x3(t)
+    assert p.shape == (64, 3, 96) and p.dtype == torch.bfloat16
+    back = p[:, 0].double() + p[:, 1].double() + p[:, 2].double()
+    rel = ((back - t.double()).abs() / t.double().abs().clamp_min(1e-30)).max().item()
+    assert rel <= 2.0 ** -24, rel
+
+
+def test_fp32_program_with_whole_map_ir_blocks_validates(monkeypatch):
+    """ARENA_IRC_F32=1: the fp32 MobileNetV2 14x14 / 7x7 blocks become fused ops with split-plane weights
+    (x3w field), sized 6 bytes per weight by the static validator."""
+    from inference_arena_amd.engine import plans
+    from inference_arena_amd.engine.planner import OP_IRBLOCK
+    from inference_arena_amd.engine.validate import validate_program
+    from inference_arena_amd.models.zoo import default_models
+
+    monkeypatch.setenv("ARENA_IRC_F32", "1")
+    y, m = default_models(0)
+    prog = plans.plan_pipeline(y, m, conf_thr=0.5, iou_thr=0.45, dtype="fp32")
+    ir = [o for o in prog.ops if int(o[0]) == OP_IRBLOCK]
+    assert [int(o[4]) for o in ir] == [112, 112, 56, 56, 28, 28, 28] + [14] * 7 + [7] * 3
+    assert [int(o[26]) for o in ir] == [0] * 7 + [1] * 10
+    for B in (1, 32):
+        validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)

@@ -32,6 +32,7 @@ SOURCES = [
     "kernels/conv_mfma.hip",
     "kernels/conv_f32.hip",
     "kernels/ir_f32.hip",
+    "kernels/ir_crop_f32.hip",
     "kernels/dwconv.hip",
     "kernels/ir_block.hip",
     "kernels/ir_block_wave.hip",
