@@ -290,7 +290,10 @@ def main(argv=None) -> int:
     from inference_arena_amd.server.decode_pool import ProcessDecodePool
 
     ncpu = host_cpus()
-    workers = a.decode_workers or max(2, min(15, ncpu // max(1, world) - 1))
+    # 10 decode processes (~8.5k decodes/s) keep a GPU's engine (~7k req/s fp32) fed; more of them compete with
+    # the batcher / packing threads for the box's CPU share and lowered the e2e rate (16-CPU box: 15 workers
+    # 6.0-6.4k req/s, 8-10 workers 6.78k; profiles/r2_decode_workers_sweep.md)
+    workers = a.decode_workers or max(2, min(10, ncpu // max(1, world) - 1))
     pool = ProcessDecodePool(workers=workers, slots=max(256, a.users + 64))
 
     import torch
