@@ -959,10 +959,20 @@ static void launch_x3_halo(const ConvParams& p, hipStream_t s) {
   hipLaunchKernelGGL((conv_x3_halo_kernel<NF>), grid, dim3(256), 0, s, p);
 }
 
-// impl kF32X3Halo: 3x3 stride-1 convs with Kpad == 9 * Cin (tap-major K) and Cin % 4 == 0
-static bool x3_halo(const ConvParams& p, hipStream_t s) {
+// impl kF32X3Halo: 3x3 stride-1 convs with Kpad == 9 * Cin (tap-major K) and Cin % 4 == 0.  nf > 0 forces the
+// channel tile (impl kF32X3HaloN3 / N2: BN 48 / 32): the 80-channel detect-head convs at NF = 5 need 89 KB of
+// LDS (one workgroup, one wave per SIMD); two 48-channel tiles fit twice per CU at 17 % padded channels.
+static bool x3_halo(const ConvParams& p, hipStream_t s, int nf = 0) {
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.Kpad != 9 * p.Cin || p.Cin % 4 != 0) return false;
   const int ncf = p.Cout_pad / 16;
+  if (nf == 3) {
+    launch_x3_halo<3>(p, s);
+    return true;
+  }
+  if (nf == 2) {
+    launch_x3_halo<2>(p, s);
+    return true;
+  }
   if (ncf == 1) launch_x3_halo<1>(p, s);
   else if (ncf == 2) launch_x3_halo<2>(p, s);
   else if (ncf == 3 || ncf == 9) launch_x3_halo<3>(p, s);
@@ -1005,8 +1015,9 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
   const int ncf = p.Cout_pad / 16;
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
-    if (p.impl == kF32X3Halo) {
-      if (!x3_halo(p, s)) throw std::runtime_error("conv2d_f32: not an x3-halo-eligible conv");
+    if (p.impl == kF32X3Halo || p.impl == kF32X3HaloN3 || p.impl == kF32X3HaloN2) {
+      const int nf = p.impl == kF32X3HaloN3 ? 3 : p.impl == kF32X3HaloN2 ? 2 : 0;
+      if (!x3_halo(p, s, nf)) throw std::runtime_error("conv2d_f32: not an x3-halo-eligible conv");
       return;
     }
     if (p.impl == kF32Halo) {

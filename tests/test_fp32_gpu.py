@@ -77,7 +77,7 @@ def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
         assert torch.equal(out2, up_ref)
 
 
-X3_IMPLS = [40 + v for v in range(12)] + [101]  # triple-bf16-split tile variants + split halo (launch.h)
+X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103]  # x3 tile variants + split halo (auto / 48 / 32 ch tiles)
 
 
 @pytest.mark.parametrize(
