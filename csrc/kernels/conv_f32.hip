@@ -1001,6 +1001,184 @@ static bool halo_f32(const ConvParams& p, hipStream_t s, bool force = false) {
   return false;
 }
 
+// ---------------------------------------------------------------------------
+// Weight-stationary streaming 1x1 conv, fp32-accurate on the bf16 matrix cores (triple-bf16 split).
+// The small-K 1x1 convs (K <= 192: YOLO C3 / neck pointwise layers, MobileNetV2 expand GEMMs) ran 2-10x
+// off their memory floor in the tiled kernels above (profiles/r2_fp32_irprefetch_ops.md: 10-30 % MFMA
+// busy, each workgroup's life one load latency + 2-6 k-chunks + its stores): here a workgroup splits its
+// BN x K weight tile into three bf16 planes in LDS once, then its four waves stream 16-pixel tiles through
+// a grid-stride loop, the next tile's activations loaded into registers while the current tile's
+// 6 x KS x NF MFMAs run.  Lane l takes pixel (l & 15) and k = 8 (l >> 4) .. +7 of each 32-deep slab (two
+// float4 of the NHWC row), splits them in registers, and reads the weight fragment of every channel tile
+// from LDS (row pitch 6K + 32 B = 2 (mod 4) 16-B slots: conflict-free ds_read_b128).
+constexpr int STR_THREADS = 256;
+
+__device__ __forceinline__ f32x4 mfma_x3f(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                          const bf16x8& bm, const bf16x8& bl, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+
+template <int NF, int KS>
+__global__ __launch_bounds__(STR_THREADS) void conv_x3_stream_kernel(const ConvParams p) {
+  constexpr int BN = NF * 16, K = KS * 32, WP = 6 * K + 32;
+  __shared__ __attribute__((aligned(16))) uint8_t sW[BN * WP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int n0 = blockIdx.y * BN;
+  const int M = live_batch(p.B, p.bdev) * p.Ho * p.Wo;
+  const int tiles = (M + 15) / 16;
+  int t = blockIdx.x * 4 + wave;
+  if (blockIdx.x * 4 >= tiles) return;
+
+  // weight tile -> three bf16 planes (zero past Cout_pad / Kpad)
+  const float* __restrict__ w = (const float*)p.w;
+  for (int i = tid; i < BN * K / 4; i += STR_THREADS) {
+    const int row = i / (K / 4), k = 4 * (i - row * (K / 4));
+    const bool ok = n0 + row < p.Cout_pad && k < p.Kpad;
+    float4 v = *(const float4*)(ok ? w + (size_t)(n0 + row) * p.Kpad + k : w);
+    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    bf16x4 h, m, l;
+    bf16 th, tm, tl;
+    split3(v.x, th, tm, tl); h[0] = th; m[0] = tm; l[0] = tl;
+    split3(v.y, th, tm, tl); h[1] = th; m[1] = tm; l[1] = tl;
+    split3(v.z, th, tm, tl); h[2] = th; m[2] = tm; l[2] = tl;
+    split3(v.w, th, tm, tl); h[3] = th; m[3] = tm; l[3] = tl;
+    uint8_t* r = sW + row * WP + k * 2;
+    *(bf16x4*)r = h;
+    *(bf16x4*)(r + 2 * K) = m;
+    *(bf16x4*)(r + 4 * K) = l;
+  }
+  float4 bias[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int cb = n0 + j * 16 + 4 * kq;
+    bias[j] = cb < p.Cout ? *(const float4*)(p.bias + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+
+  const float* __restrict__ x = (const float*)p.x;
+  const int tstride = gridDim.x * 4;
+  float4 b0[KS], b1[KS];
+  auto load_b = [&](int tt) {
+    const int pix = tt * 16 + col;
+#pragma unroll
+    for (int sl = 0; sl < KS; ++sl) {
+      const int k0 = sl * 32 + kq * 8;
+      const bool ok = pix < M && k0 < p.Cin;
+      const float* ptr = x + (size_t)pix * p.xs + k0;
+      b0[sl] = load_f4_or_zero(ptr, x, ok);
+      b1[sl] = load_f4_or_zero(ptr + 4, x, ok);
+    }
+  };
+  if (t < tiles) load_b(t);
+  const int HWo = p.Ho * p.Wo;
+  for (; t < tiles; t += tstride) {
+    float4 c0[KS], c1[KS];
+#pragma unroll
+    for (int sl = 0; sl < KS; ++sl) {
+      c0[sl] = b0[sl];
+      c1[sl] = b1[sl];
+    }
+    if (t + tstride < tiles) load_b(t + tstride);  // next tile's activations in flight during this tile
+    f32x4 acc[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int sl = 0; sl < KS; ++sl) {
+      const float v[8] = {c0[sl].x, c0[sl].y, c0[sl].z, c0[sl].w, c1[sl].x, c1[sl].y, c1[sl].z, c1[sl].w};
+      bf16x8 bh, bm, bl;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        bf16 th, tm, tl;
+        split3(v[i], th, tm, tl);
+        bh[i] = th;
+        bm[i] = tm;
+        bl[i] = tl;
+      }
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const uint8_t* ra = sW + (j * 16 + col) * WP + sl * 64 + kq * 16;
+        acc[j] = mfma_x3f(*(const bf16x8*)ra, *(const bf16x8*)(ra + 2 * K), *(const bf16x8*)(ra + 4 * K), bh, bm,
+                          bl, acc[j]);
+      }
+    }
+    const int pix = t * 16 + col;
+    if (pix >= M) continue;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int cb = n0 + j * 16 + kq * 4;
+      if (cb >= p.Cout) continue;
+      float v[4] = {acc[j][0] + bias[j].x, acc[j][1] + bias[j].y, acc[j][2] + bias[j].z, acc[j][3] + bias[j].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      if (p.res != nullptr) {
+        const float4 rv = *(const float4*)((const float*)p.res + (size_t)pix * p.rs + cb);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      }
+      const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)p.y + (size_t)pix * p.ys + cb) = o;
+      if (p.y2 != nullptr) {
+        const int b = pix / HWo;
+        const int r = pix - b * HWo;
+        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+        const int W2 = 2 * p.Wo;
+        float* y2 = (float*)p.y2;
+        const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+        *(float4*)(y2 + base * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + 1) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2 + 1) * p.y2s + cb) = o;
+      }
+    }
+  }
+}
+
+template <int NF, int KS>
+static void launch_stream(const ConvParams& p, hipStream_t s) {
+  constexpr int BN = NF * 16;
+  const int ny = (p.Cout_pad + BN - 1) / BN;
+  const long tiles = ((long)p.B * p.Ho * p.Wo + 15) / 16;
+  // ~1024 resident workgroups over the chip (4 per CU), each streaming tiles of 16 pixels per wave
+  const long gx = std::max(1L, std::min((tiles + 3) / 4, (long)std::max(1, 1024 / ny)));
+  hipLaunchKernelGGL((conv_x3_stream_kernel<NF, KS>), dim3((unsigned)gx, (unsigned)ny), dim3(STR_THREADS), 0, s, p);
+}
+
+template <int NF>
+static bool launch_stream_k(const ConvParams& p, hipStream_t s) {
+  switch ((p.Kpad + 31) / 32) {
+    case 1: launch_stream<NF, 1>(p, s); return true;
+    case 2: launch_stream<NF, 2>(p, s); return true;
+    case 3: launch_stream<NF, 3>(p, s); return true;
+    case 4: launch_stream<NF, 4>(p, s); return true;
+    case 5: launch_stream<NF, 5>(p, s); return true;
+    case 6: launch_stream<NF, 6>(p, s); return true;
+    default: return false;
+  }
+}
+
+// impl kF32Stream (channel tile by Cout) / kF32StreamN2 (32-channel tiles): 1x1 stride-1 convs, Kpad <= 192
+static bool x3_stream(const ConvParams& p, hipStream_t s, int nf_force) {
+  if (p.KH != 1 || p.KW != 1 || p.stride != 1 || p.pad_t != 0 || p.pad_l != 0 || p.Cin % 8 != 0 ||
+      p.Kpad > 192 || p.Ho != p.H || p.Wo != p.W || p.xs % 4 != 0)
+    return false;
+  const int ncf = p.Cout_pad / 16;
+  const int nf = nf_force ? nf_force
+                          : ncf <= 5 ? ncf : ncf % 4 == 0 ? 4 : ncf % 3 == 0 ? 3 : ncf % 5 == 0 ? 5 : ncf % 2 == 0 ? 2 : 1;
+  switch (nf) {
+    case 1: return launch_stream_k<1>(p, s);
+    case 2: return launch_stream_k<2>(p, s);
+    case 3: return launch_stream_k<3>(p, s);
+    case 4: return launch_stream_k<4>(p, s);
+    case 5: return launch_stream_k<5>(p, s);
+    default: return false;
+  }
+}
+
 void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (p.Cin % 4 != 0 || p.xs % 4 != 0 || p.Kpad % 16 != 0 || p.Cout_pad % 16 != 0 || p.Cout % 4 != 0 ||
       p.Cout > p.Cout_pad || p.ys % 4 != 0)
@@ -1015,6 +1193,11 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
   const int ncf = p.Cout_pad / 16;
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
+    if (p.impl == kF32Stream || p.impl == kF32StreamN2) {
+      if (!x3_stream(p, s, p.impl == kF32StreamN2 ? 2 : 0))
+        throw std::runtime_error("conv2d_f32: not a stream-eligible conv (1x1 stride 1, Kpad <= 192)");
+      return;
+    }
     if (p.impl == kF32X3Halo || p.impl == kF32X3HaloN3 || p.impl == kF32X3HaloN2) {
       const int nf = p.impl == kF32X3HaloN3 ? 3 : p.impl == kF32X3HaloN2 ? 2 : 0;
       if (!x3_halo(p, s, nf)) throw std::runtime_error("conv2d_f32: not an x3-halo-eligible conv");

@@ -48,7 +48,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
     A float32 ``x`` runs the exact-fp32 kernel (fp32 weights, v_mfma_f32_16x16x4_f32, fp32 output).
     ``impl`` pins a kernel (0 = the dispatch policy; fp32: 1 direct, 2 LDS, 10 + v LDS tile variant v,
     40 + v triple-bf16-split variant v, 100 halo, 101 split halo, 102 / 103 split halo with 48 / 32-channel
-    tiles — csrc/kernels/launch.h).
+    tiles, 104 / 105 weight-stationary streaming 1x1 (auto / 32-channel tiles) — csrc/kernels/launch.h).
     """
     f32 = x.dtype == torch.float32
     B, H, W, Cx = x.shape

@@ -77,7 +77,7 @@ def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
         assert torch.equal(out2, up_ref)
 
 
-X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103]  # x3 tile variants + split halo (auto / 48 / 32 ch tiles)
+X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105]  # x3 tile variants, split halo, 1x1 stream
 
 
 @pytest.mark.parametrize(
@@ -115,7 +115,7 @@ def test_conv_x3_split_matches_fp64(device, B, H, Cin, Cout, k, s, act, res):
         try:
             y = AF.conv2d_nhwc(xd, w32, b32, stride=s, act=act, res=rd, packed=packed, impl=impl)
         except RuntimeError as e:
-            assert "eligible" in str(e), e  # the split halo only takes 3x3 stride-1 convs
+            assert "eligible" in str(e), e  # split halo: 3x3 stride 1 only; stream: 1x1 stride 1, K <= 192
             continue
         torch.cuda.synchronize()
         _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
