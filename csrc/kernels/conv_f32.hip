@@ -1002,7 +1002,7 @@ static bool halo_f32(const ConvParams& p, hipStream_t s, bool force = false) {
 }
 
 // ---------------------------------------------------------------------------
-// Weight-stationary streaming 1x1 conv, fp32-accurate on the bf16 matrix cores (triple-bf16 split).
+// Weight-stationary streaming small-K conv, fp32-accurate on the bf16 matrix cores (triple-bf16 split).
 // The small-K 1x1 convs (K <= 192: YOLO C3 / neck pointwise layers, MobileNetV2 expand GEMMs) ran 2-10x
 // off their memory floor in the tiled kernels above (profiles/r2_fp32_irprefetch_ops.md: 10-30 % MFMA
 // busy, each workgroup's life one load latency + 2-6 k-chunks + its stores): here a workgroup splits its
@@ -1030,7 +1030,8 @@ __global__ __launch_bounds__(STR_THREADS) void conv_x3_stream_kernel(const ConvP
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, kq = lane >> 4;
   const int n0 = blockIdx.y * BN;
-  const int M = live_batch(p.B, p.bdev) * p.Ho * p.Wo;
+  const int HWo = p.Ho * p.Wo;
+  const int M = live_batch(p.B, p.bdev) * HWo;
   const int tiles = (M + 15) / 16;
   int t = blockIdx.x * 4 + wave;
   if (blockIdx.x * 4 >= tiles) return;
@@ -1063,20 +1064,32 @@ __global__ __launch_bounds__(STR_THREADS) void conv_x3_stream_kernel(const ConvP
 
   const float* __restrict__ x = (const float*)p.x;
   const int tstride = gridDim.x * 4;
+  // implicit im2col: this lane's 8 k of slab sl are input channels ci..ci+7 of one tap (Cin % 8 == 0)
+  int tdy[KS], tdx[KS], tci[KS];
+#pragma unroll
+  for (int sl = 0; sl < KS; ++sl) {
+    const int k0 = sl * 32 + kq * 8, tap = k0 / p.Cin;
+    const int kh = tap / p.KW;
+    tci[sl] = k0 - tap * p.Cin;
+    tdy[sl] = tap < p.KH * p.KW ? kh - p.pad_t : -(1 << 20);  // past the last tap: zero (fails the bounds test)
+    tdx[sl] = tap - kh * p.KW - p.pad_l;
+  }
   float4 b0[KS], b1[KS];
   auto load_b = [&](int tt) {
     const int pix = tt * 16 + col;
+    const int b = pix / HWo, r = pix - b * HWo;
+    const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+    const float* xb = x + (size_t)b * p.H * p.W * p.xs;
 #pragma unroll
     for (int sl = 0; sl < KS; ++sl) {
-      const int k0 = sl * 32 + kq * 8;
-      const bool ok = pix < M && k0 < p.Cin;
-      const float* ptr = x + (size_t)pix * p.xs + k0;
+      const int iy = oy * p.stride + tdy[sl], ix = ox * p.stride + tdx[sl];
+      const bool ok = pix < M && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      const float* ptr = xb + ((size_t)iy * p.W + ix) * p.xs + tci[sl];
       b0[sl] = load_f4_or_zero(ptr, x, ok);
       b1[sl] = load_f4_or_zero(ptr + 4, x, ok);
     }
   };
   if (t < tiles) load_b(t);
-  const int HWo = p.Ho * p.Wo;
   for (; t < tiles; t += tstride) {
     float4 c0[KS], c1[KS];
 #pragma unroll
@@ -1161,11 +1174,11 @@ static bool launch_stream_k(const ConvParams& p, hipStream_t s) {
   }
 }
 
-// impl kF32Stream (channel tile by Cout) / kF32StreamN2 (32-channel tiles): 1x1 stride-1 convs, Kpad <= 192
+// impl kF32Stream (channel tile by Cout) / kF32StreamN2 (32-channel tiles): any conv with Cin % 8 == 0 and
+// Kpad <= 192 (1x1 pointwise layers, and the 3x3 / 2x2 convs over 16-channel space-to-depth stems, whose
+// taps are gathered per lane: 8 k of a slab never straddle two taps)
 static bool x3_stream(const ConvParams& p, hipStream_t s, int nf_force) {
-  if (p.KH != 1 || p.KW != 1 || p.stride != 1 || p.pad_t != 0 || p.pad_l != 0 || p.Cin % 8 != 0 ||
-      p.Kpad > 192 || p.Ho != p.H || p.Wo != p.W || p.xs % 4 != 0)
-    return false;
+  if (p.Cin % 8 != 0 || p.Kpad > 192 || p.Kpad < p.KH * p.KW * p.Cin || p.xs % 4 != 0) return false;
   const int ncf = p.Cout_pad / 16;
   const int nf = nf_force ? nf_force
                           : ncf <= 5 ? ncf : ncf % 4 == 0 ? 4 : ncf % 3 == 0 ? 3 : ncf % 5 == 0 ? 5 : ncf % 2 == 0 ? 2 : 1;
@@ -1195,7 +1208,7 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
     if (p.impl == kF32Stream || p.impl == kF32StreamN2) {
       if (!x3_stream(p, s, p.impl == kF32StreamN2 ? 2 : 0))
-        throw std::runtime_error("conv2d_f32: not a stream-eligible conv (1x1 stride 1, Kpad <= 192)");
+        throw std::runtime_error("conv2d_f32: not a stream-eligible conv (Cin % 8, Kpad <= 192)");
       return;
     }
     if (p.impl == kF32X3Halo || p.impl == kF32X3HaloN3 || p.impl == kF32X3HaloN2) {

@@ -68,7 +68,7 @@ constexpr int kF32Halo = 100;
 constexpr int kF32X3Halo = 101;  // 3x3 stride-1 halo tiles with the triple-bf16 split
 constexpr int kF32X3HaloN3 = 102;  // ... with 48-channel tiles
 constexpr int kF32X3HaloN2 = 103;  // ... with 32-channel tiles
-constexpr int kF32Stream = 104;    // weight-stationary streaming 1x1 conv, triple-bf16 split (Kpad <= 192)
+constexpr int kF32Stream = 104;    // weight-stationary streaming conv, triple-bf16 split (Cin % 8, Kpad <= 192)
 constexpr int kF32StreamN2 = 105;  // ... with 32-channel tiles
 void conv2d_f32(const ConvParams& p, hipStream_t s);
 

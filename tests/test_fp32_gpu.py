@@ -87,6 +87,8 @@ X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105]  # x3 tile va
         (2, 24, 80, 80, 3, 1, "silu", False),      # Cin 80: a partial 32-channel chunk in the halo kernel
         (2, 20, 64, 144, 3, 1, "silu", False),     # detect head (Cout 144)
         (2, 40, 16, 32, 3, 2, "silu", False),      # 3x3 stride 2
+        (2, 12, 16, 32, 2, 1, "relu6", False),     # 2x2 over a space-to-depth stem (MobileNetV2 stem)
+        (2, 20, 16, 16, 3, 1, "silu", True),       # YOLO s2d stem 3x3 over 16 channels (+ residual)
         (4, 7, 160, 960, 1, 1, "relu6", False),    # MobileNet expand
         (4, 7, 960, 160, 1, 1, None, True),        # MobileNet project + residual
     ],
@@ -115,7 +117,7 @@ def test_conv_x3_split_matches_fp64(device, B, H, Cin, Cout, k, s, act, res):
         try:
             y = AF.conv2d_nhwc(xd, w32, b32, stride=s, act=act, res=rd, packed=packed, impl=impl)
         except RuntimeError as e:
-            assert "eligible" in str(e), e  # split halo: 3x3 stride 1 only; stream: 1x1 stride 1, K <= 192
+            assert "eligible" in str(e), e  # split halo: 3x3 stride 1 only; stream: Cin % 8, K <= 192
             continue
         torch.cuda.synchronize()
         _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
