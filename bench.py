@@ -17,10 +17,12 @@ each request end to end, reference experiment.yaml:178-181,300-318):
   ONNX Runtime numerics (reference experiment.yaml:202,207,220,225); ``bf16`` the tuned
   bf16 kernels.
 * steady state: the clients run continuously from the warm-up into the timed window, so
-  the window contains no pipeline fill or drain.  A "step" is ``--batch`` (32) completed
-  requests: ``--warmup`` steps complete untimed, then a barrier + device sync open the
-  window, the window closes (device sync + barrier) once exactly ``--steps`` more steps
-  have completed on the rank.  ``value`` = steps * batch * world / max-over-ranks window.
+  the window contains no pipeline fill or drain.  A "step" is ``--step-batches`` (8) dynamic
+  batches of ``--batch`` (32) = 256 completed requests (a 32-request step made a 20-step
+  window ~85 ms long, where one host hiccup moved the result by 20 %): ``--warmup`` steps
+  complete untimed, then a barrier + device sync open the window, the window closes (device
+  sync + barrier) once exactly ``--steps`` more steps have completed on the rank.
+  ``value`` = steps * requests per step * world / max-over-ranks window.
   P50/P99 are per-request end-to-end latencies of the requests completed in the window.
 
 Multi-GPU: ``--gpus N`` under torchrun (RANK/LOCAL_RANK/WORLD_SIZE from the environment)
@@ -35,6 +37,7 @@ Secondary keys: ``engine_req_s`` (device pipeline fed pre-decoded images, same d
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import subprocess
@@ -212,33 +215,39 @@ def measure(pipe, pool, jpegs, a, info, D, torch):
 
     C = native()
     B = a.batch
+    R = B * a.step_batches  # requests per step
     batcher = C.DynamicBatcher([pipe.ex], {"max_batch": B, "max_queue_delay_us": a.queue_delay_us,
                                            "max_queue_size": 0})
     loop = ClosedLoop(pool, batcher, jpegs, a.users, offset=(info.rank * 37) % len(jpegs))
+    gc.collect()
+    gc.freeze()  # the long-lived heap (models, workload) leaves the collector's generations before the loop runs
     loop.start()
     try:
         # W warm-up steps at least; the closed loop also has to leave its start-up transient (all users
         # arrive at once, first graph replays) before the window opens: >= 4 requests per user and
         # --min-warmup-s seconds, so the window's value does not depend on --steps / --warmup
         tw = time.perf_counter()
-        loop.wait_for(max(a.warmup * B, 4 * a.users))
+        loop.wait_for(max(a.warmup * R, 4 * a.users))
         while time.perf_counter() - tw < a.min_warmup_s:
             time.sleep(0.05)
         D.barrier(info)
         torch.cuda.synchronize()
+        gc.disable()  # no collector pauses inside the window (the loop allocates per request)
         with loop.lock:
             c0 = loop.done
         t0 = time.perf_counter()
-        loop.wait_for(c0 + a.steps * B)
+        loop.wait_for(c0 + a.steps * R)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
+        gc.enable()
         D.barrier(info)
     finally:
+        gc.enable()
         loop.stop()
         batcher.shutdown()
-    lat = loop.lat[c0:c0 + a.steps * B]
-    crops = loop.crops[c0:c0 + a.steps * B]
-    bs = loop.batch[c0:c0 + a.steps * B]
+    lat = loop.lat[c0:c0 + a.steps * R]
+    crops = loop.crops[c0:c0 + a.steps * R]
+    bs = loop.batch[c0:c0 + a.steps * R]
     return t1 - t0, lat, crops, bs, loop.errors
 
 
@@ -260,10 +269,12 @@ def bs1_latency(pipe, pool, jpegs, n: int, a):
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100, help="timed steps (a step = --batch completed requests)")
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=30,
+                    help="timed steps (a step = --step-batches x --batch completed requests)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--min-warmup-s", type=float, default=2.0, help="minimum warm-up time of the closed loop")
-    ap.add_argument("--batch", type=int, default=32, help="requests per step = dynamic batcher max_batch")
+    ap.add_argument("--batch", type=int, default=32, help="dynamic batcher max_batch")
+    ap.add_argument("--step-batches", type=int, default=8, help="batches of --batch requests per step")
     ap.add_argument("--users", type=int, default=192, help="closed-loop clients per GPU")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--decode-workers", type=int, default=0, help="JPEG decode processes per rank (0: auto)")
@@ -343,7 +354,7 @@ def main(argv=None) -> int:
                               dtype="bf16")
             w2, lat2, _, _, _ = measure(alt, pool, jpegs, a, info, D, torch)
             w2 = D.allreduce_max(w2, info)
-            sec = {"bf16": {"value": round(a.steps * a.batch * info.world / w2, 2),
+            sec = {"bf16": {"value": round(a.steps * a.batch * a.step_batches * info.world / w2, 2),
                             "p50_ms": round(float(np.percentile(lat2, 50)) * 1e3, 3),
                             "p99_ms": round(float(np.percentile(lat2, 99)) * 1e3, 3),
                             "engine_req_s": round(engine_throughput(alt, images, a.batch, a.engine_batches), 1)}}
@@ -355,7 +366,7 @@ def main(argv=None) -> int:
         D.barrier(info)
         if info.is_main:
             flat = np.asarray([x for lst in all_lat for x in lst]) * 1e3
-            total_req = a.steps * a.batch * info.world
+            total_req = a.steps * a.batch * a.step_batches * info.world
             fan = float(np.sum([x for lst in all_crops for x in lst]) / max(1, len(flat)))
             out = {
                 "metric": METRIC,
@@ -379,6 +390,7 @@ def main(argv=None) -> int:
                     "seq_len": None,
                     "parallelism": f"dp{info.world}",
                     "per_gpu_batch": a.batch,
+                    "requests_per_step_per_gpu": a.batch * a.step_batches,
                     "users_per_gpu": a.users,
                     "image_size": 640,
                     "crop_size": 224,

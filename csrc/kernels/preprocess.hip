@@ -87,13 +87,24 @@ __global__ __launch_bounds__(256) void letterbox_s2d_kernel(const LetterboxParam
   const float sy = (float)((double)m.h / (double)m.new_h);
   const float sx = (float)((double)m.w / (double)m.new_w);
   float out[16];
+  // unit scale (the image's long side is already T: COCO's 640x480 / 640x427 ...): the bilinear taps have zero
+  // weight, so the letterboxed pixel is the source pixel (bitwise the same value) — 3 byte loads instead of 12
+  const bool unit = m.new_h == m.h && m.new_w == m.w;
 #pragma unroll
   for (int pq = 0; pq < 4; ++pq) {
     const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
     const int dy = oy - m.pad_h, dx = ox - m.pad_w;
     float rgb[3] = {114.f, 114.f, 114.f};
-    if (dy >= 0 && dy < m.new_h && dx >= 0 && dx < m.new_w)
-      bilinear_rgb(img, m.w, lin_tap(dy, sy, m.h), lin_tap(dx, sx, m.w), rgb);
+    if (dy >= 0 && dy < m.new_h && dx >= 0 && dx < m.new_w) {
+      if (unit) {
+        const uint8_t* px = img + ((size_t)dy * m.w + dx) * 3;
+        rgb[0] = (float)px[0];
+        rgb[1] = (float)px[1];
+        rgb[2] = (float)px[2];
+      } else {
+        bilinear_rgb(img, m.w, lin_tap(dy, sy, m.h), lin_tap(dx, sx, m.w), rgb);
+      }
+    }
 #pragma unroll
     for (int c = 0; c < 3; ++c) out[pq * 3 + c] = div255<T>(rgb[c]);
   }

@@ -76,7 +76,8 @@ def test_model_server_pipeline_matches_fused(gpu_server):
     direct = GpuPipeline(*default_models(0), device=0, buckets=[4]).infer(imgs)
     for o, d in zip(outs, direct):
         assert o["DETECTIONS"].shape[0] == len(d) >= 1
-        np.testing.assert_allclose(o["DETECTIONS"][:, :4], d.boxes, atol=1e-3)
+        # bucket 4 here vs the model server's buckets: separately tuned tilings, fp32 summation order
+        np.testing.assert_allclose(o["DETECTIONS"][:, :4], d.boxes, rtol=2e-5, atol=5e-3)
         np.testing.assert_array_equal(o["CLASS_IDS"], d.topk_idx)
 
 

@@ -35,10 +35,16 @@ def test_split_matches_fused(dense_models, device, dtype):
     assert sum(len(r) for r in fused) > 5
     for a, b in zip(fused, got):
         assert len(a) == len(b)
-        np.testing.assert_array_equal(a.boxes, b.boxes)
+        if dtype == "bf16":
+            np.testing.assert_array_equal(a.boxes, b.boxes)
+            np.testing.assert_allclose(a.topk_logit, b.topk_logit, rtol=1e-6, atol=1e-6)
+        else:
+            # the split detector / classifier programs are tuned on their own: other conv tilings of the
+            # same layers, i.e. other fp32 summation orders (~1e-5 relative after 60 layers and the DFL)
+            np.testing.assert_allclose(a.boxes, b.boxes, rtol=2e-5, atol=5e-3)
+            np.testing.assert_allclose(a.topk_logit, b.topk_logit, rtol=1e-4, atol=1e-4)
         np.testing.assert_array_equal(a.classes, b.classes)
         np.testing.assert_array_equal(a.topk_idx, b.topk_idx)
-        np.testing.assert_allclose(a.topk_logit, b.topk_logit, rtol=1e-6, atol=1e-6)
 
 
 def test_split_overflow_passes_and_batcher(dense_models, device):
