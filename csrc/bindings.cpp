@@ -254,7 +254,11 @@ void py_head_pool(const py::dict& d) {
   p.act = get<int>(d, "act", 0);
   p.B = req<int>(d, "B");
   p.bdev = ptr<const int*>(d, "bdev");
-  head_pool(p, stream_of(d));
+  prepare_kernels();
+  if (get<int>(d, "f32", 0))
+    head_pool_f32(p, stream_of(d));
+  else
+    head_pool(p, stream_of(d));
 }
 
 void py_avgpool(const py::dict& d) {

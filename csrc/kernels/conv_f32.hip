@@ -1206,6 +1206,10 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
   const int ncf = p.Cout_pad / 16;
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
+    if (p.impl == kF32Fc) {
+      if (!conv_fc_f32(p, s)) throw std::runtime_error("conv2d_f32: not an FC-eligible conv (1x1 map, Kpad 1280)");
+      return;
+    }
     if (p.impl == kF32Stream || p.impl == kF32StreamN2) {
       if (!x3_stream(p, s, p.impl == kF32StreamN2 ? 2 : 0))
         throw std::runtime_error("conv2d_f32: not a stream-eligible conv (Cin % 8, Kpad <= 192)");
@@ -1228,6 +1232,7 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
     if (p.impl >= 10 + kF32Variants || !launch_lds_variant(p, s, M, p.impl - 10)) throw std::runtime_error("conv2d_f32: unknown variant");
     return;
   }
+  if (p.impl == 0 && conv_fc_f32(p, s)) return;  // classifier FC: split-K over the 1x1 map
   const int impl = p.impl == 1 ? 1 : p.impl >= 2 ? 2 : f32_conv_family();
   if (impl == 2 && halo_f32(p, s)) return;
   if (impl == 2) {

@@ -306,6 +306,7 @@ void prepare_kernels() {
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
   ir_prepare();
+  head_pool_f32_prepare();
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)sppf_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
   done = true;

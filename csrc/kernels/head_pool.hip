@@ -23,6 +23,9 @@
 //           scale by 1/HW, bf16 store of 4 channels per lane group.
 // The pooled vector is summed in fp32 before a single bf16 rounding (the
 // unfused path rounds every 7x7 activation to bf16 first).
+#include <stdexcept>
+#include <string>
+
 #include "common.h"
 #include "launch.h"
 
@@ -124,6 +127,153 @@ void head_pool(const HeadPoolParams& p, hipStream_t s) {
   const long grid = (long)p.B * ((p.N + kNS - 1) / kNS);
   if (grid <= 0) return;
   hipLaunchKernelGGL(head_pool_kernel<10>, dim3((unsigned)grid), dim3(256), 0, s, p);
+}
+
+
+// ---------------------------------------------------------------------------
+// fp32 programs: the same fusion at fp32 accuracy on the bf16 matrix cores (triple-bf16 split, six partial
+// products per MFMA step, conv_f32.hip).  Unfused, the fp32 head was a 1x1 conv writing the 7x7x1280 fp32 map
+// (251 KB per crop) plus an avgpool kernel reading it back: 73 + 17 us for 128 crops
+// (profiles/r2_fp32_stream2_ops.md ops 109-110).  The crop's pixels are split into [h|m|l] bf16 planes in LDS
+// once (64 rows x 1952 B: a pitch of 2 (mod 4) 16-B slots); each wave splits its weight fragments in
+// registers, one K slab ahead of use.
+// 8 waves x 32 channels = 256 output channels per workgroup (5 per crop for 1280): the staged, split pixel
+// block (the workgroup's fixed cost) is shared by twice the channels of a 4-wave workgroup.
+constexpr int kNSF = 256, kHeadF32Threads = 512;
+
+template <int KSLABS>
+__global__ __launch_bounds__(kHeadF32Threads) void head_pool_f32_kernel(const HeadPoolParams p) {
+  constexpr int K = KSLABS * 32;
+  constexpr int PITCH = 6 * K + 32;  // bytes per staged pixel row: three bf16 planes + pad
+  extern __shared__ __align__(16) uint8_t xsf[];
+
+  const int nslices = (p.N + kNSF - 1) / kNSF;
+  const int b = blockIdx.x / nslices;
+  const int n0 = (blockIdx.x - b * nslices) * kNSF;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = lane & 15, kq = lane >> 4;
+  const float* w = (const float*)p.w;
+  const int nw = n0 + wave * (16 * kNF);
+
+  float4 wr[kNF][2];
+  auto load_w = [&](int s) {
+#pragma unroll
+    for (int f = 0; f < kNF; ++f) {
+      const int n = nw + f * 16 + row;
+      const float* src = w + (size_t)(n < p.Npad ? n : 0) * p.Kpad + s * 32 + kq * 8;
+      wr[f][0] = *(const float4*)src;
+      wr[f][1] = *(const float4*)(src + 4);
+      if (n >= p.Npad) wr[f][0] = wr[f][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  load_w(0);
+
+  // ---- stage the crop's pixels as split planes (pixels HW..63 and channels past K are zero)
+  const float* xb = (const float*)p.x + (size_t)b * p.HW * p.xs;
+  constexpr int CPR = K / 4;
+  for (int i = tid; i < kMaxHW * CPR; i += kHeadF32Threads) {
+    const int px = i / CPR, c = i - px * CPR;
+    const bool ok = px < p.HW && c * 4 < p.K;
+    float4 v = *(const float4*)(ok ? xb + (size_t)px * p.xs + c * 4 : xb);
+    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float f[4] = {v.x, v.y, v.z, v.w};
+    bf16x4 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      h[j] = (bf16)f[j];
+      const float r = f[j] - (float)h[j];
+      m[j] = (bf16)r;
+      l[j] = (bf16)(r - (float)m[j]);
+    }
+    uint8_t* d = xsf + px * PITCH + c * 8;
+    *(bf16x4*)d = h;
+    *(bf16x4*)(d + 2 * K) = m;
+    *(bf16x4*)(d + 4 * K) = l;
+  }
+  __syncthreads();
+
+  f32x4 acc[kNF][4];
+#pragma unroll
+  for (int f = 0; f < kNF; ++f)
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) acc[f][mm] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+  for (int s = 0; s < KSLABS; ++s) {
+    bf16x8 ah[kNF], am[kNF], al[kNF];
+#pragma unroll
+    for (int f = 0; f < kNF; ++f) {
+      const float v[8] = {wr[f][0].x, wr[f][0].y, wr[f][0].z, wr[f][0].w, wr[f][1].x, wr[f][1].y, wr[f][1].z, wr[f][1].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ah[f][j] = (bf16)v[j];
+        const float r = v[j] - (float)ah[f][j];
+        am[f][j] = (bf16)r;
+        al[f][j] = (bf16)(r - (float)am[f][j]);
+      }
+    }
+    if (s + 1 < KSLABS) load_w(s + 1);  // next slab's weights in flight during this slab's MFMAs
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      const uint8_t* r = xsf + (mm * 16 + row) * PITCH + s * 64 + kq * 16;
+      const bf16x8 bh = *(const bf16x8*)r, bm = *(const bf16x8*)(r + 2 * K), bl = *(const bf16x8*)(r + 4 * K);
+#pragma unroll
+      for (int f = 0; f < kNF; ++f) {
+        f32x4 c = acc[f][mm];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[f], bm, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[f], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[f], bh, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bm, c, 0, 0, 0);
+        acc[f][mm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bh, c, 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: bias + act, mean over the valid pixels, fp32 store of 4 channels per lane group
+  const float inv = 1.0f / (float)p.HW;
+  float* y = (float*)p.y + (size_t)b * p.ys;
+#pragma unroll
+  for (int f = 0; f < kNF; ++f) {
+    const int cb = nw + f * 16 + kq * 4;
+    const bool cok = cb < p.N;
+    const float4 bias = cok ? *(const float4*)(p.bias + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float sum[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      if (mm * 16 + row < p.HW) {
+        sum[0] += apply_act(acc[f][mm][0] + bias.x, p.act);
+        sum[1] += apply_act(acc[f][mm][1] + bias.y, p.act);
+        sum[2] += apply_act(acc[f][mm][2] + bias.z, p.act);
+        sum[3] += apply_act(acc[f][mm][3] + bias.w, p.act);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) sum[i] += __shfl_xor(sum[i], o, 64);
+      sum[i] *= inv;
+    }
+    if (row == 0 && cok) *(float4*)(y + cb) = make_float4(sum[0], sum[1], sum[2], sum[3]);
+  }
+}
+
+constexpr int kHeadF32Lds = kMaxHW * (6 * 320 + 32);
+
+void head_pool_f32_prepare() {
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)head_pool_f32_kernel<10>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+
+void head_pool_f32(const HeadPoolParams& p, hipStream_t s) {
+  if (p.HW <= 0 || p.HW > kMaxHW) throw std::runtime_error("head_pool_f32: HW must be 1..64");
+  if (p.Kpad != 320 || p.K > p.Kpad || p.K % 4) throw std::runtime_error("head_pool_f32: instantiated for Kpad 320");
+  if (p.N % 4 || p.Npad % 16 || p.Npad < p.N) throw std::runtime_error("head_pool_f32: bad output channel geometry");
+  if (p.xs % 4 || p.ys % 4) throw std::runtime_error("head_pool_f32: strides must keep 16-B alignment");
+  const long grid = (long)p.B * ((p.N + kNSF - 1) / kNSF);
+  if (grid <= 0) return;
+  hipLaunchKernelGGL(head_pool_f32_kernel<10>, dim3((unsigned)grid), dim3(kHeadF32Threads), kHeadF32Lds, s, p);
 }
 
 }  // namespace arena

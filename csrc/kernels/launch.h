@@ -70,6 +70,8 @@ constexpr int kF32X3HaloN3 = 102;  // ... with 48-channel tiles
 constexpr int kF32X3HaloN2 = 103;  // ... with 32-channel tiles
 constexpr int kF32Stream = 104;    // weight-stationary streaming conv, triple-bf16 split (Cin % 8, Kpad <= 192)
 constexpr int kF32StreamN2 = 105;  // ... with 32-channel tiles
+constexpr int kF32Fc = 106;        // split-K FC over a 1x1 map (fc_splitk.hip), exact fp32
+bool conv_fc_f32(const ConvParams& p, hipStream_t s);
 void conv2d_f32(const ConvParams& p, hipStream_t s);
 
 // ---------------------------------------------------------------- depthwise 3x3 (K12)
@@ -365,6 +367,9 @@ struct HeadPoolParams {
   const int* bdev;
 };
 void head_pool(const HeadPoolParams& p, hipStream_t s);
+// fp32 programs (x fp32 [B][HW][xs], w fp32 [Npad][Kpad], y fp32): triple-bf16-split MFMA, fp32-level error
+void head_pool_f32(const HeadPoolParams& p, hipStream_t s);
+void head_pool_f32_prepare();
 
 struct TopkResult {
   int idx[5];

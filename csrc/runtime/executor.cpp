@@ -258,7 +258,8 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
       const bool f32 = prog_[i][kDtypeField] == 1;
       const bool ok = f32 ? (v >= 0 && v <= 2) || (v >= 10 && v < 10 + kF32Variants) ||
                                 (v >= kF32X3 && v < kF32X3 + kF32X3Variants) || v == kF32Halo || v == kF32X3Halo ||
-                                v == kF32X3HaloN3 || v == kF32X3HaloN2 || v == kF32Stream || v == kF32StreamN2
+                                v == kF32X3HaloN3 || v == kF32X3HaloN2 || v == kF32Stream || v == kF32StreamN2 ||
+                                v == kF32Fc
                           : v >= 0 && v <= 3;
       if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
       bk.impl[i] = (int8_t)v;
@@ -301,7 +302,7 @@ void Executor::autotune(Bucket& bk) {
   static const int kF32Candidates[] = {0,      12,     13,     14,     17,     19,     20,         21,
                                        23,     24,     kF32Halo, kF32X3, kF32X3 + 1, kF32X3 + 4, kF32X3 + 5,
                                        kF32X3 + 6, kF32X3 + 7, kF32X3 + 8, kF32X3Halo, kF32X3HaloN3,
-                                       kF32X3HaloN2, kF32Stream, kF32StreamN2};
+                                       kF32X3HaloN2, kF32Stream, kF32StreamN2, kF32Fc};
   static const int kBf16Candidates[] = {1, 2, 3};
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;
@@ -404,7 +405,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
     // field 47: activation precision of the op (0 bf16, 1 exact fp32; planner.OP_DTYPE_FIELD)
     const bool f32 = r[kDtypeField] == 1;
     const int eb = f32 ? 4 : 2;
-    if (f32 && (r[0] == OP_STEMFUSED || r[0] == OP_C3FUSED || r[0] == OP_HEADPOOL))
+    if (f32 && (r[0] == OP_STEMFUSED || r[0] == OP_C3FUSED))
       throw std::runtime_error("op " + std::to_string(r[0]) + " has no fp32 kernel");
     switch (r[0]) {
       case OP_CONV: {
@@ -679,7 +680,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       }
       case OP_HEADPOOL: {
         HeadPoolParams p{};
-        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.x = resolve(bk, sl, r[1], r[2], eb);
         p.xs = (int)r[3];
         p.HW = (int)r[4];
         p.K = (int)r[5];
@@ -688,12 +689,15 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.bias = (const float*)(W + r[8]);
         p.N = (int)r[9];
         p.Npad = (int)r[10];
-        p.y = resolve(bk, sl, r[11], r[12], 2);
+        p.y = resolve(bk, sl, r[11], r[12], eb);
         p.ys = (int)r[13];
         p.act = (int)r[14];
         p.B = batch(r[15]);
         p.bdev = bdev(r[15]);
-        head_pool(p, s);
+        if (f32)
+          head_pool_f32(p, s);
+        else
+          head_pool(p, s);
         break;
       }
       case OP_AVGPOOL: {

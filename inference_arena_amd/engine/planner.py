@@ -478,12 +478,12 @@ class ProgramBuilder:
 
     def head_pool(self, src: View, dst: View, w: torch.Tensor, b: torch.Tensor, *, act: str | None = "relu6",
                   kind: int = CROPS) -> None:
-        """1x1 conv + activation + global average pool in one kernel: ``dst`` is a 1x1 map."""
-        self._bf16_only("head_pool")
+        """1x1 conv + activation + global average pool in one kernel: ``dst`` is a 1x1 map (bf16:
+        csrc/kernels/head_pool.hip head_pool; fp32: head_pool_f32, triple-bf16-split MFMA)."""
         cout, cin, kh, kw = w.shape
         if (kh, kw) != (1, 1) or cin != src.C or cout != dst.C or dst.buf.H * dst.buf.W != 1:
             raise ValueError("head_pool: expects 1x1 weights [N, C, 1, 1] and a 1x1 destination")
-        wb, bb, kpad, cpad = pack_conv_weight(w, b)
+        wb, bb, kpad, cpad = pack_conv_weight(w, b, self.dtype)
         rec = [OP_HEADPOOL, src.bid, src.coff, src.cs, src.buf.H * src.buf.W, cin, self.weights.add(wb), kpad,
                self.weights.add(bb), cout, cpad, dst.bid, dst.coff, dst.cs, ACT[act], kind]
         self._emit(rec, src, dst)

@@ -336,7 +336,7 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
                 res=View(cur, 0, blk.inp) if blk.use_res else None, kind=CROPS_)
         cur, H = O, Ho
     PO = pb.tensor("m.pool", 1, 1, 1280, kind=CROPS_)
-    if fuse_head_pool_default() and not pb.f32 and H * H <= 64 and cur.C == 320:
+    if fuse_head_pool_default() and H * H <= 64 and cur.C == 320:
         pb.head_pool(View(cur, 0, cur.C), View(PO, 0, 1280), *fold(m.head), act="relu6", kind=CROPS_)
     else:
         HD = pb.tensor("m.head", H, H, 1280, kind=CROPS_)

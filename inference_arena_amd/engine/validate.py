@@ -111,7 +111,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         if off < 0 or off + n > wbytes:
             raise ProgramError(f"op {i}: {what} reads weights [{off}, {off + n}) of {wbytes}")
 
-    fused = (OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL)
+    fused = (OP_STEMFUSED, OP_C3FUSED)  # bf16-only fused kernels
     for i, r in enumerate(prog.ops):
         op = int(r[0])
         kind_n = lambda k: crop_cap if int(k) == CROPS else B  # noqa: E731
@@ -250,10 +250,10 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             HW, K, Kpad, N, Npad = int(r[4]), int(r[5]), int(r[7]), int(r[9]), int(r[10])
             if not (0 < HW <= 64) or Kpad != 320 or K > Kpad or N % 4 or Npad % 16 or Npad < N:
                 raise ProgramError(f"op {i}: head_pool geometry HW={HW} K={K} Kpad={Kpad} N={N} unsupported")
-            view(i, r[1], int(r[2]), int(r[3]), n * HW, K, 2, "head_pool input")
-            weights(i, int(r[6]), Npad * Kpad * 2, "head_pool weight")
+            view(i, r[1], int(r[2]), int(r[3]), n * HW, K, el, "head_pool input")
+            weights(i, int(r[6]), Npad * Kpad * el, "head_pool weight")
             weights(i, int(r[8]), Npad * 4, "head_pool bias")
-            view(i, r[11], int(r[12]), int(r[13]), n, N, 2, "head_pool output")
+            view(i, r[11], int(r[12]), int(r[13]), n, N, el, "head_pool output")
         elif op == OP_AVGPOOL:
             n = kind_n(r[5])
             need(i, r[1], 0, n * int(r[2]) * int(r[3]) * el, "avgpool input")

@@ -180,18 +180,20 @@ def avgpool_nhwc(x: torch.Tensor) -> torch.Tensor:
 
 def head_pool_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, act: str | None = "relu6",
                    bdev: torch.Tensor | None = None) -> torch.Tensor:
-    """mean over pixels of act(conv1x1(x, w) + b): [B,H,W,C] bf16 -> [B, N] bf16 (head_pool.hip)."""
+    """mean over pixels of act(conv1x1(x, w) + b): [B,H,W,C] -> [B, N] (head_pool.hip); bf16 in/out, or fp32
+    in/out (fp32-accurate triple-bf16-split kernel) for a float32 ``x``."""
     from ..engine.planner import ACT, pack_conv_weight
 
     B, H, W, C = x.shape
     N = w.shape[0]
-    wb, bb, kpad, npad = pack_conv_weight(w, b)
-    wd = torch.frombuffer(bytearray(wb), dtype=torch.bfloat16).to(x.device)
+    f32 = x.dtype == torch.float32
+    wb, bb, kpad, npad = pack_conv_weight(w, b, "fp32" if f32 else "bf16")
+    wd = torch.frombuffer(bytearray(wb), dtype=torch.float32 if f32 else torch.bfloat16).to(x.device)
     bd = torch.frombuffer(bytearray(bb), dtype=torch.float32).to(x.device)
-    y = torch.empty(B, N, dtype=torch.bfloat16, device=x.device)
+    y = torch.empty(B, N, dtype=x.dtype, device=x.device)
     native().head_pool({"x": _ptr(x), "xs": C, "HW": H * W, "K": C, "w": _ptr(wd), "Kpad": kpad, "bias": _ptr(bd),
                         "N": N, "Npad": npad, "y": _ptr(y), "ys": N, "act": ACT[act], "B": B, "bdev": _ptr(bdev),
-                        "stream": _stream()})
+                        "stream": _stream(), "f32": int(f32)})
     torch.cuda.synchronize(x.device)  # keep the packed weights alive until the kernel ran
     return y
 

@@ -77,7 +77,7 @@ def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
         assert torch.equal(out2, up_ref)
 
 
-X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105]  # x3 tile variants, split halo, 1x1 stream
+X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105, 106]  # x3 variants, split halo, stream, FC
 
 
 @pytest.mark.parametrize(
@@ -117,7 +117,7 @@ def test_conv_x3_split_matches_fp64(device, B, H, Cin, Cout, k, s, act, res):
         try:
             y = AF.conv2d_nhwc(xd, w32, b32, stride=s, act=act, res=rd, packed=packed, impl=impl)
         except RuntimeError as e:
-            assert "eligible" in str(e), e  # split halo: 3x3 stride 1 only; stream: Cin % 8, K <= 192
+            assert "eligible" in str(e), e  # split halo: 3x3 s1; stream: Cin % 8, K <= 192; FC: 1x1 map, K 1280
             continue
         torch.cuda.synchronize()
         _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
@@ -336,3 +336,18 @@ def test_fp32_program_fuses_the_high_resolution_blocks():
     # >= 28x28: ir_f32.hip tile kernel; 14x14 and 7x7 run unfused (ir_crop_f32.hip is opt-in)
     assert [h for h, _ in fused] == [112, 112, 56, 56, 28, 28, 28]
     assert all(int(o[47]) == 1 for o in p.ops)
+
+
+@pytest.mark.parametrize("B,HW", [(5, 49), (3, 64), (2, 1)])
+def test_head_pool_f32_matches_fp64(device, B, HW):
+    """MobileNetV2 head conv (320 -> 1280) + ReLU6 + global average pool in one fp32-accurate kernel."""
+    g = torch.Generator().manual_seed(B * 7 + HW)
+    H = int(round(HW ** 0.5)) if int(round(HW ** 0.5)) ** 2 == HW else 1
+    W = HW // H
+    x = torch.randn(B, 320, H, W, generator=g)
+    w = torch.randn(1280, 320, 1, 1, generator=g) / 320 ** 0.5
+    b = torch.randn(1280, generator=g) * 0.1
+    y = AF.head_pool_nhwc(_nhwc(x).to(device), w, b, "relu6")
+    ref = F.conv2d(x.double(), w.double(), b.double()).clamp(0, 6).mean(dim=(2, 3))
+    scale = F.conv2d(x.double().abs(), w.double().abs(), b.double().abs()).mean(dim=(2, 3))
+    _fp32_check(y.double().cpu(), ref, scale, rel=4e-6)
