@@ -1174,6 +1174,151 @@ static bool launch_stream_k(const ConvParams& p, hipStream_t s) {
   }
 }
 
+// Exact-fp32 streaming variant (impl kF32StreamExact): the same weight-stationary pixel stream on
+// v_mfma_f32_16x16x4_f32 with fp32 operands and no split.  The split variant ran VALU-bound on the small-K
+// layers (profiles/r2_fp32_pmc_ops_v2.md: 10-30 VALU per MFMA — eight splits per lane per 32-deep slab plus the
+// SiLU epilogue for a K = 32 conv's 12 MFMAs): at K <= 64 the 4x-slower fp32 MFMA costs less than the split.
+// Lane l supplies k = 16 c + 4 (l >> 4) + s in step s of chunk c (one float4 per chunk: Cin % 4 == 0 keeps the 4
+// channels in one tap); weight rows are fp32 in LDS at a K + 8 float pitch (2 (mod 4) 16-B slots).
+template <int NF, int KC>
+__global__ __launch_bounds__(STR_THREADS) void conv_f32_stream_kernel(const ConvParams p) {
+  constexpr int BN = NF * 16, K = KC * 16, WPF = K + 8;
+  __shared__ __attribute__((aligned(16))) float sW[BN * WPF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int n0 = blockIdx.y * BN;
+  const int HWo = p.Ho * p.Wo;
+  const int M = live_batch(p.B, p.bdev) * HWo;
+  const int tiles = (M + 15) / 16;
+  int t = blockIdx.x * 4 + wave;
+  if (blockIdx.x * 4 >= tiles) return;
+
+  const float* __restrict__ w = (const float*)p.w;
+  for (int i = tid; i < BN * K / 4; i += STR_THREADS) {
+    const int row = i / (K / 4), k = 4 * (i - row * (K / 4));
+    const bool ok = n0 + row < p.Cout_pad && k < p.Kpad;
+    *(float4*)&sW[row * WPF + k] = load_f4_or_zero(w + (size_t)(n0 + row) * p.Kpad + k, w, ok);
+  }
+  float4 bias[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int cb = n0 + j * 16 + 4 * kq;
+    bias[j] = cb < p.Cout ? *(const float4*)(p.bias + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+
+  const float* __restrict__ x = (const float*)p.x;
+  const int tstride = gridDim.x * 4;
+  int tdy[KC], tdx[KC], tci[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const int k0 = c * 16 + kq * 4, tap = k0 / p.Cin;
+    const int kh = tap / p.KW;
+    tci[c] = k0 - tap * p.Cin;
+    tdy[c] = (tap < p.KH * p.KW && k0 < p.Kpad) ? kh - p.pad_t : -(1 << 20);
+    tdx[c] = tap - kh * p.KW - p.pad_l;
+  }
+  float4 bnext[KC];
+  auto load_b = [&](int tt) {
+    const int pix = tt * 16 + col;
+    const int b = pix / HWo, r = pix - b * HWo;
+    const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+    const float* xb = x + (size_t)b * p.H * p.W * p.xs;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int iy = oy * p.stride + tdy[c], ix = ox * p.stride + tdx[c];
+      const bool ok = pix < M && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      bnext[c] = load_f4_or_zero(xb + ((size_t)iy * p.W + ix) * p.xs + tci[c], x, ok);
+    }
+  };
+  if (t < tiles) load_b(t);
+  for (; t < tiles; t += tstride) {
+    float4 bc[KC];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) bc[c] = bnext[c];
+    if (t + tstride < tiles) load_b(t + tstride);
+    f32x4 acc[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const float4 a = *(const float4*)&sW[(j * 16 + col) * WPF + c * 16 + kq * 4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4_get(a, s4), f4_get(bc[c], s4), acc[j], 0, 0, 0);
+      }
+    }
+    const int pix = t * 16 + col;
+    if (pix >= M) continue;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int cb = n0 + j * 16 + kq * 4;
+      if (cb >= p.Cout) continue;
+      float v[4] = {acc[j][0] + bias[j].x, acc[j][1] + bias[j].y, acc[j][2] + bias[j].z, acc[j][3] + bias[j].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      if (p.res != nullptr) {
+        const float4 rv = *(const float4*)((const float*)p.res + (size_t)pix * p.rs + cb);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      }
+      const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)p.y + (size_t)pix * p.ys + cb) = o;
+      if (p.y2 != nullptr) {
+        const int b = pix / HWo;
+        const int r = pix - b * HWo;
+        const int oy = r / p.Wo, ox = r - (r / p.Wo) * p.Wo;
+        const int W2 = 2 * p.Wo;
+        float* y2 = (float*)p.y2;
+        const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+        *(float4*)(y2 + base * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + 1) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2 + 1) * p.y2s + cb) = o;
+      }
+    }
+  }
+}
+
+template <int NF, int KC>
+static void launch_stream_exact(const ConvParams& p, hipStream_t s) {
+  constexpr int BN = NF * 16;
+  const int ny = (p.Cout_pad + BN - 1) / BN;
+  const long tiles = ((long)p.B * p.Ho * p.Wo + 15) / 16;
+  const long gx = std::max(1L, std::min((tiles + 3) / 4, (long)std::max(1, 1024 / ny)));
+  hipLaunchKernelGGL((conv_f32_stream_kernel<NF, KC>), dim3((unsigned)gx, (unsigned)ny), dim3(STR_THREADS), 0, s, p);
+}
+
+template <int NF>
+static bool launch_stream_exact_k(const ConvParams& p, hipStream_t s) {
+  const int kc = p.Kpad / 16;  // chunk counts rounded up to an instantiated one (weights / taps past Kpad are zero)
+  if (kc <= 1) launch_stream_exact<NF, 1>(p, s);
+  else if (kc <= 2) launch_stream_exact<NF, 2>(p, s);
+  else if (kc <= 4) launch_stream_exact<NF, 4>(p, s);
+  else if (kc <= 6) launch_stream_exact<NF, 6>(p, s);
+  else if (kc <= 8) launch_stream_exact<NF, 8>(p, s);
+  else if (kc <= 10) launch_stream_exact<NF, 10>(p, s);
+  else if (kc <= 12) launch_stream_exact<NF, 12>(p, s);
+  else return false;
+  return true;
+}
+
+static bool f32_stream(const ConvParams& p, hipStream_t s) {
+  if (p.Cin % 4 != 0 || p.Kpad > 192 || p.Kpad % 16 != 0 || p.Kpad < p.KH * p.KW * p.Cin || p.xs % 4 != 0)
+    return false;
+  const int ncf = p.Cout_pad / 16;
+  const int nf = ncf <= 5 ? ncf : ncf % 4 == 0 ? 4 : ncf % 3 == 0 ? 3 : ncf % 5 == 0 ? 5 : ncf % 2 == 0 ? 2 : 1;
+  switch (nf) {
+    case 1: return launch_stream_exact_k<1>(p, s);
+    case 2: return launch_stream_exact_k<2>(p, s);
+    case 3: return launch_stream_exact_k<3>(p, s);
+    case 4: return launch_stream_exact_k<4>(p, s);
+    case 5: return launch_stream_exact_k<5>(p, s);
+    default: return false;
+  }
+}
+
 // impl kF32Stream (channel tile by Cout) / kF32StreamN2 (32-channel tiles): any conv with Cin % 8 == 0 and
 // Kpad <= 192 (1x1 pointwise layers, and the 3x3 / 2x2 convs over 16-channel space-to-depth stems, whose
 // taps are gathered per lane: 8 k of a slab never straddle two taps)
@@ -1208,6 +1353,10 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
     if (p.impl == kF32Fc) {
       if (!conv_fc_f32(p, s)) throw std::runtime_error("conv2d_f32: not an FC-eligible conv (1x1 map, Kpad 1280)");
+      return;
+    }
+    if (p.impl == kF32StreamExact) {
+      if (!f32_stream(p, s)) throw std::runtime_error("conv2d_f32: not a stream-eligible conv (Cin % 4, Kpad <= 192)");
       return;
     }
     if (p.impl == kF32Stream || p.impl == kF32StreamN2) {

@@ -71,6 +71,7 @@ constexpr int kF32X3HaloN2 = 103;  // ... with 32-channel tiles
 constexpr int kF32Stream = 104;    // weight-stationary streaming conv, triple-bf16 split (Cin % 8, Kpad <= 192)
 constexpr int kF32StreamN2 = 105;  // ... with 32-channel tiles
 constexpr int kF32Fc = 106;        // split-K FC over a 1x1 map (fc_splitk.hip), exact fp32
+constexpr int kF32StreamExact = 107;  // streaming small-K conv on exact fp32 MFMA (no split)
 bool conv_fc_f32(const ConvParams& p, hipStream_t s);
 void conv2d_f32(const ConvParams& p, hipStream_t s);
 

@@ -77,7 +77,8 @@ def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
         assert torch.equal(out2, up_ref)
 
 
-X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105, 106]  # x3 variants, split halo, stream, FC
+# x3 tile variants, split halo (auto/48/32), split stream (auto/32), FC, exact-fp32 stream — same fp32 bound
+X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105, 106, 107]
 
 
 @pytest.mark.parametrize(
