@@ -371,6 +371,7 @@ static void ir_set_attr() {
 void ir_wave_prepare();
 void ir_crop_prepare();
 void ir_crop_f32_prepare();
+void ir_f32_prepare();
 bool ir_block_crop(const IrParams& p, hipStream_t s);
 bool ir_block_wave(const IrParams& p, int tile, hipStream_t s);
 static bool g_ir_wave = [] {
@@ -383,6 +384,7 @@ void ir_prepare() {
   ir_wave_prepare();
   ir_crop_prepare();
   ir_crop_f32_prepare();
+  ir_f32_prepare();
 #define X(S, TH, TW, MP, E) ir_set_attr<S, TH, TW, MP, E>();
   ARENA_IR_CONFIGS(X)
 #undef X

@@ -34,6 +34,7 @@
 //     conflict-free at the cost of a 2-way conflict on the (6x rarer) epilogue
 //     writes; at stride 2 the conflict-free layout (48 floats) cost more in
 //     occupancy than it saved, so E keeps 36 floats there.
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -256,9 +257,10 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
   }
 }
 
-// LDS bytes of one workgroup (kept <= 64 KiB: no dynamic-LDS attribute, which must not be set during capture)
-static size_t irf_lds_bytes(int S, int inp_pad, int expand) {
-  const int TH = S == 1 ? 8 : 4, TW = 8;
+// LDS bytes of one workgroup (<= 64 KiB, or an instantiation whose dynamic-LDS limit ir_f32_prepare raised
+// before any graph capture)
+static size_t irf_lds_bytes(int S, int inp_pad, int expand, int TW = 8) {
+  const int TH = S == 1 ? 8 : 4;
   const int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   const size_t rows = (size_t)(PH * PW + 15) / 16 * 16;
   return sizeof(float) * (rows * irf_xp(inp_pad, expand) + (expand ? rows * irf_ep(S) : 0) +
@@ -267,7 +269,7 @@ static size_t irf_lds_bytes(int S, int inp_pad, int expand) {
 
 template <int S, int TH, int TW, int NTO, bool EXPAND, int KIN>
 static void irf_launch_k(const IrParams& p, hipStream_t s) {
-  const size_t lds = irf_lds_bytes(S, p.inp_pad, EXPAND);
+  const size_t lds = irf_lds_bytes(S, p.inp_pad, EXPAND, TW);
   const int tiles = ((p.Wo + TW - 1) / TW) * ((p.Ho + TH - 1) / TH);
   hipLaunchKernelGGL((ir_f32_kernel<S, TH, TW, NTO, EXPAND, KIN>), dim3((unsigned)(p.B * tiles)), dim3(256), lds, s,
                      p);
@@ -298,6 +300,32 @@ static bool irf_nto(const IrParams& p, hipStream_t s) {
   }
 }
 
+// Stride-1 tiles of 8 x 16 output pixels (default; ARENA_IRF_TW=8 restores 8 x 8): the 10 x 18 halo re-expands
+// 1.41x the output
+// instead of 1.56x for 8 x 8 tiles and each workgroup's fixed cost (staging latency, 3 barriers per hidden
+// chunk) is spread over twice the pixels, at 2 instead of 3 workgroups per CU (76 KB LDS with an expansion).
+// tools/bench_irc.py, 128 crops: 112x112 t=1 block 167 -> 152 us, 56x56 hid144 228 -> 216, 28x28 hid192 92 -> 76.
+static int irf_tw_env() {
+  static const int v = [] {
+    const char* e = std::getenv("ARENA_IRF_TW");
+    return e ? std::atoi(e) : 16;
+  }();
+  return v;
+}
+static bool irf_tw16(const IrParams& p) { return irf_tw_env() == 16 && p.Wo >= 16; }
+
+void ir_f32_prepare() {
+#define IRF_ATTR(NTO_, KIN_)                                                                                 \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, NTO_, true, KIN_>,               \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#define IRF_ATTR_K(NTO_) IRF_ATTR(NTO_, 1) IRF_ATTR(NTO_, 2) IRF_ATTR(NTO_, 3) IRF_ATTR(NTO_, 4)
+  IRF_ATTR_K(1) IRF_ATTR_K(2) IRF_ATTR_K(4) IRF_ATTR_K(6)
+#undef IRF_ATTR_K
+#undef IRF_ATTR
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, 1, false, 1>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+
 bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand) {
   const int nto = oup_pad / 16;
   return (stride == 1 || stride == 2) && inp_pad % 16 == 0 && inp_pad <= 64 && hid_pad % IRF_HC == 0 &&
@@ -316,7 +344,9 @@ void ir_block_f32(const IrParams& p, hipStream_t s) {
     throw std::runtime_error("ir_block_f32: output size mismatch");
   if (p.B <= 0) return;
   bool ok;
-  if (p.stride == 1)
+  if (p.stride == 1 && irf_tw16(p))
+    ok = p.expand ? irf_nto<1, 8, 16, true>(p, s) : irf_nto<1, 8, 16, false>(p, s);
+  else if (p.stride == 1)
     ok = p.expand ? irf_nto<1, 8, 8, true>(p, s) : irf_nto<1, 8, 8, false>(p, s);
   else
     ok = p.expand ? irf_nto<2, 4, 8, true>(p, s) : irf_nto<2, 4, 8, false>(p, s);
