@@ -110,6 +110,9 @@ struct IrParams {
   int B;
   const int* bdev;
   int x3w;                  // fp32: we / wp pre-split into bf16 [h|m|l] planes for ir_crop_f32.hip
+  int dwp;                  // fp32: x is the block's hidden tensor (expand ran separately): dw + project only
+  const void* rx;           // dwp: residual (the block input, output geometry), pixel stride rx_cs
+  int rx_cs;
 };
 void ir_block(const IrParams& p, hipStream_t s);
 // Exact-fp32 fused block (csrc/kernels/ir_f32.hip): fp32 views / weights; we [hid_pad][inp_pad],
@@ -120,6 +123,7 @@ bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, i
 // MFMA); ir_block_f32 dispatches blocks with split-plane weights (x3w, set by the planner) to it.
 bool ir_block_crop_f32(const IrParams& p, hipStream_t s);
 bool ir_block_crop_f32_supported(int H, int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
+bool ir_dwproj_f32_supported(int stride, int hid_pad, int oup_pad);  // IrParams.dwp blocks (ir_f32.hip)
 void ir_prepare();
 void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole-crop tile
 void set_ir_crop(bool v);

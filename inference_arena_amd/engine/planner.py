@@ -366,6 +366,30 @@ class ProgramBuilder:
                int(expand is not None), int(res), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind, x3w]
         self._emit(rec, src, dst)
 
+    def ir_dwproj(self, src: View, dst: View, dw, project, *, stride: int, res: View | None,
+                  kind: int = CROPS) -> None:
+        """fp32: depthwise 3x3 (+ReLU6) -> 1x1 project (+ ``res``) of an inverted residual whose expand ran as its
+        own conv; ``src`` is the hidden tensor (csrc/kernels/ir_f32.hip, IrParams.dwp).  The depthwise output
+        never leaves the kernel."""
+        if not self.f32:
+            raise ValueError("ir_dwproj is an fp32-program op")
+        if dst.C != project[0].shape[0] or src.C != dw[0].shape[0]:
+            raise ValueError("ir_dwproj: channel mismatch")
+        pk = pack_ir_weights(None, dw, project, src.C, k_align=32)
+        f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
+        offs = [0, self.weights.add(f32(torch.zeros(4))), self.weights.add(f32(pk["wd"])),
+                self.weights.add(f32(pk["bd"])), self.weights.add(f32(pk["wp"])), self.weights.add(f32(pk["bp"]))]
+        offs[0] = offs[1]  # no expand weights: a valid offset the kernel never reads
+        H, W = src.buf.H, src.buf.W
+        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        rec = [OP_IRBLOCK, src.bid, src.coff, src.cs, H, W, pk["inp"], pk["inp_pad"], pk["hid_pad"], pk["oup"],
+               pk["oup_pad"], stride, 0, int(res is not None), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind, 0, 1,
+               res.bid if res is not None else 0, res.coff if res is not None else 0, res.cs if res is not None else 0]
+        if res is not None:
+            self._emit(rec, src, dst, res)
+        else:
+            self._emit(rec, src, dst)
+
     def sppf(self, buf: Buffer, C: int, kind: int = IMAGES) -> None:
         self._emit([OP_SPPF, buf.id, 0, buf.C, buf.H, buf.W, C, kind], buf)
 
