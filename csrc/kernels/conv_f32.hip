@@ -798,17 +798,27 @@ static bool launch_halo_n(const ConvParams& p, hipStream_t s) {
 // and at ky = 2 the next chunk's halo) are issued into registers before the
 // current stage's 3 taps x MF x NF x 6 MFMAs run.  Cin need not be a multiple
 // of 32: the tail chunk's missing channels stage as zeros.
-constexpr int X3H_TH = 8, X3H_TW = 16, X3H_HR = X3H_TH + 2, X3H_HC = X3H_TW + 2, X3H_HPIX = X3H_HR * X3H_HC;
+// TH = 8 output rows per workgroup (4 waves) or 16 (8 waves, x3h16 variants): the stage's weights are
+// re-read from L2 by every workgroup, and at 8 x 16 output pixels per stage that stream (~25 KB per
+// 2.3k MFMA cycles) runs the L2 near its bandwidth; 16 x 16 tiles halve it per pixel (and the halo
+// overhead drops from 1.41x to 1.27x) at one workgroup of 8 waves per CU.
+constexpr int X3H_TW = 16, X3H_HC = X3H_TW + 2;
 constexpr int X3H_XP = 3 * 32 + 16;      // bf16 per halo pixel (224 B)
 constexpr int X3H_WP = 3 * 3 * 32 + 16;  // bf16 per weight row of one ky (3 taps x 3 planes x 32 k; 608 B)
-constexpr int X3H_XV = (X3H_HPIX * 8 + 255) / 256;  // halo float4 per thread
+__host__ __device__ constexpr int x3h_lds_bytes(int NF, int TH) {
+  return ((TH + 2) * X3H_HC * X3H_XP + NF * 16 * X3H_WP) * 2;
+}
 
-template <int NF>
-__global__ __launch_bounds__(256) void conv_x3_halo_kernel(const ConvParams p) {
+template <int NF, int X3H_TH = 8>
+__global__ __launch_bounds__(X3H_TH * 32) void conv_x3_halo_kernel(const ConvParams p) {
+  constexpr int NT = X3H_TH * 32, NW = X3H_TH / 2;     // threads, waves (wave w: rows w and w + NW)
+  constexpr int X3H_HR = X3H_TH + 2, X3H_HPIX = X3H_HR * X3H_HC;
+  constexpr int X3H_XV = (X3H_HPIX * 8 + NT - 1) / NT;  // halo float4 per thread
   constexpr int BN = NF * 16, MF = 2;
-  constexpr int WV = (BN * 3 * 8 + 255) / 256;  // weight float4 per thread per ky stage
-  __shared__ __attribute__((aligned(16))) bf16 sX[X3H_HPIX * X3H_XP];
-  __shared__ __attribute__((aligned(16))) bf16 sW[BN * X3H_WP];
+  constexpr int WV = (BN * 3 * 8 + NT - 1) / NT;  // weight float4 per thread per ky stage
+  extern __shared__ __attribute__((aligned(16))) bf16 x3h_lds[];
+  bf16* sX = x3h_lds;                              // [HPIX][X3H_XP]
+  bf16* sW = x3h_lds + X3H_HPIX * X3H_XP;          // [BN][X3H_WP]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, kq = lane >> 4;
@@ -830,7 +840,7 @@ __global__ __launch_bounds__(256) void conv_x3_halo_kernel(const ConvParams p) {
   auto load_x = [&](int c0) {
 #pragma unroll
     for (int j = 0; j < X3H_XV; ++j) {
-      const int i = tid + 256 * j;
+      const int i = tid + NT * j;
       const int px = i >> 3, g = i & 7;
       const int hy = px / X3H_HC, hx = px - hy * X3H_HC;
       const int iy = iy0 + hy, ix = ix0 + hx, c = c0 + 4 * g;
@@ -841,7 +851,7 @@ __global__ __launch_bounds__(256) void conv_x3_halo_kernel(const ConvParams p) {
   auto load_w = [&](int c0, int ky) {
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
-      const int i = tid + 256 * j;  // (row, kx, g)
+      const int i = tid + NT * j;  // (row, kx, g)
       const int row = i / 24, e = i - row * 24;
       const int kx = e >> 3, g = e & 7;
       const int n = n0 + row, c = c0 + 4 * g;
@@ -852,14 +862,14 @@ __global__ __launch_bounds__(256) void conv_x3_halo_kernel(const ConvParams p) {
   auto store_x = [&]() {
 #pragma unroll
     for (int j = 0; j < X3H_XV; ++j) {
-      const int i = tid + 256 * j;
+      const int i = tid + NT * j;
       if (i < X3H_HPIX * 8) store_split4(&sX[(i >> 3) * X3H_XP], 4 * (i & 7), rx[j]);
     }
   };
   auto store_w = [&]() {
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
-      const int i = tid + 256 * j;
+      const int i = tid + NT * j;
       if (i < BN * 24) {
         const int row = i / 24, e = i - row * 24;
         store_split4(&sW[row * X3H_WP + (e >> 3) * 96], 4 * (e & 7), rw[j]);
@@ -898,7 +908,7 @@ __global__ __launch_bounds__(256) void conv_x3_halo_kernel(const ConvParams p) {
       }
 #pragma unroll
       for (int f = 0; f < MF; ++f) {
-        const int oy = wave + 4 * f;
+        const int oy = wave + NW * f;
         const bf16* r = &sX[((oy + ky) * X3H_HC + col + kx) * X3H_XP + 8 * kq];
         const bf16x8 bh = *(const bf16x8*)r;
         const bf16x8 bm = *(const bf16x8*)(r + 32);
@@ -926,7 +936,7 @@ __global__ __launch_bounds__(256) void conv_x3_halo_kernel(const ConvParams p) {
     const float4 bias = *(const float4*)(p.bias + cb);
 #pragma unroll
     for (int f = 0; f < MF; ++f) {
-      const int oy = oy0 + wave + 4 * f, ox = ox0 + col;
+      const int oy = oy0 + wave + NW * f, ox = ox0 + col;
       if (oy >= p.Ho || ox >= p.Wo) continue;
       const size_t pix = (size_t)b * HWo + (size_t)oy * p.Wo + ox;
       float v[4] = {acc[f][j][0] + bias.x, acc[f][j][1] + bias.y, acc[f][j][2] + bias.z, acc[f][j][3] + bias.w};
@@ -951,20 +961,35 @@ __global__ __launch_bounds__(256) void conv_x3_halo_kernel(const ConvParams p) {
   }
 }
 
-template <int NF>
+template <int NF, int TH = 8>
 static void launch_x3_halo(const ConvParams& p, hipStream_t s) {
   constexpr int BN = NF * 16;
-  const int tiles = ((p.Wo + X3H_TW - 1) / X3H_TW) * ((p.Ho + X3H_TH - 1) / X3H_TH);
+  const int tiles = ((p.Wo + X3H_TW - 1) / X3H_TW) * ((p.Ho + TH - 1) / TH);
   dim3 grid((unsigned)(p.B * tiles), (unsigned)((p.Cout_pad + BN - 1) / BN));
-  hipLaunchKernelGGL((conv_x3_halo_kernel<NF>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((conv_x3_halo_kernel<NF, TH>), grid, dim3(TH * 32), x3h_lds_bytes(NF, TH), s, p);
+}
+
+void x3_halo_prepare() {
+#define X3H_ATTR(NF_, TH_)                                                                            \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)conv_x3_halo_kernel<NF_, TH_>,                       \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  X3H_ATTR(1, 8) X3H_ATTR(2, 8) X3H_ATTR(3, 8) X3H_ATTR(4, 8) X3H_ATTR(5, 8)
+  X3H_ATTR(2, 16) X3H_ATTR(3, 16) X3H_ATTR(4, 16)
+#undef X3H_ATTR
 }
 
 // impl kF32X3Halo: 3x3 stride-1 convs with Kpad == 9 * Cin (tap-major K) and Cin % 4 == 0.  nf > 0 forces the
 // channel tile (impl kF32X3HaloN3 / N2: BN 48 / 32): the 80-channel detect-head convs at NF = 5 need 89 KB of
 // LDS (one workgroup, one wave per SIMD); two 48-channel tiles fit twice per CU at 17 % padded channels.
-static bool x3_halo(const ConvParams& p, hipStream_t s, int nf = 0) {
+static bool x3_halo(const ConvParams& p, hipStream_t s, int nf = 0, int th = 8) {
   if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.Kpad != 9 * p.Cin || p.Cin % 4 != 0) return false;
   const int ncf = p.Cout_pad / 16;
+  if (th == 16) {  // 16-row tiles (8 waves): 48 / 64-channel tiles, or 32 for narrow layers
+    if (nf == 3 || (nf == 0 && (ncf == 3 || ncf == 5 || ncf == 9))) launch_x3_halo<3, 16>(p, s);
+    else if (nf == 2 || (nf == 0 && ncf <= 2)) launch_x3_halo<2, 16>(p, s);
+    else launch_x3_halo<4, 16>(p, s);
+    return true;
+  }
   if (nf == 3) {
     launch_x3_halo<3>(p, s);
     return true;
@@ -1364,9 +1389,11 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
         throw std::runtime_error("conv2d_f32: not a stream-eligible conv (Cin % 8, Kpad <= 192)");
       return;
     }
-    if (p.impl == kF32X3Halo || p.impl == kF32X3HaloN3 || p.impl == kF32X3HaloN2) {
-      const int nf = p.impl == kF32X3HaloN3 ? 3 : p.impl == kF32X3HaloN2 ? 2 : 0;
-      if (!x3_halo(p, s, nf)) throw std::runtime_error("conv2d_f32: not an x3-halo-eligible conv");
+    if (p.impl == kF32X3Halo || p.impl == kF32X3HaloN3 || p.impl == kF32X3HaloN2 || p.impl == kF32X3Halo16 ||
+        p.impl == kF32X3Halo16N3) {
+      const int nf = (p.impl == kF32X3HaloN3 || p.impl == kF32X3Halo16N3) ? 3 : p.impl == kF32X3HaloN2 ? 2 : 0;
+      const int th = (p.impl == kF32X3Halo16 || p.impl == kF32X3Halo16N3) ? 16 : 8;
+      if (!x3_halo(p, s, nf, th)) throw std::runtime_error("conv2d_f32: not an x3-halo-eligible conv");
       return;
     }
     if (p.impl == kF32Halo) {

@@ -307,6 +307,7 @@ void prepare_kernels() {
                                       160 * 1024));
   ir_prepare();
   head_pool_f32_prepare();
+  x3_halo_prepare();
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)sppf_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
   done = true;
