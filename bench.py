@@ -31,8 +31,8 @@ without WORLD_SIZE and N > 1 it launches ``torch.distributed.run`` itself as a c
 process (before any GPU call) and exits with its code.
 
 Secondary keys: ``engine_req_s`` (device pipeline fed pre-decoded images, same dtype),
-``bf16`` (the same end-to-end measurement on the bf16 kernels, rank 0's share only when
-``--secondary-bf16``), bs=1 latency (one client).
+``bf16`` (the same end-to-end measurement on the bf16 kernels; on by default,
+``--no-secondary-bf16`` skips it), bs=1 latency (one client).
 """
 from __future__ import annotations
 
@@ -284,7 +284,8 @@ def main(argv=None) -> int:
     ap.add_argument("--images", type=int, default=100, help="curated workload size")
     ap.add_argument("--bs1-requests", type=int, default=50)
     ap.add_argument("--engine-batches", type=int, default=40, help="batches for the engine-only secondary key")
-    ap.add_argument("--secondary-bf16", action="store_true", help="also measure the bf16 kernels end to end")
+    ap.add_argument("--secondary-bf16", action=argparse.BooleanOptionalAction, default=True,
+                    help="also measure the bf16 kernels (secondary key 'bf16': e2e, P50/P99, engine req/s)")
     ap.add_argument("--crop-cap", type=int, default=None)
     a = ap.parse_args(argv)
     raw_argv = list(sys.argv[1:] if argv is None else argv)
