@@ -148,6 +148,12 @@ def get_gpu_config() -> dict[str, Any]:
     return dflt
 
 
+def get_cost_config() -> dict:
+    """RQ2 cost model prices (``cost`` section; defaults when absent)."""
+    c = get_config().get("cost") or {}
+    return {"gpu_hour_usd": float(c.get("gpu_hour_usd", 0.0)), "vcpu_hour_usd": float(c.get("vcpu_hour_usd", 0.0))}
+
+
 def validate_config() -> list[str]:
     """Schema check; returns a list of human-readable problems (empty = valid)."""
     try:
@@ -182,6 +188,12 @@ def validate_config() -> list[str]:
                 errors.append(f"Hypothesis {hid} missing required field: {field}")
         if "testable_prediction" not in h and "prediction" not in h:
             errors.append(f"Hypothesis {hid} missing testable_prediction or prediction")
+    cost = cfg.get("cost")
+    if cost is not None:
+        for k in ("gpu_hour_usd", "vcpu_hour_usd"):
+            v = cost.get(k)
+            if not isinstance(v, (int, float)) or v < 0:
+                errors.append(f"cost.{k} must be a non-negative number")
     gpu = cfg.get("gpu")
     if gpu is not None:
         buckets = gpu.get("batch_buckets", [])

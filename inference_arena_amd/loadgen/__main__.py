@@ -27,6 +27,9 @@ def main(argv=None) -> int:
     ap.add_argument("--images", type=int, default=100, help="curated workload images to cycle through")
     ap.add_argument("--out", default="results/load")
     ap.add_argument("--evaluate", nargs="*", default=None, help="sweep CSVs to evaluate hypotheses over")
+    ap.add_argument("--sample-ports", default="", help="comma list: sample CPU / memory of the processes "
+                    "listening on these ports (and their children) during each level (RQ2)")
+    ap.add_argument("--sample-pids", default="", help="comma list of server PIDs to sample (RQ2)")
     a = ap.parse_args(argv)
     if a.evaluate is not None:
         import csv
@@ -43,7 +46,12 @@ def main(argv=None) -> int:
     images = [encode_jpeg(im, quality=95) for im in workload_images(a.images)]
     base = LoadConfig(url=a.url, warmup_s=a.warmup, measure_s=a.measure, cooldown_s=a.cooldown, procs=a.procs)
     users = [int(u) for u in a.users.split(",") if u]
-    run_sweep(base, users, a.runs, images, Path(a.out), a.arch)
+    pids = [int(p) for p in a.sample_pids.split(",") if p]
+    if a.sample_ports:
+        from .resources import pids_listening_on
+
+        pids += pids_listening_on([int(p) for p in a.sample_ports.split(",") if p])
+    run_sweep(base, users, a.runs, images, Path(a.out), a.arch, sample_pids=sorted(set(pids)) or None)
     return 0
 
 

@@ -1,0 +1,126 @@
+"""Resource sampling during a load level (experiment.yaml RQ2: ``cpu_utilization_percent``,
+``memory_usage_mb``; reference: /root/reference/experiment.yaml:47-53 — the reference collects these from
+cAdvisor through Prometheus, infrastructure/prometheus/prometheus.yml:17-20, and has no in-process sampler).
+
+``ResourceSampler`` follows the arm's server processes — given as PIDs, or discovered as the processes listening
+on the arm's ports (``gpu.ports`` in experiment.yaml) — and all their children (decode workers, replicas), and
+samples every ``interval`` seconds: summed CPU % (100 = one core), summed resident memory, and, when the MI355X
+telemetry reader (metrics/gpu.py) finds a device, GPU busy % and VRAM.
+"""
+from __future__ import annotations
+
+import threading
+import time
+
+import numpy as np
+
+
+def pids_listening_on(ports: list[int]) -> list[int]:
+    """PIDs of the processes holding a listening TCP socket on any of ``ports`` (best effort)."""
+    import psutil
+
+    out = set()
+    try:
+        conns = psutil.net_connections(kind="tcp")
+    except (psutil.AccessDenied, PermissionError):
+        conns = []
+    for c in conns:
+        if c.status == psutil.CONN_LISTEN and c.laddr and c.laddr.port in ports and c.pid:
+            out.add(c.pid)
+    return sorted(out)
+
+
+class ResourceSampler:
+    def __init__(self, pids: list[int], interval: float = 1.0, gpu: bool = True) -> None:
+        import psutil
+
+        self.interval = interval
+        self.roots = [psutil.Process(p) for p in pids if psutil.pid_exists(p)]
+        self.samples: list[tuple[float, float, float, float | None, float | None]] = []
+        self._stop = threading.Event()
+        self._thread: threading.Thread | None = None
+        self._gpu = None
+        if gpu:
+            try:
+                from ..metrics.gpu import GpuTelemetry
+
+                t = GpuTelemetry()
+                # amdsmi / amd-smi only: the torch fallback would initialise a GPU context in the load generator
+                self._gpu = t if t.source in ("amdsmi", "cli") else None
+            except Exception:  # noqa: BLE001 - no device / reader: CPU-side metrics only
+                self._gpu = None
+
+    def _procs(self):
+        import psutil
+
+        seen = {}
+        for r in self.roots:
+            try:
+                for p in [r] + r.children(recursive=True):
+                    seen[p.pid] = p
+            except psutil.NoSuchProcess:
+                continue
+        return list(seen.values())
+
+    def _sample(self, procs) -> None:
+        import psutil
+
+        cpu = mem = 0.0
+        for p in procs:
+            try:
+                cpu += p.cpu_percent(None)
+                mem += p.memory_info().rss / 2 ** 20
+            except psutil.NoSuchProcess:
+                continue
+        busy = vram = None
+        if self._gpu is not None:
+            try:
+                rows = self._gpu.sample()
+                util = [r["util"] for r in rows if "util" in r]
+                mems = [r["mem"] for r in rows if "mem" in r]
+                busy = float(np.mean(util)) if util else None
+                vram = float(np.sum(mems)) / 2 ** 20 if mems else None
+            except Exception:  # noqa: BLE001
+                pass
+        self.samples.append((time.time(), cpu, mem, busy, vram))
+
+    def _run(self) -> None:
+        procs = self._procs()
+        for p in procs:  # first cpu_percent call primes the per-process counters
+            try:
+                p.cpu_percent(None)
+            except Exception:  # noqa: BLE001
+                pass
+        while not self._stop.wait(self.interval):
+            procs = self._procs()
+            self._sample(procs)
+
+    def start(self) -> "ResourceSampler":
+        self._thread = threading.Thread(target=self._run, daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self) -> dict:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5 * self.interval + 1)
+        return self.summary()
+
+    def summary(self) -> dict:
+        if not self.samples:
+            return {"cpu_utilization_percent": float("nan"), "memory_usage_mb": float("nan"), "resource_samples": 0}
+        a = np.asarray([s[1:3] for s in self.samples], dtype=np.float64)
+        out = {
+            "cpu_utilization_percent": float(a[:, 0].mean()),   # 100 = one core busy
+            "cpu_utilization_percent_max": float(a[:, 0].max()),
+            "memory_usage_mb": float(a[:, 1].mean()),
+            "memory_usage_mb_max": float(a[:, 1].max()),
+            "resource_samples": len(self.samples),
+        }
+        busy = [s[3] for s in self.samples if s[3] is not None]
+        vram = [s[4] for s in self.samples if s[4] is not None]
+        if busy:
+            out["gpu_busy_percent"] = float(np.mean(busy))
+        if vram:
+            out["gpu_vram_mb"] = float(np.mean(vram))
+        return out

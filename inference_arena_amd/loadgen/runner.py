@@ -154,13 +154,22 @@ def write_level(out_dir: Path, tag: str, res: PhaseResult, summary: dict) -> Non
 
 
 def run_sweep(base: LoadConfig, user_levels: list[int], runs: int, images: list[bytes], out_dir: Path,
-              arch: str, log=print) -> list[dict]:
+              arch: str, log=print, sample_pids: list[int] | None = None) -> list[dict]:
+    """``sample_pids``: server processes (children included) whose CPU % / memory (and GPU busy / VRAM) are
+    sampled during each level (loadgen/resources.py; experiment.yaml RQ2 metrics)."""
     rows = []
     for users in user_levels:
         for run in range(1, runs + 1):
             cfg = LoadConfig(**{**asdict(base), "users": users, "seed": base.seed + run})
+            sampler = None
+            if sample_pids:
+                from .resources import ResourceSampler
+
+                sampler = ResourceSampler(sample_pids).start()
             res = run_level(cfg, images)
             s = summarize(res, cfg)
+            if sampler is not None:
+                s.update(sampler.stop())
             s.update({"architecture": arch, "run": run})
             write_level(out_dir, f"{arch}_u{users}_r{run}", res, s)
             rows.append(s)

@@ -50,11 +50,19 @@ def main(argv=None) -> int:
                 continue
             base = LoadConfig(url=f"http://127.0.0.1:{ports[arch]}/predict", warmup_s=a.warmup, measure_s=a.measure,
                               cooldown_s=a.cooldown, procs=a.procs)
+            # RQ2: CPU % / memory of the arm's processes (and children: replicas, decode workers) per level
+            pids = [p.pid for p in procs if getattr(p, "pid", None)]
             rows += run_sweep(base, [int(u) for u in a.users.split(",")], a.runs, images, out, arch,
-                              log=lambda *x: print(*x, flush=True))
+                              log=lambda *x: print(*x, flush=True), sample_pids=pids or None)
         finally:
             stop(procs)
     (out / "hypotheses.json").write_text(json.dumps(evaluate(rows), indent=2, default=str) + "\n")
+    if rows:  # RQ2 cost per 1000 requests + RQ3 complexity (inference_arena_amd/analysis)
+        from inference_arena_amd.analysis import complexity_report, enrich_sweep_rows
+        from inference_arena_amd.config import get_cost_config
+
+        rq = {"rows": enrich_sweep_rows(rows, gpus=a.gpus, cost=get_cost_config()), "rq3": complexity_report()}
+        (out / "rq2_rq3.json").write_text(json.dumps(rq, indent=2, default=str) + "\n")
     print(json.dumps(evaluate(rows), default=str))
     return 0
 
