@@ -39,6 +39,7 @@ class ResourceSampler:
         self.samples: list[tuple[float, float, float, float | None, float | None]] = []
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
+        self._cache: dict = {}
         self._gpu = None
         if gpu:
             try:
@@ -51,16 +52,25 @@ class ResourceSampler:
                 self._gpu = None
 
     def _procs(self):
+        """The process trees, as the same psutil.Process objects from sample to sample: cpu_percent(None) measures
+        since the previous call on that object, so a fresh object per sample would always read 0."""
         import psutil
 
-        seen = {}
+        live = {}
         for r in self.roots:
             try:
                 for p in [r] + r.children(recursive=True):
-                    seen[p.pid] = p
+                    live[p.pid] = self._cache.get(p.pid, p)
             except psutil.NoSuchProcess:
                 continue
-        return list(seen.values())
+        for pid, p in live.items():
+            if pid not in self._cache:
+                self._cache[pid] = p
+                try:
+                    p.cpu_percent(None)  # prime: its first real reading comes at the next sample
+                except psutil.NoSuchProcess:
+                    pass
+        return list(live.values())
 
     def _sample(self, procs) -> None:
         import psutil
@@ -85,12 +95,7 @@ class ResourceSampler:
         self.samples.append((time.time(), cpu, mem, busy, vram))
 
     def _run(self) -> None:
-        procs = self._procs()
-        for p in procs:  # first cpu_percent call primes the per-process counters
-            try:
-                p.cpu_percent(None)
-            except Exception:  # noqa: BLE001
-                pass
+        self._procs()  # prime every process's cpu counter
         while not self._stop.wait(self.interval):
             procs = self._procs()
             self._sample(procs)

@@ -36,15 +36,24 @@ def test_complexity_report_covers_the_three_arms():
 
 
 def test_resource_sampler_follows_a_process_tree():
+    """A busy child process (not the root) shows up in the CPU reading: children are followed and their CPU
+    counters kept from sample to sample."""
+    import subprocess
+    import sys
+
     from inference_arena_amd.loadgen.resources import ResourceSampler
 
-    s = ResourceSampler([os.getpid()], interval=0.05, gpu=False).start()
-    t = time.time()
-    while time.time() - t < 0.4:
-        sum(i * i for i in range(20000))  # some CPU
-    out = s.stop()
-    assert out["resource_samples"] >= 3
-    assert out["memory_usage_mb"] > 10 and out["cpu_utilization_percent"] >= 0.0
+    child = subprocess.Popen([sys.executable, "-c", "import time\nt=time.time()\nwhile time.time()-t<3: pass"])
+    try:
+        s = ResourceSampler([os.getpid()], interval=0.2, gpu=False).start()
+        time.sleep(1.5)
+        out = s.stop()
+    finally:
+        child.kill()
+        child.wait()
+    assert out["resource_samples"] >= 4
+    assert out["memory_usage_mb"] > 10
+    assert out["cpu_utilization_percent_max"] > 50.0, out  # the spinning child: ~100 % of one core
 
 
 def test_cost_config_validates():
