@@ -978,6 +978,170 @@ void x3_halo_prepare() {
 #undef X3H_ATTR
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 stride-1 conv over 16 input channels (the YOLO space-to-depth stem's 320x320 and 160x160 layers) on the
+// bf16 matrix cores with the triple-bf16 split.  The generic halo kernel runs a 16-channel input as a 32-deep
+// chunk half zero (9 slabs of 32 per output tile); here one kernel row's three taps x 16 channels (48 k, laid
+// out contiguously in the [Cout][ky][kx][c] weight row) fill 2 slabs: kx 0-1 in the first, kx 2 plus zeros in
+// the second (6 slabs, 1.5x fewer MFMAs), and the whole input halo (10 x 18 pixels x 16 channels x 3 planes =
+// 17 KB) and all weights (BN x 3 rows x 416 B) are staged once: no K loop, one barrier.  Lane (col, kq) of
+// slab s reads channels c0..c0+7 of tap kx = (32 s + 8 kq) / 16 at pixel column col + kx (kx = 3 is the zero
+// half: it re-reads a valid pixel, its weights are zero).  Pitches (LDS bank model of MI355X_MICROARCH.md
+// §LDS): 96 B per halo pixel and 3 x 416 B per weight row are conflict-free for these ds_read_b128 patterns.
+constexpr int H16_TH = 8, H16_TW = 16, H16_HR = H16_TH + 2, H16_HC = H16_TW + 2, H16_HPIX = H16_HR * H16_HC;
+constexpr int H16_XP = 48;    // bf16 per halo pixel: [h|m|l][16]
+constexpr int H16_WPK = 208;  // bf16 per (row, ky): [2 slabs][h|m|l][32] = 192 + 16 pad (416 B)
+
+template <int NF>
+__global__ __launch_bounds__(256) void conv_x3_h16_kernel(const ConvParams p) {
+  constexpr int BN = NF * 16, MF = 2;
+  __shared__ __attribute__((aligned(16))) bf16 sX[H16_HPIX * H16_XP];
+  __shared__ __attribute__((aligned(16))) bf16 sW[BN * 3 * H16_WPK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int tiles_x = (p.Wo + H16_TW - 1) / H16_TW, tiles_y = (p.Ho + H16_TH - 1) / H16_TH;
+  const int tiles = tiles_x * tiles_y;
+  const int bx = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = bx / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int t = bx - b * tiles;
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int oy0 = ty * H16_TH, ox0 = tx * H16_TW;
+  const int iy0 = oy0 - p.pad_t, ix0 = ox0 - p.pad_l;
+  const int n0 = blockIdx.y * BN;
+  const float* __restrict__ x = (const float*)p.x + (size_t)b * p.H * p.W * p.xs;
+  const float* __restrict__ w = (const float*)p.w;
+
+  // input halo: 4 float4 (16 channels) per pixel, split into three planes
+  for (int i = tid; i < H16_HPIX * 4; i += 256) {
+    const int px = i >> 2, g = i & 3;
+    const int hy = px / H16_HC, hx = px - hy * H16_HC;
+    const int iy = iy0 + hy, ix = ix0 + hx;
+    const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+    const float4 v = load_f4_or_zero(x + ((size_t)iy * p.W + ix) * p.xs + 4 * g, x, ok);
+    bf16x4 h, m, l;
+    bf16 th, tm, tl;
+    split3(v.x, th, tm, tl); h[0] = th; m[0] = tm; l[0] = tl;
+    split3(v.y, th, tm, tl); h[1] = th; m[1] = tm; l[1] = tl;
+    split3(v.z, th, tm, tl); h[2] = th; m[2] = tm; l[2] = tl;
+    split3(v.w, th, tm, tl); h[3] = th; m[3] = tm; l[3] = tl;
+    bf16* d = &sX[px * H16_XP + 4 * g];
+    *(bf16x4*)d = h;
+    *(bf16x4*)(d + 16) = m;
+    *(bf16x4*)(d + 32) = l;
+  }
+  // weights: row n, kernel row ky -> 64 k (48 real: kx 0..2 x 16 channels) in two 32-deep slabs
+  for (int i = tid; i < BN * 3 * 16; i += 256) {
+    const int row = i / 48, e = i - row * 48;
+    const int ky = e >> 4, q = e & 15;  // q: float4 index within the 64-k row (12..15 are the zero half)
+    const int n = n0 + row, k = ky * 48 + 4 * q;
+    const bool ok = n < p.Cout_pad && q < 12;
+    const float4 v = load_f4_or_zero(w + (size_t)n * p.Kpad + k, w, ok);
+    bf16x4 h, m, l;
+    bf16 th, tm, tl;
+    split3(v.x, th, tm, tl); h[0] = th; m[0] = tm; l[0] = tl;
+    split3(v.y, th, tm, tl); h[1] = th; m[1] = tm; l[1] = tl;
+    split3(v.z, th, tm, tl); h[2] = th; m[2] = tm; l[2] = tl;
+    split3(v.w, th, tm, tl); h[3] = th; m[3] = tm; l[3] = tl;
+    const int slab = q >> 3, kk = 4 * (q & 7);
+    bf16* d = &sW[(row * 3 + ky) * H16_WPK + slab * 96 + kk];
+    *(bf16x4*)d = h;
+    *(bf16x4*)(d + 32) = m;
+    *(bf16x4*)(d + 64) = l;
+  }
+  __syncthreads();
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int kabs = sl * 32 + kq * 8;
+      const int kx = kabs >> 4 < 3 ? kabs >> 4 : 2, c0 = kabs & 15;
+      bf16x8 ah[NF], am[NF], al[NF];
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const bf16* r = &sW[((j * 16 + col) * 3 + ky) * H16_WPK + sl * 96 + 8 * kq];
+        ah[j] = *(const bf16x8*)r;
+        am[j] = *(const bf16x8*)(r + 32);
+        al[j] = *(const bf16x8*)(r + 64);
+      }
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        const int oy = wave + 4 * f;
+        const bf16* r = &sX[((oy + ky) * H16_HC + col + kx) * H16_XP + c0];
+        const bf16x8 bh = *(const bf16x8*)r, bm = *(const bf16x8*)(r + 16), bl = *(const bf16x8*)(r + 32);
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+          f32x4 c = acc[f][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[j], bm, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[j], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[j], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bm, c, 0, 0, 0);
+          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bh, c, 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  const int HWo = p.Ho * p.Wo;
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int cb = n0 + j * 16 + kq * 4;
+    if (cb >= p.Cout) continue;
+    const float4 bias = *(const float4*)(p.bias + cb);
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int oy = oy0 + wave + 4 * f, ox = ox0 + col;
+      if (oy >= p.Ho || ox >= p.Wo) continue;
+      const size_t pix = (size_t)b * HWo + (size_t)oy * p.Wo + ox;
+      float v[4] = {acc[f][j][0] + bias.x, acc[f][j][1] + bias.y, acc[f][j][2] + bias.z, acc[f][j][3] + bias.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+      if (p.res != nullptr) {
+        const float4 rv = *(const float4*)((const float*)p.res + pix * p.rs + cb);
+        v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+      }
+      const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)((float*)p.y + pix * p.ys + cb) = o;
+      if (p.y2 != nullptr) {
+        const int W2 = 2 * p.Wo;
+        float* y2 = (float*)p.y2;
+        const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+        *(float4*)(y2 + base * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + 1) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2) * p.y2s + cb) = o;
+        *(float4*)(y2 + (base + W2 + 1) * p.y2s + cb) = o;
+      }
+    }
+  }
+}
+
+template <int NF>
+static void launch_x3_h16(const ConvParams& p, hipStream_t s) {
+  constexpr int BN = NF * 16;
+  const int tiles = ((p.Wo + H16_TW - 1) / H16_TW) * ((p.Ho + H16_TH - 1) / H16_TH);
+  dim3 grid((unsigned)(p.B * tiles), (unsigned)((p.Cout_pad + BN - 1) / BN));
+  hipLaunchKernelGGL((conv_x3_h16_kernel<NF>), grid, dim3(256), 0, s, p);
+}
+
+// impl kF32X3H16: 3x3 stride-1 pad-1 convs over exactly 16 input channels (Kpad 144)
+static bool x3_h16(const ConvParams& p, hipStream_t s) {
+  if (p.KH != 3 || p.KW != 3 || p.stride != 1 || p.Cin != 16 || p.Kpad != 144 || p.pad_t != 1 || p.pad_l != 1 ||
+      p.xs % 4 != 0)
+    return false;
+  const int ncf = p.Cout_pad / 16;
+  if (ncf == 1) launch_x3_h16<1>(p, s);
+  else if (ncf % 2 == 0) launch_x3_h16<2>(p, s);
+  else launch_x3_h16<1>(p, s);
+  return true;
+}
+
 // impl kF32X3Halo: 3x3 stride-1 convs with Kpad == 9 * Cin (tap-major K) and Cin % 4 == 0.  nf > 0 forces the
 // channel tile (impl kF32X3HaloN3 / N2: BN 48 / 32): the 80-channel detect-head convs at NF = 5 need 89 KB of
 // LDS (one workgroup, one wave per SIMD); two 48-channel tiles fit twice per CU at 17 % padded channels.
@@ -1376,6 +1540,10 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
   const int ncf = p.Cout_pad / 16;
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
+    if (p.impl == kF32X3H16) {
+      if (!x3_h16(p, s)) throw std::runtime_error("conv2d_f32: not an x3-h16-eligible conv (3x3 s1 over 16 channels)");
+      return;
+    }
     if (p.impl == kF32Fc) {
       if (!conv_fc_f32(p, s)) throw std::runtime_error("conv2d_f32: not an FC-eligible conv (1x1 map, Kpad 1280)");
       return;

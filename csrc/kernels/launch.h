@@ -74,6 +74,7 @@ constexpr int kF32Fc = 106;        // split-K FC over a 1x1 map (fc_splitk.hip),
 constexpr int kF32StreamExact = 107;  // streaming small-K conv on exact fp32 MFMA (no split)
 constexpr int kF32X3Halo16 = 108;    // x3 halo tiles of 16 x 16 output pixels (8 waves)
 constexpr int kF32X3Halo16N3 = 109;  // ... with 48-channel tiles
+constexpr int kF32X3H16 = 110;       // x3 3x3 stride-1 conv over exactly 16 input channels (s2d stems)
 void x3_halo_prepare();
 bool conv_fc_f32(const ConvParams& p, hipStream_t s);
 void conv2d_f32(const ConvParams& p, hipStream_t s);

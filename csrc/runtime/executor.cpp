@@ -259,7 +259,8 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
       const bool ok = f32 ? (v >= 0 && v <= 2) || (v >= 10 && v < 10 + kF32Variants) ||
                                 (v >= kF32X3 && v < kF32X3 + kF32X3Variants) || v == kF32Halo || v == kF32X3Halo ||
                                 v == kF32X3HaloN3 || v == kF32X3HaloN2 || v == kF32Stream || v == kF32StreamN2 ||
-                                v == kF32Fc || v == kF32StreamExact || v == kF32X3Halo16 || v == kF32X3Halo16N3
+                                v == kF32Fc || v == kF32StreamExact || v == kF32X3Halo16 || v == kF32X3Halo16N3 ||
+                                v == kF32X3H16
                           : v >= 0 && v <= 3;
       if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
       bk.impl[i] = (int8_t)v;
@@ -303,7 +304,7 @@ void Executor::autotune(Bucket& bk) {
                                        23,     24,     kF32Halo, kF32X3, kF32X3 + 1, kF32X3 + 4, kF32X3 + 5,
                                        kF32X3 + 6, kF32X3 + 7, kF32X3 + 8, kF32X3Halo, kF32X3HaloN3,
                                        kF32X3HaloN2, kF32Stream, kF32StreamN2, kF32Fc, kF32StreamExact,
-                                       kF32X3Halo16, kF32X3Halo16N3};
+                                       kF32X3Halo16, kF32X3Halo16N3, kF32X3H16};
   static const int kBf16Candidates[] = {1, 2, 3};
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;

@@ -78,7 +78,7 @@ def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
 
 
 # x3 tile variants, split halo (auto/48/32), split stream (auto/32), FC, exact-fp32 stream — same fp32 bound
-X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105, 106, 107, 108, 109]
+X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105, 106, 107, 108, 109, 110]
 
 
 @pytest.mark.parametrize(
