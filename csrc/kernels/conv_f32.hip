@@ -31,6 +31,7 @@
 
 #include "common.h"
 #include "launch.h"
+#include "letterbox.h"
 
 namespace arena {
 
@@ -992,7 +993,11 @@ constexpr int H16_TH = 8, H16_TW = 16, H16_HR = H16_TH + 2, H16_HC = H16_TW + 2,
 constexpr int H16_XP = 48;    // bf16 per halo pixel: [h|m|l][16]
 constexpr int H16_WPK = 208;  // bf16 per (row, ky): [2 slabs][h|m|l][32] = 192 + 16 pad (416 B)
 
-template <int NF>
+//
+// LB: the input is the letterboxed space-to-depth image itself (the stem conv of the fp32 detector): each halo
+// pixel is sampled from the uint8 image (letterbox_s2d_px, the letterbox kernel's own sampler, so the values
+// are bitwise those of the unfused program) and the 320x320x16 fp32 s2d tensor is never written or re-read.
+template <int NF, bool LB>
 __global__ __launch_bounds__(256) void conv_x3_h16_kernel(const ConvParams p) {
   constexpr int BN = NF * 16, MF = 2;
   __shared__ __attribute__((aligned(16))) bf16 sX[H16_HPIX * H16_XP];
@@ -1012,6 +1017,34 @@ __global__ __launch_bounds__(256) void conv_x3_h16_kernel(const ConvParams p) {
   const float* __restrict__ x = (const float*)p.x + (size_t)b * p.H * p.W * p.xs;
   const float* __restrict__ w = (const float*)p.w;
 
+  if constexpr (LB) {
+    // one thread per halo pixel: 12 live channels sampled from the image, 4 zero; conv padding is zero
+    const ImageMeta m = p.lb_meta[b];
+    for (int px = tid; px < H16_HPIX; px += 256) {
+      const int hy = px / H16_HC, hx = px - hy * H16_HC;
+      const int iy = iy0 + hy, ix = ix0 + hx;
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = 0.f;
+      if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W) letterbox_s2d_px<float>(p.lb_pool, m, iy, ix, v);
+      bf16x8 h[2], mm[2], l[2];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        bf16 th, tm, tl;
+        split3(v[c], th, tm, tl);
+        h[c >> 3][c & 7] = th;
+        mm[c >> 3][c & 7] = tm;
+        l[c >> 3][c & 7] = tl;
+      }
+      bf16* d = &sX[px * H16_XP];
+      *(bf16x8*)d = h[0];
+      *(bf16x8*)(d + 8) = h[1];
+      *(bf16x8*)(d + 16) = mm[0];
+      *(bf16x8*)(d + 24) = mm[1];
+      *(bf16x8*)(d + 32) = l[0];
+      *(bf16x8*)(d + 40) = l[1];
+    }
+  } else {
   // input halo: 4 float4 (16 channels) per pixel, split into three planes
   for (int i = tid; i < H16_HPIX * 4; i += 256) {
     const int px = i >> 2, g = i & 3;
@@ -1029,6 +1062,7 @@ __global__ __launch_bounds__(256) void conv_x3_h16_kernel(const ConvParams p) {
     *(bf16x4*)d = h;
     *(bf16x4*)(d + 16) = m;
     *(bf16x4*)(d + 32) = l;
+  }
   }
   // weights: row n, kernel row ky -> 64 k (48 real: kx 0..2 x 16 channels) in two 32-deep slabs
   for (int i = tid; i < BN * 3 * 16; i += 256) {
@@ -1127,7 +1161,10 @@ static void launch_x3_h16(const ConvParams& p, hipStream_t s) {
   constexpr int BN = NF * 16;
   const int tiles = ((p.Wo + H16_TW - 1) / H16_TW) * ((p.Ho + H16_TH - 1) / H16_TH);
   dim3 grid((unsigned)(p.B * tiles), (unsigned)((p.Cout_pad + BN - 1) / BN));
-  hipLaunchKernelGGL((conv_x3_h16_kernel<NF>), grid, dim3(256), 0, s, p);
+  if (p.lb_meta != nullptr)
+    hipLaunchKernelGGL((conv_x3_h16_kernel<NF, true>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_x3_h16_kernel<NF, false>), grid, dim3(256), 0, s, p);
 }
 
 // impl kF32X3H16: 3x3 stride-1 pad-1 convs over exactly 16 input channels (Kpad 144)
@@ -1539,6 +1576,11 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (M <= 0) return;
   if (M > 0x7fffffffL || (long)p.B * p.H * p.W * p.xs > 0x7fffffffL) throw std::runtime_error("conv2d_f32: too large");
   const int ncf = p.Cout_pad / 16;
+  if (p.lb_meta != nullptr) {  // letterbox source: only the x3-h16 stem kernel samples images
+    if (p.lb_pool == nullptr || !x3_h16(p, s))
+      throw std::runtime_error("conv2d_f32: a letterbox-source conv must be a 3x3 s1 pad-1 conv over 16 channels");
+    return;
+  }
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
     if (p.impl == kF32X3H16) {
       if (!x3_h16(p, s)) throw std::runtime_error("conv2d_f32: not an x3-h16-eligible conv (3x3 s1 over 16 channels)");

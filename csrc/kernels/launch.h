@@ -16,6 +16,7 @@ namespace arena {
 // Implicit-GEMM NHWC convolution on MFMA (v_mfma_f32_16x16x32_bf16) with a
 // fused epilogue: + bias, activation, + residual, store into a channel slice
 // of a concat buffer, optional second store nearest-upsampled x2 (FPN).
+struct ImageMeta;
 struct ConvParams {
   const void* x;  // bf16 input, already offset to its channel slice
   int B, H, W;    // batch capacity and input spatial dims
@@ -43,6 +44,10 @@ struct ConvParams {
   const float* pw_bias; // fp32 [pw_cout_pad]
   void* pw_y;           // bf16 output, pixel stride pw_ys
   int pw_ys, pw_cout, pw_kpad, pw_act;
+  // Letterbox source (fp32 x3-h16 stem only): when lb_meta is set the input is not read from x but sampled
+  // from the batch's uint8 images (letterbox.h), H x W being the space-to-depth grid (T / 2) of the target.
+  const uint8_t* lb_pool;
+  const ImageMeta* lb_meta;
 };
 void conv2d(const ConvParams& p, hipStream_t s);
 void conv_igemm(const ConvParams& p, hipStream_t s);  // LDS-pipelined implicit GEMM (impl 3)

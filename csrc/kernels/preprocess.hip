@@ -18,53 +18,9 @@
 // stem becomes a 3x3/s1 conv, MobileNet's 3x3/s2 stem a 2x2/s1 conv.
 #include "common.h"
 #include "launch.h"
+#include "letterbox.h"
 
 namespace arena {
-
-struct LinTap {
-  int i0, i1;
-  float f;
-};
-
-__device__ __forceinline__ LinTap lin_tap(int d, float scale, int n) {
-#pragma clang fp contract(off)  // (d + 0.5) * scale - 0.5 rounded twice, as the host computes it
-  float fx = ((float)d + 0.5f) * scale - 0.5f;
-  int s0 = (int)floorf(fx);
-  float f = fx - (float)s0;
-  if (s0 < 0) { s0 = 0; f = 0.f; }
-  if (s0 >= n - 1) { s0 = n - 1; f = 0.f; }
-  LinTap t;
-  t.i0 = s0;
-  t.i1 = s0 + 1 < n ? s0 + 1 : n - 1;
-  t.f = f;
-  return t;
-}
-
-__device__ __forceinline__ void bilinear_rgb(const uint8_t* img, int stride_px, LinTap ty, LinTap tx,
-                                             float* rgb) {
-  // separately rounded multiply and add, as the host resize (numpy) computes them: a fused multiply-add
-  // moves values that sit at x.5 to the other side of the uint8 rounding
-#pragma clang fp contract(off)
-  const uint8_t* r0 = img + (size_t)ty.i0 * stride_px * 3;
-  const uint8_t* r1 = img + (size_t)ty.i1 * stride_px * 3;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const float a = (float)r0[tx.i0 * 3 + c], b = (float)r0[tx.i1 * 3 + c];
-    const float d = (float)r1[tx.i0 * 3 + c], e = (float)r1[tx.i1 * 3 + c];
-    const float top = a + (b - a) * tx.f;
-    const float bot = d + (e - d) * tx.f;
-    float v = top + (bot - top) * ty.f;
-    rgb[c] = floorf(v + 0.5f);  // cv2 returns uint8: round to nearest
-  }
-}
-
-// /255 of a uint8 value: the exact-fp32 pipeline divides as the host preprocessor does; the bf16 pipeline
-// multiplies by the reciprocal (the difference is far below its rounding).
-template <typename T>
-__device__ __forceinline__ float div255(float v) {
-  if constexpr (sizeof(T) == 4) return v / 255.0f;
-  else return v * (1.0f / 255.0f);
-}
 
 template <typename T>
 __device__ __forceinline__ void store16(T* dst, const float* v) {
@@ -82,32 +38,8 @@ __global__ __launch_bounds__(256) void letterbox_s2d_kernel(const LetterboxParam
   const int X = (int)(tid % T2);
   const int Y = (int)((tid / T2) % T2);
   const int b = (int)(tid / ((long)T2 * T2));
-  const ImageMeta m = p.meta[b];
-  const uint8_t* img = p.pool + m.offset;
-  const float sy = (float)((double)m.h / (double)m.new_h);
-  const float sx = (float)((double)m.w / (double)m.new_w);
   float out[16];
-  // unit scale (the image's long side is already T: COCO's 640x480 / 640x427 ...): the bilinear taps have zero
-  // weight, so the letterboxed pixel is the source pixel (bitwise the same value) — 3 byte loads instead of 12
-  const bool unit = m.new_h == m.h && m.new_w == m.w;
-#pragma unroll
-  for (int pq = 0; pq < 4; ++pq) {
-    const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
-    const int dy = oy - m.pad_h, dx = ox - m.pad_w;
-    float rgb[3] = {114.f, 114.f, 114.f};
-    if (dy >= 0 && dy < m.new_h && dx >= 0 && dx < m.new_w) {
-      if (unit) {
-        const uint8_t* px = img + ((size_t)dy * m.w + dx) * 3;
-        rgb[0] = (float)px[0];
-        rgb[1] = (float)px[1];
-        rgb[2] = (float)px[2];
-      } else {
-        bilinear_rgb(img, m.w, lin_tap(dy, sy, m.h), lin_tap(dx, sx, m.w), rgb);
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = div255<T>(rgb[c]);
-  }
+  letterbox_s2d_px<T>(p.pool, p.meta[b], Y, X, out);
   out[12] = out[13] = out[14] = out[15] = 0.f;
   store16((T*)p.out + (size_t)tid * 16, out);
 }

@@ -309,6 +309,10 @@ void Executor::autotune(Bucket& bk) {
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;
     const bool f32 = prog_[i][kDtypeField] == 1;
+    if (prog_[i][1] == BUF_POOL) {  // letterbox-source stem: one kernel implements it
+      bk.impl[i] = kF32X3H16;
+      continue;
+    }
     if (!f32 && prog_[i][34] > 0) {  // fused pointwise epilogue: only the v3 halo-tile kernel implements it
       bk.impl[i] = 2;
       continue;
@@ -441,6 +445,13 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.act = (int)r[28];
         p.B = batch(r[30]);
         p.bdev = bdev(r[30]);
+        if (r[1] == BUF_POOL) {  // the stem conv samples the letterboxed images itself (fp32 x3-h16 kernel)
+          if (!f32 || r[30] != 0) throw std::runtime_error("executor: letterbox-source conv must be fp32 over images");
+          p.x = nullptr;
+          p.lb_pool = pool;
+          p.lb_meta = meta;
+          p.impl = kF32X3H16;
+        }
         if (r[34] > 0) {  // fused pointwise epilogue (Detect head 3x3 -> 1x1)
           p.pw_w = W + r[31];
           p.pw_kpad = (int)r[32];

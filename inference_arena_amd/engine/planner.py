@@ -396,6 +396,16 @@ class ProgramBuilder:
     def letterbox(self, out: Buffer, T: int) -> None:
         self._emit([OP_LETTERBOX, out.id, T], out)
 
+    def letterbox_conv(self, dst: View, w: torch.Tensor, b: torch.Tensor, *, T: int, act: str = "silu") -> None:
+        """fp32 stem conv (3x3 s1 over the 16-channel space-to-depth grid) whose input is the letterboxed
+        batch images themselves (source buffer BUF_POOL): the kernel samples the uint8 images as the letterbox
+        op would, so the T/2 x T/2 x 16 fp32 input tensor is never materialised (executor OP_CONV, x3-h16)."""
+        if not self.f32:
+            raise ValueError("letterbox_conv: fp32 programs only (bf16 programs use stem_fused)")
+        if w.shape[1:] != (16, 3, 3) or T % 2:
+            raise ValueError("letterbox_conv: expects [Cout, 16, 3, 3] weights and an even target size")
+        self.conv(View(BUF_POOL, 0, 16), dst, w, b, act=act, src_hw=(T // 2, T // 2))
+
     def c3_fused(self, src: View, dst: View, H: int, W: int, cv12: tuple, bottlenecks: list, cv3: tuple, *,
                  res: bool, kind: int = IMAGES) -> None:
         """A whole C3 block as one op: ``cv12`` = (w, b) of cv1|cv2 stacked [2CH, C1, 1, 1]; ``bottlenecks`` =

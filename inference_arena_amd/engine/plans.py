@@ -133,6 +133,12 @@ def fuse_head_pool_default() -> bool:
     return os.environ.get("ARENA_FUSE_POOL", "1").lower() not in ("0", "false", "no", "off")
 
 
+def fuse_letterbox_f32_default() -> bool:
+    """``ARENA_F32_LB_STEM`` (default 1): in fp32 programs the stem conv samples the letterboxed images
+    itself (letterbox_conv); the 320x320x16 fp32 space-to-depth input is never stored."""
+    return os.environ.get("ARENA_F32_LB_STEM", "1").lower() not in ("0", "false", "no", "off")
+
+
 def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool = False,
               fuse_stem: bool | None = None):
     h = T // 2
@@ -148,6 +154,10 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
     elif fuse_stem and not tensor_input:
         A0 = pb.tensor("b0", h, h, 16)
         pb.stem_fused(View(A0, 0, 16), s2d_stem_6x6(w), b, S=T, act="silu")
+        pb.conv(View(A0, 0, 16), View(A1, 0, 32), *fold(y.b1), stride=2)
+    elif pb.f32 and not tensor_input and fuse_letterbox_f32_default():
+        A0 = pb.tensor("b0", h, h, 16)
+        pb.letterbox_conv(View(A0, 0, 16), s2d_stem_6x6(w), b, T=T)
         pb.conv(View(A0, 0, 16), View(A1, 0, 32), *fold(y.b1), stride=2)
     else:
         A0 = pb.tensor("b0", h, h, 16)

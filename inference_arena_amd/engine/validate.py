@@ -135,7 +135,12 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 raise ProgramError(f"op {i}: bad conv geometry")
             if f32 and (Cin < 16 or Cin % 4 or int(r[34]) > 0):
                 raise ProgramError(f"op {i}: unsupported fp32 conv geometry")
-            view(i, r[1], int(r[2]), int(r[3]), n * H * W, Cin, el, "conv input")
+            if int(r[1]) == BUF_POOL:  # letterbox-source stem (x3-h16 kernel samples the images)
+                if not f32 or int(r[30]) == CROPS or (KH, KW, Cin, kpad, int(r[19]), int(r[20]), int(r[21])) != \
+                        (3, 3, 16, 144, 1, 1, 1) or H != W or (Ho, Wo) != (H, W):
+                    raise ProgramError(f"op {i}: letterbox-source conv must be an fp32 3x3 s1 conv over 16 channels")
+            else:
+                view(i, r[1], int(r[2]), int(r[3]), n * H * W, Cin, el, "conv input")
             oel = 4 if int(r[29]) else el
             view(i, r[10], int(r[11]), int(r[12]), n * Ho * Wo, Cout, oel, "conv output")
             view(i, r[22], int(r[23]), int(r[24]), n * Ho * Wo, Cout, el, "conv residual")

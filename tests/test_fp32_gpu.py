@@ -247,6 +247,33 @@ def test_fp32_pipeline_matches_reference(dense_models, device):
     assert max(rel) < 1e-3, max(rel)
 
 
+def test_fp32_letterbox_stem_matches_unfused(dense_models, device, monkeypatch):
+    """The fp32 stem conv sampling the letterboxed images itself (letterbox_conv, ARENA_F32_LB_STEM) vs the
+    letterbox op + stem conv: the same stem activations (fp32 rounding) and the same results.  Covers
+    unit-scale (640x480 / 640x427), bilinear (333x500) and padded images and a partial batch."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+    from inference_arena_amd.engine.planner import BUF_POOL, OP_CONV, OP_LETTERBOX
+
+    imgs = synthetic_images(3, 71) + synthetic_images(1, 72, hw=(333, 500)) + synthetic_images(1, 73, hw=(640, 427))
+    monkeypatch.setenv("ARENA_F32_LB_STEM", "0")
+    plain = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="fp32")
+    monkeypatch.setenv("ARENA_F32_LB_STEM", "1")
+    fused = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="fp32")
+    assert any(int(op[0]) == OP_LETTERBOX for op in plain.program.ops)
+    assert not any(int(op[0]) == OP_LETTERBOX for op in fused.program.ops)
+    assert any(int(op[0]) == OP_CONV and int(op[1]) == BUF_POOL for op in fused.program.ops)
+    a, b = plain.infer(imgs), fused.infer(imgs)
+    for i in range(len(imgs)):
+        x1, x2 = plain.read_buffer("b0", 8, i), fused.read_buffer("b0", 8, i)
+        np.testing.assert_allclose(x2, x1, rtol=1e-5, atol=1e-5)
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        if len(x):
+            np.testing.assert_allclose(y.boxes, x.boxes, rtol=2e-5, atol=5e-3)
+            np.testing.assert_array_equal(y.topk_idx[:, 0], x.topk_idx[:, 0])
+
+
 def test_fp32_tensor_models_match_torch(models, device):
     """Reference tensor contracts in fp32: yolov5n [3,640,640] -> [84,8400], mobilenetv2 -> [1000]."""
     from inference_arena_amd.engine.pipeline import GpuTensorModel

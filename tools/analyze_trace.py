@@ -71,6 +71,8 @@ def main(argv=None) -> int:
     first = FIRST_KERNEL.get(int(op0[0]), "letterbox")
     if int(op0[0]) == 15:  # detector stem: single-stage kernel or letterbox+stem+conv (stem2_kernel)
         first = "stem2_kernel" if int(op0[20]) else "stem_fused_kernel<0"
+    if int(op0[0]) == 1 and int(op0[1]) == -12:  # fp32 stem conv sampling the letterboxed images (BUF_POOL)
+        first = "conv_x3_h16_kernel<1, true>"
     replays = []
     for q in by_q.values():
         q.sort(key=lambda r: int(r["Start_Timestamp"]))
