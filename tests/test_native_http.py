@@ -135,11 +135,20 @@ def test_health_metrics_and_concurrency(server):
     assert s["ok"] >= 48 and s["errors"] >= 1
     import time
 
-    time.sleep(1.2)  # the metrics text refreshes once a second
-    c.request("GET", "/metrics")
-    r = c.getresponse()
-    text = r.read().decode()
-    assert r.status == 200 and 'arena_requests_total{arch="monolithic",status="ok"}' in text
+    # the metrics text refreshes once a second; poll (a loaded CI host can be late)
+    c.close()
+    deadline = time.monotonic() + 10.0
+    while True:
+        time.sleep(0.3)
+        c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=30)
+        c.request("GET", "/metrics")
+        r = c.getresponse()
+        text = r.read().decode()
+        ok = r.status == 200 and 'arena_requests_total{arch="monolithic",status="ok"}' in text
+        if ok or time.monotonic() > deadline:
+            break
+        c.close()
+    assert ok, text[:400]
     fe.set_healthy(False)
     c.request("GET", "/health")
     r = c.getresponse()
