@@ -634,6 +634,41 @@ PYBIND11_MODULE(_C, m) {
              return new HttpFrontEnd(&batcher, dc, std::move(labels), c);
            }),
            py::keep_alive<1, 2>())
+      // handler mode: HTTP/multipart natively, the request handler in Python (take / complete)
+      .def(py::init([](const py::dict& cfg) {
+        FrontConfig c;
+        c.host = get<std::string>(cfg, "host", c.host);
+        c.port = get<int>(cfg, "port", c.port);
+        c.io_threads = get<int>(cfg, "io_threads", c.io_threads);
+        c.reuse_port = get<bool>(cfg, "reuse_port", c.reuse_port);
+        c.max_body = get<int64_t>(cfg, "max_body", c.max_body);
+        c.replica_tag = get<std::string>(cfg, "replica_tag", c.replica_tag);
+        c.max_handler_queue = get<int>(cfg, "max_queue", c.max_handler_queue);
+        c.handler_mode = true;
+        py::gil_scoped_release nogil;
+        return new HttpFrontEnd(nullptr, DecodeChannel{}, {}, c);
+      }))
+      .def_property_readonly("handler_mode", &HttpFrontEnd::handler_mode)
+      .def(
+          "take",
+          [](HttpFrontEnd& f, int max_n, int timeout_ms) {
+            std::vector<HandlerRequest> v;
+            {
+              py::gil_scoped_release nogil;
+              v = f.take(max_n, timeout_ms);
+            }
+            py::list out;
+            for (auto& r : v) out.append(py::make_tuple(r.key, py::bytes(r.data)));
+            return out;
+          },
+          py::arg("max_n") = 64, py::arg("timeout_ms") = 100)
+      .def(
+          "complete",
+          [](HttpFrontEnd& f, uint64_t key, int code, const std::string& body, int n_det) {
+            py::gil_scoped_release nogil;
+            return f.complete(key, code, body, n_det);
+          },
+          py::arg("key"), py::arg("code"), py::arg("body"), py::arg("n_det") = 0)
       .def_property_readonly("port", &HttpFrontEnd::port)
       .def("set_healthy", &HttpFrontEnd::set_healthy)
       .def("set_metrics_text", &HttpFrontEnd::set_metrics_text)

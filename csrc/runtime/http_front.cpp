@@ -185,13 +185,21 @@ struct HttpFrontEnd::Pending {
   Clock::time_point t0, t_dec;
 };
 
+struct HttpFrontEnd::HandlerPending {
+  std::shared_ptr<Conn> conn;
+  Clock::time_point t0;
+};
+
 HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vector<std::string> labels,
                            FrontConfig cfg)
     : batcher_(batcher), dc_(std::move(dc)), labels_(std::move(labels)), cfg_(std::move(cfg)) {
-  if (batcher_ == nullptr) throw std::runtime_error("HttpFrontEnd: no batcher");
-  if (dc_.shm == nullptr || dc_.slots <= 0 || dc_.task_fds.empty() || dc_.result_fd < 0 || dc_.result_wfd < 0)
-    throw std::runtime_error("HttpFrontEnd: incomplete decode channel");
-  if (dc_.big_fds.size() != dc_.task_fds.size()) throw std::runtime_error("HttpFrontEnd: big_fds / task_fds mismatch");
+  if (!cfg_.handler_mode) {
+    if (batcher_ == nullptr) throw std::runtime_error("HttpFrontEnd: no batcher");
+    if (dc_.shm == nullptr || dc_.slots <= 0 || dc_.task_fds.empty() || dc_.result_fd < 0 || dc_.result_wfd < 0)
+      throw std::runtime_error("HttpFrontEnd: incomplete decode channel");
+    if (dc_.big_fds.size() != dc_.task_fds.size())
+      throw std::runtime_error("HttpFrontEnd: big_fds / task_fds mismatch");
+  }
   stats_.latency_hist.assign(kLatencyBucketsMs.size() + 1, 0);
   for (int s = dc_.slots - 1; s >= 0; --s) free_slots_.push_back(s);
   for (size_t i = 0; i < dc_.task_fds.size(); ++i) task_mu_.emplace_back(new std::mutex);
@@ -231,7 +239,7 @@ HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vecto
     epfds_.push_back(ep);
   }
   for (int i = 0; i < n; ++i) io_threads_.emplace_back([this, i] { io_loop(i); });
-  collector_ = std::thread([this] { collector_loop(); });
+  if (!cfg_.handler_mode) collector_ = std::thread([this] { collector_loop(); });
 }
 
 HttpFrontEnd::~HttpFrontEnd() { stop(); }
@@ -240,9 +248,14 @@ void HttpFrontEnd::stop() {
   if (stop_.exchange(true)) return;
   uint64_t one = 1;
   if (write(stop_efd_, &one, sizeof one) < 0) { /* the flag alone stops the loops on their next wakeup */ }
-  // wake the collector with a sentinel completion record (key < 0)
-  int64_t rec[4] = {-1, 0, 0, 0};
-  write_all(dc_.result_wfd, rec, sizeof rec);
+  if (cfg_.handler_mode) {
+    std::lock_guard<std::mutex> lk(hq_mu_);
+    hq_cv_.notify_all();  // wake take()
+  } else {
+    // wake the collector with a sentinel completion record (key < 0)
+    int64_t rec[4] = {-1, 0, 0, 0};
+    write_all(dc_.result_wfd, rec, sizeof rec);
+  }
   for (auto& t : io_threads_)
     if (t.joinable()) t.join();
   if (collector_.joinable()) collector_.join();
@@ -252,8 +265,59 @@ void HttpFrontEnd::stop() {
   listen_fd_ = -1;
   if (stop_efd_ >= 0) ::close(stop_efd_);
   stop_efd_ = -1;
+  {
+    std::lock_guard<std::mutex> lk(hq_mu_);
+    hq_.clear();
+    hpend_.clear();
+  }
   std::lock_guard<std::mutex> lk(pend_mu_);
   pending_.clear();
+}
+
+std::vector<HandlerRequest> HttpFrontEnd::take(int max_n, int timeout_ms) {
+  std::vector<HandlerRequest> out;
+  std::unique_lock<std::mutex> lk(hq_mu_);
+  hq_cv_.wait_for(lk, std::chrono::milliseconds(std::max(0, timeout_ms)),
+                  [this] { return !hq_.empty() || stop_.load(); });
+  while (!hq_.empty() && (int)out.size() < std::max(1, max_n)) {
+    out.push_back(std::move(hq_.front()));
+    hq_.pop_front();
+  }
+  return out;
+}
+
+bool HttpFrontEnd::complete(uint64_t key, int code, const std::string& body, int n_det) {
+  std::shared_ptr<HandlerPending> hp;
+  {
+    std::lock_guard<std::mutex> lk(hq_mu_);
+    auto it = hpend_.find(key);
+    if (it == hpend_.end()) return false;
+    hp = it->second;
+    hpend_.erase(it);
+  }
+  const double total_ms = ms_since(hp->t0);
+  {
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    ++stats_.requests;
+    if (code == 200) {
+      ++stats_.ok;
+      stats_.detections += n_det;
+      stats_.sum_total_ms += total_ms;
+      size_t b = 0;
+      while (b < kLatencyBucketsMs.size() && total_ms > kLatencyBucketsMs[b]) ++b;
+      ++stats_.latency_hist[b];
+    } else if (code == 413) {
+      ++stats_.too_large;
+    } else if (code == 503) {
+      ++stats_.unavailable;
+    } else if (code >= 500) {
+      ++stats_.errors;
+    } else {
+      ++stats_.bad_request;
+    }
+  }
+  respond(hp->conn, code, "application/json", body);
+  return true;
 }
 
 void HttpFrontEnd::set_metrics_text(std::string text) {
@@ -590,6 +654,27 @@ void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, c
     if (!multipart_field(body, ctype, "file", off, len, err)) return fail(422, err);
   }
   if (len == 0) return fail(422, "empty request body");
+  if (cfg_.handler_mode) {
+    const uint64_t key = next_key_.fetch_add(1);
+    auto hp = std::make_shared<HandlerPending>();
+    hp->conn = c;
+    hp->t0 = t0;
+    {
+      std::lock_guard<std::mutex> lk(hq_mu_);
+      if ((int)hpend_.size() >= cfg_.max_handler_queue) {
+        hp.reset();
+      } else {
+        hpend_[key] = hp;
+        HandlerRequest r;
+        r.key = key;
+        r.data.assign(body, off, len);
+        hq_.push_back(std::move(r));
+      }
+    }
+    if (!hp) return fail(503, "request queue is full");
+    hq_cv_.notify_one();
+    return;
+  }
   int slot;
   {
     std::lock_guard<std::mutex> lk(slot_mu_);

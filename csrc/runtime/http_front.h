@@ -20,13 +20,24 @@
 //     -> the reference's JSON schema (request_id, detections[{detection,
 //        classification}], timing) -> the connection's I/O thread writes it.
 //
+// Handler mode (FrontConfig.handler_mode, no batcher / decode channel): the
+// same HTTP/1.1 + multipart layer in front of a Python topology whose request
+// path is not one batcher (microservices detection service, model-server
+// gateway).  predict() queues (key, upload bytes); the owner drains the queue
+// with take() (GIL released while waiting), runs its async handler and hands
+// the finished JSON back with complete(key, status, body).  The Python HTTP
+// stack (uvicorn/h11 + starlette + multipart parsing, ~0.7-1.4 ms of
+// interpreter time per request) is what capped those arms' processes.
+//
 // GET /health (503 once set_healthy(false)), GET /metrics (text supplied by
 // the Python owner, which renders Prometheus from stats()).  Errors follow the
 // FastAPI handler: 422 bad upload, 413 too large, 503 queue full / not ready,
 // 500 decode or device failure, each with {"detail": ...}.
 #pragma once
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -59,6 +70,14 @@ struct FrontConfig {
   bool softmax_confidence = false;  // ARENA_CONFIDENCE=softmax (default: the top-1 logit, as the reference)
   int64_t max_body = 64 << 20;
   std::string replica_tag;  // non-empty: an "x-arena-replica" header on every response (server/replica.py)
+  bool handler_mode = false;  // uploads go to take() / complete() instead of decode pool + batcher
+  int max_handler_queue = 4096;  // queued + in-handler requests before 503
+};
+
+// One upload handed to the Python handler (handler mode).
+struct HandlerRequest {
+  uint64_t key = 0;
+  std::string data;  // the multipart "file" field (or the raw body)
 };
 
 struct FrontStats {
@@ -82,6 +101,13 @@ class HttpFrontEnd {
   void set_metrics_text(std::string text);
   FrontStats stats();
   void stop();
+
+  // handler mode: up to max_n queued uploads; waits up to timeout_ms for the first one (empty on timeout / stop)
+  std::vector<HandlerRequest> take(int max_n, int timeout_ms);
+  // handler mode: answer request `key` (status code, JSON body); n_det counts into the detections total.
+  // Returns false when the key is unknown (connection gone, already answered).
+  bool complete(uint64_t key, int code, const std::string& body, int n_det = 0);
+  bool handler_mode() const { return cfg_.handler_mode; }
 
   struct Conn;
   struct Pending;
@@ -119,6 +145,13 @@ class HttpFrontEnd {
   std::mutex pend_mu_;
   std::unordered_map<uint64_t, std::shared_ptr<Pending>> pending_;
   std::atomic<uint64_t> next_key_{1};
+
+  // handler mode
+  struct HandlerPending;
+  std::mutex hq_mu_;
+  std::condition_variable hq_cv_;
+  std::deque<HandlerRequest> hq_;
+  std::unordered_map<uint64_t, std::shared_ptr<HandlerPending>> hpend_;  // queued or in the handler
 
   std::mutex metrics_mu_;
   std::string metrics_text_;

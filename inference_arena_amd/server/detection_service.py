@@ -65,8 +65,8 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
     app = FastAPI(title="Detection Service (MI355X)", version="2.0.0", lifespan=lifespan)
     app.state.arena = state
 
-    @app.post("/predict", response_model=PredictResponse)
-    async def predict(request: Request):
+    async def predict_bytes(data: bytes) -> PredictResponse:
+        """The /predict handler on the upload's bytes (shared by FastAPI and the native front end)."""
         rid = new_request_id()
         tm = Timer()
         det_be: DetectorBackend | None = state.get("detector")
@@ -75,7 +75,6 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
         if det_be is None or cl is None or not cl.connected:
             metrics.observe("unavailable")
             raise HTTPException(status_code=503, detail="Service not ready")
-        data = await read_upload(request)
         try:
             state["faults"].check()
             image = await state["decode"].decode(data)
@@ -120,6 +119,17 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
         log.info("Predict complete", extra={"endpoint": "/predict", "latency_ms": timing["total_ms"],
                                             "detections": len(results), "status_code": 200})
         return PredictResponse(request_id=rid, detections=results, timing=timing)
+
+    def healthy() -> bool:
+        cl, det = state.get("client"), state.get("detector")
+        return device_fault(state) is None and det is not None and cl is not None and cl.connected
+
+    state["predict_bytes"] = predict_bytes
+    state["healthy"] = healthy
+
+    @app.post("/predict", response_model=PredictResponse)
+    async def predict(request: Request):
+        return await predict_bytes(await read_upload(request))
 
     @app.get("/health", response_model=HealthResponse)
     async def health():

@@ -29,7 +29,7 @@ from ..postprocess import parse_yolo_output
 from ..processing import MobileNetPreprocessor, YOLOPreprocessor, extract_crop
 from ..utils.logging import request_id_var, setup_logging
 from ..utils.settings import Settings
-from .app_common import DecodePool, FaultInjector, Timer, new_request_id, read_upload
+from .app_common import DecodePool, FaultInjector, Timer, device_fault, new_request_id, read_upload
 from .kserve_client import ModelServerClient
 from .schemas import Classification, DetectionBox, DetectionWithClassification, HealthResponse, PredictResponse
 
@@ -109,15 +109,14 @@ def create_app(settings: Settings | None = None, client: ModelServerClient | Non
             dets = [await one(d) for d in det]
         return dets, {"detection_ms": detection_ms, "classification_ms": t.ms()}
 
-    @app.post("/predict", response_model=PredictResponse)
-    async def predict(request: Request):
+    async def predict_bytes(data: bytes) -> PredictResponse:
+        """The /predict handler on the upload's bytes (shared by FastAPI and the native front end)."""
         rid = new_request_id()
         tm = Timer()
         metrics: ArenaMetrics = state["metrics"]
         if not state["ready"]:
             metrics.observe("unavailable")
             raise HTTPException(status_code=503, detail="Service not ready")
-        data = await read_upload(request)
         try:
             state["faults"].check()
             if settings.ARENA_GATEWAY_MODE == "pipeline":
@@ -133,6 +132,16 @@ def create_app(settings: Settings | None = None, client: ModelServerClient | Non
         log.info("Predict complete", extra={"endpoint": "/predict", "latency_ms": timing["total_ms"],
                                             "detections": len(dets), "status_code": 200})
         return PredictResponse(request_id=rid, detections=dets, timing=timing)
+
+    state["predict_bytes"] = predict_bytes
+    state["healthy"] = lambda: bool(state["ready"]) and device_fault(state) is None
+
+    @app.post("/predict", response_model=PredictResponse)
+    async def predict(request: Request):
+        if not state["ready"]:
+            state["metrics"].observe("unavailable")
+            raise HTTPException(status_code=503, detail="Service not ready")
+        return await predict_bytes(await read_upload(request))
 
     @app.get("/health", response_model=HealthResponse)
     async def health():

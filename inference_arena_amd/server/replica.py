@@ -165,6 +165,17 @@ def main(argv=None) -> int:
     D.shutdown(info)  # the group is only needed for start-up
 
     port = a.port + a.port_stride * info.rank
+    if a.arch in ("detection", "gateway") and os.environ.get("ARENA_NATIVE_HTTP") == "1":
+        # native HTTP/multipart layer, the arm's request handler stays in Python (server/native_handler.py)
+        from .native_handler import serve_app
+
+        rc = asyncio.run(serve_app(app, port=port, host=a.host, replica_tag=str(info.rank),
+                                   io_threads=int(os.environ.get("ARENA_HTTP_THREADS", "2")),
+                                   reuse_port=a.port_stride == 0))
+        if rc and os.environ.get("ARENA_EXIT_ON_FAULT", "1") == "1":
+            print(f"replica {info.rank}: device fault, exiting for restart", flush=True)
+            return 3
+        return 0
     sock = _socket(a.host, port, reuse_port=a.port_stride == 0)
     server = uvicorn.Server(uvicorn.Config(ReplicaTag(app, info.rank), log_level="warning", access_log=False))
     fault: list[str] = []

@@ -196,3 +196,102 @@ def test_detection_service_drops_failed_crops():
         srv.stop()
         r = c.post("/predict", content=body, headers={"content-type": ctype})
         assert r.status_code == 200 and r.json()["detections"] == []
+
+
+def _native_serve(app, port=0):
+    """Run ``native_handler.serve_app`` on a thread; returns (server, stop, thread)."""
+    from inference_arena_amd.server.native_handler import serve_app
+
+    box, ready = {}, threading.Event()
+    loop = asyncio.new_event_loop()
+
+    async def main():
+        box["stop"] = asyncio.Event()
+        box["rc"] = await serve_app(app, port=port, host="127.0.0.1", stop=box["stop"],
+                                    on_ready=lambda srv: (box.__setitem__("srv", srv), ready.set()))
+
+    t = threading.Thread(target=lambda: loop.run_until_complete(main()), daemon=True)
+    t.start()
+    assert ready.wait(30)
+    return box, loop, t
+
+
+def test_detection_service_native_handler_front(fake_server):
+    """ARENA_NATIVE_HTTP=1 detection service: C++ HTTP/multipart, Python handler (take/complete): same JSON
+    as the FastAPI route, concurrent keep-alive clients, 422 / 404 / health / metrics."""
+    import http.client
+    import json
+    import time
+
+    from inference_arena_amd.server.detection_service import create_app
+
+    s = Settings(LOG_LEVEL="WARNING", CLASSIFICATION_GRPC_ENDPOINT=f"127.0.0.1:{fake_server.port}",
+                 ARENA_FANOUT="batch", ARENA_CROP_TRANSPORT="raw")
+    img = synthetic_images(1, 5)[0]
+    body, ctype = encode_multipart("file", encode_jpeg(img))
+    box, loop, t = _native_serve(create_app(s, detector=FakeDetector()))
+    port = box["srv"].port
+    try:
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=30)
+        c.request("POST", "/predict", body=body, headers={"Content-Type": ctype})
+        r = c.getresponse()
+        js = json.loads(r.read())
+        assert r.status == 200, js
+        h, w = img.shape[:2]
+        assert [d["classification"]["class_id"] for d in js["detections"]] == [20, h - 5, 1]
+        assert {"detection_ms", "classification_ms", "total_ms"} <= set(js["timing"])
+        # a raw JPEG body works too; an empty multipart field is a 422 from the native layer
+        c.request("POST", "/predict", body=encode_jpeg(img), headers={"Content-Type": "image/jpeg"})
+        r = c.getresponse()
+        assert r.status == 200 and len(json.loads(r.read())["detections"]) == 3
+        bad, bct = encode_multipart("other", b"x")
+        c.request("POST", "/predict", body=bad, headers={"Content-Type": bct})
+        r = c.getresponse()
+        assert r.status == 422 and "detail" in json.loads(r.read())
+        # undecodable upload -> the handler's 500 with {"detail": ...}
+        c.request("POST", "/predict", body=b"not a jpeg", headers={"Content-Type": "image/jpeg"})
+        r = c.getresponse()
+        assert r.status == 500 and json.loads(r.read())["detail"]
+        c.request("GET", "/nope")
+        r = c.getresponse()
+        r.read()
+        assert r.status == 404
+        errors, ok = [], []
+
+        def worker():
+            try:
+                cc = http.client.HTTPConnection("127.0.0.1", port, timeout=30)
+                for _ in range(8):
+                    cc.request("POST", "/predict", body=body, headers={"Content-Type": ctype})
+                    rr = cc.getresponse()
+                    assert rr.status == 200 and len(json.loads(rr.read())["detections"]) == 3
+                    ok.append(1)
+                cc.close()
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        ts = [threading.Thread(target=worker) for _ in range(6)]
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join()
+        assert not errors and len(ok) == 48
+        st = box["srv"].stats()
+        assert st["ok"] >= 50 and st["detections"] >= 150 and st["bad_request"] >= 1 and st["errors"] >= 1
+        deadline = time.monotonic() + 5
+        while True:
+            c.request("GET", "/metrics")
+            r = c.getresponse()
+            text = r.read().decode()
+            if "arena_requests_total" in text or time.monotonic() > deadline:
+                break
+            time.sleep(0.3)
+        assert r.status == 200 and "arena_requests_total" in text
+        c.request("GET", "/health")
+        r = c.getresponse()
+        assert r.status == 200 and json.loads(r.read())["models_loaded"] is True
+        c.close()
+    finally:
+        loop.call_soon_threadsafe(box["stop"].set)
+        t.join(30)
+    assert box["rc"] == 0

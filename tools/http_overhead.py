@@ -65,6 +65,69 @@ def _serve_native(port: int, seconds: float, decode_procs: int) -> None:  # prag
     batcher.shutdown()
 
 
+def _stub_classifier(gport: int, seconds: float) -> None:  # pragma: no cover - child process
+    import numpy as np
+
+    from inference_arena_amd.server.classification_service import start_server
+    from inference_arena_amd.server.service_backends import ClassifierBackend
+    from inference_arena_amd.utils.settings import Settings
+
+    class StubClassifier(ClassifierBackend):
+        async def classify(self, crop):
+            return (np.arange(5, dtype=np.int32), np.array([5, 4, 3, 2, 1], np.float32),
+                    np.array([0.6, 0.2, 0.1, 0.05, 0.05], np.float32))
+
+    async def run():
+        srv = await start_server(Settings(LOG_LEVEL="WARNING", HOST="127.0.0.1"), StubClassifier(), port=gport)
+        await asyncio.sleep(seconds)
+        await srv[0].stop(0)
+
+    asyncio.run(run())
+
+
+def _serve_detection(port: int, seconds: float, native_front: bool) -> None:  # pragma: no cover - child process
+    """The microservices detection service (stub detector: 4 boxes) fanning out to a stub classification gRPC
+    service (its own process); FastAPI/uvicorn or the native front end in handler mode (server/native_handler.py)."""
+    import socket
+    import threading
+
+    import numpy as np
+
+    from inference_arena_amd.server.detection_service import create_app
+    from inference_arena_amd.server.service_backends import DetectorBackend
+    from inference_arena_amd.utils.settings import Settings
+
+    class StubDetector(DetectorBackend):
+        async def detect(self, image):
+            return np.tile(np.array([[10, 20, 110, 220, 0.9, 1]], np.float32), (4, 1)), {"batch_size": 1.0}
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        gport = sk.getsockname()[1]
+    cls = mp.get_context("spawn").Process(target=_stub_classifier, args=(gport, seconds + 5), daemon=True)
+    cls.start()
+    s = Settings.from_env(PORT=port)
+    s.CLASSIFICATION_GRPC_ENDPOINT = f"127.0.0.1:{gport}"
+    s.ARENA_FANOUT, s.ARENA_CROP_TRANSPORT, s.LOG_LEVEL = "batch", "raw", "WARNING"
+    app = create_app(s, detector=StubDetector())
+    if native_front:
+        from inference_arena_amd.server.native_handler import serve_app
+
+        async def run():
+            stop = asyncio.Event()
+            asyncio.get_running_loop().call_later(seconds, stop.set)
+            await serve_app(app, port=port, host="127.0.0.1", stop=stop)
+
+        asyncio.run(run())
+    else:
+        import uvicorn
+
+        server = uvicorn.Server(uvicorn.Config(app, host="127.0.0.1", port=port, log_level="warning",
+                                               access_log=False))
+        threading.Timer(seconds, lambda: setattr(server, "should_exit", True)).start()
+        server.run()
+
+
 def _serve(port: int, profile: str | None, seconds: float) -> None:  # pragma: no cover - child process
     import uvicorn
 
@@ -122,6 +185,8 @@ def main(argv=None) -> int:
     ap.add_argument("--profile", default=None)
     ap.add_argument("--tiny", action="store_true", help="a 32x32 upload: decode cost ~0, isolates the HTTP path")
     ap.add_argument("--native", action="store_true", help="the native C++ front end instead of FastAPI")
+    ap.add_argument("--arm", default="monolithic", choices=["monolithic", "detection"],
+                    help="detection: the microservices detection service + stub gRPC classifier")
     a = ap.parse_args(argv)
     os.environ["ARENA_DECODE_PROCS"] = str(a.decode_procs)
     os.environ.setdefault("LOG_LEVEL", "INFO")
@@ -131,7 +196,9 @@ def main(argv=None) -> int:
     img = workload_images(1)[0]
     jpeg = encode_jpeg(img[:32, :32].copy() if a.tiny else img, 90)
     ctx = mp.get_context("spawn")
-    if a.native:
+    if a.arm == "detection":
+        srv = ctx.Process(target=_serve_detection, args=(a.port, a.seconds + 8, a.native))
+    elif a.native:
         srv = ctx.Process(target=_serve_native, args=(a.port, a.seconds + 8, a.decode_procs or 4))
     else:  # not daemonic: it spawns decode workers
         srv = ctx.Process(target=_serve, args=(a.port, a.profile, a.seconds + 6))
@@ -161,7 +228,7 @@ def main(argv=None) -> int:
 
     out = {"req_s": round(len(lat) / a.seconds, 1), "p50_ms": round(float(np.percentile(lat, 50)) * 1e3, 2),
            "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 2), "users": a.users * a.clients,
-           "decode_procs": a.decode_procs, "front_end": "native" if a.native else "fastapi", "tiny": a.tiny}
+           "decode_procs": a.decode_procs, "front_end": "native" if a.native else "fastapi", "tiny": a.tiny, "arm": a.arm}
     print(json.dumps(out), flush=True)
     if a.profile:
         srv.join(timeout=a.seconds + 30)
