@@ -29,7 +29,7 @@ from ..labels import load_labels
 from ..proto import inference_api as pb
 from ..utils.logging import request_id_var, setup_logging
 from ..utils.settings import Settings
-from .crop_codec import decode_crop
+from .crop_codec import RAW_MAGIC, decode_crop
 from .service_backends import ClassifierBackend, build_classifier_backend
 
 log = logging.getLogger("arena.classification")
@@ -55,23 +55,22 @@ class ClassificationServicer:
         request_id_var.set(request.request_id)
         self.n_requests += 1
         try:
-            crop = await asyncio.get_running_loop().run_in_executor(self.pool, decode_crop, request.image_crop)
+            data = request.image_crop
+            if data[:4] == RAW_MAGIC:  # raw crops are a header + a view: no codec, no thread hop
+                crop = decode_crop(data)
+            else:
+                crop = await asyncio.get_running_loop().run_in_executor(self.pool, decode_crop, data)
             t1 = time.perf_counter()
             idx, _logit, prob = await self.backend.classify(crop)
             t2 = time.perf_counter()
-            resp = pb.ClassificationResponse(request_id=request.request_id)
-            cid = int(idx[0])
-            resp.result.class_id = cid
-            resp.result.class_name = self._name(cid)
-            resp.result.confidence = float(prob[0])
-            for k in range(len(idx)):
-                resp.top_k.add(class_id=int(idx[k]), class_name=self._name(int(idx[k])), confidence=float(prob[k]))
+            ids, probs = idx.tolist(), prob.tolist()
+            top = [pb.ClassificationResult(class_id=c, class_name=self._name(c), confidence=p)
+                   for c, p in zip(ids, probs)]
             t3 = time.perf_counter()
-            resp.timing.preprocessing_ms = (t1 - t0) * 1e3
-            resp.timing.inference_ms = (t2 - t1) * 1e3
-            resp.timing.postprocessing_ms = (t3 - t2) * 1e3
-            resp.timing.total_ms = (t3 - t0) * 1e3
-            return resp
+            return pb.ClassificationResponse(
+                request_id=request.request_id, result=top[0], top_k=top,
+                timing=pb.TimingInfo(preprocessing_ms=(t1 - t0) * 1e3, inference_ms=(t2 - t1) * 1e3,
+                                     postprocessing_ms=(t3 - t2) * 1e3, total_ms=(t3 - t0) * 1e3))
         except Exception as e:  # in-band error, like the reference
             self.n_errors += 1
             log.error(f"Classification failed: {e}")

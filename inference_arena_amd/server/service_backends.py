@@ -14,6 +14,7 @@ CPU: fp32 torch oracles with the reference's two intra-op threads
 from __future__ import annotations
 
 import asyncio
+import os
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -208,8 +209,10 @@ def build_classifier_backend(settings) -> ClassifierBackend:
                                                                               "intra_op_num_threads")))
     from .backends import settings_devices
 
+    # one classification batch holds the crops of about one detection batch (reference fan-out mu = 4)
     return GpuClassifierBackend(mnet, device=int(settings.ARENA_GPU), devices=settings_devices(settings),
-                                max_batch=max(32, int(settings.ARENA_MAX_BATCH)),
+                                max_batch=int(os.environ.get("ARENA_CLS_MAX_BATCH", "0"))
+                                or max(32, 4 * int(settings.ARENA_MAX_BATCH)),
                                 max_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))
 
 

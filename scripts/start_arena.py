@@ -51,17 +51,20 @@ def classification_ports(n: int, base: int = 8201) -> list[int]:
     return [base + 10 * i for i in range(max(1, n))]
 
 
-def plan_microservices(gpus: int, split: bool = False) -> dict:
-    """GPU assignment of the microservices arm: detection GPUs, classification (GPU, port) pairs."""
+def plan_microservices(gpus: int, split: bool = False, cls_procs_per_gpu: int = 1) -> dict:
+    """GPU assignment of the microservices arm: detection GPUs, classification (GPU, port) pairs —
+    ``cls_procs_per_gpu`` classification processes per GPU (ports 8201+10*i+k), all behind the detection
+    services' least-outstanding channel pool, so the per-crop Python gRPC work scales past one process."""
     if split and gpus >= 2:
         det = list(range(gpus // 2))
         cls = list(range(gpus // 2, gpus))
     else:
         det = list(range(max(1, gpus)))
         cls = list(range(max(1, gpus)))
-    ports = classification_ports(len(cls))
-    return {"detection_gpus": det, "classification": list(zip(cls, ports)),
-            "endpoint": ",".join(f"127.0.0.1:{p}" for p in ports)}
+    k = max(1, int(cls_procs_per_gpu))
+    pairs = [(g, p + j) for g, p in zip(cls, classification_ports(len(cls))) for j in range(k)]
+    return {"detection_gpus": det, "classification": pairs,
+            "endpoint": ",".join(f"127.0.0.1:{p}" for _, p in pairs)}
 
 
 def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = "model_repository",
@@ -75,10 +78,11 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
                             "--port", "8100", "--procs-per-gpu", str(procs_per_gpu)], env, log_dir, "monolithic"))
         ok = wait_http("http://127.0.0.1:8100/health", 600, procs)
     elif arch == "microservices":
-        plan = plan_microservices(gpus, split)
+        plan = plan_microservices(gpus, split, int(os.environ.get("ARENA_CLS_PROCS_PER_GPU", "1")))
         for g, port in plan["classification"]:
             procs.append(spawn(["inference_arena_amd.server.classification_service"],
-                               dict(env, PORT=str(port), ARENA_GPU=str(g)), log_dir, f"classification_gpu{g}"))
+                               dict(env, PORT=str(port), ARENA_GPU=str(g)), log_dir,
+                               f"classification_gpu{g}_{port}"))
         time.sleep(1)
         det = plan["detection_gpus"]
         procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "detection", "--gpus", str(len(det)),

@@ -62,6 +62,9 @@ def test_microservices_gpu_plan():
     s = plan_microservices(8, split=True)
     assert s["detection_gpus"] == [0, 1, 2, 3] and [g for g, _ in s["classification"]] == [4, 5, 6, 7]
     assert plan_microservices(1, split=True)["detection_gpus"] == [0]
+    m = plan_microservices(2, cls_procs_per_gpu=3)  # several classification processes per GPU
+    assert m["classification"] == [(0, 8201), (0, 8202), (0, 8203), (1, 8211), (1, 8212), (1, 8213)]
+    assert len(m["endpoint"].split(",")) == 6
 
 
 def test_classification_pool_least_outstanding():
