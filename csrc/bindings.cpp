@@ -508,7 +508,8 @@ PYBIND11_MODULE(_C, m) {
       .def("buckets", &SplitInstance::buckets);
 
   py::class_<EchoInstance, std::shared_ptr<EchoInstance>>(m, "EchoInstance")
-      .def(py::init<int, int, int>(), py::arg("slots") = 2, py::arg("max_batch") = 32, py::arg("max_det") = 4);
+      .def(py::init<int, int, int, int>(), py::arg("slots") = 2, py::arg("max_batch") = 32, py::arg("max_det") = 4,
+           py::arg("latency_us") = 0);
 
   py::class_<DynamicBatcher>(m, "DynamicBatcher")
       .def(py::init([](py::list executors, const py::dict& cfg) {

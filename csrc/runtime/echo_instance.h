@@ -6,7 +6,9 @@
 #pragma once
 #include <algorithm>
 #include <cstring>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <vector>
 
@@ -16,8 +18,10 @@ namespace arena {
 
 class EchoInstance : public BatchInstance {
  public:
-  EchoInstance(int slots, int max_batch, int max_det = 4) : slots_(slots), max_batch_(max_batch), max_det_(max_det),
-                                                            results_(slots), busy_(slots, false) {}
+  // latency_us: collect() returns no earlier than this long after submit (a stand-in for device time)
+  EchoInstance(int slots, int max_batch, int max_det = 4, int latency_us = 0)
+      : slots_(slots), max_batch_(max_batch), max_det_(max_det), latency_us_(latency_us), results_(slots),
+        busy_(slots, false), t_submit_(slots) {}
   std::vector<int> buckets() const override {
     std::vector<int> b;
     for (int v = 1; v < max_batch_; v *= 2) b.push_back(v);
@@ -70,20 +74,28 @@ class EchoInstance : public BatchInstance {
     r.total_crops = total;
     results_[s] = std::move(r);
     busy_[s] = true;
+    t_submit_[s] = std::chrono::steady_clock::now();
     return s;
   }
 
   BatchResult collect(int slot) override {
+    std::chrono::steady_clock::time_point due;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (slot < 0 || slot >= slots_ || !busy_[slot]) throw std::runtime_error("EchoInstance: bad slot");
+      due = t_submit_[slot] + std::chrono::microseconds(latency_us_);
+    }
+    std::this_thread::sleep_until(due);
     std::lock_guard<std::mutex> lk(mu_);
-    if (slot < 0 || slot >= slots_ || !busy_[slot]) throw std::runtime_error("EchoInstance: bad slot");
     busy_[slot] = false;
     return std::move(results_[slot]);
   }
 
  private:
-  int slots_, max_batch_, max_det_;
+  int slots_, max_batch_, max_det_, latency_us_;
   std::vector<BatchResult> results_;
   std::vector<bool> busy_;
+  std::vector<std::chrono::steady_clock::time_point> t_submit_;
   std::mutex mu_;
 };
 

@@ -30,7 +30,6 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ..processing import load_image_from_bytes
 from ..repository import model_config as mc
 from ..repository.store import ARCHS, ModelEntry, load_module, scan_repository
 from .batching import AsyncBatcher
@@ -195,7 +194,11 @@ class PipelineModel(ModelHandle):
         mnet = load_module(cls_e.model_file(), cls_e.name)
         params = {k: v.string_value for k, v in entry.config.parameters.items()}
         self.device = device
-        self.decode_pool = ThreadPoolExecutor(max_workers=max(1, decode_threads), thread_name_prefix="ms-decode")
+        # ARENA_DECODE_PROCS > 0: spawned decode processes with shared-memory delivery (PIL's numpy
+        # conversion holds the GIL, so decode threads serialise against the gRPC handlers)
+        from .app_common import DecodePool
+
+        self.decode_pool = DecodePool(decode_threads)
         if device == "gpu":
             from .backends import GpuBatchedBackend
 
@@ -225,8 +228,7 @@ class PipelineModel(ModelHandle):
             if raw.size != 1:
                 raise InferError("IMAGE_BYTES must hold exactly one encoded image")
             try:
-                img = await asyncio.get_running_loop().run_in_executor(self.decode_pool, load_image_from_bytes,
-                                                                       bytes(raw[0]))
+                img = await self.decode_pool.decode(bytes(raw[0]))
             except Exception as e:
                 raise InferError(str(e)) from e
         else:
@@ -244,7 +246,7 @@ class PipelineModel(ModelHandle):
 
     def close(self) -> None:
         self.backend.close()
-        self.decode_pool.shutdown(wait=False)
+        self.decode_pool.close()
 
 
 class ModelServer:

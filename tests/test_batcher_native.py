@@ -45,3 +45,33 @@ def test_batcher_stress_under_sanitizer(sanitizer):
     assert "ThreadSanitizer" not in report and "AddressSanitizer" not in report, report[-6000:]
     assert r.returncode == 0, report[-6000:]
     assert "batcher_stress: ok" in r.stdout
+
+
+
+def test_arrivals_merge_while_a_batch_is_in_flight():
+    """Requests trickling in (1 per ms) while the instance is busy (10 ms of 'device' time per batch,
+    EchoInstance latency_us) are merged into the next batch rather than launched one by one: the instance
+    loop blocks on the oldest in-flight batch before it looks at the queue again (batcher.cpp)."""
+    import threading
+    import time
+
+    import numpy as np
+
+    from inference_arena_amd.ops import native
+
+    C = native()
+    b = C.DynamicBatcher([C.EchoInstance(4, 32, 4, 10000)], {"max_batch": 32, "max_queue_delay_us": 500})
+    done = threading.Semaphore(0)
+    img = np.full((8, 8, 3), 7, np.uint8)
+    t0 = time.perf_counter()
+    for _ in range(40):
+        assert b.enqueue(img, lambda d: done.release()) >= 0
+        time.sleep(0.001)
+    for _ in range(40):
+        assert done.acquire(timeout=10)
+    elapsed = time.perf_counter() - t0
+    hist = b.stats()["batch_hist"]
+    b.shutdown()
+    sizes = [n for n, c in enumerate(hist) for _ in range(c)]
+    assert sum(sizes) == 40 and len(sizes) <= 10 and max(sizes) >= 5, sizes
+    assert elapsed >= 0.01  # the simulated device time was honoured
