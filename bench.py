@@ -5,7 +5,7 @@ YOLOv5n -> MobileNetV2 request pipeline on 1..8 MI355X (BASELINE.json metric).
 Metric definition (reference protocol: closed-loop users sending JPEG uploads and timing
 each request end to end, reference experiment.yaml:178-181,300-318):
 
-* every rank (one per GPU) runs ``--users`` closed-loop clients.  A client sends one
+* every rank (one per GPU) runs ``--users`` (256) closed-loop clients.  A client sends one
   encoded JPEG of the curated synthetic workload (3-5 detections per image, mean 4: the
   reference's thesis test-set protocol), waits for its result and immediately sends the
   next one.  A request is timed from the moment its JPEG bytes are handed to the server
@@ -275,7 +275,10 @@ def main(argv=None) -> int:
     ap.add_argument("--min-warmup-s", type=float, default=2.0, help="minimum warm-up time of the closed loop")
     ap.add_argument("--batch", type=int, default=32, help="dynamic batcher max_batch")
     ap.add_argument("--step-batches", type=int, default=8, help="batches of --batch requests per step")
-    ap.add_argument("--users", type=int, default=192, help="closed-loop clients per GPU")
+    # 256: enough requests in flight that every dynamic batch is full (4 staging slots x 32 on the device plus
+    # the decode pipeline); 192 left the batcher short (mean batch 30.5: 7.0k vs 7.5k req/s, P50 25 vs 33 ms;
+    # profiles/r2_final_bench_20steps.json vs r2_bench_users256.json)
+    ap.add_argument("--users", type=int, default=256, help="closed-loop clients per GPU")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--decode-workers", type=int, default=0, help="JPEG decode processes per rank (0: auto)")
     ap.add_argument("--queue-delay-us", type=int, default=2000)
