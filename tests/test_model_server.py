@@ -244,3 +244,51 @@ def test_gateway_modes_agree(model_server):
     da = [(round(d["detection"]["x1"], 1), d["classification"]["class_id"]) for d in a["detections"]]
     db = [(round(d["detection"]["x1"], 1), d["classification"]["class_id"]) for d in b["detections"]]
     assert sorted(da) == sorted(db)
+
+
+def test_gateway_native_handler_front_matches_fastapi(model_server):
+    """ARENA_NATIVE_HTTP=1 gateway (server/native_handler.py): the C++ HTTP layer + the same predict_bytes
+    coroutine give the FastAPI route's detections; /health answers natively."""
+    import asyncio
+    import http.client
+    import json
+    import threading
+
+    from inference_arena_amd.data.curator import workload_images
+    from inference_arena_amd.server.gateway import create_app
+    from inference_arena_amd.server.multipart import encode_multipart
+    from inference_arena_amd.server.native_handler import serve_app
+    from inference_arena_amd.utils.settings import Settings
+
+    ref = _gateway_predict(model_server, "pipeline")
+    s = Settings(LOG_LEVEL="WARNING", TRITON_GRPC_ENDPOINT=f"127.0.0.1:{model_server.port}",
+                 ARENA_GATEWAY_MODE="pipeline", TRITON_TIMEOUT_SECONDS=30)
+    box, ready = {}, threading.Event()
+    loop = asyncio.new_event_loop()
+
+    async def main():
+        box["stop"] = asyncio.Event()
+        box["rc"] = await serve_app(create_app(s), port=0, host="127.0.0.1", stop=box["stop"],
+                                    on_ready=lambda srv: (box.__setitem__("srv", srv), ready.set()))
+
+    t = threading.Thread(target=lambda: loop.run_until_complete(main()), daemon=True)
+    t.start()
+    assert ready.wait(60)
+    try:
+        body, ctype = encode_multipart("file", encode_jpeg(workload_images(1)[0]))
+        c = http.client.HTTPConnection("127.0.0.1", box["srv"].port, timeout=60)
+        c.request("POST", "/predict", body=body, headers={"Content-Type": ctype})
+        r = c.getresponse()
+        js = json.loads(r.read())
+        assert r.status == 200, js
+        c.request("GET", "/health")
+        h = c.getresponse()
+        assert h.status == 200 and json.loads(h.read())["status"] == "healthy"
+        c.close()
+    finally:
+        loop.call_soon_threadsafe(box["stop"].set)
+        t.join(30)
+    assert box["rc"] == 0
+    got = sorted((round(d["detection"]["x1"], 1), d["classification"]["class_id"]) for d in js["detections"])
+    want = sorted((round(d["detection"]["x1"], 1), d["classification"]["class_id"]) for d in ref["detections"])
+    assert got == want and len(got) >= 3
