@@ -22,7 +22,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
-def replays(path: Path, n_ops: int, keep: int):
+def replays(path: Path, n_ops: int, keep: int, first: str = "letterbox"):
     rows = [r for r in csv.DictReader(open(path)) if "arena::" in r["Kernel_Name"]]
     by_dispatch = defaultdict(dict)
     names = {}
@@ -31,8 +31,7 @@ def replays(path: Path, n_ops: int, keep: int):
         by_dispatch[d][r["Counter_Name"]] = float(r["Counter_Value"])
         names[d] = r["Kernel_Name"]
     order = sorted(by_dispatch)
-    starts = [i for i, d in enumerate(order) if "letterbox" in names[d] or "stem_fused_kernel<0" in names[d]
-              or "stem2_kernel" in names[d]]
+    starts = [i for i, d in enumerate(order) if first in names[d]]
     out = []
     for s in starts:
         seq = order[s:s + n_ops]
@@ -44,7 +43,7 @@ def replays(path: Path, n_ops: int, keep: int):
 def main(argv=None) -> int:
     from inference_arena_amd.engine.plans import plan_pipeline
     from inference_arena_amd.models.zoo import default_models
-    from tools.analyze_trace import KIND, describe
+    from tools.analyze_trace import KIND, describe, first_kernel
 
     ap = argparse.ArgumentParser()
     ap.add_argument("csvs", nargs="+")
@@ -57,7 +56,7 @@ def main(argv=None) -> int:
     vals = defaultdict(lambda: defaultdict(list))
     kname = {}
     for f in a.csvs:
-        for rp in replays(Path(f), n_ops, a.replays):
+        for rp in replays(Path(f), n_ops, a.replays, first_kernel(prog.ops[0])):
             for k, (name, cnt) in enumerate(rp):
                 kname[k] = name.replace("void arena::", "").split("(")[0]
                 for c, v in cnt.items():

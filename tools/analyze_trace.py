@@ -46,6 +46,16 @@ def describe(rec) -> str:
     return ""
 
 
+def first_kernel(op0) -> str:
+    """Name fragment of the kernel that starts one replay of the program (its first op)."""
+    first = FIRST_KERNEL.get(int(op0[0]), "letterbox")
+    if int(op0[0]) == 15:  # detector stem: single-stage kernel or letterbox+stem+conv (stem2_kernel)
+        first = "stem2_kernel" if int(op0[20]) else "stem_fused_kernel<0"
+    if int(op0[0]) == 1 and int(op0[1]) == -12:  # fp32 stem conv sampling the letterboxed images (BUF_POOL)
+        first = "conv_x3_h16_kernel<1, true>"
+    return first
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -67,12 +77,7 @@ def main(argv=None) -> int:
     by_q = defaultdict(list)
     for r in rows:
         by_q[r[qkey] if qkey else 0].append(r)
-    op0 = prog.ops[0]
-    first = FIRST_KERNEL.get(int(op0[0]), "letterbox")
-    if int(op0[0]) == 15:  # detector stem: single-stage kernel or letterbox+stem+conv (stem2_kernel)
-        first = "stem2_kernel" if int(op0[20]) else "stem_fused_kernel<0"
-    if int(op0[0]) == 1 and int(op0[1]) == -12:  # fp32 stem conv sampling the letterboxed images (BUF_POOL)
-        first = "conv_x3_h16_kernel<1, true>"
+    first = first_kernel(prog.ops[0])
     replays = []
     for q in by_q.values():
         q.sort(key=lambda r: int(r["Start_Timestamp"]))
