@@ -234,3 +234,25 @@ def test_fused_c3_matches_unfused(dense_models, device, monkeypatch):
         assert abs(len(x) - len(y)) <= 1
         if len(x) == len(y) and len(x):
             np.testing.assert_allclose(y.boxes, x.boxes, atol=1.5)
+
+
+def test_overflow_passes_serialised_two_in_flight(dense_models, device, monkeypatch):
+    """ARENA_CONCURRENT=0 (one stream, two slots): with two batches in flight, collect() of the first runs its
+    overflow classification passes after the second batch's graph — every slot owns its arena and crop plan,
+    so the results equal those of each batch run alone (aliased arenas mixed the batches)."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    monkeypatch.setenv("ARENA_CONCURRENT", "0")
+    tiny = GpuPipeline(*dense_models, device=0, buckets=[4], crop_cap_per_image=1, dtype="bf16")
+    monkeypatch.delenv("ARENA_CONCURRENT")
+    big = GpuPipeline(*dense_models, device=0, buckets=[4], crop_cap_per_image=64, dtype="bf16")
+    a_imgs, b_imgs = synthetic_images(4, 21), synthetic_images(4, 45)
+    sa = tiny.submit(a_imgs)
+    sb = tiny.submit(b_imgs)  # second batch in flight before the first is collected
+    ra, rb = tiny.collect(sa, len(a_imgs)), tiny.collect(sb, len(b_imgs))
+    assert sum(len(r) for r in ra) > 16  # the first batch needs overflow passes (pass capacity 16)
+    for got, imgs in ((ra, a_imgs), (rb, b_imgs)):
+        for x, y in zip(got, big.infer(imgs)):
+            np.testing.assert_array_equal(x.topk_idx, y.topk_idx)
+            np.testing.assert_allclose(x.topk_logit, y.topk_logit, rtol=1e-5, atol=1e-5)
