@@ -1651,22 +1651,25 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- depthwise 3x3 (fp32)
-// One thread = 4 consecutive channels (one float4) of a vertical strip of R
-// output rows; the (R-1)*S+3 input rows are loaded once per strip and the 9
-// taps' weights stay in registers.  Consecutive threads take consecutive
-// channel groups of the same pixel (coalesced NHWC rows).
-template <int R, int S>
+// One thread = 4 consecutive channels (one float4) of an R-row x CX-column
+// output block; each of the (R-1)*S+3 input rows is loaded once per block as
+// (CX-1)*S+3 float4 columns (CX = 2 at stride 1: 24 loads for 8 outputs instead
+// of 18 for 4), and the 9 taps' weights stay in registers.  Consecutive
+// threads take consecutive channel groups of the same pixel (coalesced NHWC
+// rows).  Every output sums bias + taps in (ky, kx) order, as a plain 3x3 loop.
+template <int R, int S, int CX>
 __global__ __launch_bounds__(256) void dwconv_f32_kernel(const DwParams p) {
   const int B = live_batch(p.B, p.bdev);
   const int cg = p.C >> 2;
   const int strips = (p.Ho + R - 1) / R;
-  const int total = B * strips * p.Wo * cg;
+  const int colb = (p.Wo + CX - 1) / CX;
+  const int total = B * strips * colb * cg;
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= total) return;
   const int g = tid % cg;
   int t = tid / cg;
-  const int ox = t % p.Wo;
-  t /= p.Wo;
+  const int ox0 = (t % colb) * CX;
+  t /= colb;
   const int st = t % strips;
   const int b = t / strips;
   const int c0 = g * 4;
@@ -1677,32 +1680,37 @@ __global__ __launch_bounds__(256) void dwconv_f32_kernel(const DwParams p) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) wt[k] = *(const float4*)(w + k * p.C);
   const float4 bias = *(const float4*)(p.bias + c0);
-  float4 acc[R];
+  float4 acc[R][CX];
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = bias;
-  constexpr int NIN = (R - 1) * S + 3;
-  const int iy0 = oy0 * S - 1, ix0 = ox * S - 1;
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < CX; ++c) acc[r][c] = bias;
+  constexpr int NIN = (R - 1) * S + 3, NCOL = (CX - 1) * S + 3;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
 #pragma unroll
   for (int ri = 0; ri < NIN; ++ri) {
     const int iy = iy0 + ri;
     if ((unsigned)iy >= (unsigned)p.H) continue;
     const float* row = x + (size_t)iy * p.W * p.xs;
-    float4 v[3];
+    float4 v[NCOL];
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx)
-      v[kx] = load_f4_or_zero(row + (ix0 + kx) * p.xs, x, (unsigned)(ix0 + kx) < (unsigned)p.W);
+    for (int q = 0; q < NCOL; ++q)
+      v[q] = load_f4_or_zero(row + (ix0 + q) * p.xs, x, (unsigned)(ix0 + q) < (unsigned)p.W);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int ky = ri - r * S;
       if (ky < 0 || ky > 2) continue;  // compile-time after unrolling
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const float4 ww = wt[ky * 3 + kx];
-        acc[r].x = fmaf(v[kx].x, ww.x, acc[r].x);
-        acc[r].y = fmaf(v[kx].y, ww.y, acc[r].y);
-        acc[r].z = fmaf(v[kx].z, ww.z, acc[r].z);
-        acc[r].w = fmaf(v[kx].w, ww.w, acc[r].w);
-      }
+      for (int c = 0; c < CX; ++c)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float4 ww = wt[ky * 3 + kx];
+          const float4 vv = v[c * S + kx];
+          acc[r][c].x = fmaf(vv.x, ww.x, acc[r][c].x);
+          acc[r][c].y = fmaf(vv.y, ww.y, acc[r][c].y);
+          acc[r][c].z = fmaf(vv.z, ww.z, acc[r][c].z);
+          acc[r][c].w = fmaf(vv.w, ww.w, acc[r][c].w);
+        }
     }
   }
   float* y = (float*)p.y + (size_t)b * p.Ho * p.Wo * p.ys + c0;
@@ -1710,28 +1718,42 @@ __global__ __launch_bounds__(256) void dwconv_f32_kernel(const DwParams p) {
   for (int r = 0; r < R; ++r) {
     const int oy = oy0 + r;
     if (oy >= p.Ho) break;
-    const float4 o = make_float4(apply_act(acc[r].x, p.act), apply_act(acc[r].y, p.act), apply_act(acc[r].z, p.act),
-                                 apply_act(acc[r].w, p.act));
-    *(float4*)(y + (size_t)(oy * p.Wo + ox) * p.ys) = o;
+#pragma unroll
+    for (int c = 0; c < CX; ++c) {
+      const int ox = ox0 + c;
+      if (ox >= p.Wo) break;
+      const float4 a = acc[r][c];
+      *(float4*)(y + (size_t)(oy * p.Wo + ox) * p.ys) =
+          make_float4(apply_act(a.x, p.act), apply_act(a.y, p.act), apply_act(a.z, p.act), apply_act(a.w, p.act));
+    }
   }
 }
 
-template <int R, int S>
+template <int R, int S, int CX>
 static void dw_f32_launch(const DwParams& p, hipStream_t s) {
-  const long total = (long)p.B * ((p.Ho + R - 1) / R) * p.Wo * (p.C / 4);
+  const long total = (long)p.B * ((p.Ho + R - 1) / R) * ((p.Wo + CX - 1) / CX) * (p.C / 4);
   if (total <= 0) return;
   if (total >= (1L << 31) || (long)p.B * p.H * p.W * p.xs >= (1L << 31))
     throw std::runtime_error("dwconv3x3_f32: too large");
-  hipLaunchKernelGGL((dwconv_f32_kernel<R, S>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((dwconv_f32_kernel<R, S, CX>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+}
+
+static int dw_f32_cols() {  // ARENA_DW_CX=1: the one-column variant (A/B switch)
+  static const int v = [] {
+    const char* e = std::getenv("ARENA_DW_CX");
+    return (e != nullptr && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  return v;
 }
 
 void dwconv3x3_f32(const DwParams& p, hipStream_t s) {
   if (p.C % 4 != 0 || p.xs % 4 != 0 || p.ys % 4 != 0)
     throw std::runtime_error("dwconv3x3_f32: C, xs, ys must be multiples of 4");
+  const bool two = dw_f32_cols() == 2;
   if (p.stride == 1)
-    dw_f32_launch<4, 1>(p, s);
+    two ? dw_f32_launch<4, 1, 2>(p, s) : dw_f32_launch<4, 1, 1>(p, s);
   else if (p.stride == 2)
-    dw_f32_launch<2, 2>(p, s);
+    two ? dw_f32_launch<2, 2, 2>(p, s) : dw_f32_launch<2, 2, 1>(p, s);
   else
     throw std::runtime_error("dwconv3x3_f32: stride must be 1 or 2");
 }
