@@ -62,6 +62,12 @@ def test_microservices_gpu_plan():
     s = plan_microservices(8, split=True)
     assert s["detection_gpus"] == [0, 1, 2, 3] and [g for g, _ in s["classification"]] == [4, 5, 6, 7]
     assert plan_microservices(1, split=True)["detection_gpus"] == [0]
+    from start_arena import _queue_env, hw_queues_per_process
+
+    # hardware queues per process when several GPU processes share a device (HIP default 4 up to 3 processes)
+    assert [hw_queues_per_process(n) for n in (1, 3, 4, 5, 6, 11)] == [None, None, 2, 2, 1, 1]
+    assert _queue_env({}, 5) == {"GPU_MAX_HW_QUEUES": "2"} and _queue_env({}, 2) == {}
+    assert _queue_env({"GPU_MAX_HW_QUEUES": "4"}, 5) == {"GPU_MAX_HW_QUEUES": "4"}  # explicit setting wins
     m = plan_microservices(2, cls_procs_per_gpu=3)  # several classification processes per GPU
     assert m["classification"] == [(0, 8201), (0, 8202), (0, 8203), (1, 8211), (1, 8212), (1, 8213)]
     assert len(m["endpoint"].split(",")) == 6
