@@ -9,10 +9,10 @@ for q in default 2; do
   O=gpurun_out/micro_hwq_$q
   mkdir -p $O
   if [ $q = default ]; then
-    timeout -k 10 400 python scripts/serving_sweep.py --archs microservices --users ${USERS:-1,10,100} --procs 4 \
+    ARENA_HW_QUEUES=4 timeout -k 10 400 python scripts/serving_sweep.py --archs microservices --users ${USERS:-1,10,100} --procs 4 \
       --procs-per-gpu 3 --out $O > $O/sweep.log 2>&1
   else
-    GPU_MAX_HW_QUEUES=$q timeout -k 10 400 python scripts/serving_sweep.py --archs microservices --users ${USERS:-1,10,100} \
+    ARENA_HW_QUEUES=$q timeout -k 10 400 python scripts/serving_sweep.py --archs microservices --users ${USERS:-1,10,100} \
       --procs 4 --procs-per-gpu 3 --out $O > $O/sweep.log 2>&1
   fi
   grep "users=" $O/sweep.log

@@ -6,7 +6,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1 ARENA_NATIVE_HTTP=1 LOG_LEVEL=WARNING AREN
 for q in 4 2; do
   O=gpurun_out/triton_hwq_$q
   mkdir -p $O
-  GPU_MAX_HW_QUEUES=$q timeout -k 10 400 python scripts/serving_sweep.py --archs triton --users ${USERS:-1,10,100} \
+  ARENA_HW_QUEUES=$q timeout -k 10 400 python scripts/serving_sweep.py --archs triton --users ${USERS:-1,10,100} \
     --procs 4 --procs-per-gpu 3 --out $O > $O/sweep.log 2>&1
   grep "users=" $O/sweep.log
 done

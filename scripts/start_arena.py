@@ -77,10 +77,12 @@ def hw_queues_per_process(procs_on_gpu: int) -> int | None:
 
 
 def _queue_env(env: dict, procs_on_gpu: int) -> dict:
+    """The children's environment with the queue cap applied.  ``ARENA_HW_QUEUES`` overrides the cap; an
+    inherited ``GPU_MAX_HW_QUEUES`` does not (the GPU pool exports HIP's default 4 to every job)."""
+    if env.get("ARENA_HW_QUEUES"):
+        return dict(env, GPU_MAX_HW_QUEUES=str(int(env["ARENA_HW_QUEUES"])))
     q = hw_queues_per_process(procs_on_gpu)
-    if q is None or "GPU_MAX_HW_QUEUES" in env:  # an explicit setting wins
-        return env
-    return dict(env, GPU_MAX_HW_QUEUES=str(q))
+    return env if q is None else dict(env, GPU_MAX_HW_QUEUES=str(q))
 
 
 def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = "model_repository",

@@ -67,7 +67,8 @@ def test_microservices_gpu_plan():
     # hardware queues per process when several GPU processes share a device (HIP default 4 up to 3 processes)
     assert [hw_queues_per_process(n) for n in (1, 3, 4, 5, 6, 11)] == [None, None, 2, 2, 1, 1]
     assert _queue_env({}, 5) == {"GPU_MAX_HW_QUEUES": "2"} and _queue_env({}, 2) == {}
-    assert _queue_env({"GPU_MAX_HW_QUEUES": "4"}, 5) == {"GPU_MAX_HW_QUEUES": "4"}  # explicit setting wins
+    assert _queue_env({"GPU_MAX_HW_QUEUES": "4"}, 5) == {"GPU_MAX_HW_QUEUES": "2"}  # inherited default: capped
+    assert _queue_env({"ARENA_HW_QUEUES": "3"}, 5)["GPU_MAX_HW_QUEUES"] == "3"  # explicit arena override wins
     m = plan_microservices(2, cls_procs_per_gpu=3)  # several classification processes per GPU
     assert m["classification"] == [(0, 8201), (0, 8202), (0, 8203), (1, 8211), (1, 8212), (1, 8213)]
     assert len(m["endpoint"].split(",")) == 6
