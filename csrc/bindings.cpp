@@ -650,6 +650,11 @@ PYBIND11_MODULE(_C, m) {
         return new HttpFrontEnd(nullptr, DecodeChannel{}, {}, c);
       }))
       .def_property_readonly("handler_mode", &HttpFrontEnd::handler_mode)
+      .def("drain", [](HttpFrontEnd& f) {
+        py::gil_scoped_release nogil;
+        f.drain();
+      })
+      .def("handler_pending", &HttpFrontEnd::handler_pending)
       .def(
           "take",
           [](HttpFrontEnd& f, int max_n, int timeout_ms) {

@@ -274,6 +274,19 @@ void HttpFrontEnd::stop() {
   pending_.clear();
 }
 
+void HttpFrontEnd::drain() {
+  std::lock_guard<std::mutex> lk(drain_mu_);
+  if (drained_ || listen_fd_ < 0) return;
+  drained_ = true;
+  for (int ep : epfds_) epoll_ctl(ep, EPOLL_CTL_DEL, listen_fd_, nullptr);
+  ::shutdown(listen_fd_, SHUT_RDWR);  // the fd itself is closed by stop(), after the I/O threads joined
+}
+
+int HttpFrontEnd::handler_pending() {
+  std::lock_guard<std::mutex> lk(hq_mu_);
+  return (int)hpend_.size();
+}
+
 std::vector<HandlerRequest> HttpFrontEnd::take(int max_n, int timeout_ms) {
   std::vector<HandlerRequest> out;
   std::unique_lock<std::mutex> lk(hq_mu_);

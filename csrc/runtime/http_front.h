@@ -108,6 +108,11 @@ class HttpFrontEnd {
   // Returns false when the key is unknown (connection gone, already answered).
   bool complete(uint64_t key, int code, const std::string& body, int n_det = 0);
   bool handler_mode() const { return cfg_.handler_mode; }
+  // Stop accepting: the listening socket leaves the epoll sets and is shut down (Linux unhashes it, so an
+  // SO_REUSEPORT group stops routing new connections here); open connections keep being served.
+  void drain();
+  // handler mode: requests queued or inside the Python handler
+  int handler_pending();
 
   struct Conn;
   struct Pending;
@@ -152,6 +157,9 @@ class HttpFrontEnd {
   std::condition_variable hq_cv_;
   std::deque<HandlerRequest> hq_;
   std::unordered_map<uint64_t, std::shared_ptr<HandlerPending>> hpend_;  // queued or in the handler
+
+  std::mutex drain_mu_;
+  bool drained_ = false;
 
   std::mutex metrics_mu_;
   std::string metrics_text_;

@@ -153,6 +153,7 @@ def serve(settings: Settings | None = None, *, weights=None, replica_tag: str = 
         if batcher.stats()["failed"] > 0:  # a failed batch = a device fault: leave rotation, let the launcher restart
             log.error("device fault: batches failed; exiting for a restart")
             front.set_healthy(False)
+            front.fe.drain()  # leave the SO_REUSEPORT group; answer what is in flight
             time.sleep(1.0)
             rc = 3
             break

@@ -90,6 +90,13 @@ class NativeHandlerServer:
         self._taker = threading.Thread(target=taker, name="native-handler-take", daemon=True)
         self._taker.start()
 
+    def drain(self) -> None:
+        """Stop accepting connections; open connections and queued requests are still answered."""
+        self.fe.drain()
+
+    def pending(self) -> int:
+        return int(self.fe.handler_pending())
+
     def close(self) -> None:
         self._stop.set()
         self.fe.stop()
@@ -98,7 +105,8 @@ class NativeHandlerServer:
 
 
 async def serve_app(app, *, port: int, host: str = "0.0.0.0", replica_tag: str = "", io_threads: int = 2,
-                    stop: asyncio.Event | None = None, on_ready=None, reuse_port: bool = True) -> int:
+                    stop: asyncio.Event | None = None, on_ready=None, reuse_port: bool = True,
+                    drain_s: float = 10.0) -> int:
     """Run a FastAPI arm app (its lifespan, then ``state['predict_bytes']``) behind the native front end until
     ``stop`` is set or SIGTERM/SIGINT; returns 3 after a device fault (the replica supervisor restarts it)."""
     from .app_common import device_fault
@@ -136,10 +144,12 @@ async def serve_app(app, *, port: int, host: str = "0.0.0.0", replica_tag: str =
                 if metrics is not None and ticks % 5 == 1:
                     srv.set_metrics_text(metrics.render().decode())
         finally:
-            srv.close()
-            # let in-flight handlers finish their awaits before the lifespan closes the clients
-            for _ in range(50):
-                if srv.inflight == 0:
+            # like uvicorn's shutdown: leave the port first (an SO_REUSEPORT peer takes new connections), answer
+            # what is queued or in the handler (bounded), then stop the I/O threads
+            srv.drain()
+            for _ in range(int(drain_s / 0.02)):
+                if srv.pending() == 0:
                     break
                 await asyncio.sleep(0.02)
+            srv.close()
     return rc

@@ -295,3 +295,46 @@ def test_detection_service_native_handler_front(fake_server):
         loop.call_soon_threadsafe(box["stop"].set)
         t.join(30)
     assert box["rc"] == 0
+
+
+def test_native_handler_drains_in_flight_requests_on_stop():
+    """Shutdown of the handler-mode front end: the listening socket goes first (new connections are refused),
+    a request already inside the (slow) handler is still answered."""
+    import http.client
+    import json
+    import time
+
+
+    from fastapi import FastAPI
+
+    from inference_arena_amd.server.schemas import PredictResponse
+
+    app = FastAPI()
+
+    async def slow_predict(data: bytes):
+        await asyncio.sleep(0.6)
+        return PredictResponse(request_id="r", detections=[], timing={"total_ms": 600.0})
+
+    app.state.arena = {"predict_bytes": slow_predict, "healthy": lambda: True, "metrics": None}
+    box, loop, t = _native_serve(app)
+    port = box["srv"].port
+    got = {}
+
+    def client():
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=30)
+        c.request("POST", "/predict", body=b"x", headers={"Content-Type": "image/jpeg"})
+        r = c.getresponse()
+        got["status"], got["body"] = r.status, json.loads(r.read())
+
+    th = threading.Thread(target=client)
+    th.start()
+    time.sleep(0.25)  # the request is inside slow_predict
+    loop.call_soon_threadsafe(box["stop"].set)
+    time.sleep(0.15)
+    with pytest.raises(OSError):  # drained: the port no longer accepts
+        socket.create_connection(("127.0.0.1", port), timeout=2).close()
+    th.join(10)
+    t.join(30)
+    assert got.get("status") == 200 and got["body"]["request_id"] == "r"
+    assert box["rc"] == 0
+
