@@ -213,7 +213,9 @@ def build_classifier_backend(settings) -> ClassifierBackend:
     return GpuClassifierBackend(mnet, device=int(settings.ARENA_GPU), devices=settings_devices(settings),
                                 max_batch=int(os.environ.get("ARENA_CLS_MAX_BATCH", "0"))
                                 or max(32, 4 * int(settings.ARENA_MAX_BATCH)),
-                                max_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))
+                                # ARENA_CLS_QUEUE_DELAY_US: the classifier's own delay (crops arrive ~4x as often)
+                                max_queue_delay_us=int(os.environ.get("ARENA_CLS_QUEUE_DELAY_US", "0"))
+                                or int(settings.ARENA_QUEUE_DELAY_US))
 
 
 def build_detector_backend(settings) -> DetectorBackend:
