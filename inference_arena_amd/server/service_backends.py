@@ -213,9 +213,10 @@ def build_classifier_backend(settings) -> ClassifierBackend:
     return GpuClassifierBackend(mnet, device=int(settings.ARENA_GPU), devices=settings_devices(settings),
                                 max_batch=int(os.environ.get("ARENA_CLS_MAX_BATCH", "0"))
                                 or max(32, 4 * int(settings.ARENA_MAX_BATCH)),
-                                # ARENA_CLS_QUEUE_DELAY_US: the classifier's own delay (crops arrive ~4x as often)
-                                max_queue_delay_us=int(os.environ.get("ARENA_CLS_QUEUE_DELAY_US", "0"))
-                                or int(settings.ARENA_QUEUE_DELAY_US))
+                                # ARENA_CLS_QUEUE_DELAY_US (default 2 ms): the classifier's own delay; with 500 us
+                                # its batches stayed at a few crops (2.50k vs 2.86k req/s at 50 users, 2.68k vs 2.94k
+                                # at 100; 4 ms cost 27 % at 10 users; profiles/serving_r2d/cls_delay/)
+                                max_queue_delay_us=int(os.environ.get("ARENA_CLS_QUEUE_DELAY_US", "2000")))
 
 
 def build_detector_backend(settings) -> DetectorBackend:
