@@ -210,7 +210,9 @@ class PipelineModel(ModelHandle):
             self.backend = GpuBatchedBackend(yolo, mnet, device=gpu, devices=devs,
                                              instances=int(params.get("instance_count", 1)),
                                              max_batch=mb,
-                                             max_queue_delay_us=int(params.get("max_queue_delay_microseconds", 500)))
+                                             # ARENA_ENSEMBLE_QUEUE_DELAY_US overrides the config's delay
+                                             max_queue_delay_us=int(os.environ.get("ARENA_ENSEMBLE_QUEUE_DELAY_US", "0")
+                                                                    or params.get("max_queue_delay_microseconds", 500)))
         else:
             from .backends import CpuReferenceBackend
 
