@@ -526,6 +526,7 @@ PYBIND11_MODULE(_C, m) {
              c.max_batch = get<int>(cfg, "max_batch", c.max_batch);
              c.preferred = get<std::vector<int>>(cfg, "preferred", {});
              c.max_queue_delay_us = get<int64_t>(cfg, "max_queue_delay_us", c.max_queue_delay_us);
+             c.idle_queue_delay_us = get<int64_t>(cfg, "idle_queue_delay_us", c.idle_queue_delay_us);
              c.max_queue_size = get<int64_t>(cfg, "max_queue_size", c.max_queue_size);
              return new DynamicBatcher(inst, c);
            }),

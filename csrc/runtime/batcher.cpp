@@ -85,7 +85,9 @@ int64_t DynamicBatcher::enqueue(const uint8_t* data, int h, int w, ResultCallbac
 
 bool DynamicBatcher::take_batch(Batch& out, bool can_wait) {
   std::unique_lock<std::mutex> lk(mu_);
-  const auto delay = std::chrono::microseconds(cfg_.max_queue_delay_us);
+  // can_wait == no batch of this instance in flight: the idle delay applies
+  const auto delay = std::chrono::microseconds(can_wait && cfg_.idle_queue_delay_us >= 0 ? cfg_.idle_queue_delay_us
+                                                                                         : cfg_.max_queue_delay_us);
   for (;;) {
     if (q_.empty()) {
       if (stop_ || !can_wait) return false;

@@ -48,6 +48,10 @@ struct BatcherConfig {
   std::vector<int> preferred;          // preferred batch sizes (ascending)
   int64_t max_queue_delay_us = 500;
   int64_t max_queue_size = 4096;       // 0 = unbounded
+  // Delay used while the instance has no batch in flight (-1: max_queue_delay_us).  A short idle delay keeps
+  // the single-request latency low while a longer max_queue_delay_us still grows the batches once the device
+  // is busy (arrivals during device work merge into the next batch).
+  int64_t idle_queue_delay_us = -1;
 };
 
 struct BatcherStats {

@@ -51,7 +51,7 @@ class GpuClassifierBackend(ClassifierBackend):
 
     def __init__(self, mnet, *, device: int = 0, instances: int = 1, max_batch: int = 64,
                  max_queue_delay_us: int = 300, preferred: list[int] | None = None,
-                 devices: list[int] | None = None):
+                 devices: list[int] | None = None, idle_queue_delay_us: int = -1):
         from ..engine.registry import build_session
 
         bk = _default_buckets(max_batch)
@@ -59,7 +59,7 @@ class GpuClassifierBackend(ClassifierBackend):
         self.runners = [build_session("classifier", mnet=mnet, device=d, buckets=bk)
                         for d in self.devices for _ in range(instances)]
         self.batcher = AsyncBatcher(self.runners, max_batch=max_batch, preferred=preferred,
-                                    max_queue_delay_us=max_queue_delay_us)
+                                    max_queue_delay_us=max_queue_delay_us, idle_queue_delay_us=idle_queue_delay_us)
 
     def ready(self) -> bool:
         return self.batcher.healthy
@@ -216,7 +216,10 @@ def build_classifier_backend(settings) -> ClassifierBackend:
                                 # ARENA_CLS_QUEUE_DELAY_US (default 2 ms): the classifier's own delay; with 500 us
                                 # its batches stayed at a few crops (2.50k vs 2.86k req/s at 50 users, 2.68k vs 2.94k
                                 # at 100; 4 ms cost 27 % at 10 users; profiles/serving_r2d/cls_delay/)
-                                max_queue_delay_us=int(os.environ.get("ARENA_CLS_QUEUE_DELAY_US", "2000")))
+                                max_queue_delay_us=int(os.environ.get("ARENA_CLS_QUEUE_DELAY_US", "2000")),
+                                # while no batch is in flight the detection side's short delay applies, so a lone
+                                # request is not held for 2 ms (1 user: P50 6.8 ms with 2 ms, 5.1 ms with 0.5 ms)
+                                idle_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))
 
 
 def build_detector_backend(settings) -> DetectorBackend:

@@ -75,3 +75,30 @@ def test_arrivals_merge_while_a_batch_is_in_flight():
     sizes = [n for n, c in enumerate(hist) for _ in range(c)]
     assert sum(sizes) == 40 and len(sizes) <= 10 and max(sizes) >= 5, sizes
     assert elapsed >= 0.01  # the simulated device time was honoured
+
+
+def test_idle_queue_delay_applies_only_while_idle():
+    """idle_queue_delay_us: a lone request on an idle instance waits the short idle delay, not
+    max_queue_delay_us (default -1: the max delay, Triton semantics)."""
+    import threading
+    import time
+
+    import numpy as np
+
+    from inference_arena_amd.ops import native
+
+    C = native()
+    img = np.full((8, 8, 3), 7, np.uint8)
+
+    def lone_request_s(cfg) -> float:
+        b = C.DynamicBatcher([C.EchoInstance(4, 32, 4)], {"max_batch": 32, **cfg})
+        done = threading.Event()
+        t0 = time.perf_counter()
+        assert b.enqueue(img, lambda d: done.set()) >= 0
+        assert done.wait(10)
+        dt = time.perf_counter() - t0
+        b.shutdown()
+        return dt
+
+    assert lone_request_s({"max_queue_delay_us": 300000}) >= 0.25  # Triton semantics: waits for company
+    assert lone_request_s({"max_queue_delay_us": 300000, "idle_queue_delay_us": 1000}) < 0.1
