@@ -604,6 +604,8 @@ PYBIND11_MODULE(_C, m) {
              d["mean_queue_us"] = s.requests ? s.sum_queue_us / s.requests : 0.0;
              d["mean_compute_us"] = s.batches ? s.sum_compute_us / s.batches : 0.0;
              d["batch_hist"] = s.batch_hist;
+             d["device_faults"] = s.device_faults;
+             d["last_error"] = s.last_error;
              return d;
            })
       .def("shutdown", [](DynamicBatcher& b) {
@@ -632,6 +634,8 @@ PYBIND11_MODULE(_C, m) {
              c.softmax_confidence = get<bool>(cfg, "softmax_confidence", c.softmax_confidence);
              c.max_body = get<int64_t>(cfg, "max_body", c.max_body);
              c.replica_tag = get<std::string>(cfg, "replica_tag", c.replica_tag);
+             c.idle_timeout_ms = get<int64_t>(cfg, "idle_timeout_ms", c.idle_timeout_ms);
+             c.read_timeout_ms = get<int64_t>(cfg, "read_timeout_ms", c.read_timeout_ms);
              py::gil_scoped_release nogil;
              return new HttpFrontEnd(&batcher, dc, std::move(labels), c);
            }),
@@ -646,6 +650,8 @@ PYBIND11_MODULE(_C, m) {
         c.max_body = get<int64_t>(cfg, "max_body", c.max_body);
         c.replica_tag = get<std::string>(cfg, "replica_tag", c.replica_tag);
         c.max_handler_queue = get<int>(cfg, "max_queue", c.max_handler_queue);
+        c.idle_timeout_ms = get<int64_t>(cfg, "idle_timeout_ms", c.idle_timeout_ms);
+        c.read_timeout_ms = get<int64_t>(cfg, "read_timeout_ms", c.read_timeout_ms);
         c.handler_mode = true;
         py::gil_scoped_release nogil;
         return new HttpFrontEnd(nullptr, DecodeChannel{}, {}, c);
@@ -693,6 +699,7 @@ PYBIND11_MODULE(_C, m) {
              d["connections"] = s.connections;
              d["open_connections"] = s.open_connections;
              d["detections"] = s.detections;
+             d["timeouts"] = s.timeouts;
              d["sum_total_ms"] = s.sum_total_ms;
              d["sum_decode_ms"] = s.sum_decode_ms;
              d["sum_queue_ms"] = s.sum_queue_ms;

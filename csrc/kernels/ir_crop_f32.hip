@@ -1,32 +1,38 @@
-// Whole-map fused MobileNetV2 inverted residual at fp32 accuracy for the 14x14 and 7x7 stages
-// (torchvision mobilenet_v2 features[11..17]; the reference runs them as fp32 ONNX per crop,
+// Fused MobileNetV2 inverted residual at fp32 accuracy for the 14x14 and 7x7 stages
+// (torchvision mobilenet_v2 features[8..17]; the reference runs them as fp32 ONNX per crop,
 // architectures/monolithic/app/inference.py:196).
 //
-// Unfused, each of these ten blocks is three latency-bound kernels over all crops (1x1 expand GEMM
-// with K = 64..160, depthwise, 1x1 project): 85-150 us per block for 128 crops, ~1.07 ms of the fp32
-// device time per batch of 32 requests (profiles/r2_fp32_irprefetch_ops.md ops 79-108), the 1x1
-// GEMMs at 20-30 % of the fp32 matrix-core rate.  Here one workgroup owns RS = 2 row halves of one
-// crop's map (7 of 14 output rows, or 4 / 3 of 7) over OG output-channel groups, the tile spans the
-// whole map width (no halo columns, no recomputed expansion except the one or two shared input
-// rows), and every GEMM runs on the bf16 matrix cores with the triple-bf16 split of conv_f32.hip
-// (v = h + m + l exactly; six partial products, the dropped ones below fp32's own product rounding):
+// Unfused, each of these ten blocks is three kernels over all crops (1x1 expand GEMM, depthwise, 1x1
+// project): 77-134 us per block for 128 crops, 0.99 ms of the 5.18 ms fp32 device time per batch of 32
+// requests (profiles/r2_fp32_final_ops.md ops 78-107), with the expanded map crossing the memory system
+// twice.  The round-2 whole-map kernel lost to them (profiles/r2_irc_f32_experiment.md: VALU / MFMA ~10,
+// 60 % of wave cycles parked at barriers) because the depthwise recomputed its addresses and bounds per
+// tap and per chunk and went through an LDS round trip for the project operand.  This version:
 //
-//   X (the WG's input rows, all channels) ..... LDS, split into [h | m | l] bf16 planes once
-//   (weights arrive pre-split from the host, engine/planner.py::split_bf16x3)
-//   for each chunk of 32 hidden channels (2 workgroup barriers per chunk):
-//     E = relu6(We[chunk] . X + be)     x3 MFMA 16x16x32 -> fp32 LDS (XOR-swizzled 16-B groups)
-//     D = relu6(dw3x3_S(E) + bd)        fp32 FMA, zero padding = tap bounds test -> split planes
-//     Wp[:, chunk] -> split planes      (staged alongside the depthwise)
-//     acc += Wp[:, chunk] . D           x3 MFMA, accumulators in registers for the whole loop
-//   y = acc + bp (+ x from global memory)                      fp32 NHWC
+//   * one workgroup = one half (row band) of one crop, all hidden and all output channels, 8 waves;
+//     grid = 2 x crops (256 workgroups for 128 crops: one per CU);
+//   * the block input X is loaded ONCE into the expand B-operand registers of the wave that owns its
+//     16-pixel tile, already split into three bf16 planes (x = h + m + l exactly to fp32 rounding);
+//   * per chunk of HC hidden channels:
+//       E = relu6(We[chunk] . X + be)        x3 MFMA 16x16x32 -> fp32 LDS map with a zero border
+//       D = relu6(dw3x3_S(E) + bd)           fp32 FMA straight into the project B-operand registers:
+//                                            lane (pixel, 8 channels) == the MFMA fragment, no LDS trip,
+//                                            tap addresses = one base + constants (the border is the pad)
+//       acc += Wp[:, chunk] . D              x3 MFMA, accumulators in registers for the whole loop
+//   * chunk weights (pre-split bf16 planes from the host, engine/planner.py::split_bf16x3) are fetched
+//     into registers two phases ahead and stored to LDS by all threads: every weight byte leaves L2 once
+//     per workgroup; two barriers per chunk.
+//   y = acc + bp (+ x, stride 1)                                              fp32 NHWC
 //
 // Operand mapping of v_mfma_f32_16x16x32_bf16: lane l supplies A[row = l & 15][k = 8 (l >> 4) .. +7]
-// and B[k = 8 (l >> 4) .. +7][col = l & 15] and receives D[row = 4 (l >> 4) + r][col = l & 15]: the
-// expand's rows are hidden channels and its columns pixels (a lane ends with 4 consecutive hidden
-// channels of one pixel: one float4 into E), the project's rows output channels, columns pixels.
+// and B[k = 8 (l >> 4) .. +7][col = l & 15] and receives D[row = 4 (l >> 4) + r][col = l & 15].  Expand:
+// rows = hidden channels (A = We), columns = pixels (B = X).  Project: rows = output channels (A = Wp),
+// columns = output pixels (B = D).
 //
-// LDS rows that feed ds_read_b128 operand reads (16 rows x 4 k-groups per instruction) have pitches of
-// 2 (mod 4) 16-byte slots (conflict-free, MI355X_MICROARCH.md §LDS): X 6 inp + 32 B, D / Wp 224 B.
+// LDS bank notes (MI355X_MICROARCH.md §LDS: ds_read_b128 serves 16-lane groups from 16 16-B slots):
+//   * weight rows are read 16 rows x 4 k-groups per instruction: row pitch 2 (mod 4) slots;
+//   * E is stored as [channel group of 8][pixel][8 fp32] with an odd-slot plane stride: the 16-lane
+//     groups of a depthwise read mix k-groups of both parities, which then land on disjoint slot parities.
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -38,29 +44,23 @@ namespace arena {
 
 namespace {
 
-__device__ __forceinline__ void split1(float v, bf16& h, bf16& m, bf16& l) {
-  h = (bf16)v;
-  const float r = v - (float)h;
-  m = (bf16)r;
-  l = (bf16)(r - (float)m);
-}
+constexpr int IRX_THREADS = 512, IRX_WAVES = IRX_THREADS / 64;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// 4 fp32 -> three bf16x4 planes at row + {0, PLANE, 2 PLANE} bytes
-template <int PLANE>
-__device__ __forceinline__ void store_split4(uint8_t* row, const float4& v) {
-  bf16x4 h, m, l;
-  const float f[4] = {v.x, v.y, v.z, v.w};
+constexpr int imin(int a, int b) { return a < b ? a : b; }
+constexpr int imax(int a, int b) { return a > b ? a : b; }
+
+// 8 fp32 -> three bf16x8 planes with v = h + m + l (round to nearest even at each step)
+__device__ __forceinline__ void split8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    bf16 th, tm, tl;
-    split1(f[i], th, tm, tl);
+  for (int i = 0; i < 8; ++i) {
+    const bf16 th = (bf16)v[i];
+    const float r = v[i] - (float)th;
+    const bf16 tm = (bf16)r;
     h[i] = th;
     m[i] = tm;
-    l[i] = tl;
+    l[i] = (bf16)(r - (float)tm);
   }
-  *(bf16x4*)row = h;
-  *(bf16x4*)(row + PLANE) = m;
-  *(bf16x4*)(row + 2 * PLANE) = l;
 }
 
 // a*b to fp32 accuracy from the split planes; smallest terms first (added while the sum is smallest)
@@ -74,278 +74,304 @@ __device__ __forceinline__ f32x4 mfma_x3(const bf16x8& ah, const bf16x8& am, con
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float4 relu6x4(float4 v) {
-  return make_float4(relu6f(v.x), relu6f(v.y), relu6f(v.z), relu6f(v.w));
-}
-
-constexpr int imin(int a, int b) { return a < b ? a : b; }
-
 }  // namespace
 
-// HO: output side; S: stride; KS: inp_pad / 32; MT: output-channel tiles of 16 per workgroup; RS: row parts.
-// 512 threads = 8 waves, two per SIMD.  Every weight of a chunk is fetched from global memory once per
-// workgroup and staged in LDS (expand rows and depthwise taps one chunk ahead, single-buffered: each is
-// rewritten only in the phase after its last reader's barrier): per-wave register fetches of the expand
-// fragments were 4x redundant across the waves sharing a hidden tile and, with per-thread depthwise taps,
-// made the vector-memory path the bottleneck (tools/bench_irc.py: 34-143 us per block with every MFMA off).
-constexpr int IRC_THREADS = 512, IRC_WAVES = IRC_THREADS / 64;
-
-template <int HO, int S, int KS, int MT, int RS>
-struct IrcGeom {
-  static constexpr int HI = HO * S;                                  // input side
-  static constexpr int NOR = RS == 1 ? HO : (HO + 1) / 2;            // output rows of part 0 (the larger)
-  static constexpr int IR = RS == 1 ? HI : imin(HI, (NOR - 1) * S + 2);  // input rows of part 0 (>= part 1)
-  static constexpr int PIN_PAD = (IR * HI + 15) / 16 * 16;
-  static constexpr int NE = PIN_PAD / 16;                            // expand pixel tiles
-  static constexpr int NP = (NOR * HO + 15) / 16;                    // project pixel tiles
+// HO: output side; S: stride; KS: inp_pad / 32; NOT: oup_pad / 16; HC: hidden channels per chunk.
+template <int HO, int S, int KS, int NOT, int HC>
+struct IrxGeom {
+  static constexpr int HI = HO * S;                   // input side
+  static constexpr int NOR0 = (HO + 1) / 2;           // output rows of part 0 (the larger band)
+  static constexpr int ER = (NOR0 - 1) * S + 3;       // E rows incl. the zero border
+  static constexpr int EW = HI + 2;                   // E columns incl. the zero border
+  static constexpr int NEP = ER * EW;                 // E pixels
+  static constexpr int NKG = HC / 8;                  // 8-channel groups of a chunk
+  static constexpr int EPS = (2 * NEP + 1) * 16;      // bytes per E channel-group plane (odd slot count)
+  static constexpr int XR0 = imin(HI, (NOR0 - 1) * S + 2);                          // input rows, part 0
+  static constexpr int XR1 = imin(HI - 1, (HO - 1) * S + 1) - (NOR0 * S - 1) + 1;    // input rows, part 1
+  static constexpr int NX = imax(XR0, XR1) * HI;
+  static constexpr int NXT = (NX + 15) / 16;          // expand pixel tiles
   static constexpr int INP = KS * 32;
-  static constexpr int XP = 6 * INP + 32;                            // bytes per X / We row: [h|m|l][INP] bf16 + pad
-  static constexpr int EP = 128;                                     // bytes per E row: 32 fp32
-  static constexpr int DP = 224;                                     // bytes per D / Wp row: [h|m|l][32] bf16 + pad
-  static constexpr int X_BYTES = PIN_PAD * XP, E_BYTES = PIN_PAD * EP, D_BYTES = NP * 16 * DP;
-  static constexpr int W_BYTES = MT * 16 * DP, WE_BYTES = 32 * XP, WD_BYTES = 10 * 32 * 4;  // WD: 9 taps + bias
-  static constexpr int LDS = X_BYTES + E_BYTES + D_BYTES + W_BYTES + WE_BYTES + WD_BYTES;
-  static constexpr int PAIRS = MT * NP, PPW = (PAIRS + IRC_WAVES - 1) / IRC_WAVES;  // project tiles (per wave)
-  static constexpr int ET = (NE + IRC_WAVES / 2 - 1) / (IRC_WAVES / 2);   // expand pixel tiles per wave
-  static constexpr int WPC = (MT * 16 * 12 + IRC_THREADS - 1) / IRC_THREADS;  // Wp 16-B pieces per thread
-  static constexpr int WEC = (32 * 3 * INP / 8 + IRC_THREADS - 1) / IRC_THREADS;  // We 16-B pieces per thread
+  static constexpr int NHT = HC / 16;                 // expand hidden tiles per chunk
+  static constexpr int EWPT = (NXT <= IRX_WAVES / 2 && NHT % 2 == 0) ? 2 : 1;  // waves sharing an X tile
+  static constexpr int HTW = NHT / EWPT;              // expand hidden tiles per wave
+  static constexpr int NPT = (NOR0 * HO + 15) / 16;   // project pixel tiles
+  static constexpr int NOG = imax(1, IRX_WAVES / NPT);  // output-channel groups (one wave each per tile)
+  static constexpr int OTG = (NOT + NOG - 1) / NOG;   // output tiles of 16 per group
+  static constexpr int NKS = HC / 32;                 // project K-steps per chunk
+  static constexpr int WEB = 6 * INP + 32;            // bytes per We row: [h|m|l][INP] bf16 + pad
+  static constexpr int WPB = 6 * HC + 32;             // bytes per Wp row: [h|m|l][HC] bf16 + pad
+  static constexpr int E_BYTES = NKG * EPS, WE_BYTES = HC * WEB, WBE_BYTES = HC * 4;
+  static constexpr int WP_BYTES = NOT * 16 * WPB, WD_BYTES = 10 * HC * 4;  // WD: 9 taps + bias
+  static constexpr int LDS = E_BYTES + WE_BYTES + WBE_BYTES + WP_BYTES + WD_BYTES;
+  // 16-byte staging pieces of one chunk
+  static constexpr int WE_PPR = 3 * INP / 8, WE_PIECES = HC * WE_PPR + HC / 4;  // + the expand bias
+  static constexpr int WP_PPR = 3 * HC / 8, WP_PIECES = NOT * 16 * WP_PPR + 10 * HC / 4;  // + taps, dw bias
+  static constexpr int WE_PT = (WE_PIECES + IRX_THREADS - 1) / IRX_THREADS;
+  static constexpr int WP_PT = (WP_PIECES + IRX_THREADS - 1) / IRX_THREADS;
 };
 
 // Weights (IrParams.x3w = 1, packed by engine/planner.py::split_bf16x3): we bf16 [hid_pad][3][inp_pad] and
 // wp bf16 [oup_pad][3][hid_pad] (planes h, m, l of the fp32 weight), wd fp32 [9][hid_pad], biases fp32.
-template <int HO, int S, int KS, int MT, int RS>
-__global__ __launch_bounds__(IRC_THREADS) void ir_crop_f32_kernel(const IrParams p) {
-  using G = IrcGeom<HO, S, KS, MT, RS>;
-  constexpr int HI = G::HI, INP = G::INP, XP = G::XP, NE = G::NE, DP = G::DP;
+template <int HO, int S, int KS, int NOT, int HC>
+__global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
+  using G = IrxGeom<HO, S, KS, NOT, HC>;
+  constexpr int HI = G::HI, INP = G::INP, EW = G::EW;
   extern __shared__ __align__(16) uint8_t lds[];
-  uint8_t* Xs = lds;
-  uint8_t* Es = Xs + G::X_BYTES;
-  uint8_t* Ds = Es + G::E_BYTES;
-  uint8_t* Ws = Ds + G::D_BYTES;
-  uint8_t* WEs = Ws + G::W_BYTES;
-  float* WDs = (float*)(WEs + G::WE_BYTES);  // [10][32]: taps 0..8, bias
+  uint8_t* Es = lds;
+  uint8_t* WEs = Es + G::E_BYTES;
+  float* WBEs = (float*)(WEs + G::WE_BYTES);
+  uint8_t* WPs = (uint8_t*)WBEs + G::WBE_BYTES;
+  float* WDs = (float*)(WPs + G::WP_BYTES);  // [10][HC]: taps 0..8, bias
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, kq = lane >> 4;
-  const int og_n = p.oup_pad / (MT * 16);
-  const int b = blockIdx.x / (RS * og_n), rem = blockIdx.x - b * RS * og_n;
-  const int part = rem / og_n, og = rem - part * og_n, oc_base = og * MT * 16;
+  const int b = blockIdx.x >> 1, part = blockIdx.x & 1;
   if (b >= live_batch(p.B, p.bdev)) return;
-  const int oy0 = part * G::NOR;
-  const int nor = RS == 1 ? HO : (part ? HO - G::NOR : G::NOR);
+  const int oy0 = part * G::NOR0;
+  const int nor = part ? HO - G::NOR0 : G::NOR0;
   const int nout = nor * HO;
-  const int iy_lo = oy0 * S - 1 < 0 ? 0 : oy0 * S - 1;
-  const int iy_hi = (oy0 + nor - 1) * S + 2 > HI ? HI : (oy0 + nor - 1) * S + 2;  // exclusive
-  const int pin = (iy_hi - iy_lo) * HI;
-  const float* xb = (const float*)p.x + ((size_t)b * HI * HI + (size_t)iy_lo * HI) * p.x_cs;
-  const bf16* we = (const bf16*)p.we;
-  const float* wd = (const float*)p.wd;
-  const bf16* wp = (const bf16*)p.wp;
-  const int hid_pad = p.hid_pad, nchunks = hid_pad >> 5;
+  const int iy0 = oy0 * S - 1;                          // image row of E row 0
+  const int iy_lo = iy0 < 0 ? 0 : iy0;
+  const int iy_hi = imin(HI - 1, (oy0 + nor - 1) * S + 1);
+  const int nx = (iy_hi - iy_lo + 1) * HI;
+  const float* __restrict__ x = (const float*)p.x;
+  const bf16* __restrict__ we = (const bf16*)p.we;
+  const bf16* __restrict__ wp = (const bf16*)p.wp;
+  const float* __restrict__ wd = (const float*)p.wd;
+  const int hid_pad = p.hid_pad, nch = hid_pad / HC;
 
-  // chunk weight fetches into registers (global -> VGPR), stored to LDS a phase later
-  uint4 wec[G::WEC], wpc[G::WPC];
-  float4 wdc;
-  auto fetch_we = [&](int h0) {  // piece e = (hidden row, plane, 16-B column) of the chunk's expand rows
-#pragma unroll
-    for (int j = 0; j < G::WEC; ++j) {
-      const int e = tid + IRC_THREADS * j, row = e / (3 * KS * 4), pc = e - row * (3 * KS * 4);
-      const bool ok = e < 32 * 3 * KS * 4;
-      wec[j] = *(const uint4*)(we + (size_t)(h0 + (ok ? row : 0)) * (3 * INP) + pc * 8);
-    }
-  };
-  auto store_we = [&]() {
-#pragma unroll
-    for (int j = 0; j < G::WEC; ++j) {
-      const int e = tid + IRC_THREADS * j, row = e / (3 * KS * 4), pc = e - row * (3 * KS * 4);
-      if (e < 32 * 3 * KS * 4) *(uint4*)(WEs + row * XP + pc * 16) = wec[j];
-    }
-  };
-  auto fetch_wd = [&](int h0) {  // 80 float4: taps 0..8 and the bias, 8 per row
-    const int r = tid >> 3, g = tid & 7;
-    if (tid < 80) wdc = *(const float4*)((r < 9 ? wd + (size_t)r * hid_pad : p.bd) + h0 + 4 * g);
-  };
-  auto store_wd = [&]() {
-    if (tid < 80) *(float4*)(WDs + tid * 4) = wdc;
-  };
-  auto fetch_wp = [&](int h0) {  // piece e = (output row, plane, 16-B column) of the chunk's project columns
-#pragma unroll
-    for (int j = 0; j < G::WPC; ++j) {
-      const int e = tid + IRC_THREADS * j, row = e / 12, pc = e - row * 12;
-      const bool ok = e < MT * 16 * 12;
-      wpc[j] = *(const uint4*)(wp + ((size_t)(oc_base + (ok ? row : 0)) * 3 + (pc >> 2)) * hid_pad + h0 +
-                               (pc & 3) * 8);
-    }
-  };
-  auto store_wp = [&]() {
-#pragma unroll
-    for (int j = 0; j < G::WPC; ++j) {
-      const int e = tid + IRC_THREADS * j, row = e / 12, pc = e - row * 12;
-      if (e < MT * 16 * 12) *(uint4*)(Ws + row * DP + (pc >> 2) * 64 + (pc & 3) * 16) = wpc[j];
-    }
-  };
-  fetch_we(0);
-  fetch_wd(0);
-
-  // ---- X: the workgroup's input rows, split into three bf16 planes (zero past inp and past pin)
-  constexpr int CG = INP / 4;
-  for (int i = tid; i < G::PIN_PAD * CG; i += IRC_THREADS) {
-    const int pix = i / CG, g = i - pix * CG;
-    const bool ok = pix < pin && 4 * g < p.inp;
-    float4 v = *(const float4*)(ok ? xb + (size_t)pix * p.x_cs + 4 * g : xb);
-    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
-    store_split4<INP * 2>(Xs + pix * XP + g * 8, v);
+  // ---- chunk weight staging (global -> registers -> LDS); plain unrolled loops, not lambdas: a lambda
+  // capturing the staging arrays by reference put them in scratch memory (80-208 B per lane)
+  u32x4 rwe[G::WE_PT], rwp[G::WP_PT];  // native vector type: the HIP uint4 struct kept them in scratch
+// Every thread loads every piece slot (out-of-range slots re-read a valid address) and the source / destination
+// addresses are selects: with per-slot branches the compiler kept the staging arrays in scratch memory.
+#define IRX_FETCH_WE(h0_)                                                                   \
+  _Pragma("unroll") for (int j = 0; j < G::WE_PT; ++j) {                                   \
+    const int e = tid + IRX_THREADS * j;                                                    \
+    const int row = e / G::WE_PPR, pc = e - row * G::WE_PPR;                                \
+    const bool isw = e < HC * G::WE_PPR;                                                    \
+    const int eb = e - HC * G::WE_PPR;                                                      \
+    const uint8_t* src = isw ? (const uint8_t*)(we + (size_t)((h0_) + row) * (3 * INP) + pc * 8) \
+                             : (const uint8_t*)(p.be + (h0_) + 4 * (eb < HC / 4 ? eb : 0)); \
+    rwe[j] = *(const u32x4*)src;                                                            \
   }
-  store_we();
-  store_wd();
+#define IRX_STORE_WE()                                                                      \
+  _Pragma("unroll") for (int j = 0; j < G::WE_PT; ++j) {                                   \
+    const int e = tid + IRX_THREADS * j;                                                    \
+    const int row = e / G::WE_PPR, pc = e - row * G::WE_PPR;                                \
+    uint8_t* dst = e < HC * G::WE_PPR ? WEs + row * G::WEB + pc * 16                        \
+                                      : (uint8_t*)WBEs + 16 * (e - HC * G::WE_PPR);         \
+    if (e < G::WE_PIECES) *(u32x4*)dst = rwe[j];                                            \
+  }
+#define IRX_FETCH_WP(h0_)                                                                   \
+  _Pragma("unroll") for (int j = 0; j < G::WP_PT; ++j) {                                   \
+    const int e = tid + IRX_THREADS * j;                                                    \
+    const int row = e / G::WP_PPR, pc = e - row * G::WP_PPR;                                \
+    const int pl = pc / (HC / 8), c8 = pc - pl * (HC / 8);                                  \
+    const bool isw = e < NOT * 16 * G::WP_PPR;                                              \
+    const int i = isw ? 0 : imin(e - NOT * 16 * G::WP_PPR, 10 * HC / 4 - 1);               \
+    const int r = i / (HC / 4), g = i - r * (HC / 4);                                       \
+    const float* dsrc = (r < 9 ? wd + (size_t)r * hid_pad : p.bd) + (h0_) + 4 * g;          \
+    const uint8_t* src = isw ? (const uint8_t*)(wp + ((size_t)row * 3 + pl) * hid_pad + (h0_) + c8 * 8) \
+                             : (const uint8_t*)dsrc;                                        \
+    rwp[j] = *(const u32x4*)src;                                                            \
+  }
+#define IRX_STORE_WP()                                                                      \
+  _Pragma("unroll") for (int j = 0; j < G::WP_PT; ++j) {                                   \
+    const int e = tid + IRX_THREADS * j;                                                    \
+    const int row = e / G::WP_PPR, pc = e - row * G::WP_PPR;                                \
+    uint8_t* dst = e < NOT * 16 * G::WP_PPR ? WPs + row * G::WPB + pc * 16                  \
+                                            : (uint8_t*)WDs + 16 * (e - NOT * 16 * G::WP_PPR); \
+    if (e < G::WP_PIECES) *(u32x4*)dst = rwp[j];                                            \
+  }
+  IRX_FETCH_WE(0)
+  IRX_FETCH_WP(0)
 
-  f32x4 acc[G::PPW];
+  // ---- E: zero everywhere (the border stays zero: it is the depthwise padding)
+  for (int i = tid; i < G::E_BYTES / 16; i += IRX_THREADS) ((uint4*)Es)[i] = make_uint4(0u, 0u, 0u, 0u);
+
+  // ---- this wave's expand pixel tile: the block input, split, resident in registers for the whole kernel
+  const int xt = wave / G::EWPT, hpart = wave - xt * G::EWPT;
+  const bool xw = xt < G::NXT;
+  bf16x8 xh[KS], xm[KS], xl[KS];
+  int e_off = -1;  // byte offset of this lane's pixel in an E plane (-1: padding pixel)
+  {
+    const int xp = xt * 16 + col;
+    const bool ok = xw && xp < nx;
+    const int iy = iy_lo + xp / HI, ix = xp - (xp / HI) * HI;
+    const float* src = x + (((size_t)b * HI + (ok ? iy : 0)) * HI + (ok ? ix : 0)) * p.x_cs;
 #pragma unroll
-  for (int j = 0; j < G::PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ks * 32 + 8 * kq;
+      float v[8];
+      const bool kk = ok && k < p.inp;
+      const float4 a = *(const float4*)(src + (kk ? k : 0)), c = *(const float4*)(src + (kk ? k + 4 : 0));
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+      if (!kk) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 0.f;
+      }
+      split8(v, xh[ks], xm[ks], xl[ks]);
+    }
+    if (ok) e_off = ((iy - iy0) * EW + ix + 1) * 32;
+  }
 
-  const int mt_e = wave & 1;  // expand: this wave's hidden tile; pixel tiles (wave >> 1) + 4 i
-  const int g8 = tid & 7;     // depthwise: this thread's 4-channel group of the chunk
+  // ---- this wave's depthwise + project unit: (output pixel tile, output-channel group)
+  const int upt = wave % G::NPT, uog = wave / G::NPT;
+  const bool pw = uog < G::NOG;
+  const int ot0 = uog * G::OTG;
+  const int q = upt * 16 + col;
+  const bool qok = pw && q < nout;
+  const int qq = qok ? q : 0;
+  const int dw_off = ((qq / HO) * S * EW + (qq - (qq / HO) * HO) * S) * 32;  // tap (0, 0), bytes in a plane
+  f32x4 acc[G::OTG];
+#pragma unroll
+  for (int j = 0; j < G::OTG; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  IRX_STORE_WE()
+  IRX_STORE_WP()
+  if (nch > 1) {
+    IRX_FETCH_WE(HC)
+    IRX_FETCH_WP(HC)
+  }
   __syncthreads();
 
-  for (int h = 0; h < nchunks; ++h) {
-    const int h0 = h * 32;
-    const bool more = h + 1 < nchunks;
-    // global fetches for later phases: this chunk's project columns, the next chunk's expand rows / taps
-    fetch_wp(h0);
-    if (more) {
-      fetch_we(h0 + 32);
-      fetch_wd(h0 + 32);
-    }
-
-    // ---- expand: E[pix][32] = relu6(We[chunk] . X + be) for this wave's hidden tile
-    {
-      const float4 be = *(const float4*)(p.be + h0 + mt_e * 16 + 4 * kq);
-      f32x4 e[G::ET];
+  for (int c = 0; c < nch; ++c) {
+    // ---- expand: E[pix][chunk] = relu6(We[chunk] . X + be) for this wave's hidden tiles
+    if (xw) {
 #pragma unroll
-      for (int i = 0; i < G::ET; ++i) e[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < G::HTW; ++i) {
+        const int ht = hpart * G::HTW + i;
+        f32x4 e = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int sl = 0; sl < KS; ++sl) {
-        const uint8_t* ra = WEs + (mt_e * 16 + col) * XP + sl * 64 + kq * 16;
-        const bf16x8 ah = *(const bf16x8*)ra, am = *(const bf16x8*)(ra + INP * 2), al = *(const bf16x8*)(ra + INP * 4);
-#pragma unroll
-        for (int i = 0; i < G::ET; ++i) {
-          const int j = (wave >> 1) + (IRC_WAVES / 2) * i;
-          if (j >= NE) break;
-          const uint8_t* r = Xs + (j * 16 + col) * XP + sl * 64 + kq * 16;
-          const bf16x8 bh = *(const bf16x8*)r, bm = *(const bf16x8*)(r + INP * 2),
-                       bl = *(const bf16x8*)(r + INP * 4);
-          e[i] = mfma_x3(ah, am, al, bh, bm, bl, e[i]);
+        for (int ks = 0; ks < KS; ++ks) {
+          const uint8_t* ra = WEs + (ht * 16 + col) * G::WEB + (ks * 32 + 8 * kq) * 2;
+          e = mfma_x3(*(const bf16x8*)ra, *(const bf16x8*)(ra + INP * 2), *(const bf16x8*)(ra + INP * 4), xh[ks],
+                      xm[ks], xl[ks], e);
+        }
+        if (e_off >= 0) {
+          const int ch = ht * 16 + 4 * kq;
+          const float4 be = *(const float4*)(WBEs + ch);
+          const float4 v = make_float4(relu6f(e[0] + be.x), relu6f(e[1] + be.y), relu6f(e[2] + be.z),
+                                       relu6f(e[3] + be.w));
+          *(float4*)(Es + (ch >> 3) * G::EPS + e_off + (ch & 7) * 4) = v;
         }
       }
-#pragma unroll
-      for (int i = 0; i < G::ET; ++i) {
-        const int j = (wave >> 1) + (IRC_WAVES / 2) * i;
-        if (j >= NE) break;
-        const int pix = j * 16 + col, grp = mt_e * 4 + kq;
-        const float4 v = relu6x4(make_float4(e[i][0] + be.x, e[i][1] + be.y, e[i][2] + be.z, e[i][3] + be.w));
-        *(float4*)(Es + pix * G::EP + ((grp ^ (pix & 7)) << 4)) = v;
+    }
+    __syncthreads();  // A: E complete; every wave is past its reads of We / be
+    if (c + 1 < nch) {
+      IRX_STORE_WE()
+      if (c + 2 < nch) {
+        IRX_FETCH_WE((c + 2) * HC)
       }
     }
-    __syncthreads();  // E complete; every wave is past its expand reads of WEs
 
-    // ---- depthwise 3x3 (stride S) + bias + ReLU6 -> D planes; Wp(h) and We(h+1) -> LDS
-    {
-      float4 wk[9];
+    // ---- depthwise (into the project B operand) + project
+    if (pw) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) wk[t] = *(const float4*)(WDs + t * 32 + 4 * g8);
-      const float4 bdw = *(const float4*)(WDs + 9 * 32 + 4 * g8);
-      for (int q = tid >> 3; q < nout; q += IRC_THREADS / 8) {
-        const int oy = oy0 + q / HO, ox = q - (q / HO) * HO;
-        float4 a = bdw;
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const int iy = oy * S - 1 + ky;
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int ix = ox * S - 1 + kx;
-            const bool ok = (unsigned)iy < (unsigned)HI && (unsigned)ix < (unsigned)HI;
-            const int lp = ok ? (iy - iy_lo) * HI + ix : 0;
-            float4 v = *(const float4*)(Es + lp * G::EP + ((g8 ^ (lp & 7)) << 4));
-            if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
-            const float4 w = wk[ky * 3 + kx];
-            a.x = fmaf(v.x, w.x, a.x);
-            a.y = fmaf(v.y, w.y, a.y);
-            a.z = fmaf(v.z, w.z, a.z);
-            a.w = fmaf(v.w, w.w, a.w);
-          }
+      for (int ks = 0; ks < G::NKS; ++ks) {
+        const int kg = ks * 4 + kq;
+        const float* wk = WDs + kg * 8;
+        float a[8];
+        {
+          const float4 b0 = *(const float4*)(wk + 9 * HC), b1 = *(const float4*)(wk + 9 * HC + 4);
+          a[0] = b0.x; a[1] = b0.y; a[2] = b0.z; a[3] = b0.w; a[4] = b1.x; a[5] = b1.y; a[6] = b1.z; a[7] = b1.w;
         }
-        store_split4<64>(Ds + q * DP + g8 * 8, relu6x4(a));
+        const uint8_t* eb = Es + kg * G::EPS + dw_off;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const uint8_t* ep = eb + ((t / 3) * EW + (t % 3)) * 32;
+          const float4 v0 = *(const float4*)ep, v1 = *(const float4*)(ep + 16);
+          const float4 w0 = *(const float4*)(wk + t * HC), w1 = *(const float4*)(wk + t * HC + 4);
+          a[0] = fmaf(v0.x, w0.x, a[0]);
+          a[1] = fmaf(v0.y, w0.y, a[1]);
+          a[2] = fmaf(v0.z, w0.z, a[2]);
+          a[3] = fmaf(v0.w, w0.w, a[3]);
+          a[4] = fmaf(v1.x, w1.x, a[4]);
+          a[5] = fmaf(v1.y, w1.y, a[5]);
+          a[6] = fmaf(v1.z, w1.z, a[6]);
+          a[7] = fmaf(v1.w, w1.w, a[7]);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = relu6f(a[i]);
+        bf16x8 dh, dm, dl;
+        split8(a, dh, dm, dl);
+#pragma unroll
+        for (int j = 0; j < G::OTG; ++j) {
+          const int ot = ot0 + j;
+          if (ot >= NOT) break;
+          const uint8_t* ra = WPs + (ot * 16 + col) * G::WPB + (ks * 32 + 8 * kq) * 2;
+          acc[j] = mfma_x3(*(const bf16x8*)ra, *(const bf16x8*)(ra + HC * 2), *(const bf16x8*)(ra + HC * 4), dh, dm,
+                           dl, acc[j]);
+        }
       }
     }
-    store_wp();
-    if (more) store_we();
-    __syncthreads();  // D and Wp complete; every wave is past its depthwise reads of WDs
-
-    if (more) store_wd();
-    // ---- project: acc[pair] += Wp[oc tile][chunk] . D[pixel tile]
-#pragma unroll
-    for (int j = 0; j < G::PPW; ++j) {
-      const int pr = wave + IRC_WAVES * j;
-      if (pr >= G::PAIRS) break;
-      const int mt = pr % MT, nt = pr / MT;
-      const uint8_t* ra = Ws + (mt * 16 + col) * DP + kq * 16;
-      const uint8_t* rb = Ds + (nt * 16 + col) * DP + kq * 16;
-      acc[j] = mfma_x3(*(const bf16x8*)ra, *(const bf16x8*)(ra + 64), *(const bf16x8*)(ra + 128),
-                       *(const bf16x8*)rb, *(const bf16x8*)(rb + 64), *(const bf16x8*)(rb + 128), acc[j]);
+    __syncthreads();  // B: every wave is past its reads of E, Wp and the taps
+    if (c + 1 < nch) {
+      IRX_STORE_WP()
+      if (c + 2 < nch) {
+        IRX_FETCH_WP((c + 2) * HC)
+      }
     }
   }
 
+#undef IRX_FETCH_WE
+#undef IRX_STORE_WE
+#undef IRX_FETCH_WP
+#undef IRX_STORE_WP
+
   // ---- epilogue: + bp (+ residual, stride 1: the block input at the same pixel) -> NHWC fp32
-  float* yb = (float*)p.y + ((size_t)b * HO * HO + (size_t)oy0 * HO) * p.y_cs;
-  const float* xr = (const float*)p.x + ((size_t)b * HI * HI + (size_t)oy0 * HI) * p.x_cs;
+  if (qok) {
+    const int oy = oy0 + q / HO, ox = q - (q / HO) * HO;
+    float* yp = (float*)p.y + (((size_t)b * HO + oy) * HO + ox) * p.y_cs;
+    const float* xr = x + (((size_t)b * HI + oy) * HI + ox) * p.x_cs;
 #pragma unroll
-  for (int j = 0; j < G::PPW; ++j) {
-    const int pr = wave + IRC_WAVES * j;
-    if (pr >= G::PAIRS) break;
-    const int mt = pr % MT, nt = pr / MT;
-    const int q = nt * 16 + col, co = oc_base + mt * 16 + 4 * kq;
-    if (q >= nout || co >= p.oup) continue;
-    const float4 bp = *(const float4*)(p.bp + co);
-    float4 v = make_float4(acc[j][0] + bp.x, acc[j][1] + bp.y, acc[j][2] + bp.z, acc[j][3] + bp.w);
-    if (S == 1 && p.res) {
-      const float4 r = *(const float4*)(xr + (size_t)q * p.x_cs + co);
-      v.x += r.x;
-      v.y += r.y;
-      v.z += r.z;
-      v.w += r.w;
+    for (int j = 0; j < G::OTG; ++j) {
+      const int ot = ot0 + j;
+      const int co = ot * 16 + 4 * kq;
+      if (ot >= NOT || co >= p.oup) continue;
+      const float4 bp = *(const float4*)(p.bp + co);
+      float4 v = make_float4(acc[j][0] + bp.x, acc[j][1] + bp.y, acc[j][2] + bp.z, acc[j][3] + bp.w);
+      if (S == 1 && p.res) {
+        const float4 r = *(const float4*)(xr + co);
+        v.x += r.x;
+        v.y += r.y;
+        v.z += r.z;
+        v.w += r.w;
+      }
+      *(float4*)(yp + co) = v;
     }
-    *(float4*)(yb + (size_t)q * p.y_cs + co) = v;
   }
 }
 
-// (HO, S, KS, MT): the MobileNetV2 14x14 / 7x7 stages at 224 (RS = 2 row parts per crop)
-#define ARENA_IRC_F32_CONFIGS(X) \
-  X(14, 1, 2, 4)                 \
-  X(14, 1, 2, 6)                 \
-  X(14, 1, 3, 6)                 \
-  X(7, 2, 3, 10)                 \
-  X(7, 1, 5, 10)
+// (HO, S, KS, NOT, HC): the MobileNetV2 14x14 / 7x7 stages at 224 (two row bands per crop)
+#define ARENA_IRX_CONFIGS(X) \
+  X(14, 1, 2, 4, 32)         \
+  X(14, 1, 2, 6, 32)         \
+  X(14, 1, 3, 6, 32)         \
+  X(7, 2, 3, 10, 32)         \
+  X(7, 1, 5, 10, 32)         \
+  X(7, 1, 5, 20, 32)
 
 void ir_crop_f32_prepare() {
-#define X(HO_, S_, KS_, MT_)                                                                                   \
-  static_assert(IrcGeom<HO_, S_, KS_, MT_, 2>::LDS <= 160 * 1024, "ir_crop_f32: LDS budget");                  \
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_crop_f32_kernel<HO_, S_, KS_, MT_, 2>,                  \
+#define X(HO_, S_, KS_, NOT_, HC_)                                                                         \
+  static_assert(IrxGeom<HO_, S_, KS_, NOT_, HC_>::LDS <= 160 * 1024, "ir_x3: LDS budget");                 \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_x3_kernel<HO_, S_, KS_, NOT_, HC_>,                 \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  ARENA_IRC_F32_CONFIGS(X)
+  ARENA_IRX_CONFIGS(X)
 #undef X
 }
 
-// Shapes this kernel takes (mirrored by engine/validate.py::ir_crop_f32_supported; the planner decides which
-// blocks use it and marks them with split-plane weights, IrParams.x3w): an expanding block on a
-// 14x14 (stride 1 or 2) or 7x7 (stride 1) input map whose (inp_pad, oup_pad) has a configuration above.
+// Shapes this kernel takes (mirrored by engine/validate.py::ir_crop_f32_supported; the planner marks the
+// blocks that use it with split-plane weights, IrParams.x3w): an expanding block on a 14x14 (stride 1 or 2)
+// or 7x7 (stride 1) input map whose (inp_pad, oup_pad) has a configuration above.
 bool ir_block_crop_f32_supported(int H, int stride, int inp_pad, int hid_pad, int oup_pad, int expand) {
-  if (!expand || hid_pad % 32 || oup_pad % 16) return false;
+  if (!expand || oup_pad % 16) return false;
   const int HO = (H + 2 - 3) / stride + 1;
   if (H != HO * stride) return false;
-#define X(HO_, S_, KS_, MT_) \
-  if (HO == HO_ && stride == S_ && inp_pad == KS_ * 32 && oup_pad % (MT_ * 16) == 0 && oup_pad <= 2 * MT_ * 16) \
-    return true;
-  ARENA_IRC_F32_CONFIGS(X)
+#define X(HO_, S_, KS_, NOT_, HC_) \
+  if (HO == HO_ && stride == S_ && inp_pad == KS_ * 32 && oup_pad == NOT_ * 16 && hid_pad % HC_ == 0) return true;
+  ARENA_IRX_CONFIGS(X)
 #undef X
   return false;
 }
@@ -354,21 +380,20 @@ bool ir_block_crop_f32(const IrParams& p, hipStream_t s) {
   if (!p.x3w) return false;  // only blocks planned for this kernel carry its split-plane weights
   if (p.H != p.W || p.Ho != p.Wo || !ir_block_crop_f32_supported(p.H, p.stride, p.inp_pad, p.hid_pad, p.oup_pad,
                                                                  p.expand))
-    throw std::runtime_error("ir_crop_f32: split-plane weights for a block this kernel does not take");
-  if (p.inp % 4 || p.oup % 4 || p.inp > p.inp_pad || p.oup > p.oup_pad || p.x_cs % 4 || p.y_cs % 4)
-    throw std::runtime_error("ir_crop_f32: unsupported channel geometry");
-  if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_crop_f32: residual needs s1, inp == oup");
-  if (p.Ho != (p.H + 2 - 3) / p.stride + 1) throw std::runtime_error("ir_crop_f32: output size mismatch");
+    throw std::runtime_error("ir_x3: split-plane weights for a block this kernel does not take");
+  if (p.inp % 8 || p.oup % 4 || p.inp > p.inp_pad || p.oup > p.oup_pad || p.x_cs % 4 || p.y_cs % 4)
+    throw std::runtime_error("ir_x3: unsupported channel geometry");
+  if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_x3: residual needs s1, inp == oup");
+  if (p.Ho != (p.H + 2 - 3) / p.stride + 1) throw std::runtime_error("ir_x3: output size mismatch");
   if (p.B <= 0) return true;
-#define X(HO_, S_, KS_, MT_)                                                                              \
-  if (p.Ho == HO_ && p.stride == S_ && p.inp_pad == KS_ * 32 && p.oup_pad % (MT_ * 16) == 0) {             \
-    using G = IrcGeom<HO_, S_, KS_, MT_, 2>;                                                              \
-    const unsigned grid = (unsigned)(p.B * 2 * (p.oup_pad / (MT_ * 16)));                                 \
-    hipLaunchKernelGGL((ir_crop_f32_kernel<HO_, S_, KS_, MT_, 2>), dim3(grid),                            \
-                       dim3(IRC_THREADS), G::LDS, s, p);                                                  \
-    return true;                                                                                          \
+#define X(HO_, S_, KS_, NOT_, HC_)                                                                             \
+  if (p.Ho == HO_ && p.stride == S_ && p.inp_pad == KS_ * 32 && p.oup_pad == NOT_ * 16 && p.hid_pad % HC_ == 0) { \
+    using G = IrxGeom<HO_, S_, KS_, NOT_, HC_>;                                                                \
+    hipLaunchKernelGGL((ir_x3_kernel<HO_, S_, KS_, NOT_, HC_>), dim3((unsigned)(p.B * 2)), dim3(IRX_THREADS),   \
+                       G::LDS, s, p);                                                                          \
+    return true;                                                                                               \
   }
-  ARENA_IRC_F32_CONFIGS(X)
+  ARENA_IRX_CONFIGS(X)
 #undef X
   return false;
 }

@@ -173,6 +173,10 @@ void DynamicBatcher::fail(Batch& batch, const std::string& err) {
   {
     std::lock_guard<std::mutex> lk(mu_);
     stats_.failed += (int64_t)batch.size();
+    stats_.last_error = err;
+    // a HIP runtime error (ARENA_HIP_CHECK) poisons the device context; anything else (an input the staging
+    // pool cannot take, an empty image) fails only this batch (server/batching.py is_device_fault)
+    if (err.rfind("HIP error", 0) == 0) ++stats_.device_faults;
   }
   for (auto& rq : batch) {
     RequestResult rr;

@@ -23,6 +23,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -60,6 +61,8 @@ struct BatcherStats {
   double sum_batch = 0;
   double sum_queue_us = 0, sum_compute_us = 0;
   std::vector<int64_t> batch_hist;  // index = batch size
+  int64_t device_faults = 0;        // failed batches whose error is a HIP runtime error ("HIP error ...")
+  std::string last_error;           // text of the most recent failed batch
 };
 
 class DynamicBatcher {

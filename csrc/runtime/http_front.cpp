@@ -172,11 +172,18 @@ bool multipart_field(const std::string& body, const std::string& ctype, const st
 
 struct HttpFrontEnd::Conn {
   int fd = -1, ep = -1;
-  std::mutex mu;             // out / closed / busy (the response may come from any thread)
+  std::mutex mu;             // out / closed / busy / paused (the response may come from any thread)
   std::string in;            // I/O thread only
   std::string out;
   size_t out_off = 0;
   bool closed = false, busy = false, close_after = false;
+  bool paused = false;       // input buffer at its cap: EPOLLIN off until the in-flight response is written
+  // I/O thread only: timeouts and the incremental chunked-body parse (a body arriving over many reads is
+  // scanned once, not from its start on every read)
+  Clock::time_point last_rx, req_start;
+  bool in_request = false;
+  size_t chunk_pos = 0;      // next chunk-size line (0: not started)
+  std::string chunk_body;
 };
 
 struct HttpFrontEnd::Pending {
@@ -347,8 +354,34 @@ void HttpFrontEnd::io_loop(int idx) {
   const int ep = epfds_[idx];
   std::unordered_map<int, std::shared_ptr<Conn>> conns;
   std::vector<epoll_event> evs(256);
+  auto last_sweep = Clock::now();
   while (!stop_.load()) {
     const int n = epoll_wait(ep, evs.data(), (int)evs.size(), 200);
+    const auto now = Clock::now();
+    if (now - last_sweep > std::chrono::milliseconds(500) && (cfg_.idle_timeout_ms > 0 || cfg_.read_timeout_ms > 0)) {
+      last_sweep = now;
+      std::vector<std::shared_ptr<Conn>> expired;
+      for (auto& kv : conns) {
+        const auto& c = kv.second;
+        bool busy;
+        {
+          std::lock_guard<std::mutex> lk(c->mu);
+          busy = c->busy || c->out_off < c->out.size();
+        }
+        if (busy) continue;  // a request in flight is answered, never cut off
+        const double idle = std::chrono::duration<double, std::milli>(now - c->last_rx).count();
+        const double reading = std::chrono::duration<double, std::milli>(now - c->req_start).count();
+        if ((c->in_request && cfg_.read_timeout_ms > 0 && reading > cfg_.read_timeout_ms) ||
+            (!c->in_request && cfg_.idle_timeout_ms > 0 && idle > cfg_.idle_timeout_ms))
+          expired.push_back(c);
+      }
+      for (auto& c : expired) {
+        conns.erase(c->fd);
+        close_conn(ep, c);
+        std::lock_guard<std::mutex> sl(stats_mu_);
+        ++stats_.timeouts;
+      }
+    }
     for (int i = 0; i < n && !stop_.load(); ++i) {
       const int fd = evs[i].data.fd;
       if (fd == stop_efd_) continue;
@@ -361,6 +394,7 @@ void HttpFrontEnd::io_loop(int idx) {
           auto conn = std::make_shared<Conn>();
           conn->fd = c;
           conn->ep = ep;
+          conn->last_rx = Clock::now();
           conns[c] = conn;
           epoll_event ev{};
           ev.events = EPOLLIN | EPOLLRDHUP;
@@ -401,16 +435,36 @@ void HttpFrontEnd::close_conn(int ep, const std::shared_ptr<Conn>& c) {
 void HttpFrontEnd::handle_readable(int ep, const std::shared_ptr<Conn>& c) {
   char buf[65536];
   bool eof = false;
-  while (true) {
-    const ssize_t k = ::read(c->fd, buf, sizeof buf);
+  // Buffer at most one maximal request (body + headers) plus one read: a client pipelining while a request
+  // is in flight, or streaming an endless chunked body, cannot grow the buffer without bound.
+  const size_t cap = (size_t)cfg_.max_body + (64u << 10);
+  while (c->in.size() < cap) {
+    const ssize_t k = ::read(c->fd, buf, std::min(sizeof buf, cap - c->in.size() + 1));
     if (k > 0) {
       c->in.append(buf, (size_t)k);
+      c->last_rx = Clock::now();
+      if (!c->in_request) {
+        c->in_request = true;
+        c->req_start = c->last_rx;
+      }
       continue;
     }
     if (k == 0) eof = true;
     else if (errno == EINTR) continue;
     else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
     break;
+  }
+  if (c->in.size() >= cap) {  // stop reading until the connection's response is out (handle_writable re-arms)
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!c->closed && !c->paused) {
+      c->paused = true;
+      epoll_event ev{};
+      // no EPOLLIN / EPOLLRDHUP (both level-triggered: a half-closed peer would spin the loop); a vanished
+      // peer shows up as a failed send of the response
+      ev.events = c->out_off < c->out.size() ? EPOLLOUT : 0u;
+      ev.data.fd = c->fd;
+      epoll_ctl(ep, EPOLL_CTL_MOD, c->fd, &ev);
+    }
   }
   while (true) {
     {
@@ -457,6 +511,7 @@ void HttpFrontEnd::handle_writable(int ep, const std::shared_ptr<Conn>& c) {
       c->out.clear();
       c->out_off = 0;
       c->busy = false;
+      c->paused = false;
       done = true;
       if (c->close_after) close_now = true;
       else {
@@ -508,6 +563,9 @@ bool HttpFrontEnd::parse_one(const std::shared_ptr<Conn>& c) {
       c->close_after = true;
     }
     in.clear();
+    c->in_request = false;
+    c->chunk_pos = 0;
+    c->chunk_body.clear();
     {
       std::lock_guard<std::mutex> sl(stats_mu_);
       ++stats_.requests;
@@ -549,24 +607,41 @@ bool HttpFrontEnd::parse_one(const std::shared_ptr<Conn>& c) {
   std::string body;
   size_t consumed;
   if (chunked) {
-    size_t pos = body0;
+    // resume where the previous read stopped: chunks already appended stay in chunk_body
+    size_t pos = c->chunk_pos ? c->chunk_pos : body0;
+    body = std::move(c->chunk_body);
+    auto suspend = [&]() {
+      c->chunk_pos = pos;
+      c->chunk_body = std::move(body);
+      return false;
+    };
     while (true) {
       const size_t e = in.find("\r\n", pos);
-      if (e == std::string::npos) return false;
-      const long long n = std::strtoll(in.substr(pos, e - pos).c_str(), nullptr, 16);
-      if (n < 0) return bad(400, "malformed chunk size");
-      if ((int64_t)body.size() + n > cfg_.max_body) return bad(413, "request body too large");
-      if (in.size() < e + 2 + (size_t)n + 2) return false;
+      if (e == std::string::npos) {
+        if (in.size() - pos > 64) return bad(400, "malformed chunk size");
+        return suspend();
+      }
+      errno = 0;
+      char* endp = nullptr;
+      const std::string field = in.substr(pos, e - pos);
+      const long long n = std::strtoll(field.c_str(), &endp, 16);
+      if (n < 0 || endp == field.c_str()) return bad(400, "malformed chunk size");
+      if (errno == ERANGE) return bad(413, "request body too large");  // saturated: beyond any limit
+      // compare without overflow: n may be up to LLONG_MAX
+      if (n > cfg_.max_body - (int64_t)body.size()) return bad(413, "request body too large");
+      if (in.size() < e + 2 + (size_t)n + 2) return suspend();
       if (n == 0) {  // last chunk, then optional trailers ending with an empty line
         const size_t tend = in.find("\r\n\r\n", e);
         if (in.compare(e + 2, 2, "\r\n") == 0) consumed = e + 4;
         else if (tend != std::string::npos) consumed = tend + 4;
-        else return false;
+        else return suspend();
         break;
       }
       body.append(in, e + 2, (size_t)n);
       pos = e + 2 + (size_t)n + 2;
     }
+    c->chunk_pos = 0;
+    c->chunk_body.clear();
   } else {
     if (clen < 0) clen = 0;
     if (clen > cfg_.max_body) return bad(413, "request body too large");
@@ -575,6 +650,8 @@ bool HttpFrontEnd::parse_one(const std::shared_ptr<Conn>& c) {
     consumed = body0 + (size_t)clen;
   }
   in.erase(0, consumed);
+  c->in_request = !in.empty();  // a pipelined request's bytes already count from now
+  if (c->in_request) c->req_start = Clock::now();
   {
     std::lock_guard<std::mutex> lk(c->mu);
     c->busy = true;
@@ -637,7 +714,7 @@ void HttpFrontEnd::respond(const std::shared_ptr<Conn>& c, int code, const std::
   if (c->closed) return;
   c->out += r;
   epoll_event ev{};
-  ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;  // the connection's I/O thread writes it
+  ev.events = c->paused ? EPOLLOUT : (EPOLLIN | EPOLLOUT | EPOLLRDHUP);  // the connection's I/O thread writes it
   ev.data.fd = c->fd;
   epoll_ctl(c->ep, EPOLL_CTL_MOD, c->fd, &ev);
 }
@@ -805,7 +882,8 @@ void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int statu
   if (status == 1) {
     const std::string text((const char*)out, (size_t)std::max<int64_t>(0, std::min<int64_t>(aux, dc_.slot_bytes)));
     release_slot(slot);
-    return fail(500, text);
+    // a header declaring more pixels than the decoder accepts (processing/transforms.py ImageTooLargeError)
+    return fail(text.find("image too large") != std::string::npos ? 413 : 500, text);
   }
   if (status == 2 && big.size() != (size_t)h * w * 3) {
     release_slot(slot);

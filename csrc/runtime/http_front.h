@@ -72,6 +72,11 @@ struct FrontConfig {
   std::string replica_tag;  // non-empty: an "x-arena-replica" header on every response (server/replica.py)
   bool handler_mode = false;  // uploads go to take() / complete() instead of decode pool + batcher
   int max_handler_queue = 4096;  // queued + in-handler requests before 503
+  // A keep-alive connection with nothing in flight and no bytes received for idle_timeout_ms is closed; so is
+  // one whose request has been arriving for longer than read_timeout_ms (a client trickling its headers or
+  // body would otherwise hold a descriptor and its buffer forever).  0 disables the check.
+  int64_t idle_timeout_ms = 60000;
+  int64_t read_timeout_ms = 30000;
 };
 
 // One upload handed to the Python handler (handler mode).
@@ -82,7 +87,7 @@ struct HandlerRequest {
 
 struct FrontStats {
   int64_t requests = 0, ok = 0, bad_request = 0, too_large = 0, unavailable = 0, errors = 0, not_found = 0;
-  int64_t connections = 0, open_connections = 0, detections = 0;
+  int64_t connections = 0, open_connections = 0, detections = 0, timeouts = 0;
   double sum_total_ms = 0, sum_decode_ms = 0, sum_queue_ms = 0, sum_gpu_ms = 0;
   std::vector<int64_t> latency_hist;  // counts per bucket of kLatencyBucketsMs (last = +Inf)
 };

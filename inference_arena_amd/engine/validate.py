@@ -63,9 +63,9 @@ def ir_f32_supported(stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expa
             and ir_f32_lds_bytes(stride, inp_pad, bool(expand)) <= 64 * 1024)
 
 
-# (output side, stride, inp_pad, oup_pad) of csrc/kernels/ir_crop_f32.hip ARENA_IRC_F32_CONFIGS
-# (oup_pad may be 1 or 2 output-channel groups of the configuration's width: 160 -> 320 runs as 2 x 160)
-IR_CROP_F32_CONFIGS = {(14, 1, 64, 64), (14, 1, 64, 96), (14, 1, 96, 96), (7, 2, 96, 160), (7, 1, 160, 160)}
+# (output side, stride, inp_pad, oup_pad) of csrc/kernels/ir_crop_f32.hip ARENA_IRX_CONFIGS (hidden chunks of 32)
+IR_CROP_F32_CONFIGS = {(14, 1, 64, 64), (14, 1, 64, 96), (14, 1, 96, 96), (7, 2, 96, 160), (7, 1, 160, 160),
+                       (7, 1, 160, 320)}
 
 
 def ir_dwproj_f32_supported(stride: int, hid_pad: int, oup_pad: int) -> bool:
@@ -77,7 +77,7 @@ def ir_crop_f32_supported(H: int, stride: int, inp_pad: int, hid_pad: int, oup_p
     """Mirror of arena::ir_block_crop_f32_supported (whole-map x3 kernel for the 14x14 / 7x7 stages)."""
     Ho = (H - 1) // stride + 1
     return (bool(expand) and hid_pad % 32 == 0 and H == Ho * stride
-            and any((Ho, stride, inp_pad) == c[:3] and oup_pad in (c[3], 2 * c[3]) for c in IR_CROP_F32_CONFIGS))
+            and (Ho, stride, inp_pad, oup_pad) in IR_CROP_F32_CONFIGS)
 
 
 def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand_cap: int,

@@ -18,7 +18,7 @@ import socket
 import subprocess
 import sys
 import time
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 
 def free_port() -> int:
@@ -35,6 +35,17 @@ class Replicas:
     specs: list = None  # (argv, env, gpu, log path) per replica, for restarts
     restarts: int = 0
     stopping: bool = False
+    # restart policy: the first restart of a replica is immediate, each further one waits backoff_s * 2^k
+    # (capped at backoff_max_s); a replica that failed max_restarts times in a row (each run shorter than
+    # healthy_s) is left down instead of crash-looping (every attempt initialises a GPU)
+    max_restarts: int = 5
+    backoff_s: float = 0.5
+    backoff_max_s: float = 30.0
+    healthy_s: float = 60.0
+    given_up: set = field(default_factory=set)
+    _fails: dict = field(default_factory=dict)
+    _next: dict = field(default_factory=dict)
+    _started: dict = field(default_factory=dict)
 
     def ports(self) -> list[int]:
         return [self.port + self.stride * r for r in range(len(self.procs))] if self.stride else [self.port]
@@ -62,22 +73,35 @@ class Replicas:
 
     def supervise(self) -> int:
         """Restart replicas that exited with a non-zero code (device fault: code 3) as fresh child
-        processes on the same GPU and port; returns the number restarted by this call."""
+        processes on the same GPU, port and replica rank; returns the number restarted by this call."""
         n = 0
         if self.stopping or not self.specs:
             return 0
+        now = time.time()
         for i, p in enumerate(self.procs):
             rc = p.poll()
-            if rc is None or rc == 0:
+            if rc is None or rc == 0 or i in self.given_up or now < self._next.get(i, 0.0):
+                continue
+            if now - self._started.get(i, 0.0) >= self.healthy_s:
+                self._fails[i] = 0  # it served for a while before failing: not a crash loop
+            k = self._fails.get(i, 0)
+            if k >= self.max_restarts:
+                self.given_up.add(i)
+                print(f"replica {i}: exited rc={rc} after {k} restarts in a row; leaving it down", flush=True)
                 continue
             argv, env, gpu, log = self.specs[i]
             e = dict(env)
-            # the start-up process group is gone: the new process serves alone with the seeded weights
+            # the start-up process group is gone: the new process serves alone with the seeded weights, on
+            # its original port and replica tag (ARENA_REPLICA_RANK; RANK is 0 in its one-process world)
             e.update({"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "ARENA_REPLICA_GPU": str(gpu),
+                      "ARENA_REPLICA_RANK": env.get("ARENA_REPLICA_RANK", env.get("RANK", str(i))),
                       "ARENA_RESTARTED": str(self.restarts + 1)})
             e.pop("MASTER_PORT", None)
             out = open(log, "a") if log else subprocess.DEVNULL
             self.procs[i] = subprocess.Popen(argv, env=e, stdout=out, stderr=subprocess.STDOUT)
+            self._fails[i] = k + 1
+            self._started[i] = now
+            self._next[i] = now + min(self.backoff_max_s, self.backoff_s * 2 ** k)
             self.restarts += 1
             n += 1
         return n
@@ -118,7 +142,9 @@ def launch(arch: str, n: int, *, port: int = 8100, stride: int = 0, host: str = 
                 "--port", str(port), "--port-stride", str(stride)]
         procs.append(subprocess.Popen(argv, env=e, stdout=out, stderr=subprocess.STDOUT))
         specs.append((argv, e, first_gpu + r // procs_per_gpu, log))
-    return Replicas(procs, port, stride, specs)
+    rep = Replicas(procs, port, stride, specs)
+    rep._started = {i: time.time() for i in range(world)}
+    return rep
 
 
 def main(argv=None) -> int:

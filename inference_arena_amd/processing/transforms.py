@@ -37,15 +37,39 @@ def _imagenet_stats() -> tuple[np.ndarray, np.ndarray]:
 IMAGENET_MEAN, IMAGENET_STD = _imagenet_stats()
 
 
+class ImageTooLargeError(ValueError):
+    """An upload whose header declares more pixels than ``max_image_pixels()`` (a decompression bomb: a few KB
+    of JPEG that would decode to gigabytes).  Servers answer 413."""
+
+
+def max_image_pixels() -> int:
+    """``ARENA_MAX_IMAGE_PIXELS`` (default 50 MP, above any camera frame the arena serves; the reference's
+    cv2.imdecode stops at 2^30 pixels, CV_IO_MAX_IMAGE_PIXELS)."""
+    import os
+
+    return int(os.environ.get("ARENA_MAX_IMAGE_PIXELS", str(50_000_000)))
+
+
+def _check_size(im, what: str) -> None:
+    w, h = im.size
+    if w * h > max_image_pixels():
+        raise ImageTooLargeError(f"{what}: image too large ({w}x{h} pixels > {max_image_pixels()})")
+
+
 def _decode(data: bytes | Path | str, what: str) -> np.ndarray:
     from PIL import Image, UnidentifiedImageError
 
     try:
         src = io.BytesIO(data) if isinstance(data, (bytes, bytearray, memoryview)) else str(data)
         with Image.open(src) as im:
+            _check_size(im, what)
             if im.mode != "RGB":  # convert() of an RGB image is a full copy
                 im = im.convert("RGB")
             arr = np.asarray(im, dtype=np.uint8)
+    except ImageTooLargeError:
+        raise
+    except Image.DecompressionBombError as e:
+        raise ImageTooLargeError(f"{what}: image too large ({e})") from e
     except (UnidentifiedImageError, OSError, ValueError) as e:
         raise ValueError(f"{what}: {e}") from e
     return np.ascontiguousarray(arr)
@@ -60,10 +84,15 @@ def decode_rgb(data: bytes | memoryview) -> tuple[int, int, bytes]:
         raise ValueError("Failed to decode image: empty payload")
     try:
         with Image.open(io.BytesIO(data)) as im:
+            _check_size(im, "Failed to decode image")
             if im.mode != "RGB":
                 im = im.convert("RGB")
             w, h = im.size
             return h, w, im.tobytes()
+    except ImageTooLargeError:
+        raise
+    except Image.DecompressionBombError as e:
+        raise ImageTooLargeError(f"Failed to decode image: image too large ({e})") from e
     except (UnidentifiedImageError, OSError, ValueError) as e:
         raise ValueError(f"Failed to decode image: {e}") from e
 

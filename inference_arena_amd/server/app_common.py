@@ -51,8 +51,16 @@ class DecodePool:
             self.pool = ThreadPoolExecutor(max_workers=max(1, threads), thread_name_prefix="decode")
 
     async def decode(self, data: bytes) -> np.ndarray:
+        """Raises ``TooLarge`` (servers answer 413) for a header that declares more pixels than the decoder
+        accepts (processing/transforms.py ImageTooLargeError), ``ValueError`` for any other decode failure."""
+        from ..processing.transforms import ImageTooLargeError
+        from .batching import TooLarge
+
         if self.procs is None:
-            return await asyncio.get_running_loop().run_in_executor(self.pool, load_image_from_bytes, data)
+            try:
+                return await asyncio.get_running_loop().run_in_executor(self.pool, load_image_from_bytes, data)
+            except ImageTooLargeError as e:
+                raise TooLarge(str(e)) from e
         loop = asyncio.get_running_loop()
         fut: asyncio.Future = loop.create_future()
 
@@ -64,7 +72,7 @@ class DecodePool:
         await loop.run_in_executor(None, self.procs.submit, data, None, done)
         img, err = await fut
         if err is not None:
-            raise ValueError(err)
+            raise TooLarge(err) if "image too large" in err else ValueError(err)
         return img
 
     def close(self) -> None:

@@ -65,8 +65,8 @@ def _worker(idx: int, shm_name: str, in_bytes: int, slot_bytes: int, tasks, resu
             data = msg[_TASK.size:] if n < 0 else buf[base:base + n]
             try:
                 h, w, px = decode_rgb(data)
-            except ValueError as e:
-                text = str(e).encode()[:slot_bytes]
+            except Exception as e:  # noqa: BLE001 - any decoder failure (MemoryError included) is this upload's
+                text = (str(e) or type(e).__name__).encode()[:slot_bytes]
                 buf[base + in_bytes:base + in_bytes + len(text)] = text
                 os.write(rfd, _DONE.pack(key, slot, 0, 0, _ERR, len(text)))
                 continue
@@ -117,7 +117,11 @@ class ProcessDecodePool:
         self._free: queue.SimpleQueue = queue.SimpleQueue()
         for s in range(self.slots):
             self._free.put(s)
-        self._cbs: dict[int, tuple[object, DecodeCallback, int]] = {}
+        self._cbs: dict[int, tuple[object, DecodeCallback, int, int]] = {}  # key -> (tag, callback, worker, slot)
+        self._ctx = ctx
+        self._handled_dead: set[int] = set()
+        self.dead_workers = 0      # workers that died (native mode: the owner restarts the process)
+        self.respawned = 0
         self._lock = threading.Lock()
         self._seq = 0
         self._closed = False
@@ -127,6 +131,60 @@ class ProcessDecodePool:
         if not self.native:
             self._collector = threading.Thread(target=self._collect, name="arena-decode-collector", daemon=True)
             self._collector.start()
+        self._watcher = threading.Thread(target=self._watch, name="arena-decode-watchdog", daemon=True)
+        self._watcher.start()
+
+    def _spawn(self, i: int):
+        tr, tw = self._ctx.Pipe(duplex=False)
+        br, bw = self._ctx.Pipe(duplex=False)
+        p = self._ctx.Process(target=_worker, args=(i, self.shm.name, self.in_bytes, self.slot_bytes, tr,
+                                                    self._res_w, bw), daemon=True, name=f"arena-decode-{i}")
+        p.start()
+        tr.close()
+        bw.close()
+        return p, tw, br
+
+    def _watch(self) -> None:
+        """A worker that died (killed, or a crash in the decoder library) would leave its pending uploads
+        unanswered and their slots taken forever.  Python mode: fail those uploads, free their slots and
+        spawn a replacement worker.  Native mode (the C++ front end owns the pipes): count the death; the
+        owner leaves rotation and exits non-zero so its supervisor restarts the process
+        (server/native_front.py)."""
+        import time
+
+        while not self._closed:
+            time.sleep(0.2)
+            for i, proc in enumerate(list(self.procs)):
+                if self._closed or proc.is_alive() or (self.native and i in self._handled_dead):
+                    continue
+                self._worker_died(i)
+
+    def _worker_died(self, i: int) -> None:
+        if self.native:
+            self._handled_dead.add(i)
+            self.dead_workers += 1
+            return
+        with self._send_locks[i]:
+            if self._closed or self.procs[i].is_alive():
+                return
+            self.dead_workers += 1
+            with self._lock:
+                failed = [(k, self._cbs.pop(k)) for k in [k for k, v in self._cbs.items() if v[2] == i]]
+                self._load[i] = 0
+            for c in (self._tasks[i], self._big[i]):
+                try:
+                    c.close()
+                except OSError:
+                    pass
+            self.procs[i], self._tasks[i], self._big[i] = self._spawn(i)
+            self.respawned += 1
+        for _key, (tag, cb, _w, slot) in failed:
+            try:
+                cb(tag, None, "Failed to decode image: decode worker died")
+            except Exception:  # noqa: BLE001 - a failing consumer must not stop the pool
+                pass
+            finally:
+                self._free.put(slot)
 
     def native_channel(self) -> dict:
         """Shared-memory address, geometry and pipe descriptors for a native driver (see __init__)."""
@@ -149,20 +207,32 @@ class ProcessDecodePool:
             raise RuntimeError("a native decode pool is driven through native_channel()")
         slot = self._free.get()
         n = len(data)
+        if n <= self.in_bytes:
+            base = slot * self._stride
+            self.shm.buf[base:base + n] = data
         with self._lock:
             self._seq += 1
             key = self._seq
             w = min(range(self.workers), key=self._load.__getitem__)
-            self._load[w] += 1
-            self._cbs[key] = (tag, callback, w)
-        if n <= self.in_bytes:
-            base = slot * self._stride
-            self.shm.buf[base:base + n] = data
-            msg = _TASK.pack(key, slot, n)
-        else:
-            msg = _TASK.pack(key, slot, -1) + bytes(data)
+        # registration and send under the worker's send lock: the watchdog fails a dead worker's keys and
+        # replaces its pipe under the same lock, so a key is never sent to a worker it was not failed for
         with self._send_locks[w]:
-            self._tasks[w].send_bytes(msg)
+            with self._lock:
+                self._load[w] += 1
+                self._cbs[key] = (tag, callback, w, slot)
+            msg = _TASK.pack(key, slot, n) if n <= self.in_bytes else _TASK.pack(key, slot, -1) + bytes(data)
+            try:
+                self._tasks[w].send_bytes(msg)
+                return
+            except OSError:  # the worker died: answer this upload now; the watchdog replaces the worker
+                with self._lock:
+                    entry = self._cbs.pop(key, None)
+                    self._load[w] -= 1
+        if entry is not None:
+            try:
+                callback(tag, None, "Failed to decode image: decode worker unavailable")
+            finally:
+                self._free.put(slot)
 
     def _collect(self) -> None:
         fd = self._res_r.fileno()
@@ -183,14 +253,21 @@ class ProcessDecodePool:
 
     def _complete(self, key, slot, h, w, status, aux) -> None:
         with self._lock:
-            tag, cb, worker = self._cbs.pop(key)
+            entry = self._cbs.pop(key, None)
+            if entry is None:  # already failed by the watchdog (its worker died after posting): slot freed there
+                return
+            tag, cb, worker, _ = entry
             self._load[worker] -= 1
         out = slot * self._stride + self.in_bytes
         try:
             if status == _ERR:
                 cb(tag, None, bytes(self.shm.buf[out:out + aux]).decode(errors="replace"))
             elif status == _BIG:
-                px = self._big[aux].recv_bytes()
+                try:
+                    px = self._big[aux].recv_bytes()
+                except (EOFError, OSError):
+                    cb(tag, None, "Failed to decode image: decode worker died")
+                    return
                 cb(tag, np.frombuffer(px, dtype=np.uint8).reshape(h, w, 3), None)
             else:
                 cb(tag, np.ndarray((h, w, 3), dtype=np.uint8, buffer=self.shm.buf, offset=out), None)

@@ -74,19 +74,30 @@ class _Collector:
         yield oc
 
 
+def _http_timeouts() -> dict:
+    out = {}
+    for key, env in (("idle_timeout_ms", "ARENA_HTTP_IDLE_TIMEOUT_MS"), ("read_timeout_ms", "ARENA_HTTP_READ_TIMEOUT_MS")):
+        if os.environ.get(env):
+            out[key] = int(os.environ[env])
+    return out
+
+
 class NativeFrontEnd:
     """The native HTTP server over a DynamicBatcher plus its decode processes."""
 
     def __init__(self, batcher, labels: list[str], *, port: int = 8100, host: str = "0.0.0.0",
                  io_threads: int = 4, decode_procs: int = 8, slots: int = 512, softmax: bool = False,
-                 arch: str = "monolithic", gpu: str = "0", replica_tag: str = ""):
+                 arch: str = "monolithic", gpu: str = "0", replica_tag: str = "", **http: int):
+        """``http``: further FrontConfig fields (max_body, idle_timeout_ms, read_timeout_ms; defaults from
+        ARENA_HTTP_IDLE_TIMEOUT_MS / ARENA_HTTP_READ_TIMEOUT_MS, else csrc/runtime/http_front.h)."""
         from ..ops import native
 
         self.batcher = batcher
         self.pool = ProcessDecodePool(workers=decode_procs, slots=slots, native=True)
         self.fe = native().HttpFrontEnd(batcher, self.pool.native_channel(), list(labels),
                                         {"host": host, "port": int(port), "io_threads": int(io_threads),
-                                         "softmax_confidence": bool(softmax), "replica_tag": str(replica_tag)})
+                                         "softmax_confidence": bool(softmax), "replica_tag": str(replica_tag),
+                                         **_http_timeouts(), **{k: int(v) for k, v in http.items()}})
         self.registry = CollectorRegistry()
         self.registry.register(_Collector(self, arch, gpu))
         self._stop = threading.Event()
@@ -152,8 +163,15 @@ def serve(settings: Settings | None = None, *, weights=None, replica_tag: str = 
             signal.signal(sig, lambda *_: done.set())
     rc = 0
     while not done.wait(0.5):
-        if batcher.stats()["failed"] > 0:  # a failed batch = a device fault: leave rotation, let the launcher restart
-            log.error("device fault: batches failed; exiting for a restart")
+        # A batch that failed with a HIP runtime error poisons this process's device context, and a dead decode
+        # worker leaves its uploads unanswered (the native front end owns its pipes): leave rotation and exit 3
+        # so the replica launcher restarts the process.  Other failed batches (an input the staging pool cannot
+        # take) only fail their own requests (batching.is_device_fault; reference: 500 per request).
+        st = batcher.stats()
+        reason = (f"device fault: {st.get('last_error', '')}" if st.get("device_faults", 0) > 0 else
+                  "decode worker died" if front.pool.dead_workers > 0 else None)
+        if reason:
+            log.error(f"{reason}; exiting for a restart")
             front.set_healthy(False)
             front.fe.drain()  # leave the SO_REUSEPORT group; answer what is in flight
             time.sleep(1.0)

@@ -109,7 +109,7 @@ def build_app(arch: str, settings, info):
     raise ValueError(f"unknown arch '{arch}'")
 
 
-def _serve_native(settings, info, port: int) -> int:
+def _serve_native(settings, info, port: int, rank: int | None = None) -> int:
     """``ARENA_NATIVE_HTTP=1``: the monolithic replica behind the native C++ front end
     (server/native_front.py) with rank 0's broadcast weights; exits 3 after a device fault."""
     import numpy as np
@@ -127,7 +127,7 @@ def _serve_native(settings, info, port: int) -> int:
     D.barrier(info)
     D.shutdown(info)
     settings.PORT = port
-    return serve(settings, weights=np.ascontiguousarray(blob), replica_tag=str(info.rank),
+    return serve(settings, weights=np.ascontiguousarray(blob), replica_tag=str(info.rank if rank is None else rank),
                  devices=[int(settings.ARENA_GPU)])
 
 
@@ -158,18 +158,20 @@ def main(argv=None) -> int:
             import torch
 
             torch.cuda.set_device(settings.ARENA_GPU)
+    # a restarted replica runs in a one-process world (RANK 0) but keeps its original port and tag
+    rank = int(os.environ.get("ARENA_REPLICA_RANK", info.rank))
     if a.arch == "monolithic" and settings.ARENA_DEVICE != "cpu" and os.environ.get("ARENA_NATIVE_HTTP") == "1":
-        return _serve_native(settings, info, a.port + a.port_stride * info.rank)
+        return _serve_native(settings, info, a.port + a.port_stride * rank, rank)
     app = build_app(a.arch, settings, info)
     D.barrier(info)
     D.shutdown(info)  # the group is only needed for start-up
 
-    port = a.port + a.port_stride * info.rank
+    port = a.port + a.port_stride * rank
     if a.arch in ("detection", "gateway") and os.environ.get("ARENA_NATIVE_HTTP") == "1":
         # native HTTP/multipart layer, the arm's request handler stays in Python (server/native_handler.py)
         from .native_handler import serve_app
 
-        rc = asyncio.run(serve_app(app, port=port, host=a.host, replica_tag=str(info.rank),
+        rc = asyncio.run(serve_app(app, port=port, host=a.host, replica_tag=str(rank),
                                    io_threads=int(os.environ.get("ARENA_HTTP_THREADS", "2")),
                                    reuse_port=a.port_stride == 0))
         if rc and os.environ.get("ARENA_EXIT_ON_FAULT", "1") == "1":
@@ -177,7 +179,7 @@ def main(argv=None) -> int:
             return 3
         return 0
     sock = _socket(a.host, port, reuse_port=a.port_stride == 0)
-    server = uvicorn.Server(uvicorn.Config(ReplicaTag(app, info.rank), log_level="warning", access_log=False))
+    server = uvicorn.Server(uvicorn.Config(ReplicaTag(app, rank), log_level="warning", access_log=False))
     fault: list[str] = []
 
     async def watchdog():

@@ -2,8 +2,9 @@
 # hardware counters of the fused fp32 IR kernels on MobileNetV2 block shapes (tools/bench_irc.py),
 # one rocprofv3 --pmc pass per counter set; prints per-kernel averages
 set -u
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 export TMPDIR=/tmp
+export ARENA_IRC_F32=1
 T=${1:-pmc_irc}
 mkdir -p gpurun_out/$T
 i=0
@@ -12,7 +13,7 @@ for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_IN
            "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 -s KILL 120 rocprofv3 --kernel-trace --pmc $set --output-format csv -d gpurun_out/$T/s$i -o run -- \
-    python3 tools/bench_irc.py --reps 3 > gpurun_out/$T/s$i.log 2>&1
+    python3 tools/bench_irc.py --small --reps 3 > gpurun_out/$T/s$i.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "set $i failed rc=$rc"; tail -5 gpurun_out/$T/s$i.log; exit 99; fi
 done
@@ -24,7 +25,7 @@ acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"gpurun_out/{T}/s*/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        if "ir_crop_f32" not in k and "ir_f32" not in k:
+        if "ir_x3" not in k and "ir_f32" not in k:
             continue
         acc[k[k.find("<"):k.find(">") + 1] or k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in acc.items():

@@ -63,3 +63,46 @@ def test_pool_paths(payloads):
         else:
             assert err is None
             assert np.array_equal(view, load_image_from_bytes(p))
+
+
+def _bomb_jpeg(h: int = 40000, w: int = 40000) -> bytes:
+    """A valid 16x16 JPEG whose SOF0 header declares h x w pixels: a few hundred bytes that would decode to
+    gigabytes (one such upload used to kill a decode worker)."""
+    data = bytearray(_jpeg(16, 16, 5))
+    i = data.index(b"\xff\xc0")  # baseline SOF0: marker, length(2), precision(1), height(2), width(2)
+    data[i + 5:i + 7] = h.to_bytes(2, "big")
+    data[i + 7:i + 9] = w.to_bytes(2, "big")
+    return bytes(data)
+
+
+def test_decode_rgb_rejects_decompression_bomb():
+    from inference_arena_amd.processing.transforms import ImageTooLargeError
+
+    with pytest.raises(ImageTooLargeError, match="image too large"):
+        decode_rgb(_bomb_jpeg())
+    with pytest.raises(ImageTooLargeError):
+        load_image_from_bytes(_bomb_jpeg())
+
+
+def test_pool_survives_bomb_and_dead_worker(payloads):
+    """A bomb upload comes back as an error and the worker keeps serving; a worker killed from outside is
+    replaced by the watchdog, and the pool keeps answering (no slot or callback is lost)."""
+    import os
+    import signal
+    import time
+
+    with ProcessDecodePool(workers=2, slots=8) as pool:
+        out = _run(pool, [_bomb_jpeg(), payloads[0], _bomb_jpeg(30000, 5000), payloads[1]])
+        assert out[0][0] is None and "image too large" in out[0][1]
+        assert out[2][0] is None and "image too large" in out[2][1]
+        np.testing.assert_array_equal(out[1][0], load_image_from_bytes(payloads[0]))
+        assert out[3][1] is None
+        os.kill(pool.procs[0].pid, signal.SIGKILL)
+        t0 = time.time()
+        while pool.respawned < 1 and time.time() - t0 < 30:
+            time.sleep(0.1)
+        assert pool.respawned == 1 and pool.dead_workers == 1
+        out = _run(pool, payloads * 3)  # more uploads than slots: every slot came back
+        assert all(err is None for _, err in out.values())
+        for i, p in enumerate(payloads * 3):
+            np.testing.assert_array_equal(out[i][0], load_image_from_bytes(p))

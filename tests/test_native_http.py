@@ -155,3 +155,96 @@ def test_health_metrics_and_concurrency(server):
     assert r.status == 503 and json.loads(r.read())["status"] == "unhealthy"
     fe.set_healthy(True)
     c.close()
+
+
+@pytest.fixture(scope="module")
+def tight_server():
+    """A front end with a 1 MB body limit and short timeouts (the hardening paths)."""
+    C = native()
+    batcher = C.DynamicBatcher([C.EchoInstance(2, 8, 4)], {"max_batch": 8, "max_queue_delay_us": 200})
+    fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=2, decode_procs=1,
+                        slots=8, max_body=1 << 20, idle_timeout_ms=1500, read_timeout_ms=1500)
+    yield fe
+    fe.close()
+    batcher.shutdown()
+
+
+def _raw(port, data: bytes, read_timeout=10.0) -> bytes:
+    import socket
+
+    s = socket.create_connection(("127.0.0.1", port), timeout=read_timeout)
+    try:
+        s.sendall(data)
+        out = b""
+        while True:
+            try:
+                k = s.recv(65536)
+            except (ConnectionResetError, socket.timeout):
+                break
+            if not k:
+                break
+            out += k
+            if b"\r\n\r\n" in out and b"Connection: close" in out:
+                break
+        return out
+    finally:
+        s.close()
+
+
+def test_chunked_overflow_and_saturated_size_rejected(tight_server):
+    """A chunk size that saturates strtoll (or simply exceeds the body limit) is a 413, not an endless wait
+    (the signed sum overflowed and bypassed max_body)."""
+    fe = tight_server
+    head = b"POST /predict HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\nContent-Type: image/png\r\n\r\n"
+    r = _raw(fe.port, head + b"7fffffffffffffffffff\r\nabc")
+    assert r.startswith(b"HTTP/1.1 413"), r[:80]
+    r = _raw(fe.port, head + b"200000\r\n" + b"x" * 100)  # 2 MB chunk > 1 MB limit, announced up front
+    assert r.startswith(b"HTTP/1.1 413"), r[:80]
+    r = _raw(fe.port, head + b"zz\r\n")
+    assert r.startswith(b"HTTP/1.1 400"), r[:80]
+
+
+def test_pipelined_flood_does_not_grow_unbounded(tight_server):
+    """A client that keeps sending while its request is in flight is read up to one maximal request, then
+    paused; its first request is still answered and the server keeps serving others."""
+    import socket
+
+    fe = tight_server
+    body, ct = _multipart(_jpeg(16, 16, 1))
+    req = (f"POST /predict HTTP/1.1\r\nHost: x\r\nContent-Type: {ct}\r\nContent-Length: {len(body)}\r\n\r\n"
+           ).encode() + body
+    s = socket.create_connection(("127.0.0.1", fe.port), timeout=10)
+    sent = 0
+    junk = b"GET /health HTTP/1.1\r\nHost: x\r\n\r\n" * 2000
+    try:
+        s.sendall(req)
+        s.setblocking(False)
+        for _ in range(400):  # ~27 MB offered: far beyond the 1 MB + 64 KB input cap
+            try:
+                sent += s.send(junk)
+            except BlockingIOError:
+                break
+        assert sent < 8 << 20  # the kernel buffers filled: the server stopped reading
+    finally:
+        s.close()
+    st, _, c = _post(fe.port, body, ct)  # still serving
+    assert st == 200
+    c.close()
+
+
+def test_idle_and_trickling_connections_time_out(tight_server):
+    import socket
+    import time
+
+    fe = tight_server
+    before = fe.stats()["timeouts"]
+    idle = socket.create_connection(("127.0.0.1", fe.port), timeout=10)
+    trickle = socket.create_connection(("127.0.0.1", fe.port), timeout=10)
+    trickle.sendall(b"POST /predict HTTP/1.1\r\nHost: x\r\n")  # headers never finish
+    t0 = time.time()
+    for s in (idle, trickle):
+        assert s.recv(1) == b""  # closed by the server
+    assert 1.0 < time.time() - t0 < 8.0
+    assert fe.stats()["timeouts"] >= before + 2
+    idle.close()
+    trickle.close()

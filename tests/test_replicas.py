@@ -108,3 +108,34 @@ def test_router_forwards_to_live_replicas(tmp_path):
         for s, t, _ in servers:
             s.should_exit = True
             t.join(10)
+
+
+def test_supervise_keeps_rank_and_backs_off(tmp_path):
+    """A restarted replica keeps its port / tag (ARENA_REPLICA_RANK = its original rank), the first restart is
+    immediate, further ones back off exponentially, and a crash-looping replica is left down after
+    max_restarts (restarts came back as rank 0 every 0.5 s forever)."""
+    import time
+
+    from inference_arena_amd.parallel.replicas import Replicas
+
+    # each "replica" writes its ARENA_REPLICA_RANK and exits 3 (a device fault) at once
+    out = tmp_path / "ranks.txt"
+    argv = [sys.executable, "-c",
+            f"import os; open({str(out)!r}, 'a').write(os.environ['ARENA_REPLICA_RANK'] + '\\n'); raise SystemExit(3)"]
+    procs = [subprocess.Popen([sys.executable, "-c", "raise SystemExit(3)"]) for _ in range(2)]
+    for p in procs:
+        p.wait()
+    specs = [(argv, {"RANK": str(r), "PATH": os.environ.get("PATH", "")}, r, None) for r in range(2)]
+    rep = Replicas(procs, 8100, 1, specs, max_restarts=3, backoff_s=0.2, healthy_s=60.0)
+    assert rep.supervise() == 2  # first restart: immediate
+    for p in rep.procs:
+        p.wait()
+    assert rep.supervise() == 0  # inside the backoff window
+    deadline = time.time() + 30
+    while len(rep.given_up) < 2 and time.time() < deadline:
+        rep.supervise()
+        for p in rep.procs:
+            p.wait()
+        time.sleep(0.05)
+    assert rep.given_up == {0, 1} and rep.restarts == 6  # 3 restarts each, then left down
+    assert sorted(out.read_text().split()) == ["0", "0", "0", "1", "1", "1"]
