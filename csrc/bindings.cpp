@@ -14,6 +14,7 @@
 #include "runtime/executor.h"
 #include "runtime/echo_instance.h"
 #include "runtime/http_front.h"
+#include "runtime/http_loadgen.h"
 #include "runtime/batcher.h"
 #include "runtime/split.h"
 
@@ -406,6 +407,15 @@ PYBIND11_MODULE(_C, m) {
              py::gil_scoped_release nogil;
              e.set_weights_device((const void*)ptr, bytes);
            })
+      .def("weights_host",
+           [](Executor& e) {
+             std::vector<uint8_t> v;
+             {
+               py::gil_scoped_release nogil;
+               v = e.weights_host();
+             }
+             return py::bytes((const char*)v.data(), v.size());
+           })
       .def("set_program",
            [](Executor& e, py::array_t<int64_t, py::array::c_style> ops, py::array_t<int64_t, py::array::c_style> cls) {
              if (ops.ndim() != 2 || ops.shape(1) != kOpFields || cls.ndim() != 2 || cls.shape(1) != kOpFields)
@@ -612,6 +622,61 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         b.shutdown();
       });
+
+  // closed-loop HTTP load generator (bench.py --path http, serving sweeps)
+  py::class_<HttpLoadGen>(m, "HttpLoadGen")
+      .def(py::init([](const py::dict& cfg, const py::list& requests) {
+             LoadGenConfig c;
+             c.host = get<std::string>(cfg, "host", c.host);
+             c.port = get<int>(cfg, "port", c.port);
+             c.users = get<int>(cfg, "users", c.users);
+             c.threads = get<int>(cfg, "threads", c.threads);
+             c.max_requests = get<int64_t>(cfg, "max_requests", c.max_requests);
+             std::vector<std::string> reqs;
+             for (auto r : requests) reqs.push_back(r.cast<std::string>());
+             return new HttpLoadGen(c, std::move(reqs));
+           }))
+      .def("start", [](HttpLoadGen& g) {
+        py::gil_scoped_release nogil;
+        g.start();
+      })
+      .def(
+          "stop",
+          [](HttpLoadGen& g, double timeout_s) {
+            py::gil_scoped_release nogil;
+            g.stop(timeout_s);
+          },
+          py::arg("timeout_s") = 30.0)
+      .def("completed", &HttpLoadGen::completed)
+      .def("connect_failures", &HttpLoadGen::connect_failures)
+      .def(
+          "wait_completed",
+          [](HttpLoadGen& g, int64_t n, double timeout_s) {
+            py::gil_scoped_release nogil;
+            return g.wait_completed(n, timeout_s);
+          },
+          py::arg("n"), py::arg("timeout_s") = 600.0)
+      .def(
+          "records",
+          [](HttpLoadGen& g, int64_t from, int64_t to) {
+            std::vector<LoadGenRecord> r = g.records(from, to);
+            py::array_t<double> t((py::ssize_t)r.size());
+            py::array_t<float> lat((py::ssize_t)r.size());
+            py::array_t<int16_t> st((py::ssize_t)r.size()), dets((py::ssize_t)r.size());
+            for (size_t i = 0; i < r.size(); ++i) {
+              t.mutable_data()[i] = r[i].t_done;
+              lat.mutable_data()[i] = r[i].latency;
+              st.mutable_data()[i] = r[i].status;
+              dets.mutable_data()[i] = r[i].dets;
+            }
+            py::dict d;
+            d["t_done"] = t;
+            d["latency"] = lat;
+            d["status"] = st;
+            d["dets"] = dets;
+            return d;
+          },
+          py::arg("from") = 0, py::arg("to") = -1);
 
   py::class_<HttpFrontEnd>(m, "HttpFrontEnd")
       .def(py::init([](DynamicBatcher& batcher, const py::dict& ch, std::vector<std::string> labels,

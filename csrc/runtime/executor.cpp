@@ -191,6 +191,15 @@ void Executor::set_weights_device(const void* dev, size_t bytes) {
   ARENA_HIP_CHECK(hipMemcpy(d_weights_, dev, bytes, hipMemcpyDeviceToDevice));
 }
 
+std::vector<uint8_t> Executor::weights_host() {
+  std::vector<uint8_t> out(weights_bytes_);
+  if (d_weights_ == nullptr || weights_bytes_ == 0) return out;
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  sync_slots();
+  ARENA_HIP_CHECK(hipMemcpy(out.data(), d_weights_, weights_bytes_, hipMemcpyDeviceToHost));
+  return out;
+}
+
 void Executor::set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops, int n_cls_ops) {
   prog_.resize(n_ops);
   for (int i = 0; i < n_ops; ++i) std::memcpy(prog_[i].data(), ops + (size_t)i * kOpFields, sizeof(OpRecord));

@@ -110,6 +110,8 @@ class Executor : public BatchInstance {
   void set_weights(const void* host, size_t bytes);
   // Same-size update from device memory of this executor's GPU (e.g. an RCCL broadcast buffer): D2D copy.
   void set_weights_device(const void* dev, size_t bytes);
+  // the device weight blob copied back to the host (replica bring-up check: every rank's bytes must hash equal)
+  std::vector<uint8_t> weights_host();
   void set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops, int n_cls_ops);
   // `impl` (optional, one entry per program op): conv kernel family per op from a persisted tuning table;
   // when given, the bucket is captured with exactly these choices and no timing runs (deterministic).

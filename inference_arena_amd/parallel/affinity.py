@@ -1,0 +1,118 @@
+"""Host-CPU placement of one serving rank per GPU.
+
+The reference runs every service in a container limited to 2 vCPU (experiment.yaml:250-267); on an
+MI355X node the host work per request (HTTP, multipart, JPEG decode, batching) is what scales with
+the GPU count, so each rank gets its own CPU share next to its GPU:
+
+* ``gpu_local_cpus(local_rank)`` reads the KFD topology in sysfs (no HIP call, so it is safe before
+  any process is spawned or exec'd): the ``local_rank``-th GPU node, its PCI address and that
+  device's ``local_cpulist`` (the CPUs of its NUMA node);
+* ``rank_cpu_share(local_rank, local_world)`` splits those CPUs between the ranks whose GPUs sit on
+  the same NUMA node, intersected with the CPUs this process may use; the decode workers pin
+  themselves to that share (server/decode_pool.py ``cpus=``) and the rank process keeps the same set.
+
+Everything degrades to "no pinning" (None) when the topology is unreadable (CPU-only hosts, containers
+without /sys/class/kfd)."""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+KFD_NODES = Path("/sys/class/kfd/kfd/topology/nodes")
+
+
+def _parse_cpulist(text: str) -> list[int]:
+    out: list[int] = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return out
+
+
+def _props(node: Path) -> dict[str, int]:
+    d: dict[str, int] = {}
+    try:
+        for line in (node / "properties").read_text().splitlines():
+            k, _, v = line.partition(" ")
+            try:
+                d[k] = int(v)
+            except ValueError:
+                pass
+    except OSError:
+        pass
+    return d
+
+
+def gpu_nodes(root: Path = KFD_NODES) -> list[dict[str, int]]:
+    """KFD GPU nodes (simd_count > 0) in node order, which is HIP's device order without HIP_VISIBLE_DEVICES."""
+    if not root.is_dir():
+        return []
+    nodes = sorted((p for p in root.iterdir() if p.name.isdigit()), key=lambda p: int(p.name))
+    return [pr for pr in (_props(n) for n in nodes) if pr.get("simd_count", 0) > 0]
+
+
+def _pci_dir(props: dict[str, int], pci_root: Path = Path("/sys/bus/pci/devices")) -> Path | None:
+    loc = props.get("location_id")
+    if loc is None:
+        return None
+    bus, dev, fn = (loc >> 8) & 0xFF, (loc >> 3) & 0x1F, loc & 0x7
+    p = pci_root / f"{props.get('domain', 0):04x}:{bus:02x}:{dev:02x}.{fn:x}"
+    return p if p.exists() else None
+
+
+def gpu_local_cpus(local_rank: int, root: Path = KFD_NODES, pci_root: Path = Path("/sys/bus/pci/devices")
+                   ) -> tuple[list[int] | None, int]:
+    """(CPUs of the NUMA node of GPU ``local_rank`` or None, that NUMA node id or -1)."""
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    nodes = gpu_nodes(root)
+    idx = local_rank
+    if vis:
+        try:
+            idx = [int(v) for v in vis.split(",")][local_rank]
+        except (ValueError, IndexError):
+            return None, -1
+    if idx >= len(nodes):
+        return None, -1
+    d = _pci_dir(nodes[idx], pci_root)
+    if d is None:
+        return None, -1
+    try:
+        cpus = _parse_cpulist((d / "local_cpulist").read_text())
+        numa = int((d / "numa_node").read_text().strip())
+    except (OSError, ValueError):
+        return None, -1
+    return (cpus or None), numa
+
+
+def rank_cpu_share(local_rank: int, local_world: int, root: Path = KFD_NODES,
+                   pci_root: Path = Path("/sys/bus/pci/devices")) -> list[int] | None:
+    """This rank's CPUs: its GPU's NUMA-local CPUs that this process may use, split evenly (contiguous
+    blocks) between the ranks whose GPUs share that NUMA node.  None when unknown."""
+    mine, numa = gpu_local_cpus(local_rank, root, pci_root)
+    if not mine:
+        return None
+    allowed = set(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else set(mine)
+    local = [c for c in mine if c in allowed]
+    if not local:
+        return None
+    peers = [r for r in range(local_world) if gpu_local_cpus(r, root, pci_root)[1] == numa] or [local_rank]
+    k, n = peers.index(local_rank) if local_rank in peers else 0, len(peers)
+    per = max(1, len(local) // n)
+    share = local[k * per:(k + 1) * per] if k < n - 1 else local[k * per:]
+    return share or local
+
+
+def pin(cpus: list[int] | None) -> bool:
+    """Restrict the calling process (and the threads it creates afterwards) to ``cpus``."""
+    if not cpus or not hasattr(os, "sched_setaffinity"):
+        return False
+    try:
+        os.sched_setaffinity(0, cpus)
+        return True
+    except OSError:
+        return False

@@ -48,8 +48,15 @@ _DONE = struct.Struct("<qiiiiq")   # key, slot, h, w, status, aux
 _OK, _ERR, _BIG = 0, 1, 2          # pixels in slot / error text in slot (aux = length) / pixels on worker conn
 
 
-def _worker(idx: int, shm_name: str, in_bytes: int, slot_bytes: int, tasks, results_w, big_w) -> None:  # pragma: no cover - runs in a child
+def _worker(idx: int, shm_name: str, in_bytes: int, slot_bytes: int, tasks, results_w, big_w,
+            cpus=None) -> None:  # pragma: no cover - runs in a child
     from ..processing.transforms import decode_rgb
+
+    if cpus:  # this rank's host-CPU share (parallel/affinity.py), set inside the child
+        try:
+            os.sched_setaffinity(0, cpus)
+        except OSError:
+            pass
 
     shm = shared_memory.SharedMemory(name=shm_name)
     buf = shm.buf
@@ -89,7 +96,7 @@ class ProcessDecodePool:
     pool's collector thread and must consume the view before returning (the slot is reused afterwards)."""
 
     def __init__(self, workers: int | None = None, slots: int = 256, slot_pixels: int = 1024 * 1024,
-                 in_bytes: int = 1 << 20, native: bool = False):
+                 in_bytes: int = 1 << 20, native: bool = False, cpus: list[int] | None = None):
         """``native=True``: the parent side of the transport is driven by C++ (the native HTTP front end,
         csrc/runtime/http_front.h) through ``native_channel()``; no collector thread runs here."""
         self.workers = max(1, int(workers or min(16, os.cpu_count() or 4)))
@@ -97,18 +104,14 @@ class ProcessDecodePool:
         self.slot_bytes = int(slot_pixels) * 3
         self.in_bytes = int(in_bytes)
         self._stride = self.in_bytes + self.slot_bytes
+        self.cpus = list(cpus) if cpus else None
         self.shm = shared_memory.SharedMemory(create=True, size=self.slots * self._stride)
         ctx = mp.get_context("spawn")
+        self._ctx = ctx
         self._res_r, self._res_w = ctx.Pipe(duplex=False)
         self._tasks, self._big, self.procs = [], [], []
         for i in range(self.workers):
-            tr, tw = ctx.Pipe(duplex=False)
-            br, bw = ctx.Pipe(duplex=False)
-            p = ctx.Process(target=_worker, args=(i, self.shm.name, self.in_bytes, self.slot_bytes, tr,
-                                                  self._res_w, bw), daemon=True, name=f"arena-decode-{i}")
-            p.start()
-            tr.close()
-            bw.close()
+            p, tw, br = self._spawn(i)
             self._tasks.append(tw)
             self._big.append(br)
             self.procs.append(p)
@@ -118,7 +121,6 @@ class ProcessDecodePool:
         for s in range(self.slots):
             self._free.put(s)
         self._cbs: dict[int, tuple[object, DecodeCallback, int, int]] = {}  # key -> (tag, callback, worker, slot)
-        self._ctx = ctx
         self._handled_dead: set[int] = set()
         self.dead_workers = 0      # workers that died (native mode: the owner restarts the process)
         self.respawned = 0
@@ -138,7 +140,8 @@ class ProcessDecodePool:
         tr, tw = self._ctx.Pipe(duplex=False)
         br, bw = self._ctx.Pipe(duplex=False)
         p = self._ctx.Process(target=_worker, args=(i, self.shm.name, self.in_bytes, self.slot_bytes, tr,
-                                                    self._res_w, bw), daemon=True, name=f"arena-decode-{i}")
+                                                    self._res_w, bw, self.cpus), daemon=True,
+                              name=f"arena-decode-{i}")
         p.start()
         tr.close()
         bw.close()

@@ -248,3 +248,28 @@ def test_idle_and_trickling_connections_time_out(tight_server):
     assert fe.stats()["timeouts"] >= before + 2
     idle.close()
     trickle.close()
+
+
+def _http_request(body: bytes, ctype: str) -> bytes:
+    return (f"POST /predict HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: {ctype}\r\nContent-Length: {len(body)}\r\n"
+            f"\r\n").encode() + body
+
+
+def test_native_load_generator_closed_loop(server):
+    """The native closed-loop client (csrc/runtime/http_loadgen.cpp, bench.py's HTTP path): every response
+    is counted once, with its status and its detection count parsed from the JSON."""
+    fe, _ = server
+    reqs = []
+    for first in (1, 2, 3, 4):
+        body, ct = _multipart(_jpeg(24, 32, first))
+        reqs.append(_http_request(body, ct))
+    lg = native().HttpLoadGen({"host": "127.0.0.1", "port": fe.port, "users": 8, "threads": 2}, reqs)
+    lg.start()
+    assert lg.wait_completed(400, 60)
+    lg.stop(30)
+    r = lg.records(0, -1)
+    n = len(r["latency"])
+    assert n >= 400 and lg.completed() == n
+    assert (r["status"] == 200).all()
+    assert set(r["dets"].tolist()) <= {2, 3, 4, 1} and (r["latency"] > 0).all()
+    assert (np.diff(r["t_done"]) >= 0).all()  # completion order

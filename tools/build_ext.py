@@ -50,6 +50,7 @@ SOURCES = [
     "runtime/executor.cpp",
     "runtime/batcher.cpp",
     "runtime/http_front.cpp",
+    "runtime/http_loadgen.cpp",
     "runtime/trace.cpp",
     "bindings.cpp",
 ]
