@@ -110,6 +110,15 @@ def allgather_floats(vals: list[float], info: DistInfo) -> list[list[float]]:
     return out
 
 
+def allgather_objects(obj, info: DistInfo) -> list:
+    """Every rank's ``obj`` (picklable), in rank order."""
+    if info.world <= 1:
+        return [obj]
+    out: list = [None] * info.world
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def barrier(info: DistInfo) -> None:
     if info.world > 1:
         if info.backend == "nccl":

@@ -91,6 +91,15 @@ def _worker(idx: int, shm_name: str, in_bytes: int, slot_bytes: int, tasks, resu
         shm.close()
 
 
+def prestart() -> None:
+    """Start the multiprocessing fork server now.  Call this before the process initialises the GPU: decode
+    workers created later (pools built after the engines, replacements for dead workers) are then forked from
+    that GPU-free server instead of being fork+exec'd from a process holding GPU state."""
+    from multiprocessing import forkserver
+
+    forkserver.ensure_running()
+
+
 class ProcessDecodePool:
     """``submit(jpeg_bytes, tag, callback)``; ``callback(tag, rgb_view_or_None, error_or_None)`` runs on the
     pool's collector thread and must consume the view before returning (the slot is reused afterwards)."""
@@ -106,7 +115,10 @@ class ProcessDecodePool:
         self._stride = self.in_bytes + self.slot_bytes
         self.cpus = list(cpus) if cpus else None
         self.shm = shared_memory.SharedMemory(create=True, size=self.slots * self._stride)
-        ctx = mp.get_context("spawn")
+        # forkserver, not spawn: the fork server starts here (before this process touches the GPU) and every
+        # worker, including a replacement spawned after a worker died, is forked from it, never fork+exec'd from
+        # a process that holds GPU state
+        ctx = mp.get_context("forkserver")
         self._ctx = ctx
         self._res_r, self._res_w = ctx.Pipe(duplex=False)
         self._tasks, self._big, self.procs = [], [], []
@@ -188,6 +200,16 @@ class ProcessDecodePool:
                 pass
             finally:
                 self._free.put(slot)
+
+    def to_python_mode(self) -> None:
+        """Hand a native-mode pool back to Python (``submit``): call after the native driver stopped reading the
+        completion pipe (HttpFrontEnd.stop()); the same worker processes then serve Python callers."""
+        if not self.native:
+            return
+        self.native = False
+        self._handled_dead.clear()
+        self._collector = threading.Thread(target=self._collect, name="arena-decode-collector", daemon=True)
+        self._collector.start()
 
     def native_channel(self) -> dict:
         """Shared-memory address, geometry and pipe descriptors for a native driver (see __init__)."""

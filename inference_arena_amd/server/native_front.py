@@ -137,6 +137,9 @@ def serve(settings: Settings | None = None, *, weights=None, replica_tag: str = 
     from ..ops import native
     from .backends import settings_devices
 
+    from .decode_pool import prestart
+
+    prestart()  # the decode workers' fork server, before the engines touch the GPU
     settings = settings or Settings.from_env()
     setup_logging(settings.LOG_LEVEL)
     devices = list(devices) if devices is not None else settings_devices(settings)

@@ -146,6 +146,9 @@ def main(argv=None) -> int:
 
     import os
 
+    from .decode_pool import prestart
+
+    prestart()  # decode-worker fork server before any GPU initialisation (server/decode_pool.py)
     settings = Settings.from_env()
     per_gpu = max(1, int(os.environ.get("ARENA_PROCS_PER_GPU", "1")))
     backend = "gloo" if settings.ARENA_DEVICE == "cpu" or per_gpu > 1 else None

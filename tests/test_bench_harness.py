@@ -1,0 +1,71 @@
+"""bench.py's harness on CPU: the N-rank self-launch over gloo with the host-only
+fake engine, the HTTP path through the native front end and load generator, the replica weight check, and
+the per-rank CPU share derived from the KFD topology."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _bench(*args, env=None):
+    e = dict(os.environ, ARENA_DIST_BACKEND="gloo", PYTHONPATH=str(ROOT), **(env or {}))
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), "--fake-engine", "--steps", "2", "--warmup", "1",
+                           "--min-warmup-s", "0.3", "--users", "16", "--decode-workers", "2", *args],
+                          capture_output=True, text=True, timeout=600, env=e)
+
+
+def test_bench_two_ranks_self_launch_http():
+    r = _bench("--gpus", "2", "--latency-levels", "1,4")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["world_size_checked"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["path"] == "http" and out["errors"] == 0 and out["value"] > 0
+    assert out["weights_verified"] is True and out["collective_backend"] == "gloo"
+    assert len(out["per_rank_req_s"]) == 2 and len(out["cpu_share_per_rank"]) == 2
+    assert set(out["levels"]) == {"1", "4"} and out["bs1_p50_ms"] == out["levels"]["1"]["p50_ms"]
+    assert out["inproc"]["value"] > 0
+    assert out["ms_per_step"] * out["steps"] / 1e3 == pytest.approx(2 * 256 * 2 / out["value"], rel=1e-3)
+
+
+def test_bench_detects_diverging_replica_weights():
+    r = _bench("--gpus", "2", "--latency-levels", "", "--no-secondary-inproc", env={"ARENA_TEST_CORRUPT_WEIGHTS": "1"})
+    assert r.returncode != 0
+    assert "replica weights differ" in r.stderr
+
+
+def _fake_topology(tmp: Path, gpus_numa: list[int], cpus_per_numa: int = 8):
+    nodes = tmp / "nodes"
+    pci = tmp / "pci"
+    (nodes / "0").mkdir(parents=True)
+    (nodes / "0" / "properties").write_text("cpu_cores_count 64\nsimd_count 0\n")  # the CPU node
+    for g, numa in enumerate(gpus_numa):
+        n = nodes / str(g + 1)
+        n.mkdir()
+        bus = 0x10 + g
+        (n / "properties").write_text(f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+        d = pci / f"0000:{bus:02x}:00.0"
+        d.mkdir(parents=True)
+        lo = numa * cpus_per_numa
+        (d / "local_cpulist").write_text(f"{lo}-{lo + cpus_per_numa - 1}\n")
+        (d / "numa_node").write_text(f"{numa}\n")
+    return nodes, pci
+
+
+def test_rank_cpu_share_splits_numa_nodes(tmp_path, monkeypatch):
+    from inference_arena_amd.parallel import affinity
+
+    nodes, pci = _fake_topology(tmp_path, [0, 0, 1, 1])
+    monkeypatch.setattr(affinity.os, "sched_getaffinity", lambda pid: set(range(16)), raising=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    shares = [affinity.rank_cpu_share(r, 4, nodes, pci) for r in range(4)]
+    assert shares == [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9, 10, 11], [12, 13, 14, 15]]
+    assert affinity.gpu_local_cpus(2, nodes, pci) == (list(range(8, 16)), 1)
+    assert affinity.rank_cpu_share(0, 1, tmp_path / "missing", pci) is None
