@@ -363,6 +363,7 @@ def main(argv=None) -> int:
     ap.add_argument("--seed", type=int, default=0, help="weight seed")
     ap.add_argument("--images", type=int, default=100, help="curated workload size")
     ap.add_argument("--latency-levels", default="1,10,100", help="closed-loop user levels for P50/P99 ('' = skip)")
+    ap.add_argument("--level-delay-us", type=int, default=500, help="batcher busy delay of the latency levels")
     ap.add_argument("--engine-batches", type=int, default=40, help="batches for the engine-only secondary key")
     ap.add_argument("--secondary-inproc", action=argparse.BooleanOptionalAction, default=True,
                     help="also measure the pipeline without the HTTP layer (secondary key 'inproc')")
@@ -491,12 +492,23 @@ def main(argv=None) -> int:
             errs = int((status != 200).sum())
             lat = list(lat)
             bs = []
-            if info.is_main and a.latency_levels:
-                levels = latency_levels(fe.port, reqs, [int(u) for u in a.latency_levels.split(",") if u], a)
-            D.barrier(info)
             fe.stop()
             fe = None
             batcher.shutdown()
+            if info.is_main and a.latency_levels:
+                # the reference's low user levels behind a batcher with a short busy delay (a lone request
+                # waits 100 us, a loaded device 500 us for its batch to fill), on the same decode processes
+                cfg = dict(batcher_config(a), max_queue_delay_us=a.level_delay_us)
+                batcher = native().DynamicBatcher([ex], cfg)
+                fe = native().HttpFrontEnd(batcher, pool.native_channel(), list(load_labels(None)),
+                                           {"host": "127.0.0.1", "port": 0, "io_threads": a.http_threads})
+                levels = latency_levels(fe.port, reqs, [int(u) for u in a.latency_levels.split(",") if u], a)
+                levels["batcher"] = {"max_queue_delay_us": cfg["max_queue_delay_us"],
+                                     "idle_queue_delay_us": cfg["idle_queue_delay_us"]}
+                fe.stop()
+                fe = None
+                batcher.shutdown()
+            D.barrier(info)
             pool.to_python_mode()
             if a.secondary_inproc:
                 w2, lat2, _, _, _ = measure_inproc(ex, pool, jpegs, a, info, D, sync)
@@ -581,8 +593,8 @@ def main(argv=None) -> int:
                 "errors": int(sum(x for lst in all_err for x in lst)),
                 "engine_req_s": round(float(sum(x for lst in all_eng for x in lst)), 1) if eng else None,
                 "levels": levels,
-                "bs1_p50_ms": levels.get("1", {}).get("p50_ms"),
-                "bs1_p99_ms": levels.get("1", {}).get("p99_ms"),
+                "bs1_p50_ms": (levels.get("1") or {}).get("p50_ms"),
+                "bs1_p99_ms": (levels.get("1") or {}).get("p99_ms"),
                 "per_rank_req_s": [round(x[0], 1) for x in per_rank],
                 "collective_backend": info.backend,
                 "weights_verified": bool(weights_verified),

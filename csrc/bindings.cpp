@@ -356,6 +356,8 @@ py::dict result_to_py(const BatchResult& r, int max_det) {
   out["topk_logit"] = tk_logit;
   out["topk_prob"] = tk_prob;
   out["gpu_ms"] = r.gpu_ms;
+  out["detection_ms"] = r.det_ms;
+  out["classification_ms"] = r.cls_ms;
   out["bucket"] = r.bucket;
   out["total_crops"] = r.total_crops;
   if (!r.raw.empty()) {
@@ -591,6 +593,8 @@ PYBIND11_MODULE(_C, m) {
                d["batch_size"] = r.batch_size;
                d["queue_us"] = r.queue_us;
                d["compute_us"] = r.compute_us;
+               d["detection_ms"] = r.det_ms;       // device stage times of the batch (OP_STAMP); -1: none
+               d["classification_ms"] = r.cls_ms;
                try {
                  (*pycb)(d);
                } catch (py::error_already_set& e) {
@@ -769,6 +773,10 @@ PYBIND11_MODULE(_C, m) {
              d["sum_decode_ms"] = s.sum_decode_ms;
              d["sum_queue_ms"] = s.sum_queue_ms;
              d["sum_gpu_ms"] = s.sum_gpu_ms;
+             py::dict st;
+             for (size_t k = 0; k < kStages.size() && k < s.stage_hist.size(); ++k)
+               st[py::str(kStages[k])] = py::make_tuple(s.stage_hist[k], s.stage_sum_ms[k]);
+             d["stages"] = st;
              d["latency_hist"] = s.latency_hist;
              d["latency_buckets_ms"] = kLatencyBucketsMs;
              return d;

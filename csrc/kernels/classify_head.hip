@@ -160,6 +160,18 @@ __global__ __launch_bounds__(256) void zero_fill_kernel(uint4* p, size_t n16, ui
   if (i < (size_t)n_tail) tail[i] = 0;
 }
 
+// Stage timestamp (planner OP_STAMP): the device's constant-rate wall clock (wall_clock64, the 100 MHz
+// REALTIME counter; rate from hipDeviceAttributeWallClockRate) written where the graph reaches this op, so the
+// executor reports detection / classification device time per batch without breaking the graph up.
+__global__ void stamp_kernel(unsigned long long* dst) {
+  const unsigned long long t = wall_clock64();
+  if (threadIdx.x == 0) dst[threadIdx.x] = t;
+}
+
+void stamp(void* dst, hipStream_t s) {
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, s, (unsigned long long*)dst);
+}
+
 void zero_fill(void* ptr, size_t bytes, hipStream_t s) {
   if (bytes == 0) return;
   if (((uintptr_t)ptr & 15) != 0) throw std::runtime_error("zero_fill: pointer must be 16-byte aligned");

@@ -40,6 +40,7 @@
 
 #include "common.h"
 #include "launch.h"
+#include "letterbox.h"
 
 namespace arena {
 
@@ -70,7 +71,9 @@ __device__ __forceinline__ float4 relu6x4(float4 v) {
 // DWP (dw + project): the block's hidden tensor comes from memory (the expand ran as its own streaming GEMM)
 // and is staged chunk by chunk: one kernel instead of a depthwise kernel writing the fp32 depthwise map and a
 // project GEMM reading it back; the residual comes from IrParams.rx.
-template <int S, int TH, int TW, int NTO, bool EXPAND, int KIN, bool DWP = false>
+// STEM (classifier front end, t = 1 block 1 only): X is the 2x2 stem conv of the crop-gathered space-to-depth
+// tile, computed here (IrParams.stem); the s2d tile and the 112 x 112 x 32 stem map never leave LDS.
+template <int S, int TH, int TW, int NTO, bool EXPAND, int KIN, bool DWP = false, bool STEM = false>
 __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   constexpr int PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
@@ -95,21 +98,81 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
   const int ty = t / tiles_x, tx = t - ty * tiles_x;
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
-  const float* xb = (const float*)p.x + (size_t)b * p.H * p.W * p.x_cs;
+  const float* xb = STEM ? nullptr : (const float*)p.x + (size_t)b * p.H * p.W * p.x_cs;
   const float* we = (const float*)p.we;
   const float* wd = (const float*)p.wd;
   const float* wp = (const float*)p.wp;
 
   // ---- A: the input halo tile (channels >= inp and pixels outside the image are zero)
-  const int cg = DWP ? 0 : p.inp_pad >> 2;
-  for (int i = tid; i < ROWS * cg; i += 256) {
-    const int r = i / cg, g = i - r * cg;
-    const int iy = iy0 + r / PW, ix = ix0 + r % PW;
-    const bool in = r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (in && 4 * g < p.inp) v = *(const float4*)(xb + ((size_t)iy * p.W + ix) * p.x_cs + 4 * g);
-    *(float4*)&Xs[r * XP + 4 * (EXPAND ? g : eswz<S>(r, g))] = v;
-    if (g == 0) Ms[r] = in ? 1.f : 0.f;
+  if constexpr (STEM) {
+    static_assert(S == 1 && !EXPAND && !DWP, "the fused stem feeds a stride-1 t = 1 block");
+    // A1: crop gather -> s2d tile (SH x SW pixels of 16 fp32, origin (iy0 - 1, ix0 - 1): the 2x2 stem conv
+    // pads the s2d map top / left by one), exactly as crop_gather_s2d_kernel<float> computes each pixel
+    constexpr int SH = PH + 1, SW = PW + 1, SP = 20;
+    static_assert(SH * SW * SP <= POUT * IRF_DP, "s2d tile must fit the D region");
+    float* Ss = Ds;
+    const int S2 = p.st_S >> 1;
+    const CropRef cr = p.st_crops[(p.st_ctrl != nullptr ? p.st_ctrl->crop_base : 0) + b];
+    const ImageMeta m = p.st_meta[cr.img];
+    const int cw = cr.x2 - cr.x1, chh = cr.y2 - cr.y1;
+    const bool empty = cw <= 0 || chh <= 0;
+    const float sx = empty ? 1.f : (float)((double)cw / (double)p.st_S);
+    const float sy = empty ? 1.f : (float)((double)chh / (double)p.st_S);
+    const uint8_t* img = p.st_pool + m.offset + ((size_t)cr.y1 * m.w + cr.x1) * 3;
+    for (int i = tid; i < SH * SW; i += 256) {
+      const int Y = iy0 - 1 + i / SW, X = ix0 - 1 + i % SW;
+      float out[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) out[k] = 0.f;
+      if ((unsigned)Y < (unsigned)S2 && (unsigned)X < (unsigned)S2) {
+#pragma unroll
+        for (int pq = 0; pq < 4; ++pq) {
+          const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
+          float rgb[3] = {0.f, 0.f, 0.f};
+          if (!empty) bilinear_rgb(img, m.w, lin_tap(oy, sy, chh), lin_tap(ox, sx, cw), rgb);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (div255<float>(rgb[c]) - p.st_mean[c]) * p.st_inv_std[c];
+        }
+      }
+      float* d = Ss + i * SP;
+#pragma unroll
+      for (int k = 0; k < 16; k += 4) *(float4*)(d + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+    }
+    __syncthreads();
+    // A2: X = relu6(stem(s2d) + b) on the halo pixels (exact fp32 MFMA, K = 4 taps x 16), zero outside the map
+    for (int pr = wave; pr < MT_IN * 2; pr += 4) {
+      const int mt = pr >> 1, nt = pr & 1;
+      const int r = mt * 16 + col;
+      const int rr = r < PIN ? r : 0;
+      const int ry = rr / PW, rx = rr - (rr / PW) * PW;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float4 bv = *(const float4*)(Ss + ((ry + (t >> 1)) * SW + rx + (t & 1)) * SP + 4 * kq);
+        const float4 av = *(const float4*)(p.st_w + (size_t)(nt * 16 + col) * 64 + t * 16 + 4 * kq);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(av, s4), f4c(bv, s4), acc, 0, 0, 0);
+      }
+      const int co = nt * 16 + 4 * kq;
+      const float4 bb = *(const float4*)(p.st_b + co);
+      const int iy = iy0 + ry, ix = ix0 + rx;
+      const bool in = r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      const float4 v = in ? relu6x4(make_float4(acc[0] + bb.x, acc[1] + bb.y, acc[2] + bb.z, acc[3] + bb.w))
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      *(float4*)&Xs[r * XP + 4 * eswz<S>(r, co >> 2)] = v;
+    }
+  } else {
+    const int cg = DWP ? 0 : p.inp_pad >> 2;
+    for (int i = tid; i < ROWS * cg; i += 256) {
+      const int r = i / cg, g = i - r * cg;
+      const int iy = iy0 + r / PW, ix = ix0 + r % PW;
+      const bool in = r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (in && 4 * g < p.inp) v = *(const float4*)(xb + ((size_t)iy * p.W + ix) * p.x_cs + 4 * g);
+      *(float4*)&Xs[r * XP + 4 * (EXPAND ? g : eswz<S>(r, g))] = v;
+      if (g == 0) Ms[r] = in ? 1.f : 0.f;
+    }
   }
   __syncthreads();
 
@@ -354,6 +417,8 @@ void ir_f32_prepare() {
 #undef IRF_ATTR
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, 1, false, 1>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, 1, false, 1, false, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
 bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand) {
@@ -406,7 +471,26 @@ static void ir_dwproj_f32(const IrParams& p, hipStream_t s) {
   if (!ok) throw std::runtime_error("ir_dwproj_f32: no kernel for oup_pad " + std::to_string(p.oup_pad));
 }
 
+// Classifier front end: crop gather + 2x2 s2d stem (16 -> 32, ReLU6) + MobileNetV2 block 1 (t = 1: depthwise
+// 32 + ReLU6, project 32 -> 16) in one kernel (IrParams.stem).
+static void ir_stem_f32(const IrParams& p, hipStream_t s) {
+  if (p.stride != 1 || p.expand || p.res || p.inp != 32 || p.inp_pad != 32 || p.hid_pad != 32 || p.oup_pad != 16 ||
+      p.oup > 16 || p.oup % 4 || p.H != p.W || p.H * 2 != p.st_S || p.Ho != p.H || p.Wo != p.W || p.W < 16 ||
+      p.y_cs % 4 || p.st_w == nullptr || p.st_b == nullptr || p.st_crops == nullptr || p.st_meta == nullptr ||
+      p.st_pool == nullptr)
+    throw std::runtime_error("ir_stem_f32: unsupported geometry (needs MobileNetV2 block 1 at S/2 x S/2)");
+  if (p.B <= 0) return;
+  const size_t lds = irf_lds_bytes(1, 32, 0, 16);
+  const int tiles = ((p.Wo + 15) / 16) * ((p.Ho + 7) / 8);
+  hipLaunchKernelGGL((ir_f32_kernel<1, 8, 16, 1, false, 1, false, true>), dim3((unsigned)(p.B * tiles)), dim3(256),
+                     lds, s, p);
+}
+
 void ir_block_f32(const IrParams& p, hipStream_t s) {
+  if (p.stem) {
+    ir_stem_f32(p, s);
+    return;
+  }
   if (p.dwp) {
     ir_dwproj_f32(p, s);
     return;

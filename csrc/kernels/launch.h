@@ -17,6 +17,8 @@ namespace arena {
 // fused epilogue: + bias, activation, + residual, store into a channel slice
 // of a concat buffer, optional second store nearest-upsampled x2 (FPN).
 struct ImageMeta;
+struct CropRef;
+struct Ctrl;
 struct ConvParams {
   const void* x;  // bf16 input, already offset to its channel slice
   int B, H, W;    // batch capacity and input spatial dims
@@ -122,6 +124,18 @@ struct IrParams {
   int dwp;                  // fp32: x is the block's hidden tensor (expand ran separately): dw + project only
   const void* rx;           // dwp: residual (the block input, output geometry), pixel stride rx_cs
   int rx_cs;
+  // fp32 classifier front end (stem = 1, t = 1 blocks, ir_f32.hip): X is not read from memory but built per
+  // tile from the batch's uint8 images: crop gather + ImageNet normalisation (crop_gather_s2d semantics) into a
+  // space-to-depth tile in LDS, then the 2x2 stem conv over it (+ bias, ReLU6; zero outside the H x W map).
+  int stem;
+  const uint8_t* st_pool;
+  const ImageMeta* st_meta;
+  const CropRef* st_crops;
+  const Ctrl* st_ctrl;
+  int st_S;                 // crop side (224): the stem map is st_S / 2 = H
+  float st_mean[3], st_inv_std[3];
+  const float* st_w;        // fp32 [inp_pad][64], k = (a * 2 + b) * 16 + c over the s2d input
+  const float* st_b;        // fp32 [inp_pad]
 };
 void ir_block(const IrParams& p, hipStream_t s);
 // Exact-fp32 fused block (csrc/kernels/ir_f32.hip): fp32 views / weights; we [hid_pad][inp_pad],
@@ -402,5 +416,7 @@ void topk_softmax(const TopkParams& p, hipStream_t s);
 
 // Graph-safe memset replacement (kernel node).
 void zero_fill(void* ptr, size_t bytes, hipStream_t s);
+// One 64-bit device wall-clock stamp at `dst` (a kernel node: stage timing inside a captured graph).
+void stamp(void* dst, hipStream_t s);
 
 }  // namespace arena

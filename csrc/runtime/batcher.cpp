@@ -165,6 +165,8 @@ void DynamicBatcher::finish(Batch& batch, const BatchResult& r, clk::time_point 
     rr.batch_size = (int)batch.size();
     rr.queue_us = std::chrono::duration<double, std::micro>(t_submit - batch[i]->t_enq).count();
     rr.compute_us = compute_us;
+    rr.det_ms = r.det_ms;
+    rr.cls_ms = r.cls_ms;
     batch[i]->cb(std::move(rr));
   }
 }

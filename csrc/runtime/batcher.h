@@ -39,6 +39,7 @@ struct RequestResult {
   std::vector<uint8_t> raw;      // raw tensor output (raw-output programs)
   int batch_size = 0;
   double queue_us = 0, compute_us = 0;
+  double det_ms = -1, cls_ms = -1;  // device stage times of the request's batch (BatchResult)
   std::string error;
 };
 

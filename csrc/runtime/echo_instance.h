@@ -88,6 +88,10 @@ class EchoInstance : public BatchInstance {
     std::this_thread::sleep_until(due);
     std::lock_guard<std::mutex> lk(mu_);
     busy_[slot] = false;
+    // stand-in stage times (the executor derives them from the program's wall-clock stamps): 60 % / 30 % of
+    // the simulated device latency, so the stage plumbing is testable without a GPU
+    results_[slot].det_ms = 0.6e-3 * latency_us_;
+    results_[slot].cls_ms = 0.3e-3 * latency_us_;
     return std::move(results_[slot]);
   }
 

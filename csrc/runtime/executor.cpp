@@ -35,6 +35,11 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
   prepare_kernels();
   max_B_ = cfg_.max_batch;
   {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg_.device) == hipSuccess && khz > 0)
+      wall_khz_ = (double)khz;
+  }
+  {
     const char* e = std::getenv("ARENA_DEBUG_SYNC");
     debug_sync_ = e != nullptr ? std::atoi(e) : 0;
     const char* at = std::getenv("ARENA_AUTOTUNE");
@@ -133,9 +138,10 @@ size_t Executor::out_off_raw() const {
   return align_up(out_off_topk() + sizeof(TopkResult) * (size_t)max_B_ * cfg_.max_det, 256);
 }
 size_t Executor::out_off_xcrops() const { return align_up(out_off_raw() + (size_t)cfg_.raw_out_bytes * max_B_, 256); }
-size_t Executor::out_bytes_total() const {
-  return out_off_xcrops() + sizeof(CropRef) * (size_t)max_B_ * cfg_.max_det;
+size_t Executor::out_off_stamps() const {
+  return align_up(out_off_xcrops() + sizeof(CropRef) * (size_t)max_B_ * cfg_.max_det, 256);
 }
+size_t Executor::out_bytes_total() const { return out_off_stamps() + 4 * sizeof(uint64_t); }
 
 void Executor::sync_slots() {
   for (int i = 0; i < n_streams_; ++i) ARENA_HIP_CHECK(hipStreamSynchronize(streams_[i]));
@@ -206,9 +212,10 @@ void Executor::set_program(const int64_t* ops, int n_ops, const int64_t* cls_ops
   cls_prog_.resize(n_cls_ops);
   for (int i = 0; i < n_cls_ops; ++i)
     std::memcpy(cls_prog_[i].data(), cls_ops + (size_t)i * kOpFields, sizeof(OpRecord));
-  has_topk_ = has_det_ = has_raw_ = false;
+  has_topk_ = has_det_ = has_raw_ = has_stamps_ = false;
   for (const auto& r : prog_) {
     has_topk_ |= r[0] == OP_TOPK;
+    has_stamps_ |= r[0] == OP_STAMP;
     has_det_ |= r[0] == OP_NMS || r[0] == OP_CROPPLAN;
     for (int f = 1; f < kOpFields; ++f) has_raw_ |= r[f] == BUF_RAWOUT && (r[0] == OP_YOLORAW || r[0] == OP_CONV);
   }
@@ -532,6 +539,20 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
           p.rx = resolve(bk, sl, r[28], r[29], eb);
           p.rx_cs = (int)r[30];
         }
+        p.stem = (int)r[31];
+        if (p.stem) {  // fp32 classifier front end: crop gather + stem conv feed the block (ir_f32.hip)
+          p.st_pool = pool;
+          p.st_meta = meta;
+          p.st_crops = (const CropRef*)resolve(bk, sl, r[32], 0, 1);
+          p.st_ctrl = ctrl;
+          p.st_S = (int)r[33];
+          for (int c = 0; c < 3; ++c) {
+            p.st_mean[c] = bits_to_float(r[34 + c]);
+            p.st_inv_std[c] = bits_to_float(r[37 + c]);
+          }
+          p.st_w = (const float*)(W + r[40]);
+          p.st_b = (const float*)(W + r[41]);
+        }
         if (f32)
           ir_block_f32(p, s);
         else
@@ -563,6 +584,11 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.T = (int)r[2];
         p.f32 = f32;
         letterbox_s2d(p, s);
+        break;
+      }
+      case OP_STAMP: {
+        if (r[1] < 0 || r[1] >= 4) throw std::runtime_error("OP_STAMP: stamp index out of range");
+        stamp(sl.d_out + out_off_stamps() + sizeof(uint64_t) * (size_t)r[1], s);
         break;
       }
       case OP_ZERO: {
@@ -819,6 +845,9 @@ void Executor::enqueue_results_d2h(Bucket& bk, Slot& sl, int n) {
   size_t d2h = out_off_topk();
   if (has_topk_) d2h += sizeof(TopkResult) * (size_t)bk.info.crop_cap;
   ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out, sl.d_out, d2h, hipMemcpyDeviceToHost, sl.stream));
+  if (has_stamps_)
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out + out_off_stamps(), sl.d_out + out_off_stamps(), 4 * sizeof(uint64_t),
+                                   hipMemcpyDeviceToHost, sl.stream));
   if (has_raw_)
     ARENA_HIP_CHECK(hipMemcpyAsync(sl.h_out + out_off_raw(), sl.d_out + out_off_raw(), (size_t)cfg_.raw_out_bytes * n,
                                    hipMemcpyDeviceToHost, sl.stream));
@@ -970,6 +999,13 @@ BatchResult Executor::collect(int s) {
   float ms = 0.f;
   hipEventElapsedTime(&ms, sl.started, sl.done);
   res.gpu_ms = ms;
+  if (has_stamps_) {  // device wall clock at program start, classifier start, program end (OP_STAMP 0 / 1 / 2)
+    const uint64_t* st = (const uint64_t*)(sl.h_out + out_off_stamps());
+    if (st[1] >= st[0] && st[2] >= st[1] && st[0] != 0) {
+      res.det_ms = (double)(st[1] - st[0]) / wall_khz_;
+      res.cls_ms = (double)(st[2] - st[1]) / wall_khz_;
+    }
+  }
   const int n = sl.n_images;
   const int* cnt = (const int*)sl.h_out;
   const Detection* det = (const Detection*)(sl.h_out + out_off_det());

@@ -61,6 +61,7 @@ enum OpType : int64_t {
   OP_STEMFUSED = 15,
   OP_C3FUSED = 16,
   OP_HEADPOOL = 17,
+  OP_STAMP = 18,  // 1: stamp index (0 program start, 1 classifier start, 2 end): device wall clock -> results
 };
 
 // Reserved buffer ids (the planner's arena buffers are ids >= 0).
@@ -216,6 +217,7 @@ class Executor : public BatchInstance {
   size_t out_bytes_total() const;
   size_t out_off_raw() const;
   size_t out_off_xcrops() const;
+  size_t out_off_stamps() const;  // 4 x uint64 device wall-clock stamps (OP_STAMP)
   int acquire_slot();
   void parallel_copy(std::vector<std::function<void()>>& jobs);
 
@@ -232,7 +234,8 @@ class Executor : public BatchInstance {
   hipStream_t streams_[kMaxSlots] = {};  // compute streams (streams_[0] == compute_)
   int n_streams_ = 1;
   uint64_t seq_ = 0;                     // batches submitted
-  bool has_topk_ = false, has_det_ = false, has_raw_ = false;
+  bool has_topk_ = false, has_det_ = false, has_raw_ = false, has_stamps_ = false;
+  double wall_khz_ = 100000.0;  // wall_clock64 rate (hipDeviceAttributeWallClockRate)
   bool peer_stage_ = false;
   std::vector<int> peer_enabled_;  // devices this executor's device has peer access to
   int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on compute stream

@@ -22,6 +22,7 @@
 namespace arena {
 
 const std::vector<double> kLatencyBucketsMs = {1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, 2000, 5000};
+const std::vector<std::string> kStages = {"decode", "queue", "gpu", "detection", "classification", "total"};
 
 namespace {
 
@@ -208,6 +209,8 @@ HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vecto
       throw std::runtime_error("HttpFrontEnd: big_fds / task_fds mismatch");
   }
   stats_.latency_hist.assign(kLatencyBucketsMs.size() + 1, 0);
+  stats_.stage_hist.assign(kStages.size(), std::vector<int64_t>(kLatencyBucketsMs.size() + 1, 0));
+  stats_.stage_sum_ms.assign(kStages.size(), 0.0);
   for (int s = dc_.slots - 1; s >= 0; --s) free_slots_.push_back(s);
   for (size_t i = 0; i < dc_.task_fds.size(); ++i) task_mu_.emplace_back(new std::mutex);
   load_ = std::vector<std::atomic<int>>(dc_.task_fds.size());
@@ -947,9 +950,16 @@ void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int statu
     json_num(s, gpu_ms);
     s += ",\"batch_size\":";
     json_num(s, r.batch_size);
+    // device time of the detection network (+ decode / NMS / crop plan) and of the classification network
+    // (crop gather -> top-5) of this request's batch, from the program's wall-clock stamps (OP_STAMP); with
+    // the batch's H2D / D2H they make up gpu_ms (reference timing keys, architectures/monolithic/app/
+    // inference.py:180,224-225; there the per-request CPU time of each network)
+    const double det_ms = r.det_ms >= 0 ? r.det_ms : 0.0, cls_ms = r.cls_ms >= 0 ? r.cls_ms : 0.0;
     s += ",\"detection_ms\":";
-    json_num(s, queue_ms + gpu_ms + decode_ms);
-    s += ",\"classification_ms\":0.0,\"inference_ms\":";
+    json_num(s, det_ms);
+    s += ",\"classification_ms\":";
+    json_num(s, cls_ms);
+    s += ",\"inference_ms\":";
     json_num(s, inference_ms);
     s += ",\"decode_ms\":";
     json_num(s, decode_ms);
@@ -968,6 +978,13 @@ void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int statu
       size_t b = 0;
       while (b < kLatencyBucketsMs.size() && total_ms > kLatencyBucketsMs[b]) ++b;
       ++stats->latency_hist[b];
+      const double stage_ms[] = {decode_ms, queue_ms, gpu_ms, det_ms, cls_ms, total_ms};
+      for (size_t k = 0; k < kStages.size(); ++k) {
+        size_t bb = 0;
+        while (bb < kLatencyBucketsMs.size() && stage_ms[k] > kLatencyBucketsMs[bb]) ++bb;
+        ++stats->stage_hist[k][bb];
+        stats->stage_sum_ms[k] += stage_ms[k];
+      }
     }
     self->respond(conn, 200, "application/json", s);
   };

@@ -90,7 +90,15 @@ struct FrontStats {
   int64_t connections = 0, open_connections = 0, detections = 0, timeouts = 0;
   double sum_total_ms = 0, sum_decode_ms = 0, sum_queue_ms = 0, sum_gpu_ms = 0;
   std::vector<int64_t> latency_hist;  // counts per bucket of kLatencyBucketsMs (last = +Inf)
+  // per-stage latency histograms of the successful requests (arena_request_latency_seconds{stage=...}):
+  // kStages order, each counts per bucket of kLatencyBucketsMs (last = +Inf), with its sum in ms
+  std::vector<std::vector<int64_t>> stage_hist;
+  std::vector<double> stage_sum_ms;
 };
+
+// decode, queue (dynamic batcher), gpu (batch submit -> results), detection / classification (device time of
+// the two networks, from the program's wall-clock stamps), total (request received -> response queued)
+extern const std::vector<std::string> kStages;
 
 extern const std::vector<double> kLatencyBucketsMs;
 

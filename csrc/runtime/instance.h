@@ -27,6 +27,9 @@ struct BatchResult {
   std::vector<TopkResult> topk;      // [total crops], in crop-plan order
   std::vector<int> crop_offset;      // [n + 1] first crop of each image
   double gpu_ms = 0.0;               // graph wall time from events
+  // device time of the detection part (program start -> classifier start) and of the classification part
+  // (classifier start -> end), from OP_STAMP wall-clock stamps; -1 when the program has no stamps
+  double det_ms = -1.0, cls_ms = -1.0;
   std::vector<uint8_t> raw;          // [n * raw_out_bytes] when the program exports raw tensors
 };
 

@@ -37,7 +37,10 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   YOLORAW  1-12 heads as DECODE, 13-15 strides, 16 out_buf (raw [84, A] fp32 per image)
   IRBLOCK  1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 inp 7 inp_pad 8 hid_pad 9 oup 10 oup_pad 11 stride
            12 expand 13 res 14 we 15 be 16 wd 17 bd 18 wp 19 bp 20 y_buf 21 y_coff 22 y_cs 23 Ho 24 Wo
-           25 batch_kind   (fused MobileNetV2 inverted residual, csrc/kernels/ir_block.hip)
+           25 batch_kind 26 x3w 27 dwp 28-30 residual view (dwp) 31 stem 32 crops_buf 33 S 34-36 mean
+           37-39 inv_std (float bits) 40 stem w_off 41 stem b_off
+           (fused MobileNetV2 inverted residual, csrc/kernels/ir_block.hip / ir_f32.hip; stem = 1: fp32 crop
+            gather + s2d stem conv computed inside the block-1 kernel, x_buf unused)
   STEMFUSED 1 src (0 letterbox, 1 crop gather) 2 y_buf 3 y_coff 4 y_cs 5 S 6 w_off 7 Kpad 8 b_off
            9 Cout 10 act 11 crops_buf 12-14 mean 15-17 inv_std (float bits) 18 batch_kind 19 KS
            20 second-conv flag 21 w2_off 22 Kpad2 23 b2_off 24 Cout2 25 act2 (y = the second conv's output)
@@ -50,6 +53,8 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   HEADPOOL 1 x_buf 2 x_coff 3 x_cs 4 HW 5 K 6 w_off 7 Kpad 8 b_off 9 N 10 Npad 11 y_buf 12 y_coff 13 y_cs
            14 act 15 batch_kind
            (MobileNetV2 head 1x1 conv + activation + global average pool, csrc/kernels/head_pool.hip)
+  STAMP    1 index (0 program start, 1 classifier start, 2 end): the device wall clock into the results
+           (per-batch detection / classification device time; executor BatchResult det_ms / cls_ms)
 
 Every record: field 47 (``OP_DTYPE_FIELD``) = activation precision of the op, 0 = bf16 activations and
 weights with fp32 accumulation (the tuned fused kernels), 1 = exact fp32 (fp32 activations and weights,
@@ -72,7 +77,7 @@ OP_FIELDS = 48
 OP_DTYPE_FIELD = 47
 DTYPES = ("bf16", "fp32")
 (OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
- OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL) = range(1, 18)
+ OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL, OP_STAMP) = range(1, 19)
 BUF_NONE, BUF_CTRL, BUF_META, BUF_POOL, BUF_DET, BUF_DETCOUNT, BUF_TOPK, BUF_RAWOUT = -1, -10, -11, -12, -13, -14, -15, -16
 BUF_XCROPS = -17  # crop plan exported to a second-stage executor (split topology; executor.h)
 
@@ -218,18 +223,29 @@ def pack_ir_weights(expand, dw, project, inp: int, k_align: int = 32) -> dict:
             "hid_pad": hid_pad, "oup": oup, "oup_pad": oup_pad}
 
 
+def ir_crop_f32_policy() -> str:
+    """``ARENA_IRC_F32``: ``auto`` (default), ``all``/``1`` or ``none``/``0`` — which fp32 MobileNetV2 14x14 / 7x7
+    blocks run as the fused x3 kernel (csrc/kernels/ir_crop_f32.hip).  ``auto`` takes the stride-1 14x14 blocks,
+    where it measured faster than the unfused expand GEMM + depthwise + project GEMM in the pipeline (128 crops:
+    hid 384 61-63 vs 77 us, hid 384 -> 96 70 vs 90 us, hid 576 106-107 vs 134 us); the 14 -> 7 block and the
+    7x7 blocks stay unfused (103 vs 88, 149 vs 97, 194 vs 120 us): each of their workgroups streams the block's
+    whole 1.8-2.8 MB of split weights for 21-28 output pixels (profiles/r3_irx_ops.md)."""
+    v = os.environ.get("ARENA_IRC_F32", "auto").lower()
+    return {"1": "all", "true": "all", "yes": "all", "on": "all", "0": "none", "false": "none", "no": "none",
+            "off": "none"}.get(v, v)
+
+
 def ir_crop_f32_enabled() -> bool:
-    """``ARENA_IRC_F32=1`` (default 0): fp32 programs run MobileNetV2's 14x14 / 7x7 blocks as the fused
-    whole-map kernel (csrc/kernels/ir_crop_f32.hip).  Off by default: on MI355X it measured slower than the
-    unfused batched 1x1 GEMMs + depthwise (1.21 ms vs 1.07 ms per batch of 32 requests;
-    profiles/r2_irc_f32_experiment.md)."""
-    return os.environ.get("ARENA_IRC_F32", "0").lower() in ("1", "true", "yes", "on")
+    return ir_crop_f32_policy() != "none"
 
 
 def ir_crop_f32_planned(H: int, stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
     from .validate import ir_crop_f32_supported
 
-    return ir_crop_f32_enabled() and ir_crop_f32_supported(H, stride, inp_pad, hid_pad, oup_pad, expand)
+    policy = ir_crop_f32_policy()
+    if policy == "none" or (policy == "auto" and not (H == 14 and stride == 1)):
+        return False
+    return ir_crop_f32_supported(H, stride, inp_pad, hid_pad, oup_pad, expand)
 
 
 class ProgramBuilder:
@@ -366,6 +382,32 @@ class ProgramBuilder:
                int(expand is not None), int(res), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind, x3w]
         self._emit(rec, src, dst)
 
+    def ir_block_stem(self, crops: Buffer, dst: View, stem, dw, project, *, S: int, mean, std,
+                      kind: int = CROPS) -> None:
+        """fp32 classifier front end in one op: crop gather + ImageNet normalisation -> space-to-depth -> the
+        2x2 stem conv (``stem`` = (w [32, 16, 2, 2] over the s2d input, b), ReLU6) -> MobileNetV2 block 1 (t = 1:
+        ``dw`` depthwise 32 + ReLU6, ``project`` 32 -> 16); ``dst`` is the block output (S/2 x S/2 x 16).  Neither
+        the s2d crops nor the 112 x 112 x 32 stem map is stored (csrc/kernels/ir_f32.hip, IrParams.stem)."""
+        if not self.f32:
+            raise ValueError("ir_block_stem is an fp32-program op (bf16 programs use stem_fused)")
+        ws, bs = stem
+        if ws.shape != (32, 16, 2, 2) or dw[0].shape != (32, 1, 3, 3) or project[0].shape[1:] != (32, 1, 1) \
+                or project[0].shape[0] != dst.C or dst.C > 16 or S % 2:
+            raise ValueError("ir_block_stem: needs a [32,16,2,2] s2d stem, a 32-channel t = 1 block and <= 16 outputs")
+        pk = pack_ir_weights(None, dw, project, 32, k_align=16)
+        f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
+        offs = [self.weights.add(f32(pk["we"])), self.weights.add(f32(pk["be"])), self.weights.add(f32(pk["wd"])),
+                self.weights.add(f32(pk["bd"])), self.weights.add(f32(pk["wp"])), self.weights.add(f32(pk["bp"]))]
+        wsb, bsb, kpad, cpad = pack_conv_weight(ws, bs, "fp32")
+        if kpad != 64 or cpad != 32:
+            raise ValueError("ir_block_stem: stem weights must pack to [32][64]")
+        H = S // 2
+        rec = [OP_IRBLOCK, BUF_NONE, 0, 0, H, H, 32, pk["inp_pad"], pk["hid_pad"], pk["oup"], pk["oup_pad"], 1, 0, 0,
+               *offs, dst.bid, dst.coff, dst.cs, H, H, kind, 0, 0, 0, 0, 0,
+               1, crops.id, S] + [fbits(m) for m in mean] + [fbits(1.0 / s) for s in std] + \
+              [self.weights.add(wsb), self.weights.add(bsb)]
+        self._emit(rec, dst, crops)
+
     def ir_dwproj(self, src: View, dst: View, dw, project, *, stride: int, res: View | None,
                   kind: int = CROPS) -> None:
         """fp32: depthwise 3x3 (+ReLU6) -> 1x1 project (+ ``res``) of an inverted residual whose expand ran as its
@@ -479,6 +521,11 @@ class ProgramBuilder:
             rec += [1, self.weights.add(bf16_bytes(pk["wd"])), self.weights.add(f32(pk["bd"])),
                     self.weights.add(bf16_bytes(pk["wp"])), self.weights.add(f32(pk["bp"])), pk["oup"]]
         self._emit(rec, dst, crops)
+
+    def stamp(self, k: int) -> None:
+        if not 0 <= k < 4:
+            raise ValueError("stamp index must be 0..3")
+        self._emit([OP_STAMP, int(k)])
 
     def zero(self, buf: Buffer, kind: int = IMAGES) -> None:
         self._emit([OP_ZERO, buf.id, buf.per_item, kind], buf)

@@ -262,6 +262,12 @@ def fuse_block_f32(blk, H: int) -> bool:
     return ir_crop_f32_planned(H, blk.stride, inp_pad, hid_pad, oup_pad, expand)
 
 
+def fuse_stem_ir_f32_default() -> bool:
+    """``ARENA_F32_STEM_IR`` (default 1): fp32 programs run crop gather + stem conv + MobileNetV2 block 1 as one
+    kernel (ProgramBuilder.ir_block_stem); the s2d crops and the 112 x 112 x 32 stem map are never stored."""
+    return os.environ.get("ARENA_F32_STEM_IR", "1").lower() not in ("0", "false", "no", "off")
+
+
 def dwproj_f32_default() -> bool:
     """``ARENA_F32_DWPROJ=1`` (default 0): fp32 programs run the unfused MobileNetV2 blocks' depthwise + project as
     one kernel (csrc/kernels/ir_f32.hip, IrParams.dwp) after the expand GEMM.  Off by default: measured slower
@@ -312,12 +318,22 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
     first_fused = (fuse_stem and crops is not None and fuse_stem_ir_default() and S % 32 == 0
                    and b0.expand is None and b0.stride == 1 and not b0.use_res and b0.inp == 32 and b0.oup == 16
                    and fuse_block(b0, h, fuse_ir))
+    first_fused_f32 = (pb.f32 and crops is not None and fuse_stem_ir_f32_default() and S % 2 == 0
+                       and b0.expand is None and b0.stride == 1 and not b0.use_res and b0.inp == 32
+                       and b0.oup <= 16 and h >= 16)
     if first_fused:
         # crop gather + stem + block 1 in one kernel: the 112x112x32 stem output stays in LDS
         O0 = pb.tensor("m0.out", h, h, b0.oup, kind=CROPS_)
         pb.stem_fused(View(O0, 0, b0.oup), s2d_stem_3x3(w), b, S=S, act="relu6", crops=crops, mean=mean, std=std,
                       kind=CROPS_, ir=(fold(b0.dw), fold(b0.project)))
         F = O0
+    elif first_fused_f32:
+        # fp32: crop gather + s2d stem conv + block 1 in one kernel (csrc/kernels/ir_f32.hip, IrParams.stem)
+        O0 = pb.tensor("m0.out", h, h, b0.oup, kind=CROPS_)
+        pb.ir_block_stem(crops, View(O0, 0, b0.oup), (s2d_stem_3x3(w), b), fold(b0.dw), fold(b0.project), S=S,
+                         mean=mean, std=std, kind=CROPS_)
+        F = O0
+        first_fused = True
     elif fuse_stem and crops is not None:
         F = pb.tensor("m.stem", h, h, 32, kind=CROPS_)
         pb.stem_fused(View(F, 0, 32), s2d_stem_3x3(w), b, S=S, act="relu6", crops=crops, mean=mean, std=std,
@@ -386,6 +402,7 @@ def plan_pipeline(yolo: YOLOv5nu, mnet: MobileNetV2, *, conf_thr: float, iou_thr
                   cls_size: int = 224, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225),
                   cand_cap: int = 8400, max_det: int = 300, dtype: str = "bf16") -> Program:
     pb = ProgramBuilder(dtype)
+    pb.stamp(0)  # device wall-clock stamps: detection = [0, 1), classification = [1, 2) (reference timing keys)
     heads = plan_yolo(pb, yolo, det_size)
     cand = pb.raw("cand", cand_cap * CAND_BYTES)
     count = pb.raw("cand_count", 4)
@@ -395,7 +412,9 @@ def plan_pipeline(yolo: YOLOv5nu, mnet: MobileNetV2, *, conf_thr: float, iou_thr
     crops = pb.raw("crops", max_det * CROPREF_BYTES, pinned=True)
     pb.crop_plan(crops)
     pb.begin_classifier()
+    pb.stamp(1)
     plan_mobilenet(pb, mnet, crops, cls_size, mean, std)
+    pb.stamp(2)
     return pb.build({"kind": "pipeline", "conf_thr": conf_thr, "iou_thr": iou_thr, "det_size": det_size, "cls_size": cls_size,
                      "cand_cap": cand_cap, "max_det": max_det})
 

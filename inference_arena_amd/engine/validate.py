@@ -30,6 +30,7 @@ from ..engine.planner import (
     OP_LETTERBOX,
     OP_NMS,
     OP_SPPF,
+    OP_STAMP,
     OP_STEMFUSED,
     OP_TENSORIN,
     OP_TOPK,
@@ -181,7 +182,15 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 raise ProgramError(f"op {i}: ir_block output size mismatch")
             if int(r[13]) and (S != 1 or (inp != oup and not dwp)):
                 raise ProgramError(f"op {i}: ir_block residual needs stride 1 and inp == oup")
-            view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, el, "ir input")
+            if int(r[31]):  # fp32 crop gather + stem computed in the kernel: no input view, the crop plan instead
+                if not (f32 and S == 1 and not int(r[12]) and not int(r[13]) and inp == 32 and inp_pad == 32
+                        and hid_pad == 32 and oup_pad == 16 and H == W and 2 * H == int(r[33]) and int(r[25]) == CROPS):
+                    raise ProgramError(f"op {i}: unsupported fused stem + block geometry")
+                need(i, r[32], 0, B * max_det * CROP_BYTES, "stem crop refs")
+                weights(i, int(r[40]), 32 * 64 * 4, "stem weight")
+                weights(i, int(r[41]), 32 * 4, "stem bias")
+            else:
+                view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, el, "ir input")
             view(i, r[20], int(r[21]), int(r[22]), n * Ho * Wo, oup, el, "ir output")
             if dwp and int(r[13]):
                 view(i, r[28], int(r[29]), int(r[30]), n * Ho * Wo, oup, el, "ir residual")
@@ -288,5 +297,8 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 A += hw * hw
             if int(r[16]) != BUF_RAWOUT or 84 * A * 4 > raw:
                 raise ProgramError(f"op {i}: raw output needs {84 * A * 4} bytes per image, have {raw}")
+        elif op == OP_STAMP:
+            if not 0 <= int(r[1]) < 4:
+                raise ProgramError(f"op {i}: stamp index {int(r[1])} out of range")
         else:
             raise ProgramError(f"op {i}: unknown op {op}")

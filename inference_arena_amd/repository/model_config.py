@@ -197,6 +197,7 @@ def generate_pipeline(name: str = "arena_pipeline", detector: str = "yolov5n", c
     cfg.output.add(name="CLASS_IDS", data_type=DataType.Value("TYPE_INT32"), dims=[-1, 5])
     cfg.output.add(name="CLASS_LOGITS", data_type=DataType.Value("TYPE_FP32"), dims=[-1, 5])
     cfg.output.add(name="CLASS_PROBS", data_type=DataType.Value("TYPE_FP32"), dims=[-1, 5])
+    cfg.output.add(name="STAGE_MS", data_type=DataType.Value("TYPE_FP32"), dims=[4])
     s1 = cfg.ensemble_scheduling.step.add(model_name=detector, model_version=-1)
     s1.input_map["images"] = "IMAGE"
     s1.output_map["output0"] = "DETECTIONS"

@@ -96,8 +96,11 @@ class GpuBatchedBackend(Backend):
         total = (time.perf_counter() - t0) * 1e3
         q = d["queue_us"] / 1e3
         gpu = d["compute_us"] / 1e3
+        # device time of the two networks in this request's batch (the program's wall-clock stamps, executor
+        # OP_STAMP); together with H2D / D2H they make up gpu_ms.  Programs without stamps report 0.
+        det_ms, cls_ms = float(d.get("detection_ms", -1.0)), float(d.get("classification_ms", -1.0))
         timing = {"queue_ms": q, "gpu_ms": gpu, "batch_size": float(d["batch_size"]),
-                  "detection_ms": q + gpu, "classification_ms": 0.0, "inference_ms": total}
+                  "detection_ms": max(0.0, det_ms), "classification_ms": max(0.0, cls_ms), "inference_ms": total}
         return _result_from_dict(d), timing
 
     def stats(self) -> dict:

@@ -85,7 +85,15 @@ def create_app(settings: Settings | None = None, client: ModelServerClient | Non
         dets = [DetectionWithClassification(detection=_box(det[i]),
                                             classification=_cls(int(out["CLASS_IDS"][i, 0]), float(conf[i, 0])))
                 for i in range(det.shape[0])]
-        return dets, {"detection_ms": ms, "classification_ms": 0.0, "inference_ms": ms}
+        st = out.get("STAGE_MS")
+        timing = {"inference_ms": ms}
+        if st is not None and np.asarray(st).size >= 4:
+            st = np.asarray(st, np.float64).ravel()
+            timing.update({"detection_ms": float(st[0]), "classification_ms": float(st[1]),
+                           "queue_ms": float(st[2]), "gpu_ms": float(st[3])})
+        else:  # a model server without stage outputs: the whole round trip counts as detection
+            timing.update({"detection_ms": ms, "classification_ms": 0.0})
+        return dets, timing
 
     async def predict_tensor(rid: str, data: bytes):
         cl: ModelServerClient = state["client"]

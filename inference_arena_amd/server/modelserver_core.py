@@ -241,7 +241,11 @@ class PipelineModel(ModelHandle):
         self.stats.record(True, 1, (time.perf_counter() - t0) * 1e6, timing.get("queue_ms", 0) * 1e3,
                           timing.get("gpu_ms", 0) * 1e3)
         k = len(res)
-        return {"DETECTIONS": det.astype(np.float32),
+        # [detection_ms, classification_ms, queue_ms, gpu_ms] of this request's batch (device stage times from
+        # the program's wall-clock stamps): the gateway's timing keys without a second clock
+        stage = np.asarray([timing.get("detection_ms", 0.0), timing.get("classification_ms", 0.0),
+                            timing.get("queue_ms", 0.0), timing.get("gpu_ms", 0.0)], np.float32)
+        return {"DETECTIONS": det.astype(np.float32), "STAGE_MS": stage,
                 "CLASS_IDS": res.topk_idx[:k].astype(np.int32).reshape(k, 5),
                 "CLASS_LOGITS": res.topk_logit[:k].astype(np.float32).reshape(k, 5),
                 "CLASS_PROBS": res.topk_prob[:k].astype(np.float32).reshape(k, 5)}

@@ -80,7 +80,6 @@ def create_app(settings: Settings | None = None, backend: Backend | None = None)
             raise HTTPException(status_code=500, detail=str(e)) from e
         timing = dict(timing)
         timing["decode_ms"] = decode_ms
-        timing["detection_ms"] = timing.get("detection_ms", 0.0) + decode_ms
         timing["total_ms"] = tm.ms()
         metrics.observe("ok", {k: v for k, v in timing.items() if k.endswith("_ms")}, len(res),
                         int(timing.get("batch_size", 1)))

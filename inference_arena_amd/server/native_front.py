@@ -48,13 +48,20 @@ class _Collector:
         det.add_metric([self.arch], s["detections"])
         yield det
         bounds = [v / 1e3 for v in s["latency_buckets_ms"]]
-        cum, buckets = 0, []
-        for i, n in enumerate(s["latency_hist"]):
-            cum += n
-            buckets.append((str(bounds[i]) if i < len(bounds) else "+Inf", cum))
+
+        def cumulative(hist):
+            cum, out = 0, []
+            for i, n in enumerate(hist):
+                cum += n
+                out.append((str(bounds[i]) if i < len(bounds) else "+Inf", cum))
+            return out
         lat = HistogramMetricFamily("arena_request_latency_seconds", "Request latency by stage",
                                     labels=["arch", "stage"])
-        lat.add_metric([self.arch, "total"], buckets, s["sum_total_ms"] / 1e3)
+        # decode / queue / gpu / detection / classification / total (the dashboards' stage panels); the device
+        # stage times come from the program's wall-clock stamps (csrc/runtime/http_front.cpp kStages)
+        stages = s.get("stages") or {"total": (s["latency_hist"], s["sum_total_ms"])}
+        for stage, (hist, sum_ms) in stages.items():
+            lat.add_metric([self.arch, stage], cumulative(hist), sum_ms / 1e3)
         yield lat
         q = GaugeMetricFamily("arena_queue_depth", "Requests waiting in the dynamic batcher", labels=["arch", "gpu"])
         q.add_metric([self.arch, self.gpu], b["queue_depth"])

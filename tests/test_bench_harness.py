@@ -29,7 +29,7 @@ def test_bench_two_ranks_self_launch_http():
     assert out["path"] == "http" and out["errors"] == 0 and out["value"] > 0
     assert out["weights_verified"] is True and out["collective_backend"] == "gloo"
     assert len(out["per_rank_req_s"]) == 2 and len(out["cpu_share_per_rank"]) == 2
-    assert set(out["levels"]) == {"1", "4"} and out["bs1_p50_ms"] == out["levels"]["1"]["p50_ms"]
+    assert set(out["levels"]) == {"1", "4", "batcher"} and out["bs1_p50_ms"] == out["levels"]["1"]["p50_ms"]
     assert out["inproc"]["value"] > 0
     assert out["ms_per_step"] * out["steps"] / 1e3 == pytest.approx(2 * 256 * 2 / out["value"], rel=1e-3)
 

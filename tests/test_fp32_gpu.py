@@ -247,6 +247,21 @@ def test_fp32_pipeline_matches_reference(dense_models, device):
     assert max(rel) < 1e-3, max(rel)
 
 
+def test_pipeline_stage_stamps(dense_models, device):
+    """The program's wall-clock stamps (planner OP_STAMP): detection and classification device time per batch,
+    both positive, together within the batch's event-timed gpu_ms (which adds H2D / D2H)."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    pipe = GpuPipeline(*dense_models, device=0, buckets=[8], dtype="fp32")
+    imgs = synthetic_images(8, 91)
+    pipe.ex.run(imgs)
+    r = pipe.ex.run(imgs)
+    assert r["detection_ms"] > 0 and r["classification_ms"] > 0
+    assert r["detection_ms"] + r["classification_ms"] <= r["gpu_ms"] * 1.02 + 0.01
+    assert r["detection_ms"] > r["classification_ms"] * 0.2  # YOLOv5nu is the larger share at 4 crops / image
+
+
 def test_fp32_letterbox_stem_matches_unfused(dense_models, device, monkeypatch):
     """The fp32 stem conv sampling the letterboxed images itself (letterbox_conv, ARENA_F32_LB_STEM) vs the
     letterbox op + stem conv: the same stem activations (fp32 rounding) and the same results.  Covers
@@ -272,6 +287,34 @@ def test_fp32_letterbox_stem_matches_unfused(dense_models, device, monkeypatch):
         if len(x):
             np.testing.assert_allclose(y.boxes, x.boxes, rtol=2e-5, atol=5e-3)
             np.testing.assert_array_equal(y.topk_idx[:, 0], x.topk_idx[:, 0])
+
+
+def test_fp32_stem_block1_fused_matches_unfused(dense_models, device, monkeypatch):
+    """crop gather + s2d stem conv + MobileNetV2 block 1 in one kernel (ARENA_F32_STEM_IR, ir_f32.hip stem mode)
+    vs the crop-gather op + stem conv + block-1 kernel: the same block-1 output for every crop (fp32 rounding:
+    the stem sums run on the same fp32 MFMA, the depthwise / project code is shared) and the same results."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+    from inference_arena_amd.engine.planner import OP_CROPGATHER
+
+    imgs = synthetic_images(5, 81) + synthetic_images(1, 82, hw=(333, 500))
+    monkeypatch.setenv("ARENA_F32_STEM_IR", "0")
+    plain = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="fp32")
+    monkeypatch.setenv("ARENA_F32_STEM_IR", "1")
+    fused = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="fp32")
+    assert any(int(op[0]) == OP_CROPGATHER for op in plain.program.ops)
+    assert not any(int(op[0]) == OP_CROPGATHER for op in fused.program.ops)
+    a, b = plain.infer(imgs), fused.infer(imgs)
+    n_crops = sum(len(x) for x in a)
+    assert n_crops >= 5
+    for i in range(n_crops):
+        x1, x2 = plain.read_buffer("m0.out", 8, i), fused.read_buffer("m0.out", 8, i)
+        np.testing.assert_allclose(x2, x1, rtol=1e-5, atol=2e-5)
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        if len(x):
+            np.testing.assert_array_equal(y.topk_idx, x.topk_idx)
+            np.testing.assert_allclose(y.topk_logit, x.topk_logit, rtol=1e-5, atol=1e-5)
 
 
 def test_fp32_tensor_models_match_torch(models, device):
@@ -360,10 +403,12 @@ def test_fp32_program_fuses_the_high_resolution_blocks():
     from inference_arena_amd.models.zoo import default_models
 
     p = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="fp32")
-    fused = [(int(o[4]), int(o[11])) for o in p.ops if int(o[0]) == 14 and int(o[27]) == 0]
-    # >= 28x28: ir_f32.hip tile kernel; 14x14 and 7x7 run unfused (ir_crop_f32 / dw + project kernels opt-in)
-    assert [h for h, _ in fused] == [112, 112, 56, 56, 28, 28, 28]
-    assert not [o for o in p.ops if int(o[0]) == 14 and int(o[27]) == 1]
+    ir = [o for o in p.ops if int(o[0]) == 14]
+    # block 1 fused with crop gather + stem (ir_f32.hip stem mode), >= 28x28: ir_f32.hip tile kernel,
+    # stride-1 14x14: the x3 whole-map kernel (ir_crop_f32.hip); 14 -> 7 and 7x7 blocks run unfused
+    assert [(int(o[4]), int(o[26]), int(o[31])) for o in ir] == \
+        [(112, 0, 1), (112, 0, 0), (56, 0, 0), (56, 0, 0), (28, 0, 0), (28, 0, 0), (28, 0, 0)] + [(14, 1, 0)] * 6
+    assert not [o for o in p.ops if int(o[0]) == 9]  # no separate crop gather
     assert all(int(o[47]) == 1 for o in p.ops)
 
 

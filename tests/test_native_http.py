@@ -37,7 +37,7 @@ def _multipart(data: bytes, field="file"):
 @pytest.fixture(scope="module")
 def server():
     C = native()
-    batcher = C.DynamicBatcher([C.EchoInstance(2, 8, 4)], {"max_batch": 8, "max_queue_delay_us": 200})
+    batcher = C.DynamicBatcher([C.EchoInstance(2, 8, 4, 1000)], {"max_batch": 8, "max_queue_delay_us": 200})
     labels = load_labels(None)
     fe = NativeFrontEnd(batcher, labels, port=0, host="127.0.0.1", io_threads=2, decode_procs=2, slots=16)
     yield fe, labels
@@ -273,3 +273,25 @@ def test_native_load_generator_closed_loop(server):
     assert (r["status"] == 200).all()
     assert set(r["dets"].tolist()) <= {2, 3, 4, 1} and (r["latency"] > 0).all()
     assert (np.diff(r["t_done"]) >= 0).all()  # completion order
+
+
+def test_stage_timing_and_stage_histograms(server):
+    """detection_ms / classification_ms are the device stage times of the request's batch (never the old
+    constants): positive, and together no more than gpu_ms; /metrics exports a histogram per stage."""
+    import urllib.request
+
+    fe, _ = server
+    body, ct = _multipart(_jpeg(40, 40, 3))
+    st, data, c = _post(fe.port, body, ct)
+    c.close()
+    t = json.loads(data)["timing"]
+    assert st == 200 and t["detection_ms"] > 0 and t["classification_ms"] > 0
+    assert t["detection_ms"] + t["classification_ms"] <= t["gpu_ms"] + 1e-6
+    stages = fe.stats()["stages"]
+    assert set(stages) == {"decode", "queue", "gpu", "detection", "classification", "total"}
+    assert all(sum(h) >= 1 for h, _ in stages.values())
+    fe.fe.set_metrics_text(__import__("prometheus_client").generate_latest(fe.registry).decode())
+    with urllib.request.urlopen(f"http://127.0.0.1:{fe.port}/metrics", timeout=10) as r:
+        text = r.read().decode()
+    for stage in ("decode", "queue", "gpu", "detection", "classification", "total"):
+        assert f'arena_request_latency_seconds_count{{arch="monolithic",stage="{stage}"}}' in text

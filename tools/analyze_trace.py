@@ -21,8 +21,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 KIND = {1: "conv", 2: "dwconv", 3: "sppf", 4: "letterbox", 5: "zero", 6: "decode", 7: "nms", 8: "cropplan",
         9: "cropgather", 10: "avgpool", 11: "topk", 12: "tensorin", 13: "yoloraw", 14: "irblock", 15: "stemfused", 16: "c3fused",
-        17: "headpool"}
-FIRST_KERNEL = {4: "letterbox", 12: "tensor_in", 15: "stem_fused"}
+        17: "headpool", 18: "stamp"}
+FIRST_KERNEL = {4: "letterbox", 12: "tensor_in", 15: "stem_fused", 18: "stamp_kernel"}
 
 
 def describe(rec) -> str:
@@ -40,6 +40,8 @@ def describe(rec) -> str:
         d = f"{'letterbox' if rec[1] == 0 else 'crop gather'} + stem k{int(rec[19])} -> {int(rec[9])}"
         return d + (f" + k3 s2 -> {int(rec[24])}" if int(rec[20]) else "") + \
             (f" + ir t1 -> {int(rec[31])}" if int(rec[26]) else "")
+    if t == 14 and int(rec[31]):
+        return f"crop gather + stem -> ir {int(rec[4])}x{int(rec[5])}x{int(rec[6])} -> {int(rec[9])} (t1)"
     if t == 14:
         return (f"ir {int(rec[4])}x{int(rec[5])}x{int(rec[6])}->{int(rec[23])}x{int(rec[24])}x{int(rec[9])} "
                 f"hid{int(rec[8])} s{int(rec[11])}{' res' if rec[13] else ''}")
