@@ -135,9 +135,6 @@ void py_ir_block(const py::dict& d) {
   p.B = req<int>(d, "B");
   p.bdev = ptr<const int*>(d, "bdev");
   p.x3w = get<int>(d, "x3w", 0);
-  p.dwp = get<int>(d, "dwp", 0);
-  p.rx = ptr<const void*>(d, "rx");
-  p.rx_cs = get<int>(d, "rx_cs", 0);
   prepare_kernels();
   if (get<int>(d, "f32", 0))
     ir_block_f32(p, stream_of(d));

@@ -68,12 +68,9 @@ __device__ __forceinline__ float4 relu6x4(float4 v) {
 
 }  // namespace
 
-// DWP (dw + project): the block's hidden tensor comes from memory (the expand ran as its own streaming GEMM)
-// and is staged chunk by chunk: one kernel instead of a depthwise kernel writing the fp32 depthwise map and a
-// project GEMM reading it back; the residual comes from IrParams.rx.
 // STEM (classifier front end, t = 1 block 1 only): X is the 2x2 stem conv of the crop-gathered space-to-depth
 // tile, computed here (IrParams.stem); the s2d tile and the 112 x 112 x 32 stem map never leave LDS.
-template <int S, int TH, int TW, int NTO, bool EXPAND, int KIN, bool DWP = false, bool STEM = false>
+template <int S, int TH, int TW, int NTO, bool EXPAND, int KIN, bool STEM = false>
 __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   constexpr int PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
@@ -82,10 +79,10 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
   constexpr int PAIRS = MT_OUT * NTO, PPW = (PAIRS + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) float irf_lds[];
   constexpr int EP = irf_ep(S);
-  const int XP = DWP ? 0 : irf_xp(p.inp_pad, EXPAND);
+  const int XP = irf_xp(p.inp_pad, EXPAND);
   float* Xs = irf_lds;                                   // [ROWS][XP]
-  float* Es = Xs + ROWS * XP;                            // [ROWS][EP] (EXPAND, DWP)
-  float* Ds = Es + ((EXPAND || DWP) ? ROWS * EP : 0);    // [POUT][IRF_DP]
+  float* Es = Xs + ROWS * XP;                            // [ROWS][EP] (EXPAND)
+  float* Ds = Es + (EXPAND ? ROWS * EP : 0);             // [POUT][IRF_DP]
   float* Ms = Ds + POUT * IRF_DP;                        // [ROWS] 1 inside the image, 0 outside
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -105,7 +102,7 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
 
   // ---- A: the input halo tile (channels >= inp and pixels outside the image are zero)
   if constexpr (STEM) {
-    static_assert(S == 1 && !EXPAND && !DWP, "the fused stem feeds a stride-1 t = 1 block");
+    static_assert(S == 1 && !EXPAND, "the fused stem feeds a stride-1 t = 1 block");
     // A1: crop gather -> s2d tile (SH x SW pixels of 16 fp32, origin (iy0 - 1, ix0 - 1): the 2x2 stem conv
     // pads the s2d map top / left by one), exactly as crop_gather_s2d_kernel<float> computes each pixel
     constexpr int SH = PH + 1, SW = PW + 1, SP = 20;
@@ -163,7 +160,7 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
       *(float4*)&Xs[r * XP + 4 * eswz<S>(r, co >> 2)] = v;
     }
   } else {
-    const int cg = DWP ? 0 : p.inp_pad >> 2;
+    const int cg = p.inp_pad >> 2;
     for (int i = tid; i < ROWS * cg; i += 256) {
       const int r = i / cg, g = i - r * cg;
       const int iy = iy0 + r / PW, ix = ix0 + r % PW;
@@ -219,21 +216,6 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
   constexpr bool PREFETCH_DW = S == 2;
   if constexpr (EXPAND) load_expand(0);
   if constexpr (PREFETCH_DW) load_dw(0);
-  // DWP: the chunk's hidden halo tile, fetched into registers one chunk ahead (during the project GEMM)
-  constexpr int EPT = DWP ? (ROWS * 8 + 255) / 256 : 1;
-  float4 epf[EPT];
-  auto fetch_e = [&](int h0) {
-#pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      const int i = tid + 256 * j, r = i >> 3, gg = i & 7;
-      const int iy = iy0 + r / PW, ix = ix0 + r % PW;
-      const bool in = i < ROWS * 8 && r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W &&
-                      h0 + 4 * gg < p.inp;
-      float4 v = *(const float4*)(in ? xb + ((size_t)iy * p.W + ix) * p.x_cs + h0 + 4 * gg : xb);
-      epf[j] = in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  if constexpr (DWP) fetch_e(0);
 
   for (int h0 = 0; h0 < p.hid_pad; h0 += IRF_HC) {
     // ---- B: expand GEMM for this chunk, rows = hidden channel, columns = halo pixel
@@ -269,15 +251,6 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
       __syncthreads();
       E = Es;
       ep = EP;
-    } else if constexpr (DWP) {
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        const int i = tid + 256 * j, r = i >> 3;
-        if (i < ROWS * 8) *(float4*)&Es[r * EP + 4 * eswz<S>(r, i & 7)] = epf[j];
-      }
-      __syncthreads();
-      E = Es;
-      ep = EP;
     } else {
       E = Xs + h0;  // t = 1 block: the depthwise runs on the input channels themselves
       ep = XP;
@@ -307,7 +280,6 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
     if (h0 + IRF_HC < p.hid_pad) {  // next chunk's expand / depthwise weights, in flight during the project GEMM
       if constexpr (EXPAND) load_expand(h0 + IRF_HC);
       if constexpr (PREFETCH_DW) load_dw(h0 + IRF_HC);
-      if constexpr (DWP) fetch_e(h0 + IRF_HC);
     }
 
     // ---- D: project GEMM accumulate, rows = output channel, columns = output pixel
@@ -341,9 +313,7 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
     const float4 bp = *(const float4*)((const float*)p.bp + co);
     float4 v = make_float4(acc[j][0] + bp.x, acc[j][1] + bp.y, acc[j][2] + bp.z, acc[j][3] + bp.w);
     if (p.res) {
-      const float4 r = DWP ? *(const float4*)((const float*)p.rx + ((size_t)b * p.Ho * p.Wo + (size_t)oy * p.Wo + ox) *
-                                                                       p.rx_cs + co)
-                           : *(const float4*)(xb + ((size_t)oy * p.W + ox) * p.x_cs + co);
+      const float4 r = *(const float4*)(xb + ((size_t)oy * p.W + ox) * p.x_cs + co);
       v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
     }
     *(float4*)(yb + ((size_t)oy * p.Wo + ox) * p.y_cs + co) = v;
@@ -352,11 +322,11 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
 
 // LDS bytes of one workgroup (<= 64 KiB, or an instantiation whose dynamic-LDS limit ir_f32_prepare raised
 // before any graph capture)
-static size_t irf_lds_bytes(int S, int inp_pad, int expand, int TW = 8, bool dwp = false) {
+static size_t irf_lds_bytes(int S, int inp_pad, int expand, int TW = 8) {
   const int TH = S == 1 ? 8 : 4;
   const int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   const size_t rows = (size_t)(PH * PW + 15) / 16 * 16;
-  return sizeof(float) * ((dwp ? 0 : rows * irf_xp(inp_pad, expand)) + ((expand || dwp) ? rows * irf_ep(S) : 0) +
+  return sizeof(float) * (rows * irf_xp(inp_pad, expand) + (expand ? rows * irf_ep(S) : 0) +
                           (size_t)TH * TW * IRF_DP + rows);
 }
 
@@ -417,7 +387,7 @@ void ir_f32_prepare() {
 #undef IRF_ATTR
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, 1, false, 1>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, 1, false, 1, false, true>,
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, 1, false, 1, true>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 }
 
@@ -427,48 +397,6 @@ bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, i
          oup_pad % 16 == 0 &&
          (nto == 1 || nto == 2 || nto == 4 || nto == 6) && (expand || hid_pad == inp_pad) &&
          irf_lds_bytes(stride, inp_pad, expand) <= 64 * 1024;
-}
-
-// ---- dw + project blocks (DWP): MobileNetV2's 14x14 / 7x7 blocks, whose expand runs as a streaming GEMM
-template <int S, int TH, int TW, int NTO>
-static void irf_launch_dwp(const IrParams& p, hipStream_t s) {
-  const size_t lds = irf_lds_bytes(S, p.inp_pad, 0, TW, true);
-  const int tiles = ((p.Wo + TW - 1) / TW) * ((p.Ho + TH - 1) / TH);
-  hipLaunchKernelGGL((ir_f32_kernel<S, TH, TW, NTO, false, 1, true>), dim3((unsigned)(p.B * tiles)), dim3(256), lds, s,
-                     p);
-}
-
-template <int S, int TH, int TW>
-static bool irf_dwp_nto(const IrParams& p, hipStream_t s) {
-  switch (p.oup_pad / 16) {
-    case 4: irf_launch_dwp<S, TH, TW, 4>(p, s); return true;
-    case 6: irf_launch_dwp<S, TH, TW, 6>(p, s); return true;
-    case 10: irf_launch_dwp<S, TH, TW, 10>(p, s); return true;
-    default: return false;
-  }
-}
-
-bool ir_dwproj_f32_supported(int stride, int hid_pad, int oup_pad) {
-  const int nto = oup_pad / 16;
-  return (stride == 1 || stride == 2) && hid_pad % 32 == 0 && oup_pad % 16 == 0 && (nto == 4 || nto == 6 || nto == 10);
-}
-
-static void ir_dwproj_f32(const IrParams& p, hipStream_t s) {
-  if (!ir_dwproj_f32_supported(p.stride, p.hid_pad, p.oup_pad) || p.inp_pad != p.hid_pad || p.inp % 4 ||
-      p.oup % 4 || p.inp > p.inp_pad || p.oup > p.oup_pad || p.x_cs % 4 || p.y_cs % 4 || (p.res && p.rx_cs % 4))
-    throw std::runtime_error("ir_dwproj_f32: unsupported channel geometry");
-  if (p.res && p.rx == nullptr) throw std::runtime_error("ir_dwproj_f32: residual without a residual tensor");
-  if (p.Ho != (p.H + 2 - 3) / p.stride + 1 || p.Wo != (p.W + 2 - 3) / p.stride + 1)
-    throw std::runtime_error("ir_dwproj_f32: output size mismatch");
-  if (p.B <= 0) return;
-  bool ok;
-  if (p.stride == 1 && p.Wo >= 16)
-    ok = irf_dwp_nto<1, 8, 16>(p, s);
-  else if (p.stride == 1)
-    ok = irf_dwp_nto<1, 8, 8>(p, s);
-  else
-    ok = irf_dwp_nto<2, 4, 8>(p, s);
-  if (!ok) throw std::runtime_error("ir_dwproj_f32: no kernel for oup_pad " + std::to_string(p.oup_pad));
 }
 
 // Classifier front end: crop gather + 2x2 s2d stem (16 -> 32, ReLU6) + MobileNetV2 block 1 (t = 1: depthwise
@@ -482,17 +410,13 @@ static void ir_stem_f32(const IrParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   const size_t lds = irf_lds_bytes(1, 32, 0, 16);
   const int tiles = ((p.Wo + 15) / 16) * ((p.Ho + 7) / 8);
-  hipLaunchKernelGGL((ir_f32_kernel<1, 8, 16, 1, false, 1, false, true>), dim3((unsigned)(p.B * tiles)), dim3(256),
+  hipLaunchKernelGGL((ir_f32_kernel<1, 8, 16, 1, false, 1, true>), dim3((unsigned)(p.B * tiles)), dim3(256),
                      lds, s, p);
 }
 
 void ir_block_f32(const IrParams& p, hipStream_t s) {
   if (p.stem) {
     ir_stem_f32(p, s);
-    return;
-  }
-  if (p.dwp) {
-    ir_dwproj_f32(p, s);
     return;
   }
   if (ir_block_crop_f32(p, s)) return;  // 14x14 / 7x7 maps: whole-map x3 kernel (ir_crop_f32.hip)

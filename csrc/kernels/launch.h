@@ -121,9 +121,6 @@ struct IrParams {
   int B;
   const int* bdev;
   int x3w;                  // fp32: we / wp pre-split into bf16 [h|m|l] planes for ir_crop_f32.hip
-  int dwp;                  // fp32: x is the block's hidden tensor (expand ran separately): dw + project only
-  const void* rx;           // dwp: residual (the block input, output geometry), pixel stride rx_cs
-  int rx_cs;
   // fp32 classifier front end (stem = 1, t = 1 blocks, ir_f32.hip): X is not read from memory but built per
   // tile from the batch's uint8 images: crop gather + ImageNet normalisation (crop_gather_s2d semantics) into a
   // space-to-depth tile in LDS, then the 2x2 stem conv over it (+ bias, ReLU6; zero outside the H x W map).
@@ -146,7 +143,6 @@ bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, i
 // MFMA); ir_block_f32 dispatches blocks with split-plane weights (x3w, set by the planner) to it.
 bool ir_block_crop_f32(const IrParams& p, hipStream_t s);
 bool ir_block_crop_f32_supported(int H, int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
-bool ir_dwproj_f32_supported(int stride, int hid_pad, int oup_pad);  // IrParams.dwp blocks (ir_f32.hip)
 void ir_prepare();
 void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole-crop tile
 void set_ir_crop(bool v);

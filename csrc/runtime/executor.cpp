@@ -534,11 +534,6 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.B = batch(r[25]);
         p.bdev = bdev(r[25]);
         p.x3w = (int)r[26];
-        p.dwp = (int)r[27];
-        if (p.dwp && p.res) {
-          p.rx = resolve(bk, sl, r[28], r[29], eb);
-          p.rx_cs = (int)r[30];
-        }
         p.stem = (int)r[31];
         if (p.stem) {  // fp32 classifier front end: crop gather + stem conv feed the block (ir_f32.hip)
           p.st_pool = pool;

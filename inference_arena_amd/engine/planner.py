@@ -37,7 +37,7 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   YOLORAW  1-12 heads as DECODE, 13-15 strides, 16 out_buf (raw [84, A] fp32 per image)
   IRBLOCK  1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 inp 7 inp_pad 8 hid_pad 9 oup 10 oup_pad 11 stride
            12 expand 13 res 14 we 15 be 16 wd 17 bd 18 wp 19 bp 20 y_buf 21 y_coff 22 y_cs 23 Ho 24 Wo
-           25 batch_kind 26 x3w 27 dwp 28-30 residual view (dwp) 31 stem 32 crops_buf 33 S 34-36 mean
+           25 batch_kind 26 x3w 27-30 reserved (0) 31 stem 32 crops_buf 33 S 34-36 mean
            37-39 inv_std (float bits) 40 stem w_off 41 stem b_off
            (fused MobileNetV2 inverted residual, csrc/kernels/ir_block.hip / ir_f32.hip; stem = 1: fp32 crop
             gather + s2d stem conv computed inside the block-1 kernel, x_buf unused)
@@ -407,30 +407,6 @@ class ProgramBuilder:
                1, crops.id, S] + [fbits(m) for m in mean] + [fbits(1.0 / s) for s in std] + \
               [self.weights.add(wsb), self.weights.add(bsb)]
         self._emit(rec, dst, crops)
-
-    def ir_dwproj(self, src: View, dst: View, dw, project, *, stride: int, res: View | None,
-                  kind: int = CROPS) -> None:
-        """fp32: depthwise 3x3 (+ReLU6) -> 1x1 project (+ ``res``) of an inverted residual whose expand ran as its
-        own conv; ``src`` is the hidden tensor (csrc/kernels/ir_f32.hip, IrParams.dwp).  The depthwise output
-        never leaves the kernel."""
-        if not self.f32:
-            raise ValueError("ir_dwproj is an fp32-program op")
-        if dst.C != project[0].shape[0] or src.C != dw[0].shape[0]:
-            raise ValueError("ir_dwproj: channel mismatch")
-        pk = pack_ir_weights(None, dw, project, src.C, k_align=32)
-        f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
-        offs = [0, self.weights.add(f32(torch.zeros(4))), self.weights.add(f32(pk["wd"])),
-                self.weights.add(f32(pk["bd"])), self.weights.add(f32(pk["wp"])), self.weights.add(f32(pk["bp"]))]
-        offs[0] = offs[1]  # no expand weights: a valid offset the kernel never reads
-        H, W = src.buf.H, src.buf.W
-        Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
-        rec = [OP_IRBLOCK, src.bid, src.coff, src.cs, H, W, pk["inp"], pk["inp_pad"], pk["hid_pad"], pk["oup"],
-               pk["oup_pad"], stride, 0, int(res is not None), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind, 0, 1,
-               res.bid if res is not None else 0, res.coff if res is not None else 0, res.cs if res is not None else 0]
-        if res is not None:
-            self._emit(rec, src, dst, res)
-        else:
-            self._emit(rec, src, dst)
 
     def sppf(self, buf: Buffer, C: int, kind: int = IMAGES) -> None:
         self._emit([OP_SPPF, buf.id, 0, buf.C, buf.H, buf.W, C, kind], buf)

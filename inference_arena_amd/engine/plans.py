@@ -38,7 +38,6 @@ from ..models.common import fold, fold_conv_bn
 from ..models.mobilenetv2 import MobileNetV2
 from ..models.yolov5nu import STRIDES, YOLOv5nu
 from .planner import BUF_NONE, BUF_RAWOUT, BUF_XCROPS, CROPS, IMAGES, Program, ProgramBuilder, Reserved, View
-from .validate import ir_dwproj_f32_supported
 
 CAND_BYTES = 32
 CROPREF_BYTES = 32
@@ -268,15 +267,6 @@ def fuse_stem_ir_f32_default() -> bool:
     return os.environ.get("ARENA_F32_STEM_IR", "1").lower() not in ("0", "false", "no", "off")
 
 
-def dwproj_f32_default() -> bool:
-    """``ARENA_F32_DWPROJ=1`` (default 0): fp32 programs run the unfused MobileNetV2 blocks' depthwise + project as
-    one kernel (csrc/kernels/ir_f32.hip, IrParams.dwp) after the expand GEMM.  Off by default: measured slower
-    than the depthwise kernel + project GEMM (14x14 hid 384: 82 vs 52 us, hid 576: 212 vs 92 us, 7x7 hid 960:
-    163 vs 62 us per 128 crops, profiles/r2_irc_f32_experiment.md) — the per-chunk barriers of a 64-pixel tile
-    over 12-30 hidden chunks cost more than the depthwise map's round trip through L2."""
-    return os.environ.get("ARENA_F32_DWPROJ", "0").lower() in ("1", "true", "yes", "on")
-
-
 def fuse_block(blk, H: int, policy) -> bool:
     if policy == "f32":
         return fuse_block_f32(blk, H)
@@ -364,14 +354,6 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
             pb.conv(View(cur, 0, blk.inp), View(E, 0, blk.hidden), *fold(blk.expand), act="relu6", kind=CROPS_)
         else:
             E = cur
-        if pb.f32 and dwproj_f32_default() and ir_dwproj_f32_supported(
-                blk.stride, (blk.hidden + 31) // 32 * 32, (blk.oup + 15) // 16 * 16):
-            # fp32: depthwise + project in one kernel, the depthwise map never stored (ir_f32.hip, dwp)
-            O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup, kind=CROPS_)
-            pb.ir_dwproj(View(E, 0, blk.hidden), View(O, 0, blk.oup), fold(blk.dw), fold(blk.project),
-                         stride=blk.stride, res=View(cur, 0, blk.inp) if blk.use_res else None, kind=CROPS_)
-            cur, H = O, Ho
-            continue
         Dw = pb.tensor(f"m{i}.dw", Ho, Ho, blk.hidden, kind=CROPS_)
         wd, bd = fold(blk.dw)
         pb.dwconv(View(E, 0, blk.hidden), View(Dw, 0, blk.hidden), wd, bd, stride=blk.stride, kind=CROPS_)

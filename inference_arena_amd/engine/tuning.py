@@ -60,15 +60,36 @@ def lookup(ops: np.ndarray, B: int, path: Path | None = None) -> list[int] | Non
 
 
 def store(ops: np.ndarray, B: int, choices: list[int], path: Path | None = None) -> bool:
+    """Add one entry.  Several replicas / services that miss the table at start-up store concurrently: the
+    load-modify-write runs under an fcntl lock on ``<table>.lock`` (across processes; ``_lock`` within one)
+    and the new table goes to a per-process temporary file that is renamed over the table atomically, so a
+    reader never sees a torn file and no writer loses another's entry."""
+    import fcntl
+    import os
+    import tempfile
+
     p = path or table_path()
     with _lock:
-        t = load_table(p)
-        t[f"{fingerprint(ops)}:{B}"] = [int(v) for v in choices]
         try:
             p.parent.mkdir(parents=True, exist_ok=True)
-            tmp = p.with_suffix(".tmp")
-            tmp.write_text(json.dumps(t, indent=0, sort_keys=True) + "\n")
-            tmp.replace(p)
+            with open(p.with_suffix(".lock"), "a+") as lk:
+                fcntl.flock(lk.fileno(), fcntl.LOCK_EX)
+                try:
+                    t = load_table(p)
+                    t[f"{fingerprint(ops)}:{B}"] = [int(v) for v in choices]
+                    fd, tmp = tempfile.mkstemp(prefix=p.name + ".", suffix=".tmp", dir=str(p.parent))
+                    try:
+                        with os.fdopen(fd, "w") as f:
+                            f.write(json.dumps(t, indent=0, sort_keys=True) + "\n")
+                        os.replace(tmp, p)
+                    except BaseException:
+                        try:
+                            os.unlink(tmp)
+                        except OSError:
+                            pass
+                        raise
+                finally:
+                    fcntl.flock(lk.fileno(), fcntl.LOCK_UN)
             return True
         except OSError:
             return False

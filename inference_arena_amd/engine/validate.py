@@ -69,11 +69,6 @@ IR_CROP_F32_CONFIGS = {(14, 1, 64, 64), (14, 1, 64, 96), (14, 1, 96, 96), (7, 2,
                        (7, 1, 160, 320)}
 
 
-def ir_dwproj_f32_supported(stride: int, hid_pad: int, oup_pad: int) -> bool:
-    """Mirror of arena::ir_dwproj_f32_supported (fp32 dw + project blocks, IrParams.dwp)."""
-    return stride in (1, 2) and hid_pad % 32 == 0 and oup_pad % 16 == 0 and oup_pad // 16 in (4, 6, 10)
-
-
 def ir_crop_f32_supported(H: int, stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
     """Mirror of arena::ir_block_crop_f32_supported (whole-map x3 kernel for the 14x14 / 7x7 stages)."""
     Ho = (H - 1) // stride + 1
@@ -170,17 +165,16 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             if inp_pad % (16 if f32 else 32) or hid_pad % 32 or oup_pad % 16 or inp > inp_pad or oup > oup_pad \
                     or inp % (4 if f32 else 8):
                 raise ProgramError(f"op {i}: bad ir_block channel geometry")
-            x3w, dwp = int(r[26]), int(r[27])
+            x3w = int(r[26])
+            if any(int(v) for v in r[27:31]):
+                raise ProgramError(f"op {i}: ir_block fields 27-30 are reserved (0)")
             if x3w and not (f32 and H == W and ir_crop_f32_supported(H, S, inp_pad, hid_pad, oup_pad, int(r[12]))):
                 raise ProgramError(f"op {i}: split-plane weights for a block the whole-map kernel does not take")
-            if dwp and not (f32 and not int(r[12]) and inp_pad == hid_pad
-                            and ir_dwproj_f32_supported(S, hid_pad, oup_pad)):
-                raise ProgramError(f"op {i}: no fp32 dw + project kernel for this block")
-            if f32 and not x3w and not dwp and not ir_f32_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])):
+            if f32 and not x3w and not ir_f32_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])):
                 raise ProgramError(f"op {i}: no fp32 fused kernel for this block")
             if Ho != (H - 1) // S + 1 or Wo != (W - 1) // S + 1:
                 raise ProgramError(f"op {i}: ir_block output size mismatch")
-            if int(r[13]) and (S != 1 or (inp != oup and not dwp)):
+            if int(r[13]) and (S != 1 or inp != oup):
                 raise ProgramError(f"op {i}: ir_block residual needs stride 1 and inp == oup")
             if int(r[31]):  # fp32 crop gather + stem computed in the kernel: no input view, the crop plan instead
                 if not (f32 and S == 1 and not int(r[12]) and not int(r[13]) and inp == 32 and inp_pad == 32
@@ -192,12 +186,9 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             else:
                 view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, el, "ir input")
             view(i, r[20], int(r[21]), int(r[22]), n * Ho * Wo, oup, el, "ir output")
-            if dwp and int(r[13]):
-                view(i, r[28], int(r[29]), int(r[30]), n * Ho * Wo, oup, el, "ir residual")
             wel = 6 if x3w else el  # three bf16 planes per weight
-            if not dwp:  # dw + project blocks have no expand weights
-                weights(i, int(r[14]), hid_pad * inp_pad * wel, "ir expand weight")
-                weights(i, int(r[15]), hid_pad * 4, "ir expand bias")
+            weights(i, int(r[14]), hid_pad * inp_pad * wel, "ir expand weight")
+            weights(i, int(r[15]), hid_pad * 4, "ir expand bias")
             weights(i, int(r[16]), 9 * hid_pad * el, "ir dw weight")
             weights(i, int(r[17]), hid_pad * 4, "ir dw bias")
             weights(i, int(r[18]), oup_pad * hid_pad * wel, "ir project weight")

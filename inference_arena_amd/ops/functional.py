@@ -121,28 +121,6 @@ def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: boo
     return y
 
 
-def ir_dwproj_nhwc(e: torch.Tensor, dw, project, *, stride: int, res: torch.Tensor | None = None,
-                   bdev: torch.Tensor | None = None) -> torch.Tensor:
-    """fp32 depthwise 3x3 (+ReLU6) -> 1x1 project (+ ``res``) of an inverted residual's hidden tensor ``e``
-    [B, H, W, hid] in one kernel (csrc/kernels/ir_f32.hip, IrParams.dwp)."""
-    from ..engine.planner import pack_ir_weights
-
-    B, H, W, C = e.shape
-    assert e.dtype == torch.float32
-    pk = pack_ir_weights(None, dw, project, C, k_align=32)
-    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
-    y = torch.empty(B, Ho, Wo, pk["oup"], dtype=e.dtype, device=e.device)
-    dev = {k: pk[k].float().contiguous().to(e.device) for k in ("wd", "bd", "wp", "bp")}
-    native().ir_block({"x": _ptr(e), "x_cs": C, "H": H, "W": W, "inp": C, "inp_pad": pk["inp_pad"],
-                       "hid_pad": pk["hid_pad"], "oup": pk["oup"], "oup_pad": pk["oup_pad"], "stride": stride,
-                       "expand": 0, "res": int(res is not None), "we": _ptr(dev["wd"]), "be": _ptr(dev["bd"]),
-                       **{k: _ptr(v) for k, v in dev.items()}, "y": _ptr(y), "y_cs": pk["oup"], "Ho": Ho, "Wo": Wo,
-                       "B": B, "bdev": _ptr(bdev), "stream": _stream(), "f32": 1, "dwp": 1,
-                       "rx": _ptr(res), "rx_cs": res.shape[-1] if res is not None else 0})
-    torch.cuda.synchronize(e.device)
-    return y
-
-
 def sppf_nhwc(buf: torch.Tensor, C: int) -> torch.Tensor:
     """In place: buf[..., C:4C] = cascaded 5x5 max pools of buf[..., :C]."""
     B, H, W, Ct = buf.shape

