@@ -3,7 +3,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-S=scripts/gpu_step.sh
+S=scripts/gpurun/gpu_step.sh
 T=${1:-gputests}
 K=${2:-}
 mkdir -p gpurun_out/$T

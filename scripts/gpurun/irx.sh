@@ -4,7 +4,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-S=scripts/gpu_step.sh
+S=scripts/gpurun/gpu_step.sh
 T=${1:-irx}
 mkdir -p gpurun_out/$T
 $S 300 gpurun_out/$T/tests.log python -u -m pytest tests/test_fp32_gpu.py -x -q -k "ir_block_f32" --timeout 120 --timeout-method thread -p no:cacheprovider || exit 1
