@@ -78,6 +78,7 @@ void py_conv2d(const py::dict& d) {
   p.pw_cout = get<int>(d, "pw_cout", 0);
   p.pw_kpad = get<int>(d, "pw_kpad", 0);
   p.pw_act = get<int>(d, "pw_act", 0);
+  p.w3 = ptr<const void*>(d, "w3");
   prepare_kernels();  // dynamic-LDS limits of the x3 halo / fused kernels (before any launch)
   if (get<int>(d, "f32", 0))
     conv2d_f32(p, stream_of(d));

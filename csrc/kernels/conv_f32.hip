@@ -1582,6 +1582,11 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
     return;
   }
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
+    if (p.impl >= kF32X3G && p.impl < kF32X3G + kF32X3GVariants) {
+      if (!conv_x3g(p, s, p.impl - kF32X3G))
+        throw std::runtime_error("conv2d_f32: not an x3g-eligible conv (needs pre-split weights; 1x1 or Cin % 32)");
+      return;
+    }
     if (p.impl == kF32X3H16) {
       if (!x3_h16(p, s)) throw std::runtime_error("conv2d_f32: not an x3-h16-eligible conv (3x3 s1 over 16 channels)");
       return;

@@ -50,6 +50,9 @@ struct ConvParams {
   // from the batch's uint8 images (letterbox.h), H x W being the space-to-depth grid (T / 2) of the target.
   const uint8_t* lb_pool;
   const ImageMeta* lb_meta;
+  // fp32 programs: the weights pre-split into bf16 planes, [ceil(Kpad/32)][Cout_pad][h 32 | m 32 | l 32]
+  // (engine/planner.py pack_conv_weight_x3), read by the x3g kernels (gemm_x3.hip); nullptr when absent
+  const void* w3;
 };
 void conv2d(const ConvParams& p, hipStream_t s);
 void conv_igemm(const ConvParams& p, hipStream_t s);  // LDS-pipelined implicit GEMM (impl 3)
@@ -82,7 +85,12 @@ constexpr int kF32StreamExact = 107;  // streaming small-K conv on exact fp32 MF
 constexpr int kF32X3Halo16 = 108;    // x3 halo tiles of 16 x 16 output pixels (8 waves)
 constexpr int kF32X3Halo16N3 = 109;  // ... with 48-channel tiles
 constexpr int kF32X3H16 = 110;       // x3 3x3 stride-1 conv over exactly 16 input channels (s2d stems)
+constexpr int kF32X3G = 111;         // x3g: 32x32x16 MFMA implicit GEMM over pre-split weights, variant v
+constexpr int kF32X3GVariants = 20;  // v >= 10: v - 10 with the interleaved schedule   // impl kF32X3G + v, v < kF32X3GVariants (gemm_x3.hip XG_VARIANTS)
 void x3_halo_prepare();
+bool x3g_supported(const ConvParams& p);
+bool conv_x3g(const ConvParams& p, hipStream_t s, int v);  // false if the conv or variant is not supported
+void x3g_prepare();
 bool conv_fc_f32(const ConvParams& p, hipStream_t s);
 void conv2d_f32(const ConvParams& p, hipStream_t s);
 

@@ -276,7 +276,7 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
                                 (v >= kF32X3 && v < kF32X3 + kF32X3Variants) || v == kF32Halo || v == kF32X3Halo ||
                                 v == kF32X3HaloN3 || v == kF32X3HaloN2 || v == kF32Stream || v == kF32StreamN2 ||
                                 v == kF32Fc || v == kF32StreamExact || v == kF32X3Halo16 || v == kF32X3Halo16N3 ||
-                                v == kF32X3H16
+                                v == kF32X3H16 || (v >= kF32X3G && v < kF32X3G + kF32X3GVariants)
                           : v >= 0 && v <= 3;
       if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
       bk.impl[i] = (int8_t)v;
@@ -320,7 +320,10 @@ void Executor::autotune(Bucket& bk) {
                                        23,     24,     kF32Halo, kF32X3, kF32X3 + 1, kF32X3 + 4, kF32X3 + 5,
                                        kF32X3 + 6, kF32X3 + 7, kF32X3 + 8, kF32X3Halo, kF32X3HaloN3,
                                        kF32X3HaloN2, kF32Stream, kF32StreamN2, kF32Fc, kF32StreamExact,
-                                       kF32X3Halo16, kF32X3Halo16N3, kF32X3H16};
+                                       kF32X3Halo16, kF32X3Halo16N3, kF32X3H16,
+                                       // x3g variants that won a layer in tools/bench_x3g.py (impl 111 + v)
+                                       kF32X3G + 5, kF32X3G + 6, kF32X3G + 7, kF32X3G + 9, kF32X3G + 15,
+                                       kF32X3G + 16, kF32X3G + 17, kF32X3G + 19};
   static const int kBf16Candidates[] = {1, 2, 3};
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;
@@ -461,6 +464,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.act = (int)r[28];
         p.B = batch(r[30]);
         p.bdev = bdev(r[30]);
+        if (r[41] != 0) p.w3 = W + r[40];  // fp32: pre-split bf16 weight planes for the x3g kernels
         if (r[1] == BUF_POOL) {  // the stem conv samples the letterboxed images itself (fp32 x3-h16 kernel)
           if (!f32 || r[30] != 0) throw std::runtime_error("executor: letterbox-source conv must be fp32 over images");
           p.x = nullptr;

@@ -21,6 +21,7 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
          27 y2_cs 28 act 29 f32out 30 batch_kind
          31 pw_w_off 32 pw_kpad 33 pw_b_off 34 pw_cout (0 = none) 35 pw_cout_pad 36 pw_y_buf 37 pw_y_coff
          38 pw_y_cs 39 pw_act   (pointwise conv fused into the 3x3 epilogue; y_buf may then be BUF_NONE)
+         40 w3_off 41 has_w3 (fp32: weights pre-split into bf16 planes, pack_conv_weight_x3)
   DWCONV 1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 C 7 w_off 8 b_off 9 y_buf 10 y_coff
          11 y_cs 12 Ho 13 Wo 14 stride 15 act 16 batch_kind
   SPPF   1 buf 2 coff 3 cs 4 H 5 W 6 C 7 batch_kind
@@ -194,6 +195,22 @@ def pack_conv_weight(w: torch.Tensor, b: torch.Tensor, dtype: str = "bf16") -> t
     return (f32_bytes(wk) if dtype == "fp32" else bf16_bytes(wk)), bb.numpy().tobytes(), kpad, cpad
 
 
+def pack_conv_weight_x3(w: torch.Tensor) -> bytes:
+    """[Cout, Cin, KH, KW] fp32 -> the x3g kernels' pre-split operand (csrc/kernels/gemm_x3.hip): the fp32
+    [Cout_pad][Kpad] matrix of ``pack_conv_weight`` zero-padded to K32 = ceil(Kpad / 32) * 32 and split into
+    bf16 planes (split_bf16x3), stored [K32 / 32][Cout_pad][h 32 | m 32 | l 32] so that one 32-deep K chunk of
+    consecutive output channels is one contiguous run of 192-byte rows."""
+    cout, cin, kh, kw = w.shape
+    k = kh * kw * cin
+    kpad = _round(k, 16)
+    k32 = _round(kpad, 32)
+    cpad = _round(cout, 16)
+    wk = torch.zeros(cpad, k32, dtype=torch.float32)
+    wk[:cout, :k] = w.detach().float().permute(0, 2, 3, 1).reshape(cout, k)
+    planes = split_bf16x3(wk.reshape(cpad, k32 // 32, 32))  # [cpad][kc][3][32]
+    return bf16_raw_bytes(planes.permute(1, 0, 2, 3).contiguous())
+
+
 def pack_ir_weights(expand, dw, project, inp: int, k_align: int = 32) -> dict:
     """Padded operand layouts of the fused inverted-residual kernels (csrc/kernels/ir_block.hip, ir_f32.hip):
     we [hid_pad][inp_pad], wd [9][hid_pad], wp [oup_pad][hid_pad] + fp32 biases.  ``k_align``: inp_pad
@@ -343,6 +360,9 @@ class ProgramBuilder:
             wb2, bb2, kpad2, cpad2 = pack_conv_weight(w2, b2)
             rec += [self.weights.add(wb2), kpad2, self.weights.add(bb2), co2, cpad2, pw_dst.bid, pw_dst.coff,
                     pw_dst.cs, ACT[act2]]
+        elif self.f32 and src.bid != BUF_POOL:
+            # fp32: the weights once more as pre-split bf16 planes for the x3g kernels (fields 40-41)
+            rec += [0] * 9 + [self.weights.add(pack_conv_weight_x3(w)), 1]
         self._emit(rec, src, dst, res, dst2, pw_dst)
 
     def dwconv(self, src: View, dst: View, w: torch.Tensor, b: torch.Tensor, *, stride: int, act: str = "relu6",

@@ -14,7 +14,7 @@ import struct
 import numpy as np
 import torch
 
-from ..engine.planner import ACT, pack_conv_weight
+from ..engine.planner import ACT, pack_conv_weight, pack_conv_weight_x3
 from . import native
 
 IMAGE_META = struct.Struct("<qiiiiiif12x")  # must match arena::ImageMeta (48 bytes)
@@ -30,11 +30,16 @@ def _ptr(t: torch.Tensor | None, elem_off: int = 0) -> int:
     return t.data_ptr() + elem_off * t.element_size()
 
 
-def pack_weights(w: torch.Tensor, b: torch.Tensor, device, dtype: str = "bf16") -> tuple[torch.Tensor, torch.Tensor, int, int]:
+def pack_weights(w: torch.Tensor, b: torch.Tensor, device, dtype: str = "bf16"):
+    """-> (weights, bias, Kpad, Cout_pad, w3): ``w3`` the pre-split bf16 planes of the fp32 x3g kernels
+    (planner.pack_conv_weight_x3; None for bf16)."""
     wb, bb, kpad, cpad = pack_conv_weight(w.detach().cpu().float(), b.detach().cpu().float(), dtype)
     wt = torch.frombuffer(bytearray(wb), dtype=torch.float32 if dtype == "fp32" else torch.bfloat16).to(device)
     bt = torch.frombuffer(bytearray(bb), dtype=torch.float32).to(device)
-    return wt, bt, kpad, cpad
+    w3 = None
+    if dtype == "fp32":
+        w3 = torch.frombuffer(bytearray(pack_conv_weight_x3(w.detach().cpu().float())), dtype=torch.int16).to(device)
+    return wt, bt, kpad, cpad, w3
 
 
 def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: int = 1, pad=None, act=None,
@@ -48,7 +53,8 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
     A float32 ``x`` runs the exact-fp32 kernel (fp32 weights, v_mfma_f32_16x16x4_f32, fp32 output).
     ``impl`` pins a kernel (0 = the dispatch policy; fp32: 1 direct, 2 LDS, 10 + v LDS tile variant v,
     40 + v triple-bf16-split variant v, 100 halo, 101 split halo, 102 / 103 split halo with 48 / 32-channel
-    tiles, 104 / 105 weight-stationary streaming 1x1 (auto / 32-channel tiles) — csrc/kernels/launch.h).
+    tiles, 104 / 105 weight-stationary streaming 1x1 (auto / 32-channel tiles), 111 + v the x3g 32x32x16 GEMM
+    over pre-split weights — csrc/kernels/launch.h).
     """
     f32 = x.dtype == torch.float32
     B, H, W, Cx = x.shape
@@ -65,7 +71,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
         Ho, Wo = out_hw
     if out is None:
         out = torch.empty(B, Ho, Wo, cout, dtype=torch.float32 if (f32out or f32) else torch.bfloat16, device=x.device)
-    wt, bt, kpad, cpad = packed if packed is not None else pack_weights(w, b, x.device, "fp32" if f32 else "bf16")
+    wt, bt, kpad, cpad, w3 = packed if packed is not None else pack_weights(w, b, x.device, "fp32" if f32 else "bf16")
     native().conv2d({
         "x": _ptr(x, x_coff), "B": B, "H": H, "W": W, "xs": Cx, "Cin": cin,
         "w": _ptr(wt), "Kpad": kpad, "bias": _ptr(bt),
@@ -74,7 +80,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
         "res": _ptr(res, res_coff), "rs": res.shape[-1] if res is not None else 0,
         "y2": _ptr(out2, out2_coff), "y2s": out2.shape[-1] if out2 is not None else 0,
         "act": ACT[act], "f32out": int(f32out), "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32),
-        "impl": int(impl),
+        "impl": int(impl), "w3": _ptr(w3),
     })
     return out
 

@@ -78,7 +78,73 @@ def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
 
 
 # x3 tile variants, split halo (auto/48/32), split stream (auto/32), FC, exact-fp32 stream — same fp32 bound
-X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105, 106, 107, 108, 109, 110]
+X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105, 106, 107, 108, 109, 110] + \
+    [111 + v for v in range(6)]
+X3G_IMPLS = [111 + v for v in range(20)]  # x3g: 32x32x16 MFMA GEMM over pre-split weights (gemm_x3.hip)
+
+
+@pytest.mark.parametrize(
+    "B,H,Cin,Cout,k,s,act,res,up",
+    [
+        (2, 40, 32, 64, 3, 2, "silu", False, False),    # detector 3x3 s2 (160 -> 80 geometry)
+        (3, 20, 64, 128, 3, 2, "silu", False, False),   # 3x3 s2, Cin 64
+        (2, 10, 128, 256, 3, 2, "silu", False, False),  # 3x3 s2, Cin 128, 8 N tiles of 32
+        (3, 13, 128, 128, 1, 1, "silu", False, False),  # C3 1x1, partial pixel tiles
+        (2, 9, 256, 128, 1, 1, "silu", False, True),    # neck 1x1 with the 2x upsampled copy
+        (2, 11, 80, 80, 1, 1, "silu", False, False),    # Cin 80: a partial K chunk
+        (5, 7, 160, 960, 1, 1, "relu6", False, False),  # MobileNet expand
+        (5, 7, 960, 160, 1, 1, None, True, False),      # MobileNet project + residual
+        (5, 7, 960, 320, 1, 1, None, False, False),     # last MobileNet project
+        (2, 5, 512, 256, 1, 1, "silu", False, False),   # SPPF cv2 (K 512)
+    ],
+)
+def test_conv_x3g_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
+    """Every x3g variant (pre-split weights, activations split on staging) at the fp32 bound, incl. the
+    residual and upsampled-copy epilogues."""
+    g = torch.Generator().manual_seed(B * 1000 + H + Cin + Cout + k)
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64) / (Cin * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g, dtype=torch.float64) * 0.1
+    x32, w32, b32 = x.float(), w.float(), b.float()
+    pad = k // 2
+    ref = _act64(F.conv2d(x32.double(), w32.double(), b32.double(), stride=s, padding=pad), act)
+    scale = F.conv2d(x32.double().abs(), w32.double().abs(), b32.double().abs(), stride=s, padding=pad)
+    Ho = ref.shape[2]
+    r = torch.randn(B, Cout, Ho, Ho, generator=g).float() if res else None
+    if res:
+        ref = ref + r.double()
+        scale = scale + r.double().abs()
+    xd = _nhwc(x32).to(device)
+    rd = _nhwc(r).to(device) if res else None
+    packed = AF.pack_weights(w32, b32, device, "fp32")
+    for impl in X3G_IMPLS:
+        out2 = torch.full((B, 2 * Ho, 2 * Ho, Cout), float("nan"), device=device) if up else None
+        y = AF.conv2d_nhwc(xd, w32, b32, stride=s, act=act, res=rd, packed=packed, impl=impl, out2=out2)
+        torch.cuda.synchronize()
+        _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
+        if up:
+            want = y.permute(0, 3, 1, 2).repeat_interleave(2, 2).repeat_interleave(2, 3)
+            assert torch.equal(out2.permute(0, 3, 1, 2), want), impl
+
+
+def test_conv_x3g_channel_slices_and_live_batch(device):
+    """Reads a channel slice of a wider buffer, stores into a channel slice, and honours the device-side live
+    batch count (blocks past it leave the output untouched)."""
+    g = torch.Generator().manual_seed(11)
+    buf = torch.randn(4, 12, 12, 96, generator=g)
+    w = torch.randn(64, 32, 3, 3, generator=g) * 0.05
+    b = torch.randn(64, generator=g) * 0.1
+    packed = AF.pack_weights(w, b, device, "fp32")
+    ref = F.conv2d(buf[..., 32:64].permute(0, 3, 1, 2).double(), w.double(), b.double(), stride=2, padding=1)
+    live = torch.tensor([3], dtype=torch.int32, device=device)
+    for impl in X3G_IMPLS:
+        out = torch.full((4, 6, 6, 128), 7.0, device=device)
+        AF.conv2d_nhwc(buf.to(device), w, b, stride=2, act=None, x_coff=32, cin=32, out=out, out_coff=64,
+                       packed=packed, impl=impl, bdev=live)
+        torch.cuda.synchronize()
+        got = out[:3, :, :, 64:].permute(0, 3, 1, 2).double().cpu()
+        assert (got - ref[:3]).abs().max().item() < 1e-5, impl
+        assert torch.all(out[:, :, :, :64] == 7.0) and torch.all(out[3] == 7.0), impl
 
 
 @pytest.mark.parametrize(

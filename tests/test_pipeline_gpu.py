@@ -256,3 +256,29 @@ def test_overflow_passes_serialised_two_in_flight(dense_models, device, monkeypa
         for x, y in zip(got, big.infer(imgs)):
             np.testing.assert_array_equal(x.topk_idx, y.topk_idx)
             np.testing.assert_allclose(x.topk_logit, y.topk_logit, rtol=1e-5, atol=1e-5)
+
+
+def test_set_weights_device_from_torch_tensor(device):
+    """The N-rank weight path (bench.py: RCCL broadcast -> Executor.set_weights_device): a pipeline built with
+    other weights, given another pipeline's folded weight blob as a torch CUDA tensor (device-to-device copy),
+    reads back the same bytes and produces bit-identical outputs."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+    from inference_arena_amd.models.zoo import make_mobilenet, make_yolo
+
+    a = GpuPipeline(make_yolo(0, cls_shift=-20.0), make_mobilenet(1), device=0, buckets=[4], dtype="fp32")
+    b = GpuPipeline(make_yolo(5, cls_shift=-20.0), make_mobilenet(6), device=0, buckets=[4], dtype="fp32")
+    blob = np.ascontiguousarray(a.program.weights)
+    assert blob.nbytes == np.ascontiguousarray(b.program.weights).nbytes
+    assert bytes(b.ex.weights_host()) != blob.tobytes()
+    t = torch.from_numpy(blob.view(np.uint8).copy()).to("cuda:0")
+    b.ex.set_weights_device(t.data_ptr(), t.numel())
+    torch.cuda.synchronize()
+    assert bytes(b.ex.weights_host()) == blob.tobytes()
+    imgs = synthetic_images(4, 21)
+    ra, rb = a.infer(imgs), b.infer(imgs)
+    assert sum(len(r) for r in ra) > 0
+    for x, y in zip(ra, rb):
+        np.testing.assert_array_equal(x.boxes, y.boxes)
+        np.testing.assert_array_equal(x.topk_idx, y.topk_idx)
+        np.testing.assert_array_equal(x.topk_logit, y.topk_logit)

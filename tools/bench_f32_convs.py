@@ -52,7 +52,8 @@ def main(argv=None) -> int:
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(0)
     x3 = [int(v) for v in a.x3.split(",") if v != ""]
-    cols = ["default"] + [f"v{v}" for v in variants] + [f"x{v}" for v in x3] + ["halo", "xhalo"]
+    cols = ["default"] + [f"v{v}" for v in variants] + [f"x{v}" for v in x3] + ["halo", "xhalo"] + \
+        [f"g{v}" for v in range(6)]
     lines = ["| op | shape | " + " | ".join(cols) + " | best | gain us | max rel err fp32 | max rel err x3 |",
              "|---|---|" + "---|" * len(cols) + "---|---|---|---|"]
     tot_default = tot_best = 0.0
@@ -76,7 +77,7 @@ def main(argv=None) -> int:
             continue
         times, errs = {}, {}
         impls = ([("default", 0)] + [(f"v{v}", 10 + v) for v in variants] + [(f"x{v}", 40 + v) for v in x3] +
-                 [("halo", 100), ("xhalo", 101)])
+                 [("halo", 100), ("xhalo", 101)] + [(f"g{v}", 111 + v) for v in range(6)])
         for name, impl in impls:
             y = torch.empty_like(ref)
 
@@ -118,7 +119,7 @@ def main(argv=None) -> int:
 
 def _conv(C, AF, x, packed, y, impl, base, KH, KW, Cout, res):
     """conv2d_f32 with an explicit ConvParams.impl (bypasses the global policy)."""
-    wt, bt, kpad, cpad = packed
+    wt, bt, kpad, cpad, w3 = packed
     B, H, W, Cx = x.shape
     Ho, Wo = base["out_hw"]
     pt, pl = base["pad"]
@@ -129,7 +130,7 @@ def _conv(C, AF, x, packed, y, impl, base, KH, KW, Cout, res):
         "KH": KH, "KW": KW, "stride": base["stride"], "pad_t": pt, "pad_l": pl,
         "res": res.data_ptr() if res is not None else 0, "rs": Cout if res is not None else 0,
         "y2": 0, "y2s": 0, "act": AF.ACT["silu"], "f32out": 0, "bdev": 0,
-        "stream": AF._stream(), "f32": 1, "impl": impl,
+        "stream": AF._stream(), "f32": 1, "impl": impl, "w3": w3.data_ptr(),
     })
 
 

@@ -31,6 +31,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = [
     "kernels/conv_mfma.hip",
     "kernels/conv_f32.hip",
+    "kernels/gemm_x3.hip",
     "kernels/ir_f32.hip",
     "kernels/ir_crop_f32.hip",
     "kernels/dwconv.hip",
