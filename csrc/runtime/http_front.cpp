@@ -436,6 +436,12 @@ void HttpFrontEnd::close_conn(int ep, const std::shared_ptr<Conn>& c) {
 }
 
 void HttpFrontEnd::handle_readable(int ep, const std::shared_ptr<Conn>& c) {
+  {
+    // handle_writable of the same event may have closed it: its descriptor number can already belong to a
+    // connection another I/O thread accepted (found by tests/test_native_http.py's TSAN stress)
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->closed) return;
+  }
   char buf[65536];
   bool eof = false;
   // Buffer at most one maximal request (body + headers) plus one read: a client pipelining while a request
@@ -543,7 +549,7 @@ void HttpFrontEnd::handle_writable(int ep, const std::shared_ptr<Conn>& c) {
 bool HttpFrontEnd::parse_one(const std::shared_ptr<Conn>& c) {
   std::string& in = c->in;
   const size_t hend = in.find("\r\n\r\n");
-  if (hend == std::string::npos) {
+  if (hend == std::string::npos || hend > 65536) {  // the header block is capped whether or not it is complete
     if (in.size() > 65536) {
       {
         std::lock_guard<std::mutex> lk(c->mu);

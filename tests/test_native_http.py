@@ -295,3 +295,40 @@ def test_stage_timing_and_stage_histograms(server):
         text = r.read().decode()
     for stage in ("decode", "queue", "gpu", "detection", "classification", "total"):
         assert f'arena_request_latency_seconds_count{{arch="monolithic",stage="{stage}"}}' in text
+
+
+_FRONT_SRCS = ["csrc/tests/front_stress.cpp", "csrc/runtime/http_front.cpp", "csrc/runtime/batcher.cpp",
+               "csrc/runtime/trace.cpp"]
+
+
+@pytest.mark.parametrize("sanitizer", ["thread", "address"])
+def test_front_end_stress_under_sanitizer(sanitizer):
+    """The native HTTP front end (I/O threads, collector, batcher threads, handler-mode owners) under TSAN /
+    ASAN: keep-alive and pipelined clients with checked answers, half-close, oversized headers, malformed
+    requests, decoder errors, oversize results on the worker pipe, dropped connections, drain() and stop()
+    under load (csrc/tests/front_stress.cpp)."""
+    import os
+    import shutil
+    import subprocess
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not (Path(hipcc).exists() or shutil.which(hipcc)):
+        pytest.skip("hipcc not available")
+    srcs = [root / s for s in _FRONT_SRCS]
+    out = root / "build" / f"front_stress_{sanitizer}"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    newest = max(p.stat().st_mtime for p in srcs + list((root / "csrc" / "runtime").glob("*.h")))
+    if not out.exists() or out.stat().st_mtime < newest:
+        cmd = [hipcc, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", f"-fsanitize={sanitizer}",
+               "-I" + str(root / "csrc"), *map(str, srcs), "-ldl", "-o", str(out)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-4000:]
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1",
+               ASAN_OPTIONS="detect_leaks=1:halt_on_error=1")
+    r = subprocess.run([str(out)], capture_output=True, text=True, timeout=600, env=env)
+    report = r.stdout + r.stderr
+    assert "ThreadSanitizer" not in report and "AddressSanitizer" not in report, report[-6000:]
+    assert r.returncode == 0, report[-6000:]
+    assert "front_stress: ok" in r.stdout
