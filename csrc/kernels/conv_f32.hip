@@ -1584,7 +1584,7 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (p.impl >= 10) {  // explicit variant (autotune table / microbenchmarks)
     if (p.impl >= kF32X3G && p.impl < kF32X3G + kF32X3GVariants) {
       if (!conv_x3g(p, s, p.impl - kF32X3G))
-        throw std::runtime_error("conv2d_f32: not an x3g-eligible conv (needs pre-split weights; 1x1 or Cin % 32)");
+        throw std::runtime_error("conv2d_f32: not an x3g-eligible conv (needs pre-split weights)");
       return;
     }
     if (p.impl == kF32X3H16) {

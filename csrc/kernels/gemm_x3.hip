@@ -115,7 +115,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams
   // are one per-thread constant plus a uniform per-chunk step (host: both tensors < 2 GiB, x3g_supported).
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.x), (short)0, (int)((size_t)p.B * p.H * p.W * p.xs * 4), 0x00020000);
-  const int nk = (p.Kpad + 31) >> 5;
+  const int Cin32 = (p.Cin + 31) & ~31;          // each tap's channels padded to whole 32-deep chunks
+  const int nk = p.KH * p.KW * (Cin32 >> 5);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.w3), (short)0, (int)((size_t)nk * p.Cout_pad * 192), 0x00020000);
   const int Cin = p.Cin, H = p.H, W = p.W, S = p.stride;
@@ -152,12 +153,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams
   f32x4 ra0[AI][2], ra1[AI][2];
   u32x4 rw0[WI], rw1[WI];
   // (ky, kx, c0) of the next chunk to load: chunks are loaded strictly in order, so a running position
-  // replaces a division per chunk (Cin % 32 == 0 for multi-tap kernels: a chunk never straddles two taps)
+  // replaces a division per chunk (the weight layout pads each tap to Cin32: a chunk never straddles two taps)
   int ld_ky = 0, ld_kx = 0, ld_c0 = 0;
   auto load = [&](int kc, f32x4 (&ra)[AI][2], u32x4 (&rw)[WI]) {
     const int ky = ld_ky, kx = ld_kx, c0 = ld_c0;
     ld_c0 += 32;  // advanced with selects, not branches: the K step stays one scheduling region
-    const bool wrap = ld_c0 >= Cin && p.KH * p.KW > 1;
+    const bool wrap = ld_c0 >= Cin32;
     ld_c0 = wrap ? 0 : ld_c0;
     ld_kx += wrap ? 1 : 0;
     const bool wrap2 = ld_kx == p.KW;
@@ -310,6 +311,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams
   }
 }
 
+
 namespace {
 
 template <int WM, int WN, int TM, int TN, bool IL>
@@ -333,13 +335,14 @@ void xg_launch(const ConvParams& p, hipStream_t s) {
   X(8, 4, 2, 2, 1)     /* 256 px x  64 ch, 8 waves */ \
   X(9, 4, 2, 1, 1)     /* 128 px x  64 ch, 8 waves */
 
+
 }  // namespace
 
 bool x3g_supported(const ConvParams& p) {
   const size_t x_bytes = (size_t)p.B * p.H * p.W * p.xs * 4;
-  const size_t w_bytes = (size_t)((p.Kpad + 31) / 32) * p.Cout_pad * 192;
+  const size_t w_bytes = (size_t)p.KH * p.KW * ((p.Cin + 31) / 32) * p.Cout_pad * 192;
   return p.w3 != nullptr && x_bytes < (1u << 31) - (1u << 20) && w_bytes < (1u << 31) - (1u << 20) && p.Cin % 4 == 0 && p.xs % 4 == 0 && p.Kpad >= p.KH * p.KW * p.Cin &&
-         ((p.KH == 1 && p.KW == 1) || p.Cin % 32 == 0) && p.Cout % 4 == 0 && p.ys % 4 == 0 &&
+         p.Cout % 4 == 0 && p.ys % 4 == 0 &&
          (p.res == nullptr || p.rs % 4 == 0) && (p.y2 == nullptr || p.y2s % 4 == 0) && p.lb_meta == nullptr &&
          p.pw_w == nullptr;
 }

@@ -196,18 +196,17 @@ def pack_conv_weight(w: torch.Tensor, b: torch.Tensor, dtype: str = "bf16") -> t
 
 
 def pack_conv_weight_x3(w: torch.Tensor) -> bytes:
-    """[Cout, Cin, KH, KW] fp32 -> the x3g kernels' pre-split operand (csrc/kernels/gemm_x3.hip): the fp32
-    [Cout_pad][Kpad] matrix of ``pack_conv_weight`` zero-padded to K32 = ceil(Kpad / 32) * 32 and split into
-    bf16 planes (split_bf16x3), stored [K32 / 32][Cout_pad][h 32 | m 32 | l 32] so that one 32-deep K chunk of
-    consecutive output channels is one contiguous run of 192-byte rows."""
+    """[Cout, Cin, KH, KW] fp32 -> the pre-split operand of the x3g / x3h kernels (csrc/kernels/gemm_x3.hip):
+    K ordered (ky, kx, c) with each tap's channels zero-padded to Cin32 = ceil(Cin / 32) * 32, so that a 32-deep
+    K chunk kc = tap * Cin32 / 32 + c0 / 32 is one tap's channels c0 .. c0 + 31; split into bf16 planes
+    (split_bf16x3) and stored [KH * KW * Cin32 / 32][Cout_pad][h 32 | m 32 | l 32]: one chunk of consecutive
+    output channels is one contiguous run of 192-byte rows."""
     cout, cin, kh, kw = w.shape
-    k = kh * kw * cin
-    kpad = _round(k, 16)
-    k32 = _round(kpad, 32)
+    cin32 = _round(cin, 32)
     cpad = _round(cout, 16)
-    wk = torch.zeros(cpad, k32, dtype=torch.float32)
-    wk[:cout, :k] = w.detach().float().permute(0, 2, 3, 1).reshape(cout, k)
-    planes = split_bf16x3(wk.reshape(cpad, k32 // 32, 32))  # [cpad][kc][3][32]
+    wk = torch.zeros(cpad, kh * kw, cin32, dtype=torch.float32)
+    wk[:cout, :, :cin] = w.detach().float().permute(0, 2, 3, 1).reshape(cout, kh * kw, cin)
+    planes = split_bf16x3(wk.reshape(cpad, kh * kw * cin32 // 32, 32))  # [cpad][kc][3][32]
     return bf16_raw_bytes(planes.permute(1, 0, 2, 3).contiguous())
 
 

@@ -151,10 +151,10 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 view(i, r[36], int(r[37]), int(r[38]), n * Ho * Wo, co2, 2, "fused pointwise output")
                 weights(i, int(r[31]), cpad2 * kpad2 * 2, "pointwise weight")
                 weights(i, int(r[33]), cpad2 * 4, "pointwise bias")
-            if int(r[41]):  # pre-split bf16 weight planes (x3g kernels): [ceil(Kpad/32)][Cout_pad][3][32]
+            if int(r[41]):  # pre-split bf16 weight planes (x3g / x3h kernels): [KH*KW*Cin32/32][Cout_pad][3][32]
                 if not f32 or int(r[41]) != 1 or int(r[34]) > 0:
                     raise ProgramError(f"op {i}: pre-split weights belong to fp32 convs without a fused epilogue")
-                weights(i, int(r[40]), (kpad + 31) // 32 * Cpad * 192, "conv x3 weight")
+                weights(i, int(r[40]), KH * KW * ((Cin + 31) // 32) * Cpad * 192, "conv x3 weight")
         elif op == OP_DWCONV:
             n = kind_n(r[16])
             H, W, C, Ho, Wo = (int(v) for v in (r[4], r[5], r[6], r[12], r[13]))

@@ -284,23 +284,23 @@ def test_tuning_table_concurrent_writers(tmp_path):
 
 
 def test_pack_conv_weight_x3_layout():
-    """Pre-split x3g weights: [ceil(Kpad/32)][Cout_pad][h|m|l][32] bf16 whose planes sum back to the fp32
-    [Cout_pad][Kpad] matrix of pack_conv_weight (zero-padded to the 32-deep chunk)."""
+    """Pre-split x3g / x3h weights: [KH*KW*Cin32/32][Cout_pad][h|m|l][32] bf16, each tap's channels padded to
+    Cin32, whose planes sum back to the fp32 weights of pack_conv_weight (tap-major K, zeros in the padding)."""
     import numpy as np
     import torch
 
     from inference_arena_amd.engine.planner import pack_conv_weight, pack_conv_weight_x3
 
     g = torch.Generator().manual_seed(3)
-    for cout, cin, k in [(64, 32, 3), (80, 80, 1), (20, 16, 1), (960, 160, 1)]:
+    for cout, cin, k in [(64, 32, 3), (80, 80, 1), (20, 16, 1), (960, 160, 1), (48, 80, 3)]:
         w = torch.randn(cout, cin, k, k, generator=g)
         b = torch.randn(cout, generator=g)
         wb, _, kpad, cpad = pack_conv_weight(w, b, "fp32")
-        ref = np.frombuffer(wb, dtype=np.float32).reshape(cpad, kpad)
-        k32 = (kpad + 31) // 32 * 32
-        raw = np.frombuffer(pack_conv_weight_x3(w), dtype=np.uint16).reshape(k32 // 32, cpad, 3, 32)
+        ref = np.frombuffer(wb, dtype=np.float32).reshape(cpad, kpad)[:, :k * k * cin].reshape(cpad, k * k, cin)
+        cin32 = (cin + 31) // 32 * 32
+        raw = np.frombuffer(pack_conv_weight_x3(w), dtype=np.uint16).reshape(k * k * cin32 // 32, cpad, 3, 32)
         planes = torch.from_numpy(raw.astype(np.int32) << 16).view(torch.float32).double()
-        full = planes.sum(dim=2).permute(1, 0, 2).reshape(cpad, k32).numpy()
-        assert np.array_equal(full[:, kpad:], np.zeros_like(full[:, kpad:]))
-        np.testing.assert_allclose(full[:, :kpad], ref, rtol=2 ** -23, atol=0)
+        full = planes.sum(dim=2).permute(1, 0, 2).reshape(cpad, k * k, cin32).numpy()
+        assert np.array_equal(full[:, :, cin:], np.zeros_like(full[:, :, cin:]))
+        np.testing.assert_allclose(full[:, :, :cin], ref, rtol=2 ** -23, atol=0)
         assert (planes[:, :, 0].abs() >= planes[:, :, 1].abs()).all()

@@ -24,6 +24,13 @@ SHAPES = {  # name: (B, H, Cin, Cout, k, stride)
     "mb_expand": (192, 7, 160, 960, 1, 1),
     "mb_project": (192, 7, 960, 320, 1, 1),
     "head_3x3": (32, 80, 64, 64, 3, 1),
+    "head_144": (32, 80, 64, 144, 3, 1),
+    "head_80": (32, 80, 80, 80, 3, 1),
+    "c3_3x3_32": (32, 80, 32, 32, 3, 1),
+    "c3_3x3_64": (32, 40, 64, 64, 3, 1),
+    "c3_3x3_128": (32, 20, 128, 128, 3, 1),
+    "head_144_40": (32, 40, 128, 144, 3, 1),
+    "stem_16": (32, 160, 16, 16, 3, 1),
 }
 
 
