@@ -279,7 +279,7 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
                                 v == kF32X3H16 || (v >= kF32X3G && v < kF32X3G + kF32X3GVariants)
                           : v >= 0 && v <= 3;
       if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
-      bk.impl[i] = (int8_t)v;
+      bk.impl[i] = (int16_t)v;
     }
   } else if (autotune_) {
     autotune(bk);
@@ -362,7 +362,7 @@ void Executor::autotune(Bucket& bk) {
         best_impl = impl;
       }
     }
-    bk.impl[i] = (int8_t)std::max(best_impl, 0);
+    bk.impl[i] = (int16_t)std::max(best_impl, 0);
     if (autotune_ > 1)
       fprintf(stderr, "[arena autotune] B=%d op %zu -> impl %d (%.1f us)\n", bk.info.B, i, best_impl,
               best * 1e3f / reps);

@@ -187,7 +187,7 @@ class Executor : public BatchInstance {
     uint8_t* d_arena[kMaxSlots] = {};  // per slot (all aliased when concurrency is off)
     int last_slot = 0;                 // slot whose arena read_arena() inspects
     hipGraphExec_t graph[kMaxSlots] = {};
-    std::vector<int8_t> impl;  // per op of prog_: conv kernel family chosen by autotune (0 = default)
+    std::vector<int16_t> impl;  // per op of prog_: conv kernel family chosen by autotune (0 = default)
   };
 
   void alloc_slots();
