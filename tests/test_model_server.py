@@ -324,6 +324,15 @@ def test_model_server_process_stops_cleanly_on_signals(repo):
                             break
                 except OSError:
                     time.sleep(0.3)
+            # the segments this server (and its decode workers) map, not whatever other tests create meanwhile
+            owned = set()
+            for pid in [p.pid] + _children(p.pid):
+                try:
+                    for line in open(f"/proc/{pid}/maps"):
+                        if "/dev/shm/" in line:
+                            owned.add(line.split("/dev/shm/")[1].split()[0])
+                except OSError:
+                    pass
             p.send_signal(sig)
             out, _ = p.communicate(timeout=60)
         finally:
@@ -331,4 +340,20 @@ def test_model_server_process_stops_cleanly_on_signals(repo):
                 p.kill()
         assert p.returncode == 0, out[-2000:]
         assert "Traceback" not in out, out[-2000:]
-        assert not (set(os.listdir("/dev/shm")) - shm_before), "shared memory leaked"
+        assert owned, "the server maps no shared memory (decode pool missing?)"
+        assert not (owned & (set(os.listdir("/dev/shm")) - shm_before)), "shared memory leaked"
+
+
+def _children(pid: int) -> list[int]:
+    import os
+
+    out = []
+    for d in os.listdir("/proc"):
+        if d.isdigit():
+            try:
+                with open(f"/proc/{d}/stat") as f:
+                    if int(f.read().rsplit(")", 1)[1].split()[1]) == pid:
+                        out.append(int(d))
+            except (OSError, ValueError, IndexError):
+                pass
+    return out
