@@ -25,9 +25,33 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 
 
+_next_cpu = [0]
+
+
+def _envelope_cpus() -> list[int] | None:
+    """``ARENA_SERVICE_CPUS=N``: every spawned service process (and its children: replicas, decode workers) is
+    confined to N CPUs of its own, disjoint between services — the reference's per-container envelope of 2
+    vCPU (experiment.yaml:250-267, docker-compose cpus: 2).  GPUs are not partitioned."""
+    n = int(os.environ.get("ARENA_SERVICE_CPUS", "0") or 0)
+    if n <= 0 or not hasattr(os, "sched_getaffinity"):
+        return None
+    allowed = sorted(os.sched_getaffinity(0))
+    start = _next_cpu[0]
+    if start + n > len(allowed):
+        raise RuntimeError(f"ARENA_SERVICE_CPUS={n}: not enough CPUs for another service ({len(allowed)} allowed)")
+    _next_cpu[0] = start + n
+    return allowed[start:start + n]
+
+
 def spawn(args, env, log_dir: Path, name: str):
     log = open(log_dir / f"{name}.log", "w")
-    return subprocess.Popen([sys.executable, "-m", *args], env=env, stdout=log, stderr=subprocess.STDOUT, cwd=ROOT)
+    cpus = _envelope_cpus()
+    if cpus is not None:
+        print(f"[start_arena] {name}: CPUs {cpus}", flush=True)
+    # affinity is set in the child before exec (the parent never initialises the GPU)
+    pre = (lambda: os.sched_setaffinity(0, cpus)) if cpus is not None else None
+    return subprocess.Popen([sys.executable, "-m", *args], env=env, stdout=log, stderr=subprocess.STDOUT, cwd=ROOT,
+                            preexec_fn=pre)
 
 
 def wait_http(url: str, timeout: float, procs) -> bool:
@@ -90,6 +114,7 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
     env = dict(os.environ, PYTHONPATH=str(ROOT), HSA_ENABLE_IPC_MODE_LEGACY="0", ARENA_DEVICE=device,
                **(extra_env or {}))
     log_dir.mkdir(parents=True, exist_ok=True)
+    _next_cpu[0] = 0  # CPU envelopes are allocated per arm
     procs = []
     if arch == "monolithic":
         procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "monolithic", "--gpus", str(gpus),
