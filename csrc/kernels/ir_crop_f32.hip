@@ -377,10 +377,10 @@ bool ir_block_crop_f32_supported(int H, int stride, int inp_pad, int hid_pad, in
 }
 
 bool ir_block_crop_f32(const IrParams& p, hipStream_t s) {
-  if (!p.x3w) return false;  // only blocks planned for this kernel carry its split-plane weights
+  if (!p.x3w) return false;  // only blocks planned for an x3 kernel carry split-plane weights
   if (p.H != p.W || p.Ho != p.Wo || !ir_block_crop_f32_supported(p.H, p.stride, p.inp_pad, p.hid_pad, p.oup_pad,
                                                                  p.expand))
-    throw std::runtime_error("ir_x3: split-plane weights for a block this kernel does not take");
+    return false;  // the tiled x3 kernel (ir_tile_x3.hip) takes it
   if (p.inp % 8 || p.oup % 4 || p.inp > p.inp_pad || p.oup > p.oup_pad || p.x_cs % 4 || p.y_cs % 4)
     throw std::runtime_error("ir_x3: unsupported channel geometry");
   if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_x3: residual needs s1, inp == oup");

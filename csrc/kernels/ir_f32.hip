@@ -389,6 +389,7 @@ void ir_f32_prepare() {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, 1, false, 1, true>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  ir_tile_x3_prepare();
 }
 
 bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand) {
@@ -420,6 +421,10 @@ void ir_block_f32(const IrParams& p, hipStream_t s) {
     return;
   }
   if (ir_block_crop_f32(p, s)) return;  // 14x14 / 7x7 maps: whole-map x3 kernel (ir_crop_f32.hip)
+  if (p.x3w) {  // split-plane weights for the tiled x3 kernel (ir_tile_x3.hip)
+    if (ir_tile_x3(p, s)) return;
+    throw std::runtime_error("ir_block_f32: split-plane weights for a block no x3 kernel takes");
+  }
   if (!ir_block_f32_supported(p.stride, p.inp_pad, p.hid_pad, p.oup_pad, p.expand) || p.inp % 4 || p.oup % 4 ||
       p.inp > p.inp_pad || p.oup > p.oup_pad || p.x_cs % 4 || p.y_cs % 4)
     throw std::runtime_error("ir_block_f32: unsupported channel geometry");

@@ -1,0 +1,324 @@
+// Fused MobileNetV2 inverted residual, fp32-accurate on the bf16 matrix cores (triple-bf16 split), for the
+// tiled 112x112 .. 28x28 stages (torchvision mobilenet_v2 features[2..7]; the reference runs them as fp32
+// ONNX per crop, architectures/monolithic/app/inference.py:196).
+//
+// Same tiling and phase structure as ir_f32.hip (one workgroup = a TH x TW output tile of one crop; per chunk
+// of 32 hidden channels: expand GEMM -> fp32 E tile in LDS -> depthwise -> project GEMM accumulate), but the
+// two GEMMs run as six v_mfma_f32_16x16x32_bf16 per operand pair on split planes (v = h + m + l exactly, see
+// conv_x3_lds_kernel) instead of v_mfma_f32_16x16x4_f32: 16 cycles per 16x16x32 step against 8 x 32 for the
+// exact fp32 instruction, 2.7x less matrix time at fp32-level error (tests/test_fp32_gpu.py, fp64 reference).
+//
+//   X: each wave loads the input pixels of its expand tiles straight from global memory into B-operand
+//      registers, split once; X never goes through LDS (ir_f32 kept a fp32 copy there);
+//   E = relu6(We[chunk] . X + be), zero outside the image        -> fp32 LDS (the depthwise reads it)
+//   D = relu6(dw3x3_S(E) + bd)                                    -> split, bf16 planes in LDS
+//   acc += Wp[:, chunk] . D                                       registers for the whole chunk loop
+//   y = acc + bp (+ x)
+// Weights: the x3w planes the planner packs for these blocks (engine/planner.py split_bf16x3): we bf16
+// [hid_pad][3][inp_pad], wp bf16 [oup_pad][3][hid_pad]; wd fp32 [9][hid_pad]; biases fp32.
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "launch.h"
+
+namespace arena {
+
+namespace {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int ITX_HC = 32;                    // hidden channels per chunk
+constexpr int ITX_DPB = 3 * ITX_HC * 2 + 32;  // bytes per D pixel row: [h|m|l][32] bf16 + pad (14 slots)
+
+__host__ __device__ constexpr int itx_ep(int S) { return S == 1 ? ITX_HC : ITX_HC + 4; }  // E pixel pitch
+
+template <int S>
+__device__ __forceinline__ int itx_eswz(int pix, int g) {
+  const int f = S == 1 ? ((pix ^ (4 * (pix >> 2))) & 7) : 0;
+  return (g & ~7) | ((g & 7) ^ f);
+}
+
+__device__ __forceinline__ void itx_split8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bf16 th = (bf16)v[i];
+    const float r = v[i] - (float)th;
+    const bf16 tm = (bf16)r;
+    h[i] = th;
+    m[i] = tm;
+    l[i] = (bf16)(r - (float)tm);
+  }
+}
+
+__device__ __forceinline__ void itx_split4(const float4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
+  const float a[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16 th = (bf16)a[i];
+    const float r = a[i] - (float)th;
+    const bf16 tm = (bf16)r;
+    h[i] = th;
+    m[i] = tm;
+    l[i] = (bf16)(r - (float)tm);
+  }
+}
+
+__device__ __forceinline__ f32x4 itx_mfma(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                          const bf16x8& bm, const bf16x8& bl, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float4 itx_relu6x4(float4 v) {
+  return make_float4(relu6f(v.x), relu6f(v.y), relu6f(v.z), relu6f(v.w));
+}
+
+}  // namespace
+
+// S: stride; TH x TW: output tile; NTO: oup_pad / 16; KS: inp_pad / 32.
+template <int S, int TH, int TW, int NTO, int KS>
+__global__ __launch_bounds__(256) void ir_tile_x3_kernel(const IrParams p) {
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
+  constexpr int PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
+  constexpr int POUT = TH * TW, MT_OUT = POUT / 16;
+  static_assert(POUT % 16 == 0, "output tile must be a multiple of 16 pixels");
+  constexpr int PAIRS = MT_OUT * NTO, PPW = (PAIRS + 3) / 4;
+  constexpr int ET = (MT_IN * 2 + 3) / 4;  // expand tiles per wave (pixel tile x hidden half)
+  constexpr int EP = itx_ep(S);
+  constexpr int INP = KS * 32;
+  extern __shared__ __attribute__((aligned(16))) uint8_t itx_lds[];
+  float* Es = (float*)itx_lds;                            // [ROWS][EP] fp32
+  uint8_t* Ds = itx_lds + ROWS * EP * sizeof(float);      // [POUT][ITX_DPB] bf16 planes
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int tiles_x = (p.Wo + TW - 1) / TW, tiles_y = (p.Ho + TH - 1) / TH;
+  const int tiles = tiles_x * tiles_y;
+  const int b = blockIdx.x / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int t = blockIdx.x - b * tiles;
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  const float* xb = (const float*)p.x + (size_t)b * p.H * p.W * p.x_cs;
+  const bf16* we = (const bf16*)p.we;
+  const bf16* wp = (const bf16*)p.wp;
+  const float* wd = (const float*)p.wd;
+  const int hid_pad = p.hid_pad;
+
+  // ---- this wave's expand tiles: tile tt = wave + 4 i covers halo pixels 16 (tt >> 1) .. +15 and hidden
+  // half tt & 1 = wave & 1; the pixels' channels are loaded once, split, and stay in registers
+  const int nt_e = wave & 1;
+  bf16x8 xh[ET][KS], xm[ET][KS], xl[ET][KS];
+  float xin[ET];  // 1: the lane's halo pixel is inside the image (the expanded map is zero-padded)
+#pragma unroll
+  for (int i = 0; i < ET; ++i) {
+    const int tt = wave + 4 * i;
+    const int r = (tt >> 1) * 16 + col;
+    const int iy = iy0 + r / PW, ix = ix0 + r % PW;
+    const bool in = tt < MT_IN * 2 && r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+    xin[i] = in ? 1.f : 0.f;
+    const float* src = xb + ((size_t)(in ? iy : 0) * p.W + (in ? ix : 0)) * p.x_cs;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ks * 32 + 8 * kq;
+      const bool ok = in && k < p.inp;
+      const float4 a = *(const float4*)(src + (ok ? k : 0)), c = *(const float4*)(src + (ok ? k + 4 : 0));
+      float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      if (!ok) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      } else if (k + 4 > p.inp) {  // inp % 8 == 4: the upper half of this 8-channel group is padding
+#pragma unroll
+        for (int j = 4; j < 8; ++j) v[j] = 0.f;
+      }
+      itx_split8(v, xh[i][ks], xm[i][ks], xl[i][ks]);
+    }
+  }
+
+  f32x4 acc[PPW];
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // expand weights of a chunk (A operand: hidden row h0 + 16 nt_e + col, k 8 kq of each 32-step), fetched one
+  // chunk ahead; project weights of a chunk (A: output row 16 nt + col, hidden k h0 + 8 kq) at the chunk start
+  u32x4 wexp[3 * KS], wnext[3 * KS];
+  float4 bexp, bnext;
+  auto load_expand = [&](int h0, u32x4 (&w)[3 * KS], float4& be) {
+    const bf16* row = we + (size_t)(h0 + nt_e * 16 + col) * 3 * INP + 8 * kq;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) w[ks * 3 + pl] = *(const u32x4*)(row + pl * INP + ks * 32);
+    be = *(const float4*)((const float*)p.be + h0 + nt_e * 16 + 4 * kq);
+  };
+  const int g = tid & 7;  // depthwise channel group (4 channels) of this thread
+  load_expand(0, wexp, bexp);
+
+  for (int h0 = 0; h0 < hid_pad; h0 += ITX_HC) {
+    if (h0 + ITX_HC < hid_pad) load_expand(h0 + ITX_HC, wnext, bnext);
+    // ---- expand: E = relu6(We . X + be) * inside, fp32 into LDS
+#pragma unroll
+    for (int i = 0; i < ET; ++i) {
+      const int tt = wave + 4 * i;
+      if (tt >= MT_IN * 2) break;
+      f32x4 e = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        e = itx_mfma(__builtin_bit_cast(bf16x8, wexp[ks * 3]), __builtin_bit_cast(bf16x8, wexp[ks * 3 + 1]),
+                     __builtin_bit_cast(bf16x8, wexp[ks * 3 + 2]), xh[i][ks], xm[i][ks], xl[i][ks], e);
+      const int pix = (tt >> 1) * 16 + col;
+      const int hc = nt_e * 16 + 4 * kq;
+      // the lane holds hidden channels hc..hc+3 of pixel `pix` (16x16 output layout); its own inside flag
+      // belongs to pixel 16 (tt >> 1) + col, the same pixel
+      const float m = xin[i];
+      const float4 v = make_float4(relu6f(e[0] + bexp.x) * m, relu6f(e[1] + bexp.y) * m,
+                                   relu6f(e[2] + bexp.z) * m, relu6f(e[3] + bexp.w) * m);
+      *(float4*)&Es[pix * EP + 4 * itx_eswz<S>(pix, hc >> 2)] = v;
+    }
+    __syncthreads();
+
+    // ---- depthwise 3x3 (stride S) + bias + ReLU6 -> split planes of D
+    {
+      float4 wk[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)(wd + (size_t)k * hid_pad + h0 + 4 * g);
+      const float4 bdw = *(const float4*)((const float*)p.bd + h0 + 4 * g);
+      for (int q = tid >> 3; q < POUT; q += 32) {
+        const int oy = q / TW, ox = q - oy * TW;
+        float4 a = bdw;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int px = (oy * S + ky) * PW + ox * S + kx;
+            const float4 v = *(const float4*)&Es[px * EP + 4 * itx_eswz<S>(px, g)];
+            const float4 w = wk[ky * 3 + kx];
+            a.x = fmaf(v.x, w.x, a.x);
+            a.y = fmaf(v.y, w.y, a.y);
+            a.z = fmaf(v.z, w.z, a.z);
+            a.w = fmaf(v.w, w.w, a.w);
+          }
+        bf16x4 dh, dm, dl;
+        itx_split4(itx_relu6x4(a), dh, dm, dl);
+        uint8_t* d = Ds + q * ITX_DPB + 8 * g;
+        *(bf16x4*)d = dh;
+        *(bf16x4*)(d + 64) = dm;
+        *(bf16x4*)(d + 128) = dl;
+      }
+    }
+    __syncthreads();
+
+    // ---- project GEMM accumulate (rows = output channels, columns = output pixels)
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int pr = wave + 4 * j;
+      if (pr >= PAIRS) break;
+      const int mt = pr / NTO, nt = pr - (pr / NTO) * NTO;
+      const bf16* wrow = wp + (size_t)(nt * 16 + col) * 3 * hid_pad + h0 + 8 * kq;
+      const bf16x8 ah = *(const bf16x8*)wrow, am = *(const bf16x8*)(wrow + hid_pad),
+                   al = *(const bf16x8*)(wrow + 2 * hid_pad);
+      const uint8_t* d = Ds + (mt * 16 + col) * ITX_DPB + 16 * kq;
+      acc[j] = itx_mfma(ah, am, al, *(const bf16x8*)d, *(const bf16x8*)(d + 64), *(const bf16x8*)(d + 128), acc[j]);
+    }
+    if (h0 + ITX_HC < hid_pad) {
+#pragma unroll
+      for (int k = 0; k < 3 * KS; ++k) wexp[k] = wnext[k];
+      bexp = bnext;
+    }
+    // no barrier here: the next chunk's expand writes E, which every wave finished reading before the
+    // barrier above, and its depthwise writes D only after the next expand barrier, which every wave reaches
+    // after this project
+  }
+
+  // ---- epilogue: + bias (+ residual) -> NHWC fp32
+  float* yb = (float*)p.y + (size_t)b * p.Ho * p.Wo * p.y_cs;
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int pr = wave + 4 * j;
+    if (pr >= PAIRS) break;
+    const int mt = pr / NTO, nt = pr - mt * NTO;
+    const int q = mt * 16 + col;
+    const int oy = oy0 + q / TW, ox = ox0 + q % TW;
+    const int co = nt * 16 + 4 * kq;
+    if (oy >= p.Ho || ox >= p.Wo || co >= p.oup) continue;
+    const float4 bp = *(const float4*)((const float*)p.bp + co);
+    float4 v = make_float4(acc[j][0] + bp.x, acc[j][1] + bp.y, acc[j][2] + bp.z, acc[j][3] + bp.w);
+    if (p.res) {
+      const float4 r = *(const float4*)(xb + ((size_t)oy * p.W + ox) * p.x_cs + co);
+      v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+    }
+    *(float4*)(yb + ((size_t)oy * p.Wo + ox) * p.y_cs + co) = v;
+  }
+}
+
+namespace {
+
+template <int S, int TH, int TW, int NTO, int KS>
+void itx_launch(const IrParams& p, hipStream_t s) {
+  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
+  constexpr int ROWS = (PH * PW + 15) / 16 * 16;
+  constexpr size_t lds = (size_t)ROWS * itx_ep(S) * 4 + (size_t)TH * TW * ITX_DPB;
+  static_assert(lds <= 160 * 1024, "ir_tile_x3: LDS budget");
+  const int tiles = ((p.Wo + TW - 1) / TW) * ((p.Ho + TH - 1) / TH);
+  hipLaunchKernelGGL((ir_tile_x3_kernel<S, TH, TW, NTO, KS>), dim3((unsigned)(p.B * tiles)), dim3(256), lds, s, p);
+}
+
+// (S, TH, TW, NTO, KS): stride-1 blocks on 8 x 16 tiles, stride-2 blocks on 4 x 8 tiles (as ir_f32.hip)
+#define ITX_CONFIGS(X) \
+  X(1, 8, 16, 1, 1)    \
+  X(1, 8, 16, 2, 1)    \
+  X(1, 8, 16, 4, 1)    \
+  X(1, 8, 16, 2, 2)    \
+  X(1, 8, 16, 4, 2)    \
+  X(2, 4, 8, 1, 1)     \
+  X(2, 4, 8, 2, 1)     \
+  X(2, 4, 8, 4, 1)     \
+  X(2, 4, 8, 4, 2)
+
+}  // namespace
+
+// Shapes this kernel takes (mirrored by engine/validate.py::ir_tile_x3_supported): expanding blocks with
+// inp_pad 32 / 64, hid_pad a multiple of 32 and oup_pad 16 / 32 / 64 (stride-2: 16 .. 64, and 64 with inp 64).
+bool ir_tile_x3_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand) {
+  if (!expand || hid_pad % ITX_HC) return false;
+#define X(S_, TH_, TW_, NTO_, KS_) \
+  if (stride == S_ && oup_pad == NTO_ * 16 && inp_pad == KS_ * 32) return true;
+  ITX_CONFIGS(X)
+#undef X
+  return false;
+}
+
+void ir_tile_x3_prepare() {
+#define X(S_, TH_, TW_, NTO_, KS_)                                                                       \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_tile_x3_kernel<S_, TH_, TW_, NTO_, KS_>,           \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  ITX_CONFIGS(X)
+#undef X
+}
+
+bool ir_tile_x3(const IrParams& p, hipStream_t s) {
+  if (!ir_tile_x3_supported(p.stride, p.inp_pad, p.hid_pad, p.oup_pad, p.expand)) return false;
+  if (p.inp % 4 || p.oup % 4 || p.inp > p.inp_pad || p.oup > p.oup_pad || p.x_cs % 4 || p.y_cs % 4)
+    throw std::runtime_error("ir_tile_x3: unsupported channel geometry");
+  if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_tile_x3: residual needs s1, inp == oup");
+  if (p.Ho != (p.H + 2 - 3) / p.stride + 1 || p.Wo != (p.W + 2 - 3) / p.stride + 1)
+    throw std::runtime_error("ir_tile_x3: output size mismatch");
+  if (p.B <= 0) return true;
+#define X(S_, TH_, TW_, NTO_, KS_)                                                  \
+  if (p.stride == S_ && p.oup_pad == NTO_ * 16 && p.inp_pad == KS_ * 32) {          \
+    itx_launch<S_, TH_, TW_, NTO_, KS_>(p, s);                                      \
+    return true;                                                                    \
+  }
+  ITX_CONFIGS(X)
+#undef X
+  return false;
+}
+
+}  // namespace arena

@@ -151,6 +151,10 @@ bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, i
 // MFMA); ir_block_f32 dispatches blocks with split-plane weights (x3w, set by the planner) to it.
 bool ir_block_crop_f32(const IrParams& p, hipStream_t s);
 bool ir_block_crop_f32_supported(int H, int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
+// Tiled fp32-accurate x3 block for the >= 28x28 stages (csrc/kernels/ir_tile_x3.hip), also behind x3w
+bool ir_tile_x3(const IrParams& p, hipStream_t s);
+bool ir_tile_x3_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
+void ir_tile_x3_prepare();
 void ir_prepare();
 void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole-crop tile
 void set_ir_crop(bool v);

@@ -255,6 +255,28 @@ def ir_crop_f32_enabled() -> bool:
     return ir_crop_f32_policy() != "none"
 
 
+def ir_tile_x3_enabled() -> bool:
+    """``ARENA_IR_X3T`` (default 1): fp32 programs run the expanding MobileNetV2 blocks of the >= 28x28 stages on
+    the tiled x3 kernel (csrc/kernels/ir_tile_x3.hip, split-plane weights) instead of the exact-fp32 ir_f32
+    kernel; 0 restores ir_f32 (A/B switch)."""
+    return os.environ.get("ARENA_IR_X3T", "1").lower() not in ("0", "false", "no", "off")
+
+
+def ir_x3_plan(H: int, W: int, stride: int, inp: int, hid_pad: int, oup_pad: int, expand: int) -> tuple[int, int]:
+    """fp32 block -> (x3w, inp_pad): 1 with the 32-aligned input padding of the x3 kernels when the whole-map
+    (14x14 / 7x7) or the tiled x3 kernel takes the block, else (0, the exact-fp32 16-aligned padding)."""
+    from .validate import ir_tile_x3_supported
+
+    inp16, inp32 = _round(inp, 16), _round(inp, 32)
+    if H == W and ir_crop_f32_planned(H, stride, inp16, hid_pad, oup_pad, expand):
+        return 1, inp16
+    # an input that would be half zero padding in the 32-deep x3 K step (MobileNetV2 block 2, 16 channels)
+    # stays on ir_f32: 238 vs 215 us per batch of 32 requests (profiles/r3_fp32_itx_ops.md)
+    if ir_tile_x3_enabled() and inp16 == inp32 and ir_tile_x3_supported(stride, inp32, hid_pad, oup_pad, expand):
+        return 1, inp32
+    return 0, inp16
+
+
 def ir_crop_f32_planned(H: int, stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
     from .validate import ir_crop_f32_supported
 
@@ -390,8 +412,13 @@ class ProgramBuilder:
         mat = f32 if self.f32 else bf16_bytes  # exact-fp32 programs keep fp32 weights
         H, W = src.buf.H, src.buf.W
         # fp32 14x14 / 7x7 blocks: whole-map kernel with pre-split [h|m|l] bf16 expand / project weights
-        x3w = int(self.f32 and H == W and ir_crop_f32_planned(H, stride, inp_pad, hid_pad, oup_pad,
-                                                              int(expand is not None)))
+        x3w = 0
+        if self.f32:
+            x3w, inp_x3 = ir_x3_plan(H, W, stride, inp, hid_pad, oup_pad, int(expand is not None))
+            if x3w and inp_x3 != inp_pad:  # the x3 kernels step K by 32
+                pk = pack_ir_weights(expand, dw, project, src.C, k_align=32)
+                inp, inp_pad, hid_pad, oup, oup_pad = pk["inp"], pk["inp_pad"], pk["hid_pad"], pk["oup"], \
+                    pk["oup_pad"]
         mat_x3 = (lambda t: bf16_raw_bytes(split_bf16x3(t))) if x3w else mat  # noqa: E731
         offs = [self.weights.add(mat_x3(pk["we"])), self.weights.add(f32(pk["be"])),
                 self.weights.add(mat(pk["wd"])), self.weights.add(f32(pk["bd"])),

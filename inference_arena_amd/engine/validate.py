@@ -69,6 +69,16 @@ IR_CROP_F32_CONFIGS = {(14, 1, 64, 64), (14, 1, 64, 96), (14, 1, 96, 96), (7, 2,
                        (7, 1, 160, 320)}
 
 
+# (stride, oup_pad, inp_pad) of csrc/kernels/ir_tile_x3.hip ITX_CONFIGS
+IR_TILE_X3_CONFIGS = {(1, 16, 32), (1, 32, 32), (1, 64, 32), (1, 32, 64), (1, 64, 64), (2, 16, 32), (2, 32, 32),
+                      (2, 64, 32), (2, 64, 64)}
+
+
+def ir_tile_x3_supported(stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
+    """Mirror of arena::ir_tile_x3_supported (tiled x3 block kernel for the >= 28x28 stages)."""
+    return bool(expand) and hid_pad % 32 == 0 and (stride, oup_pad, inp_pad) in IR_TILE_X3_CONFIGS
+
+
 def ir_crop_f32_supported(H: int, stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
     """Mirror of arena::ir_block_crop_f32_supported (whole-map x3 kernel for the 14x14 / 7x7 stages)."""
     Ho = (H - 1) // stride + 1
@@ -172,8 +182,9 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             x3w = int(r[26])
             if any(int(v) for v in r[27:31]):
                 raise ProgramError(f"op {i}: ir_block fields 27-30 are reserved (0)")
-            if x3w and not (f32 and H == W and ir_crop_f32_supported(H, S, inp_pad, hid_pad, oup_pad, int(r[12]))):
-                raise ProgramError(f"op {i}: split-plane weights for a block the whole-map kernel does not take")
+            if x3w and not (f32 and ((H == W and ir_crop_f32_supported(H, S, inp_pad, hid_pad, oup_pad, int(r[12])))
+                                     or ir_tile_x3_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])))):
+                raise ProgramError(f"op {i}: split-plane weights for a block no x3 kernel takes")
             if f32 and not x3w and not ir_f32_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])):
                 raise ProgramError(f"op {i}: no fp32 fused kernel for this block")
             if Ho != (H - 1) // S + 1 or Wo != (W - 1) // S + 1:

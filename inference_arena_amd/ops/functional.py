@@ -103,16 +103,19 @@ def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: boo
                   bdev: torch.Tensor | None = None) -> torch.Tensor:
     """Fused MobileNetV2 inverted residual (expand 1x1+ReLU6 -> dw3x3+ReLU6 -> project 1x1 [+x]).
     ``expand``/``dw``/``project`` are (weight, bias) pairs with BN folded; ``expand`` None for t=1."""
-    from ..engine.planner import ir_crop_f32_planned, pack_ir_weights, split_bf16x3
+    from ..engine.planner import ir_x3_plan, pack_ir_weights, split_bf16x3
 
     B, H, W, C = x.shape
-    f32 = x.dtype == torch.float32  # exact-fp32 kernels (csrc/kernels/ir_f32.hip, ir_crop_f32.hip)
+    f32 = x.dtype == torch.float32  # fp32 kernels (csrc/kernels/ir_f32.hip, ir_crop_f32.hip, ir_tile_x3.hip)
     pk = pack_ir_weights(expand, dw, project, C, k_align=16 if f32 else 32)
+    x3w = 0
+    if f32:
+        x3w, inp_x3 = ir_x3_plan(H, W, stride, C, pk["hid_pad"], pk["oup_pad"], int(expand is not None))
+        if x3w and inp_x3 != pk["inp_pad"]:
+            pk = pack_ir_weights(expand, dw, project, C, k_align=32)
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     y = torch.empty(B, Ho, Wo, pk["oup"], dtype=x.dtype, device=x.device)
     mat = torch.float32 if f32 else torch.bfloat16
-    x3w = int(f32 and H == W and ir_crop_f32_planned(H, stride, pk["inp_pad"], pk["hid_pad"], pk["oup_pad"],
-                                                     int(expand is not None)))
     dev = {k: (pk[k].to(mat) if k in ("we", "wd", "wp") else pk[k].float()).contiguous().to(x.device)
            for k in ("we", "be", "wd", "bd", "wp", "bp")}
     if x3w:  # the whole-map kernel reads pre-split [h|m|l] bf16 expand / project weights

@@ -435,7 +435,8 @@ def _ir_ref64(x, expand, dw, project, stride, res):
 
 @pytest.mark.parametrize("inp,hid,oup,stride,H,res", [
     (32, 32, 16, 1, 40, False),    # t = 1 block (no expand), MobileNetV2 block 1 geometry
-    (16, 96, 24, 2, 37, False),    # block 2: 16 -> 24, stride 2, odd size
+    (16, 96, 24, 2, 37, False),    # block 2: 16 -> 24, stride 2, odd size (ir_f32 either way)
+    (32, 96, 24, 2, 37, False),    # stride 2 with a full 32-channel input (the x3 tile kernel)
     (24, 144, 24, 1, 28, True),    # block 3 (hid 144 -> 160 padded chunks), residual
     (24, 144, 32, 2, 28, False),   # block 4
     (32, 192, 32, 1, 28, True),    # block 5/6
@@ -448,9 +449,13 @@ def _ir_ref64(x, expand, dw, project, stride, res):
     (160, 960, 160, 1, 7, True),   # blocks 15-16
     (160, 960, 320, 1, 7, False),  # block 17
 ])
-def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, monkeypatch):
+@pytest.mark.parametrize("x3t", ["1", "0"])  # >= 28x28 expanding blocks: tiled x3 kernel / exact-fp32 ir_f32
+def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, x3t, monkeypatch):
     if H <= 14:  # the whole-map kernel is opt-in for programs; the wrapper takes it when enabled
+        if x3t == "0":
+            pytest.skip("ARENA_IR_X3T does not apply to the whole-map kernel")
         monkeypatch.setenv("ARENA_IRC_F32", "1")
+    monkeypatch.setenv("ARENA_IR_X3T", x3t)
     g = torch.Generator().manual_seed(inp * 7 + hid + stride)
     x = torch.randn(3, inp, H, H, generator=g)
     expand = None if hid == inp else (torch.randn(hid, inp, 1, 1, generator=g) / inp ** 0.5,
@@ -470,10 +475,12 @@ def test_fp32_program_fuses_the_high_resolution_blocks():
 
     p = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype="fp32")
     ir = [o for o in p.ops if int(o[0]) == 14]
-    # block 1 fused with crop gather + stem (ir_f32.hip stem mode), >= 28x28: ir_f32.hip tile kernel,
-    # stride-1 14x14: the x3 whole-map kernel (ir_crop_f32.hip); 14 -> 7 and 7x7 blocks run unfused
+    # block 1 fused with crop gather + stem (ir_f32.hip stem mode), >= 28x28: the tiled x3 kernel
+    # (ir_tile_x3.hip, split-plane weights), stride-1 14x14: the x3 whole-map kernel (ir_crop_f32.hip);
+    # 14 -> 7 and 7x7 blocks run unfused
     assert [(int(o[4]), int(o[26]), int(o[31])) for o in ir] == \
-        [(112, 0, 1), (112, 0, 0), (56, 0, 0), (56, 0, 0), (28, 0, 0), (28, 0, 0), (28, 0, 0)] + [(14, 1, 0)] * 6
+        [(112, 0, 1), (112, 0, 0), (56, 1, 0), (56, 1, 0), (28, 1, 0), (28, 1, 0), (28, 1, 0)] + [(14, 1, 0)] * 6
+    assert all(int(o[7]) % 32 == 0 for o in ir if int(o[26]))  # x3 kernels step K by 32
     assert not [o for o in p.ops if int(o[0]) == 9]  # no separate crop gather
     assert all(int(o[47]) == 1 for o in p.ops)
 

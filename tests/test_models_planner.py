@@ -260,7 +260,8 @@ def test_fp32_program_with_whole_map_ir_blocks_validates(monkeypatch):
     prog = plans.plan_pipeline(y, m, conf_thr=0.5, iou_thr=0.45, dtype="fp32")
     ir = [o for o in prog.ops if int(o[0]) == OP_IRBLOCK]
     assert [int(o[4]) for o in ir] == [112, 112, 56, 56, 28, 28, 28] + [14] * 7 + [7] * 3
-    assert [int(o[26]) for o in ir] == [0] * 7 + [1] * 10
+    # block 1 (stem-fused, exact fp32) has no split weights; the >= 28x28 blocks take the tiled x3 kernel
+    assert [int(o[26]) for o in ir] == [0, 0] + [1] * 15
     for B in (1, 32):
         validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)
 

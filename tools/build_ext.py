@@ -34,6 +34,7 @@ SOURCES = [
     "kernels/gemm_x3.hip",
     "kernels/ir_f32.hip",
     "kernels/ir_crop_f32.hip",
+    "kernels/ir_tile_x3.hip",
     "kernels/dwconv.hip",
     "kernels/ir_block.hip",
     "kernels/ir_block_wave.hip",
