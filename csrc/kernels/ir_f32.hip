@@ -417,7 +417,7 @@ static void ir_stem_f32(const IrParams& p, hipStream_t s) {
 
 void ir_block_f32(const IrParams& p, hipStream_t s) {
   if (p.stem) {
-    ir_stem_f32(p, s);
+    if (!ir_stem_x3(p, s)) ir_stem_f32(p, s);  // x3w: the split-plane kernel (ir_tile_x3.hip)
     return;
   }
   if (ir_block_crop_f32(p, s)) return;  // 14x14 / 7x7 maps: whole-map x3 kernel (ir_crop_f32.hip)

@@ -22,6 +22,7 @@
 
 #include "common.h"
 #include "launch.h"
+#include "letterbox.h"
 
 namespace arena {
 
@@ -258,6 +259,169 @@ __global__ __launch_bounds__(256) void ir_tile_x3_kernel(const IrParams p) {
   }
 }
 
+
+// Classifier front end on the same operand scheme (IrParams.stem with x3w): crop gather + ImageNet
+// normalisation into a space-to-depth tile (split planes in LDS), the 2x2 stem conv (32 <- 4 taps x 16 channels)
+// as x3 MFMAs -> fp32 X (+ bias, ReLU6, zero outside the 112 x 112 map), MobileNetV2 block 1 (t = 1: depthwise 32
+// + ReLU6 on X, project 32 -> 16 as x3 MFMAs).  ir_f32.hip's stem mode ran both GEMMs on v_mfma_f32_16x16x4_f32:
+// the stem conv over the 1.41x halo alone was ~110 us of matrix time per batch of 32 requests.
+// Weights: st_w bf16 [32][3][64] (k = tap * 16 + channel), wp bf16 [16][3][32], wd fp32 [9][32], biases fp32.
+__global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
+  constexpr int S = 1, TH = 8, TW = 16;
+  constexpr int PH = TH + 2, PW = TW + 2, PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
+  constexpr int POUT = TH * TW, MT_OUT = POUT / 16;
+  constexpr int PAIRS = MT_OUT, PPW = (PAIRS + 3) / 4;  // one 16-channel output tile
+  constexpr int ET = (MT_IN * 2 + 3) / 4;
+  constexpr int XP = 32;                              // X pixel pitch (fp32): the depthwise input
+  constexpr int SH = PH + 1, SW = PW + 1, SPB = 96;   // s2d tile: [pixel][h 16 | m 16 | l 16] bf16
+  static_assert(SH * SW * SPB <= POUT * ITX_DPB, "s2d tile must fit the D region");
+  extern __shared__ __attribute__((aligned(16))) uint8_t itx_lds[];
+  float* Xs = (float*)itx_lds;                        // [ROWS][XP] fp32, swizzled 4-channel groups
+  uint8_t* Ds = itx_lds + ROWS * XP * sizeof(float);  // [POUT][ITX_DPB] bf16 planes (first: the s2d tile)
+  uint8_t* Ss = Ds;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kq = lane >> 4;
+  const int tiles_x = (p.Wo + TW - 1) / TW, tiles_y = (p.Ho + TH - 1) / TH;
+  const int tiles = tiles_x * tiles_y;
+  const int b = blockIdx.x / tiles;
+  if (b >= live_batch(p.B, p.bdev)) return;
+  const int t = blockIdx.x - b * tiles;
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+
+  // ---- A1: crop gather -> s2d tile (origin (iy0 - 1, ix0 - 1): the 2x2 stem conv pads top / left by one),
+  // each pixel exactly as crop_gather_s2d_kernel<float> computes it, split into planes
+  {
+    const int S2 = p.st_S >> 1;
+    const CropRef cr = p.st_crops[(p.st_ctrl != nullptr ? p.st_ctrl->crop_base : 0) + b];
+    const ImageMeta m = p.st_meta[cr.img];
+    const int cw = cr.x2 - cr.x1, chh = cr.y2 - cr.y1;
+    const bool empty = cw <= 0 || chh <= 0;
+    const float sx = empty ? 1.f : (float)((double)cw / (double)p.st_S);
+    const float sy = empty ? 1.f : (float)((double)chh / (double)p.st_S);
+    const uint8_t* img = p.st_pool + m.offset + ((size_t)cr.y1 * m.w + cr.x1) * 3;
+    for (int i = tid; i < SH * SW; i += 256) {
+      const int Y = iy0 - 1 + i / SW, X = ix0 - 1 + i % SW;
+      float out[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) out[k] = 0.f;
+      if ((unsigned)Y < (unsigned)S2 && (unsigned)X < (unsigned)S2) {
+#pragma unroll
+        for (int pq = 0; pq < 4; ++pq) {
+          const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
+          float rgb[3] = {0.f, 0.f, 0.f};
+          if (!empty) bilinear_rgb(img, m.w, lin_tap(oy, sy, chh), lin_tap(ox, sx, cw), rgb);
+#pragma unroll
+          for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (div255<float>(rgb[c]) - p.st_mean[c]) * p.st_inv_std[c];
+        }
+      }
+      bf16x8 h0, m0, l0, h1, m1, l1;
+      itx_split8(out, h0, m0, l0);
+      itx_split8(out + 8, h1, m1, l1);
+      uint8_t* d = Ss + i * SPB;
+      *(bf16x8*)d = h0;
+      *(bf16x8*)(d + 16) = h1;
+      *(bf16x8*)(d + 32) = m0;
+      *(bf16x8*)(d + 48) = m1;
+      *(bf16x8*)(d + 64) = l0;
+      *(bf16x8*)(d + 80) = l1;
+    }
+  }
+  __syncthreads();
+
+  // ---- A2: X = relu6(stem(s2d) + b) over the halo tile (x3 MFMAs, K = 2 steps of 32), zero outside the map
+  {
+    const int nt = wave & 1;  // this wave's 16 stem output channels
+    const bf16* wrow = (const bf16*)p.st_w + (size_t)(nt * 16 + col) * 3 * 64 + 8 * kq;
+    u32x4 ws[6];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) ws[ks * 3 + pl] = *(const u32x4*)(wrow + pl * 64 + ks * 32);
+    const float4 bb = *(const float4*)(p.st_b + nt * 16 + 4 * kq);
+#pragma unroll
+    for (int i = 0; i < ET; ++i) {
+      const int tt = wave + 4 * i;
+      if (tt >= MT_IN * 2) break;
+      const int r = (tt >> 1) * 16 + col;
+      const int rr = r < PIN ? r : 0;
+      const int ry = rr / PW, rx = rr - (rr / PW) * PW;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int tap = ks * 2 + (kq >> 1);
+        const uint8_t* sp = Ss + ((ry + (tap >> 1)) * SW + rx + (tap & 1)) * SPB + (kq & 1) * 16;
+        acc = itx_mfma(__builtin_bit_cast(bf16x8, ws[ks * 3]), __builtin_bit_cast(bf16x8, ws[ks * 3 + 1]),
+                       __builtin_bit_cast(bf16x8, ws[ks * 3 + 2]), *(const bf16x8*)sp, *(const bf16x8*)(sp + 32),
+                       *(const bf16x8*)(sp + 64), acc);
+      }
+      // lane (col, kq) holds stem channels 16 nt + 4 kq .. +3 of halo pixel r
+      const int co = nt * 16 + 4 * kq;
+      const int iy = iy0 + ry, ix = ix0 + rx;
+      const bool in = r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      const float4 v = in ? itx_relu6x4(make_float4(acc[0] + bb.x, acc[1] + bb.y, acc[2] + bb.z, acc[3] + bb.w))
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      *(float4*)&Xs[r * XP + 4 * itx_eswz<S>(r, co >> 2)] = v;
+    }
+  }
+  __syncthreads();  // X complete; the s2d tile is dead (its space becomes D)
+
+  // ---- depthwise 3x3 on X (t = 1: X is the hidden map) + bias + ReLU6 -> split planes of D
+  {
+    const int g = tid & 7;
+    const float* wd = (const float*)p.wd;
+    float4 wk[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)(wd + (size_t)k * 32 + 4 * g);
+    const float4 bdw = *(const float4*)((const float*)p.bd + 4 * g);
+    for (int q = tid >> 3; q < POUT; q += 32) {
+      const int oy = q / TW, ox = q - oy * TW;
+      float4 a = bdw;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int px = (oy + ky) * PW + ox + kx;
+          const float4 v = *(const float4*)&Xs[px * XP + 4 * itx_eswz<S>(px, g)];
+          const float4 w = wk[ky * 3 + kx];
+          a.x = fmaf(v.x, w.x, a.x);
+          a.y = fmaf(v.y, w.y, a.y);
+          a.z = fmaf(v.z, w.z, a.z);
+          a.w = fmaf(v.w, w.w, a.w);
+        }
+      bf16x4 dh, dm, dl;
+      itx_split4(itx_relu6x4(a), dh, dm, dl);
+      uint8_t* d = Ds + q * ITX_DPB + 8 * g;
+      *(bf16x4*)d = dh;
+      *(bf16x4*)(d + 64) = dm;
+      *(bf16x4*)(d + 128) = dl;
+    }
+  }
+  __syncthreads();
+
+  // ---- project 32 -> 16 (x3 MFMAs) + bias -> NHWC fp32
+  const bf16* wrow = (const bf16*)p.wp + (size_t)col * 3 * 32 + 8 * kq;
+  const bf16x8 ah = *(const bf16x8*)wrow, am = *(const bf16x8*)(wrow + 32), al = *(const bf16x8*)(wrow + 64);
+  float* yb = (float*)p.y + (size_t)b * p.Ho * p.Wo * p.y_cs;
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int mt = wave + 4 * j;
+    if (mt >= PAIRS) break;
+    const uint8_t* d = Ds + (mt * 16 + col) * ITX_DPB + 16 * kq;
+    const f32x4 acc = itx_mfma(ah, am, al, *(const bf16x8*)d, *(const bf16x8*)(d + 64), *(const bf16x8*)(d + 128),
+                               f32x4{0.f, 0.f, 0.f, 0.f});
+    const int q = mt * 16 + col;
+    const int oy = oy0 + q / TW, ox = ox0 + q % TW;
+    const int co = 4 * kq;
+    if (oy >= p.Ho || ox >= p.Wo || co >= p.oup) continue;
+    const float4 bp = *(const float4*)((const float*)p.bp + co);
+    *(float4*)(yb + ((size_t)oy * p.Wo + ox) * p.y_cs + co) =
+        make_float4(acc[0] + bp.x, acc[1] + bp.y, acc[2] + bp.z, acc[3] + bp.w);
+  }
+}
+
 namespace {
 
 template <int S, int TH, int TW, int NTO, int KS>
@@ -295,7 +459,24 @@ bool ir_tile_x3_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int
   return false;
 }
 
+constexpr size_t kStemX3Lds = (size_t)((10 * 18 + 15) / 16 * 16) * 32 * 4 + (size_t)8 * 16 * ITX_DPB;
+
+bool ir_stem_x3(const IrParams& p, hipStream_t s) {
+  if (!p.stem || !p.x3w) return false;
+  if (p.stride != 1 || p.expand || p.res || p.inp != 32 || p.inp_pad != 32 || p.hid_pad != 32 || p.oup_pad != 16 ||
+      p.oup > 16 || p.oup % 4 || p.H != p.W || p.H * 2 != p.st_S || p.Ho != p.H || p.Wo != p.W || p.W < 16 ||
+      p.y_cs % 4 || p.st_w == nullptr || p.st_b == nullptr || p.st_crops == nullptr || p.st_meta == nullptr ||
+      p.st_pool == nullptr)
+    throw std::runtime_error("ir_stem_x3: unsupported geometry (needs MobileNetV2 block 1 at S/2 x S/2)");
+  if (p.B <= 0) return true;
+  const int tiles = ((p.Wo + 15) / 16) * ((p.Ho + 7) / 8);
+  hipLaunchKernelGGL(ir_stem_x3_kernel, dim3((unsigned)(p.B * tiles)), dim3(256), kStemX3Lds, s, p);
+  return true;
+}
+
 void ir_tile_x3_prepare() {
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_stem_x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
 #define X(S_, TH_, TW_, NTO_, KS_)                                                                       \
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_tile_x3_kernel<S_, TH_, TW_, NTO_, KS_>,           \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));

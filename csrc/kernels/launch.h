@@ -155,6 +155,7 @@ bool ir_block_crop_f32_supported(int H, int stride, int inp_pad, int hid_pad, in
 bool ir_tile_x3(const IrParams& p, hipStream_t s);
 bool ir_tile_x3_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
 void ir_tile_x3_prepare();
+bool ir_stem_x3(const IrParams& p, hipStream_t s);  // IrParams.stem with x3w: split-plane stem / project weights
 void ir_prepare();
 void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole-crop tile
 void set_ir_crop(bool v);

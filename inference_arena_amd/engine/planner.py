@@ -262,6 +262,13 @@ def ir_tile_x3_enabled() -> bool:
     return os.environ.get("ARENA_IR_X3T", "1").lower() not in ("0", "false", "no", "off")
 
 
+def stem_x3_enabled() -> bool:
+    """``ARENA_STEM_X3`` (default 1): the fp32 classifier front end (crop gather + stem conv + block 1) runs its
+    two GEMMs as x3 MFMAs (csrc/kernels/ir_tile_x3.hip ir_stem_x3_kernel); 0 keeps ir_f32.hip's exact-fp32
+    stem mode (A/B switch)."""
+    return os.environ.get("ARENA_STEM_X3", "1").lower() not in ("0", "false", "no", "off")
+
+
 def ir_x3_plan(H: int, W: int, stride: int, inp: int, hid_pad: int, oup_pad: int, expand: int) -> tuple[int, int]:
     """fp32 block -> (x3w, inp_pad): 1 with the 32-aligned input padding of the x3 kernels when the whole-map
     (14x14 / 7x7) or the tiled x3 kernel takes the block, else (0, the exact-fp32 16-aligned padding)."""
@@ -442,14 +449,19 @@ class ProgramBuilder:
             raise ValueError("ir_block_stem: needs a [32,16,2,2] s2d stem, a 32-channel t = 1 block and <= 16 outputs")
         pk = pack_ir_weights(None, dw, project, 32, k_align=16)
         f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
-        offs = [self.weights.add(f32(pk["we"])), self.weights.add(f32(pk["be"])), self.weights.add(f32(pk["wd"])),
-                self.weights.add(f32(pk["bd"])), self.weights.add(f32(pk["wp"])), self.weights.add(f32(pk["bp"]))]
+        # x3w: stem and project weights as split bf16 planes for csrc/kernels/ir_tile_x3.hip (ARENA_STEM_X3)
+        x3w = int(stem_x3_enabled())
+        mat_x3 = (lambda t: bf16_raw_bytes(split_bf16x3(t.float()))) if x3w else f32  # noqa: E731
+        offs = [self.weights.add(mat_x3(pk["we"])), self.weights.add(f32(pk["be"])), self.weights.add(f32(pk["wd"])),
+                self.weights.add(f32(pk["bd"])), self.weights.add(mat_x3(pk["wp"])), self.weights.add(f32(pk["bp"]))]
         wsb, bsb, kpad, cpad = pack_conv_weight(ws, bs, "fp32")
         if kpad != 64 or cpad != 32:
             raise ValueError("ir_block_stem: stem weights must pack to [32][64]")
+        if x3w:
+            wsb = mat_x3(torch.frombuffer(bytearray(wsb), dtype=torch.float32).reshape(32, 64))
         H = S // 2
         rec = [OP_IRBLOCK, BUF_NONE, 0, 0, H, H, 32, pk["inp_pad"], pk["hid_pad"], pk["oup"], pk["oup_pad"], 1, 0, 0,
-               *offs, dst.bid, dst.coff, dst.cs, H, H, kind, 0, 0, 0, 0, 0,
+               *offs, dst.bid, dst.coff, dst.cs, H, H, kind, x3w, 0, 0, 0, 0,
                1, crops.id, S] + [fbits(m) for m in mean] + [fbits(1.0 / s) for s in std] + \
               [self.weights.add(wsb), self.weights.add(bsb)]
         self._emit(rec, dst, crops)

@@ -182,7 +182,8 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             x3w = int(r[26])
             if any(int(v) for v in r[27:31]):
                 raise ProgramError(f"op {i}: ir_block fields 27-30 are reserved (0)")
-            if x3w and not (f32 and ((H == W and ir_crop_f32_supported(H, S, inp_pad, hid_pad, oup_pad, int(r[12])))
+            if x3w and not (f32 and (int(r[31]) or (H == W and ir_crop_f32_supported(H, S, inp_pad, hid_pad, oup_pad,
+                                                                                      int(r[12])))
                                      or ir_tile_x3_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])))):
                 raise ProgramError(f"op {i}: split-plane weights for a block no x3 kernel takes")
             if f32 and not x3w and not ir_f32_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])):
@@ -196,7 +197,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                         and hid_pad == 32 and oup_pad == 16 and H == W and 2 * H == int(r[33]) and int(r[25]) == CROPS):
                     raise ProgramError(f"op {i}: unsupported fused stem + block geometry")
                 need(i, r[32], 0, B * max_det * CROP_BYTES, "stem crop refs")
-                weights(i, int(r[40]), 32 * 64 * 4, "stem weight")
+                weights(i, int(r[40]), 32 * 64 * (6 if x3w else 4), "stem weight")
                 weights(i, int(r[41]), 32 * 4, "stem bias")
             else:
                 view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, el, "ir input")

@@ -479,7 +479,7 @@ def test_fp32_program_fuses_the_high_resolution_blocks():
     # (ir_tile_x3.hip, split-plane weights), stride-1 14x14: the x3 whole-map kernel (ir_crop_f32.hip);
     # 14 -> 7 and 7x7 blocks run unfused
     assert [(int(o[4]), int(o[26]), int(o[31])) for o in ir] == \
-        [(112, 0, 1), (112, 0, 0), (56, 1, 0), (56, 1, 0), (28, 1, 0), (28, 1, 0), (28, 1, 0)] + [(14, 1, 0)] * 6
+        [(112, 1, 1), (112, 0, 0), (56, 1, 0), (56, 1, 0), (28, 1, 0), (28, 1, 0), (28, 1, 0)] + [(14, 1, 0)] * 6
     assert all(int(o[7]) % 32 == 0 for o in ir if int(o[26]))  # x3 kernels step K by 32
     assert not [o for o in p.ops if int(o[0]) == 9]  # no separate crop gather
     assert all(int(o[47]) == 1 for o in p.ops)

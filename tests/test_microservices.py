@@ -310,8 +310,10 @@ def test_native_handler_drains_in_flight_requests_on_stop():
     from inference_arena_amd.server.schemas import PredictResponse
 
     app = FastAPI()
+    entered = threading.Event()
 
     async def slow_predict(data: bytes):
+        entered.set()
         await asyncio.sleep(0.6)
         return PredictResponse(request_id="r", detections=[], timing={"total_ms": 600.0})
 
@@ -328,7 +330,7 @@ def test_native_handler_drains_in_flight_requests_on_stop():
 
     th = threading.Thread(target=client)
     th.start()
-    time.sleep(0.25)  # the request is inside slow_predict
+    assert entered.wait(20)  # the request is inside slow_predict (not a fixed sleep: loaded CI machines)
     loop.call_soon_threadsafe(box["stop"].set)
     time.sleep(0.15)
     with pytest.raises(OSError):  # drained: the port no longer accepts

@@ -261,7 +261,7 @@ def test_fp32_program_with_whole_map_ir_blocks_validates(monkeypatch):
     ir = [o for o in prog.ops if int(o[0]) == OP_IRBLOCK]
     assert [int(o[4]) for o in ir] == [112, 112, 56, 56, 28, 28, 28] + [14] * 7 + [7] * 3
     # block 1 (stem-fused, exact fp32) has no split weights; the >= 28x28 blocks take the tiled x3 kernel
-    assert [int(o[26]) for o in ir] == [0, 0] + [1] * 15
+    assert [int(o[26]) for o in ir] == [1, 0] + [1] * 15  # block 1: x3 stem kernel; block 2: exact fp32
     for B in (1, 32):
         validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)
 
