@@ -20,8 +20,8 @@ architectures/monolithic/app/main.py:102-159):
 * precision: ``--dtype fp32`` (default) runs the fp32-accurate kernels, the reference's fp32 ONNX
   Runtime numerics (reference experiment.yaml:202,207,220,225); ``bf16`` the tuned bf16 kernels.
 * steady state: the clients run continuously from the warm-up into the timed window, so the window
-  contains no pipeline fill or drain.  A "step" is ``--step-batches`` (8) dynamic batches of
-  ``--batch`` (32) = 256 completed requests: ``--warmup`` steps complete untimed, then a barrier +
+  contains no pipeline fill or drain.  A "step" is ``--step-batches`` (32) dynamic batches of
+  ``--batch`` (32) = 1024 completed requests: ``--warmup`` steps complete untimed, then a barrier +
   device sync open the window, the window closes (device sync + barrier) once exactly ``--steps`` more
   steps have completed on the rank.  ``value`` = steps * requests per step * world / max-over-ranks
   window.  P50/P99 are per-request end-to-end latencies of the requests completed in the window.
@@ -347,7 +347,9 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--min-warmup-s", type=float, default=2.0, help="minimum warm-up time of the closed loop")
     ap.add_argument("--batch", type=int, default=32, help="dynamic batcher max_batch")
-    ap.add_argument("--step-batches", type=int, default=8, help="batches of --batch requests per step")
+    ap.add_argument("--step-batches", type=int, default=32,
+                    help="batches of --batch requests per step (32 x 32 = 1024 requests: ~0.1 s per step, so the "
+                         "timed window is seconds rather than a fraction of one)")
     # 256: enough requests in flight that every dynamic batch is full (4 staging slots x 32 on the device plus
     # the decode pipeline); 192 left the batcher short (mean batch 30.5: 7.0k vs 7.5k req/s, P50 25 vs 33 ms;
     # profiles/r2_final_bench_20steps.json vs r2_bench_users256.json)

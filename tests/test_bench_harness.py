@@ -17,7 +17,8 @@ ROOT = Path(__file__).resolve().parents[1]
 def _bench(*args, env=None):
     e = dict(os.environ, ARENA_DIST_BACKEND="gloo", PYTHONPATH=str(ROOT), **(env or {}))
     return subprocess.run([sys.executable, str(ROOT / "bench.py"), "--fake-engine", "--steps", "2", "--warmup", "1",
-                           "--min-warmup-s", "0.3", "--users", "16", "--decode-workers", "2", *args],
+                           "--min-warmup-s", "0.3", "--users", "16", "--decode-workers", "2", "--step-batches", "8",
+                           *args],
                           capture_output=True, text=True, timeout=600, env=e)
 
 
