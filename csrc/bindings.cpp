@@ -15,6 +15,7 @@
 #include "runtime/echo_instance.h"
 #include "runtime/http_front.h"
 #include "runtime/http_loadgen.h"
+#include "runtime/ipc_buffer.h"
 #include "runtime/batcher.h"
 #include "runtime/split.h"
 
@@ -491,6 +492,39 @@ PYBIND11_MODULE(_C, m) {
              py::gil_scoped_release nogil;
              return e.submit_peer(src, slot);
            })
+      .def("submit_device",
+           // images: [(device_ptr, h, w, device)], boxes: per image a float32 [k, 6] array (x1, y1, x2, y2, conf,
+           // class) in image coordinates
+           [](Executor& e, const std::vector<std::tuple<uintptr_t, int, int, int>>& images,
+              const std::vector<py::array_t<float, py::array::c_style | py::array::forcecast>>& boxes) {
+             if (images.size() != boxes.size()) throw std::runtime_error("submit_device: one box array per image");
+             std::vector<Executor::DeviceImage> imgs;
+             std::vector<std::vector<Detection>> dets(images.size());
+             for (size_t i = 0; i < images.size(); ++i) {
+               Executor::DeviceImage d;
+               d.ptr = std::get<0>(images[i]);
+               d.h = std::get<1>(images[i]);
+               d.w = std::get<2>(images[i]);
+               d.device = std::get<3>(images[i]);
+               imgs.push_back(d);
+               const auto& b = boxes[i];
+               if (b.size() == 0) continue;
+               if (b.ndim() != 2 || b.shape(1) != 6) throw std::runtime_error("submit_device: boxes must be [k, 6]");
+               const float* q = b.data();
+               for (ssize_t k = 0; k < b.shape(0); ++k, q += 6) {
+                 Detection dd{};
+                 dd.x1 = q[0];
+                 dd.y1 = q[1];
+                 dd.x2 = q[2];
+                 dd.y2 = q[3];
+                 dd.conf = q[4];
+                 dd.cls = (int)q[5];
+                 dets[i].push_back(dd);
+               }
+             }
+             py::gil_scoped_release nogil;
+             return e.submit_device(imgs, dets);
+           })
       .def("conv_choices", &Executor::conv_choices)
       .def("stream", &Executor::stream);
 
@@ -626,6 +660,31 @@ PYBIND11_MODULE(_C, m) {
       });
 
   // closed-loop HTTP load generator (bench.py --path http, serving sweeps)
+  py::class_<IpcBuffer>(m, "IpcBuffer")
+      .def(py::init<size_t, int>(), py::arg("bytes"), py::arg("device") = 0)
+      .def("handle", [](const IpcBuffer& b) { return py::bytes(b.handle()); })
+      .def_property_readonly("ptr", &IpcBuffer::ptr)
+      .def_property_readonly("size", &IpcBuffer::size)
+      .def_property_readonly("device", &IpcBuffer::device)
+      .def("write",
+           [](IpcBuffer& b, size_t off, py::buffer data) {
+             py::buffer_info bi = data.request();
+             const size_t n = (size_t)bi.size * (size_t)bi.itemsize;
+             py::gil_scoped_release nogil;
+             b.write(off, bi.ptr, n);
+           })
+      .def("read", [](const IpcBuffer& b, size_t off, size_t n) {
+        std::string out(n, '\0');
+        {
+          py::gil_scoped_release nogil;
+          b.read(off, out.data(), n);
+        }
+        return py::bytes(out);
+      });
+  m.def("ipc_open", [](py::bytes handle, int device) { return ipc_open(std::string(handle), device); },
+        py::arg("handle"), py::arg("device") = 0);
+  m.def("ipc_close", &ipc_close);
+
   py::class_<HttpLoadGen>(m, "HttpLoadGen")
       .def(py::init([](const py::dict& cfg, const py::list& requests) {
              LoadGenConfig c;

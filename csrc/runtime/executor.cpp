@@ -1104,6 +1104,98 @@ int Executor::submit_peer(Executor& src, int src_slot) {
   return s;
 }
 
+int Executor::submit_device(const std::vector<DeviceImage>& imgs, const std::vector<std::vector<Detection>>& dets) {
+  trace::Range tr("arena.submit_device");
+  if (!peer_stage_) throw std::runtime_error("submit_device: executor is not a second-stage program (set_peer_stage)");
+  const int n = (int)imgs.size();
+  if (n <= 0 || dets.size() != imgs.size()) throw std::runtime_error("submit_device: one detection list per image");
+  std::lock_guard<std::mutex> lk(mu_);
+  const int B = pick_bucket(n);
+  if (B < 0) throw std::runtime_error("submit_device: batch larger than the largest bucket");
+  auto it = buckets_.find(B);
+  const int s = next_slot_;
+  Slot& sl = slots_[s];
+  if (sl.busy) throw std::runtime_error("submit_device: every staging slot is in flight; collect() first");
+  ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
+  sl.stream = streams_[seq_++ % n_streams_];
+  // host staging of the small blocks: ctrl + image metadata (d_in), detection counts + detections + crop plan
+  // (d_out); h_out is free until this slot's result copy, which the stream orders after these uploads
+  Ctrl* ctrl = (Ctrl*)sl.h_in;
+  std::memset(sl.h_in, 0, in_bytes_meta());
+  ImageMeta* meta = (ImageMeta*)(sl.h_in + kCtrlBytes);
+  int* cnt = (int*)sl.h_out;
+  Detection* det = (Detection*)(sl.h_out + out_off_det());
+  CropRef* crops = (CropRef*)(sl.h_out + out_off_xcrops());
+  std::memset(sl.h_out, 0, out_off_topk());
+  const size_t pool_cap = (size_t)cfg_.pool_bytes_per_image * max_B_;
+  size_t off = 0;
+  int total = 0;
+  const int T = cfg_.det_size > 0 ? cfg_.det_size : 640;
+  for (int i = 0; i < n; ++i) {
+    const DeviceImage& im = imgs[i];
+    if (im.h <= 0 || im.w <= 0 || im.ptr == 0) throw std::runtime_error("submit_device: empty image");
+    const size_t bytes = (size_t)im.h * im.w * 3;
+    if (off + bytes > pool_cap) throw std::runtime_error("submit_device: batch exceeds the staging pool");
+    ImageMeta& m = meta[i];
+    m.offset = (int64_t)off;
+    m.h = im.h;
+    m.w = im.w;
+    const double sc = std::min((double)T / im.h, (double)T / im.w);
+    m.new_w = (int)(im.w * sc);
+    m.new_h = (int)(im.h * sc);
+    m.pad_w = (T - m.new_w) / 2;
+    m.pad_h = (T - m.new_h) / 2;
+    m.scale = (float)sc;
+    const int k = std::min((int)dets[i].size(), cfg_.max_det);
+    cnt[i] = k;
+    for (int d = 0; d < k; ++d) {
+      const Detection& dd = dets[i][d];
+      det[(size_t)i * cfg_.max_det + d] = dd;
+      CropRef& r = crops[total + d];
+      r.img = i;
+      r.x1 = std::max(0, (int)dd.x1);
+      r.y1 = std::max(0, (int)dd.y1);
+      r.x2 = std::min(im.w, (int)dd.x2);
+      r.y2 = std::min(im.h, (int)dd.y2);
+      r.det = d;
+      r.pad_[0] = r.pad_[1] = 0;
+    }
+    total += k;
+    off = align_up(off + bytes, 256);
+  }
+  if (total > (int)max_B_ * cfg_.max_det) throw std::runtime_error("submit_device: too many crops");
+  const int CC = it->second.info.crop_cap;
+  ctrl->n_images = n;
+  ctrl->crop_base = 0;
+  ctrl->total_crops = total;
+  ctrl->n_crops = std::min(total, CC);
+  ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, in_bytes_meta(), hipMemcpyHostToDevice, sl.stream));
+  ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_out, sl.h_out, out_off_topk(), hipMemcpyHostToDevice, sl.stream));
+  ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_out + out_off_xcrops(), crops, sizeof(CropRef) * (size_t)std::max(total, 1),
+                                 hipMemcpyHostToDevice, sl.stream));
+  for (int i = 0; i < n; ++i) {  // the pixels: device to device, never through the host
+    const DeviceImage& im = imgs[i];
+    uint8_t* dst = sl.d_in + in_bytes_meta() + meta[i].offset;
+    const size_t bytes = (size_t)im.h * im.w * 3;
+    if (im.device < 0 || im.device == cfg_.device)
+      ARENA_HIP_CHECK(hipMemcpyAsync(dst, (const void*)im.ptr, bytes, hipMemcpyDeviceToDevice, sl.stream));
+    else
+      ARENA_HIP_CHECK(hipMemcpyPeerAsync(dst, cfg_.device, (const void*)im.ptr, im.device, bytes, sl.stream));
+  }
+  sl.in_used = in_bytes_meta() + off;
+  ARENA_HIP_CHECK(hipEventRecord(sl.started, sl.stream));
+  Bucket& bk = it->second;
+  ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], sl.stream));
+  enqueue_results_d2h(bk, sl, n);
+  bk.last_slot = s;
+  ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
+  sl.busy = true;
+  sl.bucket = B;
+  sl.n_images = n;
+  next_slot_ = (next_slot_ + 1) % n_slots_;
+  return s;
+}
+
 void Executor::replay(int B, int s, int iters) {
   auto it = buckets_.find(B);
   if (it == buckets_.end()) throw std::runtime_error("replay: unknown bucket");

@@ -141,6 +141,19 @@ class Executor : public BatchInstance {
   // plan (BUF_XCROPS), then this program's graph (crop gather + classifier) and the result D2H.  The
   // result of collect() on this executor is the whole request result (detections + classifications).
   int submit_peer(Executor& src, int src_slot);
+  // Cross-process device hand-off (arm B, ARENA_CROP_TRANSPORT=device): run this second-stage program (crop
+  // gather from the staged images with the exported crop plan -> classifier) on images that already sit in
+  // device memory — another process's IPC-shared buffer (IpcBuffer / ipc_open) or any device pointer — with
+  // their detections given by the host.  The images are copied device to device into the slot's pool (peer
+  // copy when they live on another GPU), the control block, image metadata, detections and the crop plan
+  // (the crop_plan_kernel's rules: int-truncated boxes clamped to the image) are staged from the host; the
+  // result of collect() is as for submit_peer.
+  struct DeviceImage {
+    uintptr_t ptr = 0;  // HWC uint8 RGB
+    int h = 0, w = 0;
+    int device = -1;    // -1: this executor's device
+  };
+  int submit_device(const std::vector<DeviceImage>& imgs, const std::vector<std::vector<Detection>>& dets);
   // Mark this executor as a second stage (its detections arrive from a peer, see submit_peer).
   void set_peer_stage(bool v) { peer_stage_ = v; }
   bool peer_stage() const { return peer_stage_; }

@@ -1,0 +1,63 @@
+// See ipc_buffer.h.
+#include "runtime/ipc_buffer.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace arena {
+
+namespace {
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e) + " (" + what + ")");
+}
+}  // namespace
+
+IpcBuffer::IpcBuffer(size_t bytes, int device) : bytes_(bytes), device_(device) {
+  if (bytes == 0) throw std::runtime_error("IpcBuffer: zero size");
+  check(hipSetDevice(device), "hipSetDevice");
+  check(hipMalloc(&ptr_, bytes), "hipMalloc");
+  hipIpcMemHandle_t h;
+  const hipError_t e = hipIpcGetMemHandle(&h, ptr_);
+  if (e != hipSuccess) {
+    (void)hipFree(ptr_);
+    ptr_ = nullptr;
+    check(e, "hipIpcGetMemHandle (dmabuf IPC needs HSA_ENABLE_IPC_MODE_LEGACY=0)");
+  }
+  handle_.assign((const char*)&h, sizeof h);
+}
+
+IpcBuffer::~IpcBuffer() {
+  if (ptr_ != nullptr) {
+    (void)hipSetDevice(device_);
+    (void)hipFree(ptr_);
+  }
+}
+
+void IpcBuffer::write(size_t off, const void* src, size_t n) {
+  if (off > bytes_ || n > bytes_ - off) throw std::runtime_error("IpcBuffer::write out of range");
+  check(hipSetDevice(device_), "hipSetDevice");
+  check(hipMemcpy((uint8_t*)ptr_ + off, src, n, hipMemcpyHostToDevice), "hipMemcpy H2D");
+}
+
+void IpcBuffer::read(size_t off, void* dst, size_t n) const {
+  if (off > bytes_ || n > bytes_ - off) throw std::runtime_error("IpcBuffer::read out of range");
+  check(hipSetDevice(device_), "hipSetDevice");
+  check(hipMemcpy(dst, (const uint8_t*)ptr_ + off, n, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+}
+
+uintptr_t ipc_open(const std::string& handle, int device) {
+  hipIpcMemHandle_t h;
+  if (handle.size() != sizeof h) throw std::runtime_error("ipc_open: handle must be " + std::to_string(sizeof h) + " bytes");
+  std::memcpy(&h, handle.data(), sizeof h);
+  check(hipSetDevice(device), "hipSetDevice");
+  void* p = nullptr;
+  check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  return (uintptr_t)p;
+}
+
+void ipc_close(uintptr_t ptr) { check(hipIpcCloseMemHandle((void*)ptr), "hipIpcCloseMemHandle"); }
+
+}  // namespace arena

@@ -300,6 +300,31 @@ class GpuClassifier(GpuProgramRunner):
         return out
 
 
+class GpuFrameClassifier(GpuProgramRunner):
+    """Crop gather + MobileNetV2 over whole frames already resident in device memory (arm B device
+    transport, server/device_transport.py): the second stage of the split topology fed by
+    ``Executor.submit_device`` — frames named by device pointer (IPC-mapped from the detection process),
+    boxes in original-image pixels — instead of by a peer executor's slot."""
+
+    def __init__(self, mnet: MobileNetV2, *, device: int = 0, buckets=None, max_det: int | None = None,
+                 max_image_pixels: int = 640 * 640, dtype: str | None = None, **kw):
+        mb = get_controlled_variable("preprocessing", "mobilenet")
+        max_det = int(max_det or get_gpu_config()["max_det"])
+        prog = plan_split_classifier(mnet, cls_size=int(mb["target_size"]), mean=mb["mean"], std=mb["std"],
+                                     max_det=max_det, dtype=resolve_dtype(dtype))
+        super().__init__(prog, device=device, buckets=buckets, max_det=max_det,
+                         pool_bytes_per_image=int(max_image_pixels) * 3, **kw)
+        self.ex.set_peer_stage(True)
+        self.max_image_pixels = int(max_image_pixels)
+
+    def submit(self, images, boxes) -> int:
+        """``images``: [(device pointer, height, width, device)]; ``boxes``: float32 [k, 6] per image."""
+        return self.ex.submit_device(list(images), [np.ascontiguousarray(b, dtype=np.float32) for b in boxes])
+
+    def collect(self, slot: int) -> dict:
+        return self.ex.collect(slot)
+
+
 class GpuTensorModel(GpuProgramRunner):
     """Reference tensor contract models served by the model server:
 

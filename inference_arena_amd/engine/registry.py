@@ -36,7 +36,7 @@ class ModelInfo:
     source: str
 
 
-MODEL_KINDS = ("yolov5n", "mobilenetv2", "pipeline", "detector", "classifier", "split")
+MODEL_KINDS = ("yolov5n", "mobilenetv2", "pipeline", "detector", "classifier", "frame_classifier", "split")
 
 
 def build_session(kind: str, yolo=None, mnet=None, *, device: int = 0, buckets=None, dtype: str | None = None,
@@ -45,9 +45,10 @@ def build_session(kind: str, yolo=None, mnet=None, *, device: int = 0, buckets=N
 
     kind: ``yolov5n`` / ``mobilenetv2`` (raw tensor models, the model server's per-model entries),
     ``pipeline`` (fused detector -> crops -> classifier), ``detector`` / ``classifier`` (the microservices
-    halves) or ``split`` (pipeline with detection on ``device`` and classification on ``cls_device``).
+    halves), ``frame_classifier`` (crop gather + classifier over device-resident frames: arm B device
+    transport) or ``split`` (pipeline with detection on ``device`` and classification on ``cls_device``).
     Extra keywords go to the engine class (weights, host_threads, crop_cap_per_image, cls_device)."""
-    from .pipeline import GpuClassifier, GpuDetector, GpuPipeline, GpuTensorModel, SplitPipeline
+    from .pipeline import GpuClassifier, GpuDetector, GpuFrameClassifier, GpuPipeline, GpuTensorModel, SplitPipeline
 
     common = dict(buckets=buckets, dtype=dtype)
     if kind == "yolov5n":
@@ -60,6 +61,8 @@ def build_session(kind: str, yolo=None, mnet=None, *, device: int = 0, buckets=N
         return GpuDetector(yolo, device=device, **common)
     if kind == "classifier":
         return GpuClassifier(mnet, device=device, **common)
+    if kind == "frame_classifier":
+        return GpuFrameClassifier(mnet, device=device, **common, **kw)
     if kind == "split":
         return SplitPipeline(yolo, mnet, det_device=device, cls_device=int(kw.pop("cls_device", 1)), **common, **kw)
     raise KeyError(f"unknown model '{kind}' (available: {', '.join(MODEL_KINDS)})")

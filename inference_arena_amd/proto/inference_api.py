@@ -20,8 +20,12 @@ _f.message("ClassificationResult", [("class_id", 1, "int32"), ("class_name", 2, 
                                     ("confidence", 3, "float")])
 _f.message("TimingInfo", [("preprocessing_ms", 1, "double"), ("inference_ms", 2, "double"),
                           ("postprocessing_ms", 3, "double"), ("total_ms", 4, "double")])
+# Arena extension (field 100, ignored by reference peers): the crop is named by a frame resident in device
+# memory that the sender exported over IPC, cut at ``source_box`` on the receiver (server/device_transport.py).
+_f.message("DeviceImageRef", [("handle", 1, "bytes"), ("device", 2, "int32"), ("offset", 3, "int64"),
+                              ("height", 4, "int32"), ("width", 5, "int32")])
 _f.message("ClassificationRequest", [("request_id", 1, "string"), ("image_crop", 2, "bytes"),
-                                     ("source_box", 3, "BoundingBox")])
+                                     ("source_box", 3, "BoundingBox"), ("device_image", 100, "DeviceImageRef")])
 _f.message("ClassificationResponse", [("request_id", 1, "string"), ("result", 2, "ClassificationResult"),
                                       ("top_k", 3, "ClassificationResult", "repeated"), ("timing", 4, "TimingInfo"),
                                       ("error", 5, "string")])
@@ -48,6 +52,7 @@ pb = _f.build()
 BoundingBox = pb.BoundingBox
 ClassificationResult = pb.ClassificationResult
 TimingInfo = pb.TimingInfo
+DeviceImageRef = pb.DeviceImageRef
 ClassificationRequest = pb.ClassificationRequest
 ClassificationResponse = pb.ClassificationResponse
 BatchClassificationRequest = pb.BatchClassificationRequest

@@ -11,7 +11,11 @@ into the GPU classifier's dynamic batcher, so crops of concurrent requests —
 and all crops of one ``ClassifyBatch`` — run as one batched MobileNetV2 graph
 replay.  ``Health/Check`` is implemented (declared only upstream), and with
 ``ARENA_INFER_SERVICE=1`` so is ``InferenceService/Infer`` (also declared
-only upstream; see server/inference_service.py).
+only upstream; see server/inference_service.py).  With
+``ARENA_CROP_TRANSPORT=device`` requests may name a frame in the detection
+process's device memory instead of carrying crop bytes
+(server/device_transport.py): those crops are cut and classified on the GPU
+straight from the IPC-mapped frame.
 
 Run: ``python -m inference_arena_amd.server.classification_service``.
 """
@@ -46,14 +50,52 @@ class ClassificationServicer:
         self.n_requests = 0
         self.n_errors = 0
         self.infer = None  # InferenceServicer when the server also serves InferenceService
+        self.frames = None  # device_transport.DeviceClassifier when device-resident frames are accepted
 
     def _name(self, cid: int) -> str:
         return self.labels[cid] if 0 <= cid < len(self.labels) else ""
+
+    def _response(self, rid: str, ids, probs, t0: float, t1: float, t2: float):
+        top = [pb.ClassificationResult(class_id=c, class_name=self._name(c), confidence=p)
+               for c, p in zip(ids, probs)]
+        t3 = time.perf_counter()
+        return pb.ClassificationResponse(
+            request_id=rid, result=top[0], top_k=top,
+            timing=pb.TimingInfo(preprocessing_ms=(t1 - t0) * 1e3, inference_ms=(t2 - t1) * 1e3,
+                                 postprocessing_ms=(t3 - t2) * 1e3, total_ms=(t3 - t0) * 1e3))
+
+    async def _classify_frames(self, requests) -> list:
+        """Crops named by device-resident frames: one DeviceClassifier entry per frame (its crops share it)."""
+        from .device_transport import group_by_image
+
+        t0 = time.perf_counter()
+        out = [None] * len(requests)
+        if self.frames is None:
+            for i, r in enumerate(requests):
+                out[i] = pb.ClassificationResponse(request_id=r.request_id,
+                                                   error="device crop transport not enabled on this service")
+            self.n_errors += len(requests)
+            return out
+        groups = group_by_image(requests)
+        t1 = time.perf_counter()
+        results = await asyncio.gather(*(self.frames.classify(k, b) for k, b, _ in groups), return_exceptions=True)
+        t2 = time.perf_counter()
+        for (_, _, idx), res in zip(groups, results):
+            for j, i in enumerate(idx):
+                rid = requests[i].request_id
+                if isinstance(res, BaseException):
+                    self.n_errors += 1
+                    out[i] = pb.ClassificationResponse(request_id=rid, error=str(res))
+                else:
+                    out[i] = self._response(rid, res[j][0], res[j][1], t0, t1, t2)
+        return out
 
     async def Classify(self, request, context=None):
         t0 = time.perf_counter()
         request_id_var.set(request.request_id)
         self.n_requests += 1
+        if request.HasField("device_image"):
+            return (await self._classify_frames([request]))[0]
         try:
             data = request.image_crop
             if data[:4] == RAW_MAGIC:  # raw crops are a header + a view: no codec, no thread hop
@@ -63,14 +105,7 @@ class ClassificationServicer:
             t1 = time.perf_counter()
             idx, _logit, prob = await self.backend.classify(crop)
             t2 = time.perf_counter()
-            ids, probs = idx.tolist(), prob.tolist()
-            top = [pb.ClassificationResult(class_id=c, class_name=self._name(c), confidence=p)
-                   for c, p in zip(ids, probs)]
-            t3 = time.perf_counter()
-            return pb.ClassificationResponse(
-                request_id=request.request_id, result=top[0], top_k=top,
-                timing=pb.TimingInfo(preprocessing_ms=(t1 - t0) * 1e3, inference_ms=(t2 - t1) * 1e3,
-                                     postprocessing_ms=(t3 - t2) * 1e3, total_ms=(t3 - t0) * 1e3))
+            return self._response(request.request_id, idx.tolist(), prob.tolist(), t0, t1, t2)
         except Exception as e:  # in-band error, like the reference
             self.n_errors += 1
             log.error(f"Classification failed: {e}")
@@ -78,13 +113,28 @@ class ClassificationServicer:
 
     async def ClassifyBatch(self, request, context=None):
         t0 = time.perf_counter()
-        responses = await asyncio.gather(*(self.Classify(r, context) for r in request.requests))
-        out = pb.BatchClassificationResponse(responses=list(responses))
+        reqs = list(request.requests)
+        dev = [i for i, r in enumerate(reqs) if r.HasField("device_image")]
+        if not dev:
+            responses = list(await asyncio.gather(*(self.Classify(r, context) for r in reqs)))
+        else:
+            self.n_requests += len(dev)
+            host = [i for i in range(len(reqs)) if i not in set(dev)]
+            dres, hres = await asyncio.gather(self._classify_frames([reqs[i] for i in dev]),
+                                              asyncio.gather(*(self.Classify(reqs[i], context) for i in host)))
+            responses = [None] * len(reqs)
+            for i, r in zip(dev, dres):
+                responses[i] = r
+            for i, r in zip(host, hres):
+                responses[i] = r
+        out = pb.BatchClassificationResponse(responses=responses)
         out.batch_timing.total_ms = (time.perf_counter() - t0) * 1e3
         return out
 
     def close(self) -> None:
         self.pool.shutdown(wait=False)
+        if self.frames is not None:
+            self.frames.close()
         if self.infer is not None:
             self.infer.backend.close()
             self.infer.close()
@@ -99,7 +149,7 @@ class HealthServicer:
 
 
 async def start_server(settings: Settings, backend: ClassifierBackend | None = None, port: int | None = None,
-                       pipeline_backend=None):
+                       pipeline_backend=None, frames=None):
     """Create and start the aio server; returns (server, servicer, bound_port).
 
     With ``pipeline_backend`` (or ``ARENA_INFER_SERVICE=1``, which builds one) the same
@@ -107,6 +157,11 @@ async def start_server(settings: Settings, backend: ClassifierBackend | None = N
     backend = backend or build_classifier_backend(settings)
     labels = load_labels(settings.LABELS_FILE or None)
     servicer = ClassificationServicer(backend, labels, settings.ARENA_DECODE_THREADS)
+    if frames is None and settings.ARENA_CROP_TRANSPORT == "device" and settings.ARENA_DEVICE != "cpu":
+        from .service_backends import build_frame_classifier
+
+        frames = build_frame_classifier(settings)
+    servicer.frames = frames
     handlers = [pb.ClassificationService.handler(servicer), pb.Health.handler(HealthServicer())]
     if pipeline_backend is None and int(settings.ARENA_INFER_SERVICE):
         from .inference_service import build_pipeline_backend

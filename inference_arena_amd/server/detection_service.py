@@ -11,12 +11,15 @@ MI355X design: detection is the ``GpuDetector`` program behind the native
 dynamic batcher (concurrent requests share one batched YOLO replay); the
 event loop never blocks.  ``ARENA_FANOUT=batch`` sends one ``ClassifyBatch``
 per request instead of N RPCs; ``ARENA_CROP_TRANSPORT`` picks jpeg (reference)
-/ png / raw crops.
+/ png / raw crops, or ``device``: the decoded frame goes into a ring of IPC-shared
+device memory and one ``ClassifyBatch`` names it with the boxes; the
+classification service cuts the crops on its GPU (server/device_transport.py).
 
 Run: ``python -m inference_arena_amd.server.detection_service``.
 """
 from __future__ import annotations
 
+import asyncio
 import logging
 from contextlib import asynccontextmanager
 
@@ -37,9 +40,9 @@ log = logging.getLogger("arena.detection")
 
 
 def create_app(settings: Settings | None = None, detector: DetectorBackend | None = None,
-               client: ClassificationClient | None = None) -> FastAPI:
+               client: ClassificationClient | None = None, ring=None) -> FastAPI:
     settings = settings or Settings.from_env(PORT=None)
-    state: dict = {"detector": detector, "client": client}
+    state: dict = {"detector": detector, "client": client, "ring": ring}
 
     @asynccontextmanager
     async def lifespan(app: FastAPI):
@@ -56,6 +59,11 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
                                                          transport=settings.ARENA_CROP_TRANSPORT)
         if not state["client"].connected:
             await state["client"].connect(ready_timeout=30.0)
+        if settings.ARENA_CROP_TRANSPORT == "device" and state.get("ring") is None and settings.ARENA_DEVICE != "cpu":
+            from .device_transport import DeviceImageRing
+
+            state["ring"] = DeviceImageRing(int(settings.ARENA_DEVICE_RING_SLOTS), 640 * 640 * 3,
+                                            device=int(settings.ARENA_GPU))
         log.info("service ready")
         yield
         await state["client"].close()
@@ -82,13 +90,20 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
             det, dtiming = await det_be.detect(image)
             detection_ms = t_det.ms()
             t_cls = Timer()
-            crops, boxes = [], []
-            for d in det:
-                crops.append(extract_crop(image, d))
-                boxes.append({"x1": float(d[0]), "y1": float(d[1]), "x2": float(d[2]), "y2": float(d[3]),
-                              "confidence": float(d[4]), "class_id": int(d[5])})
-            if not crops:
+            boxes = [{"x1": float(d[0]), "y1": float(d[1]), "x2": float(d[2]), "y2": float(d[3]),
+                      "confidence": float(d[4]), "class_id": int(d[5])} for d in det]
+            ring = state.get("ring")
+            on_device = ring is not None and image.nbytes <= ring.slot_bytes
+            crops = [] if on_device else [extract_crop(image, d) for d in det]
+            if not boxes:
                 responses = []
+            elif on_device:
+                loop = asyncio.get_running_loop()
+                slot, ref = await loop.run_in_executor(None, ring.put, image)
+                try:
+                    responses = await cl.classify_device(rid, ref, boxes)
+                finally:  # the answer (or the RPC's deadline) ends the classification side's use of the frame
+                    ring.release(slot)
             elif settings.ARENA_FANOUT == "batch":
                 responses = await cl.classify_batch(rid, crops, boxes)
             else:

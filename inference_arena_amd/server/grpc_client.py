@@ -7,8 +7,12 @@ be ready (30 s), ``classify`` encodes the crop (PIL JPEG q95) into a
 ``classify_parallel`` fans all crops of a request out with
 ``asyncio.gather`` (the H1b mechanism).
 
-Additions: ``transport`` selects jpeg (reference) / png / raw crops, and
-``classify_batch`` sends all crops in one ``ClassifyBatch`` RPC.
+Additions: ``transport`` selects jpeg (reference) / png / raw crops,
+``classify_batch`` sends all crops in one ``ClassifyBatch`` RPC and
+``classify_device`` sends one ``ClassifyBatch`` that names a device-resident
+frame instead of carrying crops (``transport="device"``,
+server/device_transport.py; crops of frames that do not fit the ring still
+go as JPEG).
 """
 from __future__ import annotations
 
@@ -20,12 +24,14 @@ import numpy as np
 from ..proto import inference_api as pb
 from .classification_service import GRPC_OPTIONS
 from .crop_codec import encode_crop
+from .device_transport import device_batch_request
 
 
 class ClassificationClient:
     def __init__(self, endpoint: str, transport: str = "jpeg", timeout_s: float = 30.0):
         self.endpoint = endpoint
         self.transport = transport
+        self.codec = "jpeg" if transport == "device" else transport  # bytes fallback of the device transport
         self.timeout_s = timeout_s
         self.channel = None
         self.stub = None
@@ -47,7 +53,7 @@ class ClassificationClient:
         return self.stub is not None
 
     def _request(self, rid: str, crop: np.ndarray, box: dict | None):
-        req = pb.ClassificationRequest(request_id=rid, image_crop=encode_crop(crop, self.transport))
+        req = pb.ClassificationRequest(request_id=rid, image_crop=encode_crop(crop, self.codec))
         if box:
             req.source_box.x1 = float(box["x1"])
             req.source_box.y1 = float(box["y1"])
@@ -68,8 +74,14 @@ class ClassificationClient:
                                       for i, (c, b) in enumerate(zip(crops, boxes))))
 
     async def classify_batch(self, request_id: str, crops: list[np.ndarray], boxes: list[dict]):
-        breq = pb.BatchClassificationRequest(requests=[self._request(f"{request_id}_{i}", c, b)
-                                                       for i, (c, b) in enumerate(zip(crops, boxes))])
+        return await self._batch(pb.BatchClassificationRequest(
+            requests=[self._request(f"{request_id}_{i}", c, b) for i, (c, b) in enumerate(zip(crops, boxes))]))
+
+    async def classify_device(self, request_id: str, ref, boxes: list[dict]):
+        """All crops of one frame: ``ref`` (pb.DeviceImageRef) names the frame, ``boxes`` the crops."""
+        return await self._batch(device_batch_request(request_id, ref, boxes))
+
+    async def _batch(self, breq):
         try:
             return list((await self.stub.ClassifyBatch(breq, timeout=self.timeout_s)).responses)
         except grpc.aio.AioRpcError as e:
@@ -132,6 +144,10 @@ class ClassificationClientPool:
     async def classify_batch(self, request_id: str, crops: list[np.ndarray], boxes: list[dict]):
         i = self.pick()
         return await self._on(i, self.clients[i].classify_batch(request_id, crops, boxes))
+
+    async def classify_device(self, request_id: str, ref, boxes: list[dict]):
+        i = self.pick()
+        return await self._on(i, self.clients[i].classify_device(request_id, ref, boxes))
 
     async def check_health(self) -> bool:
         return all(await asyncio.gather(*(c.check_health() for c in self.clients)))

@@ -222,6 +222,24 @@ def build_classifier_backend(settings) -> ClassifierBackend:
                                 idle_queue_delay_us=int(settings.ARENA_QUEUE_DELAY_US))
 
 
+def build_frame_classifier(settings):
+    """Classification side of ``ARENA_CROP_TRANSPORT=device``: a ``GpuFrameClassifier`` (crop gather +
+    MobileNetV2 over device-resident frames) behind the frame micro-batcher of server/device_transport.py."""
+    from ..engine.registry import build_session
+    from ..models.zoo import resolve_models
+    from ..ops import native
+    from .device_transport import DeviceClassifier
+
+    _, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
+    dev = int(settings.ARENA_GPU)
+    max_batch = int(settings.ARENA_MAX_BATCH)
+    runner = build_session("frame_classifier", mnet=mnet, device=dev, buckets=_default_buckets(max_batch))
+    C = native()
+    return DeviceClassifier(runner, lambda h: C.ipc_open(h, dev), max_batch=max_batch,
+                            max_crops=int(runner.ex.crop_cap_for(runner.max_batch)),
+                            max_delay_us=int(os.environ.get("ARENA_CLS_QUEUE_DELAY_US", "300")))
+
+
 def build_detector_backend(settings) -> DetectorBackend:
     from ..config import get_controlled_variable, get_model_config
     from ..models.zoo import resolve_models

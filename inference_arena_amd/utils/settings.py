@@ -54,7 +54,8 @@ class Settings(BaseModel):
     ARENA_QUEUE_DELAY_US: int = 500
     ARENA_DECODE_THREADS: int = 8
     ARENA_CONFIDENCE: str = ""          # logit | softmax ('' = topology default)
-    ARENA_CROP_TRANSPORT: str = "jpeg"  # jpeg (reference) | png | raw
+    ARENA_CROP_TRANSPORT: str = "jpeg"  # jpeg (reference) | png | raw | device (IPC frame hand-off)
+    ARENA_DEVICE_RING_SLOTS: int = 512  # device transport: frames in flight per detection process
     ARENA_FANOUT: str = "parallel"      # parallel (one Classify per crop, reference) | batch (one ClassifyBatch)
     ARENA_GATEWAY_MODE: str = "pipeline"  # pipeline (one fused ensemble RPC) | tensor (reference per-model RPCs)
     ARENA_INSTANCES: int = 1            # executor instances per GPU behind one batcher

@@ -81,7 +81,8 @@ def test_proto_field_numbers_match_reference_contract():
         return {f.name: f.number for f in msg.DESCRIPTOR.fields}
 
     assert fields(pb.BoundingBox) == {"x1": 1, "y1": 2, "x2": 3, "y2": 4, "confidence": 5, "class_id": 6}
-    assert fields(pb.ClassificationRequest) == {"request_id": 1, "image_crop": 2, "source_box": 3}
+    # + the arena's device-frame extension (field 100; reference peers skip it as an unknown field)
+    assert fields(pb.ClassificationRequest) == {"request_id": 1, "image_crop": 2, "source_box": 3, "device_image": 100}
     assert fields(pb.ClassificationResponse) == {"request_id": 1, "result": 2, "top_k": 3, "timing": 4, "error": 5}
     assert fields(pb.TimingInfo) == {"preprocessing_ms": 1, "inference_ms": 2, "postprocessing_ms": 3, "total_ms": 4}
     assert fields(pb.InferenceRequest) == {"request_id": 1, "image": 2, "detection_threshold": 3,

@@ -109,10 +109,18 @@ def test_reference_parse_matches_embedded_table(reference):
     assert svcs == SERVICES
 
 
+# arena extensions: additive fields with numbers far from the reference's (a reference peer skips them)
+EXTENSIONS = {"ClassificationRequest": {"device_image": (100, "DeviceImageRef", False)}}
+
+
 @pytest.mark.parametrize("name", sorted(EMBEDDED))
 def test_message_fields_match_reference(reference, name):
     _, msgs, _ = reference
-    assert _ours(getattr(pb, name)) == msgs[name]
+    ours = _ours(getattr(pb, name))
+    ext = EXTENSIONS.get(name, {})
+    assert {k: v for k, v in ours.items() if k not in ext} == msgs[name]
+    assert {k: ours[k] for k in ext} == ext
+    assert all(n >= 100 for n, _, _ in ext.values())
 
 
 def test_health_enum_values():

@@ -53,6 +53,7 @@ SOURCES = [
     "runtime/batcher.cpp",
     "runtime/http_front.cpp",
     "runtime/http_loadgen.cpp",
+    "runtime/ipc_buffer.cpp",
     "runtime/trace.cpp",
     "bindings.cpp",
 ]
