@@ -269,6 +269,14 @@ void HttpFrontEnd::stop() {
   for (auto& t : io_threads_)
     if (t.joinable()) t.join();
   if (collector_.joinable()) collector_.join();
+  {
+    // requests already handed to the batcher answer through callbacks that capture `this`; the batcher
+    // completes (or fails, on its own shutdown) every one of them, so wait here rather than free under them
+    std::unique_lock<std::mutex> lk(cb_mu_);
+    if (!cb_cv_.wait_for(lk, std::chrono::seconds(30), [this] { return cb_outstanding_ == 0; }))
+      std::fprintf(stderr, "http_front: %lld batcher callbacks still outstanding at stop()\n",
+                   (long long)cb_outstanding_);
+  }
   for (int ep : epfds_) ::close(ep);
   epfds_.clear();
   if (listen_fd_ >= 0) ::close(listen_fd_);
@@ -282,6 +290,11 @@ void HttpFrontEnd::stop() {
   }
   std::lock_guard<std::mutex> lk(pend_mu_);
   pending_.clear();
+}
+
+void HttpFrontEnd::callback_done() {
+  std::lock_guard<std::mutex> lk(cb_mu_);
+  if (--cb_outstanding_ == 0) cb_cv_.notify_all();
 }
 
 void HttpFrontEnd::drain() {
@@ -907,6 +920,10 @@ void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int statu
   HttpFrontEnd* self = this;
   const auto t0 = pend->t0;
   ResultCallback cb = [self, conn, t0, t_inf, decode_ms, softmax, labels, stats, smu](RequestResult&& r) {
+    struct Done {
+      HttpFrontEnd* f;
+      ~Done() { f->callback_done(); }
+    } done{self};
     if (!r.error.empty()) {
       {
         std::lock_guard<std::mutex> sl(*smu);
@@ -994,8 +1011,13 @@ void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int statu
     }
     self->respond(conn, 200, "application/json", s);
   };
+  {
+    std::lock_guard<std::mutex> lk(cb_mu_);
+    ++cb_outstanding_;
+  }
   const int64_t id = batcher_->enqueue(out, h, w, std::move(cb));
   release_slot(slot);  // the batcher copied the pixels
+  if (id < 0) callback_done();  // rejected: the batcher never calls back
   if (id == -1) return fail(503, "request queue is full");
   if (id == -2) return fail(413, "image exceeds the staging capacity of one batch");
 }

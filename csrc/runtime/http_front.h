@@ -144,6 +144,7 @@ class HttpFrontEnd {
   void close_conn(int ep, const std::shared_ptr<Conn>& c);
   void finish_decode(uint64_t key, int slot, int h, int w, int status, int64_t aux);
   void release_slot(int slot);
+  void callback_done();
 
   DynamicBatcher* batcher_;
   DecodeChannel dc_;
@@ -178,6 +179,11 @@ class HttpFrontEnd {
   std::string metrics_text_;
   std::mutex stats_mu_;
   FrontStats stats_;
+
+  // batcher callbacks capture `this`: stop() waits for the ones still outstanding before tearing down
+  std::mutex cb_mu_;
+  std::condition_variable cb_cv_;
+  int64_t cb_outstanding_ = 0;
 };
 
 }  // namespace arena
