@@ -71,7 +71,7 @@ __device__ __forceinline__ float4 relu6x4(float4 v) {
 // STEM (classifier front end, t = 1 block 1 only): X is the 2x2 stem conv of the crop-gathered space-to-depth
 // tile, computed here (IrParams.stem); the s2d tile and the 112 x 112 x 32 stem map never leave LDS.
 template <int S, int TH, int TW, int NTO, bool EXPAND, int KIN, bool STEM = false>
-__global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 2 && KIN == 1 && NTO <= 4 ? 3 : 1))) void ir_f32_kernel(const IrParams p) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   constexpr int PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
   constexpr int POUT = TH * TW, MT_OUT = POUT / 16;
@@ -259,21 +259,31 @@ __global__ __launch_bounds__(256) void ir_f32_kernel(const IrParams p) {
     if constexpr (!PREFETCH_DW) load_dw(h0);
 
     // ---- C: depthwise 3x3 (stride S) + bias + ReLU6 on the chunk; 4 channels per thread item
-    for (int q = tid >> 3; q < POUT; q += 32) {
+    static_assert(POUT % 32 == 0, "depthwise: whole passes of 32 pixels");
+    // the nine taps' LDS reads are issued before the FMA chain (interleaved, the compiler reused one register
+    // set and waited on each read in turn); the pass loop stays rolled so the addresses are not kept live
+#pragma unroll 1
+    for (int qi = 0; qi < POUT / 32; ++qi) {
+      const int q = (tid >> 3) + 32 * qi;
       const int oy = q / TW, ox = q - oy * TW;
+      int addr[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int px = (oy * S + t / 3) * PW + ox * S + t % 3;
+        addr[t] = px * ep + 4 * eswz<S>(px, g);
+      }
+      float4 v[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) v[t] = *(const float4*)&E[addr[t]];
       float4 a = bdw;
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int px = (oy * S + ky) * PW + ox * S + kx;
-          const float4 v = *(const float4*)&E[px * ep + 4 * eswz<S>(px, g)];
-          const float4 w = wk[ky * 3 + kx];
-          a.x = fmaf(v.x, w.x, a.x);
-          a.y = fmaf(v.y, w.y, a.y);
-          a.z = fmaf(v.z, w.z, a.z);
-          a.w = fmaf(v.w, w.w, a.w);
-        }
+      for (int t = 0; t < 9; ++t) {
+        const float4 w = wk[t];
+        a.x = fmaf(v[t].x, w.x, a.x);
+        a.y = fmaf(v[t].y, w.y, a.y);
+        a.z = fmaf(v[t].z, w.z, a.z);
+        a.w = fmaf(v[t].w, w.w, a.w);
+      }
       *(float4*)&Ds[q * IRF_DP + 4 * g] = relu6x4(a);
     }
     __syncthreads();

@@ -84,7 +84,7 @@ __device__ __forceinline__ float4 itx_relu6x4(float4 v) {
 
 // S: stride; TH x TW: output tile; NTO: oup_pad / 16; KS: inp_pad / 32.
 template <int S, int TH, int TW, int NTO, int KS>
-__global__ __launch_bounds__(256) void ir_tile_x3_kernel(const IrParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS == 1 ? 2 : 1))) void ir_tile_x3_kernel(const IrParams p) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   constexpr int PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
   constexpr int POUT = TH * TW, MT_OUT = POUT / 16;
@@ -96,6 +96,7 @@ __global__ __launch_bounds__(256) void ir_tile_x3_kernel(const IrParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t itx_lds[];
   float* Es = (float*)itx_lds;                            // [ROWS][EP] fp32
   uint8_t* Ds = itx_lds + ROWS * EP * sizeof(float);      // [POUT][ITX_DPB] bf16 planes
+  float* Wd = (float*)(Ds + POUT * ITX_DPB);              // [10][hid_pad]: depthwise taps 0..8, bias
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, kq = lane >> 4;
@@ -147,9 +148,15 @@ __global__ __launch_bounds__(256) void ir_tile_x3_kernel(const IrParams p) {
 #pragma unroll
   for (int j = 0; j < PPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // expand weights of a chunk (A operand: hidden row h0 + 16 nt_e + col, k 8 kq of each 32-step), fetched one
-  // chunk ahead; project weights of a chunk (A: output row 16 nt + col, hidden k h0 + 8 kq) at the chunk start
-  u32x4 wexp[3 * KS], wnext[3 * KS];
+  // Weights of chunk c + 1 are fetched into registers while chunk c runs (expand: A operand, hidden row h0 +
+  // 16 nt_e + col, k 8 kq of each 32-step; project: A operand, output row 16 nt_p + col, hidden k h0 + 8 kq).
+  // The prefetch is unconditional (the last chunk re-fetches itself): a conditional one made the wait at the
+  // loop head conservative, and the MFMAs then waited for the loads just issued.  The depthwise taps and bias of
+  // every chunk are staged in LDS once (Wd [10][hid_pad]): read at the chunk's depthwise they cost an LDS round
+  // trip instead of a global one behind the barrier.
+  static_assert(NTO == 1 || NTO == 2 || NTO == 4, "a wave's project pairs share one output-channel tile");
+  const int nt_p = wave % NTO;
+  u32x4 wexp[3 * KS], wnext[3 * KS], wprj[3], wprj_n[3];
   float4 bexp, bnext;
   auto load_expand = [&](int h0, u32x4 (&w)[3 * KS], float4& be) {
     const bf16* row = we + (size_t)(h0 + nt_e * 16 + col) * 3 * INP + 8 * kq;
@@ -159,11 +166,24 @@ __global__ __launch_bounds__(256) void ir_tile_x3_kernel(const IrParams p) {
       for (int pl = 0; pl < 3; ++pl) w[ks * 3 + pl] = *(const u32x4*)(row + pl * INP + ks * 32);
     be = *(const float4*)((const float*)p.be + h0 + nt_e * 16 + 4 * kq);
   };
+  auto load_project = [&](int h0, u32x4 (&w)[3]) {
+    const bf16* row = wp + (size_t)(nt_p * 16 + col) * 3 * hid_pad + h0 + 8 * kq;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) w[pl] = *(const u32x4*)(row + pl * hid_pad);
+  };
+  for (int i = tid; i < 10 * hid_pad / 4; i += 256) {
+    const int r = i / (hid_pad / 4), c4 = i - r * (hid_pad / 4);
+    const float* src = r < 9 ? wd + (size_t)r * hid_pad : (const float*)p.bd;
+    *(float4*)&Wd[r * hid_pad + 4 * c4] = *(const float4*)(src + 4 * c4);
+  }
   const int g = tid & 7;  // depthwise channel group (4 channels) of this thread
   load_expand(0, wexp, bexp);
+  load_project(0, wprj);
 
   for (int h0 = 0; h0 < hid_pad; h0 += ITX_HC) {
-    if (h0 + ITX_HC < hid_pad) load_expand(h0 + ITX_HC, wnext, bnext);
+    const int hn = h0 + ITX_HC < hid_pad ? h0 + ITX_HC : h0;
+    load_expand(hn, wnext, bnext);
+    load_project(hn, wprj_n);
     // ---- expand: E = relu6(We . X + be) * inside, fp32 into LDS
 #pragma unroll
     for (int i = 0; i < ET; ++i) {
@@ -189,23 +209,34 @@ __global__ __launch_bounds__(256) void ir_tile_x3_kernel(const IrParams p) {
     {
       float4 wk[9];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)(wd + (size_t)k * hid_pad + h0 + 4 * g);
-      const float4 bdw = *(const float4*)((const float*)p.bd + h0 + 4 * g);
-      for (int q = tid >> 3; q < POUT; q += 32) {
+      for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)&Wd[k * hid_pad + h0 + 4 * g];
+      const float4 bdw = *(const float4*)&Wd[9 * hid_pad + h0 + 4 * g];
+      static_assert(POUT % 32 == 0, "depthwise: whole passes of 32 pixels");
+      // all nine taps' LDS reads of a pixel are issued before its FMAs (one address each, computed up front):
+      // with the reads interleaved into the FMA chain the compiler reused one register set and waited for
+      // every read in turn (nine serialised LDS round trips per pixel)
+#pragma unroll 1
+      for (int qi = 0; qi < POUT / 32; ++qi) {  // not unrolled: 36 tap addresses would stay live over the chunk loop
+        const int q = (tid >> 3) + 32 * qi;
         const int oy = q / TW, ox = q - oy * TW;
+        int addr[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int px = (oy * S + t / 3) * PW + ox * S + t % 3;
+          addr[t] = px * EP + 4 * itx_eswz<S>(px, g);
+        }
+        float4 v[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) v[t] = *(const float4*)&Es[addr[t]];
         float4 a = bdw;
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int px = (oy * S + ky) * PW + ox * S + kx;
-            const float4 v = *(const float4*)&Es[px * EP + 4 * itx_eswz<S>(px, g)];
-            const float4 w = wk[ky * 3 + kx];
-            a.x = fmaf(v.x, w.x, a.x);
-            a.y = fmaf(v.y, w.y, a.y);
-            a.z = fmaf(v.z, w.z, a.z);
-            a.w = fmaf(v.w, w.w, a.w);
-          }
+        for (int t = 0; t < 9; ++t) {
+          const float4 w = wk[t];
+          a.x = fmaf(v[t].x, w.x, a.x);
+          a.y = fmaf(v[t].y, w.y, a.y);
+          a.z = fmaf(v[t].z, w.z, a.z);
+          a.w = fmaf(v[t].w, w.w, a.w);
+        }
         bf16x4 dh, dm, dl;
         itx_split4(itx_relu6x4(a), dh, dm, dl);
         uint8_t* d = Ds + q * ITX_DPB + 8 * g;
@@ -217,22 +248,23 @@ __global__ __launch_bounds__(256) void ir_tile_x3_kernel(const IrParams p) {
     __syncthreads();
 
     // ---- project GEMM accumulate (rows = output channels, columns = output pixels)
+    {
+      const bf16x8 ah = __builtin_bit_cast(bf16x8, wprj[0]), am = __builtin_bit_cast(bf16x8, wprj[1]),
+                   al = __builtin_bit_cast(bf16x8, wprj[2]);
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int pr = wave + 4 * j;
-      if (pr >= PAIRS) break;
-      const int mt = pr / NTO, nt = pr - (pr / NTO) * NTO;
-      const bf16* wrow = wp + (size_t)(nt * 16 + col) * 3 * hid_pad + h0 + 8 * kq;
-      const bf16x8 ah = *(const bf16x8*)wrow, am = *(const bf16x8*)(wrow + hid_pad),
-                   al = *(const bf16x8*)(wrow + 2 * hid_pad);
-      const uint8_t* d = Ds + (mt * 16 + col) * ITX_DPB + 16 * kq;
-      acc[j] = itx_mfma(ah, am, al, *(const bf16x8*)d, *(const bf16x8*)(d + 64), *(const bf16x8*)(d + 128), acc[j]);
+      for (int j = 0; j < PPW; ++j) {
+        const int pr = wave + 4 * j;
+        if (pr >= PAIRS) break;
+        const int mt = pr / NTO;
+        const uint8_t* d = Ds + (mt * 16 + col) * ITX_DPB + 16 * kq;
+        acc[j] = itx_mfma(ah, am, al, *(const bf16x8*)d, *(const bf16x8*)(d + 64), *(const bf16x8*)(d + 128), acc[j]);
+      }
     }
-    if (h0 + ITX_HC < hid_pad) {
 #pragma unroll
-      for (int k = 0; k < 3 * KS; ++k) wexp[k] = wnext[k];
-      bexp = bnext;
-    }
+    for (int k = 0; k < 3 * KS; ++k) wexp[k] = wnext[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) wprj[k] = wprj_n[k];
+    bexp = bnext;
     // no barrier here: the next chunk's expand writes E, which every wave finished reading before the
     // barrier above, and its depthwise writes D only after the next expand barrier, which every wave reaches
     // after this project
@@ -376,21 +408,28 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)(wd + (size_t)k * 32 + 4 * g);
     const float4 bdw = *(const float4*)((const float*)p.bd + 4 * g);
-    for (int q = tid >> 3; q < POUT; q += 32) {
+#pragma unroll 1
+    for (int qi = 0; qi < POUT / 32; ++qi) {  // reads issued ahead of the FMAs, as in ir_tile_x3_kernel
+      const int q = (tid >> 3) + 32 * qi;
       const int oy = q / TW, ox = q - oy * TW;
+      int addr[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int px = (oy + t / 3) * PW + ox + t % 3;
+        addr[t] = px * XP + 4 * itx_eswz<S>(px, g);
+      }
+      float4 v[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) v[t] = *(const float4*)&Xs[addr[t]];
       float4 a = bdw;
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int px = (oy + ky) * PW + ox + kx;
-          const float4 v = *(const float4*)&Xs[px * XP + 4 * itx_eswz<S>(px, g)];
-          const float4 w = wk[ky * 3 + kx];
-          a.x = fmaf(v.x, w.x, a.x);
-          a.y = fmaf(v.y, w.y, a.y);
-          a.z = fmaf(v.z, w.z, a.z);
-          a.w = fmaf(v.w, w.w, a.w);
-        }
+      for (int t = 0; t < 9; ++t) {
+        const float4 w = wk[t];
+        a.x = fmaf(v[t].x, w.x, a.x);
+        a.y = fmaf(v[t].y, w.y, a.y);
+        a.z = fmaf(v[t].z, w.z, a.z);
+        a.w = fmaf(v[t].w, w.w, a.w);
+      }
       bf16x4 dh, dm, dl;
       itx_split4(itx_relu6x4(a), dh, dm, dl);
       uint8_t* d = Ds + q * ITX_DPB + 8 * g;
@@ -428,8 +467,9 @@ template <int S, int TH, int TW, int NTO, int KS>
 void itx_launch(const IrParams& p, hipStream_t s) {
   constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3;
   constexpr int ROWS = (PH * PW + 15) / 16 * 16;
-  constexpr size_t lds = (size_t)ROWS * itx_ep(S) * 4 + (size_t)TH * TW * ITX_DPB;
-  static_assert(lds <= 160 * 1024, "ir_tile_x3: LDS budget");
+  constexpr size_t lds0 = (size_t)ROWS * itx_ep(S) * 4 + (size_t)TH * TW * ITX_DPB;
+  const size_t lds = lds0 + (size_t)10 * p.hid_pad * 4;  // + the depthwise taps / bias of every chunk
+  if (lds > 160 * 1024) throw std::runtime_error("ir_tile_x3: LDS budget exceeded (hid_pad " + std::to_string(p.hid_pad) + ")");
   const int tiles = ((p.Wo + TW - 1) / TW) * ((p.Ho + TH - 1) / TH);
   hipLaunchKernelGGL((ir_tile_x3_kernel<S, TH, TW, NTO, KS>), dim3((unsigned)(p.B * tiles)), dim3(256), lds, s, p);
 }

@@ -121,7 +121,8 @@ def test_device_classifier_batches_ipc_frames(dense_models, device, tmp_path):
         assert dc.frames == len(imgs) and dc.batches < len(imgs)
         for f, got in zip(fused, out):
             assert [list(ids) for ids, _ in got] == f.topk_idx.tolist()
-            np.testing.assert_allclose([p for _, p in got], f.topk_prob, rtol=1e-4, atol=1e-6)
+            probs = np.asarray([p for _, p in got], np.float64).reshape(-1, f.topk_prob.shape[1])  # (0, 5): no boxes
+            np.testing.assert_allclose(probs, f.topk_prob, rtol=1e-4, atol=1e-6)
     finally:
         proc.stdin.write("done\n")
         proc.stdin.flush()
