@@ -1018,7 +1018,10 @@ __global__ __launch_bounds__(256) void conv_x3_h16_kernel(const ConvParams p) {
   const float* __restrict__ w = (const float*)p.w;
 
   if constexpr (LB) {
-    // one thread per halo pixel: 12 live channels sampled from the image, 4 zero; conv padding is zero
+    // one thread per halo pixel: 12 live channels sampled from the image, 4 zero; conv padding is zero.  The
+    // letterboxed values are uint8 integers k (/255 follows): k is exact in bf16, so only the h plane is
+    // staged and the weights carry the /255 (w' = w / 255 split in three planes): k * w'_h + k * w'_m + k * w'_l
+    // is k * w / 255 to fp32 accuracy in three MFMAs instead of six, and the halo needs no split arithmetic
     const ImageMeta m = p.lb_meta[b];
     for (int px = tid; px < H16_HPIX; px += 256) {
       const int hy = px / H16_HC, hx = px - hy * H16_HC;
@@ -1026,23 +1029,13 @@ __global__ __launch_bounds__(256) void conv_x3_h16_kernel(const ConvParams p) {
       float v[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] = 0.f;
-      if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W) letterbox_s2d_px<float>(p.lb_pool, m, iy, ix, v);
-      bf16x8 h[2], mm[2], l[2];
+      if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W) letterbox_s2d_px_u8(p.lb_pool, m, iy, ix, v);
+      bf16x8 h[2];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        bf16 th, tm, tl;
-        split3(v[c], th, tm, tl);
-        h[c >> 3][c & 7] = th;
-        mm[c >> 3][c & 7] = tm;
-        l[c >> 3][c & 7] = tl;
-      }
+      for (int c = 0; c < 16; ++c) h[c >> 3][c & 7] = (bf16)v[c];
       bf16* d = &sX[px * H16_XP];
       *(bf16x8*)d = h[0];
       *(bf16x8*)(d + 8) = h[1];
-      *(bf16x8*)(d + 16) = mm[0];
-      *(bf16x8*)(d + 24) = mm[1];
-      *(bf16x8*)(d + 32) = l[0];
-      *(bf16x8*)(d + 40) = l[1];
     }
   } else {
   // input halo: 4 float4 (16 channels) per pixel, split into three planes
@@ -1070,7 +1063,8 @@ __global__ __launch_bounds__(256) void conv_x3_h16_kernel(const ConvParams p) {
     const int ky = e >> 4, q = e & 15;  // q: float4 index within the 64-k row (12..15 are the zero half)
     const int n = n0 + row, k = ky * 48 + 4 * q;
     const bool ok = n < p.Cout_pad && q < 12;
-    const float4 v = load_f4_or_zero(w + (size_t)n * p.Kpad + k, w, ok);
+    float4 v = load_f4_or_zero(w + (size_t)n * p.Kpad + k, w, ok);
+    if constexpr (LB) v = make_float4(v.x / 255.0f, v.y / 255.0f, v.z / 255.0f, v.w / 255.0f);
     bf16x4 h, m, l;
     bf16 th, tm, tl;
     split3(v.x, th, tm, tl); h[0] = th; m[0] = tm; l[0] = tl;
@@ -1108,6 +1102,17 @@ __global__ __launch_bounds__(256) void conv_x3_h16_kernel(const ConvParams p) {
       for (int f = 0; f < MF; ++f) {
         const int oy = wave + 4 * f;
         const bf16* r = &sX[((oy + ky) * H16_HC + col + kx) * H16_XP + c0];
+        if constexpr (LB) {  // exact integer activations: one plane
+          const bf16x8 bh = *(const bf16x8*)r;
+#pragma unroll
+          for (int j = 0; j < NF; ++j) {
+            f32x4 c = acc[f][j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[j], bh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[j], bh, c, 0, 0, 0);
+            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[j], bh, c, 0, 0, 0);
+          }
+          continue;
+        }
         const bf16x8 bh = *(const bf16x8*)r, bm = *(const bf16x8*)(r + 16), bl = *(const bf16x8*)(r + 32);
 #pragma unroll
         for (int j = 0; j < NF; ++j) {

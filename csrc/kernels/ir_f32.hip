@@ -203,8 +203,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 2 && K
   auto load_project = [&](int h0) {
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
-      const int pr = wave + 4 * j;
-      if (pr >= PAIRS) break;
+      // branch-free (a wave past the last pair re-reads a valid row it never uses): a divergent branch here
+      // left the wait before the project MFMAs conservative, so they waited for the next chunk's prefetch too
+      const int pr = wave + 4 * j < PAIRS ? wave + 4 * j : PAIRS - 1;
       const int nt = pr % NTO;
       const float* wrow = wp + (size_t)(nt * 16 + col) * p.hid_pad + h0 + 4 * kq;
       wprj[j][0] = *(const float4*)wrow;
@@ -218,6 +219,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 2 && K
   if constexpr (PREFETCH_DW) load_dw(0);
 
   for (int h0 = 0; h0 < p.hid_pad; h0 += IRF_HC) {
+    const int hn = h0 + IRF_HC < p.hid_pad ? h0 + IRF_HC : h0;  // the last chunk re-fetches itself: no branch
     // ---- B: expand GEMM for this chunk, rows = hidden channel, columns = halo pixel
     const float* E;
     int ep;
@@ -287,10 +289,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(S == 2 && K
       *(float4*)&Ds[q * IRF_DP + 4 * g] = relu6x4(a);
     }
     __syncthreads();
-    if (h0 + IRF_HC < p.hid_pad) {  // next chunk's expand / depthwise weights, in flight during the project GEMM
-      if constexpr (EXPAND) load_expand(h0 + IRF_HC);
-      if constexpr (PREFETCH_DW) load_dw(h0 + IRF_HC);
-    }
+    // next chunk's expand / depthwise weights, in flight during the project GEMM (unconditional: a conditional
+    // prefetch made the project's wait for its own weights cover the prefetch as well)
+    if constexpr (EXPAND) load_expand(hn);
+    if constexpr (PREFETCH_DW) load_dw(hn);
 
     // ---- D: project GEMM accumulate, rows = output channel, columns = output pixel
 #pragma unroll

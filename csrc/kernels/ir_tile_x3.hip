@@ -292,12 +292,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS == 1 ? 2
 }
 
 
-// Classifier front end on the same operand scheme (IrParams.stem with x3w): crop gather + ImageNet
-// normalisation into a space-to-depth tile (split planes in LDS), the 2x2 stem conv (32 <- 4 taps x 16 channels)
-// as x3 MFMAs -> fp32 X (+ bias, ReLU6, zero outside the 112 x 112 map), MobileNetV2 block 1 (t = 1: depthwise 32
-// + ReLU6 on X, project 32 -> 16 as x3 MFMAs).  ir_f32.hip's stem mode ran both GEMMs on v_mfma_f32_16x16x4_f32:
-// the stem conv over the 1.41x halo alone was ~110 us of matrix time per batch of 32 requests.
-// Weights: st_w bf16 [32][3][64] (k = tap * 16 + channel), wp bf16 [16][3][32], wd fp32 [9][32], biases fp32.
+// Classifier front end on the same operand scheme (IrParams.stem with x3w): crop gather into a space-to-depth
+// tile of uint8 values (one exact bf16 plane in LDS; the ImageNet normalisation is folded into the weights and
+// per-tap constants, see A1), the 2x2 stem conv (32 <- 4 taps x 16 channels) as three MFMAs per K step -> fp32 X
+// (+ bias, ReLU6, zero outside the 112 x 112 map), MobileNetV2 block 1 (t = 1: depthwise 32 + ReLU6 on X, project
+// 32 -> 16 as x3 MFMAs).  ir_f32.hip's stem mode ran both GEMMs on v_mfma_f32_16x16x4_f32: the stem conv over the
+// 1.41x halo alone was ~110 us of matrix time per batch of 32 requests.
+// Weights: st_w bf16 [32][3][64] (k = tap * 16 + channel; w / (255 std_c)), st_b fp32 [32 bias][4 taps][32]
+// (mean constants), wp bf16 [16][3][32], wd fp32 [9][32], biases fp32 (engine/planner.py ir_block_stem).
 __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
   constexpr int S = 1, TH = 8, TW = 16;
   constexpr int PH = TH + 2, PW = TW + 2, PIN = PH * PW, MT_IN = (PIN + 15) / 16, ROWS = MT_IN * 16;
@@ -323,8 +325,13 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 - 1, ix0 = ox0 - 1;
 
-  // ---- A1: crop gather -> s2d tile (origin (iy0 - 1, ix0 - 1): the 2x2 stem conv pads top / left by one),
-  // each pixel exactly as crop_gather_s2d_kernel<float> computes it, split into planes
+  // ---- A1: crop gather -> s2d tile (origin (iy0 - 1, ix0 - 1): the 2x2 stem conv pads top / left by one).
+  // The crop resize returns uint8 values k (cv2 INTER_LINEAR, bilinear_rgb), and the normalised input
+  // (k / 255 - mean_c) / std_c is affine in k: the planner folds 1 / (255 std_c) into the stem weights and the
+  // mean into per-tap constants (st_b[32 + 32 tap + co] = -sum_c w[co][tap][c] mean_c / std_c), so the tile holds
+  // k itself, exact in one bf16 plane: three MFMAs per K step instead of six, no normalisation or split
+  // arithmetic per pixel.  Outside the crop map the tile is zero and the tap's constant is not added (the
+  // normalised input is zero-padded).
   {
     const int S2 = p.st_S >> 1;
     const CropRef cr = p.st_crops[(p.st_ctrl != nullptr ? p.st_ctrl->crop_base : 0) + b];
@@ -339,26 +346,22 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
       float out[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) out[k] = 0.f;
-      if ((unsigned)Y < (unsigned)S2 && (unsigned)X < (unsigned)S2) {
+      if ((unsigned)Y < (unsigned)S2 && (unsigned)X < (unsigned)S2 && !empty) {
 #pragma unroll
         for (int pq = 0; pq < 4; ++pq) {
           const int oy = 2 * Y + (pq >> 1), ox = 2 * X + (pq & 1);
-          float rgb[3] = {0.f, 0.f, 0.f};
-          if (!empty) bilinear_rgb(img, m.w, lin_tap(oy, sy, chh), lin_tap(ox, sx, cw), rgb);
-#pragma unroll
-          for (int c = 0; c < 3; ++c) out[pq * 3 + c] = (div255<float>(rgb[c]) - p.st_mean[c]) * p.st_inv_std[c];
+          bilinear_rgb(img, m.w, lin_tap(oy, sy, chh), lin_tap(ox, sx, cw), out + pq * 3);
         }
       }
-      bf16x8 h0, m0, l0, h1, m1, l1;
-      itx_split8(out, h0, m0, l0);
-      itx_split8(out + 8, h1, m1, l1);
+      bf16x8 h0, h1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        h0[k] = (bf16)out[k];
+        h1[k] = (bf16)out[k + 8];
+      }
       uint8_t* d = Ss + i * SPB;
       *(bf16x8*)d = h0;
       *(bf16x8*)(d + 16) = h1;
-      *(bf16x8*)(d + 32) = m0;
-      *(bf16x8*)(d + 48) = m1;
-      *(bf16x8*)(d + 64) = l0;
-      *(bf16x8*)(d + 80) = l1;
     }
   }
   __syncthreads();
@@ -373,6 +376,10 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) ws[ks * 3 + pl] = *(const u32x4*)(wrow + pl * 64 + ks * 32);
     const float4 bb = *(const float4*)(p.st_b + nt * 16 + 4 * kq);
+    float4 ct[4];  // per-tap mean constants of this lane's 4 stem channels
+#pragma unroll
+    for (int tp = 0; tp < 4; ++tp) ct[tp] = *(const float4*)(p.st_b + 32 + tp * 32 + nt * 16 + 4 * kq);
+    const int S2 = p.st_S >> 1;
 #pragma unroll
     for (int i = 0; i < ET; ++i) {
       const int tt = wave + 4 * i;
@@ -385,15 +392,27 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
       for (int ks = 0; ks < 2; ++ks) {
         const int tap = ks * 2 + (kq >> 1);
         const uint8_t* sp = Ss + ((ry + (tap >> 1)) * SW + rx + (tap & 1)) * SPB + (kq & 1) * 16;
-        acc = itx_mfma(__builtin_bit_cast(bf16x8, ws[ks * 3]), __builtin_bit_cast(bf16x8, ws[ks * 3 + 1]),
-                       __builtin_bit_cast(bf16x8, ws[ks * 3 + 2]), *(const bf16x8*)sp, *(const bf16x8*)(sp + 32),
-                       *(const bf16x8*)(sp + 64), acc);
+        const bf16x8 xk = *(const bf16x8*)sp;
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ws[ks * 3 + 2]), xk, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ws[ks * 3 + 1]), xk, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ws[ks * 3]), xk, acc, 0, 0, 0);
       }
-      // lane (col, kq) holds stem channels 16 nt + 4 kq .. +3 of halo pixel r
+      // lane (col, kq) holds stem channels 16 nt + 4 kq .. +3 of halo pixel r; add the constants of the taps
+      // whose s2d pixel is inside the map
+      float4 cs = bb;
+#pragma unroll
+      for (int tp = 0; tp < 4; ++tp) {
+        const int Ys = iy0 - 1 + ry + (tp >> 1), Xs = ix0 - 1 + rx + (tp & 1);
+        const float in_t = (unsigned)Ys < (unsigned)S2 && (unsigned)Xs < (unsigned)S2 ? 1.f : 0.f;
+        cs.x += in_t * ct[tp].x;
+        cs.y += in_t * ct[tp].y;
+        cs.z += in_t * ct[tp].z;
+        cs.w += in_t * ct[tp].w;
+      }
       const int co = nt * 16 + 4 * kq;
       const int iy = iy0 + ry, ix = ix0 + rx;
       const bool in = r < PIN && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-      const float4 v = in ? itx_relu6x4(make_float4(acc[0] + bb.x, acc[1] + bb.y, acc[2] + bb.z, acc[3] + bb.w))
+      const float4 v = in ? itx_relu6x4(make_float4(acc[0] + cs.x, acc[1] + cs.y, acc[2] + cs.z, acc[3] + cs.w))
                           : make_float4(0.f, 0.f, 0.f, 0.f);
       *(float4*)&Xs[r * XP + 4 * itx_eswz<S>(r, co >> 2)] = v;
     }

@@ -59,11 +59,11 @@ __device__ __forceinline__ float div255(float v) {
   else return v * (1.0f / 255.0f);
 }
 
-// The 12 live channels of letterboxed space-to-depth pixel (Y, X) of image m: out[pq * 3 + c] is colour c of
-// sub-pixel (2Y + pq / 2, 2X + pq % 2) of the T x T letterboxed image, /255.
-template <typename T>
-__device__ __forceinline__ void letterbox_s2d_px(const uint8_t* pool, const ImageMeta& m, int Y, int X,
-                                                 float* out) {
+// The 12 live channels of letterboxed space-to-depth pixel (Y, X) of image m as uint8 values (exact small
+// integers in fp32): out[pq * 3 + c] is colour c of sub-pixel (2Y + pq / 2, 2X + pq % 2) of the T x T
+// letterboxed image (cv2 INTER_LINEAR rounded to uint8, gray 114 outside the resized image).
+__device__ __forceinline__ void letterbox_s2d_px_u8(const uint8_t* pool, const ImageMeta& m, int Y, int X,
+                                                    float* out) {
   const uint8_t* img = pool + m.offset;
   const float sy = (float)((double)m.h / (double)m.new_h);
   const float sx = (float)((double)m.w / (double)m.new_w);
@@ -86,8 +86,17 @@ __device__ __forceinline__ void letterbox_s2d_px(const uint8_t* pool, const Imag
       }
     }
 #pragma unroll
-    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = div255<T>(rgb[c]);
+    for (int c = 0; c < 3; ++c) out[pq * 3 + c] = rgb[c];
   }
+}
+
+// The same pixel normalised (/255): the letterbox op's output.
+template <typename T>
+__device__ __forceinline__ void letterbox_s2d_px(const uint8_t* pool, const ImageMeta& m, int Y, int X,
+                                                 float* out) {
+  letterbox_s2d_px_u8(pool, m, Y, X, out);
+#pragma unroll
+  for (int c = 0; c < 12; ++c) out[c] = div255<T>(out[c]);
 }
 
 }  // namespace arena

@@ -458,7 +458,21 @@ class ProgramBuilder:
         if kpad != 64 or cpad != 32:
             raise ValueError("ir_block_stem: stem weights must pack to [32][64]")
         if x3w:
-            wsb = mat_x3(torch.frombuffer(bytearray(wsb), dtype=torch.float32).reshape(32, 64))
+            # csrc/kernels/ir_tile_x3.hip ir_stem_x3_kernel stages the crop's uint8 values k, not the normalised
+            # (k / 255 - mean_c) / std_c: the weights take the 1 / (255 std_c) of their input channel (s2d channel
+            # ci = 3 pq + c) and the mean becomes a constant per (tap, output channel), added for the taps whose
+            # s2d pixel lies inside the map.  fp64 here, rounded once to fp32.
+            w64 = torch.frombuffer(bytearray(wsb), dtype=torch.float32).reshape(32, 64).double()
+            ci = torch.arange(64) % 16
+            live = ci < 12
+            inv = torch.tensor([1.0 / (255.0 * float(std[c % 3])) for c in range(12)] + [0.0] * 4, dtype=torch.float64)
+            mstd = torch.tensor([float(mean[c % 3]) / float(std[c % 3]) for c in range(12)] + [0.0] * 4,
+                                dtype=torch.float64)
+            w_int = torch.where(live[None, :], w64 * inv[ci][None, :], torch.zeros_like(w64))
+            consts = torch.stack([-(w64[:, 16 * t:16 * t + 16] * mstd[None, :]).sum(1) for t in range(4)])  # [4][32]
+            bias = torch.frombuffer(bytearray(bsb), dtype=torch.float32)[:32].double()
+            bsb = torch.cat([bias, consts.reshape(-1)]).float().contiguous().numpy().tobytes()
+            wsb = mat_x3(w_int.float())
         H = S // 2
         rec = [OP_IRBLOCK, BUF_NONE, 0, 0, H, H, 32, pk["inp_pad"], pk["hid_pad"], pk["oup"], pk["oup_pad"], 1, 0, 0,
                *offs, dst.bid, dst.coff, dst.cs, H, H, kind, x3w, 0, 0, 0, 0,

@@ -50,7 +50,17 @@ def main(argv=None) -> int:
     ap.add_argument("--replays", type=int, default=2)
     ap.add_argument("--out", default=None)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--times", default=None, help="per-op table of analyze_trace.py (mean us) for achieved TB/s")
     a = ap.parse_args(argv)
+    times = {}
+    if a.times:
+        for line in Path(a.times).read_text().splitlines():
+            cells = [c.strip() for c in line.strip().strip("|").split("|")]
+            if len(cells) >= 7 and cells[0].isdigit():
+                try:
+                    times[int(cells[0])] = float(cells[6])
+                except ValueError:
+                    pass
     prog = plan_pipeline(*default_models(0), conf_thr=0.5, iou_thr=0.45, dtype=a.dtype)
     n_ops = prog.ops.shape[0]
     vals = defaultdict(lambda: defaultdict(list))
@@ -62,8 +72,9 @@ def main(argv=None) -> int:
                 for c, v in cnt.items():
                     vals[k][c].append(v)
     counters = sorted({c for k in vals for c in vals[k]})
-    lines = ["| op | kind | shape | kernel | " + " | ".join(counters) + " | valu/mfma | lds/mfma | conflict % | mfma busy % |",
-             "|" + "---|" * (4 + len(counters) + 4)]
+    lines = ["| op | kind | shape | kernel | " + " | ".join(counters)
+             + " | valu/mfma | lds/mfma | conflict % | mfma busy % | wait % | HBM MB (rd+wr) | us | TB/s |",
+             "|" + "---|" * (4 + len(counters) + 8)]
     for k in range(n_ops):
         if k not in vals:
             continue
@@ -77,9 +88,18 @@ def main(argv=None) -> int:
         # 1024 SIMDs, GRBM_GUI_ACTIVE over the 8 XCDs (GRBM/8 reproduces the kernel-trace durations)
         mb = (f"{100 * m['SQ_VALU_MFMA_BUSY_CYCLES'] / (m['GRBM_GUI_ACTIVE'] / 8 * 1024):.1f}"
               if m.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in m else "-")
+        # share of wave cycles spent waiting (s_waitcnt / barrier / dependency), SQ_WAIT_ANY over SQ_WAVE_CYCLES
+        wt = (f"{100 * m['SQ_WAIT_ANY'] / m['SQ_WAVE_CYCLES']:.0f}"
+              if m.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in m else "-")
+        # FETCH_SIZE / WRITE_SIZE are KiB of L2 <-> memory traffic (the HBM side of the kernel)
+        mbytes = (m.get("FETCH_SIZE", 0.0) + m.get("WRITE_SIZE", 0.0)) * 1024 / 1e6
+        hb = f"{mbytes:.1f}" if ("FETCH_SIZE" in m or "WRITE_SIZE" in m) else "-"
+        us = times.get(k)
+        tbs = f"{mbytes * 1e6 / (us * 1e-6) / 1e12:.2f}" if us and hb != "-" else "-"
         kind = KIND.get(int(prog.ops[k][0]), "?")
         lines.append(f"| {k} | {kind} | {describe(prog.ops[k])} | {kname[k]} | "
-                     + " | ".join(f"{m[c]:.3g}" if c in m else "-" for c in counters) + f" | {vr} | {lr} | {cf} | {mb} |")
+                     + " | ".join(f"{m[c]:.3g}" if c in m else "-" for c in counters)
+                     + f" | {vr} | {lr} | {cf} | {mb} | {wt} | {hb} | {us if us else '-'} | {tbs} |")
     text = "\n".join(lines)
     print(text)
     if a.out:
