@@ -1574,7 +1574,14 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
     throw std::runtime_error("conv2d_f32: unsupported geometry (Cin/xs/ys %4, Kpad %16, Cout_pad %16, Cout %4)");
   if (p.Cin < 16) throw std::runtime_error("conv2d_f32: Cin must be >= 16");
   if (p.Kpad < p.KH * p.KW * p.Cin) throw std::runtime_error("conv2d_f32: Kpad < KH*KW*Cin");
-  if (p.pw_w != nullptr) throw std::runtime_error("conv2d_f32: fused pointwise epilogue is bf16-only");
+  if (p.pw_w != nullptr) {  // fused Detect-head 1x1: only the x3hg epilogue variants implement it
+    const int v = p.impl >= kF32X3HGPw && p.impl < kF32X3HGPw + kF32X3HGPwVariants ? p.impl - kF32X3HGPw
+                  : p.impl == 0                                                    ? (p.Cout_pad <= 64 ? 0 : 2)
+                                                                                   : -1;
+    if (v < 0 || !conv_x3hg_pw(p, s, v))
+      throw std::runtime_error("conv2d_f32: a fused pointwise epilogue needs an x3hg-pw variant that fits the conv");
+    return;
+  }
   if (p.res != nullptr && p.rs % 4 != 0) throw std::runtime_error("conv2d_f32: residual stride % 4");
   if (p.y2 != nullptr && p.y2s % 4 != 0) throw std::runtime_error("conv2d_f32: upsampled stride % 4");
   const long M = (long)p.B * p.Ho * p.Wo;
@@ -1590,6 +1597,11 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
     if (p.impl >= kF32X3G && p.impl < kF32X3G + kF32X3GVariants) {
       if (!conv_x3g(p, s, p.impl - kF32X3G))
         throw std::runtime_error("conv2d_f32: not an x3g-eligible conv (needs pre-split weights)");
+      return;
+    }
+    if (p.impl >= kF32X3HG && p.impl < kF32X3HG + kF32X3HGVariants) {
+      if (!conv_x3hg(p, s, p.impl - kF32X3HG))
+        throw std::runtime_error("conv2d_f32: not an x3hg-eligible conv (3x3 s1 with pre-split weights)");
       return;
     }
     if (p.impl == kF32X3H16) {

@@ -309,6 +309,7 @@ void prepare_kernels() {
   head_pool_f32_prepare();
   x3_halo_prepare();
   x3g_prepare();
+  x3hg_prepare();
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)sppf_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
   done = true;

@@ -40,9 +40,11 @@ struct ConvParams {
   int f32out;   // store fp32 instead of bf16
   const int* bdev;  // optional live batch count on device
   int impl;         // kernel family for this call (0 = process default, see set_conv_impl)
-  // Optional pointwise conv fused into the epilogue (3x3 halo-tile kernel only; YOLO Detect head):
+  // Optional pointwise conv fused into the epilogue (3x3 halo-tile kernels only; YOLO Detect head):
   //   pw_y = W2 . act(conv(x) + bias) + pw_bias  (act2 = pw_act); the 3x3 result itself is not stored.
-  const void* pw_w;     // bf16 [pw_cout_pad][pw_kpad], k = channel of the 3x3 output
+  // bf16: W2 [pw_cout_pad][pw_kpad], k = channel of the 3x3 output; fp32 (x3hg): pre-split planes with
+  // permuted K columns (halo_x3g.hip), pw_y fp32.
+  const void* pw_w;
   const float* pw_bias; // fp32 [pw_cout_pad]
   void* pw_y;           // bf16 output, pixel stride pw_ys
   int pw_ys, pw_cout, pw_kpad, pw_act;
@@ -91,6 +93,16 @@ void x3_halo_prepare();
 bool x3g_supported(const ConvParams& p);
 bool conv_x3g(const ConvParams& p, hipStream_t s, int v);  // false if the conv or variant is not supported
 void x3g_prepare();
+// x3hg: 3x3 stride-1 halo tiles on 32x32x16 MFMAs over the same pre-split weights (halo_x3g.hip), variant v
+constexpr int kF32X3HG = 131;
+constexpr int kF32X3HGVariants = 14;
+bool x3hg_supported(const ConvParams& p);
+bool conv_x3hg(const ConvParams& p, hipStream_t s, int v);  // false if the conv or variant is not supported
+void x3hg_prepare();
+// ... with the Detect head's final 1x1 fused into the epilogue (ConvParams.pw_*, fp32), variant v
+constexpr int kF32X3HGPw = 145;
+constexpr int kF32X3HGPwVariants = 6;
+bool conv_x3hg_pw(const ConvParams& p, hipStream_t s, int v);
 bool conv_fc_f32(const ConvParams& p, hipStream_t s);
 void conv2d_f32(const ConvParams& p, hipStream_t s);
 

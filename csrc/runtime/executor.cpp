@@ -276,7 +276,9 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
                                 (v >= kF32X3 && v < kF32X3 + kF32X3Variants) || v == kF32Halo || v == kF32X3Halo ||
                                 v == kF32X3HaloN3 || v == kF32X3HaloN2 || v == kF32Stream || v == kF32StreamN2 ||
                                 v == kF32Fc || v == kF32StreamExact || v == kF32X3Halo16 || v == kF32X3Halo16N3 ||
-                                v == kF32X3H16 || (v >= kF32X3G && v < kF32X3G + kF32X3GVariants)
+                                v == kF32X3H16 || (v >= kF32X3G && v < kF32X3G + kF32X3GVariants) ||
+                                (v >= kF32X3HG && v < kF32X3HG + kF32X3HGVariants) ||
+                                (v >= kF32X3HGPw && v < kF32X3HGPw + kF32X3HGPwVariants)
                           : v >= 0 && v <= 3;
       if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
       bk.impl[i] = (int16_t)v;
@@ -323,7 +325,14 @@ void Executor::autotune(Bucket& bk) {
                                        kF32X3Halo16, kF32X3Halo16N3, kF32X3H16,
                                        // x3g variants that won a layer in tools/bench_x3g.py (impl 111 + v)
                                        kF32X3G + 5, kF32X3G + 6, kF32X3G + 7, kF32X3G + 9, kF32X3G + 15,
-                                       kF32X3G + 16, kF32X3G + 17, kF32X3G + 19};
+                                       kF32X3G + 16, kF32X3G + 17, kF32X3G + 19,
+                                       // x3hg 3x3 stride-1 halo tiles that won a layer in tools/bench_x3g.py
+                                       // (halo_x3g.hip; they throw on other convs)
+                                       kF32X3HG + 0, kF32X3HG + 1, kF32X3HG + 2, kF32X3HG + 4, kF32X3HG + 6,
+                                       kF32X3HG + 7, kF32X3HG + 8, kF32X3HG + 9, kF32X3HG + 10,
+                                       // ... with the fused Detect-head 1x1 (the only kernels that take those ops)
+                                       kF32X3HGPw + 0, kF32X3HGPw + 1, kF32X3HGPw + 2, kF32X3HGPw + 3,
+                                       kF32X3HGPw + 4, kF32X3HGPw + 5};
   static const int kBf16Candidates[] = {1, 2, 3};
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;
@@ -477,10 +486,10 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
           p.pw_kpad = (int)r[32];
           p.pw_bias = (const float*)(W + r[33]);
           p.pw_cout = (int)r[34];
-          p.pw_y = resolve(bk, sl, r[36], r[37], 2);
+          p.pw_y = resolve(bk, sl, r[36], r[37], eb);
           p.pw_ys = (int)r[38];
           p.pw_act = (int)r[39];
-          p.impl = 2;
+          if (!f32) p.impl = 2;  // bf16: the v3 halo-tile kernel; fp32: the tuned x3hg-pw variant
         }
         if (f32)
           conv2d_f32(p, s);

@@ -210,6 +210,22 @@ def pack_conv_weight_x3(w: torch.Tensor) -> bytes:
     return bf16_raw_bytes(planes.permute(1, 0, 2, 3).contiguous())
 
 
+def pack_pw_weight_x3(w2: torch.Tensor, k2: int) -> bytes:
+    """Detect-head final 1x1 [Cout2, K, 1, 1] fp32 -> the operand of the fused x3hg epilogue
+    (csrc/kernels/halo_x3g.hip, PWN > 0): rows padded to 32, split into bf16 planes, stored
+    [round32(Cout2)][h | m | l][k2] with the K columns in the order the 3x3 accumulators hold the channels:
+    column 16 ks + 8 h + i is channel 16 ks + 4 h + (i & 3) + 8 (i >> 2)."""
+    co2, k = w2.shape[0], w2.shape[1]
+    rows = _round(co2, 32)
+    wk = torch.zeros(rows, k2, dtype=torch.float32)
+    wk[:co2, :k] = w2.detach().float().reshape(co2, k)
+    col = torch.arange(k2)
+    ks, h, i = col // 16, (col % 16) // 8, col % 8
+    perm = 16 * ks + 4 * h + (i & 3) + 8 * (i >> 2)
+    planes = split_bf16x3(wk[:, perm])  # [rows][3][k2]
+    return bf16_raw_bytes(planes.contiguous())
+
+
 def pack_ir_weights(expand, dw, project, inp: int, k_align: int = 32) -> dict:
     """Padded operand layouts of the fused inverted-residual kernels (csrc/kernels/ir_block.hip, ir_f32.hip):
     we [hid_pad][inp_pad], wd [9][hid_pad], wp [oup_pad][hid_pad] + fp32 biases.  ``k_align``: inp_pad
@@ -380,14 +396,24 @@ class ProgramBuilder:
                ACT[act], int(f32out), kind]
         pw_dst = None
         if pw is not None:
-            self._bf16_only("conv with a fused pointwise epilogue")
             w2, b2, pw_dst, act2 = pw
             co2, ci2 = w2.shape[0], w2.shape[1]
             if ci2 != cout or w2.shape[2:] != (1, 1) or co2 != pw_dst.C:
                 raise ValueError("conv: fused pointwise weights must be [C2, Cout, 1, 1] with C2 == pw dst C")
-            wb2, bb2, kpad2, cpad2 = pack_conv_weight(w2, b2)
+            if self.f32:  # x3hg epilogue: pre-split 1x1 planes, the 3x3 itself as x3g planes (fields 40-41)
+                if (kh, kw, stride) != (3, 3, 1):
+                    raise ValueError("conv: the fp32 fused pointwise epilogue needs a 3x3 stride-1 conv")
+                kpad2, cpad2 = _round(cout, 32), _round(co2, 16)
+                wb2 = pack_pw_weight_x3(w2, kpad2)
+                bb2 = torch.zeros(cpad2)
+                bb2[:co2] = b2.detach().float()
+                bb2 = bb2.numpy().tobytes()
+            else:
+                wb2, bb2, kpad2, cpad2 = pack_conv_weight(w2, b2)
             rec += [self.weights.add(wb2), kpad2, self.weights.add(bb2), co2, cpad2, pw_dst.bid, pw_dst.coff,
                     pw_dst.cs, ACT[act2]]
+            if self.f32:
+                rec += [self.weights.add(pack_conv_weight_x3(w)), 1]
         elif self.f32 and src.bid != BUF_POOL:
             # fp32: the weights once more as pre-split bf16 planes for the x3g kernels (fields 40-41)
             rec += [0] * 9 + [self.weights.add(pack_conv_weight_x3(w)), 1]

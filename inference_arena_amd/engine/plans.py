@@ -207,7 +207,8 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
 
     d = y.detect
     c2, c3, nc = d.c2, d.c3, d.nc
-    fuse_head = os.environ.get("ARENA_FUSE_HEAD", "1").lower() not in ("0", "false", "no", "off") and not pb.f32
+    # bf16: the v3 halo-tile kernel's epilogue; fp32: the x3hg epilogue variants (csrc/kernels/halo_x3g.hip)
+    fuse_head = os.environ.get("ARENA_FUSE_HEAD", "1").lower() not in ("0", "false", "no", "off")
     ch = c2 + c3
     heads = []
     for lvl, (P, cin, s) in enumerate(((P3, 64, s8), (P4, 128, s16), (P5, 256, s32))):

@@ -139,7 +139,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             kpad = int(r[8])
             if kpad < KH * KW * Cin or kpad % (16 if f32 else 32) or Cpad % 16 or Cout > Cpad:
                 raise ProgramError(f"op {i}: bad conv geometry")
-            if f32 and (Cin < 16 or Cin % 4 or int(r[34]) > 0):
+            if f32 and (Cin < 16 or Cin % 4 or (int(r[34]) > 0 and int(r[41]) != 1)):
                 raise ProgramError(f"op {i}: unsupported fp32 conv geometry")
             if int(r[1]) == BUF_POOL:  # letterbox-source stem (x3-h16 kernel samples the images)
                 if not f32 or int(r[30]) == CROPS or (KH, KW, Cin, kpad, int(r[19]), int(r[20]), int(r[21])) != \
@@ -158,12 +158,14 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 if KH != 3 or KW != 3 or int(r[19]) != 1 or Cout not in (64, 80) or kpad2 != (Cout + 31) // 32 * 32 \
                         or co2 > Cout or int(r[22]) != BUF_NONE or int(r[25]) != BUF_NONE:
                     raise ProgramError(f"op {i}: unsupported fused pointwise geometry")
-                view(i, r[36], int(r[37]), int(r[38]), n * Ho * Wo, co2, 2, "fused pointwise output")
-                weights(i, int(r[31]), cpad2 * kpad2 * 2, "pointwise weight")
+                view(i, r[36], int(r[37]), int(r[38]), n * Ho * Wo, co2, el, "fused pointwise output")
+                # fp32: pre-split planes [round32(co2)][3][kpad2] (pack_pw_weight_x3); bf16: [cpad2][kpad2]
+                wn = (co2 + 31) // 32 * 32 * 3 * kpad2 * 2 if f32 else cpad2 * kpad2 * 2
+                weights(i, int(r[31]), wn, "pointwise weight")
                 weights(i, int(r[33]), cpad2 * 4, "pointwise bias")
             if int(r[41]):  # pre-split bf16 weight planes (x3g / x3h kernels): [KH*KW*Cin32/32][Cout_pad][3][32]
-                if not f32 or int(r[41]) != 1 or int(r[34]) > 0:
-                    raise ProgramError(f"op {i}: pre-split weights belong to fp32 convs without a fused epilogue")
+                if not f32 or int(r[41]) != 1:
+                    raise ProgramError(f"op {i}: pre-split weights belong to fp32 convs")
                 weights(i, int(r[40]), KH * KW * ((Cin + 31) // 32) * Cpad * 192, "conv x3 weight")
         elif op == OP_DWCONV:
             n = kind_n(r[16])

@@ -46,8 +46,11 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
                 x_coff: int = 0, cin: int | None = None, out: torch.Tensor | None = None, out_coff: int = 0,
                 res: torch.Tensor | None = None, res_coff: int = 0, out2: torch.Tensor | None = None,
                 out2_coff: int = 0, f32out: bool = False, out_hw=None, bdev: torch.Tensor | None = None,
-                packed=None, impl: int = 0) -> torch.Tensor:
+                packed=None, impl: int = 0, pw=None) -> torch.Tensor:
     """NHWC conv with fused bias/act/residual/upsampled copy.
+
+    ``pw=(w2, b2)`` (fp32 3x3 stride-1 only): the Detect-head 1x1 ``w2`` [C2, Cout, 1, 1] is applied to the
+    activated result inside the x3hg epilogue (impl 145 + v) and only its [B, Ho, Wo, C2] output is returned.
 
     x: [B, H, W, Cx] bf16 or float32 (reads channels [x_coff, x_coff + Cin)); w: [Cout, Cin, KH, KW] fp32.
     A float32 ``x`` runs the exact-fp32 kernel (fp32 weights, v_mfma_f32_16x16x4_f32, fp32 output).
@@ -72,6 +75,23 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
     if out is None:
         out = torch.empty(B, Ho, Wo, cout, dtype=torch.float32 if (f32out or f32) else torch.bfloat16, device=x.device)
     wt, bt, kpad, cpad, w3 = packed if packed is not None else pack_weights(w, b, x.device, "fp32" if f32 else "bf16")
+    pwd = {}
+    if pw is not None:
+        from ..engine.planner import pack_pw_weight_x3
+
+        if not f32:
+            raise ValueError("conv2d_nhwc: the functional fused pointwise path is fp32-only")
+        w2, b2 = pw
+        co2 = w2.shape[0]
+        k2 = (cout + 31) // 32 * 32
+        w2p = torch.frombuffer(bytearray(pack_pw_weight_x3(w2.detach().cpu().float(), k2)),
+                               dtype=torch.int16).to(x.device)
+        b2p = torch.zeros((co2 + 15) // 16 * 16)
+        b2p[:co2] = b2.detach().float()
+        b2p = b2p.to(x.device)
+        out = torch.empty(B, Ho, Wo, co2, dtype=torch.float32, device=x.device)
+        pwd = {"pw_w": _ptr(w2p), "pw_bias": _ptr(b2p), "pw_y": _ptr(out), "pw_ys": co2, "pw_cout": co2,
+               "pw_kpad": k2, "pw_act": 0}
     native().conv2d({
         "x": _ptr(x, x_coff), "B": B, "H": H, "W": W, "xs": Cx, "Cin": cin,
         "w": _ptr(wt), "Kpad": kpad, "bias": _ptr(bt),
@@ -80,8 +100,10 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
         "res": _ptr(res, res_coff), "rs": res.shape[-1] if res is not None else 0,
         "y2": _ptr(out2, out2_coff), "y2s": out2.shape[-1] if out2 is not None else 0,
         "act": ACT[act], "f32out": int(f32out), "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32),
-        "impl": int(impl), "w3": _ptr(w3),
+        "impl": int(impl), "w3": _ptr(w3), **pwd,
     })
+    if pw is not None:
+        torch.cuda.synchronize(x.device)  # keep the packed 1x1 weights alive until the kernel ran
     return out
 
 

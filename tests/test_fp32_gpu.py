@@ -147,6 +147,98 @@ def test_conv_x3g_channel_slices_and_live_batch(device):
         assert torch.all(out[:, :, :, :64] == 7.0) and torch.all(out[3] == 7.0), impl
 
 
+X3HG_IMPLS = [131 + v for v in range(14)]  # x3hg: 3x3 s1 halo tiles, 32x32x16 MFMA, pre-split weights
+
+
+@pytest.mark.parametrize(
+    "B,H,Cin,Cout,act,res,up",
+    [
+        (2, 20, 64, 144, "silu", False, False),   # detect head stacked cv2|cv3 (Cout 144: a partial 160 tile)
+        (2, 19, 80, 80, "silu", False, False),    # Cin 80 (five 16-deep chunks), partial pixel tiles
+        (3, 17, 32, 32, "silu", True, False),     # C3 bottleneck 3x3 with residual
+        (2, 12, 128, 64, None, False, True),      # wide K, 2x upsampled copy, no activation
+        (2, 9, 20, 48, "relu6", False, False),    # Cin 20: a partial 16-channel chunk
+    ],
+)
+def test_conv_x3hg_matches_fp64(device, B, H, Cin, Cout, act, res, up):
+    """Every x3hg variant at the fp32 bound, incl. partial channel chunks / pixel tiles / channel tiles and
+    the residual and upsampled-copy epilogues (csrc/kernels/halo_x3g.hip)."""
+    g = torch.Generator().manual_seed(B * 977 + H + Cin + Cout)
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=g, dtype=torch.float64) * 0.1
+    x32, w32, b32 = x.float(), w.float(), b.float()
+    ref = _act64(F.conv2d(x32.double(), w32.double(), b32.double(), padding=1), act)
+    scale = F.conv2d(x32.double().abs(), w32.double().abs(), b32.double().abs(), padding=1)
+    r = torch.randn(B, Cout, H, H, generator=g).float() if res else None
+    if res:
+        ref = ref + r.double()
+        scale = scale + r.double().abs()
+    xd = _nhwc(x32).to(device)
+    rd = _nhwc(r).to(device) if res else None
+    packed = AF.pack_weights(w32, b32, device, "fp32")
+    for impl in X3HG_IMPLS:
+        out2 = torch.full((B, 2 * H, 2 * H, Cout), float("nan"), device=device) if up else None
+        y = AF.conv2d_nhwc(xd, w32, b32, stride=1, act=act, res=rd, packed=packed, impl=impl, out2=out2)
+        torch.cuda.synchronize()
+        _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
+        if up:
+            want = y.permute(0, 3, 1, 2).repeat_interleave(2, 2).repeat_interleave(2, 3)
+            assert torch.equal(out2.permute(0, 3, 1, 2), want), impl
+
+
+X3HG_PW_IMPLS = [145 + v for v in range(6)]  # x3hg with the Detect-head 1x1 fused into the epilogue
+
+
+@pytest.mark.parametrize("B,H,Cin,C", [(2, 20, 64, 64), (2, 19, 80, 80), (3, 11, 144, 64)])
+def test_conv_x3hg_fused_pointwise_matches_fp64(device, B, H, Cin, C):
+    """3x3 (+ SiLU) -> 1x1 in one kernel (the 3x3 result never stored) at the fp32 bound of the composite:
+    every variant whose channel tile fits (box branch 64 -> 64, cls branch 80 -> 80)."""
+    g = torch.Generator().manual_seed(B * 31 + H + Cin + C)
+    x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64).float()
+    w = (torch.randn(C, Cin, 3, 3, generator=g, dtype=torch.float64) / (Cin * 9) ** 0.5).float()
+    b = (torch.randn(C, generator=g, dtype=torch.float64) * 0.1).float()
+    w2 = (torch.randn(C, C, 1, 1, generator=g, dtype=torch.float64) / C ** 0.5).float()
+    b2 = (torch.randn(C, generator=g, dtype=torch.float64) * 0.1).float()
+    a = _act64(F.conv2d(x.double(), w.double(), b.double(), padding=1), "silu")
+    ref = F.conv2d(a, w2.double(), b2.double())
+    s1 = F.conv2d(x.double().abs(), w.double().abs(), b.double().abs(), padding=1)
+    scale = F.conv2d(1.2 * s1 + a.abs(), w2.double().abs(), b2.double().abs())
+    xd = _nhwc(x).to(device)
+    packed = AF.pack_weights(w, b, device, "fp32")
+    ran = 0
+    for impl in [0] + X3HG_PW_IMPLS:
+        try:
+            y = AF.conv2d_nhwc(xd, w, b, act="silu", packed=packed, impl=impl, pw=(w2, b2))
+        except RuntimeError:
+            assert impl != 0, "the default fused-pointwise variant must take the detect-head shapes"
+            continue
+        torch.cuda.synchronize()
+        assert y.shape == (B, H, H, C)
+        _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
+        ran += 1
+    assert ran >= 3
+
+
+def test_conv_x3hg_channel_slices_and_live_batch(device):
+    """Channel-slice input and output views and the device-side live batch count."""
+    g = torch.Generator().manual_seed(13)
+    buf = torch.randn(4, 11, 11, 96, generator=g)
+    w = torch.randn(64, 32, 3, 3, generator=g) * 0.05
+    b = torch.randn(64, generator=g) * 0.1
+    packed = AF.pack_weights(w, b, device, "fp32")
+    ref = F.conv2d(buf[..., 32:64].permute(0, 3, 1, 2).double(), w.double(), b.double(), padding=1)
+    live = torch.tensor([3], dtype=torch.int32, device=device)
+    for impl in X3HG_IMPLS:
+        out = torch.full((4, 11, 11, 128), 7.0, device=device)
+        AF.conv2d_nhwc(buf.to(device), w, b, stride=1, act=None, x_coff=32, cin=32, out=out, out_coff=64,
+                       packed=packed, impl=impl, bdev=live)
+        torch.cuda.synchronize()
+        got = out[:3, :, :, 64:].permute(0, 3, 1, 2).double().cpu()
+        assert (got - ref[:3]).abs().max().item() < 1e-5, impl
+        assert torch.all(out[:, :, :, :64] == 7.0) and torch.all(out[3] == 7.0), impl
+
+
 @pytest.mark.parametrize(
     "B,H,Cin,Cout,k,s,act,res",
     [
