@@ -218,7 +218,9 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
         wa, ba = fold(d.cv2[lvl][0])
         wc, bc = fold(d.cv3[lvl][0])
         pb.conv(View(P, 0, cin), View(H1, 0, ch), torch.cat([wa, wc]), torch.cat([ba, bc]))
-        if fuse_head and c2 in (64, 80) and c3 in (64, 80):
+        # fp32 at 20x20: the fused x3hg tiles (8 x 16 px) would pad the map to 24 x 32, the unfused pair is
+        # faster there (profiles/r3c_x3hg_ops.md ops 58-59: 33.6 + 48.0 us fused vs 18.7 + 9.6 + 27.0 + 9.9)
+        if fuse_head and c2 in (64, 80) and c3 in (64, 80) and (not pb.f32 or s >= 40):
             # second 3x3 of each branch with its final 1x1 in the epilogue: the 3x3 output never leaves LDS
             pb.conv(View(H1, 0, c2), View(BUF_NONE, 0, c2), *fold(d.cv2[lvl][1]),
                     pw=(*fold_conv_bn(d.cv2[lvl][2], None), View(D, 0, 4 * d.reg_max), None))

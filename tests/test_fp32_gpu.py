@@ -148,19 +148,23 @@ def test_conv_x3g_channel_slices_and_live_batch(device):
 
 
 X3HG_IMPLS = [131 + v for v in range(14)]  # x3hg: 3x3 s1 halo tiles, 32x32x16 MFMA, pre-split weights
+X3HG_S2_IMPLS = [151 + v for v in range(9)]  # ... stride 2
 
 
 @pytest.mark.parametrize(
-    "B,H,Cin,Cout,act,res,up",
+    "B,H,Cin,Cout,act,res,up,s",
     [
-        (2, 20, 64, 144, "silu", False, False),   # detect head stacked cv2|cv3 (Cout 144: a partial 160 tile)
-        (2, 19, 80, 80, "silu", False, False),    # Cin 80 (five 16-deep chunks), partial pixel tiles
-        (3, 17, 32, 32, "silu", True, False),     # C3 bottleneck 3x3 with residual
-        (2, 12, 128, 64, None, False, True),      # wide K, 2x upsampled copy, no activation
-        (2, 9, 20, 48, "relu6", False, False),    # Cin 20: a partial 16-channel chunk
+        (2, 20, 64, 144, "silu", False, False, 1),   # detect head stacked cv2|cv3 (Cout 144: a partial 160 tile)
+        (2, 19, 80, 80, "silu", False, False, 1),    # Cin 80 (five 16-deep chunks), partial pixel tiles
+        (3, 17, 32, 32, "silu", True, False, 1),     # C3 bottleneck 3x3 with residual
+        (2, 12, 128, 64, None, False, True, 1),      # wide K, 2x upsampled copy, no activation
+        (2, 9, 20, 48, "relu6", False, False, 1),    # Cin 20: a partial 16-channel chunk
+        (2, 40, 16, 32, "silu", False, False, 2),    # stride 2 over the s2d stem map (16 channels)
+        (2, 21, 64, 128, "silu", False, False, 2),   # stride 2, odd input size, partial tiles
+        (2, 10, 128, 256, "silu", False, False, 2),  # stride 2, 8 channel fragments
     ],
 )
-def test_conv_x3hg_matches_fp64(device, B, H, Cin, Cout, act, res, up):
+def test_conv_x3hg_matches_fp64(device, B, H, Cin, Cout, act, res, up, s):
     """Every x3hg variant at the fp32 bound, incl. partial channel chunks / pixel tiles / channel tiles and
     the residual and upsampled-copy epilogues (csrc/kernels/halo_x3g.hip)."""
     g = torch.Generator().manual_seed(B * 977 + H + Cin + Cout)
@@ -168,18 +172,19 @@ def test_conv_x3hg_matches_fp64(device, B, H, Cin, Cout, act, res, up):
     w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / (Cin * 9) ** 0.5
     b = torch.randn(Cout, generator=g, dtype=torch.float64) * 0.1
     x32, w32, b32 = x.float(), w.float(), b.float()
-    ref = _act64(F.conv2d(x32.double(), w32.double(), b32.double(), padding=1), act)
-    scale = F.conv2d(x32.double().abs(), w32.double().abs(), b32.double().abs(), padding=1)
-    r = torch.randn(B, Cout, H, H, generator=g).float() if res else None
+    ref = _act64(F.conv2d(x32.double(), w32.double(), b32.double(), stride=s, padding=1), act)
+    scale = F.conv2d(x32.double().abs(), w32.double().abs(), b32.double().abs(), stride=s, padding=1)
+    Ho = ref.shape[2]
+    r = torch.randn(B, Cout, Ho, Ho, generator=g).float() if res else None
     if res:
         ref = ref + r.double()
         scale = scale + r.double().abs()
     xd = _nhwc(x32).to(device)
     rd = _nhwc(r).to(device) if res else None
     packed = AF.pack_weights(w32, b32, device, "fp32")
-    for impl in X3HG_IMPLS:
-        out2 = torch.full((B, 2 * H, 2 * H, Cout), float("nan"), device=device) if up else None
-        y = AF.conv2d_nhwc(xd, w32, b32, stride=1, act=act, res=rd, packed=packed, impl=impl, out2=out2)
+    for impl in (X3HG_IMPLS if s == 1 else X3HG_S2_IMPLS):
+        out2 = torch.full((B, 2 * Ho, 2 * Ho, Cout), float("nan"), device=device) if up else None
+        y = AF.conv2d_nhwc(xd, w32, b32, stride=s, act=act, res=rd, packed=packed, impl=impl, out2=out2)
         torch.cuda.synchronize()
         _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
         if up:

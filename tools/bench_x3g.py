@@ -31,6 +31,9 @@ SHAPES = {  # name: (B, H, Cin, Cout, k, stride)
     "c3_3x3_128": (32, 20, 128, 128, 3, 1),
     "head_144_40": (32, 40, 128, 144, 3, 1),
     "stem_16": (32, 160, 16, 16, 3, 1),
+    "stem_s2": (32, 320, 16, 32, 3, 2),
+    "det_s2_128_40": (32, 40, 128, 128, 3, 2),
+    "det_s2_64_80": (32, 80, 64, 64, 3, 2),
 }
 
 
