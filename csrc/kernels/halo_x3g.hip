@@ -46,12 +46,8 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int HG_P = 56;  // bf16 per LDS row: 3 planes x 16 k + 8 pad (112 B)
 
 __host__ __device__ constexpr int hg_th(int TW, int WM, int TM) { return WM * TM * (32 / TW); }
-// halo rows / stored columns: stride 2 stores even input columns then odd ones (each half padded to the same
-// width), so the 16 lanes of a fragment row read consecutive rows at every tap (no 2-way bank conflict)
-__host__ __device__ constexpr int hg_hr(int TH, int S) { return (TH - 1) * S + 3; }
-__host__ __device__ constexpr int hg_hcs(int TW, int S) { return S == 1 ? TW + 2 : 2 * (((TW - 1) * S + 4) / 2); }
-__host__ __device__ constexpr int hg_lds_bytes(int TW, int WM, int WN, int TM, int TN, int S = 1) {
-  return (hg_hr(hg_th(TW, WM, TM), S) * hg_hcs(TW, S) + 2 * WN * TN * 32) * HG_P * 2;
+__host__ __device__ constexpr int hg_lds_bytes(int TW, int WM, int WN, int TM, int TN) {
+  return ((hg_th(TW, WM, TM) + 2) * (TW + 2) + 2 * WN * TN * 32) * HG_P * 2;
 }
 
 __device__ __forceinline__ int hg_xcd_remap(int bx, int nx) {
@@ -78,21 +74,19 @@ __device__ __forceinline__ f32x16 hg_mfma_x3(const bf16x8& ah, const bf16x8& am,
 // and 32 tn + 16 s + 8 + 4 h + {0..3}, so the split 3x3 output feeds the MFMA straight from registers and the
 // 1x1 weights are pre-split with their K columns in that order (engine/planner.py pack_pw_weight_x3):
 // [PWN * 32 rows][h | m | l][K2 = BN].
-// S = 2: the stride-2 3x3 convs (detector downsampling), same scheme over a (2 TH + 1) x (2 TW + 1) halo.
-template <int TW, int WM, int WN, int TM, int TN, int PWN = 0, int S = 1>
+template <int TW, int WM, int WN, int TM, int TN, int PWN = 0>
 __global__ __launch_bounds__(WM * WN * 64) void conv_x3hg_kernel(const ConvParams p) {
   static_assert(PWN == 0 || WN == 1, "the fused 1x1 needs every 3x3 channel of a pixel in one wave");
   constexpr int NT = WM * WN * 64;
   constexpr int RF = 32 / TW;                         // rows per pixel fragment
   constexpr int TH = WM * TM * RF;                    // tile rows
-  constexpr int HR = hg_hr(TH, S), HC = (TW - 1) * S + 3, HPIX = HR * HC;  // halo rows, columns, pixels
-  constexpr int HCS = hg_hcs(TW, S), HCH = HCS / 2;  // stored columns per halo row; stride 2: odd columns at + HCH
+  constexpr int HC = TW + 2, HPIX = (TH + 2) * HC;    // halo columns, pixels
   constexpr int BN = WN * TN * 32;
   constexpr int XI = (HPIX * 4 + NT - 1) / NT;        // halo float4 items (pixel, 4-channel quarter) per thread
   constexpr int WI = (BN * 6 + NT - 1) / NT;          // 16-B weight pieces per thread per stage (6 per row)
   extern __shared__ __attribute__((aligned(16))) bf16 hg_lds[];
   bf16* sX = hg_lds;                 // [HPIX][HG_P]
-  bf16* sW = hg_lds + HR * HCS * HG_P;  // [2][BN][HG_P]
+  bf16* sW = hg_lds + HPIX * HG_P;   // [2][BN][HG_P]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -107,7 +101,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3hg_kernel(const ConvParam
   t /= ntn;
   const int ty = t / tiles_x, tx = t - ty * tiles_x;
   const int oy0 = ty * TH, ox0 = tx * TW, n0 = nt * BN;
-  const int iy0 = oy0 * S - p.pad_t, ix0 = ox0 * S - p.pad_l;
+  const int iy0 = oy0 - p.pad_t, ix0 = ox0 - p.pad_l;
   const int H = p.H, W = p.W, Cin = p.Cin;
 
   // raw buffer loads: out-of-range offsets (halo outside the map, channels past Cin, weight rows past
@@ -168,13 +162,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3hg_kernel(const ConvParam
           m[e] = tm;
           l[e] = (bf16)(r - (float)tm);
         }
-        const int px = i >> 2;
-        int sp = px;
-        if constexpr (S == 2) {
-          const int hy = px / HC, hx = px - hy * HC;
-          sp = hy * HCS + (hx & 1) * HCH + (hx >> 1);
-        }
-        bf16* d = sX + sp * HG_P + 4 * (i & 3);
+        bf16* d = sX + (i >> 2) * HG_P + 4 * (i & 3);
         *(bf16x4*)d = h;
         *(bf16x4*)(d + 16) = m;
         *(bf16x4*)(d + 32) = l;
@@ -213,11 +201,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3hg_kernel(const ConvParam
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     const int r = (wm * TM + tm) * RF + fr / TW, c = fr % TW;
-    xpix[tm] = r * S * HCS + c;
+    xpix[tm] = r * HC + c;
   }
   auto compute = [&](int buf, int tap) {
     const int ky = tap / 3, kx = tap - ky * 3;
-    const int toff = ky * HCS + (S == 1 ? kx : (kx & 1) * HCH + (kx >> 1));
+    const int toff = ky * HC + kx;
     bf16x8 xh[TM], xm[TM], xl[TM];
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
@@ -363,12 +351,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3hg_kernel(const ConvParam
 
 namespace {
 
-template <int TW, int WM, int WN, int TM, int TN, int PWN = 0, int S = 1>
+template <int TW, int WM, int WN, int TM, int TN, int PWN = 0>
 void hg_launch(const ConvParams& p, hipStream_t s) {
   constexpr int TH = hg_th(TW, WM, TM), BN = WN * TN * 32;
   const long tiles = (long)p.B * ((p.Ho + TH - 1) / TH) * ((p.Wo + TW - 1) / TW) * ((p.Cout_pad + BN - 1) / BN);
-  hipLaunchKernelGGL((conv_x3hg_kernel<TW, WM, WN, TM, TN, PWN, S>), dim3((unsigned)tiles), dim3(WM * WN * 64),
-                     hg_lds_bytes(TW, WM, WN, TM, TN, S), s, p);
+  hipLaunchKernelGGL((conv_x3hg_kernel<TW, WM, WN, TM, TN, PWN>), dim3((unsigned)tiles), dim3(WM * WN * 64),
+                     hg_lds_bytes(TW, WM, WN, TM, TN), s, p);
 }
 
 // variant v: (TW, WM, WN, TM, TN) -> tile TH x TW pixels x BN channels
@@ -388,18 +376,6 @@ void hg_launch(const ConvParams& p, hipStream_t s) {
   X(12, 8, 2, 2, 1, 2)  /*  8 x  8 px x 128 ch */ \
   X(13, 8, 2, 1, 1, 5)  /*  8 x  8 px x 160 ch, 2 waves */
 
-// stride-2 variants v (kF32X3HGS2 + v): (TW, WM, WN, TM, TN)
-#define HG_S2_VARIANTS(X) \
-  X(0, 16, 4, 1, 1, 1)  /*  8 x 16 px x  32 ch */ \
-  X(1, 16, 4, 1, 1, 2)  /*  8 x 16 px x  64 ch */ \
-  X(2, 16, 2, 2, 2, 1)  /*  8 x 16 px x  64 ch, waves split the channels */ \
-  X(3, 16, 4, 1, 1, 4)  /*  8 x 16 px x 128 ch */ \
-  X(4, 8, 4, 1, 1, 2)   /* 16 x  8 px x  64 ch */ \
-  X(5, 8, 2, 2, 1, 2)   /*  8 x  8 px x 128 ch */ \
-  X(6, 8, 4, 1, 1, 4)   /* 16 x  8 px x 128 ch */ \
-  X(7, 8, 2, 2, 1, 4)   /*  8 x  8 px x 256 ch */ \
-  X(8, 16, 2, 2, 1, 1)  /*  4 x 16 px x  64 ch */
-
 // fused-1x1 variants v (kF32X3HGPw + v): (TW, WM, TM, TN, PWN), WN = 1
 #define HG_PW_VARIANTS(X) \
   X(0, 16, 4, 1, 2, 2)  /*  8 x 16 px, 64 -> 64 (box branch) */ \
@@ -414,8 +390,8 @@ void hg_launch(const ConvParams& p, hipStream_t s) {
 bool x3hg_supported(const ConvParams& p) {
   const size_t x_bytes = (size_t)p.B * p.H * p.W * p.xs * 4;
   const size_t w_bytes = (size_t)9 * ((p.Cin + 31) / 32) * p.Cout_pad * 192;
-  return p.w3 != nullptr && p.KH == 3 && p.KW == 3 && (p.stride == 1 || p.stride == 2) && p.Cin % 4 == 0 &&
-         p.xs % 4 == 0 && x_bytes < (1u << 31) - (1u << 20) && w_bytes < (1u << 31) - (1u << 20) && p.Cout % 4 == 0 &&
+  return p.w3 != nullptr && p.KH == 3 && p.KW == 3 && p.stride == 1 && p.Cin % 4 == 0 && p.xs % 4 == 0 &&
+         x_bytes < (1u << 31) - (1u << 20) && w_bytes < (1u << 31) - (1u << 20) && p.Cout % 4 == 0 &&
          p.ys % 4 == 0 && (p.res == nullptr || p.rs % 4 == 0) && (p.y2 == nullptr || p.y2s % 4 == 0) &&
          p.lb_meta == nullptr && p.pw_w == nullptr;
 }
@@ -440,19 +416,8 @@ bool conv_x3hg_pw(const ConvParams& p, hipStream_t s, int v) {
   }
 }
 
-bool conv_x3hg_s2(const ConvParams& p, hipStream_t s, int v) {
-  if (!x3hg_supported(p) || p.stride != 2) return false;
-  switch (v) {
-#define HG_S2_CASE(V, TW, WM, WN, TM, TN) \
-  case V: hg_launch<TW, WM, WN, TM, TN, 0, 2>(p, s); return true;
-    HG_S2_VARIANTS(HG_S2_CASE)
-#undef HG_S2_CASE
-    default: return false;
-  }
-}
-
 bool conv_x3hg(const ConvParams& p, hipStream_t s, int v) {
-  if (!x3hg_supported(p) || p.stride != 1) return false;
+  if (!x3hg_supported(p)) return false;
   switch (v) {
 #define HG_CASE(V, TW, WM, WN, TM, TN) \
   case V: hg_launch<TW, WM, WN, TM, TN>(p, s); return true;
@@ -475,12 +440,6 @@ void x3hg_prepare() {
                                       hg_lds_bytes(TW, WM, 1, TM, TN)));
   HG_PW_VARIANTS(HG_PW_ATTR)
 #undef HG_PW_ATTR
-#define HG_S2_ATTR(V, TW, WM, WN, TM, TN)                                                        \
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)conv_x3hg_kernel<TW, WM, WN, TM, TN, 0, 2>,    \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,                  \
-                                      hg_lds_bytes(TW, WM, WN, TM, TN, 2)));
-  HG_S2_VARIANTS(HG_S2_ATTR)
-#undef HG_S2_ATTR
 }
 
 }  // namespace arena

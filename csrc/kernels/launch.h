@@ -103,10 +103,6 @@ void x3hg_prepare();
 constexpr int kF32X3HGPw = 145;
 constexpr int kF32X3HGPwVariants = 6;
 bool conv_x3hg_pw(const ConvParams& p, hipStream_t s, int v);
-// ... stride 2 (the detector's downsampling 3x3 convs), variant v
-constexpr int kF32X3HGS2 = 151;
-constexpr int kF32X3HGS2Variants = 9;
-bool conv_x3hg_s2(const ConvParams& p, hipStream_t s, int v);
 bool conv_fc_f32(const ConvParams& p, hipStream_t s);
 void conv2d_f32(const ConvParams& p, hipStream_t s);
 

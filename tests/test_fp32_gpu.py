@@ -148,7 +148,6 @@ def test_conv_x3g_channel_slices_and_live_batch(device):
 
 
 X3HG_IMPLS = [131 + v for v in range(14)]  # x3hg: 3x3 s1 halo tiles, 32x32x16 MFMA, pre-split weights
-X3HG_S2_IMPLS = [151 + v for v in range(9)]  # ... stride 2
 
 
 @pytest.mark.parametrize(
@@ -159,9 +158,6 @@ X3HG_S2_IMPLS = [151 + v for v in range(9)]  # ... stride 2
         (3, 17, 32, 32, "silu", True, False, 1),     # C3 bottleneck 3x3 with residual
         (2, 12, 128, 64, None, False, True, 1),      # wide K, 2x upsampled copy, no activation
         (2, 9, 20, 48, "relu6", False, False, 1),    # Cin 20: a partial 16-channel chunk
-        (2, 40, 16, 32, "silu", False, False, 2),    # stride 2 over the s2d stem map (16 channels)
-        (2, 21, 64, 128, "silu", False, False, 2),   # stride 2, odd input size, partial tiles
-        (2, 10, 128, 256, "silu", False, False, 2),  # stride 2, 8 channel fragments
     ],
 )
 def test_conv_x3hg_matches_fp64(device, B, H, Cin, Cout, act, res, up, s):
@@ -182,7 +178,7 @@ def test_conv_x3hg_matches_fp64(device, B, H, Cin, Cout, act, res, up, s):
     xd = _nhwc(x32).to(device)
     rd = _nhwc(r).to(device) if res else None
     packed = AF.pack_weights(w32, b32, device, "fp32")
-    for impl in (X3HG_IMPLS if s == 1 else X3HG_S2_IMPLS):
+    for impl in X3HG_IMPLS:
         out2 = torch.full((B, 2 * Ho, 2 * Ho, Cout), float("nan"), device=device) if up else None
         y = AF.conv2d_nhwc(xd, w32, b32, stride=s, act=act, res=rd, packed=packed, impl=impl, out2=out2)
         torch.cuda.synchronize()
