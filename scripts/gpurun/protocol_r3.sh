@@ -18,4 +18,7 @@ esac
 [ "${ENVELOPE:-0}" != "0" ] && PPG=1
 timeout -k 10 1100 python scripts/serving_sweep.py --archs $ARCH --users $U --procs 4 --procs-per-gpu $PPG \
   --warmup 10 --measure 60 --cooldown 2 --runs 3 --out $O > $O/sweep.log 2>&1
+# keep what the analysis reads (summaries, CSV, hypotheses, the sweep log); server logs can exceed gpurun's
+# 64 MiB copy-back limit
+find $O -type f -size +2M -delete
 grep -h "users=" $O/sweep.log
