@@ -310,6 +310,7 @@ void prepare_kernels() {
   x3_halo_prepare();
   x3g_prepare();
   x3hg_prepare();
+  stem_s2_f32_prepare();
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)sppf_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
   done = true;

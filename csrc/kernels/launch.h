@@ -389,6 +389,10 @@ struct StemFusedParams {
   int ir_ys;
 };
 void stem_fused(const StemFusedParams& p, hipStream_t s);
+// fp32 detector front end (csrc/kernels/stem_x3.hip): letterbox -> stem -> 3x3 s2 conv with the stem map only in
+// LDS; w = pre-split stem planes / 255 [3 ky][2 slabs][16][3][32], w2 = pre-split [9 taps][32][3][16], y2 fp32
+void stem_s2_f32(const StemFusedParams& p, hipStream_t s);
+void stem_s2_f32_prepare();
 
 // ---------------------------------------------------------------- classification head (K13/K14)
 struct AvgPoolParams {

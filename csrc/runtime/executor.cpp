@@ -439,7 +439,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
     // field 47: activation precision of the op (0 bf16, 1 exact fp32; planner.OP_DTYPE_FIELD)
     const bool f32 = r[kDtypeField] == 1;
     const int eb = f32 ? 4 : 2;
-    if (f32 && (r[0] == OP_STEMFUSED || r[0] == OP_C3FUSED))
+    if (f32 && r[0] == OP_C3FUSED)
       throw std::runtime_error("op " + std::to_string(r[0]) + " has no fp32 kernel");
     switch (r[0]) {
       case OP_CONV: {
@@ -699,7 +699,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       case OP_STEMFUSED: {
         StemFusedParams p{};
         p.src = (int)r[1];
-        p.y = resolve(bk, sl, r[2], r[3], 2);
+        p.y = resolve(bk, sl, r[2], r[3], eb);
         p.ys = (int)r[4];
         p.S = (int)r[5];
         p.w = W + r[6];
@@ -736,7 +736,10 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.pool = pool;
         p.meta = meta;
         p.ctrl = ctrl;
-        stem_fused(p, s);
+        if (f32)
+          stem_s2_f32(p, s);  // fp32: letterbox + stem + 3x3 s2 conv (the only fp32 stem_fused form)
+        else
+          stem_fused(p, s);
         break;
       }
       case OP_HEADPOOL: {

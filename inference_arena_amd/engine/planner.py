@@ -226,6 +226,21 @@ def pack_pw_weight_x3(w2: torch.Tensor, k2: int) -> bytes:
     return bf16_raw_bytes(planes.contiguous())
 
 
+def pack_stem_s2_x3(w0: torch.Tensor, w1: torch.Tensor) -> tuple[bytes, bytes]:
+    """fp32 detector front end (csrc/kernels/stem_x3.hip): the s2d stem weights [16, 16, 3, 3] divided by 255
+    (the kernel stages the letterboxed uint8 values k) as bf16 planes [3 ky][2 slabs][16 ch][h|m|l][32 k]
+    (slab k = kx * 16 + c for k < 48, zero for 48..63), and the 3x3 s2 conv [32, 16, 3, 3] as
+    [9 taps][32 ch][h|m|l][16 c]."""
+    w0 = w0.detach().float() / 255.0
+    k = torch.zeros(16, 3, 64)
+    k[:, :, :48] = w0.permute(0, 2, 3, 1).reshape(16, 3, 48)  # [n][ky][kx * 16 + c]
+    p0 = split_bf16x3(k.reshape(16, 3, 2, 32))  # [n][ky][sl][3][32]
+    p0 = p0.permute(1, 2, 0, 3, 4).contiguous()  # [ky][sl][n][3][32]
+    w1 = w1.detach().float().permute(2, 3, 0, 1).reshape(9, 32, 16)  # [tap][n][c]
+    p1 = split_bf16x3(w1)  # [tap][n][3][16]
+    return bf16_raw_bytes(p0), bf16_raw_bytes(p1.contiguous())
+
+
 def pack_ir_weights(expand, dw, project, inp: int, k_align: int = 32) -> dict:
     """Padded operand layouts of the fused inverted-residual kernels (csrc/kernels/ir_block.hip, ir_f32.hip):
     we [hid_pad][inp_pad], wd [9][hid_pad], wp [oup_pad][hid_pad] + fp32 biases.  ``k_align``: inp_pad
@@ -557,13 +572,18 @@ class ProgramBuilder:
         kernel on the stem output kept in LDS; ``dst`` is then that conv's output (S/4 x S/4).
         ``ir=(dw, project)`` (classifier only): MobileNetV2 block 1 (t = 1, 32 -> 16, stride 1, no
         residual) runs on the stem output in LDS; ``dst`` is then the block's output (S/2 x S/2 x 16)."""
-        self._bf16_only("stem_fused")
+        if self.f32 and (second is None or crops is not None or ir is not None):
+            raise ValueError("stem_fused: the fp32 form is letterbox + stem + 3x3 s2 conv (csrc/kernels/stem_x3.hip)")
         cout, cin, ks, ks2 = w.shape
         if cin != 16 or ks != ks2:
             raise ValueError("stem_fused: weights must be [Cout, 16, KS, KS]")
         wb, bb, kpad, cpad = pack_conv_weight(w, b)
         if cpad != cout:
             raise ValueError("stem_fused: Cout must be a multiple of 16")
+        if self.f32:
+            if (cout, ks, second[0].shape) != (16, 3, (32, 16, 3, 3)):
+                raise ValueError("stem_fused: the fp32 kernel takes a 3x3 16 -> 16 stem and a 3x3 s2 16 -> 32 conv")
+            wb, wb2_x3 = pack_stem_s2_x3(w, second[0])
         w_off = self.weights.add(wb)
         b_off = self.weights.add(bb)
         src = 0 if crops is None else 1
@@ -586,6 +606,8 @@ class ProgramBuilder:
               [fbits(1.0 / s) for s in std] + [kind, ks]
         if second is not None:
             wb2, bb2, kpad2, _ = pack_conv_weight(w2, b2)
+            if self.f32:
+                wb2 = wb2_x3
             rec += [1, self.weights.add(wb2), kpad2, self.weights.add(bb2), co2, ACT[act2]]
         else:
             rec += [0] * 6

@@ -138,19 +138,27 @@ def fuse_letterbox_f32_default() -> bool:
     return os.environ.get("ARENA_F32_LB_STEM", "1").lower() not in ("0", "false", "no", "off")
 
 
+def fuse_stem_s2_f32_default() -> bool:
+    """``ARENA_F32_STEM_S2`` (default 1): fp32 programs run letterbox + stem + the 3x3 s2 conv as one kernel
+    (csrc/kernels/stem_x3.hip): the 320x320x16 fp32 stem map exists only in LDS.  0 keeps the letterbox-sampling
+    stem conv + a separate s2 conv (A/B switch)."""
+    return os.environ.get("ARENA_F32_STEM_S2", "1").lower() not in ("0", "false", "no", "off")
+
+
 def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool = False,
               fuse_stem: bool | None = None):
     h = T // 2
     w, b = fold(y.b0)
     if fuse_stem is None:
         fuse_stem = fuse_stem_default()
-    fuse_stem = fuse_stem and not pb.f32
+    # fp32: only the letterbox + stem + s2 conv form exists (csrc/kernels/stem_x3.hip, ARENA_F32_STEM_S2)
+    fuse_stem = fuse_stem and (not pb.f32 or fuse_stem_s2_f32_default())
     A1 = pb.tensor("b1", h // 2, h // 2, 32)
-    if fuse_stem and not tensor_input and fuse_stem2_default() and T % 64 == 0:
+    if fuse_stem and not tensor_input and (fuse_stem2_default() or pb.f32) and T % 64 == 0:
         # letterbox + stem + b1 (3x3 s2) in one kernel: the 320x320x16 stem output stays in LDS
         w1, b1 = fold(y.b1)
         pb.stem_fused(View(A1, 0, 32), s2d_stem_6x6(w), b, S=T, act="silu", second=(w1, b1, "silu"))
-    elif fuse_stem and not tensor_input:
+    elif fuse_stem and not tensor_input and not pb.f32:
         A0 = pb.tensor("b0", h, h, 16)
         pb.stem_fused(View(A0, 0, 16), s2d_stem_6x6(w), b, S=T, act="silu")
         pb.conv(View(A0, 0, 16), View(A1, 0, 32), *fold(y.b1), stride=2)

@@ -122,7 +122,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         if off < 0 or off + n > wbytes:
             raise ProgramError(f"op {i}: {what} reads weights [{off}, {off + n}) of {wbytes}")
 
-    fused = (OP_STEMFUSED, OP_C3FUSED)  # bf16-only fused kernels
+    fused = (OP_C3FUSED,)  # bf16-only fused kernels (fp32 stem_fused: the letterbox + stem + s2 conv form only)
     for i, r in enumerate(prog.ops):
         op = int(r[0])
         kind_n = lambda k: crop_cap if int(k) == CROPS else B  # noqa: E731
@@ -243,11 +243,14 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
             expect = {0: (3, 16, 160, 0), 1: (2, 32, 64, CROPS)}.get(src)
             if expect is None or (ks, cout, kpad, kind) != expect or S % 2:
                 raise ProgramError(f"op {i}: bad stem_fused geometry (src {src}, KS {ks}, Cout {cout}, Kpad {kpad})")
+            if f32 and not int(r[20]):
+                raise ProgramError(f"op {i}: an fp32 stem_fused op must carry the fused second conv")
             if int(r[20]):  # second conv fused: 3x3 s2 16 -> 32, output S/4
                 if src != 0 or int(r[24]) != 32 or int(r[22]) != 160 or S % 64:
                     raise ProgramError(f"op {i}: bad fused second conv (Cout2 {int(r[24])}, Kpad2 {int(r[22])})")
-                view(i, r[2], int(r[3]), int(r[4]), n * (S // 4) ** 2, 32, 2, "stem second-conv output")
-                weights(i, int(r[21]), 32 * 160 * 2, "stem second-conv weight")
+                view(i, r[2], int(r[3]), int(r[4]), n * (S // 4) ** 2, 32, el, "stem second-conv output")
+                # fp32 (stem_x3.hip): pre-split planes [9 taps][32][3][16]; bf16: [32][160]
+                weights(i, int(r[21]), 9 * 32 * 3 * 16 * 2 if f32 else 32 * 160 * 2, "stem second-conv weight")
                 weights(i, int(r[23]), 32 * 4, "stem second-conv bias")
             elif int(r[26]):  # first inverted residual fused: 32 -> 16 at S/2
                 if src != 1 or int(r[31]) != 16 or S % 32:
@@ -260,7 +263,8 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 view(i, r[2], int(r[3]), int(r[4]), n * (S // 2) ** 2, cout, 2, "stem output")
             if src == 1:
                 need(i, r[11], 0, B * max_det * CROP_BYTES, "crop refs")
-            weights(i, int(r[6]), cout * kpad * 2, "stem weight")
+            # fp32: pre-split planes / 255 [3 ky][2 slabs][16][3][32]; bf16: [Cout][Kpad]
+            weights(i, int(r[6]), 3 * 2 * 16 * 3 * 32 * 2 if f32 else cout * kpad * 2, "stem weight")
             weights(i, int(r[8]), cout * 4, "stem bias")
         elif op == OP_ZERO:
             need(i, r[1], 0, int(r[2]) * kind_n(r[3]), "zero")

@@ -430,6 +430,7 @@ def test_fp32_letterbox_stem_matches_unfused(dense_models, device, monkeypatch):
     from inference_arena_amd.engine.planner import BUF_POOL, OP_CONV, OP_LETTERBOX
 
     imgs = synthetic_images(3, 71) + synthetic_images(1, 72, hw=(333, 500)) + synthetic_images(1, 73, hw=(640, 427))
+    monkeypatch.setenv("ARENA_F32_STEM_S2", "0")  # this test pins the letterbox-sampling stem conv alone
     monkeypatch.setenv("ARENA_F32_LB_STEM", "0")
     plain = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="fp32")
     monkeypatch.setenv("ARENA_F32_LB_STEM", "1")
@@ -440,6 +441,34 @@ def test_fp32_letterbox_stem_matches_unfused(dense_models, device, monkeypatch):
     a, b = plain.infer(imgs), fused.infer(imgs)
     for i in range(len(imgs)):
         x1, x2 = plain.read_buffer("b0", 8, i), fused.read_buffer("b0", 8, i)
+        np.testing.assert_allclose(x2, x1, rtol=1e-5, atol=1e-5)
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        if len(x):
+            np.testing.assert_allclose(y.boxes, x.boxes, rtol=2e-5, atol=5e-3)
+            np.testing.assert_array_equal(y.topk_idx[:, 0], x.topk_idx[:, 0])
+
+
+@pytest.mark.parametrize("th", ["4", "8"])
+def test_fp32_stem_s2_fused_matches_unfused(dense_models, device, monkeypatch, th):
+    """letterbox + stem + 3x3 s2 conv in one kernel (csrc/kernels/stem_x3.hip, ARENA_F32_STEM_S2; both tile
+    heights) vs the letterbox-sampling stem conv + a separate s2 conv: the same 160x160x32 map to fp32 rounding
+    and the same results, over unit-scale, bilinear and padded images and a partial batch."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+    from inference_arena_amd.engine.planner import OP_STEMFUSED
+
+    imgs = synthetic_images(3, 81) + synthetic_images(1, 82, hw=(333, 500)) + synthetic_images(1, 83, hw=(640, 427))
+    monkeypatch.setenv("ARENA_STEM_X3_TH", th)
+    monkeypatch.setenv("ARENA_F32_STEM_S2", "0")
+    plain = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="fp32")
+    monkeypatch.setenv("ARENA_F32_STEM_S2", "1")
+    fused = GpuPipeline(*dense_models, device=0, buckets=[8], share_buffers=False, dtype="fp32")
+    assert not any(int(op[0]) == OP_STEMFUSED for op in plain.program.ops)
+    assert any(int(op[0]) == OP_STEMFUSED for op in fused.program.ops)
+    a, b = plain.infer(imgs), fused.infer(imgs)
+    for i in range(len(imgs)):
+        x1, x2 = plain.read_buffer("b1", 8, i), fused.read_buffer("b1", 8, i)
         np.testing.assert_allclose(x2, x1, rtol=1e-5, atol=1e-5)
     for x, y in zip(a, b):
         assert len(x) == len(y)

@@ -33,6 +33,7 @@ SOURCES = [
     "kernels/conv_f32.hip",
     "kernels/gemm_x3.hip",
     "kernels/halo_x3g.hip",
+    "kernels/stem_x3.hip",
     "kernels/ir_f32.hip",
     "kernels/ir_crop_f32.hip",
     "kernels/ir_tile_x3.hip",
