@@ -32,6 +32,9 @@ SHAPES = {  # name: (B, H, Cin, Cout, k, stride)
     "head_144_40": (32, 40, 128, 144, 3, 1),
     "stem_16": (32, 160, 16, 16, 3, 1),
     "stem_s2": (32, 320, 16, 32, 3, 2),
+    "head_144_20": (32, 20, 256, 144, 3, 1),
+    "head_64_20": (32, 20, 64, 64, 3, 1),
+    "head_80_20": (32, 20, 80, 80, 3, 1),
     "det_s2_128_40": (32, 40, 128, 128, 3, 2),
     "det_s2_64_80": (32, 80, 64, 64, 3, 2),
 }
