@@ -1599,11 +1599,6 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
         throw std::runtime_error("conv2d_f32: not an x3g-eligible conv (needs pre-split weights)");
       return;
     }
-    if (p.impl >= kF32X3HG4 && p.impl < kF32X3HG4 + kF32X3HG4Variants) {
-      if (!conv_x3hg(p, s, kF32X3HGVariants + p.impl - kF32X3HG4))
-        throw std::runtime_error("conv2d_f32: not an x3hg-eligible conv (3x3 s1 with pre-split weights)");
-      return;
-    }
     if (p.impl >= kF32X3HG && p.impl < kF32X3HG + kF32X3HGVariants) {
       if (!conv_x3hg(p, s, p.impl - kF32X3HG))
         throw std::runtime_error("conv2d_f32: not an x3hg-eligible conv (3x3 s1 with pre-split weights)");

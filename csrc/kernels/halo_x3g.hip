@@ -374,12 +374,7 @@ void hg_launch(const ConvParams& p, hipStream_t s) {
   X(10, 8, 4, 1, 1, 3)  /* 16 x  8 px x  96 ch */ \
   X(11, 16, 8, 1, 1, 5) /* 16 x 16 px x 160 ch, 8 waves */ \
   X(12, 8, 2, 2, 1, 2)  /*  8 x  8 px x 128 ch */ \
-  X(13, 8, 2, 1, 1, 5)  /*  8 x  8 px x 160 ch, 2 waves */ \
-  X(14, 4, 1, 5, 1, 1)  /*  8 x  4 px x 160 ch, 5 waves (20x20 maps: 1.2x row padding) */ \
-  X(15, 4, 1, 4, 1, 1)  /*  8 x  4 px x 128 ch, 4 waves */ \
-  X(16, 4, 1, 2, 1, 2)  /*  8 x  4 px x 128 ch, 2 waves */ \
-  X(17, 4, 1, 1, 1, 5)  /*  8 x  4 px x 160 ch, 1 wave */ \
-  X(18, 4, 1, 2, 1, 1)  /*  8 x  4 px x  64 ch, 2 waves */
+  X(13, 8, 2, 1, 1, 5)  /*  8 x  8 px x 160 ch, 2 waves */
 
 // fused-1x1 variants v (kF32X3HGPw + v): (TW, WM, TM, TN, PWN), WN = 1
 #define HG_PW_VARIANTS(X) \

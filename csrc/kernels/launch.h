@@ -96,9 +96,6 @@ void x3g_prepare();
 // x3hg: 3x3 stride-1 halo tiles on 32x32x16 MFMAs over the same pre-split weights (halo_x3g.hip), variant v
 constexpr int kF32X3HG = 131;
 constexpr int kF32X3HGVariants = 14;
-// ... 4-column tiles for the 20x20 maps: impl kF32X3HG4 + v = x3hg variant 14 + v
-constexpr int kF32X3HG4 = 160;
-constexpr int kF32X3HG4Variants = 5;
 bool x3hg_supported(const ConvParams& p);
 bool conv_x3hg(const ConvParams& p, hipStream_t s, int v);  // false if the conv or variant is not supported
 void x3hg_prepare();

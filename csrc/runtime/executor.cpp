@@ -278,8 +278,7 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
                                 v == kF32Fc || v == kF32StreamExact || v == kF32X3Halo16 || v == kF32X3Halo16N3 ||
                                 v == kF32X3H16 || (v >= kF32X3G && v < kF32X3G + kF32X3GVariants) ||
                                 (v >= kF32X3HG && v < kF32X3HG + kF32X3HGVariants) ||
-                                (v >= kF32X3HGPw && v < kF32X3HGPw + kF32X3HGPwVariants) ||
-                                (v >= kF32X3HG4 && v < kF32X3HG4 + kF32X3HG4Variants)
+                                (v >= kF32X3HGPw && v < kF32X3HGPw + kF32X3HGPwVariants)
                           : v >= 0 && v <= 3;
       if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
       bk.impl[i] = (int16_t)v;
@@ -333,9 +332,7 @@ void Executor::autotune(Bucket& bk) {
                                        kF32X3HG + 7, kF32X3HG + 8, kF32X3HG + 9, kF32X3HG + 10,
                                        // ... with the fused Detect-head 1x1 (the only kernels that take those ops)
                                        kF32X3HGPw + 0, kF32X3HGPw + 1, kF32X3HGPw + 2, kF32X3HGPw + 3,
-                                       kF32X3HGPw + 4, kF32X3HGPw + 5,
-                                       // x3hg 4-column tiles (20x20 maps)
-                                       kF32X3HG4 + 0, kF32X3HG4 + 1, kF32X3HG4 + 2, kF32X3HG4 + 3, kF32X3HG4 + 4};
+                                       kF32X3HGPw + 4, kF32X3HGPw + 5};
   static const int kBf16Candidates[] = {1, 2, 3};
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;

@@ -147,7 +147,7 @@ def test_conv_x3g_channel_slices_and_live_batch(device):
         assert torch.all(out[:, :, :, :64] == 7.0) and torch.all(out[3] == 7.0), impl
 
 
-X3HG_IMPLS = [131 + v for v in range(14)] + [160 + v for v in range(5)]  # x3hg: 3x3 s1 halo tiles (+ 4-col)
+X3HG_IMPLS = [131 + v for v in range(14)]  # x3hg: 3x3 s1 halo tiles, 32x32x16 MFMA, pre-split weights
 
 
 @pytest.mark.parametrize(
