@@ -131,6 +131,10 @@ def test_health_metrics_and_concurrency(server):
     for t in ts:
         t.join()
     assert not errors and len(n_ok) == 48
+    # one failed request of this test's own (the module's other tests may run in another xdist worker)
+    st, data, c2 = _post(fe.port, b"not an image", "image/jpeg")
+    assert st == 500
+    c2.close()
     s = fe.stats()
     assert s["ok"] >= 48 and s["errors"] >= 1
     import time
