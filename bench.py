@@ -12,11 +12,15 @@ architectures/monolithic/app/main.py:102-159):
   keep-alive connections, multipart uploads of the curated workload, 3-5 detections per image).  A
   request is timed from the moment its upload starts on the client to the moment the client has
   parsed the complete JSON response:
-    HTTP + multipart parse -> JPEG decode (spawned decode processes, shared memory) -> native dynamic
-    batcher (max_batch 32) -> H2D -> letterbox -> YOLOv5nu -> decode -> NMS -> crop gather ->
-    MobileNetV2 -> top-5 -> D2H -> JSON response (the reference's schema) -> client.
-  ``--path inproc`` measures the same pipeline without the HTTP layer (JPEG bytes handed to the decode
-  pool, results read from the batcher callback); it is also reported as the secondary key ``inproc``.
+    HTTP + multipart parse -> split JPEG decode (native C++ threads: marker parse + Huffman decode into a
+    pinned buffer, csrc/runtime/jpeg_decode.h; PIL processes only for formats it does not cover) -> native
+    dynamic batcher (max_batch 32, zero-copy) -> H2D of the coefficients -> GPU dequant + IDCT + chroma
+    upsampling + YCbCr->RGB (csrc/kernels/jpeg_idct.hip, bit-exact with PIL) -> letterbox -> YOLOv5nu ->
+    decode -> NMS -> crop gather -> MobileNetV2 -> top-5 -> D2H -> JSON response (the reference's schema)
+    -> client.
+  ``--path inproc`` measures the same pipeline without the HTTP layer (uploads handed to the front end's
+  decode stage in process by a C++ closed loop, HttpFrontEnd::submit_local; the JSON is still built); it is
+  also reported as the secondary key ``inproc``.
 * precision: ``--dtype fp32`` (default) runs the fp32-accurate kernels, the reference's fp32 ONNX
   Runtime numerics (reference experiment.yaml:202,207,220,225); ``bf16`` the tuned bf16 kernels.
 * steady state: the clients run continuously from the warm-up into the timed window, so the window
@@ -36,8 +40,12 @@ and N > 1, bench.py launches ``torch.distributed.run`` itself as a child process
 and exits with its code.
 
 Secondary keys: ``inproc`` (same pipeline, no HTTP layer), ``engine_req_s`` (device pipeline fed
-pre-decoded images), ``bf16`` (the end-to-end measurement on the bf16 kernels, in process),
-``levels`` (1/10/100 users), ``per_rank_req_s``, ``cpu_share`` per rank.
+pre-decoded images), ``bf16`` (the same HTTP measurement on the bf16 kernels: the host ceiling),
+``levels`` (1/10/100 users), ``per_rank_req_s``, ``usable_cpus_per_rank`` (pinned share capped by the job's
+cgroup quota divided between the ranks), ``host_cpu_us_per_req`` (host CPU per request by thread class:
+HTTP I/O, decode, batcher + JSON, load generator, ...; ``stage_cpu_us_per_req``: HTTP parse, entropy decode,
+JSON from thread CPU clocks), ``mean_batch``, ``shared_front`` (N > 1: every rank on one SO_REUSEPORT port
+driven by one node-level load generator; ``--front shared`` makes that the headline).
 
 ``--fake-engine`` replaces the GPU pipeline by the host-only EchoInstance (CPU tests of the whole
 harness, including the N-rank path over gloo: ARENA_DIST_BACKEND=gloo).
@@ -67,19 +75,6 @@ METRIC = "req/sec (whole node) + P50/P99 e2e latency, YOLOv5n→MobileNetV2 at 1
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
-
-
-def host_cpus() -> int:
-    """CPUs this job may use: the affinity mask, capped by a cgroup-v2 CPU quota (cpu.max) when one is set —
-    on the GPU pool the mask shows the whole machine while the quota is the job's share."""
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
-    try:
-        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
-        if quota != "max":
-            n = min(n, max(1, int(int(quota) / int(period))))
-    except (OSError, ValueError):
-        pass
-    return n
 
 
 def self_launch(argv: list[str], n: int) -> int:
@@ -133,85 +128,6 @@ def http_request(jpeg: bytes) -> bytes:
             f"Content-Length: {len(body)}\r\n\r\n").encode() + body
 
 
-class ClosedLoop:
-    """``users`` in-process closed-loop clients: JPEG -> decode pool -> native batcher -> result -> next."""
-
-    def __init__(self, pool, batcher, jpegs: list[bytes], users: int, offset: int = 0):
-        self.pool, self.batcher, self.jpegs, self.users = pool, batcher, jpegs, users
-        self.lock = threading.Lock()
-        self.cv = threading.Condition(self.lock)
-        self.done = 0
-        self.errors = 0
-        self.lat: list[float] = []    # per completed request, completion order
-        self.crops: list[int] = []
-        self.batch: list[int] = []
-        self.next_img = offset
-        self.running = False
-        self.in_flight = 0
-
-    def _issue(self) -> None:
-        with self.lock:
-            if not self.running:
-                return
-            i = self.next_img % len(self.jpegs)
-            self.next_img += 1
-            self.in_flight += 1
-        self.pool.submit(self.jpegs[i], time.perf_counter(), self._decoded)
-
-    def _decoded(self, t0, img, err) -> None:
-        if err is not None or img is None:
-            self._complete(t0, None)
-            return
-
-        def done(d, t0=t0):
-            self._complete(t0, d)
-
-        if self.batcher.enqueue(img, done) < 0:
-            self._complete(t0, None)
-
-    def _complete(self, t0, d) -> None:
-        t1 = time.perf_counter()
-        with self.lock:
-            self.in_flight -= 1
-            if d is None or d.get("error"):
-                self.errors += 1
-            else:
-                self.lat.append(t1 - t0)
-                self.crops.append(int(d["topk_idx"].shape[0]))
-                self.batch.append(int(d["batch_size"]))
-                self.done += 1
-            self.cv.notify_all()
-        self._issue()
-
-    def start(self) -> None:
-        self.running = True
-        for _ in range(self.users):
-            self._issue()
-
-    def completed(self) -> int:
-        with self.lock:
-            return self.done
-
-    def wait_for(self, n: int, timeout: float = 600.0) -> None:
-        deadline = time.time() + timeout
-        with self.lock:
-            while self.done < n:
-                if self.errors > 100 and self.done == 0:
-                    raise RuntimeError(f"{self.errors} failed requests and none completed")
-                left = deadline - time.time()
-                if left <= 0:
-                    raise TimeoutError(f"only {self.done}/{n} requests completed")
-                self.cv.wait(min(left, 1.0))
-
-    def stop(self) -> None:
-        with self.lock:
-            self.running = False
-        deadline = time.time() + 60
-        with self.lock:
-            while self.in_flight > 0 and time.time() < deadline:
-                self.cv.wait(0.5)
-
-
 def engine_throughput(ex, images, B: int, batches: int) -> float:
     """Device pipeline alone (pre-decoded images, pipelined submit/collect): requests/s between the
     completion of the first ``depth`` batches and the last one (fill and drain excluded)."""
@@ -231,7 +147,7 @@ def engine_throughput(ex, images, B: int, batches: int) -> float:
     return (len(done_t) - depth) * B / (done_t[-1] - done_t[depth - 1])
 
 
-def _window(a, info, D, sync, completed, wait_until, users: int):
+def _window(a, info, D, sync, completed, wait_until, users: int, on_open=None):
     """Warm-up (>= --warmup steps, >= 4 requests per user, >= --min-warmup-s), barrier + sync, then the window
     of exactly --steps steps; returns (seconds, first completion index of the window)."""
     R = a.batch * a.step_batches
@@ -243,6 +159,8 @@ def _window(a, info, D, sync, completed, wait_until, users: int):
     sync()
     gc.disable()  # no collector pauses inside the window
     try:
+        if on_open is not None:
+            on_open()
         c0 = completed()
         t0 = time.perf_counter()
         wait_until(c0 + a.steps * R)
@@ -261,42 +179,105 @@ def batcher_config(a) -> dict:
             "max_queue_size": 0}
 
 
-def measure_http(port: int, reqs: list[bytes], a, info, D, sync, users: int):
-    """Closed-loop HTTP window on one rank: (seconds, latencies s, detections, statuses)."""
+def _thread_cpu() -> dict[str, float]:
+    """CPU seconds (user + system) of this process's threads, summed by thread name (native threads name
+    themselves: arena-http-io, arena-jpeg, arena-batcher, arena-pack, arena-loadgen, arena-collect)."""
+    out: dict[str, float] = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    for d in Path("/proc/self/task").iterdir():
+        try:
+            stat = (d / "stat").read_text()
+        except OSError:
+            continue
+        name = stat[stat.index("(") + 1:stat.rindex(")")]
+        f = stat[stat.rindex(")") + 2:].split()
+        out[name] = out.get(name, 0.0) + (int(f[11]) + int(f[12])) / tick
+    return out
+
+
+def _children_cpu() -> float:
+    t = os.times()
+    return t.children_user + t.children_system
+
+
+class HostCpu:
+    """Host CPU per request over a window, by thread class (+ the decode-pool child processes)."""
+
+    GROUPS = {"arena-http-io": "http_io", "arena-jpeg": "decode", "arena-batcher": "batcher_json",
+              "arena-pack": "pack", "arena-loadgen": "loadgen", "arena-collect": "pil_collect"}
+
+    def __init__(self, fe=None):
+        self.fe = fe
+        self.t0, self.c0 = _thread_cpu(), _children_cpu()
+        self.s0 = fe.stats() if fe is not None else None
+
+    def per_request(self, n: int) -> tuple[dict, dict]:
+        t1, c1 = _thread_cpu(), _children_cpu()
+        by: dict[str, float] = {}
+        for name, v in t1.items():
+            g = self.GROUPS.get(name, "other")
+            by[g] = by.get(g, 0.0) + v - self.t0.get(name, 0.0)
+        by["pil_procs"] = c1 - self.c0
+        us = {k: round(v / max(1, n) * 1e6, 1) for k, v in sorted(by.items())}
+        us["total"] = round(sum(by.values()) / max(1, n) * 1e6, 1)
+        stages = {}
+        if self.fe is not None:
+            s1 = self.fe.stats()
+            for k, key in (("http_parse", "cpu_parse_ms"), ("entropy_decode", "cpu_decode_ms"), ("json", "cpu_json_ms")):
+                stages[k] = round((s1[key] - self.s0[key]) / max(1, n) * 1e3, 2)
+            stages["native_decoded"] = s1["native_decoded"] - self.s0["native_decoded"]
+            stages["fallback_decoded"] = s1["fallback_decoded"] - self.s0["fallback_decoded"]
+        return us, stages
+
+
+def _batch_mean(b0: dict, b1: dict) -> float | None:
+    """Mean executed batch size between two batcher stats snapshots."""
+    nb = b1["batches"] - b0["batches"]
+    return round((b1["requests"] - b0["requests"]) / nb, 2) if nb > 0 else None
+
+
+def measure_http(port: int, reqs: list[bytes], a, info, D, sync, users: int, threads: int, fe=None, batcher=None):
+    """Closed-loop HTTP window on one rank: (seconds, latencies s, detections, statuses, extras)."""
     from inference_arena_amd.ops import native
 
     lg = native().HttpLoadGen({"host": "127.0.0.1", "port": port, "users": users,
-                               "threads": max(1, min(a.lg_threads, users))}, reqs)
+                               "threads": max(1, min(threads, users))}, reqs)
+    return _measure(lg, a, info, D, sync, users, fe, batcher)
+
+
+def measure_inproc(fe, uploads: list[bytes], a, info, D, sync, users: int, batcher=None):
+    """The same window without the HTTP layer: a C++ closed loop submits the uploads to the front end's decode
+    stage in process (HttpFrontEnd::submit_local); decode, batching, device, JSON unchanged."""
+    from inference_arena_amd.ops import native
+
+    lg = native().LocalLoadGen(fe, uploads, users)
+    return _measure(lg, a, info, D, sync, users, fe, batcher)
+
+
+def _measure(lg, a, info, D, sync, users, fe, batcher):
     lg.start()
 
     def wait_until(n):
         if not lg.wait_completed(n, 600.0):
-            raise TimeoutError(f"HTTP load generator: {lg.completed()}/{n} responses "
-                               f"({lg.connect_failures()} failed connects)")
+            extra = f" ({lg.connect_failures()} failed connects)" if hasattr(lg, "connect_failures") else ""
+            raise TimeoutError(f"load generator: {lg.completed()}/{n} responses{extra}")
+    cpu = {}
     try:
-        window, c0 = _window(a, info, D, sync, lg.completed, wait_until, users)
+        holder = {}
+
+        def opened():
+            holder["cpu"] = HostCpu(fe)
+            holder["b0"] = batcher.stats() if batcher is not None else None
+        window, c0 = _window(a, info, D, sync, lg.completed, wait_until, users, on_open=opened)
+        n = a.steps * a.batch * a.step_batches
+        us, stages = holder["cpu"].per_request(n)
+        cpu = {"host_cpu_us_per_req": us, "stage_cpu_us_per_req": stages}
+        if batcher is not None:
+            cpu["mean_batch"] = _batch_mean(holder["b0"], batcher.stats())
     finally:
         lg.stop(60.0)
     r = lg.records(c0, c0 + a.steps * a.batch * a.step_batches)
-    return window, r["latency"].astype(np.float64), r["dets"].astype(np.int64), r["status"].astype(np.int64)
-
-
-def measure_inproc(ex, pool, jpegs, a, info, D, sync):
-    """The closed-loop window without the HTTP layer: (seconds, latencies, crops, batch sizes, errors)."""
-    from inference_arena_amd.ops import native
-
-    batcher = native().DynamicBatcher([ex], batcher_config(a))
-    loop = ClosedLoop(pool, batcher, jpegs, a.users, offset=(info.rank * 37) % len(jpegs))
-    gc.collect()
-    gc.freeze()
-    loop.start()
-    try:
-        window, c0 = _window(a, info, D, sync, loop.completed, loop.wait_for, a.users)
-    finally:
-        loop.stop()
-        batcher.shutdown()
-    n = a.steps * a.batch * a.step_batches
-    return window, loop.lat[c0:c0 + n], loop.crops[c0:c0 + n], loop.batch[c0:c0 + n], loop.errors
+    return (window, r["latency"].astype(np.float64), r["dets"].astype(np.int64), r["status"].astype(np.int64), cpu)
 
 
 def latency_levels(port: int, reqs: list[bytes], levels: list[int], a) -> dict:
@@ -305,6 +286,7 @@ def latency_levels(port: int, reqs: list[bytes], levels: list[int], a) -> dict:
 
     out = {}
     for u in levels:
+        log(f"level {u} users")
         n_warm, n_meas = max(30, 3 * u), max(300, 20 * u)
         lg = native().HttpLoadGen({"host": "127.0.0.1", "port": port, "users": u, "threads": max(1, min(2, u))},
                                   reqs)
@@ -339,6 +321,24 @@ class FakeEngine:
         return self.weights.tobytes()
 
 
+def make_front(batcher, pool, plan: dict, a, port: int = 0, reuse_port: bool = True, jpeg_device: bool = True):
+    from inference_arena_amd.labels import load_labels
+    from inference_arena_amd.ops import native
+    from inference_arena_amd.processing.transforms import max_image_pixels
+
+    return native().HttpFrontEnd(batcher, pool.native_channel(), list(load_labels(None)),
+                                 {"host": "127.0.0.1", "port": port, "io_threads": plan["http_io"],
+                                  "decode_threads": plan["decode_threads"], "jpeg_device": jpeg_device,
+                                  "max_image_pixels": max_image_pixels(), "reuse_port": reuse_port})
+
+
+def summarize(window: float, lat, a, info, D) -> dict:
+    w = D.allreduce_max(window, info)
+    flat = np.asarray([x for lst in D.allgather_floats([float(x) for x in lat], info) for x in lst]) * 1e3
+    return {"value": round(a.steps * a.batch * a.step_batches * info.world / w, 2),
+            "p50_ms": round(float(np.percentile(flat, 50)), 3), "p99_ms": round(float(np.percentile(flat, 99)), 3)}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -356,10 +356,17 @@ def main(argv=None) -> int:
     ap.add_argument("--users", type=int, default=256, help="closed-loop clients per GPU")
     ap.add_argument("--path", default="http", choices=["http", "inproc"],
                     help="http: clients upload over HTTP to the native front end (headline); inproc: no HTTP layer")
+    ap.add_argument("--front", default="per-rank", choices=["per-rank", "shared"],
+                    help="per-rank: one port + load generator per rank, value = sum (headline); shared: all ranks "
+                         "on one SO_REUSEPORT port driven by one node-level load generator on rank 0")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--decode-workers", type=int, default=0, help="JPEG decode processes per rank (0: auto)")
-    ap.add_argument("--http-threads", type=int, default=4, help="epoll I/O threads of the native front end")
-    ap.add_argument("--lg-threads", type=int, default=2, help="load-generator threads per rank")
+    ap.add_argument("--decode-threads", type=int, default=0, help="native split-decoder threads per rank (0: plan)")
+    ap.add_argument("--decode-workers", type=int, default=0,
+                    help="PIL decode processes per rank (fallback for uploads the split decoder leaves; 0: plan)")
+    ap.add_argument("--host-decode", action="store_true",
+                    help="reconstruct on the host decode threads instead of the GPU (A/B of the split decoder)")
+    ap.add_argument("--http-threads", type=int, default=0, help="epoll I/O threads of the native front end (0: plan)")
+    ap.add_argument("--lg-threads", type=int, default=0, help="load-generator threads per rank (0: plan)")
     ap.add_argument("--queue-delay-us", type=int, default=2000)
     ap.add_argument("--jpeg-quality", type=int, default=90)
     ap.add_argument("--seed", type=int, default=0, help="weight seed")
@@ -370,7 +377,9 @@ def main(argv=None) -> int:
     ap.add_argument("--secondary-inproc", action=argparse.BooleanOptionalAction, default=True,
                     help="also measure the pipeline without the HTTP layer (secondary key 'inproc')")
     ap.add_argument("--secondary-bf16", action=argparse.BooleanOptionalAction, default=True,
-                    help="also measure the bf16 kernels (secondary key 'bf16': e2e in process, engine req/s)")
+                    help="also measure the bf16 kernels over HTTP (secondary key 'bf16': the host ceiling)")
+    ap.add_argument("--secondary-shared-front", action=argparse.BooleanOptionalAction, default=True,
+                    help="N > 1: also measure one node-level front door (secondary key 'shared_front')")
     ap.add_argument("--crop-cap", type=int, default=None)
     ap.add_argument("--fake-engine", action="store_true", help="host-only EchoInstance instead of the GPU (CPU tests)")
     a = ap.parse_args(argv)
@@ -387,21 +396,27 @@ def main(argv=None) -> int:
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
 
     # this rank's host CPUs next to its GPU (sysfs only: nothing has touched the GPU yet); the decode workers
-    # are spawned after the pin and inherit it
-    from inference_arena_amd.parallel.affinity import pin, rank_cpu_share
+    # are spawned after the pin and inherit it.  The usable count is that share capped by the job's cgroup
+    # quota divided between the node's ranks (every rank sees the whole quota).
+    from inference_arena_amd.parallel.affinity import host_thread_plan, pin, rank_cpu_share, usable_cpus_per_rank
 
     share = rank_cpu_share(local_rank, local_world) if not a.fake_engine else None
     pinned = pin(share)
-    ncpu = host_cpus()
+    usable = usable_cpus_per_rank(share if pinned else None, local_world)
+    plan = host_thread_plan(usable)
+    for key, arg in (("http_io", a.http_threads), ("decode_threads", a.decode_threads),
+                     ("loadgen", a.lg_threads), ("pil_procs", a.decode_workers)):
+        if arg:
+            plan[key] = arg
+    budget_warning = None
+    if usable < 4:
+        budget_warning = (f"rank {local_rank}: only {usable} usable CPUs (pinned share {len(share) if share else '-'}, "
+                          f"job quota split {local_world} ways): the host path will bound this rank")
+        log("!" * 20 + " " + budget_warning + " " + "!" * 20)
     from inference_arena_amd.server.decode_pool import ProcessDecodePool, prestart
 
     prestart()
-    # 10 decode processes (~8.5k decodes/s) keep a GPU's engine fed; more of them compete with the batcher /
-    # HTTP threads for the box's CPU share (16-CPU box: 15 workers 6.0-6.4k req/s, 8-10 workers 6.78k;
-    # profiles/r2_decode_workers_sweep.md)
-    workers = a.decode_workers or max(2, min(10, ncpu // max(1, world if not pinned else 1) - 1))
-    pool = ProcessDecodePool(workers=workers, slots=max(256, a.users + 64), native=a.path == "http",
-                             cpus=share if pinned else None)
+    pool = ProcessDecodePool(workers=plan["pil_procs"], slots=64, native=True, cpus=share if pinned else None)
 
     torch = None
     if not a.fake_engine:
@@ -422,7 +437,7 @@ def main(argv=None) -> int:
         if torch is not None:
             torch.cuda.synchronize()
 
-    fe = None
+    fronts = []
     try:
         t0 = time.time()
         if a.fake_engine:
@@ -462,9 +477,9 @@ def main(argv=None) -> int:
         weights_verified = all(d == ref_digest for d in digests)
         if not weights_verified:
             raise RuntimeError(f"replica weights differ after the broadcast: {digests} vs rank 0 {ref_digest}")
-        cpu_note = (f"pinned to {len(share)} NUMA-local CPUs" if pinned else "not pinned") + f", {ncpu} usable"
+        cpu_note = (f"pinned to {len(share)} NUMA-local CPUs" if pinned else "not pinned") + f", {usable} usable"
         log(f"[rank {info.rank}/{info.world} {info.backend}] {a.dtype} pipeline ready in {time.time() - t0:.1f}s; "
-            f"arena MB {({b: round(v / 2**20, 1) for b, v in pipe.arena_bytes.items()})}; decode workers {workers}; "
+            f"arena MB {({b: round(v / 2**20, 1) for b, v in pipe.arena_bytes.items()})}; host plan {plan}; "
             f"{cpu_note}; weights verified")
 
         if a.fake_engine:
@@ -477,49 +492,93 @@ def main(argv=None) -> int:
         jpegs = [encode_jpeg(im, a.jpeg_quality) for im in images]
         off = (info.rank * 37) % len(jpegs)
         jpegs_r = jpegs[off:] + jpegs[:off]
-
-        from inference_arena_amd.labels import load_labels
+        reqs = [http_request(j) for j in jpegs_r]
+        jpeg_device = not (a.fake_engine or a.host_decode)
 
         levels = {}
         sec: dict = {}
+        extras: dict = {}
         R = a.batch * a.step_batches
-        if a.path == "http":
-            batcher = native().DynamicBatcher([ex], batcher_config(a))
-            fe = native().HttpFrontEnd(batcher, pool.native_channel(), list(load_labels(None)),
-                                       {"host": "127.0.0.1", "port": 0, "io_threads": a.http_threads})
-            reqs = [http_request(j) for j in jpegs_r]
-            gc.collect()
-            gc.freeze()
-            window, lat, crops, status = measure_http(fe.port, reqs, a, info, D, sync, a.users)
+
+        def serve(engine, cfg=None, port=0, reuse=True):
+            b = native().DynamicBatcher([engine], cfg or batcher_config(a))
+            f = make_front(b, pool, plan, a, port=port, reuse_port=reuse, jpeg_device=jpeg_device)
+            fronts.append((f, b))
+            return f, b
+
+        def close(f, b):
+            f.stop()
+            b.shutdown()
+            fronts.remove((f, b))
+
+        # one front end at a time: they share the PIL fallback pool's pipes (one DecodeChannel, one reader)
+        gc.collect()
+        gc.freeze()
+        headline_shared = a.front == "shared" and info.world > 1
+        errs = 0
+        if not headline_shared:
+            fe, batcher = serve(ex)
+            if a.path == "http":
+                window, lat, crops, status, extras = measure_http(fe.port, reqs, a, info, D, sync, a.users,
+                                                                  plan["loadgen"], fe, batcher)
+            else:
+                window, lat, crops, status, extras = measure_inproc(fe, jpegs_r, a, info, D, sync, a.users, batcher)
+            close(fe, batcher)
             errs = int((status != 200).sum())
             lat = list(lat)
-            bs = []
-            fe.stop()
-            fe = None
-            batcher.shutdown()
-            if info.is_main and a.latency_levels:
-                # the reference's low user levels behind a batcher with a short busy delay (a lone request
-                # waits 100 us, a loaded device 500 us for its batch to fill), on the same decode processes
-                cfg = dict(batcher_config(a), max_queue_delay_us=a.level_delay_us)
-                batcher = native().DynamicBatcher([ex], cfg)
-                fe = native().HttpFrontEnd(batcher, pool.native_channel(), list(load_labels(None)),
-                                           {"host": "127.0.0.1", "port": 0, "io_threads": a.http_threads})
-                levels = latency_levels(fe.port, reqs, [int(u) for u in a.latency_levels.split(",") if u], a)
-                levels["batcher"] = {"max_queue_delay_us": cfg["max_queue_delay_us"],
-                                     "idle_queue_delay_us": cfg["idle_queue_delay_us"]}
-                fe.stop()
-                fe = None
-                batcher.shutdown()
+            log(f"[rank {info.rank}] headline window: {a.steps * R / window:.0f} req/s")
+        if a.path == "http" and info.is_main and a.latency_levels:
+            # the reference's low user levels behind a batcher with a short busy delay (a lone request waits
+            # 100 us, a loaded device 500 us for its batch to fill)
+            cfg = dict(batcher_config(a), max_queue_delay_us=a.level_delay_us)
+            f2, b2 = serve(ex, cfg)
+            levels = latency_levels(f2.port, reqs, [int(u) for u in a.latency_levels.split(",") if u], a)
+            log(f"[rank {info.rank}] latency levels: {levels}")
+            levels["batcher"] = {"max_queue_delay_us": cfg["max_queue_delay_us"],
+                                 "idle_queue_delay_us": cfg["idle_queue_delay_us"]}
+            close(f2, b2)
+        D.barrier(info)
+        if a.path == "http" and a.secondary_inproc and not headline_shared:
+            f5, b5 = serve(ex)
+            w2, lat2, _, st2, _ = measure_inproc(f5, jpegs_r, a, info, D, sync, a.users, b5)
+            close(f5, b5)
+            sec["inproc"] = dict(summarize(w2, lat2, a, info, D), errors=int((st2 != 200).sum()))
+        if info.world > 1 and (a.secondary_shared_front or headline_shared):
+            # one node-level front door: every rank listens on the same port (SO_REUSEPORT spreads the
+            # connections), one load generator on rank 0 drives users x world connections
+            import socket
+
+            port = 0
+            if info.is_main:
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    port = sk.getsockname()[1]
+            port = D.broadcast_object(port, info)
+            f3, b3 = serve(ex, port=port)
             D.barrier(info)
-            pool.to_python_mode()
-            if a.secondary_inproc:
-                w2, lat2, _, _, _ = measure_inproc(ex, pool, jpegs, a, info, D, sync)
-                w2 = D.allreduce_max(w2, info)
-                sec["inproc"] = {"value": round(a.steps * R * info.world / w2, 2),
-                                 "p50_ms": round(float(np.percentile(lat2, 50)) * 1e3, 3),
-                                 "p99_ms": round(float(np.percentile(lat2, 99)) * 1e3, 3)}
-        else:
-            window, lat, crops, bs, errs = measure_inproc(ex, pool, jpegs, a, info, D, sync)
+            res = None
+            if info.is_main:
+                # world x the per-rank step: the same requests per GPU as the per-rank windows
+                a_node = argparse.Namespace(**vars(a))
+                a_node.step_batches = a.step_batches * info.world
+                res = measure_http(port, reqs, a_node, _Solo(), _SoloD(), sync, a.users * info.world,
+                                   plan["loadgen"] * 2, f3, b3)
+            D.barrier(info)
+            close(f3, b3)
+            if info.is_main:
+                w3, lat3, crops3, st3, ex3 = res
+                shared = {"value": round(a.steps * R * info.world / w3, 2),
+                          "p50_ms": round(float(np.percentile(lat3, 50)) * 1e3, 3),
+                          "p99_ms": round(float(np.percentile(lat3, 99)) * 1e3, 3), "errors": int((st3 != 200).sum()),
+                          "users": a.users * info.world, "ports": 1, "mean_batch": ex3.get("mean_batch")}
+                sec["shared_front"] = shared
+                if headline_shared:
+                    window, lat, crops, extras = w3, list(lat3), crops3, ex3
+                    errs = shared["errors"]
+            if headline_shared:
+                window = D.broadcast_object(window if info.is_main else None, info)
+                if not info.is_main:
+                    lat, crops = [], np.zeros(0)
         t_max = D.allreduce_max(window, info)
         per_rank = D.allgather_floats([a.steps * R / window], info)
 
@@ -528,19 +587,22 @@ def main(argv=None) -> int:
             eng = engine_throughput(ex, images, a.batch, a.engine_batches)
         if not a.fake_engine and a.secondary_bf16 and a.dtype != "bf16":
             alt = GpuPipeline(yolo, mnet, device=dev, buckets=buckets, crop_cap_per_image=a.crop_cap, dtype="bf16")
-            w2, lat2, _, _, _ = measure_inproc(alt.ex, pool, jpegs, a, info, D, sync)
-            w2 = D.allreduce_max(w2, info)
-            sec["bf16"] = {"value": round(a.steps * R * info.world / w2, 2),
-                           "p50_ms": round(float(np.percentile(lat2, 50)) * 1e3, 3),
-                           "p99_ms": round(float(np.percentile(lat2, 99)) * 1e3, 3),
-                           "path": "inproc",
-                           "engine_req_s": round(engine_throughput(alt.ex, images, a.batch, a.engine_batches), 1)}
+            f4, b4 = serve(alt.ex)
+            if a.path == "http":
+                w4, lat4, _, st4, ex4 = measure_http(f4.port, reqs, a, info, D, sync, a.users, plan["loadgen"], f4, b4)
+            else:
+                w4, lat4, _, st4, ex4 = measure_inproc(f4, jpegs_r, a, info, D, sync, a.users, b4)
+            close(f4, b4)
+            sec["bf16"] = dict(summarize(w4, lat4, a, info, D), path=a.path, errors=int((st4 != 200).sum()),
+                               mean_batch=ex4.get("mean_batch"), host_cpu_us_per_req=ex4.get("host_cpu_us_per_req"),
+                               engine_req_s=round(engine_throughput(alt.ex, images, a.batch, a.engine_batches), 1))
 
         all_lat = D.allgather_floats([float(x) for x in lat], info)
         all_crops = D.allgather_floats([float(c) for c in crops], info)
         all_eng = D.allgather_floats([eng or 0.0], info)
         all_err = D.allgather_floats([float(errs)], info)
-        all_cpu = D.allgather_floats([float(len(share)) if pinned else float(ncpu)], info)
+        all_cpu = D.allgather_floats([float(usable)], info)
+        all_ext = D.allgather_objects(extras, info)
         D.barrier(info)
         if info.is_main:
             flat = np.asarray([x for lst in all_lat for x in lst]) * 1e3
@@ -548,9 +610,10 @@ def main(argv=None) -> int:
             fan = float(np.sum([x for lst in all_crops for x in lst]) / max(1, len(flat)))
             value = total_req / t_max
             cpu_budget = min(x[0] for x in all_cpu)
-            if cpu_budget < value / info.world / 1000.0:
-                log(f"warning: {cpu_budget:.0f} CPUs per rank for {value / info.world:.0f} req/s per rank "
-                    f"(< 1 core per 1k req/s: host-bound)")
+            if cpu_budget < value / info.world / 1500.0:
+                log(f"warning: {cpu_budget:.0f} usable CPUs per rank for {value / info.world:.0f} req/s per rank "
+                    f"(< 1 core per 1.5k req/s: host-bound)")
+            ext0 = all_ext[0] or {}
             out = {
                 "metric": METRIC,
                 "value": round(value, 2),
@@ -566,9 +629,10 @@ def main(argv=None) -> int:
                 "data": ("synthetic COCO-shaped RGB images encoded as JPEG q%d (curated to 3-5 detections, mean "
                          "fan-out %.2f); random-init YOLOv5nu + MobileNetV2 weights; per-request end to end%s, "
                          "%d closed-loop users/GPU"
-                         % (a.jpeg_quality, fan, " over HTTP: multipart upload -> native front end -> JPEG decode "
-                            "-> dynamic batching -> full device pipeline -> JSON response" if a.path == "http" else
-                            ": JPEG decode + dynamic batching + full device pipeline + result split", a.users))
+                         % (a.jpeg_quality, fan, " over HTTP: multipart upload -> native front end -> split JPEG "
+                            "decode (host Huffman, GPU IDCT/colour) -> dynamic batching -> full device pipeline -> "
+                            "JSON response" if a.path == "http" else
+                            " in process: split JPEG decode + dynamic batching + full device pipeline + JSON", a.users))
                         + ("; FAKE ENGINE (host-only EchoInstance, CPU test)" if a.fake_engine else ""),
                 "config": {
                     "model": "YOLOv5nu(640)->MobileNetV2(224)",
@@ -580,18 +644,20 @@ def main(argv=None) -> int:
                     "users_per_gpu": a.users,
                     "image_size": 640,
                     "crop_size": 224,
-                    "decode_workers_per_gpu": workers,
+                    "host_plan_per_gpu": plan,
+                    "jpeg_decode": "host" if not jpeg_device else "split: host Huffman + GPU reconstruction",
                     "workload": ({"images": len(images), "distribution": man.distribution,
                                   "mean_detections": man.statistics.get("mean_detections")} if man else
                                  {"images": len(images)}),
                 },
                 "path": a.path,
+                "front": "shared" if headline_shared else "per-rank",
                 "p50_ms": round(float(np.percentile(flat, 50)), 3),
                 "p99_ms": round(float(np.percentile(flat, 99)), 3),
                 "latency": ("per-request end to end at the client (upload sent -> JSON response parsed)"
-                            if a.path == "http" else "per-request end to end (JPEG bytes in -> results out)"),
+                            if a.path == "http" else "per-request end to end (upload in -> JSON out, in process)"),
                 "mean_crops_per_request": round(fan, 3),
-                "mean_batch": round(float(np.mean(bs)), 2) if bs else None,
+                "mean_batch": ext0.get("mean_batch"),
                 "errors": int(sum(x for lst in all_err for x in lst)),
                 "engine_req_s": round(float(sum(x for lst in all_eng for x in lst)), 1) if eng else None,
                 "levels": levels,
@@ -600,17 +666,32 @@ def main(argv=None) -> int:
                 "per_rank_req_s": [round(x[0], 1) for x in per_rank],
                 "collective_backend": info.backend,
                 "weights_verified": bool(weights_verified),
-                "cpu_share_per_rank": [int(x[0]) for x in all_cpu],
+                "usable_cpus_per_rank": [int(x[0]) for x in all_cpu],
+                "cpu_budget_warning": budget_warning,
+                "host_cpu_us_per_req": ext0.get("host_cpu_us_per_req"),
+                "stage_cpu_us_per_req": ext0.get("stage_cpu_us_per_req"),
                 "world_size_checked": info.world,
             }
             out.update(sec)
             print(json.dumps(out), flush=True)
     finally:
-        if fe is not None:
-            fe.stop()
+        for f, b in list(fronts):
+            f.stop()
+            b.shutdown()
         pool.close()
     D.shutdown(info)
     return 0
+
+
+class _Solo:
+    """A one-rank view for rank 0's node-level load generator (the other ranks wait at a barrier)."""
+    world, rank, is_main = 1, 0, True
+
+
+class _SoloD:
+    @staticmethod
+    def barrier(info):
+        pass
 
 
 if __name__ == "__main__":

@@ -9,6 +9,8 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "kernels/launch.h"
 #include "runtime/executor.h"
@@ -16,11 +18,16 @@
 #include "runtime/http_front.h"
 #include "runtime/http_loadgen.h"
 #include "runtime/ipc_buffer.h"
+#include "runtime/jpeg_decode.h"
 #include "runtime/batcher.h"
 #include "runtime/split.h"
 
 namespace py = pybind11;
 using namespace arena;
+
+namespace arena {
+void bind_jpeg(py::module& m);  // bindings_jpeg.cpp
+}
 
 namespace {
 
@@ -298,6 +305,7 @@ ExecutorConfig config_from(const py::dict& d) {
   c.crop_cap_per_image = get<int>(d, "crop_cap_per_image", c.crop_cap_per_image);
   c.min_crop_cap = get<int>(d, "min_crop_cap", c.min_crop_cap);
   c.pool_bytes_per_image = get<int64_t>(d, "pool_bytes_per_image", c.pool_bytes_per_image);
+  c.pool_factor = get<int>(d, "pool_factor", c.pool_factor);
   c.det_size = get<int>(d, "det_size", c.det_size);
   c.cls_size = get<int>(d, "cls_size", c.cls_size);
   c.host_threads = get<int>(d, "host_threads", c.host_threads);
@@ -305,10 +313,38 @@ ExecutorConfig config_from(const py::dict& d) {
   return c;
 }
 
-std::vector<InputImage> images_from(const py::list& imgs, std::vector<py::array>& keep) {
+// JPEG uploads given to Executor.submit / run as `bytes`: entropy-decoded here (host half of the split decoder),
+// reconstructed on the device by the executor.  The coefficients must outlive the asynchronous H2D copy, so a
+// submitted batch's holders stay registered until its collect().
+struct JpegHolder {
+  JpegInfo info;
+  std::vector<int16_t> coef;
+};
+using JpegKeep = std::vector<std::shared_ptr<JpegHolder>>;
+std::mutex g_jkeep_mu;
+std::map<std::pair<const void*, int>, JpegKeep> g_jkeep;
+
+std::vector<InputImage> images_from(const py::list& imgs, std::vector<py::array>& keep, JpegKeep* jkeep = nullptr) {
   std::vector<InputImage> v;
   v.reserve(imgs.size());
   for (auto h : imgs) {
+    if (py::isinstance<py::bytes>(h)) {
+      if (jkeep == nullptr) throw std::runtime_error("JPEG inputs are not accepted here");
+      const std::string data = h.cast<std::string>();
+      auto jh = std::make_shared<JpegHolder>();
+      std::string err;
+      JpegStatus st = jpeg_parse((const uint8_t*)data.data(), data.size(), jh->info, err);
+      if (st == JpegStatus::Ok) {
+        jh->coef.assign((size_t)jh->info.coef_count, 0);
+        st = jpeg_decode_coefs((const uint8_t*)data.data(), data.size(), jh->info, jh->coef.data(), err);
+      }
+      if (st != JpegStatus::Ok) throw py::value_error("JPEG input not decodable by the split decoder: " + err);
+      InputImage im{(const uint8_t*)jh->coef.data(), jh->info.height, jh->info.width};
+      im.jpeg = &jh->info;
+      jkeep->push_back(jh);
+      v.push_back(im);
+      continue;
+    }
     py::array a = py::array::ensure(h, py::array::c_style);
     if (!a) throw std::runtime_error("inputs must be numpy arrays");
     InputImage im;
@@ -371,6 +407,7 @@ py::dict result_to_py(const BatchResult& r, int max_det) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native kernels and runtime of inference_arena_amd (gfx950)";
+  bind_jpeg(m);
   m.def("conv2d", &py_conv2d);
   m.def("set_conv_impl", &set_conv_impl);
   m.def("get_conv_impl", &get_conv_impl);
@@ -439,9 +476,18 @@ PYBIND11_MODULE(_C, m) {
       .def("submit",
            [](Executor& e, const py::list& imgs) {
              std::vector<py::array> keep;
-             auto v = images_from(imgs, keep);
-             py::gil_scoped_release nogil;
-             return e.submit(v);
+             JpegKeep jkeep;
+             auto v = images_from(imgs, keep, &jkeep);
+             int slot;
+             {
+               py::gil_scoped_release nogil;
+               slot = e.submit(v);
+             }
+             if (!jkeep.empty()) {
+               std::lock_guard<std::mutex> lk(g_jkeep_mu);
+               g_jkeep[{(const void*)&e, slot}] = std::move(jkeep);
+             }
+             return slot;
            })
       .def("collect",
            [](Executor& e, int slot) {
@@ -450,12 +496,17 @@ PYBIND11_MODULE(_C, m) {
                py::gil_scoped_release nogil;
                r = e.collect(slot);
              }
+             {
+               std::lock_guard<std::mutex> lk(g_jkeep_mu);
+               g_jkeep.erase({(const void*)&e, slot});
+             }
              return result_to_py(r, e.config().max_det);
            })
       .def("run",
            [](Executor& e, const py::list& imgs) {
              std::vector<py::array> keep;
-             auto v = images_from(imgs, keep);
+             JpegKeep jkeep;
+             auto v = images_from(imgs, keep, &jkeep);
              BatchResult r;
              {
                py::gil_scoped_release nogil;
@@ -684,6 +735,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("ipc_open", [](py::bytes handle, int device) { return ipc_open(std::string(handle), device); },
         py::arg("handle"), py::arg("device") = 0);
   m.def("ipc_close", &ipc_close);
+  m.def("ipc_open_range", [](py::bytes handle, int device) {
+    const uintptr_t p = ipc_open(std::string(handle), device);
+    return py::make_tuple(p, ipc_mapped_bytes(p));
+  }, py::arg("handle"), py::arg("device") = 0, "ipc_open + the mapped size: (device pointer, bytes)");
 
   py::class_<HttpLoadGen>(m, "HttpLoadGen")
       .def(py::init([](const py::dict& cfg, const py::list& requests) {
@@ -739,6 +794,53 @@ PYBIND11_MODULE(_C, m) {
           },
           py::arg("from") = 0, py::arg("to") = -1);
 
+  auto records_py = [](const std::vector<LoadGenRecord>& r) {
+    py::array_t<double> t((py::ssize_t)r.size());
+    py::array_t<float> lat((py::ssize_t)r.size());
+    py::array_t<int16_t> st((py::ssize_t)r.size()), dets((py::ssize_t)r.size());
+    for (size_t i = 0; i < r.size(); ++i) {
+      t.mutable_data()[i] = r[i].t_done;
+      lat.mutable_data()[i] = r[i].latency;
+      st.mutable_data()[i] = r[i].status;
+      dets.mutable_data()[i] = r[i].dets;
+    }
+    py::dict d;
+    d["t_done"] = t;
+    d["latency"] = lat;
+    d["status"] = st;
+    d["dets"] = dets;
+    return d;
+  };
+  py::class_<LocalLoadGen>(m, "LocalLoadGen")
+      .def(py::init([](HttpFrontEnd& fe, const py::list& uploads, int users) {
+             std::vector<std::string> u;
+             for (auto r : uploads) u.push_back(r.cast<std::string>());
+             return new LocalLoadGen(&fe, std::move(u), users);
+           }),
+           py::keep_alive<1, 2>())
+      .def("start", [](LocalLoadGen& g) {
+        py::gil_scoped_release nogil;
+        g.start();
+      })
+      .def(
+          "stop",
+          [](LocalLoadGen& g, double timeout_s) {
+            py::gil_scoped_release nogil;
+            g.stop(timeout_s);
+          },
+          py::arg("timeout_s") = 30.0)
+      .def("completed", &LocalLoadGen::completed)
+      .def(
+          "wait_completed",
+          [](LocalLoadGen& g, int64_t n, double timeout_s) {
+            py::gil_scoped_release nogil;
+            return g.wait_completed(n, timeout_s);
+          },
+          py::arg("n"), py::arg("timeout_s") = 600.0)
+      .def(
+          "records", [records_py](LocalLoadGen& g, int64_t from, int64_t to) { return records_py(g.records(from, to)); },
+          py::arg("from") = 0, py::arg("to") = -1);
+
   py::class_<HttpFrontEnd>(m, "HttpFrontEnd")
       .def(py::init([](DynamicBatcher& batcher, const py::dict& ch, std::vector<std::string> labels,
                        const py::dict& cfg) {
@@ -762,6 +864,25 @@ PYBIND11_MODULE(_C, m) {
              c.replica_tag = get<std::string>(cfg, "replica_tag", c.replica_tag);
              c.idle_timeout_ms = get<int64_t>(cfg, "idle_timeout_ms", c.idle_timeout_ms);
              c.read_timeout_ms = get<int64_t>(cfg, "read_timeout_ms", c.read_timeout_ms);
+             c.decode_threads = get<int>(cfg, "decode_threads", c.decode_threads);
+             c.jpeg_device = get<bool>(cfg, "jpeg_device", c.jpeg_device);
+             c.max_image_pixels = get<int64_t>(cfg, "max_image_pixels", c.max_image_pixels);
+             c.decode_buffer_cap = get<int64_t>(cfg, "decode_buffer_cap", c.decode_buffer_cap);
+             // decoded uploads live in pinned memory when a GPU is present (the executor DMAs from them)
+             int ndev = 0;
+             const bool gpu = hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0;
+             (void)hipGetLastError();
+             if (get<bool>(cfg, "pinned", gpu)) {
+               c.host_alloc = [](size_t n) -> void* {
+                 void* p = nullptr;
+                 if (hipHostMalloc(&p, n, hipHostMallocPortable) != hipSuccess) {
+                   (void)hipGetLastError();
+                   return nullptr;
+                 }
+                 return p;
+               };
+               c.host_free = [](void* p) { (void)hipHostFree(p); };
+             }
              py::gil_scoped_release nogil;
              return new HttpFrontEnd(&batcher, dc, std::move(labels), c);
            }),
@@ -830,6 +951,11 @@ PYBIND11_MODULE(_C, m) {
              d["sum_decode_ms"] = s.sum_decode_ms;
              d["sum_queue_ms"] = s.sum_queue_ms;
              d["sum_gpu_ms"] = s.sum_gpu_ms;
+             d["native_decoded"] = s.native_decoded;
+             d["fallback_decoded"] = s.fallback_decoded;
+             d["cpu_parse_ms"] = s.cpu_parse_ms;
+             d["cpu_decode_ms"] = s.cpu_decode_ms;
+             d["cpu_json_ms"] = s.cpu_json_ms;
              py::dict st;
              for (size_t k = 0; k < kStages.size() && k < s.stage_hist.size(); ++k)
                st[py::str(kStages[k])] = py::make_tuple(s.stage_hist[k], s.stage_sum_ms[k]);

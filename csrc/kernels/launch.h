@@ -444,4 +444,12 @@ void zero_fill(void* ptr, size_t bytes, hipStream_t s);
 // One 64-bit device wall-clock stamp at `dst` (a kernel node: stage timing inside a captured graph).
 void stamp(void* dst, hipStream_t s);
 
+// Device half of the split JPEG decoder (csrc/kernels/jpeg_idct.hip): for n_images descriptors (jpeg_desc.h)
+// reconstruct packed RGB at d_pool + desc.rgb_off from the quantized coefficient blocks at d_pool +
+// comp.coef_off (sample planes at d_pool + comp.plane_off as scratch).  max_blocks / max_pixels: the largest
+// total_blocks / width * height over the batch (grid sizes).
+struct JpegDesc;
+void jpeg_reconstruct(const JpegDesc* d_descs, uint8_t* d_pool, int n_images, int max_blocks, int64_t max_pixels,
+                      hipStream_t s);
+
 }  // namespace arena

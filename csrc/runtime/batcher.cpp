@@ -1,9 +1,12 @@
 // Native dynamic batcher; see batcher.h.
 #include "batcher.h"
 
+#include <pthread.h>
+
 #include <algorithm>
 #include <cstring>
 
+#include "jpeg_decode.h"
 #include "trace.h"
 
 namespace arena {
@@ -46,25 +49,48 @@ void DynamicBatcher::shutdown() {
   threads_.clear();
 }
 
-namespace {
-int64_t staged_size(int64_t bytes, int h, int w) {
-  const int64_t b = bytes > 0 ? bytes : (int64_t)h * w * 3;
-  return (b + 255) / 256 * 256;
+int64_t staged_bytes(const InputImage& im) {
+  auto a = [](int64_t v) { return (v + 255) / 256 * 256; };
+  if (im.jpeg != nullptr)
+    return a((int64_t)im.h * im.w * 3) + a(im.jpeg->coef_count * 2) + a(im.jpeg->plane_bytes);
+  return a(im.bytes > 0 ? im.bytes : (int64_t)im.h * im.w * 3);
 }
-}  // namespace
 
 int64_t DynamicBatcher::enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes) {
-  if (staging_cap_ > 0 && staged_size(bytes, h, w) > staging_cap_) {
+  InputImage in{nullptr, h, w};
+  in.bytes = bytes;
+  const int64_t staged = staged_bytes(in);
+  if (staging_cap_ > 0 && staged > staging_cap_) {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++stats_.rejected;
+    return -2;
+  }
+  auto copy = std::make_shared<std::vector<uint8_t>>(data, data + (bytes > 0 ? (size_t)bytes : (size_t)h * w * 3));
+  in.data = copy->data();
+  auto r = std::make_unique<Request>();
+  r->in = in;
+  r->owner = std::move(copy);
+  r->staged = staged;
+  r->cb = std::move(cb);
+  return push(std::move(r));
+}
+
+int64_t DynamicBatcher::enqueue_input(const InputImage& in, std::shared_ptr<const void> owner, ResultCallback cb) {
+  const int64_t staged = staged_bytes(in);
+  if (staging_cap_ > 0 && staged > staging_cap_) {
     std::lock_guard<std::mutex> lk(mu_);
     ++stats_.rejected;
     return -2;
   }
   auto r = std::make_unique<Request>();
-  r->pixels.assign(data, data + (bytes > 0 ? (size_t)bytes : (size_t)h * w * 3));
-  r->h = h;
-  r->w = w;
-  r->bytes = bytes;
+  r->in = in;
+  r->owner = std::move(owner);
+  r->staged = staged;
   r->cb = std::move(cb);
+  return push(std::move(r));
+}
+
+int64_t DynamicBatcher::push(std::unique_ptr<Request> r) {
   r->t_enq = clk::now();
   int64_t id;
   {
@@ -102,7 +128,7 @@ bool DynamicBatcher::take_batch(Batch& out, bool can_wait) {
       int fit = 0;
       for (auto& rq : q_) {
         if (fit >= cfg_.max_batch) break;
-        const int64_t b = staged_size(rq->bytes, rq->h, rq->w);
+        const int64_t b = rq->staged;
         if (fit > 0 && sum + b > staging_cap_) break;
         sum += b;
         ++fit;
@@ -189,6 +215,7 @@ void DynamicBatcher::fail(Batch& batch, const std::string& err) {
 }
 
 void DynamicBatcher::instance_loop(int idx) {
+  pthread_setname_np(pthread_self(), "arena-batcher");
   BatchInstance& ex = *inst_[idx];
   struct InFlight {
     int slot;
@@ -202,11 +229,7 @@ void DynamicBatcher::instance_loop(int idx) {
       if (take_batch(b, pending.empty())) {
         std::vector<InputImage> imgs;
         imgs.reserve(b.size());
-        for (auto& rq : b) {
-          InputImage im{rq->pixels.data(), rq->h, rq->w};
-          im.bytes = rq->bytes;
-          imgs.push_back(im);
-        }
+        for (auto& rq : b) imgs.push_back(rq->in);
         try {
           trace::mark("arena.batch");
           const auto t = clk::now();

@@ -78,18 +78,23 @@ class DynamicBatcher {
   // `bytes` == 0: RGB uint8 HxWx3 image; otherwise an fp32 [3, h, w] tensor of
   // that many bytes (reference tensor contract of the model server).
   int64_t enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes = 0);
+  // Zero-copy: the request references `in` (pixels, tensor or split-decoded JPEG coefficients) and keeps
+  // `owner` alive until its callback has run — the native front end's decode threads hand over pinned
+  // buffers the executor DMAs from directly.  Same return codes as enqueue().
+  int64_t enqueue_input(const InputImage& in, std::shared_ptr<const void> owner, ResultCallback cb);
   BatcherStats stats();
   void shutdown();
 
  private:
   struct Request {
     int64_t id;
-    std::vector<uint8_t> pixels;
-    int h, w;
-    int64_t bytes;
+    InputImage in;
+    std::shared_ptr<const void> owner;  // keeps in.data (and in.jpeg) alive
+    int64_t staged;                     // staged_bytes(in)
     ResultCallback cb;
     std::chrono::steady_clock::time_point t_enq;
   };
+  int64_t push(std::unique_ptr<Request> r);
   using Batch = std::vector<std::unique_ptr<Request>>;
 
   void instance_loop(int idx);

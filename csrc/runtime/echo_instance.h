@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "instance.h"
+#include "jpeg_decode.h"
 
 namespace arena {
 
@@ -49,7 +50,13 @@ class EchoInstance : public BatchInstance {
     r.crop_offset.resize(n + 1);
     int total = 0;
     for (int i = 0; i < n; ++i) {
-      const int k_n = std::min(max_det_, 1 + imgs[i].data[0] % max_det_);
+      uint8_t first = imgs[i].data[0];
+      if (imgs[i].jpeg != nullptr) {  // split-decoded JPEG: reconstruct like the device would (host reference)
+        std::vector<uint8_t> rgb((size_t)imgs[i].h * imgs[i].w * 3);
+        jpeg_coefs_to_rgb(*imgs[i].jpeg, (const int16_t*)imgs[i].data, rgb.data());
+        first = rgb[0];
+      }
+      const int k_n = std::min(max_det_, 1 + first % max_det_);
       r.det_count[i] = k_n;
       r.crop_offset[i] = total;
       for (int k = 0; k < k_n; ++k) {

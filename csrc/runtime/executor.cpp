@@ -3,6 +3,8 @@
 // inference_arena_amd/engine/planner.py (the only producer of programs).
 #include "executor.h"
 
+#include <pthread.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -13,6 +15,8 @@
 #include <string>
 
 #include "../kernels/common.h"
+#include "../kernels/jpeg_desc.h"
+#include "jpeg_decode.h"
 #include "trace.h"
 
 namespace arena {
@@ -66,6 +70,7 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
   const int nthreads = std::max(1, cfg_.host_threads);
   for (int t = 0; t < nthreads; ++t) {
     workers_.emplace_back([this]() {
+      pthread_setname_np(pthread_self(), "arena-pack");
       uint64_t seen = 0;
       for (;;) {
         std::vector<std::function<void()>>* jobs;
@@ -124,12 +129,12 @@ Executor::~Executor() {
 }
 
 // ---------------------------------------------------------------- layout
-size_t Executor::in_bytes_meta() const {
-  return kCtrlBytes + align_up(sizeof(ImageMeta) * (size_t)max_B_, 256);
+size_t Executor::jpeg_desc_off() const { return kCtrlBytes + align_up(sizeof(ImageMeta) * (size_t)max_B_, 256); }
+size_t Executor::in_bytes_meta() const { return jpeg_desc_off() + align_up(sizeof(JpegDesc) * (size_t)max_B_, 256); }
+size_t Executor::pool_cap() const {
+  return align_up((size_t)cfg_.pool_bytes_per_image * (size_t)std::max(1, cfg_.pool_factor) * max_B_, 256);
 }
-size_t Executor::in_bytes_total() const {
-  return in_bytes_meta() + align_up((size_t)cfg_.pool_bytes_per_image * max_B_, 256);
-}
+size_t Executor::in_bytes_total() const { return in_bytes_meta() + pool_cap(); }
 size_t Executor::out_off_det() const { return align_up(sizeof(int) * (size_t)max_B_, 256); }
 size_t Executor::out_off_topk() const {
   return out_off_det() + align_up(sizeof(Detection) * (size_t)max_B_ * cfg_.max_det, 256);
@@ -880,19 +885,20 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   // of the next n_slots_ - n_streams_ batches proceeds.
   sl.stream = streams_[seq_++ % n_streams_];
   // The slot's previous graph has been collected; its input copy was consumed.
+  // Pool layout of the batch: host-packed inputs (RGB frames, tensors) first, so one H2D of the slot's
+  // [ctrl | meta | JPEG descriptors | packed inputs] covers them; then per split-decoded JPEG its RGB
+  // destination, coefficient blocks (DMA'd straight from the request's own pinned buffer: no host copy) and
+  // reconstruction planes.  Everything is validated before the first copy is queued.
   ImageMeta* meta = (ImageMeta*)(sl.h_in + kCtrlBytes);
+  JpegDesc* jdesc = (JpegDesc*)(sl.h_in + jpeg_desc_off());
   uint8_t* pool = sl.h_in + in_bytes_meta();
-  const size_t pool_cap = (size_t)cfg_.pool_bytes_per_image * max_B_;
+  const size_t cap = pool_cap();
   size_t off = 0;
   std::vector<std::function<void()>> jobs;
   const int T = cfg_.det_size;
-  for (int i = 0; i < n; ++i) {
-    const InputImage& im = imgs[i];
-    if (im.h <= 0 || im.w <= 0) throw std::runtime_error("submit: empty image");
-    const size_t bytes = im.bytes > 0 ? (size_t)im.bytes : (size_t)im.h * im.w * 3;
-    if (off + bytes > pool_cap) throw std::runtime_error("submit: batch exceeds the staging pool");
+  auto set_meta = [&](int i, const InputImage& im, size_t at) {
     ImageMeta& m = meta[i];
-    m.offset = (int64_t)off;
+    m.offset = (int64_t)at;
     m.h = im.h;
     m.w = im.w;
     const double sc = std::min((double)T / im.h, (double)T / im.w);
@@ -901,6 +907,14 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     m.pad_w = (T - m.new_w) / 2;
     m.pad_h = (T - m.new_h) / 2;
     m.scale = (float)sc;
+  };
+  for (int i = 0; i < n; ++i) {
+    const InputImage& im = imgs[i];
+    if (im.h <= 0 || im.w <= 0) throw std::runtime_error("submit: empty image");
+    if (im.jpeg != nullptr) continue;
+    const size_t bytes = im.bytes > 0 ? (size_t)im.bytes : (size_t)im.h * im.w * 3;
+    if (off + bytes > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
+    set_meta(i, im, off);
     // split large images into 1 MiB copy jobs
     const size_t chunk = 1 << 20;
     for (size_t c = 0; c < bytes; c += chunk) {
@@ -910,6 +924,32 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
       jobs.emplace_back([dst, src, len]() { std::memcpy(dst, src, len); });
     }
     off = align_up(off + bytes, 256);
+  }
+  const size_t packed_end = off;
+  struct JpegCopy {
+    size_t dst;
+    const uint8_t* src;
+    size_t bytes;
+  };
+  std::vector<JpegCopy> jcopies;
+  int nj = 0, max_blocks = 0;
+  int64_t max_pix = 0;
+  for (int i = 0; i < n; ++i) {
+    const InputImage& im = imgs[i];
+    if (im.jpeg == nullptr) continue;
+    const JpegInfo& ji = *im.jpeg;
+    if (ji.width != im.w || ji.height != im.h) throw std::runtime_error("submit: JPEG geometry mismatch");
+    const size_t rgb = off, coef = align_up(rgb + (size_t)im.h * im.w * 3, 256);
+    const size_t planes = align_up(coef + (size_t)ji.coef_count * 2, 256);
+    const size_t end = align_up(planes + (size_t)ji.plane_bytes, 256);
+    if (end > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
+    set_meta(i, im, rgb);
+    jdesc[nj] = jpeg_device_desc(ji, (int64_t)coef, (int64_t)planes, (int64_t)rgb);
+    max_blocks = std::max(max_blocks, jdesc[nj].total_blocks);
+    max_pix = std::max(max_pix, (int64_t)im.h * im.w);
+    jcopies.push_back({coef, im.data, (size_t)ji.coef_count * 2});
+    ++nj;
+    off = end;
   }
   {
     trace::Range tp("arena.pack");
@@ -924,17 +964,24 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   std::memset(ctrl, 0, sizeof(Ctrl));
   ctrl->n_images = n;
   ctrl->crop_base = 0;
-  const size_t bytes = in_bytes_meta() + off;
-  sl.in_used = bytes;
-  if (copy_mode_ == 2) {
-    ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, sl.stream));
-  } else {
-    ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, bytes, hipMemcpyHostToDevice, copy_));
+  sl.in_used = in_bytes_meta() + off;
+  hipStream_t cs = copy_mode_ == 2 ? sl.stream : copy_;
+  ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, in_bytes_meta() + packed_end, hipMemcpyHostToDevice, cs));
+  for (const JpegCopy& c : jcopies)
+    ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in + in_bytes_meta() + c.dst, c.src, c.bytes, hipMemcpyHostToDevice, cs));
+  if (copy_mode_ != 2) {
     ARENA_HIP_CHECK(hipEventRecord(sl.copied, copy_));
     if (copy_mode_ == 1) ARENA_HIP_CHECK(hipEventSynchronize(sl.copied));
     ARENA_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.copied, 0));
   }
   ARENA_HIP_CHECK(hipEventRecord(sl.started, sl.stream));
+  // split-decoded JPEGs: dequantize + IDCT + upsample + colour-convert into their RGB slots before the program
+  if (nj > 0) {
+    trace::Range tj("arena.jpeg_reconstruct");
+    jpeg_reconstruct((const JpegDesc*)(sl.d_in + jpeg_desc_off()), sl.d_in + in_bytes_meta(), nj, max_blocks, max_pix,
+                     sl.stream);
+    ARENA_HIP_CHECK(hipGetLastError());
+  }
   if (debug_sync_ >= 3) {
     // 3: whole program as one graph without the D2H node, D2H issued eagerly after it.
     // 4: whole program graph including the D2H node, built fresh.
@@ -1139,7 +1186,7 @@ int Executor::submit_device(const std::vector<DeviceImage>& imgs, const std::vec
   Detection* det = (Detection*)(sl.h_out + out_off_det());
   CropRef* crops = (CropRef*)(sl.h_out + out_off_xcrops());
   std::memset(sl.h_out, 0, out_off_topk());
-  const size_t pool_cap = (size_t)cfg_.pool_bytes_per_image * max_B_;
+  const size_t cap = pool_cap();
   size_t off = 0;
   int total = 0;
   const int T = cfg_.det_size > 0 ? cfg_.det_size : 640;
@@ -1147,7 +1194,7 @@ int Executor::submit_device(const std::vector<DeviceImage>& imgs, const std::vec
     const DeviceImage& im = imgs[i];
     if (im.h <= 0 || im.w <= 0 || im.ptr == 0) throw std::runtime_error("submit_device: empty image");
     const size_t bytes = (size_t)im.h * im.w * 3;
-    if (off + bytes > pool_cap) throw std::runtime_error("submit_device: batch exceeds the staging pool");
+    if (off + bytes > cap) throw std::runtime_error("submit_device: batch exceeds the staging pool");
     ImageMeta& m = meta[i];
     m.offset = (int64_t)off;
     m.h = im.h;
@@ -1162,6 +1209,9 @@ int Executor::submit_device(const std::vector<DeviceImage>& imgs, const std::vec
     cnt[i] = k;
     for (int d = 0; d < k; ++d) {
       const Detection& dd = dets[i][d];
+      const float lim = 1e6f;  // casting a non-finite / huge float to int is undefined behaviour
+      if (!(std::fabs(dd.x1) < lim && std::fabs(dd.y1) < lim && std::fabs(dd.x2) < lim && std::fabs(dd.y2) < lim))
+        throw std::runtime_error("submit_device: box coordinates are not finite or out of range");
       det[(size_t)i * cfg_.max_det + d] = dd;
       CropRef& r = crops[total + d];
       r.img = i;

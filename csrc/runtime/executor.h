@@ -87,7 +87,11 @@ struct ExecutorConfig {
   int cand_cap = 8400;        // candidates per image entering NMS (= anchors)
   int crop_cap_per_image = 6; // crops one classification pass holds, per image (overflow -> extra pass)
   int min_crop_cap = 16;
-  int64_t pool_bytes_per_image = 640LL * 640 * 3;  // staging bytes per image slot
+  int64_t pool_bytes_per_image = 640LL * 640 * 3;  // RGB staging bytes per image of a full batch
+  // The device image pool of a slot holds pool_factor x that: room for split-decoded JPEGs, whose coefficient
+  // blocks (2 B per sample) and reconstruction planes sit next to the RGB frame they turn into (4:2:0 frames
+  // need 2.5x, 4:4:4 ones 3x; the batcher closes a batch early when its inputs would not fit).
+  int pool_factor = 3;
   int det_size = 640;
   int cls_size = 224;
   int host_threads = 8;
@@ -123,7 +127,7 @@ class Executor : public BatchInstance {
   const ExecutorConfig& config() const { return cfg_; }
   int max_det() const override { return cfg_.max_det; }
   int64_t raw_out_bytes() const override { return cfg_.raw_out_bytes; }
-  int64_t staging_bytes() const override { return cfg_.pool_bytes_per_image * (int64_t)max_B_; }
+  int64_t staging_bytes() const override { return (int64_t)pool_cap(); }
 
   // Asynchronous pipelined API: submit() packs the images into a free staging
   // slot, enqueues H2D + graph and returns the slot id; collect() waits for
@@ -223,7 +227,9 @@ class Executor : public BatchInstance {
   void enqueue_results_d2h(Bucket& bk, Slot& sl, int n);
   uint8_t* resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff_elems, int elem_bytes);
   int pick_bucket(int n) const;
-  size_t in_bytes_meta() const;
+  size_t in_bytes_meta() const;   // ctrl | ImageMeta[max_B] | JpegDesc[max_B]
+  size_t jpeg_desc_off() const;
+  size_t pool_cap() const;        // image pool bytes of a slot
   size_t in_bytes_total() const;
   size_t out_off_det() const;
   size_t out_off_topk() const;

@@ -5,6 +5,7 @@
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <pthread.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -17,7 +18,10 @@
 #include <cstdio>
 #include <cstring>
 #include <random>
+#include <ctime>
 #include <stdexcept>
+
+#include "jpeg_decode.h"
 
 namespace arena {
 
@@ -29,6 +33,15 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+// CPU time of the calling thread (ms): the per-stage host cost breakdown of FrontStats
+double thread_cpu_ms() {
+  timespec ts;
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+thread_local bool t_predict_dispatched = false;  // parse_one dispatched a /predict (its CPU counts as "parse")
 
 std::string lower(std::string s) {
   for (auto& ch : s) ch = (char)std::tolower((unsigned char)ch);
@@ -185,6 +198,7 @@ struct HttpFrontEnd::Conn {
   bool in_request = false;
   size_t chunk_pos = 0;      // next chunk-size line (0: not started)
   std::string chunk_body;
+  HttpFrontEnd::LocalDone local;  // in-process request (submit_local): the answer goes here, not to a socket
 };
 
 struct HttpFrontEnd::Pending {
@@ -198,15 +212,36 @@ struct HttpFrontEnd::HandlerPending {
   Clock::time_point t0;
 };
 
+struct HttpFrontEnd::DecodeTask {
+  std::shared_ptr<Conn> conn;
+  Clock::time_point t0, t_queued;
+  std::string body;  // the request body (moved in); the upload is body[off, off + len)
+  size_t off = 0, len = 0;
+};
+
+namespace {
+// A split-decoded upload in flight: its parsed header (the device descriptor's source) and the buffer holding
+// its coefficients (or, host-only mode, its RGB frame); kept alive by the batcher until the request completes.
+struct NativeUpload {
+  JpegInfo info;
+  std::shared_ptr<uint8_t> buf;
+};
+}  // namespace
+
 HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vector<std::string> labels,
                            FrontConfig cfg)
     : batcher_(batcher), dc_(std::move(dc)), labels_(std::move(labels)), cfg_(std::move(cfg)) {
   if (!cfg_.handler_mode) {
     if (batcher_ == nullptr) throw std::runtime_error("HttpFrontEnd: no batcher");
-    if (dc_.shm == nullptr || dc_.slots <= 0 || dc_.task_fds.empty() || dc_.result_fd < 0 || dc_.result_wfd < 0)
-      throw std::runtime_error("HttpFrontEnd: incomplete decode channel");
-    if (dc_.big_fds.size() != dc_.task_fds.size())
-      throw std::runtime_error("HttpFrontEnd: big_fds / task_fds mismatch");
+    has_pool_ = dc_.shm != nullptr;
+    if (has_pool_ || cfg_.decode_threads <= 0) {
+      if (dc_.shm == nullptr || dc_.slots <= 0 || dc_.task_fds.empty() || dc_.result_fd < 0 || dc_.result_wfd < 0)
+        throw std::runtime_error("HttpFrontEnd: incomplete decode channel");
+      if (dc_.big_fds.size() != dc_.task_fds.size())
+        throw std::runtime_error("HttpFrontEnd: big_fds / task_fds mismatch");
+    }
+    if (cfg_.decode_threads > 0)
+      host_pool_ = HostBufferPool::create(cfg_.decode_buffer_cap, cfg_.host_alloc, cfg_.host_free);
   }
   stats_.latency_hist.assign(kLatencyBucketsMs.size() + 1, 0);
   stats_.stage_hist.assign(kStages.size(), std::vector<int64_t>(kLatencyBucketsMs.size() + 1, 0));
@@ -249,7 +284,9 @@ HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vecto
     epfds_.push_back(ep);
   }
   for (int i = 0; i < n; ++i) io_threads_.emplace_back([this, i] { io_loop(i); });
-  if (!cfg_.handler_mode) collector_ = std::thread([this] { collector_loop(); });
+  if (!cfg_.handler_mode && has_pool_) collector_ = std::thread([this] { collector_loop(); });
+  if (!cfg_.handler_mode)
+    for (int i = 0; i < cfg_.decode_threads; ++i) decode_threads_.emplace_back([this, i] { decode_loop(i); });
 }
 
 HttpFrontEnd::~HttpFrontEnd() { stop(); }
@@ -261,14 +298,24 @@ void HttpFrontEnd::stop() {
   if (cfg_.handler_mode) {
     std::lock_guard<std::mutex> lk(hq_mu_);
     hq_cv_.notify_all();  // wake take()
-  } else {
+  } else if (has_pool_) {
     // wake the collector with a sentinel completion record (key < 0)
     int64_t rec[4] = {-1, 0, 0, 0};
     write_all(dc_.result_wfd, rec, sizeof rec);
   }
+  {
+    std::lock_guard<std::mutex> lk(dq_mu_);
+    dq_cv_.notify_all();
+  }
   for (auto& t : io_threads_)
     if (t.joinable()) t.join();
+  for (auto& t : decode_threads_)
+    if (t.joinable()) t.join();
   if (collector_.joinable()) collector_.join();
+  {
+    std::lock_guard<std::mutex> lk(dq_mu_);
+    dq_.clear();  // never started: their connections are closing with the front end
+  }
   {
     // requests already handed to the batcher answer through callbacks that capture `this`; the batcher
     // completes (or fails, on its own shutdown) every one of them, so wait here rather than free under them
@@ -367,6 +414,7 @@ FrontStats HttpFrontEnd::stats() {
 }
 
 void HttpFrontEnd::io_loop(int idx) {
+  pthread_setname_np(pthread_self(), "arena-http-io");
   const int ep = epfds_[idx];
   std::unordered_map<int, std::shared_ptr<Conn>> conns;
   std::vector<epoll_event> evs(256);
@@ -495,6 +543,26 @@ void HttpFrontEnd::handle_readable(int ep, const std::shared_ptr<Conn>& c) {
     }
     if (!parse_one(c)) break;
   }
+  if (c->in.size() >= cap) {
+    // a full buffer that still holds no complete request (a chunked body of many tiny chunks costs more wire
+    // bytes than its decoded size): nothing in flight will ever re-arm the connection, so answer now
+    bool idle;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      idle = !c->busy && !c->closed;
+      if (idle) {
+        c->busy = true;
+        c->close_after = true;
+      }
+    }
+    if (idle) {
+      c->in.clear();
+      c->in_request = false;
+      c->chunk_pos = 0;
+      c->chunk_body.clear();
+      fail_request(c, 413, "request body too large");
+    }
+  }
   if (eof) {
     bool busy;
     {
@@ -560,6 +628,18 @@ void HttpFrontEnd::handle_writable(int ep, const std::shared_ptr<Conn>& c) {
 }
 
 bool HttpFrontEnd::parse_one(const std::shared_ptr<Conn>& c) {
+  t_predict_dispatched = false;
+  const double c0 = thread_cpu_ms();
+  const bool r = parse_one_impl(c);
+  if (t_predict_dispatched) {
+    const double dt = thread_cpu_ms() - c0;
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    stats_.cpu_parse_ms += dt;
+  }
+  return r;
+}
+
+bool HttpFrontEnd::parse_one_impl(const std::shared_ptr<Conn>& c) {
   std::string& in = c->in;
   const size_t hend = in.find("\r\n\r\n");
   if (hend == std::string::npos || hend > 65536) {  // the header block is capped whether or not it is complete
@@ -718,6 +798,10 @@ void HttpFrontEnd::dispatch(const std::shared_ptr<Conn>& c, const std::string& m
 
 void HttpFrontEnd::respond(const std::shared_ptr<Conn>& c, int code, const std::string& ctype,
                            const std::string& body, bool) {
+  if (c->local) {
+    c->local(code, body);
+    return;
+  }
   std::string r;
   r.reserve(body.size() + 160);
   char head[256];
@@ -787,6 +871,129 @@ void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, c
     hq_cv_.notify_one();
     return;
   }
+  t_predict_dispatched = true;
+  if (cfg_.decode_threads > 0) {
+    auto t = std::make_unique<DecodeTask>();
+    t->conn = c;
+    t->t0 = t0;
+    t->t_queued = Clock::now();
+    t->body = std::move(body);
+    t->off = off;
+    t->len = len;
+    {
+      std::lock_guard<std::mutex> lk(dq_mu_);
+      dq_.push_back(std::move(t));
+    }
+    dq_cv_.notify_one();
+    return;
+  }
+  pool_submit(c, t0, body, off, len);
+}
+
+void HttpFrontEnd::submit_local(std::string upload, LocalDone done) {
+  auto c = std::make_shared<Conn>();
+  c->local = std::move(done);
+  c->busy = true;
+  const auto t0 = Clock::now();
+  if (upload.empty()) return fail_request(c, 422, "empty request body");
+  if (cfg_.decode_threads <= 0) return pool_submit(c, t0, upload, 0, upload.size());
+  auto t = std::make_unique<DecodeTask>();
+  t->conn = c;
+  t->t0 = t0;
+  t->t_queued = t0;
+  t->len = upload.size();
+  t->body = std::move(upload);
+  {
+    std::lock_guard<std::mutex> lk(dq_mu_);
+    dq_.push_back(std::move(t));
+  }
+  dq_cv_.notify_one();
+}
+
+LocalLoadGen::LocalLoadGen(HttpFrontEnd* fe, std::vector<std::string> uploads, int users)
+    : fe_(fe), uploads_(std::move(uploads)), users_(std::max(1, users)) {
+  if (uploads_.empty()) throw std::runtime_error("LocalLoadGen: no uploads");
+}
+
+LocalLoadGen::~LocalLoadGen() { stop(30.0); }
+
+void LocalLoadGen::start() {
+  t0_ = Clock::now();
+  issuing_.store(true);
+  for (int i = 0; i < users_; ++i) issue();
+}
+
+void LocalLoadGen::issue() {
+  if (!issuing_.load()) return;
+  const int64_t k = next_.fetch_add(1);
+  in_flight_.fetch_add(1);
+  const auto t_send = Clock::now();
+  fe_->submit_local(uploads_[(size_t)(k % (int64_t)uploads_.size())], [this, t_send](int code, const std::string& body) {
+    LoadGenRecord r;
+    const auto now = Clock::now();
+    r.t_done = std::chrono::duration<double>(now - t0_).count();
+    r.latency = (float)std::chrono::duration<double>(now - t_send).count();
+    r.status = (int16_t)code;
+    int n = 0;
+    for (size_t p = body.find("\"class_name\""); p != std::string::npos; p = body.find("\"class_name\"", p + 1)) ++n;
+    r.dets = (int16_t)n;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      recs_.push_back(r);
+    }
+    cv_.notify_all();
+    // a synchronous failure would recurse through issue() -> submit_local -> this callback: cap the depth
+    thread_local int depth = 0;
+    if (depth < 16) {
+      ++depth;
+      issue();
+      --depth;
+    }
+    std::lock_guard<std::mutex> lk(mu_);  // stop() / the destructor cannot return before this unlocks
+    in_flight_.fetch_sub(1);
+    cv_.notify_all();
+  });
+}
+
+void LocalLoadGen::stop(double timeout_s) {
+  issuing_.store(false);
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [this] { return in_flight_.load() == 0; });
+}
+
+int64_t LocalLoadGen::completed() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return (int64_t)recs_.size();
+}
+
+bool LocalLoadGen::wait_completed(int64_t n, double timeout_s) {
+  std::unique_lock<std::mutex> lk(mu_);
+  return cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return (int64_t)recs_.size() >= n; });
+}
+
+std::vector<LoadGenRecord> LocalLoadGen::records(int64_t from, int64_t to) {
+  std::lock_guard<std::mutex> lk(mu_);
+  from = std::max<int64_t>(0, from);
+  to = to < 0 ? (int64_t)recs_.size() : std::min<int64_t>((int64_t)recs_.size(), to);
+  if (to <= from) return {};
+  return std::vector<LoadGenRecord>(recs_.begin() + from, recs_.begin() + to);
+}
+
+void HttpFrontEnd::fail_request(const std::shared_ptr<Conn>& c, int code, const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    ++stats_.requests;
+    if (code == 413) ++stats_.too_large;
+    else if (code == 503) ++stats_.unavailable;
+    else if (code >= 500) ++stats_.errors;
+    else ++stats_.bad_request;
+  }
+  respond(c, code, "application/json", detail_json(msg));
+}
+
+void HttpFrontEnd::pool_submit(const std::shared_ptr<Conn>& c, Clock_tp t0, const std::string& body, size_t off,
+                               size_t len) {
+  if (!has_pool_) return fail_request(c, 500, "Failed to decode image: format not supported by the native decoder");
   int slot;
   {
     std::lock_guard<std::mutex> lk(slot_mu_);
@@ -796,7 +1003,7 @@ void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, c
       free_slots_.pop_back();
     }
   }
-  if (slot < 0) return fail(503, "decode pool is saturated");
+  if (slot < 0) return fail_request(c, 503, "decode pool is saturated");
   auto pend = std::make_shared<Pending>();
   pend->conn = c;
   pend->t0 = t0;
@@ -838,12 +1045,78 @@ void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, c
       pending_.erase(key);
     }
     release_slot(slot);
-    return fail(503, "decode workers unavailable");
+    return fail_request(c, 503, "decode workers unavailable");
+  }
+  {
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    ++stats_.fallback_decoded;
   }
   // the worker's load is released when its completion record arrives (finish_decode)
 }
 
+void HttpFrontEnd::decode_loop(int idx) {
+  pthread_setname_np(pthread_self(), "arena-jpeg");
+  (void)idx;
+  for (;;) {
+    std::unique_ptr<DecodeTask> t;
+    {
+      std::unique_lock<std::mutex> lk(dq_mu_);
+      dq_cv_.wait(lk, [this] { return stop_.load() || !dq_.empty(); });
+      if (stop_.load()) return;
+      t = std::move(dq_.front());
+      dq_.pop_front();
+    }
+    native_decode(*t);
+  }
+}
+
+void HttpFrontEnd::native_decode(DecodeTask& t) {
+  const double c0 = thread_cpu_ms();
+  const uint8_t* data = (const uint8_t*)t.body.data() + t.off;
+  auto up = std::make_shared<NativeUpload>();
+  std::string err;
+  JpegStatus st = jpeg_parse(data, t.len, up->info, err, cfg_.max_image_pixels);
+  if (st == JpegStatus::Unsupported) return pool_submit(t.conn, t.t0, t.body, t.off, t.len);  // PIL fallback
+  if (st == JpegStatus::Corrupt)
+    return fail_request(t.conn, err.find("image too large") != std::string::npos ? 413 : 500, err);
+  const JpegInfo& ji = up->info;
+  InputImage in{nullptr, ji.height, ji.width};
+  if (cfg_.jpeg_device) {
+    up->buf = host_pool_->get((size_t)ji.coef_count * 2);
+    if (!up->buf) return fail_request(t.conn, 503, "decode buffers exhausted");
+    st = jpeg_decode_coefs(data, t.len, ji, (int16_t*)up->buf.get(), err);
+    in.data = up->buf.get();
+    in.jpeg = &up->info;
+  } else {
+    thread_local std::vector<int16_t> coef;
+    coef.resize((size_t)ji.coef_count);
+    st = jpeg_decode_coefs(data, t.len, ji, coef.data(), err);
+    if (st == JpegStatus::Ok) {
+      up->buf = host_pool_->get((size_t)ji.width * ji.height * 3);
+      if (!up->buf) return fail_request(t.conn, 503, "decode buffers exhausted");
+      jpeg_coefs_to_rgb(ji, coef.data(), up->buf.get());
+      in.data = up->buf.get();
+    }
+  }
+  if (st != JpegStatus::Ok) return fail_request(t.conn, 500, err);
+  const double decode_ms = ms_since(t.t_queued);
+  {
+    std::lock_guard<std::mutex> sl(stats_mu_);
+    ++stats_.native_decoded;
+    stats_.cpu_decode_ms += thread_cpu_ms() - c0;
+  }
+  {
+    std::lock_guard<std::mutex> lk(cb_mu_);
+    ++cb_outstanding_;
+  }
+  const int64_t id = batcher_->enqueue_input(in, up, make_result_cb(t.conn, t.t0, Clock::now(), decode_ms));
+  if (id < 0) callback_done();  // rejected: the batcher never calls back
+  if (id == -1) return fail_request(t.conn, 503, "request queue is full");
+  if (id == -2) return fail_request(t.conn, 413, "image exceeds the staging capacity of one batch");
+}
+
 void HttpFrontEnd::collector_loop() {
+  pthread_setname_np(pthread_self(), "arena-collect");
   // completion record (server/decode_pool.py _DONE "<qiiiiq": key, slot, h, w, status, aux)
   struct __attribute__((packed)) Done {
     int64_t key;
@@ -856,6 +1129,110 @@ void HttpFrontEnd::collector_loop() {
     if (d.key < 0 || stop_.load()) break;
     finish_decode((uint64_t)d.key, d.slot, d.h, d.w, d.status, d.aux);
   }
+}
+
+ResultCallback HttpFrontEnd::make_result_cb(const std::shared_ptr<Conn>& conn, Clock_tp t0, Clock_tp t_inf,
+                                            double decode_ms) {
+  const bool softmax = cfg_.softmax_confidence;
+  const std::vector<std::string>* labels = &labels_;
+  FrontStats* stats = &stats_;
+  std::mutex* smu = &stats_mu_;
+  HttpFrontEnd* self = this;
+  return [self, conn, t0, t_inf, decode_ms, softmax, labels, stats, smu](RequestResult&& r) {
+    struct Done {
+      HttpFrontEnd* f;
+      ~Done() { f->callback_done(); }
+    } done{self};
+    if (!r.error.empty()) {
+      {
+        std::lock_guard<std::mutex> sl(*smu);
+        ++stats->requests;
+        ++stats->errors;
+      }
+      self->respond(conn, 500, "application/json", detail_json(r.error));
+      return;
+    }
+    const double queue_ms = r.queue_us / 1e3, gpu_ms = r.compute_us / 1e3;
+    const double inference_ms = ms_since(t_inf);
+    const double cj = thread_cpu_ms();
+    std::string s;
+    s.reserve(512 + 256 * r.det.size());
+    s += "{\"request_id\":";
+    json_escape(s, uuid4());
+    s += ",\"detections\":[";
+    for (size_t i = 0; i < r.det.size(); ++i) {
+      const Detection& d = r.det[i];
+      if (i) s += ',';
+      s += "{\"detection\":{\"x1\":";
+      json_num(s, d.x1);
+      s += ",\"y1\":";
+      json_num(s, d.y1);
+      s += ",\"x2\":";
+      json_num(s, d.x2);
+      s += ",\"y2\":";
+      json_num(s, d.y2);
+      s += ",\"confidence\":";
+      json_num(s, d.conf);
+      s += ",\"class_id\":" + std::to_string(d.cls) + "},\"classification\":{\"class_id\":";
+      int cid = -1;
+      double conf = 0.0;
+      if (i < r.topk.size()) {
+        cid = r.topk[i].idx[0];
+        conf = softmax ? r.topk[i].prob[0] : r.topk[i].logit[0];
+      }
+      s += std::to_string(cid) + ",\"class_name\":";
+      json_escape(s, (cid >= 0 && cid < (int)labels->size()) ? (*labels)[cid] : std::string());
+      s += ",\"confidence\":";
+      json_num(s, conf);
+      s += "}}";
+    }
+    const double total_ms = ms_since(t0);
+    s += "],\"timing\":{\"queue_ms\":";
+    json_num(s, queue_ms);
+    s += ",\"gpu_ms\":";
+    json_num(s, gpu_ms);
+    s += ",\"batch_size\":";
+    json_num(s, r.batch_size);
+    // device time of the detection network (+ decode / NMS / crop plan) and of the classification network
+    // (crop gather -> top-5) of this request's batch, from the program's wall-clock stamps (OP_STAMP); with
+    // the batch's H2D / D2H they make up gpu_ms (reference timing keys, architectures/monolithic/app/
+    // inference.py:180,224-225; there the per-request CPU time of each network)
+    const double det_ms = r.det_ms >= 0 ? r.det_ms : 0.0, cls_ms = r.cls_ms >= 0 ? r.cls_ms : 0.0;
+    s += ",\"detection_ms\":";
+    json_num(s, det_ms);
+    s += ",\"classification_ms\":";
+    json_num(s, cls_ms);
+    s += ",\"inference_ms\":";
+    json_num(s, inference_ms);
+    s += ",\"decode_ms\":";
+    json_num(s, decode_ms);
+    s += ",\"total_ms\":";
+    json_num(s, total_ms);
+    s += "}}";
+    const double json_cpu = thread_cpu_ms() - cj;
+    {
+      std::lock_guard<std::mutex> sl(*smu);
+      ++stats->requests;
+      ++stats->ok;
+      stats->cpu_json_ms += json_cpu;
+      stats->detections += (int64_t)r.det.size();
+      stats->sum_total_ms += total_ms;
+      stats->sum_decode_ms += decode_ms;
+      stats->sum_queue_ms += queue_ms;
+      stats->sum_gpu_ms += gpu_ms;
+      size_t b = 0;
+      while (b < kLatencyBucketsMs.size() && total_ms > kLatencyBucketsMs[b]) ++b;
+      ++stats->latency_hist[b];
+      const double stage_ms[] = {decode_ms, queue_ms, gpu_ms, det_ms, cls_ms, total_ms};
+      for (size_t k = 0; k < kStages.size(); ++k) {
+        size_t bb = 0;
+        while (bb < kLatencyBucketsMs.size() && stage_ms[k] > kLatencyBucketsMs[bb]) ++bb;
+        ++stats->stage_hist[k][bb];
+        stats->stage_sum_ms[k] += stage_ms[k];
+      }
+    }
+    self->respond(conn, 200, "application/json", s);
+  };
 }
 
 void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int status, int64_t aux) {
@@ -912,105 +1289,7 @@ void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int statu
     return fail(500, "decode worker result lost");
   }
   const double decode_ms = ms_since(pend->t_dec);
-  const auto t_inf = Clock::now();
-  const bool softmax = cfg_.softmax_confidence;
-  const std::vector<std::string>* labels = &labels_;
-  FrontStats* stats = &stats_;
-  std::mutex* smu = &stats_mu_;
-  HttpFrontEnd* self = this;
-  const auto t0 = pend->t0;
-  ResultCallback cb = [self, conn, t0, t_inf, decode_ms, softmax, labels, stats, smu](RequestResult&& r) {
-    struct Done {
-      HttpFrontEnd* f;
-      ~Done() { f->callback_done(); }
-    } done{self};
-    if (!r.error.empty()) {
-      {
-        std::lock_guard<std::mutex> sl(*smu);
-        ++stats->requests;
-        ++stats->errors;
-      }
-      self->respond(conn, 500, "application/json", detail_json(r.error));
-      return;
-    }
-    const double queue_ms = r.queue_us / 1e3, gpu_ms = r.compute_us / 1e3;
-    const double inference_ms = ms_since(t_inf);
-    std::string s;
-    s.reserve(512 + 256 * r.det.size());
-    s += "{\"request_id\":";
-    json_escape(s, uuid4());
-    s += ",\"detections\":[";
-    for (size_t i = 0; i < r.det.size(); ++i) {
-      const Detection& d = r.det[i];
-      if (i) s += ',';
-      s += "{\"detection\":{\"x1\":";
-      json_num(s, d.x1);
-      s += ",\"y1\":";
-      json_num(s, d.y1);
-      s += ",\"x2\":";
-      json_num(s, d.x2);
-      s += ",\"y2\":";
-      json_num(s, d.y2);
-      s += ",\"confidence\":";
-      json_num(s, d.conf);
-      s += ",\"class_id\":" + std::to_string(d.cls) + "},\"classification\":{\"class_id\":";
-      int cid = -1;
-      double conf = 0.0;
-      if (i < r.topk.size()) {
-        cid = r.topk[i].idx[0];
-        conf = softmax ? r.topk[i].prob[0] : r.topk[i].logit[0];
-      }
-      s += std::to_string(cid) + ",\"class_name\":";
-      json_escape(s, (cid >= 0 && cid < (int)labels->size()) ? (*labels)[cid] : std::string());
-      s += ",\"confidence\":";
-      json_num(s, conf);
-      s += "}}";
-    }
-    const double total_ms = ms_since(t0);
-    s += "],\"timing\":{\"queue_ms\":";
-    json_num(s, queue_ms);
-    s += ",\"gpu_ms\":";
-    json_num(s, gpu_ms);
-    s += ",\"batch_size\":";
-    json_num(s, r.batch_size);
-    // device time of the detection network (+ decode / NMS / crop plan) and of the classification network
-    // (crop gather -> top-5) of this request's batch, from the program's wall-clock stamps (OP_STAMP); with
-    // the batch's H2D / D2H they make up gpu_ms (reference timing keys, architectures/monolithic/app/
-    // inference.py:180,224-225; there the per-request CPU time of each network)
-    const double det_ms = r.det_ms >= 0 ? r.det_ms : 0.0, cls_ms = r.cls_ms >= 0 ? r.cls_ms : 0.0;
-    s += ",\"detection_ms\":";
-    json_num(s, det_ms);
-    s += ",\"classification_ms\":";
-    json_num(s, cls_ms);
-    s += ",\"inference_ms\":";
-    json_num(s, inference_ms);
-    s += ",\"decode_ms\":";
-    json_num(s, decode_ms);
-    s += ",\"total_ms\":";
-    json_num(s, total_ms);
-    s += "}}";
-    {
-      std::lock_guard<std::mutex> sl(*smu);
-      ++stats->requests;
-      ++stats->ok;
-      stats->detections += (int64_t)r.det.size();
-      stats->sum_total_ms += total_ms;
-      stats->sum_decode_ms += decode_ms;
-      stats->sum_queue_ms += queue_ms;
-      stats->sum_gpu_ms += gpu_ms;
-      size_t b = 0;
-      while (b < kLatencyBucketsMs.size() && total_ms > kLatencyBucketsMs[b]) ++b;
-      ++stats->latency_hist[b];
-      const double stage_ms[] = {decode_ms, queue_ms, gpu_ms, det_ms, cls_ms, total_ms};
-      for (size_t k = 0; k < kStages.size(); ++k) {
-        size_t bb = 0;
-        while (bb < kLatencyBucketsMs.size() && stage_ms[k] > kLatencyBucketsMs[bb]) ++bb;
-        ++stats->stage_hist[k][bb];
-        stats->stage_sum_ms[k] += stage_ms[k];
-      }
-    }
-    self->respond(conn, 200, "application/json", s);
-  };
+  ResultCallback cb = make_result_cb(conn, pend->t0, Clock::now(), decode_ms);
   {
     std::lock_guard<std::mutex> lk(cb_mu_);
     ++cb_outstanding_;

@@ -11,9 +11,17 @@
 //
 //   epoll I/O threads: accept, HTTP/1.1 keep-alive parsing (Content-Length or
 //   chunked), multipart/form-data field "file" or a raw image body
-//     -> the JPEG bytes go into a slot of the decode pool's shared memory and a
-//        16-byte task record to the least-loaded decode worker (the spawned PIL
-//        processes of server/decode_pool.py — JPEG decode stays in PIL)
+//     -> native decode (FrontConfig.decode_threads > 0, the default of the serving
+//        paths): the upload goes to a pool of C++ decode threads running the host
+//        half of the split JPEG decoder (runtime/jpeg_decode.h): marker parse +
+//        Huffman decode straight into a pinned buffer of the HostBufferPool
+//        (runtime/host_pool.h) -> DynamicBatcher::enqueue_input, zero-copy; the
+//        executor DMAs the coefficients and reconstructs the frame on the GPU
+//        (kernels/jpeg_idct.hip).  Uploads the split decoder does not cover
+//        (progressive JPEG, PNG, ...) fall through to:
+//     -> the PIL decode pool: the bytes go into a slot of the pool's shared memory
+//        and a 16-byte task record to the least-loaded decode worker (the spawned
+//        PIL processes of server/decode_pool.py)
 //   collector thread: completion records from the workers' shared pipe
 //     -> DynamicBatcher::enqueue straight from the shared-memory pixels
 //   batcher instance threads: results
@@ -35,6 +43,7 @@
 // 500 decode or device failure, each with {"detail": ...}.
 #pragma once
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -46,6 +55,8 @@
 #include <vector>
 
 #include "batcher.h"
+#include "host_pool.h"
+#include "http_loadgen.h"
 
 namespace arena {
 
@@ -77,6 +88,15 @@ struct FrontConfig {
   // body would otherwise hold a descriptor and its buffer forever).  0 disables the check.
   int64_t idle_timeout_ms = 60000;
   int64_t read_timeout_ms = 30000;
+  // Native decode threads (0: every upload goes to the PIL decode pool of the DecodeChannel).
+  int decode_threads = 0;
+  // true: split decode (host Huffman -> device reconstruction); false: the whole decode on the host threads
+  // (same arithmetic, RGB staged like a PIL decode) — for instances without the device half and for A/B runs.
+  bool jpeg_device = true;
+  int64_t max_image_pixels = 50000000;     // decode-bomb guard (processing/transforms.py max_image_pixels)
+  int64_t decode_buffer_cap = 2LL << 30;   // host buffers of decoded uploads in flight (HostBufferPool cap)
+  HostBufferPool::AllocFn host_alloc;      // pinning allocator for those buffers (empty: plain memory)
+  HostBufferPool::FreeFn host_free;
 };
 
 // One upload handed to the Python handler (handler mode).
@@ -88,7 +108,11 @@ struct HandlerRequest {
 struct FrontStats {
   int64_t requests = 0, ok = 0, bad_request = 0, too_large = 0, unavailable = 0, errors = 0, not_found = 0;
   int64_t connections = 0, open_connections = 0, detections = 0, timeouts = 0;
+  int64_t native_decoded = 0, fallback_decoded = 0;  // uploads decoded by the split decoder / the PIL pool
   double sum_total_ms = 0, sum_decode_ms = 0, sum_queue_ms = 0, sum_gpu_ms = 0;
+  // host CPU time (thread CPU clock) of request stages, summed: HTTP + multipart parse on the I/O threads, the
+  // native decode (marker parse + entropy decode), the JSON response built in the batcher callback
+  double cpu_parse_ms = 0, cpu_decode_ms = 0, cpu_json_ms = 0;
   std::vector<int64_t> latency_hist;  // counts per bucket of kLatencyBucketsMs (last = +Inf)
   // per-stage latency histograms of the successful requests (arena_request_latency_seconds{stage=...}):
   // kStages order, each counts per bucket of kLatencyBucketsMs (last = +Inf), with its sum in ms
@@ -101,6 +125,34 @@ struct FrontStats {
 extern const std::vector<std::string> kStages;
 
 extern const std::vector<double> kLatencyBucketsMs;
+
+class HttpFrontEnd;
+
+// Closed-loop in-process users of HttpFrontEnd::submit_local (the HTTP layer left out): `users` requests in
+// flight, each completion issues the next upload (round robin over `uploads`).  Same record format as the HTTP
+// load generator (http_loadgen.h).
+class LocalLoadGen {
+ public:
+  LocalLoadGen(HttpFrontEnd* fe, std::vector<std::string> uploads, int users);
+  ~LocalLoadGen();
+  void start();
+  void stop(double timeout_s = 30.0);
+  int64_t completed();
+  bool wait_completed(int64_t n, double timeout_s);
+  std::vector<LoadGenRecord> records(int64_t from, int64_t to);
+
+ private:
+  void issue();
+  HttpFrontEnd* fe_;
+  std::vector<std::string> uploads_;
+  int users_;
+  std::atomic<bool> issuing_{false};
+  std::atomic<int64_t> next_{0}, in_flight_{0};
+  std::chrono::steady_clock::time_point t0_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<LoadGenRecord> recs_;
+};
 
 class HttpFrontEnd {
  public:
@@ -126,9 +178,15 @@ class HttpFrontEnd {
   void drain();
   // handler mode: requests queued or inside the Python handler
   int handler_pending();
+  // In-process request (no socket, no HTTP parse): `upload` takes the /predict path from the decode stage on
+  // (split decoder or PIL pool, batcher, device, JSON) and `done(status, json)` receives what a client would.
+  // Drives LocalLoadGen, the control that isolates the cost of the HTTP layer.
+  using LocalDone = std::function<void(int, const std::string&)>;
+  void submit_local(std::string upload, LocalDone done);
 
   struct Conn;
   struct Pending;
+  using Clock_tp = std::chrono::steady_clock::time_point;
 
  private:
   void io_loop(int idx);
@@ -136,6 +194,7 @@ class HttpFrontEnd {
   void handle_readable(int ep, const std::shared_ptr<Conn>& c);
   void handle_writable(int ep, const std::shared_ptr<Conn>& c);
   bool parse_one(const std::shared_ptr<Conn>& c);  // true: a full request was consumed
+  bool parse_one_impl(const std::shared_ptr<Conn>& c);
   void dispatch(const std::shared_ptr<Conn>& c, const std::string& method, const std::string& path,
                 const std::string& ctype, std::string&& body);
   void predict(const std::shared_ptr<Conn>& c, std::string&& body, const std::string& ctype);
@@ -143,6 +202,13 @@ class HttpFrontEnd {
                bool count_latency = false);
   void close_conn(int ep, const std::shared_ptr<Conn>& c);
   void finish_decode(uint64_t key, int slot, int h, int w, int status, int64_t aux);
+  struct DecodeTask;
+  void decode_loop(int idx);
+  void native_decode(DecodeTask& t);
+  // hand an upload to the PIL decode pool (also the split decoder's fallback); answers the error itself
+  void pool_submit(const std::shared_ptr<Conn>& c, Clock_tp t0, const std::string& body, size_t off, size_t len);
+  ResultCallback make_result_cb(const std::shared_ptr<Conn>& c, Clock_tp t0, Clock_tp t_inf, double decode_ms);
+  void fail_request(const std::shared_ptr<Conn>& c, int code, const std::string& msg);
   void release_slot(int slot);
   void callback_done();
 
@@ -174,6 +240,14 @@ class HttpFrontEnd {
 
   std::mutex drain_mu_;
   bool drained_ = false;
+
+  // native decode
+  std::mutex dq_mu_;
+  std::condition_variable dq_cv_;
+  std::deque<std::unique_ptr<DecodeTask>> dq_;
+  std::vector<std::thread> decode_threads_;
+  std::shared_ptr<HostBufferPool> host_pool_;
+  bool has_pool_ = false;  // a PIL decode channel is attached
 
   std::mutex metrics_mu_;
   std::string metrics_text_;

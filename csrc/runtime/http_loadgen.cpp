@@ -2,6 +2,7 @@
 #include "runtime/http_loadgen.h"
 
 #include <arpa/inet.h>
+#include <pthread.h>
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -78,6 +79,7 @@ void HttpLoadGen::start() {
 }
 
 void HttpLoadGen::loop(int idx) {
+  pthread_setname_np(pthread_self(), "arena-loadgen");
   const int ep = epfds_[idx];
   std::unordered_map<int, std::unique_ptr<Conn>> conns;
   auto arm = [&](Conn* c, bool want_out) {

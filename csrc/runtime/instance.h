@@ -11,11 +11,21 @@
 
 namespace arena {
 
+struct JpegInfo;  // runtime/jpeg_decode.h
+
 struct InputImage {
-  const uint8_t* data;  // RGB uint8 HWC, contiguous (or an fp32 tensor when bytes != 0)
+  const uint8_t* data;  // RGB uint8 HWC, contiguous (or an fp32 tensor when bytes != 0, or JPEG coefficients)
   int h, w;
   int64_t bytes = 0;    // explicit payload size (tensor inputs); 0 = h*w*3
+  // Entropy-decoded JPEG (split decoder, runtime/jpeg_decode.h): `data` holds jpeg->coef_count int16
+  // coefficients (ideally pinned host memory: the executor DMAs them straight from there) and the instance
+  // reconstructs the RGB frame on the device.
+  const JpegInfo* jpeg = nullptr;
 };
+
+// Staging-pool bytes an input occupies in one batch (each region rounded up to 256 B): the RGB frame, plus for a
+// split-decoded JPEG its coefficient blocks and the reconstruction's sample planes.
+int64_t staged_bytes(const InputImage& im);
 
 // Per-slot results copied back to pinned memory after the slot's graph.
 struct BatchResult {

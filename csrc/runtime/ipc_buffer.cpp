@@ -40,6 +40,9 @@ void IpcBuffer::write(size_t off, const void* src, size_t n) {
   if (off > bytes_ || n > bytes_ - off) throw std::runtime_error("IpcBuffer::write out of range");
   check(hipSetDevice(device_), "hipSetDevice");
   check(hipMemcpy((uint8_t*)ptr_ + off, src, n, hipMemcpyHostToDevice), "hipMemcpy H2D");
+  // another process reads these bytes on its own stream right after the RPC naming them: the copy must have
+  // landed in device memory, not just left the pageable source (hipMemcpy only promises the latter)
+  check(hipDeviceSynchronize(), "hipDeviceSynchronize after IPC write");
 }
 
 void IpcBuffer::read(size_t off, void* dst, size_t n) const {
@@ -56,6 +59,14 @@ uintptr_t ipc_open(const std::string& handle, int device) {
   void* p = nullptr;
   check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
   return (uintptr_t)p;
+}
+
+size_t ipc_mapped_bytes(uintptr_t ptr) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  check(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr), "hipMemGetAddressRange");
+  const size_t skip = (size_t)(ptr - (uintptr_t)base);
+  return size > skip ? size - skip : 0;
 }
 
 void ipc_close(uintptr_t ptr) { check(hipIpcCloseMemHandle((void*)ptr), "hipIpcCloseMemHandle"); }

@@ -40,6 +40,9 @@ class IpcBuffer {
 // Map another process's IpcBuffer (its handle()) into this process on `device`; returns the device pointer.
 // The mapping is process-wide and reference-counted by the driver; ipc_close() releases it.
 uintptr_t ipc_open(const std::string& handle, int device);
+// Size of the allocation an (IPC-)mapped device pointer belongs to, from its base (hipMemGetAddressRange):
+// the classification side bounds every frame reference against it.
+size_t ipc_mapped_bytes(uintptr_t ptr);
 void ipc_close(uintptr_t ptr);
 
 }  // namespace arena

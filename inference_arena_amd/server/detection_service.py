@@ -102,7 +102,11 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
                 slot, ref = await loop.run_in_executor(None, ring.put, image)
                 try:
                     responses = await cl.classify_device(rid, ref, boxes)
-                finally:  # the answer (or the RPC's deadline) ends the classification side's use of the frame
+                finally:
+                    # the answer ends the classification side's use of the frame; after a deadline / cancellation
+                    # the classification side drops the abandoned crops before they reach the device
+                    # (DeviceClassifier._run), and a batch already on the device that reads a reused slot only
+                    # produces answers nobody waits for any more
                     ring.release(slot)
             elif settings.ARENA_FANOUT == "batch":
                 responses = await cl.classify_batch(rid, crops, boxes)

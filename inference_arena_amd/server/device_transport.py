@@ -124,7 +124,8 @@ class DeviceClassifier:
     def __init__(self, backend, open_handle, *, max_batch: int = 32, max_crops: int = 1 << 30,
                  max_delay_us: int = 300, inflight: int = 2):
         self.backend = backend
-        self.open_handle = open_handle  # handle bytes -> device pointer (native ipc_open)
+        # handle bytes -> device pointer, or (pointer, mapped bytes) (native ipc_open_range)
+        self.open_handle = open_handle
         self.max_batch = max_batch
         self.max_crops = max_crops
         self.max_delay = max_delay_us * 1e-6
@@ -137,13 +138,33 @@ class DeviceClassifier:
         self.batches = 0
         self.frames = 0
 
+    def _map(self, handle: bytes) -> tuple[int, int | None]:
+        """(device address, mapped bytes or None when the opener does not report a size)."""
+        m = self._ptrs.get(handle)
+        if m is None:
+            r = self.open_handle(handle)
+            m = self._ptrs[handle] = (int(r[0]), int(r[1])) if isinstance(r, tuple) else (int(r), None)
+        return m
+
     def _ptr(self, handle: bytes) -> int:
-        p = self._ptrs.get(handle)
-        if p is None:
-            p = self._ptrs[handle] = int(self.open_handle(handle))
-        return p
+        return self._map(handle)[0]
+
+    def validate(self, key: ImageKey, boxes: np.ndarray) -> None:
+        """A frame reference must lie inside the exported ring and its boxes must be finite and in a sane range:
+        the device copy and the crop plan trust both (a bad or stale DeviceImageRef would otherwise read out of
+        bounds on the GPU and take down every in-flight batch).  Raises ValueError -> in-band per-crop error."""
+        if key.height <= 0 or key.width <= 0 or key.offset < 0:
+            raise ValueError(f"device frame: bad geometry {key.height}x{key.width} at offset {key.offset}")
+        _, size = self._map(key.handle)
+        nbytes = key.height * key.width * 3
+        if size is not None and key.offset + nbytes > size:
+            raise ValueError(f"device frame: {nbytes} bytes at offset {key.offset} exceed the {size}-byte ring")
+        b = np.asarray(boxes, dtype=np.float64)
+        if b.ndim != 2 or b.shape[1] < 4 or not np.isfinite(b[:, :4]).all() or (np.abs(b[:, :4]) > 1e6).any():
+            raise ValueError("device frame: box coordinates are not finite or out of range")
 
     async def classify(self, key: ImageKey, boxes: np.ndarray):
+        self.validate(key, boxes)
         if self._queue is None:
             from concurrent.futures import ThreadPoolExecutor
 
@@ -178,6 +199,11 @@ class DeviceClassifier:
                     break
                 items.append(nxt)
                 crops += len(nxt[1])
+            # a waiter whose RPC was cancelled (deadline, client gone) no longer owns its frame: the detection side
+            # may already have reused the ring slot, so its crops are dropped before they reach the device
+            items = [it for it in items if not it[2].done()]
+            if not items:
+                continue
             await self._sem.acquire()
             asyncio.get_running_loop().create_task(self._dispatch(items))
 

@@ -2,10 +2,13 @@
 
 Same contract as ``server/monolithic.py`` (reference architectures/monolithic/app/main.py: ``POST
 /predict`` multipart field ``file`` -> detections with classifications and timing; ``GET /health``;
-``GET /metrics``), but the request path never enters Python: C++ epoll threads parse HTTP, hand the
-JPEG to the spawned PIL decode processes through shared memory (server/decode_pool.py, native mode),
-enqueue the pixels into the native dynamic batcher and write the JSON response.  Python only builds
-the engines, renders Prometheus text once a second and watches for device faults.
+``GET /metrics``), but the request path never enters Python: C++ epoll threads parse HTTP, C++ decode
+threads run the host half of the split JPEG decoder (csrc/runtime/jpeg_decode.h: marker parse + Huffman
+decode into pinned buffers; the GPU reconstructs the frame inside the batch, csrc/kernels/jpeg_idct.hip),
+the native dynamic batcher takes the upload without a copy, and C++ writes the JSON response.  Uploads the
+split decoder does not cover (progressive JPEG, PNG, ...) go to the spawned PIL decode processes through
+shared memory (server/decode_pool.py, native mode).  Python only builds the engines, renders Prometheus text
+once a second and watches for device faults.
 
 Run: ``python -m inference_arena_amd.server.native_front`` (PORT, ARENA_GPUS / ARENA_GPU,
 ARENA_INSTANCES, ARENA_DECODE_PROCS, ARENA_HTTP_THREADS, ...) or ``ARENA_NATIVE_HTTP=1`` with the
@@ -93,17 +96,24 @@ class NativeFrontEnd:
     """The native HTTP server over a DynamicBatcher plus its decode processes."""
 
     def __init__(self, batcher, labels: list[str], *, port: int = 8100, host: str = "0.0.0.0",
-                 io_threads: int = 4, decode_procs: int = 8, slots: int = 512, softmax: bool = False,
-                 arch: str = "monolithic", gpu: str = "0", replica_tag: str = "", **http: int):
-        """``http``: further FrontConfig fields (max_body, idle_timeout_ms, read_timeout_ms; defaults from
-        ARENA_HTTP_IDLE_TIMEOUT_MS / ARENA_HTTP_READ_TIMEOUT_MS, else csrc/runtime/http_front.h)."""
+                 io_threads: int = 4, decode_procs: int = 2, slots: int = 512, softmax: bool = False,
+                 arch: str = "monolithic", gpu: str = "0", replica_tag: str = "", decode_threads: int = 8,
+                 jpeg_device: bool = True, **http: int):
+        """``decode_threads``: native split-decoder threads (0: every upload to the ``decode_procs`` PIL
+        processes, the round-3 path); ``jpeg_device=False`` reconstructs on the host threads instead of the GPU
+        (instances without the device half, e.g. the host-only EchoInstance, take either).  ``http``: further
+        FrontConfig fields (max_body, idle_timeout_ms, read_timeout_ms; defaults from ARENA_HTTP_IDLE_TIMEOUT_MS
+        / ARENA_HTTP_READ_TIMEOUT_MS, else csrc/runtime/http_front.h)."""
         from ..ops import native
+        from ..processing.transforms import max_image_pixels
 
         self.batcher = batcher
-        self.pool = ProcessDecodePool(workers=decode_procs, slots=slots, native=True)
+        self.pool = ProcessDecodePool(workers=max(1, decode_procs), slots=slots, native=True)
         self.fe = native().HttpFrontEnd(batcher, self.pool.native_channel(), list(labels),
                                         {"host": host, "port": int(port), "io_threads": int(io_threads),
                                          "softmax_confidence": bool(softmax), "replica_tag": str(replica_tag),
+                                         "decode_threads": int(decode_threads), "jpeg_device": bool(jpeg_device),
+                                         "max_image_pixels": int(max_image_pixels()),
                                          **_http_timeouts(), **{k: int(v) for k, v in http.items()}})
         self.registry = CollectorRegistry()
         self.registry.register(_Collector(self, arch, gpu))
@@ -161,9 +171,11 @@ def serve(settings: Settings | None = None, *, weights=None, replica_tag: str = 
         "max_queue_size": int(os.environ.get("ARENA_MAX_QUEUE", "4096"))})
     front = NativeFrontEnd(batcher, load_labels(settings.LABELS_FILE or None), port=int(settings.PORT),
                            io_threads=int(os.environ.get("ARENA_HTTP_THREADS", "4")),
-                           # 10 PIL processes (~8.5k decodes/s) keep the fp32 engine fed: 7.9k req/s at 256 users
-                           # vs 6.5k with 8 (profiles/serving_r2d/monolithic_hi_d*)
-                           decode_procs=int(os.environ.get("ARENA_DECODE_PROCS", "0") or 10),
+                           # native split-decoder threads; the PIL processes only take what it does not cover
+                           # (ARENA_DECODE_THREADS=0: all uploads through 10 PIL processes, the round-3 setup)
+                           decode_threads=int(os.environ.get("ARENA_DECODE_THREADS", "8")),
+                           decode_procs=int(os.environ.get("ARENA_DECODE_PROCS", "0") or
+                                            (2 if int(os.environ.get("ARENA_DECODE_THREADS", "8")) > 0 else 10)),
                            softmax=(settings.ARENA_CONFIDENCE or "logit") == "softmax",
                            gpu=",".join(str(d) for d in devices), replica_tag=replica_tag)
     log.info("native monolithic front end ready", extra={"port": front.port, "gpus": devices})

@@ -235,7 +235,7 @@ def build_frame_classifier(settings):
     max_batch = int(settings.ARENA_MAX_BATCH)
     runner = build_session("frame_classifier", mnet=mnet, device=dev, buckets=_default_buckets(max_batch))
     C = native()
-    return DeviceClassifier(runner, lambda h: C.ipc_open(h, dev), max_batch=max_batch,
+    return DeviceClassifier(runner, lambda h: C.ipc_open_range(h, dev), max_batch=max_batch,
                             max_crops=int(runner.ex.crop_cap_for(runner.max_batch)),
                             max_delay_us=int(os.environ.get("ARENA_CLS_QUEUE_DELAY_US", "300")))
 

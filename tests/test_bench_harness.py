@@ -17,8 +17,7 @@ ROOT = Path(__file__).resolve().parents[1]
 def _bench(*args, env=None):
     e = dict(os.environ, ARENA_DIST_BACKEND="gloo", PYTHONPATH=str(ROOT), **(env or {}))
     return subprocess.run([sys.executable, str(ROOT / "bench.py"), "--fake-engine", "--steps", "2", "--warmup", "1",
-                           "--min-warmup-s", "0.3", "--users", "16", "--decode-workers", "2", "--step-batches", "8",
-                           *args],
+                           "--min-warmup-s", "0.3", "--users", "16", "--step-batches", "8", *args],
                           capture_output=True, text=True, timeout=600, env=e)
 
 
@@ -29,10 +28,39 @@ def test_bench_two_ranks_self_launch_http():
     assert out["n_gpus"] == 2 and out["world_size_checked"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["path"] == "http" and out["errors"] == 0 and out["value"] > 0
     assert out["weights_verified"] is True and out["collective_backend"] == "gloo"
-    assert len(out["per_rank_req_s"]) == 2 and len(out["cpu_share_per_rank"]) == 2
+    assert len(out["per_rank_req_s"]) == 2 and len(out["usable_cpus_per_rank"]) == 2
     assert set(out["levels"]) == {"1", "4", "batcher"} and out["bs1_p50_ms"] == out["levels"]["1"]["p50_ms"]
-    assert out["inproc"]["value"] > 0
+    assert out["inproc"]["value"] > 0 and out["inproc"]["errors"] == 0
     assert out["ms_per_step"] * out["steps"] / 1e3 == pytest.approx(2 * 256 * 2 / out["value"], rel=1e-3)
+    # one node-level front door (SO_REUSEPORT, one load generator) next to the per-rank sum
+    assert out["front"] == "per-rank" and out["shared_front"]["value"] > 0 and out["shared_front"]["errors"] == 0
+    assert out["shared_front"]["users"] == 32 and out["mean_batch"] > 0
+    # the per-request host CPU breakdown: every upload went through the native split decoder
+    assert out["stage_cpu_us_per_req"]["native_decoded"] >= 2 * 256 and out["stage_cpu_us_per_req"]["fallback_decoded"] == 0
+    assert out["host_cpu_us_per_req"]["total"] > 0 and out["host_cpu_us_per_req"]["decode"] > 0
+
+
+def test_bench_shared_front_headline():
+    r = _bench("--gpus", "2", "--front", "shared", "--latency-levels", "", "--no-secondary-inproc")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["front"] == "shared" and out["errors"] == 0 and out["value"] == out["shared_front"]["value"]
+    assert out["ms_per_step"] * out["steps"] / 1e3 == pytest.approx(2 * 256 * 2 / out["value"], rel=1e-3)
+
+
+def test_bench_divides_the_job_cpu_quota_between_ranks():
+    """4 ranks on a job quota of 8 CPUs: each rank sizes its host threads for 2 CPUs, says so loudly, and the
+    node's decode processes stay within the quota."""
+    r = _bench("--gpus", "4", "--latency-levels", "", "--no-secondary-inproc", "--no-secondary-shared-front",
+               env={"ARENA_CPU_QUOTA": "8"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["usable_cpus_per_rank"] == [2, 2, 2, 2]
+    plan = out["config"]["host_plan_per_gpu"]
+    assert plan["decode_threads"] == 1 and plan["http_io"] == 1 and plan["loadgen"] == 1
+    assert 4 * plan["pil_procs"] <= 8  # decode processes of the whole node within the job quota
+    assert out["cpu_budget_warning"] and "only 2 usable CPUs" in r.stderr
+    assert out["errors"] == 0 and out["value"] > 0
 
 
 def test_bench_detects_diverging_replica_weights():

@@ -29,9 +29,10 @@ class FakeDevice:
         self.mem: dict[bytes, tuple[int, bytearray]] = {}
         self.opened: list[bytes] = []
 
-    def open(self, handle: bytes) -> int:
+    def open(self, handle: bytes) -> tuple[int, int]:
         self.opened.append(handle)
-        return self.mem[handle][0]
+        base, buf = self.mem[handle]
+        return base, len(buf)
 
     def resolve(self, ptr: int) -> tuple[bytearray, int]:
         for base, buf in self.mem.values():
@@ -274,3 +275,53 @@ def test_device_request_without_frame_classifier_is_an_in_band_error():
         assert len(out) == 1 and "not enabled" in out[0].error and out[0].request_id == "r_0"
     finally:
         srv.stop()
+
+
+def test_device_classifier_rejects_out_of_range_references():
+    """A frame reference outside the exported ring, or non-finite / huge boxes, is an in-band error before any
+    device work (no out-of-bounds device reads from a bad DeviceImageRef)."""
+    dev = FakeDevice()
+    ring = DeviceImageRing(2, 300, buffer=FakeIpcBuffer(dev, 600, 4))
+    _, ref = ring.put(np.zeros((10, 10, 3), np.uint8))
+    be = FakeFrameBackend(dev)
+    dc = DeviceClassifier(be, dev.open, max_delay_us=1000)
+    ok = np.array([[0, 0, 5, 5, 0.9, 1]], np.float32)
+    cases = [
+        (ImageKey(ref.handle, 0, 500, 10, 10), ok),                 # 300 bytes at 500 > 600-byte ring
+        (ImageKey(ref.handle, 0, -3, 10, 10), ok),                  # negative offset
+        (ImageKey(ref.handle, 0, 0, 0, 10), ok),                    # empty frame
+        (ImageKey(ref.handle, 0, 0, 10, 10), np.array([[np.nan, 0, 5, 5, 0.9, 1]], np.float32)),
+        (ImageKey(ref.handle, 0, 0, 10, 10), np.array([[0, 0, 3e9, 5, 0.9, 1]], np.float32)),
+    ]
+
+    async def go():
+        r = await asyncio.gather(*(dc.classify(k, b) for k, b in cases), dc.classify(ImageKey(ref.handle, 0, 0, 10, 10), ok),
+                                 return_exceptions=True)
+        dc.close()
+        return r
+
+    out = asyncio.run(go())
+    assert all(isinstance(e, ValueError) for e in out[:-1]), out
+    assert not isinstance(out[-1], BaseException) and be.batches == [1]  # only the valid frame reached the device
+
+
+def test_device_classifier_drops_cancelled_waiters():
+    dev = FakeDevice()
+    ring = DeviceImageRing(2, 300, buffer=FakeIpcBuffer(dev, 600, 5))
+    _, ref = ring.put(np.zeros((10, 10, 3), np.uint8))
+    be = FakeFrameBackend(dev)
+    dc = DeviceClassifier(be, dev.open, max_delay_us=50000)
+    key = ImageKey(ref.handle, 0, 0, 10, 10)
+    box = np.array([[0, 0, 5, 5, 0.9, 1]], np.float32)
+
+    async def go():
+        t1 = asyncio.ensure_future(dc.classify(key, box))
+        t2 = asyncio.ensure_future(dc.classify(key, box))
+        await asyncio.sleep(0.005)
+        t1.cancel()  # the RPC's deadline fired while the batch was still filling
+        r = await t2
+        dc.close()
+        return r
+
+    assert len(asyncio.run(go())) == 1
+    assert be.batches == [1]  # the cancelled waiter's frame never reached the device

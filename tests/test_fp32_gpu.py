@@ -573,7 +573,7 @@ def _ir_ref64(x, expand, dw, project, stride, res):
 ])
 @pytest.mark.parametrize("x3t", ["1", "0"])  # >= 28x28 expanding blocks: tiled x3 kernel / exact-fp32 ir_f32
 def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, x3t, monkeypatch):
-    if H <= 14:  # the whole-map kernel is opt-in for programs; the wrapper takes it when enabled
+    if H <= 14:  # the whole-map kernel (ARENA_IRC_F32=auto: the planner's default for these blocks); forced on here
         if x3t == "0":
             pytest.skip("ARENA_IR_X3T does not apply to the whole-map kernel")
         monkeypatch.setenv("ARENA_IRC_F32", "1")

@@ -1,0 +1,135 @@
+"""Host half of the split JPEG decoder (csrc/runtime/jpeg_decode.h) on CPU.
+
+The reference decodes uploads with cv2 / PIL (src/shared/processing/transforms.py:77-110; PIL for arm B,
+architectures/microservices/classification/app/servicer.py:65-76).  The split decoder must produce exactly the
+pixels PIL produces, so every detection / classification downstream is unchanged: the host reference
+reconstruction (``jpeg_decode_host``, the same integer arithmetic the GPU kernels run, kernels/jpeg_math.h) is
+compared bit for bit with PIL over qualities, chroma samplings, grayscale, odd sizes and restart intervals;
+formats it does not cover are reported as unsupported (the server sends them to the PIL pool) and broken files
+as corrupt with PIL's messages."""
+from __future__ import annotations
+
+import io
+
+import numpy as np
+import pytest
+from PIL import Image
+
+from inference_arena_amd.ops import native
+
+
+def _enc(arr, **kw) -> bytes:
+    b = io.BytesIO()
+    Image.fromarray(arr).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def _pil(data: bytes) -> np.ndarray:
+    with Image.open(io.BytesIO(data)) as im:
+        return np.asarray(im.convert("RGB"))
+
+
+def _scene(h, w, seed=0):
+    """A natural-ish frame: smooth gradients + blobs + noise (every DCT frequency band populated)."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w].astype(np.float32)
+    img = np.stack([x / max(w, 1) * 200, y / max(h, 1) * 180, (x + y) / max(h + w, 1) * 150], -1)
+    for _ in range(6):
+        cy, cx, r = rng.uniform(0, h), rng.uniform(0, w), rng.uniform(3, max(4, min(h, w) / 3))
+        img += (((y - cy) ** 2 + (x - cx) ** 2) < r * r)[..., None] * rng.uniform(-90, 90, 3)
+    img += rng.normal(0, 12, img.shape)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("quality", [50, 75, 90, 95, 100])
+@pytest.mark.parametrize("subsampling", [0, 1, 2])  # 4:4:4, 4:2:2, 4:2:0
+def test_bit_exact_with_pil(quality, subsampling):
+    C = native()
+    for i, (h, w) in enumerate([(427, 640), (480, 640), (37, 53), (16, 16), (9, 7), (101, 3)]):
+        data = _enc(_scene(h, w, i), quality=quality, subsampling=subsampling)
+        st, err, rgb = C.jpeg_decode_host(data)
+        if subsampling and w <= 4:  # chroma narrower than 3 samples: libjpeg box-upsamples -> PIL fallback
+            assert st == "unsupported"
+            continue
+        assert st == "ok", err
+        np.testing.assert_array_equal(rgb, _pil(data))
+
+
+@pytest.mark.parametrize("blocks", [1, 3, 7])
+def test_restart_intervals_and_grayscale(blocks):
+    C = native()
+    img = _scene(120, 170, blocks)
+    for arr in (img, np.asarray(Image.fromarray(img).convert("L"))):
+        data = _enc(arr, quality=88, restart_marker_blocks=blocks)
+        assert b"\xff\xdd" in data
+        st, err, rgb = C.jpeg_decode_host(data)
+        assert st == "ok", err
+        np.testing.assert_array_equal(rgb, _pil(data))
+
+
+def test_curated_workload_is_bit_exact():
+    """The bench's own uploads (curated synthetic frames, JPEG q90)."""
+    from inference_arena_amd.data.synthetic import encode_jpeg, synthetic_images
+
+    C = native()
+    for img in synthetic_images(12, 5):
+        data = encode_jpeg(img, 90)
+        st, err, rgb = C.jpeg_decode_host(data)
+        assert st == "ok", err
+        np.testing.assert_array_equal(rgb, _pil(data))
+
+
+def test_coefficient_layout():
+    C = native()
+    data = _enc(_scene(40, 56), quality=90, subsampling=2)
+    d = C.jpeg_coefs(data)
+    assert d["status"] == "ok" and (d["width"], d["height"], d["layout"]) == (56, 40, 3)
+    y, cb, cr = d["comps"]
+    assert (y["h"], y["v"], cb["h"], cb["v"]) == (2, 2, 1, 1)
+    assert (y["bw"], y["bh"]) == (8, 6) and (cb["bw"], cb["bh"]) == (4, 3)  # MCU grid 4 x 3 of 16x16
+    assert (cb["cw"], cb["ch"]) == (28, 20)
+    assert d["coef_count"] == (48 + 12 + 12) * 64 == len(d["coef"])
+    assert cb["coef_off"] == 48 * 64 and cr["coef_off"] == 60 * 64
+
+
+def test_unsupported_formats_go_to_the_fallback():
+    C = native()
+    img = _scene(64, 64)
+    cases = {
+        "progressive": _enc(img, quality=90, progressive=True),
+    }
+    b = io.BytesIO()
+    Image.fromarray(img).convert("CMYK").save(b, "JPEG")
+    cases["cmyk"] = b.getvalue()
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "PNG")
+    cases["png"] = b.getvalue()
+    for name, data in cases.items():
+        st, err, rgb = C.jpeg_decode_host(data)
+        assert st == "unsupported" and rgb is None, (name, st, err)
+
+
+def test_corrupt_and_oversized_inputs():
+    C = native()
+    good = _enc(_scene(64, 80), quality=90)
+    st, err, _ = C.jpeg_decode_host(good[: len(good) // 2])  # cut inside the scan
+    assert st == "corrupt" and "truncated" in err
+    with pytest.raises(OSError):  # PIL agrees that this upload is broken
+        _pil(good[: len(good) // 2])
+    st, err, _ = C.jpeg_decode_host(good[:30])  # cut inside the headers
+    assert st == "corrupt"
+    st, err, _ = C.jpeg_decode_host(good, max_pixels=64 * 80 - 1)
+    assert st == "corrupt" and "image too large" in err
+    # a scan cut short by a marker decodes (libjpeg warns; PIL returns the image)
+    sos = good.rfind(b"\xff\xda")
+    cut = good[: sos + 40] + b"\xff\xd9"
+    st, err, rgb = C.jpeg_decode_host(cut)
+    assert st == "ok", err
+    np.testing.assert_array_equal(rgb, _pil(cut))
+    rng = np.random.default_rng(3)
+    for _ in range(200):  # fuzz: random byte flips never crash the decoder
+        bad = bytearray(good)
+        for k in rng.integers(2, len(bad), 8):
+            bad[k] = int(rng.integers(0, 256))
+        st, _, _ = C.jpeg_decode_host(bytes(bad))
+        assert st in ("ok", "corrupt", "unsupported")

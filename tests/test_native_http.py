@@ -302,7 +302,7 @@ def test_stage_timing_and_stage_histograms(server):
 
 
 _FRONT_SRCS = ["csrc/tests/front_stress.cpp", "csrc/runtime/http_front.cpp", "csrc/runtime/batcher.cpp",
-               "csrc/runtime/trace.cpp"]
+               "csrc/runtime/trace.cpp", "csrc/runtime/jpeg_decode.cpp"]
 
 
 @pytest.mark.parametrize("sanitizer", ["thread", "address"])
@@ -336,3 +336,74 @@ def test_front_end_stress_under_sanitizer(sanitizer):
     assert "ThreadSanitizer" not in report and "AddressSanitizer" not in report, report[-6000:]
     assert r.returncode == 0, report[-6000:]
     assert "front_stress: ok" in r.stdout
+
+
+def test_tiny_chunks_beyond_the_input_cap_get_413():
+    """A chunked upload whose wire size passes max_body + 64 KiB while its decoded body stays under max_body
+    is answered 413 (it used to sit paused until the read timeout closed it without a status)."""
+    import socket
+
+    C = native()
+    batcher = C.DynamicBatcher([C.EchoInstance(2, 8, 4, 0)], {"max_batch": 8, "max_queue_delay_us": 200})
+    fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=1, decode_procs=1, slots=4,
+                        max_body=100_000)
+    try:
+        s = socket.create_connection(("127.0.0.1", fe.port), timeout=20)
+        s.sendall(b"POST /predict HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\nContent-Type: image/jpeg\r\n\r\n")
+        chunk = b"1\r\nX\r\n" * 4096  # 6 wire bytes per body byte
+        resp = b""
+        try:
+            for _ in range(60):  # ~1.4 MB on the wire, 240 KB decoded... the server answers well before that
+                s.sendall(chunk)
+        except (BrokenPipeError, ConnectionResetError):
+            pass
+        s.settimeout(20)
+        try:
+            while b"\r\n\r\n" not in resp:
+                d = s.recv(65536)
+                if not d:
+                    break
+                resp += d
+        except ConnectionResetError:
+            pass
+        assert resp.startswith(b"HTTP/1.1 413"), resp[:200]
+        s.close()
+    finally:
+        fe.close()
+        batcher.shutdown()
+
+
+@pytest.mark.parametrize("jpeg_device", [True, False])
+def test_split_decoder_answers_like_the_pil_pool(jpeg_device):
+    """JPEG uploads through the native split decoder (coefficients handed to the instance, or reconstructed on
+    the host threads) answer exactly like the PIL decode processes: the echo instance's detections depend on the
+    decoded first pixel, which must be bit-identical."""
+    C = native()
+    rng = np.random.default_rng(11)
+    uploads = []
+    for i in range(8):
+        arr = (rng.random((40 + 8 * i, 56 + 4 * i, 3)) * 255).astype(np.uint8)
+        b = io.BytesIO()
+        Image.fromarray(arr).save(b, format="JPEG", quality=90, subsampling=i % 3)
+        uploads.append(b.getvalue())
+    answers = {}
+    for threads in (3, 0):
+        batcher = C.DynamicBatcher([C.EchoInstance(2, 8, 4, 200)], {"max_batch": 8, "max_queue_delay_us": 200})
+        fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=2, decode_procs=1,
+                            slots=16, decode_threads=threads, jpeg_device=jpeg_device)
+        try:
+            out = []
+            for u in uploads:
+                body, ct = _multipart(u)
+                st, data, c = _post(fe.port, body, ct)
+                c.close()
+                assert st == 200
+                out.append([(d["detection"], d["classification"]) for d in json.loads(data)["detections"]])
+            answers[threads] = out
+            s = fe.stats()
+            assert (s["native_decoded"], s["fallback_decoded"]) == ((8, 0) if threads else (0, 8))
+        finally:
+            fe.close()
+            batcher.shutdown()
+    assert answers[3] == answers[0]
+    assert len({len(a) for a in answers[3]}) > 1  # the first pixels differ, so the checks are not vacuous

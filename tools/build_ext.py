@@ -51,12 +51,15 @@ SOURCES = [
     "kernels/classify_head.hip",
     "kernels/head_pool.hip",
     "kernels/fc_splitk.hip",
+    "kernels/jpeg_idct.hip",
     "runtime/executor.cpp",
     "runtime/batcher.cpp",
     "runtime/http_front.cpp",
     "runtime/http_loadgen.cpp",
     "runtime/ipc_buffer.cpp",
     "runtime/trace.cpp",
+    "runtime/jpeg_decode.cpp",
+    "bindings_jpeg.cpp",
     "bindings.cpp",
 ]
 
