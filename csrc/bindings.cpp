@@ -627,7 +627,7 @@ PYBIND11_MODULE(_C, m) {
            }),
            py::keep_alive<1, 2>())
       .def("enqueue",
-           [](DynamicBatcher& b, py::array img_in, py::function cb) {
+           [](DynamicBatcher& b, py::array img_in, py::function cb, uintptr_t export_to) {
              py::array img = py::array::ensure(img_in, py::array::c_style);
              int h = 0, w = 0;
              int64_t bytes = 0;
@@ -686,8 +686,9 @@ PYBIND11_MODULE(_C, m) {
              };
              const uint8_t* data = (const uint8_t*)img.data();
              py::gil_scoped_release nogil;
-             return b.enqueue(data, h, w, std::move(f), bytes);
-           })
+             return b.enqueue(data, h, w, std::move(f), bytes, (uint8_t*)export_to);
+           },
+           py::arg("img"), py::arg("cb"), py::arg("export_to") = 0)
       .def("stats",
            [](DynamicBatcher& b) {
              BatcherStats s = b.stats();

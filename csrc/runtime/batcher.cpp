@@ -56,9 +56,11 @@ int64_t staged_bytes(const InputImage& im) {
   return a(im.bytes > 0 ? im.bytes : (int64_t)im.h * im.w * 3);
 }
 
-int64_t DynamicBatcher::enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes) {
+int64_t DynamicBatcher::enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes,
+                                uint8_t* export_dst) {
   InputImage in{nullptr, h, w};
   in.bytes = bytes;
+  in.export_dst = export_dst;
   const int64_t staged = staged_bytes(in);
   if (staging_cap_ > 0 && staged > staging_cap_) {
     std::lock_guard<std::mutex> lk(mu_);

@@ -77,7 +77,8 @@ class DynamicBatcher {
   // an instance can stage in one batch (the caller answers 413 / INVALID_ARGUMENT).
   // `bytes` == 0: RGB uint8 HxWx3 image; otherwise an fp32 [3, h, w] tensor of
   // that many bytes (reference tensor contract of the model server).
-  int64_t enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes = 0);
+  int64_t enqueue(const uint8_t* data, int h, int w, ResultCallback cb, int64_t bytes = 0,
+                  uint8_t* export_dst = nullptr);
   // Zero-copy: the request references `in` (pixels, tensor or split-decoded JPEG coefficients) and keeps
   // `owner` alive until its callback has run — the native front end's decode threads hand over pinned
   // buffers the executor DMAs from directly.  Same return codes as enqueue().

@@ -982,6 +982,13 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
                      sl.stream);
     ARENA_HIP_CHECK(hipGetLastError());
   }
+  // frames exported to another buffer on this device (arm B's IPC ring): device to device, in stream order
+  for (int i = 0; i < n; ++i) {
+    const InputImage& im = imgs[i];
+    if (im.export_dst == nullptr || im.bytes > 0) continue;
+    ARENA_HIP_CHECK(hipMemcpyAsync(im.export_dst, sl.d_in + in_bytes_meta() + meta[i].offset, (size_t)im.h * im.w * 3,
+                                   hipMemcpyDeviceToDevice, sl.stream));
+  }
   if (debug_sync_ >= 3) {
     // 3: whole program as one graph without the D2H node, D2H issued eagerly after it.
     // 4: whole program graph including the D2H node, built fresh.

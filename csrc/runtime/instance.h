@@ -21,6 +21,10 @@ struct InputImage {
   // coefficients (ideally pinned host memory: the executor DMAs them straight from there) and the instance
   // reconstructs the RGB frame on the device.
   const JpegInfo* jpeg = nullptr;
+  // Optional device address (on the instance's GPU) that receives a copy of the staged RGB frame, device to
+  // device on the batch's stream (arm B device transport: the detector exports the frame it already uploaded
+  // into the IPC ring slot the classification service reads; no second host -> device copy).
+  uint8_t* export_dst = nullptr;
 };
 
 // Staging-pool bytes an input occupies in one batch (each region rounded up to 256 B): the RGB frame, plus for a

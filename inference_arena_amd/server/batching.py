@@ -73,14 +73,16 @@ class AsyncBatcher:
             return np.ascontiguousarray(x)
         return np.ascontiguousarray(x, dtype=np.float32)
 
-    async def run(self, x: np.ndarray) -> dict:
+    async def run(self, x: np.ndarray, export_to: int = 0) -> dict:
+        """``export_to``: device address on the instance's GPU that receives the staged frame (D2D, in the
+        batch's stream order) — complete when this returns."""
         loop = asyncio.get_running_loop()
         fut: asyncio.Future = loop.create_future()
 
         def done(d):
             loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(d))
 
-        _enqueue_or_raise(self._b.enqueue(self._prep(x), done))
+        _enqueue_or_raise(self._b.enqueue(self._prep(x), done, int(export_to)))
         return self._check(await fut)
 
     async def run_many(self, xs: list[np.ndarray]) -> list[dict]:

@@ -86,20 +86,34 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
         try:
             state["faults"].check()
             image = await state["decode"].decode(data)
+            ring = state.get("ring")
+            on_device = ring is not None and image.nbytes <= ring.slot_bytes
+            # device transport with a GPU detector: the detector copies the frame it already staged for YOLO into
+            # a ring slot, device to device inside its batch — the frame crosses PCIe once
+            slot = ring.try_acquire() if on_device and getattr(det_be, "exports_frames", False) else None
             t_det = Timer()
-            det, dtiming = await det_be.detect(image)
+            try:
+                det, dtiming = await (det_be.detect(image, export_to=ring.slot_ptr(slot)) if slot is not None
+                                      else det_be.detect(image))
+            except BaseException:
+                if slot is not None:
+                    ring.release(slot)
+                raise
             detection_ms = t_det.ms()
             t_cls = Timer()
             boxes = [{"x1": float(d[0]), "y1": float(d[1]), "x2": float(d[2]), "y2": float(d[3]),
                       "confidence": float(d[4]), "class_id": int(d[5])} for d in det]
-            ring = state.get("ring")
-            on_device = ring is not None and image.nbytes <= ring.slot_bytes
             crops = [] if on_device else [extract_crop(image, d) for d in det]
             if not boxes:
+                if slot is not None:
+                    ring.release(slot)
                 responses = []
             elif on_device:
-                loop = asyncio.get_running_loop()
-                slot, ref = await loop.run_in_executor(None, ring.put, image)
+                if slot is not None:
+                    ref = ring.ref(slot, image.shape[0], image.shape[1])
+                else:  # no exporting detector (or no free slot before detection): upload the frame once more
+                    loop = asyncio.get_running_loop()
+                    slot, ref = await loop.run_in_executor(None, ring.put, image)
                 try:
                     responses = await cl.classify_device(rid, ref, boxes)
                 finally:

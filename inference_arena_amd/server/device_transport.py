@@ -60,10 +60,24 @@ class DeviceImageRing:
                 raise TimeoutError("device image ring: no free slot")
             return self._free.pop()
 
+    def try_acquire(self) -> int | None:
+        with self._cv:
+            return self._free.pop() if self._free else None
+
     def release(self, slot: int) -> None:
         with self._cv:
             self._free.append(slot)
             self._cv.notify()
+
+    def slot_ptr(self, slot: int) -> int:
+        """Device address of a slot (the detector exports its staged frame there: server/detection_service.py)."""
+        return int(self.buf.ptr) + slot * self.slot_bytes
+
+    def ref(self, slot: int, height: int, width: int) -> "pb.DeviceImageRef":
+        if height * width * 3 > self.slot_bytes:
+            raise ValueError(f"frame of {height * width * 3} bytes exceeds the ring slot ({self.slot_bytes})")
+        return pb.DeviceImageRef(handle=self.handle, device=self.device, offset=slot * self.slot_bytes,
+                                 height=height, width=width)
 
     def put(self, image: np.ndarray) -> tuple[int, "pb.DeviceImageRef"]:
         img = np.ascontiguousarray(image, dtype=np.uint8)

@@ -148,8 +148,10 @@ class GpuDetectorBackend(DetectorBackend):
     def device_error(self) -> str | None:
         return self.batcher.device_error
 
-    async def detect(self, image: np.ndarray):
-        d = await self.batcher.run(np.ascontiguousarray(image, dtype=np.uint8))
+    exports_frames = True  # detect(export_to=...) copies the staged frame to a device buffer (arm B device ring)
+
+    async def detect(self, image: np.ndarray, export_to: int = 0):
+        d = await self.batcher.run(np.ascontiguousarray(image, dtype=np.uint8), export_to=export_to)
         det = d["det"]
         out = np.concatenate([det[:, :5], det[:, 5:6].copy().view(np.int32).astype(np.float32)], 1)
         return out, {"queue_ms": d["queue_us"] / 1e3, "gpu_ms": d["compute_us"] / 1e3,

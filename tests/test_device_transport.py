@@ -325,3 +325,53 @@ def test_device_classifier_drops_cancelled_waiters():
 
     assert len(asyncio.run(go())) == 1
     assert be.batches == [1]  # the cancelled waiter's frame never reached the device
+
+
+def test_predict_exports_the_detector_frame_into_the_ring():
+    """With an exporting detector (the GPU one copies its staged frame into the ring slot device to device), the
+    detection service never uploads the frame again (no DeviceImageRing.put), and the answers are unchanged."""
+    from inference_arena_amd.server.detection_service import create_app
+
+    dev = FakeDevice()
+
+    class ExportingDetector(FakeDetector):
+        exports_frames = True
+
+        def __init__(self):
+            self.exports = 0
+
+        async def detect(self, image, export_to=0):
+            if export_to:
+                buf, off = dev.resolve(export_to)
+                b = np.ascontiguousarray(image).tobytes()
+                buf[off: off + len(b)] = b
+                self.exports += 1
+            return await super().detect(image)
+
+    class CountingRing(DeviceImageRing):
+        puts = 0
+
+        def put(self, image):
+            CountingRing.puts += 1
+            return super().put(image)
+
+    be = FakeFrameBackend(dev)
+    srv = ClassificationThread(DeviceClassifier(be, dev.open, max_delay_us=200))
+    ring = CountingRing(4, 640 * 640 * 3, buffer=FakeIpcBuffer(dev, 4 * 640 * 640 * 3, 12))
+    ring.buf.ptr = dev.mem[ring.handle][0]
+    det = ExportingDetector()
+    try:
+        s = Settings(LOG_LEVEL="WARNING", CLASSIFICATION_GRPC_ENDPOINT=f"127.0.0.1:{srv.port}",
+                     ARENA_CROP_TRANSPORT="device", ARENA_FANOUT="batch")
+        img = synthetic_images(1, 6)[0]
+        body, ctype = encode_multipart("file", encode_jpeg(img))
+        with TestClient(create_app(s, detector=det, ring=ring)) as c:
+            outs = [c.post("/predict", content=body, headers={"content-type": ctype}) for _ in range(3)]
+        h = img.shape[0]
+        for r in outs:
+            assert r.status_code == 200, r.text
+            assert [d["classification"]["class_id"] for d in r.json()["detections"]][:3] == [20, h - 5, 1]
+        assert det.exports == 3 and CountingRing.puts == 0 and sum(be.batches) == 3
+        assert len(ring._free) == ring.slots
+    finally:
+        srv.stop()

@@ -127,3 +127,35 @@ def test_device_classifier_batches_ipc_frames(dense_models, device, tmp_path):
         proc.stdin.write("done\n")
         proc.stdin.flush()
         assert proc.wait(60) == 0
+
+
+def test_detector_exports_its_staged_frames_into_the_ring(dense_models, device):
+    """The GPU detector copies each frame it staged for YOLO into the given ring slot, device to device in its
+    batch (InputImage.export_dst): the slot holds the exact frame once the detection answer is back, and the
+    detections are those of a run without export (server/detection_service.py's device transport)."""
+    import asyncio
+
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.server.batching import AsyncBatcher
+    from inference_arena_amd.engine.registry import build_session
+    from inference_arena_amd.server.device_transport import DeviceImageRing
+
+    imgs = synthetic_images(5, 41) + synthetic_images(2, 42, hw=(333, 500))
+    runner = build_session("detector", dense_models[0], device=0, buckets=[1, 8])
+    b = AsyncBatcher([runner], max_batch=8, max_queue_delay_us=2000)
+    ring = DeviceImageRing(len(imgs), 640 * 640 * 3, device=0)
+    slots = [ring.acquire() for _ in imgs]
+
+    async def go(export: bool):
+        return await asyncio.gather(*(b.run(im, export_to=ring.slot_ptr(s) if export else 0)
+                                      for im, s in zip(imgs, slots)))
+
+    try:
+        plain = asyncio.run(go(False))
+        exported = asyncio.run(go(True))
+        for im, s, p, e in zip(imgs, slots, plain, exported):
+            got = np.frombuffer(ring.buf.read(s * ring.slot_bytes, im.nbytes), np.uint8).reshape(im.shape)
+            np.testing.assert_array_equal(got, im)
+            np.testing.assert_array_equal(p["det"], e["det"])
+    finally:
+        b.close()
