@@ -22,6 +22,7 @@ constexpr uint8_t kNatural[64 + 16] = {
 uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 
 constexpr int kFastBits = 11;
+constexpr int kEobRun = 127;  // ac_fast run of an EOB entry
 
 inline int extend(uint32_t v, int s) { return (int)v - ((v < (1u << (s - 1))) ? (int)((1u << s) - 1) : 0); }
 
@@ -59,6 +60,10 @@ struct HuffTable {
                 const uint32_t bitsv = (uint32_t)(j >> (shift - mag)) & ((1u << mag) - 1);
                 const int v = extend(bitsv, mag);
                 ac_fast[idx] = (int32_t)((uint32_t)v << 16) | (run << 8) | (l + mag);
+              } else if (ac && sym == 0x00) {
+                ac_fast[idx] = (kEobRun << 8) | l;  // EOB: the run pushes k past the block
+              } else if (ac && sym == 0xF0) {
+                ac_fast[idx] = (15 << 8) | l;       // ZRL: 15 zeros + a stored zero = 16 positions
               }
             }
           }
@@ -203,9 +208,10 @@ __attribute__((always_inline)) inline bool decode_block(BitReader& br, const Huf
   for (int k = 1; k < 64;) {
     br.need(32);  // a code (<= 16 bits) and its magnitude (<= 15 bits)
     const int32_t f = ac.ac_fast[br.buf >> (64 - kFastBits)];
-    if (f) {
+    if (f) {  // one lookup: coefficient, ZRL or EOB
       br.skip(f & 0xFF);
       k += (f >> 8) & 0xFF;
+      if (k > 63) break;  // EOB (or a corrupt run past the block)
       blk[kNatural[k]] = (int16_t)(f >> 16);
       ++k;
       continue;
