@@ -21,6 +21,7 @@ from __future__ import annotations
 import asyncio
 import csv
 import json
+import os
 import multiprocessing as mp
 import random
 import time
@@ -150,6 +151,9 @@ def write_level(out_dir: Path, tag: str, res: PhaseResult, summary: dict) -> Non
         w.writerow(["POST", "/predict", summary["requests"], summary["failures"], summary["p50_latency_ms"],
                     summary["mean_latency_ms"], summary["max_latency_ms"], summary["throughput_rps"],
                     summary["p95_latency_ms"], summary["p99_latency_ms"]])
+    # the serving configuration the level ran against (transport, fan-out, process layout, envelope ...)
+    summary = dict(summary, env={k: v for k, v in sorted(os.environ.items())
+                                 if k.startswith("ARENA_") or k in ("CONTAINER_VCPU", "LOG_LEVEL")})
     (out_dir / f"{tag}_summary.json").write_text(json.dumps(summary, indent=2) + "\n")
 
 
