@@ -417,6 +417,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_pw", &set_conv_pw);
   m.def("set_conv_v3", &set_conv_v3);
   m.def("set_ir_wave", &set_ir_wave);
+  m.def("set_irx_parts", &set_irx_parts);
   m.def("set_ir_t14", &set_ir_t14);
   m.def("set_ir_crop", &set_ir_crop);
   m.def("set_ir_crop_split", &set_ir_crop_split);

@@ -76,19 +76,30 @@ __device__ __forceinline__ f32x4 mfma_x3(const bf16x8& ah, const bf16x8& am, con
 
 }  // namespace
 
-// HO: output side; S: stride; KS: inp_pad / 32; NOT: oup_pad / 16; HC: hidden channels per chunk.
-template <int HO, int S, int KS, int NOT, int HC>
+// input rows the widest of NP bands of NOR rows reads (its E rows without the zero border)
+constexpr int band_rows(int HO, int S, int NP, int NOR) {
+  int m = 0;
+  for (int p = 0; p < NP; ++p) {
+    const int oy0 = p * NOR, nor = imin(NOR, HO - oy0);
+    if (nor <= 0) continue;
+    const int lo = imax(0, oy0 * S - 1), hi = imin(HO * S - 1, (oy0 + nor - 1) * S + 1);
+    m = imax(m, hi - lo + 1);
+  }
+  return m;
+}
+
+// HO: output side; S: stride; KS: inp_pad / 32; NOT: oup_pad / 16; HC: hidden channels per chunk; NP: row bands
+// (workgroups) per crop.
+template <int HO, int S, int KS, int NOT, int HC, int NP = 2>
 struct IrxGeom {
   static constexpr int HI = HO * S;                   // input side
-  static constexpr int NOR0 = (HO + 1) / 2;           // output rows of part 0 (the larger band)
+  static constexpr int NOR0 = (HO + NP - 1) / NP;     // output rows of a band (the last one may be shorter)
   static constexpr int ER = (NOR0 - 1) * S + 3;       // E rows incl. the zero border
   static constexpr int EW = HI + 2;                   // E columns incl. the zero border
   static constexpr int NEP = ER * EW;                 // E pixels
   static constexpr int NKG = HC / 8;                  // 8-channel groups of a chunk
   static constexpr int EPS = (2 * NEP + 1) * 16;      // bytes per E channel-group plane (odd slot count)
-  static constexpr int XR0 = imin(HI, (NOR0 - 1) * S + 2);                          // input rows, part 0
-  static constexpr int XR1 = imin(HI - 1, (HO - 1) * S + 1) - (NOR0 * S - 1) + 1;    // input rows, part 1
-  static constexpr int NX = imax(XR0, XR1) * HI;
+  static constexpr int NX = band_rows(HO, S, NP, NOR0) * HI;  // input pixels of the largest band
   static constexpr int NXT = (NX + 15) / 16;          // expand pixel tiles
   static constexpr int INP = KS * 32;
   static constexpr int NHT = HC / 16;                 // expand hidden tiles per chunk
@@ -112,9 +123,9 @@ struct IrxGeom {
 
 // Weights (IrParams.x3w = 1, packed by engine/planner.py::split_bf16x3): we bf16 [hid_pad][3][inp_pad] and
 // wp bf16 [oup_pad][3][hid_pad] (planes h, m, l of the fp32 weight), wd fp32 [9][hid_pad], biases fp32.
-template <int HO, int S, int KS, int NOT, int HC>
+template <int HO, int S, int KS, int NOT, int HC, int NP>
 __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
-  using G = IrxGeom<HO, S, KS, NOT, HC>;
+  using G = IrxGeom<HO, S, KS, NOT, HC, NP>;
   constexpr int HI = G::HI, INP = G::INP, EW = G::EW;
   extern __shared__ __align__(16) uint8_t lds[];
   uint8_t* Es = lds;
@@ -125,10 +136,11 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, kq = lane >> 4;
-  const int b = blockIdx.x >> 1, part = blockIdx.x & 1;
+  const int b = blockIdx.x / NP, part = blockIdx.x - (blockIdx.x / NP) * NP;
   if (b >= live_batch(p.B, p.bdev)) return;
   const int oy0 = part * G::NOR0;
-  const int nor = part ? HO - G::NOR0 : G::NOR0;
+  const int nor = imin(G::NOR0, HO - oy0);
+  if (nor <= 0) return;
   const int nout = nor * HO;
   const int iy0 = oy0 * S - 1;                          // image row of E row 0
   const int iy_lo = iy0 < 0 ? 0 : iy0;
@@ -344,7 +356,7 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
   }
 }
 
-// (HO, S, KS, NOT, HC): the MobileNetV2 14x14 / 7x7 stages at 224 (two row bands per crop)
+// (HO, S, KS, NOT, HC): the MobileNetV2 14x14 / 7x7 stages at 224
 #define ARENA_IRX_CONFIGS(X) \
   X(14, 1, 2, 4, 32)         \
   X(14, 1, 2, 6, 32)         \
@@ -353,13 +365,31 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
   X(7, 1, 5, 10, 32)         \
   X(7, 1, 5, 20, 32)
 
+// Row bands per crop: 2, or ARENA_IRX_PARTS (3 / 4) for the 14x14 stage — more, shorter bands double the
+// workgroups of a launch (one per CU at batch 32 with two; four workgroups per crop at bs 1) at the price of
+// recomputing the expand halo rows.
+int g_irx_parts = -1;  // -1: ARENA_IRX_PARTS (default 2)
+
+int irx_parts(int HO) {
+  if (g_irx_parts < 0) {
+    const char* e = std::getenv("ARENA_IRX_PARTS");
+    g_irx_parts = e != nullptr ? std::atoi(e) : 2;
+  }
+  const int n = (g_irx_parts == 3 || g_irx_parts == 4) ? g_irx_parts : 2;
+  return HO == 14 ? n : 2;
+}
+
+void set_irx_parts(int n) { g_irx_parts = n; }
+
 void ir_crop_f32_prepare() {
-#define X(HO_, S_, KS_, NOT_, HC_)                                                                         \
-  static_assert(IrxGeom<HO_, S_, KS_, NOT_, HC_>::LDS <= 160 * 1024, "ir_x3: LDS budget");                 \
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_x3_kernel<HO_, S_, KS_, NOT_, HC_>,                 \
+#define X1(HO_, S_, KS_, NOT_, HC_, NP_)                                                                   \
+  static_assert(IrxGeom<HO_, S_, KS_, NOT_, HC_, NP_>::LDS <= 160 * 1024, "ir_x3: LDS budget");            \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_x3_kernel<HO_, S_, KS_, NOT_, HC_, NP_>,            \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#define X(HO_, S_, KS_, NOT_, HC_) X1(HO_, S_, KS_, NOT_, HC_, 2) X1(HO_, S_, KS_, NOT_, HC_, 3) X1(HO_, S_, KS_, NOT_, HC_, 4)
   ARENA_IRX_CONFIGS(X)
 #undef X
+#undef X1
 }
 
 // Shapes this kernel takes (mirrored by engine/validate.py::ir_crop_f32_supported; the planner marks the
@@ -386,15 +416,21 @@ bool ir_block_crop_f32(const IrParams& p, hipStream_t s) {
   if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_x3: residual needs s1, inp == oup");
   if (p.Ho != (p.H + 2 - 3) / p.stride + 1) throw std::runtime_error("ir_x3: output size mismatch");
   if (p.B <= 0) return true;
+  const int np = irx_parts(p.Ho);
+#define X1(HO_, S_, KS_, NOT_, HC_, NP_)                                                                      \
+  if (np == NP_) {                                                                                            \
+    using G = IrxGeom<HO_, S_, KS_, NOT_, HC_, NP_>;                                                          \
+    hipLaunchKernelGGL((ir_x3_kernel<HO_, S_, KS_, NOT_, HC_, NP_>), dim3((unsigned)(p.B * NP_)),             \
+                       dim3(IRX_THREADS), G::LDS, s, p);                                                      \
+    return true;                                                                                              \
+  }
 #define X(HO_, S_, KS_, NOT_, HC_)                                                                             \
   if (p.Ho == HO_ && p.stride == S_ && p.inp_pad == KS_ * 32 && p.oup_pad == NOT_ * 16 && p.hid_pad % HC_ == 0) { \
-    using G = IrxGeom<HO_, S_, KS_, NOT_, HC_>;                                                                \
-    hipLaunchKernelGGL((ir_x3_kernel<HO_, S_, KS_, NOT_, HC_>), dim3((unsigned)(p.B * 2)), dim3(IRX_THREADS),   \
-                       G::LDS, s, p);                                                                          \
-    return true;                                                                                               \
+    X1(HO_, S_, KS_, NOT_, HC_, 2) X1(HO_, S_, KS_, NOT_, HC_, 3) X1(HO_, S_, KS_, NOT_, HC_, 4)               \
   }
   ARENA_IRX_CONFIGS(X)
 #undef X
+#undef X1
   return false;
 }
 

@@ -572,11 +572,16 @@ def _ir_ref64(x, expand, dw, project, stride, res):
     (160, 960, 320, 1, 7, False),  # block 17
 ])
 @pytest.mark.parametrize("x3t", ["1", "0"])  # >= 28x28 expanding blocks: tiled x3 kernel / exact-fp32 ir_f32
-def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, x3t, monkeypatch):
+def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, x3t, monkeypatch, request):
     if H <= 14:  # the whole-map kernel (ARENA_IRC_F32=auto: the planner's default for these blocks); forced on here
-        if x3t == "0":
-            pytest.skip("ARENA_IR_X3T does not apply to the whole-map kernel")
+        # ARENA_IR_X3T does not apply to it: the "0" slot runs the 14x14 kernel with four row bands per crop
+        if x3t == "0" and H != 14:
+            pytest.skip("one row-band layout at 7x7")
         monkeypatch.setenv("ARENA_IRC_F32", "1")
+        from inference_arena_amd.ops import native
+
+        native().set_irx_parts(4 if x3t == "0" else 2)
+        request.addfinalizer(lambda: native().set_irx_parts(-1))
     monkeypatch.setenv("ARENA_IR_X3T", x3t)
     g = torch.Generator().manual_seed(inp * 7 + hid + stride)
     x = torch.randn(3, inp, H, H, generator=g)
