@@ -528,9 +528,10 @@ def main(argv=None) -> int:
             lat = list(lat)
             log(f"[rank {info.rank}] headline window: {a.steps * R / window:.0f} req/s")
         if a.path == "http" and info.is_main and a.latency_levels:
-            # the reference's low user levels behind a batcher with a short busy delay (a lone request waits
-            # 100 us, a loaded device 500 us for its batch to fill)
-            cfg = dict(batcher_config(a), max_queue_delay_us=a.level_delay_us)
+            # the reference's low user levels behind a batcher with a short busy delay: a request that finds the
+            # device idle is dispatched at once (the reference runs every request alone), a loaded device waits
+            # up to 500 us for its batch to fill
+            cfg = dict(batcher_config(a), max_queue_delay_us=a.level_delay_us, idle_queue_delay_us=0)
             f2, b2 = serve(ex, cfg)
             levels = latency_levels(f2.port, reqs, [int(u) for u in a.latency_levels.split(",") if u], a)
             log(f"[rank {info.rank}] latency levels: {levels}")
