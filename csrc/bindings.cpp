@@ -19,6 +19,7 @@
 #include "runtime/http_loadgen.h"
 #include "runtime/ipc_buffer.h"
 #include "runtime/jpeg_decode.h"
+#include "runtime/jpeg_ingest.h"
 #include "runtime/batcher.h"
 #include "runtime/split.h"
 
@@ -311,6 +312,54 @@ ExecutorConfig config_from(const py::dict& d) {
   c.host_threads = get<int>(d, "host_threads", c.host_threads);
   c.raw_out_bytes = get<int64_t>(d, "raw_out_bytes", c.raw_out_bytes);
   return c;
+}
+
+// A DynamicBatcher result callback that calls a Python function with the result dict (GIL taken on the batcher
+// thread; the function's reference is dropped under the GIL too).
+ResultCallback py_result_cb(py::function cb) {
+  // The callback is released on a batcher thread: drop the Python reference under the GIL.
+  std::shared_ptr<py::function> pycb(new py::function(std::move(cb)), [](py::function* fn) {
+    py::gil_scoped_acquire gil;
+    delete fn;
+  });
+  return [pycb](RequestResult&& r) {
+    py::gil_scoped_acquire gil;
+    py::dict d;
+    d["id"] = r.id;
+    d["error"] = r.error;
+    d["det_count"] = r.det_count;
+    const int k = (int)r.det.size();
+    py::array_t<float> det({k, 8});
+    if (k) std::memcpy(det.mutable_data(), r.det.data(), sizeof(Detection) * k);
+    const int t = (int)r.topk.size();
+    py::array_t<int32_t> ti({t, 5});
+    py::array_t<float> tl({t, 5}), tp({t, 5});
+    for (int i = 0; i < t; ++i)
+      for (int j = 0; j < 5; ++j) {
+        ti.mutable_at(i, j) = r.topk[i].idx[j];
+        tl.mutable_at(i, j) = r.topk[i].logit[j];
+        tp.mutable_at(i, j) = r.topk[i].prob[j];
+      }
+    d["det"] = det;
+    d["topk_idx"] = ti;
+    d["topk_logit"] = tl;
+    d["topk_prob"] = tp;
+    if (!r.raw.empty()) {
+      py::array_t<uint8_t> raw((py::ssize_t)r.raw.size());
+      std::memcpy(raw.mutable_data(), r.raw.data(), r.raw.size());
+      d["raw"] = raw;
+    }
+    d["batch_size"] = r.batch_size;
+    d["queue_us"] = r.queue_us;
+    d["compute_us"] = r.compute_us;
+    d["detection_ms"] = r.det_ms;       // device stage times of the batch (OP_STAMP); -1: none
+    d["classification_ms"] = r.cls_ms;
+    try {
+      (*pycb)(d);
+    } catch (py::error_already_set& e) {
+      e.discard_as_unraisable("DynamicBatcher callback");
+    }
+  };
 }
 
 // JPEG uploads given to Executor.submit / run as `bytes`: entropy-decoded here (host half of the split decoder),
@@ -642,49 +691,7 @@ PYBIND11_MODULE(_C, m) {
              } else {
                throw std::runtime_error("input must be a uint8 HxWx3 image or a float32 [3,S,S] tensor");
              }
-             // The callback is released on a batcher thread: drop the Python reference under the GIL.
-             std::shared_ptr<py::function> pycb(new py::function(std::move(cb)), [](py::function* fn) {
-               py::gil_scoped_acquire gil;
-               delete fn;
-             });
-             ResultCallback f = [pycb](RequestResult&& r) {
-               py::gil_scoped_acquire gil;
-               py::dict d;
-               d["id"] = r.id;
-               d["error"] = r.error;
-               d["det_count"] = r.det_count;
-               const int k = (int)r.det.size();
-               py::array_t<float> det({k, 8});
-               if (k) std::memcpy(det.mutable_data(), r.det.data(), sizeof(Detection) * k);
-               const int t = (int)r.topk.size();
-               py::array_t<int32_t> ti({t, 5});
-               py::array_t<float> tl({t, 5}), tp({t, 5});
-               for (int i = 0; i < t; ++i)
-                 for (int j = 0; j < 5; ++j) {
-                   ti.mutable_at(i, j) = r.topk[i].idx[j];
-                   tl.mutable_at(i, j) = r.topk[i].logit[j];
-                   tp.mutable_at(i, j) = r.topk[i].prob[j];
-                 }
-               d["det"] = det;
-               d["topk_idx"] = ti;
-               d["topk_logit"] = tl;
-               d["topk_prob"] = tp;
-               if (!r.raw.empty()) {
-                 py::array_t<uint8_t> raw((py::ssize_t)r.raw.size());
-                 std::memcpy(raw.mutable_data(), r.raw.data(), r.raw.size());
-                 d["raw"] = raw;
-               }
-               d["batch_size"] = r.batch_size;
-               d["queue_us"] = r.queue_us;
-               d["compute_us"] = r.compute_us;
-               d["detection_ms"] = r.det_ms;       // device stage times of the batch (OP_STAMP); -1: none
-               d["classification_ms"] = r.cls_ms;
-               try {
-                 (*pycb)(d);
-               } catch (py::error_already_set& e) {
-                 e.discard_as_unraisable("DynamicBatcher callback");
-               }
-             };
+             ResultCallback f = py_result_cb(std::move(cb));
              const uint8_t* data = (const uint8_t*)img.data();
              py::gil_scoped_release nogil;
              return b.enqueue(data, h, w, std::move(f), bytes, (uint8_t*)export_to);
@@ -713,6 +720,68 @@ PYBIND11_MODULE(_C, m) {
       });
 
   // closed-loop HTTP load generator (bench.py --path http, serving sweeps)
+  py::class_<JpegIngest>(m, "JpegIngest")
+      .def(py::init([](DynamicBatcher& batcher, const py::dict& cfg) {
+             IngestConfig c;
+             c.threads = get<int>(cfg, "threads", c.threads);
+             c.jpeg_device = get<bool>(cfg, "jpeg_device", c.jpeg_device);
+             c.max_image_pixels = get<int64_t>(cfg, "max_image_pixels", c.max_image_pixels);
+             c.buffer_cap = get<int64_t>(cfg, "buffer_cap", c.buffer_cap);
+             int ndev = 0;
+             const bool gpu = hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0;
+             (void)hipGetLastError();
+             if (get<bool>(cfg, "pinned", gpu)) {
+               c.host_alloc = [](size_t n) -> void* {
+                 void* p = nullptr;
+                 if (hipHostMalloc(&p, n, hipHostMallocPortable) != hipSuccess) {
+                   (void)hipGetLastError();
+                   return nullptr;
+                 }
+                 return p;
+               };
+               c.host_free = [](void* p) { (void)hipHostFree(p); };
+             }
+             py::gil_scoped_release nogil;
+             return new JpegIngest(&batcher, c);
+           }),
+           py::keep_alive<1, 2>())
+      .def(
+          "submit",
+          [](JpegIngest& g, py::bytes upload, py::function done, py::function fallback) {
+            std::string u = upload;
+            std::shared_ptr<py::function> fb(new py::function(std::move(fallback)), [](py::function* fn) {
+              py::gil_scoped_acquire gil;
+              delete fn;
+            });
+            ResultCallback cb = py_result_cb(std::move(done));
+            py::gil_scoped_release nogil;
+            g.submit(std::move(u), std::move(cb), [fb](std::string&&) {
+              py::gil_scoped_acquire gil;
+              try {
+                (*fb)();
+              } catch (py::error_already_set& e) {
+                e.discard_as_unraisable("JpegIngest fallback");
+              }
+            });
+          },
+          py::arg("upload"), py::arg("done"), py::arg("fallback"),
+          "Split-decode `upload` into the batcher: done(result dict) after its batch; fallback() (no arguments) "
+          "when the split decoder does not cover the format (the caller decodes and enqueues it itself).")
+      .def("stats",
+           [](JpegIngest& g) {
+             IngestStats s = g.stats();
+             py::dict d;
+             d["native"] = s.native;
+             d["fallback"] = s.fallback;
+             d["errors"] = s.errors;
+             d["cpu_decode_ms"] = s.cpu_decode_ms;
+             return d;
+           })
+      .def("stop", [](JpegIngest& g) {
+        py::gil_scoped_release nogil;
+        g.stop();
+      });
+
   py::class_<IpcBuffer>(m, "IpcBuffer")
       .def(py::init<size_t, int>(), py::arg("bytes"), py::arg("device") = 0)
       .def("handle", [](const IpcBuffer& b) { return py::bytes(b.handle()); })

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import asyncio
 import threading
+import os
 import time
 from concurrent.futures import ThreadPoolExecutor
 
@@ -93,6 +94,16 @@ class GpuBatchedBackend(Backend):
     async def infer(self, image: np.ndarray) -> tuple[ImageResult, dict]:
         t0 = time.perf_counter()
         d = await self.batcher.run(np.ascontiguousarray(image, dtype=np.uint8))
+        return self._finish(d, t0)
+
+    async def infer_bytes(self, data: bytes, decode) -> tuple[ImageResult, dict]:
+        """An encoded upload through the native split decoder (batching.AsyncBatcher.run_jpeg); ``decode`` is
+        the fallback for formats it does not cover."""
+        t0 = time.perf_counter()
+        d = await self.batcher.run_jpeg(data, decode, threads=int(os.environ.get("ARENA_INGEST_THREADS", "4")))
+        return self._finish(d, t0)
+
+    def _finish(self, d: dict, t0: float) -> tuple[ImageResult, dict]:
         total = (time.perf_counter() - t0) * 1e3
         q = d["queue_us"] / 1e3
         gpu = d["compute_us"] / 1e3

@@ -85,6 +85,43 @@ class AsyncBatcher:
         _enqueue_or_raise(self._b.enqueue(self._prep(x), done, int(export_to)))
         return self._check(await fut)
 
+    async def run_jpeg(self, data: bytes, decode, threads: int = 4) -> dict:
+        """An encoded upload through the native split decoder (csrc/runtime/jpeg_ingest.h: Huffman decode on C++
+        threads into pinned memory, frame reconstructed on the GPU inside the batch); formats it does not cover
+        go through ``await decode(data)`` (the caller's PIL path) and ``run``.  Decode failures raise
+        ValueError / TooLarge like the PIL path."""
+        if getattr(self, "_ingest", None) is None:
+            from ..ops import native
+            from ..processing.transforms import max_image_pixels
+
+            self._ingest = native().JpegIngest(self._b, {"threads": int(threads),
+                                                         "max_image_pixels": int(max_image_pixels())})
+        loop = asyncio.get_running_loop()
+        fut: asyncio.Future = loop.create_future()
+
+        def done(d):
+            loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(("ok", d)))
+
+        def fallback():
+            loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(("fallback", None)))
+
+        self._ingest.submit(data, done, fallback)
+        kind, d = await fut
+        if kind == "fallback":
+            return await self.run(await decode(data))
+        err = d["error"]
+        if err.startswith("Failed to decode image"):
+            raise (TooLarge(err) if "image too large" in err else ValueError(err))
+        if err == "request queue is full":
+            raise Overloaded(err)
+        if err.startswith("image exceeds"):
+            raise TooLarge(err)
+        return self._check(d)
+
+    def ingest_stats(self) -> dict | None:
+        ing = getattr(self, "_ingest", None)
+        return dict(ing.stats()) if ing is not None else None
+
     async def run_many(self, xs: list[np.ndarray]) -> list[dict]:
         return list(await asyncio.gather(*(self.run(x) for x in xs)))
 
@@ -107,4 +144,6 @@ class AsyncBatcher:
     def close(self) -> None:
         if not self._closed:
             self._closed = True
+            if getattr(self, "_ingest", None) is not None:
+                self._ingest.stop()
             self._b.shutdown()

@@ -32,7 +32,7 @@ import numpy as np
 
 from ..repository import model_config as mc
 from ..repository.store import ARCHS, ModelEntry, load_module, scan_repository
-from .batching import AsyncBatcher
+from .batching import AsyncBatcher, TooLarge
 
 log = logging.getLogger("arena.modelserver")
 
@@ -199,6 +199,7 @@ class PipelineModel(ModelHandle):
         from .app_common import DecodePool
 
         self.decode_pool = DecodePool(decode_threads)
+        self.native_decode = device == "gpu" and os.environ.get("ARENA_NATIVE_DECODE", "1") != "0"
         if device == "gpu":
             from .backends import GpuBatchedBackend
 
@@ -229,13 +230,23 @@ class PipelineModel(ModelHandle):
             raw = inputs["IMAGE_BYTES"].ravel()
             if raw.size != 1:
                 raise InferError("IMAGE_BYTES must hold exactly one encoded image")
-            try:
-                img = await self.decode_pool.decode(bytes(raw[0]))
-            except Exception as e:
-                raise InferError(str(e)) from e
+            img = None
+            if self.native_decode:
+                # split decoder: Huffman on C++ threads, reconstruction on the GPU inside the batch (PIL only for
+                # formats it does not cover); ARENA_NATIVE_DECODE=0 keeps every upload on the PIL pool
+                try:
+                    res, timing = await self.backend.infer_bytes(bytes(raw[0]), self.decode_pool.decode)
+                except (ValueError, TooLarge) as e:
+                    raise InferError(str(e)) from e
+            else:
+                try:
+                    img = await self.decode_pool.decode(bytes(raw[0]))
+                except Exception as e:
+                    raise InferError(str(e)) from e
         else:
             raise InferError("expected input IMAGE or IMAGE_BYTES")
-        res, timing = await self.backend.infer(img)
+        if img is not None:
+            res, timing = await self.backend.infer(img)
         det = np.concatenate([res.boxes, res.scores[:, None], res.classes[:, None].astype(np.float32)], 1) \
             if len(res) else np.zeros((0, 6), np.float32)
         self.stats.record(True, 1, (time.perf_counter() - t0) * 1e6, timing.get("queue_ms", 0) * 1e3,

@@ -133,3 +133,52 @@ def test_corrupt_and_oversized_inputs():
             bad[k] = int(rng.integers(0, 256))
         st, _, _ = C.jpeg_decode_host(bytes(bad))
         assert st in ("ok", "corrupt", "unsupported")
+
+
+@pytest.mark.parametrize("jpeg_device", [True, False])
+def test_ingest_matches_pil_decode_and_falls_back(jpeg_device):
+    """csrc/runtime/jpeg_ingest.h behind AsyncBatcher.run_jpeg (the model server's IMAGE_BYTES path): the same
+    answer as the PIL-decoded frame through run(); PNG goes back to the caller's decoder; a broken JPEG is a
+    ValueError like PIL's."""
+    import asyncio
+    import types
+
+    from inference_arena_amd.processing.transforms import load_image_from_bytes
+    from inference_arena_amd.server.batching import AsyncBatcher
+
+    C = native()
+    runner = types.SimpleNamespace(ex=C.EchoInstance(2, 8, 4, 200))
+    b = AsyncBatcher([runner], max_batch=8, max_queue_delay_us=500)
+    if not jpeg_device:  # host reconstruction mode of the ingest
+        b._ingest = C.JpegIngest(b._b, {"threads": 2, "jpeg_device": False})
+    rng = np.random.default_rng(4)
+    frames = [(rng.random((30 + 5 * i, 41 + 3 * i, 3)) * 255).astype(np.uint8) for i in range(6)]
+    uploads = [_enc(f, quality=85, subsampling=i % 3) for i, f in enumerate(frames)]
+    png = io.BytesIO()
+    Image.fromarray(frames[0]).save(png, "PNG")
+    calls = []
+
+    async def decode(data):
+        calls.append(len(data))
+        return load_image_from_bytes(data)
+
+    async def go():
+        a = await asyncio.gather(*(b.run_jpeg(u, decode) for u in uploads))
+        r = await asyncio.gather(*(b.run(_pil(u)) for u in uploads))
+        p = await b.run_jpeg(png.getvalue(), decode)
+        with pytest.raises(ValueError):
+            await b.run_jpeg(uploads[0][: len(uploads[0]) // 2], decode)
+        return a, r, p
+
+    try:
+        a, r, p = asyncio.run(go())
+    finally:
+        b.close()
+    for x, y in zip(a, r):
+        np.testing.assert_array_equal(x["det"], y["det"])
+        np.testing.assert_array_equal(x["topk_idx"], y["topk_idx"])
+    assert len({x["det_count"] for x in a}) > 1
+    assert calls == [len(png.getvalue())] and p["det_count"] >= 1
+    st = b.ingest_stats() if jpeg_device else None
+    if st is not None:
+        assert st["native"] == 6 and st["fallback"] == 1 and st["errors"] == 1

@@ -59,6 +59,7 @@ SOURCES = [
     "runtime/ipc_buffer.cpp",
     "runtime/trace.cpp",
     "runtime/jpeg_decode.cpp",
+    "runtime/jpeg_ingest.cpp",
     "bindings_jpeg.cpp",
     "bindings.cpp",
 ]
