@@ -747,7 +747,7 @@ PYBIND11_MODULE(_C, m) {
            py::keep_alive<1, 2>())
       .def(
           "submit",
-          [](JpegIngest& g, py::bytes upload, py::function done, py::function fallback) {
+          [](JpegIngest& g, py::bytes upload, py::function done, py::function fallback, uintptr_t export_to) {
             std::string u = upload;
             std::shared_ptr<py::function> fb(new py::function(std::move(fallback)), [](py::function* fn) {
               py::gil_scoped_acquire gil;
@@ -762,9 +762,9 @@ PYBIND11_MODULE(_C, m) {
               } catch (py::error_already_set& e) {
                 e.discard_as_unraisable("JpegIngest fallback");
               }
-            });
+            }, (uint8_t*)export_to);
           },
-          py::arg("upload"), py::arg("done"), py::arg("fallback"),
+          py::arg("upload"), py::arg("done"), py::arg("fallback"), py::arg("export_to") = 0,
           "Split-decode `upload` into the batcher: done(result dict) after its batch; fallback() (no arguments) "
           "when the split decoder does not cover the format (the caller decodes and enqueues it itself).")
       .def("stats",

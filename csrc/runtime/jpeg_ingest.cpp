@@ -57,11 +57,11 @@ void JpegIngest::stop() {
   for (auto& t : left) fail(t.done, "ingest stopped");
 }
 
-void JpegIngest::submit(std::string upload, ResultCallback done, Fallback fallback) {
+void JpegIngest::submit(std::string upload, ResultCallback done, Fallback fallback, uint8_t* export_dst) {
   {
     std::lock_guard<std::mutex> lk(mu_);
     if (!stop_) {
-      q_.push_back(Task{std::move(upload), std::move(done), std::move(fallback)});
+      q_.push_back(Task{std::move(upload), std::move(done), std::move(fallback), export_dst});
       cv_.notify_one();
       return;
     }
@@ -107,6 +107,7 @@ void JpegIngest::run(Task& t) {
   }
   const JpegInfo& ji = up->info;
   InputImage in{nullptr, ji.height, ji.width};
+  in.export_dst = t.export_dst;
   if (st == JpegStatus::Ok) {
     if (cfg_.jpeg_device) {
       up->buf = pool_->get((size_t)ji.coef_count * 2);

@@ -46,7 +46,8 @@ class JpegIngest {
   JpegIngest(const JpegIngest&) = delete;
   JpegIngest& operator=(const JpegIngest&) = delete;
 
-  void submit(std::string upload, ResultCallback done, Fallback fallback);
+  // export_dst: device address that receives the reconstructed frame (InputImage::export_dst)
+  void submit(std::string upload, ResultCallback done, Fallback fallback, uint8_t* export_dst = nullptr);
   IngestStats stats();
   void stop();
 
@@ -55,6 +56,7 @@ class JpegIngest {
     std::string upload;
     ResultCallback done;
     Fallback fallback;
+    uint8_t* export_dst = nullptr;
   };
   void loop();
   void run(Task& t);

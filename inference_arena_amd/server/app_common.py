@@ -34,6 +34,28 @@ from .schemas import Classification, DetectionBox, DetectionWithClassification, 
 log = logging.getLogger("arena.server")
 
 
+def probe_size(data: bytes) -> tuple[int, int]:
+    """(height, width) of an encoded upload from its header alone (PIL's lazy open, no pixel decode); the
+    errors of a failed decode: ValueError, TooLarge beyond ``max_image_pixels``."""
+    import io
+
+    from PIL import Image, UnidentifiedImageError
+
+    from ..processing.transforms import max_image_pixels
+    from .batching import TooLarge
+
+    if not data:
+        raise ValueError("Failed to decode image: empty payload")
+    try:
+        with Image.open(io.BytesIO(data)) as im:
+            w, h = im.size
+    except (UnidentifiedImageError, OSError, ValueError) as e:
+        raise ValueError(f"Failed to decode image: {e}") from e
+    if w * h > max_image_pixels():
+        raise TooLarge(f"Failed to decode image: image too large ({w}x{h} pixels > {max_image_pixels()})")
+    return h, w
+
+
 class DecodePool:
     """Upload decode off the event loop.  ``procs`` > 0 (``ARENA_DECODE_PROCS``): spawned decode processes
     with shared-memory delivery (server/decode_pool.py; scales with cores, unlike PIL threads whose

@@ -85,7 +85,7 @@ class AsyncBatcher:
         _enqueue_or_raise(self._b.enqueue(self._prep(x), done, int(export_to)))
         return self._check(await fut)
 
-    async def run_jpeg(self, data: bytes, decode, threads: int = 4) -> dict:
+    async def run_jpeg(self, data: bytes, decode, threads: int = 4, export_to: int = 0) -> dict:
         """An encoded upload through the native split decoder (csrc/runtime/jpeg_ingest.h: Huffman decode on C++
         threads into pinned memory, frame reconstructed on the GPU inside the batch); formats it does not cover
         go through ``await decode(data)`` (the caller's PIL path) and ``run``.  Decode failures raise
@@ -105,10 +105,10 @@ class AsyncBatcher:
         def fallback():
             loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(("fallback", None)))
 
-        self._ingest.submit(data, done, fallback)
+        self._ingest.submit(data, done, fallback, int(export_to))
         kind, d = await fut
         if kind == "fallback":
-            return await self.run(await decode(data))
+            return await self.run(await decode(data), export_to=export_to)
         err = d["error"]
         if err.startswith("Failed to decode image"):
             raise (TooLarge(err) if "image too large" in err else ValueError(err))

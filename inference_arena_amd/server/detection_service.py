@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 from contextlib import asynccontextmanager
 
 from fastapi import FastAPI, HTTPException, Request
@@ -30,7 +31,7 @@ from ..metrics import ArenaMetrics
 from ..processing import extract_crop
 from ..utils.logging import request_id_var, setup_logging
 from ..utils.settings import Settings
-from .app_common import DecodePool, FaultInjector, Timer, device_fault, new_request_id, read_upload
+from .app_common import DecodePool, FaultInjector, Timer, device_fault, new_request_id, probe_size, read_upload
 from .batching import Overloaded
 from .grpc_client import ClassificationClient, make_classification_client
 from .schemas import Classification, DetectionBox, DetectionWithClassification, HealthResponse, PredictResponse
@@ -85,16 +86,32 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
             raise HTTPException(status_code=503, detail="Service not ready")
         try:
             state["faults"].check()
-            image = await state["decode"].decode(data)
             ring = state.get("ring")
-            on_device = ring is not None and image.nbytes <= ring.slot_bytes
-            # device transport with a GPU detector: the detector copies the frame it already staged for YOLO into
-            # a ring slot, device to device inside its batch — the frame crosses PCIe once
+            image = None
+            if ring is not None:
+                h, w = probe_size(data)  # header only: decides the transport before any decode
+            else:
+                image = await state["decode"].decode(data)
+                h, w = image.shape[:2]
+            on_device = ring is not None and h * w * 3 <= ring.slot_bytes
+            # device transport with a GPU detector: the detector copies the frame it staged for YOLO into a ring
+            # slot, device to device inside its batch — the frame crosses PCIe once; with the split decoder
+            # (ARENA_NATIVE_DECODE, default on) not even as pixels: the Huffman stage runs on C++ threads and the
+            # GPU reconstructs the frame (PIL only for formats the split decoder does not cover)
             slot = ring.try_acquire() if on_device and getattr(det_be, "exports_frames", False) else None
+            split = slot is not None and hasattr(det_be, "detect_bytes") and os.environ.get(
+                "ARENA_NATIVE_DECODE", "1") != "0"
+            if image is None and not split:
+                image = await state["decode"].decode(data)
             t_det = Timer()
             try:
-                det, dtiming = await (det_be.detect(image, export_to=ring.slot_ptr(slot)) if slot is not None
-                                      else det_be.detect(image))
+                if split:
+                    det, dtiming = await det_be.detect_bytes(data, state["decode"].decode,
+                                                             export_to=ring.slot_ptr(slot))
+                elif slot is not None:
+                    det, dtiming = await det_be.detect(image, export_to=ring.slot_ptr(slot))
+                else:
+                    det, dtiming = await det_be.detect(image)
             except BaseException:
                 if slot is not None:
                     ring.release(slot)
@@ -110,7 +127,7 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
                 responses = []
             elif on_device:
                 if slot is not None:
-                    ref = ring.ref(slot, image.shape[0], image.shape[1])
+                    ref = ring.ref(slot, h, w)
                 else:  # no exporting detector (or no free slot before detection): upload the frame once more
                     loop = asyncio.get_running_loop()
                     slot, ref = await loop.run_in_executor(None, ring.put, image)

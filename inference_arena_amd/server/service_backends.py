@@ -150,8 +150,19 @@ class GpuDetectorBackend(DetectorBackend):
 
     exports_frames = True  # detect(export_to=...) copies the staged frame to a device buffer (arm B device ring)
 
+    async def detect_bytes(self, data: bytes, decode, export_to: int = 0):
+        """An encoded upload through the native split decoder (the frame is reconstructed on the GPU inside the
+        batch and, with ``export_to``, copied into the device ring from there); ``decode`` is the fallback."""
+        d = await self.batcher.run_jpeg(data, decode, threads=int(os.environ.get("ARENA_INGEST_THREADS", "4")),
+                                        export_to=export_to)
+        return self._detections(d)
+
     async def detect(self, image: np.ndarray, export_to: int = 0):
         d = await self.batcher.run(np.ascontiguousarray(image, dtype=np.uint8), export_to=export_to)
+        return self._detections(d)
+
+    @staticmethod
+    def _detections(d: dict):
         det = d["det"]
         out = np.concatenate([det[:, :5], det[:, 5:6].copy().view(np.int32).astype(np.float32)], 1)
         return out, {"queue_ms": d["queue_us"] / 1e3, "gpu_ms": d["compute_us"] / 1e3,

@@ -375,3 +375,47 @@ def test_predict_exports_the_detector_frame_into_the_ring():
         assert len(ring._free) == ring.slots
     finally:
         srv.stop()
+
+
+def test_predict_device_transport_with_the_split_decoder():
+    """Device transport + an exporting detector with the split decoder (detect_bytes): the detection service never
+    decodes the upload itself (only its header is probed for the frame size) and the answers are unchanged."""
+    from inference_arena_amd.processing.transforms import load_image_from_bytes
+    from inference_arena_amd.server.detection_service import create_app
+
+    dev = FakeDevice()
+
+    class SplitDetector(FakeDetector):
+        exports_frames = True
+
+        def __init__(self):
+            self.bytes_calls = 0
+
+        async def detect_bytes(self, data, decode, export_to=0):
+            self.bytes_calls += 1
+            image = load_image_from_bytes(data)  # stands in for the GPU reconstruction
+            buf, off = dev.resolve(export_to)
+            b = np.ascontiguousarray(image).tobytes()
+            buf[off: off + len(b)] = b
+            return await super().detect(image)
+
+    be = FakeFrameBackend(dev)
+    srv = ClassificationThread(DeviceClassifier(be, dev.open, max_delay_us=200))
+    ring = DeviceImageRing(4, 640 * 640 * 3, buffer=FakeIpcBuffer(dev, 4 * 640 * 640 * 3, 13))
+    ring.buf.ptr = dev.mem[ring.handle][0]
+    det = SplitDetector()
+    try:
+        s = Settings(LOG_LEVEL="WARNING", CLASSIFICATION_GRPC_ENDPOINT=f"127.0.0.1:{srv.port}",
+                     ARENA_CROP_TRANSPORT="device", ARENA_FANOUT="batch")
+        img = synthetic_images(1, 8)[0]
+        body, ctype = encode_multipart("file", encode_jpeg(img))
+        app = create_app(s, detector=det, ring=ring)
+        with TestClient(app) as c:
+            outs = [c.post("/predict", content=body, headers={"content-type": ctype}) for _ in range(2)]
+        h = img.shape[0]
+        for r in outs:
+            assert r.status_code == 200, r.text
+            assert [d["classification"]["class_id"] for d in r.json()["detections"]][:3] == [20, h - 5, 1]
+        assert det.bytes_calls == 2 and sum(be.batches) == 2 and len(ring._free) == ring.slots
+    finally:
+        srv.stop()
