@@ -37,6 +37,7 @@ class ResourceSampler:
         self.interval = interval
         self.roots = [psutil.Process(p) for p in pids if psutil.pid_exists(p)]
         self.samples: list[tuple[float, float, float, float | None, float | None]] = []
+        self.by_role: dict[str, list[float]] = {}  # CPU % per process role, summed over that role's processes
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
         self._cache: dict = {}
@@ -76,12 +77,18 @@ class ResourceSampler:
         import psutil
 
         cpu = mem = 0.0
+        roles: dict[str, float] = {}
         for p in procs:
             try:
-                cpu += p.cpu_percent(None)
+                c = p.cpu_percent(None)
+                cpu += c
                 mem += p.memory_info().rss / 2 ** 20
+                r = self._role(p)
+                roles[r] = roles.get(r, 0.0) + c
             except psutil.NoSuchProcess:
                 continue
+        for r, c in roles.items():
+            self.by_role.setdefault(r, []).append(c)
         busy = vram = None
         if self._gpu is not None:
             try:
@@ -93,6 +100,26 @@ class ResourceSampler:
             except Exception:  # noqa: BLE001
                 pass
         self.samples.append((time.time(), cpu, mem, busy, vram))
+
+    def _role(self, p) -> str:
+        """Process role from its command line: the arm's server modules, decode workers, model servers, ..."""
+        role = self._cache.get(("role", p.pid))
+        if role is None:
+            try:
+                cmd = " ".join(p.cmdline())
+            except Exception:  # noqa: BLE001 - vanished / no access
+                cmd = ""
+            role = "other"
+            for key, name in (("model_server", "model_server"), ("gateway", "gateway"),
+                              ("detection_service", "detection"), ("classification_service", "classification"),
+                              ("native_front", "monolithic"), ("monolithic", "monolithic"),
+                              ("forkserver", "decode_workers"), ("multiprocessing", "decode_workers"),
+                              ("start_arena", "launcher")):
+                if key in cmd:
+                    role = name
+                    break
+            self._cache[("role", p.pid)] = role
+        return role
 
     def _run(self) -> None:
         self._procs()  # prime every process's cpu counter
@@ -122,6 +149,7 @@ class ResourceSampler:
             "memory_usage_mb_max": float(a[:, 1].max()),
             "resource_samples": len(self.samples),
         }
+        out["cpu_percent_by_role"] = {r: round(float(np.mean(v)), 1) for r, v in sorted(self.by_role.items())}
         busy = [s[3] for s in self.samples if s[3] is not None]
         vram = [s[4] for s in self.samples if s[4] is not None]
         if busy:

@@ -158,9 +158,10 @@ def write_level(out_dir: Path, tag: str, res: PhaseResult, summary: dict) -> Non
 
 
 def run_sweep(base: LoadConfig, user_levels: list[int], runs: int, images: list[bytes], out_dir: Path,
-              arch: str, log=print, sample_pids: list[int] | None = None) -> list[dict]:
+              arch: str, log=print, sample_pids: list[int] | None = None, scrape: list[str] | None = None) -> list[dict]:
     """``sample_pids``: server processes (children included) whose CPU % / memory (and GPU busy / VRAM) are
-    sampled during each level (loadgen/resources.py; experiment.yaml RQ2 metrics)."""
+    sampled during each level (loadgen/resources.py; experiment.yaml RQ2 metrics).  ``scrape``: Prometheus URLs
+    (the arm's /metrics: per-stage latency histograms of the servers themselves) saved after every level."""
     rows = []
     for users in user_levels:
         for run in range(1, runs + 1):
@@ -176,6 +177,14 @@ def run_sweep(base: LoadConfig, user_levels: list[int], runs: int, images: list[
                 s.update(sampler.stop())
             s.update({"architecture": arch, "run": run})
             write_level(out_dir, f"{arch}_u{users}_r{run}", res, s)
+            for i, url in enumerate(scrape or []):
+                try:
+                    import urllib.request
+
+                    with urllib.request.urlopen(url, timeout=5) as r:
+                        (out_dir / f"{arch}_u{users}_r{run}_metrics{i}.txt").write_bytes(r.read())
+                except Exception as e:  # noqa: BLE001 - diagnostics only
+                    log(f"[{arch}] scrape {url} failed: {e}")
             rows.append(s)
             log(f"[{arch}] users={users} run={run}: {s['throughput_rps']:.1f} req/s "
                 f"p50={s['p50_latency_ms']:.1f} ms p99={s['p99_latency_ms']:.1f} ms err={s['error_rate_percent']:.2f}%")

@@ -52,8 +52,12 @@ def main(argv=None) -> int:
                               cooldown_s=a.cooldown, procs=a.procs)
             # RQ2: CPU % / memory of the arm's processes (and children: replicas, decode workers) per level
             pids = [p.pid for p in procs if getattr(p, "pid", None)]
+            # the servers' own stage histograms (cumulative: diff consecutive levels); triton: the gateway and the
+            # model server's KServe metrics port
+            scrape = [f"http://127.0.0.1:{ports[arch]}/metrics"] + (["http://127.0.0.1:8002/metrics"]
+                                                                    if arch == "triton" else [])
             rows += run_sweep(base, [int(u) for u in a.users.split(",")], a.runs, images, out, arch,
-                              log=lambda *x: print(*x, flush=True), sample_pids=pids or None)
+                              log=lambda *x: print(*x, flush=True), sample_pids=pids or None, scrape=scrape)
         finally:
             stop(procs)
     (out / "hypotheses.json").write_text(json.dumps(evaluate(rows), indent=2, default=str) + "\n")
