@@ -176,7 +176,13 @@ void Executor::alloc_slots() {
     std::memset(sl.h_in, 0, in_bytes_meta());
     ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
     ARENA_HIP_CHECK(hipEventCreate(&sl.started));
-    ARENA_HIP_CHECK(hipEventCreate(&sl.done));
+    // ARENA_SYNC=blocking: collect() sleeps on the completion interrupt instead of polling the event (HIP's
+    // default), which otherwise keeps a core busy per waiting thread for the whole device time of a batch
+    static const bool blocking = [] {
+      const char* e = std::getenv("ARENA_SYNC");
+      return e != nullptr && std::string(e) == "blocking";
+    }();
+    ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.done, blocking ? hipEventBlockingSync : hipEventDefault));
   }
 }
 
