@@ -102,23 +102,36 @@ class ResourceSampler:
         self.samples.append((time.time(), cpu, mem, busy, vram))
 
     def _role(self, p) -> str:
-        """Process role from its command line: the arm's server modules, decode workers, model servers, ..."""
-        role = self._cache.get(("role", p.pid))
-        if role is None:
+        """Process role from the command line: the arm's services (``--arch X`` of the replica launcher, the model
+        server, the classification service), the decode workers (forked from the multiprocessing fork server),
+        and for spawned children (replicas) the role of the parent."""
+        key = ("role", p.pid)
+        role = self._cache.get(key)
+        if role is not None:
+            return role
+        try:
+            args = p.cmdline()
+        except Exception:  # noqa: BLE001 - vanished / no access
+            args = []
+        cmd = " ".join(args)
+        role = "other"
+        if "forkserver" in cmd:
+            role = "decode_workers"
+        elif "--arch" in args and args.index("--arch") + 1 < len(args):
+            role = args[args.index("--arch") + 1]
+        elif "model_server" in cmd:
+            role = "model_server"
+        elif "classification_service" in cmd:
+            role = "classification"
+        elif "native_front" in cmd:
+            role = "monolithic"
+        elif "spawn_main" in cmd or "multiprocessing" in cmd:
             try:
-                cmd = " ".join(p.cmdline())
-            except Exception:  # noqa: BLE001 - vanished / no access
-                cmd = ""
-            role = "other"
-            for key, name in (("model_server", "model_server"), ("gateway", "gateway"),
-                              ("detection_service", "detection"), ("classification_service", "classification"),
-                              ("native_front", "monolithic"), ("monolithic", "monolithic"),
-                              ("forkserver", "decode_workers"), ("multiprocessing", "decode_workers"),
-                              ("start_arena", "launcher")):
-                if key in cmd:
-                    role = name
-                    break
-            self._cache[("role", p.pid)] = role
+                parent = p.parent()
+                role = self._role(parent) if parent is not None else "other"
+            except Exception:  # noqa: BLE001
+                role = "other"
+        self._cache[key] = role
         return role
 
     def _run(self) -> None:
