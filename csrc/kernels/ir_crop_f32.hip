@@ -368,14 +368,19 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
 // Row bands per crop: 2, or ARENA_IRX_PARTS (3 / 4) for the 14x14 stage — more, shorter bands double the
 // workgroups of a launch (one per CU at batch 32 with two; four workgroups per crop at bs 1) at the price of
 // recomputing the expand halo rows.
-int g_irx_parts = -1;  // -1: ARENA_IRX_PARTS (default 2)
+int g_irx_parts = -1;  // -1: ARENA_IRX_PARTS, else auto
 
-int irx_parts(int HO) {
+// Row bands per crop of the 14x14 kernel.  Auto: two for a full batch (256 workgroups for 128 crops: one per
+// CU), four for small crop capacities (bucket 1: 16 crops), where the launch is otherwise a few dozen
+// workgroups on 256 CUs — ops 73-78 at bs 1: 233 -> 211 us; at batch 32 four bands cost more than they gain
+// (479 -> 571 us; three: 446 us but a lower engine rate), profiles/r4b_irx_parts.md.
+int irx_parts(int HO, int crops) {
   if (g_irx_parts < 0) {
     const char* e = std::getenv("ARENA_IRX_PARTS");
-    g_irx_parts = e != nullptr ? std::atoi(e) : 2;
+    g_irx_parts = e != nullptr ? std::atoi(e) : 0;
   }
-  const int n = (g_irx_parts == 3 || g_irx_parts == 4) ? g_irx_parts : 2;
+  int n = g_irx_parts;
+  if (n != 2 && n != 3 && n != 4) n = crops <= 32 ? 4 : 2;
   return HO == 14 ? n : 2;
 }
 
@@ -416,7 +421,7 @@ bool ir_block_crop_f32(const IrParams& p, hipStream_t s) {
   if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_x3: residual needs s1, inp == oup");
   if (p.Ho != (p.H + 2 - 3) / p.stride + 1) throw std::runtime_error("ir_x3: output size mismatch");
   if (p.B <= 0) return true;
-  const int np = irx_parts(p.Ho);
+  const int np = irx_parts(p.Ho, p.B);
 #define X1(HO_, S_, KS_, NOT_, HC_, NP_)                                                                      \
   if (np == NP_) {                                                                                            \
     using G = IrxGeom<HO_, S_, KS_, NOT_, HC_, NP_>;                                                          \

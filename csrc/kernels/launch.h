@@ -173,7 +173,7 @@ void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole
 void set_ir_crop(bool v);
 void set_ir_crop_split(int v);  // ARENA_IR_CROP_SPLIT: workgroups per crop in ir_crop (1 or 2)  // ARENA_IR_CROP=0: 7x7-output blocks use the tile kernel (ir_crop.hip)
 void set_ir_wave(bool v);
-void set_irx_parts(int n);  // row bands per crop of the 14x14 whole-map fp32 IR kernel (2, 3, 4; ARENA_IRX_PARTS)  // ARENA_IR_WAVE=0: stride-1 blocks use the block-cooperative kernel
+void set_irx_parts(int n);  // row bands per crop of the 14x14 whole-map fp32 IR kernel (2, 3, 4; else auto)  // ARENA_IR_WAVE=0: stride-1 blocks use the block-cooperative kernel
 
 // ---------------------------------------------------------------- fused C3 block (K2/K3/K4 at 160x160 / 80x80)
 // cv1|cv2 (1x1) -> NB x Bottleneck(1x1, 3x3 [+res]) -> cv3 (1x1) with every intermediate in LDS
