@@ -145,6 +145,8 @@ void py_ir_block(const py::dict& d) {
   p.B = req<int>(d, "B");
   p.bdev = ptr<const int*>(d, "bdev");
   p.x3w = get<int>(d, "x3w", 0);
+  p.x_parts = get<int>(d, "x_parts", 0);
+  p.y_parts = get<int>(d, "y_parts", 0);
   prepare_kernels();
   if (get<int>(d, "f32", 0))
     ir_block_f32(p, stream_of(d));
@@ -467,6 +469,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_conv_v3", &set_conv_v3);
   m.def("set_ir_wave", &set_ir_wave);
   m.def("set_irx_parts", &set_irx_parts);
+  m.def("set_irx_slices_big", &set_irx_slices_big);
   m.def("set_ir_t14", &set_ir_t14);
   m.def("set_ir_crop", &set_ir_crop);
   m.def("set_ir_crop_split", &set_ir_crop_split);

@@ -136,7 +136,9 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, kq = lane >> 4;
-  const int b = blockIdx.x / NP, part = blockIdx.x - (blockIdx.x / NP) * NP;
+  const int xparts = p.x_parts > 1 ? p.x_parts : 1, yparts = p.y_parts > 1 ? p.y_parts : 1;
+  const int slice = blockIdx.x % yparts, bp_idx = blockIdx.x / yparts;
+  const int b = bp_idx / NP, part = bp_idx - (bp_idx / NP) * NP;
   if (b >= live_batch(p.B, p.bdev)) return;
   const int oy0 = part * G::NOR0;
   const int nor = imin(G::NOR0, HO - oy0);
@@ -150,7 +152,8 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
   const bf16* __restrict__ we = (const bf16*)p.we;
   const bf16* __restrict__ wp = (const bf16*)p.wp;
   const float* __restrict__ wd = (const float*)p.wd;
-  const int hid_pad = p.hid_pad, nch = hid_pad / HC;
+  const int hid_pad = p.hid_pad, nch_all = hid_pad / HC;
+  const int cb = slice * nch_all / yparts, ce = (slice + 1) * nch_all / yparts;  // this slice's hidden chunks
 
   // ---- chunk weight staging (global -> registers -> LDS); plain unrolled loops, not lambdas: a lambda
   // capturing the staging arrays by reference put them in scratch memory (80-208 B per lane)
@@ -196,8 +199,8 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
                                             : (uint8_t*)WDs + 16 * (e - NOT * 16 * G::WP_PPR); \
     if (e < G::WP_PIECES) *(u32x4*)dst = rwp[j];                                            \
   }
-  IRX_FETCH_WE(0)
-  IRX_FETCH_WP(0)
+  IRX_FETCH_WE(cb * HC)
+  IRX_FETCH_WP(cb * HC)
 
   // ---- E: zero everywhere (the border stays zero: it is the depthwise padding)
   for (int i = tid; i < G::E_BYTES / 16; i += IRX_THREADS) ((uint4*)Es)[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -217,7 +220,13 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
       const int k = ks * 32 + 8 * kq;
       float v[8];
       const bool kk = ok && k < p.inp;
-      const float4 a = *(const float4*)(src + (kk ? k : 0)), c = *(const float4*)(src + (kk ? k + 4 : 0));
+      float4 a = *(const float4*)(src + (kk ? k : 0)), c = *(const float4*)(src + (kk ? k + 4 : 0));
+      for (int j = 1; j < xparts; ++j) {  // partial sums of a hidden-sliced producer, added in order
+        const float* sj = src + j * p.inp + (kk ? k : 0);
+        const float4 a2 = *(const float4*)sj, c2 = *(const float4*)(sj + 4);
+        a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+        c.x += c2.x; c.y += c2.y; c.z += c2.z; c.w += c2.w;
+      }
       v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
       if (!kk) {
 #pragma unroll
@@ -242,13 +251,13 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
 
   IRX_STORE_WE()
   IRX_STORE_WP()
-  if (nch > 1) {
-    IRX_FETCH_WE(HC)
-    IRX_FETCH_WP(HC)
+  if (ce - cb > 1) {
+    IRX_FETCH_WE((cb + 1) * HC)
+    IRX_FETCH_WP((cb + 1) * HC)
   }
   __syncthreads();
 
-  for (int c = 0; c < nch; ++c) {
+  for (int c = cb; c < ce; ++c) {
     // ---- expand: E[pix][chunk] = relu6(We[chunk] . X + be) for this wave's hidden tiles
     if (xw) {
 #pragma unroll
@@ -271,9 +280,9 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
       }
     }
     __syncthreads();  // A: E complete; every wave is past its reads of We / be
-    if (c + 1 < nch) {
+    if (c + 1 < ce) {
       IRX_STORE_WE()
-      if (c + 2 < nch) {
+      if (c + 2 < ce) {
         IRX_FETCH_WE((c + 2) * HC)
       }
     }
@@ -319,9 +328,9 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
       }
     }
     __syncthreads();  // B: every wave is past its reads of E, Wp and the taps
-    if (c + 1 < nch) {
+    if (c + 1 < ce) {
       IRX_STORE_WP()
-      if (c + 2 < nch) {
+      if (c + 2 < ce) {
         IRX_FETCH_WP((c + 2) * HC)
       }
     }
@@ -332,24 +341,35 @@ __global__ __launch_bounds__(IRX_THREADS) void ir_x3_kernel(const IrParams p) {
 #undef IRX_FETCH_WP
 #undef IRX_STORE_WP
 
-  // ---- epilogue: + bp (+ residual, stride 1: the block input at the same pixel) -> NHWC fp32
+  // ---- epilogue: + bp (+ residual, stride 1: the block input at the same pixel) -> NHWC fp32; a hidden slice
+  // > 0 writes its bare partial sum at channel offset slice * oup
   if (qok) {
     const int oy = oy0 + q / HO, ox = q - (q / HO) * HO;
-    float* yp = (float*)p.y + (((size_t)b * HO + oy) * HO + ox) * p.y_cs;
+    float* yp = (float*)p.y + (((size_t)b * HO + oy) * HO + ox) * p.y_cs + slice * p.oup;
     const float* xr = x + (((size_t)b * HI + oy) * HI + ox) * p.x_cs;
 #pragma unroll
     for (int j = 0; j < G::OTG; ++j) {
       const int ot = ot0 + j;
       const int co = ot * 16 + 4 * kq;
       if (ot >= NOT || co >= p.oup) continue;
-      const float4 bp = *(const float4*)(p.bp + co);
-      float4 v = make_float4(acc[j][0] + bp.x, acc[j][1] + bp.y, acc[j][2] + bp.z, acc[j][3] + bp.w);
-      if (S == 1 && p.res) {
-        const float4 r = *(const float4*)(xr + co);
-        v.x += r.x;
-        v.y += r.y;
-        v.z += r.z;
-        v.w += r.w;
+      float4 v = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+      if (slice == 0) {
+        const float4 bp = *(const float4*)(p.bp + co);
+        v.x += bp.x;
+        v.y += bp.y;
+        v.z += bp.z;
+        v.w += bp.w;
+        if (S == 1 && p.res) {
+          float4 r = *(const float4*)(xr + co);
+          for (int jp = 1; jp < xparts; ++jp) {  // the block input: its partial sums in the load's order
+            const float4 r2 = *(const float4*)(xr + jp * p.inp + co);
+            r.x += r2.x; r.y += r2.y; r.z += r2.z; r.w += r2.w;
+          }
+          v.x += r.x;
+          v.y += r.y;
+          v.z += r.z;
+          v.w += r.w;
+        }
       }
       *(float4*)(yp + co) = v;
     }
@@ -374,24 +394,43 @@ int g_irx_parts = -1;  // -1: ARENA_IRX_PARTS, else auto
 // CU), four for small crop capacities (bucket 1: 16 crops), where the launch is otherwise a few dozen
 // workgroups on 256 CUs — ops 73-78 at bs 1: 233 -> 211 us; at batch 32 four bands cost more than they gain
 // (479 -> 571 us; three: 446 us but a lower engine rate), profiles/r4b_irx_parts.md.
-int irx_parts(int HO, int crops) {
+// The 7x7 stage: two bands, or one when the hidden channels are sliced over workgroups (the slices already fill
+// the chip; one band halves the split weights streamed per output pixel).
+int irx_parts(int HO, int S, int crops, int yparts) {
   if (g_irx_parts < 0) {
     const char* e = std::getenv("ARENA_IRX_PARTS");
     g_irx_parts = e != nullptr ? std::atoi(e) : 0;
   }
   int n = g_irx_parts;
   if (n != 2 && n != 3 && n != 4) n = crops <= 32 ? 4 : 2;
-  return HO == 14 ? n : 2;
+  return HO == 14 ? n : (yparts > 1 && S == 1 ? 1 : 2);
 }
 
 void set_irx_parts(int n) { g_irx_parts = n; }
+
+// Hidden slices actually used for a planned partial-sum count: all of them for small crop capacities (bucket 1:
+// a few dozen workgroups otherwise), at most ARENA_IRX_SLICES_BIG (default 2) for full batches, whose row bands
+// already give every CU a workgroup (ops 73-77 at batch 32: 3 slices 367 us, 2 slices 346 us, 1: 382 us;
+// profiles/r4c).  Producer and consumer of a partial-sum tensor see the same capacity, so they agree.
+int g_irx_big = -1;
+void set_irx_slices_big(int n) { g_irx_big = n >= 1 ? n : -1; }
+int irx_effective_parts(int planned, int crops) {
+  if (planned <= 1) return 1;
+  if (g_irx_big < 0) {
+    const char* e = std::getenv("ARENA_IRX_SLICES_BIG");
+    g_irx_big = e != nullptr ? std::atoi(e) : 2;
+    if (g_irx_big < 1) g_irx_big = 1;
+  }
+  return crops > 32 && planned > g_irx_big ? g_irx_big : planned;
+}
 
 void ir_crop_f32_prepare() {
 #define X1(HO_, S_, KS_, NOT_, HC_, NP_)                                                                   \
   static_assert(IrxGeom<HO_, S_, KS_, NOT_, HC_, NP_>::LDS <= 160 * 1024, "ir_x3: LDS budget");            \
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_x3_kernel<HO_, S_, KS_, NOT_, HC_, NP_>,            \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-#define X(HO_, S_, KS_, NOT_, HC_) X1(HO_, S_, KS_, NOT_, HC_, 2) X1(HO_, S_, KS_, NOT_, HC_, 3) X1(HO_, S_, KS_, NOT_, HC_, 4)
+#define X(HO_, S_, KS_, NOT_, HC_) \
+  X1(HO_, S_, KS_, NOT_, HC_, 1) X1(HO_, S_, KS_, NOT_, HC_, 2) X1(HO_, S_, KS_, NOT_, HC_, 3) X1(HO_, S_, KS_, NOT_, HC_, 4)
   ARENA_IRX_CONFIGS(X)
 #undef X
 #undef X1
@@ -420,18 +459,29 @@ bool ir_block_crop_f32(const IrParams& p, hipStream_t s) {
     throw std::runtime_error("ir_x3: unsupported channel geometry");
   if (p.res && (p.stride != 1 || p.inp != p.oup)) throw std::runtime_error("ir_x3: residual needs s1, inp == oup");
   if (p.Ho != (p.H + 2 - 3) / p.stride + 1) throw std::runtime_error("ir_x3: output size mismatch");
+  if ((p.x_parts > 1 ? p.x_parts : 1) * p.inp > p.x_cs || (p.y_parts > 1 ? p.y_parts : 1) * p.oup > p.y_cs)
+    throw std::runtime_error("ir_x3: partial-sum tensor narrower than its planned parts");
+  const int xparts = irx_effective_parts(p.x_parts, p.B), yparts = irx_effective_parts(p.y_parts, p.B);
+  IrParams q = p;  // the kernel reads the effective counts
+  q.x_parts = xparts;
+  q.y_parts = yparts;
+  if (xparts > 8 || yparts > 8 || yparts > p.hid_pad / 32 || p.x_cs < xparts * p.inp || p.y_cs < yparts * p.oup)
+    throw std::runtime_error("ir_x3: unsupported partial-sum geometry (<= 8 parts, <= 1 per hidden chunk)");
   if (p.B <= 0) return true;
-  const int np = irx_parts(p.Ho, p.B);
+  const int np = irx_parts(p.Ho, p.stride, p.B, yparts);
 #define X1(HO_, S_, KS_, NOT_, HC_, NP_)                                                                      \
   if (np == NP_) {                                                                                            \
     using G = IrxGeom<HO_, S_, KS_, NOT_, HC_, NP_>;                                                          \
-    hipLaunchKernelGGL((ir_x3_kernel<HO_, S_, KS_, NOT_, HC_, NP_>), dim3((unsigned)(p.B * NP_)),             \
-                       dim3(IRX_THREADS), G::LDS, s, p);                                                      \
+    if (G::NXT * G::EWPT > IRX_WAVES) /* a band's expand tiles must fit the waves */                          \
+      throw std::runtime_error("ir_x3: " + std::to_string(NP_) + " row band(s) do not fit this geometry");    \
+    hipLaunchKernelGGL((ir_x3_kernel<HO_, S_, KS_, NOT_, HC_, NP_>), dim3((unsigned)(p.B * NP_ * yparts)),    \
+                       dim3(IRX_THREADS), G::LDS, s, q);                                                      \
     return true;                                                                                              \
   }
 #define X(HO_, S_, KS_, NOT_, HC_)                                                                             \
   if (p.Ho == HO_ && p.stride == S_ && p.inp_pad == KS_ * 32 && p.oup_pad == NOT_ * 16 && p.hid_pad % HC_ == 0) { \
-    X1(HO_, S_, KS_, NOT_, HC_, 2) X1(HO_, S_, KS_, NOT_, HC_, 3) X1(HO_, S_, KS_, NOT_, HC_, 4)               \
+    X1(HO_, S_, KS_, NOT_, HC_, 1) X1(HO_, S_, KS_, NOT_, HC_, 2) X1(HO_, S_, KS_, NOT_, HC_, 3)               \
+    X1(HO_, S_, KS_, NOT_, HC_, 4)                                                                            \
   }
   ARENA_IRX_CONFIGS(X)
 #undef X

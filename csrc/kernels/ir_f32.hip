@@ -433,6 +433,8 @@ void ir_block_f32(const IrParams& p, hipStream_t s) {
     return;
   }
   if (ir_block_crop_f32(p, s)) return;  // 14x14 / 7x7 maps: whole-map x3 kernel (ir_crop_f32.hip)
+  if (p.x_parts > 1 || p.y_parts > 1)
+    throw std::runtime_error("ir_block_f32: partial-sum tensors belong to the whole-map 14x14 kernel");
   if (p.x3w) {  // split-plane weights for the tiled x3 kernel (ir_tile_x3.hip)
     if (ir_tile_x3(p, s)) return;
     throw std::runtime_error("ir_block_f32: split-plane weights for a block no x3 kernel takes");

@@ -141,6 +141,11 @@ struct IrParams {
   int B;
   const int* bdev;
   int x3w;                  // fp32: we / wp pre-split into bf16 [h|m|l] planes for ir_crop_f32.hip
+  // Hidden-sliced 14x14 blocks (ir_crop_f32.hip only; 0 / 1 = a plain tensor): the input holds x_parts partial
+  // sums at channel offsets j * inp (the block input is their sum, j = 0, 1, ... in order), and the block's
+  // hidden channels are split over y_parts workgroups per band, each writing its partial output at channel
+  // offset j * oup (partial 0 carries the project bias and the residual).
+  int x_parts, y_parts;
   // fp32 classifier front end (stem = 1, t = 1 blocks, ir_f32.hip): X is not read from memory but built per
   // tile from the batch's uint8 images: crop gather + ImageNet normalisation (crop_gather_s2d semantics) into a
   // space-to-depth tile in LDS, then the 2x2 stem conv over it (+ bias, ReLU6; zero outside the H x W map).
@@ -173,6 +178,7 @@ void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole
 void set_ir_crop(bool v);
 void set_ir_crop_split(int v);  // ARENA_IR_CROP_SPLIT: workgroups per crop in ir_crop (1 or 2)  // ARENA_IR_CROP=0: 7x7-output blocks use the tile kernel (ir_crop.hip)
 void set_ir_wave(bool v);
+void set_irx_slices_big(int n);  // hidden slices at most for crop capacities > 32 (< 1: ARENA_IRX_SLICES_BIG, default 2)
 void set_irx_parts(int n);  // row bands per crop of the 14x14 whole-map fp32 IR kernel (2, 3, 4; else auto)  // ARENA_IR_WAVE=0: stride-1 blocks use the block-cooperative kernel
 
 // ---------------------------------------------------------------- fused C3 block (K2/K3/K4 at 160x160 / 80x80)

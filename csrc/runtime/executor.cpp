@@ -558,6 +558,10 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.B = batch(r[25]);
         p.bdev = bdev(r[25]);
         p.x3w = (int)r[26];
+        p.x_parts = (int)r[27];
+        p.y_parts = (int)r[28];
+        if (!f32 && (p.x_parts > 1 || p.y_parts > 1))
+          throw std::runtime_error("executor: partial-sum ir_block tensors are fp32-only");
         p.stem = (int)r[31];
         if (p.stem) {  // fp32 classifier front end: crop gather + stem conv feed the block (ir_f32.hip)
           p.st_pool = pool;

@@ -38,7 +38,8 @@ Op record layouts (index: field) — keep in sync with executor.cpp:
   YOLORAW  1-12 heads as DECODE, 13-15 strides, 16 out_buf (raw [84, A] fp32 per image)
   IRBLOCK  1 x_buf 2 x_coff 3 x_cs 4 H 5 W 6 inp 7 inp_pad 8 hid_pad 9 oup 10 oup_pad 11 stride
            12 expand 13 res 14 we 15 be 16 wd 17 bd 18 wp 19 bp 20 y_buf 21 y_coff 22 y_cs 23 Ho 24 Wo
-           25 batch_kind 26 x3w 27-30 reserved (0) 31 stem 32 crops_buf 33 S 34-36 mean
+           25 batch_kind 26 x3w 27 x_parts 28 y_parts (0 / 1: plain tensors; > 1: partial sums of a
+           hidden-sliced 14x14 block, IrParams.x_parts) 29-30 reserved (0) 31 stem 32 crops_buf 33 S 34-36 mean
            37-39 inv_std (float bits) 40 stem w_off 41 stem b_off
            (fused MobileNetV2 inverted residual, csrc/kernels/ir_block.hip / ir_f32.hip; stem = 1: fp32 crop
             gather + s2d stem conv computed inside the block-1 kernel, x_buf unused)
@@ -315,11 +316,23 @@ def ir_x3_plan(H: int, W: int, stride: int, inp: int, hid_pad: int, oup_pad: int
     return 0, inp16
 
 
+def irx_tail() -> bool:
+    """``ARENA_IRX_TAIL`` (default 0): with hidden slicing (``ARENA_IRX_SLICES`` > 1) the 14 -> 7 block and the
+    7x7 blocks also run as the whole-map x3 kernel (one row band, hidden channels over workgroups, partial sums
+    between blocks) instead of expand GEMM + depthwise + project GEMM."""
+    if os.environ.get("ARENA_IRX_TAIL", "0").lower() in ("0", "false", "no", "off"):
+        return False
+    try:
+        return int(os.environ.get("ARENA_IRX_SLICES", "6")) > 1
+    except ValueError:
+        return True
+
+
 def ir_crop_f32_planned(H: int, stride: int, inp_pad: int, hid_pad: int, oup_pad: int, expand: int) -> bool:
     from .validate import ir_crop_f32_supported
 
     policy = ir_crop_f32_policy()
-    if policy == "none" or (policy == "auto" and not (H == 14 and stride == 1)):
+    if policy == "none" or (policy == "auto" and not (H == 14 and stride == 1) and not (irx_tail() and H in (14, 7))):
         return False
     return ir_crop_f32_supported(H, stride, inp_pad, hid_pad, oup_pad, expand)
 
@@ -449,12 +462,17 @@ class ProgramBuilder:
         self._emit(rec, src, dst)
 
     def ir_block(self, src: View, dst: View, expand, dw, project, *, stride: int, res: bool,
-                 kind: int = CROPS) -> None:
+                 kind: int = CROPS, x_parts: int = 1, y_parts: int = 1) -> None:
         """Fused inverted residual: ``expand`` = (w [hid,inp,1,1], b) or None (t = 1 blocks),
-        ``dw`` = (w [hid,1,3,3], b), ``project`` = (w [oup,hid,1,1], b); BN already folded."""
-        if dst.C != project[0].shape[0]:
-            raise ValueError(f"ir_block: destination C {dst.C} != oup {project[0].shape[0]}")
-        pk = pack_ir_weights(expand, dw, project, src.C, k_align=16 if self.f32 else 32)
+        ``dw`` = (w [hid,1,3,3], b), ``project`` = (w [oup,hid,1,1], b); BN already folded.
+
+        ``x_parts`` / ``y_parts`` > 1 (fp32 14x14 whole-map blocks, csrc/kernels/ir_crop_f32.hip): the source view
+        holds ``x_parts`` partial sums of the block input side by side (C = x_parts * inp), and the block's hidden
+        channels are split over ``y_parts`` workgroups per row band that write ``y_parts`` partial outputs
+        (dst C = y_parts * oup) — the next block adds them while loading its input."""
+        if dst.C != project[0].shape[0] * y_parts:
+            raise ValueError(f"ir_block: destination C {dst.C} != oup {project[0].shape[0]} x {y_parts} parts")
+        pk = pack_ir_weights(expand, dw, project, src.C // max(1, x_parts), k_align=16 if self.f32 else 32)
         inp, inp_pad, hid_pad, oup, oup_pad = pk["inp"], pk["inp_pad"], pk["hid_pad"], pk["oup"], pk["oup_pad"]
         f32 = lambda t: t.float().contiguous().numpy().tobytes()  # noqa: E731
         mat = f32 if self.f32 else bf16_bytes  # exact-fp32 programs keep fp32 weights
@@ -464,7 +482,7 @@ class ProgramBuilder:
         if self.f32:
             x3w, inp_x3 = ir_x3_plan(H, W, stride, inp, hid_pad, oup_pad, int(expand is not None))
             if x3w and inp_x3 != inp_pad:  # the x3 kernels step K by 32
-                pk = pack_ir_weights(expand, dw, project, src.C, k_align=32)
+                pk = pack_ir_weights(expand, dw, project, src.C // max(1, x_parts), k_align=32)
                 inp, inp_pad, hid_pad, oup, oup_pad = pk["inp"], pk["inp_pad"], pk["hid_pad"], pk["oup"], \
                     pk["oup_pad"]
         mat_x3 = (lambda t: bf16_raw_bytes(split_bf16x3(t))) if x3w else mat  # noqa: E731
@@ -472,8 +490,12 @@ class ProgramBuilder:
                 self.weights.add(mat(pk["wd"])), self.weights.add(f32(pk["bd"])),
                 self.weights.add(mat_x3(pk["wp"])), self.weights.add(f32(pk["bp"]))]
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+        if (x_parts > 1 or y_parts > 1) and not (x3w and H == W and H in (14, 7) and inp % 4 == 0
+                                                 and src.C == inp * x_parts and y_parts <= hid_pad // 32 and max(x_parts, y_parts) <= 8):
+            raise ValueError("ir_block: partial-sum tensors need the fp32 14x14 whole-map kernel")
         rec = [OP_IRBLOCK, src.bid, src.coff, src.cs, H, W, inp, inp_pad, hid_pad, oup, oup_pad, stride,
-               int(expand is not None), int(res), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind, x3w]
+               int(expand is not None), int(res), *offs, dst.bid, dst.coff, dst.cs, Ho, Wo, kind, x3w,
+               int(x_parts) if x_parts > 1 else 0, int(y_parts) if y_parts > 1 else 0]
         self._emit(rec, src, dst)
 
     def ir_block_stem(self, crops: Buffer, dst: View, stem, dw, project, *, S: int, mean, std,

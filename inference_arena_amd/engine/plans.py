@@ -272,6 +272,32 @@ def fuse_block_f32(blk, H: int) -> bool:
     return ir_crop_f32_planned(H, blk.stride, inp_pad, hid_pad, oup_pad, expand)
 
 
+def irx_slices() -> int:
+    """``ARENA_IRX_SLICES`` (default 6): fp32 14x14 stride-1 blocks (MobileNetV2 features[8..13]; with
+    ``ARENA_IRX_TAIL`` also 14 -> 7 and 7x7) split their hidden channels over up to this many workgroups per row
+    band and hand the next block partial sums (csrc/kernels/ir_crop_f32.hip, IrParams.x_parts / y_parts; the
+    executor uses all of them for small crop capacities, ``ARENA_IRX_SLICES_BIG`` for full batches); 1 keeps one
+    workgroup per band and plain tensors."""
+    try:
+        return max(1, min(8, int(os.environ.get("ARENA_IRX_SLICES", "6"))))
+    except ValueError:
+        return 6
+
+
+def _sliceable_f32(blk, H: int) -> bool:
+    """A block the hidden-sliced whole-map kernel takes: a 14x14 or 7x7 input the kernel is planned for (stride-1
+    14x14 blocks; with ``ARENA_IRX_TAIL`` also 14 -> 7 and 7x7), expanding, with at least as many 32-channel
+    hidden chunks as slices (the kernel's partial-sum geometry)."""
+    from .planner import ir_crop_f32_planned
+
+    if H not in (14, 7) or blk.expand is None or blk.inp % 4 or blk.oup % 4:
+        return False
+    inp_pad = (blk.inp + 15) // 16 * 16
+    hid_pad = (blk.hidden + 31) // 32 * 32
+    oup_pad = (blk.oup + 15) // 16 * 16
+    return hid_pad // 32 >= irx_slices() and ir_crop_f32_planned(H, blk.stride, inp_pad, hid_pad, oup_pad, 1)
+
+
 def fuse_stem_ir_f32_default() -> bool:
     """``ARENA_F32_STEM_IR`` (default 1): fp32 programs run crop gather + stem conv + MobileNetV2 block 1 as one
     kernel (ProgramBuilder.ir_block_stem); the s2d crops and the 112 x 112 x 32 stem map are never stored."""
@@ -349,17 +375,24 @@ def plan_mobilenet(pb: ProgramBuilder, m: MobileNetV2, crops, S: int, mean, std,
         pb.conv(View(X, 0, 16), View(F, 0, 32), s2d_stem_3x3(w), b, pad=(1, 1), act="relu6", kind=CROPS_,
                 out_hw=(h, h))
     cur, H = F, h
+    parts = 1  # partial sums held by `cur` (hidden-sliced 14x14 blocks)
+    slices = irx_slices() if pb.f32 and fuse_ir == "f32" else 1
     for i, blk in enumerate(m.blocks):
         if i == 0 and first_fused:
             continue
         Ho = (H + 2 - 3) // blk.stride + 1
         if fuse_block(blk, H, fuse_ir):
-            O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup, kind=CROPS_)
-            pb.ir_block(View(cur, 0, blk.inp), View(O, 0, blk.oup),
+            nxt = m.blocks[i + 1] if i + 1 < len(m.blocks) else None
+            yp = slices if (slices > 1 and _sliceable_f32(blk, H) and nxt is not None
+                            and fuse_block(nxt, Ho, fuse_ir) and _sliceable_f32(nxt, Ho)) else 1
+            O = pb.tensor(f"m{i}.out", Ho, Ho, blk.oup * yp, kind=CROPS_)
+            pb.ir_block(View(cur, 0, blk.inp * parts), View(O, 0, blk.oup * yp),
                         fold(blk.expand) if blk.expand is not None else None, fold(blk.dw), fold(blk.project),
-                        stride=blk.stride, res=blk.use_res, kind=CROPS_)
-            cur, H = O, Ho
+                        stride=blk.stride, res=blk.use_res, kind=CROPS_, x_parts=parts, y_parts=yp)
+            cur, H, parts = O, Ho, yp
             continue
+        if parts != 1:
+            raise AssertionError("partial-sum tensor feeds an unfused block")
         if blk.expand is not None:
             E = pb.tensor(f"m{i}.exp", H, H, blk.hidden, kind=CROPS_)
             pb.conv(View(cur, 0, blk.inp), View(E, 0, blk.hidden), *fold(blk.expand), act="relu6", kind=CROPS_)

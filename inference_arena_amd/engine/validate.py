@@ -182,8 +182,12 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                     or inp % (4 if f32 else 8):
                 raise ProgramError(f"op {i}: bad ir_block channel geometry")
             x3w = int(r[26])
-            if any(int(v) for v in r[27:31]):
-                raise ProgramError(f"op {i}: ir_block fields 27-30 are reserved (0)")
+            if any(int(v) for v in r[29:31]):
+                raise ProgramError(f"op {i}: ir_block fields 29-30 are reserved (0)")
+            xp, yp = max(1, int(r[27])), max(1, int(r[28]))
+            if (xp > 1 or yp > 1) and not (f32 and x3w and H == W and H in (14, 7) and max(xp, yp) <= 8
+                                           and yp <= hid_pad // 32 and inp % 4 == 0 and oup % 4 == 0):
+                raise ProgramError(f"op {i}: partial-sum ir_block tensors need the fp32 14x14 whole-map kernel")
             if x3w and not (f32 and (int(r[31]) or (H == W and ir_crop_f32_supported(H, S, inp_pad, hid_pad, oup_pad,
                                                                                       int(r[12])))
                                      or ir_tile_x3_supported(S, inp_pad, hid_pad, oup_pad, int(r[12])))):
@@ -202,8 +206,8 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
                 weights(i, int(r[40]), 32 * 64 * (6 if x3w else 4), "stem weight")
                 weights(i, int(r[41]), 32 * 4, "stem bias")
             else:
-                view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp, el, "ir input")
-            view(i, r[20], int(r[21]), int(r[22]), n * Ho * Wo, oup, el, "ir output")
+                view(i, r[1], int(r[2]), int(r[3]), n * H * W, inp * xp, el, "ir input")
+            view(i, r[20], int(r[21]), int(r[22]), n * Ho * Wo, oup * yp, el, "ir output")
             wel = 6 if x3w else el  # three bf16 planes per weight
             weights(i, int(r[14]), hid_pad * inp_pad * wel, "ir expand weight")
             weights(i, int(r[15]), hid_pad * 4, "ir expand bias")

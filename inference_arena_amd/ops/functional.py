@@ -122,12 +122,15 @@ def dwconv3x3_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride:
 
 
 def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: bool = False,
-                  bdev: torch.Tensor | None = None) -> torch.Tensor:
+                  bdev: torch.Tensor | None = None, x_parts: int = 1, y_parts: int = 1) -> torch.Tensor:
     """Fused MobileNetV2 inverted residual (expand 1x1+ReLU6 -> dw3x3+ReLU6 -> project 1x1 [+x]).
-    ``expand``/``dw``/``project`` are (weight, bias) pairs with BN folded; ``expand`` None for t=1."""
+    ``expand``/``dw``/``project`` are (weight, bias) pairs with BN folded; ``expand`` None for t=1.
+    ``x_parts`` / ``y_parts`` (fp32 14x14 whole-map kernel): ``x`` holds x_parts partial sums of the input side by
+    side on the channel axis; the result holds y_parts partial sums (hidden channels split over workgroups)."""
     from ..engine.planner import ir_x3_plan, pack_ir_weights, split_bf16x3
 
-    B, H, W, C = x.shape
+    B, H, W, Ct = x.shape
+    C = Ct // x_parts
     f32 = x.dtype == torch.float32  # fp32 kernels (csrc/kernels/ir_f32.hip, ir_crop_f32.hip, ir_tile_x3.hip)
     pk = pack_ir_weights(expand, dw, project, C, k_align=16 if f32 else 32)
     x3w = 0
@@ -136,18 +139,19 @@ def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: boo
         if x3w and inp_x3 != pk["inp_pad"]:
             pk = pack_ir_weights(expand, dw, project, C, k_align=32)
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
-    y = torch.empty(B, Ho, Wo, pk["oup"], dtype=x.dtype, device=x.device)
+    y = torch.empty(B, Ho, Wo, pk["oup"] * y_parts, dtype=x.dtype, device=x.device)
     mat = torch.float32 if f32 else torch.bfloat16
     dev = {k: (pk[k].to(mat) if k in ("we", "wd", "wp") else pk[k].float()).contiguous().to(x.device)
            for k in ("we", "be", "wd", "bd", "wp", "bp")}
     if x3w:  # the whole-map kernel reads pre-split [h|m|l] bf16 expand / project weights
         dev["we"] = split_bf16x3(pk["we"]).to(x.device)
         dev["wp"] = split_bf16x3(pk["wp"]).to(x.device)
-    native().ir_block({"x": _ptr(x), "x_cs": C, "H": H, "W": W, "inp": C, "inp_pad": pk["inp_pad"],
+    native().ir_block({"x": _ptr(x), "x_cs": Ct, "H": H, "W": W, "inp": C, "inp_pad": pk["inp_pad"],
                        "hid_pad": pk["hid_pad"], "oup": pk["oup"], "oup_pad": pk["oup_pad"], "stride": stride,
                        "expand": int(expand is not None), "res": int(res),
-                       **{k: _ptr(v) for k, v in dev.items()}, "y": _ptr(y), "y_cs": pk["oup"], "Ho": Ho,
-                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32), "x3w": x3w})
+                       **{k: _ptr(v) for k, v in dev.items()}, "y": _ptr(y), "y_cs": pk["oup"] * y_parts, "Ho": Ho,
+                       "Wo": Wo, "B": B, "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32), "x3w": x3w,
+                       "x_parts": x_parts, "y_parts": y_parts})
     torch.cuda.synchronize(x.device)  # keep the packed weights alive until the kernel ran
     return y
 

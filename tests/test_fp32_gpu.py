@@ -596,6 +596,62 @@ def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, x3t, m
     assert err < 2e-5 * (1.0 + ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("parts,crops", [(2, 5), (3, 5), (6, 5), (6, 40)])
+@pytest.mark.parametrize("bands", [2, 4])
+def test_ir_block_f32_hidden_slices_chain(device, parts, crops, bands, request):
+    """Hidden-sliced 14x14 blocks (IrParams.x_parts / y_parts): block A writes its partial sums, block B adds
+    them while loading its input (and for its residual) and writes one tensor — equal to the fp64 chain.  Crop
+    capacities > 32 use at most set_irx_slices_big of the planned parts (3 here), on both sides."""
+    from inference_arena_amd.ops import native
+
+    native().set_irx_parts(bands)
+    native().set_irx_slices_big(3)
+    request.addfinalizer(lambda: (native().set_irx_parts(-1), native().set_irx_slices_big(-1)))
+    eff = min(parts, 3) if crops > 32 else parts
+    g = torch.Generator().manual_seed(parts * 11 + bands)
+    blocks = []
+    for inp, hid, oup in ((64, 384, 96), (96, 576, 96)):
+        blocks.append(((torch.randn(hid, inp, 1, 1, generator=g) / inp ** 0.5, torch.randn(hid, generator=g) * 0.1),
+                       (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1),
+                       (torch.randn(oup, hid, 1, 1, generator=g) / hid ** 0.5, torch.randn(oup, generator=g) * 0.1)))
+    x = torch.randn(crops, 64, 14, 14, generator=g)
+    mid = AF.ir_block_nhwc(_nhwc(x).to(device), *blocks[0], stride=1, res=False, y_parts=parts)
+    assert mid.shape[-1] == 96 * parts
+    y = AF.ir_block_nhwc(mid, *blocks[1], stride=1, res=True, x_parts=parts)
+    r0 = _ir_ref64(x, *blocks[0], 1, False)
+    ref = _ir_ref64(r0.float(), *blocks[1], 1, True)
+    got = y.permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs().max().item()
+    assert err < 2e-5 * (1.0 + ref.abs().max().item()), err
+    summed = mid.reshape(crops, 14, 14, parts, 96)[..., :eff, :].double().sum(3).permute(0, 3, 1, 2).cpu()
+    assert (summed - r0).abs().max().item() < 2e-5 * (1.0 + r0.abs().max().item())
+
+
+@pytest.mark.parametrize("parts", [1, 3, 5])
+def test_ir_block_f32_hidden_slices_tail(device, parts, monkeypatch):
+    """The 14 -> 7 block and the 7x7 blocks on the whole-map kernel with hidden slices (ARENA_IRX_TAIL): one row
+    band per crop at 7x7, partial sums from block 14 through block 16 into block 17's plain output."""
+    monkeypatch.setenv("ARENA_IRC_F32", "1")  # the whole-map kernel for every 14x14 / 7x7 block
+    g = torch.Generator().manual_seed(parts + 70)
+
+    def blk(inp, hid, oup):
+        return ((torch.randn(hid, inp, 1, 1, generator=g) / inp ** 0.5, torch.randn(hid, generator=g) * 0.1),
+                (torch.randn(hid, 1, 3, 3, generator=g) / 3, torch.randn(hid, generator=g) * 0.1),
+                (torch.randn(oup, hid, 1, 1, generator=g) / hid ** 0.5, torch.randn(oup, generator=g) * 0.1))
+
+    b14, b15, b17 = blk(96, 576, 160), blk(160, 960, 160), blk(160, 960, 320)
+    x = torch.randn(6, 96, 14, 14, generator=g)
+    a = AF.ir_block_nhwc(_nhwc(x).to(device), *b14, stride=2, res=False, y_parts=parts)
+    c = AF.ir_block_nhwc(a, *b15, stride=1, res=True, x_parts=parts, y_parts=parts)
+    y = AF.ir_block_nhwc(c, *b17, stride=1, res=False, x_parts=parts)
+    r14 = _ir_ref64(x, *b14, 2, False)
+    r15 = _ir_ref64(r14.float(), *b15, 1, True)
+    ref = _ir_ref64(r15.float(), *b17, 1, False)
+    got = y.permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs().max().item()
+    assert err < 2e-5 * (1.0 + ref.abs().max().item()), err
+
+
 def test_fp32_program_fuses_the_high_resolution_blocks():
     from inference_arena_amd.engine.plans import plan_pipeline
     from inference_arena_amd.models.zoo import default_models

@@ -266,6 +266,30 @@ def test_fp32_program_with_whole_map_ir_blocks_validates(monkeypatch):
         validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)
 
 
+@pytest.mark.parametrize("slices", ["1", "3", "6"])
+def test_fp32_hidden_sliced_14x14_chain(monkeypatch, slices):
+    """ARENA_IRX_SLICES: the stride-1 14x14 blocks (features 8-13) hand partial sums to each other — block 8
+    reads a plain tensor, blocks 9-13 read `slices` parts, blocks 8-12 write them, block 13 writes one tensor for
+    the unfused 14 -> 7 block; the buffers are sized for the parts (static validator)."""
+    from inference_arena_amd.engine import plans
+    from inference_arena_amd.engine.planner import OP_IRBLOCK
+    from inference_arena_amd.engine.validate import validate_program
+    from inference_arena_amd.models.zoo import default_models
+
+    monkeypatch.setenv("ARENA_IRX_SLICES", slices)
+    y, m = default_models(0)
+    prog = plans.plan_pipeline(y, m, conf_thr=0.5, iou_thr=0.45, dtype="fp32")
+    ir = [o for o in prog.ops if int(o[0]) == OP_IRBLOCK and int(o[4]) == 14 and int(o[11]) == 1]
+    n = int(slices)
+    assert [max(1, int(o[27])) for o in ir] == [1] + [n] * 5
+    assert [max(1, int(o[28])) for o in ir] == [n] * 5 + [1]
+    bufs = {b.id: b for b in prog.buffers}
+    for o in ir:
+        assert bufs[int(o[20])].C == int(o[9]) * max(1, int(o[28]))
+    for B in (1, 32):
+        validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)
+
+
 def test_tuning_table_concurrent_writers(tmp_path):
     """Several processes storing different entries at once (replicas missing the table together): every entry
     survives and the table is valid JSON throughout (one shared .tmp name tore the file)."""
