@@ -97,7 +97,7 @@ class Replicas:
                       "ARENA_REPLICA_RANK": env.get("ARENA_REPLICA_RANK", env.get("RANK", str(i))),
                       "ARENA_RESTARTED": str(self.restarts + 1)})
             e.pop("MASTER_PORT", None)
-            out = open(log, "a") if log else subprocess.DEVNULL
+            out = open(log, "a") if log else None  # None: the supervisor's own stdout (its log file)
             self.procs[i] = subprocess.Popen(argv, env=e, stdout=out, stderr=subprocess.STDOUT)
             self._fails[i] = k + 1
             self._started[i] = now
@@ -137,7 +137,7 @@ def launch(arch: str, n: int, *, port: int = 8100, stride: int = 0, host: str = 
                   "MASTER_PORT": str(master), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
                   "ARENA_PROCS_PER_GPU": str(procs_per_gpu), "ARENA_FIRST_GPU": str(first_gpu)})
         log = os.path.join(log_dir, f"replica_{r}.log") if log_dir else None
-        out = open(log, "w") if log else subprocess.DEVNULL
+        out = open(log, "w") if log else None  # None: the supervisor's own stdout (a failed start stays visible)
         argv = [sys.executable, "-m", "inference_arena_amd.server.replica", "--arch", arch, "--host", host,
                 "--port", str(port), "--port-stride", str(stride)]
         procs.append(subprocess.Popen(argv, env=e, stdout=out, stderr=subprocess.STDOUT))

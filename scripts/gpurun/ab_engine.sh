@@ -20,7 +20,7 @@ for v in $VALS; do
   for bs in 32 1; do
     env $VAR=$v $S 300 gpurun_out/$T/prof_${v}_$bs.log rocprofv3 --kernel-trace --output-format csv -d gpurun_out/$T/p_${v}_$bs -o eng -- python3 tools/profile_engine.py --dtype fp32 --batch $bs --batches 12 || exit 1
     f=$(find gpurun_out/$T/p_${v}_$bs -name "eng_kernel_trace.csv" | head -1)
-    python tools/analyze_trace.py "$f" --dtype fp32 --replays 8 --out gpurun_out/$T/ops_${v}_bs$bs.md > /dev/null 2>&1
+    env $VAR=$v python tools/analyze_trace.py "$f" --dtype fp32 --replays 8 --out gpurun_out/$T/ops_${v}_bs$bs.md > /dev/null 2>&1
     echo "$VAR=$v bs=$bs: $(grep 'device time' gpurun_out/$T/ops_${v}_bs$bs.md)"
     rm -rf gpurun_out/$T/p_${v}_$bs
   done

@@ -28,6 +28,6 @@ LIMIT=$(( (W + M + C) * R * $(echo $U | tr ',' '\n' | wc -l) + 240 ))
 timeout -k 10 $LIMIT python scripts/serving_sweep.py --archs $ARCH --users $U --procs 4 --procs-per-gpu $PPG \
   --warmup $W --measure $M --cooldown $C --runs $R --out $O > $O/sweep.log 2>&1
 # keep what the analysis reads (summaries, CSV, hypotheses, the sweep log); server logs can exceed gpurun's
-# 64 MiB copy-back limit
-find $O -type f -size +2M -delete
+# 64 MiB copy-back limit: keep their last 256 KiB (a failed start's traceback is at the end)
+for f in $(find $O -type f -size +2M); do tail -c 262144 "$f" > "$f.tail" && mv "$f.tail" "$f"; done
 grep -h "users=" $O/sweep.log
