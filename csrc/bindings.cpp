@@ -154,6 +154,36 @@ void py_ir_block(const py::dict& d) {
     ir_block(p, stream_of(d));
 }
 
+// one fused C3 block (fp32: c3_x3.hip over pre-split weights; bf16: c3_fused.hip)
+void py_c3_block(const py::dict& d) {
+  C3Params p{};
+  p.x = ptr<const void*>(d, "x");
+  p.xs = req<int>(d, "xs");
+  p.B = req<int>(d, "B");
+  p.H = req<int>(d, "H");
+  p.W = req<int>(d, "W");
+  p.bdev = ptr<const int*>(d, "bdev");
+  p.C1 = req<int>(d, "C1");
+  p.CH = req<int>(d, "CH");
+  p.NB = req<int>(d, "NB");
+  p.res = req<int>(d, "res");
+  p.w12 = ptr<const void*>(d, "w12");
+  p.b12 = ptr<const float*>(d, "b12");
+  p.wb1[0] = p.wb1[1] = ptr<const void*>(d, "wb1");
+  p.bb1[0] = p.bb1[1] = ptr<const float*>(d, "bb1");
+  p.wb2[0] = p.wb2[1] = ptr<const void*>(d, "wb2");
+  p.bb2[0] = p.bb2[1] = ptr<const float*>(d, "bb2");
+  p.w3 = ptr<const void*>(d, "w3");
+  p.b3 = ptr<const float*>(d, "b3");
+  p.y = ptr<void*>(d, "y");
+  p.ys = req<int>(d, "ys");
+  prepare_kernels();
+  if (get<int>(d, "f32", 0))
+    c3_x3(p, stream_of(d));
+  else
+    c3_fused(p, stream_of(d));
+}
+
 void py_sppf(const py::dict& d) {
   SppfParams p{};
   p.buf = ptr<void*>(d, "buf");
@@ -465,6 +495,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dwconv3x3", &py_dwconv);
   m.def("sppf_pool", &py_sppf);
   m.def("ir_block", &py_ir_block);
+  m.def("c3_block", &py_c3_block);
   m.def("set_conv_pw", &set_conv_pw);
   m.def("set_conv_v3", &set_conv_v3);
   m.def("set_ir_wave", &set_ir_wave);

@@ -309,6 +309,7 @@ void prepare_kernels() {
   head_pool_f32_prepare();
   x3_halo_prepare();
   x3g_prepare();
+  c3_x3_prepare();
   x3hg_prepare();
   stem_s2_f32_prepare();
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)sppf_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

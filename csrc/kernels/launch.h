@@ -203,6 +203,11 @@ struct C3Params {
   int ys;
 };
 bool c3_fused_supported(int C1, int CH, int NB, bool res, int H, int W);
+// fp32 form (csrc/kernels/c3_x3.hip): fp32 x / y, weights as pre-split bf16 planes [rows][3][K] (w12 [32][3][32],
+// wb1 [16][3][16], wb2 [16][3][160] with k = tap * 16 + c, w3 [32][3][32]); the 160x160 block only.
+bool c3_x3_supported(int C1, int CH, int NB, bool res, int H, int W);
+void c3_x3(const C3Params& p, hipStream_t s);
+void c3_x3_prepare();
 void c3_fused(const C3Params& p, hipStream_t s);
 
 // ---------------------------------------------------------------- SPPF pools (K5)

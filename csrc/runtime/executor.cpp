@@ -450,8 +450,6 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
     // field 47: activation precision of the op (0 bf16, 1 exact fp32; planner.OP_DTYPE_FIELD)
     const bool f32 = r[kDtypeField] == 1;
     const int eb = f32 ? 4 : 2;
-    if (f32 && r[0] == OP_C3FUSED)
-      throw std::runtime_error("op " + std::to_string(r[0]) + " has no fp32 kernel");
     switch (r[0]) {
       case OP_CONV: {
         ConvParams p{};
@@ -686,7 +684,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
       }
       case OP_C3FUSED: {
         C3Params p{};
-        p.x = resolve(bk, sl, r[1], r[2], 2);
+        p.x = resolve(bk, sl, r[1], r[2], eb);
         p.xs = (int)r[3];
         p.H = (int)r[4];
         p.W = (int)r[5];
@@ -704,11 +702,14 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         }
         p.w3 = W + r[20];
         p.b3 = (const float*)(W + r[21]);
-        p.y = resolve(bk, sl, r[22], r[23], 2);
+        p.y = resolve(bk, sl, r[22], r[23], eb);
         p.ys = (int)r[24];
         p.B = batch(r[25]);
         p.bdev = bdev(r[25]);
-        c3_fused(p, s);
+        if (f32)
+          c3_x3(p, s);  // fp32-accurate form over pre-split weights (c3_x3.hip)
+        else
+          c3_fused(p, s);
         break;
       }
       case OP_STEMFUSED: {

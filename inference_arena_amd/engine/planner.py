@@ -562,14 +562,29 @@ class ProgramBuilder:
     def c3_fused(self, src: View, dst: View, H: int, W: int, cv12: tuple, bottlenecks: list, cv3: tuple, *,
                  res: bool, kind: int = IMAGES) -> None:
         """A whole C3 block as one op: ``cv12`` = (w, b) of cv1|cv2 stacked [2CH, C1, 1, 1]; ``bottlenecks`` =
-        [((w1, b1), (w2, b2)), ...] with w1 [CH, CH, 1, 1], w2 [CH, CH, 3, 3]; ``cv3`` = (w, b) [2CH, 2CH, 1, 1]."""
-        self._bf16_only("c3_fused")
+        [((w1, b1), (w2, b2)), ...] with w1 [CH, CH, 1, 1], w2 [CH, CH, 3, 3]; ``cv3`` = (w, b) [2CH, 2CH, 1, 1].
+        fp32 programs: the 160x160 block only (C1 32, CH 16, one bottleneck with shortcut), weights as pre-split
+        bf16 planes for csrc/kernels/c3_x3.hip."""
         w12, b12 = cv12
         ch2, c1 = w12.shape[0], w12.shape[1]
         CH, NB = ch2 // 2, len(bottlenecks)
         if c1 != src.C or dst.C != ch2 or not 1 <= NB <= 2:
             raise ValueError("c3_fused: channel / bottleneck count mismatch")
         rec = [OP_C3FUSED, src.bid, src.coff, src.cs, H, W, c1, CH, NB, int(res)]
+        if self.f32:
+            if (c1, CH, NB, bool(res)) != (32, 16, 1, True) or H % 8 or W % 16:
+                raise ValueError("c3_fused: the fp32 kernel takes the 160x160 block (C1 32, c_ 16, n 1, shortcut)")
+            x3 = lambda t: bf16_raw_bytes(split_bf16x3(t))  # noqa: E731
+            (w1, b1), (w2, b2) = bottlenecks[0]
+            w2k = torch.zeros(CH, 160)  # k = (ky * 3 + kx) * CH + ci, 144 -> 160 (five 32-deep K steps)
+            w2k[:, :9 * CH] = w2.detach().float().permute(0, 2, 3, 1).reshape(CH, 9 * CH)
+            w3, b3 = cv3
+            parts = [x3(w12.reshape(ch2, c1)), f32_bytes(b12)]
+            parts += [x3(w1.reshape(CH, CH)), f32_bytes(b1), x3(w2k), f32_bytes(b2)] * 2  # slot 1 unused (NB 1)
+            parts += [x3(w3.reshape(ch2, ch2)), f32_bytes(b3)]
+            rec += [self.weights.add(b) for b in parts] + [dst.bid, dst.coff, dst.cs, kind]
+            self._emit(rec, src, dst)
+            return
         wb, bb, _, _ = pack_conv_weight(w12, b12)
         rec += [self.weights.add(wb), self.weights.add(bb)]
         for k in range(2):

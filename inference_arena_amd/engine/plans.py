@@ -83,11 +83,20 @@ def fuse_c3_policy() -> str:
     return {"0": "none", "false": "none", "off": "none", "1": "auto", "true": "auto"}.get(v, v)
 
 
+def fuse_c3_f32() -> bool:
+    """``ARENA_FUSE_C3_F32`` (default 0 until measured faster): fp32 programs run the 160x160 C3 block (C1 32,
+    c_ 16, one bottleneck) as one fp32-accurate kernel (csrc/kernels/c3_x3.hip) instead of four convs."""
+    return os.environ.get("ARENA_FUSE_C3_F32", "0").lower() not in ("0", "false", "no", "off")
+
+
 def _c3(pb: ProgramBuilder, m, src: View, dst: View, H: int, W: int, name: str) -> None:
     c_ = m.c_
     res = bool(m.m[0].add)
-    policy = fuse_c3_policy() if not pb.f32 else "none"
-    allowed = C3_FUSED if policy == "all" else C3_FUSED_AUTO if policy == "auto" else set()
+    if pb.f32:
+        allowed = {(32, 16, 1, True)} if fuse_c3_f32() and fuse_c3_policy() != "none" else set()
+    else:
+        policy = fuse_c3_policy()
+        allowed = C3_FUSED if policy == "all" else C3_FUSED_AUTO if policy == "auto" else set()
     if ((src.C, c_, len(m.m), res) in allowed and H % 8 == 0 and W % 16 == 0
             and all(bool(bn.add) == res for bn in m.m)):
         w1, b1 = fold(m.cv1)

@@ -122,7 +122,7 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         if off < 0 or off + n > wbytes:
             raise ProgramError(f"op {i}: {what} reads weights [{off}, {off + n}) of {wbytes}")
 
-    fused = (OP_C3FUSED,)  # bf16-only fused kernels (fp32 stem_fused: the letterbox + stem + s2 conv form only)
+    fused = ()  # bf16-only fused kernels (fp32 stem_fused: the letterbox + stem + s2 conv form only; fp32 C3: 160x160)
     for i, r in enumerate(prog.ops):
         op = int(r[0])
         kind_n = lambda k: crop_cap if int(k) == CROPS else B  # noqa: E731
@@ -226,11 +226,21 @@ def validate_program(prog: Program, B: int, crop_cap: int, *, max_det: int, cand
         elif op == OP_C3FUSED:
             n = kind_n(r[25])
             H, W, C1, CH, NB, res = (int(v) for v in r[4:10])
-            if (C1, CH, NB, bool(res)) not in {(32, 16, 1, True), (64, 32, 2, True), (128, 32, 1, False)} \
-                    or H % 8 or W % 16:
+            ok = {(32, 16, 1, True)} if f32 else {(32, 16, 1, True), (64, 32, 2, True), (128, 32, 1, False)}
+            if (C1, CH, NB, bool(res)) not in ok or H % 8 or W % 16:
                 raise ProgramError(f"op {i}: unsupported fused C3 geometry {(C1, CH, NB, res, H, W)}")
-            view(i, r[1], int(r[2]), int(r[3]), n * H * W, C1, 2, "c3 input")
-            view(i, r[22], int(r[23]), int(r[24]), n * H * W, 2 * CH, 2, "c3 output")
+            view(i, r[1], int(r[2]), int(r[3]), n * H * W, C1, el, "c3 input")
+            view(i, r[22], int(r[23]), int(r[24]), n * H * W, 2 * CH, el, "c3 output")
+            if f32:  # pre-split planes (c3_x3.hip): [2CH][3][C1], [CH][3][CH], [CH][3][160], [2CH][3][2CH]
+                weights(i, int(r[10]), 2 * CH * 3 * C1 * 2, "c3 cv1|cv2 weight")
+                weights(i, int(r[11]), 2 * CH * 4, "c3 cv1|cv2 bias")
+                weights(i, int(r[12]), CH * 3 * CH * 2, "c3 bottleneck cv1 weight")
+                weights(i, int(r[13]), CH * 4, "c3 bottleneck cv1 bias")
+                weights(i, int(r[14]), CH * 3 * 160 * 2, "c3 bottleneck cv2 weight")
+                weights(i, int(r[15]), CH * 4, "c3 bottleneck cv2 bias")
+                weights(i, int(r[20]), 2 * CH * 3 * 2 * CH * 2, "c3 cv3 weight")
+                weights(i, int(r[21]), 2 * CH * 4, "c3 cv3 bias")
+                continue
             weights(i, int(r[10]), 2 * CH * C1 * 2, "c3 cv1|cv2 weight")
             weights(i, int(r[11]), 2 * CH * 4, "c3 cv1|cv2 bias")
             k3 = (9 * CH + 31) // 32 * 32

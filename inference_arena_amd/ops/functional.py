@@ -156,6 +156,28 @@ def ir_block_nhwc(x: torch.Tensor, expand, dw, project, *, stride: int, res: boo
     return y
 
 
+def c3_x3_nhwc(x: torch.Tensor, cv12, bottleneck, cv3) -> torch.Tensor:
+    """fp32 YOLOv5 C3 block at 160x160 geometry (C1 32, c_ 16, one bottleneck with shortcut) as one kernel
+    (csrc/kernels/c3_x3.hip); ``cv12`` = (w [32, 32, 1, 1], b) of cv1|cv2 stacked, ``bottleneck`` =
+    ((w1 [16, 16, 1, 1], b1), (w2 [16, 16, 3, 3], b2)), ``cv3`` = (w [32, 32, 1, 1], b); BN folded."""
+    from ..engine.planner import split_bf16x3
+
+    B, H, W, C = x.shape
+    (w1, b1), (w2, b2) = bottleneck
+    w2k = torch.zeros(16, 160)
+    w2k[:, :144] = w2.detach().float().permute(0, 2, 3, 1).reshape(16, 144)
+    dev = {"w12": split_bf16x3(cv12[0].reshape(32, 32)), "b12": cv12[1].float(),
+           "wb1": split_bf16x3(w1.reshape(16, 16)), "bb1": b1.float(), "wb2": split_bf16x3(w2k), "bb2": b2.float(),
+           "w3": split_bf16x3(cv3[0].reshape(32, 32)), "b3": cv3[1].float()}
+    dev = {k: v.contiguous().to(x.device) for k, v in dev.items()}
+    y = torch.empty(B, H, W, 32, dtype=torch.float32, device=x.device)
+    native().c3_block({"x": _ptr(x), "xs": C, "B": B, "H": H, "W": W, "bdev": 0, "C1": 32, "CH": 16, "NB": 1,
+                       "res": 1, **{k: _ptr(v) for k, v in dev.items()}, "y": _ptr(y), "ys": 32,
+                       "stream": _stream(), "f32": 1})
+    torch.cuda.synchronize(x.device)
+    return y
+
+
 def sppf_nhwc(buf: torch.Tensor, C: int) -> torch.Tensor:
     """In place: buf[..., C:4C] = cascaded 5x5 max pools of buf[..., :C]."""
     B, H, W, Ct = buf.shape

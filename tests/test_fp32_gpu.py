@@ -652,6 +652,52 @@ def test_ir_block_f32_hidden_slices_tail(device, parts, monkeypatch):
     assert err < 2e-5 * (1.0 + ref.abs().max().item()), err
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 24, 48), (1, 8, 16), (3, 16, 32)])
+def test_c3_x3_matches_fp64(device, B, H, W):
+    """The fp32 C3 block kernel (csrc/kernels/c3_x3.hip: cv1|cv2, bottleneck 1x1 + 3x3 + shortcut, cv3, all in
+    one workgroup per 8 x 16 tile with a recomputed halo) against the four convs in fp64."""
+    g = torch.Generator().manual_seed(B * 100 + H + W)
+    x = torch.randn(B, 32, H, W, generator=g)
+    cv12 = (torch.randn(32, 32, 1, 1, generator=g) / 32 ** 0.5, torch.randn(32, generator=g) * 0.1)
+    bn = ((torch.randn(16, 16, 1, 1, generator=g) / 4, torch.randn(16, generator=g) * 0.1),
+          (torch.randn(16, 16, 3, 3, generator=g) / 12, torch.randn(16, generator=g) * 0.1))
+    cv3 = (torch.randn(32, 32, 1, 1, generator=g) / 32 ** 0.5, torch.randn(32, generator=g) * 0.1)
+    y = AF.c3_x3_nhwc(_nhwc(x).to(device), cv12, bn, cv3)
+    silu = lambda t: t * torch.sigmoid(t)  # noqa: E731
+    d = lambda t: t.double()  # noqa: E731
+    T = silu(F.conv2d(d(x), d(cv12[0]), d(cv12[1])))
+    U = silu(F.conv2d(T[:, :16], d(bn[0][0]), d(bn[0][1])))
+    T1 = T[:, :16] + silu(F.conv2d(U, d(bn[1][0]), d(bn[1][1]), padding=1))
+    ref = silu(F.conv2d(torch.cat([T1, T[:, 16:]], 1), d(cv3[0]), d(cv3[1])))
+    got = y.permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs().max().item()
+    assert err < 2e-5 * (1.0 + ref.abs().max().item()), err
+
+
+def test_fp32_fused_c3_program_matches_unfused(dense_models, device, monkeypatch):
+    """fp32 pipeline with the 160x160 C3 block as one kernel vs the four-conv program: the block output at the
+    fp32 level and identical detections / classifications."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    imgs = synthetic_images(3, 51) + synthetic_images(1, 52, hw=(333, 500))
+    monkeypatch.setenv("ARENA_FUSE_C3_F32", "0")
+    plain = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False, dtype="fp32")
+    monkeypatch.setenv("ARENA_FUSE_C3_F32", "1")
+    fused = GpuPipeline(*dense_models, device=0, buckets=[4], share_buffers=False, dtype="fp32")
+    assert sum(1 for op in fused.program.ops if int(op[0]) == 16) == 1
+    assert sum(1 for op in plain.program.ops if int(op[0]) == 16) == 0
+    a, b = plain.infer(imgs), fused.infer(imgs)
+    for i in range(len(imgs)):
+        x, y = plain.read_buffer("b2", 4, i), fused.read_buffer("b2", 4, i)
+        np.testing.assert_allclose(y, x, rtol=0, atol=2e-5 * (1.0 + np.abs(x).max()))
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        if len(x):
+            np.testing.assert_allclose(y.boxes, x.boxes, atol=1e-2)
+            assert [int(t) for t in x.topk_idx[:, 0]] == [int(t) for t in y.topk_idx[:, 0]]
+
+
 def test_fp32_program_fuses_the_high_resolution_blocks():
     from inference_arena_amd.engine.plans import plan_pipeline
     from inference_arena_amd.models.zoo import default_models

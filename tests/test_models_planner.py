@@ -290,6 +290,26 @@ def test_fp32_hidden_sliced_14x14_chain(monkeypatch, slices):
         validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)
 
 
+@pytest.mark.parametrize("flag,n", [("1", 1), ("0", 0)])
+def test_fp32_program_fuses_the_160_c3_block(monkeypatch, flag, n):
+    """ARENA_FUSE_C3_F32: the fp32 program runs the 160x160 C3 block (C1 32, c_ 16, one bottleneck) as one op
+    with pre-split weight planes (csrc/kernels/c3_x3.hip); the other C3 blocks stay four-conv."""
+    from inference_arena_amd.engine import plans
+    from inference_arena_amd.engine.planner import OP_C3FUSED
+    from inference_arena_amd.engine.validate import validate_program
+    from inference_arena_amd.models.zoo import default_models
+
+    monkeypatch.setenv("ARENA_FUSE_C3_F32", flag)
+    y, m = default_models(0)
+    prog = plans.plan_pipeline(y, m, conf_thr=0.5, iou_thr=0.45, dtype="fp32")
+    c3 = [o for o in prog.ops if int(o[0]) == OP_C3FUSED]
+    assert len(c3) == n
+    if n:
+        assert [int(v) for v in c3[0][4:10]] == [160, 160, 32, 16, 1, 1] and int(c3[0][47]) == 1
+    for B in (1, 32):
+        validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)
+
+
 def test_tuning_table_concurrent_writers(tmp_path):
     """Several processes storing different entries at once (replicas missing the table together): every entry
     survives and the table is valid JSON throughout (one shared .tmp name tore the file)."""

@@ -126,7 +126,7 @@ def test_supervise_keeps_rank_and_backs_off(tmp_path):
     for p in procs:
         p.wait()
     specs = [(argv, {"RANK": str(r), "PATH": os.environ.get("PATH", "")}, r, None) for r in range(2)]
-    rep = Replicas(procs, 8100, 1, specs, max_restarts=3, backoff_s=0.2, healthy_s=60.0)
+    rep = Replicas(procs, 8100, 1, specs, max_restarts=3, backoff_s=1.0, healthy_s=60.0)  # > a loaded spawn
     assert rep.supervise() == 2  # first restart: immediate
     for p in rep.procs:
         p.wait()
