@@ -9,3 +9,6 @@ T=${1:-rehearse2}
 mkdir -p gpurun_out/$T
 $S 600 gpurun_out/$T/bench2.log python bench.py --gpus 2 --steps 10 --warmup 3 --no-secondary-bf16 --no-secondary-inproc || exit 1
 grep -v "^\[Gloo\]" gpurun_out/$T/bench2.log | tail -4 | cut -c1-900
+# the node-level front door: both ranks bind one port (SO_REUSEPORT), rank 0's load generator drives it
+$S 600 gpurun_out/$T/bench2_shared.log python bench.py --gpus 2 --steps 10 --warmup 3 --front shared --no-secondary-bf16 --no-secondary-inproc || exit 1
+grep -v "^\[Gloo\]" gpurun_out/$T/bench2_shared.log | tail -4 | cut -c1-900
