@@ -45,6 +45,7 @@ SOURCES = [
     "kernels/conv_pw.hip",
     "kernels/conv3x3_v3.hip",
     "kernels/c3_fused.hip",
+    "kernels/c3_x3.hip",
     "kernels/preprocess.hip",
     "kernels/stem_fused.hip",
     "kernels/detect.hip",
