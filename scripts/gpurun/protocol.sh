@@ -24,6 +24,7 @@ if [ "${ENVELOPE:-0}" != "0" ]; then
   PPG=1
   export ARENA_DECODE_THREADS=${DTHREADS:-2}
 fi
+PPG=${PROCS_PER_GPU:-$PPG}  # serving processes per GPU (triton: model-server and gateway processes each)
 LIMIT=$(( (W + M + C) * R * $(echo $U | tr ',' '\n' | wc -l) + 240 ))
 timeout -k 10 $LIMIT python scripts/serving_sweep.py --archs $ARCH --users $U --procs 4 --procs-per-gpu $PPG \
   --warmup $W --measure $M --cooldown $C --runs $R --out $O > $O/sweep.log 2>&1
