@@ -14,7 +14,11 @@ experiment.yaml lists for the hypotheses.
 
 Many users need many sockets: the generator runs one aiohttp session per
 process and can fan out over ``procs`` processes (multiprocessing) so that
-the client is never the bottleneck at high load.
+the client is never the bottleneck at high load.  ``engine="native"``
+(``ARENA_LOADGEN=native``) drives the same closed loop from the C++ epoll
+load generator (csrc/runtime/http_loadgen.cpp, ``procs`` threads): at
+thousands of requests/s the Python client's own CPU competes with the servers
+on a shared box.
 """
 from __future__ import annotations
 
@@ -26,6 +30,7 @@ import multiprocessing as mp
 import random
 import time
 from dataclasses import asdict, dataclass, field
+from dataclasses import field as dc_field
 from pathlib import Path
 
 import numpy as np
@@ -42,6 +47,7 @@ class LoadConfig:
     procs: int = 1
     seed: int = 42
     field: str = "file"
+    engine: str = dc_field(default_factory=lambda: os.environ.get("ARENA_LOADGEN", "aiohttp"))
 
 
 @dataclass
@@ -101,9 +107,36 @@ def _proc_main(args):
     return asyncio.run(_drive(cfg, users, images))
 
 
+def _run_native(cfg: LoadConfig, images: list[bytes]) -> list:
+    """The closed loop on the C++ load generator: every user keeps one keep-alive connection busy for the three
+    phases; samples carry user -1 (the generator does not tag requests by user)."""
+    from urllib.parse import urlsplit
+
+    from ..ops import native
+    from ..server.multipart import encode_multipart
+
+    u = urlsplit(cfg.url)
+    reqs = []
+    for img in images:
+        body, ctype = encode_multipart(cfg.field, img, filename="image.jpg", content_type="image/jpeg")
+        reqs.append((f"POST {u.path or '/'} HTTP/1.1\r\nHost: {u.hostname}\r\nContent-Type: {ctype}\r\n"
+                     f"Content-Length: {len(body)}\r\n\r\n").encode() + body)
+    random.Random(cfg.seed).shuffle(reqs)
+    lg = native().HttpLoadGen({"host": u.hostname or "127.0.0.1", "port": u.port or 80, "users": cfg.users,
+                               "threads": max(1, min(cfg.procs, cfg.users))}, reqs)
+    lg.start()
+    time.sleep(cfg.warmup_s + cfg.measure_s + cfg.cooldown_s)
+    lg.stop(cfg.timeout_s)
+    r = lg.records()
+    return [(float(t), -1, float(lat) * 1e3, int(st) if st > 0 else 599, int(d))
+            for t, lat, st, d in zip(r["t_done"], r["latency"], r["status"], r["dets"])]
+
+
 def run_level(cfg: LoadConfig, images: list[bytes]) -> PhaseResult:
     """Run one (users) level with all phases; returns every completed request."""
     t0 = time.perf_counter()
+    if cfg.engine == "native":
+        return PhaseResult(cfg.users, sorted(_run_native(cfg, images)), time.perf_counter() - t0)
     procs = max(1, min(cfg.procs, cfg.users))
     if procs == 1:
         samples = asyncio.run(_drive(cfg, range(cfg.users), images))
@@ -134,6 +167,7 @@ def summarize(res: PhaseResult, cfg: LoadConfig) -> dict:
         "max_latency_ms": float(lat.max()) if lat.size else float("nan"),
         "mean_detections": float(np.mean(ndet)) if ndet else float("nan"),
         "measure_s": cfg.measure_s,
+        "loadgen": cfg.engine,
     }
 
 

@@ -54,6 +54,30 @@ def test_closed_loop_against_live_server(tmp_path):
     assert {r[1] for r in res.samples} == {0, 1, 2}
 
 
+def test_native_engine_closed_loop(tmp_path):
+    """ARENA_LOADGEN=native: the same closed loop from the C++ load generator (csrc/runtime/http_loadgen.cpp) —
+    requests counted in the window, the injected failures as errors, detections parsed from the JSON."""
+    from tests.test_server_monolithic import FakeBackend
+
+    from inference_arena_amd.server.monolithic import create_app
+    from inference_arena_amd.utils.settings import Settings
+
+    app = create_app(Settings(LOG_LEVEL="WARNING", ARENA_FAULT_EVERY=10), FakeBackend())
+    server, t, port = _serve(app)
+    try:
+        imgs = [encode_jpeg(im) for im in synthetic_images(3, 1, hw=(120, 160))]
+        cfg = LoadConfig(url=f"http://127.0.0.1:{port}/predict", users=3, warmup_s=0.3, measure_s=1.0,
+                         cooldown_s=0.2, procs=2, engine="native")
+        res = run_level(cfg, imgs)
+        s = summarize(res, cfg)
+    finally:
+        server.should_exit = True
+        t.join(10)
+    assert s["loadgen"] == "native" and s["requests"] > 10 and s["throughput_rps"] > 5
+    assert 5 <= s["error_rate_percent"] <= 15
+    assert s["p50_latency_ms"] <= s["p99_latency_ms"] and s["mean_detections"] == 2
+
+
 def test_hypothesis_evaluation():
     rows = []
     for arch, p99, p50 in (("monolithic", 10, 5), ("microservices", 11, 6), ("triton", 12, 5)):
