@@ -325,6 +325,30 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 - 1, ix0 = ox0 - 1;
 
+  // Every weight / constant of the three GEMM phases is requested here, before the gather: fetched at the head of
+  // each phase (after its barrier), they were three serial global round trips per workgroup.
+  const int nt = wave & 1;  // this wave's 16 stem output channels (A2)
+  u32x4 ws[6];
+  {
+    const bf16* wrow = (const bf16*)p.st_w + (size_t)(nt * 16 + col) * 3 * 64 + 8 * kq;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) ws[ks * 3 + pl] = *(const u32x4*)(wrow + pl * 64 + ks * 32);
+  }
+  const float4 bb = *(const float4*)(p.st_b + nt * 16 + 4 * kq);
+  float4 ct[4];  // per-tap mean constants of this lane's 4 stem channels
+#pragma unroll
+  for (int tp = 0; tp < 4; ++tp) ct[tp] = *(const float4*)(p.st_b + 32 + tp * 32 + nt * 16 + 4 * kq);
+  const int g = tid & 7;  // depthwise channel group (4 channels) of this thread
+  float4 wk[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)((const float*)p.wd + (size_t)k * 32 + 4 * g);
+  const float4 bdw = *(const float4*)((const float*)p.bd + 4 * g);
+  const bf16* wprow = (const bf16*)p.wp + (size_t)col * 3 * 32 + 8 * kq;
+  const bf16x8 pah = *(const bf16x8*)wprow, pam = *(const bf16x8*)(wprow + 32), pal = *(const bf16x8*)(wprow + 64);
+  const float4 bpv = *(const float4*)((const float*)p.bp + 4 * kq);
+
   // ---- A1: crop gather -> s2d tile (origin (iy0 - 1, ix0 - 1): the 2x2 stem conv pads top / left by one).
   // The crop resize returns uint8 values k (cv2 INTER_LINEAR, bilinear_rgb), and the normalised input
   // (k / 255 - mean_c) / std_c is affine in k: the planner folds 1 / (255 std_c) into the stem weights and the
@@ -368,17 +392,6 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
 
   // ---- A2: X = relu6(stem(s2d) + b) over the halo tile (x3 MFMAs, K = 2 steps of 32), zero outside the map
   {
-    const int nt = wave & 1;  // this wave's 16 stem output channels
-    const bf16* wrow = (const bf16*)p.st_w + (size_t)(nt * 16 + col) * 3 * 64 + 8 * kq;
-    u32x4 ws[6];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) ws[ks * 3 + pl] = *(const u32x4*)(wrow + pl * 64 + ks * 32);
-    const float4 bb = *(const float4*)(p.st_b + nt * 16 + 4 * kq);
-    float4 ct[4];  // per-tap mean constants of this lane's 4 stem channels
-#pragma unroll
-    for (int tp = 0; tp < 4; ++tp) ct[tp] = *(const float4*)(p.st_b + 32 + tp * 32 + nt * 16 + 4 * kq);
     const int S2 = p.st_S >> 1;
 #pragma unroll
     for (int i = 0; i < ET; ++i) {
@@ -421,12 +434,6 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
 
   // ---- depthwise 3x3 on X (t = 1: X is the hidden map) + bias + ReLU6 -> split planes of D
   {
-    const int g = tid & 7;
-    const float* wd = (const float*)p.wd;
-    float4 wk[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) wk[k] = *(const float4*)(wd + (size_t)k * 32 + 4 * g);
-    const float4 bdw = *(const float4*)((const float*)p.bd + 4 * g);
 #pragma unroll 1
     for (int qi = 0; qi < POUT / 32; ++qi) {  // reads issued ahead of the FMAs, as in ir_tile_x3_kernel
       const int q = (tid >> 3) + 32 * qi;
@@ -460,23 +467,20 @@ __global__ __launch_bounds__(256) void ir_stem_x3_kernel(const IrParams p) {
   __syncthreads();
 
   // ---- project 32 -> 16 (x3 MFMAs) + bias -> NHWC fp32
-  const bf16* wrow = (const bf16*)p.wp + (size_t)col * 3 * 32 + 8 * kq;
-  const bf16x8 ah = *(const bf16x8*)wrow, am = *(const bf16x8*)(wrow + 32), al = *(const bf16x8*)(wrow + 64);
   float* yb = (float*)p.y + (size_t)b * p.Ho * p.Wo * p.y_cs;
 #pragma unroll
   for (int j = 0; j < PPW; ++j) {
     const int mt = wave + 4 * j;
     if (mt >= PAIRS) break;
     const uint8_t* d = Ds + (mt * 16 + col) * ITX_DPB + 16 * kq;
-    const f32x4 acc = itx_mfma(ah, am, al, *(const bf16x8*)d, *(const bf16x8*)(d + 64), *(const bf16x8*)(d + 128),
+    const f32x4 acc = itx_mfma(pah, pam, pal, *(const bf16x8*)d, *(const bf16x8*)(d + 64), *(const bf16x8*)(d + 128),
                                f32x4{0.f, 0.f, 0.f, 0.f});
     const int q = mt * 16 + col;
     const int oy = oy0 + q / TW, ox = ox0 + q % TW;
     const int co = 4 * kq;
     if (oy >= p.Ho || ox >= p.Wo || co >= p.oup) continue;
-    const float4 bp = *(const float4*)((const float*)p.bp + co);
     *(float4*)(yb + ((size_t)oy * p.Wo + ox) * p.y_cs + co) =
-        make_float4(acc[0] + bp.x, acc[1] + bp.y, acc[2] + bp.z, acc[3] + bp.w);
+        make_float4(acc[0] + bpv.x, acc[1] + bpv.y, acc[2] + bpv.z, acc[3] + bpv.w);
   }
 }
 

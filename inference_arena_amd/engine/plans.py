@@ -84,9 +84,10 @@ def fuse_c3_policy() -> str:
 
 
 def fuse_c3_f32() -> bool:
-    """``ARENA_FUSE_C3_F32`` (default 0 until measured faster): fp32 programs run the 160x160 C3 block (C1 32,
-    c_ 16, one bottleneck) as one fp32-accurate kernel (csrc/kernels/c3_x3.hip) instead of four convs."""
-    return os.environ.get("ARENA_FUSE_C3_F32", "0").lower() not in ("0", "false", "no", "off")
+    """``ARENA_FUSE_C3_F32`` (default 1): fp32 programs run the 160x160 C3 block (C1 32, c_ 16, one bottleneck) as
+    one fp32-accurate kernel (csrc/kernels/c3_x3.hip) instead of four convs (101.7 vs 156 us per batch of 32,
+    profiles/r4h/)."""
+    return os.environ.get("ARENA_FUSE_C3_F32", "1").lower() not in ("0", "false", "no", "off")
 
 
 def _c3(pb: ProgramBuilder, m, src: View, dst: View, H: int, W: int, name: str) -> None:

@@ -23,6 +23,24 @@ def _other_gpu() -> int:
     return 1 if torch.cuda.device_count() > 1 else 0
 
 
+def _same_topk(a, b, tol=1e-4, boxes=None):
+    """fp32 programs of other crop capacities sum in other orders (the 14x14 blocks split their hidden channels
+    over more workgroups at small capacities, engine/plans.py irx_slices; the split detector is tuned on its own):
+    logits agree to ~1e-6, so the top-5 may only differ where two logits are within that of each other.  With
+    ``boxes`` (both sides' detections) only crops whose integer window (int() of each coordinate, the reference's
+    crop rule) is the same are compared: a box ~1e-5 px from an integer crops one pixel row / column apart."""
+    rows = np.arange(len(a.topk_idx))
+    if boxes is not None:
+        win = lambda bx: tuple(int(v) for v in bx[:4])  # noqa: E731
+        rows = np.array([i for i, (p, q) in enumerate(zip(*boxes)) if win(p) == win(q)], dtype=np.int64)
+        assert len(rows) >= 0.8 * len(a.topk_idx), "too many crops moved between the programs"
+    np.testing.assert_allclose(a.topk_logit[rows], b.topk_logit[rows], rtol=tol, atol=tol)
+    for ia, ib, la in zip(a.topk_idx[rows], b.topk_idx[rows], a.topk_logit[rows]):
+        for j in np.nonzero(ia != ib)[0]:
+            gaps = [abs(la[j] - la[k]) for k in (j - 1, j + 1) if 0 <= k < len(la)]
+            assert min(gaps) <= 2 * tol * (1 + abs(la[j])), (ia, ib, la)
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_split_matches_fused(dense_models, device, dtype):
     from inference_arena_amd.data.synthetic import synthetic_images
@@ -42,9 +60,11 @@ def test_split_matches_fused(dense_models, device, dtype):
             # the split detector / classifier programs are tuned on their own: other conv tilings of the
             # same layers, i.e. other fp32 summation orders (~1e-5 relative after 60 layers and the DFL)
             np.testing.assert_allclose(a.boxes, b.boxes, rtol=2e-5, atol=5e-3)
-            np.testing.assert_allclose(a.topk_logit, b.topk_logit, rtol=1e-4, atol=1e-4)
         np.testing.assert_array_equal(a.classes, b.classes)
-        np.testing.assert_array_equal(a.topk_idx, b.topk_idx)
+        if dtype == "bf16":
+            np.testing.assert_array_equal(a.topk_idx, b.topk_idx)
+        else:
+            _same_topk(a, b)
 
 
 def test_split_overflow_passes_and_batcher(dense_models, device):
@@ -61,7 +81,7 @@ def test_split_overflow_passes_and_batcher(dense_models, device):
     got = split.infer(imgs)
     assert sum(len(r) for r in got) > 16
     for a, b in zip(ref, got):
-        np.testing.assert_array_equal(a.topk_idx, b.topk_idx)
+        _same_topk(a, b, boxes=(a.boxes, b.boxes))
     bat = native().DynamicBatcher([split.instance], {"max_batch": 4, "max_queue_delay_us": 2000})
     done = threading.Event()
     res = {}
@@ -78,4 +98,7 @@ def test_split_overflow_passes_and_batcher(dense_models, device):
         d = res[i]
         assert not d["error"], d["error"]
         assert d["det_count"] == len(a)
-        np.testing.assert_array_equal(d["topk_idx"], a.topk_idx)
+        from types import SimpleNamespace
+
+        _same_topk(a, SimpleNamespace(topk_idx=np.asarray(d["topk_idx"]), topk_logit=np.asarray(d["topk_logit"])),
+                   boxes=(a.boxes, np.asarray(d["det"])[:, :4]))
