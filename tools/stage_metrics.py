@@ -80,9 +80,10 @@ def stages(after: str, before: str | None = None) -> list[dict]:
     # KServe statistics counters (microseconds, cumulative): mean per request
     kv = defaultdict(dict)
     for (name, labels), v in d.items():
-        if name.startswith("nv_inference_") and name.endswith("_duration_us"):
-            kv[labels][name] = v
-        elif name == "nv_inference_request_success":
+        base = name[:-6] if name.endswith("_total") else name  # prometheus_client names counters *_total
+        if base.startswith("nv_inference_") and base.endswith("_duration_us"):
+            kv[labels][base] = v
+        elif base == "nv_inference_request_success":
             kv[labels]["n"] = v
     for labels, vals in kv.items():
         n = vals.get("n", 0.0)
