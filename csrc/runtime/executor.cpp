@@ -122,6 +122,11 @@ Executor::~Executor() {
     if (sl.copied) hipEventDestroy(sl.copied);
     if (sl.started) hipEventDestroy(sl.started);
     if (sl.done) hipEventDestroy(sl.done);
+    if (sl.fork_ev) hipEventDestroy(sl.fork_ev);
+    for (int l = 0; l < kMaxLanes; ++l) {
+      if (sl.lane_ev[l]) hipEventDestroy(sl.lane_ev[l]);
+      if (sl.lane_stream[l]) hipStreamDestroy(sl.lane_stream[l]);
+    }
   }
   if (d_weights_) hipFree(d_weights_);
   if (compute_) hipStreamDestroy(compute_);
@@ -184,6 +189,20 @@ void Executor::alloc_slots() {
     }();
     ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.done, blocking ? hipEventBlockingSync : hipEventDefault));
   }
+}
+
+// Side streams of a slot, created the first time a program with lane ops (kLaneField) runs on it: programs
+// without lanes never create them (no extra queues per process).
+void Executor::ensure_lanes(Slot& sl) {
+  if (sl.fork_ev != nullptr) return;
+  bool lanes = false;
+  for (const OpRecord& r : prog_) lanes |= r[kLaneField] > 0;
+  if (!lanes) return;
+  for (int l = 0; l < kMaxLanes; ++l) {
+    ARENA_HIP_CHECK(hipStreamCreateWithFlags(&sl.lane_stream[l], hipStreamNonBlocking));
+    ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.lane_ev[l], hipEventDisableTiming));
+  }
+  ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.fork_ev, hipEventDisableTiming));
 }
 
 void Executor::set_weights(const void* host, size_t bytes) {
@@ -395,6 +414,7 @@ void Executor::autotune(Bucket& bk) {
 void Executor::capture(Bucket& bk, int s) {
   Slot& sl = slots_[s];
   hipStream_t st = sl.stream;
+  ensure_lanes(sl);
   // Validate the program eagerly once (launch errors surface here, not in the graph).
   ARENA_HIP_CHECK(hipStreamSynchronize(st));
   hipGraph_t g = nullptr;
@@ -435,7 +455,7 @@ uint8_t* Executor::resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff, int 
   return base + coff * eb;
 }
 
-void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s,
+void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s_main,
                                int op_offset, int force_impl) {
   Ctrl* ctrl = (Ctrl*)resolve(bk, sl, BUF_CTRL, 0, 1);
   const ImageMeta* meta = (const ImageMeta*)resolve(bk, sl, BUF_META, 0, 1);
@@ -445,8 +465,30 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
   auto bdev = [&](int64_t kind) -> const int* { return kind == BATCH_CROPS ? &ctrl->n_crops : &ctrl->n_images; };
   const uint8_t* W = d_weights_;
 
+  // Lanes (kLaneField): a run of lane ops forks each lane's side stream off the main stream at its first op and
+  // joins every forked lane back before the next lane-0 op (and at the end).  Single-op programs (autotune timing)
+  // stay on the main stream.
+  bool forked[kMaxLanes] = {};
+  auto join_lanes = [&]() {
+    for (int l = 0; l < kMaxLanes; ++l)
+      if (forked[l]) {
+        ARENA_HIP_CHECK(hipEventRecord(sl.lane_ev[l], sl.lane_stream[l]));
+        ARENA_HIP_CHECK(hipStreamWaitEvent(s_main, sl.lane_ev[l], 0));
+        forked[l] = false;
+      }
+  };
+  const bool use_lanes = prog.size() > 1 && sl.fork_ev != nullptr;
   for (size_t oi = 0; oi < prog.size(); ++oi) {
     const OpRecord& r = prog[oi];
+    const int lane = use_lanes && r[kLaneField] >= 1 && r[kLaneField] <= kMaxLanes ? (int)r[kLaneField] : 0;
+    if (lane == 0) {
+      join_lanes();
+    } else if (!forked[lane - 1]) {
+      ARENA_HIP_CHECK(hipEventRecord(sl.fork_ev, s_main));  // everything before this op on the main stream
+      ARENA_HIP_CHECK(hipStreamWaitEvent(sl.lane_stream[lane - 1], sl.fork_ev, 0));
+      forked[lane - 1] = true;
+    }
+    hipStream_t s = lane ? sl.lane_stream[lane - 1] : s_main;
     // field 47: activation precision of the op (0 bf16, 1 exact fp32; planner.OP_DTYPE_FIELD)
     const bool f32 = r[kDtypeField] == 1;
     const int eb = f32 ? 4 : 2;
@@ -836,6 +878,7 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
     }
     ARENA_HIP_CHECK(hipGetLastError());
   }
+  join_lanes();
 }
 
 // ---------------------------------------------------------------- host packing

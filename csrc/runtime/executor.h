@@ -40,6 +40,11 @@ namespace arena {
 
 constexpr int kOpFields = 48;
 constexpr int kDtypeField = 47;  // per-op activation precision: 0 bf16, 1 exact fp32
+// Per-op stream lane (planner.OP_LANE_FIELD): 0 = the batch's stream; 1..kMaxLanes = a side stream forked from
+// it before the first op of a run of lane ops and joined back at the next lane-0 op (independent branches such
+// as the three Detect-head levels run concurrently, inside the captured graph as parallel branches).
+constexpr int kLaneField = 46;
+constexpr int kMaxLanes = 3;
 constexpr int kMaxSlots = 6;
 using OpRecord = std::array<int64_t, kOpFields>;
 
@@ -193,6 +198,8 @@ class Executor : public BatchInstance {
     // batch's work.  More slots than streams lets the next batches' packing
     // and H2D copies run ahead while the device is busy.
     hipStream_t stream = nullptr;  // stream of the slot's current batch
+    hipStream_t lane_stream[kMaxLanes] = {};  // side streams of program lanes (kLaneField)
+    hipEvent_t fork_ev = nullptr, lane_ev[kMaxLanes] = {};
     int idx = 0;
     bool busy = false;
     int bucket = 0;
@@ -208,6 +215,7 @@ class Executor : public BatchInstance {
   };
 
   void alloc_slots();
+  void ensure_lanes(Slot& sl);
   void sync_slots();
   void free_arenas(Bucket& bk);
   void capture(Bucket& bk, int slot);

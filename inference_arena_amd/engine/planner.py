@@ -77,6 +77,8 @@ import torch
 
 OP_FIELDS = 48
 OP_DTYPE_FIELD = 47
+OP_LANE_FIELD = 46  # stream lane of the op (0: the batch's stream; 1-3: side streams, executor.h kLaneField)
+MAX_LANES = 3
 DTYPES = ("bf16", "fp32")
 (OP_CONV, OP_DWCONV, OP_SPPF, OP_LETTERBOX, OP_ZERO, OP_DECODE, OP_NMS, OP_CROPPLAN, OP_CROPGATHER, OP_AVGPOOL,
  OP_TOPK, OP_TENSORIN, OP_YOLORAW, OP_IRBLOCK, OP_STEMFUSED, OP_C3FUSED, OP_HEADPOOL, OP_STAMP) = range(1, 19)
@@ -338,6 +340,8 @@ def ir_crop_f32_planned(H: int, stride: int, inp_pad: int, hid_pad: int, oup_pad
 
 
 class ProgramBuilder:
+    _lane = 0
+
     def __init__(self, dtype: str = "bf16") -> None:
         if dtype not in DTYPES:
             raise ValueError(f"dtype must be one of {DTYPES}, got {dtype!r}")
@@ -380,11 +384,43 @@ class ProgramBuilder:
 
     def _emit(self, rec: list[int], *touch) -> None:
         self._touch(*touch)
-        if len(rec) > OP_DTYPE_FIELD:
-            raise ValueError("op record overlaps the dtype field")
+        if len(rec) > OP_LANE_FIELD:
+            raise ValueError("op record overlaps the lane / dtype fields")
         r = list(rec) + [0] * (OP_FIELDS - len(rec))
         r[OP_DTYPE_FIELD] = int(self.f32)
+        r[OP_LANE_FIELD] = self._lane
         self.ops.append(r)
+
+    def parallel(self):
+        """Context for a region of independent branches: ``with pb.parallel() as lane: lane(1); ...ops...;
+        lane(2); ...``.  Each branch's ops carry its lane (OP_LANE_FIELD) and run on a side stream of the batch
+        (executor.cpp enqueue_program: forked before the region, joined at the next lane-0 op).  Every buffer the
+        region touches stays allocated for the whole region: the arena layout must not let two branches share
+        memory they now use at the same time."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def region():
+            start = len(self.ops)
+
+            def lane(k: int) -> None:
+                if not 0 <= k <= MAX_LANES:
+                    raise ValueError(f"lane {k} outside 0..{MAX_LANES}")
+                self._lane = k
+
+            try:
+                yield lane
+            finally:
+                self._lane = 0
+                end = len(self.ops)
+                if not any(self.ops[i][OP_LANE_FIELD] for i in range(start, end)):
+                    return  # every branch on the main stream: sequential lifetimes stay valid
+                for b in self.buffers:
+                    if b.last >= start and b.first < end:
+                        b.first = min(b.first, start)
+                        b.last = max(b.last, end - 1)
+
+        return region()
 
     def begin_classifier(self) -> None:
         """Ops from here on form the overflow classification program."""

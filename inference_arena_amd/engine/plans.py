@@ -229,7 +229,11 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
     fuse_head = os.environ.get("ARENA_FUSE_HEAD", "1").lower() not in ("0", "false", "no", "off")
     ch = c2 + c3
     heads = []
+    lanes = head_lanes()
+    region = pb.parallel()
+    lane = region.__enter__()
     for lvl, (P, cin, s) in enumerate(((P3, 64, s8), (P4, 128, s16), (P5, 256, s32))):
+        lane(lvl + 1 if lanes else 0)  # the three levels are independent: one side stream each
         H1 = pb.tensor(f"det{lvl}.h1", s, s, ch)
         H2 = pb.tensor(f"det{lvl}.h2", s, s, ch)
         D = pb.tensor(f"det{lvl}.out", s, s, 4 * d.reg_max + nc)
@@ -250,7 +254,15 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
             pb.conv(View(H2, 0, c2), View(D, 0, 4 * d.reg_max), *fold_conv_bn(d.cv2[lvl][2], None), act=None)
             pb.conv(View(H2, c2, c3), View(D, 4 * d.reg_max, nc), *fold_conv_bn(d.cv3[lvl][2], None), act=None)
         heads.append(View(D, 0, 4 * d.reg_max + nc))
+    region.__exit__(None, None, None)
     return heads
+
+
+def head_lanes() -> bool:
+    """``ARENA_HEAD_LANES`` (default 0): the Detect head's three levels run as parallel branches of the batch's
+    graph (side streams, ProgramBuilder.parallel); their small-grid convs (15-50 workgroups each at bs 1) leave
+    most CUs idle when serialised."""
+    return os.environ.get("ARENA_HEAD_LANES", "0").lower() not in ("0", "false", "no", "off")
 
 
 def fuse_ir_default() -> str:

@@ -40,8 +40,14 @@ def table_path() -> Path:
 
 
 def fingerprint(ops: np.ndarray) -> str:
-    """Program identity: the op records (kinds, shapes, buffer ids, weight offsets), not the weight values."""
-    return hashlib.sha256(np.ascontiguousarray(ops, dtype=np.int64).tobytes()).hexdigest()[:24]
+    """Program identity: the op records (kinds, shapes, buffer ids, weight offsets), not the weight values, and
+    not the stream lane of an op (planner.OP_LANE_FIELD): lanes change where an op runs, not which kernel fits it."""
+    from .planner import OP_LANE_FIELD
+
+    a = np.array(ops, dtype=np.int64, copy=True)
+    if a.ndim == 2 and a.shape[1] > OP_LANE_FIELD:
+        a[:, OP_LANE_FIELD] = 0
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:24]
 
 
 def load_table(path: Path | None = None) -> dict:

@@ -310,6 +310,40 @@ def test_fp32_program_fuses_the_160_c3_block(monkeypatch, flag, n):
         validate_program(prog, B, 6 * B, max_det=300, cand_cap=8400)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_head_lanes_program(monkeypatch, dtype):
+    """ARENA_HEAD_LANES: the Detect head's three levels carry lanes 1-3 (side streams in the executor), every other
+    op lane 0; buffers the head touches stay live over the whole head region (no arena sharing between
+    branches that now run at the same time); off, every op is lane 0 and the program is unchanged."""
+    from inference_arena_amd.engine import plans
+    from inference_arena_amd.engine.planner import OP_LANE_FIELD, layout
+    from inference_arena_amd.engine.validate import validate_program
+    from inference_arena_amd.models.zoo import default_models
+
+    y, m = default_models(0)
+    monkeypatch.setenv("ARENA_HEAD_LANES", "0")
+    off = plans.plan_pipeline(y, m, conf_thr=0.5, iou_thr=0.45, dtype=dtype)
+    assert not off.ops[:, OP_LANE_FIELD].any()
+    monkeypatch.setenv("ARENA_HEAD_LANES", "1")
+    on = plans.plan_pipeline(y, m, conf_thr=0.5, iou_thr=0.45, dtype=dtype)
+    lanes = on.ops[:, OP_LANE_FIELD]
+    idx = np.nonzero(lanes)[0]
+    assert set(lanes[idx].tolist()) == {1, 2, 3}
+    assert list(idx) == list(range(idx[0], idx[-1] + 1))  # one contiguous region
+    assert list(lanes[idx]) == sorted(lanes[idx])          # level by level
+    np.testing.assert_array_equal(np.delete(on.ops, OP_LANE_FIELD, 1), np.delete(off.ops, OP_LANE_FIELD, 1))
+    s, e = int(idx[0]), int(idx[-1]) + 1
+    for B in (1, 32):
+        validate_program(on, B, 6 * B, max_det=300, cand_cap=8400)
+        offs, _ = layout(on.buffers, B, 6 * B)
+        live = [b for b in on.buffers if b.last >= 0 and b.last >= s and b.first < e]
+        for i, a in enumerate(live):
+            sa = a.per_item * (6 * B if a.kind == CROPS else B)
+            for b in live[i + 1:]:
+                sb = b.per_item * (6 * B if b.kind == CROPS else B)
+                assert offs[a.id] + sa <= offs[b.id] or offs[b.id] + sb <= offs[a.id], (a.name, b.name)
+
+
 def test_tuning_table_concurrent_writers(tmp_path):
     """Several processes storing different entries at once (replicas missing the table together): every entry
     survives and the table is valid JSON throughout (one shared .tmp name tore the file)."""

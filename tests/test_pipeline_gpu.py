@@ -212,6 +212,27 @@ def test_fused_head_pointwise_matches_unfused(dense_models, device, monkeypatch)
             np.testing.assert_allclose(y.boxes, x.boxes, atol=1.0)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_head_lanes_match_sequential(dense_models, device, monkeypatch, dtype):
+    """ARENA_HEAD_LANES=1: the Detect head's three levels run as parallel graph branches on side streams; the
+    kernels and each branch's order are unchanged, so the results are bit-identical to the sequential program
+    (buckets 1 and 8, several batches through the captured graphs)."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+
+    imgs = synthetic_images(7, 61) + synthetic_images(1, 62, hw=(333, 500))
+    monkeypatch.setenv("ARENA_HEAD_LANES", "0")
+    seq = GpuPipeline(*dense_models, device=0, buckets=[1, 8], dtype=dtype)
+    monkeypatch.setenv("ARENA_HEAD_LANES", "1")
+    par = GpuPipeline(*dense_models, device=0, buckets=[1, 8], dtype=dtype)
+    assert par.program.ops[:, 46].any() and not seq.program.ops[:, 46].any()
+    for batch in (imgs, imgs[:1], imgs[3:]):
+        for a, b in zip(seq.infer(batch), par.infer(batch)):
+            np.testing.assert_array_equal(a.boxes, b.boxes)
+            np.testing.assert_array_equal(a.topk_idx, b.topk_idx)
+            np.testing.assert_array_equal(a.topk_logit, b.topk_logit)
+
+
 def test_fused_c3_matches_unfused(dense_models, device, monkeypatch):
     """Whole C3 blocks as one kernel (160x160 c_=16 n=1, 80x80 c_=32 n=2, head P3 c_=32 n=1 without
     shortcut) vs the per-conv program: same block outputs and the same detections."""
