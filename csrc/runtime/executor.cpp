@@ -477,7 +477,13 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         forked[l] = false;
       }
   };
-  const bool use_lanes = prog.size() > 1 && sl.fork_ev != nullptr;
+  // Lanes pay off where one batch leaves most CUs idle (small buckets); for full batches the slots already
+  // overlap batches on the compute streams and side streams only add contention (profiles/r4lanes/).
+  static const int lanes_max_b = [] {
+    const char* e = std::getenv("ARENA_LANES_MAX_BATCH");
+    return e != nullptr ? std::atoi(e) : 2;
+  }();
+  const bool use_lanes = prog.size() > 1 && sl.fork_ev != nullptr && bk.info.B <= lanes_max_b;
   for (size_t oi = 0; oi < prog.size(); ++oi) {
     const OpRecord& r = prog[oi];
     const int lane = use_lanes && r[kLaneField] >= 1 && r[kLaneField] <= kMaxLanes ? (int)r[kLaneField] : 0;

@@ -132,8 +132,33 @@ def _run_native(cfg: LoadConfig, images: list[bytes]) -> list:
             for t, lat, st, d in zip(r["t_done"], r["latency"], r["status"], r["dets"])]
 
 
+def _heartbeat(cfg: LoadConfig, stop) -> None:
+    """A progress line every 30 s: a level at the reference's length (60 + 180 + 30 s) is otherwise silent for
+    minutes, which supervisors of batch jobs read as a hang."""
+    import threading
+
+    def run():
+        t0 = time.perf_counter()
+        total = cfg.warmup_s + cfg.measure_s + cfg.cooldown_s
+        while not stop.wait(30.0):
+            print(f"[loadgen] users={cfg.users}: {time.perf_counter() - t0:.0f} / {total:.0f} s", flush=True)
+
+    threading.Thread(target=run, daemon=True, name="loadgen-heartbeat").start()
+
+
 def run_level(cfg: LoadConfig, images: list[bytes]) -> PhaseResult:
     """Run one (users) level with all phases; returns every completed request."""
+    import threading
+
+    stop = threading.Event()
+    _heartbeat(cfg, stop)
+    try:
+        return _run_level(cfg, images)
+    finally:
+        stop.set()
+
+
+def _run_level(cfg: LoadConfig, images: list[bytes]) -> PhaseResult:
     t0 = time.perf_counter()
     if cfg.engine == "native":
         return PhaseResult(cfg.users, sorted(_run_native(cfg, images)), time.perf_counter() - t0)
