@@ -8,7 +8,7 @@ T=${1:-pmc_fp32}
 mkdir -p gpurun_out/$T
 i=0
 for set in "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAVES" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
-           "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 -s KILL 180 rocprofv3 --kernel-trace --pmc $set --output-format csv -d gpurun_out/$T/s$i -o run -- \
     python3 tools/profile_engine.py --dtype fp32 --batches 4 > gpurun_out/$T/s$i.log 2>&1
