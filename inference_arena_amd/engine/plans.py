@@ -259,12 +259,14 @@ def plan_yolo(pb: ProgramBuilder, y: YOLOv5nu, T: int = 640, tensor_input: bool 
 
 
 def head_lanes() -> bool:
-    """``ARENA_HEAD_LANES`` (default 1): the Detect head's three levels run as parallel branches of the batch's
+    """``ARENA_HEAD_LANES`` (default 0): the Detect head's three levels run as parallel branches of the batch's
     graph (side streams, ProgramBuilder.parallel) in buckets up to ``ARENA_LANES_MAX_BATCH`` (2; the executor
     keeps larger buckets on one stream: with four slots in flight the side streams only add contention,
     profiles/r4lanes/); their small-grid convs (15-50 workgroups each at bs 1) leave most CUs idle when
-    serialised.  1-user HTTP P50 1.705 -> 1.690 ms, P99 1.818 -> 1.784 ms (profiles/r4lanes_bs1/)."""
-    return os.environ.get("ARENA_HEAD_LANES", "1").lower() not in ("0", "false", "no", "off")
+    serialised.  1-user HTTP P50 1.705 -> 1.690 ms, P99 1.818 -> 1.784 ms (profiles/r4lanes_bs1/).  Off by
+    default: the arm-B detection service (detector-only program, several processes per GPU) crashed with it on in
+    a protocol run (profiles/r4lanes/README.md); the monolithic / model-server paths and the GPU tests ran clean."""
+    return os.environ.get("ARENA_HEAD_LANES", "0").lower() not in ("0", "false", "no", "off")
 
 
 def fuse_ir_default() -> str:
