@@ -477,6 +477,18 @@ def main(argv=None) -> int:
         weights_verified = all(d == ref_digest for d in digests)
         if not weights_verified:
             raise RuntimeError(f"replica weights differ after the broadcast: {digests} vs rank 0 {ref_digest}")
+        # which physical GPU each rank drove: N distinct PCI bus ids for an N-GPU record
+        rank_devices = D.allgather_objects(D.device_identity(None if a.fake_engine else dev, info.rank,
+                                                             a.fake_engine), info)
+        shared_gpu = os.environ.get("ARENA_SHARED_GPU") == "1"
+        D.check_distinct_devices(rank_devices, shared_gpu)
+        torch_world = None
+        if not a.fake_engine or info.world > 1:
+            import torch.distributed as tdist
+
+            torch_world = tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1
+        if torch_world is not None and torch_world != info.world:
+            raise RuntimeError(f"torch.distributed world size {torch_world} != WORLD_SIZE {info.world}")
         cpu_note = (f"pinned to {len(share)} NUMA-local CPUs" if pinned else "not pinned") + f", {usable} usable"
         log(f"[rank {info.rank}/{info.world} {info.backend}] {a.dtype} pipeline ready in {time.time() - t0:.1f}s; "
             f"arena MB {({b: round(v / 2**20, 1) for b, v in pipe.arena_bytes.items()})}; host plan {plan}; "
@@ -672,6 +684,10 @@ def main(argv=None) -> int:
                 "host_cpu_us_per_req": ext0.get("host_cpu_us_per_req"),
                 "stage_cpu_us_per_req": ext0.get("stage_cpu_us_per_req"),
                 "world_size_checked": info.world,
+                "torch_world_size": torch_world,
+                "rank_devices": rank_devices,
+                "distinct_gpus": len({d["pci_bus_id"] for d in rank_devices}),
+                "shared_gpu_rehearsal": shared_gpu,
             }
             out.update(sec)
             print(json.dumps(out), flush=True)

@@ -18,6 +18,7 @@
 #include "runtime/http_front.h"
 #include "runtime/http_loadgen.h"
 #include "runtime/ipc_buffer.h"
+#include "runtime/peer.h"
 #include "runtime/jpeg_decode.h"
 #include "runtime/jpeg_ingest.h"
 #include "runtime/batcher.h"
@@ -687,8 +688,8 @@ PYBIND11_MODULE(_C, m) {
       .def("buckets", &SplitInstance::buckets);
 
   py::class_<EchoInstance, std::shared_ptr<EchoInstance>>(m, "EchoInstance")
-      .def(py::init<int, int, int, int>(), py::arg("slots") = 2, py::arg("max_batch") = 32, py::arg("max_det") = 4,
-           py::arg("latency_us") = 0);
+      .def(py::init<int, int, int, int, int64_t>(), py::arg("slots") = 2, py::arg("max_batch") = 32,
+           py::arg("max_det") = 4, py::arg("latency_us") = 0, py::arg("staging_cap") = 0);
 
   py::class_<DynamicBatcher>(m, "DynamicBatcher")
       .def(py::init([](py::list executors, const py::dict& cfg) {
@@ -837,13 +838,22 @@ PYBIND11_MODULE(_C, m) {
         }
         return py::bytes(out);
       });
-  m.def("ipc_open", [](py::bytes handle, int device) { return ipc_open(std::string(handle), device); },
-        py::arg("handle"), py::arg("device") = 0);
+  m.def("ipc_open", [](py::bytes handle, int device, int src_device) {
+    return ipc_open(std::string(handle), device, src_device);
+  }, py::arg("handle"), py::arg("device") = 0, py::arg("src_device") = -1);
   m.def("ipc_close", &ipc_close);
-  m.def("ipc_open_range", [](py::bytes handle, int device) {
-    const uintptr_t p = ipc_open(std::string(handle), device);
+  m.def("ipc_open_range", [](py::bytes handle, int device, int src_device) {
+    const uintptr_t p = ipc_open(std::string(handle), device, src_device);
     return py::make_tuple(p, ipc_mapped_bytes(p));
-  }, py::arg("handle"), py::arg("device") = 0, "ipc_open + the mapped size: (device pointer, bytes)");
+  }, py::arg("handle"), py::arg("device") = 0, py::arg("src_device") = -1,
+     "ipc_open + the mapped size: (device pointer, bytes); src_device >= 0 is checked for peer access first");
+  m.def("can_access_peer", &hip_can_access_peer, py::arg("dst"), py::arg("src"), "hipDeviceCanAccessPeer");
+  m.def("require_peer_access", [](int dst, int src, const std::string& what, py::object can) {
+    PeerQuery q = hip_can_access_peer;
+    if (!can.is_none()) q = [can](int d, int s) { py::gil_scoped_acquire g; return can(d, s).cast<int>(); };
+    require_peer_access(dst, src, what.c_str(), q);
+  }, py::arg("dst"), py::arg("src"), py::arg("what") = "peer copy", py::arg("can_access") = py::none(),
+     "runtime/peer.h policy; can_access(dst, src) -> int overrides hipDeviceCanAccessPeer (tests)");
 
   py::class_<HttpLoadGen>(m, "HttpLoadGen")
       .def(py::init([](const py::dict& cfg, const py::list& requests) {

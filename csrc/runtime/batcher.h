@@ -68,6 +68,9 @@ struct BatcherStats {
 
 class DynamicBatcher {
  public:
+  // smallest staging capacity of the instances in bytes (0 = unlimited): inputs whose staged_bytes exceed it
+  // are rejected by enqueue (-2)
+  int64_t staging_cap() const { return staging_cap_; }
   DynamicBatcher(std::vector<std::shared_ptr<BatchInstance>> instances, const BatcherConfig& cfg);
   ~DynamicBatcher();
   DynamicBatcher(const DynamicBatcher&) = delete;

@@ -20,8 +20,10 @@ namespace arena {
 class EchoInstance : public BatchInstance {
  public:
   // latency_us: collect() returns no earlier than this long after submit (a stand-in for device time)
-  EchoInstance(int slots, int max_batch, int max_det = 4, int latency_us = 0)
-      : slots_(slots), max_batch_(max_batch), max_det_(max_det), latency_us_(latency_us), results_(slots),
+  // staging_cap: the staging_bytes() it reports (0 = unlimited), as an Executor reports its slot's image pool
+  EchoInstance(int slots, int max_batch, int max_det = 4, int latency_us = 0, int64_t staging_cap = 0)
+      : slots_(slots), max_batch_(max_batch), max_det_(max_det), latency_us_(latency_us), staging_cap_(staging_cap),
+        results_(slots),
         busy_(slots, false), t_submit_(slots) {}
   std::vector<int> buckets() const override {
     std::vector<int> b;
@@ -32,6 +34,7 @@ class EchoInstance : public BatchInstance {
   int num_slots() const override { return slots_; }
   int max_det() const override { return max_det_; }
   int64_t raw_out_bytes() const override { return 0; }
+  int64_t staging_bytes() const override { return staging_cap_; }
 
   // Image i of a batch gets min(max_det, 1 + first_byte % max_det) detections: box k spans
   // (k, k, w - k, h - k), confidence 0.9 - 0.1 k, COCO class k; crop top-5 = classes 10k .. 10k + 4.
@@ -104,6 +107,7 @@ class EchoInstance : public BatchInstance {
 
  private:
   int slots_, max_batch_, max_det_, latency_us_;
+  int64_t staging_cap_;
   std::vector<BatchResult> results_;
   std::vector<bool> busy_;
   std::vector<std::chrono::steady_clock::time_point> t_submit_;

@@ -2,6 +2,7 @@
 // See executor.h for the design; the op record layouts are documented in
 // inference_arena_amd/engine/planner.py (the only producer of programs).
 #include "executor.h"
+#include "peer.h"
 
 #include <pthread.h>
 
@@ -174,7 +175,11 @@ void Executor::alloc_slots() {
     // run up to 3 bytes past the last image of a full staging pool
     ARENA_HIP_CHECK(hipMalloc(&sl.d_in, in_bytes_total() + 256));
     ARENA_HIP_CHECK(hipMalloc(&sl.d_out, out_bytes_total()));
-    ARENA_HIP_CHECK(hipHostMalloc(&sl.h_in, in_bytes_total(), hipHostMallocDefault));
+    // pinned host staging: the meta block plus the host-packed (non-JPEG) inputs of one full batch at the
+    // nominal frame size; split-decoded JPEGs are DMA'd from their own pinned buffers, so pool_factor's extra
+    // device room needs no host twin.  A batch of larger RGB frames grows it on demand (ensure_host_staging).
+    sl.h_cap = in_bytes_meta() + align_up((size_t)cfg_.pool_bytes_per_image * max_B_, 256);
+    ARENA_HIP_CHECK(hipHostMalloc(&sl.h_in, sl.h_cap, hipHostMallocDefault));
     ARENA_HIP_CHECK(hipHostMalloc(&sl.h_out, out_bytes_total(), hipHostMallocDefault));
     ARENA_HIP_CHECK(hipMemset(sl.d_in, 0, in_bytes_total()));
     ARENA_HIP_CHECK(hipMemset(sl.d_out, 0, out_bytes_total()));
@@ -949,10 +954,28 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   // [ctrl | meta | JPEG descriptors | packed inputs] covers them; then per split-decoded JPEG its RGB
   // destination, coefficient blocks (DMA'd straight from the request's own pinned buffer: no host copy) and
   // reconstruction planes.  Everything is validated before the first copy is queued.
+  const size_t cap = pool_cap();
+  {
+    // host bytes of the packed (non-JPEG) inputs: grow the slot's pinned staging if this batch needs more (the
+    // slot is idle: its previous H2D completed before it was collected)
+    size_t need = 0;
+    for (int i = 0; i < n; ++i)
+      if (imgs[i].jpeg == nullptr)
+        need = align_up(need + (imgs[i].bytes > 0 ? (size_t)imgs[i].bytes : (size_t)imgs[i].h * imgs[i].w * 3), 256);
+    if (need > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
+    if (in_bytes_meta() + need > sl.h_cap) {
+      uint8_t* grown = nullptr;
+      const size_t want = in_bytes_meta() + std::max(need, std::min(cap, 2 * (sl.h_cap - in_bytes_meta())));
+      ARENA_HIP_CHECK(hipHostMalloc(&grown, want, hipHostMallocDefault));
+      std::memcpy(grown, sl.h_in, in_bytes_meta());
+      ARENA_HIP_CHECK(hipHostFree(sl.h_in));
+      sl.h_in = grown;
+      sl.h_cap = want;
+    }
+  }
   ImageMeta* meta = (ImageMeta*)(sl.h_in + kCtrlBytes);
   JpegDesc* jdesc = (JpegDesc*)(sl.h_in + jpeg_desc_off());
   uint8_t* pool = sl.h_in + in_bytes_meta();
-  const size_t cap = pool_cap();
   size_t off = 0;
   std::vector<std::function<void()>> jobs;
   const int T = cfg_.det_size;
@@ -1176,6 +1199,16 @@ BatchResult Executor::collect(int s) {
 
 BatchResult Executor::run(const std::vector<InputImage>& imgs) { return collect(submit(imgs)); }
 
+void Executor::enable_peer(int src, const char* what) {
+  if (src < 0 || src == cfg_.device) return;
+  if (std::find(peer_enabled_.begin(), peer_enabled_.end(), src) != peer_enabled_.end()) return;
+  require_peer_access(cfg_.device, src, what, hip_can_access_peer);  // runtime/peer.h: clear error, no fault
+  const hipError_t e = hipDeviceEnablePeerAccess(src, 0);
+  if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) ARENA_HIP_CHECK(e);
+  (void)hipGetLastError();
+  peer_enabled_.push_back(src);
+}
+
 int Executor::submit_peer(Executor& src, int src_slot) {
   trace::Range tr("arena.submit_peer");
   if (!peer_stage_) throw std::runtime_error("submit_peer: executor is not a peer stage (set_peer_stage)");
@@ -1193,16 +1226,7 @@ int Executor::submit_peer(Executor& src, int src_slot) {
   if (sl.busy) throw std::runtime_error("submit_peer: every staging slot is in flight; collect() first");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   const int sdev = src.cfg_.device;
-  if (sdev != cfg_.device && std::find(peer_enabled_.begin(), peer_enabled_.end(), sdev) == peer_enabled_.end()) {
-    int can = 0;
-    ARENA_HIP_CHECK(hipDeviceCanAccessPeer(&can, cfg_.device, sdev));
-    if (can) {
-      const hipError_t e = hipDeviceEnablePeerAccess(sdev, 0);
-      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) ARENA_HIP_CHECK(e);
-      (void)hipGetLastError();
-    }
-    peer_enabled_.push_back(sdev);
-  }
+  enable_peer(sdev, "submit_peer (split topology)");
   sl.stream = streams_[seq_++ % n_streams_];
   // the detector's graph (and its result copy) finished on the source device
   ARENA_HIP_CHECK(hipStreamWaitEvent(sl.stream, ss.done, 0));
@@ -1302,6 +1326,8 @@ int Executor::submit_device(const std::vector<DeviceImage>& imgs, const std::vec
   ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_out, sl.h_out, out_off_topk(), hipMemcpyHostToDevice, sl.stream));
   ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_out + out_off_xcrops(), crops, sizeof(CropRef) * (size_t)std::max(total, 1),
                                  hipMemcpyHostToDevice, sl.stream));
+  for (int i = 0; i < n; ++i)
+    if (imgs[i].device >= 0 && imgs[i].device != cfg_.device) enable_peer(imgs[i].device, "submit_device");
   for (int i = 0; i < n; ++i) {  // the pixels: device to device, never through the host
     const DeviceImage& im = imgs[i];
     uint8_t* dst = sl.d_in + in_bytes_meta() + meta[i].offset;

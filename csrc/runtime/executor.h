@@ -189,6 +189,7 @@ class Executor : public BatchInstance {
     uint8_t* d_out = nullptr;  // det_count | det | topk
     // pinned host
     uint8_t* h_in = nullptr;
+    size_t h_cap = 0;  // bytes of h_in (meta + host-packed inputs; grows on demand)
     uint8_t* h_out = nullptr;
     hipEvent_t copied = nullptr, started = nullptr, done = nullptr;
     // Each slot owns an activation arena; its batch runs on one of the
@@ -265,6 +266,7 @@ class Executor : public BatchInstance {
   double wall_khz_ = 100000.0;  // wall_clock64 rate (hipDeviceAttributeWallClockRate)
   bool peer_stage_ = false;
   std::vector<int> peer_enabled_;  // devices this executor's device has peer access to
+  void enable_peer(int src, const char* what);  // require_peer_access (runtime/peer.h) + hipDeviceEnablePeerAccess
   int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on compute stream
   // ARENA_CONCURRENT: 1 = per-slot streams + arenas (in-flight batches overlap on the device),
   // 0 = two slots serialised on one stream sharing one arena.  ARENA_SLOTS: staging slots when concurrent

@@ -2,6 +2,7 @@
 #include "http_front.h"
 
 #include <arpa/inet.h>
+#include <cstdlib>
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -1081,9 +1082,19 @@ void HttpFrontEnd::native_decode(DecodeTask& t) {
     return fail_request(t.conn, err.find("image too large") != std::string::npos ? 413 : 500, err);
   const JpegInfo& ji = up->info;
   InputImage in{nullptr, ji.height, ji.width};
-  if (cfg_.jpeg_device) {
+  // Device reconstruction needs the coefficients, the sample planes and the RGB frame in one batch's staging
+  // pool (staged_bytes) and the coefficients in one pooled buffer.  A frame too large for either (about
+  // > 15 MP at 4:2:0 with the default pool) is reconstructed on the host instead and staged as RGB, as the PIL
+  // path would stage it: the split decoder never turns away an upload the reference's decoder accepts.
+  const int64_t cap = batcher_->staging_cap();
+  InputImage probe = in;
+  probe.jpeg = &ji;
+  bool device = cfg_.jpeg_device && (cap <= 0 || staged_bytes(probe) <= cap);
+  if (device) {
     up->buf = host_pool_->get((size_t)ji.coef_count * 2);
-    if (!up->buf) return fail_request(t.conn, 503, "decode buffers exhausted");
+    device = (bool)up->buf;
+  }
+  if (device) {
     st = jpeg_decode_coefs(data, t.len, ji, (int16_t*)up->buf.get(), err);
     in.data = up->buf.get();
     in.jpeg = &up->info;
@@ -1092,11 +1103,17 @@ void HttpFrontEnd::native_decode(DecodeTask& t) {
     coef.resize((size_t)ji.coef_count);
     st = jpeg_decode_coefs(data, t.len, ji, coef.data(), err);
     if (st == JpegStatus::Ok) {
-      up->buf = host_pool_->get((size_t)ji.width * ji.height * 3);
-      if (!up->buf) return fail_request(t.conn, 503, "decode buffers exhausted");
+      const size_t rgb_bytes = (size_t)ji.width * ji.height * 3;
+      up->buf = host_pool_->get(rgb_bytes);
+      if (!up->buf) {  // beyond the largest size class or the pool's cap: a buffer of its own
+        uint8_t* raw = static_cast<uint8_t*>(std::malloc(rgb_bytes));
+        if (raw == nullptr) return fail_request(t.conn, 503, "decode buffers exhausted");
+        up->buf = std::shared_ptr<uint8_t>(raw, [](uint8_t* q) { std::free(q); });
+      }
       jpeg_coefs_to_rgb(ji, coef.data(), up->buf.get());
       in.data = up->buf.get();
     }
+    if (coef.capacity() > ((size_t)16 << 20)) std::vector<int16_t>().swap(coef);  // do not pin a huge frame's
   }
   if (st != JpegStatus::Ok) return fail_request(t.conn, 500, err);
   const double decode_ms = ms_since(t.t_queued);

@@ -9,6 +9,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <mutex>
 #include <string>
 
 namespace arena {
@@ -35,11 +36,15 @@ class IpcBuffer {
   size_t bytes_ = 0;
   int device_ = 0;
   std::string handle_;
+  void* stream_ = nullptr;  // hipStream_t of write(), created on first use
+  std::mutex mu_;
 };
 
 // Map another process's IpcBuffer (its handle()) into this process on `device`; returns the device pointer.
-// The mapping is process-wide and reference-counted by the driver; ipc_close() releases it.
-uintptr_t ipc_open(const std::string& handle, int device);
+// The mapping is process-wide and reference-counted by the driver; ipc_close() releases it.  `src_device`
+// (>= 0: the GPU that exported the buffer) is checked for peer access first (runtime/peer.h): a ring on
+// another GPU without an xGMI peer path is refused with a clear error instead of faulting in a kernel.
+uintptr_t ipc_open(const std::string& handle, int device, int src_device = -1);
 // Size of the allocation an (IPC-)mapped device pointer belongs to, from its base (hipMemGetAddressRange):
 // the classification side bounds every frame reference against it.
 size_t ipc_mapped_bytes(uintptr_t ptr);

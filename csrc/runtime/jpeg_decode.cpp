@@ -19,6 +19,18 @@ constexpr uint8_t kNatural[64 + 16] = {
     6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31,
     39, 46, 53, 60, 61, 54, 47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
 
+// Kraft check of a DHT's code-length counts (JPEG Annex C): the canonical code assigns codes of length l in order,
+// so after each length the next code must still fit in l bits.  An over-subscribed table is corrupt data.
+bool huff_lengths_valid(const uint8_t* bits) {
+  int64_t code = 0;
+  for (int l = 1; l <= 16; ++l) {
+    code += bits[l];
+    if (code > (int64_t(1) << l)) return false;
+    code <<= 1;
+  }
+  return true;
+}
+
 uint16_t be16(const uint8_t* p) { return (uint16_t)((p[0] << 8) | p[1]); }
 
 constexpr int kFastBits = 11;
@@ -48,6 +60,9 @@ struct HuffTable {
       valoff[l] = k - code;
       if (n) {
         for (int i = 0; i < n; ++i, ++k, ++code) {
+          // over-subscribed code (too many codes of this or a shorter length): reject it before any table
+          // write, as libjpeg's jdhuff.c does; (code << shift) | j would otherwise index past fast / ac_fast
+          if (code >= (1 << l) || k >= 256) return false;
           if (l <= kFastBits) {
             const int shift = kFastBits - l;
             const uint8_t sym = s.vals[k];
@@ -69,7 +84,6 @@ struct HuffTable {
           }
         }
         maxcode[l] = code - 1;
-        if (code > (1 << l)) return false;  // over-subscribed code
       } else {
         maxcode[l] = -1;
       }
@@ -328,7 +342,7 @@ JpegStatus jpeg_parse(const uint8_t* data, size_t n, JpegInfo& info, std::string
           h.bits[l] = seg[q + l];
           count += h.bits[l];
         }
-        if (count > 256 || q + 17 + count > sl) {
+        if (count > 256 || q + 17 + count > sl || !huff_lengths_valid(h.bits)) {
           err = "Failed to decode image: bad DHT";
           return JpegStatus::Corrupt;
         }

@@ -3,6 +3,7 @@
 
 #include <pthread.h>
 
+#include <cstdlib>
 #include <ctime>
 
 #include "runtime/jpeg_decode.h"
@@ -109,21 +110,30 @@ void JpegIngest::run(Task& t) {
   InputImage in{nullptr, ji.height, ji.width};
   in.export_dst = t.export_dst;
   if (st == JpegStatus::Ok) {
-    if (cfg_.jpeg_device) {
+    // device reconstruction when the frame's coefficients, planes and RGB fit one batch's staging pool and a
+    // pooled buffer; otherwise the host reconstructs it (bit-exact, jpeg_coefs_to_rgb) and it is staged as RGB
+    const int64_t cap = batcher_->staging_cap();
+    InputImage probe = in;
+    probe.jpeg = &ji;
+    bool device = cfg_.jpeg_device && (cap <= 0 || staged_bytes(probe) <= cap);
+    if (device) {
       up->buf = pool_->get((size_t)ji.coef_count * 2);
-      if (!up->buf) {
-        st = JpegStatus::Corrupt;
-        err = "decode buffers exhausted";
-      } else {
-        st = jpeg_decode_coefs(data, t.upload.size(), ji, (int16_t*)up->buf.get(), err);
-        in.data = up->buf.get();
-        in.jpeg = &up->info;
-      }
+      device = (bool)up->buf;
+    }
+    if (device) {
+      st = jpeg_decode_coefs(data, t.upload.size(), ji, (int16_t*)up->buf.get(), err);
+      in.data = up->buf.get();
+      in.jpeg = &up->info;
     } else {
       std::vector<int16_t> coef((size_t)ji.coef_count);
       st = jpeg_decode_coefs(data, t.upload.size(), ji, coef.data(), err);
       if (st == JpegStatus::Ok) {
-        up->buf = pool_->get((size_t)ji.width * ji.height * 3);
+        const size_t rgb_bytes = (size_t)ji.width * ji.height * 3;
+        up->buf = pool_->get(rgb_bytes);
+        if (!up->buf) {  // beyond the largest size class or the pool's cap: a buffer of its own
+          uint8_t* raw = static_cast<uint8_t*>(std::malloc(rgb_bytes));
+          if (raw != nullptr) up->buf = std::shared_ptr<uint8_t>(raw, [](uint8_t* q) { std::free(q); });
+        }
         if (!up->buf) {
           st = JpegStatus::Corrupt;
           err = "decode buffers exhausted";

@@ -16,6 +16,7 @@
 #include <stdexcept>
 
 #include "executor.h"
+#include "peer.h"
 
 namespace arena {
 
@@ -24,6 +25,8 @@ class SplitInstance : public BatchInstance {
   SplitInstance(std::shared_ptr<Executor> det, std::shared_ptr<Executor> cls) : det_(std::move(det)), cls_(std::move(cls)) {
     if (!det_ || !cls_) throw std::runtime_error("SplitInstance: null executor");
     if (!cls_->peer_stage()) throw std::runtime_error("SplitInstance: classifier executor is not a peer stage");
+    // the classifier pulls the detector's slot over xGMI: refuse a pair without peer access at construction
+    require_peer_access(cls_->device(), det_->device(), "SplitInstance", hip_can_access_peer);
   }
   std::vector<int> buckets() const override {
     std::vector<int> out;

@@ -130,3 +130,33 @@ def barrier(info: DistInfo) -> None:
 def shutdown(info: DistInfo) -> None:
     if info.world > 1 and dist.is_initialized():
         dist.destroy_process_group()
+
+
+def device_identity(dev: int | None, rank: int, fake: bool = False) -> dict:
+    """The physical GPU a rank drives: PCI domain:bus:device plus the HIP UUID when torch reports them.  The
+    scaling record (bench.py ``rank_devices``) carries one per rank, so an N-GPU result can be checked to come
+    from N distinct devices, not N ranks sharing one (``world_size_checked`` alone cannot show that).  ``fake``:
+    the CPU fake engine, one synthetic id per rank (``ARENA_TEST_DUP_BUS=1``: all ranks the same id, the
+    duplicate check's own test)."""
+    if fake or dev is None:
+        bus = "fake:00" if os.environ.get("ARENA_TEST_DUP_BUS") == "1" else f"fake:{rank:02d}"
+        return {"rank": rank, "device": dev, "pci_bus_id": bus, "uuid": None, "name": "fake-engine"}
+    import torch
+
+    p = torch.cuda.get_device_properties(dev)
+    bus = "%04x:%02x:%02x.0" % (int(getattr(p, "pci_domain_id", 0)), int(getattr(p, "pci_bus_id", 0)),
+                                int(getattr(p, "pci_device_id", 0)))
+    uuid = str(getattr(p, "uuid", "")) or None
+    return {"rank": rank, "device": int(dev), "pci_bus_id": bus, "uuid": uuid, "name": p.name}
+
+
+def check_distinct_devices(ids: list[dict], shared_ok: bool) -> None:
+    """Refuse a multi-rank result in which two ranks drove the same physical GPU, unless that is the explicit
+    rehearsal mode (``ARENA_SHARED_GPU=1``: every rank on device 0 of a one-GPU box)."""
+    seen: dict[str, int] = {}
+    for d in ids:
+        key = d.get("pci_bus_id")
+        if key in seen and not shared_ok:
+            raise RuntimeError(f"ranks {seen[key]} and {d.get('rank')} drive the same GPU ({key}); a scaling "
+                               f"result needs one device per rank (set ARENA_SHARED_GPU=1 only for a rehearsal)")
+        seen.setdefault(key, d.get("rank"))

@@ -40,6 +40,29 @@ from .service_backends import DetectorBackend, build_detector_backend
 log = logging.getLogger("arena.detection")
 
 
+
+async def _detect_holding_slot(coro, ring, slot):
+    """Await a detection whose native batch may copy its frame into IPC ring ``slot`` (export_to) and release the
+    slot if the detection fails.  A cancelled request (client gone, deadline) must not hand the slot back while
+    that batch is still queued or running: its device-to-device export would later overwrite the frame of the
+    request that reuses the slot.  The detection is shielded, so it runs to completion, and the slot
+    is released from its done-callback."""
+    task = asyncio.ensure_future(coro)
+    try:
+        return await asyncio.shield(task)
+    except BaseException:
+        if slot is not None:
+            if task.done():
+                ring.release(slot)
+            else:
+                def _late(t, s=slot):
+                    if not t.cancelled():
+                        t.exception()  # retrieved: no "exception was never retrieved" warning
+                    ring.release(s)
+
+                task.add_done_callback(_late)
+        raise
+
 def create_app(settings: Settings | None = None, detector: DetectorBackend | None = None,
                client: ClassificationClient | None = None, ring=None) -> FastAPI:
     settings = settings or Settings.from_env(PORT=None)
@@ -104,18 +127,13 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
             if image is None and not split:
                 image = await state["decode"].decode(data)
             t_det = Timer()
-            try:
-                if split:
-                    det, dtiming = await det_be.detect_bytes(data, state["decode"].decode,
-                                                             export_to=ring.slot_ptr(slot))
-                elif slot is not None:
-                    det, dtiming = await det_be.detect(image, export_to=ring.slot_ptr(slot))
-                else:
-                    det, dtiming = await det_be.detect(image)
-            except BaseException:
-                if slot is not None:
-                    ring.release(slot)
-                raise
+            if split:
+                det_coro = det_be.detect_bytes(data, state["decode"].decode, export_to=ring.slot_ptr(slot))
+            elif slot is not None:
+                det_coro = det_be.detect(image, export_to=ring.slot_ptr(slot))
+            else:
+                det_coro = det_be.detect(image)
+            det, dtiming = await _detect_holding_slot(det_coro, ring, slot)
             detection_ms = t_det.ms()
             t_cls = Timer()
             boxes = [{"x1": float(d[0]), "y1": float(d[1]), "x2": float(d[2]), "y2": float(d[3]),
@@ -130,7 +148,14 @@ def create_app(settings: Settings | None = None, detector: DetectorBackend | Non
                     ref = ring.ref(slot, h, w)
                 else:  # no exporting detector (or no free slot before detection): upload the frame once more
                     loop = asyncio.get_running_loop()
-                    slot, ref = await loop.run_in_executor(None, ring.put, image)
+                    put = loop.run_in_executor(None, ring.put, image)
+                    try:
+                        slot, ref = await asyncio.shield(put)
+                    except asyncio.CancelledError:
+                        # the copy runs on; its slot is released once it lands instead of leaking
+                        put.add_done_callback(lambda f: None if f.cancelled() or f.exception() is not None
+                                              else ring.release(f.result()[0]))
+                        raise
                 try:
                     responses = await cl.classify_device(rid, ref, boxes)
                 finally:

@@ -136,8 +136,13 @@ class DeviceClassifier:
     tests pass a fake).  ``classify(key, boxes)`` resolves to per-crop (top-5 class ids, top-5 probabilities)."""
 
     def __init__(self, backend, open_handle, *, max_batch: int = 32, max_crops: int = 1 << 30,
-                 max_delay_us: int = 300, inflight: int = 2):
+                 max_delay_us: int = 300, inflight: int = 2, peer_check=None):
         self.backend = backend
+        # peer_check(src_device): raises when this process's GPU cannot read a ring exported on src_device
+        # (native require_peer_access: hipDeviceCanAccessPeer), so a cross-GPU reference gets a clear per-crop
+        # error instead of a fault in the copy kernel
+        self.peer_check = peer_check
+        self._peer_ok: set[int] = set()
         # handle bytes -> device pointer, or (pointer, mapped bytes) (native ipc_open_range)
         self.open_handle = open_handle
         self.max_batch = max_batch
@@ -169,6 +174,12 @@ class DeviceClassifier:
         bounds on the GPU and take down every in-flight batch).  Raises ValueError -> in-band per-crop error."""
         if key.height <= 0 or key.width <= 0 or key.offset < 0:
             raise ValueError(f"device frame: bad geometry {key.height}x{key.width} at offset {key.offset}")
+        if self.peer_check is not None and key.device >= 0 and key.device not in self._peer_ok:
+            try:
+                self.peer_check(int(key.device))
+            except RuntimeError as e:
+                raise ValueError(f"device frame: {e}") from e
+            self._peer_ok.add(int(key.device))
         _, size = self._map(key.handle)
         nbytes = key.height * key.width * 3
         if size is not None and key.offset + nbytes > size:

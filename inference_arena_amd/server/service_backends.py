@@ -249,6 +249,7 @@ def build_frame_classifier(settings):
     runner = build_session("frame_classifier", mnet=mnet, device=dev, buckets=_default_buckets(max_batch))
     C = native()
     return DeviceClassifier(runner, lambda h: C.ipc_open_range(h, dev), max_batch=max_batch,
+                            peer_check=lambda src: C.require_peer_access(dev, src, "device transport"),
                             max_crops=int(runner.ex.crop_cap_for(runner.max_batch)),
                             max_delay_us=int(os.environ.get("ARENA_CLS_QUEUE_DELAY_US", "300")))
 

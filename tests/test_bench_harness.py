@@ -61,6 +61,21 @@ def test_bench_divides_the_job_cpu_quota_between_ranks():
     assert 4 * plan["pil_procs"] <= 8  # decode processes of the whole node within the job quota
     assert out["cpu_budget_warning"] and "only 2 usable CPUs" in r.stderr
     assert out["errors"] == 0 and out["value"] > 0
+    # one physical device per rank, recorded
+    assert out["torch_world_size"] == 4 and out["distinct_gpus"] == 4 and not out["shared_gpu_rehearsal"]
+    assert [d["rank"] for d in out["rank_devices"]] == [0, 1, 2, 3]
+    assert len({d["pci_bus_id"] for d in out["rank_devices"]}) == 4
+
+
+def test_bench_refuses_two_ranks_on_one_gpu():
+    r = _bench("--gpus", "2", "--latency-levels", "", "--no-secondary-inproc", "--no-secondary-shared-front",
+               env={"ARENA_TEST_DUP_BUS": "1"})
+    assert r.returncode != 0 and "drive the same GPU" in r.stderr
+    r = _bench("--gpus", "2", "--latency-levels", "", "--no-secondary-inproc", "--no-secondary-shared-front",
+               env={"ARENA_TEST_DUP_BUS": "1", "ARENA_SHARED_GPU": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["shared_gpu_rehearsal"] is True and out["distinct_gpus"] == 1
 
 
 def test_bench_detects_diverging_replica_weights():

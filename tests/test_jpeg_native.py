@@ -182,3 +182,61 @@ def test_ingest_matches_pil_decode_and_falls_back(jpeg_device):
     st = b.ingest_stats() if jpeg_device else None
     if st is not None:
         assert st["native"] == 6 and st["fallback"] == 1 and st["errors"] == 1
+
+
+def _oversubscribe(data: bytes, pattern: int) -> bytes:
+    """Rewrite the first DHT table's code-length counts so that too many short codes exist (bits[1] = 3, or
+    bits[1] = 2 and bits[2] = 1) while the symbol total stays the same: the segment still parses."""
+    d = bytearray(data)
+    p = d.find(b"\xff\xc4")
+    assert p > 0
+    t = p + 5  # marker, length, Tc/Th
+    total = sum(d[t:t + 16])
+    d[t:t + 16] = bytes(16)
+    if pattern == 0:
+        d[t] = 3
+    else:
+        d[t], d[t + 1] = 2, 1
+    d[t + 15] = total - 3
+    return bytes(d)
+
+
+@pytest.mark.parametrize("pattern", [0, 1])
+def test_oversubscribed_huffman_table_is_corrupt(pattern):
+    """An over-subscribed DHT must be rejected before any lookahead table is filled (the code index
+    would run past the 2048-entry fast tables; libjpeg's jdhuff.c rejects code >= 1 << length)."""
+    C = native()
+    bad = _oversubscribe(_enc(_scene(48, 64), quality=90), pattern)
+    st, err, rgb = C.jpeg_decode_host(bad)
+    assert st == "corrupt" and rgb is None and "DHT" in err, (st, err)
+
+
+def test_decoder_fuzz_under_address_sanitizer(tmp_path):
+    """The host decoder (csrc/runtime/jpeg_decode.cpp) built host-only with AddressSanitizer and driven by
+    csrc/tests/jpeg_fuzz.cpp: over-subscribed tables rejected, 2000 random mutations without a memory error."""
+    import os
+    import shutil
+    import subprocess
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not (Path(hipcc).exists() or shutil.which(hipcc)):
+        pytest.skip("hipcc not available")
+    srcs = [root / "csrc" / "tests" / "jpeg_fuzz.cpp", root / "csrc" / "runtime" / "jpeg_decode.cpp"]
+    exe = root / "build" / "jpeg_fuzz_address"
+    exe.parent.mkdir(parents=True, exist_ok=True)
+    newest = max(p.stat().st_mtime for p in srcs + [root / "csrc" / "runtime" / "jpeg_decode.h",
+                                                   root / "csrc" / "kernels" / "jpeg_math.h"])
+    if not exe.exists() or exe.stat().st_mtime < newest:
+        cmd = [hipcc, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", "-fsanitize=address",
+               "-I" + str(root / "csrc"), *map(str, srcs), "-o", str(exe)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-4000:]
+    seed = tmp_path / "seed.jpg"
+    seed.write_bytes(_enc(_scene(96, 128), quality=90, subsampling=2))
+    r = subprocess.run([str(exe), str(seed), "2000"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1"))
+    report = r.stdout + r.stderr
+    assert "AddressSanitizer" not in report and r.returncode == 0, report[-6000:]
+    assert "jpeg_fuzz: ok" in r.stdout

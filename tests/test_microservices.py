@@ -347,3 +347,50 @@ def test_native_handler_drains_in_flight_requests_on_stop():
     assert got.get("status") == 200 and got["body"]["request_id"] == "r"
     assert box["rc"] == 0
 
+
+
+def test_cancelled_detection_keeps_its_ring_slot_until_the_batch_lands():
+    """a request cancelled while its native batch still holds export_dst = the ring slot must not hand
+    the slot back before that batch has copied its frame; released from the detection's completion instead."""
+    import asyncio
+
+    from inference_arena_amd.server.detection_service import _detect_holding_slot
+
+    class Ring:
+        def __init__(self):
+            self.released = []
+
+        def release(self, s):
+            self.released.append(s)
+
+    async def main():
+        ring = Ring()
+        gate = asyncio.Event()
+
+        async def detect():
+            await gate.wait()  # the batch is queued / on the device
+            return [], {}
+
+        outer = asyncio.ensure_future(_detect_holding_slot(detect(), ring, 3))
+        await asyncio.sleep(0.01)
+        outer.cancel()
+        try:
+            await outer
+        except asyncio.CancelledError:
+            pass
+        assert ring.released == []  # still owned by the in-flight batch
+        gate.set()
+        await asyncio.sleep(0.01)
+        assert ring.released == [3]
+
+        async def boom():
+            raise RuntimeError("device fault")
+
+        try:
+            await _detect_holding_slot(boom(), ring, 5)
+        except RuntimeError:
+            pass
+        assert ring.released == [3, 5]  # failed detection: released at once
+        assert await _detect_holding_slot(detect(), ring, None) == ([], {})
+
+    asyncio.run(main())

@@ -407,3 +407,32 @@ def test_split_decoder_answers_like_the_pil_pool(jpeg_device):
             batcher.shutdown()
     assert answers[3] == answers[0]
     assert len({len(a) for a in answers[3]}) > 1  # the first pixels differ, so the checks are not vacuous
+
+
+def test_split_decoder_stages_oversize_frames_as_rgb():
+    """a JPEG whose coefficients + sample planes + RGB frame exceed one batch's staging pool (about
+    > 15 MP at 4:2:0 with the executor's default pool) used to get a 413 from the split decoder although the PIL
+    path serves it as RGB.  Here the instance's staging pool is 3 x the frame's RGB bytes (as the default pool is
+    3 x 640 x 640 x 3 per image): the frame is reconstructed on the host and staged as RGB, with the same answer."""
+    C = native()
+    h, w = 96, 128
+    arr = (np.random.default_rng(5).random((h, w, 3)) * 255).astype(np.uint8)
+    b = io.BytesIO()
+    Image.fromarray(arr).save(b, format="JPEG", quality=90, subsampling=0)  # 4:4:4: coefficients 6 B / px
+    upload = b.getvalue()
+    answers = []
+    for cap in (0, h * w * 3 * 3):
+        batcher = C.DynamicBatcher([C.EchoInstance(2, 8, 4, 200, cap)], {"max_batch": 8, "max_queue_delay_us": 200})
+        fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=2, decode_procs=1,
+                            slots=16, decode_threads=2, jpeg_device=True)
+        try:
+            body, ct = _multipart(upload)
+            st, data, c = _post(fe.port, body, ct)
+            c.close()
+            assert st == 200, data
+            answers.append([(d["detection"], d["classification"]) for d in json.loads(data)["detections"]])
+            assert fe.stats()["native_decoded"] == 1
+        finally:
+            fe.close()
+            batcher.shutdown()
+    assert answers[0] == answers[1]
