@@ -8,6 +8,11 @@
 // constants, same rounding biases, same edge replication), so a frame reconstructed here is bit-identical to
 // PIL's (tests/test_jpeg_native.py pins that on the curated workload).
 //
+// Attribution: the IDCT below follows the structure and fixed-point constants of libjpeg's jidctint.c (islow), the
+// chroma upsampling that of jdsample.c (h2v1 / h2v2 "fancy" upsampling) and the colour conversion that of
+// jdcolor.c (ycc_rgb_convert).  Bit-exactness with PIL / libjpeg-turbo requires exactly that arithmetic.  This
+// software is based in part on the work of the Independent JPEG Group (see NOTICE at the repository root).
+//
 // Everything is plain integer math on values the caller supplies; there is no table and no memory access, so
 // the same functions run per lane in the HIP kernel and per pixel in the host reference.
 #pragma once

@@ -62,6 +62,8 @@ def main(argv=None) -> int:
     ap.add_argument("--jpeg-quality", type=int, default=90, help="synthetic: count on JPEG round trips (0: raw)")
     ap.add_argument("--limit", type=int, default=None, help="coco: scan at most this many files")
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--coco-url", default="http://images.cocodataset.org/zips/val2017.zip",
+                    help="coco: where to fetch val2017.zip when no --archive exists ('' = never download)")
     a = ap.parse_args(argv)
     out = Path(a.out)
     if out.exists() and not a.force:
@@ -81,8 +83,8 @@ def main(argv=None) -> int:
     else:
         from inference_arena_amd.data.coco import download_coco_val2017, get_coco_image_paths
 
-        root = download_coco_val2017(a.coco_dir, archive=a.archive)
-        paths = get_coco_image_paths(root)[: a.limit]
+        download_coco_val2017(a.coco_dir, archive=a.archive, url=a.coco_url or None)
+        paths = get_coco_image_paths(a.coco_dir)[: a.limit]
         _, man = curate_paths(make_counter(a.device, a.dtype, a.seed, 0), paths, cfg, log=log)
         man.config.update({"weight_seed": a.seed, "dtype": a.dtype})
     man.save(out)

@@ -45,18 +45,81 @@ def test_coco_utils(tmp_path):
     ok, msg = coco.is_coco_downloaded(tmp_path)
     assert not ok and "does not exist" in msg
     with pytest.raises(FileNotFoundError):
-        coco.download_coco_val2017(tmp_path)
+        coco.download_coco_val2017(tmp_path, url=None)
     buf = io.BytesIO()
     with zipfile.ZipFile(buf, "w") as z:
         for i, im in enumerate(synthetic_images(3, 1, hw=(40, 60))):
             z.writestr(f"val2017/{i:012d}.jpg", encode_jpeg(im))
     (tmp_path / "val2017.zip").write_bytes(buf.getvalue())
-    d = coco.download_coco_val2017(tmp_path)
+    with pytest.raises(RuntimeError, match="incomplete"):
+        coco.download_coco_val2017(tmp_path, url=None)  # 3 images are not the 5000 of val2017
+    d = coco.download_coco_val2017(tmp_path, url=None, expected_images=3)
     assert d.is_dir() and len(coco.get_coco_image_paths(tmp_path)) == 3
+    assert (tmp_path / "val2017.zip").exists()  # a provided archive is kept
     ok, msg = coco.is_coco_downloaded(tmp_path)
     assert not ok and "3 of 5000" in msg
     imgs = list(coco.iter_coco_images(tmp_path, limit=2))
     assert len(imgs) == 2 and imgs[0][1].shape == (40, 60, 3)
+
+
+def _zip_of(n: int) -> bytes:
+    buf = io.BytesIO()
+    with zipfile.ZipFile(buf, "w", compression=zipfile.ZIP_STORED) as z:
+        for i, im in enumerate(synthetic_images(n, 2, hw=(32, 48))):
+            z.writestr(f"val2017/{i:012d}.jpg", encode_jpeg(im))
+    return buf.getvalue()
+
+
+def test_coco_http_download_resumes_and_extracts(tmp_path):
+    """The reference downloads val2017.zip over HTTP with a progress bar (coco_dataset.py:141-217).  Here against
+    a local HTTP server with Range support: a partial .part is resumed (206), the archive is extracted, the
+    downloaded zip removed, and a second call is a no-op."""
+    import http.server
+    import threading
+
+    from inference_arena_amd.data import coco
+
+    blob = _zip_of(4)
+    seen = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):  # noqa: N802
+            rng = self.headers.get("Range")
+            seen.append(rng)
+            start = int(rng.split("=")[1].split("-")[0]) if rng else 0
+            body = blob[start:]
+            self.send_response(206 if rng else 200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    t = threading.Thread(target=srv.serve_forever, daemon=True)
+    t.start()
+    try:
+        url = f"http://127.0.0.1:{srv.server_address[1]}/val2017.zip"
+        (tmp_path / "val2017.zip.part").write_bytes(blob[:1000])  # an interrupted earlier run
+        prog = []
+        d = coco.download_coco_val2017(tmp_path, url=url, expected_images=4, progress=lambda a, b: prog.append((a, b)))
+        assert seen == ["bytes=1000-"] and prog[-1] == (len(blob), len(blob))
+        assert len(coco.get_coco_image_paths(tmp_path)) == 4 and d == tmp_path / "val2017"
+        assert not (tmp_path / "val2017.zip").exists() and not (tmp_path / "val2017.zip.part").exists()
+        coco.download_coco_val2017(tmp_path, url=url, expected_images=4)  # idempotent: no request
+        assert len(seen) == 1
+        # a fresh directory: a plain 200 download; a console progress bar
+        other = tmp_path / "b"
+        sink = io.StringIO()
+        coco.download_coco_val2017(other, url=url, expected_images=4,
+                                   progress=coco.DownloadProgress(len(blob), stream=sink))
+        assert seen[-1] is None and "100%" in sink.getvalue()
+        # a server that dies mid-body leaves only the .part, and the call fails loudly
+        with pytest.raises(RuntimeError):
+            coco.fetch_url(url.replace(str(srv.server_address[1]), "1"), tmp_path / "x.zip", timeout=2)
+    finally:
+        srv.shutdown()
 
 
 def test_registry_surface():
