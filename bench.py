@@ -128,15 +128,22 @@ def http_request(jpeg: bytes) -> bytes:
             f"Content-Length: {len(body)}\r\n\r\n").encode() + body
 
 
-def engine_throughput(ex, images, B: int, batches: int) -> float:
-    """Device pipeline alone (pre-decoded images, pipelined submit/collect): requests/s between the
-    completion of the first ``depth`` batches and the last one (fill and drain excluded)."""
+def engine_throughput(ex, images, B: int, batches: int, jpeg_set=None) -> float:
+    """Device pipeline alone, pipelined submit/collect from one host thread: requests/s between the completion of
+    the first ``depth`` batches and the last one (fill and drain excluded).
+
+    ``jpeg_set`` (native ``JpegSet``: the workload's uploads entropy-decoded once into pinned buffers): every batch
+    carries the inputs the HTTP path gives the executor — coefficient blocks DMA'd from pinned memory, GPU
+    dequantisation / IDCT / colour conversion, then the program — without the per-request Huffman decode, HTTP
+    or JSON work; this is the device ceiling of the headline path (``engine_req_s``).  Without it: pre-decoded RGB
+    frames, which the executor packs into its pinned staging on the host first (``engine_rgb_req_s``)."""
     depth = ex.num_slots()
-    n = len(images)
+    n = len(jpeg_set) if jpeg_set is not None else len(images)
     q, done_t = [], []
     k = 0
     for st in range(batches + depth):
-        q.append(ex.submit([images[(k + i) % n] for i in range(B)]))
+        idx = [(k + i) % n for i in range(B)]
+        q.append(ex.submit_jpeg_set(jpeg_set, idx) if jpeg_set is not None else ex.submit([images[i] for i in idx]))
         k += B
         if len(q) == depth:
             ex.collect(q.pop(0))
@@ -595,9 +602,12 @@ def main(argv=None) -> int:
         t_max = D.allreduce_max(window, info)
         per_rank = D.allgather_floats([a.steps * R / window], info)
 
-        eng = None
+        eng = eng_rgb = None
+        jset = None
         if not a.fake_engine and a.engine_batches > 0:
-            eng = engine_throughput(ex, images, a.batch, a.engine_batches)
+            jset = native().JpegSet(jpegs_r, pinned=True)
+            eng = engine_throughput(ex, images, a.batch, a.engine_batches, jset)
+            eng_rgb = engine_throughput(ex, images, a.batch, a.engine_batches)
         if not a.fake_engine and a.secondary_bf16 and a.dtype != "bf16":
             alt = GpuPipeline(yolo, mnet, device=dev, buckets=buckets, crop_cap_per_image=a.crop_cap, dtype="bf16")
             f4, b4 = serve(alt.ex)
@@ -608,11 +618,13 @@ def main(argv=None) -> int:
             close(f4, b4)
             sec["bf16"] = dict(summarize(w4, lat4, a, info, D), path=a.path, errors=int((st4 != 200).sum()),
                                mean_batch=ex4.get("mean_batch"), host_cpu_us_per_req=ex4.get("host_cpu_us_per_req"),
-                               engine_req_s=round(engine_throughput(alt.ex, images, a.batch, a.engine_batches), 1))
+                               engine_req_s=round(engine_throughput(alt.ex, images, a.batch, a.engine_batches, jset), 1)
+                               if jset is not None else None)
 
         all_lat = D.allgather_floats([float(x) for x in lat], info)
         all_crops = D.allgather_floats([float(c) for c in crops], info)
         all_eng = D.allgather_floats([eng or 0.0], info)
+        all_eng_rgb = D.allgather_floats([eng_rgb or 0.0], info)
         all_err = D.allgather_floats([float(errs)], info)
         all_cpu = D.allgather_floats([float(usable)], info)
         all_ext = D.allgather_objects(extras, info)
@@ -672,7 +684,11 @@ def main(argv=None) -> int:
                 "mean_crops_per_request": round(fan, 3),
                 "mean_batch": ext0.get("mean_batch"),
                 "errors": int(sum(x for lst in all_err for x in lst)),
+                # device ceiling of the headline path: pre-entropy-decoded JPEG coefficients from pinned memory ->
+                # GPU reconstruction -> program (engine_throughput); engine_rgb_req_s: RGB frames packed on the host
                 "engine_req_s": round(float(sum(x for lst in all_eng for x in lst)), 1) if eng else None,
+                "engine_input": "jpeg coefficients (pinned), GPU reconstruction" if eng else None,
+                "engine_rgb_req_s": round(float(sum(x for lst in all_eng_rgb for x in lst)), 1) if eng_rgb else None,
                 "levels": levels,
                 "bs1_p50_ms": (levels.get("1") or {}).get("p50_ms"),
                 "bs1_p99_ms": (levels.get("1") or {}).get("p99_ms"),

@@ -405,6 +405,51 @@ struct JpegHolder {
 using JpegKeep = std::vector<std::shared_ptr<JpegHolder>>;
 std::mutex g_jkeep_mu;
 std::map<std::pair<const void*, int>, JpegKeep> g_jkeep;
+struct JpegSet;
+std::map<std::pair<const void*, int>, std::shared_ptr<JpegSet>> g_jset_keep;  // sets of submitted batches
+
+// Uploads entropy-decoded once into pinned host memory (what the HTTP front end's decode threads hand the batcher:
+// coefficient blocks in a pinned HostBufferPool buffer, DMA'd by the executor), so a benchmark can replay the HTTP
+// path's device inputs without paying the Huffman decode per batch (bench.py engine_req_s: the device ceiling of
+// the split-decode path).
+struct JpegSet {
+  struct Item {
+    JpegInfo info;
+    int16_t* coef = nullptr;
+    bool pinned = false;
+    ~Item() {
+      if (coef == nullptr) return;
+      if (pinned) (void)hipHostFree(coef);
+      else std::free(coef);
+    }
+  };
+  std::vector<std::shared_ptr<Item>> items;
+};
+
+std::shared_ptr<JpegSet> make_jpeg_set(const py::list& uploads, bool pinned) {
+  auto set = std::make_shared<JpegSet>();
+  for (auto h : uploads) {
+    const std::string data = h.cast<std::string>();
+    auto it = std::make_shared<JpegSet::Item>();
+    std::string err;
+    JpegStatus st = jpeg_parse((const uint8_t*)data.data(), data.size(), it->info, err);
+    if (st != JpegStatus::Ok) throw py::value_error("JpegSet: not decodable by the split decoder: " + err);
+    const size_t bytes = std::max<size_t>(2, (size_t)it->info.coef_count * 2);
+    void* p = nullptr;
+    if (pinned && hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess) {
+      it->pinned = true;
+    } else {
+      (void)hipGetLastError();
+      p = std::malloc(bytes);
+      if (p == nullptr) throw std::bad_alloc();
+    }
+    it->coef = (int16_t*)p;
+    st = jpeg_decode_coefs((const uint8_t*)data.data(), data.size(), it->info, it->coef, err);
+    if (st != JpegStatus::Ok) throw py::value_error("JpegSet: entropy decode failed: " + err);
+    set->items.push_back(it);
+  }
+  return set;
+}
 
 std::vector<InputImage> images_from(const py::list& imgs, std::vector<py::array>& keep, JpegKeep* jkeep = nullptr) {
   std::vector<InputImage> v;
@@ -574,6 +619,27 @@ PYBIND11_MODULE(_C, m) {
              }
              return slot;
            })
+      .def("submit_jpeg_set",
+           // images idx[0..n) of a JpegSet: pre-decoded coefficients, reconstructed on the device like an HTTP upload
+           [](Executor& e, std::shared_ptr<JpegSet> set, const std::vector<int>& idx) {
+             std::vector<InputImage> v;
+             v.reserve(idx.size());
+             for (int i : idx) {
+               if (i < 0 || i >= (int)set->items.size()) throw py::index_error("submit_jpeg_set: index out of range");
+               const auto& it = set->items[i];
+               InputImage im{(const uint8_t*)it->coef, it->info.height, it->info.width};
+               im.jpeg = &it->info;
+               v.push_back(im);
+             }
+             int slot;
+             {
+               py::gil_scoped_release nogil;
+               slot = e.submit(v);
+             }
+             std::lock_guard<std::mutex> lk(g_jkeep_mu);
+             g_jset_keep[{(const void*)&e, slot}] = set;
+             return slot;
+           })
       .def("collect",
            [](Executor& e, int slot) {
              BatchResult r;
@@ -584,6 +650,7 @@ PYBIND11_MODULE(_C, m) {
              {
                std::lock_guard<std::mutex> lk(g_jkeep_mu);
                g_jkeep.erase({(const void*)&e, slot});
+               g_jset_keep.erase({(const void*)&e, slot});
              }
              return result_to_py(r, e.config().max_det);
            })
@@ -686,6 +753,16 @@ PYBIND11_MODULE(_C, m) {
            })
       .def("num_slots", &SplitInstance::num_slots)
       .def("buckets", &SplitInstance::buckets);
+
+  py::class_<JpegSet, std::shared_ptr<JpegSet>>(m, "JpegSet")
+      .def(py::init(&make_jpeg_set), py::arg("uploads"), py::arg("pinned") = true,
+           "JPEG uploads entropy-decoded once into (pinned) host buffers, for Executor.submit_jpeg_set")
+      .def("__len__", [](const JpegSet& s) { return s.items.size(); })
+      .def_property_readonly("pinned", [](const JpegSet& s) {
+        for (const auto& it : s.items)
+          if (!it->pinned) return false;
+        return true;
+      });
 
   py::class_<EchoInstance, std::shared_ptr<EchoInstance>>(m, "EchoInstance")
       .def(py::init<int, int, int, int, int64_t>(), py::arg("slots") = 2, py::arg("max_batch") = 32,

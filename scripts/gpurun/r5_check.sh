@@ -1,0 +1,32 @@
+#!/usr/bin/env bash
+# Round 5 check: chosen GPU tests, smoke, the driver-shaped bench, then (PROFILE=1) fp32 kernel traces of the
+# engine on RGB and on the HTTP path's JPEG inputs (reconstruction kernels + coefficient H2D per batch).
+# usage: scripts/gpurun/r5_check.sh TAG [pytest targets] -- [bench args]
+set -u
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+S=scripts/gpurun/gpu_step.sh
+T=${1:-r5}
+shift
+TESTS=""
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do TESTS="$TESTS $1"; shift; done
+[ $# -gt 0 ] && shift
+mkdir -p gpurun_out/$T
+if [ -n "$TESTS" ]; then
+  $S 900 gpurun_out/$T/pytest.log python -u -m pytest $TESTS -x -v --timeout 180 --timeout-method thread -p no:cacheprovider || exit 1
+  grep -E "passed|failed|error" gpurun_out/$T/pytest.log | tail -3
+  grep -q " failed\| error" gpurun_out/$T/pytest.log && exit 1
+fi
+$S 300 gpurun_out/$T/smoke.log python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+if [ "${PROFILE:-0}" = "1" ]; then
+  $S 300 gpurun_out/$T/prof_rgb.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/prof_rgb -o eng -- python3 tools/profile_engine.py --dtype fp32 --batches 12 || exit 1
+  f=$(find gpurun_out/$T/prof_rgb -name "eng_kernel_trace.csv" | head -1)
+  python tools/analyze_trace.py "$f" --dtype fp32 --replays 8 --out gpurun_out/$T/ops_bs32.md > /dev/null 2>&1; tail -14 gpurun_out/$T/ops_bs32.md
+  rm -f "$f"
+  $S 300 gpurun_out/$T/prof_jpeg.log rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/$T/prof_jpeg -o eng -- python3 tools/profile_engine.py --dtype fp32 --batches 12 --inputs jpeg || exit 1
+  python tools/jpeg_stage_profile.py gpurun_out/$T/prof_jpeg --out gpurun_out/$T/jpeg_stage.md || true
+  find gpurun_out/$T/prof_jpeg -name "*kernel_trace.csv" -size +2M -delete
+fi
+$S 900 gpurun_out/$T/bench.log python -u bench.py "$@" || exit 1
+grep '^{' gpurun_out/$T/bench.log | tail -1 > gpurun_out/$T/bench.json
+cut -c1-1800 gpurun_out/$T/bench.json

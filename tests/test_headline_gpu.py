@@ -1,0 +1,135 @@
+"""The headline program, pinned.
+
+``bench.py`` serves ``GpuPipeline(*default_models(0), buckets=[1, 32], dtype="fp32")`` with the default crop
+capacity and the shipped tuning table (data/tuning/conv_tuning.json) to JPEG q90 uploads of the curated workload
+(data/synthetic_set/manifest_w0_n100.json), decoded by the split decoder (host Huffman, GPU reconstruction).  This
+test builds exactly that program and checks full batches of 32 — the bucket the headline measures — against the
+fp32 torch-CPU ``ReferencePipeline`` on the PIL-decoded frames, with the criteria of
+tests/test_fp32_gpu.py::test_fp32_pipeline_matches_reference (reference compute path:
+/root/reference/architectures/monolithic/app/inference.py:127-227)."""
+from __future__ import annotations
+
+import io
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _iou(a, b):
+    x1 = np.maximum(a[:, None, 0], b[None, :, 0])
+    y1 = np.maximum(a[:, None, 1], b[None, :, 1])
+    x2 = np.minimum(a[:, None, 2], b[None, :, 2])
+    y2 = np.minimum(a[:, None, 3], b[None, :, 3])
+    inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
+    aa = (a[:, 2] - a[:, 0]) * (a[:, 3] - a[:, 1])
+    bb = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    return inter / (aa[:, None] + bb[None, :] - inter + 1e-9)
+
+
+@pytest.fixture(scope="module")
+def headline():
+    from PIL import Image
+
+    from inference_arena_amd.data.curator import workload_images
+    from inference_arena_amd.data.synthetic import encode_jpeg
+    from inference_arena_amd.engine.pipeline import GpuPipeline
+    from inference_arena_amd.models.zoo import default_models
+
+    models = default_models(0)
+    pipe = GpuPipeline(*models, device=0, buckets=[1, 32], dtype="fp32")  # bench.py's program
+    jpegs = [encode_jpeg(im, 90) for im in workload_images(64)]
+    frames = []
+    for j in jpegs:
+        with Image.open(io.BytesIO(j)) as im:
+            frames.append(np.asarray(im.convert("RGB")))
+    return models, pipe, jpegs, frames
+
+
+def _compare(got, frames, ref):
+    n_det = n_top1 = n_same_crop = 0
+    rel = []
+    for i, (im, g) in enumerate(zip(frames, got)):
+        r = ref(im)
+        assert len(g) == len(r), f"image {i}: {len(g)} detections vs reference {len(r)}"
+        if not len(r):
+            continue
+        iou = _iou(r.boxes, g.boxes)
+        for j in range(len(r)):
+            k = int(np.argmax(iou[j]))
+            assert iou[j, k] > 0.99, (i, j, iou[j, k])
+            assert g.classes[k] == r.classes[j]
+            assert abs(float(g.scores[k]) - float(r.scores[j])) < 1e-4
+            n_det += 1
+            n_top1 += int(g.topk_idx[k, 0] == r.topk_idx[j, 0])
+            if np.array_equal(np.trunc(g.boxes[k]), np.trunc(r.boxes[j])):
+                n_same_crop += 1
+                rel.append(abs(float(g.topk_logit[k, 0]) - float(r.topk_logit[j, 0]))
+                           / (abs(float(r.topk_logit[j, 0])) + 1e-6))
+    return n_det, n_top1, n_same_crop, rel
+
+
+def test_bucket32_jpeg_path_matches_reference(headline):
+    """Two full batches of 32 JPEG uploads through the split decoder and the bucket-32 program."""
+    from inference_arena_amd.engine.pipeline import split_results
+    from inference_arena_amd.engine.reference import ReferencePipeline
+
+    models, pipe, jpegs, frames = headline
+    got = []
+    for k in (0, 32):
+        res = pipe.ex.run(list(jpegs[k:k + 32]))  # bytes: host entropy decode, GPU reconstruction
+        assert int(res["bucket"]) == 32
+        got += split_results(res, 32)
+    ref = ReferencePipeline(*models, device="cpu")
+    n_det, n_top1, n_same_crop, rel = _compare(got, frames, ref)
+    assert n_det >= 3 * 64, n_det  # the curated workload: 3-5 detections per image
+    assert n_top1 >= 0.99 * n_det, (n_top1, n_det)
+    assert n_same_crop >= 0.95 * n_det, (n_same_crop, n_det)
+    assert max(rel) < 1e-3, max(rel)
+
+
+def test_bucket32_rgb_path_and_jpeg_path_agree(headline):
+    """The same 32 frames as RGB (host pack) and as JPEG coefficients (GPU reconstruction) give the same answer:
+    the reconstruction is bit-exact with PIL, so the two programs see identical pixels."""
+    from inference_arena_amd.engine.pipeline import split_results
+
+    _, pipe, jpegs, frames = headline
+    a = split_results(pipe.ex.run(list(jpegs[:32])), 32)
+    b = pipe.infer(frames[:32])
+    for x, y in zip(a, b):
+        assert len(x) == len(y)
+        np.testing.assert_array_equal(x.boxes, y.boxes)
+        np.testing.assert_array_equal(x.topk_idx, y.topk_idx)
+        np.testing.assert_array_equal(x.topk_logit, y.topk_logit)
+
+
+def test_large_rgb_frames_grow_the_host_staging(headline):
+    """Frames larger than the nominal 640 x 640 staging share (the pinned host staging is sized for
+    nominal frames and grows on demand) give the same answer as the same frames one at a time."""
+    from inference_arena_amd.data.synthetic import synthetic_images
+
+    _, pipe, _, _ = headline
+    big = synthetic_images(10, 77, hw=(1080, 1920))  # 62 MB of RGB: past the nominal 39 MB
+    together = pipe.infer(big)
+    for im, t in zip(big, together):
+        (s,) = pipe.infer([im])
+        assert len(s) == len(t)
+        np.testing.assert_allclose(s.boxes, t.boxes, rtol=0, atol=1e-3)
+
+
+def test_engine_rate_jpeg_set(headline):
+    """bench.py engine_req_s feeds pre-entropy-decoded pinned coefficient sets (native JpegSet): the same answers
+    as the bytes path, at the bucket the headline runs."""
+    from inference_arena_amd.engine.pipeline import split_results
+    from inference_arena_amd.ops import native
+
+    _, pipe, jpegs, _ = headline
+    js = native().JpegSet(jpegs[:32], pinned=True)
+    assert len(js) == 32 and js.pinned
+    s = pipe.ex.submit_jpeg_set(js, list(range(32)))
+    a = split_results(pipe.ex.collect(s), 32)
+    b = split_results(pipe.ex.run(list(jpegs[:32])), 32)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x.boxes, y.boxes)
+        np.testing.assert_array_equal(x.topk_logit, y.topk_logit)

@@ -18,6 +18,9 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--batches", type=int, default=20)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--inputs", default="rgb", choices=["rgb", "jpeg"],
+                    help="rgb: decoded frames (host pack); jpeg: the HTTP path's device inputs (JPEG q90 uploads "
+                         "entropy-decoded once into pinned buffers: coefficient H2D + GPU reconstruction per batch)")
     a = ap.parse_args(argv)
     import torch
 
@@ -31,17 +34,28 @@ def main(argv=None) -> int:
     images = load_manifest_images(man)
     pipe = GpuPipeline(*default_models(a.seed), device=0, buckets=[a.batch], dtype=a.dtype)
     B = a.batch
+    if a.inputs == "jpeg":
+        from inference_arena_amd.data.synthetic import encode_jpeg
+        from inference_arena_amd.ops import native
+
+        js = native().JpegSet([encode_jpeg(im, int(man.config.get("jpeg_quality", 90))) for im in images])
+
+        def run(i):
+            return pipe.ex.collect(pipe.ex.submit_jpeg_set(js, [(i * B + k) % len(images) for k in range(B)]))
+    else:
+        def run(i):
+            return pipe.ex.run([images[(i * B + k) % len(images)] for k in range(B)])
     for i in range(3):
-        pipe.ex.run([images[(i * B + k) % len(images)] for k in range(B)])
+        run(i)
     torch.cuda.synchronize()
     t = time.perf_counter()
     gpu = []
     for i in range(a.batches):
-        r = pipe.ex.run([images[(i * B + k) % len(images)] for k in range(B)])
+        r = run(i)
         gpu.append(r["gpu_ms"])
     dt = time.perf_counter() - t
     gpu.sort()
-    print(f"{a.dtype}: {a.batches} sequential batches of {B}: {dt / a.batches * 1e3:.3f} ms/batch wall, "
+    print(f"{a.dtype} ({a.inputs}): {a.batches} sequential batches of {B}: {dt / a.batches * 1e3:.3f} ms/batch wall, "
           f"gpu_ms p50 {gpu[len(gpu) // 2]:.3f}", flush=True)
     return 0
 
