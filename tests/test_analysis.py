@@ -62,3 +62,81 @@ def test_cost_config_validates():
     c = get_cost_config()
     assert c["gpu_hour_usd"] > 0 and c["vcpu_hour_usd"] >= 0
     assert validate_config() == []
+
+
+def _rows():
+    """Synthetic sweep rows: monolithic fastest at low load, triton catching up past ~60 users on throughput."""
+    out = []
+    spec = {
+        "monolithic": {1: (300, 2.5, 3.0, 120, 3000), 10: (2800, 3.5, 4.0, 350, 3100),
+                       50: (5400, 9.0, 10.0, 500, 3200), 100: (6000, 15.0, 17.0, 600, 3300)},
+        "microservices": {1: (150, 6.0, 9.0, 160, 5000), 10: (950, 10.0, 17.0, 900, 5100),
+                          50: (1600, 27.0, 120.0, 1300, 5200), 100: (1700, 50.0, 200.0, 1300, 5300)},
+        "triton": {1: (280, 2.7, 3.5, 150, 6000), 10: (1300, 7.0, 13.0, 400, 6100),
+                   50: (4900, 10.0, 16.0, 1000, 6200), 100: (6500, 15.0, 28.0, 1100, 6300)},
+    }
+    for arch, lv in spec.items():
+        for u, (rps, p50, p99, cpu, mem) in lv.items():
+            for run in (1, 2):
+                out.append({"architecture": arch, "users": u, "run": run, "throughput_rps": rps + run,
+                            "p50_latency_ms": p50, "p99_latency_ms": p99, "cpu_utilization_percent": cpu,
+                            "memory_usage_mb": mem, "error_rate_percent": 0.0,
+                            "cost_per_1000_requests_usd": 1.0 / rps})
+    return out
+
+
+def test_h2_h3_and_rq4_from_sweep_rows():
+    from inference_arena_amd.analysis.decision import analyze
+
+    rq3 = {"monolithic": {"application_code_loc": 2000, "configuration_loc": 50},
+           "microservices": {"application_code_loc": 1100, "configuration_loc": 80},
+           "triton": {"application_code_loc": 1300, "configuration_loc": 70}}
+    deploy = {"monolithic": {"deployment_time_seconds": 8.0, "runs": [8, 8, 8], "baseline_memory_mb": 2900},
+              "microservices": {"deployment_time_seconds": 12.0, "runs": [12] * 3, "baseline_memory_mb": 5000},
+              "triton": {"deployment_time_seconds": 15.0, "runs": [15] * 3, "baseline_memory_mb": 6000}}
+    out = analyze(_rows(), rq3, deploy)
+    h = out["hypotheses"]
+    assert h["H2a"]["supported"] and h["H2a"]["supported_configured"]  # 2 vs 4 vCPU in deploy/compose
+    assert h["H2b"]["supported"]
+    assert h["H2c"]["supported"] and h["H2c"]["source"]["triton"] == "idle after ready"
+    assert h["H2d"]["levels"] == [50, 100] and "supported" in h["H2d"]
+    assert h["H3a"]["supported"]  # 1300 < 2000 application LOC
+    assert h["H3b"]["supported"] and h["H3c"]["supported"]
+    # throughput: triton overtakes monolithic between 50 and 100 users
+    cx = [c for c in out["rq4"]["crossover_points"] if c["pair"] == ["monolithic", "triton"]
+          and c["metric"] == "throughput_rps"]
+    assert len(cx) == 1 and 50 < cx[0]["users"] < 100
+    assert cx[0]["better_below"] == "monolithic" and cx[0]["better_above"] == "triton"
+    dm = out["rq4"]["decision_matrix"]
+    assert dm["by_load_regime"]["low (<= 10 users)"]["lowest_p99_ms"]["best"] == "monolithic"
+    assert dm["by_load_regime"]["high (>= 75 users)"]["highest_throughput_rps"]["best"] == "triton"
+    assert dm["by_p99_slo"]["p99 <= 5 ms"]["best"] == "monolithic"
+    assert dm["by_p99_slo"]["p99 <= 50 ms"]["best"] == "triton"
+
+
+def test_deploy_time_with_a_fake_launcher(tmp_path):
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "scripts"))
+    import deploy_time
+
+    started = []
+
+    def start(arch, gpus, log_dir):
+        time.sleep(0.05)
+        p = subprocess.Popen([sys.executable, "-c", "import time; x = bytearray(20 << 20); time.sleep(30)"])
+        started.append(p)
+        time.sleep(0.5)
+        return [p], True
+
+    def stop(procs):
+        for p in procs:
+            p.kill()
+            p.wait()
+
+    r = deploy_time.measure("monolithic", 2, 1, tmp_path, start=start, stop=stop, settle_s=0.1)
+    assert len(r["runs"]) == 2 and all(0.5 <= t < 5 for t in r["runs"])
+    assert r["baseline_memory_mb"] > 15  # the child's 20 MiB buffer is resident
+    assert all(p.poll() is not None for p in started)
