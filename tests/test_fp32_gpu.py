@@ -560,6 +560,8 @@ def _ir_ref64(x, expand, dw, project, stride, res):
     (16, 96, 24, 2, 37, False),    # block 2: 16 -> 24, stride 2, odd size (ir_f32 either way)
     (32, 96, 24, 2, 37, False),    # stride 2 with a full 32-channel input (the x3 tile kernel)
     (24, 144, 24, 1, 28, True),    # block 3 (hid 144 -> 160 padded chunks), residual
+    (24, 144, 24, 1, 56, True),    # block 3 at its own size (register-resident kernel, 7-row strips)
+    (32, 192, 32, 1, 30, False),   # stride 1, a map that is no multiple of the 14-column strips
     (24, 144, 32, 2, 28, False),   # block 4
     (32, 192, 32, 1, 28, True),    # block 5/6
     (32, 192, 64, 2, 28, False),   # block 7 (4 output tiles of 16)
@@ -583,6 +585,11 @@ def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, x3t, m
         native().set_irx_parts(4 if x3t == "0" else 2)
         request.addfinalizer(lambda: native().set_irx_parts(-1))
     monkeypatch.setenv("ARENA_IR_X3T", x3t)
+    if H >= 28:  # "1": the register-resident kernel (ir_reg_x3.hip) where it applies; "0" keeps the others
+        from inference_arena_amd.ops import native
+
+        native().set_ir_reg(1 if x3t == "1" else 0)
+        request.addfinalizer(lambda: native().set_ir_reg(-1))
     g = torch.Generator().manual_seed(inp * 7 + hid + stride)
     x = torch.randn(3, inp, H, H, generator=g)
     expand = None if hid == inp else (torch.randn(hid, inp, 1, 1, generator=g) / inp ** 0.5,

@@ -37,6 +37,7 @@ SOURCES = [
     "kernels/ir_f32.hip",
     "kernels/ir_crop_f32.hip",
     "kernels/ir_tile_x3.hip",
+    "kernels/ir_reg_x3.hip",
     "kernels/dwconv.hip",
     "kernels/ir_block.hip",
     "kernels/ir_block_wave.hip",
