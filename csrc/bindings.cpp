@@ -759,6 +759,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init(&make_jpeg_set), py::arg("uploads"), py::arg("pinned") = true,
            "JPEG uploads entropy-decoded once into (pinned) host buffers, for Executor.submit_jpeg_set")
       .def("__len__", [](const JpegSet& s) { return s.items.size(); })
+      .def("coef_bytes", [](const JpegSet& s, int i) { return (int64_t)s.items.at(i)->info.coef_count * 2; })
       .def_property_readonly("pinned", [](const JpegSet& s) {
         for (const auto& it : s.items)
           if (!it->pinned) return false;

@@ -72,6 +72,12 @@ __device__ __forceinline__ float irr_right(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x101, 0xf, 0xf, true));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 irr_relu6x2(f32x2 v) {
+  return f32x2{__builtin_amdgcn_fmed3f(v[0], 0.0f, 6.0f), __builtin_amdgcn_fmed3f(v[1], 0.0f, 6.0f)};
+}
+
 __host__ __device__ constexpr size_t irr_lds_bytes(int hid_pad, int nto) {
   return (size_t)hid_pad * IRR_WEP * 2 + (size_t)nto * 16 * 3 * hid_pad * 2 + (size_t)11 * hid_pad * 4;
 }
@@ -123,8 +129,9 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
     const bool xin = (unsigned)x < (unsigned)p.W;
     const float* xb = (const float*)p.x + (size_t)b * p.H * p.W * p.x_cs;
 
-    // ---- the strip's input rows y0 - 1 .. y0 + R, channels 8q .. 8q + 7 of this lane's pixel (fp32)
-    float xv[R + 2][8];
+    // ---- the strip's input rows y0 - 1 .. y0 + R, channels 8q .. 8q + 7 of this lane's pixel, split once into
+    // the expand's B operand (kept for every hidden chunk)
+    bf16x8 xh[R + 2], xm[R + 2], xl[R + 2];
     float inside[R + 2];
 #pragma unroll
     for (int i = 0; i < R + 2; ++i) {
@@ -135,14 +142,9 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
       const float* src = xb + ((size_t)(in ? y : 0) * p.W + (in ? x : 0)) * p.x_cs + (k < p.inp ? k : 0);
       const float4 a = *(const float4*)src, cc = *(const float4*)(src + 4);
       const bool lo = in && k < p.inp, hi = in && k + 4 < p.inp;
-      xv[i][0] = lo ? a.x : 0.f;
-      xv[i][1] = lo ? a.y : 0.f;
-      xv[i][2] = lo ? a.z : 0.f;
-      xv[i][3] = lo ? a.w : 0.f;
-      xv[i][4] = hi ? cc.x : 0.f;
-      xv[i][5] = hi ? cc.y : 0.f;
-      xv[i][6] = hi ? cc.z : 0.f;
-      xv[i][7] = hi ? cc.w : 0.f;
+      const float v[8] = {lo ? a.x : 0.f, lo ? a.y : 0.f, lo ? a.z : 0.f, lo ? a.w : 0.f,
+                          hi ? cc.x : 0.f, hi ? cc.y : 0.f, hi ? cc.z : 0.f, hi ? cc.w : 0.f};
+      irr_split8(v, xh[i], xm[i], xl[i]);
     }
 
     f32x4 acc[R][NTO];
@@ -168,65 +170,69 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
         wpm[o] = *(const bf16x8*)(r + hid);
         wpl[o] = *(const bf16x8*)(r + 2 * hid);
       }
-      const float4 be0 = *(const float4*)&sWd[10 * hid + h0 + 4 * q];
-      const float4 be1 = *(const float4*)&sWd[10 * hid + h0 + 16 + 4 * q];
-      const float bev[8] = {be0.x, be0.y, be0.z, be0.w, be1.x, be1.y, be1.z, be1.w};
+      // the lane's 8 hidden channels: 4q + j (j < 4) and 16 + 4q + j - 4, as float2 pairs (packed FMA)
+      f32x2 wdw[9][4], bdv[4], bev[4];
+#pragma unroll
+      for (int t = 0; t < 11; ++t) {
+        const float4 w0 = *(const float4*)&sWd[t * hid + h0 + 4 * q];
+        const float4 w1 = *(const float4*)&sWd[t * hid + h0 + 16 + 4 * q];
+        f32x2* dst = t < 9 ? wdw[t] : t == 9 ? bdv : bev;
+        dst[0] = f32x2{w0.x, w0.y};
+        dst[1] = f32x2{w0.z, w0.w};
+        dst[2] = f32x2{w1.x, w1.y};
+        dst[3] = f32x2{w1.z, w1.w};
+      }
 
-      // E of halo row i: hidden 4q + j (j < 4) / 16 + 4q + j - 4 of this lane's pixel, zero outside the image
-      auto expand = [&](int i, float (&e)[8]) {
-        bf16x8 xh, xm, xl;
-        irr_split8(xv[i], xh, xm, xl);
-        const f32x4 e0 = irr_mfma(weh[0], wem[0], wel[0], xh, xm, xl, f32x4{0.f, 0.f, 0.f, 0.f});
-        const f32x4 e1 = irr_mfma(weh[1], wem[1], wel[1], xh, xm, xl, f32x4{0.f, 0.f, 0.f, 0.f});
+      // expand every halo row first: 2 (R + 2) independent six-MFMA chains back to back
+      f32x2 E[R + 2][4];
+#pragma unroll
+      for (int i = 0; i < R + 2; ++i) {
+        const f32x4 e0 = irr_mfma(weh[0], wem[0], wel[0], xh[i], xm[i], xl[i], f32x4{0.f, 0.f, 0.f, 0.f});
+        const f32x4 e1 = irr_mfma(weh[1], wem[1], wel[1], xh[i], xm[i], xl[i], f32x4{0.f, 0.f, 0.f, 0.f});
+        const f32x2 m2 = f32x2{inside[i], inside[i]};
+        E[i][0] = irr_relu6x2(f32x2{e0[0], e0[1]} + bev[0]) * m2;
+        E[i][1] = irr_relu6x2(f32x2{e0[2], e0[3]} + bev[1]) * m2;
+        E[i][2] = irr_relu6x2(f32x2{e1[0], e1[1]} + bev[2]) * m2;
+        E[i][3] = irr_relu6x2(f32x2{e1[2], e1[3]} + bev[3]) * m2;
+      }
+      // depthwise over a rolling window of three rows, each row's left / right neighbours shifted once
+      f32x2 L[3][4], Rt[3][4];
+      auto shift_row = [&](int i, int slot) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          e[j] = relu6f(e0[j] + bev[j]) * inside[i];
-          e[4 + j] = relu6f(e1[j] + bev[4 + j]) * inside[i];
+          L[slot][j] = f32x2{irr_left(E[i][j][0]), irr_left(E[i][j][1])};
+          Rt[slot][j] = f32x2{irr_right(E[i][j][0]), irr_right(E[i][j][1])};
         }
       };
-      float E0[8], E1[8], E2[8];
-      expand(0, E0);
-      expand(1, E1);
+      shift_row(0, 0);
+      shift_row(1, 1);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        // the depthwise taps are re-read from LDS per row (broadcast reads): hoisted they would hold 72 VGPRs
-        asm volatile("" ::: "memory");
-        expand(r + 2, E2);
-        // depthwise 3x3 + bias + ReLU6 on the lane's 8 hidden channels
-        float d[8];
-        {
-          const float4 b0 = *(const float4*)&sWd[9 * hid + h0 + 4 * q];
-          const float4 b1 = *(const float4*)&sWd[9 * hid + h0 + 16 + 4 * q];
-          d[0] = b0.x; d[1] = b0.y; d[2] = b0.z; d[3] = b0.w;
-          d[4] = b1.x; d[5] = b1.y; d[6] = b1.z; d[7] = b1.w;
-        }
+        shift_row(r + 2, (r + 2) % 3);
+        f32x2 d[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = bdv[j];
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
-          const float* Er = ky == 0 ? E0 : ky == 1 ? E1 : E2;
+          const int slot = (r + ky) % 3;
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const int tap = ky * 3 + kx;
-            const float4 w0 = *(const float4*)&sWd[tap * hid + h0 + 4 * q];
-            const float4 w1 = *(const float4*)&sWd[tap * hid + h0 + 16 + 4 * q];
-            const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float v = kx == 0 ? irr_left(Er[j]) : kx == 1 ? Er[j] : irr_right(Er[j]);
-              d[j] = fmaf(v, wv[j], d[j]);
-            }
+          for (int j = 0; j < 4; ++j) {
+            d[j] = __builtin_elementwise_fma(L[slot][j], wdw[3 * ky][j], d[j]);
+            d[j] = __builtin_elementwise_fma(E[r + ky][j], wdw[3 * ky + 1][j], d[j]);
+            d[j] = __builtin_elementwise_fma(Rt[slot][j], wdw[3 * ky + 2][j], d[j]);
           }
         }
+        float dv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = relu6f(d[j]);
+        for (int j = 0; j < 4; ++j) {
+          const f32x2 v = irr_relu6x2(d[j]);
+          dv[2 * j] = v[0];
+          dv[2 * j + 1] = v[1];
+        }
         bf16x8 dh, dm, dl;
-        irr_split8(d, dh, dm, dl);
+        irr_split8(dv, dh, dm, dl);
 #pragma unroll
         for (int o = 0; o < NTO; ++o) acc[r][o] = irr_mfma(wph[o], wpm[o], wpl[o], dh, dm, dl, acc[r][o]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          E0[j] = E1[j];
-          E1[j] = E2[j];
-        }
       }
     }
 
@@ -259,7 +265,14 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
 
 namespace {
 
-int irr_rows(int H) { return H >= 56 ? 7 : 4; }
+int irr_rows(int H) {
+  static const int forced = [] {
+    const char* e = std::getenv("ARENA_IR_REG_ROWS");  // A/B: 4 or 7 rows per strip at every size
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced == 4 || forced == 7) return forced;
+  return H >= 56 ? 7 : 4;
+}
 
 template <int R, int NTO>
 void irr_launch(const IrParams& p, hipStream_t s) {

@@ -28,7 +28,7 @@ if [ "${PROFILE:-0}" = "1" ]; then
   rm -f "$f"
 fi
 if [ "${JPEGPROF:-0}" = "1" ]; then
-  $S 300 gpurun_out/$T/prof_jpeg.log rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d gpurun_out/$T/prof_jpeg -o eng -- python3 tools/profile_engine.py --dtype fp32 --batches 12 --inputs jpeg || exit 1
+  $S 300 gpurun_out/$T/prof_jpeg.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/prof_jpeg -o eng -- python3 tools/profile_engine.py --dtype fp32 --batches 12 --inputs jpeg || exit 1
   python tools/jpeg_stage_profile.py gpurun_out/$T/prof_jpeg --out gpurun_out/$T/jpeg_stage.md || true
   find gpurun_out/$T/prof_jpeg -name "*kernel_trace.csv" -size +2M -delete
 fi

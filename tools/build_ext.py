@@ -67,6 +67,11 @@ SOURCES = [
 ]
 
 
+# ir_reg_x3.hip keeps a whole strip's inputs, expanded rows and accumulators in registers: let the register
+# allocator spill the overflow to AGPRs (v_accvgpr moves) rather than scratch memory
+PER_FILE_FLAGS = {"ir_reg_x3.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]}
+
+
 def ext_path() -> Path:
     return PKG / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
 
@@ -98,6 +103,8 @@ def compile_one(src: Path, obj: Path, extra: list[str], verbose: bool) -> str:
     obj.parent.mkdir(parents=True, exist_ok=True)
     cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-c", str(src), "-o", str(obj)]
     cmd += _includes() + extra
+    if src.name in PER_FILE_FLAGS:
+        cmd += PER_FILE_FLAGS[src.name]
     if src.suffix == ".cpp":
         # host-only translation units still go through hipcc (HIP runtime headers)
         cmd += ["-x", "hip"] if "bindings" not in src.name else []

@@ -55,6 +55,23 @@ def main(argv=None) -> int:
         gpu.append(r["gpu_ms"])
     dt = time.perf_counter() - t
     gpu.sort()
+    if a.inputs == "jpeg":
+        # the coefficient bytes one batch DMAs from pinned memory, and the time of one copy of that size
+        # (pinned host -> device, timed by events) - the H2D share of the split decoder per batch
+        nbytes = int(sum(js.coef_bytes(k % len(images)) for k in range(B)))
+        h = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(3):
+            d.copy_(h, non_blocking=True)
+        e0.record()
+        for _ in range(10):
+            d.copy_(h, non_blocking=True)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"jpeg coefficients per batch of {B}: {nbytes / 1e6:.2f} MB, pinned H2D {e0.elapsed_time(e1) / 10 * 1e3:.1f} us",
+              flush=True)
+        del js
     print(f"{a.dtype} ({a.inputs}): {a.batches} sequential batches of {B}: {dt / a.batches * 1e3:.3f} ms/batch wall, "
           f"gpu_ms p50 {gpu[len(gpu) // 2]:.3f}", flush=True)
     return 0
