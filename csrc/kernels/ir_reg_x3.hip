@@ -39,7 +39,8 @@ namespace {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int IRR_WEP = 96;  // bf16 per staged expand row: h | m | l x 32 k
+constexpr int IRR_WEP = 96;
+  // bf16 per staged expand row: h | m | l x 32 k
 
 __device__ __forceinline__ void irr_split8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
 #pragma unroll
@@ -85,7 +86,7 @@ __host__ __device__ constexpr size_t irr_lds_bytes(int hid_pad, int nto) {
 }  // namespace
 
 // R: output rows per strip; NTO: oup_pad / 16; WPB: waves per workgroup (each walks its own strips)
-template <int R, int NTO, int WPB>
+template <int R, int NTO, int WPB, bool IRR_SCHED>
 __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t irr_lds[];
   const int hid = p.hid_pad;
@@ -183,43 +184,43 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
         dst[3] = f32x2{w1.z, w1.w};
       }
 
-      // expand every halo row first: 2 (R + 2) independent six-MFMA chains back to back
-      f32x2 E[R + 2][4];
-#pragma unroll
-      for (int i = 0; i < R + 2; ++i) {
+      // Software pipeline over the rows: iteration r issues the expand of halo row r + 3 (12 MFMAs, needed
+      // two iterations later) next to the depthwise of output row r (VALU on rows r .. r + 2, already done) and
+      // its project (12 MFMAs), so matrix and vector work of one wave overlap.  E and its left / right
+      // neighbours live in a rolling window of four rows.
+      f32x2 E[4][4], L[4][4], Rt[4][4];
+      auto expand = [&](int i) {
+        const int sl = i & 3;
         const f32x4 e0 = irr_mfma(weh[0], wem[0], wel[0], xh[i], xm[i], xl[i], f32x4{0.f, 0.f, 0.f, 0.f});
         const f32x4 e1 = irr_mfma(weh[1], wem[1], wel[1], xh[i], xm[i], xl[i], f32x4{0.f, 0.f, 0.f, 0.f});
         const f32x2 m2 = f32x2{inside[i], inside[i]};
-        E[i][0] = irr_relu6x2(f32x2{e0[0], e0[1]} + bev[0]) * m2;
-        E[i][1] = irr_relu6x2(f32x2{e0[2], e0[3]} + bev[1]) * m2;
-        E[i][2] = irr_relu6x2(f32x2{e1[0], e1[1]} + bev[2]) * m2;
-        E[i][3] = irr_relu6x2(f32x2{e1[2], e1[3]} + bev[3]) * m2;
-      }
-      // depthwise over a rolling window of three rows, each row's left / right neighbours shifted once
-      f32x2 L[3][4], Rt[3][4];
-      auto shift_row = [&](int i, int slot) {
+        E[sl][0] = irr_relu6x2(f32x2{e0[0], e0[1]} + bev[0]) * m2;
+        E[sl][1] = irr_relu6x2(f32x2{e0[2], e0[3]} + bev[1]) * m2;
+        E[sl][2] = irr_relu6x2(f32x2{e1[0], e1[1]} + bev[2]) * m2;
+        E[sl][3] = irr_relu6x2(f32x2{e1[2], e1[3]} + bev[3]) * m2;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          L[slot][j] = f32x2{irr_left(E[i][j][0]), irr_left(E[i][j][1])};
-          Rt[slot][j] = f32x2{irr_right(E[i][j][0]), irr_right(E[i][j][1])};
+          L[sl][j] = f32x2{irr_left(E[sl][j][0]), irr_left(E[sl][j][1])};
+          Rt[sl][j] = f32x2{irr_right(E[sl][j][0]), irr_right(E[sl][j][1])};
         }
       };
-      shift_row(0, 0);
-      shift_row(1, 1);
+      expand(0);
+      expand(1);
+      expand(2);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        shift_row(r + 2, (r + 2) % 3);
+        if (r + 3 < R + 2) expand(r + 3);
         f32x2 d[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) d[j] = bdv[j];
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
-          const int slot = (r + ky) % 3;
+          const int sl = (r + ky) & 3;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            d[j] = __builtin_elementwise_fma(L[slot][j], wdw[3 * ky][j], d[j]);
-            d[j] = __builtin_elementwise_fma(E[r + ky][j], wdw[3 * ky + 1][j], d[j]);
-            d[j] = __builtin_elementwise_fma(Rt[slot][j], wdw[3 * ky + 2][j], d[j]);
+            d[j] = __builtin_elementwise_fma(L[sl][j], wdw[3 * ky][j], d[j]);
+            d[j] = __builtin_elementwise_fma(E[sl][j], wdw[3 * ky + 1][j], d[j]);
+            d[j] = __builtin_elementwise_fma(Rt[sl][j], wdw[3 * ky + 2][j], d[j]);
           }
         }
         float dv[8];
@@ -233,6 +234,14 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
         irr_split8(dv, dh, dm, dl);
 #pragma unroll
         for (int o = 0; o < NTO; ++o) acc[r][o] = irr_mfma(wph[o], wpm[o], wpl[o], dh, dm, dl, acc[r][o]);
+        if constexpr (IRR_SCHED) {
+          // interleave: one MFMA, then a few VALU (the depthwise / split of this row)
+#pragma unroll
+          for (int k = 0; k < 12 + 6 * NTO; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+          }
+        }
       }
     }
 
@@ -274,7 +283,7 @@ int irr_rows(int H) {
   return H >= 56 ? 7 : 4;
 }
 
-template <int R, int NTO>
+template <int R, int NTO, bool SCHED>
 void irr_launch(const IrParams& p, hipStream_t s) {
   constexpr int WPB = 4;  // one wave per SIMD: the strip's rows, accumulators and inputs need ~300 VGPRs
   const size_t lds = irr_lds_bytes(p.hid_pad, NTO);
@@ -287,7 +296,7 @@ void irr_launch(const IrParams& p, hipStream_t s) {
   const long strips = (long)p.B * ((p.Wo + 13) / 14) * ((p.Ho + R - 1) / R);
   const long wgs = (strips + WPB - 1) / WPB;
   const long grid = wgs < cus ? wgs : cus;  // persistent: one workgroup per CU walks the strips
-  hipLaunchKernelGGL((ir_reg_x3_kernel<R, NTO, WPB>), dim3((unsigned)grid), dim3(WPB * 64), lds, s, p);
+  hipLaunchKernelGGL((ir_reg_x3_kernel<R, NTO, WPB, SCHED>), dim3((unsigned)grid), dim3(WPB * 64), lds, s, p);
 }
 
 int g_irr_on = -1;  // -1: ARENA_IR_REG (default on)
@@ -315,25 +324,34 @@ bool ir_reg_x3(const IrParams& p, hipStream_t s) {
     throw std::runtime_error("ir_reg_x3: unsupported geometry");
   if (p.B <= 0) return true;
   const int R = irr_rows(p.H);
-  if (R == 7 && p.oup_pad == 32) irr_launch<7, 2>(p, s);
-  else if (R == 7) irr_launch<7, 1>(p, s);
-  else if (p.oup_pad == 32) irr_launch<4, 2>(p, s);
-  else irr_launch<4, 1>(p, s);
-  return true;
+  static const bool sched = [] {
+    const char* e = std::getenv("ARENA_IR_REG_SCHED");  // A/B: MFMA / VALU interleave hints (default on)
+    return e == nullptr || std::string(e) != "0";
+  }();
+#define IRR_GO(R_, NTO_)                                   \
+  if (R == R_ && p.oup_pad == NTO_ * 16) {                 \
+    if (sched) irr_launch<R_, NTO_, true>(p, s);           \
+    else irr_launch<R_, NTO_, false>(p, s);                \
+    return true;                                           \
+  }
+  IRR_GO(7, 2)
+  IRR_GO(7, 1)
+  IRR_GO(4, 2)
+  IRR_GO(4, 1)
+#undef IRR_GO
+  return false;
 }
 
 void set_ir_reg(int v) { g_irr_on = v < 0 ? -1 : (v ? 1 : 0); }
 
 void ir_reg_x3_prepare() {
   const int bytes = 160 * 1024;
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_reg_x3_kernel<7, 2, 4>,
+#define IRR_ATTR(R_, NTO_, SC_)                                                               \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_reg_x3_kernel<R_, NTO_, 4, SC_>,         \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_reg_x3_kernel<7, 1, 4>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_reg_x3_kernel<4, 2, 4>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_reg_x3_kernel<4, 1, 4>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  IRR_ATTR(7, 2, true) IRR_ATTR(7, 1, true) IRR_ATTR(4, 2, true) IRR_ATTR(4, 1, true)
+  IRR_ATTR(7, 2, false) IRR_ATTR(7, 1, false) IRR_ATTR(4, 2, false) IRR_ATTR(4, 1, false)
+#undef IRR_ATTR
 }
 
 }  // namespace arena

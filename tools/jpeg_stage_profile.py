@@ -49,7 +49,10 @@ def main(argv=None) -> int:
         n = r["Kernel_Name"]
         if "jpeg" not in n:
             continue
-        short = n.replace("void ", "").replace("arena::", "").split("(")[0]
+        import re
+
+        m = re.search(r"(jpeg_\w+)", n)
+        short = m.group(1) if m else n
         names.add(short)
         per[batch_of(int(r["Start_Timestamp"]))][short] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
     copies = defaultdict(lambda: [0, 0.0, 0])
