@@ -1062,6 +1062,7 @@ PYBIND11_MODULE(_C, m) {
              c.jpeg_device = get<bool>(cfg, "jpeg_device", c.jpeg_device);
              c.max_image_pixels = get<int64_t>(cfg, "max_image_pixels", c.max_image_pixels);
              c.decode_buffer_cap = get<int64_t>(cfg, "decode_buffer_cap", c.decode_buffer_cap);
+             c.kserve_model = get<std::string>(cfg, "kserve_model", c.kserve_model);
              // decoded uploads live in pinned memory when a GPU is present (the executor DMAs from them)
              int ndev = 0;
              const bool gpu = hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0;
@@ -1162,4 +1163,27 @@ PYBIND11_MODULE(_C, m) {
         py::gil_scoped_release nogil;
         f.stop();
       });
+  // native gateway: /predict forwarded to a model server's KServe endpoint (FrontConfig upstream_*)
+  m.def(
+      "http_proxy_front",
+      [](std::vector<std::string> labels, const py::dict& cfg) {
+        FrontConfig c;
+        c.host = get<std::string>(cfg, "host", c.host);
+        c.port = get<int>(cfg, "port", c.port);
+        c.io_threads = get<int>(cfg, "io_threads", c.io_threads);
+        c.reuse_port = get<bool>(cfg, "reuse_port", c.reuse_port);
+        c.softmax_confidence = get<bool>(cfg, "softmax_confidence", c.softmax_confidence);
+        c.max_body = get<int64_t>(cfg, "max_body", c.max_body);
+        c.replica_tag = get<std::string>(cfg, "replica_tag", c.replica_tag);
+        c.idle_timeout_ms = get<int64_t>(cfg, "idle_timeout_ms", c.idle_timeout_ms);
+        c.read_timeout_ms = get<int64_t>(cfg, "read_timeout_ms", c.read_timeout_ms);
+        c.upstream_host = get<std::string>(cfg, "upstream_host", c.upstream_host);
+        c.upstream_port = get<int>(cfg, "upstream_port", 0);
+        c.upstream_model = get<std::string>(cfg, "upstream_model", c.upstream_model);
+        c.upstream_conns = get<int>(cfg, "upstream_conns", c.upstream_conns);
+        if (c.upstream_port <= 0) throw std::runtime_error("http_proxy_front: upstream_port required");
+        py::gil_scoped_release nogil;
+        return new HttpFrontEnd(nullptr, DecodeChannel{}, std::move(labels), c);
+      },
+      py::return_value_policy::take_ownership, py::arg("labels"), py::arg("cfg"));
 }

@@ -189,10 +189,17 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
       // its project (12 MFMAs), so matrix and vector work of one wave overlap.  E and its left / right
       // neighbours live in a rolling window of four rows.
       f32x2 E[4][4], L[4][4], Rt[4][4];
+      const int dbg = p.dbg;
       auto expand = [&](int i) {
         const int sl = i & 3;
-        const f32x4 e0 = irr_mfma(weh[0], wem[0], wel[0], xh[i], xm[i], xl[i], f32x4{0.f, 0.f, 0.f, 0.f});
-        const f32x4 e1 = irr_mfma(weh[1], wem[1], wel[1], xh[i], xm[i], xl[i], f32x4{0.f, 0.f, 0.f, 0.f});
+        f32x4 e0, e1;
+        if (dbg & 1) {  // diagnostic: no expand MFMA
+          e0 = f32x4{(float)xh[i][0], (float)xm[i][1], (float)xl[i][2], 0.f};
+          e1 = e0;
+        } else {
+          e0 = irr_mfma(weh[0], wem[0], wel[0], xh[i], xm[i], xl[i], f32x4{0.f, 0.f, 0.f, 0.f});
+          e1 = irr_mfma(weh[1], wem[1], wel[1], xh[i], xm[i], xl[i], f32x4{0.f, 0.f, 0.f, 0.f});
+        }
         const f32x2 m2 = f32x2{inside[i], inside[i]};
         E[sl][0] = irr_relu6x2(f32x2{e0[0], e0[1]} + bev[0]) * m2;
         E[sl][1] = irr_relu6x2(f32x2{e0[2], e0[3]} + bev[1]) * m2;
@@ -213,6 +220,10 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
         f32x2 d[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) d[j] = bdv[j];
+        if (dbg & 2) {  // diagnostic: no depthwise (the centre tap only)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d[j] = E[(r + 1) & 3][j] + bdv[j];
+        } else
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
           const int sl = (r + ky) & 3;
@@ -232,8 +243,13 @@ __global__ __launch_bounds__(WPB * 64) void ir_reg_x3_kernel(const IrParams p) {
         }
         bf16x8 dh, dm, dl;
         irr_split8(dv, dh, dm, dl);
+        if (dbg & 4) {  // diagnostic: no project MFMA
 #pragma unroll
-        for (int o = 0; o < NTO; ++o) acc[r][o] = irr_mfma(wph[o], wpm[o], wpl[o], dh, dm, dl, acc[r][o]);
+          for (int o = 0; o < NTO; ++o) acc[r][o] += f32x4{(float)dh[o], (float)dm[o], (float)dl[o], 0.f};
+        } else {
+#pragma unroll
+          for (int o = 0; o < NTO; ++o) acc[r][o] = irr_mfma(wph[o], wpm[o], wpl[o], dh, dm, dl, acc[r][o]);
+        }
         if constexpr (IRR_SCHED) {
           // interleave: one MFMA, then a few VALU (the depthwise / split of this row)
 #pragma unroll
@@ -284,7 +300,13 @@ int irr_rows(int H) {
 }
 
 template <int R, int NTO, bool SCHED>
-void irr_launch(const IrParams& p, hipStream_t s) {
+void irr_launch(const IrParams& p0, hipStream_t s) {
+  static const int dbg_env = [] {
+    const char* e = std::getenv("ARENA_IR_REG_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
+  IrParams p = p0;
+  p.dbg = dbg_env;
   constexpr int WPB = 4;  // one wave per SIMD: the strip's rows, accumulators and inputs need ~300 VGPRs
   const size_t lds = irr_lds_bytes(p.hid_pad, NTO);
   static int cus = 0;

@@ -146,6 +146,7 @@ struct IrParams {
   // hidden channels are split over y_parts workgroups per band, each writing its partial output at channel
   // offset j * oup (partial 0 carries the project bias and the residual).
   int x_parts, y_parts;
+  int dbg = 0;  // diagnostic phase mask of ir_reg_x3 (ARENA_IR_REG_DBG): 1 no expand MFMA, 2 no depthwise, 4 no project MFMA
   // fp32 classifier front end (stem = 1, t = 1 blocks, ir_f32.hip): X is not read from memory but built per
   // tile from the batch's uint8 images: crop gather + ImageNet normalisation (crop_gather_s2d semantics) into a
   // space-to-depth tile in LDS, then the 2x2 stem conv over it (+ bias, ReLU6; zero outside the H x W map).

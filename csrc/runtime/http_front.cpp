@@ -98,6 +98,62 @@ std::string uuid4() {
   return s;
 }
 
+// The reference /predict body (architectures/monolithic/app/models.py PredictResponse): request id, detections
+// with their top-1 classification (raw logit, or the softmax probability with ARENA_CONFIDENCE=softmax), timing.
+std::string predict_json(const RequestResult& r, const std::vector<std::string>& labels, bool softmax,
+                         double queue_ms, double gpu_ms, double det_ms, double cls_ms, double inference_ms,
+                         double decode_ms, double total_ms) {
+  std::string s;
+  s.reserve(512 + 256 * r.det.size());
+  s += "{\"request_id\":";
+  json_escape(s, uuid4());
+  s += ",\"detections\":[";
+  for (size_t i = 0; i < r.det.size(); ++i) {
+    const Detection& d = r.det[i];
+    if (i) s += ',';
+    s += "{\"detection\":{\"x1\":";
+    json_num(s, d.x1);
+    s += ",\"y1\":";
+    json_num(s, d.y1);
+    s += ",\"x2\":";
+    json_num(s, d.x2);
+    s += ",\"y2\":";
+    json_num(s, d.y2);
+    s += ",\"confidence\":";
+    json_num(s, d.conf);
+    s += ",\"class_id\":" + std::to_string(d.cls) + "},\"classification\":{\"class_id\":";
+    int cid = -1;
+    double conf = 0.0;
+    if (i < r.topk.size()) {
+      cid = r.topk[i].idx[0];
+      conf = softmax ? r.topk[i].prob[0] : r.topk[i].logit[0];
+    }
+    s += std::to_string(cid) + ",\"class_name\":";
+    json_escape(s, (cid >= 0 && cid < (int)labels.size()) ? labels[cid] : std::string());
+    s += ",\"confidence\":";
+    json_num(s, conf);
+    s += "}}";
+  }
+  s += "],\"timing\":{\"queue_ms\":";
+  json_num(s, queue_ms);
+  s += ",\"gpu_ms\":";
+  json_num(s, gpu_ms);
+  s += ",\"batch_size\":";
+  json_num(s, r.batch_size);
+  s += ",\"detection_ms\":";
+  json_num(s, det_ms);
+  s += ",\"classification_ms\":";
+  json_num(s, cls_ms);
+  s += ",\"inference_ms\":";
+  json_num(s, inference_ms);
+  s += ",\"decode_ms\":";
+  json_num(s, decode_ms);
+  s += ",\"total_ms\":";
+  json_num(s, total_ms);
+  s += "}}";
+  return s;
+}
+
 const char* reason(int code) {
   switch (code) {
     case 200: return "OK";
@@ -205,6 +261,7 @@ struct HttpFrontEnd::Conn {
 struct HttpFrontEnd::Pending {
   std::shared_ptr<Conn> conn;
   int worker = 0;
+  int kind = 0;  // 0 /predict, 1 KServe infer
   Clock::time_point t0, t_dec;
 };
 
@@ -218,6 +275,7 @@ struct HttpFrontEnd::DecodeTask {
   Clock::time_point t0, t_queued;
   std::string body;  // the request body (moved in); the upload is body[off, off + len)
   size_t off = 0, len = 0;
+  int kind = 0;      // 0 /predict, 1 KServe infer
 };
 
 namespace {
@@ -232,7 +290,13 @@ struct NativeUpload {
 HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vector<std::string> labels,
                            FrontConfig cfg)
     : batcher_(batcher), dc_(std::move(dc)), labels_(std::move(labels)), cfg_(std::move(cfg)) {
-  if (!cfg_.handler_mode) {
+  const bool proxy = cfg_.upstream_port > 0;
+  if (proxy) {
+    if (cfg_.handler_mode) throw std::runtime_error("HttpFrontEnd: proxy mode and handler mode exclude each other");
+    proxy_.reset(new KServeProxy(cfg_.upstream_host, cfg_.upstream_port, cfg_.upstream_model, cfg_.upstream_conns));
+    cfg_.decode_threads = 0;
+  }
+  if (!cfg_.handler_mode && !proxy) {
     if (batcher_ == nullptr) throw std::runtime_error("HttpFrontEnd: no batcher");
     has_pool_ = dc_.shm != nullptr;
     if (has_pool_ || cfg_.decode_threads <= 0) {
@@ -286,7 +350,7 @@ HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vecto
   }
   for (int i = 0; i < n; ++i) io_threads_.emplace_back([this, i] { io_loop(i); });
   if (!cfg_.handler_mode && has_pool_) collector_ = std::thread([this] { collector_loop(); });
-  if (!cfg_.handler_mode)
+  if (!cfg_.handler_mode && !proxy)
     for (int i = 0; i < cfg_.decode_threads; ++i) decode_threads_.emplace_back([this, i] { decode_loop(i); });
 }
 
@@ -294,6 +358,7 @@ HttpFrontEnd::~HttpFrontEnd() { stop(); }
 
 void HttpFrontEnd::stop() {
   if (stop_.exchange(true)) return;
+  if (proxy_) proxy_->stop();  // answers what it still holds; no upstream request outlives the front end
   uint64_t one = 1;
   if (write(stop_efd_, &one, sizeof one) < 0) { /* the flag alone stops the loops on their next wakeup */ }
   if (cfg_.handler_mode) {
@@ -683,7 +748,7 @@ bool HttpFrontEnd::parse_one_impl(const std::shared_ptr<Conn>& c) {
   const std::string version = line.substr(s2 + 1);
   const size_t q = path.find('?');
   if (q != std::string::npos) path = path.substr(0, q);
-  int64_t clen = -1;
+  int64_t clen = -1, ihcl = -1;
   bool chunked = false, close_req = version == "HTTP/1.0";
   std::string ctype;
   size_t p = le + 2;
@@ -698,6 +763,7 @@ bool HttpFrontEnd::parse_one_impl(const std::shared_ptr<Conn>& c) {
       if (name == "content-length") clen = std::atoll(val.c_str());
       else if (name == "transfer-encoding") chunked = lower(val).find("chunked") != std::string::npos;
       else if (name == "content-type") ctype = val;
+      else if (name == "inference-header-content-length") ihcl = std::atoll(val.c_str());
       else if (name == "connection") {
         const std::string v = lower(val);
         if (v.find("close") != std::string::npos) close_req = true;
@@ -760,12 +826,14 @@ bool HttpFrontEnd::parse_one_impl(const std::shared_ptr<Conn>& c) {
     c->busy = true;
     c->close_after = close_req;
   }
-  dispatch(c, method, path, ctype, std::move(body));
+  dispatch(c, method, path, ctype, std::move(body), ihcl);
   return true;
 }
 
 void HttpFrontEnd::dispatch(const std::shared_ptr<Conn>& c, const std::string& method, const std::string& path,
-                            const std::string& ctype, std::string&& body) {
+                            const std::string& ctype, std::string&& body, int64_t ihcl) {
+  if (!cfg_.kserve_model.empty() && path.rfind("/v2", 0) == 0 && kserve_route(c, method, path, std::move(body), ihcl))
+    return;
   if (path == "/predict") {
     if (method != "POST") {
       respond(c, 405, "application/json", detail_json("Method Not Allowed"));
@@ -798,7 +866,7 @@ void HttpFrontEnd::dispatch(const std::shared_ptr<Conn>& c, const std::string& m
 }
 
 void HttpFrontEnd::respond(const std::shared_ptr<Conn>& c, int code, const std::string& ctype,
-                           const std::string& body, bool) {
+                           const std::string& body, bool, const std::string& extra_headers) {
   if (c->local) {
     c->local(code, body);
     return;
@@ -815,6 +883,7 @@ void HttpFrontEnd::respond(const std::shared_ptr<Conn>& c, int code, const std::
            reason(code), ctype.c_str(), body.size(), close_after ? "Connection: close\r\n" : "");
   r += head;
   if (!cfg_.replica_tag.empty()) r += "x-arena-replica: " + cfg_.replica_tag + "\r\n";
+  r += extra_headers;
   r += "\r\n";
   r += body;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -873,6 +942,12 @@ void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, c
     return;
   }
   t_predict_dispatched = true;
+  if (proxy_) return proxy_predict(c, t0, body.substr(off, len));
+  start_upload(c, t0, std::move(body), off, len, 0);
+}
+
+void HttpFrontEnd::start_upload(const std::shared_ptr<Conn>& c, Clock_tp t0, std::string&& body, size_t off,
+                                size_t len, int kind) {
   if (cfg_.decode_threads > 0) {
     auto t = std::make_unique<DecodeTask>();
     t->conn = c;
@@ -881,6 +956,7 @@ void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, c
     t->body = std::move(body);
     t->off = off;
     t->len = len;
+    t->kind = kind;
     {
       std::lock_guard<std::mutex> lk(dq_mu_);
       dq_.push_back(std::move(t));
@@ -888,7 +964,91 @@ void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, c
     dq_cv_.notify_one();
     return;
   }
-  pool_submit(c, t0, body, off, len);
+  pool_submit(c, t0, body, off, len, kind);
+}
+
+bool HttpFrontEnd::kserve_route(const std::shared_ptr<Conn>& c, const std::string& method, const std::string& path,
+                                std::string&& body, int64_t ihcl) {
+  const std::string& m = cfg_.kserve_model;
+  const std::string mpre = "/v2/models/" + m;
+  auto err_json = [](const std::string& msg) {
+    std::string s = "{\"error\":";
+    json_escape(s, msg);
+    return s + "}";
+  };
+  if (method == "GET") {
+    if (path == "/v2/health/live") {
+      respond(c, 200, "application/json", "{\"live\":true}");
+      return true;
+    }
+    if (path == "/v2/health/ready" || path == mpre + "/ready" || path == mpre + "/versions/1/ready") {
+      const bool ok = healthy_.load();
+      respond(c, ok ? 200 : 503, "application/json", ok ? "{\"ready\":true}" : "{\"ready\":false}");
+      return true;
+    }
+    if (path == "/v2") {
+      respond(c, 200, "application/json",
+              "{\"name\":\"arena-modelserver-native\",\"version\":\"2.0.0\",\"extensions\":[\"binary_tensor_data\"]}");
+      return true;
+    }
+    if (path == mpre || path == mpre + "/versions/1") {
+      respond(c, 200, "application/json", kserve_model_metadata(m));
+      return true;
+    }
+    return false;
+  }
+  if (method != "POST") return false;
+  const bool infer = path == mpre + "/infer" || path == mpre + "/versions/1/infer";
+  if (!infer) {
+    if (path.size() > 6 && path.compare(path.size() - 6, 6, "/infer") == 0) {
+      respond(c, 404, "application/json", err_json("Request for unknown model: '" + path + "' is not found"));
+      return true;
+    }
+    return false;
+  }
+  const auto t0 = Clock::now();
+  size_t off = 0, len = 0;
+  std::string err;
+  if (!healthy_.load()) {
+    fail_request(c, 503, "Server not ready", 1);
+    return true;
+  }
+  if (!kserve_parse_bytes_input(body, ihcl, "IMAGE_BYTES", off, len, err) || len == 0) {
+    fail_request(c, 400, err.empty() ? "empty IMAGE_BYTES" : err, 1);
+    return true;
+  }
+  t_predict_dispatched = true;
+  start_upload(c, t0, std::move(body), off, len, 1);
+  return true;
+}
+
+void HttpFrontEnd::proxy_predict(const std::shared_ptr<Conn>& c, Clock_tp t0, std::string upload) {
+  const auto t_inf = Clock::now();
+  {
+    std::lock_guard<std::mutex> lk(cb_mu_);
+    ++cb_outstanding_;
+  }
+  proxy_->submit(std::move(upload), [this, c, t0, t_inf](ProxyReply&& rep) {
+    struct Done {
+      HttpFrontEnd* f;
+      ~Done() { f->callback_done(); }
+    } done{this};
+    if (rep.status != 200 || !rep.error.empty()) {
+      const int code = rep.status == 0 ? 502 : rep.status == 200 ? 502 : rep.status;
+      fail_request(c, code, "model server: " + (rep.error.empty() ? std::string("error") : rep.error));
+      return;
+    }
+    const double cj = thread_cpu_ms();
+    const RequestResult& r = rep.result;
+    const double inference_ms = ms_since(t_inf);
+    const double queue_ms = r.queue_us / 1e3, gpu_ms = r.compute_us / 1e3;
+    const double det_ms = r.det_ms >= 0 ? r.det_ms : 0.0, cls_ms = r.cls_ms >= 0 ? r.cls_ms : 0.0;
+    const double total_ms = ms_since(t0);
+    const std::string s = predict_json(r, labels_, cfg_.softmax_confidence, queue_ms, gpu_ms, det_ms, cls_ms,
+                                       inference_ms, 0.0, total_ms);
+    record_ok(total_ms, 0.0, queue_ms, gpu_ms, det_ms, cls_ms, (int64_t)r.det.size(), thread_cpu_ms() - cj);
+    respond(c, 200, "application/json", s);
+  });
 }
 
 void HttpFrontEnd::submit_local(std::string upload, LocalDone done) {
@@ -980,7 +1140,7 @@ std::vector<LoadGenRecord> LocalLoadGen::records(int64_t from, int64_t to) {
   return std::vector<LoadGenRecord>(recs_.begin() + from, recs_.begin() + to);
 }
 
-void HttpFrontEnd::fail_request(const std::shared_ptr<Conn>& c, int code, const std::string& msg) {
+void HttpFrontEnd::fail_request(const std::shared_ptr<Conn>& c, int code, const std::string& msg, int kind) {
   {
     std::lock_guard<std::mutex> sl(stats_mu_);
     ++stats_.requests;
@@ -989,12 +1149,19 @@ void HttpFrontEnd::fail_request(const std::shared_ptr<Conn>& c, int code, const 
     else if (code >= 500) ++stats_.errors;
     else ++stats_.bad_request;
   }
+  if (kind == 1) {  // KServe error body
+    std::string e = "{\"error\":";
+    json_escape(e, msg);
+    respond(c, code, "application/json", e + "}");
+    return;
+  }
   respond(c, code, "application/json", detail_json(msg));
 }
 
 void HttpFrontEnd::pool_submit(const std::shared_ptr<Conn>& c, Clock_tp t0, const std::string& body, size_t off,
-                               size_t len) {
-  if (!has_pool_) return fail_request(c, 500, "Failed to decode image: format not supported by the native decoder");
+                               size_t len, int kind) {
+  if (!has_pool_)
+    return fail_request(c, 500, "Failed to decode image: format not supported by the native decoder", kind);
   int slot;
   {
     std::lock_guard<std::mutex> lk(slot_mu_);
@@ -1004,9 +1171,10 @@ void HttpFrontEnd::pool_submit(const std::shared_ptr<Conn>& c, Clock_tp t0, cons
       free_slots_.pop_back();
     }
   }
-  if (slot < 0) return fail_request(c, 503, "decode pool is saturated");
+  if (slot < 0) return fail_request(c, 503, "decode pool is saturated", kind);
   auto pend = std::make_shared<Pending>();
   pend->conn = c;
+  pend->kind = kind;
   pend->t0 = t0;
   pend->t_dec = Clock::now();
   const uint64_t key = next_key_.fetch_add(1);
@@ -1046,7 +1214,7 @@ void HttpFrontEnd::pool_submit(const std::shared_ptr<Conn>& c, Clock_tp t0, cons
       pending_.erase(key);
     }
     release_slot(slot);
-    return fail_request(c, 503, "decode workers unavailable");
+    return fail_request(c, 503, "decode workers unavailable", kind);
   }
   {
     std::lock_guard<std::mutex> sl(stats_mu_);
@@ -1077,9 +1245,9 @@ void HttpFrontEnd::native_decode(DecodeTask& t) {
   auto up = std::make_shared<NativeUpload>();
   std::string err;
   JpegStatus st = jpeg_parse(data, t.len, up->info, err, cfg_.max_image_pixels);
-  if (st == JpegStatus::Unsupported) return pool_submit(t.conn, t.t0, t.body, t.off, t.len);  // PIL fallback
+  if (st == JpegStatus::Unsupported) return pool_submit(t.conn, t.t0, t.body, t.off, t.len, t.kind);  // PIL fallback
   if (st == JpegStatus::Corrupt)
-    return fail_request(t.conn, err.find("image too large") != std::string::npos ? 413 : 500, err);
+    return fail_request(t.conn, err.find("image too large") != std::string::npos ? 413 : 500, err, t.kind);
   const JpegInfo& ji = up->info;
   InputImage in{nullptr, ji.height, ji.width};
   // Device reconstruction needs the coefficients, the sample planes and the RGB frame in one batch's staging
@@ -1107,7 +1275,7 @@ void HttpFrontEnd::native_decode(DecodeTask& t) {
       up->buf = host_pool_->get(rgb_bytes);
       if (!up->buf) {  // beyond the largest size class or the pool's cap: a buffer of its own
         uint8_t* raw = static_cast<uint8_t*>(std::malloc(rgb_bytes));
-        if (raw == nullptr) return fail_request(t.conn, 503, "decode buffers exhausted");
+        if (raw == nullptr) return fail_request(t.conn, 503, "decode buffers exhausted", t.kind);
         up->buf = std::shared_ptr<uint8_t>(raw, [](uint8_t* q) { std::free(q); });
       }
       jpeg_coefs_to_rgb(ji, coef.data(), up->buf.get());
@@ -1115,7 +1283,7 @@ void HttpFrontEnd::native_decode(DecodeTask& t) {
     }
     if (coef.capacity() > ((size_t)16 << 20)) std::vector<int16_t>().swap(coef);  // do not pin a huge frame's
   }
-  if (st != JpegStatus::Ok) return fail_request(t.conn, 500, err);
+  if (st != JpegStatus::Ok) return fail_request(t.conn, 500, err, t.kind);
   const double decode_ms = ms_since(t.t_queued);
   {
     std::lock_guard<std::mutex> sl(stats_mu_);
@@ -1126,10 +1294,10 @@ void HttpFrontEnd::native_decode(DecodeTask& t) {
     std::lock_guard<std::mutex> lk(cb_mu_);
     ++cb_outstanding_;
   }
-  const int64_t id = batcher_->enqueue_input(in, up, make_result_cb(t.conn, t.t0, Clock::now(), decode_ms));
+  const int64_t id = batcher_->enqueue_input(in, up, make_result_cb(t.conn, t.t0, Clock::now(), decode_ms, t.kind));
   if (id < 0) callback_done();  // rejected: the batcher never calls back
-  if (id == -1) return fail_request(t.conn, 503, "request queue is full");
-  if (id == -2) return fail_request(t.conn, 413, "image exceeds the staging capacity of one batch");
+  if (id == -1) return fail_request(t.conn, 503, "request queue is full", t.kind);
+  if (id == -2) return fail_request(t.conn, 413, "image exceeds the staging capacity of one batch", t.kind);
 }
 
 void HttpFrontEnd::collector_loop() {
@@ -1148,106 +1316,64 @@ void HttpFrontEnd::collector_loop() {
   }
 }
 
+void HttpFrontEnd::record_ok(double total_ms, double decode_ms, double queue_ms, double gpu_ms, double det_ms,
+                             double cls_ms, int64_t n_det, double json_cpu_ms) {
+  std::lock_guard<std::mutex> sl(stats_mu_);
+  ++stats_.requests;
+  ++stats_.ok;
+  stats_.cpu_json_ms += json_cpu_ms;
+  stats_.detections += n_det;
+  stats_.sum_total_ms += total_ms;
+  stats_.sum_decode_ms += decode_ms;
+  stats_.sum_queue_ms += queue_ms;
+  stats_.sum_gpu_ms += gpu_ms;
+  size_t b = 0;
+  while (b < kLatencyBucketsMs.size() && total_ms > kLatencyBucketsMs[b]) ++b;
+  ++stats_.latency_hist[b];
+  const double stage_ms[] = {decode_ms, queue_ms, gpu_ms, det_ms, cls_ms, total_ms};
+  for (size_t k = 0; k < kStages.size(); ++k) {
+    size_t bb = 0;
+    while (bb < kLatencyBucketsMs.size() && stage_ms[k] > kLatencyBucketsMs[bb]) ++bb;
+    ++stats_.stage_hist[k][bb];
+    stats_.stage_sum_ms[k] += stage_ms[k];
+  }
+}
+
 ResultCallback HttpFrontEnd::make_result_cb(const std::shared_ptr<Conn>& conn, Clock_tp t0, Clock_tp t_inf,
-                                            double decode_ms) {
-  const bool softmax = cfg_.softmax_confidence;
-  const std::vector<std::string>* labels = &labels_;
-  FrontStats* stats = &stats_;
-  std::mutex* smu = &stats_mu_;
+                                            double decode_ms, int kind) {
   HttpFrontEnd* self = this;
-  return [self, conn, t0, t_inf, decode_ms, softmax, labels, stats, smu](RequestResult&& r) {
+  return [self, conn, t0, t_inf, decode_ms, kind](RequestResult&& r) {
     struct Done {
       HttpFrontEnd* f;
       ~Done() { f->callback_done(); }
     } done{self};
     if (!r.error.empty()) {
-      {
-        std::lock_guard<std::mutex> sl(*smu);
-        ++stats->requests;
-        ++stats->errors;
-      }
-      self->respond(conn, 500, "application/json", detail_json(r.error));
+      self->fail_request(conn, 500, r.error, kind);
       return;
     }
     const double queue_ms = r.queue_us / 1e3, gpu_ms = r.compute_us / 1e3;
     const double inference_ms = ms_since(t_inf);
-    const double cj = thread_cpu_ms();
-    std::string s;
-    s.reserve(512 + 256 * r.det.size());
-    s += "{\"request_id\":";
-    json_escape(s, uuid4());
-    s += ",\"detections\":[";
-    for (size_t i = 0; i < r.det.size(); ++i) {
-      const Detection& d = r.det[i];
-      if (i) s += ',';
-      s += "{\"detection\":{\"x1\":";
-      json_num(s, d.x1);
-      s += ",\"y1\":";
-      json_num(s, d.y1);
-      s += ",\"x2\":";
-      json_num(s, d.x2);
-      s += ",\"y2\":";
-      json_num(s, d.y2);
-      s += ",\"confidence\":";
-      json_num(s, d.conf);
-      s += ",\"class_id\":" + std::to_string(d.cls) + "},\"classification\":{\"class_id\":";
-      int cid = -1;
-      double conf = 0.0;
-      if (i < r.topk.size()) {
-        cid = r.topk[i].idx[0];
-        conf = softmax ? r.topk[i].prob[0] : r.topk[i].logit[0];
-      }
-      s += std::to_string(cid) + ",\"class_name\":";
-      json_escape(s, (cid >= 0 && cid < (int)labels->size()) ? (*labels)[cid] : std::string());
-      s += ",\"confidence\":";
-      json_num(s, conf);
-      s += "}}";
-    }
-    const double total_ms = ms_since(t0);
-    s += "],\"timing\":{\"queue_ms\":";
-    json_num(s, queue_ms);
-    s += ",\"gpu_ms\":";
-    json_num(s, gpu_ms);
-    s += ",\"batch_size\":";
-    json_num(s, r.batch_size);
     // device time of the detection network (+ decode / NMS / crop plan) and of the classification network
     // (crop gather -> top-5) of this request's batch, from the program's wall-clock stamps (OP_STAMP); with
     // the batch's H2D / D2H they make up gpu_ms (reference timing keys, architectures/monolithic/app/
     // inference.py:180,224-225; there the per-request CPU time of each network)
     const double det_ms = r.det_ms >= 0 ? r.det_ms : 0.0, cls_ms = r.cls_ms >= 0 ? r.cls_ms : 0.0;
-    s += ",\"detection_ms\":";
-    json_num(s, det_ms);
-    s += ",\"classification_ms\":";
-    json_num(s, cls_ms);
-    s += ",\"inference_ms\":";
-    json_num(s, inference_ms);
-    s += ",\"decode_ms\":";
-    json_num(s, decode_ms);
-    s += ",\"total_ms\":";
-    json_num(s, total_ms);
-    s += "}}";
-    const double json_cpu = thread_cpu_ms() - cj;
-    {
-      std::lock_guard<std::mutex> sl(*smu);
-      ++stats->requests;
-      ++stats->ok;
-      stats->cpu_json_ms += json_cpu;
-      stats->detections += (int64_t)r.det.size();
-      stats->sum_total_ms += total_ms;
-      stats->sum_decode_ms += decode_ms;
-      stats->sum_queue_ms += queue_ms;
-      stats->sum_gpu_ms += gpu_ms;
-      size_t b = 0;
-      while (b < kLatencyBucketsMs.size() && total_ms > kLatencyBucketsMs[b]) ++b;
-      ++stats->latency_hist[b];
-      const double stage_ms[] = {decode_ms, queue_ms, gpu_ms, det_ms, cls_ms, total_ms};
-      for (size_t k = 0; k < kStages.size(); ++k) {
-        size_t bb = 0;
-        while (bb < kLatencyBucketsMs.size() && stage_ms[k] > kLatencyBucketsMs[bb]) ++bb;
-        ++stats->stage_hist[k][bb];
-        stats->stage_sum_ms[k] += stage_ms[k];
-      }
+    const double cj = thread_cpu_ms();
+    if (kind == 1) {  // KServe infer: the ensemble's output tensors (binary tensor extension)
+      int64_t ihcl = -1;
+      const std::string body = kserve_build_response(self->cfg_.kserve_model, "", r, true, &ihcl);
+      const double total_ms = ms_since(t0);
+      self->record_ok(total_ms, decode_ms, queue_ms, gpu_ms, det_ms, cls_ms, (int64_t)r.det.size(),
+                      thread_cpu_ms() - cj);
+      self->respond(conn, 200, "application/octet-stream", body, false,
+                    "Inference-Header-Content-Length: " + std::to_string(ihcl) + "\r\n");
+      return;
     }
+    const double total_ms = ms_since(t0);
+    const std::string s = predict_json(r, self->labels_, self->cfg_.softmax_confidence, queue_ms, gpu_ms, det_ms,
+                                       cls_ms, inference_ms, decode_ms, total_ms);
+    self->record_ok(total_ms, decode_ms, queue_ms, gpu_ms, det_ms, cls_ms, (int64_t)r.det.size(),
+                    thread_cpu_ms() - cj);
     self->respond(conn, 200, "application/json", s);
   };
 }
@@ -1293,6 +1419,12 @@ void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int statu
       else if (code == 503) ++stats_.unavailable;
       else ++stats_.errors;
     }
+    if (pend->kind == 1) {
+      std::string e = "{\"error\":";
+      json_escape(e, msg);
+      respond(conn, code, "application/json", e + "}");
+      return;
+    }
     respond(conn, code, "application/json", detail_json(msg));
   };
   if (status == 1) {
@@ -1306,7 +1438,7 @@ void HttpFrontEnd::finish_decode(uint64_t key, int slot, int h, int w, int statu
     return fail(500, "decode worker result lost");
   }
   const double decode_ms = ms_since(pend->t_dec);
-  ResultCallback cb = make_result_cb(conn, pend->t0, Clock::now(), decode_ms);
+  ResultCallback cb = make_result_cb(conn, pend->t0, Clock::now(), decode_ms, pend->kind);
   {
     std::lock_guard<std::mutex> lk(cb_mu_);
     ++cb_outstanding_;

@@ -55,6 +55,7 @@
 #include <vector>
 
 #include "batcher.h"
+#include "kserve.h"
 #include "host_pool.h"
 #include "http_loadgen.h"
 
@@ -97,6 +98,17 @@ struct FrontConfig {
   int64_t decode_buffer_cap = 2LL << 30;   // host buffers of decoded uploads in flight (HostBufferPool cap)
   HostBufferPool::AllocFn host_alloc;      // pinning allocator for those buffers (empty: plain memory)
   HostBufferPool::FreeFn host_free;
+  // KServe-v2 REST for this ensemble model (runtime/kserve.h; empty: off): POST /v2/models/<m>/infer with the
+  // binary tensor extension takes the /predict path and answers the ensemble's output tensors; GET /v2,
+  // /v2/health/{live,ready}, /v2/models/<m>[/ready] answer the protocol's metadata / health routes
+  std::string kserve_model;
+  // Native gateway ("proxy mode", upstream_port > 0): /predict uploads are forwarded to a model server's KServe
+  // endpoint over upstream_conns keep-alive connections and its output tensors answered as the reference JSON;
+  // no batcher or decoder in this process
+  std::string upstream_host = "127.0.0.1";
+  int upstream_port = 0;
+  std::string upstream_model = "arena_pipeline";
+  int upstream_conns = 64;
 };
 
 // One upload handed to the Python handler (handler mode).
@@ -196,23 +208,34 @@ class HttpFrontEnd {
   bool parse_one(const std::shared_ptr<Conn>& c);  // true: a full request was consumed
   bool parse_one_impl(const std::shared_ptr<Conn>& c);
   void dispatch(const std::shared_ptr<Conn>& c, const std::string& method, const std::string& path,
-                const std::string& ctype, std::string&& body);
+                const std::string& ctype, std::string&& body, int64_t ihcl = -1);
   void predict(const std::shared_ptr<Conn>& c, std::string&& body, const std::string& ctype);
+  bool kserve_route(const std::shared_ptr<Conn>& c, const std::string& method, const std::string& path,
+                    std::string&& body, int64_t ihcl);
+  void start_upload(const std::shared_ptr<Conn>& c, Clock_tp t0, std::string&& body, size_t off, size_t len,
+                    int kind);
+  void proxy_predict(const std::shared_ptr<Conn>& c, Clock_tp t0, std::string upload);
+  void record_ok(double total_ms, double decode_ms, double queue_ms, double gpu_ms, double det_ms, double cls_ms,
+                 int64_t n_det, double json_cpu_ms);
   void respond(const std::shared_ptr<Conn>& c, int code, const std::string& ctype, const std::string& body,
-               bool count_latency = false);
+               bool count_latency = false, const std::string& extra_headers = "");
   void close_conn(int ep, const std::shared_ptr<Conn>& c);
   void finish_decode(uint64_t key, int slot, int h, int w, int status, int64_t aux);
   struct DecodeTask;
   void decode_loop(int idx);
   void native_decode(DecodeTask& t);
   // hand an upload to the PIL decode pool (also the split decoder's fallback); answers the error itself
-  void pool_submit(const std::shared_ptr<Conn>& c, Clock_tp t0, const std::string& body, size_t off, size_t len);
-  ResultCallback make_result_cb(const std::shared_ptr<Conn>& c, Clock_tp t0, Clock_tp t_inf, double decode_ms);
-  void fail_request(const std::shared_ptr<Conn>& c, int code, const std::string& msg);
+  // kind: 0 = /predict (reference JSON), 1 = KServe infer (binary output tensors)
+  void pool_submit(const std::shared_ptr<Conn>& c, Clock_tp t0, const std::string& body, size_t off, size_t len,
+                   int kind = 0);
+  ResultCallback make_result_cb(const std::shared_ptr<Conn>& c, Clock_tp t0, Clock_tp t_inf, double decode_ms,
+                                int kind = 0);
+  void fail_request(const std::shared_ptr<Conn>& c, int code, const std::string& msg, int kind = 0);
   void release_slot(int slot);
   void callback_done();
 
   DynamicBatcher* batcher_;
+  std::unique_ptr<KServeProxy> proxy_;  // proxy mode (cfg_.upstream_port > 0)
   DecodeChannel dc_;
   std::vector<std::string> labels_;
   FrontConfig cfg_;

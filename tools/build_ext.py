@@ -62,6 +62,7 @@ SOURCES = [
     "runtime/trace.cpp",
     "runtime/jpeg_decode.cpp",
     "runtime/jpeg_ingest.cpp",
+    "runtime/kserve.cpp",
     "bindings_jpeg.cpp",
     "bindings.cpp",
 ]
