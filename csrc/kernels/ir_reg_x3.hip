@@ -24,6 +24,14 @@
 // One barrier per workgroup (after the weights are staged); the waves then walk their strips independently.
 // Halo cost: the expand runs on R + 2 rows of 16 pixels for R x 14 outputs.
 //
+// Measured (gfx950, 128 crops, rocprofv3; gpurun_out r5c-r5e, tools/bench_irreg.py): 56x56 hid 160 block 123-148
+// us, 28x28 hid 192 56-65 us, against the tiled kernel's 170 / 69 us inside the pipeline (ops 65 / 67-68) — no net
+// gain in the pipeline (193.6 us at 56x56, profiles r5b).  The limit is vector issue, not the matrix pipe: one wave
+// per SIMD (the strip needs ~440 registers, the overflow sits in AGPRs: ~775 v_accvgpr moves per hidden chunk) and
+// ~3000 VALU instructions per 192 MFMAs (the triple-bf16 split of D, the DPP shifts, the depthwise); with every
+// phase switched off (ARENA_IR_REG_DBG=7) the strip walk alone still takes 89 us.  Kept behind ARENA_IR_REG=1 (and
+// pinned by the fp64 tests) as the starting point of a lower-register variant; the tiled kernel stays the default.
+//
 // Weights (engine/planner.py, x3w): we bf16 [hid_pad][3][32] (inp_pad 32), wp bf16 [oup_pad][3][hid_pad],
 // wd fp32 [9][hid_pad], biases fp32.
 #include <cstdlib>
@@ -321,12 +329,12 @@ void irr_launch(const IrParams& p0, hipStream_t s) {
   hipLaunchKernelGGL((ir_reg_x3_kernel<R, NTO, WPB, SCHED>), dim3((unsigned)grid), dim3(WPB * 64), lds, s, p);
 }
 
-int g_irr_on = -1;  // -1: ARENA_IR_REG (default on)
+int g_irr_on = -1;  // -1: ARENA_IR_REG (default off: see the measurements in the header)
 
 bool irr_enabled() {
   if (g_irr_on < 0) {
     const char* e = std::getenv("ARENA_IR_REG");
-    g_irr_on = (e == nullptr || (std::string(e) != "0" && std::string(e) != "off" && std::string(e) != "false")) ? 1 : 0;
+    g_irr_on = (e != nullptr && (std::string(e) == "1" || std::string(e) == "on" || std::string(e) == "true")) ? 1 : 0;
   }
   return g_irr_on == 1;
 }

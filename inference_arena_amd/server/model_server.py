@@ -304,6 +304,30 @@ def create_metrics_app(server: ModelServer) -> FastAPI:
 
 
 # ----------------------------------------------------------------------------- main
+def start_native_kserve(server: ModelServer, host: str, port: int, model: str = "arena_pipeline"):
+    """The ensemble's hot path without Python: a native HTTP front end (csrc/runtime/http_front.h with
+    ``kserve_model``) on ``port`` serving KServe-v2 REST infer requests for ``model`` (binary tensor extension)
+    straight into the ensemble's native dynamic batcher, with the split JPEG decoder on C++ threads — the endpoint
+    the native gateway (server/native_gateway.py) forwards to.  None when off (port 0), on CPU, or when the model
+    is not a GPU-batched pipeline."""
+    if port <= 0 or server.device != "gpu":
+        return None
+    m = server.models.get(model)
+    backend = getattr(m, "backend", None)
+    batcher = getattr(getattr(backend, "batcher", None), "_b", None)
+    if batcher is None:
+        log.warning(f"native KServe endpoint: model {model} has no native batcher; endpoint off")
+        return None
+    from ..labels import load_labels
+    from .native_front import NativeFrontEnd
+
+    fe = NativeFrontEnd(batcher, load_labels(None), port=port, host=host, arch="triton",
+                        io_threads=int(os.environ.get("ARENA_HTTP_THREADS", "4")),
+                        decode_threads=int(os.environ.get("ARENA_DECODE_THREADS", "8")),
+                        decode_procs=int(os.environ.get("ARENA_DECODE_PROCS", "1") or 1), kserve_model=model)
+    return fe
+
+
 async def serve(args) -> None:
     """Run until SIGINT / SIGTERM, then shut down like the reference classification service
     (architectures/microservices/classification/app/main.py:86-104): stop accepting, give in-flight RPCs a 5 s
@@ -334,7 +358,9 @@ async def serve(args) -> None:
     for app, port in apps:
         socks.append(_socket(args.host, port, reuse_port=True))
         servers.append(_Server(uvicorn.Config(app, log_level="warning", access_log=False)))
-    log.info(f"model server ready: grpc {args.grpc_port} http {args.http_port} metrics {args.metrics_port}")
+    native_fe = start_native_kserve(server, args.host, args.native_http_port)
+    log.info(f"model server ready: grpc {args.grpc_port} http {args.http_port} metrics {args.metrics_port}"
+             + (f" native-kserve {native_fe.port}" if native_fe else ""))
     tasks = [asyncio.create_task(s.serve(sockets=[k])) for s, k in zip(servers, socks)]
     try:
         await stop.wait()
@@ -344,6 +370,8 @@ async def serve(args) -> None:
             s.should_exit = True
         await g.stop(grace=5)
         await asyncio.wait(tasks, timeout=10)
+        if native_fe is not None:
+            native_fe.close()
         server.close()
         log.info("model server stopped")
 
@@ -355,9 +383,14 @@ def main(argv=None) -> None:
     ap.add_argument("--http-port", type=int, default=8000)
     ap.add_argument("--grpc-port", type=int, default=8001)
     ap.add_argument("--metrics-port", type=int, default=8002)
+    ap.add_argument("--native-http-port", type=int, default=int(os.environ.get("ARENA_KSERVE_NATIVE_PORT", "8004")),
+                    help="native KServe-v2 REST endpoint of the arena_pipeline ensemble (0: off)")
     ap.add_argument("--device", default=os.environ.get("ARENA_DEVICE", "gpu"), choices=["gpu", "cpu"])
     ap.add_argument("--gpu", type=int, default=int(os.environ.get("ARENA_GPU", "0")))
     ap.add_argument("--log-level", default=os.environ.get("LOG_LEVEL", "INFO"))
+    from .decode_pool import prestart
+
+    prestart()  # decode-worker fork server before the engines touch the GPU (the native endpoint's PIL fallback)
     asyncio.run(serve(ap.parse_args(argv)))
 
 

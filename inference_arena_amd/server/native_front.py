@@ -41,7 +41,7 @@ class _Collector:
 
     def collect(self):
         s = self.front.stats()
-        b = self.front.batcher.stats()
+        b = self.front.batcher.stats() if self.front.batcher is not None else {"queue_depth": 0, "batch_hist": []}
         req = CounterMetricFamily("arena_requests_total", "Requests by status", labels=["arch", "status"])
         for status, key in (("ok", "ok"), ("bad_request", "bad_request"), ("too_large", "too_large"),
                             ("unavailable", "unavailable"), ("error", "errors")):
@@ -98,7 +98,7 @@ class NativeFrontEnd:
     def __init__(self, batcher, labels: list[str], *, port: int = 8100, host: str = "0.0.0.0",
                  io_threads: int = 4, decode_procs: int = 2, slots: int = 512, softmax: bool = False,
                  arch: str = "monolithic", gpu: str = "0", replica_tag: str = "", decode_threads: int = 8,
-                 jpeg_device: bool = True, **http: int):
+                 jpeg_device: bool = True, kserve_model: str = "", **http: int):
         """``decode_threads``: native split-decoder threads (0: every upload to the ``decode_procs`` PIL
         processes, the round-3 path); ``jpeg_device=False`` reconstructs on the host threads instead of the GPU
         (instances without the device half, e.g. the host-only EchoInstance, take either).  ``http``: further
@@ -114,6 +114,7 @@ class NativeFrontEnd:
                                          "softmax_confidence": bool(softmax), "replica_tag": str(replica_tag),
                                          "decode_threads": int(decode_threads), "jpeg_device": bool(jpeg_device),
                                          "max_image_pixels": int(max_image_pixels()),
+                                         "kserve_model": str(kserve_model),
                                          **_http_timeouts(), **{k: int(v) for k, v in http.items()}})
         self.registry = CollectorRegistry()
         self.registry.register(_Collector(self, arch, gpu))

@@ -165,6 +165,15 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("ARENA_REPLICA_RANK", info.rank))
     if a.arch == "monolithic" and settings.ARENA_DEVICE != "cpu" and os.environ.get("ARENA_NATIVE_HTTP") == "1":
         return _serve_native(settings, info, a.port + a.port_stride * rank, rank)
+    if a.arch == "gateway" and os.environ.get("ARENA_GATEWAY_NATIVE") == "1":
+        # the gateway's request path entirely in C++: proxy to the model server's native KServe endpoint
+        # (server/native_gateway.py; TRITON_HTTP_ENDPOINT)
+        from .native_gateway import serve as serve_gateway
+
+        D.barrier(info)
+        D.shutdown(info)
+        os.environ["PORT"] = str(a.port + a.port_stride * rank)
+        return serve_gateway(settings, replica_tag=str(rank))
     app = build_app(a.arch, settings, info)
     D.barrier(info)
     D.shutdown(info)  # the group is only needed for start-up

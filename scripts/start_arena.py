@@ -147,9 +147,14 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
                                 device], ms_env, log_dir, f"model_server_{k}"))
         ok = wait_http("http://127.0.0.1:8000/v2/health/ready", 600, procs)
         if ok:
+            # ARENA_GATEWAY_NATIVE (default 1): the gateway's native proxy front end forwards to the model server's
+            # native KServe REST endpoint (:8004); 0 keeps the Python gateway on gRPC :8001
+            gw_native = os.environ.get("ARENA_GATEWAY_NATIVE", "1") != "0"
             procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "gateway", "--gpus", "1",
                                 "--port", "8300", "--procs-per-gpu", str(procs_per_gpu)],
-                               dict(env, TRITON_GRPC_ENDPOINT="127.0.0.1:8001", ARENA_DEVICE="cpu"), log_dir,
+                               dict(env, TRITON_GRPC_ENDPOINT="127.0.0.1:8001", ARENA_DEVICE="cpu",
+                                    TRITON_HTTP_ENDPOINT="127.0.0.1:" + os.environ.get("ARENA_KSERVE_NATIVE_PORT", "8004"),
+                                    ARENA_GATEWAY_NATIVE="1" if gw_native else "0"), log_dir,
                                "gateway"))
             ok = wait_http("http://127.0.0.1:8300/health", 300, procs)
     else:

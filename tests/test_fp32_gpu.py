@@ -585,7 +585,7 @@ def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, x3t, m
         native().set_irx_parts(4 if x3t == "0" else 2)
         request.addfinalizer(lambda: native().set_irx_parts(-1))
     monkeypatch.setenv("ARENA_IR_X3T", x3t)
-    if H >= 28:  # "1": the register-resident kernel (ir_reg_x3.hip) where it applies; "0" keeps the others
+    if H >= 28:  # "1": the register-resident kernel (ir_reg_x3.hip, opt-in) where it applies; "0" keeps the others
         from inference_arena_amd.ops import native
 
         native().set_ir_reg(1 if x3t == "1" else 0)

@@ -301,7 +301,7 @@ def test_stage_timing_and_stage_histograms(server):
         assert f'arena_request_latency_seconds_count{{arch="monolithic",stage="{stage}"}}' in text
 
 
-_FRONT_SRCS = ["csrc/tests/front_stress.cpp", "csrc/runtime/http_front.cpp", "csrc/runtime/batcher.cpp",
+_FRONT_SRCS = ["csrc/tests/front_stress.cpp", "csrc/runtime/http_front.cpp", "csrc/runtime/kserve.cpp", "csrc/runtime/batcher.cpp",
                "csrc/runtime/trace.cpp", "csrc/runtime/jpeg_decode.cpp"]
 
 
@@ -436,3 +436,113 @@ def test_split_decoder_stages_oversize_frames_as_rgb():
             fe.close()
             batcher.shutdown()
     assert answers[0] == answers[1]
+
+
+def _kserve_request(upload: bytes) -> tuple[bytes, int]:
+    import struct
+
+    hdr = json.dumps({"inputs": [{"name": "IMAGE_BYTES", "shape": [1], "datatype": "BYTES",
+                                  "parameters": {"binary_data_size": len(upload) + 4}}],
+                      "outputs": [{"name": n, "parameters": {"binary_data": True}}
+                                  for n in ("DETECTIONS", "CLASS_IDS", "CLASS_LOGITS", "CLASS_PROBS", "STAGE_MS")]})
+    hb = hdr.encode()
+    return hb + struct.pack("<I", len(upload)) + upload, len(hb)
+
+
+def test_kserve_rest_route_and_native_gateway():
+    """The model server's native KServe-v2 REST endpoint (binary tensor extension: IMAGE_BYTES in, the ensemble's
+    output tensors out) and the native gateway (proxy mode: /predict forwarded over keep-alive connections, the
+    output tensors turned into the reference JSON) answer exactly what the monolithic /predict answers."""
+    from inference_arena_amd.server.native_gateway import NativeGateway
+
+    C = native()
+    labels = load_labels(None)
+    batcher = C.DynamicBatcher([C.EchoInstance(2, 8, 4, 200)], {"max_batch": 8, "max_queue_delay_us": 200})
+    ms = NativeFrontEnd(batcher, labels, port=0, host="127.0.0.1", io_threads=2, decode_procs=1, slots=16,
+                        decode_threads=2, jpeg_device=False, kserve_model="arena_pipeline")
+    gw = NativeGateway(labels, upstream=f"127.0.0.1:{ms.port}", port=0, host="127.0.0.1", conns=4, io_threads=2)
+    try:
+        assert gw.wait_ready(10)
+        c = http.client.HTTPConnection("127.0.0.1", ms.port, timeout=30)
+        for path, code in (("/v2/health/live", 200), ("/v2/health/ready", 200), ("/v2/models/arena_pipeline", 200),
+                           ("/v2/models/arena_pipeline/ready", 200), ("/v2/models/nope/ready", 404)):
+            c.request("GET", path)
+            r = c.getresponse()
+            body = r.read()
+            assert r.status == code, (path, r.status, body)
+        c.request("GET", "/v2/models/arena_pipeline")
+        meta = json.loads(c.getresponse().read())
+        assert [t["name"] for t in meta["inputs"]] == ["IMAGE_BYTES"] and len(meta["outputs"]) == 5
+        rng = np.random.default_rng(4)
+        for i in range(6):
+            arr = (rng.random((40 + 8 * i, 64, 3)) * 255).astype(np.uint8)
+            b = io.BytesIO()
+            Image.fromarray(arr).save(b, format="JPEG", quality=90)
+            up = b.getvalue()
+            # direct /predict on the model server front end (the monolithic contract)
+            body, ct = _multipart(up)
+            st, data, c2 = _post(ms.port, body, ct)
+            c2.close()
+            assert st == 200
+            direct = json.loads(data)["detections"]
+            # KServe infer, binary tensors
+            req, ihcl = _kserve_request(up)
+            c.request("POST", "/v2/models/arena_pipeline/infer", body=req,
+                      headers={"Content-Type": "application/octet-stream",
+                               "Inference-Header-Content-Length": str(ihcl)})
+            r = c.getresponse()
+            raw = r.read()
+            assert r.status == 200, raw
+            n = int(r.getheader("Inference-Header-Content-Length"))
+            hdr = json.loads(raw[:n])
+            outs, pos = {}, n
+            for o in hdr["outputs"]:
+                sz = o["parameters"]["binary_data_size"]
+                dt = np.int32 if o["datatype"] == "INT32" else np.float32
+                outs[o["name"]] = np.frombuffer(raw[pos:pos + sz], dtype=dt).reshape(o["shape"])
+                pos += sz
+            assert pos == len(raw) and outs["DETECTIONS"].shape == (len(direct), 6)
+            for k, d in enumerate(direct):
+                assert outs["CLASS_IDS"][k, 0] == d["classification"]["class_id"]
+                assert outs["DETECTIONS"][k, 4] == pytest.approx(d["detection"]["confidence"])
+            # through the native gateway
+            st, data, c3 = _post(gw.port, body, ct)
+            c3.close()
+            assert st == 200, data
+            via = json.loads(data)
+            assert [(d["detection"], d["classification"]) for d in via["detections"]] == \
+                [(d["detection"], d["classification"]) for d in direct]
+            assert via["timing"]["total_ms"] > 0
+        # protocol errors: no binary extension, unknown model
+        c.request("POST", "/v2/models/arena_pipeline/infer", body=b'{"inputs":[]}',
+                  headers={"Content-Type": "application/json"})
+        r = c.getresponse()
+        assert r.status == 400 and "binary tensor" in json.loads(r.read())["error"]
+        c.request("POST", "/v2/models/yolov9/infer", body=b"{}", headers={"Content-Type": "application/json"})
+        r = c.getresponse()
+        assert r.status == 404 and "error" in json.loads(r.read())
+        assert gw.stats()["ok"] == 6 and ms.stats()["ok"] == 18  # direct + KServe + via the gateway
+    finally:
+        gw.close()
+        ms.close()
+        batcher.shutdown()
+
+
+def test_native_gateway_reports_a_dead_model_server():
+    from inference_arena_amd.server.native_gateway import NativeGateway
+
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        dead = s.getsockname()[1]
+    gw = NativeGateway(load_labels(None), upstream=f"127.0.0.1:{dead}", port=0, host="127.0.0.1", conns=2)
+    try:
+        assert not gw.wait_ready(0.5)
+        gw.fe.set_healthy(True)  # force: the proxy must answer 502, not hang
+        body, ct = _multipart(_jpeg(16, 16, 1))
+        st, data, c = _post(gw.port, body, ct)
+        c.close()
+        assert st == 502 and "model server" in json.loads(data)["detail"]
+    finally:
+        gw.close()
