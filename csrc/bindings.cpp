@@ -23,6 +23,7 @@
 #include "runtime/jpeg_ingest.h"
 #include "runtime/batcher.h"
 #include "runtime/split.h"
+#include "runtime/crash_trace.h"
 
 namespace py = pybind11;
 using namespace arena;
@@ -534,6 +535,13 @@ py::dict result_to_py(const BatchResult& r, int max_det) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native kernels and runtime of inference_arena_amd (gfx950)";
+  // native stack of a fault on a thread Python's faulthandler cannot see (ARENA_CRASH_TRACE=0 disables)
+  {
+    const char* e = std::getenv("ARENA_CRASH_TRACE");
+    if (e == nullptr || std::strcmp(e, "0") != 0) arena::install_crash_trace();
+  }
+  m.def("install_crash_trace", &arena::install_crash_trace);
+  m.def("crash_trace_installed", &arena::crash_trace_installed);
   bind_jpeg(m);
   m.def("conv2d", &py_conv2d);
   m.def("set_conv_impl", &set_conv_impl);

@@ -222,15 +222,68 @@ def test_head_lanes_match_sequential(dense_models, device, monkeypatch, dtype):
 
     imgs = synthetic_images(7, 61) + synthetic_images(1, 62, hw=(333, 500))
     monkeypatch.setenv("ARENA_HEAD_LANES", "0")
-    seq = GpuPipeline(*dense_models, device=0, buckets=[1, 8], dtype=dtype)
+    seq = GpuPipeline(*dense_models, device=0, buckets=[1, 2, 8], dtype=dtype)
     monkeypatch.setenv("ARENA_HEAD_LANES", "1")
-    par = GpuPipeline(*dense_models, device=0, buckets=[1, 8], dtype=dtype)
+    par = GpuPipeline(*dense_models, device=0, buckets=[1, 2, 8], dtype=dtype)
     assert par.program.ops[:, 46].any() and not seq.program.ops[:, 46].any()
-    for batch in (imgs, imgs[:1], imgs[3:]):
+    for batch in (imgs, imgs[:1], imgs[3:5], imgs[3:]):  # buckets 8, 1, 2 (lanes: B <= 2), 8
         for a, b in zip(seq.infer(batch), par.infer(batch)):
             np.testing.assert_array_equal(a.boxes, b.boxes)
             np.testing.assert_array_equal(a.topk_idx, b.topk_idx)
             np.testing.assert_array_equal(a.topk_logit, b.topk_logit)
+
+
+@pytest.mark.parametrize("kind", ["detector", "split"])
+def test_head_lanes_detector_programs_through_batcher(dense_models, device, monkeypatch, kind):
+    """Lanes in the detector-only program (arm B detection service) and the split topology's detector stage,
+    buckets 1 / 2 / 4, driven by concurrent requests through the native DynamicBatcher (its instance thread
+    submits and collects, several slots in flight): the same answers as the lanes-off programs."""
+    import asyncio
+
+    from inference_arena_amd.data.synthetic import synthetic_images
+    from inference_arena_amd.engine.registry import build_session
+    from inference_arena_amd.server.batching import AsyncBatcher
+
+    imgs = synthetic_images(10, 71) + synthetic_images(2, 72, hw=(333, 500))
+
+    def make(lanes: str):
+        monkeypatch.setenv("ARENA_HEAD_LANES", lanes)
+        if kind == "split":
+            return build_session("split", *dense_models, device=0, buckets=[1, 2, 4], cls_device=0)
+        return build_session("detector", dense_models[0], device=0, buckets=[1, 2, 4])
+
+    def drive(runner):
+        b = AsyncBatcher([_SplitInst(runner) if kind == "split" else runner], max_batch=4, max_queue_delay_us=300)
+
+        async def go():
+            out = []
+            for users in (1, 2, 3, 12):
+                for r in range(3):
+                    idx = [(r * users + k) % len(imgs) for k in range(users)]
+                    out += list(zip(idx, await asyncio.gather(*(b.run(imgs[i]) for i in idx))))
+            return out
+
+        try:
+            return asyncio.run(go())
+        finally:
+            b.close()
+
+    seq, par = make("0"), make("1")
+    prog = (par.det if kind == "split" else par).program
+    assert prog.ops[:, 46].any()
+    a, c = drive(seq), drive(par)
+    assert [i for i, _ in a] == [i for i, _ in c]
+    for (_, x), (_, y) in zip(a, c):
+        assert x["det_count"] == y["det_count"]
+        np.testing.assert_array_equal(x["det"], y["det"])
+        np.testing.assert_array_equal(x["topk_idx"], y["topk_idx"])
+
+
+class _SplitInst:
+    """A SplitPipeline as a batcher instance (its native SplitInstance submits / collects)."""
+
+    def __init__(self, sp):
+        self.ex = sp.instance
 
 
 def test_fused_c3_matches_unfused(dense_models, device, monkeypatch):

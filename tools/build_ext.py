@@ -63,6 +63,7 @@ SOURCES = [
     "runtime/jpeg_decode.cpp",
     "runtime/jpeg_ingest.cpp",
     "runtime/kserve.cpp",
+    "runtime/crash_trace.cpp",
     "bindings_jpeg.cpp",
     "bindings.cpp",
 ]
