@@ -108,8 +108,7 @@ Executor::~Executor() {
     if (streams_[i]) hipStreamSynchronize(streams_[i]);
   if (copy_) hipStreamSynchronize(copy_);
   for (auto& kv : buckets_) {
-    for (int s = 0; s < n_slots_; ++s)
-      if (kv.second.graph[s]) hipGraphExecDestroy(kv.second.graph[s]);
+    for (int s = 0; s < n_slots_; ++s) destroy_graphs(kv.second, s);
     free_arenas(kv.second);
   }
   for (int i = 1; i < n_streams_; ++i)
@@ -196,8 +195,8 @@ void Executor::alloc_slots() {
   }
 }
 
-// Side streams of a slot, created the first time a program with lane ops (kLaneField) runs on it: programs
-// without lanes never create them (no extra queues per process).
+// Side streams of a slot, created when a lane bucket is captured on it (launch_graph runs lane segments there):
+// programs without lanes never create them (no extra queues per process).
 void Executor::ensure_lanes(Slot& sl) {
   if (sl.fork_ev != nullptr) return;
   bool lanes = false;
@@ -416,28 +415,114 @@ void Executor::autotune(Bucket& bk) {
   ARENA_HIP_CHECK(hipMemset(bk.d_arena[0], 0, std::max<int64_t>(bk.info.arena_bytes, 256)));
 }
 
+// Lanes pay off where one batch leaves most CUs idle (small buckets); for full batches the slots already overlap
+// batches on the compute streams and side streams only add contention (profiles/r4lanes/).
+static int lanes_max_batch() {
+  static const int v = [] {
+    const char* e = std::getenv("ARENA_LANES_MAX_BATCH");
+    return e != nullptr ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
+bool Executor::lanes_for(const Bucket& bk) const {
+  if (bk.info.B > lanes_max_batch()) return false;
+  for (const OpRecord& r : prog_)
+    if (r[kLaneField] >= 1 && r[kLaneField] <= kMaxLanes) return true;
+  return false;
+}
+
+void Executor::destroy_graphs(Bucket& bk, int s) {
+  if (bk.graph[s]) hipGraphExecDestroy(bk.graph[s]);
+  bk.graph[s] = nullptr;
+  for (auto& sg : bk.segs[s])
+    if (sg.g) hipGraphExecDestroy(sg.g);
+  bk.segs[s].clear();
+}
+
 void Executor::capture(Bucket& bk, int s) {
   Slot& sl = slots_[s];
   hipStream_t st = sl.stream;
-  ensure_lanes(sl);
   // Validate the program eagerly once (launch errors surface here, not in the graph).
   ARENA_HIP_CHECK(hipStreamSynchronize(st));
-  hipGraph_t g = nullptr;
-  ARENA_HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-  try {
-    // The result D2H copy is issued after the graph launch, not captured: a
-    // captured device->pinned-host memcpy node faulted on ROCm 7.0 (torch's
-    // runtime) while the same graph without it runs cleanly.
-    enqueue_program(prog_, bk, sl, st);
-  } catch (...) {
-    hipStreamEndCapture(st, &g);
-    if (g) hipGraphDestroy(g);
-    throw;
+  destroy_graphs(bk, s);
+  // One capture of ops [a, b) on the slot's stream.  The result D2H copy is issued after the graph launch, not
+  // captured: a captured device->pinned-host memcpy node faulted on ROCm 7.0 (torch's runtime) while the same
+  // graph without it runs cleanly.
+  auto capture_range = [&](size_t a, size_t b) {
+    std::vector<OpRecord> part(prog_.begin() + a, prog_.begin() + b);
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    ARENA_HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    try {
+      enqueue_program(part, bk, sl, st, (int)a);
+    } catch (...) {
+      hipStreamEndCapture(st, &g);
+      if (g) hipGraphDestroy(g);
+      throw;
+    }
+    ARENA_HIP_CHECK(hipStreamEndCapture(st, &g));
+    ARENA_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    ARENA_HIP_CHECK(hipGraphDestroy(g));
+    return ge;
+  };
+  if (!lanes_for(bk)) {
+    bk.graph[s] = capture_range(0, prog_.size());
+    return;
   }
-  ARENA_HIP_CHECK(hipStreamEndCapture(st, &g));
-  if (bk.graph[s]) ARENA_HIP_CHECK(hipGraphExecDestroy(bk.graph[s]));
-  ARENA_HIP_CHECK(hipGraphInstantiate(&bk.graph[s], g, nullptr, nullptr, 0));
-  ARENA_HIP_CHECK(hipGraphDestroy(g));
+  // Lanes: every maximal run of ops with one lane value becomes a linear graph of its own; launch_graph() forks
+  // the side streams (ensure_lanes) off the slot's stream at a lane run and joins them at the next lane-0 run.
+  ensure_lanes(sl);
+  auto lane_of = [&](size_t i) {
+    const int64_t l = prog_[i][kLaneField];
+    return l >= 1 && l <= kMaxLanes ? (int)l : 0;
+  };
+  for (size_t a = 0; a < prog_.size();) {
+    size_t b = a + 1;
+    while (b < prog_.size() && lane_of(b) == lane_of(a)) ++b;
+    Bucket::Seg sg;
+    sg.lane = lane_of(a);
+    sg.g = capture_range(a, b);
+    bk.segs[s].push_back(sg);
+    a = b;
+  }
+}
+
+void Executor::launch_graph(Bucket& bk, int s, hipStream_t st) {
+  if (bk.segs[s].empty()) {
+    ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], st));
+    return;
+  }
+  Slot& sl = slots_[s];
+  bool forked[kMaxLanes] = {};
+  bool fork_recorded = false;
+  auto join = [&]() {
+    for (int l = 0; l < kMaxLanes; ++l)
+      if (forked[l]) {
+        ARENA_HIP_CHECK(hipEventRecord(sl.lane_ev[l], sl.lane_stream[l]));
+        ARENA_HIP_CHECK(hipStreamWaitEvent(st, sl.lane_ev[l], 0));
+        forked[l] = false;
+      }
+    fork_recorded = false;
+  };
+  for (const Bucket::Seg& sg : bk.segs[s]) {
+    if (sg.lane == 0) {
+      join();
+      ARENA_HIP_CHECK(hipGraphLaunch(sg.g, st));
+      continue;
+    }
+    const int l = sg.lane - 1;
+    if (!forked[l]) {
+      if (!fork_recorded) {  // everything before the lane region on the slot's stream
+        ARENA_HIP_CHECK(hipEventRecord(sl.fork_ev, st));
+        fork_recorded = true;
+      }
+      ARENA_HIP_CHECK(hipStreamWaitEvent(sl.lane_stream[l], sl.fork_ev, 0));
+      forked[l] = true;
+    }
+    ARENA_HIP_CHECK(hipGraphLaunch(sg.g, sl.lane_stream[l]));
+  }
+  join();
 }
 
 uint8_t* Executor::resolve(Bucket& bk, Slot& sl, int64_t buf, int64_t coff, int eb) {
@@ -470,36 +555,11 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
   auto bdev = [&](int64_t kind) -> const int* { return kind == BATCH_CROPS ? &ctrl->n_crops : &ctrl->n_images; };
   const uint8_t* W = d_weights_;
 
-  // Lanes (kLaneField): a run of lane ops forks each lane's side stream off the main stream at its first op and
-  // joins every forked lane back before the next lane-0 op (and at the end).  Single-op programs (autotune timing)
-  // stay on the main stream.
-  bool forked[kMaxLanes] = {};
-  auto join_lanes = [&]() {
-    for (int l = 0; l < kMaxLanes; ++l)
-      if (forked[l]) {
-        ARENA_HIP_CHECK(hipEventRecord(sl.lane_ev[l], sl.lane_stream[l]));
-        ARENA_HIP_CHECK(hipStreamWaitEvent(s_main, sl.lane_ev[l], 0));
-        forked[l] = false;
-      }
-  };
-  // Lanes pay off where one batch leaves most CUs idle (small buckets); for full batches the slots already
-  // overlap batches on the compute streams and side streams only add contention (profiles/r4lanes/).
-  static const int lanes_max_b = [] {
-    const char* e = std::getenv("ARENA_LANES_MAX_BATCH");
-    return e != nullptr ? std::atoi(e) : 2;
-  }();
-  const bool use_lanes = prog.size() > 1 && sl.fork_ev != nullptr && bk.info.B <= lanes_max_b;
+  // Lane ops (kLaneField) run in program order here: the lanes' side streams are driven by launch_graph() over
+  // per-lane captured segments, not by forking inside one capture.
   for (size_t oi = 0; oi < prog.size(); ++oi) {
     const OpRecord& r = prog[oi];
-    const int lane = use_lanes && r[kLaneField] >= 1 && r[kLaneField] <= kMaxLanes ? (int)r[kLaneField] : 0;
-    if (lane == 0) {
-      join_lanes();
-    } else if (!forked[lane - 1]) {
-      ARENA_HIP_CHECK(hipEventRecord(sl.fork_ev, s_main));  // everything before this op on the main stream
-      ARENA_HIP_CHECK(hipStreamWaitEvent(sl.lane_stream[lane - 1], sl.fork_ev, 0));
-      forked[lane - 1] = true;
-    }
-    hipStream_t s = lane ? sl.lane_stream[lane - 1] : s_main;
+    hipStream_t s = s_main;
     // field 47: activation precision of the op (0 bf16, 1 exact fp32; planner.OP_DTYPE_FIELD)
     const bool f32 = r[kDtypeField] == 1;
     const int eb = f32 ? 4 : 2;
@@ -889,7 +949,6 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
     }
     ARENA_HIP_CHECK(hipGetLastError());
   }
-  join_lanes();
 }
 
 // ---------------------------------------------------------------- host packing
@@ -1119,7 +1178,7 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     enqueue_results_d2h(bk, sl, n);
   } else {
     Bucket& bk = buckets_.at(B);
-    ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], sl.stream));
+    launch_graph(bk, s, sl.stream);
     enqueue_results_d2h(bk, sl, n);
   }
   buckets_.at(B).last_slot = s;
@@ -1242,7 +1301,7 @@ int Executor::submit_peer(Executor& src, int src_slot) {
   copy(sl.d_out + out_off_xcrops(), ss.d_out + out_off_xcrops(), sizeof(CropRef) * (size_t)max_B_ * cfg_.max_det);
   ARENA_HIP_CHECK(hipEventRecord(sl.started, sl.stream));
   Bucket& bk = it->second;
-  ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], sl.stream));
+  launch_graph(bk, s, sl.stream);
   enqueue_results_d2h(bk, sl, ss.n_images);
   bk.last_slot = s;
   ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
@@ -1340,7 +1399,7 @@ int Executor::submit_device(const std::vector<DeviceImage>& imgs, const std::vec
   sl.in_used = in_bytes_meta() + off;
   ARENA_HIP_CHECK(hipEventRecord(sl.started, sl.stream));
   Bucket& bk = it->second;
-  ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], sl.stream));
+  launch_graph(bk, s, sl.stream);
   enqueue_results_d2h(bk, sl, n);
   bk.last_slot = s;
   ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
@@ -1356,7 +1415,7 @@ void Executor::replay(int B, int s, int iters) {
   if (it == buckets_.end()) throw std::runtime_error("replay: unknown bucket");
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   if (s < 0 || s >= n_slots_) throw std::runtime_error("replay: bad slot");
-  for (int i = 0; i < iters; ++i) ARENA_HIP_CHECK(hipGraphLaunch(it->second.graph[s], streams_[s % n_streams_]));
+  for (int i = 0; i < iters; ++i) launch_graph(it->second, s, streams_[s % n_streams_]);
 }
 
 void Executor::synchronize() {

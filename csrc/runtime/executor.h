@@ -212,6 +212,15 @@ class Executor : public BatchInstance {
     uint8_t* d_arena[kMaxSlots] = {};  // per slot (all aliased when concurrency is off)
     int last_slot = 0;                 // slot whose arena read_arena() inspects
     hipGraphExec_t graph[kMaxSlots] = {};
+    // Lane buckets (program lanes, B <= lanes_max_batch()): the program as contiguous single-lane segments, one
+    // graph each; launch_graph() runs lane segments on the slot's side streams between fork / join events.
+    // (A single graph with forked branches made HIP's graph launch segfault with GPU_MAX_HW_QUEUES < 4 from the
+    // batcher's instance thread: profiles/r5lanes/README.md.)
+    struct Seg {
+      int lane = 0;
+      hipGraphExec_t g = nullptr;
+    };
+    std::vector<Seg> segs[kMaxSlots];
     std::vector<int16_t> impl;  // per op of prog_: conv kernel family chosen by autotune (0 = default)
   };
 
@@ -220,6 +229,9 @@ class Executor : public BatchInstance {
   void sync_slots();
   void free_arenas(Bucket& bk);
   void capture(Bucket& bk, int slot);
+  void launch_graph(Bucket& bk, int slot, hipStream_t st);
+  void destroy_graphs(Bucket& bk, int slot);
+  bool lanes_for(const Bucket& bk) const;
   void enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s,
                        int op_offset = 0, int force_impl = 0);
   void autotune(Bucket& bk);

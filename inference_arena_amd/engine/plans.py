@@ -263,9 +263,10 @@ def head_lanes() -> bool:
     graph (side streams, ProgramBuilder.parallel) in buckets up to ``ARENA_LANES_MAX_BATCH`` (2; the executor
     keeps larger buckets on one stream: with four slots in flight the side streams only add contention,
     profiles/r4lanes/); their small-grid convs (15-50 workgroups each at bs 1) leave most CUs idle when
-    serialised.  1-user HTTP P50 1.705 -> 1.690 ms, P99 1.818 -> 1.784 ms (profiles/r4lanes_bs1/).  Off by
-    default: the arm-B detection service (detector-only program, several processes per GPU) crashed with it on in
-    a protocol run (profiles/r4lanes/README.md); the monolithic / model-server paths and the GPU tests ran clean."""
+    serialised.  The executor captures each lane run as a linear graph and launches the lanes on the slot's side
+    streams (a single forked-branch graph segfaulted inside hipGraphLaunch under the arm-B services' 2-queue cap:
+    profiles/r5lanes/README.md).  Off by default: bs-1 / bs-2 latency is unchanged within noise (1.907 vs 1.904 ms,
+    1.992 vs 1.972 ms) and arm B at 10 users is 2 % slower with it (profiles/r5lanes/)."""
     return os.environ.get("ARENA_HEAD_LANES", "0").lower() not in ("0", "false", "no", "off")
 
 

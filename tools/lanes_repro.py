@@ -80,13 +80,18 @@ def main(argv=None) -> int:
         async def go():
             for users in [int(u) for u in a.users.split(",")]:
                 t0 = time.perf_counter()
+                lat = []
                 for r in range(a.rounds):
                     idx = [(r * users + k) % len(uploads) for k in range(users)]
+                    t1 = time.perf_counter()
                     res = await asyncio.gather(*(one(i) for i in idx))
+                    lat.append((time.perf_counter() - t1) * 1e3)
                     for i, d in zip(idx, res):
                         out.setdefault((users, i), d)
+                lat.sort()
                 print(f"[{tag}] users {users}: {a.rounds} rounds in {time.perf_counter() - t0:.2f} s "
-                      f"(batches {b.stats().get('batches')})", flush=True)
+                      f"(batches {b.stats().get('batches')}); round latency P50 {lat[len(lat) // 2]:.3f} ms "
+                      f"P90 {lat[int(len(lat) * 0.9)]:.3f} ms", flush=True)
 
         try:
             asyncio.run(go())
