@@ -9,6 +9,8 @@ telemetry reader (metrics/gpu.py) finds a device, GPU busy % and VRAM.
 """
 from __future__ import annotations
 
+import os
+import re
 import threading
 import time
 
@@ -41,6 +43,12 @@ class ResourceSampler:
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
         self._cache: dict = {}
+        # CPU % per (role, thread class): the native threads name themselves (arena-http-io, arena-jpeg,
+        # arena-batcher, ...); HIP runtime and Python threads keep the process name
+        self.by_thread: dict[tuple[str, str], list[float]] = {}
+        self._ticks: dict[tuple[int, int], tuple[str, int]] = {}
+        self._t_prev: float | None = None
+        self._hz = os.sysconf("SC_CLK_TCK") if hasattr(os, "sysconf") else 100
         self._gpu = None
         if gpu:
             try:
@@ -89,6 +97,7 @@ class ResourceSampler:
                 continue
         for r, c in roles.items():
             self.by_role.setdefault(r, []).append(c)
+        self._sample_threads(procs)
         busy = vram = None
         if self._gpu is not None:
             try:
@@ -100,6 +109,49 @@ class ResourceSampler:
             except Exception:  # noqa: BLE001
                 pass
         self.samples.append((time.time(), cpu, mem, busy, vram))
+
+    @staticmethod
+    def thread_class(comm: str) -> str:
+        """Thread name -> class: trailing digits / separators dropped (arena-jpeg3 -> arena-jpeg)."""
+        return re.sub(r"[-_:.]?\d+$", "", comm.strip()) or comm
+
+    def _sample_threads(self, procs) -> None:
+        """Per-thread utime + stime from /proc/<pid>/task/*/stat since the previous sample, summed by (role,
+        thread class) as CPU % (Linux only; best effort)."""
+        now = time.monotonic()
+        dt = None if self._t_prev is None else now - self._t_prev
+        self._t_prev = now
+        acc: dict[tuple[str, str], float] = {}
+        for p in procs:
+            role = self._cache.get(("role", p.pid)) or "other"
+            base = f"/proc/{p.pid}/task"
+            try:
+                tids = os.listdir(base)
+            except OSError:
+                continue
+            for tid in tids:
+                try:
+                    with open(f"{base}/{tid}/stat") as f:
+                        st = f.read()
+                except OSError:
+                    continue
+                l, r = st.find("("), st.rfind(")")
+                if l < 0 or r < 0:
+                    continue
+                fields = st[r + 2:].split()
+                try:
+                    ticks = int(fields[11]) + int(fields[12])  # utime, stime (fields 14, 15 of stat)
+                except (IndexError, ValueError):
+                    continue
+                key = (p.pid, int(tid))
+                cls = self.thread_class(st[l + 1:r])
+                prev = self._ticks.get(key)
+                self._ticks[key] = (cls, ticks)
+                if dt and prev is not None:
+                    acc[(role, cls)] = acc.get((role, cls), 0.0) + 100.0 * (ticks - prev[1]) / self._hz / dt
+        if dt:
+            for k, v in acc.items():
+                self.by_thread.setdefault(k, []).append(v)
 
     def _role(self, p) -> str:
         """Process role from the command line: the arm's services (``--arch X`` of the replica launcher, the model
@@ -163,6 +215,14 @@ class ResourceSampler:
             "resource_samples": len(self.samples),
         }
         out["cpu_percent_by_role"] = {r: round(float(np.mean(v)), 1) for r, v in sorted(self.by_role.items())}
+        if self.by_thread:
+            n = max(len(v) for v in self.by_thread.values())
+            by: dict[str, dict[str, float]] = {}
+            for (role, cls), v in sorted(self.by_thread.items()):
+                pct = float(np.sum(v)) / n  # a class absent from some samples counted 0 there
+                if pct >= 0.5:
+                    by.setdefault(role, {})[cls] = round(pct, 1)
+            out["cpu_percent_by_thread"] = by
         busy = [s[3] for s in self.samples if s[3] is not None]
         vram = [s[4] for s in self.samples if s[4] is not None]
         if busy:

@@ -56,6 +56,39 @@ def test_resource_sampler_follows_a_process_tree():
     assert out["cpu_utilization_percent_max"] > 50.0, out  # the spinning child: ~100 % of one core
 
 
+def test_resource_sampler_splits_cpu_by_thread_class():
+    """cpu_percent_by_thread: a named busy thread (prctl PR_SET_NAME, as the native threads name themselves) is
+    reported under its class, its trailing index dropped."""
+    import ctypes
+    import hashlib
+    import threading
+
+    from inference_arena_amd.loadgen.resources import ResourceSampler
+
+    assert ResourceSampler.thread_class("arena-jpeg3") == "arena-jpeg"
+    assert ResourceSampler.thread_class("python3") == "python"
+    stop = threading.Event()
+    blob = bytes(1 << 22)
+
+    def spin():  # busy in C with the GIL released (hashlib drops it for large inputs): no GIL convoy
+        ctypes.CDLL(None).prctl(15, b"arena-spin7", 0, 0, 0)  # PR_SET_NAME
+        while not stop.is_set():
+            hashlib.sha256(blob).digest()
+
+    t = threading.Thread(target=spin, daemon=True)
+    t.start()
+    try:
+        s = ResourceSampler([os.getpid()], interval=0.2, gpu=False).start()
+        time.sleep(1.5)
+        out = s.stop()
+    finally:
+        stop.set()
+        t.join()
+    by = out.get("cpu_percent_by_thread", {})
+    spin_pct = sum(v.get("arena-spin", 0.0) for v in by.values())
+    assert spin_pct > 20.0, (out, s.by_thread)
+
+
 def test_cost_config_validates():
     from inference_arena_amd.config import get_cost_config, validate_config
 
