@@ -542,6 +542,7 @@ PYBIND11_MODULE(_C, m) {
   }
   m.def("install_crash_trace", &arena::install_crash_trace);
   m.def("crash_trace_installed", &arena::crash_trace_installed);
+  m.def("dump_thread_stack", &arena::dump_thread_stack, py::arg("tid"));
   bind_jpeg(m);
   m.def("conv2d", &py_conv2d);
   m.def("set_conv_impl", &set_conv_impl);

@@ -94,7 +94,50 @@ void handler(int sig, siginfo_t* info, void* uctx) {
   raise(sig);
 }
 
+void stack_handler(int, siginfo_t*, void*) {
+  write_str("[arena stack] thread ");
+  write_num((unsigned long long)syscall(SYS_gettid), 10);
+  write_str("\n");
+  void* frames[48];
+  const int n = backtrace(frames, 48);
+  for (int i = 0; i < n; ++i) {
+    Dl_info di;
+    write_str("[arena stack]   #");
+    write_num((unsigned)i, 10);
+    write_str(" ");
+    if (dladdr(frames[i], &di) && di.dli_fname != nullptr) {
+      write_str(di.dli_fname);
+      write_str(" +");
+      write_num((unsigned long long)((uintptr_t)frames[i] - (uintptr_t)di.dli_fbase), 16);
+      if (di.dli_sname != nullptr) {
+        write_str(" ");
+        write_str(di.dli_sname);
+        write_str("+");
+        write_num((unsigned long long)((uintptr_t)frames[i] - (uintptr_t)di.dli_saddr), 16);
+      }
+    } else {
+      write_num((unsigned long long)(uintptr_t)frames[i], 16);
+    }
+    write_str("\n");
+  }
+}
+
 }  // namespace
+
+bool dump_thread_stack(int tid) {
+  static bool installed = false;
+  if (!installed) {
+    void* warm[2];
+    backtrace(warm, 2);
+    struct sigaction sa{};
+    sa.sa_sigaction = stack_handler;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGUSR2, &sa, nullptr);
+    installed = true;
+  }
+  return syscall(SYS_tgkill, getpid(), tid, SIGUSR2) == 0;
+}
 
 bool install_crash_trace() {
   if (g_installed) return false;

@@ -7,5 +7,7 @@ namespace arena {
 // registered for the calling thread only; other threads run the handler on their own stacks.
 bool install_crash_trace();
 bool crash_trace_installed();
+// Diagnostics: the native stack of thread `tid` of this process, printed to stderr by that thread (SIGUSR2).
+bool dump_thread_stack(int tid);
 
 }  // namespace arena

@@ -5,6 +5,7 @@
 #include "peer.h"
 
 #include <pthread.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -12,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <stdexcept>
 #include <string>
 
@@ -1183,11 +1185,61 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   }
   buckets_.at(B).last_slot = s;
   ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
+  sl.t_submit = std::chrono::steady_clock::now();
   sl.busy = true;
   sl.bucket = B;
   sl.n_images = n;
   next_slot_ = (next_slot_ + 1) % n_slots_;
   return s;
+}
+
+// Completion wait of a slot's batch.  HIP's hipEventSynchronize keeps the waiting thread busy for the whole
+// device time of the batch (a core per batcher thread at load; a blocking-sync event did not change that:
+// profiles/r5triton2/).  ARENA_SYNC selects:
+//   adaptive (default): sleep until shortly before the batch's expected completion (an EWMA per bucket of
+//     submit -> observed completion, updated only when the wait was real), then query the event every
+//     ARENA_POLL_US (default 20) with 1 us timer slack: ~no CPU while the device works, detection within ~30 us;
+//   poll: query + fixed ARENA_POLL_US sleeps (default 50);  spin / blocking: hipEventSynchronize (blocking: the
+//     event was created with hipEventBlockingSync).
+void Executor::wait_done(Slot& sl) {
+  enum Mode { kAdaptive, kPoll, kHip };
+  static const Mode mode = [] {
+    const char* e = std::getenv("ARENA_SYNC");
+    const std::string v = e != nullptr ? e : "adaptive";
+    return v == "poll" ? kPoll : (v == "spin" || v == "blocking") ? kHip : kAdaptive;
+  }();
+  if (mode == kHip) {
+    ARENA_HIP_CHECK(hipEventSynchronize(sl.done));
+    return;
+  }
+  static const int poll_us = [] {
+    const char* u = std::getenv("ARENA_POLL_US");
+    return std::max(1, u != nullptr ? std::atoi(u) : (mode == kPoll ? 50 : 20));
+  }();
+  thread_local bool slack_set = false;
+  if (!slack_set) {
+    prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us: the short sleeps below must not stretch to 50 us
+    slack_set = true;
+  }
+  hipError_t q = hipEventQuery(sl.done);
+  if (q != hipErrorNotReady) {
+    ARENA_HIP_CHECK(q);
+    return;  // already complete (collect came late): no sample for the estimate
+  }
+  using clk = std::chrono::steady_clock;
+  const int B = std::min(std::max(sl.bucket, 0), kMaxEstBuckets - 1);
+  const float est = wall_est_us_[B].load(std::memory_order_relaxed);
+  if (mode == kAdaptive && est > 0.f) {
+    constexpr double kMarginUs = 150.0;  // wake this early: sleep overshoot and estimate noise
+    const double elapsed = std::chrono::duration<double, std::micro>(clk::now() - sl.t_submit).count();
+    const double nap = (double)est - elapsed - kMarginUs;
+    if (nap > 2.0 * poll_us) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)nap));
+  }
+  while ((q = hipEventQuery(sl.done)) == hipErrorNotReady)
+    std::this_thread::sleep_for(std::chrono::microseconds(poll_us));
+  ARENA_HIP_CHECK(q);
+  const float seen = (float)std::chrono::duration<double, std::micro>(clk::now() - sl.t_submit).count();
+  wall_est_us_[B].store(est > 0.f ? 0.8f * est + 0.2f * seen : seen, std::memory_order_relaxed);
 }
 
 BatchResult Executor::collect(int s) {
@@ -1197,7 +1249,7 @@ BatchResult Executor::collect(int s) {
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   {
     trace::Range tw("arena.collect.wait");
-    ARENA_HIP_CHECK(hipEventSynchronize(sl.done));
+    wait_done(sl);
   }
   trace::Range tu("arena.collect.unpack");
   BatchResult res;
@@ -1305,6 +1357,7 @@ int Executor::submit_peer(Executor& src, int src_slot) {
   enqueue_results_d2h(bk, sl, ss.n_images);
   bk.last_slot = s;
   ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
+  sl.t_submit = std::chrono::steady_clock::now();
   sl.busy = true;
   sl.bucket = B;
   sl.n_images = ss.n_images;
@@ -1403,6 +1456,7 @@ int Executor::submit_device(const std::vector<DeviceImage>& imgs, const std::vec
   enqueue_results_d2h(bk, sl, n);
   bk.last_slot = s;
   ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
+  sl.t_submit = std::chrono::steady_clock::now();
   sl.busy = true;
   sl.bucket = B;
   sl.n_images = n;

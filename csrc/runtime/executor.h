@@ -21,6 +21,7 @@
 // execute concurrently on the device while the next batches are packed and
 // uploaded into the remaining slots.
 #pragma once
+#include <chrono>
 #include <hip/hip_runtime.h>
 
 #include <array>
@@ -46,6 +47,7 @@ constexpr int kDtypeField = 47;  // per-op activation precision: 0 bf16, 1 exact
 constexpr int kLaneField = 46;
 constexpr int kMaxLanes = 3;
 constexpr int kMaxSlots = 6;
+constexpr int kMaxEstBuckets = 257;  // completion-time estimates per bucket size (larger buckets share the last)
 using OpRecord = std::array<int64_t, kOpFields>;
 
 enum OpType : int64_t {
@@ -202,6 +204,7 @@ class Executor : public BatchInstance {
     hipStream_t lane_stream[kMaxLanes] = {};  // side streams of program lanes (kLaneField)
     hipEvent_t fork_ev = nullptr, lane_ev[kMaxLanes] = {};
     int idx = 0;
+    std::chrono::steady_clock::time_point t_submit{};  // host time of the submit (adaptive completion wait)
     bool busy = false;
     int bucket = 0;
     int n_images = 0;
@@ -229,6 +232,7 @@ class Executor : public BatchInstance {
   void sync_slots();
   void free_arenas(Bucket& bk);
   void capture(Bucket& bk, int slot);
+  void wait_done(Slot& sl);
   void launch_graph(Bucket& bk, int slot, hipStream_t st);
   void destroy_graphs(Bucket& bk, int slot);
   bool lanes_for(const Bucket& bk) const;
@@ -293,6 +297,7 @@ class Executor : public BatchInstance {
   std::condition_variable pool_cv_, pool_done_cv_;
   std::vector<std::function<void()>>* pool_jobs_ = nullptr;
   std::atomic<int> pool_next_{0};
+  std::atomic<float> wall_est_us_[kMaxEstBuckets] = {};  // wait_done(): submit -> completion EWMA per bucket
   int pool_active_ = 0;
   uint64_t pool_gen_ = 0;
   bool pool_stop_ = false;
