@@ -7,15 +7,17 @@
 //   jpeg_idct_kernel    one 8x8 block per 8 lanes: dequantize (row loads of 16 B), islow pass 1 over the
 //                       columns and pass 2 over the rows through an LDS transpose, 8 samples (one 8-byte store)
 //                       per lane into the component's sample plane.  grid (blocks / 32, images).
-//   jpeg_color_kernel   4 output pixels per lane: fancy chroma upsampling from the planes (h2v2 / h2v1 / none)
-//                       + YCbCr->RGB, three 4-byte stores (12 bytes = 4 RGB pixels, aligned).  grid (pixels /
-//                       1024, images).
+//   jpeg_color_kernel   4 horizontally adjacent output pixels per lane: one dword of luma, each chroma sample
+//                       loaded once per lane, fancy upsampling (h2v2 / h2v1 / none) + YCbCr->RGB, three 4-byte
+//                       stores.  grid (pixels / 1024, images), grid-stride over rows x quads.
 //
 // The arithmetic is kernels/jpeg_math.h, the same functions the host reference (jpeg_coefs_to_rgb) uses, so
 // the result is bit-identical to it and to PIL / libjpeg-turbo (tests/test_jpeg_native_gpu.py).  The work is
 // a few MB of traffic per batch of 32 frames: latency, not throughput, is what the layout optimises (every
 // lane of a wave does useful work; no divergent per-component loops).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "jpeg_desc.h"
 #include "jpeg_math.h"
@@ -90,75 +92,91 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDesc* __restri
   *dst = make_uint2(lo, hi);
 }
 
-__device__ __forceinline__ void chroma_at(const JpegDesc& d, const uint8_t* __restrict__ pool, int x, int y,
-                                          int* cb, int* cr) {
-  const int layout = d.layout;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const JpegCompDesc& C = d.comp[1 + k];
-    const uint8_t* cp = pool + C.plane_off;
-    const int64_t cs = (int64_t)C.bw * 8;
-    int val;
-    if (layout == JPEG_444) {
-      val = cp[(int64_t)y * cs + x];
-    } else {
-      const int cx = x >> 1, xo = x & 1;
-      const int nx = xo ? min(cx + 1, C.cw - 1) : max(cx - 1, 0);
-      if (layout == JPEG_422) {
-        val = jpegm::fancy_h2v1(cp[(int64_t)y * cs + cx], cp[(int64_t)y * cs + nx], xo);
-      } else {
-        const int cy = y >> 1;
-        const int ny = (y & 1) ? min(cy + 1, C.ch - 1) : max(cy - 1, 0);
-        val = jpegm::fancy_h2v2(cp[(int64_t)cy * cs + cx], cp[(int64_t)cy * cs + nx], cp[(int64_t)ny * cs + cx],
-                                cp[(int64_t)ny * cs + nx], xo);
-      }
-    }
-    if (k == 0) *cb = val;
-    else *cr = val;
-  }
+// One lane = 4 horizontally adjacent output pixels x0 .. x0 + 3 (x0 = 4q) of one row.  Their luma is one aligned
+// dword of the Y plane (row stride bw * 8, x0 % 4 == 0, planes 8-byte aligned: the IDCT's uint2 stores); with
+// 2x horizontal chroma subsampling the four pixels need chroma columns cx0 - 1 .. cx0 + 2 (cx0 = 2q) of each
+// chroma row they read, so every chroma sample is loaded once per lane instead of once per pixel and tap.  The
+// per-pixel formulas (clamped neighbours, fancy upsampling, fixed-point YCbCr) are exactly chroma_at's of the
+// host reference (jpeg_math.h), so the output stays bit-identical.  Rows of a width that is a multiple of 4 store
+// 12-byte aligned dword triples; other widths store bytes.
+struct ChromaRow {
+  int v[4];  // columns max(cx0 - 1, 0), cx0, min(cx0 + 1, cw - 1), min(cx0 + 2, cw - 1)
+};
+
+__device__ __forceinline__ ChromaRow chroma_row(const uint8_t* __restrict__ row, int cx0, int cw) {
+  ChromaRow r;
+  r.v[0] = row[max(cx0 - 1, 0)];
+  r.v[1] = row[cx0];
+  r.v[2] = row[min(cx0 + 1, cw - 1)];
+  r.v[3] = row[min(cx0 + 2, cw - 1)];
+  return r;
 }
+
+// (cx, nx) of pixel i of the quad as indices into ChromaRow: i = 0 (cx0, cx0 - 1), 1 (cx0, cx0 + 1),
+// 2 (cx0 + 1, cx0), 3 (cx0 + 1, cx0 + 2)
+__device__ __forceinline__ int quad_c(int i) { return i < 2 ? 1 : 2; }
+__device__ __forceinline__ int quad_n(int i) { return i == 0 ? 0 : i == 1 ? 2 : i == 2 ? 1 : 3; }
 
 __global__ __launch_bounds__(256) void jpeg_color_kernel(const JpegDesc* __restrict__ descs, uint8_t* __restrict__ pool) {
   const JpegDesc& d = descs[blockIdx.y];
-  const int W = d.width, H = d.height;
-  const int64_t npix = (int64_t)W * H;
-  const int64_t p0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (p0 >= npix) return;
+  const int W = d.width, H = d.height, layout = d.layout;
+  const int qpr = (W + 3) >> 2;  // quads per row
+  const int total = qpr * H;
   const uint8_t* yp = pool + d.comp[0].plane_off;
-  const int64_t ys = (int64_t)d.comp[0].bw * 8;
-  uint8_t px[12];
-  int y = (int)(p0 / W), x = (int)(p0 - (int64_t)y * W);
-  const int n = (int)min((int64_t)4, npix - p0);
+  const int ys = d.comp[0].bw * 8;
+  uint8_t* out_img = pool + d.rgb_off;
+  for (int t = (int)blockIdx.x * 256 + (int)threadIdx.x; t < total; t += (int)gridDim.x * 256) {
+    const int y = t / qpr, q = t - y * qpr;
+    const int x0 = 4 * q;
+    const int n = min(4, W - x0);
+    const uint32_t yw = *reinterpret_cast<const uint32_t*>(yp + (int64_t)y * ys + x0);
+    uint8_t px[12];
+    if (layout == JPEG_GRAY) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i < n) {
-      const int yy = yp[(int64_t)y * ys + x];
-      if (d.layout == JPEG_GRAY) {
-        px[3 * i] = px[3 * i + 1] = px[3 * i + 2] = (uint8_t)yy;
-      } else {
-        int cb, cr;
-        chroma_at(d, pool, x, y, &cb, &cr);
-        jpegm::ycc_to_rgb(yy, cb, cr, px + 3 * i);
+      for (int i = 0; i < 4; ++i) px[3 * i] = px[3 * i + 1] = px[3 * i + 2] = (uint8_t)(yw >> (8 * i));
+    } else {
+      int cb[4], cr[4];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const JpegCompDesc& C = d.comp[1 + k];
+        const uint8_t* cp = pool + C.plane_off;
+        const int cs = C.bw * 8;
+        int* dst = k == 0 ? cb : cr;
+        if (layout == JPEG_444) {
+          const uint32_t w = *reinterpret_cast<const uint32_t*>(cp + (int64_t)y * cs + x0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dst[i] = (int)((w >> (8 * i)) & 0xFF);
+        } else if (layout == JPEG_422) {
+          const ChromaRow r = chroma_row(cp + (int64_t)y * cs, 2 * q, C.cw);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dst[i] = jpegm::fancy_h2v1(r.v[quad_c(i)], r.v[quad_n(i)], i & 1);
+        } else {
+          const int cy = y >> 1;
+          const int ny = (y & 1) ? min(cy + 1, C.ch - 1) : max(cy - 1, 0);
+          const ChromaRow a = chroma_row(cp + (int64_t)cy * cs, 2 * q, C.cw);
+          const ChromaRow b = chroma_row(cp + (int64_t)ny * cs, 2 * q, C.cw);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            dst[i] = jpegm::fancy_h2v2(a.v[quad_c(i)], a.v[quad_n(i)], b.v[quad_c(i)], b.v[quad_n(i)], i & 1);
+        }
       }
-      if (++x == W) {
-        x = 0;
-        ++y;
-      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) jpegm::ycc_to_rgb((int)((yw >> (8 * i)) & 0xFF), cb[i], cr[i], px + 3 * i);
     }
-  }
-  uint8_t* out = pool + d.rgb_off + p0 * 3;
-  if (n == 4) {
-    uint32_t w[3];
+    uint8_t* out = out_img + ((int64_t)y * W + x0) * 3;
+    if (n == 4 && (W & 3) == 0) {
+      uint32_t w[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
-      w[k] = (uint32_t)px[4 * k] | ((uint32_t)px[4 * k + 1] << 8) | ((uint32_t)px[4 * k + 2] << 16) |
-             ((uint32_t)px[4 * k + 3] << 24);
-    uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
-    o32[0] = w[0];
-    o32[1] = w[1];
-    o32[2] = w[2];
-  } else {
-    for (int k = 0; k < 3 * n; ++k) out[k] = px[k];
+      for (int k = 0; k < 3; ++k)
+        w[k] = (uint32_t)px[4 * k] | ((uint32_t)px[4 * k + 1] << 8) | ((uint32_t)px[4 * k + 2] << 16) |
+               ((uint32_t)px[4 * k + 3] << 24);
+      uint32_t* o32 = reinterpret_cast<uint32_t*>(out);
+      o32[0] = w[0];
+      o32[1] = w[1];
+      o32[2] = w[2];
+    } else {
+      for (int k = 0; k < 3 * n; ++k) out[k] = px[k];
+    }
   }
 }
 
@@ -169,7 +187,8 @@ void jpeg_reconstruct(const JpegDesc* d_descs, uint8_t* d_pool, int n_images, in
   if (n_images <= 0) return;
   const dim3 g1((unsigned)((max_blocks + kBlocksPerGroup - 1) / kBlocksPerGroup), (unsigned)n_images);
   if (max_blocks > 0) hipLaunchKernelGGL(jpeg_idct_kernel, g1, dim3(256), 0, s, d_descs, d_pool);
-  const dim3 g2((unsigned)((max_pixels + 1023) / 1024), (unsigned)n_images);
+  // one lane per 4-pixel quad of a row, grid-stride over the image's rows x quads
+  const dim3 g2((unsigned)std::max<int64_t>(1, (max_pixels + 1023) / 1024), (unsigned)n_images);
   if (max_pixels > 0) hipLaunchKernelGGL(jpeg_color_kernel, g2, dim3(256), 0, s, d_descs, d_pool);
 }
 

@@ -38,6 +38,7 @@ def _frames():
     imgs = synthetic_images(6, 31) + synthetic_images(2, 32, hw=(333, 500)) + synthetic_images(2, 33, hw=(640, 427))
     rng = np.random.default_rng(5)
     imgs.append((rng.random((37, 53, 3)) * 255).astype(np.uint8))
+    imgs.append((rng.random((41, 66, 3)) * 255).astype(np.uint8))  # width 2 mod 4 (the colour kernel's quads)
     return imgs
 
 
