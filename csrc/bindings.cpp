@@ -796,6 +796,7 @@ PYBIND11_MODULE(_C, m) {
              c.max_queue_delay_us = get<int64_t>(cfg, "max_queue_delay_us", c.max_queue_delay_us);
              c.idle_queue_delay_us = get<int64_t>(cfg, "idle_queue_delay_us", c.idle_queue_delay_us);
              c.max_queue_size = get<int64_t>(cfg, "max_queue_size", c.max_queue_size);
+             c.overlap = get<int>(cfg, "overlap", c.overlap);
              return new DynamicBatcher(inst, c);
            }),
            py::keep_alive<1, 2>())

@@ -54,6 +54,11 @@ struct BatcherConfig {
   // the single-request latency low while a longer max_queue_delay_us still grows the batches once the device
   // is busy (arrivals during device work merge into the next batch).
   int64_t idle_queue_delay_us = -1;
+  // While a batch is in flight and a slot is free: 0 = collect (wait for) the oldest batch first, arrivals merge
+  // into the batch after it; 1 = admit a batch as soon as it is due (max_queue_delay_us / size) into the free
+  // slot, so batches overlap on the device (instances that answer BatchInstance::ready).  -1 = ARENA_BATCH_OVERLAP
+  // from the environment (default 0).
+  int overlap = -1;
 };
 
 struct BatcherStats {
@@ -102,7 +107,10 @@ class DynamicBatcher {
   using Batch = std::vector<std::unique_ptr<Request>>;
 
   void instance_loop(int idx);
-  bool take_batch(Batch& out, bool can_wait);
+  // can_wait: block until a batch is due.  Otherwise, with `until` in the future, wait for new requests or the
+  // queue delay to expire up to that time; return false when nothing is due by then.
+  bool take_batch(Batch& out, bool can_wait,
+                  std::chrono::steady_clock::time_point until = std::chrono::steady_clock::time_point::min());
   void finish(Batch& batch, const BatchResult& r, std::chrono::steady_clock::time_point t_submit, size_t raw_bytes);
   void fail(Batch& batch, const std::string& err);
 
@@ -113,6 +121,7 @@ class DynamicBatcher {
   std::deque<std::unique_ptr<Request>> q_;
   bool stop_ = false;
   int64_t staging_cap_ = 0;  // smallest staging capacity of the instances (0 = unlimited)
+  bool overlap_ = false;     // BatcherConfig::overlap resolved
   int64_t next_id_ = 1;
   BatcherStats stats_;
   std::vector<std::thread> threads_;

@@ -88,6 +88,20 @@ class EchoInstance : public BatchInstance {
     return s;
   }
 
+  // completion tests as the Executor answers them (the batcher's interruptible wait runs on CPU too)
+  int ready(int slot) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (slot < 0 || slot >= slots_ || !busy_[slot]) return 1;
+    return std::chrono::steady_clock::now() >= t_submit_[slot] + std::chrono::microseconds(latency_us_) ? 1 : 0;
+  }
+  double remaining_us(int slot) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (slot < 0 || slot >= slots_ || !busy_[slot]) return 0.0;
+    return std::chrono::duration<double, std::micro>(t_submit_[slot] + std::chrono::microseconds(latency_us_) -
+                                                     std::chrono::steady_clock::now())
+        .count();
+  }
+
   BatchResult collect(int slot) override {
     std::chrono::steady_clock::time_point due;
     {

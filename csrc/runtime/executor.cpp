@@ -1186,6 +1186,7 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   buckets_.at(B).last_slot = s;
   ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
   sl.t_submit = std::chrono::steady_clock::now();
+  sl.polled = false;
   sl.busy = true;
   sl.bucket = B;
   sl.n_images = n;
@@ -1201,20 +1202,27 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
 //     ARENA_POLL_US (default 20) with 1 us timer slack: ~no CPU while the device works, detection within ~30 us;
 //   poll: query + fixed ARENA_POLL_US sleeps (default 50);  spin / blocking: hipEventSynchronize (blocking: the
 //     event was created with hipEventBlockingSync).
-void Executor::wait_done(Slot& sl) {
-  enum Mode { kAdaptive, kPoll, kHip };
-  static const Mode mode = [] {
+namespace {
+enum SyncMode { kAdaptive, kPoll, kHip };
+SyncMode sync_mode() {
+  static const SyncMode mode = [] {
     const char* e = std::getenv("ARENA_SYNC");
     const std::string v = e != nullptr ? e : "adaptive";
     return v == "poll" ? kPoll : (v == "spin" || v == "blocking") ? kHip : kAdaptive;
   }();
+  return mode;
+}
+}  // namespace
+
+void Executor::wait_done(Slot& sl) {
+  const SyncMode mode = sync_mode();
   if (mode == kHip) {
     ARENA_HIP_CHECK(hipEventSynchronize(sl.done));
     return;
   }
   static const int poll_us = [] {
     const char* u = std::getenv("ARENA_POLL_US");
-    return std::max(1, u != nullptr ? std::atoi(u) : (mode == kPoll ? 50 : 20));
+    return std::max(1, u != nullptr ? std::atoi(u) : (sync_mode() == kPoll ? 50 : 20));
   }();
   thread_local bool slack_set = false;
   if (!slack_set) {
@@ -1224,22 +1232,55 @@ void Executor::wait_done(Slot& sl) {
   hipError_t q = hipEventQuery(sl.done);
   if (q != hipErrorNotReady) {
     ARENA_HIP_CHECK(q);
-    return;  // already complete (collect came late): no sample for the estimate
+    if (sl.polled) note_done(sl);  // the batcher's completion tests saw it running: a real sample
+    return;
   }
-  using clk = std::chrono::steady_clock;
-  const int B = std::min(std::max(sl.bucket, 0), kMaxEstBuckets - 1);
-  const float est = wall_est_us_[B].load(std::memory_order_relaxed);
-  if (mode == kAdaptive && est > 0.f) {
+  sl.polled = true;
+  if (mode == kAdaptive) {
     constexpr double kMarginUs = 150.0;  // wake this early: sleep overshoot and estimate noise
-    const double elapsed = std::chrono::duration<double, std::micro>(clk::now() - sl.t_submit).count();
-    const double nap = (double)est - elapsed - kMarginUs;
+    const double nap = remaining_us(sl.idx) - kMarginUs;
     if (nap > 2.0 * poll_us) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)nap));
   }
   while ((q = hipEventQuery(sl.done)) == hipErrorNotReady)
     std::this_thread::sleep_for(std::chrono::microseconds(poll_us));
   ARENA_HIP_CHECK(q);
+  note_done(sl);
+}
+
+// Completion-time sample of a batch that was seen running: EWMA per bucket of submit -> observed completion,
+// quick to follow faster batches (a late estimate makes the wait oversleep) and slow to follow slower ones.
+void Executor::note_done(Slot& sl) {
+  using clk = std::chrono::steady_clock;
+  const int B = std::min(std::max(sl.bucket, 0), kMaxEstBuckets - 1);
+  const float est = wall_est_us_[B].load(std::memory_order_relaxed);
   const float seen = (float)std::chrono::duration<double, std::micro>(clk::now() - sl.t_submit).count();
-  wall_est_us_[B].store(est > 0.f ? 0.8f * est + 0.2f * seen : seen, std::memory_order_relaxed);
+  const float a = seen < est ? 0.5f : 0.1f;
+  wall_est_us_[B].store(est > 0.f ? (1.f - a) * est + a * seen : seen, std::memory_order_relaxed);
+  sl.polled = false;
+}
+
+int Executor::ready(int s) {
+  if (s < 0 || s >= n_slots_ || sync_mode() == kHip) return -1;  // spin / blocking: the batcher just collects
+  Slot& sl = slots_[s];
+  if (!sl.busy) return 1;
+  const hipError_t q = hipEventQuery(sl.done);
+  if (q == hipErrorNotReady) {
+    sl.polled = true;
+    return 0;
+  }
+  (void)hipGetLastError();
+  if (q == hipSuccess && sl.polled) note_done(sl);
+  return 1;  // done, or an error collect() reports
+}
+
+double Executor::remaining_us(int s) {
+  if (s < 0 || s >= n_slots_) return 0.0;
+  const Slot& sl = slots_[s];
+  const int B = std::min(std::max(sl.bucket, 0), kMaxEstBuckets - 1);
+  const float est = wall_est_us_[B].load(std::memory_order_relaxed);
+  if (est <= 0.f) return 0.0;
+  return (double)est -
+         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - sl.t_submit).count();
 }
 
 BatchResult Executor::collect(int s) {
@@ -1358,6 +1399,7 @@ int Executor::submit_peer(Executor& src, int src_slot) {
   bk.last_slot = s;
   ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
   sl.t_submit = std::chrono::steady_clock::now();
+  sl.polled = false;
   sl.busy = true;
   sl.bucket = B;
   sl.n_images = ss.n_images;
@@ -1457,6 +1499,7 @@ int Executor::submit_device(const std::vector<DeviceImage>& imgs, const std::vec
   bk.last_slot = s;
   ARENA_HIP_CHECK(hipEventRecord(sl.done, sl.stream));
   sl.t_submit = std::chrono::steady_clock::now();
+  sl.polled = false;
   sl.busy = true;
   sl.bucket = B;
   sl.n_images = n;

@@ -142,6 +142,8 @@ class Executor : public BatchInstance {
   // when a batch produced more crops than one pass holds).
   int submit(const std::vector<InputImage>& imgs) override;
   BatchResult collect(int slot) override;
+  int ready(int slot) override;
+  double remaining_us(int slot) override;
   // Convenience: submit + collect.
   BatchResult run(const std::vector<InputImage>& imgs);
 
@@ -205,6 +207,7 @@ class Executor : public BatchInstance {
     hipEvent_t fork_ev = nullptr, lane_ev[kMaxLanes] = {};
     int idx = 0;
     std::chrono::steady_clock::time_point t_submit{};  // host time of the submit (adaptive completion wait)
+    bool polled = false;  // a completion test found the batch running (its completion time is a real sample)
     bool busy = false;
     int bucket = 0;
     int n_images = 0;
@@ -233,6 +236,7 @@ class Executor : public BatchInstance {
   void free_arenas(Bucket& bk);
   void capture(Bucket& bk, int slot);
   void wait_done(Slot& sl);
+  void note_done(Slot& sl);
   void launch_graph(Bucket& bk, int slot, hipStream_t st);
   void destroy_graphs(Bucket& bk, int slot);
   bool lanes_for(const Bucket& bk) const;

@@ -61,6 +61,12 @@ class BatchInstance {
   virtual int submit(const std::vector<InputImage>& imgs) = 0;
   // Wait for a slot's batch and return its results (the slot becomes free).
   virtual BatchResult collect(int slot) = 0;
+  // Non-blocking completion test of a slot's batch: 1 done (collect will not wait), 0 still running, -1 the
+  // instance cannot tell (the batcher then collects, i.e. waits).  With 0 the batcher keeps admitting new
+  // batches into free slots while the oldest one runs.
+  virtual int ready(int slot) { (void)slot; return -1; }
+  // Estimated microseconds until a running slot's batch completes (<= 0: unknown or due now).
+  virtual double remaining_us(int slot) { (void)slot; return 0.0; }
 };
 
 }  // namespace arena

@@ -109,6 +109,12 @@ class FakeInstance : public BatchInstance {
     return s;
   }
 
+  int ready(int slot) override {  // the batcher's overlap path (non-blocking completion test)
+    CHECK(slot >= 0 && slot < slots_ && busy_[slot], "ready() of idle slot %d", slot);
+    return work_[slot].wait_for(std::chrono::seconds(0)) == std::future_status::ready ? 1 : 0;
+  }
+  double remaining_us(int) override { return 100.0; }
+
   BatchResult collect(int slot) override {
     CHECK(slot >= 0 && slot < slots_ && busy_[slot], "collect of idle slot %d", slot);
     BatchResult r = work_[slot].get();
@@ -138,7 +144,7 @@ struct Outcome {
   std::string error;
 };
 
-void run_stress() {
+void run_stress(int overlap) {
   const int producers = 8, per = 1500, max_batch = 8;
   auto a = std::make_shared<FakeInstance>(3, max_batch);
   auto b = std::make_shared<FakeInstance>(2, max_batch);
@@ -147,6 +153,7 @@ void run_stress() {
   cfg.preferred = {4, 8};
   cfg.max_queue_delay_us = 200;
   cfg.max_queue_size = 0;
+  cfg.overlap = overlap;
   std::vector<Outcome> out((size_t)producers * per);
   std::vector<uint8_t> expect(out.size());
   {
@@ -289,7 +296,8 @@ void run_staging_capacity() {
 
 int main() {
   run_staging_capacity();
-  run_stress();
+  run_stress(0);
+  run_stress(1);  // overlap: ready() tests and timed takes interleaved with collects
   run_failures_and_rejection();
   if (fails.load()) {
     std::fprintf(stderr, "batcher_stress: %d check(s) failed\n", fails.load());

@@ -102,3 +102,39 @@ def test_idle_queue_delay_applies_only_while_idle():
 
     assert lone_request_s({"max_queue_delay_us": 300000}) >= 0.25  # Triton semantics: waits for company
     assert lone_request_s({"max_queue_delay_us": 300000, "idle_queue_delay_us": 1000}) < 0.1
+
+
+def test_overlap_admits_due_batches_while_one_runs():
+    """overlap=1 (ARENA_BATCH_OVERLAP): while a batch is in flight and a slot is free, a batch that comes due is
+    submitted at once instead of waiting for the oldest batch (the instance answers ready(): EchoInstance like the
+    Executor); overlap=0 keeps the merge-behind-the-oldest behaviour."""
+    import threading
+    import time
+
+    import numpy as np
+
+    from inference_arena_amd.ops import native
+
+    C = native()
+    img = np.full((8, 8, 3), 7, np.uint8)
+
+    def run(overlap):
+        b = C.DynamicBatcher([C.EchoInstance(4, 8, 4, 50000)],
+                             {"max_batch": 8, "max_queue_delay_us": 500, "overlap": overlap})
+        done = threading.Semaphore(0)
+        t0 = time.perf_counter()
+        for _ in range(4):
+            assert b.enqueue(img, lambda d: done.release()) >= 0
+            time.sleep(0.005)
+        for _ in range(4):
+            assert done.acquire(timeout=10)
+        elapsed = time.perf_counter() - t0
+        hist = b.stats()["batch_hist"]
+        b.shutdown()
+        return elapsed, [n for n, c in enumerate(hist) for _ in range(c)]
+
+    t_on, sizes_on = run(1)
+    t_off, sizes_off = run(0)
+    assert sizes_on == [1, 1, 1, 1], sizes_on  # four overlapping batches
+    assert len(sizes_off) == 2, sizes_off     # the first alone, the rest merged behind it
+    assert t_on < 0.09 and t_off >= 0.095, (t_on, t_off)
