@@ -80,8 +80,10 @@ class GpuBatchedBackend(Backend):
         self.devices = [int(d) for d in (devices or [device])]
         self.pipes = [build_session("pipeline", yolo, mnet, device=d, buckets=bk, weights=weights)
                       for d in self.devices for _ in range(instances)]
+        # one process per GPU (the monolithic arm): batches overlap in the free slots (native_front.py)
         self.batcher = AsyncBatcher(self.pipes, max_batch=max_batch, preferred=preferred,
-                                    max_queue_delay_us=max_queue_delay_us, max_queue_size=max_queue_size)
+                                    max_queue_delay_us=max_queue_delay_us, max_queue_size=max_queue_size,
+                                    overlap=int(os.environ.get("ARENA_BATCH_OVERLAP", "1")))
         self.device = device
 
     def ready(self) -> bool:

@@ -40,7 +40,8 @@ def is_device_fault(message: str) -> bool:
 
 class AsyncBatcher:
     def __init__(self, runners, *, max_batch: int, preferred: list[int] | None = None,
-                 max_queue_delay_us: int = 500, max_queue_size: int = 4096, idle_queue_delay_us: int = -1):
+                 max_queue_delay_us: int = 500, max_queue_size: int = 4096, idle_queue_delay_us: int = -1,
+                 overlap: int = -1):
         from ..ops import native
 
         self.runners = list(runners)
@@ -51,6 +52,7 @@ class AsyncBatcher:
             "max_queue_delay_us": int(max_queue_delay_us),
             "max_queue_size": int(max_queue_size),
             "idle_queue_delay_us": int(idle_queue_delay_us),  # -1: max_queue_delay_us (batcher.h)
+            "overlap": int(overlap),  # -1: ARENA_BATCH_OVERLAP (default 0); batcher.h BatcherConfig.overlap
         })
         self._closed = False
         self.device_error: str | None = None  # first HIP error seen; the instance is unhealthy from then on
