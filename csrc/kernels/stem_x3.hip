@@ -37,12 +37,17 @@ constexpr int SX_TW = 16;                   // output columns per tile
 constexpr int SX_SC = 2 * SX_TW + 1;        // stem columns per tile (33)
 constexpr int SX_SCS = 2 * ((SX_SC + 1) / 2);  // stored stem columns: 17 even, then 16 odd + 1 pad (34)
 constexpr int SX_IC = SX_SC + 2;            // s2d input columns (35)
-constexpr int SX_IP = 24;                   // bf16 per input pixel: 16 channels + 8 pad (48 B, 3 slots)
+// LDS strides, chosen with a bank model of the three access patterns (ds_read_b128 lane groups, 64 banks; wide
+// writes, 32 banks): 32-B input pixels (no pad) make the stem GEMM's fragment reads 1.5-way instead of 2.3-way,
+// and 16 bf16 of pad per stored stem row make the stride-2 conv's reads conflict-free (were 2-way: the two output
+// rows of a fragment sat 68 pixel slots apart, i.e. 48 banks)
+constexpr int SX_IP = 16;                   // bf16 per input pixel: 12 s2d channels + 4 zero (32 B)
 constexpr int SX_SP = 56;                   // bf16 per stem pixel: 3 planes x 16 channels + 8 pad (112 B)
+constexpr int SX_SRS = SX_SCS * SX_SP + 16; // bf16 per stored stem row
 
 __host__ __device__ constexpr int sx_sr(int TH) { return 2 * TH + 1; }  // stem rows per tile
 __host__ __device__ constexpr int sx_lds_bytes(int TH) {
-  return ((sx_sr(TH) + 2) * SX_IC * SX_IP + sx_sr(TH) * SX_SCS * SX_SP) * 2;
+  return ((sx_sr(TH) + 2) * SX_IC * SX_IP + sx_sr(TH) * SX_SRS) * 2;
 }
 
 __device__ __forceinline__ int sx_xcd_remap(int bx, int nx) {
@@ -62,7 +67,7 @@ __global__ __launch_bounds__(NW * 64) void stem_s2_x3_kernel(const StemFusedPara
   static_assert(TH % 2 == 0, "output fragments are two rows");
   extern __shared__ __attribute__((aligned(16))) bf16 sx_lds[];
   bf16* sIn = sx_lds;                        // [IR][35][SX_IP]
-  bf16* sSt = sx_lds + IR * SX_IC * SX_IP;   // [SR][34][SX_SP]
+  bf16* sSt = sx_lds + IR * SX_IC * SX_IP;   // [SR][SX_SRS]: 34 pixels of SX_SP + pad
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int T2 = p.S / 2, Ho = p.S / 4, Wo = p.S / 4;  // s2d / stem map side, output side
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(NW * 64) void stem_s2_x3_kernel(const StemFusedPara
         m[e] = tm;
         l[e] = (bf16)(rr - (float)tm);
       }
-      bf16* d = sSt + (sr * SX_SCS + (sc & 1) * (SX_SCS / 2) + (sc >> 1)) * SX_SP + 4 * kq;
+      bf16* d = sSt + sr * SX_SRS + ((sc & 1) * (SX_SCS / 2) + (sc >> 1)) * SX_SP + 4 * kq;
       *(bf16x4*)d = h;
       *(bf16x4*)(d + 16) = m;
       *(bf16x4*)(d + 32) = l;
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(NW * 64) void stem_s2_x3_kernel(const StemFusedPara
       const int ky = tap / 3, kx = tap - ky * 3;
       const bf16x8 wh = bwh[tap], wm = bwm[tap], wl = bwl[tap];
       const int sr = 2 * r + ky, sc = 2 * c + kx;
-      const bf16* xr = sSt + (sr * SX_SCS + (sc & 1) * (SX_SCS / 2) + (sc >> 1)) * SX_SP + 8 * fh;
+      const bf16* xr = sSt + sr * SX_SRS + ((sc & 1) * (SX_SCS / 2) + (sc >> 1)) * SX_SP + 8 * fh;
       const bf16x8 xh = *(const bf16x8*)xr, xm = *(const bf16x8*)(xr + 16), xl = *(const bf16x8*)(xr + 32);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, xm, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc, 0, 0, 0);
