@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Host memory growth of the native serving path per request, without a GPU.
+
+The protocol summaries showed the arms' resident memory rising run after run (monolithic: ~1.3 KB per request over
+a 60 s x 3 x 7-level sweep, profiles/protocol_r5/*_summary.json memory_usage_mb).  This drives the native HTTP front
+end (split JPEG decoder threads, DynamicBatcher) over the host-only EchoInstance with the native closed-loop load
+generator, in rounds, and prints the process's RSS after each round: a flat line after the first rounds (pools
+and caches at their high-water mark) is healthy, a steady slope is a leak of that many bytes per request.
+
+usage: python tools/leak_probe.py [--rounds 8] [--per-round 20000] [--users 32]
+"""
+from __future__ import annotations
+
+import argparse
+import io
+import os
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+
+def rss_mb(pid: int | None = None) -> float:
+    with open(f"/proc/{pid or os.getpid()}/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1]) / 1024.0
+    return 0.0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--per-round", type=int, default=20000)
+    ap.add_argument("--users", type=int, default=32)
+    ap.add_argument("--decode-threads", type=int, default=4)
+    a = ap.parse_args(argv)
+
+    import numpy as np
+    from PIL import Image
+
+    from inference_arena_amd.ops import native
+    from inference_arena_amd.server.native_front import NativeFrontEnd
+    from inference_arena_amd.labels import load_labels
+
+    C = native()
+    batcher = C.DynamicBatcher([C.EchoInstance(4, 32, 4, 500)], {"max_batch": 32, "max_queue_delay_us": 300})
+    fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=2, decode_procs=1,
+                        slots=64, decode_threads=a.decode_threads, jpeg_device=False)
+    rng = np.random.default_rng(0)
+    reqs = []
+    for i in range(8):
+        b = io.BytesIO()
+        Image.fromarray((rng.random((120 + 8 * i, 160, 3)) * 255).astype(np.uint8)).save(b, "JPEG", quality=90)
+        data = b.getvalue()
+        bnd = "leakprobe"
+        body = (f"--{bnd}\r\nContent-Disposition: form-data; name=\"file\"; filename=\"x.jpg\"\r\n"
+                f"Content-Type: image/jpeg\r\n\r\n").encode() + data + f"\r\n--{bnd}--\r\n".encode()
+        reqs.append((f"POST /predict HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: multipart/form-data; "
+                     f"boundary={bnd}\r\nContent-Length: {len(body)}\r\n\r\n").encode() + body)
+    base = None
+    done = 0
+    try:
+        for r in range(a.rounds):
+            lg = C.HttpLoadGen({"host": "127.0.0.1", "port": fe.port, "users": a.users, "threads": 2}, reqs)
+            t0 = time.perf_counter()
+            lg.start()
+            ok = lg.wait_completed(a.per_round, 600)
+            lg.stop(30)
+            n = lg.completed()
+            del lg  # its per-request records are freed with it
+            done += n
+            m = rss_mb()
+            base = m if base is None else base
+            print(f"round {r}: {n} requests ({n / (time.perf_counter() - t0):.0f}/s), rss {m:.1f} MB, "
+                  f"growth since round 0 {(m - base) * 1024 * 1024 / max(1, done - a.per_round):.0f} B/request"
+                  + ("" if ok else " (timeout)"), flush=True)
+    finally:
+        fe.close()
+        batcher.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
