@@ -71,7 +71,8 @@ class GpuBatchedBackend(Backend):
     def __init__(self, yolo, mnet, *, device: int = 0, instances: int = 1, max_batch: int = 32,
                  preferred: list[int] | None = None, max_queue_delay_us: int = 500, max_queue_size: int = 4096,
                  buckets: list[int] | None = None, weights: np.ndarray | None = None,
-                 devices: list[int] | None = None):
+                 devices: list[int] | None = None, overlap: int | None = None,
+                 idle_queue_delay_us: int | None = None):
         """``instances`` pipelines on each GPU of ``devices`` (default: ``[device]``) behind one batcher queue:
         each instance thread pulls the next batch for its own GPU (data parallel within one process)."""
         from ..engine.registry import build_session
@@ -80,10 +81,16 @@ class GpuBatchedBackend(Backend):
         self.devices = [int(d) for d in (devices or [device])]
         self.pipes = [build_session("pipeline", yolo, mnet, device=d, buckets=bk, weights=weights)
                       for d in self.devices for _ in range(instances)]
-        # one process per GPU (the monolithic arm): batches overlap in the free slots (native_front.py)
+        # overlap (None: ARENA_BATCH_OVERLAP, default on): batches overlap in the free slots — right for one
+        # process per GPU (the monolithic arm, native_front.py); the model server's ensemble passes 0 (three
+        # processes per GPU: profiles/r5_serving/README.md)
+        if overlap is None:
+            overlap = int(os.environ.get("ARENA_BATCH_OVERLAP", "1"))
+        if idle_queue_delay_us is None:
+            idle_queue_delay_us = int(os.environ.get("ARENA_IDLE_QUEUE_DELAY_US", "100"))
         self.batcher = AsyncBatcher(self.pipes, max_batch=max_batch, preferred=preferred,
                                     max_queue_delay_us=max_queue_delay_us, max_queue_size=max_queue_size,
-                                    overlap=int(os.environ.get("ARENA_BATCH_OVERLAP", "1")))
+                                    overlap=int(overlap), idle_queue_delay_us=int(idle_queue_delay_us))
         self.device = device
 
     def ready(self) -> bool:

@@ -169,6 +169,9 @@ def serve(settings: Settings | None = None, *, weights=None, replica_tag: str = 
              for _ in range(instances)]
     batcher = native().DynamicBatcher([p.ex for p in pipes], {
         "max_batch": max_batch, "max_queue_delay_us": int(settings.ARENA_QUEUE_DELAY_US),
+        # a lone request on an idle device is not held for the full queue delay (bench.py batcher_config; the
+        # protocol's 1-user level paid 0.51 ms of queue per request without it, profiles/protocol_r5/)
+        "idle_queue_delay_us": int(os.environ.get("ARENA_IDLE_QUEUE_DELAY_US", "100")),
         "max_queue_size": int(os.environ.get("ARENA_MAX_QUEUE", "4096")),
         # one process per GPU: admit due batches into free slots while older ones run (100 users: 8.4k vs 6.8k
         # req/s, profiles/r5ov/); the Triton arm's three model-server processes per GPU keep it off
