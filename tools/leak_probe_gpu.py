@@ -33,7 +33,7 @@ def rss_mb() -> float:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--modes", default="replay,submit,jpeg,batcher")
+    ap.add_argument("--modes", default="batcher,jpeg,submit,replay")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--batches", type=int, default=400)
     ap.add_argument("--batch", type=int, default=8)
@@ -63,7 +63,7 @@ def main(argv=None) -> int:
                 ex.collect(ex.submit(imgs))
         elif mode == "jpeg":
             for _ in range(n):
-                ex.collect(ex.submit_jpeg_set(jset))
+                ex.collect(ex.submit_jpeg_set(jset, list(range(a.batch))))
         elif mode == "batcher":
             b = C.DynamicBatcher([ex], {"max_batch": a.batch, "max_queue_delay_us": 200})
             sem = threading.Semaphore(0)
@@ -75,7 +75,11 @@ def main(argv=None) -> int:
             b.shutdown()
 
     for mode in a.modes.split(","):
-        run(mode, 20)  # warm-up: pools and caches reach their working size
+        try:
+            run(mode, 20)  # warm-up: pools and caches reach their working size
+        except Exception as e:  # noqa: BLE001 - report and go on with the next mode
+            print(f"{mode}: failed: {e}", flush=True)
+            continue
         base = rss_mb()
         for r in range(a.rounds):
             t0 = time.perf_counter()
