@@ -9,6 +9,7 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <malloc.h>
 #include <map>
 #include <mutex>
 
@@ -543,6 +544,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("install_crash_trace", &arena::install_crash_trace);
   m.def("crash_trace_installed", &arena::crash_trace_installed);
   m.def("dump_thread_stack", &arena::dump_thread_stack, py::arg("tid"));
+  // glibc: hand free heap pages of every arena back to the kernel (buffers allocated on one thread and freed on
+  // another leave per-thread arenas holding pages; the serving processes call this periodically)
+  m.def("malloc_trim", []() {
+    py::gil_scoped_release nogil;
+    return malloc_trim(0) != 0;
+  });
   bind_jpeg(m);
   m.def("conv2d", &py_conv2d);
   m.def("set_conv_impl", &set_conv_impl);

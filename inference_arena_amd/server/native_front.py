@@ -133,11 +133,22 @@ class NativeFrontEnd:
         self.fe.set_healthy(bool(ok))
 
     def _refresh(self) -> None:
+        # ARENA_MALLOC_TRIM_S (default 10, 0 = off): return free heap pages to the kernel periodically.  Buffers
+        # allocated on the decode / I/O threads and freed on the batcher thread otherwise leave glibc's per-thread
+        # arenas holding pages, and the resident size of a long-running server creeps up run after run
+        # (profiles/protocol_r5 memory_usage_mb, tools/leak_probe_gpu.py).
+        trim_s = float(os.environ.get("ARENA_MALLOC_TRIM_S", "10"))
+        last_trim = time.monotonic()
+        from ..ops import native
+
         while not self._stop.is_set():
             try:
                 self.fe.set_metrics_text(generate_latest(self.registry).decode())
             except Exception as e:  # noqa: BLE001 - metrics must never stop the server
                 log.warning(f"metrics refresh failed: {e}")
+            if trim_s > 0 and time.monotonic() - last_trim >= trim_s:
+                native().malloc_trim()
+                last_trim = time.monotonic()
             self._stop.wait(1.0)
 
     def close(self) -> None:

@@ -71,9 +71,9 @@ def main(argv=None) -> int:
     lines.append(f"\nshared engine (kernels, runtime, planner): {out['rq3']['shared_engine_loc']} LOC")
     if deploy:
         lines += ["", "| arch | deployment time s (mean of runs) | runs | idle RSS MiB |", "|---|---|---|---|"]
-        for arm, d in deploy.items():
-            lines.append(f"| {arm} | {d['deployment_time_seconds']:.2f} | {d.get('runs')} | "
-                         f"{d.get('baseline_memory_mb', float('nan')):.0f} |")
+        for arm, dt in deploy.items():
+            lines.append(f"| {arm} | {dt['deployment_time_seconds']:.2f} | {dt.get('runs')} | "
+                         f"{dt.get('baseline_memory_mb', float('nan')):.0f} |")
     lines += ["", "| hypothesis | supported | evidence |", "|---|---|---|"]
     for h in sorted(hyp):
         ev = {k: v for k, v in hyp[h].items() if k != "supported"}

@@ -6,6 +6,9 @@ import os
 import time
 
 import pytest
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
 
 from inference_arena_amd.analysis.rq import complexity_report, cost_per_1000_requests, count_loc, enrich_sweep_rows
 
@@ -173,3 +176,34 @@ def test_deploy_time_with_a_fake_launcher(tmp_path):
     assert len(r["runs"]) == 2 and all(0.5 <= t < 5 for t in r["runs"])
     assert r["baseline_memory_mb"] > 15  # the child's 20 MiB buffer is resident
     assert all(p.poll() is not None for p in started)
+
+
+def test_analyze_results_script_with_deploy_times(tmp_path):
+    """scripts/analyze_results.py end to end on sweep CSVs split over several files (one per call of a sweep) plus
+    a scripts/deploy_time.py JSON: H1-H3, the deployment-time table and the RQ4 decision matrix are written."""
+    import csv
+    import importlib.util
+    import json
+
+    rows = _rows()
+    files = []
+    for i, part in enumerate((rows[: len(rows) // 2], rows[len(rows) // 2:])):
+        f = tmp_path / f"sweep_{i}.csv"
+        with open(f, "w", newline="") as fh:
+            w = csv.DictWriter(fh, fieldnames=list(part[0]))
+            w.writeheader()
+            w.writerows(part)
+        files.append(str(f))
+    deploy = {a: {"deployment_time_seconds": t, "runs": [t, t, t], "baseline_memory_mb": m, "gpus": 1}
+              for a, t, m in (("monolithic", 2.7, 2100.0), ("microservices", 3.5, 4500.0), ("triton", 5.0, 4000.0))}
+    (tmp_path / "deploy.json").write_text(json.dumps(deploy))
+    spec = importlib.util.spec_from_file_location("analyze_results", ROOT / "scripts" / "analyze_results.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = tmp_path / "analysis"
+    assert mod.main([*files, "--deploy", str(tmp_path / "deploy.json"), "--gpus", "1", "--out", str(out)]) == 0
+    text = (out / "summary.md").read_text()
+    assert "deployment time s" in text and "| triton | 5.00 |" in text
+    assert "H3c" in text and "H1a" in text and "RQ4 crossover points" in text
+    summary = json.loads((out / "summary.json").read_text())
+    assert summary["rq3"]["triton"]["deployment_time_seconds"] == 5.0

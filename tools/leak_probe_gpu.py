@@ -37,6 +37,7 @@ def main(argv=None) -> int:
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--batches", type=int, default=400)
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--trim", action="store_true", help="malloc_trim after each round (fragmentation vs leak)")
     a = ap.parse_args(argv)
 
     import numpy as np
@@ -85,6 +86,9 @@ def main(argv=None) -> int:
             t0 = time.perf_counter()
             run(mode, a.batches)
             m = rss_mb()
+            if a.trim:
+                C.malloc_trim()
+                print(f"{mode} round {r}: after malloc_trim rss {rss_mb():.1f} MB", flush=True)
             print(f"{mode} round {r}: {a.batches} batches in {time.perf_counter() - t0:.2f} s, rss {m:.1f} MB, "
                   f"{(m - base) * 1024 * 1024 / ((r + 1) * a.batches):.0f} B/batch since warm-up", flush=True)
     return 0
