@@ -272,9 +272,11 @@ void DynamicBatcher::instance_loop(int idx) {
       // completion (sleeping until shortly before its expected end, then polling every kPollUs).
       const int rd = overlap_ ? ex.ready(pending.front().slot) : -1;
       if (rd == 0) {
-        constexpr double kPollUs = 20.0, kMarginUs = 120.0;
-        const double rem = ex.remaining_us(pending.front().slot) - kMarginUs;
-        const auto until = clk::now() + std::chrono::microseconds((int64_t)std::max(kPollUs, rem));
+        // naps of half the expected remaining time, 20-200 us (Executor::wait_done): an early completion is
+        // seen within one nap, and a new arrival ends the nap at once (take_batch waits on the queue)
+        constexpr double kPollUs = 20.0, kMaxNapUs = 200.0;
+        const double nap = std::min(kMaxNapUs, std::max(kPollUs, 0.5 * ex.remaining_us(pending.front().slot)));
+        const auto until = clk::now() + std::chrono::microseconds((int64_t)nap);
         if (take_batch(b, false, until)) {
           std::vector<InputImage> imgs;
           imgs.reserve(b.size());

@@ -1197,9 +1197,9 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
 // Completion wait of a slot's batch.  HIP's hipEventSynchronize keeps the waiting thread busy for the whole
 // device time of the batch (a core per batcher thread at load; a blocking-sync event did not change that:
 // profiles/r5triton2/).  ARENA_SYNC selects:
-//   adaptive (default): sleep until shortly before the batch's expected completion (an EWMA per bucket of
-//     submit -> observed completion, updated only when the wait was real), then query the event every
-//     ARENA_POLL_US (default 20) with 1 us timer slack: ~no CPU while the device works, detection within ~30 us;
+//   adaptive (default): naps of half the expected remaining time (an estimate per bucket of submit -> observed
+//     completion), 20 (ARENA_POLL_US) to 200 us, 1 us timer slack: little CPU while the device works, an early
+//     completion seen within one nap, the last stretch polled every 20 us;
 //   poll: query + fixed ARENA_POLL_US sleeps (default 50);  spin / blocking: hipEventSynchronize (blocking: the
 //     event was created with hipEventBlockingSync).
 namespace {
@@ -1236,26 +1236,37 @@ void Executor::wait_done(Slot& sl) {
     return;
   }
   sl.polled = true;
-  if (mode == kAdaptive) {
-    constexpr double kMarginUs = 150.0;  // wake this early: sleep overshoot and estimate noise
-    const double nap = remaining_us(sl.idx) - kMarginUs;
-    if (nap > 2.0 * poll_us) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)nap));
+  sl.t_poll = std::chrono::steady_clock::now();
+  // Naps toward the expected completion: half the remaining estimate, between ARENA_POLL_US and kMaxNapUs.  A
+  // batch that ends earlier than expected is seen within one nap (<= kMaxNapUs late), and the estimate cannot
+  // feed on its own oversleeping: a completion seen after a long nap only bounds the true time (note_done).
+  constexpr double kMaxNapUs = 200.0;
+  while ((q = hipEventQuery(sl.done)) == hipErrorNotReady) {
+    double nap = poll_us;
+    if (mode == kAdaptive) nap = std::min(kMaxNapUs, std::max((double)poll_us, 0.5 * remaining_us(sl.idx)));
+    sl.t_poll = std::chrono::steady_clock::now();
+    std::this_thread::sleep_for(std::chrono::microseconds((int64_t)nap));
   }
-  while ((q = hipEventQuery(sl.done)) == hipErrorNotReady)
-    std::this_thread::sleep_for(std::chrono::microseconds(poll_us));
   ARENA_HIP_CHECK(q);
   note_done(sl);
 }
 
-// Completion-time sample of a batch that was seen running: EWMA per bucket of submit -> observed completion,
-// quick to follow faster batches (a late estimate makes the wait oversleep) and slow to follow slower ones.
+// Completion-time sample of a batch that was seen running (submit -> observed completion), per bucket.  When the
+// previous "still running" observation is recent (<= 50 us) the sample is precise and enters an EWMA; after a
+// longer gap it is only an upper bound and may lower the estimate, never raise it (otherwise a late wake-up would
+// teach the next wait to sleep as long, and the estimate would feed on itself).
 void Executor::note_done(Slot& sl) {
   using clk = std::chrono::steady_clock;
+  const auto now = clk::now();
   const int B = std::min(std::max(sl.bucket, 0), kMaxEstBuckets - 1);
   const float est = wall_est_us_[B].load(std::memory_order_relaxed);
-  const float seen = (float)std::chrono::duration<double, std::micro>(clk::now() - sl.t_submit).count();
-  const float a = seen < est ? 0.5f : 0.1f;
-  wall_est_us_[B].store(est > 0.f ? (1.f - a) * est + a * seen : seen, std::memory_order_relaxed);
+  const float seen = (float)std::chrono::duration<double, std::micro>(now - sl.t_submit).count();
+  const bool precise = std::chrono::duration<double, std::micro>(now - sl.t_poll).count() <= 50.0;
+  float upd;
+  if (est <= 0.f) upd = seen;
+  else if (precise) upd = 0.8f * est + 0.2f * seen;
+  else upd = std::min(est, seen);
+  wall_est_us_[B].store(upd, std::memory_order_relaxed);
   sl.polled = false;
 }
 
@@ -1266,6 +1277,7 @@ int Executor::ready(int s) {
   const hipError_t q = hipEventQuery(sl.done);
   if (q == hipErrorNotReady) {
     sl.polled = true;
+    sl.t_poll = std::chrono::steady_clock::now();
     return 0;
   }
   (void)hipGetLastError();

@@ -208,6 +208,7 @@ class Executor : public BatchInstance {
     int idx = 0;
     std::chrono::steady_clock::time_point t_submit{};  // host time of the submit (adaptive completion wait)
     bool polled = false;  // a completion test found the batch running (its completion time is a real sample)
+    std::chrono::steady_clock::time_point t_poll{};  // last completion test that found it running
     bool busy = false;
     int bucket = 0;
     int n_images = 0;
