@@ -141,10 +141,15 @@ void head_pool(const HeadPoolParams& p, hipStream_t s) {
 // block (the workgroup's fixed cost) is shared by twice the channels of a 4-wave workgroup.
 constexpr int kNSF = 256, kHeadF32Threads = 512;
 
+// The split pixel block is staged in two K halves of 160 channels (64 rows x 992 B = 62 KiB, a pitch of 2 (mod 4)
+// 16-B slots): two workgroups fit a CU instead of one (the whole-K block took 122 KiB), so one workgroup's staging
+// and its weight-load latency overlap the other's MFMAs.
 template <int KSLABS>
 __global__ __launch_bounds__(kHeadF32Threads) void head_pool_f32_kernel(const HeadPoolParams p) {
   constexpr int K = KSLABS * 32;
-  constexpr int PITCH = 6 * K + 32;  // bytes per staged pixel row: three bf16 planes + pad
+  static_assert(KSLABS % 2 == 0, "two K halves of whole slabs");
+  constexpr int KH = K / 2, SH = KSLABS / 2;  // channels / slabs per staged half
+  constexpr int PITCH = 6 * KH + 32;          // bytes per staged pixel row: three bf16 planes + pad
   extern __shared__ __align__(16) uint8_t xsf[];
 
   const int nslices = (p.N + kNSF - 1) / kNSF;
@@ -169,29 +174,31 @@ __global__ __launch_bounds__(kHeadF32Threads) void head_pool_f32_kernel(const He
   };
   load_w(0);
 
-  // ---- stage the crop's pixels as split planes (pixels HW..63 and channels past K are zero)
   const float* xb = (const float*)p.x + (size_t)b * p.HW * p.xs;
-  constexpr int CPR = K / 4;
-  for (int i = tid; i < kMaxHW * CPR; i += kHeadF32Threads) {
-    const int px = i / CPR, c = i - px * CPR;
-    const bool ok = px < p.HW && c * 4 < p.K;
-    float4 v = *(const float4*)(ok ? xb + (size_t)px * p.xs + c * 4 : xb);
-    if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float f[4] = {v.x, v.y, v.z, v.w};
-    bf16x4 h, m, l;
+  constexpr int CPR = KH / 4;
+  // stage K half h of the crop's pixels as split planes (pixels HW..63 and channels past K are zero)
+  auto stage = [&](int h) {
+    for (int i = tid; i < kMaxHW * CPR; i += kHeadF32Threads) {
+      const int px = i / CPR, c = i - px * CPR;
+      const int ch = h * KH + c * 4;
+      const bool ok = px < p.HW && ch < p.K;
+      float4 v = *(const float4*)(ok ? xb + (size_t)px * p.xs + ch : xb);
+      if (!ok) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float f[4] = {v.x, v.y, v.z, v.w};
+      bf16x4 hh, m, l;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      h[j] = (bf16)f[j];
-      const float r = f[j] - (float)h[j];
-      m[j] = (bf16)r;
-      l[j] = (bf16)(r - (float)m[j]);
+      for (int j = 0; j < 4; ++j) {
+        hh[j] = (bf16)f[j];
+        const float r = f[j] - (float)hh[j];
+        m[j] = (bf16)r;
+        l[j] = (bf16)(r - (float)m[j]);
+      }
+      uint8_t* d = xsf + px * PITCH + c * 8;
+      *(bf16x4*)d = hh;
+      *(bf16x4*)(d + 2 * KH) = m;
+      *(bf16x4*)(d + 4 * KH) = l;
     }
-    uint8_t* d = xsf + px * PITCH + c * 8;
-    *(bf16x4*)d = h;
-    *(bf16x4*)(d + 2 * K) = m;
-    *(bf16x4*)(d + 4 * K) = l;
-  }
-  __syncthreads();
+  };
 
   f32x4 acc[kNF][4];
 #pragma unroll
@@ -200,33 +207,39 @@ __global__ __launch_bounds__(kHeadF32Threads) void head_pool_f32_kernel(const He
     for (int mm = 0; mm < 4; ++mm) acc[f][mm] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
-  for (int s = 0; s < KSLABS; ++s) {
-    bf16x8 ah[kNF], am[kNF], al[kNF];
-#pragma unroll
-    for (int f = 0; f < kNF; ++f) {
-      const float v[8] = {wr[f][0].x, wr[f][0].y, wr[f][0].z, wr[f][0].w, wr[f][1].x, wr[f][1].y, wr[f][1].z, wr[f][1].w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        ah[f][j] = (bf16)v[j];
-        const float r = v[j] - (float)ah[f][j];
-        am[f][j] = (bf16)r;
-        al[f][j] = (bf16)(r - (float)am[f][j]);
-      }
-    }
-    if (s + 1 < KSLABS) load_w(s + 1);  // next slab's weights in flight during this slab's MFMAs
-#pragma unroll
-    for (int mm = 0; mm < 4; ++mm) {
-      const uint8_t* r = xsf + (mm * 16 + row) * PITCH + s * 64 + kq * 16;
-      const bf16x8 bh = *(const bf16x8*)r, bm = *(const bf16x8*)(r + 2 * K), bl = *(const bf16x8*)(r + 4 * K);
+  for (int h = 0; h < 2; ++h) {
+    if (h) __syncthreads();  // every wave is done with the first half before it is replaced
+    stage(h);
+    __syncthreads();
+#pragma unroll 1
+    for (int s = h * SH; s < (h + 1) * SH; ++s) {
+      bf16x8 ah[kNF], am[kNF], al[kNF];
 #pragma unroll
       for (int f = 0; f < kNF; ++f) {
-        f32x4 c = acc[f][mm];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[f], bm, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[f], bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[f], bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bm, c, 0, 0, 0);
-        acc[f][mm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bh, c, 0, 0, 0);
+        const float v[8] = {wr[f][0].x, wr[f][0].y, wr[f][0].z, wr[f][0].w, wr[f][1].x, wr[f][1].y, wr[f][1].z, wr[f][1].w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ah[f][j] = (bf16)v[j];
+          const float r = v[j] - (float)ah[f][j];
+          am[f][j] = (bf16)r;
+          al[f][j] = (bf16)(r - (float)am[f][j]);
+        }
+      }
+      if (s + 1 < KSLABS) load_w(s + 1);  // next slab's weights in flight during this slab's MFMAs
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        const uint8_t* r = xsf + (mm * 16 + row) * PITCH + (s - h * SH) * 64 + kq * 16;
+        const bf16x8 bh = *(const bf16x8*)r, bm = *(const bf16x8*)(r + 2 * KH), bl = *(const bf16x8*)(r + 4 * KH);
+#pragma unroll
+        for (int f = 0; f < kNF; ++f) {
+          f32x4 c = acc[f][mm];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[f], bm, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[f], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[f], bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bm, c, 0, 0, 0);
+          acc[f][mm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f], bh, c, 0, 0, 0);
+        }
       }
     }
   }
@@ -259,11 +272,11 @@ __global__ __launch_bounds__(kHeadF32Threads) void head_pool_f32_kernel(const He
   }
 }
 
-constexpr int kHeadF32Lds = kMaxHW * (6 * 320 + 32);
+constexpr int kHeadF32Lds = kMaxHW * (6 * 160 + 32);  // one staged K half (head_pool_f32_kernel)
 
 void head_pool_f32_prepare() {
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)head_pool_f32_kernel<10>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kHeadF32Lds));
 }
 
 void head_pool_f32(const HeadPoolParams& p, hipStream_t s) {
