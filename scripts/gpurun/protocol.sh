@@ -17,7 +17,10 @@ mkdir -p $O
 export ARENA_SERVICE_CPUS=${ENVELOPE:-0}
 case $ARCH in
   monolithic) export ARENA_DECODE_THREADS=${DTHREADS:-8} ARENA_DECODE_PROCS=2; PPG=1 ;;
-  triton) export ARENA_DECODE_PROCS=${DECODE:-4}; PPG=3 ;;
+  # one model-server process per GPU with batch overlap (round 5: 6.78k req/s at P99 19 ms and 4.9 model-server
+  # CPUs at 100 users, 2.66k at 10 users; three processes: 6.93k at P99 22.6 ms, 7.0 CPUs, 1.98k at 10 users —
+  # profiles/r5_serving/README.md)
+  triton) export ARENA_DECODE_PROCS=${DECODE:-4}; PPG=1 ;;
   microservices) export ARENA_DECODE_PROCS=${DECODE:-3} ARENA_CLS_PROCS_PER_GPU=2; PPG=3 ;;
 esac
 if [ "${ENVELOPE:-0}" != "0" ]; then

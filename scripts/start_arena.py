@@ -142,6 +142,9 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
                            check=True, env=env)
         ms_env = _queue_env(dict(env, ARENA_GPUS=f"0-{max(1, gpus) - 1}"),  # the ensemble runs on every GPU
                             procs_per_gpu)
+        # one model-server process per GPU owns the device: its batches overlap in free slots, as the monolithic
+        # server's do (several processes per GPU keep it off: smaller overlapping batches compete for the device)
+        ms_env.setdefault("ARENA_BATCH_OVERLAP", "1" if procs_per_gpu <= 1 else "0")
         for k in range(max(1, procs_per_gpu)):  # server processes share :8000/:8001/:8002 (SO_REUSEPORT)
             procs.append(spawn(["inference_arena_amd.server.model_server", "--model-repository", repo, "--device",
                                 device], ms_env, log_dir, f"model_server_{k}"))
