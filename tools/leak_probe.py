@@ -35,6 +35,8 @@ def main(argv=None) -> int:
     ap.add_argument("--per-round", type=int, default=20000)
     ap.add_argument("--users", type=int, default=32)
     ap.add_argument("--decode-threads", type=int, default=4)
+    ap.add_argument("--gpu", action="store_true", help="the fused fp32 GPU pipeline instead of the host-only EchoInstance "
+                    "(the monolithic server's exact path: split decoder, GPU reconstruction, executor)")
     a = ap.parse_args(argv)
 
     import numpy as np
@@ -45,9 +47,18 @@ def main(argv=None) -> int:
     from inference_arena_amd.labels import load_labels
 
     C = native()
-    batcher = C.DynamicBatcher([C.EchoInstance(4, 32, 4, 500)], {"max_batch": 32, "max_queue_delay_us": 300})
+    if a.gpu:
+        from inference_arena_amd.engine.registry import build_session
+        from inference_arena_amd.models.zoo import default_models
+
+        yolo, mnet = default_models(0)
+        pipe = build_session("pipeline", yolo, mnet, device=0, buckets=[1, 2, 4, 8, 16, 32])
+        inst = pipe.ex
+    else:
+        inst = C.EchoInstance(4, 32, 4, 500)
+    batcher = C.DynamicBatcher([inst], {"max_batch": 32, "max_queue_delay_us": 300, "idle_queue_delay_us": 100})
     fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=2, decode_procs=1,
-                        slots=64, decode_threads=a.decode_threads, jpeg_device=False)
+                        slots=64, decode_threads=a.decode_threads, jpeg_device=a.gpu)
     rng = np.random.default_rng(0)
     reqs = []
     for i in range(8):
