@@ -133,10 +133,10 @@ class NativeFrontEnd:
         self.fe.set_healthy(bool(ok))
 
     def _refresh(self) -> None:
-        # ARENA_MALLOC_TRIM_S (default 10, 0 = off): return free heap pages to the kernel periodically.  Buffers
-        # allocated on the decode / I/O threads and freed on the batcher thread otherwise leave glibc's per-thread
-        # arenas holding pages, and the resident size of a long-running server creeps up run after run
-        # (profiles/protocol_r5 memory_usage_mb, tools/leak_probe_gpu.py).
+        # ARENA_MALLOC_TRIM_S (default 10, 0 = off): return free heap pages to the kernel periodically: buffers
+        # allocated on the decode / I/O threads and freed on the batcher thread leave glibc's per-thread arenas
+        # holding pages (tools/leak_probe_gpu.py --trim: 115 MB back).  The slower per-request growth of the GPU
+        # serving path is not this (docs/round5_status.md, "Memory growth").
         trim_s = float(os.environ.get("ARENA_MALLOC_TRIM_S", "10"))
         last_trim = time.monotonic()
         from ..ops import native
