@@ -1069,7 +1069,13 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     }
     off = align_up(off + bytes, 256);
   }
-  const size_t packed_end = off;
+  size_t packed_end = off;
+  // ARENA_JPEG_PACK_COEFS=1 (diagnostic): copy the coefficients into the slot's pinned staging on the host and send
+  // them with the packed frames in one DMA, instead of one DMA per JPEG straight from its pooled buffer.
+  static const bool pack_coefs = [] {
+    const char* e = std::getenv("ARENA_JPEG_PACK_COEFS");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
   struct JpegCopy {
     size_t dst;
     const uint8_t* src;
@@ -1091,7 +1097,14 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     jdesc[nj] = jpeg_device_desc(ji, (int64_t)coef, (int64_t)planes, (int64_t)rgb);
     max_blocks = std::max(max_blocks, jdesc[nj].total_blocks);
     max_pix = std::max(max_pix, (int64_t)im.h * im.w);
-    jcopies.push_back({coef, im.data, (size_t)ji.coef_count * 2});
+    if (pack_coefs) {
+      jobs.emplace_back([dst = pool + coef, src = im.data, len = (size_t)ji.coef_count * 2]() {
+        std::memcpy(dst, src, len);
+      });
+      packed_end = planes;
+    } else {
+      jcopies.push_back({coef, im.data, (size_t)ji.coef_count * 2});
+    }
     ++nj;
     off = end;
   }
