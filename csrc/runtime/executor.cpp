@@ -121,6 +121,10 @@ Executor::~Executor() {
     if (sl.d_out) hipFree(sl.d_out);
     if (sl.h_in) hipHostFree(sl.h_in);
     if (sl.h_out) hipHostFree(sl.h_out);
+    if (sl.copy_stream) {
+      hipStreamSynchronize(sl.copy_stream);
+      hipStreamDestroy(sl.copy_stream);
+    }
     if (sl.copied) hipEventDestroy(sl.copied);
     if (sl.started) hipEventDestroy(sl.started);
     if (sl.done) hipEventDestroy(sl.done);
@@ -176,9 +180,10 @@ void Executor::alloc_slots() {
     // run up to 3 bytes past the last image of a full staging pool
     ARENA_HIP_CHECK(hipMalloc(&sl.d_in, in_bytes_total() + 256));
     ARENA_HIP_CHECK(hipMalloc(&sl.d_out, out_bytes_total()));
-    // pinned host staging: the meta block plus the host-packed (non-JPEG) inputs of one full batch at the
-    // nominal frame size; split-decoded JPEGs are DMA'd from their own pinned buffers, so pool_factor's extra
-    // device room needs no host twin.  A batch of larger RGB frames grows it on demand (ensure_host_staging).
+    // pinned host staging: the meta block plus the host-packed inputs of one full batch at the nominal frame size.
+    // Split-decoded JPEGs need only their coefficients staged here (about 2/3 of an RGB frame at 4:2:0), so
+    // pool_factor's extra device room needs no host twin; a batch that needs more grows it on demand
+    // (ensure_host_staging).
     sl.h_cap = in_bytes_meta() + align_up((size_t)cfg_.pool_bytes_per_image * max_B_, 256);
     ARENA_HIP_CHECK(hipHostMalloc(&sl.h_in, sl.h_cap, hipHostMallocDefault));
     ARENA_HIP_CHECK(hipHostMalloc(&sl.h_out, out_bytes_total(), hipHostMallocDefault));
@@ -187,6 +192,7 @@ void Executor::alloc_slots() {
     std::memset(sl.h_in, 0, in_bytes_meta());
     ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
     ARENA_HIP_CHECK(hipEventCreate(&sl.started));
+    if (copy_mode_ == 3) ARENA_HIP_CHECK(hipStreamCreateWithFlags(&sl.copy_stream, hipStreamNonBlocking));
     // ARENA_SYNC=blocking: collect() sleeps on the completion interrupt instead of polling the event (HIP's
     // default), which otherwise keeps a core busy per waiting thread for the whole device time of a batch
     static const bool blocking = [] {
@@ -1012,10 +1018,18 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   sl.stream = streams_[seq_++ % n_streams_];
   // The slot's previous graph has been collected; its input copy was consumed.
   // Pool layout of the batch: host-packed inputs (RGB frames, tensors) first, so one H2D of the slot's
-  // [ctrl | meta | JPEG descriptors | packed inputs] covers them; then per split-decoded JPEG its RGB
-  // destination, coefficient blocks (DMA'd straight from the request's own pinned buffer: no host copy) and
-  // reconstruction planes.  Everything is validated before the first copy is queued.
+  // [ctrl | meta | JPEG descriptors | packed inputs] covers them (the JPEG coefficients among them, see pack_coefs);
+  // then per split-decoded JPEG its RGB destination and reconstruction planes.  Everything is validated before the first copy is queued.
   const size_t cap = pool_cap();
+  // Split-decoded JPEGs' coefficients are copied on the host into the slot's pinned staging, right after the packed
+  // frames, and go to the device in the batch's one DMA.  ARENA_JPEG_PACK_COEFS=0 instead DMAs each upload's
+  // coefficients straight from its pooled buffer: no host copy (~0.14 ms CPU per 640x480 upload), but HIP then
+  // retains ~1.3 KB of host memory per upload on the shared copy stream, without bound
+  // (profiles/r5_serving/leak/README.md).
+  static const bool pack_coefs = [] {
+    const char* e = std::getenv("ARENA_JPEG_PACK_COEFS");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
   {
     // host bytes of the packed (non-JPEG) inputs: grow the slot's pinned staging if this batch needs more (the
     // slot is idle: its previous H2D completed before it was collected)
@@ -1023,6 +1037,9 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     for (int i = 0; i < n; ++i)
       if (imgs[i].jpeg == nullptr)
         need = align_up(need + (imgs[i].bytes > 0 ? (size_t)imgs[i].bytes : (size_t)imgs[i].h * imgs[i].w * 3), 256);
+    if (pack_coefs)  // the JPEGs' coefficients follow them in the same DMA (layout below)
+      for (int i = 0; i < n; ++i)
+        if (imgs[i].jpeg != nullptr) need = align_up(need + (size_t)imgs[i].jpeg->coef_count * 2, 256);
     if (need > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
     if (in_bytes_meta() + need > sl.h_cap) {
       uint8_t* grown = nullptr;
@@ -1070,12 +1087,6 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     off = align_up(off + bytes, 256);
   }
   size_t packed_end = off;
-  // ARENA_JPEG_PACK_COEFS=1 (diagnostic): copy the coefficients into the slot's pinned staging on the host and send
-  // them with the packed frames in one DMA, instead of one DMA per JPEG straight from its pooled buffer.
-  static const bool pack_coefs = [] {
-    const char* e = std::getenv("ARENA_JPEG_PACK_COEFS");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
   struct JpegCopy {
     size_t dst;
     const uint8_t* src;
@@ -1084,27 +1095,34 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   std::vector<JpegCopy> jcopies;
   int nj = 0, max_blocks = 0;
   int64_t max_pix = 0;
+  // packed coefficients sit contiguously right after the host-packed inputs, inside the one staging DMA
+  std::vector<size_t> coef_at(n, 0);
+  if (pack_coefs) {
+    for (int i = 0; i < n; ++i) {
+      const InputImage& im = imgs[i];
+      if (im.jpeg == nullptr) continue;
+      const size_t len = (size_t)im.jpeg->coef_count * 2;
+      if (off + len > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
+      coef_at[i] = off;
+      jobs.emplace_back([dst = pool + off, src = im.data, len]() { std::memcpy(dst, src, len); });
+      off = align_up(off + len, 256);
+    }
+    packed_end = off;
+  }
   for (int i = 0; i < n; ++i) {
     const InputImage& im = imgs[i];
     if (im.jpeg == nullptr) continue;
     const JpegInfo& ji = *im.jpeg;
     if (ji.width != im.w || ji.height != im.h) throw std::runtime_error("submit: JPEG geometry mismatch");
-    const size_t rgb = off, coef = align_up(rgb + (size_t)im.h * im.w * 3, 256);
-    const size_t planes = align_up(coef + (size_t)ji.coef_count * 2, 256);
+    const size_t rgb = off, coef = pack_coefs ? coef_at[i] : align_up(rgb + (size_t)im.h * im.w * 3, 256);
+    const size_t planes = align_up((pack_coefs ? rgb + (size_t)im.h * im.w * 3 : coef + (size_t)ji.coef_count * 2), 256);
     const size_t end = align_up(planes + (size_t)ji.plane_bytes, 256);
     if (end > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
     set_meta(i, im, rgb);
     jdesc[nj] = jpeg_device_desc(ji, (int64_t)coef, (int64_t)planes, (int64_t)rgb);
     max_blocks = std::max(max_blocks, jdesc[nj].total_blocks);
     max_pix = std::max(max_pix, (int64_t)im.h * im.w);
-    if (pack_coefs) {
-      jobs.emplace_back([dst = pool + coef, src = im.data, len = (size_t)ji.coef_count * 2]() {
-        std::memcpy(dst, src, len);
-      });
-      packed_end = planes;
-    } else {
-      jcopies.push_back({coef, im.data, (size_t)ji.coef_count * 2});
-    }
+    if (!pack_coefs) jcopies.push_back({coef, im.data, (size_t)ji.coef_count * 2});
     ++nj;
     off = end;
   }
@@ -1122,12 +1140,12 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   ctrl->n_images = n;
   ctrl->crop_base = 0;
   sl.in_used = in_bytes_meta() + off;
-  hipStream_t cs = copy_mode_ == 2 ? sl.stream : copy_;
+  hipStream_t cs = copy_mode_ == 2 ? sl.stream : copy_mode_ == 3 ? sl.copy_stream : copy_;
   ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, in_bytes_meta() + packed_end, hipMemcpyHostToDevice, cs));
   for (const JpegCopy& c : jcopies)
     ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in + in_bytes_meta() + c.dst, c.src, c.bytes, hipMemcpyHostToDevice, cs));
   if (copy_mode_ != 2) {
-    ARENA_HIP_CHECK(hipEventRecord(sl.copied, copy_));
+    ARENA_HIP_CHECK(hipEventRecord(sl.copied, cs));
     if (copy_mode_ == 1) ARENA_HIP_CHECK(hipEventSynchronize(sl.copied));
     ARENA_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.copied, 0));
   }
@@ -1543,6 +1561,8 @@ void Executor::replay(int B, int s, int iters) {
 void Executor::synchronize() {
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   ARENA_HIP_CHECK(hipStreamSynchronize(copy_));
+  for (int s = 0; s < n_slots_; ++s)
+    if (slots_[s].copy_stream) ARENA_HIP_CHECK(hipStreamSynchronize(slots_[s].copy_stream));
   sync_slots();
 }
 

@@ -37,6 +37,8 @@ def main(argv=None) -> int:
     ap.add_argument("--decode-threads", type=int, default=4)
     ap.add_argument("--jpeg-host", action="store_true", help="with --gpu: reconstruct JPEGs on the host threads "
                     "(RGB inputs, no per-request coefficient DMA)")
+    ap.add_argument("--jpeg-device", action="store_true", help="without --gpu: hand split-decoded coefficient sets to "
+                    "the EchoInstance (the device-JPEG front-end branch, reconstructed on the host by the instance)")
     ap.add_argument("--gpu", action="store_true", help="the fused fp32 GPU pipeline instead of the host-only EchoInstance "
                     "(the monolithic server's exact path: split decoder, GPU reconstruction, executor)")
     a = ap.parse_args(argv)
@@ -60,7 +62,7 @@ def main(argv=None) -> int:
         inst = C.EchoInstance(4, 32, 4, 500)
     batcher = C.DynamicBatcher([inst], {"max_batch": 32, "max_queue_delay_us": 300, "idle_queue_delay_us": 100})
     fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=2, decode_procs=1,
-                        slots=64, decode_threads=a.decode_threads, jpeg_device=a.gpu and not a.jpeg_host)
+                        slots=64, decode_threads=a.decode_threads, jpeg_device=(a.gpu and not a.jpeg_host) or a.jpeg_device)
     rng = np.random.default_rng(0)
     reqs = []
     for i in range(8):
