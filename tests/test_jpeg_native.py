@@ -240,3 +240,29 @@ def test_decoder_fuzz_under_address_sanitizer(tmp_path):
     report = r.stdout + r.stderr
     assert "AddressSanitizer" not in report and r.returncode == 0, report[-6000:]
     assert "jpeg_fuzz: ok" in r.stdout
+
+
+def test_entropy_bench_builds_and_runs(tmp_path):
+    """csrc/tests/jpeg_entropy_bench.cpp (host entropy-decode throughput of the split decoder) builds host-only,
+    decodes a 4:2:0 upload and reports a stable coefficient checksum."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    root = Path(__file__).resolve().parents[1]
+    exe = tmp_path / "jpeg_entropy_bench"
+    r = subprocess.run([gxx, "-O2", "-std=c++17", "-I" + str(root / "csrc"),
+                        str(root / "csrc" / "tests" / "jpeg_entropy_bench.cpp"),
+                        str(root / "csrc" / "runtime" / "jpeg_decode.cpp"), "-o", str(exe)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    f = tmp_path / "a.jpg"
+    f.write_bytes(_enc(_scene(96, 128), quality=90, subsampling=2))
+    outs = [subprocess.run([str(exe), str(f)], capture_output=True, text=True, timeout=120) for _ in range(2)]
+    for o in outs:
+        assert o.returncode == 0 and "us per image" in o.stdout, o.stdout + o.stderr
+    sums = [o.stdout.split("checksum")[1].strip() for o in outs]
+    assert sums[0] == sums[1] and sums[0] != "0" * 16
