@@ -121,6 +121,11 @@ Executor::~Executor() {
     if (sl.d_out) hipFree(sl.d_out);
     if (sl.h_in) hipHostFree(sl.h_in);
     if (sl.h_out) hipHostFree(sl.h_out);
+  }
+  for (uint8_t* p : retired_h_in_) hipHostFree(p);
+  retired_h_in_.clear();
+  for (int s = 0; s < n_slots_; ++s) {
+    Slot& sl = slots_[s];
     if (sl.copy_stream) {
       hipStreamSynchronize(sl.copy_stream);
       hipStreamDestroy(sl.copy_stream);
@@ -1046,7 +1051,10 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
       const size_t want = in_bytes_meta() + std::max(need, std::min(cap, 2 * (sl.h_cap - in_bytes_meta())));
       ARENA_HIP_CHECK(hipHostMalloc(&grown, want, hipHostMallocDefault));
       std::memcpy(grown, sl.h_in, in_bytes_meta());
-      ARENA_HIP_CHECK(hipHostFree(sl.h_in));
+      // hipHostFree may synchronise the device, which would stall the other slots' batches: the outgrown buffer
+      // is released with the executor (the doubling bounds all retired buffers by the final size)
+      retired_h_in_.push_back(sl.h_in);
+      ++staging_growths_;
       sl.h_in = grown;
       sl.h_cap = want;
     }

@@ -187,6 +187,13 @@ class Executor : public BatchInstance {
   uintptr_t stream() const { return (uintptr_t)compute_; }
 
  private:
+  std::vector<uint8_t*> retired_h_in_;  // outgrown pinned staging, freed with the executor (submit never frees)
+  int64_t staging_growths_ = 0;
+
+ public:
+  int64_t staging_growths() const { return staging_growths_; }
+
+ private:
   struct Slot {
     // device
     uint8_t* d_in = nullptr;   // ctrl | meta | pool

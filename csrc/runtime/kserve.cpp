@@ -55,13 +55,20 @@ size_t scan_string(const std::string& s, size_t i, std::string* out) {
   return std::string::npos;
 }
 
-// index past the JSON value starting at s[i] (after whitespace), npos if malformed
-size_t skip_value(const std::string& s, size_t i) {
+// Nesting bound of skip_value: the KServe messages read here nest at most four levels (header -> inputs ->
+// tensor -> parameters); a hostile header of ~1 MB of '[' would otherwise recurse once per byte and overflow an
+// I/O thread's stack.
+constexpr int kMaxJsonDepth = 32;
+
+// index past the JSON value starting at s[i] (after whitespace), npos if malformed or nested deeper than
+// kMaxJsonDepth
+size_t skip_value(const std::string& s, size_t i, int depth = 0) {
   i = skip_ws(s, i);
   if (i >= s.size()) return std::string::npos;
   const char c = s[i];
   if (c == '"') return scan_string(s, i, nullptr);
   if (c == '{' || c == '[') {
+    if (depth >= kMaxJsonDepth) return std::string::npos;
     const char close = c == '{' ? '}' : ']';
     ++i;
     i = skip_ws(s, i);
@@ -74,7 +81,7 @@ size_t skip_value(const std::string& s, size_t i) {
         if (i >= s.size() || s[i] != ':') return std::string::npos;
         ++i;
       }
-      i = skip_value(s, i);
+      i = skip_value(s, i, depth + 1);
       if (i == std::string::npos) return i;
       i = skip_ws(s, i);
       if (i < s.size() && s[i] == ',') {
@@ -238,8 +245,18 @@ bool kserve_parse_bytes_input(const std::string& body, int64_t ihcl, const std::
     err = "malformed inference request header";
     return false;
   }
+  // every size is client data: bound each one by what is left of the body before it is added, so no sum can
+  // wrap around (sizes near 2^63 would otherwise move `bin` in front of the buffer)
   size_t bin = (size_t)ihcl;
   for (const TensorDesc& t : ins) {
+    if (t.binary_size < 0 && t.binary_size != -1) {
+      err = "negative binary_data_size";
+      return false;
+    }
+    if (t.binary_size > 0 && (uint64_t)t.binary_size > body.size() - bin) {
+      err = t.name + ": binary_data_size exceeds the request body";
+      return false;
+    }
     if (t.name != input) {
       if (t.binary_size > 0) bin += (size_t)t.binary_size;
       continue;
@@ -248,19 +265,25 @@ bool kserve_parse_bytes_input(const std::string& body, int64_t ihcl, const std::
       err = input + " must be BYTES";
       return false;
     }
-    if (t.binary_size < 4 || bin + (size_t)t.binary_size > body.size()) {
+    if (t.binary_size < 4) {
       err = input + ": missing or inconsistent binary_data_size";
       return false;
     }
     int64_t n = 1;
-    for (int64_t d : t.shape) n *= d;
+    for (int64_t d : t.shape) {
+      if (d < 0 || d > 1) {
+        n = -1;
+        break;
+      }
+      n *= d;
+    }
     if (n != 1) {
       err = input + " must hold exactly one encoded image";
       return false;
     }
     const unsigned char* p = (const unsigned char*)body.data() + bin;
     const uint32_t l = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-    if ((int64_t)l + 4 > t.binary_size) {
+    if ((uint64_t)l + 4 > (uint64_t)t.binary_size) {
       err = input + ": element length exceeds its binary data";
       return false;
     }
@@ -397,35 +420,57 @@ bool kserve_parse_response(const std::string& body, int64_t ihcl, RequestResult&
   size_t pos = (size_t)ihcl;
   const float *det = nullptr, *logit = nullptr, *prob = nullptr, *stage = nullptr;
   const int32_t* ids = nullptr;
-  int64_t n = -1;
+  int64_t n = -1, n_ids = -1, n_logit = -1, n_prob = -1;
+  // element count of a shape with every dimension checked (non-negative, product bounded by the body size), -1 if
+  // the shape is unusable
+  auto count = [&](const std::vector<int64_t>& shape) -> int64_t {
+    uint64_t c = 1;
+    for (int64_t d : shape) {
+      if (d < 0) return -1;
+      if (d != 0 && c > (uint64_t)body.size() / (uint64_t)d) return -1;
+      c *= (uint64_t)d;
+    }
+    return (int64_t)c;
+  };
+  // rows of an [n, cols] output, -1 when the shape is not that
+  auto rows = [](const std::vector<int64_t>& shape, int64_t cols) -> int64_t {
+    return shape.size() == 2 && shape[1] == cols && shape[0] >= 0 ? shape[0] : -1;
+  };
   for (const TensorDesc& t : outs) {
-    if (t.binary_size < 0 || pos + (size_t)t.binary_size > body.size()) {
+    if (t.binary_size < 0 || (uint64_t)t.binary_size > body.size() - pos) {
       err = "output " + t.name + ": missing or inconsistent binary_data_size";
       return false;
     }
     const void* p = body.data() + pos;
-    int64_t cnt = 1;
-    for (int64_t d : t.shape) cnt *= d;
-    if (cnt * 4 != t.binary_size) {
+    const int64_t cnt = count(t.shape);
+    if (cnt < 0 || (uint64_t)cnt > (uint64_t)t.binary_size / 4 || cnt * 4 != t.binary_size) {
       err = "output " + t.name + ": shape and binary size disagree";
       return false;
     }
     if (t.name == "DETECTIONS") {
       det = (const float*)p;
-      n = t.shape.empty() ? 0 : t.shape[0];
+      n = rows(t.shape, 6);
     } else if (t.name == "CLASS_IDS") {
       ids = (const int32_t*)p;
+      n_ids = rows(t.shape, 5);
     } else if (t.name == "CLASS_LOGITS") {
       logit = (const float*)p;
+      n_logit = rows(t.shape, 5);
     } else if (t.name == "CLASS_PROBS") {
       prob = (const float*)p;
+      n_prob = rows(t.shape, 5);
     } else if (t.name == "STAGE_MS" && cnt >= 4) {
       stage = (const float*)p;
     }
     pos += (size_t)t.binary_size;
   }
   if (det == nullptr || n < 0) {
-    err = "answer without DETECTIONS";
+    err = "answer without DETECTIONS [n, 6]";
+    return false;
+  }
+  const bool have_cls = ids != nullptr || logit != nullptr || prob != nullptr;
+  if (have_cls && (n_ids != n || n_logit != n || n_prob != n)) {
+    err = "CLASS_IDS / CLASS_LOGITS / CLASS_PROBS must all be [n, 5] with n the DETECTIONS rows";
     return false;
   }
   r.det.resize((size_t)n);
@@ -525,9 +570,13 @@ int KServeProxy::connect_upstream(std::string& err) const {
 }
 
 bool KServeProxy::roundtrip(int& fd, const std::string& req, int& status, int64_t& ihcl, std::string& body,
-                            std::string& err) {
+                            std::string& err, RoundtripFail* fail) {
+  RoundtripFail dummy;
+  RoundtripFail& f = fail != nullptr ? *fail : dummy;
+  f = RoundtripFail::None;
   if (!write_full(fd, req.data(), req.size())) {
     err = "send to the model server failed";
+    f = RoundtripFail::Send;
     return false;
   }
   std::string in;
@@ -560,6 +609,7 @@ bool KServeProxy::roundtrip(int& fd, const std::string& req, int& status, int64_
         }
         if (clen < 0) {
           err = "model server answer without Content-Length";
+          f = RoundtripFail::Protocol;
           return false;
         }
       }
@@ -568,13 +618,17 @@ bool KServeProxy::roundtrip(int& fd, const std::string& req, int& status, int64_
     pollfd pf{fd, POLLIN, 0};
     const int pr = ::poll(&pf, 1, timeout_ms_);
     if (pr <= 0) {
+      if (pr < 0 && errno == EINTR) continue;
       err = pr == 0 ? "model server timed out" : "poll failed";
+      f = pr == 0 ? RoundtripFail::Timeout : RoundtripFail::Protocol;
       return false;
     }
     const ssize_t r = ::recv(fd, buf, sizeof buf, 0);
     if (r <= 0) {
       if (r < 0 && errno == EINTR) continue;
       err = "model server closed the connection";
+      // a keep-alive connection the server closed before answering anything: safe to resend on a new one
+      f = in.empty() ? RoundtripFail::ClosedEarly : RoundtripFail::Protocol;
       return false;
     }
     in.append(buf, (size_t)r);
@@ -625,10 +679,18 @@ void KServeProxy::worker() {
         if (seq++ > 0) ++reconnects_;
       }
       int64_t rihcl = -1;
-      ok = roundtrip(fd, req, rep.status, rihcl, body, err);
+      RoundtripFail why = RoundtripFail::None;
+      ok = roundtrip(fd, req, rep.status, rihcl, body, err, &why);
       if (!ok) {
         ::close(fd);
         fd = -1;
+        // resend only what the model server cannot have started: a failed send or a keep-alive connection closed
+        // before any answer byte.  A timeout means an overloaded server: answer 504 rather than doubling its load.
+        if (why == RoundtripFail::Timeout) {
+          rep.status = 504;
+          break;
+        }
+        if (why != RoundtripFail::Send && why != RoundtripFail::ClosedEarly) break;
         continue;
       }
       if (rep.status == 200) {
@@ -637,7 +699,10 @@ void KServeProxy::worker() {
         rep.error = body.empty() ? "model server error " + std::to_string(rep.status) : body;
       }
     }
-    if (!ok) rep.error = err.empty() ? "model server unreachable" : err;
+    if (!ok) {
+      rep.error = err.empty() ? "model server unreachable" : err;
+      if (rep.status == 200) rep.status = 0;
+    }
     ++forwarded_;
     t.done(std::move(rep));
   }

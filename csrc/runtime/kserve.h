@@ -55,8 +55,10 @@ struct ProxyReply {
 };
 
 // Keep-alive client pool: `conns` worker threads, each with one persistent TCP connection to host:port,
-// forward uploads as KServe infer requests for `model`.  A broken connection is reopened and the request
-// retried once (inference is idempotent).  Callbacks run on the worker threads.
+// forward uploads as KServe infer requests for `model`.  A request is resent once, on a new connection, only
+// when the send failed or the kept-alive connection closed before any answer byte (the server cannot have
+// started it); a poll timeout answers 504 without a resend.  Callbacks run on the worker threads.
+enum class RoundtripFail { None, Send, ClosedEarly, Timeout, Protocol };
 class KServeProxy {
  public:
   KServeProxy(std::string host, int port, std::string model, int conns, int timeout_ms = 60000);
@@ -77,7 +79,8 @@ class KServeProxy {
   };
   void worker();
   int connect_upstream(std::string& err) const;
-  bool roundtrip(int& fd, const std::string& req, int& status, int64_t& ihcl, std::string& body, std::string& err);
+  bool roundtrip(int& fd, const std::string& req, int& status, int64_t& ihcl, std::string& body, std::string& err,
+                 RoundtripFail* fail = nullptr);
 
   std::string host_, model_;
   int port_, timeout_ms_;

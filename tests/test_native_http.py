@@ -438,6 +438,36 @@ def test_split_decoder_stages_oversize_frames_as_rgb():
     assert answers[0] == answers[1]
 
 
+def test_kserve_codec_fuzz_under_address_sanitizer():
+    """csrc/runtime/kserve.cpp built host-only with AddressSanitizer and driven by csrc/tests/kserve_fuzz.cpp:
+    deeply nested headers (stack depth), binary_data_size values that wrap a 64-bit sum, negative sizes and
+    shapes, DETECTIONS / CLASS_* shapes that disagree are all rejected; valid messages round-trip; 4000 random
+    mutations parse without a memory error (kserve.cpp:59, :244, :409)."""
+    import os
+    import shutil
+    import subprocess
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not (Path(hipcc).exists() or shutil.which(hipcc)):
+        pytest.skip("hipcc not available")
+    srcs = [root / "csrc" / "tests" / "kserve_fuzz.cpp", root / "csrc" / "runtime" / "kserve.cpp"]
+    exe = root / "build" / "kserve_fuzz_address"
+    exe.parent.mkdir(parents=True, exist_ok=True)
+    newest = max(p.stat().st_mtime for p in srcs + list((root / "csrc" / "runtime").glob("*.h")))
+    if not exe.exists() or exe.stat().st_mtime < newest:
+        cmd = [hipcc, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", "-fsanitize=address",
+               "-I" + str(root / "csrc"), *map(str, srcs), "-o", str(exe)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-4000:]
+    r = subprocess.run([str(exe), "4000"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1"))
+    report = r.stdout + r.stderr
+    assert "AddressSanitizer" not in report and r.returncode == 0, report[-6000:]
+    assert "kserve_fuzz: ok" in r.stdout
+
+
 def _kserve_request(upload: bytes) -> tuple[bytes, int]:
     import struct
 
