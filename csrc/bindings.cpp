@@ -1143,6 +1143,7 @@ PYBIND11_MODULE(_C, m) {
           py::arg("key"), py::arg("code"), py::arg("body"), py::arg("n_det") = 0)
       .def_property_readonly("port", &HttpFrontEnd::port)
       .def("set_healthy", &HttpFrontEnd::set_healthy)
+      .def("upstream_forwarded", &HttpFrontEnd::upstream_forwarded)
       .def("set_metrics_text", &HttpFrontEnd::set_metrics_text)
       .def("stats",
            [](HttpFrontEnd& f) {
@@ -1198,6 +1199,7 @@ PYBIND11_MODULE(_C, m) {
         c.upstream_port = get<int>(cfg, "upstream_port", 0);
         c.upstream_model = get<std::string>(cfg, "upstream_model", c.upstream_model);
         c.upstream_conns = get<int>(cfg, "upstream_conns", c.upstream_conns);
+        c.upstreams = get<std::string>(cfg, "upstreams", c.upstreams);
         if (c.upstream_port <= 0) throw std::runtime_error("http_proxy_front: upstream_port required");
         py::gil_scoped_release nogil;
         return new HttpFrontEnd(nullptr, DecodeChannel{}, std::move(labels), c);

@@ -293,7 +293,23 @@ HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vecto
   const bool proxy = cfg_.upstream_port > 0;
   if (proxy) {
     if (cfg_.handler_mode) throw std::runtime_error("HttpFrontEnd: proxy mode and handler mode exclude each other");
-    proxy_.reset(new KServeProxy(cfg_.upstream_host, cfg_.upstream_port, cfg_.upstream_model, cfg_.upstream_conns));
+    std::vector<KServeUpstream> ups{KServeUpstream{cfg_.upstream_host, cfg_.upstream_port}};
+    size_t p = 0;
+    while (p < cfg_.upstreams.size()) {  // "host:port,host:port"
+      size_t e = cfg_.upstreams.find(',', p);
+      if (e == std::string::npos) e = cfg_.upstreams.size();
+      const std::string item = cfg_.upstreams.substr(p, e - p);
+      p = e + 1;
+      if (item.empty()) continue;
+      const size_t colon = item.rfind(':');
+      if (colon == std::string::npos) throw std::runtime_error("HttpFrontEnd: upstream '" + item + "' is not host:port");
+      KServeUpstream u{item.substr(0, colon), std::atoi(item.c_str() + colon + 1)};
+      if (u.host.empty()) u.host = "127.0.0.1";
+      if (u.port <= 0) throw std::runtime_error("HttpFrontEnd: upstream '" + item + "' has no port");
+      if (u.host == ups[0].host && u.port == ups[0].port) continue;
+      ups.push_back(u);
+    }
+    proxy_.reset(new KServeProxy(std::move(ups), cfg_.upstream_model, cfg_.upstream_conns));
     cfg_.decode_threads = 0;
   }
   if (!cfg_.handler_mode && !proxy) {
@@ -1020,6 +1036,13 @@ bool HttpFrontEnd::kserve_route(const std::shared_ptr<Conn>& c, const std::strin
   t_predict_dispatched = true;
   start_upload(c, t0, std::move(body), off, len, 1);
   return true;
+}
+
+std::vector<int64_t> HttpFrontEnd::upstream_forwarded() const {
+  std::vector<int64_t> v;
+  if (proxy_)
+    for (int i = 0; i < proxy_->num_upstreams(); ++i) v.push_back(proxy_->forwarded_to(i));
+  return v;
 }
 
 void HttpFrontEnd::proxy_predict(const std::shared_ptr<Conn>& c, Clock_tp t0, std::string upload) {

@@ -109,6 +109,9 @@ struct FrontConfig {
   int upstream_port = 0;
   std::string upstream_model = "arena_pipeline";
   int upstream_conns = 64;
+  // more model servers ("host:port,host:port", e.g. one per GPU): with it the proxy spreads requests over
+  // upstream_host:upstream_port and these, least-outstanding first (KServeProxy)
+  std::string upstreams;
 };
 
 // One upload handed to the Python handler (handler mode).
@@ -177,6 +180,8 @@ class HttpFrontEnd {
   void set_healthy(bool h) { healthy_.store(h); }
   void set_metrics_text(std::string text);
   FrontStats stats();
+  // proxy mode: requests forwarded to each upstream so far (empty otherwise)
+  std::vector<int64_t> upstream_forwarded() const;
   void stop();
 
   // handler mode: up to max_n queued uploads; waits up to timeout_ms for the first one (empty on timeout / stop)

@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <stdexcept>
 
 namespace arena {
 
@@ -505,8 +506,32 @@ bool kserve_parse_response(const std::string& body, int64_t ihcl, RequestResult&
 }
 
 KServeProxy::KServeProxy(std::string host, int port, std::string model, int conns, int timeout_ms)
-    : host_(std::move(host)), model_(std::move(model)), port_(port), timeout_ms_(timeout_ms) {
-  for (int i = 0; i < std::max(1, conns); ++i) threads_.emplace_back([this] { worker(); });
+    : KServeProxy(std::vector<KServeUpstream>{KServeUpstream{std::move(host), port}}, std::move(model), conns,
+                  timeout_ms) {}
+
+KServeProxy::KServeProxy(std::vector<KServeUpstream> ups, std::string model, int conns, int timeout_ms)
+    : model_(std::move(model)), timeout_ms_(timeout_ms) {
+  if (ups.empty()) throw std::runtime_error("KServeProxy: no upstream");
+  for (auto& u : ups) {
+    ups_.emplace_back();
+    ups_.back().host = u.host;
+    ups_.back().port = u.port;
+  }
+  for (int i = 0; i < std::max(1, conns); ++i) threads_.emplace_back([this, i] { worker(i); });
+}
+
+int KServeProxy::pick(int rotation) const {
+  const int n = (int)ups_.size();
+  int best = rotation % n, best_load = ups_[(size_t)best].inflight.load(std::memory_order_relaxed);
+  for (int k = 1; k < n && best_load > 0; ++k) {
+    const int u = (rotation + k) % n;
+    const int l = ups_[(size_t)u].inflight.load(std::memory_order_relaxed);
+    if (l < best_load) {
+      best = u;
+      best_load = l;
+    }
+  }
+  return best;
 }
 
 KServeProxy::~KServeProxy() { stop(); }
@@ -547,18 +572,20 @@ void KServeProxy::submit(std::string upload, std::function<void(ProxyReply&&)> d
   done(std::move(r));
 }
 
-int KServeProxy::connect_upstream(std::string& err) const {
+int KServeProxy::connect_upstream(int u, std::string& err) const {
+  const std::string& host = ups_[(size_t)u].host;
+  const int port = ups_[(size_t)u].port;
   addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_INET;
   hints.ai_socktype = SOCK_STREAM;
-  const int rc = getaddrinfo(host_.c_str(), std::to_string(port_).c_str(), &hints, &res);
+  const int rc = getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res);
   if (rc != 0 || res == nullptr) {
-    err = std::string("cannot resolve model server host ") + host_ + ": " + gai_strerror(rc);
+    err = std::string("cannot resolve model server host ") + host + ": " + gai_strerror(rc);
     return -1;
   }
   const int fd = ::socket(res->ai_family, SOCK_STREAM | SOCK_CLOEXEC, 0);
   if (fd < 0 || ::connect(fd, res->ai_addr, res->ai_addrlen) != 0) {
-    err = "cannot connect to the model server at " + host_ + ":" + std::to_string(port_) + ": " + strerror(errno);
+    err = "cannot connect to the model server at " + host + ":" + std::to_string(port) + ": " + strerror(errno);
     if (fd >= 0) ::close(fd);
     freeaddrinfo(res);
     return -1;
@@ -638,22 +665,27 @@ bool KServeProxy::roundtrip(int& fd, const std::string& req, int& status, int64_
 }
 
 bool KServeProxy::upstream_ready() {
-  std::string err;
-  int fd = connect_upstream(err);
-  if (fd < 0) return false;
-  const std::string req = "GET /v2/health/ready HTTP/1.1\r\nHost: " + host_ + "\r\nContent-Length: 0\r\n\r\n";
-  int status = 0;
-  int64_t ihcl = -1;
-  std::string body;
-  const bool ok = roundtrip(fd, req, status, ihcl, body, err) && status == 200;
-  ::close(fd);
-  return ok;
+  for (int u = 0; u < (int)ups_.size(); ++u) {
+    std::string err;
+    int fd = connect_upstream(u, err);
+    if (fd < 0) return false;
+    const std::string req =
+        "GET /v2/health/ready HTTP/1.1\r\nHost: " + ups_[(size_t)u].host + "\r\nContent-Length: 0\r\n\r\n";
+    int status = 0;
+    int64_t ihcl = -1;
+    std::string body;
+    const bool ok = roundtrip(fd, req, status, ihcl, body, err) && status == 200;
+    ::close(fd);
+    if (!ok) return false;
+  }
+  return true;
 }
 
-void KServeProxy::worker() {
+void KServeProxy::worker(int index) {
   pthread_setname_np(pthread_self(), "arena-kproxy");
-  int fd = -1;
+  std::vector<int> fds(ups_.size(), -1);
   uint64_t seq = 0;
+  int rotation = index;
   while (true) {
     Task t;
     {
@@ -663,10 +695,14 @@ void KServeProxy::worker() {
       t = std::move(q_.front());
       q_.pop_front();
     }
+    const int u = pick(rotation++);
+    Up& up = ups_[(size_t)u];
+    up.inflight.fetch_add(1, std::memory_order_relaxed);
+    int& fd = fds[(size_t)u];
     ProxyReply rep;
     int64_t ihcl = -1;
     const std::string payload = kserve_build_request(t.upload, "", &ihcl);
-    std::string req = "POST /v2/models/" + model_ + "/infer HTTP/1.1\r\nHost: " + host_ +
+    std::string req = "POST /v2/models/" + model_ + "/infer HTTP/1.1\r\nHost: " + up.host +
                       "\r\nContent-Type: application/octet-stream\r\nInference-Header-Content-Length: " +
                       std::to_string(ihcl) + "\r\nContent-Length: " + std::to_string(payload.size()) + "\r\n\r\n";
     req += payload;
@@ -674,7 +710,7 @@ void KServeProxy::worker() {
     bool ok = false;
     for (int attempt = 0; attempt < 2 && !ok; ++attempt) {
       if (fd < 0) {
-        fd = connect_upstream(err);
+        fd = connect_upstream(u, err);
         if (fd < 0) break;
         if (seq++ > 0) ++reconnects_;
       }
@@ -703,10 +739,13 @@ void KServeProxy::worker() {
       rep.error = err.empty() ? "model server unreachable" : err;
       if (rep.status == 200) rep.status = 0;
     }
+    up.inflight.fetch_sub(1, std::memory_order_relaxed);
+    up.forwarded.fetch_add(1, std::memory_order_relaxed);
     ++forwarded_;
     t.done(std::move(rep));
   }
-  if (fd >= 0) ::close(fd);
+  for (int fd : fds)
+    if (fd >= 0) ::close(fd);
 }
 
 }  // namespace arena

@@ -59,31 +59,52 @@ struct ProxyReply {
 // when the send failed or the kept-alive connection closed before any answer byte (the server cannot have
 // started it); a poll timeout answers 504 without a resend.  Callbacks run on the worker threads.
 enum class RoundtripFail { None, Send, ClosedEarly, Timeout, Protocol };
+//
+// Several upstreams (one model-server process per GPU, each with its own native endpoint): every request goes to
+// the upstream with the fewest requests in flight from this proxy (ties: the worker's own rotation), each worker
+// keeping one connection per upstream.
+struct KServeUpstream {
+  std::string host;
+  int port = 0;
+};
 class KServeProxy {
  public:
   KServeProxy(std::string host, int port, std::string model, int conns, int timeout_ms = 60000);
+  KServeProxy(std::vector<KServeUpstream> ups, std::string model, int conns, int timeout_ms = 60000);
   ~KServeProxy();
   KServeProxy(const KServeProxy&) = delete;
   KServeProxy& operator=(const KServeProxy&) = delete;
   void submit(std::string upload, std::function<void(ProxyReply&&)> done);
   void stop();
-  // true when GET /v2/health/ready answers 200 (a fresh connection; used before the front end turns healthy)
+  // true when GET /v2/health/ready answers 200 on every upstream (fresh connections; used before the front end
+  // turns healthy)
   bool upstream_ready();
   int64_t forwarded() const { return forwarded_.load(); }
   int64_t reconnects() const { return reconnects_.load(); }
+  int num_upstreams() const { return (int)ups_.size(); }
+  // requests forwarded to upstream i so far
+  int64_t forwarded_to(int i) const { return ups_[(size_t)i].forwarded.load(); }
 
  private:
   struct Task {
     std::string upload;
     std::function<void(ProxyReply&&)> done;
   };
-  void worker();
-  int connect_upstream(std::string& err) const;
+  struct Up {
+    std::string host;
+    int port = 0;
+    std::atomic<int> inflight{0};
+    std::atomic<int64_t> forwarded{0};
+  };
+  void worker(int index);
+  int pick(int rotation) const;
+  int connect_upstream(int u, std::string& err) const;
   bool roundtrip(int& fd, const std::string& req, int& status, int64_t& ihcl, std::string& body, std::string& err,
                  RoundtripFail* fail = nullptr);
 
-  std::string host_, model_;
-  int port_, timeout_ms_;
+  std::deque<Up> ups_;  // deque: Up holds atomics (not movable)
+  std::string model_;
+  int timeout_ms_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Task> q_;

@@ -154,3 +154,37 @@ def pin(cpus: list[int] | None) -> bool:
         return True
     except OSError:
         return False
+
+
+def rank_host_setup(gpu_rank: int, local_world: int, *, do_pin: bool = True) -> dict:
+    """One serving process per GPU: its CPU share (the GPU's NUMA-local CPUs split between the node's ranks on
+    that NUMA node), the CPUs it may really use (capped by the job's cgroup quota divided by ``local_world``), and
+    the host thread plan for that many CPUs; pins the process to the share.  Every process of the Triton arm's
+    per-GPU layout (model servers, gateways) and the monolithic replicas size themselves with it, so the host
+    plan scales with the GPU count.  ``ARENA_HTTP_THREADS`` / ``ARENA_DECODE_THREADS``
+    still override the plan."""
+    share = rank_cpu_share(gpu_rank, max(1, local_world))
+    usable = usable_cpus_per_rank(share, max(1, local_world))
+    plan = host_thread_plan(usable)
+    if os.environ.get("ARENA_HTTP_THREADS"):
+        plan["http_io"] = int(os.environ["ARENA_HTTP_THREADS"])
+    if os.environ.get("ARENA_DECODE_THREADS"):
+        plan["decode_threads"] = int(os.environ["ARENA_DECODE_THREADS"])
+    pinned = pin(share) if do_pin else False
+    return {"gpu": int(gpu_rank), "local_world": int(local_world), "cpus": share, "usable_cpus": usable,
+            "pinned": pinned, "plan": plan}
+
+
+def rank_info_metrics(info: dict, arch: str) -> str:
+    """Prometheus text of a rank's host placement: ``arena_rank_usable_cpus`` and ``arena_rank_threads``."""
+    cpus = info.get("cpus")
+    cl = ",".join(str(c) for c in cpus) if cpus else "all"
+    g = info.get("gpu", 0)
+    lines = ["# HELP arena_rank_usable_cpus CPUs this serving process may use (its share of the node)",
+             "# TYPE arena_rank_usable_cpus gauge",
+             f'arena_rank_usable_cpus{{arch="{arch}",gpu="{g}",cpus="{cl}"}} {info.get("usable_cpus", 0)}',
+             "# HELP arena_rank_threads host threads of this serving process by role",
+             "# TYPE arena_rank_threads gauge"]
+    for role, n in sorted((info.get("plan") or {}).items()):
+        lines.append(f'arena_rank_threads{{arch="{arch}",gpu="{g}",role="{role}"}} {n}')
+    return "\n".join(lines) + "\n"

@@ -135,7 +135,10 @@ def launch(arch: str, n: int, *, port: int = 8100, stride: int = 0, host: str = 
         e.update(env or {})
         e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
                   "MASTER_PORT": str(master), "HSA_ENABLE_IPC_MODE_LEGACY": "0",
-                  "ARENA_PROCS_PER_GPU": str(procs_per_gpu), "ARENA_FIRST_GPU": str(first_gpu)})
+                  "ARENA_PROCS_PER_GPU": str(procs_per_gpu), "ARENA_FIRST_GPU": str(first_gpu),
+                  # GPUs served on this node: each replica sizes its host threads for its share of the CPUs
+                  # (parallel/affinity.py rank_host_setup)
+                  "ARENA_LOCAL_WORLD": str(n)})
         log = os.path.join(log_dir, f"replica_{r}.log") if log_dir else None
         out = open(log, "w") if log else None  # None: the supervisor's own stdout (a failed start stays visible)
         argv = [sys.executable, "-m", "inference_arena_amd.server.replica", "--arch", arch, "--host", host,

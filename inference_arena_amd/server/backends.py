@@ -130,6 +130,36 @@ class GpuBatchedBackend(Backend):
         self.batcher.close()
 
 
+def fake_instance(max_batch: int = 8):
+    """Host-only stand-in for one device (``ARENA_DEVICE=fake``, CPU tests of the node layouts): the native
+    EchoInstance answers every batch after ``ARENA_FAKE_LATENCY_US`` (default 20 ms) with ``ARENA_FAKE_SLOTS``
+    (default 2) batches in flight, so one fake device serves at most slots x max_batch / latency requests/s
+    whatever the host does; N ranks scale only if their host layout does."""
+    from ..ops import native
+
+    mb = int(os.environ.get("ARENA_FAKE_MAX_BATCH", "0") or 0) or int(max_batch)
+    return native().EchoInstance(int(os.environ.get("ARENA_FAKE_SLOTS", "2")), mb, 4,
+                                 int(os.environ.get("ARENA_FAKE_LATENCY_US", "20000")))
+
+
+class FakeBatchedBackend(GpuBatchedBackend):
+    """The GPU backend's interface (native DynamicBatcher, ``infer`` / ``infer_bytes``) over ``fake_instance``."""
+
+    name = "fake"
+
+    def __init__(self, *, max_batch: int = 8, max_queue_delay_us: int = 500, overlap: int = 1):
+        class _Inst:
+            def __init__(self, ex):
+                self.ex = ex
+
+        max_batch = int(os.environ.get("ARENA_FAKE_MAX_BATCH", "0") or 0) or int(max_batch)
+        self.devices = [0]
+        self.pipes = [_Inst(fake_instance(max_batch))]
+        self.batcher = AsyncBatcher(self.pipes, max_batch=max_batch, max_queue_delay_us=max_queue_delay_us,
+                                    overlap=int(overlap))
+        self.device = 0
+
+
 class GpuSplitBackend(GpuBatchedBackend):
     """Monolithic arm in the split topology: detection on ``det_device``, classification on ``cls_device``
     (engine.pipeline.SplitPipeline: crop plan, detections and images handed over device to device) behind

@@ -304,13 +304,14 @@ def create_metrics_app(server: ModelServer) -> FastAPI:
 
 
 # ----------------------------------------------------------------------------- main
-def start_native_kserve(server: ModelServer, host: str, port: int, model: str = "arena_pipeline"):
+def start_native_kserve(server: ModelServer, host_ip: str, port: int, model: str = "arena_pipeline",
+                        host: dict | None = None):
     """The ensemble's hot path without Python: a native HTTP front end (csrc/runtime/http_front.h with
     ``kserve_model``) on ``port`` serving KServe-v2 REST infer requests for ``model`` (binary tensor extension)
     straight into the ensemble's native dynamic batcher, with the split JPEG decoder on C++ threads — the endpoint
     the native gateway (server/native_gateway.py) forwards to.  None when off (port 0), on CPU, or when the model
     is not a GPU-batched pipeline."""
-    if port <= 0 or server.device != "gpu":
+    if port <= 0 or server.device not in ("gpu", "fake"):
         return None
     m = server.models.get(model)
     backend = getattr(m, "backend", None)
@@ -321,10 +322,16 @@ def start_native_kserve(server: ModelServer, host: str, port: int, model: str = 
     from ..labels import load_labels
     from .native_front import NativeFrontEnd
 
-    fe = NativeFrontEnd(batcher, load_labels(None), port=port, host=host, arch="triton",
-                        io_threads=int(os.environ.get("ARENA_HTTP_THREADS", "4")),
-                        decode_threads=int(os.environ.get("ARENA_DECODE_THREADS", "8")),
-                        decode_procs=int(os.environ.get("ARENA_DECODE_PROCS", "1") or 1), kserve_model=model)
+    plan = (host or {}).get("plan") or {"http_io": int(os.environ.get("ARENA_HTTP_THREADS", "4")),
+                                         "decode_threads": int(os.environ.get("ARENA_DECODE_THREADS", "8"))}
+    fe = NativeFrontEnd(batcher, load_labels(None), port=port, host=host_ip, arch="triton",
+                        io_threads=plan["http_io"], decode_threads=plan["decode_threads"],
+                        decode_procs=int(os.environ.get("ARENA_DECODE_PROCS", "1") or 1), kserve_model=model,
+                        gpu=str((host or {}).get("gpu", 0)), jpeg_device=server.device == "gpu")
+    if host:
+        from ..parallel.affinity import rank_info_metrics
+
+        fe.extra_metrics = rank_info_metrics(dict(host, plan=plan), "triton")
     return fe
 
 
@@ -345,6 +352,16 @@ async def serve(args) -> None:
     setup_logging(args.log_level)
     from .replica import _socket
 
+    # one model-server process per GPU (scripts/start_arena.py --arch triton): ARENA_LOCAL_WORLD processes on the
+    # node, this one serving GPU args.gpu; it pins itself to that GPU's CPU share and sizes its threads for it
+    world = int(os.environ.get("ARENA_LOCAL_WORLD", "1") or 1)
+    host = None
+    if world > 1 or os.environ.get("ARENA_RANK_PLAN") == "1":
+        from ..parallel.affinity import rank_host_setup
+
+        host = rank_host_setup(args.gpu, world)
+        log.info(f"model server rank: gpu {args.gpu} of {world}, cpus {host['cpus']}, usable {host['usable_cpus']}, "
+                 f"host plan {host['plan']}")
     server = ModelServer(args.model_repository, device=args.device, gpu=args.gpu)
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
@@ -358,7 +375,7 @@ async def serve(args) -> None:
     for app, port in apps:
         socks.append(_socket(args.host, port, reuse_port=True))
         servers.append(_Server(uvicorn.Config(app, log_level="warning", access_log=False)))
-    native_fe = start_native_kserve(server, args.host, args.native_http_port)
+    native_fe = start_native_kserve(server, args.host, args.native_http_port, host=host)
     log.info(f"model server ready: grpc {args.grpc_port} http {args.http_port} metrics {args.metrics_port}"
              + (f" native-kserve {native_fe.port}" if native_fe else ""))
     tasks = [asyncio.create_task(s.serve(sockets=[k])) for s, k in zip(servers, socks)]
@@ -385,7 +402,7 @@ def main(argv=None) -> None:
     ap.add_argument("--metrics-port", type=int, default=8002)
     ap.add_argument("--native-http-port", type=int, default=int(os.environ.get("ARENA_KSERVE_NATIVE_PORT", "8004")),
                     help="native KServe-v2 REST endpoint of the arena_pipeline ensemble (0: off)")
-    ap.add_argument("--device", default=os.environ.get("ARENA_DEVICE", "gpu"), choices=["gpu", "cpu"])
+    ap.add_argument("--device", default=os.environ.get("ARENA_DEVICE", "gpu"), choices=["gpu", "cpu", "fake"])
     ap.add_argument("--gpu", type=int, default=int(os.environ.get("ARENA_GPU", "0")))
     ap.add_argument("--log-level", default=os.environ.get("LOG_LEVEL", "INFO"))
     from .decode_pool import prestart

@@ -16,7 +16,8 @@ Here every model of the repository is compiled into executor programs
 * the ensemble ``arena_pipeline`` (detector -> classifier) is compiled into
   ONE fused device program (``GpuPipeline``) instead of chaining models.
 
-``device="cpu"`` serves the same models with fp32 torch (tests, CPU arm).
+``device="cpu"`` serves the same models with fp32 torch (tests, CPU arm); ``device="fake"`` serves only the
+ensemble, on the host-only EchoInstance (CPU tests of the per-GPU process layout).
 """
 from __future__ import annotations
 
@@ -190,9 +191,21 @@ class PipelineModel(ModelHandle):
         if len(steps) != 2:
             raise ValueError(f"{self.name}: expected 2 ensemble steps (detector, classifier)")
         det_e, cls_e = models[steps[0].model_name], models[steps[1].model_name]
+        params = {k: v.string_value for k, v in entry.config.parameters.items()}
+        if device == "fake":  # host-only stand-in engine (CPU tests of the node layout): no networks to load
+            from .app_common import DecodePool
+            from .backends import FakeBatchedBackend
+
+            self.device = device
+            self.decode_pool = DecodePool(decode_threads)
+            self.native_decode = True
+            self.backend = FakeBatchedBackend(max_batch=int(params.get("max_batch", 32)),
+                                              max_queue_delay_us=int(params.get("max_queue_delay_microseconds", 500)),
+                                              overlap=int(os.environ.get("ARENA_BATCH_OVERLAP", "1")))
+            self.ready = True
+            return
         yolo = load_module(det_e.model_file(), det_e.name)
         mnet = load_module(cls_e.model_file(), cls_e.name)
-        params = {k: v.string_value for k, v in entry.config.parameters.items()}
         self.device = device
         # ARENA_DECODE_PROCS > 0: spawned decode processes with shared-memory delivery (PIL's numpy
         # conversion holds the GIL, so decode threads serialise against the gRPC handlers)
@@ -284,6 +297,8 @@ class ModelServer:
         self.models: dict[str, ModelHandle] = {}
         self.failed: dict[str, str] = {}
         wanted = models or list(self.entries)
+        if device == "fake":  # the fake engine stands in for the fused ensemble only
+            wanted = [n for n in wanted if self.entries[n].config.platform == mc.ENSEMBLE]
         for name in [n for n in wanted if self.entries[n].config.platform != mc.ENSEMBLE] + \
                     [n for n in wanted if self.entries[n].config.platform == mc.ENSEMBLE]:
             e = self.entries[name]

@@ -118,6 +118,7 @@ class NativeFrontEnd:
                                          **_http_timeouts(), **{k: int(v) for k, v in http.items()}})
         self.registry = CollectorRegistry()
         self.registry.register(_Collector(self, arch, gpu))
+        self.extra_metrics = ""  # appended to /metrics (e.g. the rank's host placement, affinity.rank_info_metrics)
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._refresh, name="native-front-metrics", daemon=True)
         self._thread.start()
@@ -143,7 +144,7 @@ class NativeFrontEnd:
 
         while not self._stop.is_set():
             try:
-                self.fe.set_metrics_text(generate_latest(self.registry).decode())
+                self.fe.set_metrics_text(generate_latest(self.registry).decode() + self.extra_metrics)
             except Exception as e:  # noqa: BLE001 - metrics must never stop the server
                 log.warning(f"metrics refresh failed: {e}")
             if trim_s > 0 and time.monotonic() - last_trim >= trim_s:
@@ -174,11 +175,25 @@ def serve(settings: Settings | None = None, *, weights=None, replica_tag: str = 
     devices = list(devices) if devices is not None else settings_devices(settings)
     instances = max(1, int(settings.ARENA_INSTANCES))
     max_batch = int(settings.ARENA_MAX_BATCH)
-    yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
-    buckets = sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
-    pipes = [build_session("pipeline", yolo, mnet, device=d, buckets=buckets, weights=weights) for d in devices
-             for _ in range(instances)]
-    batcher = native().DynamicBatcher([p.ex for p in pipes], {
+    fake = settings.ARENA_DEVICE == "fake"
+    # host placement of this replica: its GPU's CPU share and a host thread plan sized for it (ARENA_LOCAL_WORLD
+    # replicas on the node; parallel/affinity.py rank_host_setup)
+    from ..parallel.affinity import rank_host_setup, rank_info_metrics
+
+    world = int(os.environ.get("ARENA_LOCAL_WORLD", "1") or 1)
+    host = rank_host_setup(devices[0] if devices else 0, world, do_pin=world > 1)
+    if fake:
+        # host-only stand-in for the device (CPU tests of the node layout): fixed per-replica capacity
+        from .backends import fake_instance
+
+        exs = [fake_instance(max_batch) for _ in range(instances)]
+    else:
+        yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
+        buckets = sorted({b for b in (1, 2, 4, 8, 16, 32, max_batch) if b <= max_batch})
+        pipes = [build_session("pipeline", yolo, mnet, device=d, buckets=buckets, weights=weights) for d in devices
+                 for _ in range(instances)]
+        exs = [p.ex for p in pipes]
+    batcher = native().DynamicBatcher(exs, {
         "max_batch": max_batch, "max_queue_delay_us": int(settings.ARENA_QUEUE_DELAY_US),
         # a lone request on an idle device is not held for the full queue delay (bench.py batcher_config; the
         # protocol's 1-user level paid 0.51 ms of queue per request without it, profiles/protocol_r5/)
@@ -187,16 +202,20 @@ def serve(settings: Settings | None = None, *, weights=None, replica_tag: str = 
         # one process per GPU: admit due batches into free slots while older ones run (100 users: 8.4k vs 6.8k
         # req/s, profiles/r5ov/); the Triton arm's three model-server processes per GPU keep it off
         "overlap": int(os.environ.get("ARENA_BATCH_OVERLAP", "1"))})
+    plan = host["plan"] if world > 1 else {"http_io": int(os.environ.get("ARENA_HTTP_THREADS", "4")),
+                                           "decode_threads": int(os.environ.get("ARENA_DECODE_THREADS", "8"))}
     front = NativeFrontEnd(batcher, load_labels(settings.LABELS_FILE or None), port=int(settings.PORT),
-                           io_threads=int(os.environ.get("ARENA_HTTP_THREADS", "4")),
+                           io_threads=plan["http_io"],
                            # native split-decoder threads; the PIL processes only take what it does not cover
                            # (ARENA_DECODE_THREADS=0: all uploads through 10 PIL processes, the round-3 setup)
-                           decode_threads=int(os.environ.get("ARENA_DECODE_THREADS", "8")),
+                           decode_threads=plan["decode_threads"],
                            decode_procs=int(os.environ.get("ARENA_DECODE_PROCS", "0") or
-                                            (2 if int(os.environ.get("ARENA_DECODE_THREADS", "8")) > 0 else 10)),
+                                            (2 if plan["decode_threads"] > 0 else 10)),
                            softmax=(settings.ARENA_CONFIDENCE or "logit") == "softmax",
-                           gpu=",".join(str(d) for d in devices), replica_tag=replica_tag)
-    log.info("native monolithic front end ready", extra={"port": front.port, "gpus": devices})
+                           gpu=",".join(str(d) for d in devices), replica_tag=replica_tag, jpeg_device=not fake)
+    front.extra_metrics = rank_info_metrics(dict(host, plan=plan), "monolithic")
+    log.info("native monolithic front end ready", extra={"port": front.port, "gpus": devices,
+                                                         "cpus": host["cpus"], "host_plan": plan})
     done = threading.Event()
     if threading.current_thread() is threading.main_thread():
         for sig in (signal.SIGTERM, signal.SIGINT):

@@ -40,15 +40,24 @@ class NativeGateway:
                  replica_tag: str = ""):
         from ..ops import native
 
-        uh, _, up = upstream.rpartition(":")
-        self.upstream = (uh or "127.0.0.1", int(up))
+        # "host:port" or "host:port,host:port,...": one model server per GPU, least-outstanding first
+        self.upstreams = []
+        for item in (u.strip() for u in upstream.split(",")):
+            if item:
+                uh, _, up = item.rpartition(":")
+                self.upstreams.append((uh or "127.0.0.1", int(up)))
+        if not self.upstreams:
+            raise ValueError("native gateway: no upstream")
+        self.upstream = self.upstreams[0]
         self.model = model
         self.batcher = None
         self.fe = native().http_proxy_front(list(labels), {
             "host": host, "port": int(port), "io_threads": int(io_threads), "softmax_confidence": bool(softmax),
             "replica_tag": str(replica_tag), "upstream_host": self.upstream[0], "upstream_port": self.upstream[1],
+            "upstreams": ",".join(f"{h}:{p}" for h, p in self.upstreams[1:]),
             "upstream_model": model, "upstream_conns": int(conns), **_http_timeouts()})
         self.fe.set_healthy(False)
+        self.extra_metrics = ""
         self.registry = CollectorRegistry()
         self.registry.register(_Collector(self, "triton", "-"))
         self._stop = threading.Event()
@@ -62,13 +71,19 @@ class NativeGateway:
     def stats(self) -> dict:
         return self.fe.stats()
 
+    def upstream_forwarded(self) -> list[int]:
+        """Requests forwarded to each upstream so far (the proxy's least-outstanding spread)."""
+        return list(self.fe.upstream_forwarded())
+
     def upstream_ready(self) -> bool:
-        url = f"http://{self.upstream[0]}:{self.upstream[1]}/v2/models/{self.model}/ready"
-        try:
-            with urllib.request.urlopen(url, timeout=2) as r:
-                return r.status == 200
-        except OSError:
-            return False
+        for h, p in self.upstreams:
+            try:
+                with urllib.request.urlopen(f"http://{h}:{p}/v2/models/{self.model}/ready", timeout=2) as r:
+                    if r.status != 200:
+                        return False
+            except OSError:
+                return False
+        return True
 
     def wait_ready(self, timeout_s: float = 60.0) -> bool:
         """Backoff capped at 10 s (reference triton_client.py wait_for_server_ready); turns healthy once the
@@ -85,7 +100,7 @@ class NativeGateway:
     def _refresh(self) -> None:
         while not self._stop.is_set():
             try:
-                self.fe.set_metrics_text(generate_latest(self.registry).decode())
+                self.fe.set_metrics_text(generate_latest(self.registry).decode() + self.extra_metrics)
             except Exception as e:  # noqa: BLE001
                 log.warning(f"metrics refresh failed: {e}")
             self._stop.wait(1.0)
@@ -100,10 +115,23 @@ def serve(settings: Settings | None = None, replica_tag: str = "") -> int:
     setup_logging(settings.LOG_LEVEL)
     upstream = os.environ.get("TRITON_HTTP_ENDPOINT", "127.0.0.1:8004")
     port = int(os.environ.get("PORT", "8300"))
+    # ARENA_LOCAL_WORLD gateway processes (one per GPU, SO_REUSEPORT on :8300) each pin to their GPU's CPU share
+    world = int(os.environ.get("ARENA_LOCAL_WORLD", "1") or 1)
+    io_threads = int(os.environ.get("ARENA_HTTP_THREADS", "4"))
+    host = None
+    if world > 1:
+        from ..parallel.affinity import rank_host_setup
+
+        host = rank_host_setup(int(os.environ.get("ARENA_REPLICA_GPU", replica_tag or "0") or 0), world)
+        io_threads = host["plan"]["http_io"]
     gw = NativeGateway(load_labels(settings.LABELS_FILE or None), upstream=upstream, port=port,
-                       conns=int(os.environ.get("ARENA_GATEWAY_CONNS", "64")),
-                       io_threads=int(os.environ.get("ARENA_HTTP_THREADS", "4")),
+                       conns=int(os.environ.get("ARENA_GATEWAY_CONNS", "64")), io_threads=io_threads,
                        softmax=(settings.ARENA_CONFIDENCE or "logit") == "softmax", replica_tag=replica_tag)
+    if host is not None:
+        from ..parallel.affinity import rank_info_metrics
+
+        gw.extra_metrics = rank_info_metrics(dict(host, plan={"http_io": io_threads}), "gateway")
+        log.info(f"gateway rank {replica_tag}: cpus {host['cpus']}, usable {host['usable_cpus']}, io {io_threads}")
     if not gw.wait_ready(float(settings.TRITON_TIMEOUT_SECONDS)):
         log.error(f"model server native endpoint {upstream} not ready")
         gw.close()

@@ -120,14 +120,17 @@ def _serve_native(settings, info, port: int, rank: int | None = None) -> int:
     from ..parallel import dist as D
     from .native_front import serve
 
-    yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
-    blob = plan_pipeline(yolo, mnet, conf_thr=0.0, iou_thr=0.0,  # weights only: thresholds unused
-                         dtype=resolve_dtype()).weights if info.is_main else None
-    blob = D.broadcast_blob(blob, info)
+    if settings.ARENA_DEVICE == "fake":  # host-only stand-in engine: no weights to broadcast
+        blob = None
+    else:
+        yolo, mnet = resolve_models(settings.MODELS_DIR, int(settings.ARENA_WEIGHT_SEED))
+        blob = plan_pipeline(yolo, mnet, conf_thr=0.0, iou_thr=0.0,  # weights only: thresholds unused
+                             dtype=resolve_dtype()).weights if info.is_main else None
+        blob = np.ascontiguousarray(D.broadcast_blob(blob, info))
     D.barrier(info)
     D.shutdown(info)
     settings.PORT = port
-    return serve(settings, weights=np.ascontiguousarray(blob), replica_tag=str(info.rank if rank is None else rank),
+    return serve(settings, weights=blob, replica_tag=str(info.rank if rank is None else rank),
                  devices=[int(settings.ARENA_GPU)])
 
 
@@ -151,13 +154,13 @@ def main(argv=None) -> int:
     prestart()  # decode-worker fork server before any GPU initialisation (server/decode_pool.py)
     settings = Settings.from_env()
     per_gpu = max(1, int(os.environ.get("ARENA_PROCS_PER_GPU", "1")))
-    backend = "gloo" if settings.ARENA_DEVICE == "cpu" or per_gpu > 1 else None
+    backend = "gloo" if settings.ARENA_DEVICE in ("cpu", "fake") or per_gpu > 1 else None
     info = D.init_from_env(backend)
     if settings.ARENA_DEVICE != "cpu":
         override = os.environ.get("ARENA_REPLICA_GPU")
         first = int(os.environ.get("ARENA_FIRST_GPU", "0"))
         settings.ARENA_GPU = int(override) if override else first + info.local_rank // per_gpu
-        if backend == "gloo":
+        if backend == "gloo" and settings.ARENA_DEVICE == "gpu":
             import torch
 
             torch.cuda.set_device(settings.ARENA_GPU)

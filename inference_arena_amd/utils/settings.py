@@ -46,7 +46,7 @@ class Settings(BaseModel):
     TRITON_HTTP_ENDPOINT: str = "127.0.0.1:8000"
     TRITON_TIMEOUT_SECONDS: float = 60.0
     # arena additions
-    ARENA_DEVICE: str = "gpu"          # gpu | cpu
+    ARENA_DEVICE: str = "gpu"          # gpu | cpu | fake (host-only EchoInstance: CPU tests of node layouts)
     ARENA_GPU: int = 0
     ARENA_GPUS: str = ""               # GPUs one process drives ("0,1" / "0-7"); '' = ARENA_GPU only
     ARENA_CLS_GPU: int = -1            # split topology: classification GPU (crops handed over device to device)

@@ -7,8 +7,8 @@ scripts/start-*.sh): each service is a child process; Ctrl-C stops them all.
                  detection HTTP :8200 replicas (one per GPU) fanning crops over all classification services
                  (least-outstanding gRPC channel pool); --split puts detection on the first half of the
                  GPUs and classification on the second half
-  triton         model server :8000/:8001/:8002 driving every GPU (ensemble pipeline on each listed GPU,
-                 tensor models: instance_group gpus) + gateway :8300
+  triton         one model server per GPU (shared :8000/:8001/:8002, native KServe :8004 + 10 g) + one native
+                 gateway per GPU on :8300 spreading requests over every model server (least outstanding)
 
 Example: python scripts/start_arena.py --arch triton --gpus 1
 """
@@ -71,6 +71,29 @@ def wait_http(url: str, timeout: float, procs) -> bool:
     return False
 
 
+def wait_replicas(url: str, n: int, timeout: float, procs) -> bool:
+    """Replicas sharing one port (SO_REUSEPORT): poll ``url`` on fresh connections until ``n`` distinct
+    ``x-arena-replica`` tags have answered 200 (the port opens with the first replica; the others may still be
+    starting)."""
+    import urllib.request
+
+    seen: set[str] = set()
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if any(p.poll() is not None for p in procs):
+            return False
+        try:
+            with urllib.request.urlopen(url, timeout=2) as r:
+                if r.status == 200:
+                    seen.add(r.headers.get("x-arena-replica", ""))
+        except OSError:
+            pass
+        if len(seen) >= n:
+            return True
+        time.sleep(0.05)
+    return False
+
+
 def classification_ports(n: int, base: int = 8201) -> list[int]:
     return [base + 10 * i for i in range(max(1, n))]
 
@@ -89,6 +112,14 @@ def plan_microservices(gpus: int, split: bool = False, cls_procs_per_gpu: int = 
     pairs = [(g, p + j) for g, p in zip(cls, classification_ports(len(cls))) for j in range(k)]
     return {"detection_gpus": det, "classification": pairs,
             "endpoint": ",".join(f"127.0.0.1:{p}" for _, p in pairs)}
+
+
+def plan_triton(gpus: int, procs_per_gpu: int = 1, base_port: int | None = None) -> dict:
+    """Process layout of the Triton arm on ``gpus`` GPUs: (gpu, k, native KServe port) per model-server process —
+    ``procs_per_gpu`` per GPU on ports base + 10 g + k — and the gateway's upstream list over all of them."""
+    base = int(base_port if base_port is not None else os.environ.get("ARENA_KSERVE_NATIVE_PORT", "8004"))
+    ms = [(g, k, base + 10 * g + k) for g in range(max(1, gpus)) for k in range(max(1, procs_per_gpu))]
+    return {"model_servers": ms, "upstreams": ",".join(f"127.0.0.1:{p}" for _, _, p in ms)}
 
 
 def hw_queues_per_process(procs_on_gpu: int) -> int | None:
@@ -120,7 +151,7 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
         procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "monolithic", "--gpus", str(gpus),
                             "--port", "8100", "--procs-per-gpu", str(procs_per_gpu)],
                            _queue_env(env, procs_per_gpu), log_dir, "monolithic"))
-        ok = wait_http("http://127.0.0.1:8100/health", 600, procs)
+        ok = wait_replicas("http://127.0.0.1:8100/health", max(1, gpus) * max(1, procs_per_gpu), 600, procs)
     elif arch == "microservices":
         cls_k = int(os.environ.get("ARENA_CLS_PROCS_PER_GPU", "1"))
         plan = plan_microservices(gpus, split, cls_k)
@@ -140,26 +171,32 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
         if not (Path(repo) / "yolov5n" / "config.pbtxt").exists():
             subprocess.run([sys.executable, str(ROOT / "scripts" / "upload_models.py"), "--repository", repo],
                            check=True, env=env)
-        ms_env = _queue_env(dict(env, ARENA_GPUS=f"0-{max(1, gpus) - 1}"),  # the ensemble runs on every GPU
-                            procs_per_gpu)
-        # one model-server process per GPU owns the device: its batches overlap in free slots, as the monolithic
-        # server's do (several processes per GPU keep it off: smaller overlapping batches compete for the device)
+        plan = plan_triton(gpus, procs_per_gpu)
+        # one model-server process per GPU: each owns its device, pins itself to that GPU's
+        # CPU share with a host plan sized for it (parallel/affinity.py rank_host_setup) and serves its own native
+        # KServe endpoint; gRPC :8001 / HTTP :8000 / metrics :8002 are shared (SO_REUSEPORT) for Triton clients.
+        # Its batches overlap in free slots, as the monolithic server's do (several processes per GPU keep it off)
+        ms_env = _queue_env(dict(env, ARENA_LOCAL_WORLD=str(max(1, gpus))), procs_per_gpu)
         ms_env.setdefault("ARENA_BATCH_OVERLAP", "1" if procs_per_gpu <= 1 else "0")
-        for k in range(max(1, procs_per_gpu)):  # server processes share :8000/:8001/:8002 (SO_REUSEPORT)
+        for g, k, port in plan["model_servers"]:
             procs.append(spawn(["inference_arena_amd.server.model_server", "--model-repository", repo, "--device",
-                                device], ms_env, log_dir, f"model_server_{k}"))
-        ok = wait_http("http://127.0.0.1:8000/v2/health/ready", 600, procs)
+                                device, "--gpu", str(g), "--native-http-port", str(port)],
+                               dict(ms_env, ARENA_GPUS=str(g), ARENA_GPU=str(g)), log_dir, f"model_server_gpu{g}_{k}"))
+        ok = all(wait_http(f"http://127.0.0.1:{port}/v2/health/ready", 600, procs)
+                 for _, _, port in plan["model_servers"])
         if ok:
-            # ARENA_GATEWAY_NATIVE (default 1): the gateway's native proxy front end forwards to the model server's
-            # native KServe REST endpoint (:8004); 0 keeps the Python gateway on gRPC :8001
+            # ARENA_GATEWAY_NATIVE (default 1): native gateway processes, one per GPU on :8300 (SO_REUSEPORT), each
+            # spreading requests over every model server's native endpoint (least outstanding); 0 keeps the Python
+            # gateway on gRPC :8001
             gw_native = os.environ.get("ARENA_GATEWAY_NATIVE", "1") != "0"
-            procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "gateway", "--gpus", "1",
-                                "--port", "8300", "--procs-per-gpu", str(procs_per_gpu)],
+            procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "gateway", "--gpus",
+                                str(max(1, gpus) if gw_native else 1), "--port", "8300",
+                                "--procs-per-gpu", str(1 if gw_native else procs_per_gpu)],
                                dict(env, TRITON_GRPC_ENDPOINT="127.0.0.1:8001", ARENA_DEVICE="cpu",
-                                    TRITON_HTTP_ENDPOINT="127.0.0.1:" + os.environ.get("ARENA_KSERVE_NATIVE_PORT", "8004"),
+                                    TRITON_HTTP_ENDPOINT=plan["upstreams"],
                                     ARENA_GATEWAY_NATIVE="1" if gw_native else "0"), log_dir,
                                "gateway"))
-            ok = wait_http("http://127.0.0.1:8300/health", 300, procs)
+            ok = wait_replicas("http://127.0.0.1:8300/health", max(1, gpus) if gw_native else 1, 300, procs)
     else:
         raise ValueError(arch)
     return procs, ok
@@ -181,7 +218,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--arch", required=True, choices=["monolithic", "microservices", "triton"])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu"])
+    ap.add_argument("--device", default="gpu", choices=["gpu", "cpu", "fake"],
+                    help="fake: host-only stand-in engines (CPU tests of the process layout)")
     ap.add_argument("--logs", default="logs")
     ap.add_argument("--procs-per-gpu", type=int, default=1)
     ap.add_argument("--split", action="store_true",
