@@ -207,6 +207,12 @@ def _children_cpu() -> float:
     return t.children_user + t.children_system
 
 
+def torch_device() -> int:
+    import torch
+
+    return int(torch.cuda.current_device())
+
+
 class HostCpu:
     """Host CPU per request over a window, by thread class (+ the decode-pool child processes)."""
 
@@ -275,10 +281,18 @@ def _measure(lg, a, info, D, sync, users, fe, batcher):
         def opened():
             holder["cpu"] = HostCpu(fe)
             holder["b0"] = batcher.stats() if batcher is not None else None
+            if not a.fake_engine:  # device busy over the timed window, 20 Hz (metrics/gpu.py BusySampler)
+                from inference_arena_amd.metrics.gpu import BusySampler
+
+                ident = D.device_identity(torch_device(), info.rank)
+                holder["busy"] = BusySampler(ident.get("pci_bus_id"), torch_device()).start()
         window, c0 = _window(a, info, D, sync, lg.completed, wait_until, users, on_open=opened)
+        busy = holder["busy"].stop() if "busy" in holder else None
         n = a.steps * a.batch * a.step_batches
         us, stages = holder["cpu"].per_request(n)
         cpu = {"host_cpu_us_per_req": us, "stage_cpu_us_per_req": stages}
+        if busy is not None:
+            cpu["gpu_busy"] = busy
         if batcher is not None:
             cpu["mean_batch"] = _batch_mean(holder["b0"], batcher.stats())
     finally:
@@ -698,6 +712,9 @@ def main(argv=None) -> int:
                 "usable_cpus_per_rank": [int(x[0]) for x in all_cpu],
                 "cpu_budget_warning": budget_warning,
                 "host_cpu_us_per_req": ext0.get("host_cpu_us_per_req"),
+                # device busy percent over each rank's timed window, sampled at 20 Hz (amdsmi gfx_activity)
+                "gpu_busy": [(x or {}).get("gpu_busy") for x in all_ext] if any(x and x.get("gpu_busy") for x in all_ext)
+                else None,
                 "stage_cpu_us_per_req": ext0.get("stage_cpu_us_per_req"),
                 "world_size_checked": info.world,
                 "torch_world_size": torch_world,

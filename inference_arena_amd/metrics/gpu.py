@@ -155,3 +155,68 @@ def main(argv=None) -> int:
 
 if __name__ == "__main__":
     raise SystemExit(main())
+
+
+class BusySampler:
+    """GPU busy percent of one device sampled at ``hz`` (default 20) on a thread over a window (bench.py's timed
+    window: VERDICT r5 asked for >= 10 Hz; the driver's own smi samples were 4 per run).  The device is found by
+    PCI bus id (``domain:bus:device.function``, as parallel/dist.py device_identity reports it), else by index.
+    ``stop()`` returns {mean_percent, samples, hz, seconds} or {"samples": 0, "error": ...} without amdsmi."""
+
+    def __init__(self, bus_id: str | None = None, index: int = 0, hz: float = 20.0):
+        self.hz = float(hz)
+        self.samples: list[float] = []
+        self.t0 = self.t1 = 0.0
+        self.error = None
+        self._stop = threading.Event()
+        self._thread = None
+        self.smi = _try_amdsmi()
+        self.handle = None
+        if self.smi is None:
+            self.error = "amdsmi not importable"
+            return
+        try:
+            hs = self.smi.amdsmi_get_processor_handles()
+            want = (bus_id or "").lower()
+            for h in hs:
+                try:
+                    if want and str(self.smi.amdsmi_get_gpu_device_bdf(h)).lower() == want:
+                        self.handle = h
+                        break
+                except Exception:  # noqa: BLE001
+                    pass
+            if self.handle is None and 0 <= index < len(hs):
+                self.handle = hs[index]
+        except Exception as e:  # noqa: BLE001
+            self.error = f"amdsmi: {e}"
+
+    def start(self) -> "BusySampler":
+        if self.handle is None:
+            return self
+        self.t0 = time.perf_counter()
+        self._thread = threading.Thread(target=self._run, name="arena-busy", daemon=True)
+        self._thread.start()
+        return self
+
+    def _run(self) -> None:
+        period = 1.0 / self.hz
+        nxt = time.perf_counter()
+        while not self._stop.is_set():
+            try:
+                self.samples.append(float(self.smi.amdsmi_get_gpu_activity(self.handle)["gfx_activity"]))
+            except Exception as e:  # noqa: BLE001
+                self.error = str(e)
+                return
+            nxt += period
+            self._stop.wait(max(0.0, nxt - time.perf_counter()))
+
+    def stop(self) -> dict:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=2.0)
+        self.t1 = time.perf_counter()
+        if not self.samples:
+            return {"samples": 0, "error": self.error or "no sample"}
+        secs = self.t1 - self.t0
+        return {"mean_percent": round(sum(self.samples) / len(self.samples), 1), "samples": len(self.samples),
+                "hz": round(len(self.samples) / secs, 1) if secs > 0 else None, "seconds": round(secs, 2)}
