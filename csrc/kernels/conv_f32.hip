@@ -1575,6 +1575,11 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
   if (p.Cin < 16) throw std::runtime_error("conv2d_f32: Cin must be >= 16");
   if (p.Kpad < p.KH * p.KW * p.Cin) throw std::runtime_error("conv2d_f32: Kpad < KH*KW*Cin");
   if (p.pw_w != nullptr) {  // fused Detect-head 1x1: only the x3hg epilogue variants implement it
+    if (p.impl >= kF32X3HRPw && p.impl < kF32X3HRPw + kF32X3HRPwVariants) {
+      if (!conv_x3hr_pw(p, s, p.impl - kF32X3HRPw))
+        throw std::runtime_error("conv2d_f32: a fused pointwise epilogue needs an x3hr-pw variant that fits the conv");
+      return;
+    }
     const int v = p.impl >= kF32X3HGPw && p.impl < kF32X3HGPw + kF32X3HGPwVariants ? p.impl - kF32X3HGPw
                   : p.impl == 0                                                    ? (p.Cout_pad <= 64 ? 0 : 2)
                                                                                    : -1;
@@ -1602,6 +1607,11 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
     if (p.impl >= kF32X3HG && p.impl < kF32X3HG + kF32X3HGVariants) {
       if (!conv_x3hg(p, s, p.impl - kF32X3HG))
         throw std::runtime_error("conv2d_f32: not an x3hg-eligible conv (3x3 s1 with pre-split weights)");
+      return;
+    }
+    if (p.impl >= kF32X3HR && p.impl < kF32X3HR + kF32X3HRVariants) {
+      if (!conv_x3hr(p, s, p.impl - kF32X3HR))
+        throw std::runtime_error("conv2d_f32: not an x3hr-eligible conv (3x3 s1 with pre-split weights)");
       return;
     }
     if (p.impl == kF32X3H16) {

@@ -103,6 +103,14 @@ void x3hg_prepare();
 constexpr int kF32X3HGPw = 145;
 constexpr int kF32X3HGPwVariants = 6;
 bool conv_x3hg_pw(const ConvParams& p, hipStream_t s, int v);
+// x3hr: the x3hg tiles with per-wave register weights (no weight LDS stage, two barriers per 16-channel chunk),
+// variant v; and with the fused Detect-head 1x1
+constexpr int kF32X3HR = 151;
+constexpr int kF32X3HRVariants = 10;
+constexpr int kF32X3HRPw = 161;
+constexpr int kF32X3HRPwVariants = 6;
+bool conv_x3hr(const ConvParams& p, hipStream_t s, int v);
+bool conv_x3hr_pw(const ConvParams& p, hipStream_t s, int v);
 bool conv_fc_f32(const ConvParams& p, hipStream_t s);
 void conv2d_f32(const ConvParams& p, hipStream_t s);
 

@@ -325,7 +325,9 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
                                 v == kF32Fc || v == kF32StreamExact || v == kF32X3Halo16 || v == kF32X3Halo16N3 ||
                                 v == kF32X3H16 || (v >= kF32X3G && v < kF32X3G + kF32X3GVariants) ||
                                 (v >= kF32X3HG && v < kF32X3HG + kF32X3HGVariants) ||
-                                (v >= kF32X3HGPw && v < kF32X3HGPw + kF32X3HGPwVariants)
+                                (v >= kF32X3HGPw && v < kF32X3HGPw + kF32X3HGPwVariants) ||
+                                (v >= kF32X3HR && v < kF32X3HR + kF32X3HRVariants) ||
+                                (v >= kF32X3HRPw && v < kF32X3HRPw + kF32X3HRPwVariants)
                           : v >= 0 && v <= 3;
       if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
       bk.impl[i] = (int16_t)v;
@@ -379,7 +381,12 @@ void Executor::autotune(Bucket& bk) {
                                        kF32X3HG + 7, kF32X3HG + 8, kF32X3HG + 9, kF32X3HG + 10,
                                        // ... with the fused Detect-head 1x1 (the only kernels that take those ops)
                                        kF32X3HGPw + 0, kF32X3HGPw + 1, kF32X3HGPw + 2, kF32X3HGPw + 3,
-                                       kF32X3HGPw + 4, kF32X3HGPw + 5};
+                                       kF32X3HGPw + 4, kF32X3HGPw + 5,
+                                       // x3hr: the same tiles with per-wave register weights (halo_x3g.hip)
+                                       kF32X3HR + 0, kF32X3HR + 1, kF32X3HR + 2, kF32X3HR + 3, kF32X3HR + 4,
+                                       kF32X3HR + 5, kF32X3HR + 6, kF32X3HR + 7, kF32X3HR + 8, kF32X3HR + 9,
+                                       kF32X3HRPw + 0, kF32X3HRPw + 1, kF32X3HRPw + 2, kF32X3HRPw + 3,
+                                       kF32X3HRPw + 4, kF32X3HRPw + 5};
   static const int kBf16Candidates[] = {1, 2, 3};
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;

@@ -148,6 +148,8 @@ def test_conv_x3g_channel_slices_and_live_batch(device):
 
 
 X3HG_IMPLS = [131 + v for v in range(14)]  # x3hg: 3x3 s1 halo tiles, 32x32x16 MFMA, pre-split weights
+X3HR_IMPLS = [151 + v for v in range(10)]  # x3hr: the same tiles, per-wave register weights (halo_x3g.hip)
+X3HG_IMPLS = X3HG_IMPLS + X3HR_IMPLS
 
 
 @pytest.mark.parametrize(
@@ -188,7 +190,7 @@ def test_conv_x3hg_matches_fp64(device, B, H, Cin, Cout, act, res, up, s):
             assert torch.equal(out2.permute(0, 3, 1, 2), want), impl
 
 
-X3HG_PW_IMPLS = [145 + v for v in range(6)]  # x3hg with the Detect-head 1x1 fused into the epilogue
+X3HG_PW_IMPLS = [145 + v for v in range(6)] + [161 + v for v in range(6)]  # x3hg / x3hr with the fused 1x1
 
 
 @pytest.mark.parametrize("B,H,Cin,C", [(2, 20, 64, 64), (2, 19, 80, 80), (3, 11, 144, 64)])
@@ -219,6 +221,38 @@ def test_conv_x3hg_fused_pointwise_matches_fp64(device, B, H, Cin, C):
         _fp32_check(y.permute(0, 3, 1, 2), ref, scale)
         ran += 1
     assert ran >= 3
+
+
+# x3hg variant -> the x3hr variant with the same tile (TW, WM, WN, TM, TN)
+X3HR_SAME_TILE = {131: 151, 132: 152, 134: 153, 135: 154, 137: 155, 142: 156, 139: 157, 140: 158, 133: 159,
+                  141: 160}
+
+
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 20, 64, 144), (2, 19, 80, 80), (3, 13, 48, 64)])
+def test_conv_x3hr_bit_identical_to_x3hg(device, B, H, Cin, Cout):
+    """x3hr changes where the weights come from (registers, not an LDS stage), not the arithmetic: same tile, same
+    products in the same order, so the outputs equal x3hg's bit for bit, plain and with the fused 1x1."""
+    g = torch.Generator().manual_seed(B + H + Cin + Cout)
+    x = torch.randn(B, H, H, Cin, generator=g).to(device)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=g) * 0.1
+    packed = AF.pack_weights(w, b, device, "fp32")
+    for hg, hr in X3HR_SAME_TILE.items():
+        y0 = AF.conv2d_nhwc(x, w, b, act="silu", packed=packed, impl=hg)
+        y1 = AF.conv2d_nhwc(x, w, b, act="silu", packed=packed, impl=hr)
+        torch.cuda.synchronize()
+        assert torch.equal(y0, y1), (hg, hr)
+    if Cout in (64, 80):
+        w2 = torch.randn(Cout, Cout, 1, 1, generator=g) / Cout ** 0.5
+        b2 = torch.randn(Cout, generator=g) * 0.1
+        for v in range(6):
+            try:
+                y0 = AF.conv2d_nhwc(x, w, b, act="silu", packed=packed, impl=145 + v, pw=(w2, b2))
+            except RuntimeError:
+                continue
+            y1 = AF.conv2d_nhwc(x, w, b, act="silu", packed=packed, impl=161 + v, pw=(w2, b2))
+            torch.cuda.synchronize()
+            assert torch.equal(y0, y1), v
 
 
 def test_conv_x3hg_channel_slices_and_live_batch(device):

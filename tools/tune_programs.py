@@ -19,6 +19,8 @@ def main(argv=None) -> int:
     ap.add_argument("--buckets", default="1,2,4,8,16,32")
     ap.add_argument("--dtypes", default="fp32,bf16")
     ap.add_argument("--base", default=None, help="table to start from (default: empty)")
+    ap.add_argument("--kinds", default="pipeline,detector,classifier,yolo_raw,mobilenet_raw",
+                    help="program kinds to retune (the others keep their --base entries)")
     a = ap.parse_args(argv)
     if a.base:
         Path(a.out).parent.mkdir(parents=True, exist_ok=True)
@@ -37,6 +39,8 @@ def main(argv=None) -> int:
                 ("classifier", lambda: GpuClassifier(m, device=0, buckets=[b for b in bk if b >= 4] + [64], dtype=dt)),
                 ("yolo_raw", lambda: GpuTensorModel.yolo(y, device=0, buckets=bk, dtype=dt)),
                 ("mobilenet_raw", lambda: GpuTensorModel.mobilenet(m, device=0, buckets=bk, dtype=dt))):
+            if name not in a.kinds.split(","):
+                continue
             r = make()
             print(dt, name, {B: sum(1 for c in r.ex.conv_choices(B) if c) for B in r.buckets}, flush=True)
             del r
