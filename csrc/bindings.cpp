@@ -436,7 +436,9 @@ std::shared_ptr<JpegSet> make_jpeg_set(const py::list& uploads, bool pinned) {
     std::string err;
     JpegStatus st = jpeg_parse((const uint8_t*)data.data(), data.size(), it->info, err);
     if (st != JpegStatus::Ok) throw py::value_error("JpegSet: not decodable by the split decoder: " + err);
-    const size_t bytes = std::max<size_t>(2, (size_t)it->info.coef_count * 2);
+    const bool compact = jpeg_compact_enabled();  // the serving paths' payload (http_front.cpp native_decode)
+    const size_t bytes =
+        std::max<size_t>(2, compact ? (size_t)jpeg_compact_capacity(it->info) : (size_t)it->info.coef_count * 2);
     void* p = nullptr;
     if (pinned && hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess) {
       it->pinned = true;
@@ -446,7 +448,8 @@ std::shared_ptr<JpegSet> make_jpeg_set(const py::list& uploads, bool pinned) {
       if (p == nullptr) throw std::bad_alloc();
     }
     it->coef = (int16_t*)p;
-    st = jpeg_decode_coefs((const uint8_t*)data.data(), data.size(), it->info, it->coef, err);
+    st = compact ? jpeg_decode_compact((const uint8_t*)data.data(), data.size(), it->info, (uint8_t*)it->coef, err)
+                 : jpeg_decode_coefs((const uint8_t*)data.data(), data.size(), it->info, it->coef, err);
     if (st != JpegStatus::Ok) throw py::value_error("JpegSet: entropy decode failed: " + err);
     set->items.push_back(it);
   }
@@ -775,7 +778,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init(&make_jpeg_set), py::arg("uploads"), py::arg("pinned") = true,
            "JPEG uploads entropy-decoded once into (pinned) host buffers, for Executor.submit_jpeg_set")
       .def("__len__", [](const JpegSet& s) { return s.items.size(); })
-      .def("coef_bytes", [](const JpegSet& s, int i) { return (int64_t)s.items.at(i)->info.coef_count * 2; })
+      .def("coef_bytes", [](const JpegSet& s, int i) { return (int64_t)jpeg_payload_bytes(s.items.at(i)->info); })
       .def_property_readonly("pinned", [](const JpegSet& s) {
         for (const auto& it : s.items)
           if (!it->pinned) return false;

@@ -27,7 +27,10 @@ struct JpegDesc {
   int64_t rgb_off;       // packed HxWx3 RGB output (the ImageMeta offset the pipeline reads)
   JpegCompDesc comp[kJpegMaxComp];
   uint16_t qt[kJpegMaxComp][64];  // dequantization table per component, natural order
-  uint8_t reserved_[32];
+  // compact payload (runtime/jpeg_decode.h jpeg_decode_compact; comp[].coef_off unused): per block a uint64
+  // zigzag mask at cmask_off, a uint32 first-value index at cvoff_off, int16 values in zigzag order at cval_off
+  int64_t cmask_off, cvoff_off, cval_off;
+  int32_t compact, pad2_;
 };
 static_assert(sizeof(JpegDesc) == 576, "JpegDesc layout is shared with the kernels");
 

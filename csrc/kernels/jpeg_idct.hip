@@ -29,6 +29,9 @@ namespace {
 
 constexpr int kBlocksPerGroup = 32;  // 8x8 blocks per 256-lane workgroup
 
+// natural index -> zigzag index (the compact payload stores each block's coded coefficients in zigzag order)
+__constant__ uint8_t kZigzagOf[64] = {0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43, 9, 11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60, 21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDesc* __restrict__ descs, uint8_t* __restrict__ pool) {
   __shared__ int32_t ws[kBlocksPerGroup][8][9];  // +1 column: pass-1 column reads hit distinct banks
   const JpegDesc& d = descs[blockIdx.y];
@@ -50,7 +53,24 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDesc* __restri
   const JpegCompDesc& cd = d.comp[c];
   // row l of the block: 8 int16 coefficients (16 B) and the matching 8 quantizer steps
   int32_t row[8];
-  if (live) {
+  if (live && d.compact) {
+    // compact payload (runtime/jpeg_decode.h jpeg_decode_compact): the block's zigzag mask and first value; the
+    // coefficient at natural (l, k) is value popcount(mask below its zigzag bit) when its bit is set
+    const uint64_t mask = reinterpret_cast<const uint64_t*>(pool + d.cmask_off)[blk];
+    const int32_t v0 = (int32_t)reinterpret_cast<const uint32_t*>(pool + d.cvoff_off)[blk];
+    const int16_t* vals = reinterpret_cast<const int16_t*>(pool + d.cval_off);
+    const uint4 qv = *reinterpret_cast<const uint4*>(&d.qt[c][l * 8]);
+    const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int z = kZigzagOf[l * 8 + k];
+      const uint64_t below = mask & ((1ull << z) - 1ull);
+      const int idx = v0 + __popcll(below);
+      const int32_t cf = (mask >> z) & 1ull ? (int32_t)vals[idx] : 0;
+      const int32_t q = (int32_t)((k & 1) ? (qw[k >> 1] >> 16) : (qw[k >> 1] & 0xFFFF));
+      row[k] = cf * q;
+    }
+  } else if (live) {
     const uint4 cv = *reinterpret_cast<const uint4*>(pool + cd.coef_off + (int64_t)b * 128 + l * 16);
     const uint4 qv = *reinterpret_cast<const uint4*>(&d.qt[c][l * 8]);
     const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w}, qw[4] = {qv.x, qv.y, qv.z, qv.w};

@@ -60,7 +60,10 @@ void DynamicBatcher::shutdown() {
 int64_t staged_bytes(const InputImage& im) {
   auto a = [](int64_t v) { return (v + 255) / 256 * 256; };
   if (im.jpeg != nullptr)
-    return a((int64_t)im.h * im.w * 3) + a(im.jpeg->coef_count * 2) + a(im.jpeg->plane_bytes);
+    return a((int64_t)im.h * im.w * 3) +
+           a(im.jpeg->compact_bytes >= 0 ? im.jpeg->compact_bytes
+                                         : std::max(im.jpeg->coef_count * 2, jpeg_compact_capacity(*im.jpeg))) +
+           a(im.jpeg->plane_bytes);
   return a(im.bytes > 0 ? im.bytes : (int64_t)im.h * im.w * 3);
 }
 

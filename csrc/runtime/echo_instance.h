@@ -56,7 +56,8 @@ class EchoInstance : public BatchInstance {
       uint8_t first = imgs[i].data[0];
       if (imgs[i].jpeg != nullptr) {  // split-decoded JPEG: reconstruct like the device would (host reference)
         std::vector<uint8_t> rgb((size_t)imgs[i].h * imgs[i].w * 3);
-        jpeg_coefs_to_rgb(*imgs[i].jpeg, (const int16_t*)imgs[i].data, rgb.data());
+        std::vector<int16_t> dense;
+        jpeg_coefs_to_rgb(*imgs[i].jpeg, jpeg_dense_coefs(*imgs[i].jpeg, imgs[i].data, dense), rgb.data());
         first = rgb[0];
       }
       const int k_n = std::min(max_det_, 1 + first % max_det_);

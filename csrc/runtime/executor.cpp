@@ -1051,7 +1051,7 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
         need = align_up(need + (imgs[i].bytes > 0 ? (size_t)imgs[i].bytes : (size_t)imgs[i].h * imgs[i].w * 3), 256);
     if (pack_coefs)  // the JPEGs' coefficients follow them in the same DMA (layout below)
       for (int i = 0; i < n; ++i)
-        if (imgs[i].jpeg != nullptr) need = align_up(need + (size_t)imgs[i].jpeg->coef_count * 2, 256);
+        if (imgs[i].jpeg != nullptr) need = align_up(need + (size_t)jpeg_payload_bytes(*imgs[i].jpeg), 256);
     if (need > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
     if (in_bytes_meta() + need > sl.h_cap) {
       uint8_t* grown = nullptr;
@@ -1116,7 +1116,7 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     for (int i = 0; i < n; ++i) {
       const InputImage& im = imgs[i];
       if (im.jpeg == nullptr) continue;
-      const size_t len = (size_t)im.jpeg->coef_count * 2;
+      const size_t len = (size_t)jpeg_payload_bytes(*im.jpeg);  // compact or dense coefficients
       if (off + len > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
       coef_at[i] = off;
       jobs.emplace_back([dst = pool + off, src = im.data, len]() { std::memcpy(dst, src, len); });
@@ -1130,14 +1130,15 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     const JpegInfo& ji = *im.jpeg;
     if (ji.width != im.w || ji.height != im.h) throw std::runtime_error("submit: JPEG geometry mismatch");
     const size_t rgb = off, coef = pack_coefs ? coef_at[i] : align_up(rgb + (size_t)im.h * im.w * 3, 256);
-    const size_t planes = align_up((pack_coefs ? rgb + (size_t)im.h * im.w * 3 : coef + (size_t)ji.coef_count * 2), 256);
+    const size_t planes =
+        align_up((pack_coefs ? rgb + (size_t)im.h * im.w * 3 : coef + (size_t)jpeg_payload_bytes(ji)), 256);
     const size_t end = align_up(planes + (size_t)ji.plane_bytes, 256);
     if (end > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
     set_meta(i, im, rgb);
     jdesc[nj] = jpeg_device_desc(ji, (int64_t)coef, (int64_t)planes, (int64_t)rgb);
     max_blocks = std::max(max_blocks, jdesc[nj].total_blocks);
     max_pix = std::max(max_pix, (int64_t)im.h * im.w);
-    if (!pack_coefs) jcopies.push_back({coef, im.data, (size_t)ji.coef_count * 2});
+    if (!pack_coefs) jcopies.push_back({coef, im.data, (size_t)jpeg_payload_bytes(ji)});
     ++nj;
     off = end;
   }

@@ -1281,12 +1281,16 @@ void HttpFrontEnd::native_decode(DecodeTask& t) {
   InputImage probe = in;
   probe.jpeg = &ji;
   bool device = cfg_.jpeg_device && (cap <= 0 || staged_bytes(probe) <= cap);
+  // compact coefficients (ARENA_JPEG_COMPACT, default 1): about a third of the dense blocks' bytes at q90, so a
+  // third of the pack copy and of the batch's H2D
+  const bool compact = jpeg_compact_enabled();
   if (device) {
-    up->buf = host_pool_->get((size_t)ji.coef_count * 2);
+    up->buf = host_pool_->get(compact ? (size_t)jpeg_compact_capacity(ji) : (size_t)ji.coef_count * 2);
     device = (bool)up->buf;
   }
   if (device) {
-    st = jpeg_decode_coefs(data, t.len, ji, (int16_t*)up->buf.get(), err);
+    st = compact ? jpeg_decode_compact(data, t.len, up->info, up->buf.get(), err)
+                 : jpeg_decode_coefs(data, t.len, ji, (int16_t*)up->buf.get(), err);
     in.data = up->buf.get();
     in.jpeg = &up->info;
   } else {

@@ -2,6 +2,7 @@
 #include "runtime/jpeg_decode.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -244,6 +245,57 @@ __attribute__((always_inline)) inline bool decode_block(BitReader& br, const Huf
   return true;
 }
 
+
+// The same block in the compact layout (jpeg_decode.h, jpeg_decode_compact): bit k of *mask set for every coded
+// coefficient at zigzag index k, their values appended to vals in zigzag order (the DC always, even when 0).
+__attribute__((always_inline)) inline bool decode_block_compact(BitReader& br, const HuffTable& dc, const HuffTable& ac,
+                                                                int& pred, uint64_t* mask, int16_t* vals, int64_t& nv) {
+  br.need(32);
+  const int s = br.decode(dc);
+  if (s) {
+    if (s > 15) return false;
+    pred += extend(br.get(s), s);
+  }
+  uint64_t m = 1;
+  int64_t n = nv;
+  vals[n++] = (int16_t)pred;
+  for (int k = 1; k < 64;) {
+    br.need(32);
+    const int32_t f = ac.ac_fast[br.buf >> (64 - kFastBits)];
+    if (f) {
+      br.skip(f & 0xFF);
+      k += (f >> 8) & 0xFF;
+      if (k > 63) break;
+      m |= 1ull << k;
+      vals[n++] = (int16_t)(f >> 16);
+      ++k;
+      continue;
+    }
+    const int rs = br.decode(ac);
+    const int r = rs >> 4, sz = rs & 15;
+    if (sz) {
+      k += r;
+      const int16_t v = (int16_t)extend(br.get(sz), sz);
+      if (k > 63) {  // a corrupt run past the block: the dense decoder's kNatural pad stores it at 63
+        if (m >> 63) vals[n - 1] = v;  // zigzag 63 is the last value appended
+        else {
+          m |= 1ull << 63;
+          vals[n++] = v;
+        }
+      } else {
+        m |= 1ull << k;
+        vals[n++] = v;
+      }
+      ++k;
+    } else {
+      if (r != 15) break;
+      k += 16;
+    }
+  }
+  *mask = m;
+  nv = n;
+  return true;
+}
 
 }  // namespace
 
@@ -593,6 +645,131 @@ JpegStatus jpeg_decode_coefs(const uint8_t* data, size_t n, const JpegInfo& info
   return JpegStatus::Ok;
 }
 
+int64_t jpeg_total_blocks(const JpegInfo& info) {
+  int64_t t = 0;
+  for (int c = 0; c < info.ncomp; ++c) t += (int64_t)info.comp[c].bw * info.comp[c].bh;
+  return t;
+}
+
+int64_t jpeg_compact_capacity(const JpegInfo& info) {
+  const int64_t tb = jpeg_total_blocks(info);
+  return ((tb * 12 + 15) & ~(int64_t)15) + tb * 128;
+}
+
+bool jpeg_compact_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("ARENA_JPEG_COMPACT");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+int64_t jpeg_payload_bytes(const JpegInfo& info) { return info.compact_bytes >= 0 ? info.compact_bytes : info.coef_count * 2; }
+
+JpegStatus jpeg_decode_compact(const uint8_t* data, size_t n, JpegInfo& info, uint8_t* out, std::string& err) {
+  thread_local std::unique_ptr<TableCache> cache;
+  if (!cache) cache.reset(new TableCache());
+  const HuffTable* dcp[kJpegMaxComp] = {};
+  const HuffTable* acp[kJpegMaxComp] = {};
+  ++cache->gen;
+  for (int c = 0; c < info.ncomp; ++c) {
+    dcp[c] = cache->get(info.dc[info.td[c]], false);
+    acp[c] = dcp[c] ? cache->get(info.ac[info.ta[c]], true) : nullptr;
+    if (!dcp[c] || !acp[c]) {
+      err = "Failed to decode image: bad Huffman table";
+      return JpegStatus::Corrupt;
+    }
+  }
+  const int64_t tb = jpeg_total_blocks(info);
+  uint64_t* masks = (uint64_t*)out;
+  uint32_t* voff = (uint32_t*)(out + tb * 8);
+  const int64_t val_at = (tb * 12 + 15) & ~(int64_t)15;
+  int16_t* vals = (int16_t*)(out + val_at);
+  int64_t nv = 0;
+  BitReader br{data + info.scan_begin, data + n};
+  int pred[kJpegMaxComp] = {0, 0, 0};
+  const bool single = info.ncomp == 1;
+  const int64_t n_mcu = single ? (int64_t)info.comp[0].bw * info.comp[0].bh : (int64_t)info.mcux * info.mcuy;
+  const int ri = info.restart_interval;
+  int todo = ri;
+  bool starved = false;
+  auto block = [&](int c, int64_t gb) -> bool {
+    voff[gb] = (uint32_t)nv;
+    if (starved) {  // insufficient data: an all-zero block, predictions untouched (jdhuff.c decode_mcu)
+      masks[gb] = 0;
+      return true;
+    }
+    return decode_block_compact(br, *dcp[c], *acp[c], pred[c], masks + gb, vals, nv);
+  };
+  for (int64_t m = 0; m < n_mcu; ++m) {
+    if (ri) {
+      if (todo == 0) {
+        br.restart();
+        pred[0] = pred[1] = pred[2] = 0;
+        todo = ri;
+        starved = br.p + 1 < br.end && br.p[0] == 0xFF && br.p[1] != 0x00 && !(br.p[1] >= 0xD0 && br.p[1] <= 0xD7)
+                      ? starved : false;
+      }
+      --todo;
+    }
+    const bool was_starved = starved;
+    if (single) {
+      if (!block(0, m)) {
+        err = "Failed to decode image: bad DC magnitude";
+        return JpegStatus::Corrupt;
+      }
+    } else {
+      const int my = (int)(m / info.mcux), mx = (int)(m % info.mcux);
+      for (int c = 0; c < info.ncomp; ++c) {
+        const JpegCompDesc& d = info.comp[c];
+        for (int v = 0; v < d.v; ++v)
+          for (int h = 0; h < d.h; ++h) {
+            const int64_t gb = d.coef_off / 64 + ((int64_t)my * d.v + v) * d.bw + (int64_t)mx * d.h + h;
+            if (!block(c, gb)) {
+              err = "Failed to decode image: bad DC magnitude";
+              return JpegStatus::Corrupt;
+            }
+          }
+      }
+    }
+    if (!was_starved) starved = br.starved();
+  }
+  if (br.truncated || br.overran()) {
+    err = "Failed to decode image: image file is truncated";
+    return JpegStatus::Corrupt;
+  }
+  info.compact_bytes = val_at + nv * 2;
+  info.cmask_off = 0;
+  info.cvoff_off = tb * 8;
+  info.cval_off = val_at;
+  return JpegStatus::Ok;
+}
+
+void jpeg_compact_to_dense(const JpegInfo& info, const uint8_t* payload, int16_t* coef) {
+  const int64_t tb = jpeg_total_blocks(info);
+  const uint64_t* masks = (const uint64_t*)(payload + info.cmask_off);
+  const uint32_t* voff = (const uint32_t*)(payload + info.cvoff_off);
+  const int16_t* vals = (const int16_t*)(payload + info.cval_off);
+  for (int64_t b = 0; b < tb; ++b) {
+    int16_t* blk = coef + b * 64;
+    std::memset(blk, 0, 64 * sizeof(int16_t));
+    uint64_t m = masks[b];
+    int64_t i = voff[b];
+    while (m) {
+      const int k = __builtin_ctzll(m);
+      blk[kNatural[k]] = vals[i++];
+      m &= m - 1;
+    }
+  }
+}
+
+const int16_t* jpeg_dense_coefs(const JpegInfo& info, const uint8_t* payload, std::vector<int16_t>& scratch) {
+  if (info.compact_bytes < 0) return (const int16_t*)payload;
+  scratch.resize((size_t)info.coef_count);
+  jpeg_compact_to_dense(info, payload, scratch.data());
+  return scratch.data();
+}
+
 void jpeg_coefs_to_rgb(const JpegInfo& info, const int16_t* coef, uint8_t* rgb) {
   using namespace jpegm;
   std::vector<uint8_t> planes((size_t)info.plane_bytes);
@@ -670,6 +847,12 @@ JpegDesc jpeg_device_desc(const JpegInfo& info, int64_t coef_base, int64_t plane
     std::memcpy(d.qt[c], info.qt[c], sizeof d.qt[c]);
   }
   d.total_blocks = (int32_t)total;
+  if (info.compact_bytes >= 0) {  // compact payload at coef_base (jpeg_decode_compact)
+    d.compact = 1;
+    d.cmask_off = coef_base + info.cmask_off;
+    d.cvoff_off = coef_base + info.cvoff_off;
+    d.cval_off = coef_base + info.cval_off;
+  }
   return d;
 }
 

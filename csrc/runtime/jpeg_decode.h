@@ -18,6 +18,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../kernels/jpeg_desc.h"
 
@@ -41,6 +42,9 @@ struct JpegInfo {
   int64_t coef_count = 0;                // int16 coefficients of all components
   int64_t plane_bytes = 0;               // reconstructed sample planes of all components
   size_t scan_begin = 0;                 // first byte of the entropy-coded segment
+  // compact payload (jpeg_decode_compact): its bytes and the byte offsets of its three arrays; -1 = dense int16
+  int64_t compact_bytes = -1;
+  int64_t cmask_off = 0, cvoff_off = 0, cval_off = 0;
   JpegHuffSpec dc[4], ac[4];
 };
 
@@ -55,6 +59,24 @@ JpegStatus jpeg_parse(const uint8_t* data, size_t n, JpegInfo& info, std::string
 // marker is padded with zero bits (libjpeg's warning, which PIL ignores); a file that simply ends inside the
 // scan is Corrupt ("image file is truncated", as PIL raises), like structurally broken streams.
 JpegStatus jpeg_decode_coefs(const uint8_t* data, size_t n, const JpegInfo& info, int16_t* coef, std::string& err);
+
+// The same scan into the compact payload the split decoder ships (3-4x fewer bytes than the dense blocks at q90:
+// most AC coefficients are zero).  Per 8x8 block, in the dense layout's block order (component 0's blocks row by
+// row, then 1, 2): a uint64 mask (bit k: the coefficient at zigzag index k is coded), then per block the uint32
+// index of its first value, then the int16 values of every block in zigzag order (16-byte aligned array).  `out`
+// holds jpeg_compact_capacity(info) bytes; on success info.compact_bytes / cmask_off / cvoff_off / cval_off
+// describe what was written.  Status and error messages as jpeg_decode_coefs.
+JpegStatus jpeg_decode_compact(const uint8_t* data, size_t n, JpegInfo& info, uint8_t* out, std::string& err);
+int64_t jpeg_total_blocks(const JpegInfo& info);
+int64_t jpeg_compact_capacity(const JpegInfo& info);
+// bytes of the decoded payload (compact, or dense int16)
+int64_t jpeg_payload_bytes(const JpegInfo& info);
+// ARENA_JPEG_COMPACT (default 1): the serving paths decode into the compact payload; 0 keeps dense blocks
+bool jpeg_compact_enabled();
+// compact payload -> dense int16 blocks (host reference paths)
+void jpeg_compact_to_dense(const JpegInfo& info, const uint8_t* payload, int16_t* coef);
+// the payload as dense blocks: itself when dense, else expanded into `scratch`
+const int16_t* jpeg_dense_coefs(const JpegInfo& info, const uint8_t* payload, std::vector<int16_t>& scratch);
 
 // Host reconstruction with the device kernels' exact arithmetic (kernels/jpeg_math.h): packed HxWx3 RGB.
 void jpeg_coefs_to_rgb(const JpegInfo& info, const int16_t* coef, uint8_t* rgb);

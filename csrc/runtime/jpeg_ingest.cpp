@@ -116,12 +116,14 @@ void JpegIngest::run(Task& t) {
     InputImage probe = in;
     probe.jpeg = &ji;
     bool device = cfg_.jpeg_device && (cap <= 0 || staged_bytes(probe) <= cap);
+    const bool compact = jpeg_compact_enabled();
     if (device) {
-      up->buf = pool_->get((size_t)ji.coef_count * 2);
+      up->buf = pool_->get(compact ? (size_t)jpeg_compact_capacity(ji) : (size_t)ji.coef_count * 2);
       device = (bool)up->buf;
     }
     if (device) {
-      st = jpeg_decode_coefs(data, t.upload.size(), ji, (int16_t*)up->buf.get(), err);
+      st = compact ? jpeg_decode_compact(data, t.upload.size(), up->info, up->buf.get(), err)
+                   : jpeg_decode_coefs(data, t.upload.size(), ji, (int16_t*)up->buf.get(), err);
       in.data = up->buf.get();
       in.jpeg = &up->info;
     } else {

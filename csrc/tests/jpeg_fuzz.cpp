@@ -21,6 +21,10 @@ using arena::JpegStatus;
 
 namespace {
 
+int compact_mismatches = 0;
+
+// dense decode, and the compact decode (jpeg_decode_compact) of the same bytes: same status, and the compact
+// payload expanded equals the dense blocks coefficient for coefficient
 JpegStatus run(const std::vector<uint8_t>& d) {
   JpegInfo info;
   std::string err;
@@ -28,6 +32,20 @@ JpegStatus run(const std::vector<uint8_t>& d) {
   if (st != JpegStatus::Ok) return st;
   std::vector<int16_t> coef((size_t)info.coef_count);
   st = arena::jpeg_decode_coefs(d.data(), d.size(), info, coef.data(), err);
+  {
+    JpegInfo ci = info;
+    std::vector<uint8_t> payload((size_t)arena::jpeg_compact_capacity(ci));
+    std::string cerr;
+    const JpegStatus cs = arena::jpeg_decode_compact(d.data(), d.size(), ci, payload.data(), cerr);
+    if (cs != st) {
+      ++compact_mismatches;
+    } else if (cs == JpegStatus::Ok) {
+      if (ci.compact_bytes > (int64_t)payload.size()) ++compact_mismatches;
+      std::vector<int16_t> dense((size_t)ci.coef_count);
+      arena::jpeg_compact_to_dense(ci, payload.data(), dense.data());
+      if (dense != coef) ++compact_mismatches;
+    }
+  }
   if (st != JpegStatus::Ok) return st;
   std::vector<uint8_t> rgb((size_t)info.width * info.height * 3);
   arena::jpeg_coefs_to_rgb(info, coef.data(), rgb.data());
@@ -124,7 +142,12 @@ int main(int argc, char** argv) {
     }
     counts[(int)run(d)]++;
   }
-  std::printf("jpeg_fuzz: ok (%d over-subscribed tables rejected; random: %d ok, %d unsupported, %d corrupt)\n",
+  if (compact_mismatches) {
+    std::printf("jpeg_fuzz: %d compact decodes differ from the dense decode\n", compact_mismatches);
+    return 1;
+  }
+  std::printf("jpeg_fuzz: ok (%d over-subscribed tables rejected; random: %d ok, %d unsupported, %d corrupt; compact "
+              "== dense on all)\n",
               rejected, counts[0], counts[1], counts[2]);
   return 0;
 }
