@@ -14,6 +14,17 @@ if [ -n "$TESTS" ]; then
   tail -2 gpurun_out/$T/pytest.log
   grep -q " failed\| error" gpurun_out/$T/pytest.log && exit 1
 fi
+if [ -n "${TESTS2:-}" ]; then
+  $S 900 gpurun_out/$T/pytest2.log python -u -m pytest $TESTS2 -x -q --timeout 180 --timeout-method thread -p no:cacheprovider || exit 1
+  tail -2 gpurun_out/$T/pytest2.log
+  grep -q " failed\| error" gpurun_out/$T/pytest2.log && exit 1
+fi
+if [ -n "${REPRO:-}" ]; then  # HIP-only retention repro (csrc/tests/hip_retention_repro.cpp), each mode
+  for m in $REPRO; do
+    $S 240 gpurun_out/$T/repro_$m.log tools/bin/hip_retention_repro $m 6000 32 || exit 1
+    tail -1 gpurun_out/$T/repro_$m.log
+  done
+fi
 if [ -n "$MB" ]; then
   $S 600 gpurun_out/$T/mb.log python -u tools/bench_x3g.py $MB || exit 1
   grep -v "^\[gpu_step\]" gpurun_out/$T/mb.log | cut -c1-2000
