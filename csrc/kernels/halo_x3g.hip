@@ -534,12 +534,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3hr_kernel(const ConvParam
       __syncthreads();
     }
   };
-  int cc = 0;
-  for (; cc + 1 < nc; cc += 2) {
-    chunk(cc, wa, wb);      // taps 0, 2, .. 8 in wa; the next chunk's tap 0 lands in wb
-    chunk(cc + 1, wb, wa);
+  // even chunks run taps 0, 2, .. 8 from wa and leave the next chunk's tap 0 in wb; odd chunks the other way round
+  // (one loop, two bodies: a separate odd-count remainder body miscompiled for one tile shape on ROCm 7.2)
+  for (int cc = 0; cc < nc; ++cc) {
+    if ((cc & 1) == 0) chunk(cc, wa, wb);
+    else chunk(cc, wb, wa);
   }
-  if (cc < nc) chunk(cc, wa, wb);
 
   hg_epilogue<TW, WM, WN, TM, TN, PWN>(p, acc, b, oy0, ox0, n0, wm, wn, lane);
 }
