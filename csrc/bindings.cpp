@@ -1169,6 +1169,8 @@ PYBIND11_MODULE(_C, m) {
              d["sum_gpu_ms"] = s.sum_gpu_ms;
              d["native_decoded"] = s.native_decoded;
              d["fallback_decoded"] = s.fallback_decoded;
+             d["bodies_recycled"] = s.bodies_recycled;
+             d["bodies_allocated"] = s.bodies_allocated;
              d["cpu_parse_ms"] = s.cpu_parse_ms;
              d["cpu_decode_ms"] = s.cpu_decode_ms;
              d["cpu_json_ms"] = s.cpu_json_ms;

@@ -29,8 +29,13 @@ namespace {
 
 constexpr int kBlocksPerGroup = 32;  // 8x8 blocks per 256-lane workgroup
 
-// natural index -> zigzag index (the compact payload stores each block's coded coefficients in zigzag order)
-__constant__ uint8_t kZigzagOf[64] = {0, 1, 5, 6, 14, 15, 27, 28, 2, 4, 7, 13, 16, 26, 29, 42, 3, 8, 12, 17, 25, 30, 41, 43, 9, 11, 18, 24, 31, 40, 44, 53, 10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60, 21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
+// natural index -> zigzag index (the compact payload stores each block's coded coefficients in zigzag order),
+// packed for the lanes of a block: byte l of kZigzagCol[k] is the zigzag index of natural (row l, column k).  The
+// row is a lane's, so an indexed table would be one divergent memory load per coefficient; as 64-bit literals
+// the lookup is a shift of an immediate.
+constexpr uint64_t kZigzagCol[8] = {0x2315140a09030200ull, 0x242216130b080401ull, 0x30252117120c0705ull,
+                                    0x312f262018110d06ull, 0x39322e271f19100eull, 0x3a38332d281e1a0full,
+                                    0x3e3b37342c291d1bull, 0x3f3d3c36352b2a1cull};
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDesc* __restrict__ descs, uint8_t* __restrict__ pool) {
   __shared__ int32_t ws[kBlocksPerGroup][8][9];  // +1 column: pass-1 column reads hit distinct banks
@@ -63,10 +68,10 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegDesc* __restri
     const uint32_t qw[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int z = kZigzagOf[l * 8 + k];
-      const uint64_t below = mask & ((1ull << z) - 1ull);
-      const int idx = v0 + __popcll(below);
-      const int32_t cf = (mask >> z) & 1ull ? (int32_t)vals[idx] : 0;
+      const int z = (int)((kZigzagCol[k] >> (8 * l)) & 0xFF);
+      const int idx = v0 + __popcll(mask & ((1ull << z) - 1ull));
+      int32_t cf = 0;
+      if ((mask >> z) & 1ull) cf = (int32_t)vals[idx];  // zero coefficients issue no load
       const int32_t q = (int32_t)((k & 1) ? (qw[k >> 1] >> 16) : (qw[k >> 1] & 0xFFFF));
       row[k] = cf * q;
     }

@@ -203,6 +203,7 @@ class Executor : public BatchInstance {
     size_t h_cap = 0;  // bytes of h_in (meta + host-packed inputs; grows on demand)
     uint8_t* h_out = nullptr;
     hipEvent_t copied = nullptr, started = nullptr, done = nullptr;
+    hipEvent_t phase = nullptr;  // staggered launch: the batch reached the program's split op (ARENA_STAGGER)
     hipStream_t copy_stream = nullptr;  // ARENA_COPY_MODE=3: this slot's own copy stream
     // Each slot owns an activation arena; its batch runs on one of the
     // executor's compute streams (round-robin by submission), so in-flight
@@ -227,6 +228,8 @@ class Executor : public BatchInstance {
     uint8_t* d_arena[kMaxSlots] = {};  // per slot (all aliased when concurrency is off)
     int last_slot = 0;                 // slot whose arena read_arena() inspects
     hipGraphExec_t graph[kMaxSlots] = {};
+    // staggered launch (ARENA_STAGGER): graph[s] holds ops [0, split), graph2[s] ops [split, end)
+    hipGraphExec_t graph2[kMaxSlots] = {};
     // Lane buckets (program lanes, B <= lanes_max_batch()): the program as contiguous single-lane segments, one
     // graph each; launch_graph() runs lane segments on the slot's side streams between fork / join events.
     // (A single graph with forked branches made HIP's graph launch segfault with GPU_MAX_HW_QUEUES < 4 from the
@@ -291,6 +294,12 @@ class Executor : public BatchInstance {
   hipStream_t streams_[kMaxSlots] = {};  // compute streams (streams_[0] == compute_)
   int n_streams_ = 1;
   uint64_t seq_ = 0;                     // batches submitted
+  // Staggered launch (ARENA_STAGGER = fraction f of the program's ops, 0 = off): a batch's graph starts only once
+  // the previously launched batch passed op round(f * ops), so the batches in flight on the compute streams sit
+  // at different phases of the program instead of drifting into step (launch_graph)
+  double stagger_ = 0.0;
+  int stagger_min_batch_ = 16;  // ARENA_STAGGER_MIN_BATCH: buckets below it launch unstaggered
+  int last_launched_ = -1;  // slot of the last staggered launch
   bool has_topk_ = false, has_det_ = false, has_raw_ = false, has_stamps_ = false;
   double wall_khz_ = 100000.0;  // wall_clock64 rate (hipDeviceAttributeWallClockRate)
   bool peer_stage_ = false;

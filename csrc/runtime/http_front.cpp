@@ -310,6 +310,7 @@ HttpFrontEnd::HttpFrontEnd(DynamicBatcher* batcher, DecodeChannel dc, std::vecto
       ups.push_back(u);
     }
     proxy_.reset(new KServeProxy(std::move(ups), cfg_.upstream_model, cfg_.upstream_conns));
+    proxy_->set_recycler(&bodies_);
     cfg_.decode_threads = 0;
   }
   if (!cfg_.handler_mode && !proxy) {
@@ -491,8 +492,14 @@ void HttpFrontEnd::set_metrics_text(std::string text) {
 }
 
 FrontStats HttpFrontEnd::stats() {
-  std::lock_guard<std::mutex> lk(stats_mu_);
-  return stats_;
+  FrontStats s;
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    s = stats_;
+  }
+  s.bodies_recycled = (int64_t)bodies_.hits();
+  s.bodies_allocated = (int64_t)bodies_.misses();
+  return s;
 }
 
 void HttpFrontEnd::io_loop(int idx) {
@@ -794,7 +801,7 @@ bool HttpFrontEnd::parse_one_impl(const std::shared_ptr<Conn>& c) {
   if (chunked) {
     // resume where the previous read stopped: chunks already appended stay in chunk_body
     size_t pos = c->chunk_pos ? c->chunk_pos : body0;
-    body = std::move(c->chunk_body);
+    body = c->chunk_pos ? std::move(c->chunk_body) : bodies_.get();
     auto suspend = [&]() {
       c->chunk_pos = pos;
       c->chunk_body = std::move(body);
@@ -831,6 +838,7 @@ bool HttpFrontEnd::parse_one_impl(const std::shared_ptr<Conn>& c) {
     if (clen < 0) clen = 0;
     if (clen > cfg_.max_body) return bad(413, "request body too large");
     if (in.size() < body0 + (size_t)clen) return false;
+    body = bodies_.get();  // a recycled body's capacity: no allocation in steady state
     body.assign(in, body0, (size_t)clen);
     consumed = body0 + (size_t)clen;
   }
@@ -958,7 +966,12 @@ void HttpFrontEnd::predict(const std::shared_ptr<Conn>& c, std::string&& body, c
     return;
   }
   t_predict_dispatched = true;
-  if (proxy_) return proxy_predict(c, t0, body.substr(off, len));
+  if (proxy_) {
+    std::string upload = bodies_.get();
+    upload.assign(body, off, len);
+    bodies_.put(std::move(body));
+    return proxy_predict(c, t0, std::move(upload));  // the proxy worker recycles it once forwarded
+  }
   start_upload(c, t0, std::move(body), off, len, 0);
 }
 
@@ -1259,6 +1272,7 @@ void HttpFrontEnd::decode_loop(int idx) {
       dq_.pop_front();
     }
     native_decode(*t);
+    bodies_.put(std::move(t->body));  // back to the I/O threads' next requests, not to this thread's allocator
   }
 }
 

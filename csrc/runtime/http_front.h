@@ -58,6 +58,7 @@
 #include "kserve.h"
 #include "host_pool.h"
 #include "http_loadgen.h"
+#include "string_pool.h"
 
 namespace arena {
 
@@ -124,6 +125,7 @@ struct FrontStats {
   int64_t requests = 0, ok = 0, bad_request = 0, too_large = 0, unavailable = 0, errors = 0, not_found = 0;
   int64_t connections = 0, open_connections = 0, detections = 0, timeouts = 0;
   int64_t native_decoded = 0, fallback_decoded = 0;  // uploads decoded by the split decoder / the PIL pool
+  int64_t bodies_recycled = 0, bodies_allocated = 0;  // request bodies served by the body pool / newly grown
   double sum_total_ms = 0, sum_decode_ms = 0, sum_queue_ms = 0, sum_gpu_ms = 0;
   // host CPU time (thread CPU clock) of request stages, summed: HTTP + multipart parse on the I/O threads, the
   // native decode (marker parse + entropy decode), the JSON response built in the batcher callback
@@ -240,6 +242,9 @@ class HttpFrontEnd {
   void callback_done();
 
   DynamicBatcher* batcher_;
+  // request bodies: filled on the I/O threads, released on the decode threads / proxy workers, recycled here
+  // instead of freed (runtime/string_pool.h); declared before proxy_, so it outlives the proxy's workers
+  StringPool bodies_;
   std::unique_ptr<KServeProxy> proxy_;  // proxy mode (cfg_.upstream_port > 0)
   DecodeChannel dc_;
   std::vector<std::string> labels_;

@@ -686,6 +686,7 @@ void KServeProxy::worker(int index) {
   std::vector<int> fds(ups_.size(), -1);
   uint64_t seq = 0;
   int rotation = index;
+  std::string req;
   while (true) {
     Task t;
     {
@@ -702,9 +703,11 @@ void KServeProxy::worker(int index) {
     ProxyReply rep;
     int64_t ihcl = -1;
     const std::string payload = kserve_build_request(t.upload, "", &ihcl);
-    std::string req = "POST /v2/models/" + model_ + "/infer HTTP/1.1\r\nHost: " + up.host +
-                      "\r\nContent-Type: application/octet-stream\r\nInference-Header-Content-Length: " +
-                      std::to_string(ihcl) + "\r\nContent-Length: " + std::to_string(payload.size()) + "\r\n\r\n";
+    if (recycle_) recycle_->put(std::move(t.upload));
+    req.clear();  // the worker's request buffer, reused
+    req += "POST /v2/models/" + model_ + "/infer HTTP/1.1\r\nHost: " + up.host +
+           "\r\nContent-Type: application/octet-stream\r\nInference-Header-Content-Length: " +
+           std::to_string(ihcl) + "\r\nContent-Length: " + std::to_string(payload.size()) + "\r\n\r\n";
     req += payload;
     std::string body, err;
     bool ok = false;

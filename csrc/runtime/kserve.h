@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "batcher.h"
+#include "string_pool.h"
 
 namespace arena {
 
@@ -84,6 +85,8 @@ class KServeProxy {
   int num_upstreams() const { return (int)ups_.size(); }
   // requests forwarded to upstream i so far
   int64_t forwarded_to(int i) const { return ups_[(size_t)i].forwarded.load(); }
+  // uploads go back to this pool once forwarded (the front end's body pool: no cross-thread frees)
+  void set_recycler(StringPool* pool) { recycle_ = pool; }
 
  private:
   struct Task {
@@ -111,6 +114,7 @@ class KServeProxy {
   bool stop_ = false;
   std::vector<std::thread> threads_;
   std::atomic<int64_t> forwarded_{0}, reconnects_{0};
+  StringPool* recycle_ = nullptr;
 };
 
 }  // namespace arena

@@ -402,6 +402,8 @@ def test_split_decoder_answers_like_the_pil_pool(jpeg_device):
             answers[threads] = out
             s = fe.stats()
             assert (s["native_decoded"], s["fallback_decoded"]) == ((8, 0) if threads else (0, 8))
+            if threads:  # request bodies come back from the decode threads to the body pool (string_pool.h)
+                assert s["bodies_recycled"] >= 4, s
         finally:
             fe.close()
             batcher.shutdown()
@@ -552,6 +554,7 @@ def test_kserve_rest_route_and_native_gateway():
         r = c.getresponse()
         assert r.status == 404 and "error" in json.loads(r.read())
         assert gw.stats()["ok"] == 6 and ms.stats()["ok"] == 18  # direct + KServe + via the gateway
+        assert gw.stats()["bodies_recycled"] >= 3  # uploads return from the proxy workers to the body pool
     finally:
         gw.close()
         ms.close()

@@ -18,6 +18,10 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--batches", type=int, default=150)
     ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--inputs", default="rgb", choices=["rgb", "jpeg"],
+                    help="rgb: decoded frames packed on the host (engine_rgb_req_s); jpeg: the workload encoded as "
+                         "JPEG q90 and entropy-decoded once into pinned buffers, coefficient H2D + GPU "
+                         "reconstruction per batch (bench.py engine_req_s)")
     a = ap.parse_args(argv)
     import torch
 
@@ -30,12 +34,19 @@ def main(argv=None) -> int:
     yolo, mnet = default_models(0)
     pipe = GpuPipeline(yolo, mnet, device=0, buckets=sorted({1, a.batch}), dtype=a.dtype)
     info = DistInfo(rank=0, world=1, local_rank=0, backend="none")
-    images, _ = bench.load_workload(pipe, info, 100, 0, a.dtype)
-    bench.engine_throughput(pipe.ex, images, a.batch, 10)
+    images, man = bench.load_workload(pipe, info, 100, 0, a.dtype)
+    jset = None
+    if a.inputs == "jpeg":
+        from inference_arena_amd.data.synthetic import encode_jpeg
+        from inference_arena_amd.ops import native
+
+        q = int(man.config.get("jpeg_quality", 90))
+        jset = native().JpegSet([encode_jpeg(im, q) for im in images], pinned=True)
+    bench.engine_throughput(pipe.ex, images, a.batch, 10, jset)
     t = time.perf_counter()
-    r = bench.engine_throughput(pipe.ex, images, a.batch, a.batches)
+    r = bench.engine_throughput(pipe.ex, images, a.batch, a.batches, jset)
     knobs = {k: v for k, v in os.environ.items() if k.startswith("ARENA_")}
-    print(f"engine {r:.0f} req/s ({a.batches} batches of {a.batch}, {time.perf_counter() - t:.1f}s) {knobs}", flush=True)
+    print(f"engine {r:.0f} req/s ({a.inputs}, {a.batches} batches of {a.batch}, {time.perf_counter() - t:.1f}s) {knobs}", flush=True)
     return 0
 
 

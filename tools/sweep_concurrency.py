@@ -24,6 +24,7 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--batches", type=int, default=60)
     ap.add_argument("--configs", default="4x3,2x2,3x3,5x4,6x4,6x3,8x4")
+    ap.add_argument("--inputs", default="jpeg", choices=["rgb", "jpeg"], help="see tools/engine_probe.py")
     a = ap.parse_args(argv)
     import torch
 
@@ -36,14 +37,20 @@ def main(argv=None) -> int:
     man = DatasetManifest.load(ROOT / "data" / "synthetic_set" / f"manifest_w0_n100{sfx}.json")
     images = load_manifest_images(man)
     models = default_models(0)
+    jset = None
+    if a.inputs == "jpeg":
+        from inference_arena_amd.data.synthetic import encode_jpeg
+        from inference_arena_amd.ops import native
+
+        jset = native().JpegSet([encode_jpeg(im, 90) for im in images], pinned=True)
     torch.cuda.set_device(0)
     out = []
     for cfg in a.configs.split(","):
         slots, conc = (int(v) for v in cfg.split("x"))
         os.environ["ARENA_SLOTS"], os.environ["ARENA_CONCURRENCY"] = str(slots), str(conc)
         pipe = GpuPipeline(*models, device=0, buckets=[a.batch], dtype=a.dtype)
-        engine_throughput(pipe, images, a.batch, 10)
-        r = [engine_throughput(pipe, images, a.batch, a.batches) for _ in range(2)]
+        engine_throughput(pipe.ex, images, a.batch, 10, jset)
+        r = [engine_throughput(pipe.ex, images, a.batch, a.batches, jset) for _ in range(2)]
         row = {"slots": pipe.ex.num_slots(), "streams": conc, "req_s": [round(v, 1) for v in r]}
         print(json.dumps(row), flush=True)
         out.append(row)
