@@ -63,7 +63,17 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
     // staggered launch: 0.25 of the ops is ~22 % of the fp32 program's device time; measured on 1x MI355X
     // (profiles/r6_stagger): engine req/s 9491 -> 10080 with the compact JPEG payload, 9707 -> 10105 dense
     const char* sg = std::getenv("ARENA_STAGGER");
-    stagger_ = concurrent_ && n_streams_ > 1 ? std::min(0.95, std::max(0.0, sg != nullptr ? std::atof(sg) : 0.25)) : 0.0;
+    if (concurrent_ && n_streams_ > 1) {
+      std::string spec = sg != nullptr ? sg : "0.25";
+      for (size_t a = 0; a < spec.size();) {
+        size_t e = spec.find(',', a);
+        if (e == std::string::npos) e = spec.size();
+        const double f = std::atof(spec.substr(a, e - a).c_str());
+        if (f > 0.0 && f < 1.0 && (int)stagger_.size() < kMaxStaggerParts - 1) stagger_.push_back(f);
+        a = e + 1;
+      }
+      std::sort(stagger_.begin(), stagger_.end());
+    }
     const char* sm = std::getenv("ARENA_STAGGER_MIN_BATCH");
     stagger_min_batch_ = sm != nullptr ? std::max(1, std::atoi(sm)) : 16;
   }
@@ -140,7 +150,8 @@ Executor::~Executor() {
     if (sl.started) hipEventDestroy(sl.started);
     if (sl.done) hipEventDestroy(sl.done);
     if (sl.fork_ev) hipEventDestroy(sl.fork_ev);
-    if (sl.phase) hipEventDestroy(sl.phase);
+    for (hipEvent_t& e : sl.phase)
+      if (e) hipEventDestroy(e);
     for (int l = 0; l < kMaxLanes; ++l) {
       if (sl.lane_ev[l]) hipEventDestroy(sl.lane_ev[l]);
       if (sl.lane_stream[l]) hipStreamDestroy(sl.lane_stream[l]);
@@ -203,7 +214,7 @@ void Executor::alloc_slots() {
     ARENA_HIP_CHECK(hipMemset(sl.d_out, 0, out_bytes_total()));
     std::memset(sl.h_in, 0, in_bytes_meta());
     ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
-    ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.phase, hipEventDisableTiming));
+    for (hipEvent_t& e : sl.phase) ARENA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ARENA_HIP_CHECK(hipEventCreate(&sl.started));
     if (copy_mode_ == 3) ARENA_HIP_CHECK(hipStreamCreateWithFlags(&sl.copy_stream, hipStreamNonBlocking));
     // ARENA_SYNC=blocking: collect() sleeps on the completion interrupt instead of polling the event (HIP's
@@ -463,8 +474,9 @@ bool Executor::lanes_for(const Bucket& bk) const {
 void Executor::destroy_graphs(Bucket& bk, int s) {
   if (bk.graph[s]) hipGraphExecDestroy(bk.graph[s]);
   bk.graph[s] = nullptr;
-  if (bk.graph2[s]) hipGraphExecDestroy(bk.graph2[s]);
-  bk.graph2[s] = nullptr;
+  for (hipGraphExec_t g : bk.parts[s])
+    if (g) hipGraphExecDestroy(g);
+  bk.parts[s].clear();
   for (auto& sg : bk.segs[s])
     if (sg.g) hipGraphExecDestroy(sg.g);
   bk.segs[s].clear();
@@ -498,11 +510,15 @@ void Executor::capture(Bucket& bk, int s) {
   };
   if (!lanes_for(bk)) {
     // small buckets (light load) launch unstaggered: a wait there would only add latency
-    const size_t split =
-        bk.info.B >= stagger_min_batch_ ? (size_t)std::lround(stagger_ * (double)prog_.size()) : (size_t)0;
-    if (split > 0 && split < prog_.size()) {
-      bk.graph[s] = capture_range(0, split);
-      bk.graph2[s] = capture_range(split, prog_.size());
+    std::vector<size_t> cuts{0};
+    if (bk.info.B >= stagger_min_batch_)
+      for (double f : stagger_) {
+        const size_t k = (size_t)std::lround(f * (double)prog_.size());
+        if (k > cuts.back() && k < prog_.size()) cuts.push_back(k);
+      }
+    if (cuts.size() > 1) {
+      cuts.push_back(prog_.size());
+      for (size_t i = 0; i + 1 < cuts.size(); ++i) bk.parts[s].push_back(capture_range(cuts[i], cuts[i + 1]));
     } else {
       bk.graph[s] = capture_range(0, prog_.size());
     }
@@ -528,14 +544,17 @@ void Executor::capture(Bucket& bk, int s) {
 
 void Executor::launch_graph(Bucket& bk, int s, hipStream_t st) {
   if (bk.segs[s].empty()) {
-    if (bk.graph2[s]) {
-      // after the previously launched batch's split op (an event already passed, or re-recorded by a later
-      // launch of that slot, costs nothing); then this batch's first part, its own phase event, the rest
-      if (last_launched_ >= 0 && last_launched_ != s)
-        ARENA_HIP_CHECK(hipStreamWaitEvent(st, slots_[last_launched_].phase, 0));
-      ARENA_HIP_CHECK(hipGraphLaunch(bk.graph[s], st));
-      ARENA_HIP_CHECK(hipEventRecord(slots_[s].phase, st));
-      ARENA_HIP_CHECK(hipGraphLaunch(bk.graph2[s], st));
+    if (!bk.parts[s].empty()) {
+      // part i (all but the last) after the previously launched batch finished its part i: at most one batch in
+      // each gated part at a time, any number in the last (an event already passed, or re-recorded by a later
+      // launch of that slot, costs nothing)
+      const Slot* prev = last_launched_ >= 0 && last_launched_ != s ? &slots_[last_launched_] : nullptr;
+      const size_t np = bk.parts[s].size();
+      for (size_t i = 0; i < np; ++i) {
+        if (prev && i + 1 < np) ARENA_HIP_CHECK(hipStreamWaitEvent(st, prev->phase[i], 0));
+        ARENA_HIP_CHECK(hipGraphLaunch(bk.parts[s][i], st));
+        ARENA_HIP_CHECK(hipEventRecord(slots_[s].phase[i], st));
+      }
       last_launched_ = s;
       return;
     }

@@ -47,6 +47,7 @@ constexpr int kDtypeField = 47;  // per-op activation precision: 0 bf16, 1 exact
 constexpr int kLaneField = 46;
 constexpr int kMaxLanes = 3;
 constexpr int kMaxSlots = 6;
+constexpr int kMaxStaggerParts = 5;  // staggered launch: at most 4 split points (executor.cpp launch_graph)
 constexpr int kMaxEstBuckets = 257;  // completion-time estimates per bucket size (larger buckets share the last)
 using OpRecord = std::array<int64_t, kOpFields>;
 
@@ -203,7 +204,8 @@ class Executor : public BatchInstance {
     size_t h_cap = 0;  // bytes of h_in (meta + host-packed inputs; grows on demand)
     uint8_t* h_out = nullptr;
     hipEvent_t copied = nullptr, started = nullptr, done = nullptr;
-    hipEvent_t phase = nullptr;  // staggered launch: the batch reached the program's split op (ARENA_STAGGER)
+    // staggered launch: phase[i] = the batch finished part i of its program (ARENA_STAGGER)
+    hipEvent_t phase[kMaxStaggerParts] = {};
     hipStream_t copy_stream = nullptr;  // ARENA_COPY_MODE=3: this slot's own copy stream
     // Each slot owns an activation arena; its batch runs on one of the
     // executor's compute streams (round-robin by submission), so in-flight
@@ -228,8 +230,9 @@ class Executor : public BatchInstance {
     uint8_t* d_arena[kMaxSlots] = {};  // per slot (all aliased when concurrency is off)
     int last_slot = 0;                 // slot whose arena read_arena() inspects
     hipGraphExec_t graph[kMaxSlots] = {};
-    // staggered launch (ARENA_STAGGER): graph[s] holds ops [0, split), graph2[s] ops [split, end)
-    hipGraphExec_t graph2[kMaxSlots] = {};
+    // staggered launch (ARENA_STAGGER): the program as consecutive parts split at the stagger points, one graph
+    // each (graph[s] unused then)
+    std::vector<hipGraphExec_t> parts[kMaxSlots];
     // Lane buckets (program lanes, B <= lanes_max_batch()): the program as contiguous single-lane segments, one
     // graph each; launch_graph() runs lane segments on the slot's side streams between fork / join events.
     // (A single graph with forked branches made HIP's graph launch segfault with GPU_MAX_HW_QUEUES < 4 from the
@@ -294,10 +297,11 @@ class Executor : public BatchInstance {
   hipStream_t streams_[kMaxSlots] = {};  // compute streams (streams_[0] == compute_)
   int n_streams_ = 1;
   uint64_t seq_ = 0;                     // batches submitted
-  // Staggered launch (ARENA_STAGGER = fraction f of the program's ops, 0 = off): a batch's graph starts only once
-  // the previously launched batch passed op round(f * ops), so the batches in flight on the compute streams sit
-  // at different phases of the program instead of drifting into step (launch_graph)
-  double stagger_ = 0.0;
+  // Staggered launch (ARENA_STAGGER = "f1[,f2...]", fractions of the program's ops; 0 = off): the program runs as
+  // parts split at those ops, and a batch starts part i only once the previously launched batch has finished its
+  // part i, so the batches in flight on the compute streams sit at different phases of the program instead of
+  // drifting into step (launch_graph)
+  std::vector<double> stagger_;  // split points as fractions of the program's ops, ascending
   int stagger_min_batch_ = 16;  // ARENA_STAGGER_MIN_BATCH: buckets below it launch unstaggered
   int last_launched_ = -1;  // slot of the last staggered launch
   bool has_topk_ = false, has_det_ = false, has_raw_ = false, has_stamps_ = false;
