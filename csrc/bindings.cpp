@@ -553,6 +553,18 @@ PYBIND11_MODULE(_C, m) {
     py::gil_scoped_release nogil;
     return malloc_trim(0) != 0;
   });
+  // glibc heap totals (mallinfo2): RSS growth with flat in_use bytes is free pages the heap holds (fragmentation);
+  // growth of in_use is live allocations; growth outside both is mmap'd memory of someone other than malloc
+  m.def("malloc_info", []() {
+    const struct mallinfo2 mi = mallinfo2();
+    py::dict d;
+    d["arena"] = (uint64_t)mi.arena;        // bytes of the main and thread heaps (sbrk / heap mmaps)
+    d["mmapped"] = (uint64_t)mi.hblkhd;     // bytes in malloc's own per-chunk mmaps
+    d["in_use"] = (uint64_t)mi.uordblks;    // allocated bytes inside the heaps
+    d["free"] = (uint64_t)mi.fordblks;      // free bytes inside the heaps
+    d["releasable"] = (uint64_t)mi.keepcost;
+    return d;
+  });
   bind_jpeg(m);
   m.def("conv2d", &py_conv2d);
   m.def("set_conv_impl", &set_conv_impl);

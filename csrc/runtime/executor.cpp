@@ -1390,6 +1390,28 @@ double Executor::remaining_us(int s) {
          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - sl.t_submit).count();
 }
 
+// The batch's input DMA ran on the shared copy stream and only device streams waited for it (hipStreamWaitEvent).
+// Left at that, HIP keeps ~2 KB of host memory per batch without bound (profiles/r6_serving/leak: 65 B/request
+// of live malloc'd bytes; the same server with the copy on the batch's own stream stays flat).  A host-side look
+// at the copy's completion lets it release them.  ARENA_COPY_RELEASE: 1 (default) hipEventQuery of the slot's
+// copy event at collect, 2 hipEventSynchronize of it (complete by then), 3 hipStreamSynchronize(copy stream)
+// every 64 batches, 0 off.
+void Executor::release_copy(Slot& sl) {
+  static const int mode = [] {
+    const char* e = std::getenv("ARENA_COPY_RELEASE");
+    return e != nullptr ? std::atoi(e) : 1;
+  }();
+  if (copy_mode_ == 2 || mode == 0) return;
+  if (mode == 1) {
+    (void)hipEventQuery(sl.copied);
+    (void)hipGetLastError();
+  } else if (mode == 2) {
+    ARENA_HIP_CHECK(hipEventSynchronize(sl.copied));
+  } else if (mode == 3 && ++copy_release_n_ % 64 == 0) {
+    ARENA_HIP_CHECK(hipStreamSynchronize(copy_mode_ == 3 ? sl.copy_stream : copy_));
+  }
+}
+
 BatchResult Executor::collect(int s) {
   if (s < 0 || s >= n_slots_) throw std::runtime_error("collect: bad slot");
   Slot& sl = slots_[s];
@@ -1399,6 +1421,7 @@ BatchResult Executor::collect(int s) {
     trace::Range tw("arena.collect.wait");
     wait_done(sl);
   }
+  release_copy(sl);
   trace::Range tu("arena.collect.unpack");
   BatchResult res;
   res.n_images = sl.n_images;

@@ -252,6 +252,8 @@ class Executor : public BatchInstance {
   void capture(Bucket& bk, int slot);
   void wait_done(Slot& sl);
   void note_done(Slot& sl);
+  void release_copy(Slot& sl);
+  uint64_t copy_release_n_ = 0;
   void launch_graph(Bucket& bk, int slot, hipStream_t st);
   void destroy_graphs(Bucket& bk, int slot);
   bool lanes_for(const Bucket& bk) const;

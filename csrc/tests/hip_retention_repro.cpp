@@ -7,6 +7,10 @@
 //         pack : the uploads memcpy'd into one pinned staging buffer per slot, one copy per batch on the side
 //                stream (the round-5 fix)
 //         same : one copy per upload, issued on the batch's own compute stream (no side stream, no event)
+//         pack_same     : pack, the one copy on the batch's compute stream (no side stream, no event)
+//         pack_hostwait : pack on the side stream, the host waits for the copy (no cross-stream event wait)
+//         pack_sync     : pack, and the side stream synchronized by the host every 64 batches
+//         pack_rec      : pack, a fresh event per batch (created and destroyed) instead of the slot's
 //
 // Prints RSS (/proc/self/statm) every 500 batches and the growth per upload after a 500-batch warm-up.
 #include <hip/hip_runtime.h>
@@ -59,18 +63,30 @@ int main(int argc, char** argv) {
     const int s = b % kSlots;
     hipStream_t cs = comp[b % kStreams];
     if (b >= kSlots) CK(hipEventSynchronize(done[s]));  // the slot's previous batch completed (collect)
-    if (mode == "pack") {
+    const bool pack = mode.rfind("pack", 0) == 0;
+    const bool on_compute = mode == "same" || mode == "pack_same";
+    if (pack) {
       for (int i = 0; i < per; ++i) std::memcpy(stage[s] + i * bytes, up[(b * per + i) % kUploads], bytes);
-      CK(hipMemcpyAsync(dev[s], stage[s], bytes * per, hipMemcpyHostToDevice, copy));
+      CK(hipMemcpyAsync(dev[s], stage[s], bytes * per, hipMemcpyHostToDevice, on_compute ? cs : copy));
     } else {
       for (int i = 0; i < per; ++i)
         CK(hipMemcpyAsync(dev[s] + i * bytes, up[(b * per + i) % kUploads], bytes, hipMemcpyHostToDevice,
                           mode == "same" ? cs : copy));
     }
-    if (mode != "same") {
+    if (mode == "pack_hostwait") {
+      CK(hipEventRecord(copied[s], copy));
+      CK(hipEventSynchronize(copied[s]));
+    } else if (mode == "pack_rec") {
+      hipEvent_t ev;
+      CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      CK(hipEventRecord(ev, copy));
+      CK(hipStreamWaitEvent(cs, ev, 0));
+      CK(hipEventDestroy(ev));
+    } else if (!on_compute) {
       CK(hipEventRecord(copied[s], copy));
       CK(hipStreamWaitEvent(cs, copied[s], 0));
     }
+    if (mode == "pack_sync" && b % 64 == 63) CK(hipStreamSynchronize(copy));
     consume<<<(unsigned)((bytes * per / 4096 + 255) / 256), 256, 0, cs>>>(dev[s], bytes * per, hits);
     CK(hipEventRecord(done[s], cs));
     if (b == 500) rss0 = rss_mb();

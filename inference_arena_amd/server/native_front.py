@@ -134,11 +134,11 @@ class NativeFrontEnd:
         self.fe.set_healthy(bool(ok))
 
     def _refresh(self) -> None:
-        # ARENA_MALLOC_TRIM_S (default 10, 0 = off): return free heap pages to the kernel periodically: buffers
-        # allocated on the decode / I/O threads and freed on the batcher thread leave glibc's per-thread arenas
-        # holding pages (tools/leak_probe_gpu.py --trim: 115 MB back).  The slower per-request growth of the GPU
-        # serving path is not this (docs/round5_status.md, "Memory growth").
-        trim_s = float(os.environ.get("ARENA_MALLOC_TRIM_S", "10"))
+        # ARENA_MALLOC_TRIM_S (default 0 = off): return free heap pages to the kernel every that many seconds.  Round 5
+        # needed it (115 MB back, tools/leak_probe_gpu.py --trim): request bodies were allocated on the I/O threads
+        # and freed on the decode threads.  They now go back to the front end's body pool (csrc/runtime/
+        # string_pool.h) instead of to the allocator, so no per-request buffer crosses threads.
+        trim_s = float(os.environ.get("ARENA_MALLOC_TRIM_S", "0"))
         last_trim = time.monotonic()
         from ..ops import native
 

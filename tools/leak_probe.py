@@ -29,6 +29,38 @@ def rss_mb(pid: int | None = None) -> float:
     return 0.0
 
 
+def make_reqs() -> list[bytes]:
+    """8 small multipart JPEG uploads (noise, 120-176 x 160, q90)."""
+    import numpy as np
+    from PIL import Image
+
+    rng = np.random.default_rng(0)
+    reqs = []
+    for i in range(8):
+        b = io.BytesIO()
+        Image.fromarray((rng.random((120 + 8 * i, 160, 3)) * 255).astype(np.uint8)).save(b, "JPEG", quality=90)
+        data = b.getvalue()
+        bnd = "leakprobe"
+        body = (f"--{bnd}\r\nContent-Disposition: form-data; name=\"file\"; filename=\"x.jpg\"\r\n"
+                f"Content-Type: image/jpeg\r\n\r\n").encode() + data + f"\r\n--{bnd}--\r\n".encode()
+        reqs.append((f"POST /predict HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: multipart/form-data; "
+                     f"boundary={bnd}\r\nContent-Length: {len(body)}\r\n\r\n").encode() + body)
+    return reqs
+
+
+def load_only(port: int, n: int, users: int) -> int:
+    """--load-only: the closed-loop load of one round from a process of its own (--external-load), so the probed
+    process's RSS is the server's alone"""
+    from inference_arena_amd.ops import native
+
+    lg = native().HttpLoadGen({"host": "127.0.0.1", "port": port, "users": users, "threads": 2}, make_reqs())
+    lg.start()
+    ok = lg.wait_completed(n, 600)
+    lg.stop(30)
+    print(lg.completed(), flush=True)
+    return 0 if ok else 1
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--rounds", type=int, default=8)
@@ -41,7 +73,12 @@ def main(argv=None) -> int:
                     "the EchoInstance (the device-JPEG front-end branch, reconstructed on the host by the instance)")
     ap.add_argument("--gpu", action="store_true", help="the fused fp32 GPU pipeline instead of the host-only EchoInstance "
                     "(the monolithic server's exact path: split decoder, GPU reconstruction, executor)")
+    ap.add_argument("--external-load", action="store_true", help="run each round's load generator in a child "
+                    "process (the probed RSS is then the server's alone)")
+    ap.add_argument("--load-only", nargs=3, type=int, metavar=("PORT", "N", "USERS"), help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
+    if a.load_only:
+        return load_only(*a.load_only)
 
     import numpy as np
     from PIL import Image
@@ -63,33 +100,34 @@ def main(argv=None) -> int:
     batcher = C.DynamicBatcher([inst], {"max_batch": 32, "max_queue_delay_us": 300, "idle_queue_delay_us": 100})
     fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=2, decode_procs=1,
                         slots=64, decode_threads=a.decode_threads, jpeg_device=(a.gpu and not a.jpeg_host) or a.jpeg_device)
-    rng = np.random.default_rng(0)
-    reqs = []
-    for i in range(8):
-        b = io.BytesIO()
-        Image.fromarray((rng.random((120 + 8 * i, 160, 3)) * 255).astype(np.uint8)).save(b, "JPEG", quality=90)
-        data = b.getvalue()
-        bnd = "leakprobe"
-        body = (f"--{bnd}\r\nContent-Disposition: form-data; name=\"file\"; filename=\"x.jpg\"\r\n"
-                f"Content-Type: image/jpeg\r\n\r\n").encode() + data + f"\r\n--{bnd}--\r\n".encode()
-        reqs.append((f"POST /predict HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: multipart/form-data; "
-                     f"boundary={bnd}\r\nContent-Length: {len(body)}\r\n\r\n").encode() + body)
+    reqs = make_reqs()
     base = None
     done = 0
     try:
         for r in range(a.rounds):
-            lg = C.HttpLoadGen({"host": "127.0.0.1", "port": fe.port, "users": a.users, "threads": 2}, reqs)
             t0 = time.perf_counter()
-            lg.start()
-            ok = lg.wait_completed(a.per_round, 600)
-            lg.stop(30)
-            n = lg.completed()
-            del lg  # its per-request records are freed with it
+            if a.external_load:
+                import subprocess
+
+                pr = subprocess.run([sys.executable, __file__, "--load-only", str(fe.port), str(a.per_round),
+                                     str(a.users)], capture_output=True, text=True, timeout=700)
+                ok = pr.returncode == 0
+                n = int(pr.stdout.split()[-1]) if pr.stdout.split() else 0
+            else:
+                lg = C.HttpLoadGen({"host": "127.0.0.1", "port": fe.port, "users": a.users, "threads": 2}, reqs)
+                lg.start()
+                ok = lg.wait_completed(a.per_round, 600)
+                lg.stop(30)
+                n = lg.completed()
+                del lg  # its per-request records are freed with it
             done += n
             m = rss_mb()
             base = m if base is None else base
+            mi = C.malloc_info()
             print(f"round {r}: {n} requests ({n / (time.perf_counter() - t0):.0f}/s), rss {m:.1f} MB, "
-                  f"growth since round 0 {(m - base) * 1024 * 1024 / max(1, done - a.per_round):.0f} B/request"
+                  f"growth since round 0 {(m - base) * 1024 * 1024 / max(1, done - a.per_round):.0f} B/request; "
+                  f"malloc: in use {mi['in_use'] / 2**20:.1f} MB, free {mi['free'] / 2**20:.1f} MB, "
+                  f"chunk mmaps {mi['mmapped'] / 2**20:.1f} MB"
                   + ("" if ok else " (timeout)"), flush=True)
     finally:
         fe.close()
