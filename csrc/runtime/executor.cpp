@@ -1391,15 +1391,16 @@ double Executor::remaining_us(int s) {
 }
 
 // The batch's input DMA ran on the shared copy stream and only device streams waited for it (hipStreamWaitEvent).
-// Left at that, HIP keeps ~2 KB of host memory per batch without bound (profiles/r6_serving/leak: 65 B/request
-// of live malloc'd bytes; the same server with the copy on the batch's own stream stays flat).  A host-side look
-// at the copy's completion lets it release them.  ARENA_COPY_RELEASE: 1 (default) hipEventQuery of the slot's
-// copy event at collect, 2 hipEventSynchronize of it (complete by then), 3 hipStreamSynchronize(copy stream)
-// every 64 batches, 0 off.
+// Left at that, HIP keeps ~2 KB of live host allocations per batch without bound (profiles/r6_serving/leak:
+// +65 B/request of malloc'd bytes in use).  A host synchronisation of the copy stream releases them; a query or a
+// synchronize of the copy's event does not.  ARENA_COPY_RELEASE: 3 (default) hipStreamSynchronize(copy stream)
+// every 64 batches at collect (waits at most for the H2D copies queued behind this batch's: ~0.2 ms per 64
+// batches), 1 hipEventQuery / 2 hipEventSynchronize of the slot's copy event (both measured: still leaking),
+// 0 off.
 void Executor::release_copy(Slot& sl) {
   static const int mode = [] {
     const char* e = std::getenv("ARENA_COPY_RELEASE");
-    return e != nullptr ? std::atoi(e) : 1;
+    return e != nullptr ? std::atoi(e) : 3;
   }();
   if (copy_mode_ == 2 || mode == 0) return;
   if (mode == 1) {

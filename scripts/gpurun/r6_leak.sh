@@ -18,7 +18,7 @@ for cfg in "$@"; do
   i=$((i + 1))
   envs=$(echo "$cfg" | tr '+' ' ')
   [ "$cfg" = "-" ] && envs="ARENA_X=0"
-  env $envs $S 400 $O/srv_$i.log python -u tools/leak_probe.py --gpu --rounds ${ROUNDS:-6} --per-round ${PER:-30000} --users 64 ${LP_ARGS:-} || exit 1
+  env $envs $S ${STEP_S:-400} $O/srv_$i.log python -u tools/leak_probe.py --gpu --rounds ${ROUNDS:-6} --per-round ${PER:-30000} --users 64 ${LP_ARGS:-} || exit 1
   echo "[$cfg]" | tee -a $O/summary.txt
   grep "^round" $O/srv_$i.log | tee -a $O/summary.txt
 done

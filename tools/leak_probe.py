@@ -29,17 +29,28 @@ def rss_mb(pid: int | None = None) -> float:
     return 0.0
 
 
-def make_reqs() -> list[bytes]:
-    """8 small multipart JPEG uploads (noise, 120-176 x 160, q90)."""
+def make_reqs(workload: bool = False) -> list[bytes]:
+    """8 small multipart JPEG uploads (noise, 120-176 x 160, q90); ``workload``: the bench's 100 curated COCO-shaped
+    frames as JPEG q90 (bench.py's uploads)"""
     import numpy as np
     from PIL import Image
 
-    rng = np.random.default_rng(0)
+    if workload:
+        from inference_arena_amd.data.curator import DatasetManifest, load_manifest_images
+        from inference_arena_amd.data.synthetic import encode_jpeg
+
+        root = Path(__file__).resolve().parents[1]
+        man = DatasetManifest.load(root / "data" / "synthetic_set" / "manifest_w0_n100.json")
+        jpegs = [encode_jpeg(im, 90) for im in load_manifest_images(man)]
+    else:
+        rng = np.random.default_rng(0)
+        jpegs = []
+        for i in range(8):
+            b = io.BytesIO()
+            Image.fromarray((rng.random((120 + 8 * i, 160, 3)) * 255).astype(np.uint8)).save(b, "JPEG", quality=90)
+            jpegs.append(b.getvalue())
     reqs = []
-    for i in range(8):
-        b = io.BytesIO()
-        Image.fromarray((rng.random((120 + 8 * i, 160, 3)) * 255).astype(np.uint8)).save(b, "JPEG", quality=90)
-        data = b.getvalue()
+    for data in jpegs:
         bnd = "leakprobe"
         body = (f"--{bnd}\r\nContent-Disposition: form-data; name=\"file\"; filename=\"x.jpg\"\r\n"
                 f"Content-Type: image/jpeg\r\n\r\n").encode() + data + f"\r\n--{bnd}--\r\n".encode()
@@ -48,12 +59,13 @@ def make_reqs() -> list[bytes]:
     return reqs
 
 
-def load_only(port: int, n: int, users: int) -> int:
+def load_only(port: int, n: int, users: int, workload: int = 0) -> int:
     """--load-only: the closed-loop load of one round from a process of its own (--external-load), so the probed
     process's RSS is the server's alone"""
     from inference_arena_amd.ops import native
 
-    lg = native().HttpLoadGen({"host": "127.0.0.1", "port": port, "users": users, "threads": 2}, make_reqs())
+    lg = native().HttpLoadGen({"host": "127.0.0.1", "port": port, "users": users, "threads": 2},
+                              make_reqs(bool(workload)))
     lg.start()
     ok = lg.wait_completed(n, 600)
     lg.stop(30)
@@ -75,7 +87,9 @@ def main(argv=None) -> int:
                     "(the monolithic server's exact path: split decoder, GPU reconstruction, executor)")
     ap.add_argument("--external-load", action="store_true", help="run each round's load generator in a child "
                     "process (the probed RSS is then the server's alone)")
-    ap.add_argument("--load-only", nargs=3, type=int, metavar=("PORT", "N", "USERS"), help=argparse.SUPPRESS)
+    ap.add_argument("--workload", action="store_true", help="upload the bench's curated frames (JPEG q90, "
+                    "COCO-shaped) instead of 8 small noise JPEGs")
+    ap.add_argument("--load-only", nargs=4, type=int, metavar=("PORT", "N", "USERS", "WORKLOAD"), help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     if a.load_only:
         return load_only(*a.load_only)
@@ -100,7 +114,7 @@ def main(argv=None) -> int:
     batcher = C.DynamicBatcher([inst], {"max_batch": 32, "max_queue_delay_us": 300, "idle_queue_delay_us": 100})
     fe = NativeFrontEnd(batcher, load_labels(None), port=0, host="127.0.0.1", io_threads=2, decode_procs=1,
                         slots=64, decode_threads=a.decode_threads, jpeg_device=(a.gpu and not a.jpeg_host) or a.jpeg_device)
-    reqs = make_reqs()
+    reqs = make_reqs(a.workload)
     base = None
     done = 0
     try:
@@ -110,7 +124,7 @@ def main(argv=None) -> int:
                 import subprocess
 
                 pr = subprocess.run([sys.executable, __file__, "--load-only", str(fe.port), str(a.per_round),
-                                     str(a.users)], capture_output=True, text=True, timeout=700)
+                                     str(a.users), str(int(a.workload))], capture_output=True, text=True, timeout=700)
                 ok = pr.returncode == 0
                 n = int(pr.stdout.split()[-1]) if pr.stdout.split() else 0
             else:
