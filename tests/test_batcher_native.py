@@ -17,7 +17,7 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SRCS = [ROOT / "csrc" / "tests" / "batcher_stress.cpp", ROOT / "csrc" / "runtime" / "batcher.cpp",
-        ROOT / "csrc" / "runtime" / "trace.cpp"]
+        ROOT / "csrc" / "runtime" / "trace.cpp", ROOT / "csrc" / "runtime" / "jpeg_decode.cpp"]
 
 
 def _build(sanitizer: str) -> Path:
