@@ -91,6 +91,8 @@ void py_conv2d(const py::dict& d) {
   p.pw_kpad = get<int>(d, "pw_kpad", 0);
   p.pw_act = get<int>(d, "pw_act", 0);
   p.w3 = ptr<const void*>(d, "w3");
+  p.sk_ws = ptr<float*>(d, "sk_ws");
+  p.sk_ws_bytes = get<int64_t>(d, "sk_ws_bytes", 0);
   prepare_kernels();  // dynamic-LDS limits of the x3 halo / fused kernels (before any launch)
   if (get<int>(d, "f32", 0))
     conv2d_f32(p, stream_of(d));

@@ -1604,6 +1604,11 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
         throw std::runtime_error("conv2d_f32: not an x3g-eligible conv (needs pre-split weights)");
       return;
     }
+    if (p.impl >= kF32X3GSK && p.impl < kF32X3GSK + kF32X3GSKVariants) {
+      if (!conv_x3g_sk(p, s, p.impl - kF32X3GSK))
+        throw std::runtime_error("conv2d_f32: not a split-K x3g-eligible conv (pre-split weights, workspace)");
+      return;
+    }
     if (p.impl >= kF32X3HG && p.impl < kF32X3HG + kF32X3HGVariants) {
       if (!conv_x3hg(p, s, p.impl - kF32X3HG))
         throw std::runtime_error("conv2d_f32: not an x3hg-eligible conv (3x3 s1 with pre-split weights)");

@@ -88,7 +88,7 @@ __device__ __forceinline__ f32x16 xg_mfma_x3(const bf16x8& ah, const bf16x8& am,
 // IL: shape the schedule of each K step (sched_group_barrier) so the next chunk's split arithmetic and LDS stores
 // issue between this chunk's MFMAs instead of after them (a wave's vector issue is free for 24 of each
 // 32x32x16 MFMA's 32 cycles)
-template <int WM, int WN, int TM, int TN, bool IL = false>
+template <int WM, int WN, int TM, int TN, bool IL = false, bool SK = false>
 __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams p) {
   constexpr int NT = WM * WN * 64;  // 4 or 8 waves
   static_assert(WM * WN == 4 || WM * WN == 8, "four or eight waves");
@@ -105,7 +105,12 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams
   const int HWo = p.Ho * p.Wo;
   const int M = live_batch(p.B, p.bdev) * HWo;
   const int ntn = (p.Cout_pad + BN - 1) / BN;
-  const int bx = xg_xcd_remap(blockIdx.x, gridDim.x);
+  // split-K (SK): the grid is splits x tiles, split-major; each split walks its own range of K chunks and stores
+  // its raw partial tile into the workspace (x3g_sk_reduce sums them in split order and runs the epilogue)
+  const int nsplit = SK ? p.sk_splits : 1;
+  const int ntiles = (int)gridDim.x / nsplit;
+  const int split = SK ? (int)blockIdx.x / ntiles : 0;
+  const int bx = xg_xcd_remap((int)blockIdx.x - split * ntiles, ntiles);
   const int mt = bx / ntn, nt = bx - mt * ntn;
   const int m0 = mt * BM, n0 = nt * BN;
   if (m0 >= M) return;
@@ -116,9 +121,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.x), (short)0, (int)((size_t)p.B * p.H * p.W * p.xs * 4), 0x00020000);
   const int Cin32 = (p.Cin + 31) & ~31;          // each tap's channels padded to whole 32-deep chunks
-  const int nk = p.KH * p.KW * (Cin32 >> 5);
+  const int nk_all = p.KH * p.KW * (Cin32 >> 5);
+  const int kc_begin = SK ? split * nk_all / nsplit : 0;
+  const int nk = SK ? (split + 1) * nk_all / nsplit - kc_begin : nk_all;  // chunks of this workgroup
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.w3), (short)0, (int)((size_t)nk * p.Cout_pad * 192), 0x00020000);
+      const_cast<void*>(p.w3), (short)0, (int)((size_t)nk_all * p.Cout_pad * 192), 0x00020000);
   const int Cin = p.Cin, H = p.H, W = p.W, S = p.stride;
   constexpr int kOob = 0x7fffffff & ~15;  // past every buffer: the load returns zeros
 
@@ -155,7 +162,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams
   // (ky, kx, c0) of the next chunk to load: chunks are loaded strictly in order, so a running position
   // replaces a division per chunk (the weight layout pads each tap to Cin32: a chunk never straddles two taps)
   int ld_ky = 0, ld_kx = 0, ld_c0 = 0;
-  auto load = [&](int kc, f32x4 (&ra)[AI][2], u32x4 (&rw)[WI]) {
+  if (SK) {  // the split's first chunk
+    const int cpt = Cin32 >> 5, tap = kc_begin / cpt;
+    ld_c0 = (kc_begin - tap * cpt) * 32;
+    ld_ky = tap / p.KW;
+    ld_kx = tap - ld_ky * p.KW;
+  }
+  auto load = [&](int kc_local, f32x4 (&ra)[AI][2], u32x4 (&rw)[WI]) {
+    const int kc = kc_begin + kc_local;  // weight chunk index
     const int ky = ld_ky, kx = ld_kx, c0 = ld_c0;
     ld_c0 += 32;  // advanced with selects, not branches: the K step stays one scheduling region
     const bool wrap = ld_c0 >= Cin32;
@@ -267,8 +281,28 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams
   }
   if (kc < nk) compute(0);  // odd chunk count: the last chunk is in buffer 0
 
-  // ---- epilogue: bias, activation, residual, NHWC fp32 (+ 2x nearest-upsampled copy)
   const int kh4 = 4 * (lane >> 5);
+  if constexpr (SK) {  // raw partial sums: ws[split][m][Cout_pad]
+    const int Mcap = p.B * HWo;
+    float* ws = p.sk_ws + (size_t)split * Mcap * p.Cout_pad;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int m = m0 + (wm * TM + tm) * 32 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = n0 + (wn * TN + tn) * 32 + 8 * g + kh4;
+          if (c >= p.Cout) continue;
+          *(float4*)(ws + (size_t)m * p.Cout_pad + c) =
+              make_float4(acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2], acc[tm][tn][4 * g + 3]);
+        }
+    }
+    return;
+  }
+
+  // ---- epilogue: bias, activation, residual, NHWC fp32 (+ 2x nearest-upsampled copy)
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     const int m = m0 + (wm * TM + tm) * 32 + fr;
@@ -312,6 +346,42 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_x3g_kernel(const ConvParams
 }
 
 
+// Split-K second pass: out = act(sum_s ws[s] + bias) (+ residual), the x3g epilogue per 4 channels of a pixel.
+// The partials are summed in split order, so the result does not depend on which split finished first.
+__global__ __launch_bounds__(256) void x3g_sk_reduce_kernel(const ConvParams p) {
+  const int HWo = p.Ho * p.Wo;
+  const int M = live_batch(p.B, p.bdev) * HWo, Mcap = p.B * HWo;
+  const int c4n = p.Cout >> 2;
+  const int i = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  if (i >= M * c4n) return;
+  const int m = i / c4n, c = 4 * (i - m * c4n);
+  float4 a = *(const float4*)(p.sk_ws + (size_t)m * p.Cout_pad + c);
+  for (int k = 1; k < p.sk_splits; ++k) {
+    const float4 v = *(const float4*)(p.sk_ws + ((size_t)k * Mcap + m) * p.Cout_pad + c);
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  const float4 bias = *(const float4*)(p.bias + c);
+  float v[4] = {a.x + bias.x, a.y + bias.y, a.z + bias.z, a.w + bias.w};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], p.act);
+  if (p.res != nullptr) {
+    const float4 rv = *(const float4*)((const float*)p.res + (size_t)m * p.rs + c);
+    v[0] += rv.x; v[1] += rv.y; v[2] += rv.z; v[3] += rv.w;
+  }
+  const float4 o = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)((float*)p.y + (size_t)m * p.ys + c) = o;
+  if (p.y2 != nullptr) {
+    const int b = m / HWo, r = m - b * HWo, oy = r / p.Wo, ox = r - oy * p.Wo;
+    const int W2 = 2 * p.Wo;
+    float* y2 = (float*)p.y2;
+    const size_t base = ((size_t)(b * 2 * p.Ho + 2 * oy) * W2 + 2 * ox);
+    *(float4*)(y2 + base * p.y2s + c) = o;
+    *(float4*)(y2 + (base + 1) * p.y2s + c) = o;
+    *(float4*)(y2 + (base + W2) * p.y2s + c) = o;
+    *(float4*)(y2 + (base + W2 + 1) * p.y2s + c) = o;
+  }
+}
+
 namespace {
 
 template <int WM, int WN, int TM, int TN, bool IL>
@@ -322,6 +392,37 @@ void xg_launch(const ConvParams& p, hipStream_t s) {
   hipLaunchKernelGGL((conv_x3g_kernel<WM, WN, TM, TN, IL>), dim3((unsigned)tiles), dim3(WM * WN * 64), xg_lds_bytes(BM, BN), s,
                      p);
 }
+
+// split-K: tile variant (XG_VARIANTS id) x splits; a workspace of splits x B x Ho x Wo x Cout_pad fp32 (ConvParams
+// sk_ws, per executor slot and lane) holds the partial tiles
+template <int WM, int WN, int TM, int TN>
+bool xg_launch_sk(const ConvParams& p, hipStream_t s, int splits) {
+  constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  const long M = (long)p.B * p.Ho * p.Wo;
+  const int nk = p.KH * p.KW * ((p.Cin + 31) / 32);
+  splits = splits < nk ? splits : nk;  // at most one K chunk per split
+  if (p.sk_ws == nullptr || splits < 2 || (long)splits * M * p.Cout_pad * 4 > p.sk_ws_bytes || p.Cout_pad % 4)
+    return false;
+  const long tiles = ((M + BM - 1) / BM) * ((p.Cout_pad + BN - 1) / BN);
+  ConvParams q = p;
+  q.sk_splits = splits;
+  hipLaunchKernelGGL((conv_x3g_kernel<WM, WN, TM, TN, false, true>), dim3((unsigned)(tiles * splits)),
+                     dim3(WM * WN * 64), xg_lds_bytes(BM, BN), s, q);
+  const long items = M * (p.Cout / 4);
+  hipLaunchKernelGGL(x3g_sk_reduce_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, q);
+  return true;
+}
+
+#define XG_SK_VARIANTS(X) \
+  X(0, 2, 2, 1, 1, 2)  /* 64 px x 64 ch */ \
+  X(1, 2, 2, 1, 1, 4)  \
+  X(2, 2, 2, 1, 1, 8)  \
+  X(3, 4, 1, 1, 1, 2)  /* 128 px x 32 ch */ \
+  X(4, 4, 1, 1, 1, 4)  \
+  X(5, 4, 1, 1, 1, 8)  \
+  X(6, 2, 2, 1, 2, 2)  /* 64 px x 128 ch */ \
+  X(7, 2, 2, 1, 2, 4)  \
+  X(8, 2, 2, 1, 2, 8)
 
 #define XG_VARIANTS(X) \
   X(0, 2, 2, 2, 1)     /* 128 px x  64 ch */ \
@@ -359,6 +460,17 @@ bool conv_x3g(const ConvParams& p, hipStream_t s, int v) {
   }
 }
 
+bool conv_x3g_sk(const ConvParams& p, hipStream_t s, int v) {
+  if (!x3g_supported(p) || p.Cout % 4) return false;
+  switch (v) {
+#define XG_SK_CASE(V, WM, WN, TM, TN, S) \
+  case V: return xg_launch_sk<WM, WN, TM, TN>(p, s, S);
+    XG_SK_VARIANTS(XG_SK_CASE)
+#undef XG_SK_CASE
+    default: return false;
+  }
+}
+
 void x3g_prepare() {
 #define XG_ATTR(V, WM, WN, TM, TN)                                                                       \
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)conv_x3g_kernel<WM, WN, TM, TN, false>,                \
@@ -369,6 +481,12 @@ void x3g_prepare() {
                                       xg_lds_bytes(WM * TM * 32, WN * TN * 32)));
   XG_VARIANTS(XG_ATTR)
 #undef XG_ATTR
+#define XG_SK_ATTR(V, WM, WN, TM, TN, S)                                                                  \
+  ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)conv_x3g_kernel<WM, WN, TM, TN, false, true>,          \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,                         \
+                                      xg_lds_bytes(WM * TM * 32, WN * TN * 32)));
+  XG_SK_VARIANTS(XG_SK_ATTR)
+#undef XG_SK_ATTR
 }
 
 }  // namespace arena

@@ -55,6 +55,11 @@ struct ConvParams {
   // fp32 programs: the weights pre-split into bf16 planes, [ceil(Kpad/32)][Cout_pad][h 32 | m 32 | l 32]
   // (engine/planner.py pack_conv_weight_x3), read by the x3g kernels (gemm_x3.hip); nullptr when absent
   const void* w3;
+  // split-K x3g (kF32X3GSK): fp32 workspace for the partial tiles, splits x B x Ho x Wo x Cout_pad (executor: one
+  // per slot and lane); sk_splits is set by the launcher
+  float* sk_ws;
+  int64_t sk_ws_bytes;
+  int sk_splits;
 };
 void conv2d(const ConvParams& p, hipStream_t s);
 void conv_igemm(const ConvParams& p, hipStream_t s);  // LDS-pipelined implicit GEMM (impl 3)
@@ -92,6 +97,11 @@ constexpr int kF32X3GVariants = 20;  // v >= 10: v - 10 with the interleaved sch
 void x3_halo_prepare();
 bool x3g_supported(const ConvParams& p);
 bool conv_x3g(const ConvParams& p, hipStream_t s, int v);  // false if the conv or variant is not supported
+// split-K x3g for small grids (bucket-1 latency): variant v = tile x splits (gemm_x3.hip XG_SK_VARIANTS); false when
+// the workspace is missing or too small
+constexpr int kF32X3GSK = 171;
+constexpr int kF32X3GSKVariants = 9;
+bool conv_x3g_sk(const ConvParams& p, hipStream_t s, int v);
 void x3g_prepare();
 // x3hg: 3x3 stride-1 halo tiles on 32x32x16 MFMAs over the same pre-split weights (halo_x3g.hip), variant v
 constexpr int kF32X3HG = 131;

@@ -135,6 +135,7 @@ Executor::~Executor() {
     Slot& sl = slots_[s];
     if (sl.d_in) hipFree(sl.d_in);
     if (sl.d_out) hipFree(sl.d_out);
+    if (sl.sk_ws) hipFree(sl.sk_ws);
     if (sl.h_in) hipHostFree(sl.h_in);
     if (sl.h_out) hipHostFree(sl.h_out);
   }
@@ -203,6 +204,8 @@ void Executor::alloc_slots() {
     // run up to 3 bytes past the last image of a full staging pool
     ARENA_HIP_CHECK(hipMalloc(&sl.d_in, in_bytes_total() + 256));
     ARENA_HIP_CHECK(hipMalloc(&sl.d_out, out_bytes_total()));
+    // split-K conv workspace (kF32X3GSK), one region per program lane: lanes run concurrently within a slot
+    ARENA_HIP_CHECK(hipMalloc(&sl.sk_ws, (size_t)sk_lane_bytes() * (kMaxLanes + 1)));
     // pinned host staging: the meta block plus the host-packed inputs of one full batch at the nominal frame size.
     // Split-decoded JPEGs need only their coefficients staged here (about 2/3 of an RGB frame at 4:2:0), so
     // pool_factor's extra device room needs no host twin; a batch that needs more grows it on demand
@@ -346,7 +349,8 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
                                 (v >= kF32X3HG && v < kF32X3HG + kF32X3HGVariants) ||
                                 (v >= kF32X3HGPw && v < kF32X3HGPw + kF32X3HGPwVariants) ||
                                 (v >= kF32X3HR && v < kF32X3HR + kF32X3HRVariants) ||
-                                (v >= kF32X3HRPw && v < kF32X3HRPw + kF32X3HRPwVariants)
+                                (v >= kF32X3HRPw && v < kF32X3HRPw + kF32X3HRPwVariants) ||
+                                (v >= kF32X3GSK && v < kF32X3GSK + kF32X3GSKVariants)
                           : v >= 0 && v <= 3;
       if (!ok || (v != 0 && prog_[i][0] != OP_CONV)) throw std::runtime_error("add_bucket: bad tuning entry");
       bk.impl[i] = (int16_t)v;
@@ -405,7 +409,11 @@ void Executor::autotune(Bucket& bk) {
                                        kF32X3HR + 0, kF32X3HR + 1, kF32X3HR + 2, kF32X3HR + 3, kF32X3HR + 4,
                                        kF32X3HR + 5, kF32X3HR + 6, kF32X3HR + 7, kF32X3HR + 8, kF32X3HR + 9,
                                        kF32X3HRPw + 0, kF32X3HRPw + 1, kF32X3HRPw + 2, kF32X3HRPw + 3,
-                                       kF32X3HRPw + 4, kF32X3HRPw + 5};
+                                       kF32X3HRPw + 4, kF32X3HRPw + 5,
+                                       // split-K x3g (small grids: bucket 1 / 2); skipped where the workspace
+                                       // is too small
+                                       kF32X3GSK + 0, kF32X3GSK + 1, kF32X3GSK + 2, kF32X3GSK + 3, kF32X3GSK + 4,
+                                       kF32X3GSK + 5, kF32X3GSK + 6, kF32X3GSK + 7, kF32X3GSK + 8};
   static const int kBf16Candidates[] = {1, 2, 3};
   for (size_t i = 0; i < prog_.size(); ++i) {
     if (prog_[i][0] != OP_CONV) continue;
@@ -469,6 +477,16 @@ bool Executor::lanes_for(const Bucket& bk) const {
   for (const OpRecord& r : prog_)
     if (r[kLaneField] >= 1 && r[kLaneField] <= kMaxLanes) return true;
   return false;
+}
+
+// bytes of one lane's split-K workspace (ARENA_SPLITK_WS_MB, default 16): the largest bucket-1 split (the 7x7x960
+// -> 320 classifier conv over 16 crops, 8 splits) needs 8 MB
+int64_t Executor::sk_lane_bytes() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("ARENA_SPLITK_WS_MB");
+    return (int64_t)std::max(1, e != nullptr ? std::atoi(e) : 16) << 20;
+  }();
+  return v;
 }
 
 void Executor::destroy_graphs(Bucket& bk, int s) {
@@ -664,6 +682,12 @@ void Executor::enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Sl
         p.B = batch(r[30]);
         p.bdev = bdev(r[30]);
         if (r[41] != 0) p.w3 = W + r[40];  // fp32: pre-split bf16 weight planes for the x3g kernels
+        {
+          const int64_t ln = r[kLaneField];
+          const int li = ln >= 1 && ln <= kMaxLanes ? (int)ln : 0;
+          p.sk_ws = (float*)((uint8_t*)sl.sk_ws + (size_t)li * sk_lane_bytes());
+          p.sk_ws_bytes = sk_lane_bytes();
+        }
         if (r[1] == BUF_POOL) {  // the stem conv samples the letterboxed images itself (fp32 x3-h16 kernel)
           if (!f32 || r[30] != 0) throw std::runtime_error("executor: letterbox-source conv must be fp32 over images");
           p.x = nullptr;

@@ -199,6 +199,7 @@ class Executor : public BatchInstance {
     // device
     uint8_t* d_in = nullptr;   // ctrl | meta | pool
     uint8_t* d_out = nullptr;  // det_count | det | topk
+    float* sk_ws = nullptr;    // split-K conv workspace: (kMaxLanes + 1) x sk_lane_bytes()
     // pinned host
     uint8_t* h_in = nullptr;
     size_t h_cap = 0;  // bytes of h_in (meta + host-packed inputs; grows on demand)
@@ -253,6 +254,7 @@ class Executor : public BatchInstance {
   void wait_done(Slot& sl);
   void note_done(Slot& sl);
   void release_copy(Slot& sl);
+  static int64_t sk_lane_bytes();
   uint64_t copy_release_n_ = 0;
   void launch_graph(Bucket& bk, int slot, hipStream_t st);
   void destroy_graphs(Bucket& bk, int slot);

@@ -92,6 +92,10 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
         out = torch.empty(B, Ho, Wo, co2, dtype=torch.float32, device=x.device)
         pwd = {"pw_w": _ptr(w2p), "pw_bias": _ptr(b2p), "pw_y": _ptr(out), "pw_ys": co2, "pw_cout": co2,
                "pw_kpad": k2, "pw_act": 0}
+    skd = {}
+    if 171 <= int(impl) < 180:  # split-K x3g: a workspace for the partial tiles (splits <= 8)
+        ws = torch.empty(8 * B * Ho * Wo * cpad, dtype=torch.float32, device=x.device)
+        skd = {"sk_ws": _ptr(ws), "sk_ws_bytes": ws.numel() * 4}
     native().conv2d({
         "x": _ptr(x, x_coff), "B": B, "H": H, "W": W, "xs": Cx, "Cin": cin,
         "w": _ptr(wt), "Kpad": kpad, "bias": _ptr(bt),
@@ -100,7 +104,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, stride: in
         "res": _ptr(res, res_coff), "rs": res.shape[-1] if res is not None else 0,
         "y2": _ptr(out2, out2_coff), "y2s": out2.shape[-1] if out2 is not None else 0,
         "act": ACT[act], "f32out": int(f32out), "bdev": _ptr(bdev), "stream": _stream(), "f32": int(f32),
-        "impl": int(impl), "w3": _ptr(w3), **pwd,
+        "impl": int(impl), "w3": _ptr(w3), **pwd, **skd,
     })
     if pw is not None:
         torch.cuda.synchronize(x.device)  # keep the packed 1x1 weights alive until the kernel ran

@@ -34,11 +34,13 @@ if [ "${RETUNE:-1}" = "1" ]; then
   tail -2 gpurun_out/$T/tune.log
   export ARENA_TUNING_FILE=gpurun_out/$T/conv_tuning.json
 fi
-$S 300 gpurun_out/$T/prof.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/p -o eng -- python3 tools/profile_engine.py --dtype fp32 --batch 32 --batches 12 || exit 1
-f=$(find gpurun_out/$T/p -name "eng_kernel_trace.csv" | head -1)
-python tools/analyze_trace.py "$f" --dtype fp32 --replays 8 --out gpurun_out/$T/ops_bs32.md > /dev/null 2>&1
-grep "device time" gpurun_out/$T/ops_bs32.md
-rm -rf gpurun_out/$T/p
+for bs in ${PROF_BS:-32}; do
+  $S 300 gpurun_out/$T/prof_$bs.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/p -o eng -- python3 tools/profile_engine.py --dtype fp32 --batch $bs --batches 12 || exit 1
+  f=$(find gpurun_out/$T/p -name "eng_kernel_trace.csv" | head -1)
+  python tools/analyze_trace.py "$f" --dtype fp32 --replays 8 --out gpurun_out/$T/ops_bs$bs.md > /dev/null 2>&1
+  echo "bs $bs: $(grep 'device time' gpurun_out/$T/ops_bs$bs.md)"
+  rm -rf gpurun_out/$T/p
+done
 if [ "${BENCH:-0}" = "1" ]; then
   $S 900 gpurun_out/$T/bench.log python -u bench.py --steps 20 --warmup 5 --latency-levels "" --no-secondary-inproc --no-secondary-bf16 || exit 1
   grep '^{' gpurun_out/$T/bench.log | tail -1 | cut -c1-600

@@ -81,6 +81,7 @@ def test_conv_f32_matches_fp64(device, B, H, Cin, Cout, k, s, act, res, up):
 X3_IMPLS = [40 + v for v in range(12)] + [101, 102, 103, 104, 105, 106, 107, 108, 109, 110] + \
     [111 + v for v in range(20)]
 X3G_IMPLS = [111 + v for v in range(20)]  # x3g: 32x32x16 MFMA GEMM over pre-split weights (gemm_x3.hip)
+X3G_IMPLS += [171 + v for v in range(9)]  # ... split-K (partials in a workspace, summed in split order)
 
 
 @pytest.mark.parametrize(
