@@ -256,7 +256,7 @@ class Executor : public BatchInstance {
   void release_copy(Slot& sl);
   static int64_t sk_lane_bytes();
   uint64_t copy_release_n_ = 0;
-  void launch_graph(Bucket& bk, int slot, hipStream_t st);
+  void launch_graph(Bucket& bk, int slot, hipStream_t st, int n_live = -1);  // n_live: images of the batch
   void destroy_graphs(Bucket& bk, int slot);
   bool lanes_for(const Bucket& bk) const;
   void enqueue_program(const std::vector<OpRecord>& prog, Bucket& bk, Slot& sl, hipStream_t s,
@@ -306,7 +306,7 @@ class Executor : public BatchInstance {
   // part i, so the batches in flight on the compute streams sit at different phases of the program instead of
   // drifting into step (launch_graph)
   std::vector<double> stagger_;  // split points as fractions of the program's ops, ascending
-  int stagger_min_batch_ = 16;  // ARENA_STAGGER_MIN_BATCH: buckets below it launch unstaggered
+  int stagger_min_batch_ = 32;  // ARENA_STAGGER_MIN_BATCH: batches with fewer live images launch unstaggered
   int last_launched_ = -1;  // slot of the last staggered launch
   bool has_topk_ = false, has_det_ = false, has_raw_ = false, has_stamps_ = false;
   double wall_khz_ = 100000.0;  // wall_clock64 rate (hipDeviceAttributeWallClockRate)

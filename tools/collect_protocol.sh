@@ -12,10 +12,12 @@ for d in $SRC/*/; do
   a=$(basename $d)
   mkdir -p $DST/$a
   cp $d/*_summary.json $DST/$a/ 2>/dev/null || true
-  cp $d/*_sweep_L*.csv $DST/$a/ 2>/dev/null || true
+  cp $d/*_sweep_L*.csv $d/*_sweep_all.csv $DST/$a/ 2>/dev/null || true
   cp $d/sweep.log $DST/$a/ 2>/dev/null || true
   label=$a
   [ "$a" = "microservices" ] && label="microservices, reference mode"
+  [ "$a" = "microservices_device" ] && label="microservices, device mode"
+  [ "$a" = "triton_tensor" ] && label="triton, reference-shaped tensor mode"
   args+=("$DST/$a:$label")
 done
 python tools/protocol_table.py "${args[@]}" > $DST/table.md
