@@ -463,8 +463,12 @@ bool conv_x3g(const ConvParams& p, hipStream_t s, int v) {
 bool conv_x3g_sk(const ConvParams& p, hipStream_t s, int v) {
   if (!x3g_supported(p) || p.Cout % 4) return false;
   switch (v) {
-#define XG_SK_CASE(V, WM, WN, TM, TN, S) \
-  case V: return xg_launch_sk<WM, WN, TM, TN>(p, s, S);
+// a shape the workspace cannot hold (a larger crop capacity than the table was tuned with) or with a single K chunk
+// runs the same tile unsplit
+#define XG_SK_CASE(V, WM, WN, TM, TN, S)                                   \
+  case V:                                                                  \
+    if (!xg_launch_sk<WM, WN, TM, TN>(p, s, S)) xg_launch<WM, WN, TM, TN, false>(p, s); \
+    return true;
     XG_SK_VARIANTS(XG_SK_CASE)
 #undef XG_SK_CASE
     default: return false;
