@@ -581,7 +581,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_irx_parts", &set_irx_parts);
   m.def("set_irx_slices_big", &set_irx_slices_big);
   m.def("set_ir_t14", &set_ir_t14);
-  m.def("set_ir_reg", &set_ir_reg);
   m.def("set_ir_crop", &set_ir_crop);
   m.def("set_ir_crop_split", &set_ir_crop_split);
   m.def("letterbox_s2d", &py_letterbox);

@@ -402,7 +402,6 @@ void ir_f32_prepare() {
   ARENA_HIP_CHECK(hipFuncSetAttribute((const void*)ir_f32_kernel<1, 8, 16, 1, false, 1, true>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   ir_tile_x3_prepare();
-  ir_reg_x3_prepare();
 }
 
 bool ir_block_f32_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand) {
@@ -436,8 +435,7 @@ void ir_block_f32(const IrParams& p, hipStream_t s) {
   if (ir_block_crop_f32(p, s)) return;  // 14x14 / 7x7 maps: whole-map x3 kernel (ir_crop_f32.hip)
   if (p.x_parts > 1 || p.y_parts > 1)
     throw std::runtime_error("ir_block_f32: partial-sum tensors belong to the whole-map 14x14 kernel");
-  if (p.x3w) {  // split-plane weights: the register-resident kernel (ir_reg_x3.hip), else the tiled one
-    if (ir_reg_x3(p, s)) return;
+  if (p.x3w) {  // split-plane weights: the tiled x3 kernel (ir_tile_x3.hip)
     if (ir_tile_x3(p, s)) return;
     throw std::runtime_error("ir_block_f32: split-plane weights for a block no x3 kernel takes");
   }

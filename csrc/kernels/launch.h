@@ -164,7 +164,6 @@ struct IrParams {
   // hidden channels are split over y_parts workgroups per band, each writing its partial output at channel
   // offset j * oup (partial 0 carries the project bias and the residual).
   int x_parts, y_parts;
-  int dbg = 0;  // diagnostic phase mask of ir_reg_x3 (ARENA_IR_REG_DBG): 1 no expand MFMA, 2 no depthwise, 4 no project MFMA
   // fp32 classifier front end (stem = 1, t = 1 blocks, ir_f32.hip): X is not read from memory but built per
   // tile from the batch's uint8 images: crop gather + ImageNet normalisation (crop_gather_s2d semantics) into a
   // space-to-depth tile in LDS, then the 2x2 stem conv over it (+ bias, ReLU6; zero outside the H x W map).
@@ -191,12 +190,6 @@ bool ir_block_crop_f32_supported(int H, int stride, int inp_pad, int hid_pad, in
 bool ir_tile_x3(const IrParams& p, hipStream_t s);
 bool ir_tile_x3_supported(int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
 void ir_tile_x3_prepare();
-// Register-resident fp32-accurate x3 block for the stride-1 56x56 / 28x28 stages (csrc/kernels/ir_reg_x3.hip);
-// tried before ir_tile_x3 (ARENA_IR_REG=0 turns it off)
-bool ir_reg_x3(const IrParams& p, hipStream_t s);
-bool ir_reg_x3_supported(int H, int stride, int inp_pad, int hid_pad, int oup_pad, int expand);
-void ir_reg_x3_prepare();
-void set_ir_reg(int v);  // 1 / 0: force the register-resident kernel on / off; -1: ARENA_IR_REG
 bool ir_stem_x3(const IrParams& p, hipStream_t s);  // IrParams.stem with x3w: split-plane stem / project weights
 void ir_prepare();
 void set_ir_t14(bool v);  // ARENA_IR_T14=1: stride-1 14x14 blocks use one whole-crop tile

@@ -52,7 +52,11 @@ Executor::Executor(const ExecutorConfig& cfg) : cfg_(cfg) {
     const char* at = std::getenv("ARENA_AUTOTUNE");
     autotune_ = at != nullptr ? std::atoi(at) : 1;
     const char* c = std::getenv("ARENA_COPY_MODE");
-    copy_mode_ = c != nullptr ? std::atoi(c) : 0;
+    // 0 (default): the input DMA on the shared copy stream, an event hands it to the batch's stream; 2: the DMA on
+    // the batch's own stream (no overlap with that stream's previous batch: -0.8 % engine req/s,
+    // profiles/r6_serving/leak).  Round 5's modes 1 (host wait) and 3 (per-slot copy streams) measured neutral or
+    // worse and are retired (profiles/r5_serving/leak/copy_ab).
+    copy_mode_ = c != nullptr && std::atoi(c) == 2 ? 2 : 0;
     const char* cc = std::getenv("ARENA_CONCURRENT");
     concurrent_ = cc != nullptr ? std::atoi(cc) : 1;
     if (debug_sync_) concurrent_ = 0;
@@ -146,10 +150,6 @@ Executor::~Executor() {
   retired_h_in_.clear();
   for (int s = 0; s < n_slots_; ++s) {
     Slot& sl = slots_[s];
-    if (sl.copy_stream) {
-      hipStreamSynchronize(sl.copy_stream);
-      hipStreamDestroy(sl.copy_stream);
-    }
     if (sl.copied) hipEventDestroy(sl.copied);
     if (sl.started) hipEventDestroy(sl.started);
     if (sl.done) hipEventDestroy(sl.done);
@@ -222,7 +222,6 @@ void Executor::alloc_slots() {
     ARENA_HIP_CHECK(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
     for (hipEvent_t& e : sl.phase) ARENA_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ARENA_HIP_CHECK(hipEventCreate(&sl.started));
-    if (copy_mode_ == 3) ARENA_HIP_CHECK(hipStreamCreateWithFlags(&sl.copy_stream, hipStreamNonBlocking));
     // ARENA_SYNC=blocking: collect() sleeps on the completion interrupt instead of polling the event (HIP's
     // default), which otherwise keeps a core busy per waiting thread for the whole device time of a batch
     static const bool blocking = [] {
@@ -1235,13 +1234,12 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   ctrl->n_images = n;
   ctrl->crop_base = 0;
   sl.in_used = in_bytes_meta() + off;
-  hipStream_t cs = copy_mode_ == 2 ? sl.stream : copy_mode_ == 3 ? sl.copy_stream : copy_;
+  hipStream_t cs = copy_mode_ == 2 ? sl.stream : copy_;
   ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, in_bytes_meta() + packed_end, hipMemcpyHostToDevice, cs));
   for (const JpegCopy& c : jcopies)
     ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in + in_bytes_meta() + c.dst, c.src, c.bytes, hipMemcpyHostToDevice, cs));
   if (copy_mode_ != 2) {
     ARENA_HIP_CHECK(hipEventRecord(sl.copied, cs));
-    if (copy_mode_ == 1) ARENA_HIP_CHECK(hipEventSynchronize(sl.copied));
     ARENA_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.copied, 0));
   }
   ARENA_HIP_CHECK(hipEventRecord(sl.started, sl.stream));
@@ -1424,24 +1422,17 @@ double Executor::remaining_us(int s) {
 // The batch's input DMA ran on the shared copy stream and only device streams waited for it (hipStreamWaitEvent).
 // Left at that, HIP keeps ~2 KB of live host allocations per batch without bound (profiles/r6_serving/leak:
 // +65 B/request of malloc'd bytes in use).  A host synchronisation of the copy stream releases them; a query or a
-// synchronize of the copy's event does not.  ARENA_COPY_RELEASE: 3 (default) hipStreamSynchronize(copy stream)
-// every 64 batches at collect (waits at most for the H2D copies queued behind this batch's: ~0.2 ms per 64
-// batches), 1 hipEventQuery / 2 hipEventSynchronize of the slot's copy event (both measured: still leaking),
-// 0 off.
+// synchronize of the copy's event does not (measured, same README).  Every 64 batches the collect synchronizes the
+// copy stream: it waits at most for the H2D copies queued behind this batch's, ~0.2 ms per 64 batches.
+// ARENA_COPY_RELEASE=0 turns it off.
 void Executor::release_copy(Slot& sl) {
-  static const int mode = [] {
+  (void)sl;
+  static const bool on = [] {
     const char* e = std::getenv("ARENA_COPY_RELEASE");
-    return e != nullptr ? std::atoi(e) : 3;
+    return e == nullptr || std::atoi(e) != 0;
   }();
-  if (copy_mode_ == 2 || mode == 0) return;
-  if (mode == 1) {
-    (void)hipEventQuery(sl.copied);
-    (void)hipGetLastError();
-  } else if (mode == 2) {
-    ARENA_HIP_CHECK(hipEventSynchronize(sl.copied));
-  } else if (mode == 3 && ++copy_release_n_ % 64 == 0) {
-    ARENA_HIP_CHECK(hipStreamSynchronize(copy_mode_ == 3 ? sl.copy_stream : copy_));
-  }
+  if (copy_mode_ == 2 || !on) return;
+  if (++copy_release_n_ % 64 == 0) ARENA_HIP_CHECK(hipStreamSynchronize(copy_));
 }
 
 BatchResult Executor::collect(int s) {
@@ -1680,8 +1671,6 @@ void Executor::replay(int B, int s, int iters) {
 void Executor::synchronize() {
   ARENA_HIP_CHECK(hipSetDevice(cfg_.device));
   ARENA_HIP_CHECK(hipStreamSynchronize(copy_));
-  for (int s = 0; s < n_slots_; ++s)
-    if (slots_[s].copy_stream) ARENA_HIP_CHECK(hipStreamSynchronize(slots_[s].copy_stream));
   sync_slots();
 }
 

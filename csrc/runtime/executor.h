@@ -207,7 +207,6 @@ class Executor : public BatchInstance {
     hipEvent_t copied = nullptr, started = nullptr, done = nullptr;
     // staggered launch: phase[i] = the batch finished part i of its program (ARENA_STAGGER)
     hipEvent_t phase[kMaxStaggerParts] = {};
-    hipStream_t copy_stream = nullptr;  // ARENA_COPY_MODE=3: this slot's own copy stream
     // Each slot owns an activation arena; its batch runs on one of the
     // executor's compute streams (round-robin by submission), so in-flight
     // batches overlap on the device: the small-grid tail of one batch's layers
@@ -313,8 +312,7 @@ class Executor : public BatchInstance {
   bool peer_stage_ = false;
   std::vector<int> peer_enabled_;  // devices this executor's device has peer access to
   void enable_peer(int src, const char* what);  // require_peer_access (runtime/peer.h) + hipDeviceEnablePeerAccess
-  int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 1 + host wait, 2 copy on the slot's stream,
-                        // 3 per-slot copy stream + event
+  int copy_mode_ = 0;   // ARENA_COPY_MODE: 0 copy stream + event, 2 copy on the slot's stream
   // ARENA_CONCURRENT: 1 = per-slot streams + arenas (in-flight batches overlap on the device),
   // 0 = two slots serialised on one stream sharing one arena.  ARENA_SLOTS: staging slots when concurrent
   // (default 4), ARENA_CONCURRENCY: compute streams = graphs running at once (default 3).

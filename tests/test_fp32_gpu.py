@@ -626,11 +626,6 @@ def test_ir_block_f32_matches_fp64(device, inp, hid, oup, stride, H, res, x3t, m
         native().set_irx_parts(4 if x3t == "0" else 2)
         request.addfinalizer(lambda: native().set_irx_parts(-1))
     monkeypatch.setenv("ARENA_IR_X3T", x3t)
-    if H >= 28:  # "1": the register-resident kernel (ir_reg_x3.hip, opt-in) where it applies; "0" keeps the others
-        from inference_arena_amd.ops import native
-
-        native().set_ir_reg(1 if x3t == "1" else 0)
-        request.addfinalizer(lambda: native().set_ir_reg(-1))
     g = torch.Generator().manual_seed(inp * 7 + hid + stride)
     x = torch.randn(3, inp, H, H, generator=g)
     expand = None if hid == inp else (torch.randn(hid, inp, 1, 1, generator=g) / inp ** 0.5,

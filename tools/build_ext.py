@@ -37,7 +37,6 @@ SOURCES = [
     "kernels/ir_f32.hip",
     "kernels/ir_crop_f32.hip",
     "kernels/ir_tile_x3.hip",
-    "kernels/ir_reg_x3.hip",
     "kernels/dwconv.hip",
     "kernels/ir_block.hip",
     "kernels/ir_block_wave.hip",
@@ -69,9 +68,7 @@ SOURCES = [
 ]
 
 
-# ir_reg_x3.hip keeps a whole strip's inputs, expanded rows and accumulators in registers: let the register
-# allocator spill the overflow to AGPRs (v_accvgpr moves) rather than scratch memory
-PER_FILE_FLAGS = {"ir_reg_x3.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]}
+PER_FILE_FLAGS: dict[str, list[str]] = {}
 
 
 def ext_path() -> Path:
