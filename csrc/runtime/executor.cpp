@@ -1108,18 +1108,12 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   sl.stream = streams_[seq_++ % n_streams_];
   // The slot's previous graph has been collected; its input copy was consumed.
   // Pool layout of the batch: host-packed inputs (RGB frames, tensors) first, so one H2D of the slot's
-  // [ctrl | meta | JPEG descriptors | packed inputs] covers them (the JPEG coefficients among them, see pack_coefs);
+  // [ctrl | meta | JPEG descriptors | packed inputs] covers them (the JPEG coefficients packed after them);
   // then per split-decoded JPEG its RGB destination and reconstruction planes.  Everything is validated before the first copy is queued.
   const size_t cap = pool_cap();
   // Split-decoded JPEGs' coefficients are copied on the host into the slot's pinned staging, right after the packed
-  // frames, and go to the device in the batch's one DMA.  ARENA_JPEG_PACK_COEFS=0 instead DMAs each upload's
-  // coefficients straight from its pooled buffer: no host copy (~0.14 ms CPU per 640x480 upload), but HIP then
-  // retains ~1.3 KB of host memory per upload on the shared copy stream, without bound
-  // (profiles/r5_serving/leak/README.md).
-  static const bool pack_coefs = [] {
-    const char* e = std::getenv("ARENA_JPEG_PACK_COEFS");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
+  // frames, and go to the device in the batch's one DMA.  (Round 5's alternative, one DMA per upload straight from
+  // its pooled buffer, made HIP retain ~1.3 KB of host memory per upload: profiles/r5_serving/leak/README.md.)
   {
     // host bytes of the packed (non-JPEG) inputs: grow the slot's pinned staging if this batch needs more (the
     // slot is idle: its previous H2D completed before it was collected)
@@ -1127,9 +1121,9 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     for (int i = 0; i < n; ++i)
       if (imgs[i].jpeg == nullptr)
         need = align_up(need + (imgs[i].bytes > 0 ? (size_t)imgs[i].bytes : (size_t)imgs[i].h * imgs[i].w * 3), 256);
-    if (pack_coefs)  // the JPEGs' coefficients follow them in the same DMA (layout below)
-      for (int i = 0; i < n; ++i)
-        if (imgs[i].jpeg != nullptr) need = align_up(need + (size_t)jpeg_payload_bytes(*imgs[i].jpeg), 256);
+    // the JPEGs' coefficients follow them in the same DMA (layout below)
+    for (int i = 0; i < n; ++i)
+      if (imgs[i].jpeg != nullptr) need = align_up(need + (size_t)jpeg_payload_bytes(*imgs[i].jpeg), 256);
     if (need > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
     if (in_bytes_meta() + need > sl.h_cap) {
       uint8_t* grown = nullptr;
@@ -1180,17 +1174,11 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     off = align_up(off + bytes, 256);
   }
   size_t packed_end = off;
-  struct JpegCopy {
-    size_t dst;
-    const uint8_t* src;
-    size_t bytes;
-  };
-  std::vector<JpegCopy> jcopies;
   int nj = 0, max_blocks = 0;
   int64_t max_pix = 0;
   // packed coefficients sit contiguously right after the host-packed inputs, inside the one staging DMA
   std::vector<size_t> coef_at(n, 0);
-  if (pack_coefs) {
+  {
     for (int i = 0; i < n; ++i) {
       const InputImage& im = imgs[i];
       if (im.jpeg == nullptr) continue;
@@ -1207,16 +1195,15 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
     if (im.jpeg == nullptr) continue;
     const JpegInfo& ji = *im.jpeg;
     if (ji.width != im.w || ji.height != im.h) throw std::runtime_error("submit: JPEG geometry mismatch");
-    const size_t rgb = off, coef = pack_coefs ? coef_at[i] : align_up(rgb + (size_t)im.h * im.w * 3, 256);
+    const size_t rgb = off, coef = coef_at[i];
     const size_t planes =
-        align_up((pack_coefs ? rgb + (size_t)im.h * im.w * 3 : coef + (size_t)jpeg_payload_bytes(ji)), 256);
+        align_up(rgb + (size_t)im.h * im.w * 3, 256);
     const size_t end = align_up(planes + (size_t)ji.plane_bytes, 256);
     if (end > cap) throw std::runtime_error("submit: batch exceeds the staging pool");
     set_meta(i, im, rgb);
     jdesc[nj] = jpeg_device_desc(ji, (int64_t)coef, (int64_t)planes, (int64_t)rgb);
     max_blocks = std::max(max_blocks, jdesc[nj].total_blocks);
     max_pix = std::max(max_pix, (int64_t)im.h * im.w);
-    if (!pack_coefs) jcopies.push_back({coef, im.data, (size_t)jpeg_payload_bytes(ji)});
     ++nj;
     off = end;
   }
@@ -1236,8 +1223,6 @@ int Executor::submit(const std::vector<InputImage>& imgs) {
   sl.in_used = in_bytes_meta() + off;
   hipStream_t cs = copy_mode_ == 2 ? sl.stream : copy_;
   ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in, sl.h_in, in_bytes_meta() + packed_end, hipMemcpyHostToDevice, cs));
-  for (const JpegCopy& c : jcopies)
-    ARENA_HIP_CHECK(hipMemcpyAsync(sl.d_in + in_bytes_meta() + c.dst, c.src, c.bytes, hipMemcpyHostToDevice, cs));
   if (copy_mode_ != 2) {
     ARENA_HIP_CHECK(hipEventRecord(sl.copied, cs));
     ARENA_HIP_CHECK(hipStreamWaitEvent(sl.stream, sl.copied, 0));
