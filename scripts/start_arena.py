@@ -189,14 +189,17 @@ def start(arch: str, gpus: int, log_dir: Path, device: str = "gpu", repo: str = 
             # spreading requests over every model server's native endpoint (least outstanding); 0 keeps the Python
             # gateway on gRPC :8001
             gw_native = os.environ.get("ARENA_GATEWAY_NATIVE", "1") != "0"
+            # Python gateway processes (SO_REUSEPORT on :8300): ARENA_GATEWAY_PROCS, default procs_per_gpu (the
+            # reference-shaped tensor mode is one GIL-bound process per gateway, ~15 ms CPU per request)
+            gw_py = int(os.environ.get("ARENA_GATEWAY_PROCS", str(procs_per_gpu)))
             procs.append(spawn(["inference_arena_amd.parallel.replicas", "--arch", "gateway", "--gpus",
                                 str(max(1, gpus) if gw_native else 1), "--port", "8300",
-                                "--procs-per-gpu", str(1 if gw_native else procs_per_gpu)],
+                                "--procs-per-gpu", str(1 if gw_native else gw_py)],
                                dict(env, TRITON_GRPC_ENDPOINT="127.0.0.1:8001", ARENA_DEVICE="cpu",
                                     TRITON_HTTP_ENDPOINT=plan["upstreams"],
                                     ARENA_GATEWAY_NATIVE="1" if gw_native else "0"), log_dir,
                                "gateway"))
-            ok = wait_replicas("http://127.0.0.1:8300/health", max(1, gpus) if gw_native else 1, 300, procs)
+            ok = wait_replicas("http://127.0.0.1:8300/health", max(1, gpus) if gw_native else gw_py, 300, procs)
     else:
         raise ValueError(arch)
     return procs, ok
