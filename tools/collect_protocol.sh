@@ -18,6 +18,7 @@ for d in $SRC/*/; do
   [ "$a" = "microservices" ] && label="microservices, reference mode"
   [ "$a" = "microservices_device" ] && label="microservices, device mode"
   [ "$a" = "triton_tensor" ] && label="triton, reference-shaped tensor mode"
+  [ "$a" = "triton_tensor8" ] && label="triton, reference-shaped tensor mode, 8 gateway processes"
   args+=("$DST/$a:$label")
 done
 python tools/protocol_table.py "${args[@]}" > $DST/table.md
