@@ -1581,8 +1581,10 @@ void conv2d_f32(const ConvParams& p, hipStream_t s) {
       return;
     }
     const int v = p.impl >= kF32X3HGPw && p.impl < kF32X3HGPw + kF32X3HGPwVariants ? p.impl - kF32X3HGPw
-                  : p.impl == 0                                                    ? (p.Cout_pad <= 64 ? 0 : 2)
-                                                                                   : -1;
+                  : p.impl >= kF32X3HGPwSmall && p.impl < kF32X3HGPwSmall + kF32X3HGPwSmallVariants
+                      ? kF32X3HGPwVariants + p.impl - kF32X3HGPwSmall
+                  : p.impl == 0 ? (p.Cout_pad <= 64 ? 0 : 2)
+                                : -1;
     if (v < 0 || !conv_x3hg_pw(p, s, v))
       throw std::runtime_error("conv2d_f32: a fused pointwise epilogue needs an x3hg-pw variant that fits the conv");
     return;

@@ -586,7 +586,9 @@ void hr_launch(const ConvParams& p, hipStream_t s) {
   X(2, 16, 4, 1, 3, 3)  /*  8 x 16 px, 80 -> 80 (cls branch) */ \
   X(3, 16, 4, 2, 3, 3)  /* 16 x 16 px */ \
   X(4, 8, 4, 1, 2, 2)   /* 16 x  8 px, 64 -> 64 */ \
-  X(5, 8, 4, 1, 3, 3)   /* 16 x  8 px, 80 -> 80 */
+  X(5, 8, 4, 1, 3, 3)   /* 16 x  8 px, 80 -> 80 */ \
+  X(6, 8, 2, 1, 2, 2)   /*  8 x  8 px, 2 waves: small buckets (kF32X3HGPwSmall) */ \
+  X(7, 8, 2, 1, 3, 3)   /*  8 x  8 px, 80 -> 80, 2 waves */
 
 // x3hr variants v (kF32X3HR + v): (TW, WM, WN, TM, TN)
 #define HR_VARIANTS(X) \
@@ -602,7 +604,13 @@ void hr_launch(const ConvParams& p, hipStream_t s) {
   X(9, 8, 4, 1, 1, 3)   /* 16 x  8 px x  96 ch */
 
 // x3hr with the fused Detect-head 1x1 (kF32X3HRPw + v): (TW, WM, TM, TN, PWN), WN = 1
-#define HR_PW_VARIANTS(X) HG_PW_VARIANTS(X)
+#define HR_PW_VARIANTS(X) \
+  X(0, 16, 4, 1, 2, 2)  \
+  X(1, 16, 4, 2, 2, 2)  \
+  X(2, 16, 4, 1, 3, 3)  \
+  X(3, 16, 4, 2, 3, 3)  \
+  X(4, 8, 4, 1, 2, 2)   \
+  X(5, 8, 4, 1, 3, 3)
 
 }  // namespace
 

@@ -112,6 +112,9 @@ void x3hg_prepare();
 // ... with the Detect head's final 1x1 fused into the epilogue (ConvParams.pw_*, fp32), variant v
 constexpr int kF32X3HGPw = 145;
 constexpr int kF32X3HGPwVariants = 6;
+// ... two more fused-1x1 tiles of 8 x 8 pixels on 2 waves (more workgroups for bucket 1 / 2): variants 6, 7
+constexpr int kF32X3HGPwSmall = 181;
+constexpr int kF32X3HGPwSmallVariants = 2;
 bool conv_x3hg_pw(const ConvParams& p, hipStream_t s, int v);
 // x3hr: the x3hg tiles with per-wave register weights (no weight LDS stage, two barriers per 16-channel chunk),
 // variant v; and with the fused Detect-head 1x1

@@ -350,6 +350,7 @@ void Executor::add_bucket(int B, const int64_t* offsets, int n_buffers, int64_t 
                                 v == kF32X3H16 || (v >= kF32X3G && v < kF32X3G + kF32X3GVariants) ||
                                 (v >= kF32X3HG && v < kF32X3HG + kF32X3HGVariants) ||
                                 (v >= kF32X3HGPw && v < kF32X3HGPw + kF32X3HGPwVariants) ||
+                                (v >= kF32X3HGPwSmall && v < kF32X3HGPwSmall + kF32X3HGPwSmallVariants) ||
                                 (v >= kF32X3HR && v < kF32X3HR + kF32X3HRVariants) ||
                                 (v >= kF32X3HRPw && v < kF32X3HRPw + kF32X3HRPwVariants) ||
                                 (v >= kF32X3GSK && v < kF32X3GSK + kF32X3GSKVariants)
@@ -406,7 +407,7 @@ void Executor::autotune(Bucket& bk) {
                                        kF32X3HG + 7, kF32X3HG + 8, kF32X3HG + 9, kF32X3HG + 10,
                                        // ... with the fused Detect-head 1x1 (the only kernels that take those ops)
                                        kF32X3HGPw + 0, kF32X3HGPw + 1, kF32X3HGPw + 2, kF32X3HGPw + 3,
-                                       kF32X3HGPw + 4, kF32X3HGPw + 5,
+                                       kF32X3HGPw + 4, kF32X3HGPw + 5, kF32X3HGPwSmall + 0, kF32X3HGPwSmall + 1,
                                        // x3hr: the same tiles with per-wave register weights (halo_x3g.hip)
                                        kF32X3HR + 0, kF32X3HR + 1, kF32X3HR + 2, kF32X3HR + 3, kF32X3HR + 4,
                                        kF32X3HR + 5, kF32X3HR + 6, kF32X3HR + 7, kF32X3HR + 8, kF32X3HR + 9,

@@ -198,6 +198,7 @@ def test_conv_x3hg_matches_fp64(device, B, H, Cin, Cout, act, res, up, s):
 
 
 X3HG_PW_IMPLS = [145 + v for v in range(6)] + [161 + v for v in range(6)]  # x3hg / x3hr with the fused 1x1
+X3HG_PW_IMPLS += [181, 182]  # x3hg-pw 8 x 8 pixel tiles on 2 waves (small buckets)
 
 
 @pytest.mark.parametrize("B,H,Cin,C", [(2, 20, 64, 64), (2, 19, 80, 80), (3, 11, 144, 64)])
