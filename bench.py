@@ -282,10 +282,15 @@ def _measure(lg, a, info, D, sync, users, fe, batcher):
             holder["cpu"] = HostCpu(fe)
             holder["b0"] = batcher.stats() if batcher is not None else None
             if not a.fake_engine:  # device busy over the timed window, 20 Hz (metrics/gpu.py BusySampler)
+                # (local query only: ``D`` is the solo stand-in in the node-wide shared-front window)
                 from inference_arena_amd.metrics.gpu import BusySampler
+                from inference_arena_amd.parallel.dist import device_identity
 
-                ident = D.device_identity(torch_device(), info.rank)
-                holder["busy"] = BusySampler(ident.get("pci_bus_id"), torch_device()).start()
+                try:
+                    ident = device_identity(torch_device(), info.rank)
+                    holder["busy"] = BusySampler(ident.get("pci_bus_id"), torch_device()).start()
+                except Exception as e:  # noqa: BLE001 - a missing sampler must not fail the measurement
+                    log(f"gpu busy sampler unavailable: {e}")
         window, c0 = _window(a, info, D, sync, lg.completed, wait_until, users, on_open=opened)
         busy = holder["busy"].stop() if "busy" in holder else None
         n = a.steps * a.batch * a.step_batches
