@@ -48,6 +48,28 @@ def test_batcher_stress_under_sanitizer(sanitizer):
 
 
 
+@pytest.mark.parametrize("sanitizer", ["thread", "address"])
+def test_string_pool_under_sanitizer(sanitizer):
+    """The front end's request-body pool (csrc/runtime/string_pool.h): bodies filled on producer threads, put back
+    from consumer threads, oversized ones freed, the pool bounded (csrc/tests/string_pool_stress.cpp)."""
+    if not (Path(HIPCC).exists() or shutil.which(HIPCC)):
+        pytest.skip("hipcc not available")
+    src = ROOT / "csrc" / "tests" / "string_pool_stress.cpp"
+    out = ROOT / "build" / f"string_pool_stress_{sanitizer}"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    newest = max(src.stat().st_mtime, (ROOT / "csrc" / "runtime" / "string_pool.h").stat().st_mtime)
+    if not out.exists() or out.stat().st_mtime < newest:
+        cmd = [HIPCC, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-Xarch_host", f"-fsanitize={sanitizer}",
+               "-I" + str(ROOT / "csrc"), str(src), "-o", str(out)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-4000:]
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1:halt_on_error=1")
+    r = subprocess.run([str(out), "5000"], capture_output=True, text=True, timeout=300, env=env)
+    report = r.stdout + r.stderr
+    assert "ThreadSanitizer" not in report and "AddressSanitizer" not in report, report[-6000:]
+    assert r.returncode == 0 and "string_pool_stress: ok" in r.stdout, report[-3000:]
+
+
 def test_arrivals_merge_while_a_batch_is_in_flight():
     """Requests trickling in (1 per ms) while the instance is busy (10 ms of 'device' time per batch,
     EchoInstance latency_us) are merged into the next batch rather than launched one by one: the instance
