@@ -58,6 +58,22 @@ def first_kernel(op0) -> str:
     return first
 
 
+def merge_split_k(q: list[dict]) -> list[dict]:
+    """One queue's dispatches in start order, with each split-K conv's second kernel (gemm_x3.hip, impl 171+: the
+    partial GEMM, then x3g_sk_reduce_kernel) folded into its op: the reduce's time is added to the GEMM row
+    (``_extra_ns``), so one row stays one program op."""
+    merged: list[dict] = []
+    for r in q:
+        if "x3g_sk_reduce_kernel" in r["Kernel_Name"] and merged:
+            prev = dict(merged[-1])
+            prev["_extra_ns"] = prev.get("_extra_ns", 0) + int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            prev["Kernel_Name"] = prev["Kernel_Name"].split("(")[0] + " + sk_reduce("
+            merged[-1] = prev
+        else:
+            merged.append(r)
+    return merged
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -82,19 +98,7 @@ def main(argv=None) -> int:
     first = first_kernel(prog.ops[0])
     replays = []
     for qk in list(by_q):
-        q = sorted(by_q[qk], key=lambda r: int(r["Start_Timestamp"]))
-        # a split-K conv (gemm_x3.hip, impl 171+) is two kernels: the partial GEMM and x3g_sk_reduce_kernel; the
-        # reduce's time counts to its op
-        merged = []
-        for r in q:
-            if "x3g_sk_reduce_kernel" in r["Kernel_Name"] and merged:
-                prev = dict(merged[-1])
-                prev["_extra_ns"] = prev.get("_extra_ns", 0) + int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                prev["Kernel_Name"] = prev["Kernel_Name"].split("(")[0] + " + sk_reduce("
-                merged[-1] = prev
-            else:
-                merged.append(r)
-        by_q[qk] = merged
+        by_q[qk] = merge_split_k(sorted(by_q[qk], key=lambda r: int(r["Start_Timestamp"])))
     for q in by_q.values():
         starts = [i for i, r in enumerate(q) if first in r["Kernel_Name"]]
         replays += [q[s:s + n_ops] for s in starts if s + n_ops <= len(q)]
