@@ -40,6 +40,7 @@ class ResourceSampler:
         self.roots = [psutil.Process(p) for p in pids if psutil.pid_exists(p)]
         self.samples: list[tuple[float, float, float, float | None, float | None]] = []
         self.by_role: dict[str, list[float]] = {}  # CPU % per process role, summed over that role's processes
+        self.mem_by_role: dict[str, list[float]] = {}  # RSS MB per process role (which service grows)
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
         self._cache: dict = {}
@@ -86,17 +87,22 @@ class ResourceSampler:
 
         cpu = mem = 0.0
         roles: dict[str, float] = {}
+        role_mem: dict[str, float] = {}
         for p in procs:
             try:
                 c = p.cpu_percent(None)
+                m = p.memory_info().rss / 2 ** 20
                 cpu += c
-                mem += p.memory_info().rss / 2 ** 20
+                mem += m
                 r = self._role(p)
                 roles[r] = roles.get(r, 0.0) + c
+                role_mem[r] = role_mem.get(r, 0.0) + m
             except psutil.NoSuchProcess:
                 continue
         for r, c in roles.items():
             self.by_role.setdefault(r, []).append(c)
+        for r, m in role_mem.items():
+            self.mem_by_role.setdefault(r, []).append(m)
         self._sample_threads(procs)
         busy = vram = None
         if self._gpu is not None:
@@ -215,6 +221,9 @@ class ResourceSampler:
             "resource_samples": len(self.samples),
         }
         out["cpu_percent_by_role"] = {r: round(float(np.mean(v)), 1) for r, v in sorted(self.by_role.items())}
+        # RSS per role, mean and last sample: run-to-run growth can be pinned to one service
+        out["memory_mb_by_role"] = {r: {"mean": round(float(np.mean(v)), 1), "last": round(float(v[-1]), 1)}
+                                    for r, v in sorted(self.mem_by_role.items())}
         if self.by_thread:
             n = max(len(v) for v in self.by_thread.values())
             by: dict[str, dict[str, float]] = {}

@@ -57,6 +57,10 @@ def test_resource_sampler_follows_a_process_tree():
     assert out["resource_samples"] >= 4
     assert out["memory_usage_mb"] > 10
     assert out["cpu_utilization_percent_max"] > 50.0, out  # the spinning child: ~100 % of one core
+    # RSS per role: the roles' last samples add up to about the total
+    by = out["memory_mb_by_role"]
+    assert by and all(v["mean"] > 0 and v["last"] > 0 for v in by.values()), by
+    assert abs(sum(v["mean"] for v in by.values()) - out["memory_usage_mb"]) < 0.05 * out["memory_usage_mb"] + 5
 
 
 def test_resource_sampler_splits_cpu_by_thread_class():
