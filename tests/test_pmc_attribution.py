@@ -76,3 +76,19 @@ def test_duration_check_flags_misattributed_counters():
     wrong[1] = {"GRBM_GUI_ACTIVE": list(good[0]["GRBM_GUI_ACTIVE"])}
     bad, _ = P.duration_check(wrong, dur, times, 0.30)
     assert len(bad) == 1 and bad[0].startswith("op 1:")
+
+
+def test_split_k_reduce_counts_to_its_op(tmp_path):
+    """A split-K conv dispatches the partial GEMM and x3g_sk_reduce_kernel; the op table (analyze_trace) names the op
+    "<gemm> + sk_reduce", and the counters of both dispatches belong to it."""
+    gemm = "conv_x3g_kernel<2, 2, 1, 1, false, true>"
+    rows = [(0, "1", "conv_x3_halo_kernel<2, 8>", 40.0, 7.7e5), (2, "1", gemm, 10.0, 3.0e5),
+            (4, "1", "x3g_sk_reduce_kernel", 3.0, 0.0), (6, "1", "conv_x3_stream_kernel<2, 1>", 12.0, 1.9e5)]
+    f = tmp_path / "run_counter_collection.csv"
+    _write(f, rows)
+    by_q = P.load_dispatches(f)
+    names = [d["name"] for d in by_q["1"]]
+    assert names == ["conv_x3_halo_kernel<2, 8>", gemm + " + sk_reduce", "conv_x3_stream_kernel<2, 1>"]
+    sk = by_q["1"][1]
+    assert sk["counters"]["SQ_INSTS_MFMA"] == 3.0e5
+    assert sk["counters"]["GRBM_GUI_ACTIVE"] == ((10.0 + FLOOR_US) + (3.0 + FLOOR_US)) * MHZ * 8

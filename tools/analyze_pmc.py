@@ -82,7 +82,19 @@ def load_dispatches(counter_csv: Path) -> dict[str, list[dict]]:
         e["counters"][r["Counter_Name"]] = e["counters"].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     by_q: dict[str, list[dict]] = defaultdict(list)
     for d in sorted(by_id):
-        by_q[by_id[d]["queue"]].append(by_id[d])
+        e = by_id[d]
+        q = by_q[e["queue"]]
+        if e["name"] == "x3g_sk_reduce_kernel" and q:
+            # a split-K conv's second kernel (gemm_x3.hip): its counters and time count to the op, as in the op
+            # table (tools/analyze_trace.py merge_split_k names the op "<gemm kernel> + sk_reduce")
+            prev = q[-1]
+            for k, v in e["counters"].items():
+                prev["counters"][k] = prev["counters"].get(k, 0.0) + v
+            prev["end"] = max(prev["end"], e["end"])
+            if not prev["name"].endswith(" + sk_reduce"):
+                prev["name"] += " + sk_reduce"
+            continue
+        q.append(e)
     return by_q
 
 
